@@ -1,0 +1,13 @@
+"""paddle.amp (reference: python/paddle/amp/{auto_cast,grad_scaler}.py).
+
+* ``auto_cast(level='O1')`` runs white-listed ops (matmul/conv/linear) in bf16/fp16 via the
+  storage layer's autocast; ``level='O2'`` expects parameters already cast by ``decorate``.
+* ``decorate(level='O2')`` casts parameters to the low-precision dtype except normalisation
+  layers (kept fp32, like the reference) and turns on optimizer master weights.
+* ``GradScaler`` — dynamic loss scaling with found-inf skip (needed for fp16; bf16 runs
+  with ``enable=False`` semantics by default).
+"""
+from .auto_cast import auto_cast, amp_guard, decorate, amp_decorate, is_float16_supported, is_bfloat16_supported  # noqa: F401
+from .grad_scaler import GradScaler, AmpScaler, OptimizerState  # noqa: F401
+from . import debugging  # noqa: F401
+from .amp_lists import white_list, black_list  # noqa: F401

@@ -1,0 +1,276 @@
+// Fused activation / dropout kernels (vectorised 16-byte, grid-stride, fp32 math).
+//
+// Reference semantics: paddle/phi/kernels/gpu/gelu_kernel.cu / gelu_grad_kernel.cu,
+// paddle/phi/kernels/fusion/gpu/fused_bias_act_kernel.cu (bias + act in one pass),
+// paddle/phi/kernels/fusion/gpu/fused_dropout_add_kernel.cu, swiglu (incubate).
+//
+// Dropout masks are never stored: the keep-decision is a stateless hash of
+// (seed, offset, element index), so backward regenerates it bit-exactly.
+#include "common.h"
+
+namespace pa {
+
+struct GeluErf {
+  static __device__ __forceinline__ float f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+  static __device__ __forceinline__ float df(float x) {
+    return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+  }
+};
+struct GeluTanh {
+  static __device__ __forceinline__ float f(float x) {
+    const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
+    return 0.5f * x * (1.f + tanhf(u));
+  }
+  static __device__ __forceinline__ float df(float x) {
+    const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
+    const float t = tanhf(u);
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.79788456080286536f * (1.f + 3.f * 0.044715f * x * x);
+  }
+};
+struct Silu {
+  static __device__ __forceinline__ float f(float x) { return x / (1.f + __expf(-x)); }
+  static __device__ __forceinline__ float df(float x) {
+    const float s = 1.f / (1.f + __expf(-x));
+    return s * (1.f + x * (1.f - s));
+  }
+};
+struct Relu {
+  static __device__ __forceinline__ float f(float x) { return x > 0.f ? x : 0.f; }
+  static __device__ __forceinline__ float df(float x) { return x > 0.f ? 1.f : 0.f; }
+};
+struct Ident {
+  static __device__ __forceinline__ float f(float x) { return x; }
+  static __device__ __forceinline__ float df(float) { return 1.f; }
+};
+
+// y = act(x + bias[col])   (bias may be null);   cols = size of the bias (last dim)
+template <typename T, typename Act>
+__global__ __launch_bounds__(256) void bias_act_fwd(const T* __restrict__ x, const T* __restrict__ bias,
+                                                    T* __restrict__ y, long long n, int cols) {
+  constexpr int E = 16 / sizeof(T);
+  const long long nv = n / E;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) {
+    float v[E];
+    load_f<T, E>(x + i * E, v);
+    if (bias != nullptr) {
+      float b[E];
+      load_f<T, E>(bias + (int)((i * E) % cols), b);
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[e] += b[e];
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = Act::f(v[e]);
+    store_f<T, E>(y + i * E, v);
+  }
+  // tail (n % E elements) handled by the first block
+  if (blockIdx.x == 0) {
+    for (long long i = nv * E + threadIdx.x; i < n; i += 256) {
+      float v = to_f(x[i]) + (bias != nullptr ? to_f(bias[i % cols]) : 0.f);
+      y[i] = from_f<T>(Act::f(v));
+    }
+  }
+}
+
+// dx = dy * act'(x + bias);  dbias is reduced by the caller from dx (bias grad = colsum(dx))
+template <typename T, typename Act>
+__global__ __launch_bounds__(256) void bias_act_bwd(const T* __restrict__ dy, const T* __restrict__ x,
+                                                    const T* __restrict__ bias, T* __restrict__ dx, long long n,
+                                                    int cols) {
+  constexpr int E = 16 / sizeof(T);
+  const long long nv = n / E;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) {
+    float v[E], g[E];
+    load_f<T, E>(x + i * E, v);
+    load_f<T, E>(dy + i * E, g);
+    if (bias != nullptr) {
+      float b[E];
+      load_f<T, E>(bias + (int)((i * E) % cols), b);
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[e] += b[e];
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) g[e] *= Act::df(v[e]);
+    store_f<T, E>(dx + i * E, g);
+  }
+  if (blockIdx.x == 0) {
+    for (long long i = nv * E + threadIdx.x; i < n; i += 256) {
+      float v = to_f(x[i]) + (bias != nullptr ? to_f(bias[i % cols]) : 0.f);
+      dx[i] = from_f<T>(to_f(dy[i]) * Act::df(v));
+    }
+  }
+}
+
+// swiglu: y = silu(a) * b   (a, b: separate tensors of n elements, both contiguous)
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_fwd(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ y,
+                                                  long long n, int a_stride_rows, int cols) {
+  constexpr int E = 16 / sizeof(T);
+  const long long nv = n / E;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) {
+    const long long e0 = i * E;
+    const long long r = e0 / cols, c = e0 % cols;
+    const long long src = r * a_stride_rows + c;
+    float va[E], vb[E], o[E];
+    load_f<T, E>(a + src, va);
+    load_f<T, E>(b + src, vb);
+#pragma unroll
+    for (int e = 0; e < E; ++e) o[e] = Silu::f(va[e]) * vb[e];
+    store_f<T, E>(y + e0, o);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_bwd(const T* __restrict__ a, const T* __restrict__ b,
+                                                  const T* __restrict__ dy, T* __restrict__ da, T* __restrict__ db,
+                                                  long long n, int a_stride_rows, int cols) {
+  constexpr int E = 16 / sizeof(T);
+  const long long nv = n / E;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) {
+    const long long e0 = i * E;
+    const long long r = e0 / cols, c = e0 % cols;
+    const long long src = r * a_stride_rows + c;
+    float va[E], vb[E], g[E], oa[E], ob[E];
+    load_f<T, E>(a + src, va);
+    load_f<T, E>(b + src, vb);
+    load_f<T, E>(dy + e0, g);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      oa[e] = g[e] * vb[e] * Silu::df(va[e]);
+      ob[e] = g[e] * Silu::f(va[e]);
+    }
+    store_f<T, E>(da + src, oa);
+    store_f<T, E>(db + src, ob);
+  }
+}
+
+// out = (residual ? residual : 0) + x * keep / (1 - p)
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_add_fwd(const T* __restrict__ x, const T* __restrict__ residual,
+                                                       T* __restrict__ y, long long n, float p, uint32_t seed,
+                                                       uint32_t offset) {
+  constexpr int E = 16 / sizeof(T);
+  const float scale = 1.f / (1.f - p);
+  const long long nv = n / E;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) {
+    float v[E];
+    load_f<T, E>(x + i * E, v);
+    const uint32_t h0 = hash3(seed, offset, (uint32_t)(i));
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const uint32_t h = (e == 0) ? h0 : hash3(h0, (uint32_t)e, 0x2545F491u);
+      v[e] = uniform01(h) >= p ? v[e] * scale : 0.f;
+    }
+    if (residual != nullptr) {
+      float r[E];
+      load_f<T, E>(residual + i * E, r);
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[e] += r[e];
+    }
+    store_f<T, E>(y + i * E, v);
+  }
+  if (blockIdx.x == 0) {
+    for (long long i = nv * E + threadIdx.x; i < n; i += 256) {
+      const uint32_t h = hash3(seed ^ 0x5bd1e995u, offset, (uint32_t)i);
+      float v = uniform01(h) >= p ? to_f(x[i]) * scale : 0.f;
+      if (residual != nullptr) v += to_f(residual[i]);
+      y[i] = from_f<T>(v);
+    }
+  }
+}
+
+// dx = dy * keep / (1 - p)   (same hash stream as the forward)
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_bwd(const T* __restrict__ dy, T* __restrict__ dx, long long n, float p,
+                                                   uint32_t seed, uint32_t offset) {
+  constexpr int E = 16 / sizeof(T);
+  const float scale = 1.f / (1.f - p);
+  const long long nv = n / E;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) {
+    float v[E];
+    load_f<T, E>(dy + i * E, v);
+    const uint32_t h0 = hash3(seed, offset, (uint32_t)(i));
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const uint32_t h = (e == 0) ? h0 : hash3(h0, (uint32_t)e, 0x2545F491u);
+      v[e] = uniform01(h) >= p ? v[e] * scale : 0.f;
+    }
+    store_f<T, E>(dx + i * E, v);
+  }
+  if (blockIdx.x == 0) {
+    for (long long i = nv * E + threadIdx.x; i < n; i += 256) {
+      const uint32_t h = hash3(seed ^ 0x5bd1e995u, offset, (uint32_t)i);
+      dx[i] = from_f<T>(uniform01(h) >= p ? to_f(dy[i]) * scale : 0.f);
+    }
+  }
+}
+
+template <typename T, typename Act>
+hipError_t launch_act(int dir, const void* dy, const void* x, const void* bias, void* out, long long n, int cols,
+                      hipStream_t st) {
+  constexpr int E = 16 / sizeof(T);
+  const int g = grid_for(n / E + 1, 256, 256 * 8);
+  if (dir == 0) bias_act_fwd<T, Act><<<g, 256, 0, st>>>((const T*)x, (const T*)bias, (T*)out, n, cols);
+  else bias_act_bwd<T, Act><<<g, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)bias, (T*)out, n, cols);
+  return hipGetLastError();
+}
+
+}  // namespace pa
+
+using namespace pa;
+
+// act: 0 = gelu(erf), 1 = gelu(tanh), 2 = silu, 3 = relu, 4 = identity (bias add only)
+// dir: 0 = forward (out = act(x + bias)), 1 = backward (out = dy * act'(x + bias))
+PA_API hipError_t pa_bias_act(int act, int dir, const void* dy, const void* x, const void* bias, void* out,
+                              long long n, int cols, int dt, hipStream_t st) {
+  PA_DISPATCH_DTYPE(dt, T, {
+    switch (act) {
+      case 0: return launch_act<T, GeluErf>(dir, dy, x, bias, out, n, cols, st);
+      case 1: return launch_act<T, GeluTanh>(dir, dy, x, bias, out, n, cols, st);
+      case 2: return launch_act<T, Silu>(dir, dy, x, bias, out, n, cols, st);
+      case 3: return launch_act<T, Relu>(dir, dy, x, bias, out, n, cols, st);
+      case 4: return launch_act<T, Ident>(dir, dy, x, bias, out, n, cols, st);
+      default: return hipErrorInvalidValue;
+    }
+  });
+  return hipSuccess;
+}
+
+// a, b: [rows, cols] views with row stride a_stride (elements); y / da / db dense [rows, cols]
+// (da/db written with the same strided layout as a/b, so a fused [rows, 2*cols] gate buffer works).
+PA_API hipError_t pa_swiglu_fwd(const void* a, const void* b, void* y, long long n, int a_stride, int cols, int dt,
+                                hipStream_t st) {
+  if (cols % 8 != 0 && dt != 0) return hipErrorInvalidValue;
+  PA_DISPATCH_DTYPE(dt, T, {
+    const int g = grid_for(n / (16 / sizeof(T)) + 1, 256, 256 * 8);
+    swiglu_fwd<T><<<g, 256, 0, st>>>((const T*)a, (const T*)b, (T*)y, n, a_stride, cols);
+  });
+  return hipGetLastError();
+}
+
+PA_API hipError_t pa_swiglu_bwd(const void* a, const void* b, const void* dy, void* da, void* db, long long n,
+                                int a_stride, int cols, int dt, hipStream_t st) {
+  if (cols % 8 != 0 && dt != 0) return hipErrorInvalidValue;
+  PA_DISPATCH_DTYPE(dt, T, {
+    const int g = grid_for(n / (16 / sizeof(T)) + 1, 256, 256 * 8);
+    swiglu_bwd<T><<<g, 256, 0, st>>>((const T*)a, (const T*)b, (const T*)dy, (T*)da, (T*)db, n, a_stride, cols);
+  });
+  return hipGetLastError();
+}
+
+PA_API hipError_t pa_dropout_add_fwd(const void* x, const void* residual, void* y, long long n, float p, uint32_t seed,
+                                     uint32_t offset, int dt, hipStream_t st) {
+  PA_DISPATCH_DTYPE(dt, T, {
+    const int g = grid_for(n / (16 / sizeof(T)) + 1, 256, 256 * 8);
+    dropout_add_fwd<T><<<g, 256, 0, st>>>((const T*)x, (const T*)residual, (T*)y, n, p, seed, offset);
+  });
+  return hipGetLastError();
+}
+
+PA_API hipError_t pa_dropout_bwd(const void* dy, void* dx, long long n, float p, uint32_t seed, uint32_t offset, int dt,
+                                 hipStream_t st) {
+  PA_DISPATCH_DTYPE(dt, T, {
+    const int g = grid_for(n / (16 / sizeof(T)) + 1, 256, 256 * 8);
+    dropout_bwd<T><<<g, 256, 0, st>>>((const T*)dy, (T*)dx, n, p, seed, offset);
+  });
+  return hipGetLastError();
+}

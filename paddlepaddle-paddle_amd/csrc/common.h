@@ -1,0 +1,118 @@
+// Shared device helpers for the paddle_amd HIP kernel library (gfx950 / CDNA4 only).
+//
+// Conventions
+//  * dtype codes passed from Python: 0 = fp32, 1 = bf16, 2 = fp16.
+//  * All launchers are extern "C", take raw device pointers and the caller's hipStream_t,
+//    never allocate or synchronise (so they can be captured into hipGraphs), and return
+//    hipError_t of the launch.
+//  * Wave = 64 lanes. Block sizes are multiples of 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PA_API extern "C" __attribute__((visibility("default")))
+
+namespace pa {
+
+constexpr int kWave = 64;
+
+using bf16_t = __bf16;
+using f16_t = _Float16;
+
+template <typename T> struct Vec8;  // 16-byte vector of 8 x 16-bit or 4 x fp32 (handled separately)
+
+__device__ __forceinline__ float to_f(float v) { return v; }
+__device__ __forceinline__ float to_f(bf16_t v) { return (float)v; }
+__device__ __forceinline__ float to_f(f16_t v) { return (float)v; }
+
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) { return (bf16_t)v; }
+template <> __device__ __forceinline__ f16_t from_f<f16_t>(float v) { return (f16_t)v; }
+
+// Load/store N contiguous elements (N*sizeof(T) must be 4, 8 or 16 bytes) as one vector access.
+template <typename T, int N> struct alignas(sizeof(T) * N) Pack { T v[N]; };
+
+template <typename T, int N>
+__device__ __forceinline__ void load_f(const T* __restrict__ p, float (&out)[N]) {
+  Pack<T, N> pk = *reinterpret_cast<const Pack<T, N>*>(p);
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = to_f(pk.v[i]);
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void store_f(T* __restrict__ p, const float (&in)[N]) {
+  Pack<T, N> pk;
+#pragma unroll
+  for (int i = 0; i < N; ++i) pk.v[i] = from_f<T>(in[i]);
+  *reinterpret_cast<Pack<T, N>*>(p) = pk;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64). `red` must hold NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += red[i];
+  __syncthreads();
+  return r;
+}
+
+template <int NT>
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float r = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r = fmaxf(r, red[i]);
+  __syncthreads();
+  return r;
+}
+
+// Counter-based RNG (for dropout): a cheap stateless hash of (seed, offset, index) → uniform [0,1).
+__device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
+  // murmur3-style finaliser chain
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u);
+  h ^= c * 0x85EBCA77u;
+  h ^= h >> 16; h *= 0x7FEB352Du;
+  h ^= h >> 15; h *= 0x846CA68Bu;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ float uniform01(uint32_t h) { return (h >> 8) * (1.0f / 16777216.0f); }
+
+// Grid size for memory-bound grid-stride kernels: enough waves to fill 256 CUs.
+inline int grid_for(long long work_items, int per_block, int cap = 256 * 16) {
+  long long g = (work_items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+}  // namespace pa
+
+#define PA_DISPATCH_DTYPE(code, T, ...)                         \
+  switch (code) {                                               \
+    case 0: { using T = float; __VA_ARGS__; break; }            \
+    case 1: { using T = pa::bf16_t; __VA_ARGS__; break; }       \
+    case 2: { using T = pa::f16_t; __VA_ARGS__; break; }        \
+    default: return hipErrorInvalidValue;                       \
+  }

@@ -1,0 +1,199 @@
+// Embedding gather/scatter-add, fused rotary position embedding, and the fused AdamW update
+// over flat parameter buffers.
+//
+// Reference semantics: paddle/phi/kernels/gpu/embedding_kernel.cu / embedding_grad_kernel.cu,
+// paddle/phi/kernels/fusion/gpu/fused_rope_kernel.cu (+ fused_rope_grad), paddle/phi/kernels/
+// gpu/adamw_kernel.cu (paddle's AdamW: decoupled decay p *= 1 - lr*coeff, epsilon scaled by
+// sqrt(1 - beta2^t)), multi_precision master weights.
+#include "common.h"
+
+namespace pa {
+
+// out[i, :] = w[ids[i], :]   — one wave per row, 16-byte vectors
+template <typename T>
+__global__ __launch_bounds__(256) void embedding_fwd(const int64_t* __restrict__ ids, const T* __restrict__ w,
+                                                     T* __restrict__ out, int n, int dim, int64_t vocab) {
+  constexpr int E = 16 / sizeof(T);
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  int64_t id = ids[row];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  const T* src = w + id * dim;
+  T* dst = out + (size_t)row * dim;
+  for (int j = lane * E; j < dim; j += 64 * E)
+    *reinterpret_cast<Pack<T, E>*>(dst + j) = *reinterpret_cast<const Pack<T, E>*>(src + j);
+}
+
+// dw32[ids[i], :] += dy[i, :]  (fp32 accumulation; 256-byte contiguous atomics per wave instruction)
+template <typename T>
+__global__ __launch_bounds__(256) void embedding_bwd(const int64_t* __restrict__ ids, const T* __restrict__ dy,
+                                                     float* __restrict__ dw32, int n, int dim, int64_t vocab) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  int64_t id = ids[row];
+  if (id < 0 || id >= vocab) return;
+  const T* src = dy + (size_t)row * dim;
+  float* dst = dw32 + id * dim;
+  for (int j = lane; j < dim; j += 64) atomicAdd(dst + j, to_f(src[j]));
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void cast_f32(const float* __restrict__ in, T* __restrict__ out, long long n,
+                                                int accumulate) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    out[i] = from_f<T>(in[i] + (accumulate ? to_f(out[i]) : 0.f));
+}
+
+// Rotary embedding over x[B, S, H, D] (row stride = H*D, contiguous D).
+//   half style (neox=0): pairs (i, i + D/2);  interleaved (neox=1): pairs (2i, 2i+1)
+//   cos/sin: [S, D/2] fp32 tables;  sign = +1 forward, -1 backward (rotation by -theta)
+template <typename T>
+__global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                   const float* __restrict__ cosb, const float* __restrict__ sinb,
+                                                   const int64_t* __restrict__ pos, int B, int S, int H, int D,
+                                                   int interleaved, float sign) {
+  const long long npairs = (long long)B * S * H * (D / 2);
+  const int half = D / 2;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < npairs; i += (long long)gridDim.x * 256) {
+    const int p = (int)(i % half);
+    const long long bsh = i / half;
+    const int s = (int)((bsh / H) % S);
+    const int b = (int)(bsh / ((long long)H * S));
+    const int ps = pos != nullptr ? (int)pos[(long long)b * S + s] : s;
+    const float c = cosb[(size_t)ps * half + p];
+    const float sn = sign * sinb[(size_t)ps * half + p];
+    const long long base = bsh * D;
+    const int i0 = interleaved ? 2 * p : p;
+    const int i1 = interleaved ? 2 * p + 1 : p + half;
+    const float a = to_f(x[base + i0]), bb = to_f(x[base + i1]);
+    y[base + i0] = from_f<T>(a * c - bb * sn);
+    y[base + i1] = from_f<T>(bb * c + a * sn);
+  }
+}
+
+// Paddle AdamW on a flat fp32 master buffer:
+//   p *= (1 - lr * wd);  m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2
+//   p -= lr * sqrt(1-b2^t)/(1-b1^t) * m / (sqrt(v) + eps * sqrt(1-b2^t))
+// grad may be bf16/fp16/fp32; `lowp` (optional) receives the updated param in the model dtype.
+// lr/b1pow/b2pow are read from device scalars so a captured hipGraph replays with fresh values.
+template <typename G, typename P>
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const G* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, P* __restrict__ lowp,
+                                                    long long n, const float* __restrict__ lr_ptr, float lr_host,
+                                                    float b1, float b2, float eps, float wd, float b1pow, float b2pow,
+                                                    const float* __restrict__ grad_scale) {
+  const float lr = lr_ptr != nullptr ? *lr_ptr : lr_host;
+  const float gs = grad_scale != nullptr ? *grad_scale : 1.f;
+  const float bc2 = sqrtf(1.f - b2pow);
+  const float step = lr * bc2 / (1.f - b1pow);
+  const float decay = 1.f - lr * wd;
+  const float eps_hat = eps * bc2;
+  constexpr int E = 4;
+  const long long nv = n / E;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) {
+    float pv[E], gv[E], mv[E], vv[E];
+    load_f<float, E>(p + i * E, pv);
+    load_f<G, E>(g + i * E, gv);
+    load_f<float, E>(m + i * E, mv);
+    load_f<float, E>(v + i * E, vv);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float gg = gv[e] * gs;
+      pv[e] *= decay;
+      mv[e] = b1 * mv[e] + (1.f - b1) * gg;
+      vv[e] = b2 * vv[e] + (1.f - b2) * gg * gg;
+      pv[e] -= step * mv[e] / (sqrtf(vv[e]) + eps_hat);
+    }
+    store_f<float, E>(p + i * E, pv);
+    store_f<float, E>(m + i * E, mv);
+    store_f<float, E>(v + i * E, vv);
+    if (lowp != nullptr) store_f<P, E>(lowp + i * E, pv);
+  }
+  if (blockIdx.x == 0) {
+    for (long long i = nv * E + threadIdx.x; i < n; i += 256) {
+      const float gg = to_f(g[i]) * gs;
+      float pv = p[i] * decay;
+      const float mv = b1 * m[i] + (1.f - b1) * gg;
+      const float vv = b2 * v[i] + (1.f - b2) * gg * gg;
+      pv -= step * mv / (sqrtf(vv) + eps_hat);
+      p[i] = pv;
+      m[i] = mv;
+      v[i] = vv;
+      if (lowp != nullptr) lowp[i] = from_f<P>(pv);
+    }
+  }
+}
+
+// sum of squares of a flat buffer into out[blockIdx] (for global-norm clipping / found-inf check)
+template <typename T>
+__global__ __launch_bounds__(256) void sumsq_kernel(const T* __restrict__ x, long long n, float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const float v = to_f(x[i]);
+    s += v * v;
+  }
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+}  // namespace pa
+
+using namespace pa;
+
+PA_API hipError_t pa_embedding_fwd(const int64_t* ids, const void* w, void* out, int n, int dim, long long vocab,
+                                   int dt, hipStream_t st) {
+  if ((dim * (dt == 0 ? 4 : 2)) % 16 != 0) return hipErrorInvalidValue;
+  PA_DISPATCH_DTYPE(dt, T, embedding_fwd<T><<<(n + 3) / 4, 256, 0, st>>>(ids, (const T*)w, (T*)out, n, dim, vocab));
+  return hipGetLastError();
+}
+
+// dw32 must be zeroed by the caller (hipMemsetAsync); out (param dtype) = dw32 (+ out if accumulate)
+PA_API hipError_t pa_embedding_bwd(const int64_t* ids, const void* dy, float* dw32, void* out, int n, int dim,
+                                   long long vocab, int accumulate, int dt, hipStream_t st) {
+  PA_DISPATCH_DTYPE(dt, T, {
+    embedding_bwd<T><<<(n + 3) / 4, 256, 0, st>>>(ids, (const T*)dy, dw32, n, dim, vocab);
+    if (out != nullptr && (void*)out != (void*)dw32) {
+      const long long tot = vocab * dim;
+      cast_f32<T><<<grid_for(tot, 256, 256 * 8), 256, 0, st>>>(dw32, (T*)out, tot, accumulate);
+    }
+  });
+  return hipGetLastError();
+}
+
+PA_API hipError_t pa_rope(const void* x, void* y, const float* cosb, const float* sinb, const int64_t* pos, int B,
+                          int S, int H, int D, int interleaved, float sign, int dt, hipStream_t st) {
+  const long long npairs = (long long)B * S * H * (D / 2);
+  PA_DISPATCH_DTYPE(dt, T, rope_kernel<T><<<grid_for(npairs, 256, 256 * 8), 256, 0, st>>>(
+                               (const T*)x, (T*)y, cosb, sinb, pos, B, S, H, D, interleaved, sign));
+  return hipGetLastError();
+}
+
+// gd = grad dtype, pd = low-precision param copy dtype (-1 = none)
+PA_API hipError_t pa_adamw(float* p, const void* g, float* m, float* v, void* lowp, long long n, const float* lr_ptr,
+                           float lr, float b1, float b2, float eps, float wd, float b1pow, float b2pow,
+                           const float* grad_scale, int gd, int pd, hipStream_t st) {
+  const int grid = grid_for(n / 4 + 1, 256, 256 * 8);
+#define PA_ADAM(G, P) \
+  adamw_kernel<G, P><<<grid, 256, 0, st>>>(p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1, b2, eps, wd, b1pow, b2pow, grad_scale)
+  if (pd < 0) lowp = nullptr;
+  const int pp = pd < 0 ? 0 : pd;
+  if (gd == 0 && pp == 0) PA_ADAM(float, float);
+  else if (gd == 1 && pp == 1) PA_ADAM(bf16_t, bf16_t);
+  else if (gd == 1 && pp == 0) PA_ADAM(bf16_t, float);
+  else if (gd == 0 && pp == 1) PA_ADAM(float, bf16_t);
+  else if (gd == 2 && pp == 2) PA_ADAM(f16_t, f16_t);
+  else if (gd == 0 && pp == 2) PA_ADAM(float, f16_t);
+  else return hipErrorInvalidValue;
+#undef PA_ADAM
+  return hipGetLastError();
+}
+
+PA_API int pa_sumsq_parts() { return 1024; }
+
+PA_API hipError_t pa_sumsq(const void* x, long long n, float* part, int dt, hipStream_t st) {
+  PA_DISPATCH_DTYPE(dt, T, sumsq_kernel<T><<<1024, 256, 0, st>>>((const T*)x, n, part));
+  return hipGetLastError();
+}

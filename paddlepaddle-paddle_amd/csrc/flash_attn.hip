@@ -1,0 +1,622 @@
+// Flash attention forward + backward on MFMA (gfx950, bf16 / fp16, head_dim 64 or 128).
+//
+// Reference semantics: paddle/phi/kernels/gpu/flash_attn_kernel.cu, flash_attn_grad_kernel.cu
+// (python/paddle/nn/functional/flash_attention.py): layout [batch, seq, heads, head_dim] (BSHD),
+// causal mask aligned bottom-right (key <= query + Sk - Sq), GQA (Hq % Hk == 0), softmax_lse
+// saved as fp32 [B, Hq, Sq] for the backward.
+//
+// CDNA4 design (not a translation of the CUDA kernel):
+//  * 64-wide waves, v_mfma_f32_16x16x32_{bf16,f16}.  Forward uses the *swapped* product
+//    S^T = K·Q^T so a lane owns one query row (query = lane & 15) in every accumulator:
+//    row max / row sum need only 2 cross-lane shuffles and the rescale of O is lane-local.
+//    P stays in registers and feeds P·V directly as the MFMA B operand (K-permutation trick:
+//    element j of lane group g is key 4g+j / 16+4g+j-4, matched by the V operand).
+//  * V is consumed column-wise with ds_read_b64_tr_b16 (hardware transposed LDS read), so V
+//    is staged row-major exactly as it sits in HBM.
+//  * K/V tiles XOR-swizzled in LDS (16-byte chunk ^ f(row)) → conflict-free ds_read_b128 and
+//    tr reads; register-staged prefetch of tile t+1 is issued before computing tile t.
+//  * Backward = dK/dV kernel (keys stationary per wave, non-swapped products) + dQ kernel
+//    (queries stationary, swapped products).  No float atomics: dQ is deterministic.
+//  * Strided q/k/v/o (element strides for batch/seq/head) so q, k, v can be slices of a fused
+//    QKV projection with no copies.
+#include "common.h"
+
+namespace pa {
+namespace fa {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+template <typename T> struct Mfma;
+template <> struct Mfma<bf16_t> {
+  static __device__ __forceinline__ f32x4 run(s16x8 a, s16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mfma<f16_t> {
+  static __device__ __forceinline__ f32x4 run(s16x8 a, s16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  }
+};
+
+template <typename T>
+__device__ __forceinline__ short f2s(float v) {
+  return __builtin_bit_cast(short, from_f<T>(v));
+}
+
+// 16-byte-chunk swizzles (see header comment). D=128 → 256-B rows, D=64 → 128-B rows.
+template <int D> __device__ __forceinline__ int swz_b128(int row) { return D == 128 ? (row & 15) : ((row >> 1) & 7); }
+template <int D> __device__ __forceinline__ int swz_tr(int row) { return D == 128 ? ((row & 7) << 1) : (((row >> 1) & 3) << 1); }
+
+// LDS byte offset of 16-byte chunk `ch` of row `row` in a [rows][D] 16-bit tile.
+template <int D, bool TR>
+__device__ __forceinline__ int lds_off(int row, int ch) {
+  return row * (D * 2) + ((ch ^ (TR ? swz_tr<D>(row) : swz_b128<D>(row))) << 4);
+}
+
+// Stage helpers: a [64][D] tile of 16-bit elements, 256 threads, NLD 16-byte chunks per thread.
+template <int D>
+struct Tile {
+  static constexpr int CH = D / 8;               // 16-byte chunks per row
+  static constexpr int NLD = 64 * CH / 256;      // chunks per thread
+  uint4 r[NLD];
+  __device__ __forceinline__ void load(const uint16_t* base, long long row_stride, int row0, int nrows) {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int row = c / CH, ch = c % CH;
+      if (row0 + row < nrows)
+        r[i] = *reinterpret_cast<const uint4*>(base + (long long)(row0 + row) * row_stride + ch * 8);
+      else
+        r[i] = make_uint4(0, 0, 0, 0);
+    }
+  }
+  template <bool TR>
+  __device__ __forceinline__ void store(char* lds) const {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int row = c / CH, ch = c % CH;
+      *reinterpret_cast<uint4*>(lds + lds_off<D, TR>(row, ch)) = r[i];
+    }
+  }
+};
+
+// A/B operand read: row `row`, d-range [32ks + 8g, +8) → 8 x 16-bit
+template <int D, bool TR>
+__device__ __forceinline__ s16x8 ld_row8(const char* lds, int row, int ks, int g) {
+  return *reinterpret_cast<const s16x8*>(lds + lds_off<D, TR>(row, 4 * ks + g));
+}
+
+// Transposed operand: lane (16g + i) gets column (16db + i) of rows {r0+4g+q} (elements 0..3) and
+// {r0+16+4g+q} (elements 4..7).  Lane 16g+4q+p supplies the address of row r0+4g+q, col 16db+4p.
+template <int D, bool TR>
+__device__ __forceinline__ s16x8 ld_tr8(const char* lds, int r0, int db, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int ch = 2 * db + (p >> 1);
+  const int byte_in = (p & 1) * 8;
+  const int rowa = r0 + 4 * g + q, rowb = rowa + 16;
+  typedef __attribute__((address_space(3))) s16x4 lds_v4;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(lds + lds_off<D, TR>(rowa, ch) + byte_in));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(lds + lds_off<D, TR>(rowb, ch) + byte_in));
+  s16x8 r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
+struct Strides {
+  long long b, s, h;
+};
+
+// ============================================================================ forward
+// grid: (ceil(Sq/128), Hq, B), block 256 (4 waves x 32 query rows = 2 tiles of 16)
+template <typename T, int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+                                                     const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
+                                                     float* __restrict__ LSE, int Sq, int Sk, int Hq, int Hk,
+                                                     Strides qs, Strides ks_, Strides vs, Strides os, float scale_log2) {
+  constexpr int KS = D / 32;   // k-steps over head_dim
+  constexpr int DB = D / 16;   // 16-wide d blocks
+  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * D * 2];
+  char* k_lds = smem;
+  char* v_lds = smem + 64 * D * 2;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int g = lane >> 4;
+  const int nqb = (Sq + 127) / 128;
+  const int qb = nqb - 1 - (int)blockIdx.x;  // heavy (late, causal) blocks first
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int hk = h / (Hq / Hk);
+  const int q0 = qb * 128;
+  const int qw0 = q0 + wave * 32;
+  const int off = Sk - Sq;  // bottom-right causal alignment
+
+  const uint16_t* qbase = Q + b * qs.b + h * qs.h;
+  const uint16_t* kbase = K + b * ks_.b + hk * ks_.h;
+  const uint16_t* vbase = V + b * vs.b + hk * vs.h;
+
+  // Q fragments (B operand of S^T = K Q^T): lane holds Q[qw0 + 16t + (lane&15)][32ks + 8g .. +8]
+  s16x8 qf[2][KS];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int q = qw0 + 16 * t + (lane & 15);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      if (q < Sq)
+        qf[t][k] = *reinterpret_cast<const s16x8*>(qbase + (long long)q * qs.s + 32 * k + 8 * g);
+      else
+        qf[t][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+
+  f32x4 acc_o[2][DB];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int d = 0; d < DB; ++d) acc_o[t][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run[2] = {-INFINITY, -INFINITY};
+  float l_run[2] = {0.f, 0.f};
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + 128 + off);
+  const int nkb = kend > 0 ? (kend + 63) / 64 : 0;
+
+  Tile<D> kt, vt;
+  if (nkb > 0) {
+    kt.load(kbase, ks_.s, 0, Sk);
+    vt.load(vbase, vs.s, 0, Sk);
+  }
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * 64;
+    __syncthreads();
+    kt.template store<false>(k_lds);
+    vt.template store<true>(v_lds);
+    __syncthreads();
+    if (kb + 1 < nkb) {
+      kt.load(kbase, ks_.s, k0 + 64, Sk);
+      vt.load(vbase, vs.s, k0 + 64, Sk);
+    }
+    // wave-uniform skip of key blocks fully above this wave's diagonal
+    if (CAUSAL && k0 > qw0 + 31 + off) continue;
+
+    // S^T = K Q^T : acc_s[t][kbk] holds S^T[key 16kbk + 4g + r][query 16t + (lane&15)]
+    f32x4 acc_s[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc_s[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const s16x8 kf = ld_row8<D, false>(k_lds, 16 * j + (lane & 15), k, g);
+        acc_s[0][j] = Mfma<T>::run(kf, qf[0][k], acc_s[0][j]);
+        acc_s[1][j] = Mfma<T>::run(kf, qf[1][k], acc_s[1][j]);
+      }
+    }
+    // online softmax (log2 domain), per tile
+    s16x8 pf[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int q = qw0 + 16 * t + (lane & 15);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 16 * j + 4 * g + r;
+          float s = acc_s[t][j][r] * scale_log2;
+          const bool masked = (key >= Sk) || (CAUSAL && key > q + off);
+          s = masked ? -INFINITY : s;
+          acc_s[t][j][r] = s;
+          mx = fmaxf(mx, s);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run[t], mx);
+      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+      const float alpha = exp2f(m_run[t] - m_use);
+      m_run[t] = m_new;
+      float ls = 0.f;
+      float p[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          p[j][r] = exp2f(acc_s[t][j][r] - m_use);
+          ls += p[j][r];
+        }
+      l_run[t] = l_run[t] * alpha + ls;
+#pragma unroll
+      for (int d = 0; d < DB; ++d) acc_o[t][d] *= alpha;
+      // P^T as B operand: k-step s covers keys 32s..32s+31; element j<4 → (16*(2s)+4g+j), j>=4 → (16*(2s+1)+4g+j-4)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pf[t][s][r] = f2s<T>(p[2 * s][r]);
+          pf[t][s][4 + r] = f2s<T>(p[2 * s + 1][r]);
+        }
+      }
+    }
+    // O^T += V^T P^T
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const s16x8 vf = ld_tr8<D, true>(v_lds, 32 * s, d, lane);
+        acc_o[0][d] = Mfma<T>::run(vf, pf[0][s], acc_o[0][d]);
+        acc_o[1][d] = Mfma<T>::run(vf, pf[1][s], acc_o[1][d]);
+      }
+    }
+  }
+  // epilogue: O = acc / l ; lane holds O[query][16d + 4g + r]
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    float l = l_run[t];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int q = qw0 + 16 * t + (lane & 15);
+    if (q < Sq) {
+      uint16_t* orow = O + b * os.b + h * os.h + (long long)q * os.s;
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        s16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2s<T>(acc_o[t][d][r] * inv);
+        *reinterpret_cast<s16x4*>(orow + 16 * d + 4 * g) = o;
+      }
+      if (g == 0) {
+        const float mm = (m_run[t] == -INFINITY) ? 0.f : m_run[t];
+        LSE[((long long)b * Hq + h) * Sq + q] = l > 0.f ? (mm + log2f(l)) * kLn2 : -INFINITY;
+      }
+    }
+  }
+}
+
+// ============================================================================ backward
+// delta[b, h, q] = sum_d dO[q, d] * O[q, d]   (one 16-lane group per row)
+template <typename T, int D>
+__global__ __launch_bounds__(256) void bwd_delta_kernel(const uint16_t* __restrict__ dO, const uint16_t* __restrict__ O,
+                                                        float* __restrict__ delta, int B, int Sq, int Hq, Strides dos,
+                                                        Strides os) {
+  const int rid = blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int sub = threadIdx.x & 15;
+  const long long nrows = (long long)B * Hq * Sq;
+  if (rid >= nrows) return;
+  const int q = rid % Sq;
+  const int h = (rid / Sq) % Hq;
+  const int b = rid / (Sq * Hq);
+  const uint16_t* dp = dO + b * dos.b + h * dos.h + (long long)q * dos.s;
+  const uint16_t* op = O + b * os.b + h * os.h + (long long)q * os.s;
+  float s = 0.f;
+  for (int j = sub * 8; j < D; j += 128) {
+    float a[8], c[8];
+    load_f<T, 8>((const T*)(dp + j), a);
+    load_f<T, 8>((const T*)(op + j), c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += a[e] * c[e];
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
+  if (sub == 0) delta[rid] = s;
+}
+
+// dK/dV: grid (ceil(Sk/64), Hq, B); 4 waves x 16 keys; loop over 64-query blocks.
+// dK/dV are written per q-head ([B, Sk, Hq, D] strides given by dks/dvs); GQA sums outside.
+template <typename T, int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
+    uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq, int Sk, int Hq, int Hk, Strides qs, Strides ks_,
+    Strides vs, Strides dos, Strides dks, Strides dvs, float scale) {
+  constexpr int KS = D / 32;
+  constexpr int DB = D / 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * D * 2 + 2 * 64 * 4];
+  char* q_lds = smem;
+  char* do_lds = smem + 64 * D * 2;
+  float* lse_lds = reinterpret_cast<float*>(smem + 2 * 64 * D * 2);
+  float* dl_lds = lse_lds + 64;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int g = lane >> 4;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int hk = h / (Hq / Hk);
+  const int k0 = blockIdx.x * 64;
+  const int kw = k0 + wave * 16;
+  const int mykey = kw + (lane & 15);
+  const int off = Sk - Sq;
+  const float scale_log2 = scale * kLog2e;
+
+  const uint16_t* qbase = Q + b * qs.b + h * qs.h;
+  const uint16_t* dobase = dO + b * dos.b + h * dos.h;
+  // K, V of this wave's 16 keys as B operands: lane holds K[key][32ks + 8g .. +8]
+  s16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    if (mykey < Sk) {
+      kf[k] = *reinterpret_cast<const s16x8*>(K + b * ks_.b + hk * ks_.h + (long long)mykey * ks_.s + 32 * k + 8 * g);
+      vf[k] = *reinterpret_cast<const s16x8*>(V + b * vs.b + hk * vs.h + (long long)mykey * vs.s + 32 * k + 8 * g);
+    } else {
+      kf[k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      vf[k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  f32x4 acc_dk[DB], acc_dv[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d) {
+    acc_dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc_dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  int qstart = 0;
+  if (CAUSAL) qstart = max(0, (k0 - off) / 64 * 64);
+  const int nqb = (Sq - qstart + 63) / 64;
+  const float* lse_b = LSE + ((long long)b * Hq + h) * Sq;
+  const float* dl_b = Delta + ((long long)b * Hq + h) * Sq;
+
+  Tile<D> qt, dot;
+  if (nqb > 0) {
+    qt.load(qbase, qs.s, qstart, Sq);
+    dot.load(dobase, dos.s, qstart, Sq);
+  }
+  for (int i = 0; i < nqb; ++i) {
+    const int q0 = qstart + i * 64;
+    __syncthreads();
+    qt.template store<false>(q_lds);
+    dot.template store<false>(do_lds);
+    if (threadIdx.x < 64) {
+      const int q = q0 + threadIdx.x;
+      lse_lds[threadIdx.x] = q < Sq ? lse_b[q] * kLog2e : INFINITY;
+      dl_lds[threadIdx.x] = q < Sq ? dl_b[q] : 0.f;
+    }
+    __syncthreads();
+    if (i + 1 < nqb) {
+      qt.load(qbase, qs.s, q0 + 64, Sq);
+      dot.load(dobase, dos.s, q0 + 64, Sq);
+    }
+    if (CAUSAL && q0 + 63 + off < kw) continue;  // whole query block above this wave's keys
+
+    // S = Q K^T, dP = dO V^T : acc[m] holds [query 16m + 4g + r][key lane&15]
+    f32x4 acc_s[4], acc_dp[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      acc_s[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc_dp[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const s16x8 qa = ld_row8<D, false>(q_lds, 16 * m + (lane & 15), k, g);
+        acc_s[m] = Mfma<T>::run(qa, kf[k], acc_s[m]);
+        const s16x8 da = ld_row8<D, false>(do_lds, 16 * m + (lane & 15), k, g);
+        acc_dp[m] = Mfma<T>::run(da, vf[k], acc_dp[m]);
+      }
+    }
+    // P and dS, packed as B operands (k = query, permuted as in the forward)
+    s16x8 pb[2], db_[2];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = 16 * m + 4 * g + r;
+        const int q = q0 + ql;
+        const bool masked = (q >= Sq) || (mykey >= Sk) || (CAUSAL && mykey > q + off);
+        const float p = masked ? 0.f : exp2f(acc_s[m][r] * scale_log2 - lse_lds[ql]);
+        const float ds = p * (acc_dp[m][r] - dl_lds[ql]);
+        pb[m >> 1][(m & 1) * 4 + r] = f2s<T>(p);
+        db_[m >> 1][(m & 1) * 4 + r] = f2s<T>(ds);
+      }
+    }
+    // dV^T += dO^T P ;  dK^T += Q^T dS
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const s16x8 doa = ld_tr8<D, false>(do_lds, 32 * s, d, lane);
+        acc_dv[d] = Mfma<T>::run(doa, pb[s], acc_dv[d]);
+        const s16x8 qa = ld_tr8<D, false>(q_lds, 32 * s, d, lane);
+        acc_dk[d] = Mfma<T>::run(qa, db_[s], acc_dk[d]);
+      }
+    }
+  }
+  // epilogue: lane holds d[16d + 4g + r][key lane&15]
+  if (mykey < Sk) {
+    uint16_t* dkrow = dK + b * dks.b + h * dks.h + (long long)mykey * dks.s;
+    uint16_t* dvrow = dV + b * dvs.b + h * dvs.h + (long long)mykey * dvs.s;
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+      s16x4 a, c;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a[r] = f2s<T>(acc_dk[d][r] * scale);
+        c[r] = f2s<T>(acc_dv[d][r]);
+      }
+      *reinterpret_cast<s16x4*>(dkrow + 16 * d + 4 * g) = a;
+      *reinterpret_cast<s16x4*>(dvrow + 16 * d + 4 * g) = c;
+    }
+  }
+}
+
+// dQ: grid (ceil(Sq/64), Hq, B); 4 waves x 16 queries; loop over 64-key blocks (swapped products).
+template <typename T, int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void bwd_dq_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
+    uint16_t* __restrict__ dQ, int Sq, int Sk, int Hq, int Hk, Strides qs, Strides ks_, Strides vs, Strides dos,
+    Strides dqs, float scale) {
+  constexpr int KS = D / 32;
+  constexpr int DB = D / 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * D * 2];
+  char* k_lds = smem;
+  char* v_lds = smem + 64 * D * 2;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int g = lane >> 4;
+  const int nqb = (Sq + 63) / 64;
+  const int qb = nqb - 1 - (int)blockIdx.x;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int hk = h / (Hq / Hk);
+  const int q0 = qb * 64;
+  const int qw = q0 + wave * 16;
+  const int myq = qw + (lane & 15);
+  const int off = Sk - Sq;
+  const float scale_log2 = scale * kLog2e;
+
+  s16x8 qf[KS], dof[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    if (myq < Sq) {
+      qf[k] = *reinterpret_cast<const s16x8*>(Q + b * qs.b + h * qs.h + (long long)myq * qs.s + 32 * k + 8 * g);
+      dof[k] = *reinterpret_cast<const s16x8*>(dO + b * dos.b + h * dos.h + (long long)myq * dos.s + 32 * k + 8 * g);
+    } else {
+      qf[k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      dof[k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  const long long lrow = ((long long)b * Hq + h) * Sq;
+  const float lse2 = myq < Sq ? LSE[lrow + myq] * kLog2e : INFINITY;
+  const float dlt = myq < Sq ? Delta[lrow + myq] : 0.f;
+  f32x4 acc[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const uint16_t* kbase = K + b * ks_.b + hk * ks_.h;
+  const uint16_t* vbase = V + b * vs.b + hk * vs.h;
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + 64 + off);
+  const int nkb = kend > 0 ? (kend + 63) / 64 : 0;
+  Tile<D> kt, vt;
+  if (nkb > 0) {
+    kt.load(kbase, ks_.s, 0, Sk);
+    vt.load(vbase, vs.s, 0, Sk);
+  }
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * 64;
+    __syncthreads();
+    kt.template store<false>(k_lds);
+    vt.template store<false>(v_lds);
+    __syncthreads();
+    if (kb + 1 < nkb) {
+      kt.load(kbase, ks_.s, k0 + 64, Sk);
+      vt.load(vbase, vs.s, k0 + 64, Sk);
+    }
+    if (CAUSAL && k0 > qw + 15 + off) continue;
+    f32x4 acc_s[4], acc_dp[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc_s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc_dp[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const s16x8 ka = ld_row8<D, false>(k_lds, 16 * j + (lane & 15), k, g);
+        acc_s[j] = Mfma<T>::run(ka, qf[k], acc_s[j]);
+        const s16x8 va = ld_row8<D, false>(v_lds, 16 * j + (lane & 15), k, g);
+        acc_dp[j] = Mfma<T>::run(va, dof[k], acc_dp[j]);
+      }
+    }
+    s16x8 dsb[2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 16 * j + 4 * g + r;
+        const bool masked = (key >= Sk) || (myq >= Sq) || (CAUSAL && key > myq + off);
+        const float p = masked ? 0.f : exp2f(acc_s[j][r] * scale_log2 - lse2);
+        dsb[j >> 1][(j & 1) * 4 + r] = f2s<T>(p * (acc_dp[j][r] - dlt));
+      }
+    }
+    // dQ^T += K^T dS^T
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const s16x8 ka = ld_tr8<D, false>(k_lds, 32 * s, d, lane);
+        acc[d] = Mfma<T>::run(ka, dsb[s], acc[d]);
+      }
+    }
+  }
+  if (myq < Sq) {
+    uint16_t* row = dQ + b * dqs.b + h * dqs.h + (long long)myq * dqs.s;
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+      s16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = f2s<T>(acc[d][r] * scale);
+      *reinterpret_cast<s16x4*>(row + 16 * d + 4 * g) = o;
+    }
+  }
+}
+
+}  // namespace fa
+}  // namespace pa
+
+using namespace pa;
+using namespace pa::fa;
+
+#define FA_DISPATCH(dt, D, causal, ...)                                                            \
+  if (dt == 1 && D == 128 && causal) { using T = bf16_t; constexpr int DD = 128; constexpr bool CC = true; __VA_ARGS__; } \
+  else if (dt == 1 && D == 128 && !causal) { using T = bf16_t; constexpr int DD = 128; constexpr bool CC = false; __VA_ARGS__; } \
+  else if (dt == 1 && D == 64 && causal) { using T = bf16_t; constexpr int DD = 64; constexpr bool CC = true; __VA_ARGS__; } \
+  else if (dt == 1 && D == 64 && !causal) { using T = bf16_t; constexpr int DD = 64; constexpr bool CC = false; __VA_ARGS__; } \
+  else if (dt == 2 && D == 128 && causal) { using T = f16_t; constexpr int DD = 128; constexpr bool CC = true; __VA_ARGS__; } \
+  else if (dt == 2 && D == 128 && !causal) { using T = f16_t; constexpr int DD = 128; constexpr bool CC = false; __VA_ARGS__; } \
+  else if (dt == 2 && D == 64 && causal) { using T = f16_t; constexpr int DD = 64; constexpr bool CC = true; __VA_ARGS__; } \
+  else if (dt == 2 && D == 64 && !causal) { using T = f16_t; constexpr int DD = 64; constexpr bool CC = false; __VA_ARGS__; } \
+  else return hipErrorInvalidValue;
+
+// strides: [b, s, h] element strides for each tensor (head_dim stride must be 1)
+PA_API hipError_t pa_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int Sq, int Sk,
+                               int Hq, int Hk, int D, const long long* qst, const long long* kst, const long long* vst,
+                               const long long* ost, float scale, int causal, int dt, hipStream_t st) {
+  if (Hk <= 0 || Hq % Hk != 0) return hipErrorInvalidValue;
+  Strides qs{qst[0], qst[1], qst[2]}, ks{kst[0], kst[1], kst[2]}, vs{vst[0], vst[1], vst[2]}, os{ost[0], ost[1], ost[2]};
+  dim3 grid((Sq + 127) / 128, Hq, B);
+  FA_DISPATCH(dt, D, causal,
+              fwd_kernel<T, DD, CC><<<grid, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                                                          (uint16_t*)o, lse, Sq, Sk, Hq, Hk, qs, ks, vs, os,
+                                                          scale * kLog2e));
+  return hipGetLastError();
+}
+
+// dk/dv are per-q-head buffers (caller reduces over GQA groups when Hq != Hk).
+PA_API hipError_t pa_flash_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                               const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk,
+                               int Hq, int Hk, int D, const long long* qst, const long long* kst, const long long* vst,
+                               const long long* ost, const long long* dost, const long long* dqst,
+                               const long long* dkst, const long long* dvst, float scale, int causal, int dt,
+                               hipStream_t st) {
+  if (Hk <= 0 || Hq % Hk != 0) return hipErrorInvalidValue;
+  Strides qs{qst[0], qst[1], qst[2]}, ks{kst[0], kst[1], kst[2]}, vs{vst[0], vst[1], vst[2]},
+      os{ost[0], ost[1], ost[2]}, dos{dost[0], dost[1], dost[2]}, dqs{dqst[0], dqst[1], dqst[2]},
+      dks{dkst[0], dkst[1], dkst[2]}, dvs{dvst[0], dvst[1], dvst[2]};
+  const long long nrows = (long long)B * Hq * Sq;
+  FA_DISPATCH(dt, D, causal, {
+    bwd_delta_kernel<T, DD><<<(int)((nrows + 15) / 16), 256, 0, st>>>((const uint16_t*)dout, (const uint16_t*)o, delta,
+                                                                      B, Sq, Hq, dos, os);
+    dim3 g1((Sk + 63) / 64, Hq, B);
+    bwd_dkdv_kernel<T, DD, CC><<<g1, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                                                   (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv,
+                                                   Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs, scale);
+    dim3 g2((Sq + 63) / 64, Hq, B);
+    bwd_dq_kernel<T, DD, CC><<<g2, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                                                 (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk, Hq, Hk, qs,
+                                                 ks, vs, dos, dqs, scale);
+  });
+  return hipGetLastError();
+}

@@ -1,0 +1,269 @@
+"""paddle.nn.functional conv / pooling (reference: python/paddle/nn/functional/{conv,pooling}.py).
+
+Convolutions run on MIOpen through the storage layer (library path); channels-last
+(NHWC) input is kept channels-last in memory, which is MIOpen's fast layout on CDNA.
+"""
+import numpy as np
+import torch
+import torch.nn.functional as TF
+
+from ...core.tensor import Tensor, _wrap as _w, _unwrap as _u
+from ...tensor._helpers import _shape
+
+
+def _ntuple(v, n):
+    if isinstance(v, Tensor):
+        v = v.tolist()
+    if isinstance(v, (list, tuple)):
+        v = [int(e) for e in v]
+        return tuple(v) if len(v) == n else tuple(v * n if len(v) == 1 else v)
+    return (int(v),) * n
+
+
+def _same_pads(in_sz, k, s, d):
+    pads = []
+    for i, kk, ss, dd in zip(in_sz, k, s, d):
+        out = (i + ss - 1) // ss
+        tot = max((out - 1) * ss + (kk - 1) * dd + 1 - i, 0)
+        pads.append((tot // 2, tot - tot // 2))
+    return pads
+
+
+def _resolve_padding(padding, nd, in_sz=None, k=None, s=None, d=None):
+    """Return (torch_padding_tuple, extra_F_pad or None)."""
+    if isinstance(padding, str):
+        p = padding.upper()
+        if p == 'VALID':
+            return (0,) * nd, None
+        pads = _same_pads(in_sz, k, s, d)
+        if all(a == b for a, b in pads):
+            return tuple(a for a, _ in pads), None
+        flat = []
+        for a, b in reversed(pads):
+            flat += [a, b]
+        return (0,) * nd, flat
+    if isinstance(padding, (list, tuple)):
+        padding = [(_u(p).item() if isinstance(p, Tensor) else p) for p in padding]
+        if len(padding) == nd and all(isinstance(p, int) for p in padding):
+            return tuple(padding), None
+        if len(padding) == 2 * nd and all(isinstance(p, int) for p in padding):
+            pairs = [(padding[2 * i], padding[2 * i + 1]) for i in range(nd)]
+            if all(a == b for a, b in pairs):
+                return tuple(a for a, _ in pairs), None
+            flat = []
+            for a, b in reversed(pairs):
+                flat += [a, b]
+            return (0,) * nd, flat
+        if len(padding) == nd + 2:  # [[0,0],[0,0],[a,b],[c,d]] form
+            pairs = [tuple(p) for p in padding if isinstance(p, (list, tuple))]
+            pairs = pairs[2:] if len(pairs) == nd + 2 else pairs
+            if all(a == b for a, b in pairs):
+                return tuple(a for a, _ in pairs), None
+            flat = []
+            for a, b in reversed(pairs):
+                flat += [a, b]
+            return (0,) * nd, flat
+    return _ntuple(padding, nd), None
+
+
+def _conv(x, weight, bias, stride, padding, dilation, groups, data_format, nd, fn):
+    t, w = _u(x), _u(weight)
+    b = _u(bias) if bias is not None else None
+    cl = data_format[-1] == 'C'
+    if cl:
+        t = t.permute(0, nd + 1, *range(1, nd + 1))
+    s, d = _ntuple(stride, nd), _ntuple(dilation, nd)
+    p, extra = _resolve_padding(padding, nd, list(t.shape[2:]), list(w.shape[2:]), s, d)
+    if extra is not None:
+        t = TF.pad(t, extra)
+    out = fn(t, w, b, s, p, d, groups)
+    if cl:
+        out = out.permute(0, *range(2, nd + 2), 1)
+    return _w(out)
+
+
+def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format='NCL', name=None):
+    return _conv(x, weight, bias, stride, padding, dilation, groups, data_format, 1, TF.conv1d)
+
+
+def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format='NCHW', name=None):
+    return _conv(x, weight, bias, stride, padding, dilation, groups, data_format, 2, TF.conv2d)
+
+
+def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format='NCDHW', name=None):
+    return _conv(x, weight, bias, stride, padding, dilation, groups, data_format, 3, TF.conv3d)
+
+
+def _conv_t(x, weight, bias, stride, padding, output_padding, dilation, groups, output_size, data_format, nd, fn):
+    t, w = _u(x), _u(weight)
+    b = _u(bias) if bias is not None else None
+    cl = data_format[-1] == 'C'
+    if cl:
+        t = t.permute(0, nd + 1, *range(1, nd + 1))
+    s, d = _ntuple(stride, nd), _ntuple(dilation, nd)
+    if isinstance(padding, str):
+        p = (0,) * nd if padding.upper() == 'VALID' else tuple(((w.shape[2 + i] - 1) * d[i]) // 2 for i in range(nd))
+    else:
+        p, _ = _resolve_padding(padding, nd)
+    op = _ntuple(output_padding, nd)
+    if output_size is not None:
+        osz = _ntuple(output_size, nd) if not isinstance(output_size, int) else (output_size,) * nd
+        op = tuple(osz[i] - ((t.shape[2 + i] - 1) * s[i] - 2 * p[i] + d[i] * (w.shape[2 + i] - 1) + 1) for i in range(nd))
+    out = fn(t, w, b, s, p, op, groups, d)
+    if cl:
+        out = out.permute(0, *range(2, nd + 2), 1)
+    return _w(out)
+
+
+def conv1d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1,
+                     output_size=None, data_format='NCL', name=None):
+    return _conv_t(x, weight, bias, stride, padding, output_padding, dilation, groups, output_size, data_format, 1,
+                   TF.conv_transpose1d)
+
+
+def conv2d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, dilation=1, groups=1,
+                     output_size=None, data_format='NCHW', name=None):
+    return _conv_t(x, weight, bias, stride, padding, output_padding, dilation, groups, output_size, data_format, 2,
+                   TF.conv_transpose2d)
+
+
+def conv3d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1,
+                     output_size=None, data_format='NCDHW', name=None):
+    return _conv_t(x, weight, bias, stride, padding, output_padding, dilation, groups, output_size, data_format, 3,
+                   TF.conv_transpose3d)
+
+
+# ----------------------------------------------------------------------------- pooling
+def _pool(x, kernel_size, stride, padding, ceil_mode, data_format, nd, fn, extra=None, return_mask=False):
+    t = _u(x)
+    cl = data_format[-1] == 'C'
+    if cl:
+        t = t.permute(0, nd + 1, *range(1, nd + 1))
+    k = _ntuple(kernel_size, nd)
+    s = k if stride is None else _ntuple(stride, nd)
+    p, pre = _resolve_padding(padding, nd, list(t.shape[2:]), k, s, (1,) * nd)
+    if pre is not None:
+        t = TF.pad(t, pre, value=float('-inf') if fn in (TF.max_pool1d, TF.max_pool2d, TF.max_pool3d) else 0.0)
+    kw = dict(extra or {})
+    if return_mask:
+        out, mask = fn(t, k, s, p, ceil_mode=ceil_mode, return_indices=True, **kw)
+        if cl:
+            out = out.permute(0, *range(2, nd + 2), 1)
+            mask = mask.permute(0, *range(2, nd + 2), 1)
+        return _w(out), _w(mask)
+    out = fn(t, k, s, p, ceil_mode=ceil_mode, **kw)
+    if cl:
+        out = out.permute(0, *range(2, nd + 2), 1)
+    return _w(out)
+
+
+def max_pool1d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False, name=None):
+    return _pool(x, kernel_size, stride, padding, ceil_mode, 'NCL', 1, TF.max_pool1d, return_mask=return_mask)
+
+
+def max_pool2d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False, data_format='NCHW',
+               name=None):
+    return _pool(x, kernel_size, stride, padding, ceil_mode, data_format, 2, TF.max_pool2d, return_mask=return_mask)
+
+
+def max_pool3d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False, data_format='NCDHW',
+               name=None):
+    return _pool(x, kernel_size, stride, padding, ceil_mode, data_format, 3, TF.max_pool3d, return_mask=return_mask)
+
+
+def avg_pool1d(x, kernel_size, stride=None, padding=0, exclusive=True, ceil_mode=False, name=None):
+    return _pool(x, kernel_size, stride, padding, ceil_mode, 'NCL', 1, TF.avg_pool1d,
+                 {'count_include_pad': not exclusive})
+
+
+def avg_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False, exclusive=True, divisor_override=None,
+               data_format='NCHW', name=None):
+    return _pool(x, kernel_size, stride, padding, ceil_mode, data_format, 2, TF.avg_pool2d,
+                 {'count_include_pad': not exclusive, 'divisor_override': divisor_override})
+
+
+def avg_pool3d(x, kernel_size, stride=None, padding=0, ceil_mode=False, exclusive=True, divisor_override=None,
+               data_format='NCDHW', name=None):
+    return _pool(x, kernel_size, stride, padding, ceil_mode, data_format, 3, TF.avg_pool3d,
+                 {'count_include_pad': not exclusive, 'divisor_override': divisor_override})
+
+
+def lp_pool1d(x, norm_type, kernel_size, stride=None, ceil_mode=False, data_format='NCL', name=None):
+    return _w(TF.lp_pool1d(_u(x), norm_type, kernel_size, stride, ceil_mode))
+
+
+def lp_pool2d(x, norm_type, kernel_size, stride=None, ceil_mode=False, data_format='NCHW', name=None):
+    return _w(TF.lp_pool2d(_u(x), norm_type, kernel_size, stride, ceil_mode))
+
+
+def _adaptive(x, output_size, data_format, nd, fn, return_mask=False):
+    t = _u(x)
+    cl = data_format[-1] == 'C'
+    if cl:
+        t = t.permute(0, nd + 1, *range(1, nd + 1))
+    if isinstance(output_size, (list, tuple)):
+        output_size = tuple(t.shape[2 + i] if o is None else int(o) for i, o in enumerate(output_size))
+    if return_mask:
+        out, m = fn(t, output_size, return_indices=True)
+        if cl:
+            out, m = out.permute(0, *range(2, nd + 2), 1), m.permute(0, *range(2, nd + 2), 1)
+        return _w(out), _w(m)
+    out = fn(t, output_size)
+    if cl:
+        out = out.permute(0, *range(2, nd + 2), 1)
+    return _w(out)
+
+
+def adaptive_avg_pool1d(x, output_size, name=None):
+    return _adaptive(x, output_size, 'NCL', 1, TF.adaptive_avg_pool1d)
+
+
+def adaptive_avg_pool2d(x, output_size, data_format='NCHW', name=None):
+    return _adaptive(x, output_size, data_format, 2, TF.adaptive_avg_pool2d)
+
+
+def adaptive_avg_pool3d(x, output_size, data_format='NCDHW', name=None):
+    return _adaptive(x, output_size, data_format, 3, TF.adaptive_avg_pool3d)
+
+
+def adaptive_max_pool1d(x, output_size, return_mask=False, name=None):
+    return _adaptive(x, output_size, 'NCL', 1, TF.adaptive_max_pool1d, return_mask)
+
+
+def adaptive_max_pool2d(x, output_size, return_mask=False, name=None):
+    return _adaptive(x, output_size, 'NCHW', 2, TF.adaptive_max_pool2d, return_mask)
+
+
+def adaptive_max_pool3d(x, output_size, return_mask=False, name=None):
+    return _adaptive(x, output_size, 'NCDHW', 3, TF.adaptive_max_pool3d, return_mask)
+
+
+def _unpool(x, indices, kernel_size, stride, padding, output_size, nd, fn, data_format):
+    k = _ntuple(kernel_size, nd)
+    s = k if stride is None else _ntuple(stride, nd)
+    p = _ntuple(padding, nd)
+    return _w(fn(_u(x), _u(indices), k, s, p, output_size))
+
+
+def max_unpool1d(x, indices, kernel_size, stride=None, padding=0, data_format='NCL', output_size=None, name=None):
+    return _unpool(x, indices, kernel_size, stride, padding, output_size, 1, TF.max_unpool1d, data_format)
+
+
+def max_unpool2d(x, indices, kernel_size, stride=None, padding=0, data_format='NCHW', output_size=None, name=None):
+    return _unpool(x, indices, kernel_size, stride, padding, output_size, 2, TF.max_unpool2d, data_format)
+
+
+def max_unpool3d(x, indices, kernel_size, stride=None, padding=0, data_format='NCDHW', output_size=None, name=None):
+    return _unpool(x, indices, kernel_size, stride, padding, output_size, 3, TF.max_unpool3d, data_format)
+
+
+def fractional_max_pool2d(x, output_size, kernel_size=None, random_u=None, return_mask=False, name=None):
+    k = kernel_size or 2
+    r = TF.fractional_max_pool2d(_u(x), k, output_size=output_size, return_indices=return_mask)
+    return (_w(r[0]), _w(r[1])) if return_mask else _w(r)
+
+
+def fractional_max_pool3d(x, output_size, kernel_size=None, random_u=None, return_mask=False, name=None):
+    k = kernel_size or 2
+    r = TF.fractional_max_pool3d(_u(x), k, output_size=output_size, return_indices=return_mask)
+    return (_w(r[0]), _w(r[1])) if return_mask else _w(r)

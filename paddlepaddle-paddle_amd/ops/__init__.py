@@ -1,0 +1,37 @@
+"""Hand-written HIP/CDNA4 operator library (python side).
+
+``use_hip(t)`` decides whether a tensor takes the native kernel path: it is True for every
+tensor on the GPU.  If the kernel library is missing on a GPU process it raises instead of
+silently falling back (``PADDLE_AMD_DISABLE_HIP_KERNELS=1`` opts out explicitly, for A/B).
+"""
+import os
+
+import torch
+
+from . import _native
+
+_disabled = os.environ.get('PADDLE_AMD_DISABLE_HIP_KERNELS', '0') == '1'
+
+
+def enabled():
+    return not _disabled
+
+
+def set_enabled(v):
+    global _disabled
+    _disabled = not v
+
+
+def use_hip(t):
+    if _disabled or not isinstance(t, torch.Tensor) or t.device.type != 'cuda':
+        return False
+    if _native.lib is None and _native._load() is None:
+        raise RuntimeError("paddle_amd HIP kernel library not available on a GPU process: " + str(_native.load_error))
+    return True
+
+
+def native_loaded():
+    return _native.lib is not None
+
+
+from . import norm, softmax, act, xent, embedding, rope, optim, flash_attn, gemm  # noqa: E402,F401

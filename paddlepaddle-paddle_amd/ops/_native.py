@@ -1,0 +1,98 @@
+"""ctypes binding of ``_lib/libpaddle_amd_kernels.so`` (the hand-written HIP kernel library).
+
+Every launcher takes raw device pointers and the caller's current HIP stream, so the
+kernels interleave correctly with the storage layer's own work and can be captured into
+hipGraphs.  A failed launch raises immediately (the hipError_t is checked per call).
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_HERE, '_lib', 'libpaddle_amd_kernels.so')
+
+lib = None
+load_error = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+LL = ctypes.c_longlong
+F = ctypes.c_float
+U32 = ctypes.c_uint32
+LLP = ctypes.POINTER(ctypes.c_longlong)
+
+_SIGS = {
+    'pa_layernorm_fwd': [P, P, P, P, P, P, P, P, I, I, F, I, I, P],
+    'pa_rmsnorm_fwd': [P, P, P, P, P, P, I, I, F, I, I, P],
+    'pa_layernorm_bwd': [P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
+    'pa_rmsnorm_bwd': [P, P, P, P, P, P, P, P, I, I, I, I, P],
+    'pa_norm_bwd_nparts': [I],
+    'pa_softmax_fwd': [P, P, I, I, I, I, P],
+    'pa_softmax_bwd': [P, P, P, I, I, I, P],
+    'pa_xent_fwd': [P, P, P, P, I, I, LL, I, P],
+    'pa_xent_bwd': [P, P, P, P, I, P, I, I, LL, I, P],
+    'pa_bias_act': [I, I, P, P, P, P, LL, I, I, P],
+    'pa_swiglu_fwd': [P, P, P, LL, I, I, I, P],
+    'pa_swiglu_bwd': [P, P, P, P, P, LL, I, I, I, P],
+    'pa_dropout_add_fwd': [P, P, P, LL, F, U32, U32, I, P],
+    'pa_dropout_bwd': [P, P, LL, F, U32, U32, I, P],
+    'pa_embedding_fwd': [P, P, P, I, I, LL, I, P],
+    'pa_embedding_bwd': [P, P, P, P, I, I, LL, I, I, P],
+    'pa_rope': [P, P, P, P, P, I, I, I, I, I, F, I, P],
+    'pa_adamw': [P, P, P, P, P, LL, P, F, F, F, F, F, F, F, P, I, I, P],
+    'pa_sumsq': [P, LL, P, I, P],
+    'pa_sumsq_parts': [],
+    'pa_flash_fwd': [P, P, P, P, P, I, I, I, I, I, I, LLP, LLP, LLP, LLP, F, I, I, P],
+    'pa_flash_bwd': [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, LLP, LLP, LLP, LLP, LLP, LLP, LLP, LLP, F, I, I,
+                     P],
+}
+
+
+def _load():
+    global lib, load_error
+    if lib is not None:
+        return lib
+    if not os.path.exists(LIB_PATH):
+        load_error = f"{LIB_PATH} not built (run __graft_entry__.build() or python paddlepaddle-paddle_amd/_build.py)"
+        return None
+    try:
+        l = ctypes.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            fn = getattr(l, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        lib = l
+    except OSError as e:  # pragma: no cover
+        load_error = str(e)
+    return lib
+
+
+def check(err, name):
+    if err != 0:
+        raise RuntimeError(f"HIP kernel launch {name} failed with hipError_t={err}")
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def dtcode(dt):
+    if dt == torch.float32:
+        return 0
+    if dt == torch.bfloat16:
+        return 1
+    if dt == torch.float16:
+        return 2
+    raise TypeError(f"unsupported dtype for HIP kernel: {dt}")
+
+
+def strides3(t):
+    """(batch, seq, head) element strides of a [B, S, H, D] tensor with unit D stride."""
+    s = t.stride()
+    arr = (ctypes.c_longlong * 3)(s[0], s[1], s[2])
+    return arr

@@ -1,0 +1,26 @@
+"""Fused AdamW over flat buffers on csrc/embed_rope_optim.hip.
+
+Reference: paddle/phi/kernels/gpu/adamw_kernel.cu (multi_precision: fp32 master weight,
+low-precision model copy written in the same pass).  One launch updates an entire flat
+parameter shard: master (fp32), m, v, and the bf16 model parameters.
+"""
+import torch
+
+from . import _native as N
+
+
+def adamw_flat(master, grad, m, v, lowp, lr, beta1, beta2, eps, weight_decay, beta1_pow, beta2_pow, lr_tensor=None,
+               grad_scale=None):
+    n = master.numel()
+    assert grad.numel() == n and m.numel() == n and v.numel() == n
+    pd = -1 if lowp is None else N.dtcode(lowp.dtype)
+    N.check(N.lib.pa_adamw(N.ptr(master), N.ptr(grad), N.ptr(m), N.ptr(v), N.ptr(lowp), n, N.ptr(lr_tensor),
+                           float(lr), beta1, beta2, eps, weight_decay, float(beta1_pow), float(beta2_pow),
+                           N.ptr(grad_scale), N.dtcode(grad.dtype), pd, N.stream()), 'adamw')
+
+
+def sumsq(x):
+    """Sum of squares of a flat buffer as a 0-d fp32 tensor (two-stage, deterministic)."""
+    parts = torch.empty(N.lib.pa_sumsq_parts(), dtype=torch.float32, device=x.device)
+    N.check(N.lib.pa_sumsq(N.ptr(x), x.numel(), N.ptr(parts), N.dtcode(x.dtype), N.stream()), 'sumsq')
+    return parts.sum()

@@ -1,0 +1,92 @@
+"""Flat parameter / gradient buffers — the memory layout every MI355X engine here builds on.
+
+A ``FlatBuffer`` re-homes a list of parameters into ONE contiguous device buffer per
+dtype (parameters become views at fixed offsets; values and leaf-ness are preserved) and
+gives their gradients the same treatment (``p.grad`` is a view into one flat gradient
+buffer, so autograd accumulates in place).  Consequences:
+
+* the optimizer update is ONE fused kernel over the whole buffer (``ops.optim.adamw_flat``)
+* data-parallel gradient all-reduce / sharding reduce-scatter operate on contiguous
+  slices of the flat gradient buffer — no pack/unpack copies, bucket = slice
+* sharding stage 1/2/3 partitions are slices of the same buffer (rank r owns
+  ``[r*shard, (r+1)*shard)``), padded so every shard is 16-byte aligned and equal sized.
+
+Reference analogue: paddle/fluid/pybind (coalesce_tensor op / FusedAllReduce),
+python/paddle/distributed/fleet/meta_parallel/sharding/group_sharded_storage.py.
+"""
+import torch
+
+ALIGN = 64  # elements; keeps every param view 128-byte aligned for bf16
+
+
+def _align(n, a=ALIGN):
+    return (n + a - 1) // a * a
+
+
+class FlatBuffer:
+    def __init__(self, params, dtype=None, device=None, pad_to_multiple=1, grad_dtype=None):
+        """params: list of paddle Parameters (all the same dtype unless ``dtype`` is given)."""
+        self.params = list(params)
+        assert self.params, "FlatBuffer needs at least one parameter"
+        t0 = self.params[0]._t
+        self.dtype = dtype or t0.dtype
+        self.grad_dtype = grad_dtype or self.dtype
+        self.device = device or t0.device
+        self.offsets = []
+        off = 0
+        for p in self.params:
+            self.offsets.append(off)
+            off += _align(p._t.numel())
+        total = _align(off, ALIGN * pad_to_multiple)
+        self.numel = total
+        self.data = torch.zeros(total, dtype=self.dtype, device=self.device)
+        self.grad = torch.zeros(total, dtype=self.grad_dtype, device=self.device)
+        with torch.no_grad():
+            for p, o in zip(self.params, self.offsets):
+                n = p._t.numel()
+                view = self.data[o:o + n].view(p._t.shape)
+                view.copy_(p._t.detach())
+                req = p._t.requires_grad
+                p._t.data = view
+                if req:
+                    p._t.requires_grad_(True)
+                p.__dict__['_flat'] = (self, o)
+        self.attach_grads()
+
+    def attach_grads(self):
+        for p, o in zip(self.params, self.offsets):
+            if p._t.requires_grad:
+                n = p._t.numel()
+                p._t.grad = self.grad[o:o + n].view(p._t.shape)
+
+    def grads_attached(self):
+        for p, o in zip(self.params, self.offsets):
+            g = p._t.grad
+            if p._t.requires_grad and (g is None or g.data_ptr() != self.grad[o:o + 1].data_ptr()):
+                return False
+        return True
+
+    def sync_grads(self):
+        """Re-home any gradient autograd allocated outside the flat buffer (e.g. after
+        clear_grad(set_to_zero=False)); returns True when a copy was needed."""
+        copied = False
+        for p, o in zip(self.params, self.offsets):
+            g = p._t.grad
+            n = p._t.numel()
+            slot = self.grad[o:o + n]
+            if g is None:
+                if p._t.requires_grad:
+                    slot.zero_()
+                    p._t.grad = slot.view(p._t.shape)
+                continue
+            if g.data_ptr() != slot.data_ptr():
+                slot.copy_(g.reshape(-1))
+                p._t.grad = slot.view(p._t.shape)
+                copied = True
+        return copied
+
+    def data_intact(self):
+        return all(p._t.data_ptr() == self.data[o:o + 1].data_ptr() for p, o in zip(self.params, self.offsets))
+
+    def zero_grad(self):
+        self.grad.zero_()
