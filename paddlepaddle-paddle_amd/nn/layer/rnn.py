@@ -194,9 +194,11 @@ class _RNNBase(Layer):
             x = torch.nn.utils.rnn.pack_padded_sequence(x, lens, batch_first=batch_first, enforce_sorted=False)
         mod = {'LSTM': torch.nn.LSTM, 'GRU': torch.nn.GRU}.get(self._mode)
         if self._mode == 'LSTM':
-            out, (h, c) = torch._VF.lstm(x, initial_states, weights, True, self.num_layers, self.dropout,
-                                         self.training, bidir, batch_first) if sequence_length is None else \
-                _packed(torch.nn.LSTM, self, x, initial_states, weights, bidir, batch_first)
+            if sequence_length is None:
+                out, h, c = torch._VF.lstm(x, initial_states, weights, True, self.num_layers, self.dropout,
+                                           self.training, bidir, batch_first)
+            else:
+                out, (h, c) = _packed(torch.nn.LSTM, self, x, initial_states, weights, bidir, batch_first)
             state = (_wrap(h), _wrap(c))
         elif self._mode == 'GRU':
             out, h = torch._VF.gru(x, initial_states, weights, True, self.num_layers, self.dropout, self.training,
