@@ -1,0 +1,31 @@
+"""paddle.distributed.sharding (reference: python/paddle/distributed/sharding/group_sharded.py)."""
+import os
+
+import torch
+
+from ...parallel.sharding import ShardingEngine, ShardedOptimizer, GroupShardedModel, gathered_state_dict
+
+
+def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, offload=False, sync_buffers=False,
+                           buffer_max_size=2 ** 23, segment_size=2 ** 20, sync_comm=False, dp_group=None,
+                           exclude_layer=None):
+    """level: 'os' (stage 1), 'os_g' (stage 2), 'p_g_os' (stage 3). Returns (model, optimizer, scaler)."""
+    assert level in ('os', 'os_g', 'p_g_os'), f"unknown sharding level {level}"
+    engine = ShardingEngine(model, level, group=group, segment_size=segment_size)
+    wrapped = GroupShardedModel(model, engine)
+    opt = ShardedOptimizer(optimizer, engine)
+    return wrapped, opt, scaler
+
+
+def save_group_sharded_model(model, output, optimizer=None):
+    from ...framework.io import save
+    import torch.distributed as dist
+    os.makedirs(output, exist_ok=True)
+    engine = model.__dict__.get('_engine')
+    layer = model._layers if hasattr(model, '_layers') else model
+    sd = gathered_state_dict(layer, engine) if engine is not None else layer.state_dict()
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    if rank == 0:
+        save(sd, os.path.join(output, 'model.pdparams'))
+    if optimizer is not None:
+        save(optimizer.state_dict(), os.path.join(output, f'model.pdopt.rank{rank}'))

@@ -1,0 +1,589 @@
+"""Group-sharded data parallelism (ZeRO) stage 1 / 2 / 3 over RCCL.
+
+Reference: python/paddle/distributed/sharding/group_sharded.py (group_sharded_parallel),
+python/paddle/distributed/fleet/meta_parallel/sharding/group_sharded_stage2.py,
+group_sharded_stage3.py:85 (GroupShardedStage3), group_sharded_optimizer_stage2.py.
+
+MI355X design — everything is a contiguous slice:
+
+* A **unit** is a FlatBuffer of parameters padded to a multiple of (world × 64) elements.
+  Rank r owns elements [r·L, (r+1)·L) of every unit (L = numel / world).
+  - stage 1/2 ('os', 'os_g'): units are ~``bucket_mb`` slices of one flat buffer per dtype;
+    parameters stay materialised on every rank.
+  - stage 3 ('p_g_os'): one unit per layer block (greedy split of the layer tree at
+    ``segment_size`` elements); a unit's full parameter storage exists only while the block
+    runs forward or backward (storage resize to 0 otherwise), gathered by one
+    ``all_gather_into_tensor`` per unit with the next unit's gather prefetched
+    asynchronously; embedding units are kept materialised (their weights are commonly tied
+    to the LM head and used outside their own layer).
+* Gradients accumulate into per-unit flat buffers; the moment a unit's last gradient lands a
+  ``reduce_scatter_tensor`` (AVG) of the whole unit is launched asynchronously, so it
+  overlaps the backward of earlier units.  Stage 3 materialises a unit's gradient storage
+  right before its backward and releases it after its reduce-scatter.
+* The optimizer state (fp32 master, m, v) and the reduced gradient shard of every unit live
+  in ONE per-dtype **arena**; the whole sharded AdamW update is one fused HIP kernel launch
+  per dtype (ops.optim.adamw_flat), followed by async all-gathers of updated shards.
+* Global-norm clipping: sum of squares of the local gradient shards, one all-reduce.
+"""
+import math
+
+import torch
+import torch.distributed as dist
+
+from ..core.tensor import Tensor, Parameter, _wrap, _unwrap
+from .flat_buffer import FlatBuffer, ALIGN
+from .. import ops
+
+LEVELS = {'os': 1, 'os_g': 2, 'p_g_os': 3}
+
+
+def _pg(group):
+    return None if group is None else getattr(group, 'pg', group)
+
+
+class _Unit:
+    def __init__(self, engine, params, layer=None, persistent=True):
+        self.engine = engine
+        self.layer = layer
+        self.persistent = persistent
+        W = engine.world
+        self.fb = FlatBuffer(params, pad_to_multiple=W)
+        self.params = self.fb.params
+        self.L = self.fb.numel // W
+        self.dtype = self.fb.dtype
+        self.gathered = True
+        self.grad_live = True
+        self.gather_work = None
+        self.rs_work = None
+        self.pending = sum(1 for p in self.params if p._t.requires_grad)
+        self.arena_off = None  # set by engine
+        self.index = -1
+
+    # ---- local shard views
+    def shard(self, t):
+        r = self.engine.rank
+        return t[r * self.L:(r + 1) * self.L]
+
+    # ---- parameter materialisation (stage 3)
+    def free_params(self):
+        if self.persistent or not self.gathered:
+            return
+        self.fb.data.untyped_storage().resize_(0)
+        self.gathered = False
+
+    def gather_async(self):
+        if self.gathered or self.gather_work is not None:
+            return
+        st = self.fb.data.untyped_storage()
+        st.resize_(self.fb.numel * self.fb.data.element_size())
+        src = self.engine.pshard(self)
+        if self.engine.world == 1:
+            self.fb.data.copy_(src)
+            self.gathered = True
+            return
+        self.gather_work = dist.all_gather_into_tensor(self.fb.data, src, group=self.engine.pg, async_op=True)
+
+    def wait_gather(self):
+        if self.gather_work is None and not self.gathered:
+            self.gather_async()
+        if self.gather_work is not None:
+            self.gather_work.wait()
+            self.gather_work = None
+        self.gathered = True
+
+    # ---- gradient storage (stage 3 releases it between steps)
+    def alloc_grads(self):
+        if self.grad_live:
+            return
+        st = self.fb.grad.untyped_storage()
+        st.resize_(self.fb.numel * self.fb.grad.element_size())
+        self.fb.grad.zero_()
+        self.grad_live = True
+
+    def free_grads(self):
+        if self.grad_live and self.engine.release_grads:
+            self.fb.grad.untyped_storage().resize_(0)
+            self.grad_live = False
+
+
+class _PreBackward(torch.autograd.Function):
+    """Identity on a unit's outputs whose backward materialises the unit (params + grads)
+    before autograd enters the unit's own backward."""
+
+    @staticmethod
+    def forward(ctx, unit_box, *xs):
+        ctx.unit = unit_box[0]
+        return xs if len(xs) > 1 else xs[0]
+
+    @staticmethod
+    def backward(ctx, *gs):
+        u = ctx.unit
+        u.engine._pre_backward(u)
+        return (None,) + gs
+
+
+class ShardingEngine:
+    def __init__(self, model, level='p_g_os', group=None, bucket_mb=256, segment_size=2 ** 20,
+                 release_grads=True, persistent_types=None):
+        self.model = model
+        self.level = LEVELS[level] if isinstance(level, str) else int(level)
+        self.group = group
+        self.pg = _pg(group)
+        self.world = dist.get_world_size(self.pg) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(self.pg) if dist.is_initialized() else 0
+        self.release_grads = release_grads and self.level == 3
+        from ..nn.layer.common import Embedding
+        self.persistent_types = tuple(persistent_types or (Embedding,))
+        self._broadcast_params()
+        params = [p for p in model.parameters() if p._t.requires_grad or True]
+        if self.level == 3:
+            self.units = self._layer_units(model, segment_size)
+        else:
+            self.units = self._bucket_units(params, bucket_mb)
+        for i, u in enumerate(self.units):
+            u.index = i
+        self._build_arenas()
+        self._hooks = []
+        self._install_grad_hooks()
+        if self.level == 3:
+            self._install_layer_hooks()
+            for u in self.units:
+                u.free_params()
+                u.free_grads()
+        self._armed = False
+        self._fwd_order = []
+        self._recording = True
+        self.grad_fresh = True
+
+    # ------------------------------------------------------------------ construction
+    def _broadcast_params(self):
+        if self.world == 1:
+            return
+        from .data_parallel import sync_params_buffers
+        sync_params_buffers(self.model, self.group)
+
+    def _bucket_units(self, params, bucket_mb):
+        units = []
+        by_dt = {}
+        for p in params:
+            by_dt.setdefault(p._t.dtype, []).append(p)
+        cap = bucket_mb * 2 ** 20
+        for dt, ps in by_dt.items():
+            cur, size = [], 0
+            for p in ps:
+                cur.append(p)
+                size += p._t.numel() * p._t.element_size()
+                if size >= cap:
+                    units.append(_Unit(self, cur, None, True))
+                    cur, size = [], 0
+            if cur:
+                units.append(_Unit(self, cur, None, True))
+        return units
+
+    def _layer_units(self, model, segment_size):
+        """Greedy top-down split: a layer whose subtree holds <= segment_size*64 elements becomes
+        one unit (per dtype); bigger layers are descended into; a layer's *own* params are
+        grouped into a unit for that layer."""
+        limit = max(segment_size * 64, 1)
+        units = []
+        seen = set()
+
+        def count(layer):
+            return sum(p._t.numel() for p in layer.parameters() if id(p) not in seen)
+
+        def make(layer, params, persistent):
+            by_dt = {}
+            for p in params:
+                if id(p) in seen:
+                    continue
+                seen.add(id(p))
+                by_dt.setdefault(p._t.dtype, []).append(p)
+            for dt, ps in by_dt.items():
+                units.append(_Unit(self, ps, layer, persistent))
+
+        def visit(layer):
+            n = count(layer)
+            if n == 0:
+                return
+            if isinstance(layer, self.persistent_types):
+                make(layer, layer.parameters(), True)
+                return
+            children = [c for c in layer.children() if count(c) > 0]
+            from ..nn.layer.container import LayerList, LayerDict
+            container = isinstance(layer, (LayerList, LayerDict))  # never called: descend
+            if (n <= limit and not container) or not children:
+                make(layer, layer.parameters(), False)
+                return
+            own = [p for p in layer._parameters.values() if p is not None]
+            if own:
+                make(layer, own, True)
+            for c in children:
+                visit(c)
+
+        visit(model)
+        return units
+
+    def _build_arenas(self):
+        self.arenas = {}
+        for u in self.units:
+            a = self.arenas.setdefault(u.dtype, {'units': [], 'size': 0})
+            u.arena_off = a['size']
+            a['size'] += u.L
+            a['units'].append(u)
+        for dt, a in self.arenas.items():
+            n = a['size']
+            dev = a['units'][0].fb.data.device
+            a['param'] = torch.empty(n, dtype=dt, device=dev)
+            for u in a['units']:
+                a['param'][u.arena_off:u.arena_off + u.L].copy_(u.shard(u.fb.data))
+            a['master'] = a['param'].float().clone() if dt != torch.float32 else a['param']
+            a['m'] = torch.zeros(n, dtype=torch.float32, device=dev)
+            a['v'] = torch.zeros(n, dtype=torch.float32, device=dev)
+            a['grad'] = torch.zeros(n, dtype=dt, device=dev)
+            a['b1p'] = None
+
+    def pshard(self, u):
+        return self.arenas[u.dtype]['param'][u.arena_off:u.arena_off + u.L]
+
+    def gshard(self, u):
+        return self.arenas[u.dtype]['grad'][u.arena_off:u.arena_off + u.L]
+
+    # ------------------------------------------------------------------ hooks
+    def _install_grad_hooks(self):
+        for u in self.units:
+            for p in u.params:
+                if p._t.requires_grad:
+                    self._hooks.append(p._t.register_post_accumulate_grad_hook(self._grad_hook(u)))
+
+    def _grad_hook(self, u):
+        def hook(t):
+            if not self._armed:
+                self._armed = True
+                torch.autograd.Variable._execution_engine.queue_callback(self._finish_backward)
+            u.pending -= 1
+            if u.pending == 0:
+                self._reduce_scatter(u)
+        return hook
+
+    def _install_layer_hooks(self):
+        for u in self.units:
+            if u.persistent or u.layer is None:
+                continue
+            layer = u.layer
+            layer.register_forward_pre_hook(self._fwd_pre(u))
+            layer.register_forward_post_hook(self._fwd_post(u))
+        # persistent units of stage 3 are gathered at the start of every forward
+        self.model.register_forward_pre_hook(self._root_pre)
+
+    def _root_pre(self, layer, inputs):
+        for u in self.units:
+            if u.persistent or u.layer is None:
+                u.wait_gather()
+                if torch.is_grad_enabled():
+                    u.alloc_grads()
+        return None
+
+    def _fwd_pre(self, u):
+        def hook(layer, inputs):
+            if self._recording and torch.is_grad_enabled():
+                self._fwd_order.append(u)
+            u.wait_gather()
+            if torch.is_grad_enabled():
+                u.alloc_grads()
+            # prefetch the next unit in forward order
+            nxt = self._next_unit(u, +1)
+            if nxt is not None:
+                nxt.gather_async()
+            return None
+        return hook
+
+    def _fwd_post(self, u):
+        def hook(layer, inputs, outputs):
+            if torch.is_grad_enabled():
+                outs = outputs if isinstance(outputs, tuple) else (outputs,)
+                idx = [i for i, o in enumerate(outs) if isinstance(o, Tensor) and o._t.requires_grad]
+                if idx:
+                    ts = [outs[i]._t for i in idx]
+                    res = _PreBackward.apply([u], *ts)
+                    res = res if isinstance(res, tuple) else (res,)
+                    new = list(outs)
+                    for i, r in zip(idx, res):
+                        new[i] = _wrap(r)
+                    outputs = tuple(new) if isinstance(outputs, tuple) else new[0]
+            u.free_params()
+            return outputs
+        return hook
+
+    def _next_unit(self, u, direction):
+        order = self._fwd_order
+        if not order or self._recording:
+            return None
+        try:
+            i = self._order_index[id(u)]
+        except (AttributeError, KeyError):
+            return None
+        j = i + direction
+        return order[j] if 0 <= j < len(order) else None
+
+    def _pre_backward(self, u):
+        u.wait_gather()
+        u.alloc_grads()
+        prv = self._next_unit(u, -1)
+        if prv is not None:
+            prv.gather_async()
+
+    # ------------------------------------------------------------------ gradient reduction
+    def _reduce_scatter(self, u):
+        if self.world == 1:
+            u.rs_work = None
+            self._accumulate_shard(u, u.shard(u.fb.grad))
+            return
+        out = self.gshard(u) if self.grad_fresh else torch.empty(u.L, dtype=u.fb.grad.dtype, device=u.fb.grad.device)
+        u._rs_out = out
+        op = dist.ReduceOp.AVG if dist.get_backend(self.pg) == 'nccl' else dist.ReduceOp.SUM
+        u.rs_work = dist.reduce_scatter_tensor(out, u.fb.grad, op, group=self.pg, async_op=True)
+        if self.level == 3:
+            u.free_params()
+
+    def _accumulate_shard(self, u, src):
+        dst = self.gshard(u)
+        if self.grad_fresh:
+            if src.data_ptr() != dst.data_ptr():
+                dst.copy_(src)
+        else:
+            dst.add_(src)
+
+    def _finish_backward(self):
+        for u in self.units:
+            if u.pending > 0 and u.rs_work is None:
+                if not u.grad_live:
+                    u.alloc_grads()
+                self._reduce_scatter(u)
+        for u in self.units:
+            if u.rs_work is not None:
+                u.rs_work.wait()
+                u.rs_work = None
+                if dist.get_backend(self.pg) != 'nccl':
+                    u._rs_out.div_(self.world)
+                if not self.grad_fresh:
+                    self.gshard(u).add_(u._rs_out)
+            u.pending = sum(1 for p in u.params if p._t.requires_grad)
+            u.fb.grad.zero_() if u.grad_live and not self.release_grads else None
+            u.free_grads()
+            u.free_params()
+        self.grad_fresh = False
+        if self._recording and self._fwd_order:
+            self._recording = False
+            self._order_index = {id(x): i for i, x in enumerate(self._fwd_order)}
+        self._armed = False
+
+    def zero_grad(self):
+        for a in self.arenas.values():
+            a['grad'].zero_()
+        self.grad_fresh = True
+
+    # ------------------------------------------------------------------ after the update
+    def gather_params_after_step(self):
+        for u in self.units:
+            if u.persistent or self.level < 3:
+                if self.world == 1:
+                    u.fb.data[:u.L].copy_(self.pshard(u)) if u.fb.data.data_ptr() != self.pshard(u).data_ptr() else None
+                    continue
+                dist.all_gather_into_tensor(u.fb.data, self.pshard(u), group=self.pg)
+            # stage-3 non-persistent units are gathered lazily by their forward pre-hook
+
+
+class ShardedOptimizer:
+    """Wraps a paddle optimizer; updates only the local shard (one fused AdamW per dtype arena).
+
+    Reference: GroupShardedOptimizerStage2 / the stage-3 _OptimizerWrapper."""
+
+    def __init__(self, optimizer, engine):
+        self._inner = optimizer
+        self.engine = engine
+        self._step = 0
+        name = type(optimizer).__name__
+        if name not in ('AdamW', 'Adam'):
+            raise NotImplementedError(f"group-sharded training supports Adam/AdamW here, got {name}")
+        self._decoupled = name == 'AdamW'
+        self._coeff_runs = {}
+        for dt, a in engine.arenas.items():
+            self._coeff_runs[dt] = self._runs(a)
+
+    def _coeff(self, p):
+        opt = self._inner
+        if not self._decoupled:
+            return 0.0
+        f = getattr(opt, '_apply_decay_param_fun', None)
+        if f is not None and not f(p.name):
+            return 0.0
+        return float(opt._coeff)
+
+    def _runs(self, arena):
+        """(arena_lo, arena_hi, coeff) runs of equal weight decay covering [0, arena size)."""
+        segs = []
+        r = self.engine.rank
+        for u in arena['units']:
+            lo_s, hi_s = r * u.L, (r + 1) * u.L
+            for p, o in zip(u.fb.params, u.fb.offsets):
+                a, b = max(o, lo_s), min(o + p._t.numel(), hi_s)
+                if a < b:
+                    segs.append((u.arena_off + (a - lo_s), u.arena_off + (b - lo_s), self._coeff(p)))
+        segs.sort()
+        runs = []
+        for a, b, c in segs:
+            if runs and runs[-1][2] == c:
+                runs[-1][1] = b
+            else:
+                if runs:
+                    runs[-1][1] = a  # padding between params rides with the previous run
+                runs.append([a, b, c])
+        if not runs:
+            return [[0, arena['size'], 0.0]]
+        runs[0][0] = 0
+        runs[-1][1] = arena['size']
+        return runs
+
+    # ---- paddle optimizer surface
+    def get_lr(self):
+        return self._inner.get_lr()
+
+    def set_lr(self, v):
+        self._inner.set_lr(v)
+
+    @property
+    def _learning_rate(self):
+        return self._inner._learning_rate
+
+    def _clip_scale(self):
+        clip = self._inner._grad_clip
+        if clip is None:
+            return None
+        from ..nn.clip import ClipGradByGlobalNorm
+        if not isinstance(clip, ClipGradByGlobalNorm):
+            return None
+        sq = None
+        for a in self.engine.arenas.values():
+            s = a['grad'].float().pow(2).sum()
+            sq = s if sq is None else sq + s
+        if self.engine.world > 1:
+            dist.all_reduce(sq, group=self.engine.pg)
+        norm = sq.sqrt()
+        return torch.clamp(clip.clip_norm / torch.clamp(norm, min=clip.clip_norm), max=1.0)
+
+    @torch.no_grad()
+    def step(self):
+        opt = self._inner
+        b1, b2, eps = opt._beta1, opt._beta2, opt._epsilon
+        self._step += 1
+        b1p, b2p = b1 ** self._step, b2 ** self._step
+        lr = opt.get_lr()
+        scale = self._clip_scale()
+        for dt, a in self.engine.arenas.items():
+            g = a['grad']
+            if scale is not None:
+                g.mul_(scale.to(g.dtype))
+            lowp = a['param'] if dt != torch.float32 else None
+            for lo, hi, coeff in self._coeff_runs[dt]:
+                if hi <= lo:
+                    continue
+                if ops.use_hip(a['master']):
+                    ops.optim.adamw_flat(a['master'][lo:hi], g[lo:hi], a['m'][lo:hi], a['v'][lo:hi],
+                                         None if lowp is None else lowp[lo:hi], lr, b1, b2, eps, coeff, b1p, b2p)
+                else:
+                    _adamw_ref(a['master'][lo:hi], g[lo:hi], a['m'][lo:hi], a['v'][lo:hi],
+                               None if lowp is None else lowp[lo:hi], lr, b1, b2, eps, coeff, b1p, b2p)
+        self.engine.gather_params_after_step()
+        opt._global_step += 1
+
+    def clear_grad(self, set_to_zero=True):
+        self.engine.zero_grad()
+
+    clear_gradients = clear_grad
+
+    def minimize(self, loss, *a, **k):
+        loss.backward()
+        self.step()
+
+    def state_dict(self):
+        sd = {}
+        for dt, a in self.engine.arenas.items():
+            key = str(dt).replace('torch.', '')
+            sd[f'shard_master_{key}'] = _wrap(a['master'])
+            sd[f'shard_moment1_{key}'] = _wrap(a['m'])
+            sd[f'shard_moment2_{key}'] = _wrap(a['v'])
+        sd['@step@'] = self._step
+        if hasattr(self._inner._learning_rate, 'state_dict'):
+            sd['LR_Scheduler'] = self._inner._learning_rate.state_dict()
+        return sd
+
+    def set_state_dict(self, sd):
+        for dt, a in self.engine.arenas.items():
+            key = str(dt).replace('torch.', '')
+            for nm, buf in (('master', a['master']), ('moment1', a['m']), ('moment2', a['v'])):
+                v = sd.get(f'shard_{nm}_{key}')
+                if v is not None:
+                    buf.copy_(_unwrap(v).to(buf.device))
+            if dt != torch.float32:
+                a['param'].copy_(a['master'].to(dt))
+        self._step = int(sd.get('@step@', self._step))
+        if 'LR_Scheduler' in sd and hasattr(self._inner._learning_rate, 'set_state_dict'):
+            self._inner._learning_rate.set_state_dict(sd['LR_Scheduler'])
+        self.engine.gather_params_after_step()
+
+    def __getattr__(self, name):
+        return getattr(self._inner, name)
+
+
+def _adamw_ref(p, g, m, v, lowp, lr, b1, b2, eps, wd, b1p, b2p):
+    gg = g.float()
+    p.mul_(1 - lr * wd)
+    m.mul_(b1).add_(gg, alpha=1 - b1)
+    v.mul_(b2).addcmul_(gg, gg, value=1 - b2)
+    bc2 = math.sqrt(1 - b2p)
+    p.sub_(lr * bc2 / (1 - b1p) * m / (v.sqrt() + eps * bc2))
+    if lowp is not None:
+        lowp.copy_(p.to(lowp.dtype))
+
+
+class GroupShardedModel:
+    """The wrapped model returned by group_sharded_parallel (a Layer proxy)."""
+
+    def __new__(cls, layer, engine):
+        from ..nn.layer.layers import Layer
+
+        class _GS(Layer):
+            def __init__(self):
+                super().__init__()
+                self._layers = layer
+                self.__dict__['_engine'] = engine
+
+            def forward(self, *a, **k):
+                return self._layers(*a, **k)
+
+            def state_dict(self, *a, **k):
+                return gathered_state_dict(self._layers, engine)
+
+            def set_state_dict(self, sd, use_structured_name=True):
+                return self._layers.set_state_dict(sd, use_structured_name)
+
+            def get_all_parameters(self, convert2cpu=False):
+                for u in engine.units:
+                    u.wait_gather()
+                return self._layers.parameters()
+
+        _GS.__name__ = 'GroupShardedStage%d' % engine.level
+        return _GS()
+
+
+def gathered_state_dict(layer, engine):
+    """Full (unsharded) state dict: gathers any released unit, copies, releases again."""
+    out = {}
+    released = [u for u in engine.units if not u.gathered]
+    for u in released:
+        u.wait_gather()
+    for k, v in layer.state_dict().items():
+        out[k] = _wrap(v._t.detach().clone())
+    for u in released:
+        u.free_params()
+    return out
