@@ -57,11 +57,11 @@ def main():
                                      beta1=0.9, beta2=0.95, epsilon=1e-8, multi_precision=True,
                                      grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
         model, opt = paddle.amp.decorate(model, opt, level='O2', dtype='bfloat16')
-        if world > 1:
-            if args.sharding == 'dp':
+        if args.sharding == 'dp':
+            if world > 1:
                 model = pdist.DataParallel(model)
-            else:
-                model, opt, _ = pdist.sharding.group_sharded_parallel(model, opt, level=args.sharding)
+        else:  # same sharded engine at every N (degenerate single shard at N=1)
+            model, opt, _ = pdist.sharding.group_sharded_parallel(model, opt, level=args.sharding)
         B, S = args.micro_batch, args.seq
         g = torch.Generator(device=dev).manual_seed(rank)
         ids = torch.randint(0, cfg.vocab_size, (B, S + 1), device=dev, generator=g)

@@ -261,15 +261,26 @@ __global__ __launch_bounds__(256) void norm_bwd_generic(const T* __restrict__ dy
   }
 }
 
-// out[c] = sum_p part[p, c]  (column-parallel, coalesced over c)
+// out[c] = sum_p part[p, c]: block = 4 waves x 64 columns; the waves split the P partial rows
+// (each wave-row read is 256 contiguous bytes), then a 4-way LDS reduce.  Deterministic.
 template <typename WT>
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, WT* __restrict__ out, int P,
                                                      int cols) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(size_t)p * cols + c];
-  out[c] = from_f<WT>(s);
+  if (c < cols) {
+    int p = w;
+    for (; p + 12 < P; p += 16) {  // 4 independent loads in flight per lane
+      s += part[(size_t)p * cols + c] + part[(size_t)(p + 4) * cols + c] + part[(size_t)(p + 8) * cols + c] +
+           part[(size_t)(p + 12) * cols + c];
+    }
+    for (; p < P; p += 4) s += part[(size_t)p * cols + c];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < cols) out[c] = from_f<WT>(red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
 }
 
 template <typename T, typename WT, bool RMS>
@@ -317,7 +328,7 @@ hipError_t launch_bwd(const void* dy, const void* x, const void* w, const float*
 #undef PA_NB
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int g = (cols + 255) / 256;
+  const int g = (cols + 63) / 64;
   colsum_kernel<WT><<<g, 256, 0, st>>>(dw_part, (WT*)dw, nparts, cols);
   if (!RMS && db != nullptr) colsum_kernel<WT><<<g, 256, 0, st>>>(db_part, (WT*)db, nparts, cols);
   return hipGetLastError();

@@ -15,6 +15,9 @@ def linear(x, weight, bias=None, name=None):
     """y = x @ W + b with W stored [in_features, out_features] (paddle layout)."""
     t, w = _u(x), _u(weight)
     b = _u(bias) if bias is not None else None
+    if isinstance(weight, Tensor) and '_flat' in weight.__dict__ and ops.linear.eligible(weight) and \
+            (bias is None or '_flat' in bias.__dict__):
+        return _w(ops.linear.linear_accum(t, weight, bias))
     if t.dim() == 2:
         return _w(torch.addmm(b, t, w) if b is not None else torch.mm(t, w))
     if b is not None:

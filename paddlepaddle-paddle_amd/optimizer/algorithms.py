@@ -158,11 +158,7 @@ class Adam(Optimizer):
                     self._flat = None
                     return super().step()
                 fb.sync_grads()
-            # grad clip on the (flat-view) grads, per group
-            for gi, group in enumerate(self._param_groups):
-                clip = group.get('grad_clip', self._grad_clip)
-                if clip is not None:
-                    clip(self._params_grads(group))
+            self._clip_flat()
             for ent in self._flat:
                 fb = ent['fb']
                 glr = lr * self._param_groups[ent['group']].get('learning_rate', 1.0)
@@ -172,6 +168,44 @@ class Adam(Optimizer):
                 ent['b1p'] *= self._beta1
                 ent['b2p'] *= self._beta2
         self._global_step += 1
+
+    def _clip_flat(self):
+        """Global-norm clip over the flat gradient buffers: one sum-of-squares kernel per buffer,
+        one in-place scale per buffer (instead of per-parameter norm/scale launches)."""
+        from ..nn.clip import ClipGradByGlobalNorm
+        clips = {id(g.get('grad_clip', self._grad_clip)): g.get('grad_clip', self._grad_clip)
+                 for g in self._param_groups}
+        clips = [c for c in clips.values() if c is not None]
+        if not clips:
+            return
+        if len(clips) > 1 or not isinstance(clips[0], ClipGradByGlobalNorm):
+            for group in self._param_groups:
+                clip = group.get('grad_clip', self._grad_clip)
+                if clip is not None:
+                    clip(self._params_grads(group))
+            return
+        clip = clips[0]
+        bufs = {id(e['fb']): e['fb'] for e in self._flat}.values()
+        sq = None
+        for fb in bufs:
+            s = ops.optim.sumsq(fb.grad)
+            sq = s if sq is None else sq + s
+        if clip._extra_sq_norm_fn is not None:
+            sq = clip._extra_sq_norm_fn(sq)
+        scale = torch.clamp(clip.clip_norm / torch.clamp(sq.sqrt(), min=clip.clip_norm), max=1.0)
+        for fb in bufs:
+            fb.grad.mul_(scale.to(fb.grad.dtype))
+
+    def clear_grad(self, set_to_zero=True):
+        if self._flat is None:
+            return super().clear_grad(set_to_zero)
+        for fb in {id(e['fb']): e['fb'] for e in self._flat}.values():
+            fb.grad.zero_()
+        for p in self._parameter_list:  # parameters outside the flat buffers
+            if '_flat' not in p.__dict__ and p._t.grad is not None:
+                p._t.grad.zero_()
+
+    clear_gradients = clear_grad
 
     def state_dict(self):
         sd = super().state_dict()

@@ -20,7 +20,7 @@ import torch
 import torch.distributed as dist
 
 from ..core.tensor import Tensor, _wrap, _unwrap
-from .flat_buffer import FlatBuffer
+from .flat_buffer import FlatBuffer, register_grad_ready
 from ..nn.layer.layers import Layer
 
 DEFAULT_BUCKET_MB = 64
@@ -96,7 +96,7 @@ class GradAllReducer:
         self._hooks = []
         for b in self.buckets:
             for p in b.params:
-                self._hooks.append(p._t.register_post_accumulate_grad_hook(self._make_hook(b)))
+                self._hooks.append(register_grad_ready(p, self._make_hook(b)))
         self._armed = False
 
     def _add(self, fb, lo, hi, params):
@@ -106,7 +106,7 @@ class GradAllReducer:
             self._p2b[id(p)] = b
 
     def _make_hook(self, bucket):
-        def hook(t):
+        def hook():
             if not self.enabled:
                 return
             if not self._armed:

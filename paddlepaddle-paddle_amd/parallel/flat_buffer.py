@@ -90,3 +90,67 @@ class FlatBuffer:
 
     def zero_grad(self):
         self.grad.zero_()
+
+
+def register_grad_ready(p, fn):
+    """Call ``fn()`` whenever p's gradient for this backward is complete.
+
+    Fires from torch's post-accumulate-grad hook (ordinary autograd accumulation) AND from
+    kernels that accumulate straight into the flat gradient slot (ops.linear's fused
+    weight-gradient GEMM, which bypasses AccumulateGrad).  Returns a removable handle."""
+    lst = p.__dict__.setdefault('_grad_ready', [])
+    lst.append(fn)
+    h = p._t.register_post_accumulate_grad_hook(lambda t: fn())
+
+    class _Handle:
+        def remove(self):
+            h.remove()
+            if fn in lst:
+                lst.remove(fn)
+    return _Handle()
+
+
+def _hooks_fire_on_undefined_grad():
+    """Does torch run post-accumulate-grad hooks when a Function returns None for a leaf?
+    (Observed true on torch 2.x: AccumulateGrad still executes its post hooks.)  Probed once."""
+    fired = []
+
+    class _F(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, a, w):
+            return a * 2
+
+        @staticmethod
+        def backward(ctx, g):
+            return g * 2, None
+
+    a = torch.ones(2, requires_grad=True)
+    w = torch.ones(2, requires_grad=True)
+    w.register_post_accumulate_grad_hook(lambda t: fired.append(1))
+    _F.apply(a, w).sum().backward()
+    return bool(fired)
+
+
+_HOOKS_FIRE = _hooks_fire_on_undefined_grad()
+
+
+def notify_grad_ready(p):
+    """Called by kernels that wrote p's gradient directly into its flat slot.  When torch itself
+    fires the post-accumulate hook for the (undefined) autograd gradient, that hook is the single
+    notification; otherwise notify here."""
+    if _HOOKS_FIRE:
+        return
+    for fn in p.__dict__.get('_grad_ready', ()):
+        fn()
+
+
+def flat_grad_slot(p):
+    """The flat-buffer gradient view of p if p lives in a FlatBuffer (else None)."""
+    if '_flat' not in p.__dict__:
+        return None
+    g = p._t.grad
+    fb, o = p.__dict__['_flat']
+    if g is None or fb.grad.untyped_storage().nbytes() == 0 or \
+            g.data_ptr() != fb.grad.data_ptr() + o * fb.grad.element_size():
+        return None
+    return g

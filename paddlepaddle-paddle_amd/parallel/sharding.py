@@ -31,7 +31,7 @@ import torch
 import torch.distributed as dist
 
 from ..core.tensor import Tensor, Parameter, _wrap, _unwrap
-from .flat_buffer import FlatBuffer, ALIGN
+from .flat_buffer import FlatBuffer, ALIGN, register_grad_ready
 from .. import ops
 
 LEVELS = {'os': 1, 'os_g': 2, 'p_g_os': 3}
@@ -253,10 +253,10 @@ class ShardingEngine:
         for u in self.units:
             for p in u.params:
                 if p._t.requires_grad:
-                    self._hooks.append(p._t.register_post_accumulate_grad_hook(self._grad_hook(u)))
+                    self._hooks.append(register_grad_ready(p, self._grad_hook(u)))
 
     def _grad_hook(self, u):
-        def hook(t):
+        def hook():
             if not self._armed:
                 self._armed = True
                 torch.autograd.Variable._execution_engine.queue_callback(self._finish_backward)
