@@ -1,0 +1,240 @@
+"""paddle.distributed.fleet (reference: python/paddle/distributed/fleet/fleet.py:100 Fleet,
+base/distributed_strategy.py, model.py:32 distributed_model, optimizer.py distributed_optimizer).
+
+``fleet.init(is_collective=True, strategy=s)`` builds the hybrid topology from
+``s.hybrid_configs`` (dp/mp/pp/sharding/sep degrees) and one RCCL communicator per axis group;
+``distributed_model`` wraps the model for the active parallel mode (DataParallel,
+TensorParallel, PipelineParallel, or group-sharded); ``distributed_optimizer`` wraps the
+optimizer so that gradient clipping sees the global norm across model-parallel shards and
+sharding partitions.
+"""
+import copy
+
+import torch
+import torch.distributed as dist
+
+from .base.topology import CommunicateTopology, HybridCommunicateGroup, ParallelMode  # noqa: F401
+from . import layers, meta_parallel, utils  # noqa: F401
+from .recompute import recompute, recompute_sequential, recompute_hybrid  # noqa: F401
+from .meta_parallel import (LayerDesc, SharedLayerDesc, PipelineLayer, ColumnParallelLinear,  # noqa: F401
+                            RowParallelLinear, VocabParallelEmbedding, ParallelCrossEntropy, get_rng_state_tracker)
+
+
+class DistributedStrategy:
+    """Subset of the reference's protobuf-backed strategy, as plain attributes."""
+
+    def __init__(self):
+        self.hybrid_configs = {'dp_degree': -1, 'mp_degree': 1, 'pp_degree': 1, 'sharding_degree': 1,
+                               'sep_degree': 1, 'order': ['dp', 'pp', 'sharding', 'sep', 'mp'],
+                               'mp_configs': {}, 'pp_configs': {}}
+        self.pipeline_configs = {'accumulate_steps': 1, 'micro_batch_size': 1, 'schedule_mode': '1F1B'}
+        self.sharding = False
+        self.sharding_configs = {'sharding_degree': 1, 'stage': 1, 'segment_broadcast_MB': 32}
+        self.amp = False
+        self.amp_configs = {'init_loss_scaling': 32768.0, 'use_pure_fp16': False, 'use_pure_bf16': False,
+                            'custom_white_list': [], 'custom_black_list': []}
+        self.recompute = False
+        self.recompute_configs = {'checkpoints': [], 'enable_offload': False}
+        self.gradient_merge = False
+        self.gradient_merge_configs = {'k_steps': 1, 'avg': True}
+        self.tensor_parallel = False
+        self.tensor_parallel_configs = {'tensor_parallel_degree': 1}
+        self.pipeline = False
+        self.fuse_all_reduce_ops = True
+        self.fuse_grad_size_in_MB = 64
+        self.find_unused_parameters = False
+        self.without_graph_optimization = False
+        self.heter_ccl_mode = False
+        self.lamb = False
+        self.lars = False
+        self.dgc = False
+        self.localsgd = False
+        self.a_sync = False
+        self.nccl_comm_num = 1
+
+    def __setattr__(self, k, v):
+        if k.endswith('_configs') and k in self.__dict__ and isinstance(v, dict):
+            d = dict(self.__dict__[k])
+            d.update(v)
+            object.__setattr__(self, k, d)
+        else:
+            object.__setattr__(self, k, v)
+
+    def __repr__(self):
+        return f"DistributedStrategy(hybrid_configs={self.hybrid_configs})"
+
+
+class _Fleet:
+    def __init__(self):
+        self._hcg = None
+        self._strategy = None
+        self._is_collective = True
+        self._inited = False
+
+    def init(self, role_maker=None, is_collective=True, strategy=None, log_level="INFO"):
+        from ..parallel import init_parallel_env
+        init_parallel_env()
+        self._strategy = strategy or DistributedStrategy()
+        self._is_collective = is_collective
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        hc = self._strategy.hybrid_configs
+        mp, pp = int(hc.get('mp_degree', 1)), int(hc.get('pp_degree', 1))
+        sh, sep = int(hc.get('sharding_degree', 1)), int(hc.get('sep_degree', 1))
+        dp = int(hc.get('dp_degree', -1))
+        if dp == -1:
+            dp = max(world // (mp * pp * sh * sep), 1)
+        topo = CommunicateTopology(["data", "pipe", "sharding", "sep", "model"], [dp, pp, sh, sep, mp])
+        self._hcg = HybridCommunicateGroup(topo)
+        self._topology = topo
+        self._inited = True
+        if mp > 1:
+            from .layers.mpu.random import model_parallel_random_seed
+            model_parallel_random_seed(2024)
+        return None
+
+    def get_hybrid_communicate_group(self):
+        return self._hcg
+
+    def worker_index(self):
+        return dist.get_rank() if dist.is_initialized() else 0
+
+    def worker_num(self):
+        return dist.get_world_size() if dist.is_initialized() else 1
+
+    def is_first_worker(self):
+        return self.worker_index() == 0
+
+    def is_worker(self):
+        return True
+
+    def barrier_worker(self):
+        if dist.is_initialized():
+            dist.barrier()
+
+    def worker_endpoints(self, to_string=False):
+        import os
+        eps = os.environ.get('PADDLE_TRAINER_ENDPOINTS', '').split(',')
+        return ','.join(eps) if to_string else eps
+
+    def distributed_model(self, model):
+        hcg = self._hcg
+        if hcg is None:
+            return model
+        mode = hcg.get_parallel_mode()
+        if mode == ParallelMode.PIPELINE_PARALLEL:
+            return meta_parallel.PipelineParallel(model, hcg, self._strategy)
+        if mode == ParallelMode.TENSOR_PARALLEL or mode == ParallelMode.SEGMENT_PARALLEL:
+            return meta_parallel.TensorParallel(model, hcg, self._strategy)
+        if mode == ParallelMode.SHARDING_PARALLEL:
+            return model  # wrapped together with the optimizer by distributed_optimizer / group_sharded_parallel
+        from ...parallel.data_parallel import DataParallel
+        if hcg.get_data_parallel_world_size() > 1:
+            return DataParallel(model, comm_buffer_size=self._strategy.fuse_grad_size_in_MB,
+                                find_unused_parameters=self._strategy.find_unused_parameters,
+                                group=hcg.get_data_parallel_group())
+        return model
+
+    def distributed_optimizer(self, optimizer, strategy=None):
+        if strategy is not None:
+            self._strategy = strategy
+        hcg = self._hcg
+        if hcg is None:
+            return optimizer
+        return HybridParallelOptimizer(optimizer, hcg, self._strategy)
+
+    def distributed_scaler(self, scaler):
+        return scaler
+
+    def save_persistables(self, executor, dirname, main_program=None):
+        pass
+
+    @property
+    def util(self):
+        return utils
+
+
+class HybridParallelOptimizer:
+    """reference: fleet/meta_optimizers/dygraph_optimizer/hybrid_parallel_optimizer.py.
+
+    Makes ClipGradByGlobalNorm global across the hybrid topology: the squared norm of
+    tensor-parallel (distributed) parameters is summed over the mp group, replicated ones are
+    counted once; pipeline stages sum over the pp group."""
+
+    def __init__(self, optimizer, hcg, strategy):
+        self._inner_opt = optimizer
+        self._hcg = hcg
+        self._strategy = strategy
+        clip = getattr(optimizer, '_grad_clip', None)
+        from ...nn.clip import ClipGradByGlobalNorm
+        if isinstance(clip, ClipGradByGlobalNorm):
+            clip._extra_sq_norm_fn = self._global_sq
+
+    def _global_sq(self, sq):
+        mp = self._hcg.get_model_parallel_group()
+        pp = self._hcg.get_pipe_parallel_group()
+        if mp is not None and mp.nranks > 1:
+            # every param on an mp rank is either a shard (distinct) or a replica (identical on all
+            # ranks): sum shards' norms over mp, count replicas once (they were counted on every rank)
+            dist_sq = torch.zeros_like(sq)
+            rep_sq = torch.zeros_like(sq)
+            for p in self._inner_opt._parameter_list:
+                g = p._t.grad
+                if g is None:
+                    continue
+                s = g.float().pow(2).sum()
+                if getattr(p, 'is_distributed', False):
+                    dist_sq = dist_sq + s
+                else:
+                    rep_sq = rep_sq + s
+            dist.all_reduce(dist_sq, group=mp.pg)
+            sq = dist_sq + rep_sq
+        if pp is not None and pp.nranks > 1:
+            sq = sq.clone()
+            dist.all_reduce(sq, group=pp.pg)
+        return sq
+
+    def step(self):
+        self._inner_opt.step()
+
+    def minimize(self, loss, *a, **k):
+        return self._inner_opt.minimize(loss, *a, **k)
+
+    def clear_grad(self, set_to_zero=True):
+        self._inner_opt.clear_grad(set_to_zero)
+
+    def __getattr__(self, name):
+        return getattr(self._inner_opt, name)
+
+
+fleet = _Fleet()
+init = fleet.init
+get_hybrid_communicate_group = fleet.get_hybrid_communicate_group
+distributed_model = fleet.distributed_model
+distributed_optimizer = fleet.distributed_optimizer
+distributed_scaler = fleet.distributed_scaler
+worker_index = fleet.worker_index
+worker_num = fleet.worker_num
+is_first_worker = fleet.is_first_worker
+barrier_worker = fleet.barrier_worker
+worker_endpoints = fleet.worker_endpoints
+
+
+def _inited():
+    return fleet._inited
+
+
+class UserDefinedRoleMaker:
+    def __init__(self, *a, **k):
+        pass
+
+
+class PaddleCloudRoleMaker(UserDefinedRoleMaker):
+    pass
+
+
+class Role:
+    WORKER = 1
+    SERVER = 2
+
+
+_ = copy

@@ -1,0 +1,321 @@
+"""Pipeline parallelism (reference: python/paddle/distributed/fleet/meta_parallel/pipeline_parallel.py:149,
+parallel_layers/pp_layers.py: LayerDesc:56, SharedLayerDesc:76, SegmentLayers:92, PipelineLayer:257).
+
+* ``PipelineLayer`` materialises only this stage's slice of the layer list (uniform or
+  parameter-balanced segmentation); shared layers (tied embeddings) are replicated on the
+  stages that use them and their gradients are all-reduced over the stages sharing them.
+* ``PipelineParallel.train_batch`` runs the 1F1B schedule over ``accumulate_steps``
+  micro-batches: warm-up forwards, steady 1F1B, cool-down backwards.  Activations and their
+  gradients cross stages as point-to-point RCCL send/recv (one xGMI hop on an 8-GPU node);
+  tensor metadata (shape/dtype) is exchanged once per batch.
+"""
+import math
+
+import torch
+import torch.distributed as dist
+
+from ....nn.layer.layers import Layer
+from ....core.tensor import Tensor, _wrap, _unwrap
+
+
+class LayerDesc:
+    def __init__(self, layer_func, *inputs, **kwargs):
+        self.layer_func, self.inputs, self.kwargs = layer_func, inputs, kwargs
+        if not issubclass(layer_func, Layer):
+            raise TypeError("LayerDesc needs a Layer subclass")
+
+    def build_layer(self):
+        return self.layer_func(*self.inputs, **self.kwargs)
+
+    def __repr__(self):
+        return f"LayerDesc({self.layer_func.__name__})"
+
+
+class SharedLayerDesc(LayerDesc):
+    def __init__(self, key, layer_func, forward_func=None, shared_weight_attr='weight', *inputs, **kwargs):
+        super().__init__(layer_func, *inputs, **kwargs)
+        self.layer_name = key
+        self.forward_func = forward_func
+        self.shared_weight_attr = shared_weight_attr
+
+
+class SegmentLayers:
+    def __init__(self, layers_desc, num_parts, method="uniform", num_virtual_pipeline_stage=None):
+        self._layers_desc, self.num_parts, self.method = layers_desc, num_parts, method
+
+    def do_segment(self):
+        n = len(self._layers_desc)
+        if self.method == 'uniform' or not str(self.method).startswith('layer:'):
+            base, rem = divmod(n, self.num_parts)
+            bounds = [0]
+            for i in range(self.num_parts):
+                bounds.append(bounds[-1] + base + (1 if i < rem else 0))
+            return bounds
+        # 'layer:ClassName' → balance the count of that layer type across stages
+        name = self.method.split(':', 1)[1]
+        idx = [i for i, d in enumerate(self._layers_desc)
+               if (d.layer_func.__name__ if isinstance(d, LayerDesc) else type(d).__name__) == name]
+        per = math.ceil(len(idx) / self.num_parts)
+        bounds = [0]
+        for s in range(1, self.num_parts):
+            k = min(s * per, len(idx) - 1)
+            bounds.append(idx[k] if k < len(idx) else n)
+        bounds.append(n)
+        return bounds
+
+
+class PipelineLayer(Layer):
+    def __init__(self, layers, num_stages=None, topology=None, loss_fn=None, seg_method="uniform",
+                 recompute_interval=0, recompute_ctx=None, num_virtual_pipeline_stages=None):
+        super().__init__()
+        from ... import fleet as _fleet
+        hcg = _fleet.get_hybrid_communicate_group() if _fleet._inited() else None
+        self._num_stages = num_stages or (hcg.get_pipe_parallel_world_size() if hcg else 1)
+        self._stage_id = hcg.get_stage_id() if hcg else 0
+        self._hcg = hcg
+        self._loss_fn = loss_fn
+        self._recompute_interval = recompute_interval
+        self._layers_desc = list(layers)
+        self.segment_parts = SegmentLayers(self._layers_desc, self._num_stages, seg_method).do_segment()
+        lo, hi = self.segment_parts[self._stage_id], self.segment_parts[self._stage_id + 1]
+        self._start, self._end = lo, hi
+        self.run_function = []
+        self.shared_layers = {}
+        self._shared_descs = {}
+        from ....nn.layer.container import LayerList
+        built = []
+        for i, d in enumerate(self._layers_desc[lo:hi]):
+            if isinstance(d, SharedLayerDesc):
+                if d.layer_name not in self.shared_layers:
+                    self.shared_layers[d.layer_name] = d.build_layer()
+                    self._shared_descs[d.layer_name] = d
+                layer = self.shared_layers[d.layer_name]
+                fn = (lambda l, f: (lambda x: f(l, x)))(layer, d.forward_func) if d.forward_func else layer
+                self.run_function.append(fn)
+            elif isinstance(d, LayerDesc):
+                layer = d.build_layer()
+                built.append(layer)
+                self.run_function.append(layer)
+            elif isinstance(d, Layer):
+                built.append(d)
+                self.run_function.append(d)
+            else:
+                self.run_function.append(d)
+        self.layers = LayerList(built)
+        self._shared_names = list(self.shared_layers.keys())
+        self._shared_comm = self._build_shared_comm()
+
+    def _build_shared_comm(self):
+        """Groups of stages that hold a copy of each shared layer (for grad all-reduce)."""
+        comm = {}
+        if self._num_stages == 1 or not dist.is_initialized():
+            return comm
+        keys = {}
+        for s in range(self._num_stages):
+            lo, hi = self.segment_parts[s], self.segment_parts[s + 1]
+            for d in self._layers_desc[lo:hi]:
+                if isinstance(d, SharedLayerDesc):
+                    keys.setdefault(d.layer_name, set()).add(s)
+        from ...communication import new_group
+        for k, stages in sorted(keys.items()):
+            stages = sorted(stages)
+            if len(stages) < 2:
+                continue
+            ranks = [self._hcg.get_rank_from_stage(s) for s in stages]
+            g = new_group(ranks)
+            if self._stage_id in stages:
+                comm[k] = g
+        return comm
+
+    def allreduce_shared_weight_gradients(self):
+        for k, g in self._shared_comm.items():
+            for p in self.shared_layers[k].parameters():
+                if p._t.grad is not None:
+                    dist.all_reduce(p._t.grad, group=g.pg)
+
+    def get_stage_from_index(self, layer_idx):
+        for s in range(self._num_stages):
+            if self.segment_parts[s] <= layer_idx < self.segment_parts[s + 1]:
+                return s
+        return self._num_stages - 1
+
+    def forward(self, input, chunk_id=None):  # noqa: A002
+        x = input
+        for i, f in enumerate(self.run_function):
+            if self._recompute_interval and self.training and i % self._recompute_interval == 0 and \
+                    isinstance(f, Layer) and any(not p.stop_gradient for p in f.parameters()):
+                from ..recompute import recompute
+                x = recompute(f, *(x if isinstance(x, tuple) else (x,)))
+            else:
+                x = f(*x) if isinstance(x, tuple) else f(x)
+        return x
+
+
+class PipelineParallel(Layer):
+    """Wraps a PipelineLayer; ``train_batch`` runs 1F1B over micro-batches."""
+
+    def __init__(self, layers, hcg, strategy):
+        super().__init__()
+        self._layers = layers
+        self._hcg = hcg
+        cfg = getattr(strategy, 'pipeline_configs', {}) or {}
+        self.accumulate_steps = int(cfg.get('accumulate_steps', 1))
+        self.micro_batch_size = cfg.get('micro_batch_size', None)
+        self.num_stages = hcg.get_pipe_parallel_world_size()
+        self.stage_id = hcg.get_stage_id()
+        self.pp_group = hcg.get_pipe_parallel_group()
+        self.is_first = self.stage_id == 0
+        self.is_last = self.stage_id == self.num_stages - 1
+        self._prev = hcg.prev_rank
+        self._next = hcg.next_rank
+        self._dp_group = hcg.get_data_parallel_group()
+        self._meta_fwd = None
+        self._meta_bwd = None
+        self.total_loss = None
+        self._sends = []
+
+    def forward(self, *a, **k):
+        return self._layers(*a, **k)
+
+    # ---- p2p helpers (metadata once, then raw tensors)
+    def _send_meta(self, t, peer):
+        meta = torch.tensor([len(t.shape)] + list(t.shape) + [_DT.index(t.dtype)], dtype=torch.int64)
+        meta = meta.to(t.device)
+        n = torch.tensor([meta.numel()], dtype=torch.int64, device=t.device)
+        self._isend(n, peer)
+        self._isend(meta, peer)
+
+    def _isend(self, t, peer):
+        """Sends never block the schedule: in steady 1F1B a stage sends an activation forward
+        while its neighbour sends a gradient back, so blocking sends would deadlock."""
+        self._sends.append((dist.isend(t, peer), t))
+
+    def _drain_sends(self):
+        for w, _ in self._sends:
+            w.wait()
+        self._sends = []
+
+    def _recv_meta(self, peer, dev):
+        n = torch.empty(1, dtype=torch.int64, device=dev)
+        dist.recv(n, peer)
+        meta = torch.empty(int(n.item()), dtype=torch.int64, device=dev)
+        dist.recv(meta, peer)
+        m = meta.tolist()
+        nd = m[0]
+        return tuple(m[1:1 + nd]), _DT[m[1 + nd]]
+
+    def _dev(self):
+        return torch.device('cuda', torch.cuda.current_device()) if torch.cuda.is_available() else torch.device('cpu')
+
+    def _split(self, data):
+        if isinstance(data, (list, tuple)):
+            parts = [self._split(d) for d in data]
+            return [tuple(p[i] for p in parts) for i in range(self.accumulate_steps)]
+        t = _unwrap(data)
+        return [_wrap(c) for c in t.chunk(self.accumulate_steps, 0)]
+
+    def _fwd_step(self, mb_input, mb_label):
+        dev = self._dev()
+        if self.is_first:
+            x = mb_input
+        else:
+            if self._meta_fwd is None:
+                self._meta_fwd = self._recv_meta(self._prev, dev)
+            shape, dt = self._meta_fwd
+            buf = torch.empty(shape, dtype=dt, device=dev)
+            dist.recv(buf, self._prev)
+            buf.requires_grad_(True)
+            x = _wrap(buf)
+        out = self._layers(x)
+        if self.is_last:
+            loss = self._layers._loss_fn(out, mb_label) if self._layers._loss_fn is not None else out
+            loss = _wrap(_unwrap(loss) / self.accumulate_steps)
+            return x, loss
+        o = _unwrap(out)
+        if not self._sent_meta:
+            self._send_meta(o, self._next)
+            self._sent_meta = True
+        self._isend(o.detach().contiguous(), self._next)
+        return x, out
+
+    def _bwd_step(self, x, out):
+        if self.is_last:
+            _unwrap(out).backward()
+        else:
+            o = _unwrap(out)
+            g = torch.empty_like(o)
+            dist.recv(g, self._next)
+            o.backward(g)
+        if not self.is_first:
+            gx = _unwrap(x).grad
+            self._isend(gx.contiguous(), self._prev)
+
+    def train_batch(self, data, optimizer, lr_scheduler=None, scaler=None):
+        inputs, labels = data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None)
+        mbs_in = self._split(inputs) if self.is_first else [None] * self.accumulate_steps
+        mbs_lab = self._split(labels) if (self.is_last and labels is not None) else [None] * self.accumulate_steps
+        self._sent_meta = False
+        self._meta_fwd = None
+        n = self.accumulate_steps
+        warm = min(self.num_stages - self.stage_id - 1, n)
+        pending = []
+        losses = []
+        fi = 0
+        for _ in range(warm):
+            x, out = self._fwd_step(mbs_in[fi], mbs_lab[fi])
+            pending.append((x, out))
+            if self.is_last:
+                losses.append(_unwrap(out).detach())
+            fi += 1
+        for _ in range(n - warm):
+            x, out = self._fwd_step(mbs_in[fi], mbs_lab[fi])
+            pending.append((x, out))
+            if self.is_last:
+                losses.append(_unwrap(out).detach())
+            fi += 1
+            self._bwd_step(*pending.pop(0))
+        while pending:
+            self._bwd_step(*pending.pop(0))
+        self._drain_sends()
+        self._layers.allreduce_shared_weight_gradients()
+        if self._dp_group is not None and self._dp_group.nranks > 1:
+            for p in self._layers.parameters():
+                if p._t.grad is not None:
+                    dist.all_reduce(p._t.grad, dist.ReduceOp.SUM, group=self._dp_group.pg)
+                    p._t.grad.div_(self._dp_group.nranks)
+        if scaler is not None:
+            scaler.step(optimizer)
+            scaler.update()
+        else:
+            optimizer.step()
+        optimizer.clear_grad()
+        if lr_scheduler is not None:
+            lr_scheduler.step()
+        # broadcast the mean loss from the last stage to every stage
+        dev = self._dev()
+        loss = torch.stack(losses).sum() if self.is_last else torch.zeros((), device=dev)
+        loss = loss.to(dev).float()
+        if self.num_stages > 1:
+            dist.broadcast(loss, self._hcg.get_rank_from_stage(self.num_stages - 1), group=self.pp_group.pg)
+        self.total_loss = _wrap(loss)
+        return self.total_loss
+
+    def eval_batch(self, data, compute_loss=True):
+        with torch.no_grad():
+            inputs, labels = data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None)
+            mbs_in = self._split(inputs) if self.is_first else [None] * self.accumulate_steps
+            mbs_lab = self._split(labels) if (self.is_last and labels is not None) else [None] * self.accumulate_steps
+            self._sent_meta = False
+            self._meta_fwd = None
+            outs = []
+            for i in range(self.accumulate_steps):
+                _, out = self._fwd_step(mbs_in[i], mbs_lab[i])
+                if self.is_last:
+                    outs.append(_unwrap(out))
+            self._drain_sends()
+            if self.is_last:
+                return _wrap(torch.stack(outs).sum() if compute_loss else torch.cat(outs))
+            return None
+
+
+_DT = [torch.float32, torch.float16, torch.bfloat16, torch.float64, torch.int64, torch.int32, torch.bool]

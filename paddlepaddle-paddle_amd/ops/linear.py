@@ -19,6 +19,8 @@ from ..parallel.flat_buffer import flat_grad_slot, notify_grad_ready
 class _LinearAccum(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, box):
+        if w.untyped_storage().nbytes() == 0:
+            raise RuntimeError("linear weight storage is released (sharding stage-3 unit not gathered)")
         x2 = x.reshape(-1, x.shape[-1])
         y = torch.addmm(b, x2, w) if b is not None else torch.mm(x2, w)
         ctx.save_for_backward(x2, w)

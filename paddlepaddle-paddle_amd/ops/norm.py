@@ -8,7 +8,14 @@ import torch
 from . import _native as N
 
 
+def _live(t, what):
+    if t is not None and t.untyped_storage().nbytes() == 0:
+        raise RuntimeError(f"{what} storage is released (a sharding stage-3 unit used outside its layer's forward?)")
+
+
 def _fwd(x, res, w, b, eps, rms):
+    _live(w, 'norm weight')
+    _live(b, 'norm bias')
     cols = x.shape[-1]
     x2 = x.contiguous()
     rows = x2.numel() // cols

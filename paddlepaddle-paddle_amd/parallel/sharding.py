@@ -124,7 +124,7 @@ class _PreBackward(torch.autograd.Function):
 
 class ShardingEngine:
     def __init__(self, model, level='p_g_os', group=None, bucket_mb=256, segment_size=2 ** 20,
-                 release_grads=True, persistent_types=None):
+                 release_grads=True, persistent_types=None, persistent_below=None):
         self.model = model
         self.level = LEVELS[level] if isinstance(level, str) else int(level)
         self.group = group
@@ -134,6 +134,10 @@ class ShardingEngine:
         self.release_grads = release_grads and self.level == 3
         from ..nn.layer.common import Embedding
         self.persistent_types = tuple(persistent_types or (Embedding,))
+        # units smaller than this stay materialised: gathering them saves nothing, and small
+        # layers (norms, heads) are the ones parent code tends to use outside their own forward
+        # (the reference likewise leaves parameters below segment_size unsliced, group_sharded_stage3.py)
+        self.persistent_below = segment_size if persistent_below is None else persistent_below
         self._broadcast_params()
         params = [p for p in model.parameters() if p._t.requires_grad or True]
         if self.level == 3:
@@ -199,7 +203,8 @@ class ShardingEngine:
                 seen.add(id(p))
                 by_dt.setdefault(p._t.dtype, []).append(p)
             for dt, ps in by_dt.items():
-                units.append(_Unit(self, ps, layer, persistent))
+                small = sum(p._t.numel() for p in ps) < self.persistent_below
+                units.append(_Unit(self, ps, layer, persistent or small))
 
         def visit(layer):
             n = count(layer)

@@ -1,0 +1,136 @@
+"""TP (mp=2), SP and PP (pp=2) workers: results must equal the single-device computation."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import paddle  # noqa: E402
+import paddle.distributed as dist  # noqa: E402
+import paddle.nn as nn  # noqa: E402
+from paddle.distributed import fleet  # noqa: E402
+
+
+def gather_full(t, axis):
+    parts = []
+    dist.all_gather(parts, t)
+    return torch.cat([p._t for p in parts], axis)
+
+
+def tp_test():
+    s = fleet.DistributedStrategy()
+    s.hybrid_configs = {'dp_degree': 1, 'mp_degree': 2, 'pp_degree': 1}
+    fleet.init(is_collective=True, strategy=s)
+    hcg = fleet.get_hybrid_communicate_group()
+    assert hcg.get_model_parallel_world_size() == 2
+    V, H, F = 16, 8, 12
+    paddle.seed(3 + hcg.get_model_parallel_rank())
+    emb = fleet.meta_parallel.VocabParallelEmbedding(V, H)
+    col = fleet.meta_parallel.ColumnParallelLinear(H, F, gather_output=False)
+    row = fleet.meta_parallel.RowParallelLinear(F, H, input_is_parallel=True)
+    ce = fleet.meta_parallel.ParallelCrossEntropy()
+    col_gather = fleet.meta_parallel.ColumnParallelLinear(H, V, gather_output=False)
+    ids = paddle.to_tensor(np.array([[1, 9, 15, 3]]))
+    h = emb(ids)
+    logits_sh = col_gather(row(paddle.nn.functional.relu(col(h))))
+    loss = ce(logits_sh, ids.unsqueeze(-1)).mean()
+    loss.backward()
+    # single-device reference from gathered full weights
+    We = gather_full(emb.weight, 0).detach().requires_grad_()
+    W1 = gather_full(col.weight, 1).detach().requires_grad_()
+    b1 = gather_full(col.bias, 0).detach().requires_grad_()
+    W2 = gather_full(row.weight, 0).detach().requires_grad_()
+    b2 = row.bias._t.detach().requires_grad_()
+    W3 = gather_full(col_gather.weight, 1).detach().requires_grad_()
+    b3 = gather_full(col_gather.bias, 0).detach().requires_grad_()
+    x = We[ids._t]
+    z = torch.relu(x @ W1 + b1) @ W2 + b2
+    lg = z @ W3 + b3
+    ref = torch.nn.functional.cross_entropy(lg.reshape(-1, V), ids._t.reshape(-1))
+    ref.backward()
+    assert abs(float(loss) - float(ref)) < 1e-5, (float(loss), float(ref))
+    r = hcg.get_model_parallel_rank()
+    np.testing.assert_allclose(col.weight.grad.numpy(), W1.grad.chunk(2, 1)[r].numpy(), atol=1e-5)
+    np.testing.assert_allclose(row.weight.grad.numpy(), W2.grad.chunk(2, 0)[r].numpy(), atol=1e-5)
+    np.testing.assert_allclose(emb.weight.grad.numpy(), We.grad.chunk(2, 0)[r].numpy(), atol=1e-5)
+    print(f"rank{dist.get_rank()} tp OK", flush=True)
+
+
+def sp_test():
+    s = fleet.DistributedStrategy()
+    s.hybrid_configs = {'dp_degree': 1, 'mp_degree': 2, 'pp_degree': 1}
+    fleet.init(is_collective=True, strategy=s)
+    from paddle.distributed.fleet.utils.sequence_parallel_utils import (ScatterOp, GatherOp,
+                                                                        ColumnSequenceParallelLinear,
+                                                                        RowSequenceParallelLinear)
+    paddle.seed(11)
+    S, B, H = 8, 2, 4
+    x_full = paddle.randn([S, B, H])
+    x_full.stop_gradient = False
+    paddle.seed(20 + dist.get_rank())
+    col = ColumnSequenceParallelLinear(H, 6, has_bias=True)
+    row = RowSequenceParallelLinear(6, H, has_bias=True)
+    xs = ScatterOp.apply(x_full)
+    y = GatherOp.apply(row(col(xs)))
+    y.sum().backward()
+    W1 = gather_full(col.weight, 1)
+    b1 = gather_full(col.bias, 0)
+    W2 = gather_full(row.weight, 0)
+    ref = (x_full._t @ W1 + b1) @ W2 + row.bias._t
+    np.testing.assert_allclose(y.numpy(), ref.detach().numpy(), atol=1e-5)
+    print(f"rank{dist.get_rank()} sp OK", flush=True)
+
+
+class Block(nn.Layer):
+    def __init__(self, d):
+        super().__init__()
+        self.fc = nn.Linear(d, d)
+
+    def forward(self, x):
+        return paddle.tanh(self.fc(x))
+
+
+def pp_test():
+    s = fleet.DistributedStrategy()
+    s.hybrid_configs = {'dp_degree': 1, 'mp_degree': 1, 'pp_degree': 2}
+    s.pipeline_configs = {'accumulate_steps': 4, 'micro_batch_size': 2}
+    fleet.init(is_collective=True, strategy=s)
+    d = 6
+    descs = [fleet.meta_parallel.LayerDesc(Block, d) for _ in range(4)]
+    loss_fn = lambda out, y: ((out - y) ** 2).mean()  # noqa: E731
+    # build the full reference on every rank with the same seed sequence
+    paddle.seed(5)
+    full = [Block(d) for _ in range(4)]
+    paddle.seed(5)
+    pl = fleet.meta_parallel.PipelineLayer(descs, num_stages=2, loss_fn=loss_fn)
+    stage = fleet.get_hybrid_communicate_group().get_stage_id()
+    # copy the reference weights of this stage's blocks so both start equal
+    for i, blk in enumerate(pl.run_function):
+        src = full[pl._start + i]
+        blk.fc.weight.set_value(src.fc.weight)
+        blk.fc.bias.set_value(src.fc.bias)
+    model = fleet.distributed_model(pl)
+    opt = paddle.optimizer.SGD(learning_rate=0.1, parameters=pl.parameters())
+    x = paddle.to_tensor(np.random.RandomState(0).randn(8, d).astype('float32'))
+    y = paddle.to_tensor(np.random.RandomState(1).randn(8, d).astype('float32'))
+    loss = model.train_batch([x, y], opt)
+    # reference: same 4 micro-batches, mean of per-micro-batch losses
+    ropt = paddle.optimizer.SGD(learning_rate=0.1, parameters=[p for b in full for p in b.parameters()])
+    tot = 0.0
+    for mb in range(4):
+        h = x[mb * 2:(mb + 1) * 2]
+        for b in full:
+            h = b(h)
+        l = loss_fn(h, y[mb * 2:(mb + 1) * 2]) / 4
+        l.backward()
+        tot += float(l)
+    ropt.step()
+    assert abs(float(loss) - tot) < 1e-5, (float(loss), tot)
+    for i, blk in enumerate(pl.run_function):
+        np.testing.assert_allclose(blk.fc.weight.numpy(), full[pl._start + i].fc.weight.numpy(), atol=1e-5)
+    print(f"rank{dist.get_rank()} pp OK stage{stage}", flush=True)
+
+
+if __name__ == '__main__':
+    {'tp': tp_test, 'sp': sp_test, 'pp': pp_test}[sys.argv[1]]()

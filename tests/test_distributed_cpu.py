@@ -32,3 +32,15 @@ def run_workers(script, *args, nproc=2, timeout=300):
 def test_dp_and_sharding_match_single_process(mode):
     out = run_workers('worker_dp_sharding.py', mode)
     assert out.count(f'{mode} OK') == 2
+
+
+@pytest.mark.parametrize("mode", ['tp', 'sp', 'pp'])
+def test_hybrid_parallel_matches_single_device(mode):
+    out = run_workers('worker_hybrid.py', mode)
+    assert out.count(f'{mode} OK') == 2, out[-3000:]
+
+
+@pytest.mark.parametrize("mode", ['os_g', 'p_g_os'])
+def test_gpt_sharding_matches_single_process(mode):
+    out = run_workers('worker_gpt_sharding.py', mode)
+    assert out.count(f"gpt {mode} OK") == 2, out[-3000:]
