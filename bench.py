@@ -108,8 +108,11 @@ def main():
         mcfg = {'model': 'resnet50', 'global_batch': B * world, 'image': '224x224 NHWC',
                 'parallelism': f"dp{world}", 'optimizer': 'Momentum'}
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         loss = step()
+        if rank == 0:  # progress on stderr; stdout carries only the JSON line
+            torch.cuda.synchronize()
+            print(f"warmup step {i} loss {float(loss.item()):.4f}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -44,6 +44,11 @@ def seed(s):
     return torch.default_generator
 
 
+def _host_seed():
+    """A 63-bit seed drawn from the global (paddle.seed-controlled) host generator."""
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
 def get_rng_state(device=None):
     from ..core.tensor import _wrap
     st = [_wrap(torch.get_rng_state())]
