@@ -78,9 +78,8 @@ class GPTAttention(nn.Layer):
         t = _unwrap(x)
         B, S, _ = t.shape
         qkv = _unwrap(self.qkv_proj(x)).view(B, S, 3, self.num_heads, self.head_dim)
-        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]  # strided BSHD views, no copies
-        o = F.flash_attention(_wrap(q), _wrap(k), _wrap(v), dropout=self.attn_dropout, causal=True,
-                              training=self.training)[0]
+        # packed: q/k/v are strided BSHD views for the kernel and dQ/dK/dV land in one buffer
+        o = F.flash_attn_qkvpacked(_wrap(qkv), dropout=self.attn_dropout, causal=True, training=self.training)[0]
         return self.out_proj(_wrap(_unwrap(o).reshape(B, S, -1)))
 
 

@@ -53,6 +53,9 @@ def flash_attn_qkvpacked(qkv, dropout=0.0, causal=False, return_softmax=False, *
                          rng_name="", training=True, name=None):
     t = _u(qkv)  # [b, s, 3, h, d] (reference packs as [b, s, nheads/nheads_k + 2, nheads_k, d])
     q, k, v = t[:, :, 0], t[:, :, 1], t[:, :, 2]
+    if (t.dim() == 5 and t.shape[2] == 3 and not return_softmax and (dropout == 0.0 or not training)
+            and ops.use_hip(t) and ops.flash_attn.supported(q, k, v)):
+        return _w(ops.flash_attn.flash_attention_packed(t, causal)), None
     return flash_attention(_w(q), _w(k), _w(v), dropout, causal, return_softmax, training=training)
 
 

@@ -158,20 +158,22 @@ class Adam(Optimizer):
                     self._flat = None
                     return super().step()
                 fb.sync_grads()
-            self._clip_flat()
+            scale = self._clip_flat()
             for ent in self._flat:
                 fb = ent['fb']
                 glr = lr * self._param_groups[ent['group']].get('learning_rate', 1.0)
                 lowp = fb.data if fb.dtype != torch.float32 else None
                 ops.optim.adamw_flat(ent['master'], fb.grad, ent['m1'], ent['m2'], lowp, glr, self._beta1,
-                                     self._beta2, self._epsilon, ent['coeff'], ent['b1p'], ent['b2p'])
+                                     self._beta2, self._epsilon, ent['coeff'], ent['b1p'], ent['b2p'],
+                                     grad_scale=scale)
                 ent['b1p'] *= self._beta1
                 ent['b2p'] *= self._beta2
         self._global_step += 1
 
     def _clip_flat(self):
-        """Global-norm clip over the flat gradient buffers: one sum-of-squares kernel per buffer,
-        one in-place scale per buffer (instead of per-parameter norm/scale launches)."""
+        """Global-norm clip over the flat gradient buffers: one sum-of-squares kernel per buffer;
+        the resulting scale is returned and applied inside the AdamW kernel's gradient read
+        (no separate scaling pass).  Non-global clips are applied eagerly and return None."""
         from ..nn.clip import ClipGradByGlobalNorm
         clips = {id(g.get('grad_clip', self._grad_clip)): g.get('grad_clip', self._grad_clip)
                  for g in self._param_groups}
@@ -192,9 +194,7 @@ class Adam(Optimizer):
             sq = s if sq is None else sq + s
         if clip._extra_sq_norm_fn is not None:
             sq = clip._extra_sq_norm_fn(sq)
-        scale = torch.clamp(clip.clip_norm / torch.clamp(sq.sqrt(), min=clip.clip_norm), max=1.0)
-        for fb in bufs:
-            fb.grad.mul_(scale.to(fb.grad.dtype))
+        return torch.clamp(clip.clip_norm / torch.clamp(sq.sqrt(), min=clip.clip_norm), max=1.0)
 
     def clear_grad(self, set_to_zero=True):
         if self._flat is None:

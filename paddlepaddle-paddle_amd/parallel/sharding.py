@@ -469,8 +469,11 @@ class ShardedOptimizer:
             return None
         sq = None
         for a in self.engine.arenas.values():
-            s = a['grad'].float().pow(2).sum()
+            g = a['grad']
+            s = ops.optim.sumsq(g) if ops.use_hip(g) else g.float().pow(2).sum()
             sq = s if sq is None else sq + s
+        if clip._extra_sq_norm_fn is not None:
+            sq = clip._extra_sq_norm_fn(sq)
         if self.engine.world > 1:
             dist.all_reduce(sq, group=self.engine.pg)
         norm = sq.sqrt()
@@ -486,7 +489,7 @@ class ShardedOptimizer:
         scale = self._clip_scale()
         for dt, a in self.engine.arenas.items():
             g = a['grad']
-            if scale is not None:
+            if scale is not None and not ops.use_hip(g):
                 g.mul_(scale.to(g.dtype))
             lowp = a['param'] if dt != torch.float32 else None
             for lo, hi, coeff in self._coeff_runs[dt]:
@@ -494,7 +497,8 @@ class ShardedOptimizer:
                     continue
                 if ops.use_hip(a['master']):
                     ops.optim.adamw_flat(a['master'][lo:hi], g[lo:hi], a['m'][lo:hi], a['v'][lo:hi],
-                                         None if lowp is None else lowp[lo:hi], lr, b1, b2, eps, coeff, b1p, b2p)
+                                         None if lowp is None else lowp[lo:hi], lr, b1, b2, eps, coeff, b1p, b2p,
+                                         grad_scale=scale)
                 else:
                     _adamw_ref(a['master'][lo:hi], g[lo:hi], a['m'][lo:hi], a['v'][lo:hi],
                                None if lowp is None else lowp[lo:hi], lr, b1, b2, eps, coeff, b1p, b2p)

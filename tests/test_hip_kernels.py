@@ -271,6 +271,19 @@ def test_flash_attention_strided_qkv_gqa():
     _close(qkv.grad, ref_in.grad, 6e-2, 2e-2, 'gqa grads')
 
 
+def test_flash_attention_packed_qkv():
+    B, S, H, D = 2, 512, 4, 128
+    qkv = torch.randn(B, S, 3, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = ops.flash_attn.flash_attention_packed(qkv, True)
+    ref_in = qkv.detach().float().requires_grad_()
+    orf = _attn_ref(ref_in[:, :, 0], ref_in[:, :, 1], ref_in[:, :, 2], True)
+    _close(o, orf, 2e-2, name='packed fwd')
+    g = torch.randn_like(orf)
+    o.backward(g.bfloat16())
+    orf.backward(g)
+    _close(qkv.grad, ref_in.grad, 6e-2, 2e-2, 'packed grads')
+
+
 def test_flash_attention_cross_lengths():
     B, H, D = 1, 2, 64
     q = torch.randn(B, 100, H, D, device=DEV, dtype=torch.bfloat16)

@@ -1,0 +1,44 @@
+"""Times csrc/flash_attn.hip fwd / fwd+bwd against torch SDPA (library) on GPT-1.3B shapes."""
+import sys
+import os
+import time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import paddle  # noqa: F401
+from paddle import ops
+from paddle.ops import _native
+_native._load()
+
+
+def timeit(fn, n=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(n):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / n
+
+
+def main():
+    for (B, S, H, D, causal) in [(16, 1024, 16, 128, True), (4, 4096, 16, 128, True), (16, 1024, 16, 128, False),
+                                 (8, 2048, 32, 64, True)]:
+        qkv = torch.randn(B, S, 3, H, D, device='cuda', dtype=torch.bfloat16, requires_grad=True)
+        flops = 4 * B * H * S * S * D * (0.5 if causal else 1.0)
+        o = ops.flash_attn.flash_attention_packed(qkv, causal)
+        g = torch.randn_like(o)
+        tf = timeit(lambda: ops.flash_attn.flash_attention_packed(qkv.detach(), causal))
+        tfb = timeit(lambda: ops.flash_attn.flash_attention_packed(qkv, causal).backward(g))
+        q, k, v = (qkv[:, :, i].transpose(1, 2).detach().clone().requires_grad_() for i in range(3))
+        ts = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q.detach(), k.detach(), v.detach(),
+                                                                              is_causal=causal))
+        gt = g.transpose(1, 2)
+        tsb = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=causal).backward(gt))
+        print(f"B{B} S{S} H{H} D{D} causal={causal}: ours fwd {tf*1e3:.3f} ms ({flops/tf/1e12:.0f} TF) "
+              f"fwd+bwd {tfb*1e3:.3f} ms ({3.5*flops/tfb/1e12:.0f} TF) | sdpa fwd {ts*1e3:.3f} ms "
+              f"({flops/ts/1e12:.0f} TF) fwd+bwd {tsb*1e3:.3f} ms ({3.5*flops/tsb/1e12:.0f} TF)", flush=True)
+
+
+if __name__ == '__main__':
+    main()
