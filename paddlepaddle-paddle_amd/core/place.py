@@ -100,6 +100,8 @@ def current_device():
         _current = _initial_device()
         if _current.type == 'cuda':
             torch.cuda.set_device(_current)
+            from ..ops.gemm_tuning import apply_tuned_db
+            apply_tuned_db()
     return _current
 
 

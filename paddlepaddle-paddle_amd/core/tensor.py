@@ -13,6 +13,8 @@ to unwrap and one object allocation to wrap.
 import itertools
 
 import numpy as np
+import weakref
+
 import torch
 
 from . import dtype as _dt
@@ -58,7 +60,11 @@ class Tensor:
 
     @property
     def shape(self):
-        return list(self._t.shape)
+        t = self._t
+        if t.is_meta:  # static-graph Variable: dynamic dims read as -1
+            from ..static.program import static_shape
+            return static_shape(t)
+        return list(t.shape)
 
     @property
     def ndim(self):
@@ -411,6 +417,9 @@ class Tensor:
         return repr(self)
 
 
+_PARAMS = weakref.WeakValueDictionary()  # id(storage tensor) -> Parameter (static programs map consts back)
+
+
 class Parameter(Tensor):
     """EagerParamBase: a trainable leaf (reference: python/paddle/base/framework.py EagerParamBase)."""
     __slots__ = ()
@@ -430,6 +439,7 @@ class Parameter(Tensor):
         d['need_clip'] = kw.get('need_clip', True)
         d['is_distributed'] = kw.get('is_distributed', False)
         d['_trainable'] = trainable
+        _PARAMS[id(t)] = self
 
     @property
     def trainable(self):

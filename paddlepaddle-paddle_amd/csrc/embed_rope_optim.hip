@@ -126,13 +126,42 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   }
 }
 
-// sum of squares of a flat buffer into out[blockIdx] (for global-norm clipping / found-inf check)
+// sum of squares of a flat buffer into out[blockIdx] (for global-norm clipping / found-inf check).
+// 16-byte vector loads (8 x 16-bit or 4 x f32 per lane), 4 in flight per lane; scalar head/tail
+// for a misaligned start or a ragged end.
 template <typename T>
 __global__ __launch_bounds__(256) void sumsq_kernel(const T* __restrict__ x, long long n, float* __restrict__ part) {
+  constexpr int V = 16 / sizeof(T);
   __shared__ float red[4];
   float s = 0.f;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    const float v = to_f(x[i]);
+  const long long head = min(n, (long long)((16 - ((uintptr_t)x & 15)) & 15) / (long long)sizeof(T));
+  const long long tid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long nthr = (long long)gridDim.x * 256;
+  if (tid < head) {
+    const float v = to_f(x[tid]);
+    s += v * v;
+  }
+  const T* xa = x + head;
+  const long long nv = (n - head) / V;
+  long long i = tid;
+  for (; i + 3 * nthr < nv; i += 4 * nthr) {
+    float a[4][V];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load_f<T, V>(xa + (i + u * nthr) * V, a[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < V; ++e) s += a[u][e] * a[u][e];
+  }
+  for (; i < nv; i += nthr) {
+    float a[V];
+    load_f<T, V>(xa + i * V, a);
+#pragma unroll
+    for (int e = 0; e < V; ++e) s += a[e] * a[e];
+  }
+  const long long t0 = head + nv * V;
+  if (t0 + tid < n) {
+    const float v = to_f(x[t0 + tid]);
     s += v * v;
   }
   s = block_sum<256>(s, red);
@@ -191,9 +220,9 @@ PA_API hipError_t pa_adamw(float* p, const void* g, float* m, float* v, void* lo
   return hipGetLastError();
 }
 
-PA_API int pa_sumsq_parts() { return 1024; }
+PA_API int pa_sumsq_parts() { return 2048; }
 
 PA_API hipError_t pa_sumsq(const void* x, long long n, float* part, int dt, hipStream_t st) {
-  PA_DISPATCH_DTYPE(dt, T, sumsq_kernel<T><<<1024, 256, 0, st>>>((const T*)x, n, part));
+  PA_DISPATCH_DTYPE(dt, T, sumsq_kernel<T><<<2048, 256, 0, st>>>((const T*)x, n, part));
   return hipGetLastError();
 }

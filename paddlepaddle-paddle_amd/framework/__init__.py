@@ -25,10 +25,14 @@ def in_pir_mode():
 
 def enable_static():
     _static_mode[0] = True
+    from ..static.program import _start_recording
+    _start_recording()
 
 
 def disable_static(place=None):
     _static_mode[0] = False
+    from ..static.program import _stop_recording
+    _stop_recording()
     if place is not None:
         from ..core.place import set_device
         set_device(place)

@@ -1,0 +1,288 @@
+"""Executor (reference: python/paddle/base/executor.py:1182 Executor.run; global_scope,
+scope_guard; compiler.py CompiledProgram/BuildStrategy).
+
+``run`` interprets a recorded Program on real device tensors: feeds bind data values, sentinel
+extents in recorded integer arguments are specialised to the fed shapes, parameters are read
+live, and backward/update nodes drive torch autograd + our optimizers.  Programs without a
+backward node run under no_grad.
+"""
+import contextlib
+
+import numpy as np
+import torch
+
+from ..core.tensor import Tensor, _wrap
+from .program import (Program, Ref, Const, default_main_program, default_startup_program, SENTINELS, _paused,
+                      _vid_of)
+
+
+class Scope:
+    def __init__(self):
+        self.vars = {}
+
+    def var(self, name):
+        return self.vars.setdefault(name, _ScopeVar(name))
+
+    def find_var(self, name):
+        from .program import default_main_program as _m
+        prog = _m()
+        if name in prog.named_vars or name in self.vars:
+            return self.vars.setdefault(name, _ScopeVar(name))
+        for p in prog.all_parameters():
+            if p.name == name:
+                v = _ScopeVar(name)
+                v._t = p
+                return v
+        return None
+
+
+class _ScopeVar:
+    def __init__(self, name):
+        self.name = name
+        self._t = None
+
+    def get_tensor(self):
+        return self._t
+
+    def set(self, value, place=None):
+        self._t = value
+
+
+_scope = [Scope()]
+
+
+def global_scope():
+    return _scope[-1]
+
+
+@contextlib.contextmanager
+def scope_guard(scope):
+    _scope.append(scope)
+    try:
+        yield
+    finally:
+        _scope.pop()
+
+
+class BuildStrategy:
+    def __init__(self):
+        self.fuse_elewise_add_act_ops = False
+        self.fuse_bn_act_ops = False
+        self.fuse_all_reduce_ops = True
+        self.enable_inplace = True
+        self.memory_optimize = True
+        self.build_cinn_pass = False
+        self.debug_graphviz_path = ''
+
+
+class ExecutionStrategy:
+    def __init__(self):
+        self.num_threads = 1
+        self.num_iteration_per_drop_scope = 100
+
+
+class CompiledProgram:
+    def __init__(self, program_or_graph, build_strategy=None):
+        self.program = program_or_graph
+        self.build_strategy = build_strategy or BuildStrategy()
+
+    def with_data_parallel(self, loss_name=None, build_strategy=None, exec_strategy=None, share_vars_from=None,
+                           places=None):
+        return self
+
+
+def _subst_int(v, smap):
+    if isinstance(v, bool) or v == 0 or not smap:
+        return v
+    out, rest = 1, v
+    hit = False
+    for s in SENTINELS:
+        while rest % s == 0 and s in smap:
+            rest //= s
+            out *= smap[s]
+            hit = True
+    return rest * out if hit else v
+
+
+def _resolve(prog, obj, env, smap, dev):
+    if isinstance(obj, Ref):
+        return env[obj.vid]
+    if isinstance(obj, Const):
+        return prog.consts[obj.cid]
+    if isinstance(obj, bool) or obj is None:
+        return obj
+    if isinstance(obj, int):
+        return _subst_int(obj, smap)
+    if isinstance(obj, torch.device):
+        return dev if obj.type == 'meta' else obj
+    if isinstance(obj, str) and obj == 'meta':
+        return dev
+    if isinstance(obj, torch.Size):
+        return torch.Size([_subst_int(x, smap) for x in obj])
+    if isinstance(obj, tuple) and hasattr(obj, '_fields'):
+        return type(obj)(*[_resolve(prog, o, env, smap, dev) for o in obj])
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_resolve(prog, o, env, smap, dev) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _resolve(prog, v, env, smap, dev) for k, v in obj.items()}
+    if isinstance(obj, slice):
+        return slice(_resolve(prog, obj.start, env, smap, dev), _resolve(prog, obj.stop, env, smap, dev),
+                     _resolve(prog, obj.step, env, smap, dev))
+    return obj
+
+
+def _bind(env, outs, val):
+    if outs is None:
+        return
+    if isinstance(outs, int):
+        env[outs] = val
+        return
+    for o, v in zip(outs, val):
+        _bind(env, o, v)
+
+
+def _feed_tensor(v, dt, dev):
+    if isinstance(v, Tensor):
+        t = v._t
+    elif isinstance(v, torch.Tensor):
+        t = v
+    else:
+        a = np.asarray(v)
+        t = torch.from_numpy(a) if a.dtype != np.object_ else torch.tensor(a.tolist())
+    return t.to(device=dev, dtype=dt)
+
+
+def _exec(prog, nodes, env, smap, dev):
+    for n in nodes:
+        if n.kind == 'torch':
+            args = _resolve(prog, n.args, env, smap, dev)
+            kwargs = _resolve(prog, n.kwargs, env, smap, dev)
+            if n.meta.get('factory') and 'device' in kwargs and kwargs['device'] is None:
+                kwargs['device'] = dev
+            _bind(env, n.outs, n.target(*args, **kwargs))
+        elif n.kind == 'minimize':
+            loss = env[n.args[0].vid]
+            loss.backward()
+            n.target.step()
+            n.target.clear_grad()
+        elif n.kind == 'backward':
+            loss = env[n.args[0].vid]
+            loss.backward()
+            params = n.kwargs['params']
+            _bind(env, n.outs, [p._t.grad if p._t.grad is not None else torch.zeros_like(p._t) for p in params])
+            for p in params:
+                p._t.grad = None
+        elif n.kind == 'grad':
+            ts = _resolve(prog, n.args[0], env, smap, dev)
+            xs = _resolve(prog, n.args[1], env, smap, dev)
+            gs = _resolve(prog, n.args[2], env, smap, dev)
+            gs = [g if g is not None else torch.ones_like(t) for g, t in zip(gs, ts)]
+            res = torch.autograd.grad(ts, xs, gs, retain_graph=True, allow_unused=True)
+            _bind(env, n.outs, [r if r is not None else torch.zeros_like(x) for r, x in zip(res, xs)])
+        elif n.kind == 'py':
+            args = _resolve(prog, n.args, env, smap, dev)
+            out = n.target(*[_wrap(a) if isinstance(a, torch.Tensor) else a for a in args])
+            out = out if isinstance(out, (list, tuple)) else [out]
+            _bind(env, n.outs, [o._t if isinstance(o, Tensor) else o for o in out])
+        elif n.kind == 'cond':
+            t_nodes, t_refs, f_nodes, f_refs = n.kwargs['branches']
+            take = bool(_resolve(prog, n.args[0], env, smap, dev).reshape(-1)[0].item())
+            nodes_, refs = (t_nodes, t_refs) if take else (f_nodes, f_refs)
+            _exec(prog, nodes_, env, smap, dev)
+            _bind(env, n.outs, [_resolve(prog, r, env, smap, dev) for r in refs])
+        elif n.kind == 'while':
+            cur = [_resolve(prog, r, env, smap, dev) for r in n.args]
+            c_nodes, c_ref = n.kwargs['cond']
+            b_nodes, b_refs = n.kwargs['body']
+            while True:
+                for vid, v in zip(n.kwargs['carried'], cur):
+                    env[vid] = v
+                _exec(prog, c_nodes, env, smap, dev)
+                if not bool(_resolve(prog, c_ref, env, smap, dev).reshape(-1)[0].item()):
+                    break
+                _exec(prog, b_nodes, env, smap, dev)
+                cur = [_resolve(prog, r, env, smap, dev) for r in b_refs]
+            _bind(env, n.outs, cur)
+        else:
+            raise RuntimeError(f"unknown node kind {n.kind}")
+
+
+def run_program(prog, feed, dev, grad=None):
+    """Interpret ``prog``; returns the value env."""
+    env = {}
+    smap = {}
+    feed = feed or {}
+    for name, (vid, shape, dt) in prog.feeds.items():
+        if name not in feed:
+            continue
+        t = _feed_tensor(feed[name], dt, dev)
+        if len(shape) == t.dim():
+            for i, s in enumerate(shape):
+                if s == -1:
+                    sent = SENTINELS[i]
+                    if sent in smap and smap[sent] != t.shape[i]:
+                        raise ValueError(f"feed '{name}' dim {i} = {t.shape[i]} conflicts with another feed's {smap[sent]}")
+                    smap[sent] = t.shape[i]
+                elif s != t.shape[i]:
+                    raise ValueError(f"feed '{name}' expects shape {shape}, got {list(t.shape)}")
+        env[vid] = t
+    needs_grad = grad if grad is not None else any(n.kind in ('minimize', 'backward', 'grad') for n in prog.nodes)
+    ctx = contextlib.nullcontext() if needs_grad else torch.no_grad()
+    with _paused(), ctx:
+        _exec(prog, prog.nodes, env, smap, dev)
+    return env
+
+
+class Executor:
+    def __init__(self, place=None):
+        from ..core.place import to_device
+        self.place = place
+        self._dev = to_device(place)
+
+    def run(self, program=None, feed=None, fetch_list=None, feed_var_name='feed', fetch_var_name='fetch', scope=None,
+            return_numpy=True, use_program_cache=False, return_merged=True, use_prune=False):
+        if isinstance(program, CompiledProgram):
+            program = program.program
+        if program is None:
+            program = default_main_program()
+        if not isinstance(program, Program):
+            raise TypeError("Executor.run expects a static Program")
+        if program is default_startup_program() or (not program.nodes and not program.feeds):
+            return []  # parameters are initialised when their layers are created
+        env = run_program(program, feed, self._dev)
+        fetch_list = fetch_list if fetch_list is not None else []
+        if not isinstance(fetch_list, (list, tuple)):
+            fetch_list = [fetch_list]
+        out = []
+        for f in fetch_list:
+            t = self._fetch(program, env, f)
+            if return_numpy:
+                t = t.detach()
+                out.append((t.float() if t.dtype == torch.bfloat16 else t).cpu().numpy())
+            else:
+                out.append(_wrap(t))
+        return out
+
+    @staticmethod
+    def _fetch(program, env, f):
+        if isinstance(f, str):
+            if f in program.named_vars:
+                f = program.named_vars[f]
+            else:
+                for p in program.all_parameters():
+                    if p.name == f:
+                        return p._t
+                raise KeyError(f"fetch target '{f}' not found in program")
+        tt = f._t if isinstance(f, Tensor) else f
+        if tt.is_meta:
+            return env[_vid_of(program, tt)]
+        return tt
+
+    def close(self):
+        pass
+
+    def train_from_dataset(self, *a, **k):
+        raise NotImplementedError("dataset-driven training uses paddle.io.DataLoader + Executor.run")
+
+
+ParallelExecutor = Executor

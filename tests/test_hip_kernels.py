@@ -322,3 +322,13 @@ def test_gpt_tiny_train_step_gpu():
         opt.clear_grad()
         losses.append(float(loss))
     assert losses[-1] < losses[0] - 0.5, losses
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("n,off", [(1, 0), (37, 3), (100003, 5), (1 << 22, 0)])
+def test_sumsq_vectorized(dt, n, off):
+    buf = torch.randn(n + off, device=DEV, dtype=dt)
+    x = buf[off:]
+    got = ops.optim.sumsq(x)
+    ref = x.float().pow(2).sum()
+    assert abs(float(got) - float(ref)) <= 1e-4 * float(ref) + 1e-5

@@ -1,0 +1,157 @@
+"""Static graph: Program recording, Executor training, control flow, inference-model IO."""
+import numpy as np
+import pytest
+
+import paddle
+import paddle.static as static
+
+
+@pytest.fixture
+def static_mode():
+    paddle.enable_static()
+    yield
+    paddle.disable_static()
+
+
+def test_static_mlp_trains_and_matches_dygraph(static_mode):
+    paddle.seed(7)
+    main, startup = static.Program(), static.Program()
+    with static.program_guard(main, startup):
+        x = static.data('x', [None, 8], 'float32')
+        y = static.data('y', [None, 1], 'int64')
+        assert x.shape == [-1, 8]
+        h = static.nn.fc(x, 16, activation='relu')
+        logits = static.nn.fc(h, 3)
+        loss = paddle.nn.functional.cross_entropy(logits, y.squeeze(-1)).mean() if False else \
+            paddle.nn.functional.cross_entropy(logits, y)
+        opt = paddle.optimizer.SGD(learning_rate=0.5)
+        opt.minimize(loss)
+    exe = static.Executor(paddle.CPUPlace())
+    exe.run(startup)
+    rng = np.random.RandomState(0)
+    xs = rng.randn(64, 8).astype('float32')
+    ys = (xs[:, :3].argmax(1)).reshape(-1, 1).astype('int64')
+    losses = []
+    for i in range(30):
+        lv, = exe.run(main, feed={'x': xs, 'y': ys}, fetch_list=[loss])
+        losses.append(float(lv))
+    assert losses[-1] < losses[0] * 0.7, losses
+    # a different batch size runs through the same program (sentinel re-specialisation)
+    out, = exe.run(main.clone(for_test=True), feed={'x': xs[:5], 'y': ys[:5]}, fetch_list=[logits])
+    assert out.shape == (5, 3)
+
+
+def test_static_reshape_with_dynamic_dims(static_mode):
+    main = static.Program()
+    with static.program_guard(main):
+        x = static.data('x', [None, None, 4], 'float32')
+        b, s = x.shape[0], x.shape[1]
+        assert (b, s) == (-1, -1)
+        y = x.reshape([-1, 4]) * 2.0
+        z = paddle.matmul(y, paddle.ones([4, 2]))
+        n = paddle.arange(0, 10)[:3]
+    exe = static.Executor(paddle.CPUPlace())
+    a = np.random.rand(3, 5, 4).astype('float32')
+    zv, nv = exe.run(main, feed={'x': a}, fetch_list=[z, n])
+    np.testing.assert_allclose(zv, (a.reshape(-1, 4) * 2) @ np.ones((4, 2)), rtol=1e-5)
+    assert nv.tolist() == [0, 1, 2]
+
+
+def test_static_cond_and_while(static_mode):
+    main = static.Program()
+    with static.program_guard(main):
+        x = static.data('x', [1], 'float32')
+        out = static.nn.cond(x.sum() > 0, lambda: x * 10, lambda: x - 10)
+        i = paddle.zeros([1], 'int64')
+        ten = paddle.full([1], 5, 'int64')
+        i_out, acc = static.nn.while_loop(lambda i, a: i < ten, lambda i, a: [i + 1, a + x], [i, x * 0])
+    exe = static.Executor(paddle.CPUPlace())
+    o1, a1 = exe.run(main, feed={'x': np.array([2.0], 'float32')}, fetch_list=[out, acc])
+    o2, = exe.run(main, feed={'x': np.array([-1.0], 'float32')}, fetch_list=[out])
+    assert o1.tolist() == [20.0] and o2.tolist() == [-11.0] and a1.tolist() == [10.0]
+
+
+def test_gradients_and_append_backward(static_mode):
+    main = static.Program()
+    with static.program_guard(main):
+        x = static.data('x', [3], 'float32')
+        x.stop_gradient = False
+        w = static.create_parameter([3], 'float32')
+        y = (x * x * w).sum()
+        gx, = static.gradients(y, [x])
+        pg = static.append_backward(y, parameter_list=[w])
+    exe = static.Executor(paddle.CPUPlace())
+    xv = np.array([1.0, 2.0, 3.0], 'float32')
+    g, gw = exe.run(main, feed={'x': xv}, fetch_list=[gx, pg[0][1]])
+    np.testing.assert_allclose(g, 2 * xv * w.numpy(), rtol=1e-5)
+    np.testing.assert_allclose(gw, xv * xv, rtol=1e-5)
+
+
+def test_save_load_inference_model(static_mode, tmp_path):
+    main = static.Program()
+    with static.program_guard(main):
+        x = static.data('img', [None, 1, 8, 8], 'float32')
+        c = static.nn.conv2d(x, 4, 3, padding=1, act='relu')
+        f = paddle.flatten(c, 1)
+        out = static.nn.fc(f, 5)
+        prob = paddle.nn.functional.softmax(out)
+    exe = static.Executor(paddle.CPUPlace())
+    a = np.random.rand(2, 1, 8, 8).astype('float32')
+    ref, = exe.run(main, feed={'img': a}, fetch_list=[prob])
+    prefix = str(tmp_path / 'infer' / 'model')
+    static.save_inference_model(prefix, [x], [prob], exe, program=main)
+    prog, feeds, fetches = static.load_inference_model(prefix, exe)
+    assert feeds == ['img']
+    got, = exe.run(prog, feed={'img': a}, fetch_list=fetches)
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
+    got3, = exe.run(prog, feed={'img': np.concatenate([a, a, a])}, fetch_list=fetches)
+    assert got3.shape == (6, 5)
+
+
+class _Net(paddle.nn.Layer):
+    def __init__(self):
+        super().__init__()
+        self.fc1 = paddle.nn.Linear(6, 12)
+        self.ln = paddle.nn.LayerNorm(12)
+        self.fc2 = paddle.nn.Linear(12, 3)
+
+    def forward(self, x):
+        h = paddle.nn.functional.gelu(self.ln(self.fc1(x)))
+        b, d = x.shape[0], h.shape[-1]
+        return paddle.nn.functional.softmax(self.fc2(h.reshape([b, d])), -1)
+
+
+def test_jit_to_static_save_load_roundtrip(tmp_path):
+    net = _Net()
+    net.eval()
+    snet = paddle.jit.to_static(net, input_spec=[static.InputSpec([None, 6], 'float32', 'x')])
+    x = paddle.randn([4, 6])
+    ref = snet(x)
+    prog = snet.forward.concrete_program.main_program
+    assert len(prog.nodes) > 3
+    path = str(tmp_path / 'net')
+    paddle.jit.save(snet, path)
+    loaded = paddle.jit.load(path)
+    out = loaded(x)
+    np.testing.assert_allclose(out.numpy(), ref.numpy(), rtol=1e-5, atol=1e-6)
+    out7 = loaded(paddle.randn([7, 6]))
+    assert out7.shape == [7, 3]
+    assert len(loaded.parameters()) == len(net.parameters())
+
+
+def test_inference_predictor(tmp_path):
+    net = _Net()
+    net.eval()
+    path = str(tmp_path / 'inf')
+    paddle.jit.save(net, path, input_spec=[static.InputSpec([None, 6], 'float32', 'x')])
+    from paddle import inference
+    cfg = inference.Config(path + '.pdmodel', path + '.pdiparams')
+    pred = inference.create_predictor(cfg)
+    names = pred.get_input_names()
+    h = pred.get_input_handle(names[0])
+    a = np.random.rand(2, 6).astype('float32')
+    h.reshape(a.shape)
+    h.copy_from_cpu(a)
+    pred.run()
+    o = pred.get_output_handle(pred.get_output_names()[0]).copy_to_cpu()
+    np.testing.assert_allclose(o, net(paddle.to_tensor(a)).numpy(), rtol=1e-5, atol=1e-6)

@@ -10,15 +10,28 @@ from paddle.ops import _native
 _native._load()
 
 
-def timeit(fn, n=20):
-    for _ in range(3):
-        fn()
+def timeit(fn, n=10):
+    """GPU time per call: n calls captured in one HIP graph, replayed and timed with events
+    (host launch overhead excluded)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(n):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(n):
-        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        g.replay()
+    e1.record()
     torch.cuda.synchronize()
-    return (time.perf_counter() - t) / n
+    return e0.elapsed_time(e1) / 1e3 / (5 * n)
 
 
 def main():
