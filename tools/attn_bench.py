@@ -10,6 +10,17 @@ from paddle.ops import _native
 _native._load()
 
 
+def timeit_plain(fn, n=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(n):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / n
+
+
 def timeit(fn, n=10):
     """GPU time per call: n calls captured in one HIP graph, replayed and timed with events
     (host launch overhead excluded)."""
@@ -42,12 +53,12 @@ def main():
         o = ops.flash_attn.flash_attention_packed(qkv, causal)
         g = torch.randn_like(o)
         tf = timeit(lambda: ops.flash_attn.flash_attention_packed(qkv.detach(), causal))
-        tfb = timeit(lambda: ops.flash_attn.flash_attention_packed(qkv, causal).backward(g))
+        tfb = timeit_plain(lambda: ops.flash_attn.flash_attention_packed(qkv, causal).backward(g))
         q, k, v = (qkv[:, :, i].transpose(1, 2).detach().clone().requires_grad_() for i in range(3))
         ts = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q.detach(), k.detach(), v.detach(),
                                                                               is_causal=causal))
         gt = g.transpose(1, 2)
-        tsb = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=causal).backward(gt))
+        tsb = timeit_plain(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=causal).backward(gt))
         print(f"B{B} S{S} H{H} D{D} causal={causal}: ours fwd {tf*1e3:.3f} ms ({flops/tf/1e12:.0f} TF) "
               f"fwd+bwd {tfb*1e3:.3f} ms ({3.5*flops/tfb/1e12:.0f} TF) | sdpa fwd {ts*1e3:.3f} ms "
               f"({flops/ts/1e12:.0f} TF) fwd+bwd {tsb*1e3:.3f} ms ({3.5*flops/tsb/1e12:.0f} TF)", flush=True)
