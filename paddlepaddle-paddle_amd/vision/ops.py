@@ -58,7 +58,8 @@ def nms(boxes, iou_threshold=0.3, scores=None, category_idxs=None, categories=No
         keep = _greedy_nms(bx, sc, iou_threshold)
     else:
         ci = _u(category_idxs)
-        cats = _u(categories).tolist() if categories is not None else ci.unique().tolist()
+        cats = (list(categories) if isinstance(categories, (list, tuple)) else _u(categories).tolist()) \
+            if categories is not None else ci.unique().tolist()
         parts = []
         for c in cats:
             idx = torch.nonzero(ci == c).squeeze(1)
