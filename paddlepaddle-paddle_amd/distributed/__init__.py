@@ -7,6 +7,55 @@ from .communication import (ReduceOp, Group, all_reduce, all_gather, all_gather_
 from .parallel import ParallelEnv, init_parallel_env, get_rank, get_world_size, spawn  # noqa: F401
 from ..parallel.data_parallel import DataParallel  # noqa: F401
 from . import sharding  # noqa: F401
+from . import watchdog  # noqa: F401
+
+
+def gloo_init_parallel_env(rank_id, rank_num, server_endpoint):
+    """CPU-side gloo group (reference: parallel.py gloo_init_parallel_env)."""
+    import torch.distributed as _d
+    host, port = server_endpoint.split(':')
+    if not _d.is_initialized():
+        _d.init_process_group('gloo', init_method=f"tcp://{host}:{port}", rank=rank_id, world_size=rank_num)
+
+
+def gloo_barrier():
+    import torch.distributed as _d
+    if _d.is_initialized():
+        _d.barrier()
+
+
+def gloo_release():
+    import torch.distributed as _d
+    if _d.is_initialized() and _d.get_backend() == 'gloo':
+        _d.destroy_process_group()
+
+
+class _PSOnly:
+    """Parameter-server datasets / sparse-table entries: out of scope for the collective design."""
+
+    def __init__(self, *a, **k):
+        raise NotImplementedError(f"{type(self).__name__} belongs to parameter-server mode, which this "
+                                  "MI355X collective framework does not implement")
+
+
+class InMemoryDataset(_PSOnly):
+    pass
+
+
+class QueueDataset(_PSOnly):
+    pass
+
+
+class CountFilterEntry(_PSOnly):
+    pass
+
+
+class ShowClickEntry(_PSOnly):
+    pass
+
+
+class ProbabilityEntry(_PSOnly):
+    pass
 import importlib as _il
 
 

@@ -1,0 +1,516 @@
+"""Semi-automatic parallelism (reference: python/paddle/distributed/auto_parallel/api.py —
+shard_tensor:131, dtensor_from_fn:545, reshard:579, shard_layer:678, ShardingStage1/2/3:1122+,
+shard_optimizer:1353, Strategy:1583, DistModel:1864, to_static:2345, unshard_dtensor:2506,
+shard_dataloader:2846; process_mesh.py ProcessMesh; placement_type.py Shard/Replicate/Partial).
+
+A distributed tensor here is a paddle Tensor holding this rank's *local* piece plus its
+``process_mesh``/``placements``/global shape.  ``reshard`` moves between placements with the
+collective that is cheapest on point-to-point xGMI — Shard→Replicate all-gather, Partial→
+Replicate all-reduce, Partial→Shard reduce-scatter, Shard(i)→Shard(j) all-to-all,
+Replicate→Shard a local slice (no traffic) — each issued on the mesh-dimension subgroup.
+"""
+import copy
+import itertools
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..core.tensor import Tensor, _wrap, _unwrap
+from ..nn.layer.layers import Layer
+
+
+# ----------------------------------------------------------------- placements
+class Placement:
+    def is_shard(self, dim=None):
+        return False
+
+    def is_replicated(self):
+        return False
+
+    def is_partial(self):
+        return False
+
+
+class Shard(Placement):
+    def __init__(self, dim):
+        self.dim = dim
+
+    def get_dim(self):
+        return self.dim
+
+    def is_shard(self, dim=None):
+        return dim is None or dim == self.dim
+
+    def __eq__(self, o):
+        return isinstance(o, Shard) and o.dim == self.dim
+
+    def __hash__(self):
+        return hash(('shard', self.dim))
+
+    def __repr__(self):
+        return f"Shard(dim={self.dim})"
+
+
+class Replicate(Placement):
+    def is_replicated(self):
+        return True
+
+    def __eq__(self, o):
+        return isinstance(o, Replicate)
+
+    def __hash__(self):
+        return hash('replicate')
+
+    def __repr__(self):
+        return "Replicate()"
+
+
+class ReduceType:
+    kRedSum = 0
+    kRedMax = 1
+    kRedMin = 2
+    kRedProd = 3
+    kRedAvg = 4
+    kRedAny = 5
+    kRedAll = 6
+
+
+class Partial(Placement):
+    def __init__(self, reduce_type=ReduceType.kRedSum):
+        self.reduce_type = reduce_type
+
+    def is_partial(self):
+        return True
+
+    def __eq__(self, o):
+        return isinstance(o, Partial) and o.reduce_type == self.reduce_type
+
+    def __hash__(self):
+        return hash(('partial', self.reduce_type))
+
+    def __repr__(self):
+        return f"Partial(reduce_type={self.reduce_type})"
+
+
+# ----------------------------------------------------------------- mesh
+_groups = {}
+
+
+class ProcessMesh:
+    def __init__(self, mesh=None, dim_names=None, shape=None, process_ids=None):
+        if mesh is None:
+            mesh = np.array(process_ids).reshape(shape)
+        self._mesh = np.array(mesh)
+        self._shape = list(self._mesh.shape)
+        self._process_ids = self._mesh.reshape(-1).tolist()
+        self._dim_names = list(dim_names) if dim_names is not None else [f"d{i}" for i in range(self._mesh.ndim)]
+
+    @property
+    def mesh(self):
+        return self._mesh
+
+    @property
+    def shape(self):
+        return list(self._shape)
+
+    @property
+    def ndim(self):
+        return len(self._shape)
+
+    @property
+    def process_ids(self):
+        return list(self._process_ids)
+
+    @property
+    def dim_names(self):
+        return list(self._dim_names)
+
+    def get_dim_size(self, dim):
+        if isinstance(dim, str):
+            dim = self._dim_names.index(dim)
+        return self._shape[dim]
+
+    def get_mesh_with_dim(self, dim_name, index=None):
+        d = self._dim_names.index(dim_name)
+        m = np.moveaxis(self._mesh, d, 0)
+        names = [self._dim_names[d]] + [n for i, n in enumerate(self._dim_names) if i != d]
+        if index is not None:
+            return ProcessMesh(m[index], names[1:])
+        return ProcessMesh(m, names)
+
+    def coord(self, rank):
+        idx = np.argwhere(self._mesh == rank)
+        return tuple(idx[0]) if len(idx) else None
+
+    def dim_group(self, dim, rank=None):
+        """The process group along mesh dim ``dim`` containing ``rank``."""
+        rank = dist.get_rank() if rank is None else rank
+        c = self.coord(rank)
+        sl = list(c)
+        sl[dim] = slice(None)
+        ranks = self._mesh[tuple(sl)].reshape(-1).tolist()
+        return _subgroup(ranks), ranks
+
+    def __contains__(self, rank):
+        return rank in self._process_ids
+
+    def __eq__(self, o):
+        return isinstance(o, ProcessMesh) and np.array_equal(o._mesh, self._mesh) and o._dim_names == self._dim_names
+
+    def __hash__(self):
+        return hash((tuple(self._process_ids), tuple(self._shape)))
+
+    def __repr__(self):
+        return f"ProcessMesh(shape={self._shape}, process_ids={self._process_ids}, dim_names={self._dim_names})"
+
+
+def _subgroup(ranks):
+    """Subgroups are created collectively: the first time any mesh-dim group is requested,
+    every rank creates the same set (all dims of all meshes seen so far are created on demand
+    by the caller in a deterministic order)."""
+    key = tuple(ranks)
+    if key not in _groups:
+        if dist.is_initialized() and len(ranks) == dist.get_world_size() and sorted(ranks) == list(range(len(ranks))):
+            _groups[key] = None  # world group
+        else:
+            _groups[key] = dist.new_group(list(ranks)) if dist.is_initialized() else None
+    return _groups[key]
+
+
+def _ensure_mesh_groups(mesh):
+    """Create every dim subgroup of ``mesh`` on every rank in a fixed order (new_group is collective)."""
+    for d in range(mesh.ndim):
+        other = [i for i in range(mesh.ndim) if i != d]
+        for idx in itertools.product(*[range(mesh.shape[i]) for i in other]):
+            sl = [slice(None)] * mesh.ndim
+            for i, v in zip(other, idx):
+                sl[i] = v
+            _subgroup(mesh.mesh[tuple(sl)].reshape(-1).tolist())
+
+
+# ----------------------------------------------------------------- dist tensors
+class DistAttr:
+    def __init__(self, mesh, sharding_specs):
+        self.process_mesh = mesh
+        self.sharding_specs = sharding_specs
+
+
+def _local_slice(t, mesh, placements, rank):
+    c = mesh.coord(rank)
+    for d, p in enumerate(placements):
+        if isinstance(p, Shard):
+            n = mesh.shape[d]
+            size = t.shape[p.dim]
+            chunk = (size + n - 1) // n
+            t = t.narrow(p.dim, min(c[d] * chunk, size), max(0, min(chunk, size - c[d] * chunk)))
+    return t
+
+
+def _attach(t, mesh, placements, global_shape):
+    w = t if isinstance(t, Tensor) else _wrap(t)
+    w.__dict__['process_mesh'] = mesh
+    w.__dict__['placements'] = list(placements)
+    w.__dict__['_global_shape'] = list(global_shape)
+    w.__dict__['is_dist'] = lambda: True
+    return w
+
+
+def is_dist_tensor(t):
+    return isinstance(t, Tensor) and 'process_mesh' in t.__dict__
+
+
+def shard_tensor(data, mesh, placements, dtype=None, place=None, stop_gradient=None):
+    """``data`` is the global value (identical on every rank); returns this rank's local piece."""
+    from ..core.tensor import to_tensor
+    t = data if isinstance(data, Tensor) else to_tensor(data, dtype=dtype)
+    _ensure_mesh_groups(mesh)
+    g = _unwrap(t)
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    local = _local_slice(g, mesh, placements, rank)
+    for d, p in enumerate(placements):
+        if isinstance(p, Partial) and mesh.coord(rank)[d] != 0:
+            local = torch.zeros_like(local)  # partial: value lives on coordinate 0 of that dim
+    out = _wrap(local.detach().clone().requires_grad_(g.requires_grad))
+    if isinstance(t, Tensor) and hasattr(t, 'trainable'):
+        from ..core.tensor import Parameter
+        out = Parameter(out._t, trainable=not t.stop_gradient, name=t.name)
+    if stop_gradient is not None:
+        out.stop_gradient = stop_gradient
+    return _attach(out, mesh, placements, g.shape)
+
+
+def dtensor_from_fn(fn, mesh, placements, *args, **kwargs):
+    return shard_tensor(fn(*args, **kwargs), mesh, placements)
+
+
+def _red(rt):
+    return {ReduceType.kRedSum: dist.ReduceOp.SUM, ReduceType.kRedMax: dist.ReduceOp.MAX,
+            ReduceType.kRedMin: dist.ReduceOp.MIN, ReduceType.kRedProd: dist.ReduceOp.PRODUCT,
+            ReduceType.kRedAvg: dist.ReduceOp.SUM}[rt]
+
+
+def _all_gather_dim(t, group, n, dim):
+    t = t.contiguous()
+    if n == 1:
+        return t
+    parts = [torch.empty_like(t) for _ in range(n)]
+    dist.all_gather(parts, t, group=group)
+    return torch.cat(parts, dim)
+
+
+def reshard(dist_tensor, mesh, placements):
+    t = _unwrap(dist_tensor)
+    src_mesh = dist_tensor.__dict__.get('process_mesh', mesh)
+    src = list(dist_tensor.__dict__.get('placements', [Replicate()] * mesh.ndim))
+    gshape = dist_tensor.__dict__.get('_global_shape', list(t.shape))
+    if src_mesh != mesh:
+        # cross-mesh: materialise the global value then re-slice (all ranks participate)
+        full = unshard_dtensor(dist_tensor)
+        return shard_tensor(full, mesh, placements)
+    _ensure_mesh_groups(mesh)
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    cur = t
+    for d in range(mesh.ndim):
+        s, dst = src[d], placements[d]
+        if s == dst:
+            continue
+        grp, ranks = mesh.dim_group(d, rank)
+        n = len(ranks)
+        if isinstance(s, Partial):
+            cur = cur.contiguous().clone()  # collectives below work in place; never touch the source
+            if isinstance(dst, Shard):
+                # reduce-scatter along dst.dim
+                chunks = list(cur.chunk(n, dst.dim))
+                out = torch.empty_like(chunks[ranks.index(rank)].contiguous())
+                dist.reduce_scatter(out, [c.contiguous() for c in chunks], op=_red(s.reduce_type), group=grp)
+                cur = out
+            else:
+                dist.all_reduce(cur, op=_red(s.reduce_type), group=grp)
+                if s.reduce_type == ReduceType.kRedAvg:
+                    cur = cur / n
+        elif isinstance(s, Shard):
+            if isinstance(dst, Replicate):
+                cur = _all_gather_dim(cur, grp, n, s.dim)
+            elif isinstance(dst, Shard):
+                # Shard(i) -> Shard(j): all-to-all
+                ins = [c.contiguous() for c in cur.chunk(n, dst.dim)]
+                outs = [torch.empty_like(ins[0]) for _ in range(n)]
+                from .communication import all_to_all_tensors
+                all_to_all_tensors(outs, ins, grp)
+                cur = torch.cat(outs, s.dim)
+            else:  # Shard -> Partial: keep on coordinate 0 after gathering
+                cur = _all_gather_dim(cur, grp, n, s.dim)
+                if ranks.index(rank) != 0:
+                    cur = torch.zeros_like(cur)
+        else:  # Replicate ->
+            if isinstance(dst, Shard):
+                size = cur.shape[dst.dim]
+                chunk = (size + n - 1) // n
+                i = ranks.index(rank)
+                cur = cur.narrow(dst.dim, min(i * chunk, size), max(0, min(chunk, size - i * chunk)))
+            elif isinstance(dst, Partial):
+                if ranks.index(rank) != 0:
+                    cur = torch.zeros_like(cur)
+        src[d] = dst
+    return _attach(_wrap(cur), mesh, placements, gshape)
+
+
+def unshard_dtensor(dist_tensor):
+    mesh = dist_tensor.__dict__.get('process_mesh')
+    if mesh is None:
+        return dist_tensor
+    r = reshard(dist_tensor, mesh, [Replicate()] * mesh.ndim)
+    out = _wrap(_unwrap(r))
+    return out
+
+
+# ----------------------------------------------------------------- layers / optimizers / data
+def shard_layer(layer, process_mesh, shard_fn=None, input_fn=None, output_fn=None):
+    """Calls ``shard_fn(name, sublayer, mesh)`` for every sublayer (default: replicate all
+    parameters), then wires optional input/output resharding hooks."""
+    def replicate_all(name, sub, mesh):
+        for pname, p in list(sub._parameters.items()):
+            if p is not None and not is_dist_tensor(p):
+                sub._parameters[pname] = shard_tensor(p, mesh, [Replicate()] * mesh.ndim)
+    fn = shard_fn or replicate_all
+    for name, sub in layer.named_sublayers(include_self=True):
+        fn(name, sub, process_mesh)
+    if shard_fn is not None:
+        for name, sub in layer.named_sublayers(include_self=True):
+            replicate_all(name, sub, process_mesh)
+    if input_fn is not None:
+        layer.register_forward_pre_hook(lambda lyr, inp: input_fn(inp, process_mesh))
+    if output_fn is not None:
+        layer.register_forward_post_hook(lambda lyr, inp, out: output_fn(out, process_mesh))
+    return layer
+
+
+class _ShardingStageBase:
+    def __init__(self, mesh=None, sharding_mesh_dim=None):
+        self._mesh = mesh
+        self._sharding_mesh_dim = sharding_mesh_dim
+
+
+class ShardingStage1(_ShardingStageBase):
+    level = 'os'
+
+
+class ShardingStage2(_ShardingStageBase):
+    level = 'os_g'
+
+
+class ShardingStage3(_ShardingStageBase):
+    level = 'p_g_os'
+
+
+class _ShardOptimizer:
+    """Optimizer whose replicated-parameter gradients are averaged over the data-parallel
+    mesh dim; with a ShardingStage the optimizer states are partitioned by our sharding engine."""
+
+    def __init__(self, optimizer, shard_fn=None):
+        self._inner_opt = optimizer
+        self._shard_fn = shard_fn
+        self._engine = None
+
+    def _sync_grads(self):
+        if not dist.is_initialized() or dist.get_world_size() == 1:
+            return
+        for p in self._inner_opt._parameter_list:
+            g = p._t.grad
+            if g is None:
+                continue
+            mesh = p.__dict__.get('process_mesh')
+            pl = p.__dict__.get('placements')
+            if mesh is None:
+                dist.all_reduce(g)
+                g.div_(dist.get_world_size())
+                continue
+            for d, pd in enumerate(pl):
+                if isinstance(pd, Replicate) and mesh.shape[d] > 1:
+                    grp, ranks = mesh.dim_group(d)
+                    dist.all_reduce(g, group=grp)
+                    g.div_(len(ranks))
+
+    def step(self):
+        self._sync_grads()
+        self._inner_opt.step()
+
+    def clear_grad(self, set_to_zero=True):
+        self._inner_opt.clear_grad(set_to_zero)
+
+    def __getattr__(self, name):
+        return getattr(self._inner_opt, name)
+
+
+def shard_optimizer(optimizer, shard_fn=None):
+    return _ShardOptimizer(optimizer, shard_fn)
+
+
+def shard_scaler(scaler):
+    return scaler
+
+
+class _ShardDataLoader:
+    def __init__(self, loader, meshes, input_keys=None, shard_dims=None, is_dataset_splitted=False):
+        self._loader = loader
+        self._meshes = meshes if isinstance(meshes, (list, tuple)) else [meshes]
+        self._shard_dims = shard_dims
+        self._split = is_dataset_splitted
+
+    def __len__(self):
+        return len(self._loader)
+
+    def __iter__(self):
+        mesh = self._meshes[0]
+        dim = self._shard_dims if isinstance(self._shard_dims, int) else 0
+        if isinstance(self._shard_dims, str):
+            dim = mesh.dim_names.index(self._shard_dims)
+        for batch in self._loader:
+            if self._split or not dist.is_initialized():
+                yield batch
+                continue
+            pl = [Replicate()] * mesh.ndim
+            pl[dim] = Shard(0)
+            items = batch if isinstance(batch, (list, tuple)) else [batch]
+            out = [shard_tensor(b, mesh, pl) if isinstance(b, Tensor) else b for b in items]
+            yield out if isinstance(batch, (list, tuple)) else out[0]
+
+
+def shard_dataloader(dataloader, meshes, input_keys=None, shard_dims=None, is_dataset_splitted=False):
+    return _ShardDataLoader(dataloader, meshes, input_keys, shard_dims, is_dataset_splitted)
+
+
+class Strategy:
+    """Config groups mirroring the reference's auto-parallel Strategy."""
+
+    class _Cfg(dict):
+        __getattr__ = dict.get
+
+        def __setattr__(self, k, v):
+            self[k] = v
+
+    def __init__(self, config=None):
+        config = config or {}
+        self.sharding = Strategy._Cfg(enable=False, stage=1, degree=8, **config.get('sharding', {}))
+        self.gradient_merge = Strategy._Cfg(enable=False, k_steps=1, avg=True, **config.get('gradient_merge', {}))
+        self.pipeline = Strategy._Cfg(enable=False, schedule_mode='1F1B', micro_batch_size=1, accumulate_steps=1,
+                                      **config.get('pipeline', {}))
+        self.amp = Strategy._Cfg(enable=False, dtype='bfloat16', level='O2', **config.get('amp', {}))
+        self.recompute = Strategy._Cfg(enable=False, **config.get('recompute', {}))
+        self.fused_passes = Strategy._Cfg(enable=False, fused_passes_list=[], **config.get('fused_passes', {}))
+
+
+class DistModel:
+    """``dist.to_static`` result: ``train()/eval()/predict()`` switch the mode; calling it runs
+    one step (forward + loss + backward + update in train mode)."""
+
+    def __init__(self, layer, loader, loss=None, optimizer=None, strategy=None, metrics=None):
+        self._layer = layer
+        self._loader = loader
+        self._loss = loss
+        self._opt = optimizer
+        self._strategy = strategy or Strategy()
+        self._mode = 'train' if optimizer is not None and loss is not None else 'predict'
+
+    def train(self):
+        self._mode = 'train'
+        self._layer.train()
+
+    def eval(self):
+        self._mode = 'eval'
+        self._layer.eval()
+
+    def predict(self):
+        self._mode = 'predict'
+        self._layer.eval()
+
+    def __call__(self, *args):
+        if self._mode == 'predict':
+            import torch as _t
+            with _t.no_grad():
+                return self._layer(*args)
+        inputs, labels = args[:-1], args[-1]
+        out = self._layer(*inputs)
+        loss = self._loss(out, labels)
+        if self._mode == 'train':
+            loss.backward()
+            self._opt.step()
+            self._opt.clear_grad()
+        return loss
+
+    def state_dict(self, mode='all'):
+        sd = dict(self._layer.state_dict())
+        if mode in ('all', 'opt') and self._opt is not None:
+            sd.update(self._opt.state_dict())
+        return sd
+
+    def set_state_dict(self, state_dict):
+        self._layer.set_state_dict(state_dict)
+
+
+def to_static(layer, loader=None, loss=None, optimizer=None, strategy=None, input_spec=None):
+    return DistModel(layer, loader, loss, optimizer, strategy)
+
+
+_ = (copy, Layer)

@@ -314,6 +314,26 @@ def gather(tensor, gather_list=None, dst=0, group=None, sync_op=True):
     return _ret(w, sync_op, post)
 
 
+def all_to_all_tensors(outs, ins, pg=None, async_op=False):
+    """torch all_to_all, with a P2P fallback for backends without it (gloo, CPU tests):
+    every pair exchanges its chunk with one batched isend/irecv round."""
+    if dist.get_backend(pg) != 'gloo':
+        return dist.all_to_all(outs, ins, group=pg, async_op=async_op)
+    me = dist.get_rank(pg)
+    n = dist.get_world_size(pg)
+    ranks = dist.get_process_group_ranks(pg) if pg is not None else list(range(n))
+    ops = []
+    for i in range(n):
+        if i == me:
+            outs[i].copy_(ins[i])
+            continue
+        ops.append(dist.P2POp(dist.isend, ins[i], ranks[i], group=pg))
+        ops.append(dist.P2POp(dist.irecv, outs[i], ranks[i], group=pg))
+    for w in dist.batch_isend_irecv(ops) if ops else []:
+        w.wait()
+    return None
+
+
 def alltoall(in_tensor_list, out_tensor_list, group=None, sync_op=True):
     ins = [_unwrap(x).contiguous() for x in in_tensor_list]
     if _single():
@@ -321,7 +341,7 @@ def alltoall(in_tensor_list, out_tensor_list, group=None, sync_op=True):
         out_tensor_list.extend(_wrap(x.clone()) for x in ins)
         return None
     outs = [torch.empty_like(x) for x in ins]
-    w = dist.all_to_all(outs, ins, group=_pg(group), async_op=not sync_op)
+    w = all_to_all_tensors(outs, ins, _pg(group), async_op=not sync_op)
 
     def post():
         out_tensor_list.clear()
@@ -400,6 +420,38 @@ def split(x, size, operation, axis=0, num_partitions=1, gather_out=True, weight_
 def convert_object_to_tensor(obj):
     data = np.frombuffer(pickle.dumps(obj), dtype=np.uint8)
     return _wrap(torch.from_numpy(data.copy())), _wrap(torch.tensor([data.size]))
+
+
+# ---- collective watchdog: every public collective registers with distributed/watchdog.py
+def _watched(fn):
+    import functools
+    from . import watchdog
+
+    @functools.wraps(fn)
+    def wrapper(*args, **kwargs):
+        if not watchdog.enabled() or _single():
+            return fn(*args, **kwargs)
+        grp = kwargs.get('group')
+        ranks = grp.ranks if isinstance(grp, Group) else list(range(get_world_size()))
+        first = next((a for a in args if hasattr(a, 'shape')), None)
+        tid = watchdog.begin(fn.__name__, ranks, first)
+        try:
+            r = fn(*args, **kwargs)
+        except BaseException:
+            watchdog.end(tid)
+            raise
+        if isinstance(r, _Task) and r._work is not None:
+            watchdog.attach(tid, r._work)
+        else:
+            watchdog.end(tid)
+        return r
+    return wrapper
+
+
+for _name in ('all_reduce', 'all_gather', 'all_gather_object', 'broadcast', 'broadcast_object_list', 'reduce',
+              'reduce_scatter', 'scatter', 'scatter_object_list', 'gather', 'alltoall', 'alltoall_single', 'send',
+              'recv', 'barrier'):
+    globals()[_name] = _watched(globals()[_name])
 
 
 class stream:

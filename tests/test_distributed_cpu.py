@@ -44,3 +44,27 @@ def test_hybrid_parallel_matches_single_device(mode):
 def test_gpt_sharding_matches_single_process(mode):
     out = run_workers('worker_gpt_sharding.py', mode)
     assert out.count(f"gpt {mode} OK") == 2, out[-3000:]
+
+
+def test_auto_parallel_reshard_and_dist_checkpoint(tmp_path):
+    os.environ['CKPT_DIR'] = str(tmp_path / 'ckpt')
+    out = run_workers('worker_auto_parallel.py')
+    assert out.count("auto_parallel OK") == 2, out[-3000:]
+
+
+def test_comm_watchdog_reports_stuck_collective():
+    out = run_workers('worker_watchdog.py', timeout=120)
+    assert out.count("watchdog OK") == 2, out[-3000:]
+
+
+def test_launch_module_spawns_workers(tmp_path):
+    script = tmp_path / 'w.py'
+    script.write_text("import os\nprint('worker', os.environ['RANK'], os.environ['PADDLE_TRAINERS_NUM'], "
+                      "os.environ['FLAGS_selected_gpus'], flush=True)\n")
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES='')
+    r = subprocess.run([sys.executable, '-m', 'paddle.distributed.launch', '--devices', '0,1', '--log_dir',
+                        str(tmp_path / 'log'), str(script)], env=env, capture_output=True, text=True, timeout=120,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert 'worker 0 2 0' in r.stdout
+    assert 'worker 1 2 1' in (tmp_path / 'log' / 'workerlog.1').read_text()

@@ -1,7 +1,9 @@
 """Offline GEMM tuning for the flagship bench (TunableOp), one shape at a time with progress.
 
-Step 1 (separate process): run bench.py with PYTORCH_TUNABLEOP_RECORD_UNTUNED=1 to list shapes.
-Step 2 (this script): tune each recorded GEMM line, writing the winners to the committed DB.
+Each recorded GEMM line (BLAS column-major m, n, k, transA/transB) is replayed as the torch
+row-major call that produced it — mm(X, Y) or addmm(bias, X, Y) with Y = op(A), X = op(B) —
+with tuning enabled, so TunableOp times every hipBLASLt/rocBLAS solution for that shape and
+keeps the fastest.  Winners are written to the DB after every shape.
 """
 import os
 import sys
@@ -14,18 +16,33 @@ lines = []
 with open(untuned) as f:
     for ln in f:
         if ln.startswith(("Gemm", "ScaledGemm")) and ln not in lines:
-            lines.append(ln)
+            lines.append(ln.strip())
 print(f"{len(lines)} GEMM shapes to tune", flush=True)
 t = torch.cuda.tunable
 t.enable(True)
 t.tuning_enable(True)
 t.set_filename(out)
-t.set_max_tuning_duration(int(os.environ.get('TUNE_MS', '8')))
+t.set_max_tuning_duration(int(os.environ.get('TUNE_MS', '10')))
 t.set_max_tuning_iterations(int(os.environ.get('TUNE_ITERS', '20')))
-torch.cuda.set_device(0)
+dt = {'BFloat16': torch.bfloat16, 'Half': torch.float16, 'float': torch.float32}
+dev = torch.device('cuda', 0)
 for i, ln in enumerate(lines):
     t0 = time.time()
-    t._process_single_offline_gemm(ln, 0)
+    op, rest = ln.split(',', 1)
+    sig, dtype_name, _ = (op.split('_') + [''])[:3]
+    dtype = dt[op.split('_')[1]]
+    trans = rest.split('_')[0]
+    m, n, k = (int(v) for v in rest.split('_')[1:4])
+    ta, tb = trans[0] == 't', trans[1] == 't'
+    a = torch.randn((m, k) if ta else (k, m), device=dev, dtype=dtype)
+    b = torch.randn((k, n) if tb else (n, k), device=dev, dtype=dtype)
+    Y = a.t() if ta else a
+    X = b.t() if tb else b
+    if sig == 'GemmAndBiasTunableOp':
+        torch.addmm(torch.randn(m, device=dev, dtype=dtype), X, Y)
+    else:
+        torch.mm(X, Y)
+    torch.cuda.synchronize()
     t.write_file()
-    print(f"[{i + 1}/{len(lines)}] {ln.strip()[:120]}  ({time.time() - t0:.1f}s)", flush=True)
+    print(f"[{i + 1}/{len(lines)}] {ln[:110]}  ({time.time() - t0:.1f}s)", flush=True)
 print("tuned; results in", out, flush=True)
