@@ -68,3 +68,8 @@ def test_launch_module_spawns_workers(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     assert 'worker 0 2 0' in r.stdout
     assert 'worker 1 2 1' in (tmp_path / 'log' / 'workerlog.1').read_text()
+
+
+def test_moe_expert_parallel_matches_single_process():
+    out = run_workers('worker_moe.py')
+    assert out.count("moe OK") == 2, out[-3000:]
