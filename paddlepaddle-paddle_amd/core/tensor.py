@@ -404,7 +404,7 @@ class Tensor:
     def __repr__(self):
         t = self._t.detach()
         body = np.array2string(np.asarray(t.float().cpu() if t.dtype == torch.bfloat16 else t.cpu()),
-                               separator=', ', precision=8, prefix='       ')
+                               separator=', ', precision=_print_precision(), prefix='       ')
         sg = 'True' if not self._t.requires_grad else 'False'
         return (f"Tensor(shape={self.shape}, dtype={_dt.dtype_name(t.dtype)}, place={self.place}, "
                 f"stop_gradient={sg},\n       {body})")
@@ -415,6 +415,11 @@ class Tensor:
         if self._t.dim() == 0:
             return format(self._t.item(), spec)
         return repr(self)
+
+
+def _print_precision():
+    from .printing import _opts
+    return _opts['precision']
 
 
 _PARAMS = weakref.WeakValueDictionary()  # id(storage tensor) -> Parameter (static programs map consts back)
