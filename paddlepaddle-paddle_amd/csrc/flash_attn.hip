@@ -61,20 +61,32 @@ __device__ __forceinline__ int lds_off(int row, int ch) {
 }
 
 // Stage helpers: a [64][D] tile of 16-bit elements, 256 threads, NLD 16-byte chunks per thread.
+// The per-thread address is computed once (init); a tile load adds one wave-uniform offset and,
+// for full tiles, skips the per-row bounds checks entirely.
 template <int D>
 struct Tile {
   static constexpr int CH = D / 8;               // 16-byte chunks per row
   static constexpr int NLD = 64 * CH / 256;      // chunks per thread
+  static constexpr int RPL = 256 / CH;           // rows covered by one pass of the block
   uint4 r[NLD];
-  __device__ __forceinline__ void load(const uint16_t* base, long long row_stride, int row0, int nrows) {
+  const uint16_t* p;
+  long long rs;
+  int row_in;
+  __device__ __forceinline__ void init(const uint16_t* base, long long row_stride) {
+    row_in = threadIdx.x / CH;
+    rs = row_stride;
+    p = base + (long long)row_in * row_stride + (threadIdx.x % CH) * 8;
+  }
+  __device__ __forceinline__ void load(int row0, int nrows) {
+    const uint16_t* q = p + (long long)row0 * rs;
+    if (row0 + 64 <= nrows) {
 #pragma unroll
-    for (int i = 0; i < NLD; ++i) {
-      const int c = threadIdx.x + 256 * i;
-      const int row = c / CH, ch = c % CH;
-      if (row0 + row < nrows)
-        r[i] = *reinterpret_cast<const uint4*>(base + (long long)(row0 + row) * row_stride + ch * 8);
-      else
-        r[i] = make_uint4(0, 0, 0, 0);
+      for (int i = 0; i < NLD; ++i) r[i] = *reinterpret_cast<const uint4*>(q + (long long)(RPL * i) * rs);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NLD; ++i)
+        r[i] = (row0 + row_in + RPL * i < nrows) ? *reinterpret_cast<const uint4*>(q + (long long)(RPL * i) * rs)
+                                                  : make_uint4(0, 0, 0, 0);
     }
   }
   template <bool TR>
@@ -87,6 +99,13 @@ struct Tile {
     }
   }
 };
+
+// raw v_exp_f32 (2^x): exp2(-inf) = 0; no denormal range fix-up (inputs are <= ~8 here)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// lazy rescale threshold (log2 units): the running max used as the exponent base is only moved
+// when a row's new max exceeds it by more than this, so most tiles skip the O/l rescale.
+constexpr float kRescaleTau = 8.0f;
 
 // A/B operand read: row `row`, d-range [32ks + 8g, +8) → 8 x 16-bit
 template <int D, bool TR>
@@ -172,9 +191,11 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
   const int nkb = kend > 0 ? (kend + 63) / 64 : 0;
 
   Tile<D> kt, vt;
+  kt.init(kbase, ks_.s);
+  vt.init(vbase, vs.s);
   if (nkb > 0) {
-    kt.load(kbase, ks_.s, 0, Sk);
-    vt.load(vbase, vs.s, 0, Sk);
+    kt.load(0, Sk);
+    vt.load(0, Sk);
   }
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * 64;
@@ -183,8 +204,8 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
     vt.template store<true>(v_lds);
     __syncthreads();
     if (kb + 1 < nkb) {
-      kt.load(kbase, ks_.s, k0 + 64, Sk);
-      vt.load(vbase, vs.s, k0 + 64, Sk);
+      kt.load(k0 + 64, Sk);
+      vt.load(k0 + 64, Sk);
     }
     // wave-uniform skip of key blocks fully above this wave's diagonal
     if (CAUSAL && k0 > qw0 + 31 + off) continue;
@@ -204,41 +225,61 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
         acc_s[1][j] = Mfma<T>::run(kf, qf[1][k], acc_s[1][j]);
       }
     }
-    // online softmax (log2 domain), per tile
-    s16x8 pf[2][2];
+    // online softmax in the log2 domain.  Masking only on tiles that touch the diagonal or the
+    // ragged end (wave-uniform test); the scale is folded into the exponent's FMA; the running
+    // max moves lazily (kRescaleTau) so the O/l rescale is skipped on most tiles.
+    const bool need_mask = (k0 + 64 > Sk) || (CAUSAL && k0 + 63 > qw0 + off);
+    if (need_mask) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int q = qw0 + 16 * t + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = k0 + 16 * j + 4 * g + r;
+            if ((key >= Sk) || (CAUSAL && key > q + off)) acc_s[t][j][r] = -INFINITY;
+          }
+      }
+    }
+    float mnew[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int q = qw0 + 16 * t + (lane & 15);
-      float mx = -INFINITY;
+      float mx = acc_s[t][0][0];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = k0 + 16 * j + 4 * g + r;
-          float s = acc_s[t][j][r] * scale_log2;
-          const bool masked = (key >= Sk) || (CAUSAL && key > q + off);
-          s = masked ? -INFINITY : s;
-          acc_s[t][j][r] = s;
-          mx = fmaxf(mx, s);
-        }
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc_s[t][j][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run[t], mx);
-      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float alpha = exp2f(m_run[t] - m_use);
-      m_run[t] = m_new;
+      mnew[t] = mx * scale_log2;
+    }
+    const bool bump = (mnew[0] > m_run[0] + kRescaleTau) || (mnew[1] > m_run[1] + kRescaleTau);
+    if (__ballot(bump) != 0ull) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const float m_upd = fmaxf(m_run[t], mnew[t]);
+        const float alpha = (m_upd == -INFINITY) ? 1.f : fast_exp2(m_run[t] - m_upd);
+        m_run[t] = m_upd;
+        l_run[t] *= alpha;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) acc_o[t][d] *= alpha;
+      }
+    }
+    s16x8 pf[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const float neg_m = (m_run[t] == -INFINITY) ? 0.f : -m_run[t];
       float ls = 0.f;
       float p[4][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          p[j][r] = exp2f(acc_s[t][j][r] - m_use);
+          p[j][r] = fast_exp2(__builtin_fmaf(acc_s[t][j][r], scale_log2, neg_m));
           ls += p[j][r];
         }
-      l_run[t] = l_run[t] * alpha + ls;
-#pragma unroll
-      for (int d = 0; d < DB; ++d) acc_o[t][d] *= alpha;
+      l_run[t] += ls;
       // P^T as B operand: k-step s covers keys 32s..32s+31; element j<4 → (16*(2s)+4g+j), j>=4 → (16*(2s+1)+4g+j-4)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -367,9 +408,11 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
   const float* dl_b = Delta + ((long long)b * Hq + h) * Sq;
 
   Tile<D> qt, dot;
+  qt.init(qbase, qs.s);
+  dot.init(dobase, dos.s);
   if (nqb > 0) {
-    qt.load(qbase, qs.s, qstart, Sq);
-    dot.load(dobase, dos.s, qstart, Sq);
+    qt.load(qstart, Sq);
+    dot.load(qstart, Sq);
   }
   for (int i = 0; i < nqb; ++i) {
     const int q0 = qstart + i * 64;
@@ -383,8 +426,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
     }
     __syncthreads();
     if (i + 1 < nqb) {
-      qt.load(qbase, qs.s, q0 + 64, Sq);
-      dot.load(dobase, dos.s, q0 + 64, Sq);
+      qt.load(q0 + 64, Sq);
+      dot.load(q0 + 64, Sq);
     }
     if (CAUSAL && q0 + 63 + off < kw) continue;  // whole query block above this wave's keys
 
@@ -407,14 +450,17 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
     }
     // P and dS, packed as B operands (k = query, permuted as in the forward)
     s16x8 pb[2], db_[2];
+    const bool need_mask = (q0 + 64 > Sq) || (kw + 16 > Sk) || (CAUSAL && kw + 15 > q0 + off);
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ql = 16 * m + 4 * g + r;
-        const int q = q0 + ql;
-        const bool masked = (q >= Sq) || (mykey >= Sk) || (CAUSAL && mykey > q + off);
-        const float p = masked ? 0.f : exp2f(acc_s[m][r] * scale_log2 - lse_lds[ql]);
+        float p = fast_exp2(__builtin_fmaf(acc_s[m][r], scale_log2, -lse_lds[ql]));
+        if (need_mask) {
+          const int q = q0 + ql;
+          if ((q >= Sq) || (mykey >= Sk) || (CAUSAL && mykey > q + off)) p = 0.f;
+        }
         const float ds = p * (acc_dp[m][r] - dl_lds[ql]);
         pb[m >> 1][(m & 1) * 4 + r] = f2s<T>(p);
         db_[m >> 1][(m & 1) * 4 + r] = f2s<T>(ds);
@@ -499,9 +545,11 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(
   if (CAUSAL) kend = min(Sk, q0 + 64 + off);
   const int nkb = kend > 0 ? (kend + 63) / 64 : 0;
   Tile<D> kt, vt;
+  kt.init(kbase, ks_.s);
+  vt.init(vbase, vs.s);
   if (nkb > 0) {
-    kt.load(kbase, ks_.s, 0, Sk);
-    vt.load(vbase, vs.s, 0, Sk);
+    kt.load(0, Sk);
+    vt.load(0, Sk);
   }
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * 64;
@@ -510,8 +558,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(
     vt.template store<false>(v_lds);
     __syncthreads();
     if (kb + 1 < nkb) {
-      kt.load(kbase, ks_.s, k0 + 64, Sk);
-      vt.load(vbase, vs.s, k0 + 64, Sk);
+      kt.load(k0 + 64, Sk);
+      vt.load(k0 + 64, Sk);
     }
     if (CAUSAL && k0 > qw + 15 + off) continue;
     f32x4 acc_s[4], acc_dp[4];
@@ -531,13 +579,16 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(
       }
     }
     s16x8 dsb[2];
+    const bool need_mask = (k0 + 64 > Sk) || (qw + 16 > Sq) || (CAUSAL && k0 + 63 > qw + off);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int key = k0 + 16 * j + 4 * g + r;
-        const bool masked = (key >= Sk) || (myq >= Sq) || (CAUSAL && key > myq + off);
-        const float p = masked ? 0.f : exp2f(acc_s[j][r] * scale_log2 - lse2);
+        float p = fast_exp2(__builtin_fmaf(acc_s[j][r], scale_log2, -lse2));
+        if (need_mask) {
+          const int key = k0 + 16 * j + 4 * g + r;
+          if ((key >= Sk) || (myq >= Sq) || (CAUSAL && key > myq + off)) p = 0.f;
+        }
         dsb[j >> 1][(j & 1) * 4 + r] = f2s<T>(p * (acc_dp[j][r] - dlt));
       }
     }

@@ -24,6 +24,17 @@ t.tuning_enable(True)
 t.set_filename(out)
 t.set_max_tuning_duration(int(os.environ.get('TUNE_MS', '10')))
 t.set_max_tuning_iterations(int(os.environ.get('TUNE_ITERS', '20')))
+
+
+def _write_partial(path):
+    """Progress snapshot (TunableOp itself writes the final table at process exit)."""
+    with open(path, 'w') as f:
+        for k, v in t.get_validators():
+            f.write(f"Validator,{k},{v}\n")
+        for r in t.get_results():
+            f.write(','.join(str(x) for x in r) + '\n')
+
+
 dt = {'BFloat16': torch.bfloat16, 'Half': torch.float16, 'float': torch.float32}
 dev = torch.device('cuda', 0)
 for i, ln in enumerate(lines):
@@ -43,6 +54,6 @@ for i, ln in enumerate(lines):
     else:
         torch.mm(X, Y)
     torch.cuda.synchronize()
-    t.write_file()
+    _write_partial(out + '.partial')
     print(f"[{i + 1}/{len(lines)}] {ln[:110]}  ({time.time() - t0:.1f}s)", flush=True)
 print("tuned; results in", out, flush=True)

@@ -12,4 +12,4 @@ ls gpurun_out/
 UNT=$(ls gpurun_out/untuned*.csv | head -1)
 wc -l $UNT
 timeout -k 10 1000 python tools/tune_gemms.py $UNT $OUT || { echo "tune failed"; exit 1; }
-cp $OUT gpurun_out/configs/
+ls -la paddlepaddle-paddle_amd/configs/; cp $OUT* gpurun_out/configs/
