@@ -53,6 +53,21 @@ class FlatBuffer:
                 p.__dict__['_flat'] = (self, o)
         self.attach_grads()
 
+    def alias_into(self, data_view, grad_view):
+        """Move this buffer's storage into caller-provided views (e.g. slices of one larger
+        arena) and re-point every parameter / gradient at them."""
+        assert data_view.numel() == self.numel and grad_view.numel() == self.numel
+        with torch.no_grad():
+            data_view.copy_(self.data)
+            grad_view.copy_(self.grad)
+            self.data, self.grad = data_view, grad_view
+            for p, o in zip(self.params, self.offsets):
+                req = p._t.requires_grad
+                p._t.data = self.data[o:o + p._t.numel()].view(p._t.shape)
+                if req:
+                    p._t.requires_grad_(True)
+        self.attach_grads()
+
     def attach_grads(self):
         for p, o in zip(self.params, self.offsets):
             if p._t.requires_grad:

@@ -131,7 +131,10 @@ class ShardingEngine:
         self.pg = _pg(group)
         self.world = dist.get_world_size(self.pg) if dist.is_initialized() else 1
         self.rank = dist.get_rank(self.pg) if dist.is_initialized() else 0
-        self.release_grads = release_grads and self.level == 3
+        # one rank: the "shard" is the whole buffer, so units alias the optimizer arenas and
+        # nothing is ever released, gathered or copied (no degenerate collectives either)
+        self.alias = self.world == 1
+        self.release_grads = release_grads and self.level == 3 and not self.alias
         from ..nn.layer.common import Embedding
         self.persistent_types = tuple(persistent_types or (Embedding,))
         # units smaller than this stay materialised: gathering them saves nothing, and small
@@ -204,7 +207,7 @@ class ShardingEngine:
                 by_dt.setdefault(p._t.dtype, []).append(p)
             for dt, ps in by_dt.items():
                 small = sum(p._t.numel() for p in ps) < self.persistent_below
-                units.append(_Unit(self, ps, layer, persistent or small))
+                units.append(_Unit(self, ps, layer, persistent or small or self.alias))
 
         def visit(layer):
             n = count(layer)
@@ -239,12 +242,16 @@ class ShardingEngine:
             n = a['size']
             dev = a['units'][0].fb.data.device
             a['param'] = torch.empty(n, dtype=dt, device=dev)
+            a['grad'] = torch.zeros(n, dtype=dt, device=dev)
             for u in a['units']:
-                a['param'][u.arena_off:u.arena_off + u.L].copy_(u.shard(u.fb.data))
+                if self.alias:
+                    u.fb.alias_into(a['param'][u.arena_off:u.arena_off + u.L],
+                                    a['grad'][u.arena_off:u.arena_off + u.L])
+                else:
+                    a['param'][u.arena_off:u.arena_off + u.L].copy_(u.shard(u.fb.data))
             a['master'] = a['param'].float().clone() if dt != torch.float32 else a['param']
             a['m'] = torch.zeros(n, dtype=torch.float32, device=dev)
             a['v'] = torch.zeros(n, dtype=torch.float32, device=dev)
-            a['grad'] = torch.zeros(n, dtype=dt, device=dev)
             a['b1p'] = None
 
     def pshard(self, u):
@@ -339,6 +346,9 @@ class ShardingEngine:
 
     # ------------------------------------------------------------------ gradient reduction
     def _reduce_scatter(self, u):
+        if self.alias:
+            u.rs_work = None  # gradients already live in the arena
+            return
         if self.world == 1:
             u.rs_work = None
             self._accumulate_shard(u, u.shard(u.fb.grad))
@@ -373,7 +383,8 @@ class ShardingEngine:
                 if not self.grad_fresh:
                     self.gshard(u).add_(u._rs_out)
             u.pending = sum(1 for p in u.params if p._t.requires_grad)
-            u.fb.grad.zero_() if u.grad_live and not self.release_grads else None
+            if u.grad_live and not self.release_grads and not self.alias:
+                u.fb.grad.zero_()
             u.free_grads()
             u.free_params()
         self.grad_fresh = False
