@@ -122,6 +122,8 @@ class _Fleet:
             return model
         mode = hcg.get_parallel_mode()
         if mode == ParallelMode.PIPELINE_PARALLEL:
+            if getattr(model, 'get_num_virtual_stages', lambda: 1)() > 1:
+                return meta_parallel.PipelineParallelWithInterleave(model, hcg, self._strategy)
             return meta_parallel.PipelineParallel(model, hcg, self._strategy)
         if mode == ParallelMode.TENSOR_PARALLEL or mode == ParallelMode.SEGMENT_PARALLEL:
             return meta_parallel.TensorParallel(model, hcg, self._strategy)

@@ -76,14 +76,30 @@ class PipelineLayer(Layer):
         self._loss_fn = loss_fn
         self._recompute_interval = recompute_interval
         self._layers_desc = list(layers)
-        self.segment_parts = SegmentLayers(self._layers_desc, self._num_stages, seg_method).do_segment()
-        lo, hi = self.segment_parts[self._stage_id], self.segment_parts[self._stage_id + 1]
+        self._num_virtual = int(num_virtual_pipeline_stages or 1)
+        nparts = self._num_stages * self._num_virtual
+        self.segment_parts = SegmentLayers(self._layers_desc, nparts, seg_method).do_segment()
+        # virtual stage k of this rank is global chunk (k * num_stages + stage_id)
+        self._chunk_ranges = [(self.segment_parts[k * self._num_stages + self._stage_id],
+                               self.segment_parts[k * self._num_stages + self._stage_id + 1])
+                              for k in range(self._num_virtual)]
+        lo, hi = self._chunk_ranges[0]
         self._start, self._end = lo, hi
         self.run_function = []
+        self._chunks = []
         self.shared_layers = {}
         self._shared_descs = {}
         from ....nn.layer.container import LayerList
         built = []
+        for lo_k, hi_k in self._chunk_ranges:
+            start = len(self.run_function)
+            self._build_range(lo_k, hi_k, built)
+            self._chunks.append(self.run_function[start:])
+        self.layers = LayerList(built)
+        self._shared_names = list(self.shared_layers.keys())
+        self._shared_comm = self._build_shared_comm()
+
+    def _build_range(self, lo, hi, built):
         for i, d in enumerate(self._layers_desc[lo:hi]):
             if isinstance(d, SharedLayerDesc):
                 if d.layer_name not in self.shared_layers:
@@ -101,9 +117,9 @@ class PipelineLayer(Layer):
                 self.run_function.append(d)
             else:
                 self.run_function.append(d)
-        self.layers = LayerList(built)
-        self._shared_names = list(self.shared_layers.keys())
-        self._shared_comm = self._build_shared_comm()
+
+    def get_num_virtual_stages(self):
+        return self._num_virtual
 
     def _build_shared_comm(self):
         """Groups of stages that hold a copy of each shared layer (for grad all-reduce)."""
@@ -111,8 +127,9 @@ class PipelineLayer(Layer):
         if self._num_stages == 1 or not dist.is_initialized():
             return comm
         keys = {}
-        for s in range(self._num_stages):
-            lo, hi = self.segment_parts[s], self.segment_parts[s + 1]
+        for part in range(len(self.segment_parts) - 1):
+            s = part % self._num_stages
+            lo, hi = self.segment_parts[part], self.segment_parts[part + 1]
             for d in self._layers_desc[lo:hi]:
                 if isinstance(d, SharedLayerDesc):
                     keys.setdefault(d.layer_name, set()).add(s)
@@ -141,7 +158,8 @@ class PipelineLayer(Layer):
 
     def forward(self, input, chunk_id=None):  # noqa: A002
         x = input
-        for i, f in enumerate(self.run_function):
+        funcs = self._chunks[chunk_id] if chunk_id is not None else self.run_function
+        for i, f in enumerate(funcs):
             if self._recompute_interval and self.training and i % self._recompute_interval == 0 and \
                     isinstance(f, Layer) and any(not p.stop_gradient for p in f.parameters()):
                 from ..recompute import recompute
@@ -316,6 +334,89 @@ class PipelineParallel(Layer):
             if self.is_last:
                 return _wrap(torch.stack(outs).sum() if compute_loss else torch.cat(outs))
             return None
+
+
+class PipelineParallelWithInterleave(PipelineParallel):
+    """Virtual pipeline stages (reference: pipeline_parallel.py PipelineParallelWithInterleave):
+    rank r holds global chunks r, r+P, r+2P, ...; activations travel rank 0 → P-1 and wrap to
+    rank 0's next chunk.  Work items run breadth-first — all micro-batches through virtual
+    chunk 0, then chunk 1, ... (backward in reverse) — which every rank executes in the same
+    global order, so asynchronous sends and blocking receives cannot deadlock; numerics equal
+    the non-interleaved schedule (gradients accumulate over micro-batches)."""
+
+    def _peer(self, delta):
+        s = (self.stage_id + delta) % self.num_stages
+        return self._hcg.get_rank_from_stage(s)
+
+    def _send(self, t, peer):
+        self._send_meta(t, peer)
+        self._isend(t.detach().contiguous(), peer)
+
+    def _recv(self, peer, dev):
+        shape, dt = self._recv_meta(peer, dev)
+        buf = torch.empty(shape, dtype=dt, device=dev)
+        dist.recv(buf, peer)
+        return buf
+
+    def train_batch(self, data, optimizer, lr_scheduler=None, scaler=None):
+        inputs, labels = data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None)
+        n, V, P = self.accumulate_steps, self._layers.get_num_virtual_stages(), self.num_stages
+        first_rank, last_rank = self.is_first, self.is_last
+        mbs_in = self._split(inputs) if first_rank else [None] * n
+        mbs_lab = self._split(labels) if (last_rank and labels is not None) else [None] * n
+        dev = self._dev()
+        prev_rank, next_rank = self._peer(-1), self._peer(+1)
+        saved = {}
+        losses = []
+        for v in range(V):
+            for m in range(n):
+                if first_rank and v == 0:
+                    x = mbs_in[m]
+                else:
+                    buf = self._recv(prev_rank, dev)
+                    buf.requires_grad_(True)
+                    x = _wrap(buf)
+                out = self._layers(x, chunk_id=v)
+                if last_rank and v == V - 1:
+                    loss = self._layers._loss_fn(out, mbs_lab[m]) if self._layers._loss_fn is not None else out
+                    loss = _wrap(_unwrap(loss) / n)
+                    losses.append(_unwrap(loss).detach())
+                    saved[(v, m)] = (x, loss)
+                else:
+                    self._send(_unwrap(out), next_rank)
+                    saved[(v, m)] = (x, out)
+        for v in reversed(range(V)):
+            for m in range(n):
+                x, out = saved.pop((v, m))
+                if last_rank and v == V - 1:
+                    _unwrap(out).backward()
+                else:
+                    o = _unwrap(out)
+                    g = self._recv(next_rank, dev)
+                    o.backward(g)
+                if not (first_rank and v == 0):
+                    self._send(_unwrap(x).grad, prev_rank)
+        self._drain_sends()
+        self._layers.allreduce_shared_weight_gradients()
+        if self._dp_group is not None and self._dp_group.nranks > 1:
+            for p in self._layers.parameters():
+                if p._t.grad is not None:
+                    dist.all_reduce(p._t.grad, dist.ReduceOp.SUM, group=self._dp_group.pg)
+                    p._t.grad.div_(self._dp_group.nranks)
+        if scaler is not None:
+            scaler.step(optimizer)
+            scaler.update()
+        else:
+            optimizer.step()
+        optimizer.clear_grad()
+        if lr_scheduler is not None:
+            lr_scheduler.step()
+        loss = torch.stack(losses).sum() if last_rank else torch.zeros((), device=dev)
+        loss = loss.to(dev).float()
+        if P > 1:
+            dist.broadcast(loss, self._hcg.get_rank_from_stage(P - 1), group=self.pp_group.pg)
+        self.total_loss = _wrap(loss)
+        return self.total_loss
 
 
 _DT = [torch.float32, torch.float16, torch.bfloat16, torch.float64, torch.int64, torch.int32, torch.bool]

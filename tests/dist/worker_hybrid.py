@@ -91,7 +91,7 @@ class Block(nn.Layer):
         return paddle.tanh(self.fc(x))
 
 
-def pp_test():
+def pp_test(virtual=1):
     s = fleet.DistributedStrategy()
     s.hybrid_configs = {'dp_degree': 1, 'mp_degree': 1, 'pp_degree': 2}
     s.pipeline_configs = {'accumulate_steps': 4, 'micro_batch_size': 2}
@@ -103,11 +103,13 @@ def pp_test():
     paddle.seed(5)
     full = [Block(d) for _ in range(4)]
     paddle.seed(5)
-    pl = fleet.meta_parallel.PipelineLayer(descs, num_stages=2, loss_fn=loss_fn)
+    pl = fleet.meta_parallel.PipelineLayer(descs, num_stages=2, loss_fn=loss_fn,
+                                           num_virtual_pipeline_stages=virtual)
     stage = fleet.get_hybrid_communicate_group().get_stage_id()
     # copy the reference weights of this stage's blocks so both start equal
-    for i, blk in enumerate(pl.run_function):
-        src = full[pl._start + i]
+    owned = [i for lo, hi in pl._chunk_ranges for i in range(lo, hi)]
+    for blk, gi in zip(pl.run_function, owned):
+        src = full[gi]
         blk.fc.weight.set_value(src.fc.weight)
         blk.fc.bias.set_value(src.fc.bias)
     model = fleet.distributed_model(pl)
@@ -127,10 +129,11 @@ def pp_test():
         tot += float(l)
     ropt.step()
     assert abs(float(loss) - tot) < 1e-5, (float(loss), tot)
-    for i, blk in enumerate(pl.run_function):
-        np.testing.assert_allclose(blk.fc.weight.numpy(), full[pl._start + i].fc.weight.numpy(), atol=1e-5)
-    print(f"rank{dist.get_rank()} pp OK stage{stage}", flush=True)
+    for blk, gi in zip(pl.run_function, owned):
+        np.testing.assert_allclose(blk.fc.weight.numpy(), full[gi].fc.weight.numpy(), atol=1e-5)
+    tag = 'pp' if virtual == 1 else 'vpp'
+    print(f"rank{dist.get_rank()} {tag} OK stage{stage}", flush=True)
 
 
 if __name__ == '__main__':
-    {'tp': tp_test, 'sp': sp_test, 'pp': pp_test}[sys.argv[1]]()
+    {'tp': tp_test, 'sp': sp_test, 'pp': pp_test, 'vpp': lambda: pp_test(2)}[sys.argv[1]]()

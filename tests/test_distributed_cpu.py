@@ -34,7 +34,7 @@ def test_dp_and_sharding_match_single_process(mode):
     assert out.count(f'{mode} OK') == 2
 
 
-@pytest.mark.parametrize("mode", ['tp', 'sp', 'pp'])
+@pytest.mark.parametrize("mode", ['tp', 'sp', 'pp', 'vpp'])
 def test_hybrid_parallel_matches_single_device(mode):
     out = run_workers('worker_hybrid.py', mode)
     assert out.count(f'{mode} OK') == 2, out[-3000:]
