@@ -20,6 +20,7 @@
 //  * Strided q/k/v/o (element strides for batch/seq/head) so q, k, v can be slices of a fused
 //    QKV projection with no copies.
 #include "common.h"
+#include <stdlib.h>
 
 namespace pa {
 namespace fa {
@@ -354,10 +355,12 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const uint16_t* __restri
   if (sub == 0) delta[rid] = s;
 }
 
-// dK/dV: grid (ceil(Sk/64), Hq, B); 4 waves x 16 keys; loop over 64-query blocks.
+// dK/dV: grid (ceil(Sk / (64*NT)), Hq, B); 4 waves x (16*NT) keys; loop over 64-query blocks.
+// NT = 2 halves the LDS bytes per MFMA (every Q / dO fragment read from LDS feeds two key tiles)
+// at one wave per SIMD (the accumulators of 32 keys x D need the full register file).
 // dK/dV are written per q-head ([B, Sk, Hq, D] strides given by dks/dvs); GQA sums outside.
-template <typename T, int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
+template <typename T, int D, bool CAUSAL, int NT>
+__global__ __launch_bounds__(256, 3 - NT) void bwd_dkdv_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq, int Sk, int Hq, int Hk, Strides qs, Strides ks_,
@@ -375,32 +378,37 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
   const int g = lane >> 4;
   const int h = blockIdx.y, b = blockIdx.z;
   const int hk = h / (Hq / Hk);
-  const int k0 = blockIdx.x * 64;
-  const int kw = k0 + wave * 16;
-  const int mykey = kw + (lane & 15);
+  const int k0 = blockIdx.x * 64 * NT;
+  const int kw = k0 + wave * 16 * NT;
   const int off = Sk - Sq;
   const float scale_log2 = scale * kLog2e;
 
   const uint16_t* qbase = Q + b * qs.b + h * qs.h;
   const uint16_t* dobase = dO + b * dos.b + h * dos.h;
-  // K, V of this wave's 16 keys as B operands: lane holds K[key][32ks + 8g .. +8]
-  s16x8 kf[KS], vf[KS];
+  // K, V of this wave's keys as B operands: lane holds K[key][32ks + 8g .. +8]
+  s16x8 kf[NT][KS], vf[NT][KS];
 #pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    if (mykey < Sk) {
-      kf[k] = *reinterpret_cast<const s16x8*>(K + b * ks_.b + hk * ks_.h + (long long)mykey * ks_.s + 32 * k + 8 * g);
-      vf[k] = *reinterpret_cast<const s16x8*>(V + b * vs.b + hk * vs.h + (long long)mykey * vs.s + 32 * k + 8 * g);
-    } else {
-      kf[k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      vf[k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < NT; ++j) {
+    const int key = kw + 16 * j + (lane & 15);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      if (key < Sk) {
+        kf[j][k] = *reinterpret_cast<const s16x8*>(K + b * ks_.b + hk * ks_.h + (long long)key * ks_.s + 32 * k + 8 * g);
+        vf[j][k] = *reinterpret_cast<const s16x8*>(V + b * vs.b + hk * vs.h + (long long)key * vs.s + 32 * k + 8 * g);
+      } else {
+        kf[j][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        vf[j][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
     }
   }
-  f32x4 acc_dk[DB], acc_dv[DB];
+  f32x4 acc_dk[NT][DB], acc_dv[NT][DB];
 #pragma unroll
-  for (int d = 0; d < DB; ++d) {
-    acc_dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-    acc_dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+      acc_dk[j][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc_dv[j][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   int qstart = 0;
   if (CAUSAL) qstart = max(0, (k0 - off) / 64 * 64);
   const int nqb = (Sq - qstart + 63) / 64;
@@ -431,39 +439,52 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
     }
     if (CAUSAL && q0 + 63 + off < kw) continue;  // whole query block above this wave's keys
 
-    // S = Q K^T, dP = dO V^T : acc[m] holds [query 16m + 4g + r][key lane&15]
-    f32x4 acc_s[4], acc_dp[4];
+    // S = Q K^T, dP = dO V^T : acc[j][m] holds [query 16m + 4g + r][key 16j + lane&15]
+    f32x4 acc_s[NT][4], acc_dp[NT][4];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      acc_s[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-      acc_dp[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        acc_s[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc_dp[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const s16x8 qa = ld_row8<D, false>(q_lds, 16 * m + (lane & 15), k, g);
-        acc_s[m] = Mfma<T>::run(qa, kf[k], acc_s[m]);
         const s16x8 da = ld_row8<D, false>(do_lds, 16 * m + (lane & 15), k, g);
-        acc_dp[m] = Mfma<T>::run(da, vf[k], acc_dp[m]);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          acc_s[j][m] = Mfma<T>::run(qa, kf[j][k], acc_s[j][m]);
+          acc_dp[j][m] = Mfma<T>::run(da, vf[j][k], acc_dp[j][m]);
+        }
       }
     }
     // P and dS, packed as B operands (k = query, permuted as in the forward)
-    s16x8 pb[2], db_[2];
-    const bool need_mask = (q0 + 64 > Sq) || (kw + 16 > Sk) || (CAUSAL && kw + 15 > q0 + off);
+    const bool need_mask = (q0 + 64 > Sq) || (kw + 16 * NT > Sk) || (CAUSAL && kw + 16 * NT - 1 > q0 + off);
+    s16x8 pb[NT][2], db_[NT][2];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
+      const float4 lse4 = *reinterpret_cast<const float4*>(lse_lds + 16 * m + 4 * g);
+      const float4 dl4 = *reinterpret_cast<const float4*>(dl_lds + 16 * m + 4 * g);
+      const float lsev[4] = {lse4.x, lse4.y, lse4.z, lse4.w};
+      const float dlv[4] = {dl4.x, dl4.y, dl4.z, dl4.w};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ql = 16 * m + 4 * g + r;
-        float p = fast_exp2(__builtin_fmaf(acc_s[m][r], scale_log2, -lse_lds[ql]));
-        if (need_mask) {
-          const int q = q0 + ql;
-          if ((q >= Sq) || (mykey >= Sk) || (CAUSAL && mykey > q + off)) p = 0.f;
+      for (int j = 0; j < NT; ++j) {
+        const int mykey = kw + 16 * j + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float p = fast_exp2(__builtin_fmaf(acc_s[j][m][r], scale_log2, -lsev[r]));
+          if (need_mask) {
+            const int q = q0 + 16 * m + 4 * g + r;
+            const bool masked = (q >= Sq) || (mykey >= Sk) || (CAUSAL && mykey > q + off);
+            p = masked ? 0.f : p;
+          }
+          const float ds = p * (acc_dp[j][m][r] - dlv[r]);
+          pb[j][m >> 1][(m & 1) * 4 + r] = f2s<T>(p);
+          db_[j][m >> 1][(m & 1) * 4 + r] = f2s<T>(ds);
         }
-        const float ds = p * (acc_dp[m][r] - dl_lds[ql]);
-        pb[m >> 1][(m & 1) * 4 + r] = f2s<T>(p);
-        db_[m >> 1][(m & 1) * 4 + r] = f2s<T>(ds);
       }
     }
     // dV^T += dO^T P ;  dK^T += Q^T dS
@@ -472,33 +493,41 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const s16x8 doa = ld_tr8<D, false>(do_lds, 32 * s, d, lane);
-        acc_dv[d] = Mfma<T>::run(doa, pb[s], acc_dv[d]);
         const s16x8 qa = ld_tr8<D, false>(q_lds, 32 * s, d, lane);
-        acc_dk[d] = Mfma<T>::run(qa, db_[s], acc_dk[d]);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          acc_dv[j][d] = Mfma<T>::run(doa, pb[j][s], acc_dv[j][d]);
+          acc_dk[j][d] = Mfma<T>::run(qa, db_[j][s], acc_dk[j][d]);
+        }
       }
     }
   }
-  // epilogue: lane holds d[16d + 4g + r][key lane&15]
-  if (mykey < Sk) {
-    uint16_t* dkrow = dK + b * dks.b + h * dks.h + (long long)mykey * dks.s;
-    uint16_t* dvrow = dV + b * dvs.b + h * dvs.h + (long long)mykey * dvs.s;
+  // epilogue: lane holds d[16d + 4g + r][key 16j + lane&15]
 #pragma unroll
-    for (int d = 0; d < DB; ++d) {
-      s16x4 a, c;
+  for (int j = 0; j < NT; ++j) {
+    const int mykey = kw + 16 * j + (lane & 15);
+    if (mykey < Sk) {
+      uint16_t* dkrow = dK + b * dks.b + h * dks.h + (long long)mykey * dks.s;
+      uint16_t* dvrow = dV + b * dvs.b + h * dvs.h + (long long)mykey * dvs.s;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        a[r] = f2s<T>(acc_dk[d][r] * scale);
-        c[r] = f2s<T>(acc_dv[d][r]);
+      for (int d = 0; d < DB; ++d) {
+        s16x4 a, c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          a[r] = f2s<T>(acc_dk[j][d][r] * scale);
+          c[r] = f2s<T>(acc_dv[j][d][r]);
+        }
+        *reinterpret_cast<s16x4*>(dkrow + 16 * d + 4 * g) = a;
+        *reinterpret_cast<s16x4*>(dvrow + 16 * d + 4 * g) = c;
       }
-      *reinterpret_cast<s16x4*>(dkrow + 16 * d + 4 * g) = a;
-      *reinterpret_cast<s16x4*>(dvrow + 16 * d + 4 * g) = c;
     }
   }
 }
 
-// dQ: grid (ceil(Sq/64), Hq, B); 4 waves x 16 queries; loop over 64-key blocks (swapped products).
-template <typename T, int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void bwd_dq_kernel(
+// dQ: grid (ceil(Sq / (64*NT)), Hq, B); 4 waves x (16*NT) queries; loop over 64-key blocks
+// (swapped products: lane owns a query).  NT = 2: every K / V fragment read feeds two query tiles.
+template <typename T, int D, bool CAUSAL, int NT>
+__global__ __launch_bounds__(256, 3 - NT) void bwd_dq_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     uint16_t* __restrict__ dQ, int Sq, int Sk, int Hq, int Hk, Strides qs, Strides ks_, Strides vs, Strides dos,
@@ -511,38 +540,45 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane >> 4;
-  const int nqb = (Sq + 63) / 64;
+  const int nqb = (Sq + 64 * NT - 1) / (64 * NT);
   const int qb = nqb - 1 - (int)blockIdx.x;
   const int h = blockIdx.y, b = blockIdx.z;
   const int hk = h / (Hq / Hk);
-  const int q0 = qb * 64;
-  const int qw = q0 + wave * 16;
-  const int myq = qw + (lane & 15);
+  const int q0 = qb * 64 * NT;
+  const int qw = q0 + wave * 16 * NT;
   const int off = Sk - Sq;
   const float scale_log2 = scale * kLog2e;
 
-  s16x8 qf[KS], dof[KS];
-#pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    if (myq < Sq) {
-      qf[k] = *reinterpret_cast<const s16x8*>(Q + b * qs.b + h * qs.h + (long long)myq * qs.s + 32 * k + 8 * g);
-      dof[k] = *reinterpret_cast<const s16x8*>(dO + b * dos.b + h * dos.h + (long long)myq * dos.s + 32 * k + 8 * g);
-    } else {
-      qf[k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      dof[k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
-  }
+  s16x8 qf[NT][KS], dof[NT][KS];
+  float lse2[NT], dlt[NT];
   const long long lrow = ((long long)b * Hq + h) * Sq;
-  const float lse2 = myq < Sq ? LSE[lrow + myq] * kLog2e : INFINITY;
-  const float dlt = myq < Sq ? Delta[lrow + myq] : 0.f;
-  f32x4 acc[DB];
 #pragma unroll
-  for (int d = 0; d < DB; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < NT; ++t) {
+    const int myq = qw + 16 * t + (lane & 15);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      if (myq < Sq) {
+        qf[t][k] = *reinterpret_cast<const s16x8*>(Q + b * qs.b + h * qs.h + (long long)myq * qs.s + 32 * k + 8 * g);
+        dof[t][k] =
+            *reinterpret_cast<const s16x8*>(dO + b * dos.b + h * dos.h + (long long)myq * dos.s + 32 * k + 8 * g);
+      } else {
+        qf[t][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        dof[t][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+    lse2[t] = myq < Sq ? LSE[lrow + myq] * kLog2e : INFINITY;
+    dlt[t] = myq < Sq ? Delta[lrow + myq] : 0.f;
+  }
+  f32x4 acc[NT][DB];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int d = 0; d < DB; ++d) acc[t][d] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const uint16_t* kbase = K + b * ks_.b + hk * ks_.h;
   const uint16_t* vbase = V + b * vs.b + hk * vs.h;
   int kend = Sk;
-  if (CAUSAL) kend = min(Sk, q0 + 64 + off);
+  if (CAUSAL) kend = min(Sk, q0 + 64 * NT + off);
   const int nkb = kend > 0 ? (kend + 63) / 64 : 0;
   Tile<D> kt, vt;
   kt.init(kbase, ks_.s);
@@ -561,35 +597,45 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(
       kt.load(k0 + 64, Sk);
       vt.load(k0 + 64, Sk);
     }
-    if (CAUSAL && k0 > qw + 15 + off) continue;
-    f32x4 acc_s[4], acc_dp[4];
+    if (CAUSAL && k0 > qw + 16 * NT - 1 + off) continue;
+    f32x4 acc_s[NT][4], acc_dp[NT][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      acc_s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      acc_dp[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc_s[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc_dp[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const s16x8 ka = ld_row8<D, false>(k_lds, 16 * j + (lane & 15), k, g);
-        acc_s[j] = Mfma<T>::run(ka, qf[k], acc_s[j]);
         const s16x8 va = ld_row8<D, false>(v_lds, 16 * j + (lane & 15), k, g);
-        acc_dp[j] = Mfma<T>::run(va, dof[k], acc_dp[j]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          acc_s[t][j] = Mfma<T>::run(ka, qf[t][k], acc_s[t][j]);
+          acc_dp[t][j] = Mfma<T>::run(va, dof[t][k], acc_dp[t][j]);
+        }
       }
     }
-    s16x8 dsb[2];
-    const bool need_mask = (k0 + 64 > Sk) || (qw + 16 > Sq) || (CAUSAL && k0 + 63 > qw + off);
+    const bool need_mask = (k0 + 64 > Sk) || (qw + 16 * NT > Sq) || (CAUSAL && k0 + 63 > qw + off);
+    s16x8 dsb[NT][2];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int t = 0; t < NT; ++t) {
+      const int myq = qw + 16 * t + (lane & 15);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float p = fast_exp2(__builtin_fmaf(acc_s[j][r], scale_log2, -lse2));
-        if (need_mask) {
-          const int key = k0 + 16 * j + 4 * g + r;
-          if ((key >= Sk) || (myq >= Sq) || (CAUSAL && key > myq + off)) p = 0.f;
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float p = fast_exp2(__builtin_fmaf(acc_s[t][j][r], scale_log2, -lse2[t]));
+          if (need_mask) {
+            const int key = k0 + 16 * j + 4 * g + r;
+            const bool masked = (key >= Sk) || (myq >= Sq) || (CAUSAL && key > myq + off);
+            p = masked ? 0.f : p;
+          }
+          dsb[t][j >> 1][(j & 1) * 4 + r] = f2s<T>(p * (acc_dp[t][j][r] - dlt[t]));
         }
-        dsb[j >> 1][(j & 1) * 4 + r] = f2s<T>(p * (acc_dp[j][r] - dlt));
       }
     }
     // dQ^T += K^T dS^T
@@ -598,18 +644,23 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const s16x8 ka = ld_tr8<D, false>(k_lds, 32 * s, d, lane);
-        acc[d] = Mfma<T>::run(ka, dsb[s], acc[d]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t][d] = Mfma<T>::run(ka, dsb[t][s], acc[t][d]);
       }
     }
   }
-  if (myq < Sq) {
-    uint16_t* row = dQ + b * dqs.b + h * dqs.h + (long long)myq * dqs.s;
 #pragma unroll
-    for (int d = 0; d < DB; ++d) {
-      s16x4 o;
+  for (int t = 0; t < NT; ++t) {
+    const int myq = qw + 16 * t + (lane & 15);
+    if (myq < Sq) {
+      uint16_t* row = dQ + b * dqs.b + h * dqs.h + (long long)myq * dqs.s;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = f2s<T>(acc[d][r] * scale);
-      *reinterpret_cast<s16x4*>(row + 16 * d + 4 * g) = o;
+      for (int d = 0; d < DB; ++d) {
+        s16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2s<T>(acc[t][d][r] * scale);
+        *reinterpret_cast<s16x4*>(row + 16 * d + 4 * g) = o;
+      }
     }
   }
 }
@@ -645,6 +696,17 @@ PA_API hipError_t pa_flash_fwd(const void* q, const void* k, const void* v, void
   return hipGetLastError();
 }
 
+// backward tiling: 1 = 16 rows per wave (2 waves/SIMD), 2 = 32 rows per wave (1 wave/SIMD);
+// PA_FA_BWD_VARIANT selects (A/B), default 2.
+static int bwd_variant() {
+  static int v = [] {
+    const char* e = getenv("PA_FA_BWD_VARIANT");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
+
 // dk/dv are per-q-head buffers (caller reduces over GQA groups when Hq != Hk).
 PA_API hipError_t pa_flash_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                                const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk,
@@ -660,14 +722,27 @@ PA_API hipError_t pa_flash_bwd(const void* q, const void* k, const void* v, cons
   FA_DISPATCH(dt, D, causal, {
     bwd_delta_kernel<T, DD><<<(int)((nrows + 15) / 16), 256, 0, st>>>((const uint16_t*)dout, (const uint16_t*)o, delta,
                                                                       B, Sq, Hq, dos, os);
-    dim3 g1((Sk + 63) / 64, Hq, B);
-    bwd_dkdv_kernel<T, DD, CC><<<g1, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                                                   (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv,
-                                                   Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs, scale);
-    dim3 g2((Sq + 63) / 64, Hq, B);
-    bwd_dq_kernel<T, DD, CC><<<g2, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                                                 (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk, Hq, Hk, qs,
-                                                 ks, vs, dos, dqs, scale);
+    if (bwd_variant() == 2) {
+      dim3 g1((Sk + 127) / 128, Hq, B);
+      bwd_dkdv_kernel<T, DD, CC, 2><<<g1, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                                                        (const uint16_t*)dout, lse, delta, (uint16_t*)dk,
+                                                        (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs,
+                                                        scale);
+      dim3 g2((Sq + 127) / 128, Hq, B);
+      bwd_dq_kernel<T, DD, CC, 2><<<g2, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                                                      (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk, Hq,
+                                                      Hk, qs, ks, vs, dos, dqs, scale);
+    } else {
+      dim3 g1((Sk + 63) / 64, Hq, B);
+      bwd_dkdv_kernel<T, DD, CC, 1><<<g1, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                                                        (const uint16_t*)dout, lse, delta, (uint16_t*)dk,
+                                                        (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs,
+                                                        scale);
+      dim3 g2((Sq + 63) / 64, Hq, B);
+      bwd_dq_kernel<T, DD, CC, 1><<<g2, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                                                      (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk, Hq,
+                                                      Hk, qs, ks, vs, dos, dqs, scale);
+    }
   });
   return hipGetLastError();
 }

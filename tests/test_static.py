@@ -155,3 +155,28 @@ def test_inference_predictor(tmp_path):
     pred.run()
     o = pred.get_output_handle(pred.get_output_names()[0]).copy_to_cpu()
     np.testing.assert_allclose(o, net(paddle.to_tensor(a)).numpy(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_gpu_predictor_hip_graph_and_to_static_graph(tmp_path):
+    net = _Net()
+    net.eval()
+    path = str(tmp_path / 'g')
+    paddle.jit.save(net, path, input_spec=[static.InputSpec([4, 6], 'float32', 'x')])
+    from paddle import inference
+    cfg = inference.Config(path + '.pdmodel', path + '.pdiparams')
+    cfg.enable_use_gpu(100, 0)
+    cfg.enable_hip_graph()
+    pred = inference.create_predictor(cfg)
+    a = np.random.rand(4, 6).astype('float32')
+    outs = []
+    for _ in range(3):
+        outs.append(pred.run([paddle.to_tensor(a)])[0].numpy())
+    ref = net(paddle.to_tensor(a)).numpy()
+    for o in outs:
+        np.testing.assert_allclose(o, ref, rtol=1e-4, atol=1e-5)
+    g = paddle.jit.to_static(net, backend='hip_graph')
+    with paddle.no_grad():
+        for _ in range(4):
+            y = g(paddle.to_tensor(a))
+    np.testing.assert_allclose(y.numpy(), ref, rtol=1e-4, atol=1e-5)
