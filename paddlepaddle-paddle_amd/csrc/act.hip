@@ -16,14 +16,19 @@ struct GeluErf {
     return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
   }
 };
+// tanh(u) = 1 - 2 / (1 + e^{2u}) on the v_exp_f32 path (libm tanhf is a long polynomial
+// branch ladder: it made the GeLU kernels VALU-bound instead of HBM-bound).  Saturates
+// correctly at both ends (e^{2u} -> inf gives 1, -> 0 gives -1); |error| ~ 1e-7.
+__device__ __forceinline__ float fast_tanh(float u) { return 1.f - __fdividef(2.f, 1.f + __expf(2.f * u)); }
+
 struct GeluTanh {
   static __device__ __forceinline__ float f(float x) {
     const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
-    return 0.5f * x * (1.f + tanhf(u));
+    return 0.5f * x * (1.f + fast_tanh(u));
   }
   static __device__ __forceinline__ float df(float x) {
     const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
-    const float t = tanhf(u);
+    const float t = fast_tanh(u);
     return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.79788456080286536f * (1.f + 3.f * 0.044715f * x * x);
   }
 };
@@ -97,6 +102,118 @@ __global__ __launch_bounds__(256) void bias_act_bwd(const T* __restrict__ dy, co
       float v = to_f(x[i]) + (bias != nullptr ? to_f(bias[i % cols]) : 0.f);
       dx[i] = from_f<T>(to_f(dy[i]) * Act::df(v));
     }
+  }
+}
+
+// Column-blocked backward with the bias gradient fused: block (bx, by) owns columns
+// [bx*256*E, +256*E) and rows [by*rpb, +rpb); each lane keeps E per-column fp32 sums of dx in
+// registers across its rows (16-byte loads, a wave reads 1 KiB contiguous per row) and writes
+// them once to part[by, :].  colsum_finish adds the partial rows into the bias gradient.
+// ACT == nullptr-like Ident with no x: plain column sum of dy (dx, x unused).
+template <typename T, typename Act, bool HAS_X>
+__global__ __launch_bounds__(256) void bias_act_bwd_cs(const T* __restrict__ dy, const T* __restrict__ x,
+                                                       const T* __restrict__ bias, T* __restrict__ dx,
+                                                       float* __restrict__ part, int rows, int cols, int rpb) {
+  constexpr int E = 16 / sizeof(T);
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * E;
+  if (c0 >= cols) return;  // no barriers below
+  const int r0 = blockIdx.y * rpb;
+  const int r1 = min(rows, r0 + rpb);
+  float b[E], acc[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) { b[e] = 0.f; acc[e] = 0.f; }
+  if (HAS_X && bias != nullptr) load_f<T, E>(bias + c0, b);
+  int r = r0;
+  for (; r + 1 < r1; r += 2) {  // two rows in flight per lane
+    const size_t o0 = (size_t)r * cols + c0, o1 = o0 + cols;
+    float g0[E], g1[E];
+    load_f<T, E>(dy + o0, g0);
+    load_f<T, E>(dy + o1, g1);
+    if constexpr (HAS_X) {
+      float v0[E], v1[E];
+      load_f<T, E>(x + o0, v0);
+      load_f<T, E>(x + o1, v1);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        g0[e] *= Act::df(v0[e] + b[e]);
+        g1[e] *= Act::df(v1[e] + b[e]);
+      }
+      store_f<T, E>(dx + o0, g0);
+      store_f<T, E>(dx + o1, g1);
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] += g0[e] + g1[e];
+  }
+  if (r < r1) {
+    const size_t o0 = (size_t)r * cols + c0;
+    float g0[E];
+    load_f<T, E>(dy + o0, g0);
+    if constexpr (HAS_X) {
+      float v0[E];
+      load_f<T, E>(x + o0, v0);
+#pragma unroll
+      for (int e = 0; e < E; ++e) g0[e] *= Act::df(v0[e] + b[e]);
+      store_f<T, E>(dx + o0, g0);
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] += g0[e];
+  }
+  float* pp = part + (size_t)blockIdx.y * cols + c0;
+#pragma unroll
+  for (int e = 0; e < E; e += 4) *reinterpret_cast<float4*>(pp + e) = make_float4(acc[e], acc[e + 1], acc[e + 2], acc[e + 3]);
+}
+
+// out[c] (+)= sum_p part[p, c]  — 4 waves split the P partial rows of 64 columns, LDS combine.
+template <typename OT>
+__global__ __launch_bounds__(256) void colsum_finish(const float* __restrict__ part, OT* __restrict__ out, int P,
+                                                     int cols, int accum) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < cols) {
+    int p = w;
+    for (; p + 4 < P; p += 8) {
+      s0 += part[(size_t)p * cols + c];
+      s1 += part[(size_t)(p + 4) * cols + c];
+    }
+    for (; p < P; p += 4) s0 += part[(size_t)p * cols + c];
+  }
+  red[w][lane] = s0 + s1;
+  __syncthreads();
+  if (w == 0 && c < cols) {
+    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[c] = from_f<OT>(accum ? to_f(out[c]) + t : t);
+  }
+}
+
+// rows per block for the column-blocked kernels: aim at ~1024 blocks, >= 32 rows each
+inline int cs_rows_per_block(int rows, int colblocks) {
+  long long rpb = ((long long)rows * colblocks + 1023) / 1024;
+  if (rpb < 32) rpb = 32;
+  if (rpb > rows) rpb = rows < 1 ? 1 : rows;
+  return (int)rpb;
+}
+
+template <typename OT>
+hipError_t launch_finish(const float* part, void* out, int P, int cols, int accum, hipStream_t st) {
+  colsum_finish<OT><<<(cols + 63) / 64, 256, 0, st>>>(part, (OT*)out, P, cols, accum);
+  return hipGetLastError();
+}
+
+template <typename T, typename Act>
+void launch_cs(dim3 grid, const void* dy, const void* x, const void* bias, void* dx, float* part, int rows, int cols,
+               int rpb, hipStream_t st) {
+  bias_act_bwd_cs<T, Act, true><<<grid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)bias, (T*)dx, part, rows,
+                                                       cols, rpb);
+}
+
+inline hipError_t finish_dt(const float* part, void* out, int odt, int P, int cols, int accum, hipStream_t st) {
+  switch (odt) {
+    case 0: return launch_finish<float>(part, out, P, cols, accum, st);
+    case 1: return launch_finish<bf16_t>(part, out, P, cols, accum, st);
+    case 2: return launch_finish<f16_t>(part, out, P, cols, accum, st);
+    default: return hipErrorInvalidValue;
   }
 }
 
@@ -273,4 +390,54 @@ PA_API hipError_t pa_dropout_bwd(const void* dy, void* dx, long long n, float p,
     dropout_bwd<T><<<g, 256, 0, st>>>((const T*)dy, (T*)dx, n, p, seed, offset);
   });
   return hipGetLastError();
+}
+
+// Partial-row count the column-blocked kernels use (callers size `part` as nparts * cols floats).
+PA_API int pa_colsum_nparts(int rows, int cols, int dt) {
+  const int E = dt == 0 ? 4 : 8;
+  const int cb = (cols + 256 * E - 1) / (256 * E);
+  const int rpb = cs_rows_per_block(rows, cb);
+  return (rows + rpb - 1) / rpb;
+}
+
+// dx = dy * act'(x + bias) over [rows, cols] AND dbias (+)= colsum(dx) (out dtype odt, accumulated
+// in place when accum) — the bias gradient never takes a separate pass over dx.
+PA_API hipError_t pa_bias_act_bwd_dbias(int act, const void* dy, const void* x, const void* bias, void* dx,
+                                        float* part, void* dbias, int odt, int accum, int rows, int cols, int dt,
+                                        hipStream_t st) {
+  const int E = dt == 0 ? 4 : 8;
+  if (cols % E != 0) return hipErrorInvalidValue;
+  const int cb = (cols + 256 * E - 1) / (256 * E);
+  const int rpb = cs_rows_per_block(rows, cb);
+  const dim3 grid(cb, (rows + rpb - 1) / rpb);
+  PA_DISPATCH_DTYPE(dt, T, {
+    switch (act) {
+      case 0: launch_cs<T, GeluErf>(grid, dy, x, bias, dx, part, rows, cols, rpb, st); break;
+      case 1: launch_cs<T, GeluTanh>(grid, dy, x, bias, dx, part, rows, cols, rpb, st); break;
+      case 2: launch_cs<T, Silu>(grid, dy, x, bias, dx, part, rows, cols, rpb, st); break;
+      case 3: launch_cs<T, Relu>(grid, dy, x, bias, dx, part, rows, cols, rpb, st); break;
+      case 4: launch_cs<T, Ident>(grid, dy, x, bias, dx, part, rows, cols, rpb, st); break;
+      default: return hipErrorInvalidValue;
+    }
+  });
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return finish_dt(part, dbias, odt, (int)grid.y, cols, accum, st);
+}
+
+// out (+)= colsum(dy) for dy [rows, cols] with row stride ld == cols (the bias gradient of a Linear).
+PA_API hipError_t pa_colsum(const void* dy, float* part, void* out, int odt, int accum, int rows, int cols, int dt,
+                            hipStream_t st) {
+  const int E = dt == 0 ? 4 : 8;
+  if (cols % E != 0) return hipErrorInvalidValue;
+  const int cb = (cols + 256 * E - 1) / (256 * E);
+  const int rpb = cs_rows_per_block(rows, cb);
+  const dim3 grid(cb, (rows + rpb - 1) / rpb);
+  PA_DISPATCH_DTYPE(dt, T, {
+    bias_act_bwd_cs<T, Ident, false><<<grid, 256, 0, st>>>((const T*)dy, nullptr, nullptr, nullptr, part, rows, cols,
+                                                            rpb);
+  });
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return finish_dt(part, out, odt, (int)grid.y, cols, accum, st);
 }

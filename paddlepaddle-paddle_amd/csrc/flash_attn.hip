@@ -697,11 +697,12 @@ PA_API hipError_t pa_flash_fwd(const void* q, const void* k, const void* v, void
 }
 
 // backward tiling: 1 = 16 rows per wave (2 waves/SIMD), 2 = 32 rows per wave (1 wave/SIMD);
-// PA_FA_BWD_VARIANT selects (A/B), default 2.
+// PA_FA_BWD_VARIANT selects (A/B), default 1 (measured on MI355X, B16 S1024 H16 D128 causal:
+// fwd+bwd 1.04 ms with 1 vs 1.30 ms with 2 — the 32-row tiles lose occupancy to VGPR pressure).
 static int bwd_variant() {
   static int v = [] {
     const char* e = getenv("PA_FA_BWD_VARIANT");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 1;
   }();
   return v;
 }

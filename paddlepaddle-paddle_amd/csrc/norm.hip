@@ -16,12 +16,33 @@
 
 namespace pa {
 
-template <typename T, typename WT, int MAXC, bool RMS>
+// Dropout keep-mask of the fused (bias +) dropout + residual + norm path: a stateless hash of
+// (seed, offset, 16-byte vector index of the element in the [rows, cols] matrix, lane in the
+// vector), so the backward regenerates it bit-exactly without a stored mask.
+struct DropSpec {
+  float p;       // drop probability (0 < p < 1 when DROP)
+  uint32_t seed, offset;
+};
+
+template <int E>
+__device__ __forceinline__ void drop_mask(const DropSpec& d, size_t vec_index, float (&m)[E]) {
+  const float scale = 1.f / (1.f - d.p);
+  const uint32_t h0 = hash3(d.seed, d.offset, (uint32_t)vec_index);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const uint32_t h = (e == 0) ? h0 : hash3(h0, (uint32_t)e, 0x2545F491u);
+    m[e] = uniform01(h) >= d.p ? scale : 0.f;
+  }
+}
+
+// DROP: v = dropout(x + xbias) + res   (xbias optional, same dtype as x; res required)
+template <typename T, typename WT, int MAXC, bool RMS, bool DROP>
 __global__ __launch_bounds__(256) void norm_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                        const WT* __restrict__ w, const WT* __restrict__ b,
                                                        T* __restrict__ y, T* __restrict__ sum_out,
                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                       int rows, int cols, float eps) {
+                                                       int rows, int cols, float eps, const T* __restrict__ xbias,
+                                                       DropSpec dsp) {
   constexpr int E = 16 / sizeof(T);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -34,6 +55,18 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const T* __restrict__ x, 
     const int j = (c * 64 + lane) * E;
     if (j < cols) {
       load_f<T, E>(x + base + j, v[c]);
+      if constexpr (DROP) {
+        if (xbias != nullptr) {
+          float xb[E];
+          load_f<T, E>(xbias + j, xb);
+#pragma unroll
+          for (int e = 0; e < E; ++e) v[c][e] += xb[e];
+        }
+        float m[E];
+        drop_mask<E>(dsp, (base + j) / E, m);
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[c][e] *= m[e];
+      }
       if (res != nullptr) {
         float r[E];
         load_f<T, E>(res + base + j, r);
@@ -133,21 +166,30 @@ __global__ __launch_bounds__(256) void norm_fwd_generic(const T* __restrict__ x,
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w        (LayerNorm)
 // dx = rstd * (g - xhat * mean(g * xhat))                               (RMSNorm)
 // dw_part[blockIdx] += dy * xhat ; db_part[blockIdx] += dy
-template <typename T, typename WT, int MAXC, bool RMS>
+// DROP (fused bias + dropout + residual forward): dx is the residual-stream gradient,
+// dxd = dx * keep / (1 - p) the gradient of the pre-dropout input, and
+// xb_part[blockIdx] += dxd (the partial bias gradient, when xb_part != nullptr).
+template <typename T, typename WT, int MAXC, bool RMS, bool DROP>
 __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                        const WT* __restrict__ w, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd, const T* __restrict__ dsum,
                                                        T* __restrict__ dx, float* __restrict__ dw_part,
-                                                       float* __restrict__ db_part, int rows, int cols) {
+                                                       float* __restrict__ db_part, int rows, int cols,
+                                                       T* __restrict__ dxd, float* __restrict__ xb_part,
+                                                       DropSpec dsp) {
   constexpr int E = 16 / sizeof(T);
   __shared__ float red[8];
   const int tid = threadIdx.x;
-  float aw[MAXC][E], ab[MAXC][E], wv[MAXC][E];
+  float aw[MAXC][E], ab[MAXC][E], wv[MAXC][E], axb[DROP ? MAXC : 1][E];
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int j = (c * 256 + tid) * E;
 #pragma unroll
     for (int e = 0; e < E; ++e) { aw[c][e] = 0.f; ab[c][e] = 0.f; wv[c][e] = 0.f; }
+    if constexpr (DROP) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) axb[c][e] = 0.f;
+    }
     if (j < cols) load_f<WT, E>(w + j, wv[c]);
   }
   const float inv_n = 1.0f / cols;
@@ -200,6 +242,16 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dy,
           for (int e = 0; e < E; ++e) o[e] += ds[e];
         }
         store_f<T, E>(dx + base + j, o);
+        if constexpr (DROP) {
+          float m[E];
+          drop_mask<E>(dsp, (base + j) / E, m);
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            o[e] *= m[e];
+            axb[c][e] += o[e];
+          }
+          store_f<T, E>(dxd + base + j, o);
+        }
       }
     }
   }
@@ -214,6 +266,13 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dy,
         float* pb = db_part + (size_t)blockIdx.x * cols + j;
 #pragma unroll
         for (int e = 0; e < E; ++e) pb[e] = ab[c][e];
+      }
+      if constexpr (DROP) {
+        if (xb_part != nullptr) {
+          float* px = xb_part + (size_t)blockIdx.x * cols + j;
+#pragma unroll
+          for (int e = 0; e < E; ++e) px[e] = axb[c][e];
+        }
       }
     }
   }
@@ -263,9 +322,10 @@ __global__ __launch_bounds__(256) void norm_bwd_generic(const T* __restrict__ dy
 
 // out[c] = sum_p part[p, c]: block = 4 waves x 64 columns; the waves split the P partial rows
 // (each wave-row read is 256 contiguous bytes), then a 4-way LDS reduce.  Deterministic.
+// accum != 0: out[c] += sum (in-place gradient accumulation into a flat gradient slot).
 template <typename WT>
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, WT* __restrict__ out, int P,
-                                                     int cols) {
+                                                     int cols, int accum = 0) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
@@ -280,20 +340,60 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
   }
   red[w][lane] = s;
   __syncthreads();
-  if (w == 0 && c < cols) out[c] = from_f<WT>(red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
+  if (w == 0 && c < cols) {
+    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[c] = from_f<WT>(accum ? to_f(out[c]) + t : t);
+  }
+}
+
+struct FusedArgs {  // the fused (bias +) dropout + residual path; drop == false: plain (add +) norm
+  bool drop;
+  const void* xbias;  // forward: bias added to x before dropout (nullable)
+  void* dxd;          // backward: gradient of the pre-dropout input
+  void* xbgrad;       // backward: bias gradient (nullable), dtype code xbgd, accumulated if xbaccum
+  int xbgd, xbaccum;
+  DropSpec dsp;
+};
+
+template <typename OT>
+hipError_t finish_colsum(const float* part, void* out, int P, int cols, int accum, hipStream_t st) {
+  colsum_kernel<OT><<<(cols + 63) / 64, 256, 0, st>>>(part, (OT*)out, P, cols, accum);
+  return hipGetLastError();
+}
+
+inline hipError_t finish_colsum_dt(const float* part, void* out, int dt, int P, int cols, int accum, hipStream_t st) {
+  switch (dt) {
+    case 0: return finish_colsum<float>(part, out, P, cols, accum, st);
+    case 1: return finish_colsum<bf16_t>(part, out, P, cols, accum, st);
+    case 2: return finish_colsum<f16_t>(part, out, P, cols, accum, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 template <typename T, typename WT, bool RMS>
 hipError_t launch_fwd(const void* x, const void* res, const void* w, const void* b, void* y, void* sum_out,
-                      float* mean, float* rstd, int rows, int cols, float eps, hipStream_t st) {
+                      float* mean, float* rstd, int rows, int cols, float eps, hipStream_t st,
+                      const FusedArgs* fa = nullptr) {
   constexpr int E = 16 / sizeof(T);
   const T* xp = (const T*)x;
   const int chunks = (cols + 64 * E - 1) / (64 * E);
   const bool vec_ok = (cols % E) == 0;
+  const bool drop = fa != nullptr && fa->drop;
   dim3 grid((rows + 3) / 4), block(256);
-#define PA_NF(C) \
-  norm_fwd_kernel<T, WT, C, RMS><<<grid, block, 0, st>>>(xp, (const T*)res, (const WT*)w, (const WT*)b, (T*)y, \
-                                                         (T*)sum_out, mean, rstd, rows, cols, eps)
+  const T* xb = drop ? (const T*)fa->xbias : nullptr;
+  const DropSpec dsp = drop ? fa->dsp : DropSpec{0.f, 0u, 0u};
+#define PA_NF(C)                                                                                                   \
+  do {                                                                                                             \
+    if (drop)                                                                                                      \
+      norm_fwd_kernel<T, WT, C, RMS, true><<<grid, block, 0, st>>>(xp, (const T*)res, (const WT*)w, (const WT*)b,  \
+                                                                   (T*)y, (T*)sum_out, mean, rstd, rows, cols,     \
+                                                                   eps, xb, dsp);                                  \
+    else                                                                                                           \
+      norm_fwd_kernel<T, WT, C, RMS, false><<<grid, block, 0, st>>>(xp, (const T*)res, (const WT*)w, (const WT*)b, \
+                                                                    (T*)y, (T*)sum_out, mean, rstd, rows, cols,    \
+                                                                    eps, nullptr, dsp);                            \
+  } while (0)
+  if (drop && (!vec_ok || chunks > 16 || res == nullptr)) return hipErrorInvalidValue;
   if (vec_ok && chunks <= 1) PA_NF(1);
   else if (vec_ok && chunks <= 2) PA_NF(2);
   else if (vec_ok && chunks <= 4) PA_NF(4);
@@ -309,15 +409,28 @@ hipError_t launch_fwd(const void* x, const void* res, const void* w, const void*
 template <typename T, typename WT, bool RMS>
 hipError_t launch_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
                       const void* dsum, void* dx, float* part, void* dw, void* db, int rows, int cols, int nparts,
-                      hipStream_t st) {
+                      hipStream_t st, const FusedArgs* fa = nullptr) {
   constexpr int E = 16 / sizeof(T);
   const int chunks = (cols + 256 * E - 1) / (256 * E);
   const bool vec_ok = (cols % E) == 0;
+  const bool drop = fa != nullptr && fa->drop;
   float* dw_part = part;
   float* db_part = part + (size_t)nparts * cols;
-#define PA_NB(C)                                                                                              \
-  norm_bwd_kernel<T, WT, C, RMS><<<nparts, 256, 0, st>>>((const T*)dy, (const T*)x, (const WT*)w, mean, rstd, \
-                                                         (const T*)dsum, (T*)dx, dw_part, db_part, rows, cols)
+  float* xb_part = (drop && fa->xbgrad != nullptr) ? part + (size_t)2 * nparts * cols : nullptr;
+  T* dxd = drop ? (T*)fa->dxd : nullptr;
+  const DropSpec dsp = drop ? fa->dsp : DropSpec{0.f, 0u, 0u};
+#define PA_NB(C)                                                                                                 \
+  do {                                                                                                           \
+    if (drop)                                                                                                    \
+      norm_bwd_kernel<T, WT, C, RMS, true><<<nparts, 256, 0, st>>>((const T*)dy, (const T*)x, (const WT*)w,      \
+                                                                   mean, rstd, (const T*)dsum, (T*)dx, dw_part,  \
+                                                                   db_part, rows, cols, dxd, xb_part, dsp);      \
+    else                                                                                                         \
+      norm_bwd_kernel<T, WT, C, RMS, false><<<nparts, 256, 0, st>>>((const T*)dy, (const T*)x, (const WT*)w,     \
+                                                                    mean, rstd, (const T*)dsum, (T*)dx, dw_part, \
+                                                                    db_part, rows, cols, nullptr, nullptr, dsp); \
+  } while (0)
+  if (drop && (!vec_ok || chunks > 4)) return hipErrorInvalidValue;
   if (vec_ok && chunks <= 1) PA_NB(1);
   else if (vec_ok && chunks <= 2) PA_NB(2);
   else if (vec_ok && chunks <= 4) PA_NB(4);
@@ -331,6 +444,10 @@ hipError_t launch_bwd(const void* dy, const void* x, const void* w, const float*
   const int g = (cols + 63) / 64;
   colsum_kernel<WT><<<g, 256, 0, st>>>(dw_part, (WT*)dw, nparts, cols);
   if (!RMS && db != nullptr) colsum_kernel<WT><<<g, 256, 0, st>>>(db_part, (WT*)db, nparts, cols);
+  if (xb_part != nullptr) {
+    e = finish_colsum_dt(xb_part, fa->xbgrad, fa->xbgd, nparts, cols, fa->xbaccum, st);
+    if (e != hipSuccess) return e;
+  }
   return hipGetLastError();
 }
 
@@ -346,7 +463,8 @@ using namespace pa;
   if (xd == 2 && wd == 0) { using T = f16_t; using WT = float; return CALL; }      \
   return hipErrorInvalidValue;
 
-// Number of partial rows the backward writes (callers size `part` as 2 * nparts * cols floats).
+// Number of partial rows the backward writes (callers size `part` as 2 * nparts * cols floats,
+// 3 * nparts * cols for the fused-dropout backward with a bias gradient).
 PA_API int pa_norm_bwd_nparts(int rows) { return rows < 512 ? (rows < 1 ? 1 : rows) : 512; }
 
 PA_API hipError_t pa_layernorm_fwd(const void* x, const void* res, const void* w, const void* b, void* y,
@@ -376,4 +494,39 @@ PA_API hipError_t pa_rmsnorm_bwd(const void* dy, const void* x, const void* w, c
   const int np = pa_norm_bwd_nparts(rows);
   PA_NORM_DISPATCH(xd, wd, true,
                    (launch_bwd<T, WT, true>(dy, x, w, nullptr, rstd, dsum, dx, part, dw, nullptr, rows, cols, np, st)))
+}
+
+// Fused  s = dropout(x + xbias) + res ;  y = norm(s)   (reference:
+// paddle/phi/kernels/fusion/gpu/fused_bias_dropout_residual_layer_norm_kernel.cu).  rms selects
+// RMSNorm (b, mean unused).  Returns hipErrorInvalidValue when the shape has no fused kernel
+// (cols % 8 != 0 or cols > 8192 for 16-bit data): the caller then runs the unfused ops.
+PA_API hipError_t pa_dropout_add_norm_fwd(const void* x, const void* xbias, const void* res, const void* w,
+                                          const void* b, void* y, void* sum_out, float* mean, float* rstd, int rows,
+                                          int cols, float eps, int rms, float p, uint32_t seed, uint32_t offset,
+                                          int xd, int wd, hipStream_t st) {
+  FusedArgs fa{true, xbias, nullptr, nullptr, 0, 0, DropSpec{p, seed, offset}};
+  if (rms) {
+    PA_NORM_DISPATCH(xd, wd, true,
+                     (launch_fwd<T, WT, true>(x, res, w, nullptr, y, sum_out, nullptr, rstd, rows, cols, eps, st, &fa)))
+  }
+  PA_NORM_DISPATCH(xd, wd, false,
+                   (launch_fwd<T, WT, false>(x, res, w, b, y, sum_out, mean, rstd, rows, cols, eps, st, &fa)))
+}
+
+// Backward of the above: dres = norm_bwd(dy) + dsum, dx = dres * keep / (1 - p), xbgrad (+)= colsum(dx).
+// `part` holds 3 * pa_norm_bwd_nparts(rows) * cols floats.
+PA_API hipError_t pa_dropout_add_norm_bwd(const void* dy, const void* s, const void* w, const float* mean,
+                                          const float* rstd, const void* dsum, void* dres, void* dx, float* part,
+                                          void* dw, void* db, void* xbgrad, int xbgd, int xbaccum, int rows, int cols,
+                                          int rms, float p, uint32_t seed, uint32_t offset, int xd, int wd,
+                                          hipStream_t st) {
+  const int np = pa_norm_bwd_nparts(rows);
+  FusedArgs fa{true, nullptr, dx, xbgrad, xbgd, xbaccum, DropSpec{p, seed, offset}};
+  if (rms) {
+    PA_NORM_DISPATCH(xd, wd, true,
+                     (launch_bwd<T, WT, true>(dy, s, w, nullptr, rstd, dsum, dres, part, dw, nullptr, rows, cols, np,
+                                              st, &fa)))
+  }
+  PA_NORM_DISPATCH(xd, wd, false,
+                   (launch_bwd<T, WT, false>(dy, s, w, mean, rstd, dsum, dres, part, dw, db, rows, cols, np, st, &fa)))
 }

@@ -9,8 +9,9 @@ MI355X mapping (per decoder block):
   QKV / out / fc1 / fc2 → hipBLASLt GEMMs with fused bias epilogue (addmm)
   attention             → csrc/flash_attn.hip on strided q/k/v views of the QKV output
                           (no transposes, no S×S matrix)
-  GeLU                  → csrc/act.hip (vectorised, fp32 math)
-  dropout + residual    → csrc/act.hip fused dropout-add (mask regenerated in backward)
+  GeLU (+ fc1 bias)     → csrc/act.hip; backward writes dx and reduces the bias grad in one pass
+  dropout + residual + LayerNorm (+ out-proj bias) → ONE csrc/norm.hip kernel each way
+                          (mask regenerated in backward from a counter hash)
   LM head + loss        → GEMM + csrc/softmax_xent.hip (grad written in place of logits)
 """
 import math
@@ -74,13 +75,17 @@ class GPTAttention(nn.Layer):
             0.0, cfg.initializer_range / math.sqrt(2.0 * cfg.num_hidden_layers)))
         self.attn_dropout = cfg.attention_probs_dropout_prob
 
-    def forward(self, x):
+    def core(self, x):
+        """Attention up to (not including) the output projection: [B, S, hidden]."""
         t = _unwrap(x)
         B, S, _ = t.shape
         qkv = _unwrap(self.qkv_proj(x)).view(B, S, 3, self.num_heads, self.head_dim)
         # packed: q/k/v are strided BSHD views for the kernel and dQ/dK/dV land in one buffer
         o = F.flash_attn_qkvpacked(_wrap(qkv), dropout=self.attn_dropout, causal=True, training=self.training)[0]
-        return self.out_proj(_wrap(_unwrap(o).reshape(B, S, -1)))
+        return _wrap(_unwrap(o).reshape(B, S, -1))
+
+    def forward(self, x):
+        return self.out_proj(self.core(x))
 
 
 class GPTMLP(nn.Layer):
@@ -112,7 +117,13 @@ class GPTDecoderLayer(nn.Layer):
     def _drop(self, x):
         return F.dropout(x, self.p, training=self.training) if self.p > 0 else x
 
+    def _fused(self, x):
+        return self.training and ops.fused.dropout_add_norm_ok(_unwrap(x), None, self.p) and \
+            ops.fused.bias_act_ok(_unwrap(x), self.mlp.fc1.bias)
+
     def forward(self, x, residual=None):
+        if self._fused(x):
+            return self._forward_fused(x, residual)
         if residual is None:
             a, h = self.ln1(x), x
         else:
@@ -121,6 +132,24 @@ class GPTDecoderLayer(nn.Layer):
         attn = self.attn(a)
         b, h = IF.fused_layer_norm(self._drop(attn), self.ln2.weight, self.ln2.bias, self.ln2._epsilon, residual=h)
         return self.mlp(b), h
+
+    def _forward_fused(self, x, residual):
+        """Training path on the HIP kernels: dropout + residual add + LayerNorm is one kernel each
+        way, the out-projection and fc1 biases are applied (and their gradients reduced) inside
+        the consuming kernels, so those two GEMMs run without a bias epilogue."""
+        fz = ops.fused
+        if residual is None:
+            a, h = self.ln1(x), x
+        else:
+            a, h = fz.dropout_add_norm(_unwrap(x), None, _unwrap(residual), self.ln1.weight._t, self.ln1.bias._t,
+                                       self.ln1._epsilon, self.p)
+            a, h = _wrap(a), _wrap(h)
+        o = F.linear(self.attn.core(a), self.attn.out_proj.weight, None)
+        b, h = fz.dropout_add_norm(_unwrap(o), self.attn.out_proj.bias, _unwrap(h), self.ln2.weight._t,
+                                   self.ln2.bias._t, self.ln2._epsilon, self.p)
+        z = F.linear(_wrap(b), self.mlp.fc1.weight, None)
+        g = fz.bias_act(_unwrap(z), self.mlp.fc1.bias, 'gelu_tanh')
+        return self.mlp.fc2(_wrap(g)), _wrap(h)
 
 
 class GPTEmbeddings(nn.Layer):
@@ -158,6 +187,10 @@ class GPTModel(nn.Layer):
                 out, res = recompute(layer, out, res)
             else:
                 out, res = layer(out, res)
+        if res is not None and self.training and ops.fused.dropout_add_norm_ok(_unwrap(out), None, self.p):
+            y, _ = ops.fused.dropout_add_norm(_unwrap(out), None, _unwrap(res), self.final_norm.weight._t,
+                                              self.final_norm.bias._t, self.final_norm._epsilon, self.p)
+            return _wrap(y)
         if self.p > 0:
             out = F.dropout(out, self.p, training=self.training)
         y, _ = IF.fused_layer_norm(out, self.final_norm.weight, self.final_norm.bias, self.final_norm._epsilon,

@@ -3,7 +3,7 @@
 y = x @ W + b (W: [in, out], paddle layout).  Backward:
   dX = dY @ W^T                                (hipBLASLt)
   W.grad += X^T @ dY                           (hipBLASLt, beta = 1: accumulates in the GEMM epilogue)
-  b.grad += colsum(dY)
+  b.grad += colsum(dY)                         (csrc/act.hip pa_colsum, in place)
 so no per-parameter gradient temporary is allocated and no separate accumulate/add kernel
 runs (AccumulateGrad is bypassed; the DP/sharding engines are told the gradient is ready
 through parallel.flat_buffer.notify_grad_ready).  Used only for parameters that live in flat
@@ -14,6 +14,7 @@ Reference analogue: paddle/phi/kernels/fusion/gpu/fused_linear_param_grad_add_ke
 import torch
 
 from ..parallel.flat_buffer import flat_grad_slot, notify_grad_ready
+from . import fused
 
 
 class _LinearAccum(torch.autograd.Function):
@@ -43,12 +44,19 @@ class _LinearAccum(torch.autograd.Function):
         db = None
         if bp is not None:
             gb = flat_grad_slot(bp)
-            s = dy2.sum(0, dtype=torch.float32)
-            if gb is not None:
-                gb.add_(s.to(gb.dtype))
-                notify_grad_ready(bp)
+            if fused.colsum_ok(dy2):  # one column-blocked HIP pass, accumulated in place
+                if gb is not None:
+                    fused.colsum(dy2, gb, accumulate=True)
+                    notify_grad_ready(bp)
+                else:
+                    db = fused.colsum(dy2).to(dy2.dtype)
             else:
-                db = s.to(dy2.dtype)
+                s = dy2.sum(0, dtype=torch.float32)
+                if gb is not None:
+                    gb.add_(s.to(gb.dtype))
+                    notify_grad_ready(bp)
+                else:
+                    db = s.to(dy2.dtype)
         return dx, dw, db, None
 
 

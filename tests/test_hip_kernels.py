@@ -332,3 +332,135 @@ def test_sumsq_vectorized(dt, n, off):
     got = ops.optim.sumsq(x)
     ref = x.float().pow(2).sum()
     assert abs(float(got) - float(ref)) <= 1e-4 * float(ref) + 1e-5
+
+
+# ---- fused bias-gradient / dropout+residual+norm kernels (ops/fused.py) ----
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(16384, 2048), (1000, 6144), (37, 24), (3, 8192), (4097, 768)])
+def test_colsum_accumulate(dt, shape):
+    from paddle.ops import fused
+    x = torch.randn(*shape, device=DEV, dtype=dt)
+    ref = x.double().sum(0)
+    out = fused.colsum(x)
+    _close(out, ref, 1e-3 * math.sqrt(shape[0]), name='colsum')
+    acc = torch.randn(shape[1], device=DEV, dtype=torch.float32)
+    want = acc.double() + ref
+    fused.colsum(x, acc, accumulate=True)
+    _close(acc, want, 1e-3 * math.sqrt(shape[0]), name='colsum accum')
+    accb = torch.zeros(shape[1], device=DEV, dtype=torch.bfloat16)
+    fused.colsum(x, accb, accumulate=True)
+    _close(accb, ref, 1e-2 * ref.abs().max().item() + 1e-2, name='colsum bf16 out')
+
+
+@pytest.mark.parametrize("act", ['gelu_tanh', 'gelu', 'relu', 'silu'])
+@pytest.mark.parametrize("shape", [(2048, 8192), (33, 64)])
+def test_bias_act_fused_dbias(act, shape):
+    from paddle.ops import fused
+    import paddle
+    x = (torch.randn(*shape, device=DEV) * 2).to(torch.bfloat16).requires_grad_()
+    bp = paddle.create_parameter([shape[1]], 'bfloat16')
+    bp._t.data = (0.5 * torch.randn(shape[1], device=DEV)).to(torch.bfloat16)
+    bp._t.requires_grad_(True)
+    y = fused.bias_act(x, bp, act)
+    xr = x.detach().float().requires_grad_()
+    br = bp._t.detach().float().requires_grad_()
+    fns = {'gelu_tanh': lambda v: torch.nn.functional.gelu(v, approximate='tanh'),
+           'gelu': torch.nn.functional.gelu, 'relu': torch.relu, 'silu': torch.nn.functional.silu}
+    yr = fns[act](xr + br)
+    _close(y, yr, 3e-2, 1e-2, 'bias_act fwd')
+    g = torch.randn_like(yr)
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g)
+    _close(x.grad, xr.grad, 5e-2, 2e-2, 'bias_act dx')
+    _close(bp._t.grad, br.grad, 0.5, 2e-2, 'bias_act dbias')
+
+
+def _drop_norm_call(x, xb, res, w, b, p, seed, off, rms=False):
+    N = _native
+    rows, cols = x.shape
+    y, s = torch.empty_like(x), torch.empty_like(x)
+    mean = torch.empty(rows, device=DEV)
+    rstd = torch.empty(rows, device=DEV)
+    N.check(N.lib.pa_dropout_add_norm_fwd(N.ptr(x), N.ptr(xb), N.ptr(res), N.ptr(w), N.ptr(b), N.ptr(y), N.ptr(s),
+                                          N.ptr(mean), N.ptr(rstd), rows, cols, 1e-5, int(rms), p, seed, off,
+                                          N.dtcode(x.dtype), N.dtcode(w.dtype), N.stream()), 'fwd')
+    return y, s, mean, rstd
+
+
+@pytest.mark.parametrize("rms", [False, True])
+@pytest.mark.parametrize("shape", [(512, 2048), (65, 4096), (9, 8192)])
+def test_dropout_add_norm_fwd_bwd(rms, shape):
+    N = _native
+    rows, cols = shape
+    p, seed, off = 0.1, 1234, 7
+    bf = torch.bfloat16
+    w = (1 + 0.1 * torch.randn(cols, device=DEV)).to(bf)
+    b = (0.1 * torch.randn(cols, device=DEV)).to(bf)
+    # recover the keep-mask * scale: x = 1, no bias, residual 0  ->  s = mask / (1 - p)
+    _, m, _, _ = _drop_norm_call(torch.ones(rows, cols, device=DEV, dtype=bf), None,
+                                 torch.zeros(rows, cols, device=DEV, dtype=bf), w, b, p, seed, off, rms)
+    m = m.float()
+    keep = (m > 0).float().mean().item()
+    assert abs(keep - (1 - p)) < 0.02, keep
+    x = torch.randn(rows, cols, device=DEV, dtype=bf)
+    xb = (0.2 * torch.randn(cols, device=DEV)).to(bf)
+    res = torch.randn(rows, cols, device=DEV, dtype=bf)
+    y, s, mean, rstd = _drop_norm_call(x, xb, res, w, b, p, seed, off, rms)
+    xr, xbr, rr = (t.float().requires_grad_() for t in (x, xb, res))
+    wr, br = w.float().requires_grad_(), b.float().requires_grad_()
+    sr = (xr + xbr) * m + rr
+    if rms:
+        yr = sr * torch.rsqrt(sr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    else:
+        yr = torch.nn.functional.layer_norm(sr, [cols], wr, br, 1e-5)
+    _close(s, sr, 3e-2, 1e-2, 'sum')
+    _close(y, yr, 5e-2, 1e-2, 'y')
+    dy = torch.randn(rows, cols, device=DEV)
+    dsum = torch.randn(rows, cols, device=DEV)
+    (yr * dy).sum().backward(retain_graph=True)
+    (sr * dsum).sum().backward()
+    np_ = N.lib.pa_norm_bwd_nparts(rows)
+    part = torch.empty(3 * np_ * cols, device=DEV)
+    dres, dx = torch.empty_like(x), torch.empty_like(x)
+    dw, db = torch.empty_like(w), torch.empty_like(b)
+    dxb = torch.full((cols,), 0.5, device=DEV)  # accumulated into (fp32 slot)
+    N.check(N.lib.pa_dropout_add_norm_bwd(N.ptr(dy.to(bf)), N.ptr(s), N.ptr(w), N.ptr(mean), N.ptr(rstd),
+                                          N.ptr(dsum.to(bf)), N.ptr(dres), N.ptr(dx), N.ptr(part), N.ptr(dw),
+                                          N.ptr(db), N.ptr(dxb), 0, 1, rows, cols, int(rms), p, seed, off,
+                                          N.dtcode(bf), N.dtcode(bf), N.stream()), 'bwd')
+    _close(dres, rr.grad, 8e-2, 2e-2, 'dres')
+    _close(dx, xr.grad, 8e-2, 2e-2, 'dx')
+    _close(dw, wr.grad, 0.5, 2e-2, 'dw')
+    if not rms:
+        _close(db, br.grad, 0.5, 2e-2, 'db')
+    _close(dxb, xbr.grad + 0.5, 0.5, 2e-2, 'dxbias')
+
+
+def test_gpt_fused_block_path_trains():
+    """GPT-tiny under the training engines takes the fused dropout/norm/bias path and learns."""
+    import paddle
+    from paddle.models.gpt import gpt_config, GPTForPretraining
+    paddle.set_device('gpu:0')
+    paddle.seed(0)
+    cfg = gpt_config('gpt-tiny', hidden_dropout_prob=0.1)
+    model = GPTForPretraining(cfg)
+    opt = paddle.optimizer.AdamW(learning_rate=3e-3, parameters=model.parameters(), multi_precision=True)
+    model, opt = paddle.amp.decorate(model, opt, level='O2', dtype='bfloat16')
+    model, opt, _ = paddle.distributed.sharding.group_sharded_parallel(model, opt, level='p_g_os')
+    inner = model._layers if hasattr(model, '_layers') else model
+    layer0 = inner.gpt.layers[0]
+    ids = paddle.randint(0, cfg.vocab_size, [4, 65])
+    x, y = ids[:, :-1], ids[:, 1:]
+    assert layer0._fused(inner.gpt.embeddings(x))
+    losses = []
+    for _ in range(30):
+        loss = inner.loss(model(x), y)
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        losses.append(float(loss))
+    assert all(l == l for l in losses)
+    assert losses[-1] < losses[0] - 1.0, losses
+    b = inner.gpt.layers[1].attn.out_proj.bias
+    assert float(b._t.detach().float().abs().sum()) > 0  # bias updated through the fused gradient
