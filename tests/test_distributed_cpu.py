@@ -73,3 +73,8 @@ def test_launch_module_spawns_workers(tmp_path):
 def test_moe_expert_parallel_matches_single_process():
     out = run_workers('worker_moe.py')
     assert out.count("moe OK") == 2, out[-3000:]
+
+
+def test_rpc_sync_async_between_workers():
+    out = run_workers('worker_rpc.py', str(_port()), timeout=180)
+    assert out.count("rpc OK") == 2, out[-3000:]

@@ -425,8 +425,9 @@ def test_dropout_add_norm_fwd_bwd(rms, shape):
     dres, dx = torch.empty_like(x), torch.empty_like(x)
     dw, db = torch.empty_like(w), torch.empty_like(b)
     dxb = torch.full((cols,), 0.5, device=DEV)  # accumulated into (fp32 slot)
-    N.check(N.lib.pa_dropout_add_norm_bwd(N.ptr(dy.to(bf)), N.ptr(s), N.ptr(w), N.ptr(mean), N.ptr(rstd),
-                                          N.ptr(dsum.to(bf)), N.ptr(dres), N.ptr(dx), N.ptr(part), N.ptr(dw),
+    dyb, dsb = dy.to(bf), dsum.to(bf)  # keep both alive across the call (no allocator reuse)
+    N.check(N.lib.pa_dropout_add_norm_bwd(N.ptr(dyb), N.ptr(s), N.ptr(w), N.ptr(mean), N.ptr(rstd),
+                                          N.ptr(dsb), N.ptr(dres), N.ptr(dx), N.ptr(part), N.ptr(dw),
                                           N.ptr(db), N.ptr(dxb), 0, 1, rows, cols, int(rms), p, seed, off,
                                           N.dtcode(bf), N.dtcode(bf), N.stream()), 'bwd')
     _close(dres, rr.grad, 8e-2, 2e-2, 'dres')

@@ -40,6 +40,13 @@ def main():
         t2 = bench(lambda: torch.mm(dy, w.t()))
         t3 = bench(lambda: gw.addmm_(x.t(), dy))
         tot += t1 + t2 + t3
+        for sp in (2, 4, 8):  # split-M wgrad: one batched GEMM over M/sp slices + a sum of the partials
+            xs, ds_ = x.view(sp, M // sp, K).transpose(1, 2), dy.view(sp, M // sp, N)
+
+            def split_wgrad():
+                gw.add_(torch.bmm(xs, ds_).sum(0, dtype=torch.float32).to(gw.dtype))
+            ts = bench(split_wgrad)
+            print(f"      wgrad split-M x{sp}: {ts*1e6:7.1f} us {fl/ts/1e12:5.0f} TF", flush=True)
         print(f"{name:4s} K={K} N={N}: fwd {t1*1e6:7.1f} us {fl/t1/1e12:5.0f} TF | dgrad {t2*1e6:7.1f} us "
               f"{fl/t2/1e12:5.0f} TF | wgrad {t3*1e6:7.1f} us {fl/t3/1e12:5.0f} TF", flush=True)
         del x, w, b, dy, gw
