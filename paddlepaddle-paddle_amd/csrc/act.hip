@@ -115,6 +115,7 @@ __global__ __launch_bounds__(256) void bias_act_bwd_cs(const T* __restrict__ dy,
                                                        const T* __restrict__ bias, T* __restrict__ dx,
                                                        float* __restrict__ part, int rows, int cols, int rpb) {
   constexpr int E = 16 / sizeof(T);
+  constexpr int U = 4;  // rows in flight per lane
   const int c0 = (blockIdx.x * 256 + threadIdx.x) * E;
   if (c0 >= cols) return;  // no barriers below
   const int r0 = blockIdx.y * rpb;
@@ -124,27 +125,25 @@ __global__ __launch_bounds__(256) void bias_act_bwd_cs(const T* __restrict__ dy,
   for (int e = 0; e < E; ++e) { b[e] = 0.f; acc[e] = 0.f; }
   if (HAS_X && bias != nullptr) load_f<T, E>(bias + c0, b);
   int r = r0;
-  for (; r + 1 < r1; r += 2) {  // two rows in flight per lane
-    const size_t o0 = (size_t)r * cols + c0, o1 = o0 + cols;
-    float g0[E], g1[E];
-    load_f<T, E>(dy + o0, g0);
-    load_f<T, E>(dy + o1, g1);
-    if constexpr (HAS_X) {
-      float v0[E], v1[E];
-      load_f<T, E>(x + o0, v0);
-      load_f<T, E>(x + o1, v1);
+  for (; r + U <= r1; r += U) {
+    float g[U][E], v[U][E];
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        g0[e] *= Act::df(v0[e] + b[e]);
-        g1[e] *= Act::df(v1[e] + b[e]);
-      }
-      store_f<T, E>(dx + o0, g0);
-      store_f<T, E>(dx + o1, g1);
+    for (int u = 0; u < U; ++u) {
+      load_f<T, E>(dy + (size_t)(r + u) * cols + c0, g[u]);
+      if constexpr (HAS_X) load_f<T, E>(x + (size_t)(r + u) * cols + c0, v[u]);
     }
 #pragma unroll
-    for (int e = 0; e < E; ++e) acc[e] += g0[e] + g1[e];
+    for (int u = 0; u < U; ++u) {
+      if constexpr (HAS_X) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) g[u][e] *= Act::df(v[u][e] + b[e]);
+        store_f<T, E>(dx + (size_t)(r + u) * cols + c0, g[u]);
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[e] += g[u][e];
+    }
   }
-  if (r < r1) {
+  for (; r < r1; ++r) {
     const size_t o0 = (size_t)r * cols + c0;
     float g0[E];
     load_f<T, E>(dy + o0, g0);
@@ -163,42 +162,46 @@ __global__ __launch_bounds__(256) void bias_act_bwd_cs(const T* __restrict__ dy,
   for (int e = 0; e < E; e += 4) *reinterpret_cast<float4*>(pp + e) = make_float4(acc[e], acc[e + 1], acc[e + 2], acc[e + 3]);
 }
 
-// out[c] (+)= sum_p part[p, c]  — 4 waves split the P partial rows of 64 columns, LDS combine.
-template <typename OT>
-__global__ __launch_bounds__(256) void colsum_finish(const float* __restrict__ part, OT* __restrict__ out, int P,
-                                                     int cols, int accum) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
-  float s0 = 0.f, s1 = 0.f;
-  if (c < cols) {
-    int p = w;
-    for (; p + 4 < P; p += 8) {
-      s0 += part[(size_t)p * cols + c];
-      s1 += part[(size_t)(p + 4) * cols + c];
+// Column-blocked forward y = act(x + bias): the lane's E bias values stay in registers across
+// its rows (no per-element column index math), 4 rows in flight.
+template <typename T, typename Act>
+__global__ __launch_bounds__(256) void bias_act_fwd_2d(const T* __restrict__ x, const T* __restrict__ bias,
+                                                       T* __restrict__ y, int rows, int cols, int rpb) {
+  constexpr int E = 16 / sizeof(T);
+  constexpr int U = 4;
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * E;
+  if (c0 >= cols) return;
+  const int r0 = blockIdx.y * rpb;
+  const int r1 = min(rows, r0 + rpb);
+  float b[E];
+  load_f<T, E>(bias + c0, b);
+  int r = r0;
+  for (; r + U <= r1; r += U) {
+    float v[U][E];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load_f<T, E>(x + (size_t)(r + u) * cols + c0, v[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[u][e] = Act::f(v[u][e] + b[e]);
+      store_f<T, E>(y + (size_t)(r + u) * cols + c0, v[u]);
     }
-    for (; p < P; p += 4) s0 += part[(size_t)p * cols + c];
   }
-  red[w][lane] = s0 + s1;
-  __syncthreads();
-  if (w == 0 && c < cols) {
-    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    out[c] = from_f<OT>(accum ? to_f(out[c]) + t : t);
+  for (; r < r1; ++r) {
+    float v[E];
+    load_f<T, E>(x + (size_t)r * cols + c0, v);
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = Act::f(v[e] + b[e]);
+    store_f<T, E>(y + (size_t)r * cols + c0, v);
   }
 }
 
 // rows per block for the column-blocked kernels: aim at ~1024 blocks, >= 32 rows each
-inline int cs_rows_per_block(int rows, int colblocks) {
+int cs_rows_per_block(int rows, int colblocks) {
   long long rpb = ((long long)rows * colblocks + 1023) / 1024;
   if (rpb < 32) rpb = 32;
   if (rpb > rows) rpb = rows < 1 ? 1 : rows;
   return (int)rpb;
-}
-
-template <typename OT>
-hipError_t launch_finish(const float* part, void* out, int P, int cols, int accum, hipStream_t st) {
-  colsum_finish<OT><<<(cols + 63) / 64, 256, 0, st>>>(part, (OT*)out, P, cols, accum);
-  return hipGetLastError();
 }
 
 template <typename T, typename Act>
@@ -206,15 +209,6 @@ void launch_cs(dim3 grid, const void* dy, const void* x, const void* bias, void*
                int rpb, hipStream_t st) {
   bias_act_bwd_cs<T, Act, true><<<grid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)bias, (T*)dx, part, rows,
                                                        cols, rpb);
-}
-
-inline hipError_t finish_dt(const float* part, void* out, int odt, int P, int cols, int accum, hipStream_t st) {
-  switch (odt) {
-    case 0: return launch_finish<float>(part, out, P, cols, accum, st);
-    case 1: return launch_finish<bf16_t>(part, out, P, cols, accum, st);
-    case 2: return launch_finish<f16_t>(part, out, P, cols, accum, st);
-    default: return hipErrorInvalidValue;
-  }
 }
 
 // swiglu: y = silu(a) * b   (a, b: separate tensors of n elements, both contiguous)
@@ -321,10 +315,20 @@ __global__ __launch_bounds__(256) void dropout_bwd(const T* __restrict__ dy, T* 
   }
 }
 
+int cs_rows_per_block(int rows, int colblocks);
+
 template <typename T, typename Act>
 hipError_t launch_act(int dir, const void* dy, const void* x, const void* bias, void* out, long long n, int cols,
                       hipStream_t st) {
   constexpr int E = 16 / sizeof(T);
+  if (dir == 0 && bias != nullptr && cols % E == 0 && n % cols == 0 && n / cols < (1LL << 31)) {
+    const int rows = (int)(n / cols);
+    const int cb = (cols + 256 * E - 1) / (256 * E);
+    const int rpb = cs_rows_per_block(rows, cb);
+    bias_act_fwd_2d<T, Act><<<dim3(cb, (rows + rpb - 1) / rpb), 256, 0, st>>>((const T*)x, (const T*)bias, (T*)out,
+                                                                             rows, cols, rpb);
+    return hipGetLastError();
+  }
   const int g = grid_for(n / E + 1, 256, 256 * 8);
   if (dir == 0) bias_act_fwd<T, Act><<<g, 256, 0, st>>>((const T*)x, (const T*)bias, (T*)out, n, cols);
   else bias_act_bwd<T, Act><<<g, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)bias, (T*)out, n, cols);
@@ -422,7 +426,7 @@ PA_API hipError_t pa_bias_act_bwd_dbias(int act, const void* dy, const void* x, 
   });
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return finish_dt(part, dbias, odt, (int)grid.y, cols, accum, st);
+  return launch_colsum_finish_dt(part, dbias, odt, (int)grid.y, cols, accum, st);
 }
 
 // out (+)= colsum(dy) for dy [rows, cols] with row stride ld == cols (the bias gradient of a Linear).
@@ -439,5 +443,5 @@ PA_API hipError_t pa_colsum(const void* dy, float* part, void* out, int odt, int
   });
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return finish_dt(part, out, odt, (int)grid.y, cols, accum, st);
+  return launch_colsum_finish_dt(part, out, odt, (int)grid.y, cols, accum, st);
 }

@@ -1,0 +1,488 @@
+// Channels-last (NHWC) batch normalisation with fused residual add + ReLU, training and inference.
+//
+// Reference semantics: paddle/phi/kernels/gpu/batch_norm_kernel.cu / batch_norm_grad_kernel.cu
+// (NHWC path), paddle/phi/kernels/fusion/gpu/fused_bn_add_activation_kernel.cu and
+// fused_bn_activation_kernel.cu:  y = act(gamma * (x - mean) * rstd + beta [+ z]),
+// running = momentum * running + (1 - momentum) * batch (unbiased variance for the running var).
+//
+// MI355X design: an NHWC activation is a [R = N*H*W, C] row-major matrix, so every per-channel
+// statistic is a COLUMN reduction.  All kernels are column-blocked: a lane owns 8 consecutive
+// channels (one 16-byte bf16 vector), keeps their per-channel values (scale/shift, partial sums)
+// in registers and walks a chunk of rows with 4 rows of loads in flight; a wave touches 1 KiB
+// contiguous per row.  Partial statistics go to a [P, C] scratch and a 16-wave finisher combines
+// them (Chan's parallel mean/M2 merge for the forward — no E[x^2]-E[x]^2 cancellation).
+//   forward  : stats pass (read x) + apply pass (read x [+ z], write y)
+//   backward : reduce pass (read dy, x [, y]) + apply pass (read dy, x [, y], write dx [, dz])
+// ReLU's derivative is taken from the saved output y (y > 0), so no mask is stored.
+#include "common.h"
+
+namespace pa {
+namespace bn {
+
+constexpr int U = 4;  // rows in flight per lane
+
+// Lane -> (channel chunk, row phase) map.  Wide rows (>= 256 chunks of E channels): one row per
+// pass, blockIdx.x selects the chunk range.  Narrow rows (C = 64 ... 1024 in ResNet): the block
+// covers RPI = 256 / chunks rows per pass so all 256 lanes stay busy.
+struct Map {
+  int c0, sub, rpi;
+  bool active;
+};
+
+template <int E>
+__device__ __forceinline__ Map lane_map(int cols) {
+  const int cpt = cols / E;
+  Map m;
+  if (cpt >= 256) {
+    m.rpi = 1;
+    m.sub = 0;
+    m.c0 = (blockIdx.x * 256 + threadIdx.x) * E;
+    m.active = m.c0 < cols;
+  } else {
+    m.rpi = 256 / cpt;
+    m.sub = threadIdx.x / cpt;
+    m.c0 = (threadIdx.x % cpt) * E;
+    m.active = m.sub < m.rpi;
+  }
+  return m;
+}
+
+inline int col_blocks(int cols, int E) {
+  const int cpt = cols / E;
+  return cpt >= 256 ? (cpt + 255) / 256 : 1;
+}
+
+int rows_per_block(int rows, int colblocks) {
+  long long rpb = ((long long)rows * colblocks + 2047) / 2048;  // ~2048 blocks
+  if (rpb < 64) rpb = 64;
+  if (rpb > rows) rpb = rows < 1 ? 1 : rows;
+  return (int)rpb;
+}
+
+// Sum E-wide per-lane vectors over the lanes that share a channel chunk (narrow rows), result
+// valid in the sub == 0 lanes.  red: 256 * E floats of LDS.
+template <int E>
+__device__ __forceinline__ void block_colsum(float (&v)[E], const Map& m, float* red) {
+  if (m.rpi == 1) return;
+  __syncthreads();
+  if (m.active)
+#pragma unroll
+    for (int e = 0; e < E; ++e) red[threadIdx.x * E + e] = v[e];
+  __syncthreads();
+  if (m.active && m.sub == 0) {
+    const int cpt = 256 / m.rpi;
+    for (int s = 1; s < m.rpi; ++s)
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[e] += red[(threadIdx.x + s * cpt) * E + e];
+  }
+}
+
+// ---- forward statistics: per block chunk, sums shifted by the chunk's first row -> (mean, M2)
+template <typename T>
+__global__ __launch_bounds__(256) void stats_partial(const T* __restrict__ x, int rows, int cols, int rpb,
+                                                     float* __restrict__ pmean, float* __restrict__ pm2) {
+  constexpr int E = 16 / sizeof(T);
+  __shared__ float red[256 * E];
+  const Map m = lane_map<E>(cols);
+  const int r0 = blockIdx.y * rpb;
+  const int r1 = min(rows, r0 + rpb);
+  float k[E], s[E], q[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) { k[e] = 0.f; s[e] = 0.f; q[e] = 0.f; }
+  if (m.active) {
+    load_f<T, E>(x + (size_t)r0 * cols + m.c0, k);
+    int r = r0 + m.sub;
+    for (; r + (U - 1) * m.rpi < r1; r += U * m.rpi) {
+      float v[U][E];
+#pragma unroll
+      for (int u = 0; u < U; ++u) load_f<T, E>(x + (size_t)(r + u * m.rpi) * cols + m.c0, v[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const float d = v[u][e] - k[e];
+          s[e] += d;
+          q[e] += d * d;
+        }
+    }
+    for (; r < r1; r += m.rpi) {
+      float v[E];
+      load_f<T, E>(x + (size_t)r * cols + m.c0, v);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const float d = v[e] - k[e];
+        s[e] += d;
+        q[e] += d * d;
+      }
+    }
+  }
+  block_colsum<E>(s, m, red);
+  block_colsum<E>(q, m, red);
+  if (!m.active || m.sub != 0) return;
+  const float n = (float)(r1 - r0);
+  float mo[E], m2[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const float ds = s[e] / n;
+    mo[e] = k[e] + ds;
+    m2[e] = fmaxf(q[e] - s[e] * ds, 0.f);
+  }
+  float* pm = pmean + (size_t)blockIdx.y * cols + m.c0;
+  float* pq = pm2 + (size_t)blockIdx.y * cols + m.c0;
+#pragma unroll
+  for (int e = 0; e < E; e += 4) {
+    *reinterpret_cast<float4*>(pm + e) = make_float4(mo[e], mo[e + 1], mo[e + 2], mo[e + 3]);
+    *reinterpret_cast<float4*>(pq + e) = make_float4(m2[e], m2[e + 1], m2[e + 2], m2[e + 3]);
+  }
+}
+
+// Chan merge of P partials (all chunks rpb rows except the last) -> mean, rstd; running update.
+__global__ __launch_bounds__(1024) void stats_finish(const float* __restrict__ pmean, const float* __restrict__ pm2,
+                                                     int P, int rows, int rpb, int cols, float eps, float momentum,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     float* __restrict__ run_mean, float* __restrict__ run_var) {
+  __shared__ float sn[16][65], sm[16][65], sq[16][65];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  if (c < cols) {
+    for (int p = w; p < P; p += 16) {
+      const float np_ = (float)min(rpb, rows - p * rpb);
+      const float mp = pmean[(size_t)p * cols + c], qp = pm2[(size_t)p * cols + c];
+      const float nn = n + np_;
+      const float d = mp - mu;
+      mu += d * (np_ / nn);
+      m2 += qp + d * d * (n * np_ / nn);
+      n = nn;
+    }
+  }
+  sn[w][lane] = n;
+  sm[w][lane] = mu;
+  sq[w][lane] = m2;
+  __syncthreads();
+  if (w == 0 && c < cols) {
+    n = sn[0][lane];
+    mu = sm[0][lane];
+    m2 = sq[0][lane];
+    for (int i = 1; i < 16; ++i) {
+      const float np_ = sn[i][lane];
+      if (np_ == 0.f) continue;
+      const float nn = n + np_;
+      const float d = sm[i][lane] - mu;
+      mu += d * (np_ / nn);
+      m2 += sq[i][lane] + d * d * (n * np_ / nn);
+      n = nn;
+    }
+    const float var = m2 / n;
+    mean_out[c] = mu;
+    rstd_out[c] = rsqrtf(var + eps);
+    if (run_mean != nullptr) {
+      run_mean[c] = momentum * run_mean[c] + (1.f - momentum) * mu;
+      run_var[c] = momentum * run_var[c] + (1.f - momentum) * (n > 1.f ? m2 / (n - 1.f) : var);
+    }
+  }
+}
+
+// ---- y = act(x * a + b [+ z]),  a = gamma * rstd, b = beta - mean * a  (per channel)
+template <typename T, typename WT, bool RELU, bool RES>
+__global__ __launch_bounds__(256) void apply_fwd(const T* __restrict__ x, const T* __restrict__ z,
+                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                 const WT* __restrict__ gamma, const WT* __restrict__ beta,
+                                                 T* __restrict__ y, int rows, int cols, int rpb) {
+  constexpr int E = 16 / sizeof(T);
+  const Map m = lane_map<E>(cols);
+  if (!m.active) return;
+  const int c0 = m.c0, st = m.rpi;
+  const int r0 = blockIdx.y * rpb;
+  const int r1 = min(rows, r0 + rpb);
+  float a[E], b[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const float g = gamma != nullptr ? to_f(gamma[c0 + e]) : 1.f;
+    const float bt = beta != nullptr ? to_f(beta[c0 + e]) : 0.f;
+    a[e] = g * rstd[c0 + e];
+    b[e] = bt - mean[c0 + e] * a[e];
+  }
+  int r = r0 + m.sub;
+  for (; r + (U - 1) * st < r1; r += U * st) {
+    float v[U][E], zz[U][E];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      load_f<T, E>(x + (size_t)(r + u * st) * cols + c0, v[u]);
+      if constexpr (RES) load_f<T, E>(z + (size_t)(r + u * st) * cols + c0, zz[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        float o = v[u][e] * a[e] + b[e];
+        if constexpr (RES) o += zz[u][e];
+        if constexpr (RELU) o = fmaxf(o, 0.f);
+        v[u][e] = o;
+      }
+      store_f<T, E>(y + (size_t)(r + u * st) * cols + c0, v[u]);
+    }
+  }
+  for (; r < r1; r += st) {
+    float v[E], zz[E];
+    load_f<T, E>(x + (size_t)r * cols + c0, v);
+    if constexpr (RES) load_f<T, E>(z + (size_t)r * cols + c0, zz);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      float o = v[e] * a[e] + b[e];
+      if constexpr (RES) o += zz[e];
+      if constexpr (RELU) o = fmaxf(o, 0.f);
+      v[e] = o;
+    }
+    store_f<T, E>(y + (size_t)r * cols + c0, v);
+  }
+}
+
+// ---- backward reduce: per channel  s1 = sum g,  s2 = sum g * (x - mean),  g = dy [* (y > 0)]
+template <typename T, bool RELU>
+__global__ __launch_bounds__(256) void bwd_partial(const T* __restrict__ dy, const T* __restrict__ x,
+                                                   const T* __restrict__ y, const float* __restrict__ mean, int rows,
+                                                   int cols, int rpb, float* __restrict__ p1, float* __restrict__ p2) {
+  constexpr int E = 16 / sizeof(T);
+  __shared__ float red[256 * E];
+  const Map m = lane_map<E>(cols);
+  const int r0 = blockIdx.y * rpb;
+  const int r1 = min(rows, r0 + rpb);
+  float mu[E], s1[E], s2[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) { mu[e] = 0.f; s1[e] = 0.f; s2[e] = 0.f; }
+  if (m.active) {
+    const int c0 = m.c0, st = m.rpi;
+#pragma unroll
+    for (int e = 0; e < E; ++e) mu[e] = mean[c0 + e];
+    int r = r0 + m.sub;
+    for (; r + (U - 1) * st < r1; r += U * st) {
+      float g[U][E], v[U][E], o[U][E];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        load_f<T, E>(dy + (size_t)(r + u * st) * cols + c0, g[u]);
+        load_f<T, E>(x + (size_t)(r + u * st) * cols + c0, v[u]);
+        if constexpr (RELU) load_f<T, E>(y + (size_t)(r + u * st) * cols + c0, o[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          float gg = g[u][e];
+          if constexpr (RELU) gg = o[u][e] > 0.f ? gg : 0.f;
+          s1[e] += gg;
+          s2[e] += gg * (v[u][e] - mu[e]);
+        }
+    }
+    for (; r < r1; r += st) {
+      float g[E], v[E], o[E];
+      load_f<T, E>(dy + (size_t)r * cols + c0, g);
+      load_f<T, E>(x + (size_t)r * cols + c0, v);
+      if constexpr (RELU) load_f<T, E>(y + (size_t)r * cols + c0, o);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        float gg = g[e];
+        if constexpr (RELU) gg = o[e] > 0.f ? gg : 0.f;
+        s1[e] += gg;
+        s2[e] += gg * (v[e] - mu[e]);
+      }
+    }
+  }
+  block_colsum<E>(s1, m, red);
+  block_colsum<E>(s2, m, red);
+  if (!m.active || m.sub != 0) return;
+  float* q1 = p1 + (size_t)blockIdx.y * cols + m.c0;
+  float* q2 = p2 + (size_t)blockIdx.y * cols + m.c0;
+#pragma unroll
+  for (int e = 0; e < E; e += 4) {
+    *reinterpret_cast<float4*>(q1 + e) = make_float4(s1[e], s1[e + 1], s1[e + 2], s1[e + 3]);
+    *reinterpret_cast<float4*>(q2 + e) = make_float4(s2[e], s2[e + 1], s2[e + 2], s2[e + 3]);
+  }
+}
+
+// sums -> dbeta = s1, dgamma = s2 * rstd (param dtype), and fp32 copies for the apply pass
+template <typename WT>
+__global__ __launch_bounds__(1024) void bwd_finish(const float* __restrict__ p1, const float* __restrict__ p2, int P,
+                                                   int cols, const float* __restrict__ rstd, WT* __restrict__ dgamma,
+                                                   WT* __restrict__ dbeta, float* __restrict__ s_out) {
+  __shared__ float r1[16][65], r2[16][65];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float a = 0.f, b = 0.f, a2 = 0.f, b2 = 0.f;
+  if (c < cols) {
+    int p = w;
+    for (; p + 16 < P; p += 32) {
+      a += p1[(size_t)p * cols + c];
+      b += p2[(size_t)p * cols + c];
+      a2 += p1[(size_t)(p + 16) * cols + c];
+      b2 += p2[(size_t)(p + 16) * cols + c];
+    }
+    for (; p < P; p += 16) {
+      a += p1[(size_t)p * cols + c];
+      b += p2[(size_t)p * cols + c];
+    }
+  }
+  r1[w][lane] = a + a2;
+  r2[w][lane] = b + b2;
+  __syncthreads();
+  if (w == 0 && c < cols) {
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { s1 += r1[i][lane]; s2 += r2[i][lane]; }
+    s_out[c] = s1;
+    s_out[cols + c] = s2;
+    if (dbeta != nullptr) dbeta[c] = from_f<WT>(s1);
+    if (dgamma != nullptr) dgamma[c] = from_f<WT>(s2 * rstd[c]);
+  }
+}
+
+// dx = gamma * rstd * (g - s1/R - (x - mean) * rstd^2 * s2/R);  dz = g (residual branch)
+template <typename T, typename WT, bool RELU, bool RES>
+__global__ __launch_bounds__(256) void bwd_apply(const T* __restrict__ dy, const T* __restrict__ x,
+                                                 const T* __restrict__ y, const float* __restrict__ mean,
+                                                 const float* __restrict__ rstd, const WT* __restrict__ gamma,
+                                                 const float* __restrict__ sums, T* __restrict__ dx,
+                                                 T* __restrict__ dz, int rows, int cols, int rpb) {
+  constexpr int E = 16 / sizeof(T);
+  const Map m = lane_map<E>(cols);
+  if (!m.active) return;
+  const int c0 = m.c0, st = m.rpi;
+  const int r0 = blockIdx.y * rpb;
+  const int r1 = min(rows, r0 + rpb);
+  const float invR = 1.f / (float)rows;
+  float k1[E], k2[E], k3[E], mu[E];  // dx = k1 * g + k2 * (x - mu) + k3
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const float rs = rstd[c0 + e];
+    const float gr = (gamma != nullptr ? to_f(gamma[c0 + e]) : 1.f) * rs;
+    mu[e] = mean[c0 + e];
+    k1[e] = gr;
+    k2[e] = -gr * rs * rs * sums[cols + c0 + e] * invR;
+    k3[e] = -gr * sums[c0 + e] * invR;
+  }
+  int r = r0 + m.sub;
+  for (; r + (U - 1) * st < r1; r += U * st) {
+    float g[U][E], v[U][E], o[U][E];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      load_f<T, E>(dy + (size_t)(r + u * st) * cols + c0, g[u]);
+      load_f<T, E>(x + (size_t)(r + u * st) * cols + c0, v[u]);
+      if constexpr (RELU) load_f<T, E>(y + (size_t)(r + u * st) * cols + c0, o[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if constexpr (RELU) g[u][e] = o[u][e] > 0.f ? g[u][e] : 0.f;
+        v[u][e] = k1[e] * g[u][e] + k2[e] * (v[u][e] - mu[e]) + k3[e];
+      }
+      store_f<T, E>(dx + (size_t)(r + u * st) * cols + c0, v[u]);
+      if constexpr (RES) store_f<T, E>(dz + (size_t)(r + u * st) * cols + c0, g[u]);
+    }
+  }
+  for (; r < r1; r += st) {
+    float g[E], v[E], o[E];
+    load_f<T, E>(dy + (size_t)r * cols + c0, g);
+    load_f<T, E>(x + (size_t)r * cols + c0, v);
+    if constexpr (RELU) load_f<T, E>(y + (size_t)r * cols + c0, o);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if constexpr (RELU) g[e] = o[e] > 0.f ? g[e] : 0.f;
+      v[e] = k1[e] * g[e] + k2[e] * (v[e] - mu[e]) + k3[e];
+    }
+    store_f<T, E>(dx + (size_t)r * cols + c0, v);
+    if constexpr (RES) store_f<T, E>(dz + (size_t)r * cols + c0, g);
+  }
+}
+
+template <typename T, typename WT>
+hipError_t fwd(const void* x, const void* z, const void* gamma, const void* beta, void* y, float* mean, float* rstd,
+               float* run_mean, float* run_var, float* ws, int rows, int cols, float eps, float momentum, int training,
+               int relu, hipStream_t st) {
+  constexpr int E = 16 / sizeof(T);
+  const int cb = col_blocks(cols, E);
+  const int rpb = rows_per_block(rows, cb);
+  const int P = (rows + rpb - 1) / rpb;
+  const dim3 grid(cb, P);
+  if (training) {
+    stats_partial<T><<<grid, 256, 0, st>>>((const T*)x, rows, cols, rpb, ws, ws + (size_t)P * cols);
+    stats_finish<<<(cols + 63) / 64, 1024, 0, st>>>(ws, ws + (size_t)P * cols, P, rows, rpb, cols, eps, momentum,
+                                                    mean, rstd, run_mean, run_var);
+  }
+#define PA_BNF(R, Z) apply_fwd<T, WT, R, Z><<<grid, 256, 0, st>>>((const T*)x, (const T*)z, mean, rstd, \
+                                                                 (const WT*)gamma, (const WT*)beta, (T*)y, rows, cols, rpb)
+  if (relu && z) PA_BNF(true, true);
+  else if (relu) PA_BNF(true, false);
+  else if (z) PA_BNF(false, true);
+  else PA_BNF(false, false);
+#undef PA_BNF
+  return hipGetLastError();
+}
+
+template <typename T, typename WT>
+hipError_t bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
+               void* dx, void* dz, void* dgamma, void* dbeta, float* ws, int rows, int cols, int relu,
+               hipStream_t st) {
+  constexpr int E = 16 / sizeof(T);
+  const int cb = col_blocks(cols, E);
+  const int rpb = rows_per_block(rows, cb);
+  const int P = (rows + rpb - 1) / rpb;
+  const dim3 grid(cb, P);
+  float* p1 = ws;
+  float* p2 = ws + (size_t)P * cols;
+  float* sums = ws + (size_t)2 * P * cols;
+  if (relu)
+    bwd_partial<T, true><<<grid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)y, mean, rows, cols, rpb, p1, p2);
+  else
+    bwd_partial<T, false><<<grid, 256, 0, st>>>((const T*)dy, (const T*)x, nullptr, mean, rows, cols, rpb, p1, p2);
+  bwd_finish<WT><<<(cols + 63) / 64, 1024, 0, st>>>(p1, p2, P, cols, rstd, (WT*)dgamma, (WT*)dbeta, sums);
+#define PA_BNB(R, Z) bwd_apply<T, WT, R, Z><<<grid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)y, mean, rstd, \
+                                                                 (const WT*)gamma, sums, (T*)dx, (T*)dz, rows, cols, rpb)
+  if (relu && dz) PA_BNB(true, true);
+  else if (relu) PA_BNB(true, false);
+  else if (dz) PA_BNB(false, true);
+  else PA_BNB(false, false);
+#undef PA_BNB
+  return hipGetLastError();
+}
+
+}  // namespace bn
+}  // namespace pa
+
+using namespace pa;
+
+// scratch floats the kernels need (callers allocate ws of this many fp32)
+PA_API long long pa_bn_ws_floats(int rows, int cols, int dt) {
+  const int E = dt == 0 ? 4 : 8;
+  const int cb = bn::col_blocks(cols, E);
+  const int rpb = bn::rows_per_block(rows, cb);
+  const long long P = (rows + rpb - 1) / rpb;
+  return 2 * P * cols + 2LL * cols;
+}
+
+#define PA_BN_DISPATCH(xd, wd, CALL)                                             \
+  if (xd == 1 && wd == 0) { using T = bf16_t; using WT = float; return CALL; }   \
+  if (xd == 1 && wd == 1) { using T = bf16_t; using WT = bf16_t; return CALL; }  \
+  if (xd == 2 && wd == 0) { using T = f16_t; using WT = float; return CALL; }    \
+  if (xd == 2 && wd == 2) { using T = f16_t; using WT = f16_t; return CALL; }    \
+  if (xd == 0 && wd == 0) { using T = float; using WT = float; return CALL; }    \
+  return hipErrorInvalidValue;
+
+// x, z (residual, nullable), y: [rows, cols] NHWC; mean/rstd: [cols] fp32 (computed when training,
+// read otherwise: pass mean = running mean, rstd = 1/sqrt(running var + eps) for inference).
+PA_API hipError_t pa_bn_fwd(const void* x, const void* z, const void* gamma, const void* beta, void* y, float* mean,
+                            float* rstd, float* run_mean, float* run_var, float* ws, int rows, int cols, float eps,
+                            float momentum, int training, int relu, int xd, int wd, hipStream_t st) {
+  if (cols % (xd == 0 ? 4 : 8) != 0 || rows < 1) return hipErrorInvalidValue;
+  PA_BN_DISPATCH(xd, wd, (bn::fwd<T, WT>(x, z, gamma, beta, y, mean, rstd, run_mean, run_var, ws, rows, cols, eps,
+                                          momentum, training, relu, st)))
+}
+
+// dz (nullable): gradient of the residual input z (= dy masked by ReLU).  y is the saved output
+// (needed only when relu).  dgamma/dbeta in the parameter dtype (nullable).
+PA_API hipError_t pa_bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd,
+                            const void* gamma, void* dx, void* dz, void* dgamma, void* dbeta, float* ws, int rows,
+                            int cols, int relu, int xd, int wd, hipStream_t st) {
+  if (cols % (xd == 0 ? 4 : 8) != 0 || rows < 1) return hipErrorInvalidValue;
+  PA_BN_DISPATCH(xd, wd, (bn::bwd<T, WT>(dy, x, y, mean, rstd, gamma, dx, dz, dgamma, dbeta, ws, rows, cols, relu, st)))
+}

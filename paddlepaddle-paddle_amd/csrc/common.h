@@ -107,6 +107,55 @@ inline int grid_for(long long work_items, int per_block, int cap = 256 * 16) {
   return (int)g;
 }
 
+
+// out[c] (+)= sum_p part[p, c] over a [P, cols] fp32 partial-sum matrix (the second pass of every
+// column reduction here: bias / gamma / beta gradients).  Block = 16 waves x 64 columns; wave w
+// sums rows w, w+16, ... with 4 independent loads in flight per lane (each wave-row read is
+// 256 contiguous bytes), then a 16-way LDS combine.  Deterministic (fixed order, no atomics).
+template <typename OT>
+__global__ __launch_bounds__(1024) void colsum_finish(const float* __restrict__ part, OT* __restrict__ out, int P,
+                                                      int cols, int accum) {
+  __shared__ float red[16][65];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < cols) {
+    int p = w;
+    for (; p + 48 < P; p += 64) {
+      s0 += part[(size_t)p * cols + c];
+      s1 += part[(size_t)(p + 16) * cols + c];
+      s2 += part[(size_t)(p + 32) * cols + c];
+      s3 += part[(size_t)(p + 48) * cols + c];
+    }
+    for (; p < P; p += 16) s0 += part[(size_t)p * cols + c];
+  }
+  red[w][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (w == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][lane];
+    out[c] = from_f<OT>(accum ? to_f(out[c]) + t : t);
+  }
+}
+
+template <typename OT>
+inline hipError_t launch_colsum_finish(const float* part, void* out, int P, int cols, int accum, hipStream_t st) {
+  colsum_finish<OT><<<(cols + 63) / 64, 1024, 0, st>>>(part, (OT*)out, P, cols, accum);
+  return hipGetLastError();
+}
+
+// dtype-coded output (0 fp32, 1 bf16, 2 fp16)
+inline hipError_t launch_colsum_finish_dt(const float* part, void* out, int odt, int P, int cols, int accum,
+                                          hipStream_t st) {
+  switch (odt) {
+    case 0: return launch_colsum_finish<float>(part, out, P, cols, accum, st);
+    case 1: return launch_colsum_finish<bf16_t>(part, out, P, cols, accum, st);
+    case 2: return launch_colsum_finish<f16_t>(part, out, P, cols, accum, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 }  // namespace pa
 
 #define PA_DISPATCH_DTYPE(code, T, ...)                         \

@@ -79,6 +79,73 @@ __global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, T* _
 // grad may be bf16/fp16/fp32; `lowp` (optional) receives the updated param in the model dtype.
 // lr/b1pow/b2pow are read from device scalars so a captured hipGraph replays with fresh values.
 template <typename G, typename P>
+__device__ __forceinline__ void adamw_vec8(float* __restrict__ p, const G* __restrict__ g, float* __restrict__ m,
+                                           float* __restrict__ v, P* __restrict__ lowp, long long i, float gs,
+                                           float decay, float b1, float b2, float step, float eps_hat) {
+  constexpr int E = 8;
+  float pv[E], gv[E], mv[E], vv[E];
+  load_f<float, 4>(p + i, *reinterpret_cast<float(*)[4]>(pv));
+  load_f<float, 4>(p + i + 4, *reinterpret_cast<float(*)[4]>(pv + 4));
+  load_f<G, E>(g + i, gv);
+  load_f<float, 4>(m + i, *reinterpret_cast<float(*)[4]>(mv));
+  load_f<float, 4>(m + i + 4, *reinterpret_cast<float(*)[4]>(mv + 4));
+  load_f<float, 4>(v + i, *reinterpret_cast<float(*)[4]>(vv));
+  load_f<float, 4>(v + i + 4, *reinterpret_cast<float(*)[4]>(vv + 4));
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const float gg = gv[e] * gs;
+    mv[e] = b1 * mv[e] + (1.f - b1) * gg;
+    vv[e] = b2 * vv[e] + (1.f - b2) * gg * gg;
+    // fast reciprocal: the update's relative error (~1 ulp) is far below bf16 resolution
+    pv[e] = pv[e] * decay - step * mv[e] * __frcp_rn(__fsqrt_rn(vv[e]) + eps_hat);
+  }
+  store_f<float, 4>(p + i, *reinterpret_cast<float(*)[4]>(pv));
+  store_f<float, 4>(p + i + 4, *reinterpret_cast<float(*)[4]>(pv + 4));
+  store_f<float, 4>(m + i, *reinterpret_cast<float(*)[4]>(mv));
+  store_f<float, 4>(m + i + 4, *reinterpret_cast<float(*)[4]>(mv + 4));
+  store_f<float, 4>(v + i, *reinterpret_cast<float(*)[4]>(vv));
+  store_f<float, 4>(v + i + 4, *reinterpret_cast<float(*)[4]>(vv + 4));
+  if (lowp != nullptr) {
+    if constexpr (sizeof(P) == 2) {
+      store_f<P, E>(lowp + i, pv);
+    } else {
+      store_f<P, 4>(lowp + i, *reinterpret_cast<float(*)[4]>(pv));
+      store_f<P, 4>(lowp + i + 4, *reinterpret_cast<float(*)[4]>(pv + 4));
+    }
+  }
+}
+
+// Unaligned fallback (views that do not start on a 16-byte boundary): one element per lane.
+template <typename G, typename P>
+__global__ __launch_bounds__(256) void adamw_scalar_kernel(float* __restrict__ p, const G* __restrict__ g,
+                                                           float* __restrict__ m, float* __restrict__ v,
+                                                           P* __restrict__ lowp, long long n,
+                                                           const float* __restrict__ lr_ptr, float lr_host, float b1,
+                                                           float b2, float eps, float wd, float b1pow, float b2pow,
+                                                           const float* __restrict__ grad_scale) {
+  const float lr = lr_ptr != nullptr ? *lr_ptr : lr_host;
+  const float gs = grad_scale != nullptr ? *grad_scale : 1.f;
+  const float bc2 = sqrtf(1.f - b2pow);
+  const float step = lr * bc2 / (1.f - b1pow);
+  const float decay = 1.f - lr * wd;
+  const float eps_hat = eps * bc2;
+  for (long long k = (long long)blockIdx.x * 256 + threadIdx.x; k < n; k += (long long)gridDim.x * 256) {
+    const float gg = to_f(g[k]) * gs;
+    float pv = p[k] * decay;
+    const float mv = b1 * m[k] + (1.f - b1) * gg;
+    const float vv = b2 * v[k] + (1.f - b2) * gg * gg;
+    pv -= step * mv / (sqrtf(vv) + eps_hat);
+    p[k] = pv;
+    m[k] = mv;
+    v[k] = vv;
+    if (lowp != nullptr) lowp[k] = from_f<P>(pv);
+  }
+}
+
+// Memory-bound (28 B/param read+write for bf16 grads/params with fp32 master/m/v): 8 params
+// per lane per iteration (every access a full 16-byte vector, the bf16 gradient included), two
+// independent iterations in flight per lane.
+template <typename G, typename P>
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const G* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, P* __restrict__ lowp,
                                                     long long n, const float* __restrict__ lr_ptr, float lr_host,
@@ -90,38 +157,26 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   const float step = lr * bc2 / (1.f - b1pow);
   const float decay = 1.f - lr * wd;
   const float eps_hat = eps * bc2;
-  constexpr int E = 4;
+  constexpr int E = 8;
   const long long nv = n / E;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) {
-    float pv[E], gv[E], mv[E], vv[E];
-    load_f<float, E>(p + i * E, pv);
-    load_f<G, E>(g + i * E, gv);
-    load_f<float, E>(m + i * E, mv);
-    load_f<float, E>(v + i * E, vv);
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const float gg = gv[e] * gs;
-      pv[e] *= decay;
-      mv[e] = b1 * mv[e] + (1.f - b1) * gg;
-      vv[e] = b2 * vv[e] + (1.f - b2) * gg * gg;
-      pv[e] -= step * mv[e] / (sqrtf(vv[e]) + eps_hat);
-    }
-    store_f<float, E>(p + i * E, pv);
-    store_f<float, E>(m + i * E, mv);
-    store_f<float, E>(v + i * E, vv);
-    if (lowp != nullptr) store_f<P, E>(lowp + i * E, pv);
+  const long long stride = (long long)gridDim.x * 256;
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + stride < nv; i += 2 * stride) {
+    adamw_vec8<G, P>(p, g, m, v, lowp, i * E, gs, decay, b1, b2, step, eps_hat);
+    adamw_vec8<G, P>(p, g, m, v, lowp, (i + stride) * E, gs, decay, b1, b2, step, eps_hat);
   }
+  if (i < nv) adamw_vec8<G, P>(p, g, m, v, lowp, i * E, gs, decay, b1, b2, step, eps_hat);
   if (blockIdx.x == 0) {
-    for (long long i = nv * E + threadIdx.x; i < n; i += 256) {
-      const float gg = to_f(g[i]) * gs;
-      float pv = p[i] * decay;
-      const float mv = b1 * m[i] + (1.f - b1) * gg;
-      const float vv = b2 * v[i] + (1.f - b2) * gg * gg;
+    for (long long k = nv * E + threadIdx.x; k < n; k += 256) {
+      const float gg = to_f(g[k]) * gs;
+      float pv = p[k] * decay;
+      const float mv = b1 * m[k] + (1.f - b1) * gg;
+      const float vv = b2 * v[k] + (1.f - b2) * gg * gg;
       pv -= step * mv / (sqrtf(vv) + eps_hat);
-      p[i] = pv;
-      m[i] = mv;
-      v[i] = vv;
-      if (lowp != nullptr) lowp[i] = from_f<P>(pv);
+      p[k] = pv;
+      m[k] = mv;
+      v[k] = vv;
+      if (lowp != nullptr) lowp[k] = from_f<P>(pv);
     }
   }
 }
@@ -204,9 +259,18 @@ PA_API hipError_t pa_rope(const void* x, void* y, const float* cosb, const float
 PA_API hipError_t pa_adamw(float* p, const void* g, float* m, float* v, void* lowp, long long n, const float* lr_ptr,
                            float lr, float b1, float b2, float eps, float wd, float b1pow, float b2pow,
                            const float* grad_scale, int gd, int pd, hipStream_t st) {
-  const int grid = grid_for(n / 4 + 1, 256, 256 * 8);
-#define PA_ADAM(G, P) \
-  adamw_kernel<G, P><<<grid, 256, 0, st>>>(p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1, b2, eps, wd, b1pow, b2pow, grad_scale)
+  const int grid = grid_for(n / 16 + 1, 256, 256 * 8);
+  // every 8-element access is a 16-byte vector (or two): all five streams must be 16-byte aligned
+  const bool aligned = ((((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g | (uintptr_t)lowp) & 15) == 0);
+#define PA_ADAM(G, P)                                                                                          \
+  do {                                                                                                         \
+    if (aligned)                                                                                               \
+      adamw_kernel<G, P><<<grid, 256, 0, st>>>(p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1, b2, eps, wd, \
+                                               b1pow, b2pow, grad_scale);                                      \
+    else                                                                                                       \
+      adamw_scalar_kernel<G, P><<<grid_for(n, 256, 256 * 8), 256, 0, st>>>(                                    \
+          p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1, b2, eps, wd, b1pow, b2pow, grad_scale);          \
+  } while (0)
   if (pd < 0) lowp = nullptr;
   const int pp = pd < 0 ? 0 : pd;
   if (gd == 0 && pp == 0) PA_ADAM(float, float);

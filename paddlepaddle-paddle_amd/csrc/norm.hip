@@ -320,32 +320,6 @@ __global__ __launch_bounds__(256) void norm_bwd_generic(const T* __restrict__ dy
   }
 }
 
-// out[c] = sum_p part[p, c]: block = 4 waves x 64 columns; the waves split the P partial rows
-// (each wave-row read is 256 contiguous bytes), then a 4-way LDS reduce.  Deterministic.
-// accum != 0: out[c] += sum (in-place gradient accumulation into a flat gradient slot).
-template <typename WT>
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, WT* __restrict__ out, int P,
-                                                     int cols, int accum = 0) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
-  float s = 0.f;
-  if (c < cols) {
-    int p = w;
-    for (; p + 12 < P; p += 16) {  // 4 independent loads in flight per lane
-      s += part[(size_t)p * cols + c] + part[(size_t)(p + 4) * cols + c] + part[(size_t)(p + 8) * cols + c] +
-           part[(size_t)(p + 12) * cols + c];
-    }
-    for (; p < P; p += 4) s += part[(size_t)p * cols + c];
-  }
-  red[w][lane] = s;
-  __syncthreads();
-  if (w == 0 && c < cols) {
-    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    out[c] = from_f<WT>(accum ? to_f(out[c]) + t : t);
-  }
-}
-
 struct FusedArgs {  // the fused (bias +) dropout + residual path; drop == false: plain (add +) norm
   bool drop;
   const void* xbias;  // forward: bias added to x before dropout (nullable)
@@ -354,21 +328,6 @@ struct FusedArgs {  // the fused (bias +) dropout + residual path; drop == false
   int xbgd, xbaccum;
   DropSpec dsp;
 };
-
-template <typename OT>
-hipError_t finish_colsum(const float* part, void* out, int P, int cols, int accum, hipStream_t st) {
-  colsum_kernel<OT><<<(cols + 63) / 64, 256, 0, st>>>(part, (OT*)out, P, cols, accum);
-  return hipGetLastError();
-}
-
-inline hipError_t finish_colsum_dt(const float* part, void* out, int dt, int P, int cols, int accum, hipStream_t st) {
-  switch (dt) {
-    case 0: return finish_colsum<float>(part, out, P, cols, accum, st);
-    case 1: return finish_colsum<bf16_t>(part, out, P, cols, accum, st);
-    case 2: return finish_colsum<f16_t>(part, out, P, cols, accum, st);
-    default: return hipErrorInvalidValue;
-  }
-}
 
 template <typename T, typename WT, bool RMS>
 hipError_t launch_fwd(const void* x, const void* res, const void* w, const void* b, void* y, void* sum_out,
@@ -441,13 +400,11 @@ hipError_t launch_bwd(const void* dy, const void* x, const void* w, const float*
 #undef PA_NB
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int g = (cols + 63) / 64;
-  colsum_kernel<WT><<<g, 256, 0, st>>>(dw_part, (WT*)dw, nparts, cols);
-  if (!RMS && db != nullptr) colsum_kernel<WT><<<g, 256, 0, st>>>(db_part, (WT*)db, nparts, cols);
-  if (xb_part != nullptr) {
-    e = finish_colsum_dt(xb_part, fa->xbgrad, fa->xbgd, nparts, cols, fa->xbaccum, st);
-    if (e != hipSuccess) return e;
-  }
+  e = launch_colsum_finish<WT>(dw_part, dw, nparts, cols, 0, st);
+  if (e == hipSuccess && !RMS && db != nullptr) e = launch_colsum_finish<WT>(db_part, db, nparts, cols, 0, st);
+  if (e == hipSuccess && xb_part != nullptr)
+    e = launch_colsum_finish_dt(xb_part, fa->xbgrad, fa->xbgd, nparts, cols, fa->xbaccum, st);
+  if (e != hipSuccess) return e;
   return hipGetLastError();
 }
 

@@ -48,9 +48,21 @@ def init_rpc(name, rank=None, world_size=None, master_endpoint=None):
     world_size = int(os.environ["PADDLE_TRAINERS_NUM"]) if world_size is None else world_size
     master_endpoint = master_endpoint if master_endpoint is not None else os.environ["PADDLE_MASTER_ENDPOINT"]
     timeout = int(os.getenv("FLAGS_stop_check_timeout", "900"))
+    if master_endpoint.split(":")[0] in ("127.0.0.1", "localhost"):
+        os.environ.setdefault("TP_SOCKET_IFNAME", "lo")  # single node: do not resolve the hostname
+    # libuv TCP transport (the shm/ibv transports probe devices this pool does not expose)
+    transports = os.getenv("PADDLE_RPC_TRANSPORTS", "uv").split(",")
     opts = _trpc.TensorPipeRpcBackendOptions(init_method=f"tcp://{master_endpoint}", rpc_timeout=timeout,
-                                             num_worker_threads=int(os.getenv("PADDLE_RPC_THREADS", "8")))
-    _trpc.init_rpc(name, rank=rank, world_size=world_size, rpc_backend_options=opts)
+                                             num_worker_threads=int(os.getenv("PADDLE_RPC_THREADS", "8")),
+                                             _transports=transports)
+    # our rendezvous store lives at master_endpoint: under torchrun the tcp:// handler would
+    # otherwise connect to the elastic agent's store instead of hosting this one
+    agent = os.environ.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+    try:
+        _trpc.init_rpc(name, rank=rank, world_size=world_size, rpc_backend_options=opts)
+    finally:
+        if agent is not None:
+            os.environ["TORCHELASTIC_USE_AGENT_STORE"] = agent
     _state['name'] = name
     ep = os.getenv("PADDLE_WORKER_ENDPOINT", "")
     ip, port = (ep.split(":") + ["0"])[:2] if ep else ("127.0.0.1", "0")

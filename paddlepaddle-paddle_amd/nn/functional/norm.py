@@ -37,10 +37,14 @@ def batch_norm(x, running_mean, running_var, weight=None, bias=None, training=Fa
                data_format='NCHW', use_global_stats=None, name=None):
     t = _u(x)
     cl = data_format[-1] == 'C' and t.dim() > 2
-    if cl:
-        t = t.permute(0, t.dim() - 1, *range(1, t.dim() - 1))
     use_batch = training if use_global_stats is None else not use_global_stats
     rm, rv = _u(running_mean), _u(running_var)
+    if cl and use_batch and ops.use_hip(t) and ops.batchnorm.supported(t, None if weight is None else _u(weight)):
+        # channels-last activation = [rows, C] matrix: column-blocked HIP statistics + apply kernels
+        return _w(ops.batchnorm.bn_act_nhwc(t, None if weight is None else _u(weight),
+                                            None if bias is None else _u(bias), rm, rv, epsilon, momentum, True))
+    if cl:
+        t = t.permute(0, t.dim() - 1, *range(1, t.dim() - 1))
     out = TF.batch_norm(t, rm, rv, None if weight is None else _u(weight), None if bias is None else _u(bias),
                         use_batch, 1.0 - momentum, epsilon)
     if cl:

@@ -33,6 +33,9 @@ _SIGS = {
     'pa_colsum_nparts': [I, I, I],
     'pa_bias_act_bwd_dbias': [I, P, P, P, P, P, P, I, I, I, I, I, P],
     'pa_colsum': [P, P, P, I, I, I, I, I, P],
+    'pa_bn_ws_floats': [I, I, I],
+    'pa_bn_fwd': [P, P, P, P, P, P, P, P, P, P, I, I, F, F, I, I, I, I, P],
+    'pa_bn_bwd': [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     'pa_softmax_fwd': [P, P, I, I, I, I, P],
     'pa_softmax_bwd': [P, P, P, I, I, I, P],
     'pa_xent_fwd': [P, P, P, P, I, I, LL, I, P],
@@ -53,6 +56,8 @@ _SIGS = {
                      P],
 }
 
+_LL_RET = {'pa_bn_ws_floats'}
+
 
 def _load():
     global lib, load_error
@@ -66,7 +71,7 @@ def _load():
         for name, args in _SIGS.items():
             fn = getattr(l, name)
             fn.argtypes = args
-            fn.restype = ctypes.c_int
+            fn.restype = ctypes.c_longlong if name in _LL_RET else ctypes.c_int
         lib = l
     except OSError as e:  # pragma: no cover
         load_error = str(e)

@@ -1,0 +1,81 @@
+"""Channels-last batch norm (+ residual add + ReLU) on csrc/batchnorm.hip.
+
+Reference: paddle/phi/kernels/gpu/batch_norm_kernel.cu (NHWC), fusion/gpu/fused_bn_add_activation_kernel.cu.
+Training statistics are computed by the kernel (Chan-merged per-chunk mean/M2), running stats are
+updated in place with paddle's momentum convention (running = m * running + (1 - m) * batch).
+"""
+import torch
+
+from . import _native as N
+
+
+def _ws(rows, cols, dt, dev):
+    return torch.empty(N.lib.pa_bn_ws_floats(rows, cols, dt), dtype=torch.float32, device=dev)
+
+
+class _BNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, z, gamma, beta, run_mean, run_var, eps, momentum, training, relu):
+        C = x.shape[-1]
+        x2 = x.contiguous()
+        rows = x2.numel() // C
+        y = torch.empty_like(x2)
+        z2 = z.contiguous() if z is not None else None
+        dt = N.dtcode(x.dtype)
+        wd = N.dtcode(gamma.dtype) if gamma is not None else 0
+        if training:
+            mean = torch.empty(C, dtype=torch.float32, device=x.device)
+            rstd = torch.empty(C, dtype=torch.float32, device=x.device)
+        else:
+            mean = run_mean.float().contiguous()
+            rstd = torch.rsqrt(run_var.float() + eps)
+        rm = run_mean if (training and run_mean is not None and run_mean.dtype == torch.float32) else None
+        rv = run_var if rm is not None else None
+        ws = _ws(rows, C, dt, x.device)
+        N.check(N.lib.pa_bn_fwd(N.ptr(x2), N.ptr(z2), N.ptr(gamma), N.ptr(beta), N.ptr(y), N.ptr(mean), N.ptr(rstd),
+                                N.ptr(rm), N.ptr(rv), N.ptr(ws), rows, C, float(eps), float(momentum), int(training),
+                                int(relu), dt, wd, N.stream()), 'bn_fwd')
+        if training and run_mean is not None and rm is None:  # non-fp32 running buffers
+            with torch.no_grad():
+                xv = x2.reshape(rows, C).float()
+                run_mean.mul_(momentum).add_(xv.mean(0).to(run_mean.dtype), alpha=1 - momentum)
+                run_var.mul_(momentum).add_(xv.var(0).to(run_var.dtype), alpha=1 - momentum)
+        ctx.save_for_backward(x2, y if relu else None, mean, rstd, gamma)
+        ctx.relu, ctx.has_z, ctx.training = relu, z is not None, training
+        ctx.has_beta = beta is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, rstd, gamma = ctx.saved_tensors
+        if not ctx.training:
+            raise RuntimeError("fused batch-norm backward with running statistics is not supported")
+        C = x.shape[-1]
+        rows = x.numel() // C
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        dz = torch.empty_like(x) if ctx.has_z else None
+        dg = torch.empty_like(gamma) if gamma is not None else None
+        db = torch.empty_like(gamma) if (gamma is not None and ctx.has_beta) else None
+        ws = _ws(rows, C, N.dtcode(x.dtype), x.device)
+        N.check(N.lib.pa_bn_bwd(N.ptr(dy), N.ptr(x), N.ptr(y), N.ptr(mean), N.ptr(rstd), N.ptr(gamma), N.ptr(dx),
+                                N.ptr(dz), N.ptr(dg), N.ptr(db), N.ptr(ws), rows, C, int(ctx.relu), N.dtcode(x.dtype),
+                                N.dtcode(gamma.dtype) if gamma is not None else 0, N.stream()), 'bn_bwd')
+        return dx, dz, dg, db, None, None, None, None, None, None
+
+
+def supported(x, gamma=None):
+    if not x.is_cuda or x.dim() < 2 or x.dtype not in (torch.bfloat16, torch.float16, torch.float32):
+        return False
+    C = x.shape[-1]
+    if C % (16 // x.element_size()) != 0:
+        return False
+    if gamma is not None and gamma.dtype not in (torch.float32, x.dtype):
+        return False
+    return N._load() is not None
+
+
+def bn_act_nhwc(x, gamma, beta, run_mean, run_var, eps=1e-5, momentum=0.9, training=True, relu=False,
+                residual=None):
+    """act(batch_norm(x) [+ residual]) for a channels-last tensor (channel = last dim)."""
+    return _BNAct.apply(x, residual, gamma, beta, run_mean, run_var, eps, momentum, training, relu)

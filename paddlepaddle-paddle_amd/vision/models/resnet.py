@@ -5,6 +5,23 @@ so reference checkpoints map 1:1.  ``data_format='NHWC'`` keeps activations chan
 layout MIOpen's fast convolution paths want on CDNA.
 """
 from ... import nn
+from ... import ops
+from ...core.tensor import _wrap, _unwrap
+
+
+def _bn_act(bn, x, relu=True, residual=None):
+    """act(bn(x) [+ residual]) — one csrc/batchnorm.hip pass each way for channels-last training
+    on the GPU (fused_bn_add_activation); the plain layer sequence otherwise."""
+    t = _unwrap(x)
+    if (bn.training and bn._data_format[-1] == 'C' and ops.use_hip(t) and isinstance(bn, nn.BatchNorm2D)
+            and bn._use_global_stats is not True and ops.batchnorm.supported(t, None if bn.weight is None else bn.weight._t)):
+        return _wrap(ops.batchnorm.bn_act_nhwc(
+            t, None if bn.weight is None else bn.weight._t, None if bn.bias is None else bn.bias._t, bn._mean._t,
+            bn._variance._t, bn._epsilon, bn._momentum, True, relu, None if residual is None else _unwrap(residual)))
+    y = bn(x)
+    if residual is not None:
+        y = y + residual
+    return nn.functional.relu(y) if relu else y
 
 
 class BasicBlock(nn.Layer):
@@ -24,11 +41,11 @@ class BasicBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
+        out = _bn_act(self.bn1, self.conv1(x))
+        out = self.conv2(out)
         if self.downsample is not None:
             identity = self.downsample(x)
-        return self.relu(out + identity)
+        return _bn_act(self.bn2, out, True, identity)
 
 
 class BottleneckBlock(nn.Layer):
@@ -53,12 +70,12 @@ class BottleneckBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
+        out = _bn_act(self.bn1, self.conv1(x))
+        out = _bn_act(self.bn2, self.conv2(out))
+        out = self.conv3(out)
         if self.downsample is not None:
             identity = self.downsample(x)
-        return self.relu(out + identity)
+        return _bn_act(self.bn3, out, True, identity)
 
 
 class ResNet(nn.Layer):

@@ -465,3 +465,75 @@ def test_gpt_fused_block_path_trains():
     assert losses[-1] < losses[0] - 1.0, losses
     b = inner.gpt.layers[1].attn.out_proj.bias
     assert float(b._t.detach().float().abs().sum()) > 0  # bias updated through the fused gradient
+
+
+# ---- channels-last batch norm (+ residual + ReLU), csrc/batchnorm.hip ----
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(2, 8, 8, 64), (4, 28, 28, 256), (3, 7, 7, 2048), (2, 5, 5, 96), (8, 14, 14, 4096)])
+@pytest.mark.parametrize("mode", ['plain', 'relu', 'add_relu'])
+def test_batchnorm_nhwc_fused(dt, shape, mode):
+    from paddle.ops import batchnorm
+    C = shape[-1]
+    x = (torch.randn(*shape, device=DEV) * 2 + 3).to(dt).requires_grad_()
+    z = torch.randn(*shape, device=DEV).to(dt).requires_grad_() if mode == 'add_relu' else None
+    g = (1 + 0.2 * torch.randn(C, device=DEV)).requires_grad_()
+    b = (0.1 * torch.randn(C, device=DEV)).requires_grad_()
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    y = batchnorm.bn_act_nhwc(x, g, b, rm, rv, 1e-5, 0.9, True, mode != 'plain', z)
+    xr = x.detach().float().requires_grad_()
+    gr, br = g.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    rmr, rvr = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    yr = torch.nn.functional.batch_norm(xr.reshape(-1, C), rmr, rvr, gr, br, True, 0.1, 1e-5).reshape(shape)
+    zr = None
+    if z is not None:
+        zr = z.detach().float().requires_grad_()
+        yr = yr + zr
+    if mode != 'plain':
+        yr = torch.relu(yr)
+    tol = 3e-2 if dt == torch.bfloat16 else 1e-4
+    _close(y, yr, tol * 2, 1e-2, 'bn y')
+    _close(rm, rmr, 1e-3, 1e-3, 'running mean')
+    _close(rv, rvr, 1e-3, 1e-3, 'running var')
+    dy = torch.randn(*shape, device=DEV)
+    y.backward(dy.to(dt))
+    yr.backward(dy)
+    _close(x.grad, xr.grad, tol * 4, 2e-2, 'bn dx')
+    n = x.numel() // C
+    _close(g.grad, gr.grad, tol * math.sqrt(n), 2e-2, 'bn dgamma')
+    _close(b.grad, br.grad, tol * math.sqrt(n), 2e-2, 'bn dbeta')
+    if z is not None:
+        _close(z.grad, zr.grad, tol * 2, 1e-2, 'bn dz')
+
+
+def test_resnet50_nhwc_train_step_uses_fused_bn():
+    import paddle
+    from paddle.vision.models import resnet50
+    from paddle.ops import batchnorm
+    paddle.set_device('gpu:0')
+    paddle.seed(0)
+    model = resnet50(data_format='NHWC', num_classes=10)
+    opt = paddle.optimizer.Momentum(learning_rate=0.05, momentum=0.9, parameters=model.parameters(),
+                                    multi_precision=True)
+    model, opt = paddle.amp.decorate(model, opt, level='O2', dtype='bfloat16')
+    calls = []
+    orig = batchnorm._BNAct.forward
+
+    def spy(ctx, *a):
+        calls.append(1)
+        return orig(ctx, *a)
+    batchnorm._BNAct.forward = staticmethod(spy)
+    try:
+        img = paddle.to_tensor(torch.randn(8, 64, 64, 3, device=DEV, dtype=torch.bfloat16))
+        lab = paddle.to_tensor(torch.randint(0, 10, (8,), device=DEV))
+        losses = []
+        for _ in range(8):
+            loss = paddle.nn.functional.cross_entropy(model(img), lab)
+            loss.backward()
+            opt.step()
+            opt.clear_grad()
+            losses.append(float(loss))
+    finally:
+        batchnorm._BNAct.forward = staticmethod(orig)
+    assert len(calls) >= 53 * 8, len(calls)
+    assert all(l == l for l in losses) and losses[-1] < losses[0], losses
