@@ -25,7 +25,7 @@ constexpr int U = 4;  // rows in flight per lane
 // pass, blockIdx.x selects the chunk range.  Narrow rows (C = 64 ... 1024 in ResNet): the block
 // covers RPI = 256 / chunks rows per pass so all 256 lanes stay busy.
 struct Map {
-  int c0, sub, rpi;
+  int c0, sub, rpi, cpt;
   bool active;
 };
 
@@ -33,6 +33,7 @@ template <int E>
 __device__ __forceinline__ Map lane_map(int cols) {
   const int cpt = cols / E;
   Map m;
+  m.cpt = cpt;
   if (cpt >= 256) {
     m.rpi = 1;
     m.sub = 0;
@@ -70,10 +71,9 @@ __device__ __forceinline__ void block_colsum(float (&v)[E], const Map& m, float*
     for (int e = 0; e < E; ++e) red[threadIdx.x * E + e] = v[e];
   __syncthreads();
   if (m.active && m.sub == 0) {
-    const int cpt = 256 / m.rpi;
     for (int s = 1; s < m.rpi; ++s)
 #pragma unroll
-      for (int e = 0; e < E; ++e) v[e] += red[(threadIdx.x + s * cpt) * E + e];
+      for (int e = 0; e < E; ++e) v[e] += red[(threadIdx.x + s * m.cpt) * E + e];
   }
 }
 

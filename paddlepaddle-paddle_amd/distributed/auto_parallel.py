@@ -213,11 +213,47 @@ def _attach(t, mesh, placements, global_shape):
     w.__dict__['placements'] = list(placements)
     w.__dict__['_global_shape'] = list(global_shape)
     w.__dict__['is_dist'] = lambda: True
+    # the torch storage carries the dist attr too: ops see it through the SPMD mode
+    # (auto_parallel_spmd: per-op sharding propagation + differentiable reshards)
+    from . import auto_parallel_spmd as spmd
+    spmd.tag(w._t, mesh, placements, global_shape)
+    if dist.is_initialized():
+        spmd.enable()
     return w
 
 
+def _dist_meta(t):
+    """(mesh, placements, global_shape) of a dist tensor, from the handle or the storage tag."""
+    if not isinstance(t, Tensor):
+        return None
+    if 'process_mesh' in t.__dict__:
+        return t.__dict__['process_mesh'], t.__dict__['placements'], t.__dict__['_global_shape']
+    from . import auto_parallel_spmd as spmd
+    return spmd.meta(t._t)
+
+
 def is_dist_tensor(t):
-    return isinstance(t, Tensor) and 'process_mesh' in t.__dict__
+    return _dist_meta(t) is not None
+
+
+def _install_tensor_props():
+    """Tensor.placements / process_mesh / is_dist() for tensors produced by SPMD-propagated ops
+    (their dist attr lives on the storage tag; shard_tensor/reshard results also carry it on
+    the handle)."""
+    def _get(i, key):
+        def f(self):
+            d = self.__dict__
+            if key in d:
+                return d[key]
+            m = _dist_meta(self)
+            return m[i] if m else None
+        return property(f)
+    Tensor.process_mesh = _get(0, 'process_mesh')
+    Tensor.placements = _get(1, 'placements')
+    Tensor.is_dist = lambda self: _dist_meta(self) is not None
+
+
+_install_tensor_props()
 
 
 def shard_tensor(data, mesh, placements, dtype=None, place=None, stop_gradient=None):
@@ -261,9 +297,15 @@ def _all_gather_dim(t, group, n, dim):
 
 def reshard(dist_tensor, mesh, placements):
     t = _unwrap(dist_tensor)
-    src_mesh = dist_tensor.__dict__.get('process_mesh', mesh)
-    src = list(dist_tensor.__dict__.get('placements', [Replicate()] * mesh.ndim))
-    gshape = dist_tensor.__dict__.get('_global_shape', list(t.shape))
+    m = _dist_meta(dist_tensor)
+    src_mesh = m[0] if m else mesh
+    src = list(m[1]) if m else [Replicate()] * mesh.ndim
+    gshape = list(m[2]) if m else list(t.shape)
+    if src_mesh == mesh and t.requires_grad and torch.is_grad_enabled():
+        # differentiable path: conjugate collectives in backward
+        from . import auto_parallel_spmd as spmd
+        _ensure_mesh_groups(mesh)
+        return _attach(_wrap(spmd._reshard_local(t, mesh, src, list(placements))), mesh, placements, gshape)
     if src_mesh != mesh:
         # cross-mesh: materialise the global value then re-slice (all ranks participate)
         full = unshard_dtensor(dist_tensor)
@@ -317,7 +359,8 @@ def reshard(dist_tensor, mesh, placements):
 
 
 def unshard_dtensor(dist_tensor):
-    mesh = dist_tensor.__dict__.get('process_mesh')
+    m = _dist_meta(dist_tensor)
+    mesh = m[0] if m else None
     if mesh is None:
         return dist_tensor
     r = reshard(dist_tensor, mesh, [Replicate()] * mesh.ndim)
@@ -380,8 +423,8 @@ class _ShardOptimizer:
             g = p._t.grad
             if g is None:
                 continue
-            mesh = p.__dict__.get('process_mesh')
-            pl = p.__dict__.get('placements')
+            m = _dist_meta(p)
+            mesh, pl = (m[0], m[1]) if m else (None, None)
             if mesh is None:
                 dist.all_reduce(g)
                 g.div_(dist.get_world_size())

@@ -339,24 +339,72 @@ class PipelineParallel(Layer):
 class PipelineParallelWithInterleave(PipelineParallel):
     """Virtual pipeline stages (reference: pipeline_parallel.py PipelineParallelWithInterleave):
     rank r holds global chunks r, r+P, r+2P, ...; activations travel rank 0 → P-1 and wrap to
-    rank 0's next chunk.  Work items run breadth-first — all micro-batches through virtual
-    chunk 0, then chunk 1, ... (backward in reverse) — which every rank executes in the same
-    global order, so asynchronous sends and blocking receives cannot deadlock; numerics equal
-    the non-interleaved schedule (gradients accumulate over micro-batches)."""
+    rank 0's next chunk.
+
+    Schedule: interleaved 1F1B (warm-up of 2(P-r-1) + (V-1)P forward units, then alternating
+    one forward / one backward unit, then the backward cool-down), the schedule of the reference's
+    interleaved pipeline; unit k runs micro-batch ``(k // PV) P + k % P`` through chunk
+    ``(k % PV) // P`` (reversed for backward).  Needs accumulate_steps % P == 0 (as the reference
+    does); otherwise the breadth-first order (every micro-batch through chunk 0, then chunk 1, …)
+    runs instead.  Activations and gradients travel on two communicators, so each (src, dst) channel
+    carries one kind of message in one global order: sends are asynchronous, receives block, and
+    the schedule is deadlock-free for every P, V (checked by simulation and the gloo tests)."""
+
+    def __init__(self, layers, hcg, strategy):
+        super().__init__(layers, hcg, strategy)
+        # a second pipe communicator for gradients (every rank creates every pipe group, in order)
+        self._grad_pg = None
+        topo = hcg.topology()
+        for ranks in topo.get_comm_list('pipe'):
+            g = hcg._mk(ranks)
+            if hcg.global_rank in ranks:
+                self._grad_pg = g
+        self.schedule = 'interleaved_1f1b'
 
     def _peer(self, delta):
         s = (self.stage_id + delta) % self.num_stages
         return self._hcg.get_rank_from_stage(s)
 
-    def _send(self, t, peer):
-        self._send_meta(t, peer)
-        self._isend(t.detach().contiguous(), peer)
+    def _pg_of(self, kind):
+        g = self._grad_pg if kind == 'grad' else self.pp_group
+        return None if g is None else getattr(g, 'pg', None)
 
-    def _recv(self, peer, dev):
-        shape, dt = self._recv_meta(peer, dev)
-        buf = torch.empty(shape, dtype=dt, device=dev)
-        dist.recv(buf, peer)
+    def _send(self, t, peer, kind='act'):
+        pg = self._pg_of(kind)
+        t = t.detach().contiguous()
+        meta = torch.tensor([len(t.shape)] + list(t.shape) + [_DT.index(t.dtype)], dtype=torch.int64, device=t.device)
+        n = torch.tensor([meta.numel()], dtype=torch.int64, device=t.device)
+        for x in (n, meta, t):
+            self._sends.append((dist.isend(x, peer, group=pg), x))
+
+    def _recv(self, peer, dev, kind='act'):
+        pg = self._pg_of(kind)
+        n = torch.empty(1, dtype=torch.int64, device=dev)
+        dist.recv(n, peer, group=pg)
+        meta = torch.empty(int(n.item()), dtype=torch.int64, device=dev)
+        dist.recv(meta, peer, group=pg)
+        m = meta.tolist()
+        nd = m[0]
+        buf = torch.empty(tuple(m[1:1 + nd]), dtype=_DT[m[1 + nd]], device=dev)
+        dist.recv(buf, peer, group=pg)
         return buf
+
+    def _units(self, n, V, P, r):
+        """The rank's ordered list of ('F' | 'B', chunk, micro-batch) units."""
+        if V == 1 or n % P != 0:
+            self.schedule = 'breadth_first'
+            return ([('F', v, m) for v in range(V) for m in range(n)] +
+                    [('B', v, m) for v in reversed(range(V)) for m in range(n)])
+        self.schedule = 'interleaved_1f1b'
+        total = n * V
+        fch = lambda k: (k % (P * V)) // P  # noqa: E731
+        mb = lambda k: (k // (P * V)) * P + k % P  # noqa: E731
+        warm = min(total, (P - r - 1) * 2 + (V - 1) * P)
+        seq = [('F', k) for k in range(warm)]
+        for i in range(total - warm):
+            seq += [('F', warm + i), ('B', i)]
+        seq += [('B', i) for i in range(total - warm, total)]
+        return [(kind, fch(k) if kind == 'F' else V - 1 - fch(k), mb(k)) for kind, k in seq]
 
     def train_batch(self, data, optimizer, lr_scheduler=None, scaler=None):
         inputs, labels = data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None)
@@ -367,35 +415,33 @@ class PipelineParallelWithInterleave(PipelineParallel):
         dev = self._dev()
         prev_rank, next_rank = self._peer(-1), self._peer(+1)
         saved = {}
-        losses = []
-        for v in range(V):
-            for m in range(n):
+        losses = {}
+        for kind, v, m in self._units(n, V, P, self.stage_id):
+            if kind == 'F':
                 if first_rank and v == 0:
                     x = mbs_in[m]
                 else:
-                    buf = self._recv(prev_rank, dev)
+                    buf = self._recv(prev_rank, dev, 'act')
                     buf.requires_grad_(True)
                     x = _wrap(buf)
                 out = self._layers(x, chunk_id=v)
                 if last_rank and v == V - 1:
                     loss = self._layers._loss_fn(out, mbs_lab[m]) if self._layers._loss_fn is not None else out
                     loss = _wrap(_unwrap(loss) / n)
-                    losses.append(_unwrap(loss).detach())
+                    losses[m] = _unwrap(loss).detach()
                     saved[(v, m)] = (x, loss)
                 else:
-                    self._send(_unwrap(out), next_rank)
+                    self._send(_unwrap(out), next_rank, 'act')
                     saved[(v, m)] = (x, out)
-        for v in reversed(range(V)):
-            for m in range(n):
+            else:
                 x, out = saved.pop((v, m))
                 if last_rank and v == V - 1:
                     _unwrap(out).backward()
                 else:
-                    o = _unwrap(out)
-                    g = self._recv(next_rank, dev)
-                    o.backward(g)
+                    g = self._recv(next_rank, dev, 'grad')
+                    _unwrap(out).backward(g)
                 if not (first_rank and v == 0):
-                    self._send(_unwrap(x).grad, prev_rank)
+                    self._send(_unwrap(x).grad, prev_rank, 'grad')
         self._drain_sends()
         self._layers.allreduce_shared_weight_gradients()
         if self._dp_group is not None and self._dp_group.nranks > 1:
@@ -411,7 +457,7 @@ class PipelineParallelWithInterleave(PipelineParallel):
         optimizer.clear_grad()
         if lr_scheduler is not None:
             lr_scheduler.step()
-        loss = torch.stack(losses).sum() if last_rank else torch.zeros((), device=dev)
+        loss = torch.stack([losses[m] for m in sorted(losses)]).sum() if last_rank else torch.zeros((), device=dev)
         loss = loss.to(dev).float()
         if P > 1:
             dist.broadcast(loss, self._hcg.get_rank_from_stage(P - 1), group=self.pp_group.pg)

@@ -10,7 +10,7 @@ from . import _native as N
 
 
 def _ws(rows, cols, dt, dev):
-    return torch.empty(N.lib.pa_bn_ws_floats(rows, cols, dt), dtype=torch.float32, device=dev)
+    return torch.empty(N._load().pa_bn_ws_floats(rows, cols, dt), dtype=torch.float32, device=dev)
 
 
 class _BNAct(torch.autograd.Function):

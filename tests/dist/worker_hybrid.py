@@ -92,18 +92,20 @@ class Block(nn.Layer):
 
 
 def pp_test(virtual=1):
+    world = int(os.environ['WORLD_SIZE'])
     s = fleet.DistributedStrategy()
-    s.hybrid_configs = {'dp_degree': 1, 'mp_degree': 1, 'pp_degree': 2}
+    s.hybrid_configs = {'dp_degree': 1, 'mp_degree': 1, 'pp_degree': world}
     s.pipeline_configs = {'accumulate_steps': 4, 'micro_batch_size': 2}
     fleet.init(is_collective=True, strategy=s)
     d = 6
-    descs = [fleet.meta_parallel.LayerDesc(Block, d) for _ in range(4)]
+    nblk = 2 * world * virtual
+    descs = [fleet.meta_parallel.LayerDesc(Block, d) for _ in range(nblk)]
     loss_fn = lambda out, y: ((out - y) ** 2).mean()  # noqa: E731
     # build the full reference on every rank with the same seed sequence
     paddle.seed(5)
-    full = [Block(d) for _ in range(4)]
+    full = [Block(d) for _ in range(nblk)]
     paddle.seed(5)
-    pl = fleet.meta_parallel.PipelineLayer(descs, num_stages=2, loss_fn=loss_fn,
+    pl = fleet.meta_parallel.PipelineLayer(descs, num_stages=world, loss_fn=loss_fn,
                                            num_virtual_pipeline_stages=virtual)
     stage = fleet.get_hybrid_communicate_group().get_stage_id()
     # copy the reference weights of this stage's blocks so both start equal
@@ -132,6 +134,8 @@ def pp_test(virtual=1):
     for blk, gi in zip(pl.run_function, owned):
         np.testing.assert_allclose(blk.fc.weight.numpy(), full[gi].fc.weight.numpy(), atol=1e-5)
     tag = 'pp' if virtual == 1 else 'vpp'
+    if virtual > 1:
+        assert model.schedule == 'interleaved_1f1b', model.schedule
     print(f"rank{dist.get_rank()} {tag} OK stage{stage}", flush=True)
 
 

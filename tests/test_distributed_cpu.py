@@ -78,3 +78,15 @@ def test_moe_expert_parallel_matches_single_process():
 def test_rpc_sync_async_between_workers():
     out = run_workers('worker_rpc.py', str(_port()), timeout=180)
     assert out.count("rpc OK") == 2, out[-3000:]
+
+
+@pytest.mark.parametrize("mode", ['pp', 'vpp'])
+def test_pipeline_four_stages(mode):
+    """4 ranks: 1F1B and the interleaved 1F1B virtual-stage schedule match single-device SGD."""
+    out = run_workers('worker_hybrid.py', mode, nproc=4)
+    assert out.count(f'{mode} OK') == 4, out[-3000:]
+
+
+def test_auto_parallel_spmd_propagation_matches_single_process():
+    out = run_workers('worker_spmd.py', timeout=180)
+    assert out.count("spmd OK") == 2, out[-3000:]
