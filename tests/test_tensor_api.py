@@ -131,3 +131,27 @@ def test_dtypes_and_cast():
     assert paddle.finfo(paddle.float16).max == 65504.0
     assert x.numpy().dtype == np.float32
     assert x.astype('bfloat16').numpy().dtype == np.uint16  # paddle's bf16 numpy convention
+
+
+def test_onnx_export_emits_model_proto(tmp_path):
+    """paddle.onnx.export writes an ONNX ModelProto (no onnx package: decoded by paddle.onnx.inspect)."""
+    import paddle
+    from paddle.static import InputSpec
+
+    class Net(paddle.nn.Layer):
+        def __init__(self):
+            super().__init__()
+            self.conv = paddle.nn.Conv2D(3, 4, 3, padding=1)
+            self.fc = paddle.nn.Linear(4 * 8 * 8, 5)
+            self.ln = paddle.nn.LayerNorm(5)
+
+        def forward(self, x):
+            h = paddle.nn.functional.relu(self.conv(x)).flatten(1)
+            return paddle.nn.functional.softmax(self.ln(self.fc(h)), -1)
+
+    f = paddle.onnx.export(Net(), str(tmp_path / 'net'), input_spec=[InputSpec([None, 3, 8, 8], 'float32', 'img')])
+    assert f.endswith('net.onnx')
+    info = paddle.onnx.inspect(f)
+    assert info['opset'] >= 13 and info['inputs'] == ['img']
+    for op in ('Conv', 'Relu', 'Gemm', 'Softmax'):
+        assert op in info['ops'], info['ops']
