@@ -136,43 +136,69 @@ __global__ __launch_bounds__(256) void stats_partial(const T* __restrict__ x, in
   }
 }
 
-// Chan merge of P partials (all chunks rpb rows except the last) -> mean, rstd; running update.
+// Merge of the P chunk statistics (every chunk has rpb rows but the last) -> mean, rstd; running
+// update.  Two parallel passes instead of a serial Chan chain: mean = sum n_p mean_p / N, then
+// M2 = sum (M2_p + n_p (mean_p - mean)^2) — the same value, no per-step division, 4 loads in flight.
 __global__ __launch_bounds__(1024) void stats_finish(const float* __restrict__ pmean, const float* __restrict__ pm2,
                                                      int P, int rows, int rpb, int cols, float eps, float momentum,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                      float* __restrict__ run_mean, float* __restrict__ run_var) {
-  __shared__ float sn[16][65], sm[16][65], sq[16][65];
+  __shared__ float red[16][65];
+  __shared__ float mshare[64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  float n = 0.f, mu = 0.f, m2 = 0.f;
+  const float nlast = (float)(rows - (P - 1) * rpb), nfull = (float)rpb;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (c < cols) {
-    for (int p = w; p < P; p += 16) {
-      const float np_ = (float)min(rpb, rows - p * rpb);
-      const float mp = pmean[(size_t)p * cols + c], qp = pm2[(size_t)p * cols + c];
-      const float nn = n + np_;
-      const float d = mp - mu;
-      mu += d * (np_ / nn);
-      m2 += qp + d * d * (n * np_ / nn);
-      n = nn;
+    int p = w;
+    for (; p + 48 < P - 1; p += 64) {  // the (short) last chunk is left to the tail loop
+      a0 += pmean[(size_t)p * cols + c];
+      a1 += pmean[(size_t)(p + 16) * cols + c];
+      a2 += pmean[(size_t)(p + 32) * cols + c];
+      a3 += pmean[(size_t)(p + 48) * cols + c];
+    }
+    for (; p < P; p += 16) {
+      const float v = pmean[(size_t)p * cols + c];
+      if (p == P - 1) a1 += v * (nlast / nfull); else a0 += v;
     }
   }
-  sn[w][lane] = n;
-  sm[w][lane] = mu;
-  sq[w][lane] = m2;
+  red[w][lane] = ((a0 + a1) + (a2 + a3)) * nfull;
+  __syncthreads();
+  if (w == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][lane];
+    mshare[lane] = t / (float)rows;
+  }
+  __syncthreads();
+  const float mu = mshare[lane];
+  a0 = a1 = a2 = a3 = 0.f;
+  if (c < cols) {
+    int p = w;
+    for (; p + 48 < P - 1; p += 64) {
+      float d;
+      d = pmean[(size_t)p * cols + c] - mu;
+      a0 += pm2[(size_t)p * cols + c] + nfull * d * d;
+      d = pmean[(size_t)(p + 16) * cols + c] - mu;
+      a1 += pm2[(size_t)(p + 16) * cols + c] + nfull * d * d;
+      d = pmean[(size_t)(p + 32) * cols + c] - mu;
+      a2 += pm2[(size_t)(p + 32) * cols + c] + nfull * d * d;
+      d = pmean[(size_t)(p + 48) * cols + c] - mu;
+      a3 += pm2[(size_t)(p + 48) * cols + c] + nfull * d * d;
+    }
+    for (; p < P; p += 16) {
+      const float d = pmean[(size_t)p * cols + c] - mu;
+      a0 += pm2[(size_t)p * cols + c] + (p == P - 1 ? nlast : nfull) * d * d;
+    }
+  }
+  __syncthreads();
+  red[w][lane] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (w == 0 && c < cols) {
-    n = sn[0][lane];
-    mu = sm[0][lane];
-    m2 = sq[0][lane];
-    for (int i = 1; i < 16; ++i) {
-      const float np_ = sn[i][lane];
-      if (np_ == 0.f) continue;
-      const float nn = n + np_;
-      const float d = sm[i][lane] - mu;
-      mu += d * (np_ / nn);
-      m2 += sq[i][lane] + d * d * (n * np_ / nn);
-      n = nn;
-    }
+    float m2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m2 += red[i][lane];
+    const float n = (float)rows;
     const float var = m2 / n;
     mean_out[c] = mu;
     rstd_out[c] = rsqrtf(var + eps);
@@ -308,22 +334,26 @@ __global__ __launch_bounds__(1024) void bwd_finish(const float* __restrict__ p1,
   __shared__ float r1[16][65], r2[16][65];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  float a = 0.f, b = 0.f, a2 = 0.f, b2 = 0.f;
+  float a = 0.f, b = 0.f, a2 = 0.f, b2 = 0.f, a3 = 0.f, b3 = 0.f, a4 = 0.f, b4 = 0.f;
   if (c < cols) {
     int p = w;
-    for (; p + 16 < P; p += 32) {
+    for (; p + 48 < P; p += 64) {
       a += p1[(size_t)p * cols + c];
       b += p2[(size_t)p * cols + c];
       a2 += p1[(size_t)(p + 16) * cols + c];
       b2 += p2[(size_t)(p + 16) * cols + c];
+      a3 += p1[(size_t)(p + 32) * cols + c];
+      b3 += p2[(size_t)(p + 32) * cols + c];
+      a4 += p1[(size_t)(p + 48) * cols + c];
+      b4 += p2[(size_t)(p + 48) * cols + c];
     }
     for (; p < P; p += 16) {
       a += p1[(size_t)p * cols + c];
       b += p2[(size_t)p * cols + c];
     }
   }
-  r1[w][lane] = a + a2;
-  r2[w][lane] = b + b2;
+  r1[w][lane] = (a + a2) + (a3 + a4);
+  r2[w][lane] = (b + b2) + (b3 + b4);
   __syncthreads();
   if (w == 0 && c < cols) {
     float s1 = 0.f, s2 = 0.f;

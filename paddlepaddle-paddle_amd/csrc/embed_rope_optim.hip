@@ -181,6 +181,45 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   }
 }
 
+// Fused (Nesterov) momentum over a flat buffer, paddle semantics (phi momentum_kernel, multi_precision):
+//   g' = rescale * g + l2 * p ;  v = mu * v + g' ;  p -= lr * (nesterov ? g' + mu * v : v)
+// fp32 master p / velocity v, gradient in the model dtype, optional low-precision param copy.
+template <typename G, typename P>
+__global__ __launch_bounds__(256) void momentum_kernel(float* __restrict__ p, const G* __restrict__ g,
+                                                       float* __restrict__ v, P* __restrict__ lowp, long long n,
+                                                       const float* __restrict__ lr_ptr, float lr_host, float mu,
+                                                       float l2, float rescale, int nesterov,
+                                                       const float* __restrict__ grad_scale) {
+  const float lr = lr_ptr != nullptr ? *lr_ptr : lr_host;
+  const float gs = (grad_scale != nullptr ? *grad_scale : 1.f) * rescale;
+  constexpr int E = 4;
+  const long long nv = n / E;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) {
+    float pv[E], gv[E], vv[E];
+    load_f<float, E>(p + i * E, pv);
+    load_f<G, E>(g + i * E, gv);
+    load_f<float, E>(v + i * E, vv);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float gg = gv[e] * gs + l2 * pv[e];
+      vv[e] = mu * vv[e] + gg;
+      pv[e] -= lr * (nesterov ? gg + mu * vv[e] : vv[e]);
+    }
+    store_f<float, E>(p + i * E, pv);
+    store_f<float, E>(v + i * E, vv);
+    if (lowp != nullptr) store_f<P, E>(lowp + i * E, pv);
+  }
+  if (blockIdx.x == 0) {
+    for (long long k = nv * E + threadIdx.x; k < n; k += 256) {
+      const float gg = to_f(g[k]) * gs + l2 * p[k];
+      const float vk = mu * v[k] + gg;
+      v[k] = vk;
+      p[k] -= lr * (nesterov ? gg + mu * vk : vk);
+      if (lowp != nullptr) lowp[k] = from_f<P>(p[k]);
+    }
+  }
+}
+
 // sum of squares of a flat buffer into out[blockIdx] (for global-norm clipping / found-inf check).
 // 16-byte vector loads (8 x 16-bit or 4 x f32 per lane), 4 in flight per lane; scalar head/tail
 // for a misaligned start or a ragged end.
@@ -288,5 +327,25 @@ PA_API int pa_sumsq_parts() { return 2048; }
 
 PA_API hipError_t pa_sumsq(const void* x, long long n, float* part, int dt, hipStream_t st) {
   PA_DISPATCH_DTYPE(dt, T, sumsq_kernel<T><<<2048, 256, 0, st>>>((const T*)x, n, part));
+  return hipGetLastError();
+}
+
+PA_API hipError_t pa_momentum(float* p, const void* g, float* v, void* lowp, long long n, const float* lr_ptr, float lr,
+                              float mu, float l2, float rescale, int nesterov, const float* grad_scale, int gd,
+                              int pd, hipStream_t st) {
+  if ((((uintptr_t)p | (uintptr_t)v | (uintptr_t)g | (uintptr_t)lowp) & 7) != 0) return hipErrorInvalidValue;
+  const int grid = grid_for(n / 4 + 1, 256, 256 * 8);
+  if (pd < 0) lowp = nullptr;
+#define PA_MOM(G, P)                                                                                         \
+  momentum_kernel<G, P><<<grid, 256, 0, st>>>(p, (const G*)g, v, (P*)lowp, n, lr_ptr, lr, mu, l2, rescale, \
+                                              nesterov, grad_scale)
+  const int pp = pd < 0 ? 0 : pd;
+  if (gd == 0 && pp == 0) PA_MOM(float, float);
+  else if (gd == 1 && pp == 1) PA_MOM(bf16_t, bf16_t);
+  else if (gd == 1 && pp == 0) PA_MOM(bf16_t, float);
+  else if (gd == 2 && pp == 2) PA_MOM(f16_t, f16_t);
+  else if (gd == 0 && pp == 1) PA_MOM(float, bf16_t);
+  else return hipErrorInvalidValue;
+#undef PA_MOM
   return hipGetLastError();
 }

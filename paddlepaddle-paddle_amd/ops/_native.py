@@ -50,6 +50,7 @@ _SIGS = {
     'pa_rope': [P, P, P, P, P, I, I, I, I, I, F, I, P],
     'pa_adamw': [P, P, P, P, P, LL, P, F, F, F, F, F, F, F, P, I, I, P],
     'pa_sumsq': [P, LL, P, I, P],
+    'pa_momentum': [P, P, P, P, LL, P, F, F, F, F, I, P, I, I, P],
     'pa_sumsq_parts': [],
     'pa_flash_fwd': [P, P, P, P, P, I, I, I, I, I, I, LLP, LLP, LLP, LLP, F, I, I, P],
     'pa_flash_bwd': [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, LLP, LLP, LLP, LLP, LLP, LLP, LLP, LLP, F, I, I,

@@ -24,3 +24,13 @@ def sumsq(x):
     parts = torch.empty(N.lib.pa_sumsq_parts(), dtype=torch.float32, device=x.device)
     N.check(N.lib.pa_sumsq(N.ptr(x), x.numel(), N.ptr(parts), N.dtcode(x.dtype), N.stream()), 'sumsq')
     return parts.sum()
+
+
+def momentum_flat(master, grad, velocity, lowp, lr, mu, l2=0.0, rescale=1.0, nesterov=False, grad_scale=None):
+    """Fused momentum over flat buffers (csrc/embed_rope_optim.hip momentum_kernel)."""
+    n = master.numel()
+    assert grad.numel() == n and velocity.numel() == n
+    pd = -1 if lowp is None else N.dtcode(lowp.dtype)
+    N.check(N.lib.pa_momentum(N.ptr(master), N.ptr(grad), N.ptr(velocity), N.ptr(lowp), n, None, float(lr), float(mu),
+                              float(l2), float(rescale), int(bool(nesterov)), N.ptr(grad_scale), N.dtcode(grad.dtype),
+                              pd, N.stream()), 'momentum')

@@ -54,6 +54,87 @@ class Momentum(Optimizer):
         upd = (g + self._momentum * v) if self._use_nesterov else v
         _write_back(p, base - lr * upd, m)
 
+    # ---- fused flat path (GPU): one csrc momentum kernel per (dtype, L2 coeff) bucket instead of
+    # ~8 elementwise launches per parameter (ResNet50: 161 parameters)
+    _flat = None
+
+    def _l2(self, p, group):
+        from ..regularizer import L2Decay
+        reg = group.get('weight_decay', self.regularization)
+        if isinstance(reg, (int, float)):
+            return float(reg)
+        if reg is None:
+            return 0.0
+        return float(reg._coeff) if isinstance(reg, L2Decay) else None
+
+    def _fusable(self):
+        if not self._parameter_list or not ops.use_hip(self._parameter_list[0]._t):
+            return False
+        for group in self._param_groups:
+            if self._l2(None, group) is None:
+                return False
+        for p in self._parameter_list:
+            if p._t.device.type != 'cuda' or getattr(p, 'regularizer', None) is not None:
+                return False
+            if p.__dict__.get('optimize_attr', {}).get('learning_rate', 1.0) != 1.0:
+                return False
+        return True
+
+    def _build_flat(self):
+        from ..parallel.flat_buffer import FlatBuffer
+        self._flat = []
+        for gi, group in enumerate(self._param_groups):
+            buckets = {}
+            for p in group['params']:
+                if p.trainable:
+                    buckets.setdefault(p._t.dtype, []).append(p)
+            for dt, ps in buckets.items():
+                fb = ps[0].__dict__.get('_flat', (None,))[0]
+                if fb is None or set(map(id, fb.params)) != set(map(id, ps)):
+                    fb = FlatBuffer(ps)
+                master = fb.data.float().clone() if dt != torch.float32 else fb.data
+                vel = torch.zeros(fb.numel, dtype=torch.float32, device=fb.device)
+                self._flat.append({'fb': fb, 'master': master, 'v': vel, 'l2': self._l2(None, group), 'group': gi})
+                for p, o in zip(fb.params, fb.offsets):
+                    n = p._t.numel()
+                    self._accumulators['velocity'][p.name] = vel[o:o + n].view(p._t.shape)
+                    if dt != torch.float32:
+                        self._master_weights[p.name] = master[o:o + n].view(p._t.shape)
+
+    def step(self):
+        if self._flat is None and self._fusable():
+            self._build_flat()
+        if self._flat is None:
+            return super().step()
+        with torch.no_grad():
+            for ent in self._flat:
+                if not ent['fb'].data_intact():
+                    self._flat = None
+                    return super().step()
+                ent['fb'].sync_grads()
+            for group in self._param_groups:
+                clip = group.get('grad_clip', self._grad_clip)
+                if clip is not None:
+                    clip(self._params_grads(group))
+            lr = self.get_lr()
+            for ent in self._flat:
+                fb = ent['fb']
+                glr = lr * self._param_groups[ent['group']].get('learning_rate', 1.0)
+                ops.optim.momentum_flat(ent['master'], fb.grad, ent['v'], fb.data if fb.dtype != torch.float32 else None,
+                                        glr, self._momentum, ent['l2'], self._rescale, self._use_nesterov)
+        self._global_step += 1
+
+    def clear_grad(self, set_to_zero=True):
+        if self._flat is None:
+            return super().clear_grad(set_to_zero)
+        for fb in {id(e['fb']): e['fb'] for e in self._flat}.values():
+            fb.grad.zero_()
+        for p in self._parameter_list:
+            if '_flat' not in p.__dict__ and p._t.grad is not None:
+                p._t.grad.zero_()
+
+    clear_gradients = clear_grad
+
 
 class Adam(Optimizer):
     _acc_names = ('moment1', 'moment2', 'beta1_pow_acc', 'beta2_pow_acc')

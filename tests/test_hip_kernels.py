@@ -549,3 +549,27 @@ def test_resnet50_nhwc_train_step_uses_fused_bn():
                 assert losses[-1] < losses[0], losses
     finally:
         batchnorm._BNAct.forward = staticmethod(orig)
+
+
+def test_momentum_flat_matches_per_parameter_path():
+    """Fused flat momentum (csrc momentum_kernel, L2 decay, fp32 master) == per-parameter reference."""
+    import paddle
+    paddle.set_device('gpu:0')
+    res = []
+    for fused in (True, False):
+        paddle.seed(3)
+        net = paddle.nn.Sequential(paddle.nn.Linear(16, 32), paddle.nn.ReLU(), paddle.nn.Linear(32, 4))
+        opt = paddle.optimizer.Momentum(learning_rate=0.05, momentum=0.9, parameters=net.parameters(),
+                                        weight_decay=1e-3, use_nesterov=True)
+        if not fused:
+            opt._fusable = lambda: False
+        x = paddle.to_tensor(torch.randn(8, 16, device=DEV, generator=torch.Generator(device=DEV).manual_seed(0)))
+        for _ in range(4):
+            loss = (net(x) ** 2).mean()
+            loss.backward()
+            opt.step()
+            opt.clear_grad()
+        assert (opt._flat is not None) == fused
+        res.append([p._t.detach().clone() for p in net.parameters()])
+    for a, b in zip(*res):
+        _close(a, b, 1e-5, 1e-5, 'momentum fused vs reference')
