@@ -44,6 +44,8 @@ class FlatBuffer:
         with torch.no_grad():
             for p, o in zip(self.params, self.offsets):
                 n = p._t.numel()
+                if p._t.grad is not None:  # built lazily after a backward: keep that gradient
+                    self.grad[o:o + n].copy_(p._t.grad.reshape(-1))
                 view = self.data[o:o + n].view(p._t.shape)
                 view.copy_(p._t.detach())
                 req = p._t.requires_grad
