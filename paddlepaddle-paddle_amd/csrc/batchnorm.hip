@@ -19,7 +19,8 @@
 namespace pa {
 namespace bn {
 
-constexpr int U = 4;  // rows in flight per lane
+constexpr int U = 4;           // rows in flight per lane
+constexpr int kRedBlocks = 512;  // block target of the partial-sum (reduction) passes
 
 // Lane -> (channel chunk, row phase) map.  Wide rows (>= 256 chunks of E channels): one row per
 // pass, blockIdx.x selects the chunk range.  Narrow rows (C = 64 ... 1024 in ResNet): the block
@@ -53,8 +54,10 @@ inline int col_blocks(int cols, int E) {
   return cpt >= 256 ? (cpt + 255) / 256 : 1;
 }
 
-int rows_per_block(int rows, int colblocks) {
-  long long rpb = ((long long)rows * colblocks + 2047) / 2048;  // ~2048 blocks
+// target: ~2048 blocks for the streaming apply passes; the reduction passes use ~512 so the
+// finisher merges few partial rows (it is latency-bound in its serial per-lane loop).
+int rows_per_block(int rows, int colblocks, int target = 2048) {
+  long long rpb = ((long long)rows * colblocks + target - 1) / target;
   if (rpb < 64) rpb = 64;
   if (rpb > rows) rpb = rows < 1 ? 1 : rows;
   return (int)rpb;
@@ -432,11 +435,12 @@ hipError_t fwd(const void* x, const void* z, const void* gamma, const void* beta
   constexpr int E = 16 / sizeof(T);
   const int cb = col_blocks(cols, E);
   const int rpb = rows_per_block(rows, cb);
-  const int P = (rows + rpb - 1) / rpb;
-  const dim3 grid(cb, P);
+  const dim3 grid(cb, (rows + rpb - 1) / rpb);
   if (training) {
-    stats_partial<T><<<grid, 256, 0, st>>>((const T*)x, rows, cols, rpb, ws, ws + (size_t)P * cols);
-    stats_finish<<<(cols + 63) / 64, 1024, 0, st>>>(ws, ws + (size_t)P * cols, P, rows, rpb, cols, eps, momentum,
+    const int rrb = rows_per_block(rows, cb, kRedBlocks);
+    const int P = (rows + rrb - 1) / rrb;
+    stats_partial<T><<<dim3(cb, P), 256, 0, st>>>((const T*)x, rows, cols, rrb, ws, ws + (size_t)P * cols);
+    stats_finish<<<(cols + 63) / 64, 1024, 0, st>>>(ws, ws + (size_t)P * cols, P, rows, rrb, cols, eps, momentum,
                                                     mean, rstd, run_mean, run_var);
   }
 #define PA_BNF(R, Z) apply_fwd<T, WT, R, Z><<<grid, 256, 0, st>>>((const T*)x, (const T*)z, mean, rstd, \
@@ -456,15 +460,17 @@ hipError_t bwd(const void* dy, const void* x, const void* y, const float* mean, 
   constexpr int E = 16 / sizeof(T);
   const int cb = col_blocks(cols, E);
   const int rpb = rows_per_block(rows, cb);
-  const int P = (rows + rpb - 1) / rpb;
-  const dim3 grid(cb, P);
+  const dim3 grid(cb, (rows + rpb - 1) / rpb);
+  const int rrb = rows_per_block(rows, cb, kRedBlocks);
+  const int P = (rows + rrb - 1) / rrb;
   float* p1 = ws;
   float* p2 = ws + (size_t)P * cols;
   float* sums = ws + (size_t)2 * P * cols;
+  const dim3 rgrid(cb, P);
   if (relu)
-    bwd_partial<T, true><<<grid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)y, mean, rows, cols, rpb, p1, p2);
+    bwd_partial<T, true><<<rgrid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)y, mean, rows, cols, rrb, p1, p2);
   else
-    bwd_partial<T, false><<<grid, 256, 0, st>>>((const T*)dy, (const T*)x, nullptr, mean, rows, cols, rpb, p1, p2);
+    bwd_partial<T, false><<<rgrid, 256, 0, st>>>((const T*)dy, (const T*)x, nullptr, mean, rows, cols, rrb, p1, p2);
   bwd_finish<WT><<<(cols + 63) / 64, 1024, 0, st>>>(p1, p2, P, cols, rstd, (WT*)dgamma, (WT*)dbeta, sums);
 #define PA_BNB(R, Z) bwd_apply<T, WT, R, Z><<<grid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)y, mean, rstd, \
                                                                  (const WT*)gamma, sums, (T*)dx, (T*)dz, rows, cols, rpb)
@@ -485,7 +491,7 @@ using namespace pa;
 PA_API long long pa_bn_ws_floats(int rows, int cols, int dt) {
   const int E = dt == 0 ? 4 : 8;
   const int cb = bn::col_blocks(cols, E);
-  const int rpb = bn::rows_per_block(rows, cb);
+  const int rpb = bn::rows_per_block(rows, cb, bn::kRedBlocks);
   const long long P = (rows + rpb - 1) / rpb;
   return 2 * P * cols + 2LL * cols;
 }

@@ -70,8 +70,18 @@ class _Fleet:
         self._strategy = None
         self._is_collective = True
         self._inited = False
+        self._ps = None
 
     def init(self, role_maker=None, is_collective=True, strategy=None, log_level="INFO"):
+        if role_maker is not None and getattr(role_maker, '_is_collective', None) is False:
+            is_collective = False
+        if not is_collective:  # parameter-server mode (distributed/ps): no collective world
+            from ..ps import PSRuntime
+            self._strategy = strategy or DistributedStrategy()
+            self._is_collective = False
+            self._ps = PSRuntime()
+            self._inited = True
+            return None
         from ..parallel import init_parallel_env
         init_parallel_env()
         self._strategy = strategy or DistributedStrategy()
@@ -96,16 +106,46 @@ class _Fleet:
         return self._hcg
 
     def worker_index(self):
+        if not self._is_collective:
+            return 0 if self._ps.role.is_server else self._ps.role.index
         return dist.get_rank() if dist.is_initialized() else 0
 
     def worker_num(self):
+        if not self._is_collective:
+            return self._ps.role.num_trainers
         return dist.get_world_size() if dist.is_initialized() else 1
 
     def is_first_worker(self):
-        return self.worker_index() == 0
+        return self.is_worker() and self.worker_index() == 0
 
     def is_worker(self):
-        return True
+        return self._is_collective or not self._ps.role.is_server
+
+    def is_server(self):
+        return (not self._is_collective) and self._ps.role.is_server
+
+    def server_num(self):
+        return 0 if self._is_collective else self._ps.role.num_servers
+
+    def server_index(self):
+        return self._ps.role.index if self.is_server() else 0
+
+    def server_endpoints(self, to_string=False):
+        eps = [] if self._is_collective else list(self._ps.role.servers)
+        return ','.join(eps) if to_string else eps
+
+    # ---- parameter-server lifecycle (reference fleet.py:893-1063)
+    def init_server(self, *args, **kwargs):
+        self._ps.init_server()
+
+    def run_server(self):
+        self._ps.run_server()
+
+    def init_worker(self, scopes=None):
+        self._ps.init_worker()
+
+    def stop_worker(self):
+        self._ps.stop_worker()
 
     def barrier_worker(self):
         if dist.is_initialized():
@@ -139,6 +179,9 @@ class _Fleet:
     def distributed_optimizer(self, optimizer, strategy=None):
         if strategy is not None:
             self._strategy = strategy
+        if not self._is_collective:
+            from ..ps import PSOptimizer
+            return PSOptimizer(optimizer, self._ps, self._strategy)
         hcg = self._hcg
         if hcg is None:
             return optimizer
@@ -219,6 +262,15 @@ worker_num = fleet.worker_num
 is_first_worker = fleet.is_first_worker
 barrier_worker = fleet.barrier_worker
 worker_endpoints = fleet.worker_endpoints
+is_server = fleet.is_server
+is_worker = fleet.is_worker
+init_server = fleet.init_server
+run_server = fleet.run_server
+init_worker = fleet.init_worker
+stop_worker = fleet.stop_worker
+server_num = fleet.server_num
+server_index = fleet.server_index
+server_endpoints = fleet.server_endpoints
 
 
 def _inited():
@@ -231,7 +283,10 @@ class UserDefinedRoleMaker:
 
 
 class PaddleCloudRoleMaker(UserDefinedRoleMaker):
-    pass
+    """Roles from the PADDLE_* / TRAINING_ROLE environment (reference role_maker.py)."""
+
+    def __init__(self, is_collective=False, **kwargs):
+        self._is_collective = is_collective
 
 
 class Role:

@@ -90,3 +90,28 @@ def test_pipeline_four_stages(mode):
 def test_auto_parallel_spmd_propagation_matches_single_process():
     out = run_workers('worker_spmd.py', timeout=180)
     assert out.count("spmd OK") == 2, out[-3000:]
+
+
+def test_parameter_server_sync_sgd_matches_full_batch():
+    """2 parameter servers + 2 trainers (dense slices + sharded sparse embedding table)."""
+    servers = [f"127.0.0.1:{_port()}" for _ in range(2)]
+    base = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS='1', CUDA_VISIBLE_DEVICES='', HIP_VISIBLE_DEVICES='',
+                PADDLE_PSERVERS_IP_PORT_LIST=','.join(servers), PADDLE_TRAINERS_NUM='2',
+                PADDLE_PS_MASTER_ENDPOINT=f"127.0.0.1:{_port()}")
+    procs = []
+    for role, idx in (('PSERVER', 0), ('PSERVER', 1), ('TRAINER', 0), ('TRAINER', 1)):
+        env = dict(base, TRAINING_ROLE=role)
+        env['PADDLE_PSERVER_ID' if role == 'PSERVER' else 'PADDLE_TRAINER_ID'] = str(idx)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, 'tests', 'dist', 'worker_ps.py')], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=240)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    text = '\n'.join(outs)
+    assert all(p.returncode == 0 for p in procs), text[-4000:]
+    assert text.count('ps OK') == 4, text[-3000:]
