@@ -1,12 +1,20 @@
 """``python -m paddle.distributed.launch`` (reference: python/paddle/distributed/launch/main.py,
 controllers/collective.py).
 
-Collective mode only (one process per MI355X): spawns ``--nproc_per_node`` (or one per entry of
+Collective mode (one process per MI355X): spawns ``--nproc_per_node`` (or one per entry of
 ``--devices/--gpus``) workers with the env the reference sets (PADDLE_TRAINER_ID,
 PADDLE_TRAINERS_NUM, PADDLE_TRAINER_ENDPOINTS, FLAGS_selected_gpus) plus torch.distributed's
 (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT), pins each worker to its GPU through
 ``HIP_VISIBLE_DEVICES``-free LOCAL_RANK selection, writes ``<log_dir>/workerlog.<i>``, and
 tears every worker down if one fails (exit code of the first failure is returned).
+
+Elastic restart (reference launch ``--max_restart`` / fleet elastic fault tolerance): with
+``--max_restart N`` a failed job is torn down and relaunched (fresh rendezvous port) up to N
+times; workers see ``PADDLE_ELASTIC_RESTART_COUNT`` and resume from their checkpoints.
+
+Parameter-server mode (``--run_mode ps`` with ``--server_num``/``--trainer_num``, reference
+controllers/ps.py): servers and trainers get TRAINING_ROLE, PADDLE_PSERVERS_IP_PORT_LIST,
+PADDLE_PSERVER_ID / PADDLE_TRAINER_ID, PADDLE_TRAINERS_NUM (see distributed/ps).
 """
 import argparse
 import os
@@ -33,25 +41,53 @@ def parse_args(argv=None):
     ap.add_argument('--log_dir', default='log')
     ap.add_argument('--job_id', default='default')
     ap.add_argument('--run_mode', default='collective')
+    ap.add_argument('--max_restart', type=int, default=0)
+    ap.add_argument('--server_num', type=int, default=None)
+    ap.add_argument('--trainer_num', type=int, default=None)
     ap.add_argument('training_script')
     ap.add_argument('training_script_args', nargs=argparse.REMAINDER)
     return ap.parse_args(argv)
 
 
-def launch(argv=None):
-    a = parse_args(argv)
-    if a.run_mode != 'collective':
-        raise SystemExit("only collective mode is supported (parameter-server mode is out of scope)")
+def _wait(procs):
+    """Wait for all; on the first failure stop the rest.  Returns the first non-zero code."""
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p, log in list(alive):
+            r = p.poll()
+            if r is None:
+                continue
+            alive.remove((p, log))
+            if r != 0 and rc == 0:
+                rc = r
+                for q, _ in alive:  # one worker failed: stop the job
+                    try:
+                        os.killpg(q.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        time.sleep(0.2)
+    return rc
+
+
+def _spawn(cmd, env, log_path, to_console):
+    log = open(log_path, 'w')
+    p = subprocess.Popen(cmd, env=env, stdout=None if to_console else log,
+                         stderr=None if to_console else subprocess.STDOUT, start_new_session=True)
+    return p, log
+
+
+def _collective(a, attempt):
     devices = a.devices.split(',') if a.devices else None
     nproc = a.nproc_per_node or (len(devices) if devices else 1)
     devices = devices or [str(i) for i in range(nproc)]
     nnodes = int(str(a.nnodes).split(':')[0])
     if a.master:
         host, port = a.master.rsplit(':', 1)
+        port = str(int(port) + attempt) if attempt else port
     else:
         host, port = '127.0.0.1', str(_free_port())
     world = nnodes * nproc
-    os.makedirs(a.log_dir, exist_ok=True)
     endpoints = ','.join(f"{host}:{int(port) + i}" for i in range(world))
     procs = []
     for i in range(nproc):
@@ -61,39 +97,55 @@ def launch(argv=None):
                     'MASTER_ADDR': host, 'MASTER_PORT': port, 'PADDLE_TRAINER_ID': str(rank),
                     'PADDLE_TRAINERS_NUM': str(world), 'PADDLE_TRAINER_ENDPOINTS': endpoints,
                     'PADDLE_CURRENT_ENDPOINT': f"{host}:{int(port) + rank}", 'FLAGS_selected_gpus': devices[i],
-                    'PADDLE_JOB_ID': a.job_id, 'PADDLE_LOCAL_DEVICE_IDS': devices[i]})
-        log = open(os.path.join(a.log_dir, f"workerlog.{i}"), 'w')
+                    'PADDLE_JOB_ID': a.job_id, 'PADDLE_LOCAL_DEVICE_IDS': devices[i],
+                    'PADDLE_ELASTIC_RESTART_COUNT': str(attempt)})
         cmd = [sys.executable, '-u', a.training_script] + a.training_script_args
-        p = subprocess.Popen(cmd, env=env, stdout=log if i else None, stderr=subprocess.STDOUT if i else None,
-                             start_new_session=True)
-        procs.append((p, log))
+        procs.append(_spawn(cmd, env, os.path.join(a.log_dir, f"workerlog.{i}"), i == 0))
+    return procs
+
+
+def _ps(a, attempt):
+    ns, nt = a.server_num or 1, a.trainer_num or 1
+    servers = [f"127.0.0.1:{_free_port()}" for _ in range(ns)]
+    base = dict(os.environ, PADDLE_PSERVERS_IP_PORT_LIST=','.join(servers), PADDLE_TRAINERS_NUM=str(nt),
+                PADDLE_PS_MASTER_ENDPOINT=f"127.0.0.1:{_free_port()}", PADDLE_JOB_ID=a.job_id,
+                PADDLE_ELASTIC_RESTART_COUNT=str(attempt))
+    cmd = [sys.executable, '-u', a.training_script] + a.training_script_args
+    procs = []
+    for i in range(ns):
+        env = dict(base, TRAINING_ROLE='PSERVER', PADDLE_PSERVER_ID=str(i), PADDLE_PORT=servers[i].split(':')[1])
+        procs.append(_spawn(cmd, env, os.path.join(a.log_dir, f"serverlog.{i}"), False))
+    for i in range(nt):
+        env = dict(base, TRAINING_ROLE='TRAINER', PADDLE_TRAINER_ID=str(i))
+        procs.append(_spawn(cmd, env, os.path.join(a.log_dir, f"workerlog.{i}"), i == 0))
+    return procs
+
+
+def launch(argv=None):
+    a = parse_args(argv)
+    if a.run_mode not in ('collective', 'ps'):
+        raise SystemExit(f"unsupported run_mode {a.run_mode!r} (collective | ps)")
+    os.makedirs(a.log_dir, exist_ok=True)
     rc = 0
-    try:
-        alive = list(procs)
-        while alive:
-            for p, log in list(alive):
-                r = p.poll()
-                if r is None:
-                    continue
-                alive.remove((p, log))
-                if r != 0 and rc == 0:
-                    rc = r
-                    for q, _ in alive:  # one worker failed: stop the job
-                        try:
-                            os.killpg(q.pid, signal.SIGTERM)
-                        except ProcessLookupError:
-                            pass
-            time.sleep(0.2)
-    except KeyboardInterrupt:
-        for p, _ in procs:
-            try:
-                os.killpg(p.pid, signal.SIGTERM)
-            except ProcessLookupError:
-                pass
-        rc = 130
-    finally:
-        for _, log in procs:
-            log.close()
+    for attempt in range(a.max_restart + 1):
+        procs = (_ps if a.run_mode == 'ps' else _collective)(a, attempt)
+        try:
+            rc = _wait(procs)
+        except KeyboardInterrupt:
+            for p, _ in procs:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+            return 130
+        finally:
+            for _, log in procs:
+                log.close()
+        if rc == 0:
+            return 0
+        if attempt < a.max_restart:
+            print(f"[launch] job failed with exit code {rc}; elastic restart {attempt + 1}/{a.max_restart}",
+                  file=sys.stderr, flush=True)
     return rc
 
 

@@ -115,3 +115,26 @@ def test_parameter_server_sync_sgd_matches_full_batch():
     text = '\n'.join(outs)
     assert all(p.returncode == 0 for p in procs), text[-4000:]
     assert text.count('ps OK') == 4, text[-3000:]
+
+
+def test_launch_elastic_restart_and_ps_mode(tmp_path):
+    """--max_restart relaunches a failed job (workers see the restart count); --run_mode ps spawns
+    servers + trainers with the PS environment."""
+    script = tmp_path / 'flaky.py'
+    script.write_text("import os, sys\nc = int(os.environ['PADDLE_ELASTIC_RESTART_COUNT'])\n"
+                      "print('attempt', c, os.environ['RANK'], flush=True)\nsys.exit(3 if c == 0 else 0)\n")
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES='')
+    r = subprocess.run([sys.executable, '-m', 'paddle.distributed.launch', '--nproc_per_node', '2', '--max_restart', '2',
+                        '--log_dir', str(tmp_path / 'log'), str(script)], env=env, capture_output=True, text=True,
+                       timeout=120, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert 'attempt 0 0' in r.stdout and 'attempt 1 0' in r.stdout and 'elastic restart 1/2' in r.stderr
+    ps = tmp_path / 'ps.py'
+    ps.write_text("import os\nprint(os.environ['TRAINING_ROLE'], os.environ.get('PADDLE_PSERVER_ID', os.environ.get("
+                  "'PADDLE_TRAINER_ID')), os.environ['PADDLE_PSERVERS_IP_PORT_LIST'].count(','), flush=True)\n")
+    r = subprocess.run([sys.executable, '-m', 'paddle.distributed.launch', '--run_mode', 'ps', '--server_num', '2',
+                        '--trainer_num', '2', '--log_dir', str(tmp_path / 'pslog'), str(ps)], env=env,
+                       capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert 'TRAINER 0 1' in r.stdout
+    assert 'PSERVER 1 1' in (tmp_path / 'pslog' / 'serverlog.1').read_text()
