@@ -138,3 +138,8 @@ def test_launch_elastic_restart_and_ps_mode(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     assert 'TRAINER 0 1' in r.stdout
     assert 'PSERVER 1 1' in (tmp_path / 'pslog' / 'serverlog.1').read_text()
+
+
+def test_llama_hybrid_tp2_pp2_matches_single_device():
+    out = run_workers('worker_llama_hybrid.py', nproc=4, timeout=300)
+    assert out.count('llama hybrid OK') == 4, out[-4000:]

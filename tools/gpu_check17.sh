@@ -8,7 +8,7 @@ timeout -k 10 300 python bench.py --model resnet50 --steps 10 --warmup 5 > gpuru
 tail -1 gpurun_out/bench17_rn.log
 timeout -k 10 300 python bench.py --steps 10 --warmup 3 > gpurun_out/bench17_before.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench17_before.log; exit 1; }
 tail -1 gpurun_out/bench17_before.log
-TUNE_MS=60 TUNE_ITERS=50 bash tools/tune_gemms.sh > gpurun_out/tune17.log 2>&1 || { echo "tune failed"; tail -20 gpurun_out/tune17.log; exit 1; }
+TUNE_MS=40 TUNE_ITERS=30 bash tools/tune_gemms.sh > gpurun_out/tune17.log 2>&1 || { echo "tune failed"; tail -20 gpurun_out/tune17.log; exit 1; }
 tail -3 gpurun_out/tune17.log
 timeout -k 10 300 python bench.py --steps 10 --warmup 3 > gpurun_out/bench17_after.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench17_after.log; exit 1; }
 tail -1 gpurun_out/bench17_after.log
