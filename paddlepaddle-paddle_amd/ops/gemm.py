@@ -7,7 +7,92 @@ FP8 (OCP e4m3fn, CDNA4 — NOT the MI300 fnuz encoding) uses per-tensor scaling 
 
 Reference: paddle/phi/kernels/funcs/blas/blaslt_impl.cu.h, fusion/fp8_gemm.
 """
+import os
+
 import torch
+
+from . import _native as N
+
+
+def _op_layout(t):
+    """(trans, ld) of a 2-D bf16 operand: 0 = row-major [rows][cols], 1 = a transposed view."""
+    if t.stride(1) == 1 and t.stride(0) >= t.shape[1]:
+        return 0, t.stride(0)
+    if t.stride(0) == 1 and t.stride(1) >= t.shape[0]:
+        return 1, t.stride(1)
+    return None, None
+
+
+_ws_cache = {}
+
+
+def _workspace(n, device):
+    w = _ws_cache.get(device)
+    if w is None or w.numel() < n:
+        w = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=device)
+        _ws_cache[device] = w
+    return w
+
+
+def hip_mm_ok(a, b, splitk=1):
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.dim() != 2 or b.dim() != 2:
+        return False
+    ta, lda = _op_layout(a)
+    tb, ldb = _op_layout(b)
+    if ta is None or tb is None or a.shape[1] != b.shape[0]:
+        return False
+    if a.data_ptr() % 16 or b.data_ptr() % 16:
+        return False
+    M, K = a.shape
+    N_ = b.shape[1]
+    return N.lib is not None and bool(N.lib.pa_gemm_ok(M, N_, K, lda, ldb, N_, splitk))
+
+
+def hip_mm(a, b, out=None, bias=None, alpha=1.0, beta=0.0, splitk=1):
+    """out[M,N] = alpha * a @ b (+ beta * out) (+ bias) on the hand-written MFMA GEMM (csrc/gemm.hip).
+
+    a: [M,K] bf16, row-major or a transposed view of a [K,M] tensor; b: [K,N] bf16, row-major
+    or a transposed view of [N,K].  ``out`` (row-major, unit column stride) is written in
+    place (with beta = 1 this is the in-place weight-gradient accumulate).
+    """
+    ta, lda = _op_layout(a)
+    # B's "trans" flag in the kernel means stored [N][K] (k contiguous)
+    tb, ldb = _op_layout(b)
+    M, K = a.shape
+    N_ = b.shape[1]
+    if out is None:
+        out = torch.empty(M, N_, dtype=torch.bfloat16, device=a.device)
+        beta = 0.0
+    assert out.stride(1) == 1 and out.shape == (M, N_)
+    ws = _workspace(splitk * M * N_, a.device) if splitk > 1 else None
+    N.check(N.lib.pa_gemm_bf16(N.ptr(a), N.ptr(b), N.ptr(out), N.ptr(bias), N.ptr(ws), M, N_, K, lda, ldb,
+                               out.stride(0), ta, tb, float(alpha), float(beta), splitk, N.stream()), 'gemm_bf16')
+    return out
+
+
+_hip_wgrad = os.environ.get('PADDLE_AMD_HIP_GEMM', '1') != '0'
+
+
+def wgrad_accumulate(x2, dy2, gw):
+    """gw[in, out] += x2^T @ dy2 (x2: [tokens, in], dy2: [tokens, out]) — the weight-gradient GEMM.
+
+    Runs on the hand-written MFMA kernel (both operands staged as they sit in HBM and read
+    with ds_read_b64_tr_b16; measured ahead of hipBLASLt on every GPT-3 1.3B weight-gradient
+    shape, tools/hip_gemm_bench.py).  Outputs with fewer 256x256 tiles than CUs split K four
+    ways.  Returns False when the shape contract does not hold (caller uses the library).
+    """
+    if not _hip_wgrad or gw.dtype != torch.bfloat16 or not gw.is_contiguous():
+        return False
+    a, b = x2.t(), dy2
+    M, N_ = gw.shape
+    tiles = -(-M // 256) * -(-N_ // 256)
+    splitk = 4 if tiles < 256 else 1
+    if not hip_mm_ok(a, b, splitk):
+        splitk = 1
+        if not hip_mm_ok(a, b, 1):
+            return False
+    hip_mm(a, b, out=gw, beta=1.0, splitk=splitk)
+    return True
 
 
 def fp8_quantize(x, dtype=torch.float8_e4m3fn):

@@ -2,7 +2,7 @@
 
 y = x @ W + b (W: [in, out], paddle layout).  Backward:
   dX = dY @ W^T                                (hipBLASLt)
-  W.grad += X^T @ dY                           (hipBLASLt, beta = 1: accumulates in the GEMM epilogue)
+  W.grad += X^T @ dY                           (hand-written MFMA GEMM csrc/gemm.hip, beta = 1 epilogue)
   b.grad += colsum(dY)                         (csrc/act.hip pa_colsum, in place)
 so no per-parameter gradient temporary is allocated and no separate accumulate/add kernel
 runs (AccumulateGrad is bypassed; the DP/sharding engines are told the gradient is ready
@@ -14,7 +14,7 @@ Reference analogue: paddle/phi/kernels/fusion/gpu/fused_linear_param_grad_add_ke
 import torch
 
 from ..parallel.flat_buffer import flat_grad_slot, notify_grad_ready
-from . import fused
+from . import fused, gemm
 
 
 class _LinearAccum(torch.autograd.Function):
@@ -36,7 +36,8 @@ class _LinearAccum(torch.autograd.Function):
         dx = torch.mm(dy2, w.t()).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
         gw = flat_grad_slot(wp)
         if gw is not None:
-            gw.addmm_(x2.t(), dy2)
+            if not gemm.wgrad_accumulate(x2, dy2, gw):
+                gw.addmm_(x2.t(), dy2)
             notify_grad_ready(wp)
             dw = None
         else:

@@ -573,3 +573,26 @@ def test_momentum_flat_matches_per_parameter_path():
         res.append([p._t.detach().clone() for p in net.parameters()])
     for a, b in zip(*res):
         _close(a, b, 1e-5, 1e-5, 'momentum fused vs reference')
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K,splitk", [(256, 256, 64, 1), (512, 768, 512, 1), (328, 264, 384, 1),
+                                          (1024, 512, 2048, 4), (200, 1000, 256, 2)])
+def test_hip_gemm_layouts(ta, tb, M, N, K, splitk):
+    """csrc/gemm.hip: all four operand layouts, ragged M/N edges, split-K, vs an fp32 reference."""
+    from paddle.ops import gemm
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    a32 = torch.rand(M, K, device=DEV, generator=g) * 2 - 1
+    b32 = torch.rand(K, N, device=DEV, generator=g) * 2 - 1
+    a = a32.bfloat16() if ta == 0 else a32.t().contiguous().bfloat16().t()
+    b = b32.bfloat16() if tb == 0 else b32.t().contiguous().bfloat16().t()
+    assert gemm.hip_mm_ok(a, b, splitk)
+    ref = a.float() @ b.float()
+    out = gemm.hip_mm(a, b, splitk=splitk)
+    _close(out, ref, atol=0.02 * math.sqrt(K) / 8 + 0.05, rtol=0.01, name=f"gemm {ta}{tb}")
+    # in-place accumulate with bias (the weight-gradient / fused-linear epilogues)
+    c = (torch.rand(M, N, device=DEV, generator=g) - 0.5).bfloat16()
+    bias = torch.rand(N, device=DEV, generator=g).bfloat16()
+    want = 0.5 * ref + c.float() + bias.float()
+    gemm.hip_mm(a, b, out=c, bias=bias, alpha=0.5, beta=1.0, splitk=splitk)
+    _close(c, want, atol=0.02 * math.sqrt(K) / 8 + 0.05, rtol=0.01, name=f"gemm acc {ta}{tb}")
