@@ -40,18 +40,15 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int BM = 256, BN = 256, BK = 32, NT = 512;
-// K is consumed in 32-deep sub-tiles through a ring of NSLOT = PF + 1 LDS slots; the DMA for
-// sub-tile s + PF is issued while sub-tile s is multiplied, and each step retires only the
-// OLDEST outstanding sub-tile with a counted vmcnt, so PF - 1 sub-tiles stay in flight across
-// every barrier (a plain __syncthreads() would drain them all: vmcnt(0)).
-constexpr int PF = 3;
-constexpr int NSLOT = PF + 1;
+constexpr int BM = 256, BN = 256, BK = 32;
+// K is consumed in 32-deep sub-tiles through a ring of NSLOT LDS slots; the DMA for sub-tile
+// s + NSLOT is issued while sub-tile s is multiplied, and each step retires only the sub-tile
+// the NEXT step reads with a counted vmcnt, so up to two sub-tiles stay in flight across every
+// barrier (a plain __syncthreads() would drain them all: vmcnt(0)).
+constexpr int NSLOT = 4;
 constexpr int OP_BYTES = 256 * BK * 2;                // one operand image per slot: 16 KB
 constexpr int SLOT_BYTES = 2 * OP_BYTES;              // A + B
 constexpr int LDS_BYTES = NSLOT * SLOT_BYTES;         // 128 KB
-constexpr int DMA_PER_OP = OP_BYTES / (NT * 16);      // 2 x 16-B LDS-DMA per thread per operand
-constexpr int DMA_PER_SLOT = 2 * DMA_PER_OP;
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -97,38 +94,35 @@ __device__ __forceinline__ s16x8 ld_frag(const char* img, int row0, int lane) {
   }
 }
 
-// Per-thread staging source for one operand: DMA_PER_OP x 16-B LDS-DMA per sub-tile.
-// Chunk c = i*512 + tid.  K-major: row = c >> 2 (= i*128 + tid>>2), chunk c & 3.  MN-major:
-// k-row = c >> 5 (= i*16 + tid>>5), chunk c & 31.  The swizzle term is independent of i.
+// Per-thread staging source for one operand: OP_BYTES / (NT * 16) x 16-B LDS-DMA per sub-tile.
+// Chunk c = i*NT + tid.  K-major: row = c >> 2, chunk c & 3.  MN-major: k-row = c >> 5,
+// chunk c & 31.  The source chunk is pre-swizzled so the lane-linear DMA image is the XOR image.
+template <int NT>
 struct Src {
-  const uint16_t* p[DMA_PER_OP];
+  static constexpr int N = OP_BYTES / (NT * 16);
+  const uint16_t* p[N];
   long long kstep;  // elements to advance per sub-tile
 };
 
-template <bool KMAJOR>
-__device__ __forceinline__ Src make_src(const uint16_t* base, long long ld, int rc0, int rc_lim, int k0, int tid) {
-  Src s;
-  if constexpr (KMAJOR) {
-    const int rr = tid >> 2, pch = tid & 3;
+template <bool KMAJOR, int NT>
+__device__ __forceinline__ Src<NT> make_src(const uint16_t* base, long long ld, int rc0, int rc_lim, int k0, int tid) {
+  Src<NT> s;
 #pragma unroll
-    for (int i = 0; i < DMA_PER_OP; ++i) {
-      const int row = i * 128 + rr;
-      const int lch = pch ^ (((row >> 3) & 1) << 1);
+  for (int i = 0; i < Src<NT>::N; ++i) {
+    const int c = i * NT + tid;
+    if constexpr (KMAJOR) {
+      const int row = c >> 2;
+      const int lch = (c & 3) ^ (((row >> 3) & 1) << 1);
       const int grow = min(rc0 + row, rc_lim - 1);  // clamp ragged rows (their results are never stored)
       s.p[i] = base + (long long)grow * ld + k0 + lch * 8;
-    }
-    s.kstep = BK;
-  } else {
-    const int kr = tid >> 5, pch = tid & 31;
-#pragma unroll
-    for (int i = 0; i < DMA_PER_OP; ++i) {
-      const int row = i * 16 + kr;
-      const int lch = pch ^ swz_mn(row);
+    } else {
+      const int row = c >> 5;
+      const int lch = (c & 31) ^ swz_mn(row);
       const int gcol = min(rc0 + lch * 8, rc_lim - 8);  // rc_lim % 8 == 0 (checked on the host)
       s.p[i] = base + (long long)(k0 + row) * ld + gcol;
     }
-    s.kstep = (long long)BK * ld;
   }
+  s.kstep = KMAJOR ? BK : (long long)BK * ld;
   return s;
 }
 
@@ -143,10 +137,11 @@ __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
                : "memory");
 }
 
-__device__ __forceinline__ void stage(const Src& s, char* img, int t, int wave) {
+template <int NT>
+__device__ __forceinline__ void stage(const Src<NT>& s, char* img, int t, int wave) {
   const unsigned base = (unsigned)(size_t)(lds_void*)img;
 #pragma unroll
-  for (int i = 0; i < DMA_PER_OP; ++i) {
+  for (int i = 0; i < Src<NT>::N; ++i) {
     // wave-uniform LDS destination: lanes land at base + lane*16 (lane-linear DMA)
     const unsigned dst = __builtin_amdgcn_readfirstlane(base + (i * NT + wave * 64) * 16);
     glds16(s.p[i] + t * s.kstep, dst);
@@ -156,9 +151,10 @@ __device__ __forceinline__ void stage(const Src& s, char* img, int t, int wave) 
 // retire all but the youngest n sub-tiles of LDS-DMA, then a raw barrier (no vmcnt(0) fence).
 // The DMA count is inline asm (hipcc does not see the DMA); the LDS-read drain is the builtin
 // so hipcc's own scoreboard knows every ds_read has retired and adds no lgkmcnt(0) later.
+template <int PER_SLOT>
 __device__ __forceinline__ void wait_barrier(int n_inflight) {
-  if (n_inflight >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DMA_PER_SLOT) : "memory");
-  else if (n_inflight == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_PER_SLOT) : "memory");
+  if (n_inflight >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_SLOT) : "memory");
+  else if (n_inflight == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_SLOT) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt/expcnt unconstrained
   __builtin_amdgcn_s_barrier();
@@ -180,127 +176,91 @@ __device__ __forceinline__ void tile_coords(int bid, int nwg, int tm, int tn, in
   nt = in / gm;
 }
 
+// Waves: 2 (M) x WN (N).  WN = 4: 8 waves, 128x64 per wave (2 waves per SIMD, 32 accumulator
+// tiles).  WN = 2: 4 waves, 128x128 per wave (one wave per SIMD, 64 accumulator tiles that live
+// in the AGPR half of the 512-entry register file, half the LDS bytes per MFMA).
 // EPI: 0 = bf16 out (alpha, beta*C, bias);  1 = fp32 split-K slab out (raw acc)
-template <bool AK, bool BK_, int EPI, bool REGPF>
-__global__ __launch_bounds__(NT, 1) void gemm_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
-                                                      uint16_t* __restrict__ C, float* __restrict__ ws,
-                                                      const uint16_t* __restrict__ bias, int M, int N, int K,
-                                                      long long lda, long long ldb, long long ldc, float alpha,
-                                                      float beta, int ksplit) {
+template <bool AK, bool BK_, int EPI, int WN>
+__global__ __launch_bounds__(128 * WN, 1) void gemm_kernel(const uint16_t* __restrict__ A,
+                                                           const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
+                                                           float* __restrict__ ws, const uint16_t* __restrict__ bias,
+                                                           int M, int N, int K, long long lda, long long ldb,
+                                                           long long ldc, float alpha, float beta, int ksplit) {
+  constexpr int NT = 128 * WN;
+  constexpr int FM = 8, FN = 16 / WN;  // 16x16 fragments per wave along M / N
+  constexpr int PER_SLOT = 2 * Src<NT>::N;
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
+  const int wr = wave / WN, wc = wave % WN;
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   int mt, ntile;
   tile_coords(blockIdx.x, tm * tn, tm, tn, mt, ntile);
   const int m0 = mt * BM, n0 = ntile * BN;
   const int kbeg = blockIdx.z * ksplit;
-  const int ns = ksplit / BK;
+  const int ns = ksplit / BK;  // even: K % 64 == 0
 
-  const Src sa = AK ? make_src<true>(A, lda, m0, M, kbeg, tid) : make_src<false>(A, lda, m0, M, kbeg, tid);
-  const Src sb = BK_ ? make_src<true>(B, ldb, n0, N, kbeg, tid) : make_src<false>(B, ldb, n0, N, kbeg, tid);
+  const Src<NT> sa = make_src<AK, NT>(A, lda, m0, M, kbeg, tid);
+  const Src<NT> sb = make_src<BK_, NT>(B, ldb, n0, N, kbeg, tid);
 
-  f32x4 acc[8][4];
+  f32x4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (!REGPF) {
-    // prologue: PF sub-tiles in flight, wait for the first
+  // Register double-buffered fragments: step s multiplies sub-tile s from registers while its
+  // ds_reads fetch sub-tile s+1, so no step starts on an LDS-latency bubble.  The DMA runs
+  // NSLOT sub-tiles ahead into the slot of sub-tile s (read during step s-1, before the last
+  // barrier); each step retires sub-tile s+2 (read during step s+1).
 #pragma unroll
-    for (int s = 0; s < PF; ++s) {
-      if (s < ns) {
-        stage(sa, smem + s * SLOT_BYTES, s, wave);
-        stage(sb, smem + s * SLOT_BYTES + OP_BYTES, s, wave);
-      }
+  for (int s = 0; s < NSLOT; ++s) {
+    if (s < ns) {
+      stage<NT>(sa, smem + s * SLOT_BYTES, s, wave);
+      stage<NT>(sb, smem + s * SLOT_BYTES + OP_BYTES, s, wave);
     }
-    wait_barrier(min(ns, PF) - 1);
-
-    int slot = 0;
-    for (int s = 0; s < ns; ++s) {
-      if (s + PF < ns) {
-        const int ws_ = (slot + PF) % NSLOT;  // slot of sub-tile s-1: its reads ended before the last barrier
-        stage(sa, smem + ws_ * SLOT_BYTES, s + PF, wave);
-        stage(sb, smem + ws_ * SLOT_BYTES + OP_BYTES, s + PF, wave);
+  }
+  wait_barrier<PER_SLOT>(max(min(ns, NSLOT) - 2, 0));  // sub-tiles 0 and 1 landed
+  s16x8 fa[2][FM], fb[2][FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) fb[0][j] = ld_frag<BK_>(smem + OP_BYTES, wc * (16 * FN) + j * 16, lane);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) fa[0][i] = ld_frag<AK>(smem, wr * 128 + i * 16, lane);
+  // Two sub-steps per trip, fragment sets alternate without copies.  The prefetch reads are
+  // unconditional (past the last sub-tile they read a stale slot, unused) so hipcc sees no merge
+  // point that would force lgkmcnt(0) before the MFMAs.
+  for (int s = 0; s < ns; s += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int ss = s + u;
+      const int slot = ss & (NSLOT - 1);
+      if (ss + NSLOT < ns) {
+        stage<NT>(sa, smem + slot * SLOT_BYTES, ss + NSLOT, wave);
+        stage<NT>(sb, smem + slot * SLOT_BYTES + OP_BYTES, ss + NSLOT, wave);
       }
-      const char* ia = smem + slot * SLOT_BYTES;
-      const char* ib = ia + OP_BYTES;
-      s16x8 bf[4];
+      const char* ia = smem + ((ss + 1) & (NSLOT - 1)) * SLOT_BYTES;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = ld_frag<BK_>(ib, wc * 64 + j * 16, lane);
+      for (int j = 0; j < FN; ++j) fb[u ^ 1][j] = ld_frag<BK_>(ia + OP_BYTES, wc * (16 * FN) + j * 16, lane);
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        s16x8 af[4];
+      for (int i = 0; i < FM; ++i) fa[u ^ 1][i] = ld_frag<AK>(ia, wr * 128 + i * 16, lane);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = ld_frag<AK>(ia, wr * 128 + (h * 4 + i) * 16, lane);
-        __builtin_amdgcn_s_setprio(1);
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[h * 4 + i][j] = mfma(bf[j], af[i], acc[h * 4 + i][j]);
-        __builtin_amdgcn_s_setprio(0);
-      }
-      // sub-tiles issued beyond s+1: min(ns-1, s+PF) - (s+1)
-      wait_barrier(min(ns - 1, s + PF) - (s + 1));
-      slot = slot + 1 == NSLOT ? 0 : slot + 1;
-    }
-  } else {
-    // Register double-buffered fragments: step s multiplies sub-tile s from registers while its
-    // ds_reads fetch sub-tile s+1, so no step starts on an LDS-latency bubble.  The DMA runs
-    // NSLOT sub-tiles ahead into the slot of sub-tile s (read during step s-1, before the last
-    // barrier); each step retires sub-tile s+2 (read during step s+1).
-    constexpr int P = NSLOT;
-#pragma unroll
-    for (int s = 0; s < P; ++s) {
-      if (s < ns) {
-        stage(sa, smem + s * SLOT_BYTES, s, wave);
-        stage(sb, smem + s * SLOT_BYTES + OP_BYTES, s, wave);
-      }
-    }
-    wait_barrier(max(min(ns, P) - 2, 0));  // sub-tiles 0 and 1 landed
-    s16x8 fa[2][8], fb[2][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb[0][j] = ld_frag<BK_>(smem + OP_BYTES, wc * 64 + j * 16, lane);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fa[0][i] = ld_frag<AK>(smem, wr * 128 + i * 16, lane);
-    // ns is even (K % 64 == 0): two sub-steps per trip, fragment sets alternate without copies.
-    // The prefetch reads are unconditional (past the last sub-tile they read a stale slot,
-    // unused) so hipcc sees no merge point that would force lgkmcnt(0) before the MFMAs.
-    for (int s = 0; s < ns; s += 2) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int ss = s + u;
-        const int slot = ss & (NSLOT - 1);
-        if (ss + P < ns) {
-          stage(sa, smem + slot * SLOT_BYTES, ss + P, wave);
-          stage(sb, smem + slot * SLOT_BYTES + OP_BYTES, ss + P, wave);
-        }
-        const char* ia = smem + ((ss + 1) & (NSLOT - 1)) * SLOT_BYTES;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fb[u ^ 1][j] = ld_frag<BK_>(ia + OP_BYTES, wc * 64 + j * 16, lane);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) fa[u ^ 1][i] = ld_frag<AK>(ia, wr * 128 + i * 16, lane);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fb[u][j], fa[u][i], acc[i][j]);
-        __builtin_amdgcn_s_setprio(0);
-        wait_barrier(max(min(ns - 1, ss + P) - (ss + 2), 0));
-      }
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma(fb[u][j], fa[u][i], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      wait_barrier<PER_SLOT>(max(min(ns - 1, ss + NSLOT) - (ss + 2), 0));
     }
   }
 
-  // epilogue: swapped product → lane owns C[m = m0 + wr*128 + 16i + (lane&15)][n = n0 + wc*64 + 16j + 4(lane>>4) + r]
+  // epilogue: swapped product → lane owns C[m = m0 + wr*128 + 16i + (lane&15)][n = n0 + wc*16FN + 16j + 4(lane>>4) + r]
   const int g = lane >> 4;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < FM; ++i) {
     const int m = m0 + wr * 128 + i * 16 + (lane & 15);
     if (m >= M) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wc * 64 + j * 16 + 4 * g;
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wc * (16 * FN) + j * 16 + 4 * g;
       if (n >= N) continue;  // N % 4 == 0 (host check) → a 4-wide group is all in or all out
       if constexpr (EPI == 1) {
         float* dst = ws + (long long)blockIdx.z * M * N + (long long)m * N + n;
@@ -360,14 +320,14 @@ static hipError_t launch(const void* A, const void* B, void* C, float* ws, const
                          hipStream_t st) {
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   dim3 grid(tm * tn, 1, splitk);
-  if (g_variant == 1)
-    gemm_kernel<AK, BKM, EPI, true><<<grid, NT, 0, st>>>((const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, ws,
-                                                         (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
-                                                         K / splitk);
+  if (g_variant == 2)
+    gemm_kernel<AK, BKM, EPI, 2><<<grid, 256, 0, st>>>((const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, ws,
+                                                       (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
+                                                       K / splitk);
   else
-    gemm_kernel<AK, BKM, EPI, false><<<grid, NT, 0, st>>>((const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, ws,
-                                                          (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
-                                                          K / splitk);
+    gemm_kernel<AK, BKM, EPI, 4><<<grid, 512, 0, st>>>((const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, ws,
+                                                       (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
+                                                       K / splitk);
   return hipGetLastError();
 }
 
@@ -396,8 +356,7 @@ PA_API int pa_gemm_ok(int M, int N, int K, long long lda, long long ldb, long lo
   return 1;
 }
 
-// main-loop variant (A/B benchmarking): 0 = fragments read at the top of each step,
-// 1 = register double-buffered fragments (default: +2-14 % over 0 on the GPT shapes)
+// block layout (A/B benchmarking): 1 = 8 waves of 128x64, 2 = 4 waves of 128x128
 PA_API int pa_gemm_set_variant(int v) {
   const int old = g_variant;
   g_variant = v;

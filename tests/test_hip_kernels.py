@@ -575,12 +575,22 @@ def test_momentum_flat_matches_per_parameter_path():
         _close(a, b, 1e-5, 1e-5, 'momentum fused vs reference')
 
 
+@pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K,splitk", [(256, 256, 64, 1), (512, 768, 512, 1), (328, 264, 384, 1),
                                           (1024, 512, 2048, 4), (200, 1000, 256, 2)])
-def test_hip_gemm_layouts(ta, tb, M, N, K, splitk):
-    """csrc/gemm.hip: all four operand layouts, ragged M/N edges, split-K, vs an fp32 reference."""
+def test_hip_gemm_layouts(ta, tb, M, N, K, splitk, variant):
+    """csrc/gemm.hip: both block layouts, all four operand layouts, ragged M/N edges, split-K,
+    vs an fp32 reference."""
     from paddle.ops import gemm
+    old = _native.lib.pa_gemm_set_variant(variant)
+    try:
+        _gemm_case(gemm, ta, tb, M, N, K, splitk)
+    finally:
+        _native.lib.pa_gemm_set_variant(old)
+
+
+def _gemm_case(gemm, ta, tb, M, N, K, splitk):
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
     a32 = torch.rand(M, K, device=DEV, generator=g) * 2 - 1
     b32 = torch.rand(K, N, device=DEV, generator=g) * 2 - 1
