@@ -286,6 +286,151 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_kernel(const uint16_t* __res
   }
 }
 
+// ============================================================================ FP8 (OCP)
+// C[M,N] (bf16) = alpha * A[M,K] @ B[N,K]^T (+ beta*C) (+ bias), A/B in OCP e4m3 / e5m2 with
+// per-tensor dequant scales (device scalars) folded into alpha.  Both operands k-contiguous
+// (the "TN" layout of an fp8 Linear: activations [tokens][in], weight [out][in]).
+// v_mfma_scale_f32_16x16x128_f8f6f4 with unit E8M0 block scales (127 = 2^0) runs fp8 at twice
+// the bf16 MFMA rate.  Tile 256x256 x 128 k-bytes per sub-tile, 8 waves 2(M)x4(N), two LDS
+// slots (2 x (32 KB + 32 KB)), the next sub-tile's DMA in flight during the current MFMAs.
+// Fragment: lane (g = lane>>4, i = lane&15) holds 32 k-bytes of row i — 16-byte chunks g and
+// g+4 of the 128-byte row (the same k bijection for A and B, so the sum is unchanged); the image
+// is swizzled chunk ^ ((row >> 1) & 7), conflict free for both ds_read_b128 of a fragment.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+constexpr int F8_BKB = 128;                       // k-bytes per sub-tile
+constexpr int F8_OP = 256 * F8_BKB;               // 32 KB
+constexpr int F8_SLOT = 2 * F8_OP;
+constexpr int F8_DMA = F8_OP / (512 * 16);        // 4 per operand per thread
+
+__device__ __forceinline__ int f8_off(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
+
+__device__ __forceinline__ i32x8 f8_frag(const char* img, int row0, int lane) {
+  const int r = row0 + (lane & 15), g = lane >> 4;
+  const i32x4 lo = *reinterpret_cast<const i32x4*>(img + f8_off(r, g));
+  const i32x4 hi = *reinterpret_cast<const i32x4*>(img + f8_off(r, g + 4));
+  return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int FA, int FB>
+__device__ __forceinline__ f32x4 mfma_f8(i32x8 a, i32x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, FA, FB, 0, 127, 0, 127);
+}
+
+struct F8Src {
+  const uint8_t* p[F8_DMA];
+};
+
+__device__ __forceinline__ F8Src f8_src(const uint8_t* base, long long ld, int r0, int lim, int tid) {
+  F8Src s;
+#pragma unroll
+  for (int i = 0; i < F8_DMA; ++i) {
+    const int c = i * 512 + tid;
+    const int row = c >> 3;
+    const int lch = (c & 7) ^ ((row >> 1) & 7);
+    s.p[i] = base + (long long)min(r0 + row, lim - 1) * ld + lch * 16;
+  }
+  return s;
+}
+
+__device__ __forceinline__ void f8_stage(const F8Src& s, char* img, int t, int wave) {
+  const unsigned base = (unsigned)(size_t)(lds_void*)img;
+#pragma unroll
+  for (int i = 0; i < F8_DMA; ++i) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane(base + (i * 512 + wave * 64) * 16);
+    glds16(s.p[i] + (long long)t * F8_BKB, dst);
+  }
+}
+
+template <int FA, int FB>
+__global__ __launch_bounds__(512, 1) void gemm_fp8_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                          uint16_t* __restrict__ C, const uint16_t* __restrict__ bias,
+                                                          int M, int N, int K, long long lda, long long ldb,
+                                                          long long ldc, float alpha, float beta,
+                                                          const float* __restrict__ scale_a,
+                                                          const float* __restrict__ scale_b) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * F8_SLOT];
+  // device-resident per-tensor dequant scales (no host sync to read them)
+  if (scale_a) alpha *= scale_a[0];
+  if (scale_b) alpha *= scale_b[0];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  int mt, ntile;
+  tile_coords(blockIdx.x, tm * tn, tm, tn, mt, ntile);
+  const int m0 = mt * BM, n0 = ntile * BN;
+  const int ns = K / F8_BKB;
+  const F8Src sa = f8_src(A, lda, m0, M, tid);
+  const F8Src sb = f8_src(B, ldb, n0, N, tid);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  f8_stage(sa, smem, 0, wave);
+  f8_stage(sb, smem + F8_OP, 0, wave);
+  wait_barrier<2 * F8_DMA>(0);
+  if (ns > 1) {
+    f8_stage(sa, smem + F8_SLOT, 1, wave);
+    f8_stage(sb, smem + F8_SLOT + F8_OP, 1, wave);
+  }
+  for (int s = 0; s < ns; ++s) {
+    const char* ia = smem + (s & 1) * F8_SLOT;
+    const char* ib = ia + F8_OP;
+    i32x8 bf[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = f8_frag(ib, wc * 64 + j * 16, lane);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      i32x8 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = f8_frag(ia, wr * 128 + (h * 4 + i) * 16, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[h * 4 + i][j] = mfma_f8<FB, FA>(bf[j], af[i], acc[h * 4 + i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    // sub-tile s+1 landed (nothing else in flight) and every wave is done with slot s&1 ...
+    wait_barrier<2 * F8_DMA>(0);
+    // ... so sub-tile s+2 can be staged into it
+    if (s + 2 < ns) {
+      f8_stage(sa, smem + (s & 1) * F8_SLOT, s + 2, wave);
+      f8_stage(sb, smem + (s & 1) * F8_SLOT + F8_OP, s + 2, wave);
+    }
+  }
+
+  const int g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + j * 16 + 4 * g;
+      if (n >= N) continue;
+      float v[4] = {acc[i][j][0] * alpha, acc[i][j][1] * alpha, acc[i][j][2] * alpha, acc[i][j][3] * alpha};
+      uint16_t* dst = C + (long long)m * ldc + n;
+      if (beta != 0.f) {
+        float o[4];
+        load_f<bf16_t, 4>(reinterpret_cast<const bf16_t*>(dst), o);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += beta * o[r];
+      }
+      if (bias) {
+        float bb[4];
+        load_f<bf16_t, 4>(reinterpret_cast<const bf16_t*>(bias + n), bb);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += bb[r];
+      }
+      store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(dst), v);
+    }
+  }
+}
+
 // C = alpha * sum_s ws[s] + beta * C + bias, 4 columns per thread
 __global__ void splitk_reduce(const float* __restrict__ ws, uint16_t* __restrict__ C, const uint16_t* __restrict__ bias,
                               int M, int N, long long ldc, int S, float alpha, float beta) {
@@ -377,5 +522,30 @@ PA_API int pa_gemm_bf16(const void* A, const void* B, void* C, const void* bias,
   splitk_reduce<<<(unsigned)((MN / 4 + 255) / 256), 256, 0, st>>>((const float*)ws, (uint16_t*)C,
                                                                    (const uint16_t*)bias, M, N, ldc, splitk, alpha,
                                                                    beta);
+  return (int)hipGetLastError();
+}
+
+// fp8 GEMM contract: K % 128 == 0, M % 8 == 0, N % 8 == 0, lda/ldb % 16 == 0 (bytes = elements),
+// ldc % 8 == 0.  fmt: 0 = e4m3 (OCP e4m3fn), 1 = e5m2.
+PA_API int pa_gemm_fp8_ok(int M, int N, int K, long long lda, long long ldb, long long ldc) {
+  return M > 0 && N > 0 && K > 0 && K % 128 == 0 && M % 8 == 0 && N % 8 == 0 && lda % 16 == 0 && ldb % 16 == 0 &&
+         ldc % 8 == 0;
+}
+
+PA_API int pa_gemm_fp8(const void* A, const void* B, void* C, const void* bias, const void* scale_a,
+                       const void* scale_b, int M, int N, int K, long long lda, long long ldb, long long ldc,
+                       float alpha, float beta, int fmtA, int fmtB, hipStream_t st) {
+  if (!pa_gemm_fp8_ok(M, N, K, lda, ldb, ldc) || fmtA < 0 || fmtA > 1 || fmtB < 0 || fmtB > 1)
+    return (int)hipErrorInvalidValue;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  dim3 grid(tm * tn);
+  auto args = [&](auto kern) {
+    kern<<<grid, 512, 0, st>>>((const uint8_t*)A, (const uint8_t*)B, (uint16_t*)C, (const uint16_t*)bias, M, N, K,
+                               lda, ldb, ldc, alpha, beta, (const float*)scale_a, (const float*)scale_b);
+  };
+  if (fmtA == 0 && fmtB == 0) args(gemm_fp8_kernel<0, 0>);
+  else if (fmtA == 0) args(gemm_fp8_kernel<0, 1>);
+  else if (fmtB == 0) args(gemm_fp8_kernel<1, 0>);
+  else args(gemm_fp8_kernel<1, 1>);
   return (int)hipGetLastError();
 }

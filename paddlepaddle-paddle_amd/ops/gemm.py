@@ -2,8 +2,9 @@
 
 Plain bf16/fp16 GEMMs go to hipBLASLt through the storage layer (measured 1.2–1.4 PF/s
 bf16 at LLM shapes on MI355X — the library path the design brief allows for plain GEMMs).
-FP8 (OCP e4m3fn, CDNA4 — NOT the MI300 fnuz encoding) uses per-tensor scaling through
-``torch._scaled_mm``.
+FP8 (OCP e4m3fn / e5m2, CDNA4 — NOT the MI300 fnuz encoding) runs on the hand-written
+block-scaled MFMA kernel (``hip_fp8_mm``, 2x the bf16 MFMA rate) with per-tensor scales;
+``torch._scaled_mm`` only for layouts that kernel does not take.
 
 Reference: paddle/phi/kernels/funcs/blas/blaslt_impl.cu.h, fusion/fp8_gemm.
 """
@@ -95,6 +96,38 @@ def wgrad_accumulate(x2, dy2, gw):
     return True
 
 
+_FP8_FMT = {torch.float8_e4m3fn: 0, torch.float8_e5m2: 1}
+
+
+def hip_fp8_ok(a, w):
+    """a: [M,K] fp8 row-major; w: [N,K] fp8 row-major (the weight of an fp8 Linear)."""
+    if a.dtype not in _FP8_FMT or w.dtype not in _FP8_FMT or a.dim() != 2 or w.dim() != 2:
+        return False
+    if a.stride(1) != 1 or w.stride(1) != 1 or a.shape[1] != w.shape[1] or a.data_ptr() % 16 or w.data_ptr() % 16:
+        return False
+    if N.lib is None and N._load() is None:
+        return False
+    return bool(N.lib.pa_gemm_fp8_ok(a.shape[0], w.shape[0], a.shape[1], a.stride(0), w.stride(0), w.shape[0]))
+
+
+def hip_fp8_mm(a, w, scale_a=None, scale_b=None, bias=None, out=None, alpha=1.0, beta=0.0):
+    """out[M,N] (bf16) = alpha * scale_a * scale_b * a @ w^T (+ beta*out) (+ bias) on the
+    hand-written CDNA4 fp8 kernel (v_mfma_scale_f32_16x16x128_f8f6f4, csrc/gemm.hip).
+    scale_a / scale_b: device fp32 scalars (dequant scales), read on the GPU (no host sync)."""
+    M, K = a.shape
+    N_ = w.shape[0]
+    if out is None:
+        out = torch.empty(M, N_, dtype=torch.bfloat16, device=a.device)
+        beta = 0.0
+    assert out.dtype == torch.bfloat16 and out.stride(1) == 1 and out.shape == (M, N_)
+    sa = scale_a.float().reshape(1) if scale_a is not None else None
+    sb = scale_b.float().reshape(1) if scale_b is not None else None
+    N.check(N.lib.pa_gemm_fp8(N.ptr(a), N.ptr(w), N.ptr(out), N.ptr(bias), N.ptr(sa), N.ptr(sb), M, N_, K, a.stride(0),
+                              w.stride(0), out.stride(0), float(alpha), float(beta), _FP8_FMT[a.dtype],
+                              _FP8_FMT[w.dtype], N.stream()), 'gemm_fp8')
+    return out
+
+
 def fp8_quantize(x, dtype=torch.float8_e4m3fn):
     amax = x.detach().abs().amax().float().clamp_min(1e-12)
     fmax = torch.finfo(dtype).max
@@ -120,15 +153,24 @@ def fp8_gemm(x, y, transpose_x=False, transpose_y=False, bias=None, scale=1.0, o
         b, sb = fp8_quantize(b)
     else:
         sb = torch.tensor(1.0, device=b.device)
-    try:
-        out = torch._scaled_mm(a.contiguous(), b.t().contiguous().t(), scale_a=sa.float(), scale_b=sb.float(),
-                               out_dtype=od)
-    except Exception:  # CPU / unsupported shape: exact dequantised matmul
-        out = (a.float() * sa) @ (b.float() * sb)
-        out = out.to(od)
-    out = out * scale if scale != 1.0 else out
-    if bias is not None:
-        out = out + _unwrap(bias).to(out.dtype)
+    a2 = a.reshape(-1, a.shape[-1]) if a.dim() > 2 else a
+    wt = b.t() if b.dim() == 2 else None  # [N, K]
+    if (a2.is_cuda and wt is not None and od == torch.bfloat16 and hip_fp8_ok(a2.contiguous(), wt.contiguous())):
+        bb = _unwrap(bias) if bias is not None else None
+        if bb is not None and (bb.dtype != torch.bfloat16 or not bb.is_contiguous()):
+            bb = bb.to(torch.bfloat16).contiguous()
+        out = hip_fp8_mm(a2.contiguous(), wt.contiguous(), scale_a=sa, scale_b=sb, bias=bb, alpha=scale)
+        out = out.reshape(*a.shape[:-1], out.shape[-1])
+    else:
+        try:
+            out = torch._scaled_mm(a.contiguous(), b.t().contiguous().t(), scale_a=sa.float(), scale_b=sb.float(),
+                                   out_dtype=od)
+        except Exception:  # CPU / unsupported shape: exact dequantised matmul
+            out = (a.float() * sa) @ (b.float() * sb)
+            out = out.to(od)
+        out = out * scale if scale != 1.0 else out
+        if bias is not None:
+            out = out + _unwrap(bias).to(out.dtype)
     if activation_type == 'gelu':
         out = torch.nn.functional.gelu(out)
     elif activation_type == 'relu':

@@ -388,20 +388,43 @@ class _Sequential2(Layer):
 
 
 class FP8Linear(Layer):
-    """Linear on e4m3 operands with per-tensor scales (ops/gemm.py fp8 GEMM on MI355X; a
-    dequantised-matmul emulation elsewhere)."""
+    """Linear on e4m3 operands with per-tensor scales.  On MI355X the weight is quantised once
+    per weight version into the [out, in] e4m3 image the hand-written fp8 MFMA kernel reads
+    (ops.gemm.hip_fp8_mm; scales stay on the device) and activations are quantised per call;
+    elsewhere a dequantised-matmul emulation of the same numerics."""
 
     def __init__(self, linear, act_absmax=None):
         super().__init__()
         self.weight = linear.weight
         self.bias = linear.bias
         self._act_absmax = float(_unwrap(act_absmax).max()) if act_absmax is not None else None
+        self._wq = None  # (weight version, data_ptr, e4m3 [out, in], scale)
+
+    def _quant_weight(self, w):
+        key = (w._version, w.data_ptr())
+        if self._wq is None or self._wq[0] != key:
+            from ..ops.gemm import fp8_quantize
+            q, s = fp8_quantize(w.detach().t())
+            self._wq = (key, q.contiguous(), s)
+        return self._wq[1], self._wq[2]
 
     def forward(self, x):
         from .. import ops
         t = _unwrap(x)
         w = self.weight._t
         if ops.use_hip(t):
+            t2 = t.reshape(-1, t.shape[-1])
+            if self._act_absmax is not None:
+                sx = torch.full((1,), self._act_absmax / 448.0, device=t.device)
+                xq = (t2.float() / sx).clamp(-448.0, 448.0).to(torch.float8_e4m3fn)
+            else:
+                xq, sx = ops.gemm.fp8_quantize(t2)
+            wq, sw = self._quant_weight(w)
+            if t.dtype == torch.bfloat16 and ops.gemm.hip_fp8_ok(xq, wq):
+                b = self.bias._t if self.bias is not None else None
+                out = ops.gemm.hip_fp8_mm(xq, wq, scale_a=sx, scale_b=sw,
+                                          bias=None if b is None else b.to(torch.bfloat16).contiguous())
+                return _wrap(out.reshape(*t.shape[:-1], out.shape[-1]))
             out = ops.gemm.fp8_gemm(t, w, bias=None if self.bias is None else self.bias._t,
                                     output_dtype=str(t.dtype).replace('torch.', ''))
             return _wrap(out)

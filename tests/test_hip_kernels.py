@@ -606,3 +606,34 @@ def _gemm_case(gemm, ta, tb, M, N, K, splitk):
     want = 0.5 * ref + c.float() + bias.float()
     gemm.hip_mm(a, b, out=c, bias=bias, alpha=0.5, beta=1.0, splitk=splitk)
     _close(c, want, atol=0.02 * math.sqrt(K) / 8 + 0.05, rtol=0.01, name=f"gemm acc {ta}{tb}")
+
+
+@pytest.mark.parametrize("fmt", [(torch.float8_e4m3fn, torch.float8_e4m3fn), (torch.float8_e4m3fn, torch.float8_e5m2)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 1024), (328, 264, 384), (1000, 1024, 2048)])
+def test_hip_fp8_gemm(fmt, M, N, K):
+    """csrc/gemm.hip fp8 kernel (block-scaled MFMA, unit block scales, device per-tensor scales)
+    vs an fp32 matmul of the same dequantised operands."""
+    from paddle.ops import gemm
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    a = ((torch.rand(M, K, device=DEV, generator=g) * 2 - 1) * 8).to(fmt[0])
+    w = ((torch.rand(N, K, device=DEV, generator=g) * 2 - 1) * 8).to(fmt[1])
+    sa = torch.tensor([0.05], device=DEV)
+    sb = torch.tensor([0.02], device=DEV)
+    bias = torch.rand(N, device=DEV, generator=g).bfloat16()
+    ref = (a.float() @ w.float().t()) * 0.05 * 0.02 + bias.float()
+    assert gemm.hip_fp8_ok(a, w)
+    out = gemm.hip_fp8_mm(a, w, scale_a=sa, scale_b=sb, bias=bias)
+    _close(out, ref, atol=0.02, rtol=0.01, name="fp8 gemm")
+
+
+def test_fp8_linear_uses_hip_kernel():
+    from paddle.quantization import FP8Linear
+    lin = paddle.nn.Linear(512, 256)
+    lin.weight._t.data = lin.weight._t.data.cuda().bfloat16()
+    lin.bias._t.data = lin.bias._t.data.cuda().bfloat16()
+    f = FP8Linear(lin)
+    x = paddle.to_tensor(torch.randn(64, 512, device=DEV).bfloat16())
+    out = f(x)._t.float()
+    ref = x._t.float() @ lin.weight._t.float() + lin.bias._t.float()
+    rel = (out - ref).norm() / ref.norm()
+    assert rel < 0.08, rel

@@ -32,6 +32,19 @@ def main():
     M = 16 * 1024
     dev, bf = 'cuda', torch.bfloat16
     shapes = [('qkv', 2048, 6144), ('out', 2048, 2048), ('fc1', 2048, 8192), ('fc2', 8192, 2048)]
+    if len(sys.argv) > 1 and sys.argv[1] == 'fp8':
+        e4 = torch.float8_e4m3fn
+        one = torch.ones((), device=dev)
+        for name, K, N in [('qkv', 2048, 6144), ('out', 2048, 2048), ('fc1', 2048, 8192), ('fc2', 8192, 2048),
+                           ('sq8k', 8192, 8192)]:
+            a = (torch.rand(M, K, device=dev) * 2 - 1).to(e4)
+            w = (torch.rand(N, K, device=dev) * 2 - 1).to(e4)
+            fl = 2.0 * M * K * N
+            tl = bench(lambda: torch._scaled_mm(a, w.t(), scale_a=one, scale_b=one, out_dtype=bf))
+            th = bench(lambda: gemm.hip_fp8_mm(a, w, scale_a=one, scale_b=one))
+            print(f"fp8 {name} M={M} K={K} N={N}: torch._scaled_mm {tl*1e6:8.1f} us {fl/tl/1e12:6.0f} TF | "
+                  f"hip {th*1e6:8.1f} us {fl/th/1e12:6.0f} TF", flush=True)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == 'square':
         shapes = [('sq4k', 4096, 4096), ('sq8k', 8192, 8192)]
         M = None
