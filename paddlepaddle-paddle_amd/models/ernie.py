@@ -134,7 +134,8 @@ class ErnieModel(nn.Layer):
     def forward(self, input_ids, token_type_ids=None, position_ids=None, attention_mask=None):
         if attention_mask is None:
             ids = _unwrap(input_ids)
-            if (ids == self.config.pad_token_id).any():
+            # a static Program cannot branch on data: always build the padding mask there
+            if ids.is_meta or (ids == self.config.pad_token_id).any():
                 attention_mask = _wrap(ids != self.config.pad_token_id)
         h = self.embeddings(input_ids, token_type_ids, position_ids)
         for layer in self.encoder:

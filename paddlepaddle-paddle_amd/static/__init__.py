@@ -11,6 +11,7 @@ from .io import (save_inference_model, load_inference_model, serialize_program, 
                  deserialize_program, deserialize_persistables, save, load, load_program_state,
                  set_program_state)
 from . import nn  # noqa: F401
+from . import amp  # noqa: F401
 from .nn import py_func  # noqa: F401
 from ..core.tensor import Tensor as Variable  # noqa: F401
 from ..framework.param_attr import ParamAttr, WeightNormParamAttr  # noqa: F401
@@ -156,12 +157,3 @@ class ExponentialMovingAverage:
                     p._t.copy_(self._backup.pop(id(p)))
 
 
-class amp:  # noqa: N801 - namespace mirror of paddle.static.amp
-    @staticmethod
-    def decorate(optimizer, amp_lists=None, init_loss_scaling=2 ** 15, use_dynamic_loss_scaling=True,
-                 use_pure_fp16=False, use_fp16_guard=None, use_bf16=False, **kw):
-        return optimizer
-
-    @staticmethod
-    def fp16_guard():
-        return contextlib.nullcontext()

@@ -1,0 +1,226 @@
+"""paddle.static.amp — mixed precision for static Programs (O1 / O2, float16 / bfloat16).
+
+Reference: python/paddle/static/amp/decorator.py:891 (``decorate``), :86 (``OptimizerWithMixedPrecision``:
+``minimize``/``amp_init``/``get_loss_scaling``, dynamic loss scaling with
+``check_finite_and_unscale`` + ``update_loss_scaling``), fp16_utils.py (``cast_model_to_fp16``,
+``cast_parameters_to_fp16``, ``fp16_guard``), bf16/ (``decorate_bf16``, ``AutoMixedPrecisionListsBF16``,
+``bf16_guard``).
+
+Design here: the reference rewrites the ProgramDesc, inserting ``cast`` ops around white/black-list
+ops.  Our Program is a recorded list of storage-layer ops replayed by the Executor, so the same
+effect is obtained at replay time: a Program carrying an AMP config is executed under the storage
+layer's autocast (white-list ops — matmul/linear/conv/attention — in the low-precision dtype,
+black-list ops — softmax/norms/reductions/losses — in fp32).  O2 additionally casts the
+program's parameters (normalisation parameters excepted) to the low-precision dtype, with fp32
+master weights kept by the optimizer (``multi_precision``).  Loss scaling (dynamic for float16
+by default) runs inside the recorded minimize node: scale → backward → unscale + finite check →
+skip-or-step → scale update, exactly the reference's ``update_loss_scaling`` rule.
+"""
+import contextlib
+
+import torch
+
+from ..core import dtype as _dt
+from ..amp.amp_lists import white_list as _white_list, black_list as _black_list
+
+
+class AutoMixedPrecisionLists:
+    """White / black / gray op-name lists (reference fp16_lists.py AutoMixedPrecisionLists)."""
+
+    def __init__(self, custom_white_list=None, custom_black_list=None, custom_black_varnames=None,
+                 dtype='float16'):
+        d = 'bfloat16' if 'bf' in str(dtype) else 'float16'
+        self.amp_dtype = d
+        self.white_list = set(_white_list()[d]['O1'])
+        self.black_list = set(_black_list()[d]['O1'])
+        self.gray_list = set()
+        self.black_varnames = set(custom_black_varnames or [])
+        for op in custom_white_list or []:
+            self.white_list.add(op)
+            self.black_list.discard(op)
+        for op in custom_black_list or []:
+            self.black_list.add(op)
+            self.white_list.discard(op)
+
+
+CustomOpLists = AutoMixedPrecisionLists
+
+
+def _is_norm_param(p):
+    name = (getattr(p, 'name', None) or '').lower()
+    return 'norm' in name or name.startswith('bn') or '_bn' in name
+
+
+def cast_parameters_to_fp16(place=None, program=None, scope=None, to_fp16_var_names=None, dtype=torch.float16):
+    """Casts the program's floating parameters (normalisation ones excepted) in place."""
+    from .program import default_main_program
+    program = program or default_main_program()
+    names = set(to_fp16_var_names) if to_fp16_var_names else None
+    n = 0
+    for p in program.all_parameters():
+        t = p._t
+        if not t.is_floating_point() or t.dtype == dtype or _is_norm_param(p):
+            continue
+        if names is not None and p.name not in names:
+            continue
+        req = t.requires_grad
+        with torch.no_grad():
+            p._t = t.detach().to(dtype).requires_grad_(req)
+        n += 1
+    return n
+
+
+def cast_parameters_to_bf16(place=None, program=None, scope=None, to_bf16_var_names=None):
+    return cast_parameters_to_fp16(place, program, scope, to_bf16_var_names, dtype=torch.bfloat16)
+
+
+def cast_model_to_fp16(program, amp_lists=None, use_fp16_guard=True, dest_type='float16', level='O2',
+                       use_promote=False):
+    """Marks ``program`` for low-precision replay (the reference inserts cast ops instead)."""
+    program._amp = {'level': level, 'dtype': _dt.to_torch_dtype(dest_type), 'lists': amp_lists}
+    return set()
+
+
+def cast_model_to_bf16(program, startup_prog=None, amp_lists=None, use_bf16_guard=True):
+    return cast_model_to_fp16(program, amp_lists, use_bf16_guard, 'bfloat16', 'O2')
+
+
+@contextlib.contextmanager
+def fp16_guard():
+    yield
+
+
+bf16_guard = fp16_guard
+
+
+class OptimizerWithMixedPrecision:
+    def __init__(self, optimizer, amp_lists, level, dtype, init_loss_scaling, use_dynamic_loss_scaling,
+                 incr_every_n_steps, decr_every_n_nan_or_inf, incr_ratio, decr_ratio, master_weight=None,
+                 use_promote=False):
+        self._optimizer = optimizer
+        self._amp_lists = amp_lists or AutoMixedPrecisionLists(dtype=dtype)
+        self._level = level
+        self._dtype = _dt.to_torch_dtype(dtype)
+        is_fp16 = self._dtype == torch.float16
+        if use_dynamic_loss_scaling is None:
+            use_dynamic_loss_scaling = is_fp16
+        self._use_scaling = is_fp16 or bool(use_dynamic_loss_scaling)
+        self._dynamic = bool(use_dynamic_loss_scaling)
+        self._scale = float(init_loss_scaling) if self._use_scaling else 1.0
+        self._incr_every = incr_every_n_steps
+        self._decr_every = decr_every_n_nan_or_inf
+        self._incr_ratio = incr_ratio
+        self._decr_ratio = decr_ratio
+        self._good = 0
+        self._bad = 0
+        self._master_weight = True if master_weight is None else bool(master_weight)
+        self._program = None
+        self._params = None
+        self._casted = False
+        self.found_inf = False
+
+    def __getattr__(self, name):  # get_lr, set_lr_scheduler, state_dict, ...
+        return getattr(self.__dict__['_optimizer'], name)
+
+    def get_loss_scaling(self):
+        return torch.tensor([self._scale], dtype=torch.float32)
+
+    def _cast_params(self):
+        if self._level == 'O2' and not self._casted and self._program is not None:
+            cast_parameters_to_fp16(program=self._program, dtype=self._dtype)
+            self._optimizer._multi_precision = self._master_weight
+            self._casted = True
+
+    def minimize(self, loss, startup_program=None, parameter_list=None, no_grad_set=None):
+        from .program import default_main_program, _static_minimize
+        prog = default_main_program()
+        prog._amp = {'level': self._level, 'dtype': self._dtype, 'lists': self._amp_lists}
+        self._program = prog
+        opt_ops, params_grads = _static_minimize(self._optimizer, loss, parameter_list, no_grad_set)
+        prog.nodes[-1].target = self  # executed through _static_minimize_exec (loss scaling)
+        self._params = [p for p, _ in params_grads]
+        self._cast_params()
+        return opt_ops, params_grads
+
+    def amp_init(self, place=None, scope=None, test_program=None, use_fp16_test=False):
+        """Casts the parameters for O2 (idempotent: minimize already did on this runtime)."""
+        self._cast_params()
+        if test_program is not None and use_fp16_test:
+            test_program._amp = dict(self._program._amp)
+
+    # ---- executed by the Executor for the recorded minimize node
+    def _static_minimize_exec(self, loss):
+        params = [p._t for p in (self._params or []) if p._t.requires_grad]
+        if not self._use_scaling:
+            loss.backward()
+            self._optimizer.step()
+            self._optimizer.clear_grad()
+            return
+        (loss.float() * self._scale).backward()
+        inv = 1.0 / self._scale
+        finite = torch.ones((), dtype=torch.bool, device=loss.device)
+        for t in params:
+            if t.grad is not None:
+                t.grad.mul_(inv)
+                finite &= torch.isfinite(t.grad).all()
+        ok = bool(finite.item())
+        self.found_inf = not ok
+        if ok:
+            self._optimizer.step()
+        self._optimizer.clear_grad()
+        if self._dynamic:
+            if ok:
+                self._good += 1
+                self._bad = 0
+                if self._good == self._incr_every:
+                    self._scale *= self._incr_ratio
+                    self._good = 0
+            else:
+                self._bad += 1
+                self._good = 0
+                if self._bad == self._decr_every:
+                    self._scale = max(self._scale * self._decr_ratio, 1.0)
+                    self._bad = 0
+
+
+def decorate(optimizer, amp_lists=None, level='O1', dtype='float16', master_weight=None, master_grad=False,
+             init_loss_scaling=2 ** 16, incr_every_n_steps=2000, decr_every_n_nan_or_inf=1, incr_ratio=2.0,
+             decr_ratio=0.5, use_dynamic_loss_scaling=None, use_amp_guard=False, use_promote=False,
+             use_pure_fp16=False, use_fp16_guard=None, use_bf16=False, **kw):
+    if use_pure_fp16:
+        level = 'O2'
+    if use_bf16:
+        dtype = 'bfloat16'
+    if level not in ('O1', 'O2', 'OD'):
+        raise ValueError(f"static amp level must be O1/O2/OD, got {level}")
+    return OptimizerWithMixedPrecision(optimizer, amp_lists, 'O1' if level == 'OD' else level, dtype,
+                                       init_loss_scaling, use_dynamic_loss_scaling, incr_every_n_steps,
+                                       decr_every_n_nan_or_inf, incr_ratio, decr_ratio, master_weight, use_promote)
+
+
+class _BF16Namespace:  # paddle.static.amp.bf16
+    AutoMixedPrecisionListsBF16 = staticmethod(
+        lambda custom_bf16_list=None, custom_fp32_list=None, custom_fp32_varnames=None:
+        AutoMixedPrecisionLists(custom_bf16_list, custom_fp32_list, custom_fp32_varnames, 'bfloat16'))
+    bf16_guard = staticmethod(bf16_guard)
+    cast_model_to_bf16 = staticmethod(cast_model_to_bf16)
+    cast_parameters_to_bf16 = staticmethod(cast_parameters_to_bf16)
+
+    @staticmethod
+    def decorate_bf16(optimizer, amp_lists=None, use_pure_bf16=False, use_bf16_guard=None):
+        return decorate(optimizer, amp_lists, level='O2' if use_pure_bf16 else 'O1', dtype='bfloat16')
+
+    @staticmethod
+    def rewrite_program_bf16(main_prog, amp_lists=None):
+        cast_model_to_fp16(main_prog, amp_lists, dest_type='bfloat16', level='O1')
+
+
+bf16 = _BF16Namespace()
+
+
+def autocast_context(program, dev):
+    """Replay context for a Program carrying an AMP config (used by the Executor)."""
+    cfg = getattr(program, '_amp', None)
+    if not cfg:
+        return contextlib.nullcontext()
+    return torch.autocast(device_type='cuda' if dev.type == 'cuda' else 'cpu', dtype=cfg['dtype'])

@@ -108,7 +108,9 @@ def _resolve(prog, obj, env, smap, dev):
     if isinstance(obj, Ref):
         return env[obj.vid]
     if isinstance(obj, Const):
-        return prog.consts[obj.cid]
+        owner = prog._const_owner.get(obj.cid) if hasattr(prog, '_const_owner') else None
+        # a parameter resolves to its live storage (static.amp O2 / set_state_dict may replace it)
+        return owner._t if owner is not None else prog.consts[obj.cid]
     if isinstance(obj, bool) or obj is None:
         return obj
     if isinstance(obj, int):
@@ -162,9 +164,12 @@ def _exec(prog, nodes, env, smap, dev):
             _bind(env, n.outs, n.target(*args, **kwargs))
         elif n.kind == 'minimize':
             loss = env[n.args[0].vid]
-            loss.backward()
-            n.target.step()
-            n.target.clear_grad()
+            if hasattr(n.target, '_static_minimize_exec'):  # static.amp: loss scaling / skip-on-inf
+                n.target._static_minimize_exec(loss)
+            else:
+                loss.backward()
+                n.target.step()
+                n.target.clear_grad()
         elif n.kind == 'backward':
             loss = env[n.args[0].vid]
             loss.backward()
@@ -228,7 +233,8 @@ def run_program(prog, feed, dev, grad=None):
         env[vid] = t
     needs_grad = grad if grad is not None else any(n.kind in ('minimize', 'backward', 'grad') for n in prog.nodes)
     ctx = contextlib.nullcontext() if needs_grad else torch.no_grad()
-    with _paused(), ctx:
+    from .amp import autocast_context
+    with _paused(), ctx, autocast_context(prog, dev):
         _exec(prog, prog.nodes, env, smap, dev)
     return env
 

@@ -180,3 +180,78 @@ def test_gpu_predictor_hip_graph_and_to_static_graph(tmp_path):
         for _ in range(4):
             y = g(paddle.to_tensor(a))
     np.testing.assert_allclose(y.numpy(), ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("level,dtype", [("O1", "bfloat16"), ("O2", "bfloat16"), ("O2", "float16")])
+def test_ernie_static_executor_amp(static_mode, level, dtype):
+    """BASELINE config 5 on CPU: ERNIE (tiny) built as a static Program, trained by the Executor
+    under static.amp (reference: static/amp/decorator.py decorate + amp_init): O2 casts the
+    weights (norms kept fp32) with fp32 master weights; float16 uses dynamic loss scaling."""
+    import torch
+    from paddle.models import ernie_config, ErnieForSequenceClassification
+    paddle.seed(3)
+    cfg = ernie_config('ernie-tiny', hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    S, B = 16, 8
+    main, startup = static.Program(), static.Program()
+    with static.program_guard(main, startup):
+        ids = static.data('ids', [None, S], 'int64')
+        lab = static.data('lab', [None], 'int64')
+        model = ErnieForSequenceClassification(cfg, num_classes=2)
+        logits = model(ids)
+        loss = paddle.nn.functional.cross_entropy(logits, lab)
+        opt = paddle.optimizer.AdamW(learning_rate=2e-3, parameters=model.parameters())
+        opt = static.amp.decorate(opt, level=level, dtype=dtype, init_loss_scaling=1024.0)
+        opt.minimize(loss)
+    exe = static.Executor(paddle.CPUPlace())
+    exe.run(startup)
+    opt.amp_init(paddle.CPUPlace())
+    low = {'bfloat16': torch.bfloat16, 'float16': torch.float16}[dtype]
+    dts = {p.name: p._t.dtype for p in main.all_parameters()}
+    if level == 'O2':
+        assert any(d == low for d in dts.values())
+        assert all(d == torch.float32 for n, d in dts.items() if 'norm' in (n or '').lower())
+    else:
+        assert all(d == torch.float32 for d in dts.values())
+    rng = np.random.RandomState(0)
+    x = rng.randint(1, cfg.vocab_size, size=(B, S)).astype('int64')
+    y = (x[:, 0] % 2).astype('int64')
+    losses = []
+    for _ in range(25):
+        lv, = exe.run(main, feed={'ids': x, 'lab': y}, fetch_list=[loss])
+        losses.append(float(lv))
+    assert np.isfinite(losses).all(), losses
+    assert losses[-1] < losses[0] * 0.6, losses
+    if dtype == 'float16':
+        assert float(opt.get_loss_scaling()[0]) > 0
+
+
+@pytest.mark.gpu
+def test_ernie_static_executor_amp_o2_gpu(static_mode):
+    """BASELINE config 5 on the MI355X: ERNIE static Program + Executor, AMP-O2 bf16."""
+    import torch
+    from paddle.models import ernie_config, ErnieForSequenceClassification
+    paddle.set_device('gpu')
+    try:
+        paddle.seed(3)
+        cfg = ernie_config('ernie-tiny', hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+        S, B = 64, 16
+        main, startup = static.Program(), static.Program()
+        with static.program_guard(main, startup):
+            ids = static.data('ids', [None, S], 'int64')
+            lab = static.data('lab', [None], 'int64')
+            model = ErnieForSequenceClassification(cfg, num_classes=2)
+            loss = paddle.nn.functional.cross_entropy(model(ids), lab)
+            opt = paddle.optimizer.AdamW(learning_rate=2e-3, parameters=model.parameters())
+            opt = static.amp.decorate(opt, level='O2', dtype='bfloat16')
+            opt.minimize(loss)
+        exe = static.Executor(paddle.CUDAPlace(0))
+        exe.run(startup)
+        opt.amp_init(paddle.CUDAPlace(0))
+        assert any(p._t.dtype == torch.bfloat16 and p._t.is_cuda for p in main.all_parameters())
+        rng = np.random.RandomState(0)
+        x = rng.randint(1, cfg.vocab_size, size=(B, S)).astype('int64')
+        y = (x[:, 0] % 2).astype('int64')
+        losses = [float(exe.run(main, feed={'ids': x, 'lab': y}, fetch_list=[loss])[0]) for _ in range(25)]
+        assert np.isfinite(losses).all() and losses[-1] < losses[0] * 0.6, losses
+    finally:
+        paddle.set_device('cpu')
