@@ -96,8 +96,11 @@ class ErnieSelfAttention(nn.Layer):
                 m = am.bool() if am.dtype == torch.bool else am.to(q.dtype)
                 if m.dim() == 2:  # [B, S] 1 = keep
                     m = m.view(B, 1, 1, S).bool() if m.dtype != torch.bool else m.view(B, 1, 1, S)
-            o = TF.scaled_dot_product_attention(q, k, v, attn_mask=m,
-                                                dropout_p=self.p if self.training else 0.0).transpose(1, 2)
+            if m is not None and (q.is_cuda or q.is_meta):
+                o = F.masked_attention_bhsd(q, k, v, m, self.p if self.training else 0.0).transpose(1, 2)
+            else:
+                o = TF.scaled_dot_product_attention(q, k, v, attn_mask=m,
+                                                    dropout_p=self.p if self.training else 0.0).transpose(1, 2)
         return self.out(_wrap(o.reshape(B, S, -1)))
 
 

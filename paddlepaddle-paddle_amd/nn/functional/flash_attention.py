@@ -14,6 +14,26 @@ from ...core.tensor import Tensor, _wrap as _w, _unwrap as _u
 from ... import ops
 
 
+def masked_attention_bhsd(q, k, v, mask, dropout_p=0.0, scale=None):
+    """Explicit masked attention on [B, H, S, D] (scores -> masked fp32 softmax -> PV).
+
+    Used for masked attention on the GPU instead of the storage layer's fused SDPA backends
+    (their broadcast-mask kernels are not relied on here); every step is a plain op, so it also
+    records cleanly into static Programs.  Bool masks: True = keep; float masks are additive.
+    """
+    sc = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    s = torch.matmul(q, k.transpose(-1, -2)).float() * sc
+    if mask is not None:
+        if mask.dtype == torch.bool:
+            s = s.masked_fill(~mask, -1e30)
+        else:
+            s = s + mask.float()
+    p = torch.softmax(s, -1)
+    if dropout_p > 0.0:
+        p = TF.dropout(p, dropout_p)
+    return torch.matmul(p.to(v.dtype), v)
+
+
 def _sdpa_reference(q, k, v, mask, dropout_p, causal, scale=None):
     # BSHD → BHSD for the math path
     qh, kh, vh = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
@@ -21,8 +41,12 @@ def _sdpa_reference(q, k, v, mask, dropout_p, causal, scale=None):
         rep = qh.shape[1] // kh.shape[1]
         kh = kh.repeat_interleave(rep, 1)
         vh = vh.repeat_interleave(rep, 1)
-    if mask is not None and mask.dtype == torch.bool:
-        pass
+    if mask is not None and (qh.is_cuda or qh.is_meta):
+        if causal:
+            S, Sk = qh.shape[-2], kh.shape[-2]
+            cm = torch.ones(S, Sk, dtype=torch.bool, device=qh.device).tril(Sk - S)
+            mask = (mask & cm) if mask.dtype == torch.bool else mask.masked_fill(~cm, float('-inf'))
+        return masked_attention_bhsd(qh, kh, vh, mask, dropout_p, scale).transpose(1, 2)
     out = TF.scaled_dot_product_attention(qh, kh, vh, attn_mask=mask, dropout_p=dropout_p,
                                           is_causal=causal and mask is None, scale=scale)
     return out.transpose(1, 2)

@@ -94,7 +94,13 @@ def stream():
 
 
 def ptr(t):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    """Device pointer of a GPU tensor for a kernel argument.  Anything else (a CPU tensor, or a
+    meta tensor recorded into a static Program) raises here instead of reaching a kernel."""
+    if t is None:
+        return None
+    if t.device.type != 'cuda':
+        raise RuntimeError(f"HIP kernel operand on {t.device} (expected a GPU tensor)")
+    return ctypes.c_void_p(t.data_ptr())
 
 
 def dtcode(dt):
