@@ -367,6 +367,10 @@ __global__ __launch_bounds__(256, 3 - NT) void bwd_dkdv_kernel(
     Strides vs, Strides dos, Strides dks, Strides dvs, float scale) {
   constexpr int KS = D / 32;
   constexpr int DB = D / 16;
+  // D = 128: tiles read both by rows (ds_read_b128) and by columns (tr_b16) use the chunk ^
+  // ((row & 7) << 1) image, conflict free for both (the row-only swizzle leaves the tr reads
+  // 2-way: SQ_LDS_BANK_CONFLICT was 20-27 % of LDS cycles in these kernels)
+  constexpr bool BT = (D == 128);
   __shared__ __attribute__((aligned(16))) char smem[2 * 64 * D * 2 + 2 * 64 * 4];
   char* q_lds = smem;
   char* do_lds = smem + 64 * D * 2;
@@ -425,8 +429,8 @@ __global__ __launch_bounds__(256, 3 - NT) void bwd_dkdv_kernel(
   for (int i = 0; i < nqb; ++i) {
     const int q0 = qstart + i * 64;
     __syncthreads();
-    qt.template store<false>(q_lds);
-    dot.template store<false>(do_lds);
+    qt.template store<BT>(q_lds);
+    dot.template store<BT>(do_lds);
     if (threadIdx.x < 64) {
       const int q = q0 + threadIdx.x;
       lse_lds[threadIdx.x] = q < Sq ? lse_b[q] * kLog2e : INFINITY;
@@ -452,8 +456,8 @@ __global__ __launch_bounds__(256, 3 - NT) void bwd_dkdv_kernel(
     for (int k = 0; k < KS; ++k) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        const s16x8 qa = ld_row8<D, false>(q_lds, 16 * m + (lane & 15), k, g);
-        const s16x8 da = ld_row8<D, false>(do_lds, 16 * m + (lane & 15), k, g);
+        const s16x8 qa = ld_row8<D, BT>(q_lds, 16 * m + (lane & 15), k, g);
+        const s16x8 da = ld_row8<D, BT>(do_lds, 16 * m + (lane & 15), k, g);
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
           acc_s[j][m] = Mfma<T>::run(qa, kf[j][k], acc_s[j][m]);
@@ -492,8 +496,8 @@ __global__ __launch_bounds__(256, 3 - NT) void bwd_dkdv_kernel(
     for (int d = 0; d < DB; ++d) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const s16x8 doa = ld_tr8<D, false>(do_lds, 32 * s, d, lane);
-        const s16x8 qa = ld_tr8<D, false>(q_lds, 32 * s, d, lane);
+        const s16x8 doa = ld_tr8<D, BT>(do_lds, 32 * s, d, lane);
+        const s16x8 qa = ld_tr8<D, BT>(q_lds, 32 * s, d, lane);
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
           acc_dv[j][d] = Mfma<T>::run(doa, pb[j][s], acc_dv[j][d]);
@@ -534,6 +538,10 @@ __global__ __launch_bounds__(256, 3 - NT) void bwd_dq_kernel(
     Strides dqs, float scale) {
   constexpr int KS = D / 32;
   constexpr int DB = D / 16;
+  // D = 128: tiles read both by rows (ds_read_b128) and by columns (tr_b16) use the chunk ^
+  // ((row & 7) << 1) image, conflict free for both (the row-only swizzle leaves the tr reads
+  // 2-way: SQ_LDS_BANK_CONFLICT was 20-27 % of LDS cycles in these kernels)
+  constexpr bool BT = (D == 128);
   __shared__ __attribute__((aligned(16))) char smem[2 * 64 * D * 2];
   char* k_lds = smem;
   char* v_lds = smem + 64 * D * 2;
@@ -590,8 +598,8 @@ __global__ __launch_bounds__(256, 3 - NT) void bwd_dq_kernel(
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * 64;
     __syncthreads();
-    kt.template store<false>(k_lds);
-    vt.template store<false>(v_lds);
+    kt.template store<BT>(k_lds);
+    vt.template store<BT>(v_lds);
     __syncthreads();
     if (kb + 1 < nkb) {
       kt.load(k0 + 64, Sk);
@@ -610,8 +618,8 @@ __global__ __launch_bounds__(256, 3 - NT) void bwd_dq_kernel(
     for (int k = 0; k < KS; ++k) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const s16x8 ka = ld_row8<D, false>(k_lds, 16 * j + (lane & 15), k, g);
-        const s16x8 va = ld_row8<D, false>(v_lds, 16 * j + (lane & 15), k, g);
+        const s16x8 ka = ld_row8<D, BT>(k_lds, 16 * j + (lane & 15), k, g);
+        const s16x8 va = ld_row8<D, BT>(v_lds, 16 * j + (lane & 15), k, g);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           acc_s[t][j] = Mfma<T>::run(ka, qf[t][k], acc_s[t][j]);
@@ -643,7 +651,7 @@ __global__ __launch_bounds__(256, 3 - NT) void bwd_dq_kernel(
     for (int d = 0; d < DB; ++d) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const s16x8 ka = ld_tr8<D, false>(k_lds, 32 * s, d, lane);
+        const s16x8 ka = ld_tr8<D, BT>(k_lds, 32 * s, d, lane);
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[t][d] = Mfma<T>::run(ka, dsb[t][s], acc[t][d]);
       }
