@@ -64,11 +64,11 @@ __device__ __forceinline__ int lds_off(int row, int ch) {
 // Stage helpers: a [64][D] tile of 16-bit elements, 256 threads, NLD 16-byte chunks per thread.
 // The per-thread address is computed once (init); a tile load adds one wave-uniform offset and,
 // for full tiles, skips the per-row bounds checks entirely.
-template <int D>
+template <int D, int NTHR = 256>
 struct Tile {
   static constexpr int CH = D / 8;               // 16-byte chunks per row
-  static constexpr int NLD = 64 * CH / 256;      // chunks per thread
-  static constexpr int RPL = 256 / CH;           // rows covered by one pass of the block
+  static constexpr int NLD = 64 * CH / NTHR;     // chunks per thread
+  static constexpr int RPL = NTHR / CH;          // rows covered by one pass of the block
   uint4 r[NLD];
   const uint16_t* p;
   long long rs;
@@ -94,7 +94,7 @@ struct Tile {
   __device__ __forceinline__ void store(char* lds) const {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
-      const int c = threadIdx.x + 256 * i;
+      const int c = threadIdx.x + NTHR * i;
       const int row = c / CH, ch = c % CH;
       *reinterpret_cast<uint4*>(lds + lds_off<D, TR>(row, ch)) = r[i];
     }
@@ -355,12 +355,14 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const uint16_t* __restri
   if (sub == 0) delta[rid] = s;
 }
 
-// dK/dV: grid (ceil(Sk / (64*NT)), Hq, B); 4 waves x (16*NT) keys; loop over 64-query blocks.
+// dK/dV: grid (ceil(Sk / (16*NT*NW)), Hq, B); NW waves x (16*NT) keys; loop over 64-query blocks.
+// NW = 8 doubles the keys that share each staged Q/dO tile (halving the Q/dO re-reads from
+// L2/HBM, which bound the 4-wave form) at the same 2 waves/SIMD.
 // NT = 2 halves the LDS bytes per MFMA (every Q / dO fragment read from LDS feeds two key tiles)
 // at one wave per SIMD (the accumulators of 32 keys x D need the full register file).
 // dK/dV are written per q-head ([B, Sk, Hq, D] strides given by dks/dvs); GQA sums outside.
-template <typename T, int D, bool CAUSAL, int NT>
-__global__ __launch_bounds__(256, 3 - NT) void bwd_dkdv_kernel(
+template <typename T, int D, bool CAUSAL, int NT, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq, int Sk, int Hq, int Hk, Strides qs, Strides ks_,
@@ -382,7 +384,7 @@ __global__ __launch_bounds__(256, 3 - NT) void bwd_dkdv_kernel(
   const int g = lane >> 4;
   const int h = blockIdx.y, b = blockIdx.z;
   const int hk = h / (Hq / Hk);
-  const int k0 = blockIdx.x * 64 * NT;
+  const int k0 = blockIdx.x * 16 * NT * NW;
   const int kw = k0 + wave * 16 * NT;
   const int off = Sk - Sq;
   const float scale_log2 = scale * kLog2e;
@@ -419,7 +421,7 @@ __global__ __launch_bounds__(256, 3 - NT) void bwd_dkdv_kernel(
   const float* lse_b = LSE + ((long long)b * Hq + h) * Sq;
   const float* dl_b = Delta + ((long long)b * Hq + h) * Sq;
 
-  Tile<D> qt, dot;
+  Tile<D, 64 * NW> qt, dot;
   qt.init(qbase, qs.s);
   dot.init(dobase, dos.s);
   if (nqb > 0) {
@@ -528,10 +530,10 @@ __global__ __launch_bounds__(256, 3 - NT) void bwd_dkdv_kernel(
   }
 }
 
-// dQ: grid (ceil(Sq / (64*NT)), Hq, B); 4 waves x (16*NT) queries; loop over 64-key blocks
+// dQ: grid (ceil(Sq / (16*NT*NW)), Hq, B); NW waves x (16*NT) queries; loop over 64-key blocks
 // (swapped products: lane owns a query).  NT = 2: every K / V fragment read feeds two query tiles.
-template <typename T, int D, bool CAUSAL, int NT>
-__global__ __launch_bounds__(256, 3 - NT) void bwd_dq_kernel(
+template <typename T, int D, bool CAUSAL, int NT, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     uint16_t* __restrict__ dQ, int Sq, int Sk, int Hq, int Hk, Strides qs, Strides ks_, Strides vs, Strides dos,
@@ -548,11 +550,11 @@ __global__ __launch_bounds__(256, 3 - NT) void bwd_dq_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane >> 4;
-  const int nqb = (Sq + 64 * NT - 1) / (64 * NT);
+  const int nqb = (Sq + 16 * NT * NW - 1) / (16 * NT * NW);
   const int qb = nqb - 1 - (int)blockIdx.x;
   const int h = blockIdx.y, b = blockIdx.z;
   const int hk = h / (Hq / Hk);
-  const int q0 = qb * 64 * NT;
+  const int q0 = qb * 16 * NT * NW;
   const int qw = q0 + wave * 16 * NT;
   const int off = Sk - Sq;
   const float scale_log2 = scale * kLog2e;
@@ -586,9 +588,9 @@ __global__ __launch_bounds__(256, 3 - NT) void bwd_dq_kernel(
   const uint16_t* kbase = K + b * ks_.b + hk * ks_.h;
   const uint16_t* vbase = V + b * vs.b + hk * vs.h;
   int kend = Sk;
-  if (CAUSAL) kend = min(Sk, q0 + 64 * NT + off);
+  if (CAUSAL) kend = min(Sk, q0 + 16 * NT * NW + off);
   const int nkb = kend > 0 ? (kend + 63) / 64 : 0;
-  Tile<D> kt, vt;
+  Tile<D, 64 * NW> kt, vt;
   kt.init(kbase, ks_.s);
   vt.init(vbase, vs.s);
   if (nkb > 0) {
@@ -704,15 +706,23 @@ PA_API hipError_t pa_flash_fwd(const void* q, const void* k, const void* v, void
   return hipGetLastError();
 }
 
-// backward tiling: 1 = 16 rows per wave (2 waves/SIMD), 2 = 32 rows per wave (1 wave/SIMD);
+// backward tiling: 1 = 16 rows per wave (2 waves/SIMD), 2 = 32 rows per wave (1 wave/SIMD),
+// 3 = 16 rows per wave in 8-wave blocks (128 rows share each staged tile);
 // PA_FA_BWD_VARIANT selects (A/B), default 1 (measured on MI355X, B16 S1024 H16 D128 causal:
 // fwd+bwd 1.04 ms with 1 vs 1.30 ms with 2 — the 32-row tiles lose occupancy to VGPR pressure).
+static int g_bwd_variant = -1;
 static int bwd_variant() {
-  static int v = [] {
+  if (g_bwd_variant < 0) {
     const char* e = getenv("PA_FA_BWD_VARIANT");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
+    g_bwd_variant = e ? atoi(e) : 1;
+  }
+  return g_bwd_variant;
+}
+
+PA_API int pa_flash_set_bwd_variant(int v) {
+  const int old = bwd_variant();
+  g_bwd_variant = v;
+  return old;
 }
 
 
@@ -731,7 +741,17 @@ PA_API hipError_t pa_flash_bwd(const void* q, const void* k, const void* v, cons
   FA_DISPATCH(dt, D, causal, {
     bwd_delta_kernel<T, DD><<<(int)((nrows + 15) / 16), 256, 0, st>>>((const uint16_t*)dout, (const uint16_t*)o, delta,
                                                                       B, Sq, Hq, dos, os);
-    if (bwd_variant() == 2) {
+    if (bwd_variant() == 3) {
+      dim3 g1((Sk + 127) / 128, Hq, B);
+      bwd_dkdv_kernel<T, DD, CC, 1, 8><<<g1, 512, 0, st>>>((const uint16_t*)q, (const uint16_t*)k,
+                                                           (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                                                           (uint16_t*)dk, (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs,
+                                                           dos, dks, dvs, scale);
+      dim3 g2((Sq + 127) / 128, Hq, B);
+      bwd_dq_kernel<T, DD, CC, 1, 8><<<g2, 512, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                                                         (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk,
+                                                         Hq, Hk, qs, ks, vs, dos, dqs, scale);
+    } else if (bwd_variant() == 2) {
       dim3 g1((Sk + 127) / 128, Hq, B);
       bwd_dkdv_kernel<T, DD, CC, 2><<<g1, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                                                         (const uint16_t*)dout, lse, delta, (uint16_t*)dk,

@@ -53,6 +53,7 @@ _SIGS = {
     'pa_momentum': [P, P, P, P, LL, P, F, F, F, F, I, P, I, I, P],
     'pa_sumsq_parts': [],
     'pa_gemm_set_variant': [I],
+    'pa_flash_set_bwd_variant': [I],
     'pa_gemm_fp8_ok': [I, I, I, LL, LL, LL],
     'pa_gemm_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
     'pa_gemm_ok': [I, I, I, LL, LL, LL, I],

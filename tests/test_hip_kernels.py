@@ -237,10 +237,19 @@ def _attn_ref(q, k, v, causal):
     return (torch.softmax(s, -1) @ vf).transpose(1, 2)
 
 
+@pytest.mark.parametrize("variant", [1, 3])
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("S", [128, 200, 1024])
-def test_flash_attention_fwd_bwd(D, causal, S):
+def test_flash_attention_fwd_bwd(D, causal, S, variant):
+    old = _native.lib.pa_flash_set_bwd_variant(variant)
+    try:
+        _flash_case(D, causal, S)
+    finally:
+        _native.lib.pa_flash_set_bwd_variant(old)
+
+
+def _flash_case(D, causal, S):
     B, H = 2, 4
     q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     k = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)

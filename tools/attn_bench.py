@@ -46,6 +46,13 @@ def timeit(fn, n=10):
 
 
 def main():
+    for var in [int(x) for x in os.environ.get('FA_VARIANTS', '1').split(',')]:
+        _native.lib.pa_flash_set_bwd_variant(var)
+        print(f"-- backward variant {var}", flush=True)
+        run()
+
+
+def run():
     for (B, S, H, D, causal) in [(16, 1024, 16, 128, True), (4, 4096, 16, 128, True), (16, 1024, 16, 128, False),
                                  (8, 2048, 32, 64, True)]:
         qkv = torch.randn(B, S, 3, H, D, device='cuda', dtype=torch.bfloat16, requires_grad=True)
