@@ -12,6 +12,14 @@ Elastic restart (reference launch ``--max_restart`` / fleet elastic fault tolera
 ``--max_restart N`` a failed job is torn down and relaunched (fresh rendezvous port) up to N
 times; workers see ``PADDLE_ELASTIC_RESTART_COUNT`` and resume from their checkpoints.
 
+Elastic scale in / out (reference fleet/elastic/manager.py, launch ``--elastic_server``/``--np``):
+with ``--elastic_server host:port --np MIN:MAX`` each launcher is one node of an elastic job
+(distributed/elastic.py, a TCPStore registry with heartbeats): it waits until MIN..MAX nodes
+are alive, launches its workers with that generation's ranks/world, and when nodes join or
+disappear tears its workers down and re-rendezvouses with the new world
+(``PADDLE_ELASTIC_GEN`` / ``PADDLE_ELASTIC_RESTART_COUNT`` tell workers to resume from their
+checkpoints).  A worker failure is retried up to ``--max_restart`` times.
+
 Parameter-server mode (``--run_mode ps`` with ``--server_num``/``--trainer_num``, reference
 controllers/ps.py): servers and trainers get TRAINING_ROLE, PADDLE_PSERVERS_IP_PORT_LIST,
 PADDLE_PSERVER_ID / PADDLE_TRAINER_ID, PADDLE_TRAINERS_NUM (see distributed/ps).
@@ -44,6 +52,11 @@ def parse_args(argv=None):
     ap.add_argument('--max_restart', type=int, default=0)
     ap.add_argument('--server_num', type=int, default=None)
     ap.add_argument('--trainer_num', type=int, default=None)
+    ap.add_argument('--elastic_server', default=None, help='host:port of the elastic TCPStore')
+    ap.add_argument('--np', default=None, help='elastic node count: N or MIN:MAX')
+    ap.add_argument('--host', default=None, help='this node\'s name in the elastic registry')
+    ap.add_argument('--elastic_ttl', type=float, default=6.0)
+    ap.add_argument('--elastic_timeout', type=float, default=600.0)
     ap.add_argument('training_script')
     ap.add_argument('training_script_args', nargs=argparse.REMAINDER)
     return ap.parse_args(argv)
@@ -77,7 +90,7 @@ def _spawn(cmd, env, log_path, to_console):
     return p, log
 
 
-def _collective(a, attempt):
+def _collective(a, attempt, restart_count=None):
     devices = a.devices.split(',') if a.devices else None
     nproc = a.nproc_per_node or (len(devices) if devices else 1)
     devices = devices or [str(i) for i in range(nproc)]
@@ -98,10 +111,79 @@ def _collective(a, attempt):
                     'PADDLE_TRAINERS_NUM': str(world), 'PADDLE_TRAINER_ENDPOINTS': endpoints,
                     'PADDLE_CURRENT_ENDPOINT': f"{host}:{int(port) + rank}", 'FLAGS_selected_gpus': devices[i],
                     'PADDLE_JOB_ID': a.job_id, 'PADDLE_LOCAL_DEVICE_IDS': devices[i],
-                    'PADDLE_ELASTIC_RESTART_COUNT': str(attempt)})
+                    'PADDLE_ELASTIC_RESTART_COUNT': str(attempt if restart_count is None else restart_count)})
         cmd = [sys.executable, '-u', a.training_script] + a.training_script_args
         procs.append(_spawn(cmd, env, os.path.join(a.log_dir, f"workerlog.{i}"), i == 0))
     return procs
+
+
+def _kill(procs):
+    for p, _ in procs:
+        try:
+            os.killpg(p.pid, signal.SIGTERM)
+        except ProcessLookupError:
+            pass
+    for p, _ in procs:
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+
+
+def _elastic(a):
+    """One node of an elastic collective job (see module docstring)."""
+    from .elastic import ElasticManager, connect_store
+    node = a.host or f"{socket.gethostname()}-{os.getpid()}"
+    store = connect_store(a.elastic_server)
+    mgr = ElasticManager(store, a.job_id, node, a.np or a.nnodes, ttl=a.elastic_ttl)
+    mgr.register()
+    restarts = 0
+    try:
+        while True:
+            if mgr.completed():
+                return 0
+            gen, members = mgr.wait_for_np(timeout=a.elastic_timeout)
+            nrank, nnodes = mgr.rank(), len(members)
+            if nrank == 0:
+                mgr.publish_master(f"127.0.0.1:{_free_port()}")
+            master = mgr.wait_master()
+            print(f"[launch] elastic generation {gen}: node {node} rank {nrank}/{nnodes} master {master}",
+                  file=sys.stderr, flush=True)
+            a2 = argparse.Namespace(**vars(a))
+            a2.master, a2.rank, a2.nnodes = master, nrank, str(nnodes)
+            os.environ['PADDLE_ELASTIC_GEN'] = str(gen)
+            procs = _collective(a2, 0, restart_count=restarts)
+            try:
+                while True:
+                    codes = [p.poll() for p, _ in procs]
+                    if all(c == 0 for c in codes):
+                        mgr.exit(completed=True)
+                        return 0
+                    if any(c not in (None, 0) for c in codes):
+                        rc = next(c for c in codes if c not in (None, 0))
+                        if mgr.completed():
+                            return rc
+                        if restarts >= a.max_restart and not mgr.changed():
+                            mgr.exit()
+                            return rc
+                        break  # fault tolerance: re-rendezvous (peers see the same failure)
+                    if not mgr.completed() and mgr.changed():
+                        print(f"[launch] elastic membership changed (generation {gen}); relaunching",
+                              file=sys.stderr, flush=True)
+                        break
+                    time.sleep(0.25)
+            finally:
+                _kill(procs)
+                for _, log in procs:
+                    log.close()
+            restarts += 1
+    except KeyboardInterrupt:
+        return 130
+    finally:
+        mgr._stop.set()
 
 
 def _ps(a, attempt):
@@ -126,6 +208,10 @@ def launch(argv=None):
     if a.run_mode not in ('collective', 'ps'):
         raise SystemExit(f"unsupported run_mode {a.run_mode!r} (collective | ps)")
     os.makedirs(a.log_dir, exist_ok=True)
+    if a.elastic_server:
+        if a.run_mode != 'collective':
+            raise SystemExit("elastic scaling is supported for collective jobs")
+        return _elastic(a)
     rc = 0
     for attempt in range(a.max_restart + 1):
         procs = (_ps if a.run_mode == 'ps' else _collective)(a, attempt)

@@ -143,3 +143,71 @@ def test_launch_elastic_restart_and_ps_mode(tmp_path):
 def test_llama_hybrid_tp2_pp2_matches_single_device():
     out = run_workers('worker_llama_hybrid.py', nproc=4, timeout=300)
     assert out.count('llama hybrid OK') == 4, out[-4000:]
+
+
+def test_elastic_scale_out_and_in(tmp_path):
+    """Elastic collective job (reference fleet/elastic ElasticManager, np=MIN:MAX): 2 nodes start a
+    world of 2; a third node joining re-launches everyone with world 3 (scale out); killing it
+    re-launches the survivors with world 2 (scale in); workers see the restart count."""
+    import json
+    import signal
+    import time
+    import datetime
+    from torch.distributed import TCPStore
+    port = _port()
+    store = TCPStore('127.0.0.1', port, is_master=True, wait_for_workers=False,
+                     timeout=datetime.timedelta(seconds=30))
+    out = tmp_path / 'out'
+    out.mkdir()
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES='', HIP_VISIBLE_DEVICES='', OMP_NUM_THREADS='1')
+
+    def node(name):
+        cmd = [sys.executable, '-m', 'paddle.distributed.launch', '--elastic_server', f'127.0.0.1:{port}',
+               '--np', '2:3', '--job_id', 'ej', '--host', name, '--elastic_ttl', '3', '--log_dir',
+               str(tmp_path / name), os.path.join(ROOT, 'tests', 'dist', 'worker_elastic.py'), str(out)]
+        return subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                start_new_session=True)
+
+    def worlds(timeout, want_world, nranks):
+        t_end = time.time() + timeout
+        while time.time() < t_end:
+            gens = {}
+            for f in out.glob('gen*_rank*'):
+                g, r = f.name[3:].split('_rank')
+                txt = f.read_text().split()
+                if len(txt) == 3:
+                    gens.setdefault(int(g), {})[int(r)] = tuple(map(int, txt))
+            for g in sorted(gens, reverse=True):
+                if len(gens[g]) == nranks and all(v[0] == want_world and v[1] == want_world
+                                                   for v in gens[g].values()):
+                    return g, gens[g]
+            time.sleep(0.2)
+        raise AssertionError(f"no generation with world {want_world}: {sorted(p.name for p in out.iterdir())}")
+
+    procs = {n: node(n) for n in ('nodeA', 'nodeB')}
+    try:
+        g1, _ = worlds(90, 2, 2)
+        procs['nodeC'] = node('nodeC')
+        g2, r2 = worlds(90, 3, 3)
+        assert g2 > g1 and max(v[2] for v in r2.values()) >= 1  # relaunched workers see the restart count
+        os.killpg(procs['nodeC'].pid, signal.SIGKILL)  # node failure
+        procs['nodeC'].wait()
+        t_end = time.time() + 90
+        while True:
+            g3, _ = worlds(max(1, t_end - time.time()), 2, 2)
+            if g3 > g2:
+                break
+        (out / 'stop').write_text('1')
+        for n in ('nodeA', 'nodeB'):
+            rc = procs[n].wait(timeout=60)
+            log = procs[n].stdout.read().decode(errors='replace')
+            assert rc == 0, log[-3000:]
+        assert json.loads(store.get('ej/members').decode()) == []
+        assert store.get('ej/done').decode() == '1'
+    finally:
+        for p in procs.values():
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
