@@ -7,6 +7,8 @@ import numpy as np
 import torch
 import torch.nn.functional as TF
 
+from ... import ops
+
 from ...core.tensor import Tensor, _wrap as _w, _unwrap as _u
 from ...tensor._helpers import _shape
 
@@ -76,6 +78,9 @@ def _conv(x, weight, bias, stride, padding, dilation, groups, data_format, nd, f
     p, extra = _resolve_padding(padding, nd, list(t.shape[2:]), list(w.shape[2:]), s, d)
     if extra is not None:
         t = TF.pad(t, extra)
+    if cl and nd == 2 and ops.use_hip(t) and ops.conv.supported(t.permute(0, 2, 3, 1), w, groups):
+        # NHWC conv2d forward on the hand-written implicit-GEMM kernel (csrc/conv.hip)
+        return _w(ops.conv.conv2d_nhwc(t.permute(0, 2, 3, 1), w, b, s, p, d))
     out = fn(t, w, b, s, p, d, groups)
     if cl:
         out = out.permute(0, *range(2, nd + 2), 1)

@@ -56,6 +56,8 @@ _SIGS = {
     'pa_flash_set_bwd_variant': [I],
     'pa_gemm_fp8_ok': [I, I, I, LL, LL, LL],
     'pa_gemm_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
+    'pa_conv2d_fwd_ok': [I, I, I, I],
+    'pa_conv2d_fwd': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
     'pa_gemm_ok': [I, I, I, LL, LL, LL, I],
     'pa_gemm_bf16': [P, P, P, P, P, I, I, I, LL, LL, LL, I, I, F, F, I, P],
     'pa_flash_fwd': [P, P, P, P, P, I, I, I, I, I, I, LLP, LLP, LLP, LLP, F, I, I, P],

@@ -646,3 +646,50 @@ def test_fp8_linear_uses_hip_kernel():
     ref = x._t.float() @ lin.weight._t.float() + lin.bias._t.float()
     rel = (out - ref).norm() / ref.norm()
     assert rel < 0.08, rel
+
+
+@pytest.mark.parametrize("N,H,W,C,Cout,R,stride,pad,dil", [
+    (2, 14, 14, 64, 64, 1, 1, 0, 1), (2, 14, 14, 64, 128, 3, 1, 1, 1), (3, 15, 13, 128, 256, 3, 2, 1, 1),
+    (2, 9, 9, 256, 512, 1, 2, 0, 1), (1, 12, 12, 64, 72, 3, 1, 2, 2), (2, 7, 7, 512, 2048, 1, 1, 0, 1)])
+def test_hip_conv2d_nhwc(N, H, W, C, Cout, R, stride, pad, dil):
+    """csrc/conv.hip implicit-GEMM forward (+ MIOpen backward through the same op) vs fp32."""
+    from paddle.ops import conv
+    g = torch.Generator(device=DEV).manual_seed(N * H * C + Cout)
+    x = (torch.rand(N, H, W, C, device=DEV, generator=g) * 2 - 1).bfloat16().requires_grad_()
+    w = (torch.rand(Cout, C, R, R, device=DEV, generator=g) * 2 - 1).mul(0.1).bfloat16().requires_grad_()
+    b = torch.rand(Cout, device=DEV, generator=g).bfloat16().requires_grad_()
+    assert conv.supported(x, w, 1)
+    y = conv.conv2d_nhwc(x, w, b, (stride, stride), (pad, pad), (dil, dil))
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.conv2d(xr.permute(0, 3, 1, 2), wr, br, stride, pad, dil).permute(0, 2, 3, 1)
+    assert y.shape == yr.shape
+    _close(y, yr, atol=0.03 * math.sqrt(C * R * R) / 8 + 0.02, rtol=0.01, name='conv fwd')
+    gy = torch.randn_like(yr)
+    y.backward(gy.bfloat16())
+    yr.backward(gy)
+    _close(x.grad, xr.grad, atol=0.05 * math.sqrt(Cout * R * R) / 8 + 0.05, rtol=0.02, name='conv dx')
+    _close(b.grad, br.grad, atol=0.5, rtol=0.02, name='conv db')
+    _close(w.grad, wr.grad, atol=0.05 * math.sqrt(N * yr.shape[1] * yr.shape[2]) / 8 + 0.05, rtol=0.02,
+           name='conv dw')
+
+
+def test_resnet_conv_routes_to_hip():
+    from paddle.vision.models import resnet50
+    m = resnet50(data_format='NHWC')
+    m.to('gpu')
+    x = paddle.to_tensor(torch.randn(2, 64, 64, 3, device=DEV))
+    from paddle.ops import conv
+    calls = []
+    orig = conv.conv2d_fwd
+
+    def spy(*a, **k):
+        calls.append(a[1].shape)
+        return orig(*a, **k)
+    conv.conv2d_fwd = spy
+    try:
+        paddle.amp.decorate(m, level='O2', dtype='bfloat16')
+        out = m(paddle.to_tensor(x._t.bfloat16()))
+    finally:
+        conv.conv2d_fwd = orig
+    assert out.shape == [2, 1000]
+    assert len(calls) >= 50, len(calls)  # every conv but the 3-channel stem

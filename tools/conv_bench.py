@@ -1,0 +1,52 @@
+"""Hand-written implicit-GEMM conv2d forward (csrc/conv.hip) vs the storage layer's conv (MIOpen)
+on the ResNet50 NHWC bf16 layer shapes at batch 256."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+
+def bench(fn, n=10):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 1e3 / n
+
+
+def main():
+    import paddle  # noqa: F401
+    from paddle.ops import conv, _native
+    _native._load()
+    B = 256
+    shapes = [  # (H, C, Cout, R, stride)
+        (56, 64, 64, 1, 1), (56, 64, 64, 3, 1), (56, 64, 256, 1, 1), (56, 256, 64, 1, 1), (56, 256, 128, 1, 1),
+        (56, 128, 128, 3, 2), (28, 128, 512, 1, 1), (56, 256, 512, 1, 2), (28, 512, 128, 1, 1), (28, 128, 128, 3, 1),
+        (28, 512, 256, 1, 1), (28, 256, 256, 3, 2), (14, 256, 1024, 1, 1), (14, 1024, 256, 1, 1),
+        (14, 256, 256, 3, 1), (14, 1024, 512, 1, 1), (14, 512, 512, 3, 2), (7, 512, 2048, 1, 1), (7, 2048, 512, 1, 1),
+        (7, 512, 512, 3, 1)]
+    tot_h = tot_l = 0.0
+    for H, C, Cout, R, s in shapes:
+        p = R // 2
+        x = torch.randn(B, H, H, C, device='cuda', dtype=torch.bfloat16)
+        w = torch.randn(Cout, C, R, R, device='cuda', dtype=torch.bfloat16) * 0.05
+        xc = x.permute(0, 3, 1, 2)
+        Ho = (H + 2 * p - R) // s + 1
+        fl = 2.0 * B * Ho * Ho * Cout * C * R * R
+        tl = bench(lambda: torch.nn.functional.conv2d(xc, w, None, s, p))
+        th = bench(lambda: conv.conv2d_fwd(x, w, None, (s, s), (p, p), (1, 1)))
+        tot_h += th
+        tot_l += tl
+        print(f"H{H} C{C} Cout{Cout} R{R} s{s}: MIOpen {tl*1e6:8.1f} us {fl/tl/1e12:5.0f} TF | hip {th*1e6:8.1f} us "
+              f"{fl/th/1e12:5.0f} TF", flush=True)
+    print(f"sum over shapes: MIOpen {tot_l*1e3:.2f} ms, hip {tot_h*1e3:.2f} ms", flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,12 @@
+#!/bin/bash
+# hand-written conv2d: numerics, per-shape A/B vs MIOpen, ResNet bench A/B
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_hip_kernels.py -x -q -m gpu -k "conv" --timeout 120 --timeout-method thread > gpurun_out/pytest32.log 2>&1 || { echo "conv tests failed"; tail -40 gpurun_out/pytest32.log; exit 1; }
+tail -1 gpurun_out/pytest32.log
+timeout -k 10 300 python -u tools/conv_bench.py > gpurun_out/conv32.log 2>&1 || { echo "conv bench failed"; tail -20 gpurun_out/conv32.log; exit 1; }
+cat gpurun_out/conv32.log
+timeout -k 10 300 python bench.py --model resnet50 --steps 10 --warmup 5 > gpurun_out/bench32_rn.log 2>&1 || { echo "rn bench failed"; tail -20 gpurun_out/bench32_rn.log; exit 1; }
+tail -1 gpurun_out/bench32_rn.log
+PADDLE_AMD_HIP_CONV=0 timeout -k 10 300 python bench.py --model resnet50 --steps 10 --warmup 5 > gpurun_out/bench32_rn_lib.log 2>&1 || { echo "rn bench failed"; tail -20 gpurun_out/bench32_rn_lib.log; exit 1; }
+tail -1 gpurun_out/bench32_rn_lib.log
