@@ -659,7 +659,16 @@ def test_hip_conv2d_nhwc(N, H, W, C, Cout, R, stride, pad, dil):
     w = (torch.rand(Cout, C, R, R, device=DEV, generator=g) * 2 - 1).mul(0.1).bfloat16().requires_grad_()
     b = torch.rand(Cout, device=DEV, generator=g).bfloat16().requires_grad_()
     assert conv.supported(x, w, 1)
-    y = conv.conv2d_nhwc(x, w, b, (stride, stride), (pad, pad), (dil, dil))
+    old = conv._bwd_wins
+    conv._bwd_wins = lambda dy, x: True  # exercise the hand-written backward paths on every shape
+    try:
+        y = conv.conv2d_nhwc(x, w, b, (stride, stride), (pad, pad), (dil, dil))
+        _conv_check(y, x, w, b, N, C, Cout, R, stride, pad, dil)
+    finally:
+        conv._bwd_wins = old
+
+
+def _conv_check(y, x, w, b, N, C, Cout, R, stride, pad, dil):
     xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
     yr = torch.nn.functional.conv2d(xr.permute(0, 3, 1, 2), wr, br, stride, pad, dil).permute(0, 2, 3, 1)
     assert y.shape == yr.shape

@@ -31,7 +31,7 @@ def main():
         (28, 512, 256, 1, 1), (28, 256, 256, 3, 2), (14, 256, 1024, 1, 1), (14, 1024, 256, 1, 1),
         (14, 256, 256, 3, 1), (14, 1024, 512, 1, 1), (14, 512, 512, 3, 2), (7, 512, 2048, 1, 1), (7, 2048, 512, 1, 1),
         (7, 512, 512, 3, 1)]
-    tot_h = tot_l = 0.0
+    tot_h = tot_l = tot_bh = tot_bl = 0.0
     for H, C, Cout, R, s in shapes:
         p = R // 2
         x = torch.randn(B, H, H, C, device='cuda', dtype=torch.bfloat16)
@@ -43,9 +43,22 @@ def main():
         th = bench(lambda: conv.conv2d_fwd(x, w, None, (s, s), (p, p), (1, 1)))
         tot_h += th
         tot_l += tl
-        print(f"H{H} C{C} Cout{Cout} R{R} s{s}: MIOpen {tl*1e6:8.1f} us {fl/tl/1e12:5.0f} TF | hip {th*1e6:8.1f} us "
-              f"{fl/th/1e12:5.0f} TF", flush=True)
-    print(f"sum over shapes: MIOpen {tot_l*1e3:.2f} ms, hip {tot_h*1e3:.2f} ms", flush=True)
+        # backward: MIOpen data+filter grads vs the hand-written paths (MIOpen where not covered)
+        y = conv.conv2d_fwd(x, w, None, (s, s), (p, p), (1, 1))
+        dy = torch.randn_like(y)
+        dyc = dy.permute(0, 3, 1, 2)
+        tbl = bench(lambda: torch.ops.aten.convolution_backward(dyc, xc, w, None, [s, s], [p, p], [1, 1], False,
+                                                                [0, 0], 1, [True, True, False]))
+        xg = x.detach().requires_grad_()
+        wg = w.detach().requires_grad_()
+        yy = conv.conv2d_nhwc(xg, wg, None, (s, s), (p, p), (1, 1))
+        tbh = bench(lambda: torch.autograd.grad(yy, (xg, wg), dy, retain_graph=True))
+        tot_bh += tbh
+        tot_bl += tbl
+        print(f"H{H} C{C} Cout{Cout} R{R} s{s}: fwd MIOpen {tl*1e6:7.1f} us {fl/tl/1e12:4.0f} TF | hip {th*1e6:7.1f} us "
+              f"{fl/th/1e12:4.0f} TF || bwd MIOpen {tbl*1e6:7.1f} us | ours {tbh*1e6:7.1f} us", flush=True)
+    print(f"sum over shapes: fwd MIOpen {tot_l*1e3:.2f} ms, hip {tot_h*1e3:.2f} ms; bwd MIOpen {tot_bl*1e3:.2f} ms, "
+          f"ours {tot_bh*1e3:.2f} ms", flush=True)
 
 
 if __name__ == '__main__':
