@@ -154,8 +154,11 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
   const int wave = threadIdx.x >> 6;
   const int g = lane >> 4;
   const int nqb = (Sq + 127) / 128;
-  const int qb = nqb - 1 - (int)blockIdx.x;  // heavy (late, causal) blocks first
-  const int h = blockIdx.y, b = blockIdx.z;
+  // grid (Hq, B, q-blocks): the q-block index is the slowest-dispatched dimension, so every
+  // head's heaviest (late, causal) block is issued before any lighter one (longest-first order
+  // over the whole grid: the tail of the launch is the short blocks)
+  const int qb = nqb - 1 - (int)blockIdx.z;
+  const int h = blockIdx.x, b = blockIdx.y;
   const int hk = h / (Hq / Hk);
   const int q0 = qb * 128;
   const int qw0 = q0 + wave * 32;
@@ -382,9 +385,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane >> 4;
-  const int h = blockIdx.y, b = blockIdx.z;
+  // grid (Hq, B, key-blocks): early key blocks (the most causal queries) dispatched first
+  const int h = blockIdx.x, b = blockIdx.y;
   const int hk = h / (Hq / Hk);
-  const int k0 = blockIdx.x * 16 * NT * NW;
+  const int k0 = blockIdx.z * 16 * NT * NW;
   const int kw = k0 + wave * 16 * NT;
   const int off = Sk - Sq;
   const float scale_log2 = scale * kLog2e;
@@ -551,8 +555,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
   const int wave = threadIdx.x >> 6;
   const int g = lane >> 4;
   const int nqb = (Sq + 16 * NT * NW - 1) / (16 * NT * NW);
-  const int qb = nqb - 1 - (int)blockIdx.x;
-  const int h = blockIdx.y, b = blockIdx.z;
+  const int qb = nqb - 1 - (int)blockIdx.z;  // grid (Hq, B, q-blocks): heaviest first
+  const int h = blockIdx.x, b = blockIdx.y;
   const int hk = h / (Hq / Hk);
   const int q0 = qb * 16 * NT * NW;
   const int qw = q0 + wave * 16 * NT;
@@ -698,7 +702,7 @@ PA_API hipError_t pa_flash_fwd(const void* q, const void* k, const void* v, void
                                const long long* ost, float scale, int causal, int dt, hipStream_t st) {
   if (Hk <= 0 || Hq % Hk != 0) return hipErrorInvalidValue;
   Strides qs{qst[0], qst[1], qst[2]}, ks{kst[0], kst[1], kst[2]}, vs{vst[0], vst[1], vst[2]}, os{ost[0], ost[1], ost[2]};
-  dim3 grid((Sq + 127) / 128, Hq, B);
+  dim3 grid(Hq, B, (Sq + 127) / 128);
   FA_DISPATCH(dt, D, causal,
               fwd_kernel<T, DD, CC><<<grid, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                                                           (uint16_t*)o, lse, Sq, Sk, Hq, Hk, qs, ks, vs, os,
@@ -707,21 +711,26 @@ PA_API hipError_t pa_flash_fwd(const void* q, const void* k, const void* v, void
 }
 
 // backward tiling: 1 = 16 rows per wave (2 waves/SIMD), 2 = 32 rows per wave (1 wave/SIMD),
-// 3 = 16 rows per wave in 8-wave blocks (128 rows share each staged tile);
+// 3 = 16 rows per wave in 8-wave blocks (128 rows share each staged tile; default at D = 128);
 // PA_FA_BWD_VARIANT selects (A/B), default 1 (measured on MI355X, B16 S1024 H16 D128 causal:
 // fwd+bwd 1.04 ms with 1 vs 1.30 ms with 2 — the 32-row tiles lose occupancy to VGPR pressure).
-static int g_bwd_variant = -1;
-static int bwd_variant() {
-  if (g_bwd_variant < 0) {
+static int g_bwd_variant = -2;  // -2: not read yet, -1: automatic (by head dim)
+static int bwd_variant(int D) {
+  if (g_bwd_variant == -2) {
     const char* e = getenv("PA_FA_BWD_VARIANT");
-    g_bwd_variant = e ? atoi(e) : 1;
+    g_bwd_variant = e ? atoi(e) : -1;
   }
-  return g_bwd_variant;
+  if (g_bwd_variant > 0) return g_bwd_variant;
+  // measured (tools/attn_bench.py, longest-first grids): 8-wave blocks win at D = 128
+  // (B16 S1024 H16 causal fwd+bwd 0.695 vs 0.755 ms), 4-wave blocks at D = 64
+  return D == 128 ? 3 : 1;
 }
 
+// v <= 0: automatic; returns the previous setting (-1 = automatic)
 PA_API int pa_flash_set_bwd_variant(int v) {
-  const int old = bwd_variant();
-  g_bwd_variant = v;
+  bwd_variant(128);
+  const int old = g_bwd_variant;
+  g_bwd_variant = v > 0 ? v : -1;
   return old;
 }
 
@@ -741,33 +750,33 @@ PA_API hipError_t pa_flash_bwd(const void* q, const void* k, const void* v, cons
   FA_DISPATCH(dt, D, causal, {
     bwd_delta_kernel<T, DD><<<(int)((nrows + 15) / 16), 256, 0, st>>>((const uint16_t*)dout, (const uint16_t*)o, delta,
                                                                       B, Sq, Hq, dos, os);
-    if (bwd_variant() == 3) {
-      dim3 g1((Sk + 127) / 128, Hq, B);
+    if (bwd_variant(D) == 3) {
+      dim3 g1(Hq, B, (Sk + 127) / 128);
       bwd_dkdv_kernel<T, DD, CC, 1, 8><<<g1, 512, 0, st>>>((const uint16_t*)q, (const uint16_t*)k,
                                                            (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
                                                            (uint16_t*)dk, (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs,
                                                            dos, dks, dvs, scale);
-      dim3 g2((Sq + 127) / 128, Hq, B);
+      dim3 g2(Hq, B, (Sq + 127) / 128);
       bwd_dq_kernel<T, DD, CC, 1, 8><<<g2, 512, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                                                          (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk,
                                                          Hq, Hk, qs, ks, vs, dos, dqs, scale);
-    } else if (bwd_variant() == 2) {
-      dim3 g1((Sk + 127) / 128, Hq, B);
+    } else if (bwd_variant(D) == 2) {
+      dim3 g1(Hq, B, (Sk + 127) / 128);
       bwd_dkdv_kernel<T, DD, CC, 2><<<g1, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                                                         (const uint16_t*)dout, lse, delta, (uint16_t*)dk,
                                                         (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs,
                                                         scale);
-      dim3 g2((Sq + 127) / 128, Hq, B);
+      dim3 g2(Hq, B, (Sq + 127) / 128);
       bwd_dq_kernel<T, DD, CC, 2><<<g2, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                                                       (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk, Hq,
                                                       Hk, qs, ks, vs, dos, dqs, scale);
     } else {
-      dim3 g1((Sk + 63) / 64, Hq, B);
+      dim3 g1(Hq, B, (Sk + 63) / 64);
       bwd_dkdv_kernel<T, DD, CC, 1><<<g1, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                                                         (const uint16_t*)dout, lse, delta, (uint16_t*)dk,
                                                         (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs,
                                                         scale);
-      dim3 g2((Sq + 63) / 64, Hq, B);
+      dim3 g2(Hq, B, (Sq + 63) / 64);
       bwd_dq_kernel<T, DD, CC, 1><<<g2, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                                                       (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk, Hq,
                                                       Hk, qs, ks, vs, dos, dqs, scale);
