@@ -78,19 +78,48 @@ __global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, T* _
 //   p -= lr * sqrt(1-b2^t)/(1-b1^t) * m / (sqrt(v) + eps * sqrt(1-b2^t))
 // grad may be bf16/fp16/fp32; `lowp` (optional) receives the updated param in the model dtype.
 // lr/b1pow/b2pow are read from device scalars so a captured hipGraph replays with fresh values.
-template <typename G, typename P>
+typedef int nt_i4 __attribute__((ext_vector_type(4)));
+
+// 16-byte streaming (nontemporal: no reuse, keep the caches for the rest) load / store of N
+// elements of T (N * sizeof(T) == 16), converted to / from fp32
+template <typename T, int N>
+__device__ __forceinline__ void ld16(const T* __restrict__ ptr, float (&out)[N], bool nt) {
+  static_assert(N * sizeof(T) == 16, "16-byte access");
+  nt_i4 raw = nt ? __builtin_nontemporal_load(reinterpret_cast<const nt_i4*>(ptr)) : *reinterpret_cast<const nt_i4*>(ptr);
+  const Pack<T, N> pk = __builtin_bit_cast(Pack<T, N>, raw);
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = to_f(pk.v[i]);
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void st16(T* __restrict__ ptr, const float* in, bool nt) {
+  static_assert(N * sizeof(T) == 16, "16-byte access");
+  Pack<T, N> pk;
+#pragma unroll
+  for (int i = 0; i < N; ++i) pk.v[i] = from_f<T>(in[i]);
+  const nt_i4 raw = __builtin_bit_cast(nt_i4, pk);
+  if (nt) __builtin_nontemporal_store(raw, reinterpret_cast<nt_i4*>(ptr));
+  else *reinterpret_cast<nt_i4*>(ptr) = raw;
+}
+
+template <typename G, typename P, bool NTS = true>
 __device__ __forceinline__ void adamw_vec8(float* __restrict__ p, const G* __restrict__ g, float* __restrict__ m,
                                            float* __restrict__ v, P* __restrict__ lowp, long long i, float gs,
                                            float decay, float b1, float b2, float step, float eps_hat) {
   constexpr int E = 8;
   float pv[E], gv[E], mv[E], vv[E];
-  load_f<float, 4>(p + i, *reinterpret_cast<float(*)[4]>(pv));
-  load_f<float, 4>(p + i + 4, *reinterpret_cast<float(*)[4]>(pv + 4));
-  load_f<G, E>(g + i, gv);
-  load_f<float, 4>(m + i, *reinterpret_cast<float(*)[4]>(mv));
-  load_f<float, 4>(m + i + 4, *reinterpret_cast<float(*)[4]>(mv + 4));
-  load_f<float, 4>(v + i, *reinterpret_cast<float(*)[4]>(vv));
-  load_f<float, 4>(v + i + 4, *reinterpret_cast<float(*)[4]>(vv + 4));
+  ld16<float, 4>(p + i, *reinterpret_cast<float(*)[4]>(pv), NTS);
+  ld16<float, 4>(p + i + 4, *reinterpret_cast<float(*)[4]>(pv + 4), NTS);
+  if constexpr (sizeof(G) == 2) {
+    ld16<G, 8>(g + i, gv, NTS);
+  } else {
+    ld16<G, 4>(g + i, *reinterpret_cast<float(*)[4]>(gv), NTS);
+    ld16<G, 4>(g + i + 4, *reinterpret_cast<float(*)[4]>(gv + 4), NTS);
+  }
+  ld16<float, 4>(m + i, *reinterpret_cast<float(*)[4]>(mv), NTS);
+  ld16<float, 4>(m + i + 4, *reinterpret_cast<float(*)[4]>(mv + 4), NTS);
+  ld16<float, 4>(v + i, *reinterpret_cast<float(*)[4]>(vv), NTS);
+  ld16<float, 4>(v + i + 4, *reinterpret_cast<float(*)[4]>(vv + 4), NTS);
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const float gg = gv[e] * gs;
@@ -99,18 +128,18 @@ __device__ __forceinline__ void adamw_vec8(float* __restrict__ p, const G* __res
     // fast reciprocal: the update's relative error (~1 ulp) is far below bf16 resolution
     pv[e] = pv[e] * decay - step * mv[e] * __frcp_rn(__fsqrt_rn(vv[e]) + eps_hat);
   }
-  store_f<float, 4>(p + i, *reinterpret_cast<float(*)[4]>(pv));
-  store_f<float, 4>(p + i + 4, *reinterpret_cast<float(*)[4]>(pv + 4));
-  store_f<float, 4>(m + i, *reinterpret_cast<float(*)[4]>(mv));
-  store_f<float, 4>(m + i + 4, *reinterpret_cast<float(*)[4]>(mv + 4));
-  store_f<float, 4>(v + i, *reinterpret_cast<float(*)[4]>(vv));
-  store_f<float, 4>(v + i + 4, *reinterpret_cast<float(*)[4]>(vv + 4));
+  st16<float, 4>(p + i, pv, NTS);
+  st16<float, 4>(p + i + 4, pv + 4, NTS);
+  st16<float, 4>(m + i, mv, NTS);
+  st16<float, 4>(m + i + 4, mv + 4, NTS);
+  st16<float, 4>(v + i, vv, NTS);
+  st16<float, 4>(v + i + 4, vv + 4, NTS);
   if (lowp != nullptr) {
     if constexpr (sizeof(P) == 2) {
-      store_f<P, E>(lowp + i, pv);
+      st16<P, 8>(lowp + i, pv, NTS);
     } else {
-      store_f<P, 4>(lowp + i, *reinterpret_cast<float(*)[4]>(pv));
-      store_f<P, 4>(lowp + i + 4, *reinterpret_cast<float(*)[4]>(pv + 4));
+      st16<P, 4>(lowp + i, pv, NTS);
+      st16<P, 4>(lowp + i + 4, pv + 4, NTS);
     }
   }
 }
@@ -145,7 +174,7 @@ __global__ __launch_bounds__(256) void adamw_scalar_kernel(float* __restrict__ p
 // Memory-bound (28 B/param read+write for bf16 grads/params with fp32 master/m/v): 8 params
 // per lane per iteration (every access a full 16-byte vector, the bf16 gradient included), two
 // independent iterations in flight per lane.
-template <typename G, typename P>
+template <typename G, typename P, bool NTS>
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const G* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, P* __restrict__ lowp,
                                                     long long n, const float* __restrict__ lr_ptr, float lr_host,
@@ -162,10 +191,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   const long long stride = (long long)gridDim.x * 256;
   long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   for (; i + stride < nv; i += 2 * stride) {
-    adamw_vec8<G, P>(p, g, m, v, lowp, i * E, gs, decay, b1, b2, step, eps_hat);
-    adamw_vec8<G, P>(p, g, m, v, lowp, (i + stride) * E, gs, decay, b1, b2, step, eps_hat);
+    adamw_vec8<G, P, NTS>(p, g, m, v, lowp, i * E, gs, decay, b1, b2, step, eps_hat);
+    adamw_vec8<G, P, NTS>(p, g, m, v, lowp, (i + stride) * E, gs, decay, b1, b2, step, eps_hat);
   }
-  if (i < nv) adamw_vec8<G, P>(p, g, m, v, lowp, i * E, gs, decay, b1, b2, step, eps_hat);
+  if (i < nv) adamw_vec8<G, P, NTS>(p, g, m, v, lowp, i * E, gs, decay, b1, b2, step, eps_hat);
   if (blockIdx.x == 0) {
     for (long long k = nv * E + threadIdx.x; k < n; k += 256) {
       const float gg = to_f(g[k]) * gs;
@@ -294,18 +323,28 @@ PA_API hipError_t pa_rope(const void* x, void* y, const float* cosb, const float
   return hipGetLastError();
 }
 
+// A/B knobs for the streaming update: nontemporal 16-byte accesses, and blocks per CU
+static int g_adamw_nt = 1, g_adamw_bpc = 8;
+PA_API void pa_adamw_tune(int nt, int blocks_per_cu) {
+  g_adamw_nt = nt;
+  g_adamw_bpc = blocks_per_cu > 0 ? blocks_per_cu : 8;
+}
+
 // gd = grad dtype, pd = low-precision param copy dtype (-1 = none)
 PA_API hipError_t pa_adamw(float* p, const void* g, float* m, float* v, void* lowp, long long n, const float* lr_ptr,
                            float lr, float b1, float b2, float eps, float wd, float b1pow, float b2pow,
                            const float* grad_scale, int gd, int pd, hipStream_t st) {
-  const int grid = grid_for(n / 16 + 1, 256, 256 * 8);
+  const int grid = grid_for(n / 16 + 1, 256, 256 * g_adamw_bpc);
   // every 8-element access is a 16-byte vector (or two): all five streams must be 16-byte aligned
   const bool aligned = ((((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g | (uintptr_t)lowp) & 15) == 0);
 #define PA_ADAM(G, P)                                                                                          \
   do {                                                                                                         \
-    if (aligned)                                                                                               \
-      adamw_kernel<G, P><<<grid, 256, 0, st>>>(p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1, b2, eps, wd, \
-                                               b1pow, b2pow, grad_scale);                                      \
+    if (aligned && g_adamw_nt)                                                                                 \
+      adamw_kernel<G, P, true><<<grid, 256, 0, st>>>(p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1, b2, eps, \
+                                                     wd, b1pow, b2pow, grad_scale);                            \
+    else if (aligned)                                                                                          \
+      adamw_kernel<G, P, false><<<grid, 256, 0, st>>>(p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1, b2,   \
+                                                      eps, wd, b1pow, b2pow, grad_scale);                      \
     else                                                                                                       \
       adamw_scalar_kernel<G, P><<<grid_for(n, 256, 256 * 8), 256, 0, st>>>(                                    \
           p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1, b2, eps, wd, b1pow, b2pow, grad_scale);          \

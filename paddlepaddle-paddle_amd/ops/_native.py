@@ -53,6 +53,7 @@ _SIGS = {
     'pa_momentum': [P, P, P, P, LL, P, F, F, F, F, I, P, I, I, P],
     'pa_sumsq_parts': [],
     'pa_gemm_set_variant': [I],
+    'pa_adamw_tune': [I, I],
     'pa_flash_set_bwd_variant': [I],
     'pa_gemm_fp8_ok': [I, I, I, LL, LL, LL],
     'pa_gemm_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
@@ -66,6 +67,7 @@ _SIGS = {
 }
 
 _LL_RET = {'pa_bn_ws_floats'}
+_VOID_RET = {'pa_adamw_tune'}
 
 
 def _load():
@@ -80,7 +82,7 @@ def _load():
         for name, args in _SIGS.items():
             fn = getattr(l, name)
             fn.argtypes = args
-            fn.restype = ctypes.c_longlong if name in _LL_RET else ctypes.c_int
+            fn.restype = None if name in _VOID_RET else (ctypes.c_longlong if name in _LL_RET else ctypes.c_int)
         lib = l
     except OSError as e:  # pragma: no cover
         load_error = str(e)
