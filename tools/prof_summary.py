@@ -13,7 +13,8 @@ def cat(name):
         return 'optimizer'
     if 'conv' in n or 'miopen' in n or 'igemm' in n or 'xdlops' in n:
         return 'conv'
-    if 'norm' in n or 'colsum' in n or 'act' in n or 'dropout' in n or 'xent' in n or 'embedding' in n:
+    if ('norm' in n or 'colsum' in n or 'act' in n or 'dropout' in n or 'xent' in n or 'embedding' in n
+            or 'bn::' in n or '2bn' in n or 'momentum' in n):
         return 'fused-hip'
     return 'other'
 
