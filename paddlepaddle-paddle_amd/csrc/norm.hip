@@ -193,33 +193,50 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dy,
     if (j < cols) load_f<WT, E>(w + j, wv[c]);
   }
   const float inv_n = 1.0f / cols;
+  // Rows are software-pipelined: the next row's x / dy / dsum are loaded into registers before
+  // this row's block reductions, so the HBM latency overlaps the barriers (the kernel was
+  // latency-bound at one row in flight per block).
+  Pack<T, E> px[MAXC], pd[MAXC], ps[MAXC];
+  auto prefetch = [&](int r) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int j = (c * 256 + tid) * E;
+      if (r < rows && j < cols) {
+        const size_t b = (size_t)r * cols + j;
+        px[c] = *reinterpret_cast<const Pack<T, E>*>(x + b);
+        pd[c] = *reinterpret_cast<const Pack<T, E>*>(dy + b);
+        if (dsum != nullptr) ps[c] = *reinterpret_cast<const Pack<T, E>*>(dsum + b);
+      }
+    }
+  };
+  prefetch(blockIdx.x);
   for (int row = blockIdx.x; row < rows; row += gridDim.x) {
     const size_t base = (size_t)row * cols;
     const float mu = RMS ? 0.f : mean[row];
     const float rs = rstd[row];
-    float xh[MAXC][E], g[MAXC][E];
+    float xh[MAXC][E], g[MAXC][E], dsv[MAXC][E];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       const int j = (c * 256 + tid) * E;
       if (j < cols) {
-        float xv[E], dv[E];
-        load_f<T, E>(x + base + j, xv);
-        load_f<T, E>(dy + base + j, dv);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-          xh[c][e] = (xv[e] - mu) * rs;
-          g[c][e] = dv[e] * wv[c][e];
+          const float xv = to_f(px[c].v[e]), dv = to_f(pd[c].v[e]);
+          xh[c][e] = (xv - mu) * rs;
+          g[c][e] = dv * wv[c][e];
           s1 += g[c][e];
           s2 += g[c][e] * xh[c][e];
-          aw[c][e] += dv[e] * xh[c][e];
-          ab[c][e] += dv[e];
+          aw[c][e] += dv * xh[c][e];
+          ab[c][e] += dv;
+          dsv[c][e] = dsum != nullptr ? to_f(ps[c].v[e]) : 0.f;
         }
       } else {
 #pragma unroll
-        for (int e = 0; e < E; ++e) { xh[c][e] = 0.f; g[c][e] = 0.f; }
+        for (int e = 0; e < E; ++e) { xh[c][e] = 0.f; g[c][e] = 0.f; dsv[c][e] = 0.f; }
       }
     }
+    prefetch(row + gridDim.x);
     // two block reductions fused into one barrier pair
     s1 = wave_sum(s1);
     s2 = wave_sum(s2);
@@ -234,13 +251,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dy,
       if (j < cols) {
         float o[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) o[e] = rs * (g[c][e] - m1 - xh[c][e] * m2);
-        if (dsum != nullptr) {  // gradient flowing into the residual stream from later layers
-          float ds[E];
-          load_f<T, E>(dsum + base + j, ds);
-#pragma unroll
-          for (int e = 0; e < E; ++e) o[e] += ds[e];
-        }
+        for (int e = 0; e < E; ++e) o[e] = rs * (g[c][e] - m1 - xh[c][e] * m2) + dsv[c][e];
         store_f<T, E>(dx + base + j, o);
         if constexpr (DROP) {
           float m[E];
