@@ -153,7 +153,8 @@ __device__ __forceinline__ void stage(const Src<NT>& s, char* img, int t, int wa
 // so hipcc's own scoreboard knows every ds_read has retired and adds no lgkmcnt(0) later.
 template <int PER_SLOT>
 __device__ __forceinline__ void wait_barrier(int n_inflight) {
-  if (n_inflight >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_SLOT) : "memory");
+  if (n_inflight >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER_SLOT) : "memory");
+  else if (n_inflight == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_SLOT) : "memory");
   else if (n_inflight == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_SLOT) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt/expcnt unconstrained
@@ -180,7 +181,7 @@ __device__ __forceinline__ void tile_coords(int bid, int nwg, int tm, int tn, in
 // tiles).  WN = 2: 4 waves, 128x128 per wave (one wave per SIMD, 64 accumulator tiles that live
 // in the AGPR half of the 512-entry register file, half the LDS bytes per MFMA).
 // EPI: 0 = bf16 out (alpha, beta*C, bias);  1 = fp32 split-K slab out (raw acc)
-template <bool AK, bool BK_, int EPI, int WN>
+template <bool AK, bool BK_, int EPI, int WN, int NS = NSLOT>
 __global__ __launch_bounds__(128 * WN, 1) void gemm_kernel(const uint16_t* __restrict__ A,
                                                            const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
                                                            float* __restrict__ ws, const uint16_t* __restrict__ bias,
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_kernel(const uint16_t* __res
   constexpr int NT = 128 * WN;
   constexpr int FM = 8, FN = 16 / WN;  // 16x16 fragments per wave along M / N
   constexpr int PER_SLOT = 2 * Src<NT>::N;
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  __shared__ __attribute__((aligned(1024))) char smem[NS * SLOT_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WN, wc = wave % WN;
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
@@ -213,13 +214,13 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_kernel(const uint16_t* __res
   // NSLOT sub-tiles ahead into the slot of sub-tile s (read during step s-1, before the last
   // barrier); each step retires sub-tile s+2 (read during step s+1).
 #pragma unroll
-  for (int s = 0; s < NSLOT; ++s) {
+  for (int s = 0; s < NS; ++s) {
     if (s < ns) {
       stage<NT>(sa, smem + s * SLOT_BYTES, s, wave);
       stage<NT>(sb, smem + s * SLOT_BYTES + OP_BYTES, s, wave);
     }
   }
-  wait_barrier<PER_SLOT>(max(min(ns, NSLOT) - 2, 0));  // sub-tiles 0 and 1 landed
+  wait_barrier<PER_SLOT>(max(min(ns, NS) - 2, 0));  // sub-tiles 0 and 1 landed
   s16x8 fa[2][FM], fb[2][FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) fb[0][j] = ld_frag<BK_>(smem + OP_BYTES, wc * (16 * FN) + j * 16, lane);
@@ -228,16 +229,17 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_kernel(const uint16_t* __res
   // Two sub-steps per trip, fragment sets alternate without copies.  The prefetch reads are
   // unconditional (past the last sub-tile they read a stale slot, unused) so hipcc sees no merge
   // point that would force lgkmcnt(0) before the MFMAs.
+  int slot = 0;  // ring slot of sub-tile ss (wave-uniform, wrapped incrementally)
   for (int s = 0; s < ns; s += 2) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int ss = s + u;
-      const int slot = ss & (NSLOT - 1);
-      if (ss + NSLOT < ns) {
-        stage<NT>(sa, smem + slot * SLOT_BYTES, ss + NSLOT, wave);
-        stage<NT>(sb, smem + slot * SLOT_BYTES + OP_BYTES, ss + NSLOT, wave);
+      const int nslot = slot + 1 == NS ? 0 : slot + 1;
+      if (ss + NS < ns) {
+        stage<NT>(sa, smem + slot * SLOT_BYTES, ss + NS, wave);
+        stage<NT>(sb, smem + slot * SLOT_BYTES + OP_BYTES, ss + NS, wave);
       }
-      const char* ia = smem + ((ss + 1) & (NSLOT - 1)) * SLOT_BYTES;
+      const char* ia = smem + nslot * SLOT_BYTES;
 #pragma unroll
       for (int j = 0; j < FN; ++j) fb[u ^ 1][j] = ld_frag<BK_>(ia + OP_BYTES, wc * (16 * FN) + j * 16, lane);
 #pragma unroll
@@ -248,7 +250,8 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_kernel(const uint16_t* __res
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma(fb[u][j], fa[u][i], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
-      wait_barrier<PER_SLOT>(max(min(ns - 1, ss + NSLOT) - (ss + 2), 0));
+      wait_barrier<PER_SLOT>(max(min(ns - 1, ss + NS) - (ss + 2), 0));
+      slot = nslot;
     }
   }
 
@@ -457,7 +460,7 @@ __global__ void splitk_reduce(const float* __restrict__ ws, uint16_t* __restrict
   store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(dst), v);
 }
 
-static int g_variant = 1;
+static int g_variant = 3;
 
 template <bool AK, bool BKM, int EPI>
 static hipError_t launch(const void* A, const void* B, void* C, float* ws, const void* bias, int M, int N, int K,
@@ -465,7 +468,11 @@ static hipError_t launch(const void* A, const void* B, void* C, float* ws, const
                          hipStream_t st) {
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   dim3 grid(tm * tn, 1, splitk);
-  if (g_variant == 2)
+  if (g_variant == 3)
+    gemm_kernel<AK, BKM, EPI, 4, 5><<<grid, 512, 0, st>>>((const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, ws,
+                                                          (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
+                                                          K / splitk);
+  else if (g_variant == 2)
     gemm_kernel<AK, BKM, EPI, 2><<<grid, 256, 0, st>>>((const uint16_t*)A, (const uint16_t*)B, (uint16_t*)C, ws,
                                                        (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
                                                        K / splitk);
@@ -501,7 +508,9 @@ PA_API int pa_gemm_ok(int M, int N, int K, long long lda, long long ldb, long lo
   return 1;
 }
 
-// block layout (A/B benchmarking): 1 = 8 waves of 128x64, 2 = 4 waves of 128x128
+// block layout (A/B benchmarking): 1 = 8 waves of 128x64, 2 = 4 waves of 128x128,
+// 3 = 8 waves with a 5-slot ring (160 KB LDS: three sub-tiles of DMA in flight; default:
+// +2-9 % over 1 on the GPT-3 shapes, profiles/hip_gemm_r1_v3.log)
 PA_API int pa_gemm_set_variant(int v) {
   const int old = g_variant;
   g_variant = v;

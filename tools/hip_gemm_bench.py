@@ -21,7 +21,7 @@ def bench(fn, n=20):
     return e0.elapsed_time(e1) / 1e3 / n
 
 
-VARIANTS = [int(v) for v in os.environ.get('GEMM_VARIANTS', '1,2').split(',')]
+VARIANTS = [int(v) for v in os.environ.get('GEMM_VARIANTS', '1,3').split(',')]
 
 
 def main():
