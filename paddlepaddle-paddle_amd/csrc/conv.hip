@@ -29,7 +29,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int BM = 256, BK = 32, NT = 512, NSLOT = 4;
+constexpr int BM = 256, BK = 32, NT = 512;
 
 // DMA source for taps in the zero padding (and clamped-away rows never stored)
 __device__ uint4 g_zero16[4];
@@ -59,11 +59,19 @@ __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
                : "memory");
 }
 
+template <int PER_SLOT, int N = 6>
+__device__ __forceinline__ void wait_vm(int n_inflight) {
+  if constexpr (N == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (n_inflight >= N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N * PER_SLOT) : "memory");
+    else wait_vm<PER_SLOT, N - 1>(n_inflight);
+  }
+}
+
 template <int PER_SLOT>
 __device__ __forceinline__ void wait_barrier(int n_inflight) {
-  if (n_inflight >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_SLOT) : "memory");
-  else if (n_inflight == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_SLOT) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  wait_vm<PER_SLOT>(n_inflight);
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -93,6 +101,9 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
   constexpr int NBC = BN * 4;                 // 16-B chunks of one B sub-tile
   constexpr int DMA_B = NBC >= NT ? NBC / NT : 1;  // BN = 64: waves 4-7 repeat waves 0-3 (same bytes, same place)
   constexpr int PER_SLOT = 2 + DMA_B;
+  // ring depth 4: filling all 160 KB (5-8 slots) measured slower on the ResNet shapes (short K
+  // loops pay the longer prologue, and BN = 64/128 blocks lose their second block per CU)
+  constexpr int NSLOT = 4;
   __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
@@ -166,13 +177,14 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
   for (int j = 0; j < FN; ++j) fb[0][j] = ld_frag(smem + OPA, wc * (16 * FN) + j * 16, lane);
 #pragma unroll
   for (int i = 0; i < 8; ++i) fa[0][i] = ld_frag(smem, wr * 128 + i * 16, lane);
+  int slot = 0;
   for (int s = 0; s < ns; s += 2) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int ss = s + u;
-      const int slot = ss & (NSLOT - 1);
+      const int nslot = slot + 1 == NSLOT ? 0 : slot + 1;
       if (ss + NSLOT < ns) stage(ss + NSLOT, slot);
-      const char* ia = smem + ((ss + 1) & (NSLOT - 1)) * SLOT;
+      const char* ia = smem + nslot * SLOT;
 #pragma unroll
       for (int j = 0; j < FN; ++j) fb[u ^ 1][j] = ld_frag(ia + OPA, wc * (16 * FN) + j * 16, lane);
 #pragma unroll
@@ -184,6 +196,7 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma(fb[u][j], fa[u][i], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
       wait_barrier<PER_SLOT>(max(min(ns - 1, ss + NSLOT) - (ss + 2), 0));
+      slot = nslot;
     }
   }
 
