@@ -2,8 +2,8 @@
 
 Reference: paddle/phi/kernels/gpudnn/conv_kernel.cu (forward), conv_grad_kernel.cu (backward).
 Forward runs csrc/conv.hip (im2col folded into the LDS-DMA source addresses, zero padding via a
-zero block, bias fused); the weight is packed once per weight version into the [Cout][R][S][C]
-k-contiguous image the kernel stages.  Backward: the stride-1 data gradient is the same kernel
+zero block, bias fused); the weight is packed into the [Cout][R][S][C]
+k-contiguous image the kernel stages (re-packed per call).  Backward: the stride-1 data gradient is the same kernel
 run on dY with the flipped, transposed filter; the 1x1 filter gradient is the hand-written GEMM
 (dY^T X, split-K over pixels); strided data gradients and k>1 filter gradients use the storage
 layer's convolution backward (MIOpen NHWC kernels).
@@ -16,7 +16,6 @@ from . import _native as N
 
 _enabled = os.environ.get('PADDLE_AMD_HIP_CONV', '1') != '0'
 _bwd_enabled = os.environ.get('PADDLE_AMD_HIP_CONV_BWD', '1') != '0'
-_pack_cache = {}
 
 
 def supported(x, w, groups):
@@ -31,15 +30,11 @@ def supported(x, w, groups):
 
 
 def _packed(w):
-    key = id(w)
-    ent = _pack_cache.get(key)
-    ver = (w._version, w.data_ptr())
-    if ent is None or ent[0] != ver:
-        ent = (ver, w.detach().permute(0, 2, 3, 1).contiguous())
-        _pack_cache[key] = ent
-        if len(_pack_cache) > 512:
-            _pack_cache.pop(next(iter(_pack_cache)))
-    return ent[1]
+    """[Cout][R][S][C] image of an OIHW filter.  Re-packed on every call: the fused optimizer
+    kernels update parameters in place through raw pointers, which does not bump the tensor
+    version counter, so no cache keyed on the tensor could tell a stale image (one small copy
+    per conv per step)."""
+    return w.detach().permute(0, 2, 3, 1).contiguous()
 
 
 def _out_hw(H, W, R, S, stride, pad, dil):

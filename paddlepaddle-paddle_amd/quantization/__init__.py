@@ -388,8 +388,8 @@ class _Sequential2(Layer):
 
 
 class FP8Linear(Layer):
-    """Linear on e4m3 operands with per-tensor scales.  On MI355X the weight is quantised once
-    per weight version into the [out, in] e4m3 image the hand-written fp8 MFMA kernel reads
+    """Linear on e4m3 operands with per-tensor scales.  On MI355X the weight is quantised (once,
+    for frozen eval-mode weights) into the [out, in] e4m3 image the hand-written fp8 MFMA kernel reads
     (ops.gemm.hip_fp8_mm; scales stay on the device) and activations are quantised per call;
     elsewhere a dequantised-matmul emulation of the same numerics."""
 
@@ -401,8 +401,11 @@ class FP8Linear(Layer):
         self._wq = None  # (weight version, data_ptr, e4m3 [out, in], scale)
 
     def _quant_weight(self, w):
+        # cached only for frozen weights in eval mode: fused optimizer kernels update parameters
+        # in place without bumping the version counter, so a trainable weight is re-quantised
         key = (w._version, w.data_ptr())
-        if self._wq is None or self._wq[0] != key:
+        frozen = not self.training and not w.requires_grad
+        if self._wq is None or self._wq[0] != key or not frozen:
             from ..ops.gemm import fp8_quantize
             q, s = fp8_quantize(w.detach().t())
             self._wq = (key, q.contiguous(), s)

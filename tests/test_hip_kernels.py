@@ -702,3 +702,23 @@ def test_resnet_conv_routes_to_hip():
         conv.conv2d_fwd = orig
     assert out.shape == [2, 1000]
     assert len(calls) >= 50, len(calls)  # every conv but the 3-channel stem
+
+
+def test_conv_sees_in_place_optimizer_updates():
+    """Regression: the fused optimizer writes parameters through raw pointers (no version bump);
+    the hand-written conv must use the updated filter on the next forward."""
+    conv = paddle.nn.Conv2D(64, 128, 3, padding=1, data_format='NHWC')
+    conv.to('gpu')
+    opt = paddle.optimizer.Momentum(learning_rate=0.5, momentum=0.9, parameters=conv.parameters(),
+                                    multi_precision=True)
+    conv, opt = paddle.amp.decorate(conv, opt, level='O2', dtype='bfloat16')
+    x = paddle.to_tensor(torch.randn(2, 8, 8, 64, device=DEV).bfloat16())
+    for _ in range(2):
+        y = conv(x)
+        (y * y).mean().backward()
+        opt.step()
+        opt.clear_grad()
+    y = conv(x)._t.float()
+    w = conv.weight._t.float()
+    ref = torch.nn.functional.conv2d(x._t.float().permute(0, 3, 1, 2), w, conv.bias._t.float(), 1, 1)
+    _close(y, ref.permute(0, 2, 3, 1), atol=0.05, rtol=0.02, name='conv after optimizer steps')

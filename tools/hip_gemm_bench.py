@@ -45,6 +45,21 @@ def main():
             print(f"fp8 {name} M={M} K={K} N={N}: torch._scaled_mm {tl*1e6:8.1f} us {fl/tl/1e12:6.0f} TF | "
                   f"hip {th*1e6:8.1f} us {fl/th/1e12:6.0f} TF", flush=True)
         return
+    if len(sys.argv) > 1 and sys.argv[1] == 'lmhead':
+        V, Hd = 50304, 2048
+        h = torch.rand(M, Hd, device=dev, dtype=bf) * 2 - 1
+        E = torch.rand(V, Hd, device=dev, dtype=bf) * 2 - 1
+        dl = torch.rand(M, V, device=dev, dtype=bf) * 2 - 1
+        gE = torch.zeros(V, Hd, device=dev, dtype=bf)
+        fl = 2.0 * M * Hd * V
+        for lay, lib, mine in (('fwd h@E^T', lambda: torch.mm(h, E.t()), lambda: gemm.hip_mm(h, E.t())),
+                               ('dgrad dl@E', lambda: torch.mm(dl, E), lambda: gemm.hip_mm(dl, E)),
+                               ('wgrad dl^T@h', lambda: gE.addmm_(dl.t(), h),
+                                lambda: gemm.hip_mm(dl.t(), h, out=gE, beta=1.0))):
+            tl, th = bench(lib, 5), bench(mine, 5)
+            print(f"lmhead {lay:14s}: hipBLASLt {tl*1e6:8.1f} us {fl/tl/1e12:6.0f} TF | hip {th*1e6:8.1f} us "
+                  f"{fl/th/1e12:6.0f} TF", flush=True)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == 'square':
         shapes = [('sq4k', 4096, 4096), ('sq8k', 8192, 8192)]
         M = None
