@@ -315,6 +315,38 @@ __global__ __launch_bounds__(256) void dropout_bwd(const T* __restrict__ dy, T* 
   }
 }
 
+// y[c, r] = x[r, c] for 2-byte dtypes, [rows, cols] with both dims multiples of 64.
+// One 64x64 tile per block through LDS: 16-byte global loads along x's rows, 16-byte global
+// stores along y's rows; the LDS row pitch of 66 elements (33 banks) spreads the column reads.
+// Used to hand hipBLASLt a K-major copy of paddle's [in, out] Linear weight for the forward GEMM.
+__global__ __launch_bounds__(256) void transpose2d_b16(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                       int rows, int cols) {
+  __shared__ uint16_t tile[64][66];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int lr = tid >> 3, lc = (tid & 7) * 8;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int r = lr + p * 32;
+    const uint4 v = *reinterpret_cast<const uint4*>(x + (long long)(r0 + r) * cols + c0 + lc);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      tile[r][lc + 2 * j] = (uint16_t)(w[j] & 0xffffu);
+      tile[r][lc + 2 * j + 1] = (uint16_t)(w[j] >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int c = lr + p * 32;  // output row (input column)
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = (uint32_t)tile[lc + 2 * j][c] | ((uint32_t)tile[lc + 2 * j + 1][c] << 16);
+    *reinterpret_cast<uint4*>(y + (long long)(c0 + c) * rows + r0 + lc) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 int cs_rows_per_block(int rows, int colblocks);
 
 template <typename T, typename Act>
@@ -354,6 +386,14 @@ PA_API hipError_t pa_bias_act(int act, int dir, const void* dy, const void* x, c
     }
   });
   return hipSuccess;
+}
+
+// y = x^T for a contiguous 2-byte [rows, cols] matrix (rows, cols multiples of 64).
+PA_API hipError_t pa_transpose2d(const void* x, void* y, int rows, int cols, int elem_bytes, hipStream_t st) {
+  if (elem_bytes != 2 || rows % 64 != 0 || cols % 64 != 0 || rows <= 0 || cols <= 0 || rows / 64 > 65535)
+    return hipErrorInvalidValue;
+  transpose2d_b16<<<dim3(cols / 64, rows / 64), 256, 0, st>>>((const uint16_t*)x, (uint16_t*)y, rows, cols);
+  return hipGetLastError();
 }
 
 // a, b: [rows, cols] views with row stride a_stride (elements); y / da / db dense [rows, cols]

@@ -94,6 +94,36 @@ def wgrad_accumulate(x2, dy2, gw):
     return True
 
 
+def transpose2d(x):
+    """x^T materialised (csrc/act.hip ``pa_transpose2d``: 64x64 LDS tiles, 16-byte loads/stores)."""
+    R, C = x.shape
+    if N._load() is None:
+        raise RuntimeError("transpose2d: HIP kernel library not loaded: " + str(N.load_error))
+    y = torch.empty((C, R), dtype=x.dtype, device=x.device)
+    N.check(N.lib.pa_transpose2d(N.ptr(x), N.ptr(y), R, C, x.element_size(), N.stream()), 'transpose2d')
+    return y
+
+
+_kmajor_fwd = os.environ.get('PADDLE_AMD_KMAJOR_FWD', '1') != '0'
+
+
+def kmajor_weight(x2, w):
+    """K-major copy W^T ([out, in]) of a paddle [in, out] weight for the forward GEMM, or None.
+
+    hipBLASLt runs y = x @ W (B operand N-major) at 1.06-1.39 PF/s on the GPT-3 1.3B shapes but
+    y = x @ (W^T)^T (both operands K-major, the dgrad layout) at 1.25-1.59 PF/s
+    (tools/fwd_layout_bench.py, profiles/fwd_layout_r1.log); the transpose of a 2048x8192 weight
+    costs ~15 us, so the copy pays off once the token count is large (training micro-batches).
+    """
+    if not _kmajor_fwd or x2.shape[0] < 4096 or w.dtype not in (torch.bfloat16, torch.float16):
+        return None
+    if w.dim() != 2 or not w.is_contiguous() or w.shape[0] % 64 or w.shape[1] % 64 or not x2.is_cuda:
+        return None
+    if N._load() is None:
+        return None
+    return transpose2d(w)
+
+
 _FP8_FMT = {torch.float8_e4m3fn: 0, torch.float8_e5m2: 1}
 
 

@@ -1,6 +1,7 @@
 """Linear with the weight gradient accumulated IN PLACE into the flat gradient buffer.
 
-y = x @ W + b (W: [in, out], paddle layout).  Backward:
+y = x @ W + b (W: [in, out], paddle layout; with many tokens the GEMM reads a transient K-major
+copy W^T from ops.gemm.kmajor_weight, the operand layout hipBLASLt runs fastest).  Backward:
   dX = dY @ W^T                                (hipBLASLt)
   W.grad += X^T @ dY                           (hand-written MFMA GEMM csrc/gemm.hip, beta = 1 epilogue)
   b.grad += colsum(dY)                         (csrc/act.hip pa_colsum, in place)
@@ -23,7 +24,9 @@ class _LinearAccum(torch.autograd.Function):
         if w.untyped_storage().nbytes() == 0:
             raise RuntimeError("linear weight storage is released (sharding stage-3 unit not gathered)")
         x2 = x.reshape(-1, x.shape[-1])
-        y = torch.addmm(b, x2, w) if b is not None else torch.mm(x2, w)
+        wt = gemm.kmajor_weight(x2, w)  # K-major copy for the library's fast layout (transient)
+        wf = w if wt is None else wt.t()
+        y = torch.addmm(b, x2, wf) if b is not None else torch.mm(x2, wf)
         ctx.save_for_backward(x2, w)
         ctx.box, ctx.xshape = box, x.shape
         return y.reshape(*x.shape[:-1], w.shape[1])

@@ -722,3 +722,27 @@ def test_conv_sees_in_place_optimizer_updates():
     w = conv.weight._t.float()
     ref = torch.nn.functional.conv2d(x._t.float().permute(0, 3, 1, 2), w, conv.bias._t.float(), 1, 1)
     _close(y, ref.permute(0, 2, 3, 1), atol=0.05, rtol=0.02, name='conv after optimizer steps')
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("R,C", [(64, 64), (2048, 8192), (8192, 2048), (192, 320)])
+def test_hip_transpose2d(dt, R, C):
+    """csrc/act.hip pa_transpose2d (64x64 LDS tiles) is an exact transpose."""
+    from paddle.ops import gemm
+    x = torch.randn(R, C, device=DEV).to(dt)
+    assert torch.equal(gemm.transpose2d(x), x.t().contiguous())
+
+
+def test_linear_kmajor_forward_matches_plain_layout():
+    """Linear forward on a transient K-major weight copy (ops.gemm.kmajor_weight) gives the same
+    output and gradients as the [in, out] layout."""
+    from paddle.ops import gemm, linear
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = (torch.rand(4096, 512, device=DEV, generator=g) * 2 - 1).bfloat16()
+    w = ((torch.rand(512, 384, device=DEV, generator=g) * 2 - 1) * 0.05).bfloat16()
+    b = torch.rand(384, device=DEV, generator=g).bfloat16()
+    wt = gemm.kmajor_weight(x, w)
+    assert wt is not None and wt.shape == (384, 512)
+    ref = x.float() @ w.float() + b.float()
+    _close(torch.addmm(b, x, wt.t()), ref, atol=0.05, rtol=0.01, name='kmajor linear')
+    assert gemm.kmajor_weight(x[:64], w) is None  # small token counts keep the plain layout
