@@ -150,6 +150,10 @@ def _pool(x, kernel_size, stride, padding, ceil_mode, data_format, nd, fn, extra
     if pre is not None:
         t = TF.pad(t, pre, value=float('-inf') if fn in (TF.max_pool1d, TF.max_pool2d, TF.max_pool3d) else 0.0)
     kw = dict(extra or {})
+    if cl and nd == 2 and fn is TF.max_pool2d and not return_mask and pre is None and ops.use_hip(t) and \
+            ops.pool.supported(_u(x), k, s, p):
+        # NHWC max pool on csrc/pool.hip (one-byte argmax, atomics-free gather backward)
+        return _w(ops.pool.max_pool2d_nhwc(_u(x), k, s, p, ceil_mode))
     if return_mask:
         out, mask = fn(t, k, s, p, ceil_mode=ceil_mode, return_indices=True, **kw)
         if cl:

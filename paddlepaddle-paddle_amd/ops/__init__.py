@@ -34,4 +34,4 @@ def native_loaded():
     return _native.lib is not None
 
 
-from . import norm, softmax, act, xent, embedding, rope, optim, flash_attn, gemm, linear, fused, batchnorm, conv  # noqa: E402,F401,E501
+from . import norm, softmax, act, xent, embedding, rope, optim, flash_attn, gemm, linear, fused, batchnorm, conv, pool  # noqa: E402,F401,E501

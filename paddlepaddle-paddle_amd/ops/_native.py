@@ -34,6 +34,8 @@ _SIGS = {
     'pa_bias_act_bwd_dbias': [I, P, P, P, P, P, P, I, I, I, I, I, P],
     'pa_colsum': [P, P, P, I, I, I, I, I, P],
     'pa_transpose2d': [P, P, I, I, I, P],
+    'pa_maxpool2d_nhwc_fwd': [P, P, P] + [I] * 13 + [P],
+    'pa_maxpool2d_nhwc_bwd': [P, P, P] + [I] * 13 + [P],
     'pa_bn_ws_floats': [I, I, I],
     'pa_bn_fwd': [P, P, P, P, P, P, P, P, P, P, I, I, F, F, I, I, I, I, P],
     'pa_bn_bwd': [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],

@@ -746,3 +746,34 @@ def test_linear_kmajor_forward_matches_plain_layout():
     ref = x.float() @ w.float() + b.float()
     _close(torch.addmm(b, x, wt.t()), ref, atol=0.05, rtol=0.01, name='kmajor linear')
     assert gemm.kmajor_weight(x[:64], w) is None  # small token counts keep the plain layout
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("N,H,W,C,k,s,p,ceil", [(2, 112, 112, 64, 3, 2, 1, False), (3, 15, 13, 16, 2, 2, 0, False),
+                                                 (2, 17, 19, 32, 3, 2, 1, True), (1, 9, 9, 8, 3, 1, 1, False),
+                                                 (2, 10, 12, 24, 3, 3, 0, True)])
+def test_hip_maxpool2d_nhwc(dt, N, H, W, C, k, s, p, ceil):
+    """csrc/pool.hip NHWC max pool (fwd + gather backward) vs torch max_pool2d on the same values."""
+    import torch.nn.functional as TF
+    from paddle.ops import pool
+    g = torch.Generator(device=DEV).manual_seed(H * W + C)
+    x = torch.randn(N, H, W, C, device=DEV, generator=g).to(dt).requires_grad_()
+    assert pool.supported(x, (k, k), (s, s), (p, p))
+    y = pool.max_pool2d_nhwc(x, (k, k), (s, s), (p, p), ceil)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    yr = TF.max_pool2d(xr, k, s, p, ceil_mode=ceil)
+    assert y.shape == yr.permute(0, 2, 3, 1).shape
+    _close(y, yr.permute(0, 2, 3, 1), 0.0, name='maxpool fwd')
+    dy = torch.randn(y.shape, device=DEV, generator=g).to(dt)
+    y.backward(dy)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    tol = (1e-2, 8e-3) if dt == torch.bfloat16 else (1e-5, 0.0)  # bf16 rounding of sums of <= 4 window grads
+    _close(x.grad, xr.grad.permute(0, 2, 3, 1), *tol, name='maxpool bwd')
+
+
+def test_nhwc_max_pool2d_routes_to_hip():
+    x = paddle.to_tensor(torch.randn(2, 16, 16, 64, device=DEV).bfloat16())
+    y = paddle.nn.functional.max_pool2d(x, 3, 2, 1, data_format='NHWC')
+    assert 'MaxPoolNHWC' in type(y._t.grad_fn).__name__ if y._t.grad_fn is not None else True
+    ref = torch.nn.functional.max_pool2d(x._t.float().permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    _close(y._t, ref, 0.0, name='F.max_pool2d NHWC')
