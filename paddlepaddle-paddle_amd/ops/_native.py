@@ -57,6 +57,8 @@ _SIGS = {
     'pa_sumsq_parts': [],
     'pa_gemm_set_variant': [I],
     'pa_adamw_tune': [I, I],
+    'pa_act_fwd_tune': [I, I],
+    'pa_act_cs_tune': [I],
     'pa_flash_set_bwd_variant': [I],
     'pa_gemm_fp8_ok': [I, I, I, LL, LL, LL],
     'pa_gemm_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
@@ -70,7 +72,7 @@ _SIGS = {
 }
 
 _LL_RET = {'pa_bn_ws_floats'}
-_VOID_RET = {'pa_adamw_tune'}
+_VOID_RET = {'pa_adamw_tune', 'pa_act_fwd_tune', 'pa_act_cs_tune'}
 
 
 def _load():
