@@ -460,7 +460,7 @@ __global__ void splitk_reduce(const float* __restrict__ ws, uint16_t* __restrict
   store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(dst), v);
 }
 
-static int g_variant = 3;
+static int g_variant = 0;  // 0 = auto: the 8-phase kernel, schedule picked per operand layout
 
 template <bool AK, bool BKM, int EPI>
 static hipError_t launch(const void* A, const void* B, void* C, float* ws, const void* bias, int M, int N, int K,
@@ -499,6 +499,15 @@ static hipError_t dispatch(int transA, int transB, const void* A, const void* B,
 
 using namespace pa::gemm;
 
+// the 8-phase ping-pong kernel (csrc/gemm8.hip, its own translation unit so its register
+// allocation is not perturbed by this file's template instances)
+extern "C" int pa_gemm8_ok(int M, int N, int K, long long lda, long long ldb, long long ldc, int transA, int transB,
+                           int splitk);
+extern "C" int pa_gemm8_set_sched(int v);
+extern "C" int pa_gemm8_bf16(const void* A, const void* B, void* C, const void* bias, void* ws, int M, int N, int K,
+                             long long lda, long long ldb, long long ldc, int transA, int transB, float alpha,
+                             float beta, int splitk, hipStream_t st);
+
 // Shape contract (checked here; Python falls back to hipBLASLt when it does not hold):
 // K % (64 * splitk) == 0, N % 8 == 0, M % 8 == 0, leading dims % 8 == 0, 16-B aligned pointers.
 // splitk > 1 needs ws of splitk * M * N floats.
@@ -509,11 +518,14 @@ PA_API int pa_gemm_ok(int M, int N, int K, long long lda, long long ldb, long lo
 }
 
 // block layout (A/B benchmarking): 1 = 8 waves of 128x64, 2 = 4 waves of 128x128,
-// 3 = 8 waves with a 5-slot ring (160 KB LDS: three sub-tiles of DMA in flight; default:
-// +2-9 % over 1 on the GPT-3 shapes, profiles/hip_gemm_r1_v3.log)
+// 3 = 8 waves with a 5-slot ring (160 KB LDS: three sub-tiles of DMA in flight;
+// +2-9 % over 1 on the GPT-3 shapes, profiles/hip_gemm_r1_v3.log), 8 = the 8-phase ping-pong
+// kernel of csrc/gemm8.hip (row-half
+// staging), 9 = the same with k-half staging (balanced load segments)
 PA_API int pa_gemm_set_variant(int v) {
   const int old = g_variant;
   g_variant = v;
+  if (v >= 8) pa_gemm8_set_sched(v);
   return old;
 }
 
@@ -521,11 +533,20 @@ PA_API int pa_gemm_bf16(const void* A, const void* B, void* C, const void* bias,
                         long long lda, long long ldb, long long ldc, int transA, int transB, float alpha, float beta,
                         int splitk, hipStream_t st) {
   if (!pa_gemm_ok(M, N, K, lda, ldb, ldc, splitk)) return (int)hipErrorInvalidValue;
-  if (splitk == 1)
+  // auto: k-contiguous A -> schedule 11 (row-half staging keeps its DMA on full 128-B lines);
+  // m-contiguous A (weight gradients) -> schedule 9 (k-half staging, balanced load segments).
+  // Measured per layout on the GPT-3 1.3B shapes: profiles/r2_gemm_sched.log.
+  if (g_variant == 0) pa_gemm8_set_sched(transA == 0 ? 11 : 9);
+  const bool v8 = (g_variant == 0 || g_variant >= 8) && pa_gemm8_ok(M, N, K, lda, ldb, ldc, transA, transB, splitk);
+  if (splitk == 1) {
+    if (v8) return pa_gemm8_bf16(A, B, C, bias, nullptr, M, N, K, lda, ldb, ldc, transA, transB, alpha, beta, 1, st);
     return (int)dispatch<0>(transA, transB, A, B, C, nullptr, bias, M, N, K, lda, ldb, ldc, alpha, beta, 1, st);
+  }
   if (!ws) return (int)hipErrorInvalidValue;
-  hipError_t e = dispatch<1>(transA, transB, A, B, C, (float*)ws, nullptr, M, N, K, lda, ldb, ldc, 1.f, 0.f, splitk,
-                             st);
+  hipError_t e = v8 ? (hipError_t)pa_gemm8_bf16(A, B, C, nullptr, ws, M, N, K, lda, ldb, ldc, transA, transB, 1.f, 0.f,
+                                                splitk, st)
+                    : dispatch<1>(transA, transB, A, B, C, (float*)ws, nullptr, M, N, K, lda, ldb, ldc, 1.f, 0.f,
+                                  splitk, st);
   if (e != hipSuccess) return (int)e;
   const long long MN = (long long)M * N;
   splitk_reduce<<<(unsigned)((MN / 4 + 255) / 256), 256, 0, st>>>((const float*)ws, (uint16_t*)C,

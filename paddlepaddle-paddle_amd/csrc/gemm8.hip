@@ -1,0 +1,729 @@
+// Hand-written bf16 MFMA GEMM for gfx950, 8-phase ping-pong schedule (the main GEMM of the
+// training step: Linear forward, dgrad and weight gradient, the tied LM head).
+//
+// Reference semantics: paddle/phi/kernels/funcs/blas/blaslt_impl.cu.h (matmul),
+// fusion/gpu/fused_gemm_epilogue_kernel.cu (bias epilogue) and
+// fusion/gpu/fused_linear_param_grad_add_kernel.cu (W.grad += X^T dY, beta = 1 epilogue).
+//
+//   C[M,N] = alpha * op(A) @ op(B) (+ beta * C) (+ bias[N])
+//   AK: A stored [M][K] (k contiguous) else [K][M];  BK: B stored [N][K] else [K][N].
+//
+// CDNA4 structure (why it is shaped like this):
+//  * 256x256 block tile, K consumed 64 deep, 512 threads = 8 waves as 2 (M) x 4 (N); each wave
+//    owns 128x64 of C = 8x4 accumulators of v_mfma_f32_16x16x32_bf16 (128 acc VGPRs).
+//  * The two waves that share a SIMD (wave w and w+4) PING-PONG: waves 4-7 start one barrier
+//    late, so in every barrier interval one wave of each SIMD runs a 16-MFMA quadrant (256
+//    cycles of matrix pipe) while its partner issues the LDS reads / LDS-DMA for its next
+//    quadrant.  A K-tile is 8 intervals per wave: L0 M0 L1 M1 L2 M2 L3 M3 (L = load segment,
+//    M = 16 MFMAs on one 64x32 quadrant of the wave's 128x64).
+//  * Operands are staged HBM -> LDS by global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip),
+//    two K-tiles resident (2 x 64 KB).  Each wave group g stages the 128-row A half and the
+//    128-col B half with index g; tile t+2 is issued into tile t's buffer as soon as every
+//    reader of that half has retired its reads (B after L0 of both groups, A after L2), and
+//    retired with a COUNTED vmcnt(8) one K-tile later, so 8-12 barrier intervals of HBM/L2
+//    latency hide behind the matrix work.  The DMA is issued from inline asm (hipcc would
+//    otherwise drain it with vmcnt(0) at every ds_read).
+//  * Every layout is read as it sits in HBM: k-contiguous operands become [128][64] images
+//    read with ds_read_b128; m/n-contiguous operands become [64][128] images read with
+//    ds_read_b64_tr_b16 (hardware transpose).  Both images are XOR-swizzled on 16-B chunks
+//    (the swizzle is folded into the per-lane DMA SOURCE address, the DMA destination being
+//    lane-linear) and both read kinds are bank-conflict free (analysis at koff / moff).
+//  * Products are computed swapped (mfma(B, A) = C^T fragment) so each lane owns 4
+//    consecutive output columns (8-byte stores, 4-wide bias reads).
+//  * XCD-aware grouped tile order (blocks b and b+8 share an XCD L2).
+#include "common.h"
+
+namespace pa {
+namespace g8 {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int HALF = 128 * BK * 2;  // one 128-row (or 128-col) half of an operand tile: 16 KB
+constexpr int OPB = 2 * HALF;       // 32 KB
+constexpr int BUF = 2 * OPB;        // A + B of one K-tile: 64 KB
+constexpr int LDS_BYTES = 2 * BUF;  // two K-tiles resident: 128 KB
+
+__device__ __forceinline__ f32x4 mfma(s16x8 a, s16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+
+// K-major half image [128 rows][64 k], 128-B rows: chunk c (0..7) of row r at c ^ ((r >> 1) & 7).
+// A ds_read_b128 lane group ({0-3,12-15,20-27} etc.) holds rows {0-3,12-15} of one chunk and rows
+// {4-11} of the next (or the mirror); with this XOR the 16 (row, chunk) pairs cover the 16
+// distinct 16-B slots of the 256-B bank row: conflict free.
+__device__ __forceinline__ int koff(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+// MN-major half image [64 k][128 cols], 256-B rows: chunk c (0..15) of k-row r at c ^ hsw(r).
+// A tr-read 32-lane half touches k-rows {8g + q} (g in a pair, q = 0..3, + 4 for the second
+// read) at one aligned chunk pair; hsw maps those 8 rows to 8 distinct chunk pairs: conflict free.
+__device__ __forceinline__ int hsw(int r) { return ((r & 3) | (((r >> 3) & 1) << 2)) << 1; }
+__device__ __forceinline__ int moff(int r, int c) { return r * 256 + ((c ^ hsw(r)) << 4); }
+
+// Fragment of 16 rows (m or n) x 32 k (k-half kh of the 64-deep tile) for lane (g = lane>>4,
+// i = lane&15): element j = operand[row0 + i][32 kh + 8 g + j].
+template <bool KMAJ>
+__device__ __forceinline__ s16x8 frag(const char* img, int row0, int kh, int lane) {
+  const int g = lane >> 4;
+  if constexpr (KMAJ) {
+    return *reinterpret_cast<const s16x8*>(img + koff(row0 + (lane & 15), kh * 4 + g));
+  } else {
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    const int kr = kh * 32 + 8 * g + q;
+    const int ch = (row0 >> 3) + (p >> 1);
+    const int bi = (p & 1) * 8;
+    const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + moff(kr, ch) + bi));
+    const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + moff(kr + 4, ch) + bi));
+    return s16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  }
+}
+
+// Byte offset (from the operand base, K-tile 0 of this split) of the 16-B source chunk that
+// lane `lane` of wave-slot idx (0..15, 1 KB of the half image each) DMAs.  rc0 = first row
+// (K-major) / column (MN-major) of the half; rows / columns past lim are clamped (their
+// products land in C rows / columns that are never stored).
+template <bool KMAJ>
+__device__ __forceinline__ unsigned src_off(int idx, int lane, int rc0, int lim, long long ld, int k0) {
+  if constexpr (KMAJ) {
+    const int row = idx * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    const long long r = min(rc0 + row, lim - 1);
+    return (unsigned)((r * ld + k0 + c * 8) * 2);
+  } else {
+    const int row = idx * 4 + (lane >> 4);
+    const int c = (lane & 15) ^ hsw(row);
+    const long long col = min(rc0 + c * 8, lim - 8);  // lim % 8 == 0 (host check)
+    return (unsigned)(((long long)(k0 + row) * ld + col) * 2);
+  }
+}
+
+// One 16-B-per-lane LDS-DMA: global (saddr base + 32-bit lane offset) -> LDS (M0 base + lane*16).
+// Inline asm so hipcc does not count it (it would wait vmcnt(0) before every ds_read); the
+// queue is retired by hand with counted vmcnt (wait_vm).
+__device__ __forceinline__ void glds(const char* base, unsigned off, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(off), "s"(base), "s"(lds_dst)
+      : "memory");
+}
+
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Bijective XCD remap + grouped (GROUP_M tile rows per column sweep) tile order.
+__device__ __forceinline__ void tile_coords(int bid, int nwg, int tm, int tn, int& mt, int& nt) {
+  const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+  const int w = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+  constexpr int GROUP_M = 8;
+  const int per_group = GROUP_M * tn;
+  const int gidx = w / per_group;
+  const int first_m = gidx * GROUP_M;
+  const int gm = min(tm - first_m, GROUP_M);
+  const int in = w - gidx * per_group;
+  mt = first_m + in % gm;
+  nt = in / gm;
+}
+
+// Epilogue: lane owns C[mb + 16i + (lane&15)][nb + 16j + 4(lane>>4) + 0..3] (swapped products).
+template <int EPI>
+__device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __restrict__ C, float* __restrict__ ws,
+                                         const uint16_t* __restrict__ bias, int M, int N, long long ldc, float alpha,
+                                         float beta, int mb, int nb, int lane) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mb + i * 16 + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = nb + j * 16 + 4 * g;
+      if (n >= N) continue;  // N % 8 == 0: a 4-wide group is all in or all out
+      if constexpr (EPI == 1) {
+        *reinterpret_cast<f32x4*>(ws + (long long)blockIdx.z * M * N + (long long)m * N + n) = acc[i][j];
+      } else {
+        float v[4] = {acc[i][j][0] * alpha, acc[i][j][1] * alpha, acc[i][j][2] * alpha, acc[i][j][3] * alpha};
+        uint16_t* dst = C + (long long)m * ldc + n;
+        if (beta != 0.f) {
+          float o[4];
+          load_f<bf16_t, 4>(reinterpret_cast<const bf16_t*>(dst), o);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += beta * o[r];
+        }
+        if (bias) {
+          float bb[4];
+          load_f<bf16_t, 4>(reinterpret_cast<const bf16_t*>(bias + n), bb);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += bb[r];
+        }
+        store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(dst), v);
+      }
+    }
+  }
+}
+
+// EPI 0: bf16 C = alpha*acc (+ beta*C) (+ bias);  EPI 1: raw fp32 split-K slab (ws[z][M][N]).
+template <bool AK, bool BKM, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm8_kernel(const char* __restrict__ A, const char* __restrict__ B,
+                                                       uint16_t* __restrict__ C, float* __restrict__ ws,
+                                                       const uint16_t* __restrict__ bias, int M, int N, int K,
+                                                       long long lda, long long ldb, long long ldc, float alpha,
+                                                       float beta, int ksplit) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
+  const int wr = wave >> 2, wc = wave & 3, wq = wave & 3;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  int mt, ntile;
+  tile_coords(blockIdx.x, tm * tn, tm, tn, mt, ntile);
+  const int m0 = mt * BM, n0 = ntile * BN;
+  const int kbeg = blockIdx.z * ksplit;
+  const int nt = ksplit / BK;
+
+  // this wave's DMA slots: 4 KB of A half `wr` and 4 KB of B half `wr` per K-tile
+  unsigned offA[4], offB[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    offA[u] = src_off<AK>(wq * 4 + u, lane, m0 + wr * 128, M, lda, kbeg);
+    offB[u] = src_off<BKM>(wq * 4 + u, lane, n0 + wr * 128, N, ldb, kbeg);
+  }
+  const long long kstepA = AK ? BK * 2 : (long long)BK * lda * 2;
+  const long long kstepB = BKM ? BK * 2 : (long long)BK * ldb * 2;
+  const unsigned lds0 = (unsigned)(size_t)(lds_void*)smem;
+  const unsigned dstA = lds0 + wr * HALF + wq * 4096;
+  const unsigned dstB = lds0 + OPB + wr * HALF + wq * 4096;
+
+  auto stageA = [&](int t) {
+    const char* base = A + (long long)t * kstepA;
+    const unsigned d = dstA + (t & 1) * BUF;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) glds(base, offA[u], d + u * 1024);
+  };
+  auto stageB = [&](int t) {
+    const char* base = B + (long long)t * kstepB;
+    const unsigned d = dstB + (t & 1) * BUF;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) glds(base, offB[u], d + u * 1024);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: K-tiles 0 and 1 in flight; retire tile 0 (all waves) before the first reads
+  stageB(0);
+  stageA(0);
+  if (nt > 1) {
+    stageB(1);
+    stageA(1);
+    wait_vm<8>();
+  } else {
+    wait_vm<0>();
+  }
+  bar();
+  if (wr == 1) bar();  // stagger: waves 4-7 run one interval behind waves 0-3
+
+  const int bcol = (wc & 1) * 64;  // this wave's columns inside its B half
+  s16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  for (int t = 0; t < nt; ++t) {
+    const char* ia = smem + (t & 1) * BUF + wr * HALF;
+    const char* ib = smem + (t & 1) * BUF + OPB + (wc >> 1) * HALF;
+    const bool more = t + 2 < nt;
+    // L0: A rows 0-63 of the wave, all 64 B columns
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        fb0[j][kh] = frag<BKM>(ib, bcol + j * 16, kh, lane);
+        fb1[j][kh] = frag<BKM>(ib, bcol + 32 + j * 16, kh, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i][kh] = frag<AK>(ia, i * 16, kh, lane);
+    }
+    bar();
+    // M0: quadrant (A 0-63, B 0-31)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(fb0[j][kh], fa[i][kh], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // L1: group 1 restages B half 1 (every reader retired its L0 reads two barriers ago)
+    if (wr == 1 && more) stageB(t + 2);
+    bar();
+    // M1: quadrant (A 0-63, B 32-63)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma(fb1[j][kh], fa[i][kh], acc[i][2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // L2: A rows 64-127; group 0 restages B half 0
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i][kh] = frag<AK>(ia, 64 + i * 16, kh, lane);
+    if (wr == 0 && more) stageB(t + 2);
+    bar();
+    // M2: quadrant (A 64-127, B 32-63)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma(fb1[j][kh], fa[i][kh], acc[4 + i][2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // L3: restage this group's A half; group 1 retires K-tile t+1 before group 0 reads it
+    if (more) stageA(t + 2);
+    if (wr == 1) {
+      if (more) wait_vm<8>();
+      else wait_vm<0>();
+    }
+    bar();
+    // M3: quadrant (A 64-127, B 0-31); group 0 retires K-tile t+1
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma(fb0[j][kh], fa[i][kh], acc[4 + i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    if (wr == 0) {
+      if (more) wait_vm<8>();
+      else wait_vm<0>();
+    }
+    bar();
+  }
+  if (wr == 0) bar();  // match group 1's barrier count
+
+  epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Schedule 9: the same ping-pong, but every K-tile image is split by K HALF (k 0-31 / 32-63)
+// instead of by row half, and a phase is (A 64-row sub-tile) x (all 64 B columns) x (one k half):
+//   L0: A sub0 k0 (4 frags) + B k0 (4 frags)   M0: acc[0..3][*]
+//   L1: A sub1 k0                              M1: acc[4..7][*]
+//   L2: A sub0 k1 + B k1                       M2: acc[0..3][*]
+//   L3: A sub1 k1                              M3: acc[4..7][*]
+// so every load segment carries either 8 fragment reads or 4 reads + 4 LDS-DMA (schedule 8's
+// first segment carried 16 reads: 64 KB per CU in one 256-cycle interval = the LDS peak), only
+// 32 fragment VGPRs are live, and a k-half image is free for re-staging as soon as its last
+// readers retire (B k0 after L0, A k0 after L1, ...).  Waves 0-3 stage A (k0 in L3, k1 in L1 of
+// the next tile), waves 4-7 stage B (k0 in L1, k1 in L3); every stage is retired with a counted
+// vmcnt 9-12 barrier intervals after issue.  Images: K-major [256][32] (64-B rows),
+// MN-major [32][256] (512-B rows), both swizzled conflict free for their read kind.
+constexpr int KH = 256 * 32 * 2;  // one k-half image: 16 KB
+// K-major [256 rows][32 k]: chunk ch (0..3) of row r at ch ^ (((r >> 3) & 1) << 1)
+__device__ __forceinline__ int k9off(int r, int ch) { return r * 64 + ((ch ^ (((r >> 3) & 1) << 1)) << 4); }
+// MN-major [32 k][256 cols]: chunk ch (0..31) of k-row r at ch ^ hsw(r)
+__device__ __forceinline__ int m9off(int r, int ch) { return r * 512 + ((ch ^ hsw(r)) << 4); }
+
+template <bool KMAJ>
+__device__ __forceinline__ s16x8 frag9(const char* img, int row0, int lane) {
+  const int g = lane >> 4;
+  if constexpr (KMAJ) {
+    return *reinterpret_cast<const s16x8*>(img + k9off(row0 + (lane & 15), g));
+  } else {
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    const int kr = 8 * g + q;
+    const int ch = (row0 >> 3) + (p >> 1);
+    const int bi = (p & 1) * 8;
+    const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + m9off(kr, ch) + bi));
+    const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + m9off(kr + 4, ch) + bi));
+    return s16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  }
+}
+
+// source byte offset (k-half 0 of K-tile 0 of this split) for lane `lane` of wave-slot idx (0..15)
+template <bool KMAJ>
+__device__ __forceinline__ unsigned src9(int idx, int lane, int rc0, int lim, long long ld, int k0) {
+  if constexpr (KMAJ) {
+    const int row = idx * 16 + (lane >> 2);
+    const int ch = (lane & 3) ^ (((row >> 3) & 1) << 1);
+    const long long r = min(rc0 + row, lim - 1);
+    return (unsigned)((r * ld + k0 + ch * 8) * 2);
+  } else {
+    const int row = idx * 2 + (lane >> 5);
+    const int ch = (lane & 31) ^ hsw(row);
+    const long long col = min(rc0 + ch * 8, lim - 8);
+    return (unsigned)(((long long)(k0 + row) * ld + col) * 2);
+  }
+}
+
+__device__ __forceinline__ void wait_vm_n(int n) {  // n in {0, 4, 8, 12}, wave-uniform
+  if (n >= 12) wait_vm<12>();
+  else if (n >= 8) wait_vm<8>();
+  else if (n >= 4) wait_vm<4>();
+  else wait_vm<0>();
+}
+
+template <bool AK, bool BKM, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm9_kernel(const char* __restrict__ A, const char* __restrict__ B,
+                                                       uint16_t* __restrict__ C, float* __restrict__ ws,
+                                                       const uint16_t* __restrict__ bias, int M, int N, int K,
+                                                       long long lda, long long ldb, long long ldc, float alpha,
+                                                       float beta, int ksplit) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3, wq = wave & 3;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  int mt, ntile;
+  tile_coords(blockIdx.x, tm * tn, tm, tn, mt, ntile);
+  const int m0 = mt * BM, n0 = ntile * BN;
+  const int kbeg = blockIdx.z * ksplit;
+  const int nt = ksplit / BK;
+
+  // waves 0-3 stage A, waves 4-7 stage B: 4 x 1 KB of a k-half image each per stage
+  const bool isA = wr == 0;
+  const bool km = isA ? AK : BKM;
+  const long long ld = isA ? lda : ldb;
+  const char* opnd = isA ? A : B;
+  unsigned off[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    off[u] = isA ? src9<AK>(wq * 4 + u, lane, m0, M, lda, kbeg) : src9<BKM>(wq * 4 + u, lane, n0, N, ldb, kbeg);
+  const long long kstep = km ? BK * 2 : (long long)BK * ld * 2;    // bytes per K-tile
+  const long long khstep = km ? 32 * 2 : (long long)32 * ld * 2;   // bytes to k-half 1
+  const unsigned lds0 = (unsigned)(size_t)(lds_void*)smem;
+  // buffer layout: [A k0][A k1][B k0][B k1]
+  const unsigned dst0 = lds0 + (isA ? 0 : 2 * KH) + wq * 4096;
+  auto stage = [&](int t, int kh) {
+    const char* base = opnd + (long long)t * kstep + kh * khstep;
+    const unsigned d = dst0 + (t & 1) * BUF + kh * KH;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) glds(base, off[u], d + u * 1024);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue, in the steady-state issue order (A: k0(t+2) in L3(t), k1(t+1) in L1(t);
+  // B: k0(t+2) in L1(t), k1(t+2) in L3(t))
+  const int more1 = nt > 1;
+  if (isA) {
+    stage(0, 0);
+    stage(0, 1);
+    if (more1) stage(1, 0);
+    wait_vm_n(4 + 4 * more1);  // A k0(0) landed
+  } else {
+    stage(0, 0);
+    stage(0, 1);
+    if (more1) {
+      stage(1, 0);
+      stage(1, 1);
+    }
+    wait_vm_n(4 + 8 * more1);  // B k0(0) landed
+  }
+  bar();
+  if (wr == 1) bar();  // stagger: waves 4-7 run one interval behind waves 0-3
+
+  s16x8 fa[4], fb[4];
+  const int arow = wr * 128, bcol = wc * 64;
+  for (int t = 0; t < nt; ++t) {
+    const char* buf = smem + (t & 1) * BUF;
+    const int m1 = t + 1 < nt, m2 = t + 2 < nt;
+    // L0: A sub0 k0, B k0
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = frag9<BKM>(buf + 2 * KH, bcol + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = frag9<AK>(buf, arow + i * 16, lane);
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fb[j], fa[i], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // L1: A sub1 k0; A waves stage A k1(t+1), B waves stage B k0(t+2); B waves retire B k1(t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = frag9<AK>(buf, arow + 64 + i * 16, lane);
+    if (isA) {
+      if (m1) stage(t + 1, 1);
+    } else {
+      if (m2) stage(t + 2, 0);
+      wait_vm_n(8 * m1 + 4 * m2);
+    }
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[4 + i][j] = mfma(fb[j], fa[i], acc[4 + i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    if (isA) wait_vm_n(8 * m1);  // A k1(t) landed
+    bar();
+    // L2: A sub0 k1, B k1
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = frag9<BKM>(buf + 3 * KH, bcol + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = frag9<AK>(buf + KH, arow + i * 16, lane);
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fb[j], fa[i], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // L3: A sub1 k1; A waves stage A k0(t+2), B waves stage B k1(t+2); B waves retire B k0(t+1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = frag9<AK>(buf + KH, arow + 64 + i * 16, lane);
+    if (m2) stage(t + 2, isA ? 0 : 1);
+    if (!isA) wait_vm_n(4 * m1 + 8 * m2);
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[4 + i][j] = mfma(fb[j], fa[i], acc[4 + i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    if (isA) wait_vm_n(4 * m1 + 4 * m2);  // A k0(t+1) landed
+    bar();
+  }
+  if (wr == 0) bar();  // match waves 4-7's barrier count
+
+  epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Schedule 11: schedule 8's images (row halves, full 128-B lines for k-contiguous operands) with
+// 32 MFMAs per segment instead of 16, halving the barriers per K-tile (4 per wave):
+//   L0: A sub0 (4 frags x 2 k halves) + B (4 frags x 2 k halves)   M0: acc[0..3][*]  (32 MFMA)
+//   L1: A sub1                                                      M1: acc[4..7][*]  (32 MFMA)
+// Staging (tile t in buffer t&1): waves 0-3 issue A half 0 + B half 0 of tile t+1 in L0(t) and
+// retire them (vmcnt) at the end of M1(t); waves 4-7 issue A half 1 of tile t+1 in L0(t) and
+// B half 1 of tile t+2 in L1(t), retiring B half 1 of t+1 before the barrier that opens L0(t+1)
+// of waves 0-3 and A half 1 of t+1 at the end of their M1(t).
+template <bool AK, bool BKM, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm11_kernel(const char* __restrict__ A, const char* __restrict__ B,
+                                                        uint16_t* __restrict__ C, float* __restrict__ ws,
+                                                        const uint16_t* __restrict__ bias, int M, int N, int K,
+                                                        long long lda, long long ldb, long long ldc, float alpha,
+                                                        float beta, int ksplit) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3, wq = wave & 3;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  int mt, ntile;
+  tile_coords(blockIdx.x, tm * tn, tm, tn, mt, ntile);
+  const int m0 = mt * BM, n0 = ntile * BN;
+  const int kbeg = blockIdx.z * ksplit;
+  const int nt = ksplit / BK;
+
+  unsigned offA[4], offB[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    offA[u] = src_off<AK>(wq * 4 + u, lane, m0 + wr * 128, M, lda, kbeg);
+    offB[u] = src_off<BKM>(wq * 4 + u, lane, n0 + wr * 128, N, ldb, kbeg);
+  }
+  const long long kstepA = AK ? BK * 2 : (long long)BK * lda * 2;
+  const long long kstepB = BKM ? BK * 2 : (long long)BK * ldb * 2;
+  const unsigned lds0 = (unsigned)(size_t)(lds_void*)smem;
+  const unsigned dstA = lds0 + wr * HALF + wq * 4096;
+  const unsigned dstB = lds0 + OPB + wr * HALF + wq * 4096;
+  auto stageA = [&](int t) {
+    const char* base = A + (long long)t * kstepA;
+    const unsigned d = dstA + (t & 1) * BUF;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) glds(base, offA[u], d + u * 1024);
+  };
+  auto stageB = [&](int t) {
+    const char* base = B + (long long)t * kstepB;
+    const unsigned d = dstB + (t & 1) * BUF;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) glds(base, offB[u], d + u * 1024);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue in the steady-state issue order
+  if (wr == 0) {
+    stageA(0);
+    stageB(0);
+    wait_vm<0>();
+  } else {
+    stageB(0);
+    stageA(0);
+    if (nt > 1) {
+      stageB(1);
+      wait_vm<4>();
+    } else {
+      wait_vm<0>();
+    }
+  }
+  bar();
+  if (wr == 1) bar();  // stagger: waves 4-7 run one interval behind waves 0-3
+
+  const int bcol = (wc & 1) * 64;
+  s16x8 fa[4][2], fb[4][2];
+  for (int t = 0; t < nt; ++t) {
+    const char* ia = smem + (t & 1) * BUF + wr * HALF;
+    const char* ib = smem + (t & 1) * BUF + OPB + (wc >> 1) * HALF;
+    const int m1 = t + 1 < nt, m2 = t + 2 < nt;
+    // L0
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j][kh] = frag<BKM>(ib, bcol + j * 16, kh, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i][kh] = frag<AK>(ia, i * 16, kh, lane);
+    }
+    if (m1) {
+      stageA(t + 1);
+      if (wr == 0) stageB(t + 1);
+    }
+    bar();
+    // M0
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fb[j][kh], fa[i][kh], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // L1
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i][kh] = frag<AK>(ia, 64 + i * 16, kh, lane);
+    if (wr == 1) {
+      if (m2) stageB(t + 2);
+      // B half 1 of tile t+1 (issued in L1(t-1)) must land before L0(t+1) of waves 0-3
+      if (m2) wait_vm<8>();
+      else if (m1) wait_vm<4>();
+      else wait_vm<0>();
+    }
+    bar();
+    // M1
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[4 + i][j] = mfma(fb[j][kh], fa[i][kh], acc[4 + i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    if (wr == 0) wait_vm<0>();  // A half 0 + B half 0 of tile t+1
+    else if (m2) wait_vm<4>();  // A half 1 of tile t+1 (B half 1 of t+2 stays in flight)
+    else wait_vm<0>();
+    bar();
+  }
+  if (wr == 0) bar();
+
+  epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
+}
+
+static int g_sched = 9;
+
+template <bool AK, bool BKM, int EPI>
+static hipError_t launch(const void* A, const void* B, void* C, float* ws, const void* bias, int M, int N, int K,
+                         long long lda, long long ldb, long long ldc, float alpha, float beta, int splitk,
+                         hipStream_t st) {
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  dim3 grid(tm * tn, 1, splitk);
+  if (g_sched == 11)
+    gemm11_kernel<AK, BKM, EPI><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
+                                                      (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
+                                                      K / splitk);
+  else if (g_sched == 9)
+    gemm9_kernel<AK, BKM, EPI><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
+                                                     (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
+                                                     K / splitk);
+  else
+    gemm8_kernel<AK, BKM, EPI><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
+                                                     (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
+                                                     K / splitk);
+  return hipGetLastError();
+}
+
+template <int EPI>
+static hipError_t dispatch(int transA, int transB, const void* A, const void* B, void* C, float* ws, const void* bias,
+                           int M, int N, int K, long long lda, long long ldb, long long ldc, float alpha, float beta,
+                           int splitk, hipStream_t st) {
+  const bool ak = transA == 0, bk = transB != 0;
+  if (ak && bk) return launch<true, true, EPI>(A, B, C, ws, bias, M, N, K, lda, ldb, ldc, alpha, beta, splitk, st);
+  if (ak && !bk) return launch<true, false, EPI>(A, B, C, ws, bias, M, N, K, lda, ldb, ldc, alpha, beta, splitk, st);
+  if (!ak && bk) return launch<false, true, EPI>(A, B, C, ws, bias, M, N, K, lda, ldb, ldc, alpha, beta, splitk, st);
+  return launch<false, false, EPI>(A, B, C, ws, bias, M, N, K, lda, ldb, ldc, alpha, beta, splitk, st);
+}
+
+}  // namespace g8
+}  // namespace pa
+
+// Operand byte span as addressed by the kernel's 32-bit DMA offsets must stay below 4 GiB.
+static bool span_ok(int transX, int rows, int K, long long ld) {
+  const long long span = transX == 0 ? ((long long)rows * ld) * 2 : ((long long)K * ld) * 2;
+  return span < (1LL << 32);
+}
+
+// Contract: K % (64 * splitk) == 0, M, N, lda, ldb, ldc % 8 == 0, 16-B aligned operands, operand
+// spans < 4 GiB.  Returns hipErrorInvalidValue when the shape is outside it (caller falls back).
+PA_API int pa_gemm8_ok(int M, int N, int K, long long lda, long long ldb, long long ldc, int transA, int transB,
+                       int splitk) {
+  if (M <= 0 || N <= 0 || K <= 0 || splitk < 1) return 0;
+  if (K % (64 * splitk) != 0 || M % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8) return 0;
+  // A: transA==0 -> [M][lda]; else [K][lda].  B: transB!=0 -> [N][ldb]; else [K][ldb]
+  if (!span_ok(transA, M, K, lda)) return 0;
+  if (!span_ok(transB != 0 ? 0 : 1, N, K, ldb)) return 0;
+  return 1;
+}
+
+PA_API int pa_gemm8_bf16(const void* A, const void* B, void* C, const void* bias, void* ws, int M, int N, int K,
+                         long long lda, long long ldb, long long ldc, int transA, int transB, float alpha, float beta,
+                         int splitk, hipStream_t st) {
+  using namespace pa::g8;
+  if (!pa_gemm8_ok(M, N, K, lda, ldb, ldc, transA, transB, splitk)) return (int)hipErrorInvalidValue;
+  if (splitk == 1)
+    return (int)dispatch<0>(transA, transB, A, B, C, nullptr, bias, M, N, K, lda, ldb, ldc, alpha, beta, 1, st);
+  if (!ws) return (int)hipErrorInvalidValue;
+  return (int)dispatch<1>(transA, transB, A, B, C, (float*)ws, nullptr, M, N, K, lda, ldb, ldc, 1.f, 0.f, splitk, st);
+}
+
+// schedule select (A/B benchmarking): 8 = row-half staging, 9 = k-half staging (default),
+// 11 = row-half staging with 32-MFMA segments
+PA_API int pa_gemm8_set_sched(int v) {
+  const int old = pa::g8::g_sched;
+  pa::g8::g_sched = v;
+  return old;
+}

@@ -6,13 +6,13 @@ decoder blocks, fused QKV projection, GeLU MLP (4h), tied input/output embedding
 
 MI355X mapping (per decoder block):
   add+LayerNorm         → one HIP kernel (csrc/norm.hip, residual fused, fp32 stats)
-  QKV / out / fc1 / fc2 → hipBLASLt GEMMs with fused bias epilogue (addmm)
+  QKV / out / fc1 / fc2 → hand-written 8-phase MFMA GEMMs (csrc/gemm8.hip), bias fused in the epilogue
   attention             → csrc/flash_attn.hip on strided q/k/v views of the QKV output
                           (no transposes, no S×S matrix)
   GeLU (+ fc1 bias)     → csrc/act.hip; backward writes dx and reduces the bias grad in one pass
   dropout + residual + LayerNorm (+ out-proj bias) → ONE csrc/norm.hip kernel each way
                           (mask regenerated in backward from a counter hash)
-  LM head + loss        → GEMM + csrc/softmax_xent.hip (grad written in place of logits)
+  LM head + loss        → hand-written GEMMs (tied, E.grad accumulated in place) + csrc/softmax_xent.hip
 """
 import math
 from dataclasses import dataclass
@@ -207,7 +207,11 @@ class GPTForPretraining(nn.Layer):
     def forward(self, input_ids, position_ids=None):
         h = self.gpt(input_ids, position_ids)
         w = self.gpt.embeddings.word_embeddings.weight
-        return _wrap(torch.matmul(_unwrap(h), _unwrap(w).t()))  # tied LM head
+        t = _unwrap(h)
+        if t.is_cuda and ops.use_hip(t) and t.dtype == torch.bfloat16 and _unwrap(w).dtype == torch.bfloat16:
+            from ..ops.linear import tied_head  # hand-written GEMMs, in-place E.grad accumulate
+            return _wrap(tied_head(t, w))
+        return _wrap(torch.matmul(t, _unwrap(w).t()))  # tied LM head
 
     def loss(self, logits, labels):
         lg = _unwrap(logits)

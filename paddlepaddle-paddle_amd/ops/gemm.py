@@ -1,7 +1,8 @@
 """GEMM entry points.
 
-Plain bf16/fp16 GEMMs go to hipBLASLt through the storage layer (measured 1.2–1.4 PF/s
-bf16 at LLM shapes on MI355X — the library path the design brief allows for plain GEMMs).
+bf16 GEMMs of the training step (Linear forward / dgrad / weight gradient, the tied LM head)
+run on the hand-written 8-phase ping-pong MFMA kernel (csrc/gemm8.hip via ``hip_mm``); shapes
+outside its contract (K % 64, odd leading dims, fp32/fp16) go to the library through torch.
 FP8 (OCP e4m3fn / e5m2, CDNA4 — NOT the MI300 fnuz encoding) runs on the hand-written
 block-scaled MFMA kernel (``hip_fp8_mm``, 2x the bf16 MFMA rate) with per-tensor scales;
 ``torch._scaled_mm`` only for layouts that kernel does not take.
@@ -71,26 +72,50 @@ def hip_mm(a, b, out=None, bias=None, alpha=1.0, beta=0.0, splitk=1):
     return out
 
 
-_hip_wgrad = os.environ.get('PADDLE_AMD_HIP_GEMM', '1') != '0'
+_hip_gemm = os.environ.get('PADDLE_AMD_HIP_GEMM', '1') != '0'
+
+
+def _splitk_for(M, N_, K):
+    """Split-K factor for outputs with too few 256x256 tiles to fill 256 CUs (the 2048x2048
+    out-projection weight gradient: 64 tiles x 4 slices, profiles/r2_gemm_sched.log)."""
+    tiles = -(-M // 256) * -(-N_ // 256)
+    if tiles >= 128:
+        return 1
+    for s in (4, 2):
+        if K % (64 * s) == 0 and K // s >= 2048:
+            return s
+    return 1
+
+
+def mm(a, b, out=None, bias=None, beta=0.0):
+    """out = a @ b (+ beta*out) (+ bias) on the hand-written kernel when the operands fit its
+    contract, else on the library (torch).  a: [M,K], b: [K,N] (either may be a transposed view)."""
+    if _hip_gemm and a.is_cuda and hip_mm_ok(a, b, 1) and (bias is None or (
+            bias.dtype == torch.bfloat16 and bias.is_contiguous())) and (out is None or (
+            out.dtype == torch.bfloat16 and out.stride(1) == 1)):
+        sk = _splitk_for(a.shape[0], b.shape[1], a.shape[1]) if bias is None else 1
+        if sk > 1 and not hip_mm_ok(a, b, sk):
+            sk = 1
+        return hip_mm(a, b, out=out, bias=bias, beta=beta if out is not None else 0.0, splitk=sk)
+    if out is None:
+        return torch.addmm(bias, a, b) if bias is not None else torch.mm(a, b)
+    if beta == 0.0:
+        torch.mm(a, b, out=out)
+    else:
+        out.addmm_(a, b, beta=beta)
+    if bias is not None:
+        out.add_(bias)
+    return out
 
 
 def wgrad_accumulate(x2, dy2, gw):
-    """gw[in, out] += x2^T @ dy2 (x2: [tokens, in], dy2: [tokens, out]) — the weight-gradient GEMM.
-
-    Runs on the hand-written MFMA kernel (both operands staged as they sit in HBM and read
-    with ds_read_b64_tr_b16) when the output has enough 256x256 tiles to fill the chip
-    (>= 192: it is ahead of hipBLASLt on the GPT-3 1.3B qkv / fc1 / fc2 weight gradients,
-    tools/hip_gemm_bench.py).  Smaller outputs would need split-K, whose fp32 slabs cost more
-    in the training step than they win in isolation, so those stay on the library.
-    Returns False when the caller should use the library.
-    """
-    if not _hip_wgrad or gw.dtype != torch.bfloat16 or not gw.is_contiguous():
+    """gw[in, out] += x2^T @ dy2 (x2: [tokens, in], dy2: [tokens, out]) — the weight-gradient GEMM
+    on the hand-written kernel (both operands m/n-contiguous: k-half staged images read with
+    ds_read_b64_tr_b16, beta = 1 epilogue accumulating in place; split-K for small outputs).
+    Returns False when the caller should use the library."""
+    if not _hip_gemm or gw.dtype != torch.bfloat16 or not gw.is_contiguous() or not hip_mm_ok(x2.t(), dy2, 1):
         return False
-    a, b = x2.t(), dy2
-    M, N_ = gw.shape
-    if -(-M // 256) * -(-N_ // 256) < 192 or not hip_mm_ok(a, b, 1):
-        return False
-    hip_mm(a, b, out=gw, beta=1.0, splitk=1)
+    mm(x2.t(), dy2, out=gw, beta=1.0)
     return True
 
 

@@ -1,9 +1,11 @@
 """Linear with the weight gradient accumulated IN PLACE into the flat gradient buffer.
 
 y = x @ W + b (W: [in, out], paddle layout; with many tokens the GEMM reads a transient K-major
-copy W^T from ops.gemm.kmajor_weight, the operand layout hipBLASLt runs fastest).  Backward:
-  dX = dY @ W^T                                (hipBLASLt)
-  W.grad += X^T @ dY                           (hand-written MFMA GEMM csrc/gemm.hip, beta = 1 epilogue)
+copy W^T from ops.gemm.kmajor_weight: both operands k-contiguous is the hand-written kernel's
+fastest layout).  Every GEMM runs on the hand-written 8-phase MFMA kernel (csrc/gemm8.hip):
+  y = X @ W + b                                (bias fused in the epilogue)
+  dX = dY @ W^T                                (W read as it sits: k-contiguous)
+  W.grad += X^T @ dY                           (beta = 1 epilogue, in place; split-K for small W)
   b.grad += colsum(dY)                         (csrc/act.hip pa_colsum, in place)
 so no per-parameter gradient temporary is allocated and no separate accumulate/add kernel
 runs (AccumulateGrad is bypassed; the DP/sharding engines are told the gradient is ready
@@ -24,9 +26,9 @@ class _LinearAccum(torch.autograd.Function):
         if w.untyped_storage().nbytes() == 0:
             raise RuntimeError("linear weight storage is released (sharding stage-3 unit not gathered)")
         x2 = x.reshape(-1, x.shape[-1])
-        wt = gemm.kmajor_weight(x2, w)  # K-major copy for the library's fast layout (transient)
+        wt = gemm.kmajor_weight(x2, w)  # transient K-major copy (the kernel's fastest layout)
         wf = w if wt is None else wt.t()
-        y = torch.addmm(b, x2, wf) if b is not None else torch.mm(x2, wf)
+        y = gemm.mm(x2, wf, bias=b)
         ctx.save_for_backward(x2, w)
         ctx.box, ctx.xshape = box, x.shape
         return y.reshape(*x.shape[:-1], w.shape[1])
@@ -36,7 +38,7 @@ class _LinearAccum(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         wp, bp = ctx.box
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dx = torch.mm(dy2, w.t()).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dx = gemm.mm(dy2, w.t()).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
         gw = flat_grad_slot(wp)
         if gw is not None:
             if not gemm.wgrad_accumulate(x2, dy2, gw):
@@ -44,7 +46,7 @@ class _LinearAccum(torch.autograd.Function):
             notify_grad_ready(wp)
             dw = None
         else:
-            dw = torch.mm(x2.t(), dy2)
+            dw = gemm.mm(x2.t(), dy2)
         db = None
         if bp is not None:
             gb = flat_grad_slot(bp)
@@ -71,3 +73,33 @@ def linear_accum(x, wparam, bparam):
 
 def eligible(w):
     return w._t.requires_grad and torch.is_grad_enabled() and flat_grad_slot(w) is not None
+
+
+class _TiedHead(torch.autograd.Function):
+    """logits = h @ E^T for a tied [vocab, hidden] embedding E (GPT LM head), all three GEMMs on
+    the hand-written kernel; E.grad accumulates in place in its flat slot (beta = 1 epilogue),
+    the embedding gather's own contribution is added by autograd afterwards."""
+
+    @staticmethod
+    def forward(ctx, h, w, box):
+        h2 = h.reshape(-1, h.shape[-1])
+        y = gemm.mm(h2, w.t())
+        ctx.save_for_backward(h2, w)
+        ctx.box, ctx.hshape = box, h.shape
+        return y.reshape(*h.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dl):
+        h2, w = ctx.saved_tensors
+        dl2 = dl.reshape(-1, dl.shape[-1])
+        dh = gemm.mm(dl2, w).reshape(ctx.hshape) if ctx.needs_input_grad[0] else None
+        gw = flat_grad_slot(ctx.box)
+        if gw is not None and gemm.wgrad_accumulate(dl2, h2, gw):
+            notify_grad_ready(ctx.box)
+            return dh, None, None
+        return dh, gemm.mm(dl2.t(), h2), None
+
+
+def tied_head(h, wparam):
+    """h: torch [.., hidden]; wparam: the tied embedding Parameter [vocab, hidden]."""
+    return _TiedHead.apply(h, wparam._t, wparam)

@@ -38,6 +38,22 @@ def main(path, marker, nsteps, top=30):
     print("top kernels (ms/step, calls/step, avg us):")
     for n, (t, c) in sorted(per.items(), key=lambda kv: -kv[1][0])[:top]:
         print(f"  {t / nsteps:7.2f} {c / nsteps:6.1f} {1e3 * t / c:8.1f}  {n[:100]}")
+    # GEMMs split by launch grid (one row per distinct shape)
+    def grid(r):
+        g = [r.get(k) for k in ('Grid_Size_X', 'Grid_Size_Y', 'Grid_Size_Z') if r.get(k)]
+        return 'x'.join(g) if g else r.get('Grid_Size', '?')
+    shp = {}
+    for r in sel:
+        if 'gemm' not in r['Kernel_Name'] and 'Cijk' not in r['Kernel_Name']:
+            continue
+        k = (r['Kernel_Name'][:60], grid(r))
+        d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6
+        t, c = shp.get(k, (0.0, 0))
+        shp[k] = (t + d, c + 1)
+    if shp:
+        print("GEMM kernels by launch grid (ms/step, calls/step, avg us, grid):")
+        for (n, g), (t, c) in sorted(shp.items(), key=lambda kv: -kv[1][0]):
+            print(f"  {t / nsteps:7.2f} {c / nsteps:6.1f} {1e3 * t / c:8.1f}  {g:>14s}  {n}")
 
 
 if __name__ == '__main__':
