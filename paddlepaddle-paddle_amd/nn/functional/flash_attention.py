@@ -75,8 +75,10 @@ def flash_attention(query, key, value, dropout=0.0, causal=False, return_softmax
 
 def flash_attn_qkvpacked(qkv, dropout=0.0, causal=False, return_softmax=False, *, fixed_seed_offset=None,
                          rng_name="", training=True, name=None):
-    t = _u(qkv)  # [b, s, 3, h, d] (reference packs as [b, s, nheads/nheads_k + 2, nheads_k, d])
-    q, k, v = t[:, :, 0], t[:, :, 1], t[:, :, 2]
+    t = _u(qkv)  # [b, s, nheads/nheads_k + 2, nheads_k, d]: groups of query heads, then k, then v
+    b, s = t.shape[0], t.shape[1]
+    q = t[:, :, :-2].reshape(b, s, -1, t.shape[-1])
+    k, v = t[:, :, -2], t[:, :, -1]
     if (t.dim() == 5 and t.shape[2] == 3 and not return_softmax and (dropout == 0.0 or not training)
             and ops.use_hip(t) and ops.flash_attn.supported(q, k, v)):
         return _w(ops.flash_attn.flash_attention_packed(t, causal)), None

@@ -59,8 +59,8 @@ def cross_entropy(input, label, weight=None, ignore_index=-100, reduction='mean'
         loss = TF.cross_entropy(lg.float(), lab.reshape(-1), w, ignore_index=ignore_index, reduction='none',
                                 label_smoothing=label_smoothing)
     loss = loss.reshape(lab.shape)
-    if reduction == 'none':
-        return _w(loss.unsqueeze(-1).to(logits.dtype))
+    if reduction == 'none':  # label-shaped: the class axis kept as a unit dim at `axis`
+        return _w(loss.unsqueeze(axis).to(logits.dtype))
     if reduction == 'sum':
         return _w(loss.sum())
     if w is not None:

@@ -307,3 +307,30 @@ def set_program_state(program, state_dict):
             src = v._t if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))
             with torch.no_grad():
                 p._t.copy_(src.to(p._t.device, p._t.dtype))
+
+
+# ----------------------------------------------------------------- paddle.load fallbacks
+def load_binary_object(data):
+    """paddle.load of a non-pickle file: a serialized Program (returns it) or None."""
+    try:
+        return deserialize_program(data)
+    except Exception:  # noqa: BLE001 - not a program either
+        return None
+
+
+def load_persistables_dir(path, **configs):
+    """paddle.load on a directory / path prefix: the parameters saved by save_inference_model or
+    jit.save under that prefix, as a {name: Tensor} state dict."""
+    prefix = path[:-len('.pdiparams')] if str(path).endswith('.pdiparams') else str(path)
+    for cand in (prefix, os.path.join(prefix, 'model'), os.path.join(prefix, '__model__')):
+        if os.path.exists(cand + '.pdmodel') and os.path.exists(cand + '.pdiparams'):
+            with open(cand + '.pdmodel', 'rb') as f:
+                prog = deserialize_program(f.read())
+            with open(cand + '.pdiparams', 'rb') as f:
+                deserialize_persistables(prog, f.read())
+            out = {}
+            for cid, name in prog._const_names.items():
+                if name is not None:
+                    out[name] = prog._const_owner[cid]
+            return out
+    raise ValueError(f"`paddle.load` can not parse the file: {path} (no such file or saved model prefix)")
