@@ -533,9 +533,12 @@ PA_API int pa_gemm_bf16(const void* A, const void* B, void* C, const void* bias,
                         long long lda, long long ldb, long long ldc, int transA, int transB, float alpha, float beta,
                         int splitk, hipStream_t st) {
   if (!pa_gemm_ok(M, N, K, lda, ldb, ldc, splitk)) return (int)hipErrorInvalidValue;
-  // auto: k-contiguous A -> schedule 11 (row-half staging keeps its DMA on full 128-B lines);
+  // auto: k-contiguous A -> schedule 11 (row-half staging keeps its DMA on full 128-B lines; the
+  // persistent form 12 is within noise in isolation and 3 % slower inside the training step);
   // m-contiguous A (weight gradients) -> schedule 9 (k-half staging, balanced load segments).
-  // Measured per layout on the GPT-3 1.3B shapes: profiles/r2_gemm_sched.log.
+  // Measured per layout on the GPT-3 1.3B shapes: profiles/r2_gemm_sched*.log.  (A one-wave-
+  // per-SIMD 128x128-per-wave schedule was tried and dropped: hipcc rotates its 256 AGPR
+  // accumulators through copies, 0.87-1.0 PF.)
   if (g_variant == 0) pa_gemm8_set_sched(transA == 0 ? 11 : 9);
   const bool v8 = (g_variant == 0 || g_variant >= 8) && pa_gemm8_ok(M, N, K, lda, ldb, ldc, transA, transB, splitk);
   if (splitk == 1) {

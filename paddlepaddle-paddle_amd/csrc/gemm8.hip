@@ -177,6 +177,29 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __r
   }
 }
 
+// same, with an explicit split-K slab index (persistent kernels: blockIdx.z is not the slice)
+template <int EPI>
+__device__ __forceinline__ void epilogue_z(const f32x4 (&acc)[8][4], uint16_t* __restrict__ C,
+                                           float* __restrict__ ws, const uint16_t* __restrict__ bias, int M, int N,
+                                           long long ldc, float alpha, float beta, int mb, int nb, int lane, int z) {
+  if constexpr (EPI == 1) {
+    const int g = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mb + i * 16 + (lane & 15);
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nb + j * 16 + 4 * g;
+        if (n >= N) continue;
+        *reinterpret_cast<f32x4*>(ws + (long long)z * M * N + (long long)m * N + n) = acc[i][j];
+      }
+    }
+  } else {
+    epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, mb, nb, lane);
+  }
+}
+
 // EPI 0: bf16 C = alpha*acc (+ beta*C) (+ bias);  EPI 1: raw fp32 split-K slab (ws[z][M][N]).
 template <bool AK, bool BKM, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm8_kernel(const char* __restrict__ A, const char* __restrict__ B,
@@ -654,6 +677,193 @@ __global__ __launch_bounds__(512, 1) void gemm11_kernel(const char* __restrict__
   epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Schedule 12: schedule 11 made PERSISTENT.  A grid of at most 256 blocks (one per CU) walks its
+// work items (tile x split-K slice) as ONE continuous stream of K-tiles: the staging of item j+1's
+// first K-tiles is issued during item j's last K-tiles exactly as within an item, so the pipeline
+// never drains between tiles and the epilogue of item j (after its last M1) runs while the next
+// item's operands are already in flight — no per-tile prologue latency, no block launch.
+// Items are dealt per XCD (blocks b = x mod 8 share an XCD): each XCD owns a contiguous chunk of
+// the grouped tile order and its 32 blocks walk it 32 tiles at a time, so concurrently running
+// tiles share A row-panels / B column-panels in that XCD's L2.
+__device__ __forceinline__ void item_coords(int item, int splitk, int tm, int tn, int ksplit, int& m0, int& n0,
+                                            int& kb, int& z) {
+  z = item % splitk;
+  const int tile = item / splitk;
+  constexpr int GROUP_M = 8;
+  const int per_group = GROUP_M * tn;
+  const int gidx = tile / per_group;
+  const int first_m = gidx * GROUP_M;
+  const int gm = min(tm - first_m, GROUP_M);
+  const int in = tile - gidx * per_group;
+  m0 = (first_m + in % gm) * BM;
+  n0 = (in / gm) * BN;
+  kb = z * ksplit;
+}
+
+template <bool AK, bool BKM, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm12_kernel(const char* __restrict__ A, const char* __restrict__ B,
+                                                        uint16_t* __restrict__ C, float* __restrict__ ws,
+                                                        const uint16_t* __restrict__ bias, int M, int N, int K,
+                                                        long long lda, long long ldb, long long ldc, float alpha,
+                                                        float beta, int ksplit, int splitk) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3, wq = wave & 3;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  const int nt = ksplit / BK;
+  // this block's items: XCD x = b & 7 owns a contiguous chunk, its blocks stride through it
+  const int nitems = tm * tn * splitk;
+  const int G = gridDim.x, bpx = G >> 3, x = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int q = nitems >> 3, r = nitems & 7;
+  const int cstart = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  const int clen = q + (x < r ? 1 : 0);
+  const int nmine = clen > slot ? (clen - slot + bpx - 1) / bpx : 0;
+  const int E = nmine * nt;  // K-tiles in this block's stream
+  if (E == 0) return;
+  auto item_of = [&](int j) { return cstart + slot + j * bpx; };
+
+  const long long kstepA = AK ? BK * 2 : (long long)BK * lda * 2;
+  const long long kstepB = BKM ? BK * 2 : (long long)BK * ldb * 2;
+  const unsigned lds0 = (unsigned)(size_t)(lds_void*)smem;
+  const unsigned dstA = lds0 + wr * HALF + wq * 4096;
+  const unsigned dstB = lds0 + OPB + wr * HALF + wq * 4096;
+
+  // staging streams (wave-uniform cursors): which item / K-tile the next stage of each operand
+  // targets, and the per-lane source offsets of that item (recomputed when the item changes)
+  int ja = 0, ka = 0, jb = 0, kbt = 0, ea = 0, eb = 0;
+  int jaoff = -1, jboff = -1;
+  unsigned offA[4], offB[4];
+  auto stageA = [&]() {
+    if (ja != jaoff) {
+      int m0, n0, kb, z;
+      item_coords(item_of(ja), splitk, tm, tn, ksplit, m0, n0, kb, z);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) offA[u] = src_off<AK>(wq * 4 + u, lane, m0 + wr * 128, M, lda, kb);
+      jaoff = ja;
+    }
+    const char* base = A + (long long)ka * kstepA;
+    const unsigned d = dstA + (ea & 1) * BUF;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) glds(base, offA[u], d + u * 1024);
+    ++ea;
+    if (++ka == nt) { ka = 0; ++ja; }
+  };
+  auto stageB = [&]() {
+    if (jb != jboff) {
+      int m0, n0, kb, z;
+      item_coords(item_of(jb), splitk, tm, tn, ksplit, m0, n0, kb, z);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) offB[u] = src_off<BKM>(wq * 4 + u, lane, n0 + wr * 128, N, ldb, kb);
+      jboff = jb;
+    }
+    const char* base = B + (long long)kbt * kstepB;
+    const unsigned d = dstB + (eb & 1) * BUF;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) glds(base, offB[u], d + u * 1024);
+    ++eb;
+    if (++kbt == nt) { kbt = 0; ++jb; }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (wr == 0) {
+    stageA();
+    stageB();
+    wait_vm<0>();
+  } else {
+    stageB();
+    stageA();
+    if (E > 1) {
+      stageB();
+      wait_vm<4>();
+    } else {
+      wait_vm<0>();
+    }
+  }
+  bar();
+  if (wr == 1) bar();
+
+  const int bcol = (wc & 1) * 64;
+  s16x8 fa[4][2], fb[4][2];
+  int j = 0, kt = 0;
+  for (int e = 0; e < E; ++e) {
+    const char* ia = smem + (e & 1) * BUF + wr * HALF;
+    const char* ib = smem + (e & 1) * BUF + OPB + (wc >> 1) * HALF;
+    const int m1 = e + 1 < E, m2 = e + 2 < E;
+    // L0
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) fb[jj][kh] = frag<BKM>(ib, bcol + jj * 16, kh, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i][kh] = frag<AK>(ia, i * 16, kh, lane);
+    }
+    if (m1) {
+      stageA();
+      if (wr == 0) stageB();
+    }
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[i][jj] = mfma(fb[jj][kh], fa[i][kh], acc[i][jj]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // L1
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i][kh] = frag<AK>(ia, 64 + i * 16, kh, lane);
+    if (wr == 1) {
+      if (m2) stageB();
+      // B half 1 of era e+1 must land before L0(e+1) of waves 0-3 (after an epilogue its stores
+      // are older than that DMA and are waited for as well: correct, they had two intervals)
+      if (m2) wait_vm<8>();
+      else if (m1) wait_vm<4>();
+      else wait_vm<0>();
+    }
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[4 + i][jj] = mfma(fb[jj][kh], fa[i][kh], acc[4 + i][jj]);
+    __builtin_amdgcn_s_setprio(0);
+    if (wr == 0) wait_vm<0>();
+    else if (m2) wait_vm<4>();
+    else wait_vm<0>();
+    bar();
+    if (++kt == nt) {  // item j complete: epilogue from registers, then a fresh accumulator
+      int m0, n0, kb, z;
+      item_coords(item_of(j), splitk, tm, tn, ksplit, m0, n0, kb, z);
+      if constexpr (EPI == 1)
+        epilogue_z<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane, z);
+      else
+        epilogue_z<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane, 0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+      kt = 0;
+      ++j;
+    }
+  }
+  if (wr == 0) bar();
+}
+
+
 static int g_sched = 9;
 
 template <bool AK, bool BKM, int EPI>
@@ -662,7 +872,13 @@ static hipError_t launch(const void* A, const void* B, void* C, float* ws, const
                          hipStream_t st) {
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   dim3 grid(tm * tn, 1, splitk);
-  if (g_sched == 11)
+  if (g_sched == 12) {
+    const int items = tm * tn * splitk;
+    const int g = items >= 256 ? 256 : (items + 7) / 8 * 8;  // one block per CU, a multiple of 8 (XCDs)
+    gemm12_kernel<AK, BKM, EPI><<<g, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
+                                                   (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
+                                                   K / splitk, splitk);
+  } else if (g_sched == 11)
     gemm11_kernel<AK, BKM, EPI><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                       (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
                                                       K / splitk);
@@ -721,7 +937,7 @@ PA_API int pa_gemm8_bf16(const void* A, const void* B, void* C, const void* bias
 }
 
 // schedule select (A/B benchmarking): 8 = row-half staging, 9 = k-half staging (default),
-// 11 = row-half staging with 32-MFMA segments
+// 11 = row-half staging with 32-MFMA segments, 12 = schedule 11 persistent
 PA_API int pa_gemm8_set_sched(int v) {
   const int old = pa::g8::g_sched;
   pa::g8::g_sched = v;

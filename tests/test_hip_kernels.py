@@ -584,7 +584,7 @@ def test_momentum_flat_matches_per_parameter_path():
         _close(a, b, 1e-5, 1e-5, 'momentum fused vs reference')
 
 
-@pytest.mark.parametrize("variant", [1, 3, 8, 9, 11])
+@pytest.mark.parametrize("variant", [0, 1, 3, 8, 9, 11, 12])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K,splitk", [(256, 256, 64, 1), (512, 768, 512, 1), (328, 264, 384, 1),
                                           (1024, 512, 2048, 4), (200, 1000, 256, 2)])
