@@ -1,8 +1,10 @@
 """Headline benchmark: GPT-3 1.3B bf16 pretraining with group-sharded stage-3 (p_g_os), tokens/s.
 
 BASELINE.json metric: "samples/sec ResNet50 bf16 + tokens/sec GPT-3 1.3B sharding-3, at 1/2/4/8 MI355X".
-Default (`--model gpt3-1.3b`) reports the GPT-3 1.3B tokens/s; `--model resnet50` reports
-ResNet50 bf16 data-parallel samples/s.
+Default (`--model gpt3-1.3b`) reports the GPT-3 1.3B tokens/s as ``value`` and then times ResNet50
+(bf16 O2, NHWC, batch 256 per GPU, Momentum, data parallel) in the same run with the same K/W,
+reported under the extra key ``resnet50`` (``--no-resnet`` skips it); `--model resnet50` reports
+ResNet50 alone as ``value``.
 
 Single node, one process per GPU (torch.distributed.run sets RANK/LOCAL_RANK/WORLD_SIZE);
 collectives are RCCL over xGMI.  Synthetic data of the real shapes, random-init weights.
@@ -29,11 +31,112 @@ def parse():
     ap.add_argument('--sharding', default='p_g_os', choices=['os', 'os_g', 'p_g_os', 'dp'])
     ap.add_argument('--dropout', type=float, default=0.1)
     ap.add_argument('--resnet-batch', type=int, default=256)
+    ap.add_argument('--no-resnet', action='store_true')
     return ap.parse_args()
+
+
+def build_gpt(args, world, rank, dev):
+    import torch
+    import paddle
+    import paddle.distributed as pdist
+    from paddle.models.gpt import gpt_config, GPTForPretraining
+    cfg = gpt_config(args.model, max_position_embeddings=max(args.seq, 1024), hidden_dropout_prob=args.dropout,
+                     attention_probs_dropout_prob=0.0)
+    paddle.seed(1234)  # identical init on every rank
+    model = GPTForPretraining(cfg)
+    opt = paddle.optimizer.AdamW(learning_rate=1e-4, parameters=model.parameters(), weight_decay=0.01,
+                                 beta1=0.9, beta2=0.95, epsilon=1e-8, multi_precision=True,
+                                 grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
+    model, opt = paddle.amp.decorate(model, opt, level='O2', dtype='bfloat16')
+    if args.sharding == 'dp':
+        if world > 1:
+            model = pdist.DataParallel(model)
+    else:  # same sharded engine at every N (degenerate single shard at N=1)
+        model, opt, _ = pdist.sharding.group_sharded_parallel(model, opt, level=args.sharding)
+    B, S = args.micro_batch, args.seq
+    g = torch.Generator(device=dev).manual_seed(rank)
+    ids = torch.randint(0, cfg.vocab_size, (B, S + 1), device=dev, generator=g)
+    x, y = paddle.to_tensor(ids[:, :-1]), paddle.to_tensor(ids[:, 1:])
+    inner = model._layers if hasattr(model, '_layers') else model
+
+    def step():
+        logits = model(x)
+        loss = inner.loss(logits, y)
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        return loss
+
+    mcfg = {'model': args.model, 'global_batch': B * world, 'micro_batch_per_gpu': B, 'seq_len': S,
+            'parallelism': (f"sharding-{ {'os': 1, 'os_g': 2, 'p_g_os': 3}.get(args.sharding, 0)}x{world}"
+                            if args.sharding != 'dp' else f"dp{world}"),
+            'hidden_dropout': args.dropout, 'attention_dropout': 0.0, 'optimizer': 'AdamW (fused, fp32 master)',
+            'vocab': cfg.vocab_size}
+    return step, B * S * world, 'tokens/sec GPT-3 1.3B sharding-3', 'tokens/s', mcfg
+
+
+def build_resnet(args, world, rank, dev):
+    import torch
+    import paddle
+    import paddle.distributed as pdist
+    from paddle.vision.models import resnet50
+    paddle.seed(1234)
+    B = args.resnet_batch
+    model = resnet50(data_format='NHWC')
+    opt = paddle.optimizer.Momentum(learning_rate=0.1, momentum=0.9, parameters=model.parameters(),
+                                    weight_decay=1e-4, multi_precision=True)
+    model, opt = paddle.amp.decorate(model, opt, level='O2', dtype='bfloat16')
+    if world > 1:
+        model = pdist.DataParallel(model)
+    g = torch.Generator(device=dev).manual_seed(rank)
+    img = paddle.to_tensor(torch.randn(B, 224, 224, 3, device=dev, dtype=torch.bfloat16, generator=g))
+    lab = paddle.to_tensor(torch.randint(0, 1000, (B,), device=dev, generator=g))
+
+    def step():
+        out = model(img)
+        loss = paddle.nn.functional.cross_entropy(out, lab)
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        return loss
+
+    mcfg = {'model': 'resnet50', 'global_batch': B * world, 'image': '224x224 NHWC', 'parallelism': f"dp{world}",
+            'optimizer': 'Momentum'}
+    return step, B * world, 'samples/sec ResNet50 bf16', 'samples/s', mcfg
+
+
+def measure(step, steps, warmup, world, rank, dev, tag):
+    """W untimed warmup steps, then K timed steps bracketed by barrier + device sync; MAX over ranks."""
+    import torch
+    import torch.distributed as dist
+    loss = None
+    for i in range(warmup):
+        loss = step()
+        if rank == 0:  # progress on stderr; stdout carries only the JSON line
+            torch.cuda.synchronize()
+            print(f"[{tag}] warmup step {i} loss {float(loss.item()):.4f}", file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    if world > 1:
+        tt = torch.tensor([ms], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        ms = float(tt.item())
+    return ms, float(loss.item())
 
 
 def main():
     args = parse()
+    import gc
     import torch
     import torch.distributed as dist
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -43,99 +146,28 @@ def main():
     if world > 1:
         dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
     import paddle
-    import paddle.distributed as pdist
     paddle.seed(1234 + rank)
     dev = torch.device('cuda', local_rank)
 
-    if args.model.startswith('gpt'):
-        from paddle.models.gpt import gpt_config, GPTForPretraining
-        cfg = gpt_config(args.model, max_position_embeddings=max(args.seq, 1024), hidden_dropout_prob=args.dropout,
-                         attention_probs_dropout_prob=0.0)
-        paddle.seed(1234)  # identical init on every rank
-        model = GPTForPretraining(cfg)
-        opt = paddle.optimizer.AdamW(learning_rate=1e-4, parameters=model.parameters(), weight_decay=0.01,
-                                     beta1=0.9, beta2=0.95, epsilon=1e-8, multi_precision=True,
-                                     grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
-        model, opt = paddle.amp.decorate(model, opt, level='O2', dtype='bfloat16')
-        if args.sharding == 'dp':
-            if world > 1:
-                model = pdist.DataParallel(model)
-        else:  # same sharded engine at every N (degenerate single shard at N=1)
-            model, opt, _ = pdist.sharding.group_sharded_parallel(model, opt, level=args.sharding)
-        B, S = args.micro_batch, args.seq
-        g = torch.Generator(device=dev).manual_seed(rank)
-        ids = torch.randint(0, cfg.vocab_size, (B, S + 1), device=dev, generator=g)
-        x, y = paddle.to_tensor(ids[:, :-1]), paddle.to_tensor(ids[:, 1:])
-        inner = model._layers if hasattr(model, '_layers') else model
-
-        def step():
-            logits = model(x)
-            loss = inner.loss(logits, y)
-            loss.backward()
-            opt.step()
-            opt.clear_grad()
-            return loss
-
-        tokens_per_step = B * S * world
-        metric, unit = 'tokens/sec GPT-3 1.3B sharding-3', 'tokens/s'
-        mcfg = {'model': args.model, 'global_batch': B * world, 'micro_batch_per_gpu': B, 'seq_len': S,
-                'parallelism': (f"sharding-{ {'os': 1, 'os_g': 2, 'p_g_os': 3}.get(args.sharding, 0)}x{world}"
-                                if args.sharding != 'dp' else f"dp{world}"),
-                'hidden_dropout': args.dropout, 'attention_dropout': 0.0, 'optimizer': 'AdamW (fused, fp32 master)',
-                'vocab': cfg.vocab_size}
-    else:
-        from paddle.vision.models import resnet50
-        B = args.resnet_batch
-        model = resnet50(data_format='NHWC')
-        opt = paddle.optimizer.Momentum(learning_rate=0.1, momentum=0.9, parameters=model.parameters(),
-                                        weight_decay=1e-4, multi_precision=True)
-        model, opt = paddle.amp.decorate(model, opt, level='O2', dtype='bfloat16')
-        if world > 1:
-            model = pdist.DataParallel(model)
-        img = paddle.to_tensor(torch.randn(B, 224, 224, 3, device=dev, dtype=torch.bfloat16))
-        lab = paddle.to_tensor(torch.randint(0, 1000, (B,), device=dev))
-
-        def step():
-            out = model(img)
-            loss = paddle.nn.functional.cross_entropy(out, lab)
-            loss.backward()
-            opt.step()
-            opt.clear_grad()
-            return loss
-
-        tokens_per_step = B * world
-        metric, unit = 'samples/sec ResNet50 bf16', 'samples/s'
-        mcfg = {'model': 'resnet50', 'global_batch': B * world, 'image': '224x224 NHWC',
-                'parallelism': f"dp{world}", 'optimizer': 'Momentum'}
-
-    for i in range(args.warmup):
-        loss = step()
-        if rank == 0:  # progress on stderr; stdout carries only the JSON line
-            torch.cuda.synchronize()
-            print(f"warmup step {i} loss {float(loss.item()):.4f}", file=sys.stderr, flush=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    ms = dt / args.steps * 1e3
-    if world > 1:
-        tt = torch.tensor([ms], device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        ms = float(tt.item())
-    value = tokens_per_step / (ms / 1e3)
+    build = build_gpt if args.model.startswith('gpt') else build_resnet
+    step, work, metric, unit, mcfg = build(args, world, rank, dev)
+    ms, final_loss = measure(step, args.steps, args.warmup, world, rank, dev, args.model)
+    value = work / (ms / 1e3)
+    out = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "bf16",
+           "data": "synthetic (random token ids / random images), random-init weights",
+           "config": mcfg, "final_loss": round(final_loss, 4)}
+    if args.model.startswith('gpt') and not args.no_resnet:
+        # the second half of the BASELINE metric, same process, same K/W, GPT state released first
+        del step
+        gc.collect()
+        torch.cuda.empty_cache()
+        rstep, rwork, _, runit, rcfg = build_resnet(args, world, rank, dev)
+        rms, rloss = measure(rstep, args.steps, args.warmup, world, rank, dev, 'resnet50')
+        out["resnet50"] = {"metric": "samples/sec ResNet50 bf16", "value": round(rwork / (rms / 1e3), 2),
+                           "unit": runit, "ms_per_step": round(rms, 3), "config": rcfg, "final_loss": round(rloss, 4)}
     if rank == 0:
-        out = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random token ids / random images), random-init weights",
-               "config": mcfg, "final_loss": round(float(loss.item()), 4)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
