@@ -52,9 +52,13 @@ class AmpScaler:
         st = self._opt_state.get(id(optimizer), OptimizerState.INIT)
         if st == OptimizerState.UNSCALED:
             return
-        grads = [p._t.grad for p in optimizer._parameter_list if p._t.grad is not None]
+        engine = getattr(optimizer, 'engine', None)
+        if engine is not None and hasattr(engine, 'arenas'):  # sharded optimizer: its gradients live in the arenas
+            grads = [a['grad'] for a in engine.arenas.values()]
+        else:
+            grads = [p._t.grad for p in optimizer._parameter_list if p._t.grad is not None]
         if not grads:
-            self._found_inf = False
+            self._found_inf = self._sync_found_inf(False)
             return
         inv = 1.0 / self._scale
         found = torch.zeros((), dtype=torch.float32, device=grads[0].device)
@@ -67,8 +71,14 @@ class AmpScaler:
             torch._amp_foreach_non_finite_check_and_unscale_(gs, fi, torch.ones((), device=dev)) \
                 if dev.type == 'cuda' else fi.add_(sum(float(~torch.isfinite(g).all()) for g in gs))
             found = found + fi.to(found.device)
-        self._found_inf = bool(found.item() > 0)
+        self._found_inf = self._sync_found_inf(found)
         self._opt_state[id(optimizer)] = OptimizerState.UNSCALED
+
+    def _sync_found_inf(self, found):
+        """Hook for distributed scalers (fleet.distributed_scaler): every rank must agree."""
+        if isinstance(found, bool):
+            return found
+        return bool(found.item() > 0)
 
     def unscale_(self, optimizer):
         self._unscale(optimizer)

@@ -185,13 +185,32 @@ class _Fleet:
         hcg = self._hcg
         if hcg is None:
             return optimizer
+        if hcg.get_sharding_parallel_world_size() > 1:
+            # the sharding axis: reduce-scattered gradients, sharded optimizer state, parameter
+            # all-gather after the step (plus the dp all-reduce of the shards)
+            from .meta_optimizers.dygraph_optimizer import DygraphShardingOptimizer
+            return DygraphShardingOptimizer(optimizer, hcg, self._strategy)
         return HybridParallelOptimizer(optimizer, hcg, self._strategy)
 
     def distributed_scaler(self, scaler):
+        """reference fleet/scaler.py: the found-inf flag is max-reduced over every rank of the
+        hybrid topology (a shard or pipeline stage that overflowed makes all ranks skip the step)."""
+        def sync(found):
+            import torch
+            dev = found.device if isinstance(found, torch.Tensor) else (
+                torch.device('cuda', torch.cuda.current_device()) if torch.cuda.is_available() and
+                dist.get_backend() == 'nccl' else torch.device('cpu'))
+            t = found.detach().float().reshape(1).clone() if isinstance(found, torch.Tensor) else \
+                torch.tensor([1.0 if found else 0.0], device=dev)
+            if dist.is_initialized() and dist.get_world_size() > 1:
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return bool(t.item() > 0)
+        scaler._sync_found_inf = sync
         return scaler
 
     def save_persistables(self, executor, dirname, main_program=None):
-        pass
+        from ..io import save_persistables
+        save_persistables(executor, dirname, main_program)
 
     @property
     def util(self):
@@ -239,10 +258,20 @@ class HybridParallelOptimizer:
         return sq
 
     def step(self):
+        # tensor-parallel (and sep) models are not wrapped in DataParallel: their gradients are
+        # all-reduced over the dp group here (reference hybrid_parallel_optimizer.py: step ->
+        # fused_allreduce_gradients).  Pipeline schedules sync dp themselves before stepping.
+        mode = self._hcg.get_parallel_mode()
+        dp = self._hcg.get_data_parallel_group()
+        if mode in (ParallelMode.TENSOR_PARALLEL, ParallelMode.SEGMENT_PARALLEL) and dp is not None \
+                and dp.nranks > 1:
+            from .utils.hybrid_parallel_util import fused_allreduce_gradients
+            fused_allreduce_gradients(list(self._inner_opt._parameter_list), self._hcg)
         self._inner_opt.step()
 
     def minimize(self, loss, *a, **k):
-        return self._inner_opt.minimize(loss, *a, **k)
+        loss.backward()
+        self.step()
 
     def clear_grad(self, set_to_zero=True):
         self._inner_opt.clear_grad(set_to_zero)

@@ -295,12 +295,15 @@ class PipelineParallel(Layer):
         while pending:
             self._bwd_step(*pending.pop(0))
         self._drain_sends()
+        if getattr(optimizer, '_syncs_dp', False) and self._layers._shared_comm:
+            # the sharding optimizer reduce-scatters gradients inside backward, before this point
+            raise NotImplementedError("pipeline SharedLayerDesc weights with sharding_degree > 1: tie the "
+                                      "weights inside one stage or use sharding_degree 1")
         self._layers.allreduce_shared_weight_gradients()
-        if self._dp_group is not None and self._dp_group.nranks > 1:
-            for p in self._layers.parameters():
-                if p._t.grad is not None:
-                    dist.all_reduce(p._t.grad, dist.ReduceOp.SUM, group=self._dp_group.pg)
-                    p._t.grad.div_(self._dp_group.nranks)
+        if self._dp_group is not None and self._dp_group.nranks > 1 and not getattr(optimizer, '_syncs_dp', False):
+            # one coalesced all-reduce per dtype (a sharding optimizer syncs dp on its shards instead)
+            from ..utils.hybrid_parallel_util import fused_allreduce_gradients
+            fused_allreduce_gradients(list(self._layers.parameters()), self._hcg)
         if scaler is not None:
             scaler.step(optimizer)
             scaler.update()
@@ -443,12 +446,15 @@ class PipelineParallelWithInterleave(PipelineParallel):
                 if not (first_rank and v == 0):
                     self._send(_unwrap(x).grad, prev_rank, 'grad')
         self._drain_sends()
+        if getattr(optimizer, '_syncs_dp', False) and self._layers._shared_comm:
+            # the sharding optimizer reduce-scatters gradients inside backward, before this point
+            raise NotImplementedError("pipeline SharedLayerDesc weights with sharding_degree > 1: tie the "
+                                      "weights inside one stage or use sharding_degree 1")
         self._layers.allreduce_shared_weight_gradients()
-        if self._dp_group is not None and self._dp_group.nranks > 1:
-            for p in self._layers.parameters():
-                if p._t.grad is not None:
-                    dist.all_reduce(p._t.grad, dist.ReduceOp.SUM, group=self._dp_group.pg)
-                    p._t.grad.div_(self._dp_group.nranks)
+        if self._dp_group is not None and self._dp_group.nranks > 1 and not getattr(optimizer, '_syncs_dp', False):
+            # one coalesced all-reduce per dtype (a sharding optimizer syncs dp on its shards instead)
+            from ..utils.hybrid_parallel_util import fused_allreduce_gradients
+            fused_allreduce_gradients(list(self._layers.parameters()), self._hcg)
         if scaler is not None:
             scaler.step(optimizer)
             scaler.update()

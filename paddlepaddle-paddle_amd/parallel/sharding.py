@@ -124,9 +124,13 @@ class _PreBackward(torch.autograd.Function):
 
 class ShardingEngine:
     def __init__(self, model, level='p_g_os', group=None, bucket_mb=256, segment_size=2 ** 20,
-                 release_grads=True, persistent_types=None, persistent_below=None):
+                 release_grads=True, persistent_types=None, persistent_below=None, params=None):
+        """model: the Layer to shard; or model=None with ``params`` (a parameter list) for stage 1/2
+        (the hybrid-parallel sharding optimizer, which only sees its optimizer's parameters)."""
         self.model = model
         self.level = LEVELS[level] if isinstance(level, str) else int(level)
+        if model is None and (params is None or self.level == 3):
+            raise ValueError("ShardingEngine: stage 3 needs the model; stage 1/2 need model or params")
         self.group = group
         self.pg = _pg(group)
         self.world = dist.get_world_size(self.pg) if dist.is_initialized() else 1
@@ -141,8 +145,9 @@ class ShardingEngine:
         # layers (norms, heads) are the ones parent code tends to use outside their own forward
         # (the reference likewise leaves parameters below segment_size unsliced, group_sharded_stage3.py)
         self.persistent_below = segment_size if persistent_below is None else persistent_below
+        self._explicit_params = params
         self._broadcast_params()
-        params = [p for p in model.parameters() if p._t.requires_grad or True]
+        params = list(params) if params is not None else list(model.parameters())
         if self.level == 3:
             self.units = self._layer_units(model, segment_size)
         else:
@@ -165,6 +170,12 @@ class ShardingEngine:
     # ------------------------------------------------------------------ construction
     def _broadcast_params(self):
         if self.world == 1:
+            return
+        if self.model is None:  # replicas of every parameter start equal: broadcast from rank 0
+            src = self.group.ranks[0] if self.group is not None and hasattr(self.group, 'ranks') else 0
+            with torch.no_grad():
+                for p in self._explicit_params:
+                    dist.broadcast(p._t, src, group=self.pg)
             return
         from .data_parallel import sync_params_buffers
         sync_params_buffers(self.model, self.group)
@@ -410,17 +421,22 @@ class ShardingEngine:
 
 
 class ShardedOptimizer:
-    """Wraps a paddle optimizer; updates only the local shard (one fused AdamW per dtype arena).
+    """Wraps a paddle optimizer; updates only the local shard.  Adam/AdamW: one fused HIP AdamW
+    launch per dtype arena (fp32 master + moments); SGD / Momentum (L2 regularisation, Nesterov):
+    a flat elementwise update of the arena, the velocity sharded like the moments.
 
     Reference: GroupShardedOptimizerStage2 / the stage-3 _OptimizerWrapper."""
+
+    SUPPORTED = ('AdamW', 'Adam', 'SGD', 'Momentum')
 
     def __init__(self, optimizer, engine):
         self._inner = optimizer
         self.engine = engine
         self._step = 0
         name = type(optimizer).__name__
-        if name not in ('AdamW', 'Adam'):
-            raise NotImplementedError(f"group-sharded training supports Adam/AdamW here, got {name}")
+        if name not in self.SUPPORTED:
+            raise NotImplementedError(f"group-sharded training supports {self.SUPPORTED}, got {name}")
+        self._kind = name
         self._decoupled = name == 'AdamW'
         self._coeff_runs = {}
         for dt, a in engine.arenas.items():
@@ -428,6 +444,12 @@ class ShardedOptimizer:
 
     def _coeff(self, p):
         opt = self._inner
+        if self._kind in ('SGD', 'Momentum'):  # L2 regularisation coefficient (added to the gradient)
+            from ..regularizer import L2Decay
+            reg = getattr(p, 'regularizer', None) or opt.regularization
+            if isinstance(reg, (int, float)):
+                return float(reg)
+            return float(reg._coeff) if isinstance(reg, L2Decay) else 0.0
         if not self._decoupled:
             return 0.0
         f = getattr(opt, '_apply_decay_param_fun', None)
@@ -435,8 +457,10 @@ class ShardedOptimizer:
             return 0.0
         return float(opt._coeff)
 
-    def _runs(self, arena):
-        """(arena_lo, arena_hi, coeff) runs of equal weight decay covering [0, arena size)."""
+    def _runs(self, arena, key=None):
+        """(arena_lo, arena_hi, value) runs of equal ``key(param)`` (default: weight decay)
+        covering [0, arena size)."""
+        key = key or self._coeff
         segs = []
         r = self.engine.rank
         for u in arena['units']:
@@ -444,7 +468,7 @@ class ShardedOptimizer:
             for p, o in zip(u.fb.params, u.fb.offsets):
                 a, b = max(o, lo_s), min(o + p._t.numel(), hi_s)
                 if a < b:
-                    segs.append((u.arena_off + (a - lo_s), u.arena_off + (b - lo_s), self._coeff(p)))
+                    segs.append((u.arena_off + (a - lo_s), u.arena_off + (b - lo_s), key(p)))
         segs.sort()
         runs = []
         for a, b, c in segs:
@@ -491,13 +515,47 @@ class ShardedOptimizer:
         return torch.clamp(clip.clip_norm / torch.clamp(norm, min=clip.clip_norm), max=1.0)
 
     @torch.no_grad()
+    def _step_sgd_momentum(self, lr, scale):
+        opt = self._inner
+        mom = self._kind == 'Momentum'
+        mu = float(getattr(opt, '_momentum', 0.0))
+        nesterov = bool(getattr(opt, '_use_nesterov', False))
+        rescale = float(getattr(opt, '_rescale', 1.0))
+        for dt, a in self.engine.arenas.items():
+            lowp = a['param'] if dt != torch.float32 else None
+            for lo, hi, coeff in self._coeff_runs[dt]:
+                if hi <= lo:
+                    continue
+                master = a['master'][lo:hi]
+                g = a['grad'][lo:hi].float()
+                if scale is not None:
+                    g = g * scale
+                if coeff:
+                    g = g + coeff * master
+                if mom:
+                    v = a['m'][lo:hi]
+                    g = g * rescale
+                    v.mul_(mu).add_(g)
+                    upd = g + mu * v if nesterov else v
+                else:
+                    upd = g
+                master.sub_(lr * upd)
+                if lowp is not None:
+                    lowp[lo:hi].copy_(master.to(dt))
+
+    @torch.no_grad()
     def step(self):
         opt = self._inner
-        b1, b2, eps = opt._beta1, opt._beta2, opt._epsilon
         self._step += 1
-        b1p, b2p = b1 ** self._step, b2 ** self._step
         lr = opt.get_lr()
         scale = self._clip_scale()
+        if self._kind in ('SGD', 'Momentum'):
+            self._step_sgd_momentum(lr, scale)
+            self.engine.gather_params_after_step()
+            opt._global_step += 1
+            return
+        b1, b2, eps = opt._beta1, opt._beta2, opt._epsilon
+        b1p, b2p = b1 ** self._step, b2 ** self._step
         for dt, a in self.engine.arenas.items():
             g = a['grad']
             if scale is not None and not ops.use_hip(g):

@@ -63,18 +63,27 @@ def params_of(model):
     return {k: v.numpy().astype(np.float64) for k, v in sd.items()}
 
 
+def make_opt(kind, params):
+    clip = nn.ClipGradByGlobalNorm(0.5)
+    if kind == 'momentum':  # sharded Momentum (velocity sharded like the Adam moments), L2 decay, Nesterov
+        return paddle.optimizer.Momentum(learning_rate=0.05, momentum=0.9, parameters=params, use_nesterov=True,
+                                         weight_decay=1e-3, grad_clip=clip)
+    if kind == 'sgd':
+        return paddle.optimizer.SGD(learning_rate=0.1, parameters=params, weight_decay=1e-3, grad_clip=clip)
+    return paddle.optimizer.AdamW(learning_rate=0.01, parameters=params, grad_clip=clip)
+
+
 def main():
     mode = sys.argv[1]
+    kind = sys.argv[2] if len(sys.argv) > 2 else 'adamw'
     dist.init_parallel_env()
     rank, world = dist.get_rank(), dist.get_world_size()
     ref = make()
-    ropt = paddle.optimizer.AdamW(learning_rate=0.01, parameters=ref.parameters(),
-                                  grad_clip=nn.ClipGradByGlobalNorm(0.5))
+    ropt = make_opt(kind, ref.parameters())
     train(ref, ropt, rank, world, split=False)
 
     model = make()
-    opt = paddle.optimizer.AdamW(learning_rate=0.01, parameters=model.parameters(),
-                                 grad_clip=nn.ClipGradByGlobalNorm(0.5))
+    opt = make_opt(kind, model.parameters())
     if mode == 'dp':
         model = paddle.DataParallel(model)
     else:
@@ -83,7 +92,7 @@ def main():
     got, want = params_of(model), params_of(ref)
     for k in want:
         err = np.abs(got[k] - want[k]).max()
-        assert err < 2e-5, (mode, k, err)
+        assert err < 2e-5, (mode, kind, k, err)
     print(f"rank{rank} {mode} OK", flush=True)
 
 

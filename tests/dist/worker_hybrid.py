@@ -57,6 +57,50 @@ def tp_test():
     print(f"rank{dist.get_rank()} tp OK", flush=True)
 
 
+def tpdp_test():
+    """TP=2 x DP=2 (4 ranks): the dp replicas see different halves of the batch; the hybrid
+    optimizer all-reduces their gradients over dp, so two SGD steps equal single-device training
+    on the whole batch."""
+    s = fleet.DistributedStrategy()
+    s.hybrid_configs = {'dp_degree': 2, 'mp_degree': 2, 'pp_degree': 1}
+    fleet.init(is_collective=True, strategy=s)
+    hcg = fleet.get_hybrid_communicate_group()
+    r, dpr = hcg.get_model_parallel_rank(), hcg.get_data_parallel_rank()
+    H, F = 8, 12
+    paddle.seed(5)  # same full weights everywhere
+    W1 = torch.randn(H, F) * 0.3
+    W2 = torch.randn(F, H) * 0.3
+    col = fleet.meta_parallel.ColumnParallelLinear(H, F, gather_output=False, has_bias=False)
+    row = fleet.meta_parallel.RowParallelLinear(F, H, input_is_parallel=True, has_bias=False)
+    with torch.no_grad():
+        col.weight._t.copy_(W1.chunk(2, 1)[r])
+        row.weight._t.copy_(W2.chunk(2, 0)[r])
+    net = nn.LayerList([col, row])
+    model = fleet.distributed_model(net)
+    opt = fleet.distributed_optimizer(paddle.optimizer.SGD(learning_rate=0.5, parameters=net.parameters()))
+    g = torch.Generator().manual_seed(9)
+    ref1, ref2 = W1.clone().requires_grad_(), W2.clone().requires_grad_()
+    for step in range(2):
+        X = torch.randn(8, H, generator=g)
+        T = torch.randn(8, H, generator=g)
+        xs, ts = X[4 * dpr:4 * dpr + 4], T[4 * dpr:4 * dpr + 4]
+        y = row(paddle.nn.functional.relu(col(paddle.to_tensor(xs))))
+        loss = ((y - paddle.to_tensor(ts)) ** 2).mean()
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        lref = ((torch.relu(X @ ref1) @ ref2 - T) ** 2).mean()
+        lref.backward()
+        with torch.no_grad():
+            ref1 -= 0.5 * ref1.grad
+            ref2 -= 0.5 * ref2.grad
+            ref1.grad = None
+            ref2.grad = None
+    np.testing.assert_allclose(col.weight.numpy(), ref1.detach().chunk(2, 1)[r].numpy(), atol=1e-5)
+    np.testing.assert_allclose(row.weight.numpy(), ref2.detach().chunk(2, 0)[r].numpy(), atol=1e-5)
+    print(f"rank{dist.get_rank()} tpdp OK", flush=True)
+
+
 def sp_test():
     s = fleet.DistributedStrategy()
     s.hybrid_configs = {'dp_degree': 1, 'mp_degree': 2, 'pp_degree': 1}
@@ -140,4 +184,4 @@ def pp_test(virtual=1):
 
 
 if __name__ == '__main__':
-    {'tp': tp_test, 'sp': sp_test, 'pp': pp_test, 'vpp': lambda: pp_test(2)}[sys.argv[1]]()
+    {'tp': tp_test, 'sp': sp_test, 'pp': pp_test, 'vpp': lambda: pp_test(2), 'tpdp': tpdp_test}[sys.argv[1]]()

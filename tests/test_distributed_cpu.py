@@ -34,6 +34,18 @@ def test_dp_and_sharding_match_single_process(mode):
     assert out.count(f'{mode} OK') == 2
 
 
+def test_tensor_parallel_with_data_parallel_syncs_gradients():
+    out = run_workers('worker_hybrid.py', 'tpdp', nproc=4)
+    assert out.count('tpdp OK') == 4, out[-3000:]
+
+
+@pytest.mark.parametrize("kind", ['momentum', 'sgd'])
+@pytest.mark.parametrize("mode", ['os', 'p_g_os'])
+def test_sharded_momentum_sgd_match_single_process(mode, kind):
+    out = run_workers('worker_dp_sharding.py', mode, kind)
+    assert out.count(f'{mode} OK') == 2, out[-3000:]
+
+
 @pytest.mark.parametrize("mode", ['tp', 'sp', 'pp', 'vpp'])
 def test_hybrid_parallel_matches_single_device(mode):
     out = run_workers('worker_hybrid.py', mode)
@@ -211,3 +223,20 @@ def test_elastic_scale_out_and_in(tmp_path):
                     os.killpg(p.pid, signal.SIGKILL)
                 except ProcessLookupError:
                     pass
+
+
+@pytest.mark.parametrize("clip", ['0', '0.5'])
+def test_llama_hybrid_tp2_pp2_sharding2_matches_single_device(clip):
+    """The fleet sharding axis (8 gloo ranks): sharded AdamW state, reduce-scattered gradients,
+    global-norm clipping across sharding x mp x pp, equal to single-device training."""
+    os.environ['CLIP'] = clip
+    try:
+        out = run_workers('worker_llama_hybrid_sharding.py', nproc=8, timeout=600)
+    finally:
+        os.environ.pop('CLIP', None)
+    assert out.count("sharding2 OK") == 8, out[-3000:]
+
+
+def test_distributed_scaler_agrees_on_overflow():
+    out = run_workers('worker_scaler.py')
+    assert out.count('scaler OK') == 2, out[-3000:]
