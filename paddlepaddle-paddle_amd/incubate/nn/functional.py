@@ -11,6 +11,7 @@ import torch.nn.functional as TF
 from ...core.tensor import Tensor, _wrap as _w, _unwrap as _u
 from ... import ops
 from ...nn import functional as F
+from ...nn.functional.flash_attention import _attend
 
 
 def fused_rms_norm(x, norm_weight, norm_bias=None, epsilon=1e-6, begin_norm_axis=-1, bias=None, residual=None,
@@ -211,33 +212,258 @@ def fused_multi_head_attention(x, qkv_weight, linear_weight, pre_layer_norm=Fals
     return o
 
 
+def _rope_rows(t, cos, sin, neox):
+    """Rotary embedding on rows t [..., D] with per-row cos/sin [..., D] (full width)."""
+    tf = t.float()
+    if neox:
+        h = tf.shape[-1] // 2
+        rot = torch.cat([-tf[..., h:], tf[..., :h]], -1)
+    else:
+        rot = torch.stack([-tf[..., 1::2], tf[..., 0::2]], -1).reshape(tf.shape)
+    return (tf * cos + rot * sin).to(t.dtype)
+
+
+def _full_width(cs, D, neox):
+    """cos/sin given for D/2 frequencies -> D columns in the layout of the rotation."""
+    if cs.shape[-1] == D:
+        return cs
+    return torch.cat([cs, cs], -1) if neox else cs.repeat_interleave(2, -1)
+
+
 def masked_multihead_attention(x, cache_kv=None, bias=None, src_mask=None, cum_offsets=None, sequence_lengths=None,
                                rotary_tensor=None, beam_cache_offset=None, qkv_out_scale=None, out_shift=None,
                                out_smooth=None, seq_len=1, rotary_emb_dims=0, use_neox_rotary_style=False,
                                compute_dtype='default', out_scale=-1, quant_round_type=1, quant_max_bound=127.0,
                                quant_min_bound=-127.0):
-    """Decode-step attention over a [2, B, H, max_len, D] cache (reference masked_multihead_attention)."""
+    """One decode step of attention (reference incubate/nn/functional/masked_multihead_attention.py:19).
+
+    x: [B, 3*H*D] fused qkv of the new token; cache_kv: [2, B, H, max_len, D] (updated IN PLACE:
+    the new K/V land at step t = sequence_lengths[b] (or src_mask.shape[-1] - 1), then the token
+    attends over positions [0, t]).  bias [3, H, D], src_mask additive [B, 1, 1, >= t+1],
+    rotary_tensor [2, B, 1|seq, ..., D] (cos, sin).  Returns (out [B, H*D], cache_kv).  The
+    attention runs on the split-K HIP decode kernel (csrc/decode_attn.hip); the cache layout is
+    the natural [B, H, L, D] (the reference's CUDA kernel keeps K as [B, H, D/8, L, 8])."""
+    if beam_cache_offset is not None or qkv_out_scale is not None or out_scale > 0:
+        raise NotImplementedError("masked_multihead_attention: beam offsets / int8 quantised paths are not supported")
     t = _u(x)
     cache = _u(cache_kv)
     _, B, H, L, D = cache.shape
     qkv = t.reshape(B, 3, H, D)
+    if sequence_lengths is not None:
+        step = _u(sequence_lengths).reshape(-1).to(torch.int32)
+    elif src_mask is not None:
+        step = torch.full((B,), _u(src_mask).shape[-1] - 1, dtype=torch.int32, device=t.device)
+    else:
+        raise ValueError("masked_multihead_attention needs sequence_lengths or src_mask to know the decode step")
+    bq = bk = bv = None
     if bias is not None:
-        qkv = qkv + _u(bias).reshape(1, 3, H, D)
+        bb = _u(bias).reshape(3, H * D)
+        bq, bk, bv = bb[0], bb[1], bb[2]
     q, k, v = qkv[:, 0], qkv[:, 1], qkv[:, 2]
-    lens = _u(sequence_lengths).reshape(-1) if sequence_lengths is not None else torch.zeros(B, dtype=torch.long,
-                                                                                             device=t.device)
-    ar = torch.arange(B, device=t.device)
-    cache[0, ar, :, lens] = k
-    cache[1, ar, :, lens] = v
-    keys, vals = cache[0], cache[1]
-    s = torch.einsum('bhd,bhld->bhl', q.float(), keys.float()) / math.sqrt(D)
-    pos = torch.arange(L, device=t.device)[None, None, :]
-    s = s.masked_fill(pos > lens[:, None, None], float('-inf'))
+    if rotary_tensor is not None and rotary_emb_dims > 0:
+        rt = _u(rotary_tensor).float()
+        rt = rt.reshape(2, B, -1, rt.shape[-1])
+        idx = (step.long().clamp_min(0) if rt.shape[2] > 1 else torch.zeros(B, dtype=torch.long, device=t.device))
+        cos = _full_width(rt[0, torch.arange(B, device=t.device), idx], D, use_neox_rotary_style)[:, None]
+        sin = _full_width(rt[1, torch.arange(B, device=t.device), idx], D, use_neox_rotary_style)[:, None]
+        if bq is not None:
+            q, k = q + bq.reshape(1, H, D), k + bk.reshape(1, H, D)
+            bq = bk = None
+        q = _rope_rows(q, cos, sin, use_neox_rotary_style)
+        k = _rope_rows(k, cos, sin, use_neox_rotary_style)
+    ops.decode.kv_cache_write(k, v, cache[0], cache[1], step, k_bias=bk, v_bias=bv)
+    lens = torch.where(step >= 0, step + 1, torch.zeros_like(step))
+    mask = None
     if src_mask is not None:
-        s = s + _u(src_mask).reshape(B, 1, -1)[..., :L]
-    p = torch.softmax(s, -1)
-    o = torch.einsum('bhl,bhld->bhd', p, vals.float()).to(t.dtype)
+        mask = _u(src_mask).reshape(B, -1).float()
+    o = ops.decode.decode_attention(q, cache[0], cache[1], lens, mask=mask, q_bias=bq)
     return _w(o.reshape(B, H * D)), _w(cache)
+
+
+def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq_lens_decoder, seq_lens_this_time,
+                              padding_offsets, cum_offsets, cu_seqlens_q, cu_seqlens_k, block_tables,
+                              pre_key_cache=None, pre_value_cache=None, cache_k_quant_scales=None,
+                              cache_v_quant_scales=None, cache_k_dequant_scales=None, cache_v_dequant_scales=None,
+                              qkv_out_scale=None, qkv_bias=None, out_shift=None, out_smooth=None,
+                              max_enc_len_this_time=None, max_dec_len_this_time=None, rope_emb=None, mask=None,
+                              tgt_mask=None, max_seq_len=-1, block_size=64, use_neox_style=False,
+                              use_dynamic_cachekv_quant=False, quant_round_type=1, quant_max_bound=127.0,
+                              quant_min_bound=-127.0, out_scale=-1, compute_dtype="default"):
+    """Paged-KV-cache attention over a mixed batch (reference incubate/nn/functional/
+    block_multihead_attention.py:19): sequences with seq_lens_encoder > 0 are prompts (all their
+    tokens' K/V written into their cache blocks, causal attention over the prompt), the others
+    decode one token at position seq_lens_decoder[b] over their cached prefix (split-K HIP decode
+    kernel over the block table).  qkv: [token_num, (Hq + 2 Hkv) * D] unpadded;
+    key_cache / value_cache: [num_blocks, Hkv, block_size, D] (updated in place).
+    Returns (out [token_num, Hq*D], qkv, key_cache, value_cache)."""
+    if any(a is not None for a in (pre_key_cache, cache_k_quant_scales, qkv_out_scale)) or out_scale > 0 or \
+            use_dynamic_cachekv_quant:
+        raise NotImplementedError("block_multihead_attention: pre-caches / int8 cache quantisation are not supported")
+    t = _u(qkv)
+    kc, vc = _u(key_cache), _u(value_cache)
+    _, Hkv, bs, D = kc.shape
+    T = t.shape[0]
+    Hq = t.shape[1] // D - 2 * Hkv
+    enc = _u(seq_lens_encoder).reshape(-1).to(torch.int32)
+    dec = _u(seq_lens_decoder).reshape(-1).to(torch.int32)
+    this = _u(seq_lens_this_time).reshape(-1).to(torch.int32)
+    B = enc.shape[0]
+    dev = t.device
+    cu = _u(cu_seqlens_q).reshape(-1).to(torch.int64)
+    bt = _u(block_tables).to(torch.int32)
+    x = t + _u(qkv_bias).reshape(1, -1) if qkv_bias is not None else t
+    q = x[:, :Hq * D].reshape(T, Hq, D)
+    k = x[:, Hq * D:(Hq + Hkv) * D].reshape(T, Hkv, D)
+    v = x[:, (Hq + Hkv) * D:].reshape(T, Hkv, D)
+    # token -> (sequence, absolute position)
+    seq_of = torch.repeat_interleave(torch.arange(B, device=dev, dtype=torch.int32), this.long(), output_size=T)
+    start = cu[:-1][seq_of.long()]
+    pos = (dec[seq_of.long()].long() + (torch.arange(T, device=dev) - start)).to(torch.int32)
+    if rope_emb is not None:
+        re = _u(rope_emb).float()                      # [2, B, max_seq, 1, D/2]
+        cs = re.reshape(2, re.shape[1], re.shape[2], -1)
+        cos = _full_width(cs[0, seq_of.long(), pos.long()], D, use_neox_style)[:, None]
+        sin = _full_width(cs[1, seq_of.long(), pos.long()], D, use_neox_style)[:, None]
+        q = _rope_rows(q, cos, sin, use_neox_style)
+        k = _rope_rows(k, cos, sin, use_neox_style)
+    ops.decode.kv_cache_write(k, v, kc, vc, pos, seq_of=seq_of, block_tables=bt)
+    out = torch.empty(T, Hq, D, dtype=t.dtype, device=dev)
+    enc_l, dec_b = enc.tolist(), ((enc == 0) & (this > 0)).nonzero().reshape(-1)
+    # prompts: causal attention over the prompt's own tokens (flash kernel per prompt)
+    for b, L in enumerate(enc_l):
+        if L <= 0:
+            continue
+        s0 = int(cu[b])
+        qb, kb, vb = q[s0:s0 + L][None], k[s0:s0 + L][None], v[s0:s0 + L][None]
+        m = None if mask is None else _u(mask)[b:b + 1, :, :L, :L]
+        out[s0:s0 + L] = _attend(qb, kb, vb, m, 0.0, m is None, False)[0]
+    # decode tokens: one per sequence, over its paged prefix
+    if dec_b.numel():
+        rows = cu[:-1][dec_b.long()]
+        lens = dec[dec_b.long()] + 1
+        tm = None if tgt_mask is None else _u(tgt_mask).reshape(_u(tgt_mask).shape[0], -1)[dec_b.long()].float()
+        out[rows] = ops.decode.decode_attention(q[rows], kc, vc, lens, block_tables=bt[dec_b.long()], mask=tm)
+    return _w(out.reshape(T, Hq * D)), qkv, key_cache, value_cache
+
+
+def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, linear_weights, linear_biases,
+                            ffn_ln_scales, ffn_ln_biases, ffn1_weights, ffn1_biases, ffn2_weights, ffn2_biases,
+                            pre_layer_norm=True, epsilon=1e-05, residual_alpha=1.0, cache_kvs=None, beam_offset=None,
+                            pre_caches=None, seq_lens=None, rotary_embs=None, time_step=None, attn_mask=None,
+                            dropout_rate=0.0, rotary_emb_dims=0, activation="gelu", training=False,
+                            mode='upscale_in_train', trans_qkvw=True, ring_id=-1, norm_type="layernorm",
+                            use_neox_rotary_style=False, gqa_group_size=-1, name=None):
+    """A stack of transformer blocks in one call (reference incubate/nn/functional/
+    fused_transformer.py:964).  Per layer: (pre-)norm -> fused QKV GEMM -> attention -> out proj
+    -> residual -> (pre-)norm -> FFN1 -> activation -> FFN2 -> residual.
+
+    * context / prefill (time_step None): causal flash attention over the sequence (attn_mask,
+      if given, replaces the causal mask); with cache_kvs the K/V of every position are written
+      into cache_kvs[i] ([2, B, Hkv, max_len, D]);
+    * decode (time_step = t, x [B, 1, E]): the token's K/V are written at position t and it
+      attends over [0, t] on the split-K HIP decode kernel (attn_mask: additive [B, 1, 1, t+1]).
+    GEMMs go through ops.gemm.mm (hand-written MFMA kernel for large token counts), norms
+    through the fused norm kernels.  Returns out, or (out, cache_kvs) when caches are given."""
+    if beam_offset is not None or pre_caches is not None:
+        raise NotImplementedError("fused_multi_transformer: beam offsets / pre-caches are not supported")
+    if ring_id != -1:
+        raise NotImplementedError("fused_multi_transformer: use the mpu layers for tensor parallelism (ring_id)")
+    h = _u(x)
+    B, S, E = h.shape
+    nl = len(qkv_weights)
+    step = None if time_step is None else int(_u(time_step).reshape(-1)[0]) if isinstance(time_step, Tensor) or \
+        torch.is_tensor(time_step) else (None if time_step is None else int(time_step))
+
+    def norm(t, w, b):
+        if norm_type == 'rmsnorm':
+            return _u(fused_rms_norm(_w(t), w, b, epsilon))
+        return _u(F.layer_norm(_w(t), [E], w, b, epsilon))
+
+    def lin(t, w, b, trans=False):
+        t2 = t.reshape(-1, t.shape[-1])
+        wt = _u(w)
+        y = ops.gemm.mm(t2, wt.t() if trans else wt, bias=None)
+        if b is not None:
+            y = y + _u(b).reshape(1, -1)
+        return y
+
+    def act(t):
+        if activation == 'gelu':
+            return TF.gelu(t)
+        if activation == 'relu':
+            return torch.relu(t)
+        if activation in ('swiglu', 'geglu'):
+            a, g = t.chunk(2, -1)
+            return (TF.silu(a) if activation == 'swiglu' else TF.gelu(a)) * g
+        raise ValueError(f"unsupported activation {activation}")
+
+    caches_out = []
+    for i in range(nl):
+        resid = h
+        a = norm(h, ln_scales[i], ln_biases[i] if ln_biases is not None else None) if pre_layer_norm else h
+        w = _u(qkv_weights[i])
+        if trans_qkvw:
+            Wm = w.reshape(-1, E)                                  # [(Hq + 2 Hkv) * D, E]
+            qkv = lin(a, Wm, None, trans=True)
+        else:
+            Wm = w.reshape(E, -1)
+            qkv = lin(a, Wm, None)
+        if qkv_biases is not None and qkv_biases[i] is not None:
+            qkv = qkv + _u(qkv_biases[i]).reshape(1, -1)
+        if gqa_group_size > 0:
+            D = w.shape[-2] if trans_qkvw else w.shape[-1]
+            Hkv = gqa_group_size
+            Hq = qkv.shape[-1] // D - 2 * Hkv
+        else:
+            D = w.shape[2] if trans_qkvw else w.shape[-1]
+            Hq = Hkv = qkv.shape[-1] // (3 * D)
+        qkv = qkv.reshape(B, S, Hq + 2 * Hkv, D)
+        q, k, v = qkv[:, :, :Hq], qkv[:, :, Hq:Hq + Hkv], qkv[:, :, Hq + Hkv:]
+        if rotary_embs is not None and rotary_emb_dims > 0:
+            re = _u(rotary_embs).float().reshape(2, B, -1, D)      # [2, B, seq, D]
+            if step is None:
+                cos, sin = re[0][:, :S, None], re[1][:, :S, None]
+            else:
+                idx = min(step, re.shape[2] - 1)
+                cos, sin = re[0][:, idx:idx + 1, None], re[1][:, idx:idx + 1, None]
+            q = _rope_rows(q, cos, sin, use_neox_rotary_style)
+            k = _rope_rows(k, cos, sin, use_neox_rotary_style)
+        cache = _u(cache_kvs[i]) if cache_kvs is not None else None
+        if step is None:
+            if cache is not None:  # prefill: every position's K/V into the cache
+                pos = torch.arange(S, device=h.device, dtype=torch.int32).repeat(B)
+                seq = torch.arange(B, device=h.device, dtype=torch.int32).repeat_interleave(S)
+                if seq_lens is not None:
+                    sl = _u(seq_lens).reshape(-1).to(torch.int32)
+                    pos = torch.where(pos < sl.repeat_interleave(S), pos, torch.full_like(pos, -1))
+                ops.decode.kv_cache_write(k.reshape(B * S, Hkv, D), v.reshape(B * S, Hkv, D), cache[0], cache[1],
+                                          pos, seq_of=seq)
+            m = _u(attn_mask) if attn_mask is not None else None
+            o = _attend(q, k, v, m, 0.0, m is None, False)
+        else:
+            if cache is None:
+                raise ValueError("fused_multi_transformer decode (time_step) needs cache_kvs")
+            pos = torch.full((B,), step, dtype=torch.int32, device=h.device)
+            ops.decode.kv_cache_write(k[:, 0], v[:, 0], cache[0], cache[1], pos)
+            lens = pos + 1
+            m = None if attn_mask is None else _u(attn_mask).reshape(B, -1).float()
+            o = ops.decode.decode_attention(q[:, 0], cache[0], cache[1], lens, mask=m)[:, None]
+        if cache is not None:
+            caches_out.append(cache_kvs[i])
+        o = lin(o.reshape(B, S, Hq * D), linear_weights[i], linear_biases[i] if linear_biases is not None else None)
+        h = resid * residual_alpha + o.reshape(B, S, E).to(resid.dtype)
+        if not pre_layer_norm:
+            h = norm(h, ln_scales[i], ln_biases[i] if ln_biases is not None else None)
+        resid = h
+        f = norm(h, ffn_ln_scales[i], ffn_ln_biases[i] if ffn_ln_biases is not None else None) if pre_layer_norm \
+            else h
+        f = act(lin(f, ffn1_weights[i], ffn1_biases[i] if ffn1_biases is not None else None))
+        f = lin(f, ffn2_weights[i], ffn2_biases[i] if ffn2_biases is not None else None)
+        h = resid * residual_alpha + f.reshape(B, S, E).to(resid.dtype)
+        if not pre_layer_norm:
+            h = norm(h, ffn_ln_scales[i], ffn_ln_biases[i] if ffn_ln_biases is not None else None)
+    out = _w(h)
+    return (out, caches_out) if cache_kvs is not None else out
 
 
 def variable_length_memory_efficient_attention(query, key, value, seq_lens, kv_seq_lens, mask=None, scale=None,

@@ -117,69 +117,75 @@ class FusedTransformerEncoderLayer(Layer):
 
 
 class FusedMultiTransformer(Layer):
-    """Stack of pre-LN decoder blocks for inference (reference FusedMultiTransformer): per layer
-    ln → fused qkv → (cached) attention → out proj → residual → ln → ffn → residual."""
+    """Stack of transformer blocks for generation (reference incubate/nn/layer/fused_transformer.py:994):
+    parameters per layer in the reference shapes (qkv [3, H, D, E] with trans_qkvw, or
+    [(H + 2 Hkv), D, E] with gqa_group_size), forward = incubate.nn.functional.fused_multi_transformer
+    with caches [2, B, Hkv, max_len, D] updated in place and ``time_step`` selecting the decode step."""
 
     def __init__(self, embed_dim, num_heads, dim_feedforward, dropout_rate=0.0, activation="gelu",
                  normalize_before=True, ln_scale_attrs=None, ln_bias_attrs=None, qkv_weight_attrs=None,
                  qkv_bias_attrs=None, linear_weight_attrs=None, linear_bias_attrs=None, ffn_ln_scale_attrs=None,
                  ffn_ln_bias_attrs=None, ffn1_weight_attrs=None, ffn1_bias_attrs=None, ffn2_weight_attrs=None,
-                 ffn2_bias_attrs=None, epsilon=1e-5, num_layers=-1, nranks=1, trans_qkvw=True, ring_id=-1,
-                 name=None, **kw):
+                 ffn2_bias_attrs=None, epsilon=1e-5, residual_alpha=1.0, num_layers=-1, nranks=1, trans_qkvw=True,
+                 ring_id=-1, norm_type="layernorm", use_neox_rotary_style=False, gqa_group_size=-1, name=None):
         super().__init__()
-        from ...nn.layer.container import LayerList
-        self.num_layers = num_layers if num_layers > 0 else 1
+        assert embed_dim > 0 and num_heads > 0 and dim_feedforward > 0
+        if num_layers < 0:
+            num_layers = len(qkv_weight_attrs) if isinstance(qkv_weight_attrs, (list, tuple)) else 1
+        self.num_layers = num_layers
         self.embed_dim, self.num_heads = embed_dim, num_heads
         self.head_dim = embed_dim // num_heads
-        self.activation, self.epsilon = activation, epsilon
-        self.ln_scales, self.ln_biases, self.qkv_weights, self.qkv_biases = [], [], [], []
-        self.linear_weights, self.linear_biases, self.ffn_ln_scales, self.ffn_ln_biases = [], [], [], []
-        self.ffn1_weights, self.ffn1_biases, self.ffn2_weights, self.ffn2_biases = [], [], [], []
-        for i in range(self.num_layers):
-            mk = self.create_parameter
-            self.ln_scales.append(mk([embed_dim], default_initializer=I.Constant(1.0)))
-            self.ln_biases.append(mk([embed_dim], is_bias=True))
-            self.qkv_weights.append(mk([3, num_heads, self.head_dim, embed_dim]))
-            self.qkv_biases.append(mk([3, num_heads, self.head_dim], is_bias=True))
-            self.linear_weights.append(mk([embed_dim, embed_dim]))
-            self.linear_biases.append(mk([embed_dim], is_bias=True))
-            self.ffn_ln_scales.append(mk([embed_dim], default_initializer=I.Constant(1.0)))
-            self.ffn_ln_biases.append(mk([embed_dim], is_bias=True))
-            self.ffn1_weights.append(mk([embed_dim, dim_feedforward]))
-            self.ffn1_biases.append(mk([dim_feedforward], is_bias=True))
-            self.ffn2_weights.append(mk([dim_feedforward, embed_dim]))
-            self.ffn2_biases.append(mk([embed_dim], is_bias=True))
-            for n, lst in (('ln_scale', self.ln_scales), ('ln_bias', self.ln_biases), ('qkv_weight', self.qkv_weights),
-                           ('qkv_bias', self.qkv_biases), ('linear_weight', self.linear_weights),
-                           ('linear_bias', self.linear_biases), ('ffn_ln_scale', self.ffn_ln_scales),
-                           ('ffn_ln_bias', self.ffn_ln_biases), ('ffn1_weight', self.ffn1_weights),
-                           ('ffn1_bias', self.ffn1_biases), ('ffn2_weight', self.ffn2_weights),
-                           ('ffn2_bias', self.ffn2_biases)):
-                self.add_parameter(f"{n}_{i}", lst[-1])
+        self.activation, self.epsilon, self.residual_alpha = activation, epsilon, residual_alpha
+        self.normalize_before, self.trans_qkvw, self.norm_type = normalize_before, trans_qkvw, norm_type
+        self.use_neox_rotary_style, self.gqa_group_size = use_neox_rotary_style, gqa_group_size
+        self.dropout_rate = dropout_rate
+        H, D, E = num_heads, self.head_dim, embed_dim
+        nqkv = (H + 2 * gqa_group_size) if gqa_group_size > 0 else None
+        ffn1_out = dim_feedforward * 2 if activation in ('swiglu', 'geglu') else dim_feedforward
+        names = ['ln_scale', 'ln_bias', 'qkv_weight', 'qkv_bias', 'linear_weight', 'linear_bias', 'ffn_ln_scale',
+                 'ffn_ln_bias', 'ffn1_weight', 'ffn1_bias', 'ffn2_weight', 'ffn2_bias']
+        plural = {n: (n[:-4] + 'biases' if n.endswith('bias') else n + 's') for n in names}
+        for n in names:
+            setattr(self, plural[n], [])
 
-    def forward(self, src, attn_mask=None, caches=None, time_step=None, **kw):
-        x = src
-        B, S, E = _unwrap(x).shape
-        new_caches = []
-        for i in range(self.num_layers):
-            h = F.layer_norm(x, [E], self.ln_scales[i], self.ln_biases[i], self.epsilon)
-            w = _unwrap(self.qkv_weights[i])
-            qkv = torch.einsum('bse,thde->bsthd', _unwrap(h), w) + _unwrap(self.qkv_biases[i]).reshape(1, 1, 3,
-                                                                                                    self.num_heads,
-                                                                                                    self.head_dim)
-            q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
-            if caches is not None:
-                ck = _unwrap(caches[i])  # [2, B, S_past, H, D]
-                k = torch.cat([ck[0], k], 1)
-                v = torch.cat([ck[1], v], 1)
-                new_caches.append(_wrap(torch.stack([k, v])))
-            causal = attn_mask is None
-            o = F.scaled_dot_product_attention(_wrap(q), _wrap(k), _wrap(v), attn_mask, 0.0, causal, False)
-            o = F.linear(_wrap(_unwrap(o).reshape(B, S, E)), self.linear_weights[i], self.linear_biases[i])
-            x = _wrap(_unwrap(x) + _unwrap(o))
-            h = F.layer_norm(x, [E], self.ffn_ln_scales[i], self.ffn_ln_biases[i], self.epsilon)
-            h = F.linear(h, self.ffn1_weights[i], self.ffn1_biases[i])
-            h = getattr(F, self.activation)(h)
-            h = F.linear(h, self.ffn2_weights[i], self.ffn2_biases[i])
-            x = _wrap(_unwrap(x) + _unwrap(h))
-        return (x, new_caches) if caches is not None else x
+        def attr(a, i):
+            return a[i] if isinstance(a, (list, tuple)) else a
+
+        for i in range(num_layers):
+            mk = self.create_parameter
+            if nqkv is not None:
+                qkv_shape = [nqkv, D, E] if trans_qkvw else [E, nqkv, D]
+                qkvb_shape = [nqkv * D]
+            else:
+                qkv_shape = [3, H, D, E] if trans_qkvw else [E, 3, H, D]
+                qkvb_shape = [3, H, D]
+            vals = [mk([E], attr=attr(ln_scale_attrs, i), default_initializer=I.Constant(1.0)),
+                    mk([E], attr=attr(ln_bias_attrs, i), is_bias=True),
+                    mk(qkv_shape, attr=attr(qkv_weight_attrs, i)),
+                    mk(qkvb_shape, attr=attr(qkv_bias_attrs, i), is_bias=True),
+                    mk([H * D, E], attr=attr(linear_weight_attrs, i)),
+                    mk([E], attr=attr(linear_bias_attrs, i), is_bias=True),
+                    mk([E], attr=attr(ffn_ln_scale_attrs, i), default_initializer=I.Constant(1.0)),
+                    mk([E], attr=attr(ffn_ln_bias_attrs, i), is_bias=True),
+                    mk([E, ffn1_out], attr=attr(ffn1_weight_attrs, i)),
+                    mk([ffn1_out], attr=attr(ffn1_bias_attrs, i), is_bias=True),
+                    mk([dim_feedforward, E], attr=attr(ffn2_weight_attrs, i)),
+                    mk([E], attr=attr(ffn2_bias_attrs, i), is_bias=True)]
+            for n, v in zip(names, vals):
+                getattr(self, plural[n]).append(v)
+                self.add_parameter(f"{n}_{i}", v)
+
+    def forward(self, src, attn_mask=None, caches=None, pre_caches=None, rotary_embs=None, rotary_emb_dims=0,
+                beam_offset=None, seq_lens=None, time_step=None):
+        if caches is not None:
+            assert len(caches) == len(self.qkv_weights)
+        return IF.fused_multi_transformer(
+            src, self.ln_scales, self.ln_biases, self.qkv_weights, self.qkv_biases, self.linear_weights,
+            self.linear_biases, self.ffn_ln_scales, self.ffn_ln_biases, self.ffn1_weights, self.ffn1_biases,
+            self.ffn2_weights, self.ffn2_biases, pre_layer_norm=self.normalize_before, epsilon=self.epsilon,
+            residual_alpha=self.residual_alpha, cache_kvs=caches, beam_offset=beam_offset, pre_caches=pre_caches,
+            seq_lens=seq_lens, rotary_embs=rotary_embs, time_step=time_step, attn_mask=attn_mask,
+            dropout_rate=self.dropout_rate, rotary_emb_dims=rotary_emb_dims, activation=self.activation,
+            training=self.training, trans_qkvw=self.trans_qkvw, norm_type=self.norm_type,
+            use_neox_rotary_style=self.use_neox_rotary_style, gqa_group_size=self.gqa_group_size)
+

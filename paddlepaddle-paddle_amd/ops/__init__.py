@@ -35,3 +35,4 @@ def native_loaded():
 
 
 from . import norm, softmax, act, xent, embedding, rope, optim, flash_attn, gemm, linear, fused, batchnorm, conv, pool  # noqa: E402,F401,E501
+from . import decode  # noqa: E402,F401

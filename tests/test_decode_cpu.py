@@ -1,0 +1,153 @@
+"""Decode-phase attention APIs on CPU (torch reference paths; the HIP kernels are compared against
+the same references in tests/test_hip_kernels.py): masked_multihead_attention,
+block_multihead_attention over a paged cache, fused_multi_transformer / FusedMultiTransformer
+incremental decoding == full-sequence forward."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import paddle
+import paddle.incubate.nn.functional as IF
+from paddle.incubate.nn import FusedMultiTransformer
+from paddle.ops import decode
+
+
+def _attn(q, k, v, causal=True):
+    """q [S, H, D], k/v [L, Hkv, D] -> [S, H, D] (bottom-right causal)."""
+    S, H, D = q.shape
+    L, Hkv = k.shape[0], k.shape[1]
+    k = k.repeat_interleave(H // Hkv, 1)
+    v = v.repeat_interleave(H // Hkv, 1)
+    s = torch.einsum('shd,lhd->hsl', q.double(), k.double()) / math.sqrt(D)
+    if causal:
+        i = torch.arange(S)[:, None] + (L - S)
+        s = s.masked_fill(torch.arange(L)[None, :] > i, float('-inf'))
+    return torch.einsum('hsl,lhd->shd', torch.softmax(s, -1), v.double())
+
+
+def test_masked_multihead_attention_matches_reference():
+    torch.manual_seed(0)
+    B, H, L, D = 3, 4, 32, 16
+    cache = torch.randn(2, B, H, L, D)
+    x = torch.randn(B, 3 * H * D)
+    bias = torch.randn(3, H, D) * 0.1
+    steps = torch.tensor([[5], [0], [17]])
+    want_cache = cache.clone()
+    out, c = IF.masked_multihead_attention(paddle.to_tensor(x), paddle.to_tensor(cache), bias=paddle.to_tensor(bias),
+                                           sequence_lengths=paddle.to_tensor(steps))
+    qkv = x.reshape(B, 3, H, D) + bias
+    for b in range(B):
+        t = int(steps[b])
+        want_cache[0, b, :, t] = qkv[b, 1]
+        want_cache[1, b, :, t] = qkv[b, 2]
+        o = _attn(qkv[b, 0][None], want_cache[0, b, :, :t + 1].transpose(0, 1), want_cache[1, b, :, :t + 1].transpose(0, 1),
+                  causal=False)[0]
+        np.testing.assert_allclose(out.numpy()[b], o.reshape(-1).numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(c.numpy(), want_cache.numpy(), atol=1e-6)
+
+
+def test_decode_attention_paged_equals_contiguous():
+    torch.manual_seed(1)
+    B, Hq, Hkv, D, bs = 2, 4, 2, 8, 4
+    L = 12
+    kc = torch.randn(B, Hkv, L, D)
+    vc = torch.randn(B, Hkv, L, D)
+    nblk = B * L // bs
+    perm = torch.randperm(nblk)
+    bt = perm.reshape(B, L // bs)
+    kp = torch.empty(nblk, Hkv, bs, D)
+    vp = torch.empty(nblk, Hkv, bs, D)
+    for b in range(B):
+        for j in range(L // bs):
+            kp[bt[b, j]] = kc[b, :, j * bs:(j + 1) * bs]
+            vp[bt[b, j]] = vc[b, :, j * bs:(j + 1) * bs]
+    q = torch.randn(B, Hq, D)
+    lens = torch.tensor([7, 12])
+    a = decode.decode_attention(q, kc, vc, lens)
+    p = decode.decode_attention(q, kp, vp, lens, block_tables=bt)
+    np.testing.assert_allclose(a.numpy(), p.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def _get_padding_offset(this):
+    cu = torch.zeros(len(this) + 1, dtype=torch.int32)
+    cu[1:] = torch.cumsum(torch.tensor(this), 0)
+    return cu
+
+
+def test_block_multihead_attention_mixed_batch():
+    """two prompts (prefill into their blocks) + two decode tokens over their cached prefixes"""
+    torch.manual_seed(2)
+    Hq, Hkv, D, bs, nblk = 4, 2, 8, 4, 24
+    kc = torch.zeros(nblk, Hkv, bs, D)
+    vc = torch.zeros(nblk, Hkv, bs, D)
+    enc = [5, 0, 3, 0]
+    dec = [0, 6, 0, 9]
+    this = [5, 1, 3, 1]
+    bt = torch.arange(nblk).reshape(4, 6)
+    # pre-fill the decode sequences' prefixes
+    hist = {1: (torch.randn(6, Hkv, D), torch.randn(6, Hkv, D)), 3: (torch.randn(9, Hkv, D), torch.randn(9, Hkv, D))}
+    for b, (k, v) in hist.items():
+        for p in range(k.shape[0]):
+            kc[bt[b, p // bs], :, p % bs] = k[p]
+            vc[bt[b, p // bs], :, p % bs] = v[p]
+    T = sum(this)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D)
+    cu = _get_padding_offset(this)
+    out, _, kc2, vc2 = IF.block_multihead_attention(
+        paddle.to_tensor(qkv), paddle.to_tensor(kc), paddle.to_tensor(vc),
+        paddle.to_tensor(torch.tensor(enc)[:, None]), paddle.to_tensor(torch.tensor(dec)[:, None]),
+        paddle.to_tensor(torch.tensor(this)[:, None]), None, None, paddle.to_tensor(cu), paddle.to_tensor(cu),
+        paddle.to_tensor(bt), block_size=bs)
+    o = out.numpy()
+    for b in range(4):
+        s0, n = int(cu[b]), this[b]
+        rows = qkv[s0:s0 + n]
+        q = rows[:, :Hq * D].reshape(n, Hq, D)
+        k = rows[:, Hq * D:(Hq + Hkv) * D].reshape(n, Hkv, D)
+        v = rows[:, (Hq + Hkv) * D:].reshape(n, Hkv, D)
+        if b in hist:
+            k = torch.cat([hist[b][0], k])
+            v = torch.cat([hist[b][1], v])
+        want = _attn(q, k, v, causal=True)
+        np.testing.assert_allclose(o[s0:s0 + n], want.reshape(n, -1).numpy(), rtol=1e-4, atol=1e-5)
+        # the new tokens' K/V are in the cache at their positions
+        p_last = dec[b] + n - 1
+        np.testing.assert_allclose(kc2.numpy()[bt[b, p_last // bs], :, p_last % bs], k[-1].numpy(), atol=1e-6)
+
+
+@pytest.mark.parametrize("gqa", [-1, 2])
+@pytest.mark.parametrize("norm", ['layernorm', 'rmsnorm'])
+def test_fused_multi_transformer_incremental_decode(gqa, norm):
+    paddle.seed(3)
+    E, H, F_, nl, B, S, Lmax = 32, 4, 64, 2, 2, 6, 16
+    m = FusedMultiTransformer(E, H, F_, num_layers=nl, norm_type=norm, gqa_group_size=gqa)
+    m.eval()
+    Hkv = gqa if gqa > 0 else H
+    D = E // H
+    x = paddle.randn([B, S + 2, E])
+    full = m(x)  # causal forward over all S+2 positions (no cache)
+    caches = [paddle.zeros([2, B, Hkv, Lmax, D]) for _ in range(nl)]
+    out, caches = m(x[:, :S], caches=caches)
+    np.testing.assert_allclose(out.numpy(), full.numpy()[:, :S], rtol=1e-4, atol=1e-5)
+    for t in range(S, S + 2):
+        o, caches = m(x[:, t:t + 1], caches=caches, time_step=paddle.to_tensor([t]))
+        np.testing.assert_allclose(o.numpy()[:, 0], full.numpy()[:, t], rtol=1e-4, atol=1e-5)
+
+
+def test_fused_multi_transformer_functional_reference_shapes():
+    paddle.seed(4)
+    E, H, D = 16, 2, 8
+    x = paddle.randn([2, 3, E])
+    args = dict(ln_scales=[paddle.ones([E])], ln_biases=[paddle.zeros([E])],
+                qkv_weights=[paddle.randn([3, H, D, E]) * 0.1], qkv_biases=[paddle.zeros([3, H, D])],
+                linear_weights=[paddle.randn([E, E]) * 0.1], linear_biases=[paddle.zeros([E])],
+                ffn_ln_scales=[paddle.ones([E])], ffn_ln_biases=[paddle.zeros([E])],
+                ffn1_weights=[paddle.randn([E, 4 * E]) * 0.1], ffn1_biases=[paddle.zeros([4 * E])],
+                ffn2_weights=[paddle.randn([4 * E, E]) * 0.1], ffn2_biases=[paddle.zeros([E])])
+    out = IF.fused_multi_transformer(x, **args)
+    assert list(out.shape) == [2, 3, E]
+    mask = paddle.zeros([2, 1, 3, 3])
+    out2 = IF.fused_multi_transformer(x, attn_mask=mask, **args)  # explicit (non-causal) mask
+    assert not np.allclose(out.numpy(), out2.numpy())

@@ -777,3 +777,54 @@ def test_nhwc_max_pool2d_routes_to_hip():
     assert 'MaxPoolNHWC' in type(y._t.grad_fn).__name__ if y._t.grad_fn is not None else True
     ref = torch.nn.functional.max_pool2d(x._t.float().permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
     _close(y._t, ref, 0.0, name='F.max_pool2d NHWC')
+
+
+# ----------------------------------------------------------------------------- decode attention
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 8, 8), (128, 8, 2), (64, 16, 2), (256, 4, 4), (128, 40, 8), (64, 8, 1)])
+@pytest.mark.parametrize("paged", [False, True])
+def test_hip_decode_attention(dt, D, Hq, Hkv, paged):
+    """csrc/decode_attn.hip split-K decode kernel (contiguous and paged cache, GQA groups, additive
+    mask, ragged lengths incl. 0 and 1, many splits) vs the fp32 torch reference."""
+    from paddle.ops import decode
+    if not _native.lib.pa_decode_ok(1 if dt == torch.bfloat16 else 2, D, Hq // Hkv):
+        pytest.skip("group size outside the kernel's instantiations")
+    g = torch.Generator(device=DEV).manual_seed(D + Hq + Hkv)
+    B, L, bs = 5, 1500, 64
+    lens = torch.tensor([1, 700, 1500, 0, 257], device=DEV, dtype=torch.int32)
+    if paged:
+        nblk = B * L // bs + 8
+        kc = torch.randn(nblk, Hkv, bs, D, device=DEV, generator=g).to(dt)
+        vc = torch.randn(nblk, Hkv, bs, D, device=DEV, generator=g).to(dt)
+        bt = torch.randperm(nblk, device=DEV, generator=g)[:B * ((L + bs - 1) // bs)].reshape(B, -1).int()
+    else:
+        kc = torch.randn(B, Hkv, L, D, device=DEV, generator=g).to(dt)
+        vc = torch.randn(B, Hkv, L, D, device=DEV, generator=g).to(dt)
+        bt = None
+    q = torch.randn(B, Hq, D, device=DEV, generator=g).to(dt)
+    mask = torch.where(torch.rand(B, L, device=DEV, generator=g) < 0.1, -1e4, 0.0).float()
+    out = decode.decode_attention(q, kc, vc, lens, block_tables=bt, mask=mask)
+    ref = decode.decode_attention_ref(q, kc, vc, lens, block_tables=bt, mask=mask)
+    _close(out, ref, atol=2e-2, rtol=2e-2, name=f"decode D{D} G{Hq // Hkv} paged={paged}")
+
+
+def test_hip_kv_cache_write_and_fused_multi_transformer_decode():
+    """pa_kv_cache_write + the HIP decode kernel inside fused_multi_transformer: incremental decode on
+    the GPU matches the full causal forward."""
+    import paddle
+    from paddle.incubate.nn import FusedMultiTransformer
+    paddle.set_device('gpu:0')
+    paddle.seed(5)
+    E, H, F_, nl, B, S, Lmax = 256, 2, 512, 2, 4, 40, 64
+    m = FusedMultiTransformer(E, H, F_, num_layers=nl, gqa_group_size=1)
+    m.eval()
+    for p in m.parameters():
+        p._t.data = p._t.data.bfloat16()
+    x = paddle.to_tensor(torch.randn(B, S + 3, E, device=DEV).bfloat16() * 0.5)
+    full = m(x)
+    caches = [paddle.to_tensor(torch.zeros(2, B, 1, Lmax, E // H, device=DEV, dtype=torch.bfloat16)) for _ in range(nl)]
+    out, caches = m(x[:, :S], caches=caches)
+    _close(out._t, full._t[:, :S], atol=3e-2, rtol=3e-2, name="fmt prefill")
+    for t in range(S, S + 3):
+        o, caches = m(x[:, t:t + 1], caches=caches, time_step=paddle.to_tensor([t]))
+        _close(o._t[:, 0], full._t[:, t], atol=4e-2, rtol=4e-2, name=f"fmt decode step {t}")
