@@ -30,6 +30,8 @@ def parse():
     ap.add_argument('--seq', type=int, default=1024)
     ap.add_argument('--sharding', default='p_g_os', choices=['os', 'os_g', 'p_g_os', 'dp'])
     ap.add_argument('--dropout', type=float, default=0.1)
+    ap.add_argument('--attn-dropout', type=float, default=0.1,
+                    help='attention-probability dropout (in-kernel in csrc/flash_attn.hip)')
     ap.add_argument('--resnet-batch', type=int, default=256)
     ap.add_argument('--no-resnet', action='store_true')
     return ap.parse_args()
@@ -41,7 +43,7 @@ def build_gpt(args, world, rank, dev):
     import paddle.distributed as pdist
     from paddle.models.gpt import gpt_config, GPTForPretraining
     cfg = gpt_config(args.model, max_position_embeddings=max(args.seq, 1024), hidden_dropout_prob=args.dropout,
-                     attention_probs_dropout_prob=0.0)
+                     attention_probs_dropout_prob=args.attn_dropout)
     paddle.seed(1234)  # identical init on every rank
     model = GPTForPretraining(cfg)
     opt = paddle.optimizer.AdamW(learning_rate=1e-4, parameters=model.parameters(), weight_decay=0.01,
@@ -70,7 +72,7 @@ def build_gpt(args, world, rank, dev):
     mcfg = {'model': args.model, 'global_batch': B * world, 'micro_batch_per_gpu': B, 'seq_len': S,
             'parallelism': (f"sharding-{ {'os': 1, 'os_g': 2, 'p_g_os': 3}.get(args.sharding, 0)}x{world}"
                             if args.sharding != 'dp' else f"dp{world}"),
-            'hidden_dropout': args.dropout, 'attention_dropout': 0.0, 'optimizer': 'AdamW (fused, fp32 master)',
+            'hidden_dropout': args.dropout, 'attention_dropout': args.attn_dropout, 'optimizer': 'AdamW (fused, fp32 master)',
             'vocab': cfg.vocab_size}
     return step, B * S * world, 'tokens/sec GPT-3 1.3B sharding-3', 'tokens/s', mcfg
 

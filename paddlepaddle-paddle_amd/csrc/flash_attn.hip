@@ -137,13 +137,104 @@ struct Strides {
   long long b, s, h;
 };
 
+// Optional features (EXT kernels; the plain instantiations compile none of this):
+//  * varlen: cu_q / cu_k [B+1] token offsets of packed [total, H, D] tensors (batch strides
+//    ignored); per-sequence lengths, bottom-right causal alignment per sequence; LSE / delta
+//    laid out [Hq, total_q];
+//  * additive mask (fp32, or the activation dtype) at mask[b*mb + h*mh + q*mq + k] (broadcast
+//    dims have stride 0); -inf entries mask;
+//  * dropout on the normalised probabilities: keep(b, h, q, k) = hash(seed, offset, element)
+//    regenerated bit-identically by the backward kernels; the softmax statistics (LSE) are those
+//    of the undropped probabilities;
+//  * flashmask start-row indices (int32, rows[b*rb + h*rh + key]): key k is masked for queries
+//    q >= rows[k] (python/paddle/nn/functional/flash_attention.py:844
+//    flash_attention_with_sparse_mask), O(S) memory instead of a dense [S, S] mask.
+struct Extra {
+  const int* cu_q;
+  const int* cu_k;
+  int total_q;
+  const void* mask;
+  long long mb, mh, mq;
+  int mask_f32;
+  float p_drop;
+  uint32_t seed, offset;
+  uint32_t drop_thresh;  // keep when hash >= drop_thresh (= p_drop * 2^32)
+  float keep_scale;      // 1 / (1 - p_drop)
+  const int* rows;       // flashmask: key k masked for queries q >= rows[b*rb + h*rh + k]
+  long long rb, rh;
+};
+
+// flashmask column test (EXT & 8): true when (q, key) is masked by the start-row indices
+__device__ __forceinline__ int row_start(const Extra& ex, int b, int h, int key) {
+  return ex.rows[(long long)b * ex.rb + (long long)h * ex.rh + key];
+}
+
+template <typename T>
+__device__ __forceinline__ void mask4(const Extra& ex, int b, int h, int q, int k, float (&o)[4]) {
+  const long long i = (long long)b * ex.mb + (long long)h * ex.mh + (long long)q * ex.mq + k;
+  if (ex.mask_f32) {
+    const float* m = reinterpret_cast<const float*>(ex.mask) + i;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = m[r];
+  } else {
+    const T* m = reinterpret_cast<const T*>(ex.mask) + i;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = to_f(m[r]);
+  }
+}
+
+// mask values of keys k..k+3 (vector load when all four are in range, else per element)
+template <typename T>
+__device__ __forceinline__ void mask_row4(const Extra& ex, int b, int h, int q, int k, int Sk, float (&o)[4]) {
+  if (k + 3 < Sk) {
+    mask4<T>(ex, b, h, q, k, o);
+    return;
+  }
+  const long long i = (long long)b * ex.mb + (long long)h * ex.mh + (long long)q * ex.mq + k;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    o[r] = (k + r < Sk) ? (ex.mask_f32 ? reinterpret_cast<const float*>(ex.mask)[i + r]
+                                       : to_f(reinterpret_cast<const T*>(ex.mask)[i + r]))
+                        : 0.f;
+}
+
+// dropout keep-scale for element (bh, q, k): 1/(1-p) kept, 0 dropped (counter hash, no state)
+__device__ __forceinline__ float drop_z(const Extra& ex, int bh, int q, int k) {
+  const uint32_t hsh = hash3(ex.seed ^ (uint32_t)bh * 0x9E3779B9u, ex.offset + (uint32_t)q, (uint32_t)k);
+  return hsh < ex.drop_thresh ? 0.f : ex.keep_scale;
+}
+
+// per-sequence geometry: (q offset, Sq, k offset, Sk, LSE row base) of batch entry b
+struct Seq {
+  long long qo, ko, lrow;
+  int sq, sk;
+};
+template <bool EXT>
+__device__ __forceinline__ Seq seq_of(const Extra& ex, int b, int h, int Hq, int Sq, int Sk) {
+  Seq r;
+  if (EXT && ex.cu_q) {
+    r.qo = ex.cu_q[b];
+    r.ko = ex.cu_k[b];
+    r.sq = ex.cu_q[b + 1] - ex.cu_q[b];
+    r.sk = ex.cu_k[b + 1] - ex.cu_k[b];
+    r.lrow = (long long)h * ex.total_q + r.qo;
+  } else {
+    r.qo = r.ko = 0;
+    r.sq = Sq;
+    r.sk = Sk;
+    r.lrow = ((long long)b * Hq + h) * Sq;
+  }
+  return r;
+}
+
 // ============================================================================ forward
 // grid: (ceil(Sq/128), Hq, B), block 256 (4 waves x 32 query rows = 2 tiles of 16)
-template <typename T, int D, bool CAUSAL>
+template <typename T, int D, bool CAUSAL, int EXT = 0>
 __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                      const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
-                                                     float* __restrict__ LSE, int Sq, int Sk, int Hq, int Hk,
-                                                     Strides qs, Strides ks_, Strides vs, Strides os, float scale_log2) {
+                                                     float* __restrict__ LSE, int Sq_, int Sk_, int Hq, int Hk,
+                                                     Strides qs, Strides ks_, Strides vs, Strides os, float scale_log2,
+                                                     Extra ex = Extra{}) {
   constexpr int KS = D / 32;   // k-steps over head_dim
   constexpr int DB = D / 16;   // 16-wide d blocks
   __shared__ __attribute__((aligned(16))) char smem[2 * 64 * D * 2];
@@ -153,20 +244,27 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane >> 4;
-  const int nqb = (Sq + 127) / 128;
+  const int nqb = (Sq_ + 127) / 128;
   // grid (Hq, B, q-blocks): the q-block index is the slowest-dispatched dimension, so every
   // head's heaviest (late, causal) block is issued before any lighter one (longest-first order
   // over the whole grid: the tail of the launch is the short blocks)
   const int qb = nqb - 1 - (int)blockIdx.z;
   const int h = blockIdx.x, b = blockIdx.y;
   const int hk = h / (Hq / Hk);
+  const Seq sq_ = seq_of<EXT != 0>(ex, b, h, Hq, Sq_, Sk_);
+  const int Sq = sq_.sq, Sk = sq_.sk;
   const int q0 = qb * 128;
+  if (EXT && q0 >= Sq) return;  // varlen: this sequence is shorter
   const int qw0 = q0 + wave * 32;
   const int off = Sk - Sq;  // bottom-right causal alignment
+  // EXT: scores are brought to natural units (+ mask) right after QK^T, then exponentiated in
+  // base 2 with log2(e)
+  const float sl2 = (EXT & 2) ? kLog2e : scale_log2;
+  const float scale_n = scale_log2 / kLog2e;
 
-  const uint16_t* qbase = Q + b * qs.b + h * qs.h;
-  const uint16_t* kbase = K + b * ks_.b + hk * ks_.h;
-  const uint16_t* vbase = V + b * vs.b + hk * vs.h;
+  const uint16_t* qbase = Q + (EXT && ex.cu_q ? 0 : b * qs.b) + sq_.qo * qs.s + h * qs.h;
+  const uint16_t* kbase = K + (EXT && ex.cu_q ? 0 : b * ks_.b) + sq_.ko * ks_.s + hk * ks_.h;
+  const uint16_t* vbase = V + (EXT && ex.cu_q ? 0 : b * vs.b) + sq_.ko * vs.s + hk * vs.h;
 
   // Q fragments (B operand of S^T = K Q^T): lane holds Q[qw0 + 16t + (lane&15)][32ks + 8g .. +8]
   s16x8 qf[2][KS];
@@ -229,6 +327,31 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
         acc_s[1][j] = Mfma<T>::run(kf, qf[1][k], acc_s[1][j]);
       }
     }
+    if constexpr ((EXT & 2) != 0) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int q = qw0 + 16 * t + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float mv[4] = {0.f, 0.f, 0.f, 0.f};
+          if (q < Sq) mask_row4<T>(ex, b, h, q, k0 + 16 * j + 4 * g, Sk, mv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc_s[t][j][r] = acc_s[t][j][r] * scale_n + mv[r];
+        }
+      }
+    }
+    if constexpr ((EXT & 8) != 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 16 * j + 4 * g + r;
+          const int rs = key < Sk ? row_start(ex, b, h, key) : 0;
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+            if (qw0 + 16 * t + (lane & 15) >= rs) acc_s[t][j][r] = -INFINITY;
+        }
+    }
     // online softmax in the log2 domain.  Masking only on tiles that touch the diagonal or the
     // ragged end (wave-uniform test); the scale is folded into the exponent's FMA; the running
     // max moves lazily (kRescaleTau) so the O/l rescale is skipped on most tiles.
@@ -256,7 +379,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
         for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc_s[t][j][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      mnew[t] = mx * scale_log2;
+      mnew[t] = mx * sl2;
     }
     const bool bump = (mnew[0] > m_run[0] + kRescaleTau) || (mnew[1] > m_run[1] + kRescaleTau);
     if (__ballot(bump) != 0ull) {
@@ -280,10 +403,17 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          p[j][r] = fast_exp2(__builtin_fmaf(acc_s[t][j][r], scale_log2, neg_m));
+          p[j][r] = fast_exp2(__builtin_fmaf(acc_s[t][j][r], sl2, neg_m));
           ls += p[j][r];
         }
       l_run[t] += ls;
+      if constexpr ((EXT & 4) != 0) {  // dropout after the (undropped) row sum
+        const int q = qw0 + 16 * t + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) p[j][r] *= drop_z(ex, b * Hq + h, q, k0 + 16 * j + 4 * g + r);
+      }
       // P^T as B operand: k-step s covers keys 32s..32s+31; element j<4 → (16*(2s)+4g+j), j>=4 → (16*(2s+1)+4g+j-4)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -314,7 +444,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
     const float inv = l > 0.f ? 1.f / l : 0.f;
     const int q = qw0 + 16 * t + (lane & 15);
     if (q < Sq) {
-      uint16_t* orow = O + b * os.b + h * os.h + (long long)q * os.s;
+      uint16_t* orow = O + (EXT && ex.cu_q ? 0 : b * os.b) + h * os.h + (sq_.qo + q) * os.s;
 #pragma unroll
       for (int d = 0; d < DB; ++d) {
         s16x4 o;
@@ -324,7 +454,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
       }
       if (g == 0) {
         const float mm = (m_run[t] == -INFINITY) ? 0.f : m_run[t];
-        LSE[((long long)b * Hq + h) * Sq + q] = l > 0.f ? (mm + log2f(l)) * kLn2 : -INFINITY;
+        LSE[sq_.lrow + q] = l > 0.f ? (mm + log2f(l)) * kLn2 : -INFINITY;
       }
     }
   }
@@ -364,12 +494,12 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const uint16_t* __restri
 // NT = 2 halves the LDS bytes per MFMA (every Q / dO fragment read from LDS feeds two key tiles)
 // at one wave per SIMD (the accumulators of 32 keys x D need the full register file).
 // dK/dV are written per q-head ([B, Sk, Hq, D] strides given by dks/dvs); GQA sums outside.
-template <typename T, int D, bool CAUSAL, int NT, int NW = 4>
+template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
-    uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq, int Sk, int Hq, int Hk, Strides qs, Strides ks_,
-    Strides vs, Strides dos, Strides dks, Strides dvs, float scale) {
+    uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq_, int Sk_, int Hq, int Hk, Strides qs, Strides ks_,
+    Strides vs, Strides dos, Strides dks, Strides dvs, float scale, Extra ex = Extra{}) {
   constexpr int KS = D / 32;
   constexpr int DB = D / 16;
   // D = 128: tiles read both by rows (ds_read_b128) and by columns (tr_b16) use the chunk ^
@@ -388,13 +518,19 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
   // grid (Hq, B, key-blocks): early key blocks (the most causal queries) dispatched first
   const int h = blockIdx.x, b = blockIdx.y;
   const int hk = h / (Hq / Hk);
+  const Seq sq_ = seq_of<EXT != 0>(ex, b, h, Hq, Sq_, Sk_);
+  const int Sq = sq_.sq, Sk = sq_.sk;
   const int k0 = blockIdx.z * 16 * NT * NW;
+  if (EXT && k0 >= Sk) return;
   const int kw = k0 + wave * 16 * NT;
   const int off = Sk - Sq;
   const float scale_log2 = scale * kLog2e;
+  const bool vl = EXT && ex.cu_q;
 
-  const uint16_t* qbase = Q + b * qs.b + h * qs.h;
-  const uint16_t* dobase = dO + b * dos.b + h * dos.h;
+  const uint16_t* qbase = Q + (vl ? 0 : b * qs.b) + sq_.qo * qs.s + h * qs.h;
+  const uint16_t* dobase = dO + (vl ? 0 : b * dos.b) + sq_.qo * dos.s + h * dos.h;
+  K += (vl ? 0 : b * ks_.b) + sq_.ko * ks_.s;
+  V += (vl ? 0 : b * vs.b) + sq_.ko * vs.s;
   // K, V of this wave's keys as B operands: lane holds K[key][32ks + 8g .. +8]
   s16x8 kf[NT][KS], vf[NT][KS];
 #pragma unroll
@@ -403,8 +539,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
       if (key < Sk) {
-        kf[j][k] = *reinterpret_cast<const s16x8*>(K + b * ks_.b + hk * ks_.h + (long long)key * ks_.s + 32 * k + 8 * g);
-        vf[j][k] = *reinterpret_cast<const s16x8*>(V + b * vs.b + hk * vs.h + (long long)key * vs.s + 32 * k + 8 * g);
+        kf[j][k] = *reinterpret_cast<const s16x8*>(K + hk * ks_.h + (long long)key * ks_.s + 32 * k + 8 * g);
+        vf[j][k] = *reinterpret_cast<const s16x8*>(V + hk * vs.h + (long long)key * vs.s + 32 * k + 8 * g);
       } else {
         kf[j][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
         vf[j][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
@@ -419,11 +555,17 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
       acc_dk[j][d] = f32x4{0.f, 0.f, 0.f, 0.f};
       acc_dv[j][d] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+  int rstart[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int key = kw + 16 * j + (lane & 15);
+    rstart[j] = ((EXT & 8) != 0 && key < Sk) ? row_start(ex, b, h, key) : 0x7fffffff;
+  }
   int qstart = 0;
   if (CAUSAL) qstart = max(0, (k0 - off) / 64 * 64);
   const int nqb = (Sq - qstart + 63) / 64;
-  const float* lse_b = LSE + ((long long)b * Hq + h) * Sq;
-  const float* dl_b = Delta + ((long long)b * Hq + h) * Sq;
+  const float* lse_b = LSE + sq_.lrow;
+  const float* dl_b = Delta + sq_.lrow;
 
   Tile<D, 64 * NW> qt, dot;
   qt.init(qbase, qs.s);
@@ -439,7 +581,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
     dot.template store<BT>(do_lds);
     if (threadIdx.x < 64) {
       const int q = q0 + threadIdx.x;
-      lse_lds[threadIdx.x] = q < Sq ? lse_b[q] * kLog2e : INFINITY;
+      // a fully masked row (LSE = -inf) has P = 0: +inf makes every exp2 below vanish
+      const float lv = q < Sq ? lse_b[q] : -INFINITY;
+      lse_lds[threadIdx.x] = lv == -INFINITY ? INFINITY : lv * kLog2e;
       dl_lds[threadIdx.x] = q < Sq ? dl_b[q] : 0.f;
     }
     __syncthreads();
@@ -485,14 +629,29 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
         const int mykey = kw + 16 * j + (lane & 15);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float p = fast_exp2(__builtin_fmaf(acc_s[j][m][r], scale_log2, -lsev[r]));
+          const int q = q0 + 16 * m + 4 * g + r;
+          float sv = acc_s[j][m][r];
+          float sl = scale_log2;
+          if constexpr ((EXT & 2) != 0) {  // natural units + mask, then base-2
+            float mv = 0.f;
+            if (q < Sq && mykey < Sk) {
+              const long long mi = (long long)b * ex.mb + (long long)h * ex.mh + (long long)q * ex.mq + mykey;
+              mv = ex.mask_f32 ? reinterpret_cast<const float*>(ex.mask)[mi]
+                               : to_f(reinterpret_cast<const T*>(ex.mask)[mi]);
+            }
+            sv = sv * scale + mv;
+            sl = kLog2e;
+          }
+          float p = fast_exp2(__builtin_fmaf(sv, sl, -lsev[r]));
           if (need_mask) {
-            const int q = q0 + 16 * m + 4 * g + r;
             const bool masked = (q >= Sq) || (mykey >= Sk) || (CAUSAL && mykey > q + off);
             p = masked ? 0.f : p;
           }
-          const float ds = p * (acc_dp[j][m][r] - dlv[r]);
-          pb[j][m >> 1][(m & 1) * 4 + r] = f2s<T>(p);
+          if constexpr ((EXT & 8) != 0) p = q >= rstart[j] ? 0.f : p;
+          float z = 1.f;
+          if constexpr ((EXT & 4) != 0) z = drop_z(ex, b * Hq + h, q, mykey);
+          const float ds = p * (acc_dp[j][m][r] * z - dlv[r]);
+          pb[j][m >> 1][(m & 1) * 4 + r] = f2s<T>(p * z);
           db_[j][m >> 1][(m & 1) * 4 + r] = f2s<T>(ds);
         }
       }
@@ -517,8 +676,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
   for (int j = 0; j < NT; ++j) {
     const int mykey = kw + 16 * j + (lane & 15);
     if (mykey < Sk) {
-      uint16_t* dkrow = dK + b * dks.b + h * dks.h + (long long)mykey * dks.s;
-      uint16_t* dvrow = dV + b * dvs.b + h * dvs.h + (long long)mykey * dvs.s;
+      uint16_t* dkrow = dK + (vl ? 0 : b * dks.b) + h * dks.h + (sq_.ko + mykey) * dks.s;
+      uint16_t* dvrow = dV + (vl ? 0 : b * dvs.b) + h * dvs.h + (sq_.ko + mykey) * dvs.s;
 #pragma unroll
       for (int d = 0; d < DB; ++d) {
         s16x4 a, c;
@@ -536,12 +695,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
 
 // dQ: grid (ceil(Sq / (16*NT*NW)), Hq, B); NW waves x (16*NT) queries; loop over 64-key blocks
 // (swapped products: lane owns a query).  NT = 2: every K / V fragment read feeds two query tiles.
-template <typename T, int D, bool CAUSAL, int NT, int NW = 4>
+template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
-    uint16_t* __restrict__ dQ, int Sq, int Sk, int Hq, int Hk, Strides qs, Strides ks_, Strides vs, Strides dos,
-    Strides dqs, float scale) {
+    uint16_t* __restrict__ dQ, int Sq_, int Sk_, int Hq, int Hk, Strides qs, Strides ks_, Strides vs, Strides dos,
+    Strides dqs, float scale, Extra ex = Extra{}) {
   constexpr int KS = D / 32;
   constexpr int DB = D / 16;
   // D = 128: tiles read both by rows (ds_read_b128) and by columns (tr_b16) use the chunk ^
@@ -554,33 +713,39 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane >> 4;
-  const int nqb = (Sq + 16 * NT * NW - 1) / (16 * NT * NW);
+  const int nqb = (Sq_ + 16 * NT * NW - 1) / (16 * NT * NW);
   const int qb = nqb - 1 - (int)blockIdx.z;  // grid (Hq, B, q-blocks): heaviest first
   const int h = blockIdx.x, b = blockIdx.y;
   const int hk = h / (Hq / Hk);
+  const Seq sq_ = seq_of<EXT != 0>(ex, b, h, Hq, Sq_, Sk_);
+  const int Sq = sq_.sq, Sk = sq_.sk;
   const int q0 = qb * 16 * NT * NW;
+  if (EXT && q0 >= Sq) return;
   const int qw = q0 + wave * 16 * NT;
   const int off = Sk - Sq;
   const float scale_log2 = scale * kLog2e;
+  const bool vl = EXT && ex.cu_q;
+  Q += (vl ? 0 : b * qs.b) + sq_.qo * qs.s;
+  dO += (vl ? 0 : b * dos.b) + sq_.qo * dos.s;
 
   s16x8 qf[NT][KS], dof[NT][KS];
   float lse2[NT], dlt[NT];
-  const long long lrow = ((long long)b * Hq + h) * Sq;
+  const long long lrow = sq_.lrow;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int myq = qw + 16 * t + (lane & 15);
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
       if (myq < Sq) {
-        qf[t][k] = *reinterpret_cast<const s16x8*>(Q + b * qs.b + h * qs.h + (long long)myq * qs.s + 32 * k + 8 * g);
-        dof[t][k] =
-            *reinterpret_cast<const s16x8*>(dO + b * dos.b + h * dos.h + (long long)myq * dos.s + 32 * k + 8 * g);
+        qf[t][k] = *reinterpret_cast<const s16x8*>(Q + h * qs.h + (long long)myq * qs.s + 32 * k + 8 * g);
+        dof[t][k] = *reinterpret_cast<const s16x8*>(dO + h * dos.h + (long long)myq * dos.s + 32 * k + 8 * g);
       } else {
         qf[t][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
         dof[t][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
       }
     }
-    lse2[t] = myq < Sq ? LSE[lrow + myq] * kLog2e : INFINITY;
+    const float lv = myq < Sq ? LSE[lrow + myq] : -INFINITY;
+    lse2[t] = lv == -INFINITY ? INFINITY : lv * kLog2e;
     dlt[t] = myq < Sq ? Delta[lrow + myq] : 0.f;
   }
   f32x4 acc[NT][DB];
@@ -589,8 +754,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
 #pragma unroll
     for (int d = 0; d < DB; ++d) acc[t][d] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const uint16_t* kbase = K + b * ks_.b + hk * ks_.h;
-  const uint16_t* vbase = V + b * vs.b + hk * vs.h;
+  const uint16_t* kbase = K + (vl ? 0 : b * ks_.b) + sq_.ko * ks_.s + hk * ks_.h;
+  const uint16_t* vbase = V + (vl ? 0 : b * vs.b) + sq_.ko * vs.s + hk * vs.h;
   int kend = Sk;
   if (CAUSAL) kend = min(Sk, q0 + 16 * NT * NW + off);
   const int nkb = kend > 0 ? (kend + 63) / 64 : 0;
@@ -640,15 +805,23 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
       const int myq = qw + 16 * t + (lane & 15);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
+        float mv[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr ((EXT & 2) != 0)
+          if (myq < Sq) mask_row4<T>(ex, b, h, myq, k0 + 16 * j + 4 * g, Sk, mv);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float p = fast_exp2(__builtin_fmaf(acc_s[t][j][r], scale_log2, -lse2[t]));
+          const int key = k0 + 16 * j + 4 * g + r;
+          const float sv = (EXT & 2) ? acc_s[t][j][r] * scale + mv[r] : acc_s[t][j][r];
+          float p = fast_exp2(__builtin_fmaf(sv, (EXT & 2) ? kLog2e : scale_log2, -lse2[t]));
           if (need_mask) {
-            const int key = k0 + 16 * j + 4 * g + r;
             const bool masked = (key >= Sk) || (myq >= Sq) || (CAUSAL && key > myq + off);
             p = masked ? 0.f : p;
           }
-          dsb[t][j >> 1][(j & 1) * 4 + r] = f2s<T>(p * (acc_dp[t][j][r] - dlt[t]));
+          if constexpr ((EXT & 8) != 0)
+            if (key < Sk && myq >= row_start(ex, b, h, key)) p = 0.f;
+          float z = 1.f;
+          if constexpr ((EXT & 4) != 0) z = drop_z(ex, b * Hq + h, myq, key);
+          dsb[t][j >> 1][(j & 1) * 4 + r] = f2s<T>(p * (acc_dp[t][j][r] * z - dlt[t]));
         }
       }
     }
@@ -667,7 +840,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
   for (int t = 0; t < NT; ++t) {
     const int myq = qw + 16 * t + (lane & 15);
     if (myq < Sq) {
-      uint16_t* row = dQ + b * dqs.b + h * dqs.h + (long long)myq * dqs.s;
+      uint16_t* row = dQ + (vl ? 0 : b * dqs.b) + h * dqs.h + (sq_.qo + myq) * dqs.s;
 #pragma unroll
       for (int d = 0; d < DB; ++d) {
         s16x4 o;
@@ -780,6 +953,116 @@ PA_API hipError_t pa_flash_bwd(const void* q, const void* k, const void* v, cons
       bwd_dq_kernel<T, DD, CC, 1><<<g2, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                                                       (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk, Hq,
                                                       Hk, qs, ks, vs, dos, dqs, scale);
+    }
+  });
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- extended entry points
+// Varlen (cu_q / cu_k != null: q/k/v/o packed [total, H, D], B = number of sequences, Sq/Sk =
+// max lengths, LSE / delta [Hq, total_q]), additive masks (fp32 or the activation dtype, element
+// strides mb/mh/mq, unit key stride) and in-kernel dropout (p_drop > 0, counter-hash keep mask
+// regenerated in backward).
+static Extra make_extra(const int* cu_q, const int* cu_k, int total_q, const void* mask, long long mb, long long mh,
+                        long long mq, int mask_f32, float p_drop, unsigned seed, unsigned offset,
+                        const int* rows, long long rb, long long rh) {
+  Extra e;
+  e.rows = rows;
+  e.rb = rb;
+  e.rh = rh;
+  e.cu_q = cu_q;
+  e.cu_k = cu_k;
+  e.total_q = total_q;
+  e.mask = mask;
+  e.mb = mb;
+  e.mh = mh;
+  e.mq = mq;
+  e.mask_f32 = mask_f32;
+  e.p_drop = p_drop;
+  e.seed = seed;
+  e.offset = offset;
+  const double th = (double)p_drop * 4294967296.0;
+  e.drop_thresh = th >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)th;
+  e.keep_scale = p_drop < 1.f ? 1.f / (1.f - p_drop) : 0.f;
+  return e;
+}
+
+PA_API hipError_t pa_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, float* lse, int B, int Sq,
+                                  int Sk, int Hq, int Hk, int D, const long long* qst, const long long* kst,
+                                  const long long* vst, const long long* ost, float scale, int causal, int dt,
+                                  const int* cu_q, const int* cu_k, int total_q, const void* mask, long long mb,
+                                  long long mh, long long mq, int mask_f32, float p_drop, unsigned seed,
+                                  unsigned offset, const int* rows, long long rb, long long rh, hipStream_t st) {
+  if (Hk <= 0 || Hq % Hk != 0 || (cu_q == nullptr) != (cu_k == nullptr)) return hipErrorInvalidValue;
+  Strides qs{qst[0], qst[1], qst[2]}, ks{kst[0], kst[1], kst[2]}, vs{vst[0], vst[1], vst[2]}, os{ost[0], ost[1], ost[2]};
+  if (mask && rows) return hipErrorInvalidValue;  // one mask form per call
+  const Extra ex = make_extra(cu_q, cu_k, total_q, mask, mb, mh, mq, mask_f32, p_drop, seed, offset, rows, rb, rh);
+  dim3 grid(Hq, B, (Sq + 127) / 128);
+  const int feat = 1 | (mask ? 2 : 0) | (p_drop > 0.f ? 4 : 0) | (rows ? 8 : 0);
+#define FA_FWD_EX(F)                                                                                            \
+  fwd_kernel<T, DD, CC, F><<<grid, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,    \
+                                                 (uint16_t*)o, lse, Sq, Sk, Hq, Hk, qs, ks, vs, os, scale * kLog2e, \
+                                                 ex)
+  FA_DISPATCH(dt, D, causal, {
+    switch (feat) {
+      case 1: FA_FWD_EX(1); break;
+      case 3: FA_FWD_EX(3); break;
+      case 5: FA_FWD_EX(5); break;
+      case 7: FA_FWD_EX(7); break;
+      case 9: FA_FWD_EX(9); break;
+      default: FA_FWD_EX(13); break;
+    }
+  });
+#undef FA_FWD_EX
+  return hipGetLastError();
+}
+
+// dK/dV + dQ launches of one feature set (D = 128: 8-wave blocks, D = 64: 4-wave blocks)
+template <typename T, int DD, bool CC, int F>
+static void bwd_ex(const void* q, const void* k, const void* v, const void* dout, const float* lse, float* delta,
+                   void* dq, void* dk, void* dv, int B, int Sq, int Sk, int Hq, int Hk, Strides qs, Strides ks,
+                   Strides vs, Strides dos, Strides dqs, Strides dks, Strides dvs, float scale, const Extra& ex,
+                   hipStream_t st) {
+  constexpr int NW = DD == 128 ? 8 : 4;
+  dim3 g1(Hq, B, (Sk + 16 * NW - 1) / (16 * NW));
+  bwd_dkdv_kernel<T, DD, CC, 1, NW, F><<<g1, 64 * NW, 0, st>>>(
+      (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk,
+      (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs, scale, ex);
+  dim3 g2(Hq, B, (Sq + 16 * NW - 1) / (16 * NW));
+  bwd_dq_kernel<T, DD, CC, 1, NW, F><<<g2, 64 * NW, 0, st>>>((const uint16_t*)q, (const uint16_t*)k,
+                                                             (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                                                             (uint16_t*)dq, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs,
+                                                             scale, ex);
+}
+
+PA_API hipError_t pa_flash_bwd_ex(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                                  const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk,
+                                  int Hq, int Hk, int D, const long long* qst, const long long* kst,
+                                  const long long* vst, const long long* ost, const long long* dost,
+                                  const long long* dqst, const long long* dkst, const long long* dvst, float scale,
+                                  int causal, int dt, const int* cu_q, const int* cu_k, int total_q, const void* mask,
+                                  long long mb, long long mh, long long mq, int mask_f32, float p_drop, unsigned seed,
+                                  unsigned offset, const int* rows, long long rb, long long rh, hipStream_t st) {
+  if (Hk <= 0 || Hq % Hk != 0 || (cu_q == nullptr) != (cu_k == nullptr)) return hipErrorInvalidValue;
+  Strides qs{qst[0], qst[1], qst[2]}, ks{kst[0], kst[1], kst[2]}, vs{vst[0], vst[1], vst[2]},
+      os{ost[0], ost[1], ost[2]}, dos{dost[0], dost[1], dost[2]}, dqs{dqst[0], dqst[1], dqst[2]},
+      dks{dkst[0], dkst[1], dkst[2]}, dvs{dvst[0], dvst[1], dvst[2]};
+  if (mask && rows) return hipErrorInvalidValue;  // one mask form per call
+  const Extra ex = make_extra(cu_q, cu_k, total_q, mask, mb, mh, mq, mask_f32, p_drop, seed, offset, rows, rb, rh);
+  // delta rows: [B, Hq, Sq] or, varlen, [Hq, total_q] (one "batch" of total_q packed rows)
+  const int dB = cu_q ? 1 : B, dS = cu_q ? total_q : Sq;
+  const long long nrows = (long long)dB * Hq * dS;
+  FA_DISPATCH(dt, D, causal, {
+    bwd_delta_kernel<T, DD><<<(int)((nrows + 15) / 16), 256, 0, st>>>((const uint16_t*)dout, (const uint16_t*)o, delta,
+                                                                      dB, dS, Hq, dos, os);
+    const int feat = 1 | (mask ? 2 : 0) | (p_drop > 0.f ? 4 : 0) | (rows ? 8 : 0);
+    switch (feat) {
+      case 1: bwd_ex<T, DD, CC, 1>(q, k, v, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, dks, dvs, scale, ex, st); break;
+      case 3: bwd_ex<T, DD, CC, 3>(q, k, v, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, dks, dvs, scale, ex, st); break;
+      case 5: bwd_ex<T, DD, CC, 5>(q, k, v, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, dks, dvs, scale, ex, st); break;
+      case 7: bwd_ex<T, DD, CC, 7>(q, k, v, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, dks, dvs, scale, ex, st); break;
+      case 9: bwd_ex<T, DD, CC, 9>(q, k, v, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, dks, dvs, scale, ex, st); break;
+      default: bwd_ex<T, DD, CC, 13>(q, k, v, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, dks, dvs, scale, ex, st); break;
     }
   });
   return hipGetLastError();

@@ -42,11 +42,15 @@ NAME_TABLE = 'StructuredToParameterName@@'
 UNPACK_INFO = 'UnpackBigParamInfor@@'
 
 
+class _Refused(pickle.UnpicklingError, ValueError):
+    """A pickle that names a callable outside the tensor-container allow-list."""
+
+
 class _RestrictedUnpickler(pickle.Unpickler):
     def find_class(self, module, name):
         if (module, name) in _SAFE:
             return super().find_class(module, name)
-        raise pickle.UnpicklingError(f"paddle.load refuses to resolve {module}.{name} (not a tensor container)")
+        raise _Refused(f"paddle.load refuses to resolve {module}.{name} (not a tensor container)")
 
 
 def _ndarray(t):
@@ -245,6 +249,8 @@ def load(path, **configs):
         data = path.read()
     try:
         obj = _RestrictedUnpickler(_io.BytesIO(data), encoding='latin1').load()
+    except _Refused:
+        raise
     except (pickle.UnpicklingError, EOFError, ValueError, IndexError, KeyError) as e:
         # not a pickle: a serialized Program / binary tensor (static formats)
         from ..static.io import load_binary_object

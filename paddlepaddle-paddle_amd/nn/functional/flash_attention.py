@@ -52,11 +52,50 @@ def _sdpa_reference(q, k, v, mask, dropout_p, causal, scale=None):
     return out.transpose(1, 2)
 
 
+def _pad_head(q, k, v):
+    """Head dims the kernels do not tile (e.g. 80, 96) are zero-padded to the next tiled one
+    (64 / 128): the extra q·k terms are 0 and the extra output columns are sliced off."""
+    D = q.shape[-1]
+    Dp = 64 if D <= 64 else 128 if D <= 128 else D
+    if Dp == D:
+        return q, k, v, D
+    return (TF.pad(q, (0, Dp - D)), TF.pad(k, (0, Dp - D)), TF.pad(v, (0, Dp - D)), D)
+
+
+def _hip_ok(q, k, v):
+    if not ops.use_hip(q):
+        return False
+    D = q.shape[-1]
+    Dp = 64 if D <= 64 else 128 if D <= 128 else D
+    # shape/dtype contract of the kernels, checked on the (padded) operand geometry
+    return (q.dtype in (torch.bfloat16, torch.float16) and k.dtype == q.dtype and v.dtype == q.dtype
+            and Dp in (64, 128) and k.shape[-1] == D and v.shape[-1] == D and k.shape == v.shape
+            and k.shape[-2] > 0 and q.shape[-2] % k.shape[-2] == 0)
+
+
+def _kernel_attend(q, k, v, causal, scale, mask=None, dropout=0.0, cu_q=None, cu_k=None, max_q=None, max_k=None,
+                   start_rows=None):
+    """HIP flash attention on BSHD (or packed varlen [total, H, D]) with optional mask /
+    dropout / flashmask rows; pads unsupported head dims."""
+    q, k, v, D = _pad_head(q, k, v)
+    if scale is None:
+        scale = 1.0 / math.sqrt(D)
+    if not ops.flash_attn.supported(*(t.unsqueeze(0) if t.dim() == 3 else t for t in (q, k, v))):
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+    plain = mask is None and dropout == 0.0 and cu_q is None and start_rows is None
+    if plain:
+        out = ops.flash_attn.flash_attention(q, k, v, causal, scale)
+    else:
+        out = ops.flash_attn.flash_attention_ex(q, k, v, causal, scale, mask, dropout, cu_q, cu_k, max_q, max_k,
+                                                start_rows)
+    return out if out.shape[-1] == D else out[..., :D]
+
+
 def _attend(q, k, v, mask=None, dropout=0.0, causal=False, training=True, scale=None):
     if not training:
         dropout = 0.0
-    if mask is None and dropout == 0.0 and ops.use_hip(q) and ops.flash_attn.supported(q, k, v):
-        return ops.flash_attn.flash_attention(q, k, v, causal, scale)
+    if _hip_ok(q, k, v) and (mask is None or mask.dim() <= 4):
+        return _kernel_attend(q, k, v, causal, scale, mask, dropout)
     return _sdpa_reference(q, k, v, mask, dropout, causal, scale)
 
 
@@ -79,28 +118,48 @@ def flash_attn_qkvpacked(qkv, dropout=0.0, causal=False, return_softmax=False, *
     b, s = t.shape[0], t.shape[1]
     q = t[:, :, :-2].reshape(b, s, -1, t.shape[-1])
     k, v = t[:, :, -2], t[:, :, -1]
-    if (t.dim() == 5 and t.shape[2] == 3 and not return_softmax and (dropout == 0.0 or not training)
-            and ops.use_hip(t) and ops.flash_attn.supported(q, k, v)):
-        return _w(ops.flash_attn.flash_attention_packed(t, causal)), None
+    p = dropout if training else 0.0
+    if t.dim() == 5 and t.shape[2] == 3 and not return_softmax and ops.use_hip(t) and ops.flash_attn.supported(q, k, v):
+        # one packed gradient for the fused QKV projection (no per-view grad fill / copies)
+        if p == 0.0:
+            return _w(ops.flash_attn.flash_attention_packed(t, causal)), None
+        return _w(ops.flash_attn.flash_attention_packed_ex(t, causal, dropout=p)), None
     return flash_attention(_w(q), _w(k), _w(v), dropout, causal, return_softmax, training=training)
+
+
+def _unpadded_reference(q, k, v, cq, ck, scale, dropout, causal, training):
+    cq, ck = cq.tolist(), ck.tolist()
+    out = torch.zeros(q.shape[0], q.shape[1], v.shape[-1], dtype=q.dtype, device=q.device)
+    for i in range(len(cq) - 1):
+        qi = q[cq[i]:cq[i + 1]].unsqueeze(0)
+        ki = k[ck[i]:ck[i + 1]].unsqueeze(0)
+        vi = v[ck[i]:ck[i + 1]].unsqueeze(0)
+        out[cq[i]:cq[i + 1]] = _sdpa_reference(qi, ki, vi, None, dropout if training else 0.0, causal, scale)[0]
+    return out
 
 
 def flash_attn_unpadded(query, key, value, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, scale,
                         dropout=0.0, causal=False, return_softmax=False, fixed_seed_offset=None, rng_name="",
                         training=True, name=None):
-    """Variable-length attention over packed [total_tokens, heads, dim] tensors."""
+    """Variable-length attention over packed [total_tokens, heads, dim] tensors: one kernel
+    launch over every sequence (grid over the longest; per-sequence bounds from cu_seqlens)."""
     q, k, v = _u(query), _u(key), _u(value)
-    cq, ck = _u(cu_seqlens_q).tolist(), _u(cu_seqlens_k).tolist()
-    outs = []
-    for i in range(len(cq) - 1):
-        qi = q[cq[i]:cq[i + 1]].unsqueeze(0)
-        ki = k[ck[i]:ck[i + 1]].unsqueeze(0)
-        vi = v[ck[i]:ck[i + 1]].unsqueeze(0)
-        outs.append(_attend(qi, ki, vi, None, dropout, causal, training, scale)[0])
-    return _w(torch.cat(outs, 0)), None
+    cq, ck = _u(cu_seqlens_q), _u(cu_seqlens_k)
+    if _hip_ok(q, k, v) and not return_softmax:
+        return _w(_kernel_attend(q, k, v, causal, scale, None, dropout if training else 0.0, cq, ck,
+                                 int(max_seqlen_q), int(max_seqlen_k))), None
+    return _w(_unpadded_reference(q, k, v, cq, ck, scale, dropout, causal, training)), None
 
 
-flash_attn_varlen_qkvpacked = None
+def flash_attn_varlen_qkvpacked(qkv, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, scale, dropout=0.0,
+                                causal=False, return_softmax=False, fixed_seed_offset=None, rng_name="",
+                                varlen_padded=True, training=True, name=None):
+    """qkv [total, nheads/nheads_k + 2, nheads_k, d] (reference flash_attention.py:594); rows
+    outside every cu_seqlens span (the padding of a padded layout) come back as zeros."""
+    t = _u(qkv)
+    q = t[:, :-2].reshape(t.shape[0], -1, t.shape[-1])
+    return flash_attn_unpadded(_w(q), _w(t[:, -2]), _w(t[:, -1]), cu_seqlens_q, cu_seqlens_k, max_seqlen_q,
+                               max_seqlen_k, scale, dropout, causal, return_softmax, training=training)
 
 
 def scaled_dot_product_attention(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, training=True,
@@ -113,14 +172,21 @@ def scaled_dot_product_attention(query, key, value, attn_mask=None, dropout_p=0.
 def flash_attention_with_sparse_mask(query, key, value, attn_mask_start_row_indices, attn_mask_start_row=0,
                                      dropout_p=0.0, is_causal=False, return_softmax=False, return_softmax_lse=False,
                                      return_seed_offset=False, training=True, name=None):
+    """flashmask: key column k is masked for query rows >= attn_mask_start_row_indices[b, h, k]
+    (reference flash_attention.py:844); on HIP the kernel reads the O(S) index vector directly."""
     q, k, v = _u(query), _u(key), _u(value)
-    S = q.shape[1]
-    rows = _u(attn_mask_start_row_indices)  # [b, h, S_k]: masked from this row downward
-    r = torch.arange(S, device=q.device).view(1, 1, S, 1)
-    mask = r < rows.unsqueeze(2)
-    if is_causal:
-        mask = mask & torch.ones(S, S, dtype=torch.bool, device=q.device).tril()
-    return _w(_sdpa_reference(q, k, v, mask, dropout_p if training else 0.0, False))
+    rows = _u(attn_mask_start_row_indices)  # [b, h, S_k]
+    p = dropout_p if training else 0.0
+    if _hip_ok(q, k, v):
+        out = _kernel_attend(q, k, v, is_causal, None, None, p, start_rows=rows)
+    else:
+        S = q.shape[1]
+        r = torch.arange(S, device=q.device).view(1, 1, S, 1)
+        mask = r < rows.unsqueeze(2)
+        if is_causal:
+            mask = mask & torch.ones(S, k.shape[1], dtype=torch.bool, device=q.device).tril(k.shape[1] - S)
+        out = _sdpa_reference(q, k, v, mask, p, False)
+    return _w(out)
 
 
 def sparse_attention(query, key, value, sparse_csr_offset, sparse_csr_columns, key_padding_mask=None, attn_mask=None,

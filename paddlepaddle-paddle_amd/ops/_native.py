@@ -66,6 +66,10 @@ _SIGS = {
     'pa_conv2d_fwd': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
     'pa_gemm_ok': [I, I, I, LL, LL, LL, I],
     'pa_gemm_bf16': [P, P, P, P, P, I, I, I, LL, LL, LL, I, I, F, F, I, P],
+    'pa_flash_fwd_ex': [P, P, P, P, P, I, I, I, I, I, I, LLP, LLP, LLP, LLP, F, I, I, P, P, I, P, LL, LL, LL, I, F,
+                        U32, U32, P, LL, LL, P],
+    'pa_flash_bwd_ex': [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, LLP, LLP, LLP, LLP, LLP, LLP, LLP, LLP, F, I,
+                        I, P, P, I, P, LL, LL, LL, I, F, U32, U32, P, LL, LL, P],
     'pa_decode_nsplit': [I, I, I],
     'pa_decode_ok': [I, I, I],
     'pa_decode_attn': [I, P, LL, P, P, P, P, I, I, LL, P, P, LL, P, LL, P, I, I, I, I, I, F, P],

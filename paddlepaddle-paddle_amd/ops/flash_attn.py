@@ -9,6 +9,11 @@ import torch
 from . import _native as N
 
 
+def supported_ex(q, k, v):
+    """The extended kernels (mask / dropout / varlen) take the same operand contract."""
+    return supported(q, k, v)
+
+
 def supported(q, k, v):
     return (q.dim() == 4 and q.dtype in (torch.bfloat16, torch.float16) and k.dtype == q.dtype and v.dtype == q.dtype
             and q.shape[-1] in (64, 128) and k.shape[-1] == q.shape[-1] and v.shape[-1] == q.shape[-1]
@@ -107,3 +112,174 @@ def flash_attention_with_lse(q, k, v, causal=False, scale=None):
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
     return _fwd(q, k, v, causal, scale)
+
+
+# ------------------------------------------------------------------ masks, dropout, varlen
+def _mask_args(mask, B, H, Sq, Sk, dtype):
+    """(tensor, mb, mh, mq, is_f32) for an additive / bool mask broadcastable to [B, H, Sq, Sk]."""
+    if mask is None:
+        return None, 0, 0, 0, 0
+    m = mask
+    if m.dtype == torch.bool:
+        m = torch.zeros(m.shape, dtype=dtype, device=m.device).masked_fill(~m, float('-inf'))
+    elif m.dtype not in (torch.float32, dtype):
+        m = m.float()
+    while m.dim() < 4:
+        m = m.unsqueeze(0)
+    if m.stride(-1) != 1:
+        m = m.contiguous()
+    m = m.expand(B, H, Sq, Sk)
+    st = m.stride()
+    return m, st[0], st[1], st[2], int(m.dtype == torch.float32)
+
+
+def _rows_args(rows, B, H, Sk):
+    """(tensor, rb, rh) for flashmask start-row indices broadcastable to [B, H, Sk] (int32)."""
+    if rows is None:
+        return None, 0, 0
+    r = rows.to(torch.int32)
+    while r.dim() < 3:
+        r = r.unsqueeze(0)
+    if r.stride(-1) != 1:
+        r = r.contiguous()
+    r = r.expand(B, H, Sk)
+    return r, r.stride(0), r.stride(1)
+
+
+def _seed():
+    return int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+
+
+def _fwd_ex(q, k, v, causal, scale, mask, p_drop, seed, cu_q, cu_k, max_q, max_k, rows=None):
+    if cu_q is None:
+        B, Sq, Hq, D = q.shape
+        Sk, Hk = k.shape[1], k.shape[2]
+        total = 0
+        o = torch.empty(B, Sq, Hq, D, dtype=q.dtype, device=q.device)
+        lse = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
+        qv, kv, vv, ov = q, k, v, o
+    else:  # packed [total, H, D]
+        total, Hq, D = q.shape
+        Hk = k.shape[1]
+        B, Sq, Sk = cu_q.numel() - 1, max_q, max_k
+        # zeros: rows outside every sequence (padded varlen layouts) read back as 0
+        o = torch.zeros(total, Hq, D, dtype=q.dtype, device=q.device)
+        lse = torch.empty(Hq, total, dtype=torch.float32, device=q.device)
+        qv, kv, vv, ov = q.unsqueeze(0), k.unsqueeze(0), v.unsqueeze(0), o.unsqueeze(0)
+    m, mb, mh, mq, mf = _mask_args(mask, B, Hq, Sq, Sk, q.dtype)
+    rows, rb, rh = _rows_args(rows, B, Hq, Sk)
+    N.check(N.lib.pa_flash_fwd_ex(N.ptr(qv), N.ptr(kv), N.ptr(vv), N.ptr(ov), N.ptr(lse), B, Sq, Sk, Hq, Hk, D,
+                                  N.strides3(qv), N.strides3(kv), N.strides3(vv), N.strides3(ov), scale, int(causal),
+                                  N.dtcode(q.dtype), N.ptr(cu_q), N.ptr(cu_k), total, N.ptr(m), mb, mh, mq, mf,
+                                  float(p_drop), seed & 0xFFFFFFFF, 0, N.ptr(rows), rb, rh, N.stream()), 'flash_fwd_ex')
+    return o, lse
+
+
+class _FlashAttnEx(torch.autograd.Function):
+    """Flash attention with an additive/bool mask, in-kernel dropout and/or varlen packing."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale, mask, p_drop, cu_q, cu_k, max_q, max_k, rows):
+        seed = _seed() if p_drop > 0 else 0
+        o, lse = _fwd_ex(q, k, v, causal, scale, mask, p_drop, seed, cu_q, cu_k, max_q, max_k, rows)
+        ctx.save_for_backward(q, k, v, o, lse, mask, cu_q, cu_k, rows)
+        ctx.args = (causal, scale, p_drop, seed, max_q, max_k)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, mask, cu_q, cu_k, rows = ctx.saved_tensors
+        causal, scale, p_drop, seed, max_q, max_k = ctx.args
+        if do.stride(-1) != 1 or any(s % 8 for s in do.stride()[:-1]):
+            do = do.contiguous()
+        alloc = torch.empty if cu_q is None else torch.zeros  # varlen: rows outside every sequence
+        dq = alloc(q.shape, dtype=q.dtype, device=q.device)
+        Hq, Hk = q.shape[-2], k.shape[-2]
+        kshape = list(k.shape)
+        kshape[-2] = Hq
+        dk = alloc(kshape, dtype=q.dtype, device=q.device)
+        dv = alloc(kshape, dtype=q.dtype, device=q.device)
+        if cu_q is None:
+            B, Sq, _, D = q.shape
+            Sk = k.shape[1]
+            total = 0
+            delta = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
+            views = (q, k, v, o, do, dq, dk, dv)
+        else:
+            total, _, D = q.shape
+            B, Sq, Sk = cu_q.numel() - 1, max_q, max_k
+            delta = torch.empty(Hq, total, dtype=torch.float32, device=q.device)
+            views = tuple(t.unsqueeze(0) for t in (q, k, v, o, do, dq, dk, dv))
+        qv, kv, vv, ov, dov, dqv, dkv, dvv = views
+        m, mb, mh, mq, mf = _mask_args(mask, B, Hq, Sq, Sk, q.dtype)
+        rows, rb, rh = _rows_args(rows, B, Hq, Sk)
+        N.check(N.lib.pa_flash_bwd_ex(N.ptr(qv), N.ptr(kv), N.ptr(vv), N.ptr(ov), N.ptr(dov), N.ptr(lse),
+                                      N.ptr(delta), N.ptr(dqv), N.ptr(dkv), N.ptr(dvv), B, Sq, Sk, Hq, Hk, D,
+                                      N.strides3(qv), N.strides3(kv), N.strides3(vv), N.strides3(ov),
+                                      N.strides3(dov), N.strides3(dqv), N.strides3(dkv), N.strides3(dvv), scale,
+                                      int(causal), N.dtcode(q.dtype), N.ptr(cu_q), N.ptr(cu_k), total, N.ptr(m), mb,
+                                      mh, mq, mf, float(p_drop), seed & 0xFFFFFFFF, 0, N.ptr(rows), rb, rh, N.stream()),
+                'flash_bwd_ex')
+        if Hq != Hk:
+            dk = dk.unflatten(-2, (Hk, Hq // Hk)).sum(-2)
+            dv = dv.unflatten(-2, (Hk, Hq // Hk)).sum(-2)
+        return dq, dk, dv, None, None, None, None, None, None, None, None, None
+
+
+def flash_attention_ex(q, k, v, causal=False, scale=None, mask=None, dropout=0.0, cu_seqlens_q=None,
+                       cu_seqlens_k=None, max_seqlen_q=None, max_seqlen_k=None, start_rows=None):
+    """q/k/v [B, S, H, D] (or packed [total, H, D] with int32 cu_seqlens); mask broadcastable to
+    [B, Hq, Sq, Sk] (additive, or bool = keep); dropout on the attention probabilities;
+    start_rows [B, H|1, Sk] int32 flashmask indices (key k masked for queries >= start_rows[k])."""
+    if mask is not None and start_rows is not None:
+        raise ValueError("flash_attention_ex: pass either a dense mask or start_rows, not both")
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    cq = None if cu_seqlens_q is None else cu_seqlens_q.to(device=q.device, dtype=torch.int32).contiguous()
+    ck = None if cu_seqlens_k is None else cu_seqlens_k.to(device=q.device, dtype=torch.int32).contiguous()
+    if cq is not None and (max_seqlen_q is None or max_seqlen_k is None):
+        max_seqlen_q = int((cq[1:] - cq[:-1]).max())
+        max_seqlen_k = int((ck[1:] - ck[:-1]).max())
+    return _FlashAttnEx.apply(q, k, v, bool(causal), float(scale), mask, float(dropout), cq, ck, max_seqlen_q,
+                              max_seqlen_k, start_rows)
+
+
+class _FlashAttnPackedEx(torch.autograd.Function):
+    """Packed qkv [B, S, 3, H, D] with in-kernel dropout (and/or a mask): the training path of
+    GPT with attention dropout; dQ/dK/dV land straight in one packed gradient as in
+    _FlashAttnPacked."""
+
+    @staticmethod
+    def forward(ctx, qkv, causal, scale, mask, p_drop):
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        seed = _seed() if p_drop > 0 else 0
+        o, lse = _fwd_ex(q, k, v, causal, scale, mask, p_drop, seed, None, None, None, None)
+        ctx.save_for_backward(qkv, o, lse, mask)
+        ctx.args = (causal, scale, p_drop, seed)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse, mask = ctx.saved_tensors
+        causal, scale, p_drop, seed = ctx.args
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        B, S, H, D = q.shape
+        if do.stride(-1) != 1 or any(s % 8 for s in do.stride()[:3]):
+            do = do.contiguous()
+        dqkv = torch.empty(B, S, 3, H, D, dtype=qkv.dtype, device=qkv.device)
+        dq, dk, dv = dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2]
+        delta = torch.empty(B, H, S, dtype=torch.float32, device=q.device)
+        m, mb, mh, mq, mf = _mask_args(mask, B, H, S, S, q.dtype)
+        N.check(N.lib.pa_flash_bwd_ex(N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse), N.ptr(delta),
+                                      N.ptr(dq), N.ptr(dk), N.ptr(dv), B, S, S, H, H, D, N.strides3(q), N.strides3(k),
+                                      N.strides3(v), N.strides3(o), N.strides3(do), N.strides3(dq), N.strides3(dk),
+                                      N.strides3(dv), scale, int(causal), N.dtcode(q.dtype), None, None, 0, N.ptr(m),
+                                      mb, mh, mq, mf, float(p_drop), seed & 0xFFFFFFFF, 0, None, 0, 0, N.stream()),
+                'flash_bwd_ex')
+        return dqkv, None, None, None, None
+
+
+def flash_attention_packed_ex(qkv, causal=False, scale=None, mask=None, dropout=0.0):
+    if scale is None:
+        scale = 1.0 / math.sqrt(qkv.shape[-1])
+    return _FlashAttnPackedEx.apply(qkv, bool(causal), float(scale), mask, float(dropout))
