@@ -185,16 +185,17 @@ def test_flash_varlen_with_mask_and_dropout_runs():
     assert torch.isfinite(q.grad).all()
 
 
-@pytest.mark.parametrize("D", [80, 96])
+@pytest.mark.parametrize("D", [32, 80, 96])
 def test_flash_padded_head_dim(D):
     B, S, H = 2, 160, 4
     q, k, v = _leaf(B, S, H, D), _leaf(B, S, H, D), _leaf(B, S, H, D)
-    out, _ = paddle.nn.functional.flash_attention(paddle.to_tensor(q), paddle.to_tensor(k), paddle.to_tensor(v),
-                                                  causal=True)
+    from paddle.core.tensor import _wrap
+    out, _ = paddle.nn.functional.flash_attention(_wrap(q), _wrap(k), _wrap(v), causal=True)
     o = out._t
     ri = [t.detach().float().requires_grad_() for t in (q, k, v)]
     r = _ref(*ri, True)
     _close(o, r, 2e-2, name=f'D{D} fwd')
+    _grads_vs_ref(o, r, (q, k, v), ri, 5e-2, f'D{D}')
 
 
 def test_api_routes_mask_and_dropout_to_kernel(monkeypatch):
@@ -214,3 +215,29 @@ def test_api_routes_mask_and_dropout_to_kernel(monkeypatch):
     cu = paddle.to_tensor(torch.tensor([0, 100, 2 * S], dtype=torch.int32, device=DEV))
     paddle.nn.functional.flash_attn_unpadded(t, t, t, cu, cu, 156, 156, 0.125, causal=True)
     assert not called
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("D,Hr", [(64, 4), (128, 1)])
+def test_flash_startend_rows(causal, D, Hr):
+    """flashmask: key k hidden from query rows >= rows[b, h, k] (h broadcast when Hr == 1)."""
+    B, S, H = 2, 300, 4
+    q, k, v = _leaf(B, S, H, D), _leaf(B, S, H, D), _leaf(B, S, H, D)
+    rows = torch.randint(S // 3, S + 1, (B, Hr, S), device=DEV, dtype=torch.int32)
+    rows[..., 0] = S  # key 0 visible to every row: no empty softmax row
+    o = FA.flash_attention_ex(q, k, v, causal, start_rows=rows)
+    keep = torch.arange(S, device=DEV).view(1, 1, S, 1) < rows.unsqueeze(2)  # [B, Hr, Sq, Sk]
+    ri = [t.detach().float().requires_grad_() for t in (q, k, v)]
+    r = _ref(*ri, causal, mask=keep)
+    _close(o, r, 2e-2, name='flashmask fwd')
+    _grads_vs_ref(o, r, (q, k, v), ri, 5e-2, 'flashmask')
+
+
+def test_sparse_mask_api_matches_dense():
+    B, S, H, D = 1, 256, 2, 64
+    x = torch.randn(B, S, H, D, device=DEV).bfloat16()
+    rows = torch.randint(S // 2, S + 1, (B, H, S), device=DEV, dtype=torch.int32)
+    out = paddle.nn.functional.flash_attention_with_sparse_mask(
+        paddle.to_tensor(x), paddle.to_tensor(x), paddle.to_tensor(x), paddle.to_tensor(rows), is_causal=True)
+    keep = torch.arange(S, device=DEV).view(1, 1, S, 1) < rows.unsqueeze(2)
+    _close(out._t, _ref(x, x, x, True, mask=keep), 2e-2, name='sparse api')
