@@ -1,7 +1,8 @@
 """paddle.amp (reference: python/paddle/amp/{auto_cast,grad_scaler}.py).
 
-* ``auto_cast(level='O1')`` runs white-listed ops (matmul/conv/linear) in bf16/fp16 via the
-  storage layer's autocast; ``level='O2'`` expects parameters already cast by ``decorate``.
+* ``auto_cast(level='O1'|'O2'|'OD')`` applies the reference's per-op cast rule (white list ->
+  bf16/fp16, black list -> fp32, custom lists, O2 = pure low precision) at the paddle op
+  boundary (``core.amp_dispatch``); ``level='O2'`` expects parameters cast by ``decorate``.
 * ``decorate(level='O2')`` casts parameters to the low-precision dtype except normalisation
   layers (kept fp32, like the reference) and turns on optimizer master weights.
 * ``GradScaler`` — dynamic loss scaling with found-inf skip (needed for fp16; bf16 runs

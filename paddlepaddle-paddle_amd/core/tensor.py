@@ -114,7 +114,11 @@ class Tensor:
     @property
     def grad(self):
         g = self._t.grad
-        return None if g is None else _wrap(g)
+        if g is None:
+            return None
+        if g.dtype != torch.float32 and g.is_floating_point() and self.__dict__.get('_master_grad'):
+            return _wrap(g.float())  # amp.decorate(master_grad=True): float32 view of the gradient
+        return _wrap(g)
 
     @grad.setter
     def grad(self, v):

@@ -12,6 +12,7 @@ from ...core.tensor import Tensor, _wrap as _w, _unwrap as _u
 from ... import ops
 from ...nn import functional as F
 from ...nn.functional.flash_attention import _attend
+from ...core.amp_dispatch import amp_op as _amp_op
 
 
 def fused_rms_norm(x, norm_weight, norm_bias=None, epsilon=1e-6, begin_norm_axis=-1, bias=None, residual=None,
@@ -65,6 +66,7 @@ def fused_dropout_add(x, y, p=0.5, training=True, mode='upscale_in_train', name=
     return _w(TF.dropout(t, p, True) + r)
 
 
+@_amp_op('fused_rotary_position_embedding')
 def fused_rotary_position_embedding(q, k=None, v=None, sin=None, cos=None, position_ids=None,
                                     use_neox_rotary_style=True, time_major=False, rotary_emb_base=10000.0):
     """q/k/v: [B, S, H, D].  use_neox_rotary_style=True rotates adjacent pairs (reference docstring)."""

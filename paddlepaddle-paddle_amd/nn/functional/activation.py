@@ -9,6 +9,7 @@ import torch.nn.functional as TF
 from ...core.tensor import Tensor, _wrap as _w, _unwrap as _u
 from ...core import dtype as _dt
 from ... import ops
+from ...core.amp_dispatch import amp_op as _amp_op
 
 
 def relu(x, name=None):
@@ -103,6 +104,7 @@ def softshrink(x, threshold=0.5, name=None):
     return _w(TF.softshrink(_u(x), threshold))
 
 
+@_amp_op('tanh_shrink')
 def tanhshrink(x, name=None):
     return _w(TF.tanhshrink(_u(x)))
 
@@ -111,6 +113,7 @@ def softsign(x, name=None):
     return _w(TF.softsign(_u(x)))
 
 
+@_amp_op('softplus')
 def softplus(x, beta=1, threshold=20, name=None):
     return _w(TF.softplus(_u(x), beta, threshold))
 
@@ -163,6 +166,7 @@ def glu(x, axis=-1, name=None):
     return _w(TF.glu(_u(x), axis))
 
 
+@_amp_op('softmax')
 def softmax(x, axis=-1, dtype=None, name=None):
     t = _u(x)
     if dtype is not None:
@@ -177,6 +181,7 @@ def softmax_(x, axis=-1, dtype=None, name=None):
     return x
 
 
+@_amp_op('log_softmax')
 def log_softmax(x, axis=-1, dtype=None, name=None):
     t = _u(x)
     if dtype is not None:

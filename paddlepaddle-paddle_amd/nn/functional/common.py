@@ -9,8 +9,10 @@ from ...core.tensor import Tensor, _wrap as _w, _unwrap as _u
 from ...core import dtype as _dt
 from ...tensor._helpers import _shape
 from ... import ops
+from ...core.amp_dispatch import amp_op as _amp_op
 
 
+@_amp_op('matmul_v2')
 def linear(x, weight, bias=None, name=None):
     """y = x @ W + b with W stored [in_features, out_features] (paddle layout)."""
     t, w = _u(x), _u(weight)
@@ -110,6 +112,7 @@ def zeropad2d(x, padding, data_format='NCHW', name=None):
     return pad(x, padding, 'constant', 0.0, data_format)
 
 
+@_amp_op('bilinear_interp_v2')
 def interpolate(x, size=None, scale_factor=None, mode='nearest', align_corners=False, align_mode=0,
                 data_format=None, recompute_scale_factor=None, name=None):
     t = _u(x)
@@ -136,6 +139,7 @@ def interpolate(x, size=None, scale_factor=None, mode='nearest', align_corners=F
 upsample = interpolate
 
 
+@_amp_op('lookup_table_v2')
 def embedding(x, weight, padding_idx=None, max_norm=None, norm_type=2.0, sparse=False, scale_grad_by_freq=False,
               name=None):
     ids, w = _u(x), _u(weight)

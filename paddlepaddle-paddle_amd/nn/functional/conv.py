@@ -11,6 +11,7 @@ from ... import ops
 
 from ...core.tensor import Tensor, _wrap as _w, _unwrap as _u
 from ...tensor._helpers import _shape
+from ...core.amp_dispatch import amp_op as _amp_op
 
 
 def _ntuple(v, n):
@@ -87,14 +88,17 @@ def _conv(x, weight, bias, stride, padding, dilation, groups, data_format, nd, f
     return _w(out)
 
 
+@_amp_op('conv2d')
 def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format='NCL', name=None):
     return _conv(x, weight, bias, stride, padding, dilation, groups, data_format, 1, TF.conv1d)
 
 
+@_amp_op('conv2d')
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format='NCHW', name=None):
     return _conv(x, weight, bias, stride, padding, dilation, groups, data_format, 2, TF.conv2d)
 
 
+@_amp_op('conv3d')
 def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format='NCDHW', name=None):
     return _conv(x, weight, bias, stride, padding, dilation, groups, data_format, 3, TF.conv3d)
 
@@ -170,6 +174,7 @@ def max_pool1d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_m
     return _pool(x, kernel_size, stride, padding, ceil_mode, 'NCL', 1, TF.max_pool1d, return_mask=return_mask)
 
 
+@_amp_op('max_pool2d_with_index')
 def max_pool2d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False, data_format='NCHW',
                name=None):
     return _pool(x, kernel_size, stride, padding, ceil_mode, data_format, 2, TF.max_pool2d, return_mask=return_mask)

@@ -12,6 +12,7 @@ import torch.nn.functional as TF
 
 from ...core.tensor import Tensor, _wrap as _w, _unwrap as _u
 from ... import ops
+from ...core.amp_dispatch import amp_op as _amp_op
 
 
 def masked_attention_bhsd(q, k, v, mask, dropout_p=0.0, scale=None):
@@ -99,6 +100,7 @@ def _attend(q, k, v, mask=None, dropout=0.0, causal=False, training=True, scale=
     return _sdpa_reference(q, k, v, mask, dropout, causal, scale)
 
 
+@_amp_op('flash_attn')
 def flash_attention(query, key, value, dropout=0.0, causal=False, return_softmax=False, *, fixed_seed_offset=None,
                     rng_name="", training=True, name=None):
     q, k, v = _u(query), _u(key), _u(value)
@@ -162,6 +164,7 @@ def flash_attn_varlen_qkvpacked(qkv, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, m
                                max_seqlen_k, scale, dropout, causal, return_softmax, training=training)
 
 
+@_amp_op('flash_attn')
 def scaled_dot_product_attention(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, training=True,
                                  name=None):
     q, k, v = _u(query), _u(key), _u(value)

@@ -9,6 +9,7 @@ import torch.nn.functional as TF
 
 from ...core.tensor import Tensor, _wrap as _w, _unwrap as _u
 from ... import ops
+from ...core.amp_dispatch import amp_op as _amp_op
 
 
 def _reduce(t, reduction):
@@ -19,6 +20,7 @@ def _reduce(t, reduction):
     return t
 
 
+@_amp_op('cross_entropy')
 def cross_entropy(input, label, weight=None, ignore_index=-100, reduction='mean', soft_label=False, axis=-1,  # noqa: A002
                   use_softmax=True, label_smoothing=0.0, name=None):
     logits, lab = _u(input), _u(label)
@@ -70,6 +72,7 @@ def cross_entropy(input, label, weight=None, ignore_index=-100, reduction='mean'
     return _w(loss.sum() / valid)
 
 
+@_amp_op('softmax_with_cross_entropy')
 def softmax_with_cross_entropy(logits, label, soft_label=False, ignore_index=-100, numeric_stable_mode=True,
                                return_softmax=False, axis=-1):
     loss = cross_entropy(logits, label, soft_label=soft_label, ignore_index=ignore_index, reduction='none', axis=axis)
@@ -78,6 +81,7 @@ def softmax_with_cross_entropy(logits, label, soft_label=False, ignore_index=-10
     return loss
 
 
+@_amp_op('nll_loss')
 def nll_loss(input, label, weight=None, ignore_index=-100, reduction='mean', name=None):  # noqa: A002
     t, l = _u(input), _u(label).long()
     if t.dim() > 2:
@@ -97,6 +101,7 @@ def l1_loss(input, label, reduction='mean', name=None):  # noqa: A002
     return _w(TF.l1_loss(_u(input), _u(label), reduction=reduction))
 
 
+@_amp_op('huber_loss')
 def smooth_l1_loss(input, label, reduction='mean', delta=1.0, name=None):  # noqa: A002
     return _w(TF.huber_loss(_u(input), _u(label), reduction=reduction, delta=delta))
 
@@ -105,6 +110,7 @@ def binary_cross_entropy(input, label, weight=None, reduction='mean', name=None)
     return _w(TF.binary_cross_entropy(_u(input), _u(label), _u(weight), reduction=reduction))
 
 
+@_amp_op('sigmoid_cross_entropy_with_logits')
 def binary_cross_entropy_with_logits(logit, label, weight=None, reduction='mean', pos_weight=None, name=None):
     return _w(TF.binary_cross_entropy_with_logits(_u(logit), _u(label), _u(weight), reduction=reduction,
                                                   pos_weight=_u(pos_weight)))
@@ -144,6 +150,7 @@ def cosine_embedding_loss(input1, input2, label, margin=0, reduction='mean', nam
     return _w(TF.cosine_embedding_loss(_u(input1), _u(input2), _u(label), margin=margin, reduction=reduction))
 
 
+@_amp_op('triplet_margin_loss')
 def triplet_margin_loss(input, positive, negative, margin=1.0, p=2, epsilon=1e-6, swap=False, reduction='mean',  # noqa: A002
                         name=None):
     return _w(TF.triplet_margin_loss(_u(input), _u(positive), _u(negative), margin=margin, p=p, eps=epsilon,
@@ -179,6 +186,7 @@ def gaussian_nll_loss(input, label, variance, full=False, epsilon=1e-6, reductio
     return _w(TF.gaussian_nll_loss(_u(input), _u(label), _u(variance), full, epsilon, reduction))
 
 
+@_amp_op('log_loss')
 def log_loss(input, label, epsilon=1e-4, name=None):  # noqa: A002
     x, y = _u(input), _u(label)
     return _w(-y * torch.log(x + epsilon) - (1 - y) * torch.log(1 - x + epsilon))
@@ -215,6 +223,7 @@ def rnnt_loss(input, label, input_lengths, label_lengths, blank=0, fastemit_lamb
     raise NotImplementedError("rnnt_loss: transducer loss not provided by this build")
 
 
+@_amp_op('margin_cross_entropy')
 def margin_cross_entropy(logits, label, margin1=1.0, margin2=0.5, margin3=0.0, scale=64.0, group=None,
                          return_softmax=False, reduction='mean'):
     x, y = _u(logits), _u(label).reshape(-1).long()
@@ -229,6 +238,7 @@ def margin_cross_entropy(logits, label, margin1=1.0, margin2=0.5, margin3=0.0, s
     return loss
 
 
+@_amp_op('hsigmoid_loss')
 def hsigmoid_loss(input, label, num_classes, weight, bias=None, path_table=None, path_code=None, is_sparse=False,  # noqa: A002
                   name=None):
     x, y, w = _u(input), _u(label).reshape(-1).long(), _u(weight)

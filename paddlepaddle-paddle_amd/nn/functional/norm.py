@@ -9,8 +9,10 @@ import torch.nn.functional as TF
 
 from ...core.tensor import Tensor, _wrap as _w, _unwrap as _u
 from ... import ops
+from ...core.amp_dispatch import amp_op as _amp_op
 
 
+@_amp_op('layer_norm')
 def layer_norm(x, normalized_shape, weight=None, bias=None, epsilon=1e-05, name=None):
     t = _u(x)
     if isinstance(normalized_shape, int):
@@ -65,6 +67,7 @@ def instance_norm(x, running_mean=None, running_var=None, weight=None, bias=None
     return _w(out)
 
 
+@_amp_op('group_norm')
 def group_norm(x, num_groups, epsilon=1e-05, weight=None, bias=None, data_format='NCHW', name=None):
     t = _u(x)
     cl = data_format[-1] == 'C'

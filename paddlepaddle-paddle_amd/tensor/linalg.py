@@ -6,8 +6,10 @@ library path); fused GEMM epilogues used by the models live in ``ops/``.
 import torch
 
 from ._helpers import _w, _u, _axis, Tensor
+from ..core.amp_dispatch import amp_op as _amp_op
 
 
+@_amp_op('matmul_v2')
 def matmul(x, y, transpose_x=False, transpose_y=False, name=None):
     a, b = _u(x), _u(y)
     if transpose_x:
@@ -17,10 +19,12 @@ def matmul(x, y, transpose_x=False, transpose_y=False, name=None):
     return _w(torch.matmul(a, b))
 
 
+@_amp_op('matmul_v2')
 def mm(input, mat2, name=None):  # noqa: A002
     return _w(torch.matmul(_u(input), _u(mat2)))
 
 
+@_amp_op('matmul_v2')
 def bmm(x, y, name=None):
     return _w(torch.bmm(_u(x), _u(y)))
 
@@ -36,12 +40,14 @@ def mv(x, vec, name=None):
     return _w(torch.mv(_u(x), _u(vec)))
 
 
+@_amp_op('einsum')
 def einsum(equation, *operands):
     if len(operands) == 1 and isinstance(operands[0], (list, tuple)):
         operands = operands[0]
     return _w(torch.einsum(equation, *[_u(o) for o in operands]))
 
 
+@_amp_op('pnorm')
 def norm(x, p=None, axis=None, keepdim=False, name=None):
     t = _u(x)
     a = _axis(axis)

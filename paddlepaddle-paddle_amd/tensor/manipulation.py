@@ -5,6 +5,7 @@ import numpy as np
 import torch
 
 from ._helpers import _w, _u, _t, _axis, _shape, _dtype, Tensor
+from ..core.amp_dispatch import amp_op as _amp_op
 
 
 def cast(x, dtype):
@@ -283,6 +284,7 @@ def put_along_axis_(arr, indices, values, axis, reduce='assign', include_self=Tr
     return arr
 
 
+@_amp_op('scatter')
 def scatter(x, index, updates, overwrite=True, name=None):
     t, i, u = _u(x), _u(index).reshape(-1), _u(updates)
     if overwrite:

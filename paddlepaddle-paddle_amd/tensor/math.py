@@ -10,6 +10,7 @@ import torch
 
 from ._helpers import _w, _u, _t, _axis, _dims, _dtype, _scalar, Tensor
 from ..core import dtype as _dt
+from ..core.amp_dispatch import amp_op as _amp_op
 
 # ----------------------------------------------------------------------------- unary
 _UNARY = {
@@ -50,8 +51,14 @@ def _make_unary_(fn, name):
     return f_
 
 
+_UNARY_AMP = {'tan': 'tan', 'acos': 'acos', 'asin': 'asin', 'sinh': 'sinh', 'cosh': 'cosh', 'atanh': 'atanh',
+              'erfinv': 'erfinv', 'exp': 'exp', 'expm1': 'expm1', 'log': 'log', 'log10': 'log10', 'log2': 'log2',
+              'reciprocal': 'reciprocal', 'rsqrt': 'rsqrt', 'square': 'square'}  # reference FP16_BLACK_LIST names
+
 for _n, _f in _UNARY.items():
     globals()[_n] = _make_unary(_f, _n)
+    if _n in _UNARY_AMP:
+        globals()[_n] = _amp_op(_UNARY_AMP[_n])(globals()[_n])
     if _n not in ('isfinite', 'isinf', 'isnan', 'isneginf', 'isposinf', 'isreal', 'signbit', 'angle', 'conj'):
         globals()[_n + '_'] = _make_unary_(_f, _n)
 
@@ -117,6 +124,7 @@ def scale_(x, scale=1.0, bias=0.0, bias_after_scale=True, act=None, name=None):
     return x
 
 
+@_amp_op('pow')
 def pow(x, y, name=None):  # noqa: A001
     return _w(torch.pow(_t(x), _t(y, _u(x) if isinstance(x, Tensor) else None)))
 
@@ -248,6 +256,7 @@ def _reduce(fn, x, axis, keepdim, dtype=None):
     return _w(fn(t, dim=a, keepdim=keepdim))
 
 
+@_amp_op('reduce_sum')
 def sum(x, axis=None, dtype=None, keepdim=False, name=None):  # noqa: A001
     t = _u(x)
     if dtype is None and (t.dtype == torch.bool or (not t.is_floating_point() and not t.is_complex() and t.dtype != torch.int64)):
@@ -265,6 +274,7 @@ def nansum(x, axis=None, dtype=None, keepdim=False, name=None):
     return _reduce(torch.nansum, x, axis, keepdim, dtype)
 
 
+@_amp_op('mean')
 def mean(x, axis=None, keepdim=False, name=None):
     return _reduce(torch.mean, x, axis, keepdim)
 
@@ -273,6 +283,7 @@ def nanmean(x, axis=None, keepdim=False, name=None):
     return _reduce(torch.nanmean, x, axis, keepdim)
 
 
+@_amp_op('reduce_prod')
 def prod(x, axis=None, keepdim=False, dtype=None, name=None):
     t = _u(x)
     if dtype is not None:
@@ -350,6 +361,7 @@ def count_nonzero(x, axis=None, keepdim=False, name=None):
     return _w(r)
 
 
+@_amp_op('cumsum')
 def cumsum(x, axis=None, dtype=None, name=None):
     t = _u(x)
     if axis is None:
@@ -363,6 +375,7 @@ def cumsum_(x, axis=None, dtype=None, name=None):
     return x
 
 
+@_amp_op('cumprod')
 def cumprod(x, dim=None, dtype=None, name=None):
     t = _u(x)
     if dim is None:
@@ -431,6 +444,7 @@ def cross(x, y, axis=9, name=None):
     return _w(torch.linalg.cross(t, _u(y), dim=axis))
 
 
+@_amp_op('renorm')
 def renorm(x, p, axis, max_norm, name=None):
     return _w(torch.renorm(_u(x), p, axis, max_norm))
 
@@ -564,6 +578,7 @@ def rank(input):  # noqa: A002
     return _w(torch.tensor(_u(input).dim(), dtype=torch.int32))
 
 
+@_amp_op('dist')
 def dist(x, y, p=2, name=None):
     return _w(torch.dist(_u(x), _u(y), p=p))
 
