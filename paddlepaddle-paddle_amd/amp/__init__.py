@@ -12,3 +12,4 @@ from .auto_cast import auto_cast, amp_guard, decorate, amp_decorate, is_float16_
 from .grad_scaler import GradScaler, AmpScaler, OptimizerState  # noqa: F401
 from . import debugging  # noqa: F401
 from .amp_lists import white_list, black_list  # noqa: F401
+from ..ops.fp8 import fp8_autocast, DelayedScaling  # noqa: F401  (fp8 training: ops/fp8.py)

@@ -1,0 +1,172 @@
+// FP8 training casts for gfx950: bf16 -> OCP e4m3fn / e5m2 with delayed (amax-history) scaling,
+// writing the row-major image and/or its transpose in ONE pass over the bf16 tensor.
+//
+// An fp8 Linear needs every operand k-contiguous for the TN fp8 GEMM (csrc/gemm.hip):
+//   forward  Y  = X  @ W        A = X  [M,K]     B = W^T  [N,K]   (weight transposed)
+//   dgrad    dX = dY @ W^T      A = dY [M,N]     B = W    [K,N]   (weight as stored)
+//   wgrad    dW = X^T @ dY      A = X^T [K,M]    B = dY^T [N,M]   (both transposed)
+// so X, W and dY are each needed in both orientations: a cast that emits q and q^T together
+// reads the bf16 tensor once (reference role: the cast + transpose of an fp8 training recipe;
+// the reference framework itself has no fp8 path — see SURVEY §2 row "fp8 GEMM").
+//
+// Scaling (delayed, no host sync): hist[L] is the tensor's amax history on the device.  The
+// quantisation scale is fmax / max(hist[j], j != cur, cur+1) / 2^margin (1 when the history is
+// empty), every block folds its tile amax into hist[cur] (float atomicMax on the bit pattern —
+// amax >= 0, so the unsigned order is the float order), and block 0 zeroes hist[cur+1], the
+// slot the NEXT call records into (no reader of this call touches either slot).  Block 0 also
+// writes the dequant scale 1/scale to scale_inv, which the fp8 GEMM reads on the device.
+//
+// Tiles: 64x64 per 256-thread block; thread t owns row t/4, 16 columns (two 16-B bf16 loads),
+// stores 16 fp8 bytes of q, and scatters the bytes through an LDS tile for the 16-B row stores
+// of q^T.  Edge tiles take the guarded element path.
+#include "common.h"
+
+namespace pa {
+namespace f8 {
+
+constexpr int T = 64;
+
+template <int FMT>
+__device__ __forceinline__ float fmax_of() { return FMT == 0 ? 448.f : 57344.f; }
+
+// two floats -> two fp8 bytes (low 16 bits of the result), saturating (clamped before the cvt)
+template <int FMT>
+__device__ __forceinline__ uint32_t cvt2(float a, float b) {
+  const float m = fmax_of<FMT>();
+  a = fminf(fmaxf(a, -m), m);
+  b = fminf(fmaxf(b, -m), m);
+  if constexpr (FMT == 0)
+    return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false) & 0xFFFFu;
+  else
+    return (uint32_t)__builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false) & 0xFFFFu;
+}
+
+__device__ __forceinline__ float scale_from_hist(const float* __restrict__ hist, int L, int cur, float fmax,
+                                                 float margin_mul) {
+  float am = 0.f;
+  const int nxt = (cur + 1) % L;
+  for (int j = 0; j < L; ++j)
+    if (j != cur && j != nxt) am = fmaxf(am, hist[j]);
+  if (!(am > 0.f) || !isfinite(am)) return 1.f;
+  const float s = fmax / am * margin_mul;
+  return isfinite(s) ? s : 1.f;
+}
+
+__device__ __forceinline__ void atomic_max_pos(float* addr, float v) {
+  atomicMax(reinterpret_cast<unsigned int*>(addr), __float_as_uint(v));
+}
+
+template <int FMT>
+__global__ __launch_bounds__(256) void cast_transpose_kernel(const bf16_t* __restrict__ x, int R, int C, long long ldx,
+                                                             uint8_t* __restrict__ q, uint8_t* __restrict__ qt,
+                                                             float* __restrict__ hist, int L, int cur,
+                                                             float* __restrict__ scale_inv, float margin_mul) {
+  __shared__ uint8_t tile[T][T + 16];  // [col][row] fp8 bytes (16-B padded rows)
+  __shared__ float red[4];
+  const float fmax = fmax_of<FMT>();
+  const float s = scale_from_hist(hist, L, cur, fmax, margin_mul);
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.y * T, c0 = blockIdx.x * T;
+  const int lr = tid >> 2, lc = (tid & 3) * 16;
+  const int r = r0 + lr, c = c0 + lc;
+  const bool full = (r0 + T <= R) && (c0 + T <= C);
+  float v[16];
+  if (full) {
+    load_f<bf16_t, 8>(x + (long long)r * ldx + c, *reinterpret_cast<float(*)[8]>(&v[0]));
+    load_f<bf16_t, 8>(x + (long long)r * ldx + c + 8, *reinterpret_cast<float(*)[8]>(&v[8]));
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = (r < R && c + i < C) ? (float)x[(long long)r * ldx + c + i] : 0.f;
+  }
+  float am = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) am = fmaxf(am, fabsf(v[i]));
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = cvt2<FMT>(v[4 * i] * s, v[4 * i + 1] * s) | (cvt2<FMT>(v[4 * i + 2] * s, v[4 * i + 3] * s) << 16);
+  if (q) {
+    if (full) {
+      *reinterpret_cast<uint4*>(q + (long long)r * C + c) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else if (r < R) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (c + i < C) q[(long long)r * C + c + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    }
+  }
+  if (qt) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) tile[lc + i][lr] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    __syncthreads();
+    // q^T row (input column) c0 + lr, 16 bytes of input rows r0 + lc ..
+    const int orow = c0 + lr, ocol = r0 + lc;
+    if (full) {
+      *reinterpret_cast<uint4*>(qt + (long long)orow * R + ocol) = *reinterpret_cast<const uint4*>(&tile[lr][lc]);
+    } else if (orow < C) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (ocol + i < R) qt[(long long)orow * R + ocol + i] = tile[lr][lc + i];
+    }
+  }
+  am = wave_max(am);
+  if ((tid & 63) == 0) red[tid >> 6] = am;
+  __syncthreads();
+  if (tid == 0) {
+    const float b = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomic_max_pos(hist + cur, b);
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+      hist[(cur + 1) % L] = 0.f;
+      scale_inv[0] = 1.f / s;
+    }
+  }
+}
+
+// amax of a bf16 [R, C] tensor folded into *out (first use of a tensor: seeds the history)
+__global__ __launch_bounds__(256) void amax_kernel(const bf16_t* __restrict__ x, int R, int C, long long ldx,
+                                                   float* __restrict__ out) {
+  __shared__ float red[4];
+  float am = 0.f;
+  const long long n8 = (long long)R * (C / 8);
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long long)gridDim.x * 256) {
+    const long long row = i / (C / 8), col = (i % (C / 8)) * 8;
+    float v[8];
+    load_f<bf16_t, 8>(x + row * ldx + col, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(v[j]));
+  }
+  am = wave_max(am);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
+  __syncthreads();
+  if (threadIdx.x == 0) atomic_max_pos(out, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
+
+}  // namespace f8
+}  // namespace pa
+
+using namespace pa;
+
+// x: bf16 [R, C] (row stride ldx, 16-B aligned rows), q: [R, C] fp8 or null, qt: [C, R] fp8 or null.
+// fmt 0 = e4m3fn, 1 = e5m2.  C % 8 == 0.
+PA_API int pa_fp8_cast_transpose(const void* x, int R, int C, long long ldx, void* q, void* qt, void* hist, int L,
+                                 int cur, void* scale_inv, int fmt, float margin_mul, hipStream_t st) {
+  if (R <= 0 || C <= 0 || C % 8 || ldx % 8 || L < 3 || cur < 0 || cur >= L || !hist || !scale_inv)
+    return (int)hipErrorInvalidValue;
+  dim3 grid((C + f8::T - 1) / f8::T, (R + f8::T - 1) / f8::T);
+  if (grid.y > 65535) return (int)hipErrorInvalidValue;
+  if (fmt == 0)
+    f8::cast_transpose_kernel<0><<<grid, 256, 0, st>>>((const bf16_t*)x, R, C, ldx, (uint8_t*)q, (uint8_t*)qt,
+                                                         (float*)hist, L, cur, (float*)scale_inv, margin_mul);
+  else
+    f8::cast_transpose_kernel<1><<<grid, 256, 0, st>>>((const bf16_t*)x, R, C, ldx, (uint8_t*)q, (uint8_t*)qt,
+                                                         (float*)hist, L, cur, (float*)scale_inv, margin_mul);
+  return (int)hipGetLastError();
+}
+
+PA_API int pa_fp8_amax(const void* x, int R, int C, long long ldx, void* out, hipStream_t st) {
+  if (R <= 0 || C <= 0 || C % 8 || ldx % 8) return (int)hipErrorInvalidValue;
+  const long long n8 = (long long)R * (C / 8);
+  int g = (int)((n8 + 255) / 256);
+  if (g > 2048) g = 2048;
+  f8::amax_kernel<<<g, 256, 0, st>>>((const bf16_t*)x, R, C, ldx, (float*)out);
+  return (int)hipGetLastError();
+}

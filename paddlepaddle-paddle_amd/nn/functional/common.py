@@ -17,6 +17,8 @@ def linear(x, weight, bias=None, name=None):
     """y = x @ W + b with W stored [in_features, out_features] (paddle layout)."""
     t, w = _u(x), _u(weight)
     b = _u(bias) if bias is not None else None
+    if ops.fp8._ACTIVE['enabled'] and ops.fp8.eligible(t, w):  # paddle.amp.fp8_autocast
+        return _w(ops.fp8.fp8_linear(t, w, b, holder=weight if isinstance(weight, Tensor) else None))
     if isinstance(weight, Tensor) and '_flat' in weight.__dict__ and ops.linear.eligible(weight) and \
             (bias is None or '_flat' in bias.__dict__):
         return _w(ops.linear.linear_accum(t, weight, bias))

@@ -61,6 +61,8 @@ _SIGS = {
     'pa_act_cs_tune': [I],
     'pa_flash_set_bwd_variant': [I],
     'pa_gemm_fp8_ok': [I, I, I, LL, LL, LL],
+    'pa_fp8_cast_transpose': [P, I, I, LL, P, P, P, I, I, P, I, F, P],
+    'pa_fp8_amax': [P, I, I, LL, P, P],
     'pa_gemm_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
     'pa_conv2d_fwd_ok': [I, I, I, I],
     'pa_conv2d_fwd': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],

@@ -1,0 +1,264 @@
+"""FP8 training path: delayed-scaling fp8 Linear (forward e4m3, gradients e5m2) on the
+hand-written CDNA4 kernels.
+
+* cast: ``csrc/fp8_cast.hip`` (``pa_fp8_cast_transpose``) — bf16 -> fp8 q and q^T in one pass,
+  scale from the device-resident amax history, current amax folded in with atomics (no host
+  sync anywhere on the step).
+* GEMM: ``csrc/gemm.hip`` ``gemm_fp8_kernel`` (v_mfma_scale_f32_16x16x128_f8f6f4, 2x the bf16
+  MFMA rate), TN layout, dequant scales read on the device.  Forward X@W, dgrad dY@W^T and wgrad
+  X^T@dY are all TN GEMMs over the q / q^T images (see fp8_cast.hip's header).
+
+Recipe (``DelayedScaling``): HYBRID = e4m3 forward operands + e5m2 gradients (the usual fp8
+training recipe), E4M3 = e4m3 everywhere; ``amax_history_len`` steps of history, ``margin``
+powers of two of headroom.  The first cast of a tensor seeds its history with an exact amax
+pre-pass (so step 0 is scaled too).
+
+Used by ``paddle.amp.fp8_autocast`` (dygraph: ``nn.functional.linear``) and by
+``paddle.static.amp.decorate(..., use_fp8=True)`` (the Executor substitutes recorded
+``addmm``/``mm``/``matmul``/``linear`` nodes whose weight is a trainable 2-D parameter).
+On CPU (or for shapes outside the kernel contract) the same math runs in torch (quantise with
+the same delayed scale, dequantised matmul), so the scaling logic is testable without a GPU.
+"""
+import contextlib
+
+import torch
+
+from . import _native as N
+
+E4M3, E5M2 = torch.float8_e4m3fn, torch.float8_e5m2
+_FMT = {E4M3: 0, E5M2: 1}
+_FMAX = {E4M3: 448.0, E5M2: 57344.0}
+
+
+class DelayedScaling:
+    """fp8 recipe (names follow the common delayed-scaling recipe)."""
+
+    def __init__(self, margin=0, fp8_format='HYBRID', amax_history_len=16, amax_compute_algo='max'):
+        fmt = str(fp8_format).upper()
+        if fmt not in ('HYBRID', 'E4M3'):
+            raise ValueError("fp8_format must be 'HYBRID' or 'E4M3'")
+        if amax_history_len < 3:
+            raise ValueError("amax_history_len must be >= 3")
+        if amax_compute_algo != 'max':
+            raise ValueError("only amax_compute_algo='max' is supported")
+        self.margin = int(margin)
+        self.fp8_format = fmt
+        self.amax_history_len = int(amax_history_len)
+        self.fwd_dtype = E4M3
+        self.bwd_dtype = E5M2 if fmt == 'HYBRID' else E4M3
+
+    def __repr__(self):
+        return (f"DelayedScaling(margin={self.margin}, fp8_format={self.fp8_format}, "
+                f"amax_history_len={self.amax_history_len})")
+
+
+class FP8Meta:
+    """Scaling state of one tensor role (activation / weight / gradient of one Linear)."""
+
+    def __init__(self, dtype, history_len, margin, device):
+        self.dtype = dtype
+        self.L = history_len
+        self.margin_mul = 2.0 ** (-margin)
+        self.hist = torch.zeros(history_len, dtype=torch.float32, device=device)
+        self.cur = 0
+        self.calls = 0
+
+    def scale(self):
+        """Quantisation scale the next cast will use (torch mirror of the kernel's rule)."""
+        L, cur = self.L, self.cur
+        mask = torch.ones(L, dtype=torch.bool, device=self.hist.device)
+        mask[cur] = False
+        mask[(cur + 1) % L] = False
+        am = self.hist[mask].max()
+        s = _FMAX[self.dtype] / am * self.margin_mul
+        return torch.where((am > 0) & torch.isfinite(s), s, torch.ones_like(s))
+
+    def cast(self, x2d, want_q=True, want_qt=True):
+        """x2d: [R, C] -> (q [R,C] | None, q^T [C,R] | None, dequant scale (1-elem fp32 tensor))."""
+        x2d = x2d if x2d.dtype == torch.bfloat16 else x2d.to(torch.bfloat16)
+        if x2d.stride(-1) != 1 or x2d.stride(0) % 8 or x2d.data_ptr() % 16:
+            x2d = x2d.contiguous()
+        R, C = x2d.shape
+        L, cur = self.L, self.cur
+        dev = x2d.device
+        sinv = torch.empty(1, dtype=torch.float32, device=dev)
+        use_hip = x2d.is_cuda and C % 8 == 0 and R > 0 and (N.lib is not None or N._load() is not None)
+        if x2d.is_cuda and not use_hip and N.lib is None:
+            raise RuntimeError(f"fp8 cast: HIP kernel library not loaded ({N.load_error})")
+        if self.calls == 0:  # seed the history with this tensor's exact amax
+            prev = (cur + L - 1) % L
+            if use_hip:
+                N.check(N.lib.pa_fp8_amax(N.ptr(x2d), R, C, x2d.stride(0), N.ptr(self.hist[prev:prev + 1]),
+                                          N.stream()), 'fp8_amax')
+            else:
+                self.hist[prev] = x2d.detach().abs().max().float()
+        q = torch.empty(R, C, dtype=self.dtype, device=dev) if want_q else None
+        qt = torch.empty(C, R, dtype=self.dtype, device=dev) if want_qt else None
+        if use_hip:
+            N.check(N.lib.pa_fp8_cast_transpose(N.ptr(x2d), R, C, x2d.stride(0), N.ptr(q), N.ptr(qt),
+                                                N.ptr(self.hist), L, cur, N.ptr(sinv), _FMT[self.dtype],
+                                                float(self.margin_mul), N.stream()), 'fp8_cast_transpose')
+        else:
+            with torch.no_grad():
+                s = self.scale()
+                fm = _FMAX[self.dtype]
+                qq = (x2d.float() * s).clamp(-fm, fm).to(self.dtype)
+                if q is not None:
+                    q.copy_(qq)
+                if qt is not None:
+                    qt.copy_(qq.t())
+                self.hist[cur] = torch.maximum(self.hist[cur], x2d.detach().abs().max().float())
+                self.hist[(cur + 1) % L] = 0.0
+                sinv.copy_(1.0 / s.reshape(1))
+        self.cur = (cur + 1) % L
+        self.calls += 1
+        return q, qt, sinv
+
+
+def fp8_mm(a, b, sa, sb, bias=None, out_dtype=torch.bfloat16):
+    """out[M,N] = (sa*sb) * a[M,K] @ b[N,K]^T (+ bias) with fp8 a/b (TN layout)."""
+    from .gemm import hip_fp8_ok, hip_fp8_mm
+    if a.is_cuda and out_dtype == torch.bfloat16 and hip_fp8_ok(a, b):
+        bb = None
+        if bias is not None:
+            bb = bias if bias.dtype == torch.bfloat16 and bias.is_contiguous() else bias.to(torch.bfloat16).contiguous()
+        return hip_fp8_mm(a, b, scale_a=sa, scale_b=sb, bias=bb)
+    # outside the kernel contract (K % 128, M/N % 8) or on CPU: exact dequantised product
+    out = (a.float() @ b.float().t()) * (sa * sb)
+    if bias is not None:
+        out = out + bias.float()
+    return out.to(out_dtype)
+
+
+class FP8State:
+    """The three metas of one fp8 Linear (kept on the weight Parameter)."""
+
+    def __init__(self, recipe, device):
+        L, m = recipe.amax_history_len, recipe.margin
+        self.x = FP8Meta(recipe.fwd_dtype, L, m, device)
+        self.w = FP8Meta(recipe.fwd_dtype, L, m, device)
+        self.g = FP8Meta(recipe.bwd_dtype, L, m, device)
+        self.recipe = recipe
+
+
+class _FP8Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, st):
+        K, Nout = w.shape
+        x2 = x.reshape(-1, K)
+        need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        xq, xqt, sx = st.x.cast(x2, want_q=True, want_qt=need_dw)
+        wq, wqt, sw = st.w.cast(w, want_q=need_dx, want_qt=True)  # wqt: [N, K]
+        y = fp8_mm(xq, wqt, sx, sw, bias=b)
+        ctx.save_for_backward(xqt, wq, sx, sw)
+        ctx.st, ctx.xshape, ctx.has_b, ctx.wdt, ctx.xdt = st, x.shape, b is not None, w.dtype, x.dtype
+        ctx.bdt = b.dtype if b is not None else None
+        return y.reshape(*x.shape[:-1], Nout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xqt, wq, sx, sw = ctx.saved_tensors
+        st = ctx.st
+        Nout = dy.shape[-1]
+        dy2 = dy.reshape(-1, Nout)
+        need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        gq, gqt, sg = st.g.cast(dy2, want_q=need_dx, want_qt=need_dw)
+        dx = dw = db = None
+        if need_dx:
+            dx = fp8_mm(gq, wq, sg, sw).reshape(ctx.xshape).to(ctx.xdt)
+        if need_dw:
+            dw = fp8_mm(xqt, gqt, sx, sg).to(ctx.wdt)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = dy2.float().sum(0).to(ctx.bdt)
+        return dx, dw, db, None
+
+
+def _state_for(weight_holder, w, recipe):
+    st = weight_holder.__dict__.get('_fp8_state') if weight_holder is not None else None
+    if st is None or st.recipe is not recipe:
+        st = FP8State(recipe, w.device)
+        if weight_holder is not None:
+            weight_holder.__dict__['_fp8_state'] = st
+    return st
+
+
+_STATIC_STATES = {}
+
+
+def fp8_linear(x, w, b=None, recipe=None, holder=None, key=None):
+    """y = x @ w (+ b), w stored [in, out] (paddle layout), through the fp8 kernels."""
+    recipe = recipe or _ACTIVE['recipe'] or DelayedScaling()
+    if holder is None:  # static replay: state keyed by the weight storage
+        key = key if key is not None else (id(w), w.data_ptr())
+        st = _STATIC_STATES.get(key)
+        if st is None or st.recipe is not recipe:
+            st = _STATIC_STATES[key] = FP8State(recipe, w.device)
+    else:
+        st = _state_for(holder, w, recipe)
+    return _FP8Linear.apply(x, w, b, st)
+
+
+# ----------------------------------------------------------------------------- autocast state
+_ACTIVE = {'enabled': False, 'recipe': None}
+
+
+def fp8_enabled():
+    return _ACTIVE['enabled']
+
+
+@contextlib.contextmanager
+def fp8_autocast(enabled=True, fp8_recipe=None):
+    """Run eligible Linear layers (2-D weight, in/out features % 8) in fp8 inside the block."""
+    prev = dict(_ACTIVE)
+    _ACTIVE['enabled'] = bool(enabled)
+    _ACTIVE['recipe'] = fp8_recipe or prev['recipe'] or DelayedScaling()
+    try:
+        yield
+    finally:
+        _ACTIVE.clear()
+        _ACTIVE.update(prev)
+
+
+def eligible(x, w):
+    return (w.dim() == 2 and w.is_floating_point() and x.is_floating_point() and w.shape[0] % 8 == 0
+            and w.shape[1] % 8 == 0 and x.shape[-1] == w.shape[0] and x.numel() > 0)
+
+
+# ----------------------------------------------------------------------------- static replay
+_STATIC_RECIPE = {'recipe': None}  # set by the Executor while it replays an fp8 Program
+
+
+def _is_weight(w):
+    return isinstance(w, torch.Tensor) and w.dim() == 2 and w.is_leaf and w.requires_grad
+
+
+def _sub_addmm(orig):
+    def f(bias, x, w, *a, **k):
+        if not a and not k and _is_weight(w) and eligible(x, w) and bias.dim() == 1:
+            return fp8_linear(x, w, bias, recipe=_STATIC_RECIPE['recipe'])
+        return orig(bias, x, w, *a, **k)
+    return f
+
+
+def _sub_mm(orig):
+    def f(x, w, *a, **k):
+        if not a and not k and _is_weight(w) and eligible(x, w):
+            return fp8_linear(x, w, recipe=_STATIC_RECIPE['recipe'])
+        return orig(x, w, *a, **k)
+    return f
+
+
+def _sub_linear(orig):
+    def f(x, w, bias=None):  # torch layout w [out, in]
+        if _is_weight(w) and w.dim() == 2 and eligible(x, w.t()):
+            return fp8_linear(x, w.t(), bias, recipe=_STATIC_RECIPE['recipe'], key=(id(w), w.data_ptr()))
+        return orig(x, w, bias)
+    return f
+
+
+STATIC_SUBS = {
+    torch.addmm: _sub_addmm(torch.addmm),
+    torch.mm: _sub_mm(torch.mm),
+    torch.matmul: _sub_mm(torch.matmul),
+    torch.nn.functional.linear: _sub_linear(torch.nn.functional.linear),
+}

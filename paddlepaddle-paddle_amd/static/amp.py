@@ -96,8 +96,9 @@ bf16_guard = fp16_guard
 class OptimizerWithMixedPrecision:
     def __init__(self, optimizer, amp_lists, level, dtype, init_loss_scaling, use_dynamic_loss_scaling,
                  incr_every_n_steps, decr_every_n_nan_or_inf, incr_ratio, decr_ratio, master_weight=None,
-                 use_promote=False):
+                 use_promote=False, fp8_recipe=None):
         self._optimizer = optimizer
+        self._fp8 = fp8_recipe
         self._amp_lists = amp_lists or AutoMixedPrecisionLists(dtype=dtype)
         self._level = level
         self._dtype = _dt.to_torch_dtype(dtype)
@@ -134,7 +135,7 @@ class OptimizerWithMixedPrecision:
     def minimize(self, loss, startup_program=None, parameter_list=None, no_grad_set=None):
         from .program import default_main_program, _static_minimize
         prog = default_main_program()
-        prog._amp = {'level': self._level, 'dtype': self._dtype, 'lists': self._amp_lists}
+        prog._amp = {'level': self._level, 'dtype': self._dtype, 'lists': self._amp_lists, 'fp8': self._fp8}
         self._program = prog
         opt_ops, params_grads = _static_minimize(self._optimizer, loss, parameter_list, no_grad_set)
         prog.nodes[-1].target = self  # executed through _static_minimize_exec (loss scaling)
@@ -186,16 +187,31 @@ class OptimizerWithMixedPrecision:
 def decorate(optimizer, amp_lists=None, level='O1', dtype='float16', master_weight=None, master_grad=False,
              init_loss_scaling=2 ** 16, incr_every_n_steps=2000, decr_every_n_nan_or_inf=1, incr_ratio=2.0,
              decr_ratio=0.5, use_dynamic_loss_scaling=None, use_amp_guard=False, use_promote=False,
-             use_pure_fp16=False, use_fp16_guard=None, use_bf16=False, **kw):
+             use_pure_fp16=False, use_fp16_guard=None, use_bf16=False, use_fp8=False, fp8_recipe=None, **kw):
+    """Static AMP decorator (reference static/amp/decorator.py:755).
+
+    ``use_fp8=True`` (or ``dtype='float8_e4m3fn'``) additionally runs every recorded Linear /
+    matmul whose weight is a trainable 2-D parameter through the fp8 path (ops/fp8.py: e4m3
+    forward, e5m2 gradients, delayed scaling from ``fp8_recipe`` — a ``paddle.amp.DelayedScaling``);
+    the remaining white-list ops run in bfloat16.  The reference framework has no fp8 AMP; this
+    is the MI355X extension named by BASELINE config 5.
+    """
+    if str(dtype).lower().replace('paddle.', '') in ('float8_e4m3fn', 'fp8', 'float8'):
+        use_fp8, dtype = True, 'bfloat16'
     if use_pure_fp16:
         level = 'O2'
-    if use_bf16:
+    if use_bf16 or use_fp8:
         dtype = 'bfloat16'
     if level not in ('O1', 'O2', 'OD'):
         raise ValueError(f"static amp level must be O1/O2/OD, got {level}")
+    recipe = None
+    if use_fp8:
+        from ..ops.fp8 import DelayedScaling
+        recipe = fp8_recipe or DelayedScaling()
     return OptimizerWithMixedPrecision(optimizer, amp_lists, 'O1' if level == 'OD' else level, dtype,
                                        init_loss_scaling, use_dynamic_loss_scaling, incr_every_n_steps,
-                                       decr_every_n_nan_or_inf, incr_ratio, decr_ratio, master_weight, use_promote)
+                                       decr_every_n_nan_or_inf, incr_ratio, decr_ratio, master_weight, use_promote,
+                                       fp8_recipe=recipe)
 
 
 class _BF16Namespace:  # paddle.static.amp.bf16
@@ -218,9 +234,33 @@ class _BF16Namespace:  # paddle.static.amp.bf16
 bf16 = _BF16Namespace()
 
 
+@contextlib.contextmanager
 def autocast_context(program, dev):
     """Replay context for a Program carrying an AMP config (used by the Executor)."""
     cfg = getattr(program, '_amp', None)
     if not cfg:
-        return contextlib.nullcontext()
-    return torch.autocast(device_type='cuda' if dev.type == 'cuda' else 'cpu', dtype=cfg['dtype'])
+        yield None
+        return
+    from ..ops import fp8 as _fp8
+    prev = _fp8._STATIC_RECIPE['recipe']
+    _fp8._STATIC_RECIPE['recipe'] = cfg.get('fp8')
+    try:
+        with torch.autocast(device_type='cuda' if dev.type == 'cuda' else 'cpu', dtype=cfg['dtype']):
+            yield _fp8.STATIC_SUBS if cfg.get('fp8') is not None else None
+    finally:
+        _fp8._STATIC_RECIPE['recipe'] = prev
+
+
+class _FP8Namespace:  # paddle.static.amp.fp8
+    @staticmethod
+    def decorate_fp8(optimizer, amp_lists=None, fp8_recipe=None, use_pure_bf16=True, **kw):
+        return decorate(optimizer, amp_lists, level='O2' if use_pure_bf16 else 'O1', use_fp8=True,
+                        fp8_recipe=fp8_recipe, **kw)
+
+    @staticmethod
+    def DelayedScaling(*a, **k):
+        from ..ops.fp8 import DelayedScaling
+        return DelayedScaling(*a, **k)
+
+
+fp8 = _FP8Namespace()

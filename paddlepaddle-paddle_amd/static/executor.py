@@ -154,14 +154,19 @@ def _feed_tensor(v, dt, dev):
     return t.to(device=dev, dtype=dt)
 
 
+_SUBS = {'map': None}  # target substitutions of the running replay (static.amp fp8: ops/fp8.py)
+
+
 def _exec(prog, nodes, env, smap, dev):
+    subs = _SUBS['map']
     for n in nodes:
         if n.kind == 'torch':
             args = _resolve(prog, n.args, env, smap, dev)
             kwargs = _resolve(prog, n.kwargs, env, smap, dev)
             if n.meta.get('factory') and 'device' in kwargs and kwargs['device'] is None:
                 kwargs['device'] = dev
-            _bind(env, n.outs, n.target(*args, **kwargs))
+            fn = subs.get(n.target, n.target) if subs else n.target
+            _bind(env, n.outs, fn(*args, **kwargs))
         elif n.kind == 'minimize':
             loss = env[n.args[0].vid]
             if hasattr(n.target, '_static_minimize_exec'):  # static.amp: loss scaling / skip-on-inf
@@ -234,8 +239,12 @@ def run_program(prog, feed, dev, grad=None):
     needs_grad = grad if grad is not None else any(n.kind in ('minimize', 'backward', 'grad') for n in prog.nodes)
     ctx = contextlib.nullcontext() if needs_grad else torch.no_grad()
     from .amp import autocast_context
-    with _paused(), ctx, autocast_context(prog, dev):
-        _exec(prog, prog.nodes, env, smap, dev)
+    with _paused(), ctx, autocast_context(prog, dev) as subs:
+        prev, _SUBS['map'] = _SUBS['map'], subs
+        try:
+            _exec(prog, prog.nodes, env, smap, dev)
+        finally:
+            _SUBS['map'] = prev
     return env
 
 

@@ -20,3 +20,11 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if 'gpu' in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture
+def static_mode():
+    import paddle
+    paddle.enable_static()
+    yield
+    paddle.disable_static()

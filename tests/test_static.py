@@ -6,13 +6,6 @@ import paddle
 import paddle.static as static
 
 
-@pytest.fixture
-def static_mode():
-    paddle.enable_static()
-    yield
-    paddle.disable_static()
-
-
 def test_static_mlp_trains_and_matches_dygraph(static_mode):
     paddle.seed(7)
     main, startup = static.Program(), static.Program()
