@@ -16,15 +16,18 @@
 // slot the NEXT call records into (no reader of this call touches either slot).  Block 0 also
 // writes the dequant scale 1/scale to scale_inv, which the fp8 GEMM reads on the device.
 //
-// Tiles: 64x64 per 256-thread block; thread t owns row t/4, 16 columns (two 16-B bf16 loads),
-// stores 16 fp8 bytes of q, and scatters the bytes through an LDS tile for the 16-B row stores
-// of q^T.  Edge tiles take the guarded element path.
+// Tiles: 128x128 per 256-thread block.  Row pass: thread t owns 64 contiguous columns of row
+// t/2 (8 x 16-B bf16 loads), stores 64 fp8 bytes of q and the same bytes as 16-B LDS writes
+// into a [128][144] byte tile.  Column pass: thread t gathers 64 rows of input column t/2 from
+// the tile (byte reads: 4 lanes share a dword, conflict free) and stores them as 4 x 16-B
+// chunks of the q^T row — every q / q^T row segment a wave writes is a whole 128-B line.
+// Edge tiles take the guarded element path.
 #include "common.h"
 
 namespace pa {
 namespace f8 {
 
-constexpr int T = 64;
+constexpr int T = 128;
 
 template <int FMT>
 __device__ __forceinline__ float fmax_of() { return FMT == 0 ? 448.f : 57344.f; }
@@ -61,51 +64,67 @@ __global__ __launch_bounds__(256) void cast_transpose_kernel(const bf16_t* __res
                                                              uint8_t* __restrict__ q, uint8_t* __restrict__ qt,
                                                              float* __restrict__ hist, int L, int cur,
                                                              float* __restrict__ scale_inv, float margin_mul) {
-  __shared__ uint8_t tile[T][T + 16];  // [col][row] fp8 bytes (16-B padded rows)
+  __shared__ __attribute__((aligned(16))) uint8_t tile[T][T + 16];  // [row][col] fp8 bytes, 16-B padded rows
   __shared__ float red[4];
   const float fmax = fmax_of<FMT>();
   const float s = scale_from_hist(hist, L, cur, fmax, margin_mul);
   const int tid = threadIdx.x;
   const int r0 = blockIdx.y * T, c0 = blockIdx.x * T;
-  const int lr = tid >> 2, lc = (tid & 3) * 16;
+  const int lr = tid >> 1, lc = (tid & 1) * 64;  // row pass: 64 contiguous columns of one row
   const int r = r0 + lr, c = c0 + lc;
   const bool full = (r0 + T <= R) && (c0 + T <= C);
-  float v[16];
-  if (full) {
-    load_f<bf16_t, 8>(x + (long long)r * ldx + c, *reinterpret_cast<float(*)[8]>(&v[0]));
-    load_f<bf16_t, 8>(x + (long long)r * ldx + c + 8, *reinterpret_cast<float(*)[8]>(&v[8]));
-  } else {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = (r < R && c + i < C) ? (float)x[(long long)r * ldx + c + i] : 0.f;
-  }
   float am = 0.f;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) am = fmaxf(am, fabsf(v[i]));
-  uint32_t w[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    w[i] = cvt2<FMT>(v[4 * i] * s, v[4 * i + 1] * s) | (cvt2<FMT>(v[4 * i + 2] * s, v[4 * i + 3] * s) << 16);
-  if (q) {
+  for (int h = 0; h < 4; ++h) {  // 4 x 16 columns: two 16-B bf16 loads -> one 16-B fp8 chunk
+    float v[16];
+    const int cc = c + 16 * h;
     if (full) {
-      *reinterpret_cast<uint4*>(q + (long long)r * C + c) = make_uint4(w[0], w[1], w[2], w[3]);
-    } else if (r < R) {
+      load_f<bf16_t, 8>(x + (long long)r * ldx + cc, *reinterpret_cast<float(*)[8]>(&v[0]));
+      load_f<bf16_t, 8>(x + (long long)r * ldx + cc + 8, *reinterpret_cast<float(*)[8]>(&v[8]));
+    } else {
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (c + i < C) q[(long long)r * C + c + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+      for (int i = 0; i < 16; ++i) v[i] = (r < R && cc + i < C) ? (float)x[(long long)r * ldx + cc + i] : 0.f;
     }
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      am = fmaxf(am, fmaxf(fmaxf(fabsf(v[4 * i]), fabsf(v[4 * i + 1])), fmaxf(fabsf(v[4 * i + 2]), fabsf(v[4 * i + 3]))));
+      w[i] = cvt2<FMT>(v[4 * i] * s, v[4 * i + 1] * s) | (cvt2<FMT>(v[4 * i + 2] * s, v[4 * i + 3] * s) << 16);
+    }
+    const uint4 pk = make_uint4(w[0], w[1], w[2], w[3]);
+    if (q) {
+      if (full) {
+        *reinterpret_cast<uint4*>(q + (long long)r * C + cc) = pk;
+      } else if (r < R) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (cc + i < C) q[(long long)r * C + cc + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+      }
+    }
+    if (qt) *reinterpret_cast<uint4*>(&tile[lr][lc + 16 * h]) = pk;
   }
   if (qt) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) tile[lc + i][lr] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
     __syncthreads();
-    // q^T row (input column) c0 + lr, 16 bytes of input rows r0 + lc ..
-    const int orow = c0 + lr, ocol = r0 + lc;
-    if (full) {
-      *reinterpret_cast<uint4*>(qt + (long long)orow * R + ocol) = *reinterpret_cast<const uint4*>(&tile[lr][lc]);
-    } else if (orow < C) {
+    // column pass: q^T row (input column) c0 + oc, 64 bytes of input rows r0 + orr ..
+    const int oc = tid >> 1, orr = (tid & 1) * 64;
+    const int orow = c0 + oc;
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (ocol + i < R) qt[(long long)orow * R + ocol + i] = tile[lr][lc + i];
+    for (int h = 0; h < 4; ++h) {
+      uint32_t w[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rr = orr + 16 * h + 4 * i;
+        w[i] = (uint32_t)tile[rr][oc] | ((uint32_t)tile[rr + 1][oc] << 8) | ((uint32_t)tile[rr + 2][oc] << 16) |
+               ((uint32_t)tile[rr + 3][oc] << 24);
+      }
+      const int ocol = r0 + orr + 16 * h;
+      if (full) {
+        *reinterpret_cast<uint4*>(qt + (long long)orow * R + ocol) = make_uint4(w[0], w[1], w[2], w[3]);
+      } else if (orow < C) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (ocol + i < R) qt[(long long)orow * R + ocol + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+      }
     }
   }
   am = wave_max(am);
