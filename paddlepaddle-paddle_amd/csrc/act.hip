@@ -16,22 +16,7 @@ struct GeluErf {
     return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
   }
 };
-// tanh(u) = 1 - 2 / (1 + e^{2u}) on the v_exp_f32 path (libm tanhf is a long polynomial
-// branch ladder: it made the GeLU kernels VALU-bound instead of HBM-bound).  Saturates
-// correctly at both ends (e^{2u} -> inf gives 1, -> 0 gives -1); |error| ~ 1e-7.
-__device__ __forceinline__ float fast_tanh(float u) { return 1.f - __fdividef(2.f, 1.f + __expf(2.f * u)); }
-
-struct GeluTanh {
-  static __device__ __forceinline__ float f(float x) {
-    const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
-    return 0.5f * x * (1.f + fast_tanh(u));
-  }
-  static __device__ __forceinline__ float df(float x) {
-    const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
-    const float t = fast_tanh(u);
-    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.79788456080286536f * (1.f + 3.f * 0.044715f * x * x);
-  }
-};
+// fast_tanh / GeluTanh live in common.h (shared with the GEMM epilogues of gemm8.hip)
 struct Silu {
   static __device__ __forceinline__ float f(float x) { return x / (1.f + __expf(-x)); }
   static __device__ __forceinline__ float df(float x) {

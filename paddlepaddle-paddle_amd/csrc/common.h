@@ -87,6 +87,23 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return r;
 }
 
+// tanh(u) = 1 - 2 / (1 + e^{2u}) on the v_exp_f32 path (libm tanhf is a long polynomial
+// branch ladder: it made the GeLU kernels VALU-bound instead of HBM-bound).  Saturates
+// correctly at both ends (e^{2u} -> inf gives 1, -> 0 gives -1); |error| ~ 1e-7.
+__device__ __forceinline__ float fast_tanh(float u) { return 1.f - __fdividef(2.f, 1.f + __expf(2.f * u)); }
+
+struct GeluTanh {
+  static __device__ __forceinline__ float f(float x) {
+    const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
+    return 0.5f * x * (1.f + fast_tanh(u));
+  }
+  static __device__ __forceinline__ float df(float x) {
+    const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
+    const float t = fast_tanh(u);
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.79788456080286536f * (1.f + 3.f * 0.044715f * x * x);
+  }
+};
+
 // Counter-based RNG (for dropout): a cheap stateless hash of (seed, offset, index) → uniform [0,1).
 __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
   // murmur3-style finaliser chain

@@ -156,6 +156,28 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __r
       if (n >= N) continue;  // N % 8 == 0: a 4-wide group is all in or all out
       if constexpr (EPI == 1) {
         *reinterpret_cast<f32x4*>(ws + (long long)blockIdx.z * M * N + (long long)m * N + n) = acc[i][j];
+      } else if constexpr (EPI == 2) {  // h = alpha*acc + bias -> aux (bf16), C = gelu_tanh(h)
+        float h[4] = {acc[i][j][0] * alpha, acc[i][j][1] * alpha, acc[i][j][2] * alpha, acc[i][j][3] * alpha};
+        if (bias) {
+          float bb[4];
+          load_f<bf16_t, 4>(reinterpret_cast<const bf16_t*>(bias + n), bb);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[r] += bb[r];
+        }
+        const long long o = (long long)m * ldc + n;
+        store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(ws) + o, h);
+        float g[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) g[r] = GeluTanh::f(h[r]);
+        store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(C + o), g);
+      } else if constexpr (EPI == 3) {  // C = alpha*acc * gelu_tanh'(aux)  (aux = saved pre-activation)
+        const long long o = (long long)m * ldc + n;
+        float h[4];
+        load_f<bf16_t, 4>(reinterpret_cast<const bf16_t*>(ws) + o, h);
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * alpha * GeluTanh::df(h[r]);
+        store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(C + o), v);
       } else {
         float v[4] = {acc[i][j][0] * alpha, acc[i][j][1] * alpha, acc[i][j][2] * alpha, acc[i][j][3] * alpha};
         uint16_t* dst = C + (long long)m * ldc + n;
@@ -200,7 +222,10 @@ __device__ __forceinline__ void epilogue_z(const f32x4 (&acc)[8][4], uint16_t* _
   }
 }
 
-// EPI 0: bf16 C = alpha*acc (+ beta*C) (+ bias);  EPI 1: raw fp32 split-K slab (ws[z][M][N]).
+// EPI 0: bf16 C = alpha*acc (+ beta*C) (+ bias);  EPI 1: raw fp32 split-K slab (ws[z][M][N]);
+// EPI 2: fc1 forward, h = alpha*acc + bias stored to aux (= ws, bf16, ldc) and C = gelu_tanh(h);
+// EPI 3: fc2 dgrad, C = alpha*acc * gelu_tanh'(aux) (aux = the saved h): the bias_act kernels of
+// the MLP (reference fusion/gpu/fused_gemm_epilogue_kernel.cu, fused_gemm_epilogue_grad) vanish.
 template <bool AK, bool BKM, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm8_kernel(const char* __restrict__ A, const char* __restrict__ B,
                                                        uint16_t* __restrict__ C, float* __restrict__ ws,
@@ -904,6 +929,20 @@ static hipError_t dispatch(int transA, int transB, const void* A, const void* B,
   return launch<false, false, EPI>(A, B, C, ws, bias, M, N, K, lda, ldb, ldc, alpha, beta, splitk, st);
 }
 
+template <int EPI>
+static hipError_t launch_epi(int transB, const void* A, const void* B, void* C, void* aux, const void* bias, int M,
+                             int N, int K, long long lda, long long ldb, long long ldc, float alpha, hipStream_t st) {
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  dim3 grid(tm * tn, 1, 1);
+  if (transB)
+    gemm11_kernel<true, true, EPI><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, (float*)aux,
+                                                         (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, 0.f, K);
+  else
+    gemm11_kernel<true, false, EPI><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, (float*)aux,
+                                                          (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, 0.f, K);
+  return hipGetLastError();
+}
+
 }  // namespace g8
 }  // namespace pa
 
@@ -934,6 +973,18 @@ PA_API int pa_gemm8_bf16(const void* A, const void* B, void* C, const void* bias
     return (int)dispatch<0>(transA, transB, A, B, C, nullptr, bias, M, N, K, lda, ldb, ldc, alpha, beta, 1, st);
   if (!ws) return (int)hipErrorInvalidValue;
   return (int)dispatch<1>(transA, transB, A, B, C, (float*)ws, nullptr, M, N, K, lda, ldb, ldc, 1.f, 0.f, splitk, st);
+}
+
+// Fused-epilogue GEMMs of the GPT MLP (A k-contiguous [M][lda], schedule 11).  epi 2: C = gelu(h),
+// aux = h = alpha*A@B + bias;  epi 3: C = alpha*A@B * gelu'(aux).  aux: bf16 [M][ldc].
+PA_API int pa_gemm8_bf16_epi(const void* A, const void* B, void* C, const void* bias, void* aux, int M, int N, int K,
+                             long long lda, long long ldb, long long ldc, int transB, float alpha, int epi,
+                             hipStream_t st) {
+  using namespace pa::g8;
+  if (!pa_gemm8_ok(M, N, K, lda, ldb, ldc, 0, transB, 1) || !aux) return (int)hipErrorInvalidValue;
+  if (epi == 2) return (int)launch_epi<2>(transB, A, B, C, aux, bias, M, N, K, lda, ldb, ldc, alpha, st);
+  if (epi == 3) return (int)launch_epi<3>(transB, A, B, C, aux, nullptr, M, N, K, lda, ldb, ldc, alpha, st);
+  return (int)hipErrorInvalidValue;
 }
 
 // schedule select (A/B benchmarking): 8 = row-half staging, 9 = k-half staging (default),

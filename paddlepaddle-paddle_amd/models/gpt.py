@@ -147,9 +147,12 @@ class GPTDecoderLayer(nn.Layer):
         o = F.linear(self.attn.core(a), self.attn.out_proj.weight, None)
         b, h = fz.dropout_add_norm(_unwrap(o), self.attn.out_proj.bias, _unwrap(h), self.ln2.weight._t,
                                    self.ln2.bias._t, self.ln2._epsilon, self.p)
-        z = F.linear(_wrap(b), self.mlp.fc1.weight, None)
-        g = fz.bias_act(_unwrap(z), self.mlp.fc1.bias, 'gelu_tanh')
-        return self.mlp.fc2(_wrap(g)), _wrap(h)
+        m = self.mlp
+        if ops.linear.mlp_gelu_ok(b, m.fc1.weight, m.fc1.bias, m.fc2.weight):  # GELU in the GEMM epilogues
+            return _wrap(ops.linear.mlp_gelu(b, m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias)), _wrap(h)
+        z = F.linear(_wrap(b), m.fc1.weight, None)
+        g = fz.bias_act(_unwrap(z), m.fc1.bias, 'gelu_tanh')
+        return m.fc2(_wrap(g)), _wrap(h)
 
 
 class GPTEmbeddings(nn.Layer):

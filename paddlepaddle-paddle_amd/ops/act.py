@@ -101,13 +101,10 @@ def swiglu(a, b):
     return _Swiglu.apply(a, b)
 
 
-_seed_counter = [0]
-
-
 def _next_seed(n):
-    seed = int(torch.randint(0, 2 ** 31 - 1, (1,), device='cpu').item())
-    _seed_counter[0] += 1
-    return seed, _seed_counter[0] & 0xFFFFFFFF
+    """(seed, offset) from the paddle.seed-controlled host generator (see ops.fused._next_seed)."""
+    seed, off = torch.randint(0, 2 ** 31 - 1, (2,), device='cpu').tolist()
+    return seed, off
 
 
 class _DropoutAdd(torch.autograd.Function):

@@ -102,13 +102,12 @@ def bias_act_ok(x, bias_param):
     return _hip(x) and b.dtype == x.dtype and x.shape[-1] % (16 // x.element_size()) == 0 and N._load() is not None
 
 
-_seed = [0]
-
-
 def _next_seed():
-    s = int(torch.randint(0, 2 ** 31 - 1, (1,), device='cpu').item())
-    _seed[0] = (_seed[0] + 1) & 0xFFFFFFFF
-    return s, _seed[0]
+    """(seed, offset) of one dropout call, both drawn from the host generator, so paddle.seed
+    fully determines every keep-mask (reference: the per-op seed/offset pair of the CUDA
+    dropout kernels, derived from the paddle.seed-controlled generator)."""
+    s, o = torch.randint(0, 2 ** 31 - 1, (2,), device='cpu').tolist()
+    return s, o
 
 
 class _DropAddNorm(torch.autograd.Function):

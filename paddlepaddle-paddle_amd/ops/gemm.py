@@ -75,6 +75,34 @@ def hip_mm(a, b, out=None, bias=None, alpha=1.0, beta=0.0, splitk=1):
 _hip_gemm = os.environ.get('PADDLE_AMD_HIP_GEMM', '1') != '0'
 
 
+def epi_ok(a, b, out_cols):
+    """Shape/layout contract of the fused-epilogue GEMMs (mm_epi): a k-contiguous [M,K]."""
+    if not _hip_gemm or not a.is_cuda or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        return False
+    ta, lda = _op_layout(a)
+    tb, ldb = _op_layout(b)
+    if ta != 0 or tb is None or a.data_ptr() % 16 or b.data_ptr() % 16 or N._load() is None:
+        return False
+    return bool(N.lib.pa_gemm8_ok(a.shape[0], out_cols, a.shape[1], lda, ldb, out_cols, 0, tb, 1))
+
+
+def mm_epi(a, b, epi, aux, bias=None, out=None):
+    """Fused-epilogue GEMM of the MLP (csrc/gemm8.hip pa_gemm8_bf16_epi, schedule 11).
+
+    epi 2 (fc1 forward): h = a @ b + bias is written to ``aux`` and gelu_tanh(h) is returned;
+    epi 3 (fc2 dgrad):   returns (a @ b) * gelu_tanh'(aux).   a: [M,K] row-major; b: [K,N]
+    (row-major or a transposed view of [N,K]); aux: bf16 [M,N] contiguous."""
+    tb, ldb = _op_layout(b)
+    M, K = a.shape
+    N_ = b.shape[1]
+    if out is None:
+        out = torch.empty(M, N_, dtype=torch.bfloat16, device=a.device)
+    assert aux.shape == (M, N_) and aux.is_contiguous() and out.is_contiguous()
+    N.check(N.lib.pa_gemm8_bf16_epi(N.ptr(a), N.ptr(b), N.ptr(out), N.ptr(bias), N.ptr(aux), M, N_, K, a.stride(0),
+                                    ldb, N_, tb, 1.0, int(epi), N.stream()), f'gemm_epi{epi}')
+    return out
+
+
 def _splitk_for(M, N_, K):
     """Split-K factor for outputs with too few 256x256 tiles to fill 256 CUs (the 2048x2048
     out-projection weight gradient: 64 tiles x 4 slices, profiles/r2_gemm_sched.log)."""

@@ -39,31 +39,88 @@ class _LinearAccum(torch.autograd.Function):
         wp, bp = ctx.box
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = gemm.mm(dy2, w.t()).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
-        gw = flat_grad_slot(wp)
-        if gw is not None:
-            if not gemm.wgrad_accumulate(x2, dy2, gw):
-                gw.addmm_(x2.t(), dy2)
-            notify_grad_ready(wp)
-            dw = None
-        else:
-            dw = gemm.mm(x2.t(), dy2)
-        db = None
-        if bp is not None:
-            gb = flat_grad_slot(bp)
-            if fused.colsum_ok(dy2):  # one column-blocked HIP pass, accumulated in place
-                if gb is not None:
-                    fused.colsum(dy2, gb, accumulate=True)
-                    notify_grad_ready(bp)
-                else:
-                    db = fused.colsum(dy2).to(dy2.dtype)
-            else:
-                s = dy2.sum(0, dtype=torch.float32)
-                if gb is not None:
-                    gb.add_(s.to(gb.dtype))
-                    notify_grad_ready(bp)
-                else:
-                    db = s.to(dy2.dtype)
+        dw = _grad_w(x2, dy2, wp)
+        db = _grad_b(dy2, bp) if bp is not None else None
         return dx, dw, db, None
+
+
+def _grad_w(x2, dy2, wp):
+    """W.grad += x2^T @ dy2 in the flat slot (returns None) or the gradient tensor."""
+    gw = flat_grad_slot(wp)
+    if gw is not None:
+        if not gemm.wgrad_accumulate(x2, dy2, gw):
+            gw.addmm_(x2.t(), dy2)
+        notify_grad_ready(wp)
+        return None
+    return gemm.mm(x2.t(), dy2)
+
+
+def _grad_b(dy2, bp):
+    """b.grad += colsum(dy2) in the flat slot (returns None) or the gradient tensor."""
+    gb = flat_grad_slot(bp)
+    if fused.colsum_ok(dy2):  # one column-blocked HIP pass, accumulated in place
+        if gb is not None:
+            fused.colsum(dy2, gb, accumulate=True)
+            notify_grad_ready(bp)
+            return None
+        return fused.colsum(dy2).to(dy2.dtype)
+    s = dy2.sum(0, dtype=torch.float32)
+    if gb is not None:
+        gb.add_(s.to(gb.dtype))
+        notify_grad_ready(bp)
+        return None
+    return s.to(dy2.dtype)
+
+
+class _MLPGelu(torch.autograd.Function):
+    """y = gelu_tanh(x @ W1 + b1) @ W2 + b2 with the activation inside the GEMM epilogues:
+    forward fc1 writes h = x@W1 + b1 and g = gelu(h) in one epilogue (EPI 2), backward's fc2
+    dgrad writes dh = (dy @ W2^T) * gelu'(h) (EPI 3) — no standalone bias+activation kernel
+    either way (reference: fusion/gpu/fused_gemm_epilogue_kernel.cu + its _grad kernel)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, boxes):
+        for w in (w1, w2):
+            if w.untyped_storage().nbytes() == 0:
+                raise RuntimeError("linear weight storage is released (sharding stage-3 unit not gathered)")
+        x2 = x.reshape(-1, x.shape[-1])
+        M, F_ = x2.shape[0], w1.shape[1]
+        wt1 = gemm.kmajor_weight(x2, w1)
+        h = torch.empty(M, F_, dtype=x2.dtype, device=x2.device)
+        g = gemm.mm_epi(x2, w1 if wt1 is None else wt1.t(), 2, h, bias=b1)
+        wt2 = gemm.kmajor_weight(g, w2)
+        y = gemm.mm(g, w2 if wt2 is None else wt2.t(), bias=b2)
+        ctx.save_for_backward(x2, w1, w2, h, g)
+        ctx.boxes, ctx.xshape = boxes, x.shape
+        return y.reshape(*x.shape[:-1], w2.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w1, w2, h, g = ctx.saved_tensors
+        w1p, b1p, w2p, b2p = ctx.boxes
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dw2 = _grad_w(g, dy2, w2p)
+        db2 = _grad_b(dy2, b2p) if b2p is not None else None
+        dh = gemm.mm_epi(dy2, w2.t(), 3, h)
+        db1 = _grad_b(dh, b1p)
+        dw1 = _grad_w(x2, dh, w1p)
+        dx = gemm.mm(dh, w1.t()).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
+        return dx, dw1, db1, dw2, db2, None
+
+
+def mlp_gelu_ok(x, w1p, b1p, w2p):
+    """Fused MLP eligibility: flat-buffer params (training engines), HIP epilogue contract."""
+    if b1p is None or not (eligible(w1p) and eligible(w2p) and flat_grad_slot(b1p) is not None):
+        return False
+    w1, w2 = w1p._t, w2p._t
+    x2 = x.reshape(-1, x.shape[-1])
+    return (x2.is_contiguous() and gemm.epi_ok(x2, w1, w1.shape[1]) and b1p._t.dtype == torch.bfloat16 and
+            b1p._t.is_contiguous() and w2.shape[0] == w1.shape[1])
+
+
+def mlp_gelu(x, w1p, b1p, w2p, b2p):
+    """x: torch tensor; the four MLP parameters are paddle Parameters (flat-buffer resident)."""
+    return _MLPGelu.apply(x, w1p._t, b1p._t, w2p._t, None if b2p is None else b2p._t, (w1p, b1p, w2p, b2p))
 
 
 def linear_accum(x, wparam, bparam):
