@@ -44,6 +44,9 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int BM = 256, BN = 256, BK = 64;
+// A/B switch for the 16-B-wide epilogue of schedule 11 (pa_gemm8_set_wide_epi); read by every
+// block, set only between launches.
+__constant__ int g_wide_epi = 1;
 constexpr int HALF = 128 * BK * 2;  // one 128-row (or 128-col) half of an operand tile: 16 KB
 constexpr int OPB = 2 * HALF;       // 32 KB
 constexpr int BUF = 2 * OPB;        // A + B of one K-tile: 64 KB
@@ -194,6 +197,64 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __r
           for (int r = 0; r < 4; ++r) v[r] += bb[r];
         }
         store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(dst), v);
+      }
+    }
+  }
+}
+
+// 16-B-wide epilogue (CDNA4 v_permlane16_swap): lanes of 16-lane rows g and g^1 hold adjacent
+// 4-column groups of the same output row, so swapping the group-2p data of the upper row with
+// the group-(2p+1) data of the lower row gives every lane 8 consecutive columns: 16 stores of
+// 16 B per lane (each instruction: 16 rows x 64 contiguous bytes) instead of 32 stores of 8 B
+// (16 rows x 32 B) — the K = 2048 GEMMs of the step are epilogue-store-issue bound at the tail
+// (cdna_hip_programming T21).  Bias / beta / aux reads become 16-B loads too.
+template <int EPI>
+__device__ __forceinline__ void epilogue_wide(const f32x4 (&acc)[8][4], uint16_t* __restrict__ C,
+                                              float* __restrict__ ws, const uint16_t* __restrict__ bias, int M, int N,
+                                              long long ldc, float alpha, float beta, int mb, int nb, int lane) {
+  const int g = lane >> 4;
+  const bool upper = (g & 1) != 0;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int n = nb + (upper ? 16 * (2 * p + 1) + 4 * (g - 1) : 16 * (2 * p) + 4 * g);
+    float bb[8];
+    if (EPI != 3 && bias != nullptr && n < N) load_f<bf16_t, 8>(reinterpret_cast<const bf16_t*>(bias + n), bb);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, acc[i][2 * p][e]),
+                                                        __builtin_bit_cast(unsigned, acc[i][2 * p + 1][e]), false,
+                                                        false);
+        v[e] = __builtin_bit_cast(float, (unsigned)r[0]) * alpha;
+        v[4 + e] = __builtin_bit_cast(float, (unsigned)r[1]) * alpha;
+      }
+      const int m = mb + i * 16 + (lane & 15);
+      if (m >= M || n >= N) continue;
+      const long long o = (long long)m * ldc + n;
+      if constexpr (EPI == 3) {
+        float h[8];
+        load_f<bf16_t, 8>(reinterpret_cast<const bf16_t*>(ws) + o, h);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] *= GeluTanh::df(h[r]);
+        store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(C + o), v);
+      } else {
+        if (bias != nullptr) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] += bb[r];
+        }
+        if constexpr (EPI == 2) {
+          store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(ws) + o, v);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] = GeluTanh::f(v[r]);
+        } else if (beta != 0.f) {
+          float old[8];
+          load_f<bf16_t, 8>(reinterpret_cast<const bf16_t*>(C + o), old);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] += beta * old[r];
+        }
+        store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(C + o), v);
       }
     }
   }
@@ -699,7 +760,12 @@ __global__ __launch_bounds__(512, 1) void gemm11_kernel(const char* __restrict__
   }
   if (wr == 0) bar();
 
-  epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
+  if constexpr (EPI == 1)
+    epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
+  else if (g_wide_epi)
+    epilogue_wide<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
+  else
+    epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
 }
 
 
@@ -985,6 +1051,13 @@ PA_API int pa_gemm8_bf16_epi(const void* A, const void* B, void* C, const void* 
   if (epi == 2) return (int)launch_epi<2>(transB, A, B, C, aux, bias, M, N, K, lda, ldb, ldc, alpha, st);
   if (epi == 3) return (int)launch_epi<3>(transB, A, B, C, aux, nullptr, M, N, K, lda, ldb, ldc, alpha, st);
   return (int)hipErrorInvalidValue;
+}
+
+PA_API int pa_gemm8_set_wide_epi(int v) {
+  int old = 1;
+  (void)hipMemcpyFromSymbol(&old, HIP_SYMBOL(pa::g8::g_wide_epi), sizeof(int));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(pa::g8::g_wide_epi), &v, sizeof(int));
+  return old;
 }
 
 // schedule select (A/B benchmarking): 8 = row-half staging, 9 = k-half staging (default),

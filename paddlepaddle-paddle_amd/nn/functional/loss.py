@@ -20,6 +20,11 @@ def _reduce(t, reduction):
     return t
 
 
+def _acc(t):
+    """Accumulation dtype of a loss: float32 for half types, the input's own dtype otherwise."""
+    return t.float() if t.dtype in (torch.float16, torch.bfloat16) else t
+
+
 @_amp_op('cross_entropy')
 def cross_entropy(input, label, weight=None, ignore_index=-100, reduction='mean', soft_label=False, axis=-1,  # noqa: A002
                   use_softmax=True, label_smoothing=0.0, name=None):
@@ -27,7 +32,8 @@ def cross_entropy(input, label, weight=None, ignore_index=-100, reduction='mean'
     axis = axis % logits.dim()
     w = _u(weight) if weight is not None else None
     if soft_label or (lab.is_floating_point() and lab.shape == logits.shape):
-        logp = torch.log_softmax(logits.float(), axis) if use_softmax else torch.log(logits.float())
+        lf = _acc(logits)
+        logp = torch.log_softmax(lf, axis) if use_softmax else torch.log(lf)
         if label_smoothing:
             lab = lab * (1 - label_smoothing) + label_smoothing / logits.shape[axis]
         loss = -(lab * logp)
@@ -56,20 +62,25 @@ def cross_entropy(input, label, weight=None, ignore_index=-100, reduction='mean'
     lg = logits.reshape(-1, logits.shape[-1])
     if not use_softmax:
         lg = torch.log(lg)
-        loss = TF.nll_loss(lg.float(), lab.reshape(-1), w, ignore_index=ignore_index, reduction='none')
+        lg = _acc(lg)
+        loss = TF.nll_loss(lg, lab.reshape(-1), None if w is None else w.to(lg.dtype), ignore_index=ignore_index,
+                           reduction='none')
     else:
-        loss = TF.cross_entropy(lg.float(), lab.reshape(-1), w, ignore_index=ignore_index, reduction='none',
+        lg = _acc(lg)
+        loss = TF.cross_entropy(lg, lab.reshape(-1), None if w is None else w.to(lg.dtype), ignore_index=ignore_index,
+                                reduction='none',
                                 label_smoothing=label_smoothing)
     loss = loss.reshape(lab.shape)
     if reduction == 'none':  # label-shaped: the class axis kept as a unit dim at `axis`
         return _w(loss.unsqueeze(axis).to(logits.dtype))
+    out_dt = logits.dtype if logits.dtype in (torch.float32, torch.float64) else loss.dtype
     if reduction == 'sum':
-        return _w(loss.sum())
+        return _w(loss.sum().to(out_dt))
     if w is not None:
-        wsum = w[lab.clamp_min(0)].masked_fill(lab == ignore_index, 0).sum()
-        return _w(loss.sum() / wsum)
+        wsum = w.to(loss.dtype)[lab.clamp_min(0)].masked_fill(lab == ignore_index, 0).sum()
+        return _w((loss.sum() / wsum).to(out_dt))
     valid = (lab != ignore_index).sum().clamp_min(1)
-    return _w(loss.sum() / valid)
+    return _w((loss.sum() / valid).to(out_dt))
 
 
 @_amp_op('softmax_with_cross_entropy')

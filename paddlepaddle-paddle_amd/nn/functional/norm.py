@@ -30,8 +30,9 @@ def rms_norm(x, normalized_shape, weight=None, epsilon=1e-05, name=None):
     w = _u(weight) if weight is not None else None
     if ops.use_hip(t) and w is not None:
         return _w(ops.norm.rms_norm(t, w, epsilon))
-    var = t.float().pow(2).mean(-1, keepdim=True)
-    y = (t.float() * torch.rsqrt(var + epsilon)).to(t.dtype)
+    tf = t.float() if t.dtype in (torch.float16, torch.bfloat16) else t
+    var = tf.pow(2).mean(-1, keepdim=True)
+    y = (tf * torch.rsqrt(var + epsilon)).to(t.dtype)
     return _w(y * w if w is not None else y)
 
 

@@ -585,3 +585,15 @@ def dist(x, y, p=2, name=None):
 
 def hsigmoid_(x):
     return _w(torch.nn.functional.hardsigmoid(_u(x)))
+
+
+def real(x, name=None):
+    """Real part (reference python/paddle/tensor/attribute.py real); a copy, like the reference."""
+    t = _u(x)
+    return _w(torch.real(t).clone() if t.is_complex() else t.clone())
+
+
+def imag(x, name=None):
+    """Imaginary part (reference python/paddle/tensor/attribute.py imag)."""
+    t = _u(x)
+    return _w(torch.imag(t).clone() if t.is_complex() else torch.zeros_like(t))
