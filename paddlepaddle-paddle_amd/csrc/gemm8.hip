@@ -224,11 +224,12 @@ __device__ __forceinline__ void epilogue_wide(const f32x4 (&acc)[8][4], uint16_t
       float v[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, acc[i][2 * p][e]),
-                                                        __builtin_bit_cast(unsigned, acc[i][2 * p + 1][e]), false,
-                                                        false);
-        v[e] = __builtin_bit_cast(float, (unsigned)r[0]) * alpha;
-        v[4 + e] = __builtin_bit_cast(float, (unsigned)r[1]) * alpha;
+        // inline asm: hipcc (ROCm 7.2) CSEs the four __builtin_amdgcn_permlane16_swap calls of this
+        // loop into one (every v[e] came out as v[0]); s_nop 1 = the VALU-write -> permlane hazard
+        float lo = acc[i][2 * p][e], hi = acc[i][2 * p + 1][e];
+        asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(lo), "+v"(hi));
+        v[e] = lo * alpha;
+        v[4 + e] = hi * alpha;
       }
       const int m = mb + i * 16 + (lane & 15);
       if (m >= M || n >= N) continue;
@@ -624,6 +625,7 @@ __global__ __launch_bounds__(512, 1) void gemm9_kernel(const char* __restrict__ 
   }
   if (wr == 0) bar();  // match waves 4-7's barrier count
 
+  // (the 16-B epilogue measured neutral here: weight gradients, K = 16384, beta = 1)
   epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
 }
 
