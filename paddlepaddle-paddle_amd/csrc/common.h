@@ -92,6 +92,17 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 // correctly at both ends (e^{2u} -> inf gives 1, -> 0 gives -1); |error| ~ 1e-7.
 __device__ __forceinline__ float fast_tanh(float u) { return 1.f - __fdividef(2.f, 1.f + __expf(2.f * u)); }
 
+// gelu_tanh(x) and its derivative from one tanh evaluation (the GEMM epilogue of the fused MLP
+// stores the derivative for the backward instead of the pre-activation)
+__device__ __forceinline__ void gelu_tanh_fdf(float x, float& f, float& df) {
+  const float x2 = x * x;
+  const float u = 0.79788456080286536f * x * (1.f + 0.044715f * x2);
+  const float t = fast_tanh(u);
+  const float hx = 0.5f * x;
+  f = hx * (1.f + t);
+  df = 0.5f * (1.f + t) + hx * (1.f - t * t) * 0.79788456080286536f * (1.f + 3.f * 0.044715f * x2);
+}
+
 struct GeluTanh {
   static __device__ __forceinline__ float f(float x) {
     const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);

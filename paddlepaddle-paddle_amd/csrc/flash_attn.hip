@@ -158,8 +158,8 @@ struct Extra {
   int mask_f32;
   float p_drop;
   uint32_t seed, offset;
-  uint32_t drop_thresh;  // keep when hash >= drop_thresh (= p_drop * 2^32)
-  float keep_scale;      // 1 / (1 - p_drop)
+  uint32_t drop_thresh;  // drop when the element's random byte < drop_thresh (= round(p_drop * 256))
+  float keep_scale;      // 256 / (256 - drop_thresh): unbiased for the quantised keep probability
   const int* rows;       // flashmask: key k masked for queries q >= rows[b*rb + h*rh + k]
   long long rb, rh;
 };
@@ -198,10 +198,19 @@ __device__ __forceinline__ void mask_row4(const Extra& ex, int b, int h, int q, 
                         : 0.f;
 }
 
-// dropout keep-scale for element (bh, q, k): 1/(1-p) kept, 0 dropped (counter hash, no state)
+// Dropout keep mask: one 32-bit counter hash per (bh, q, key quad k>>2) gives the random bytes of
+// four consecutive keys (8-bit keep test, as the reference's flash-attn kernels quantise p to a
+// uint8 threshold).  The forward and dQ kernels own 4 consecutive keys of one query per lane, so
+// they pay ONE hash per 4 elements (drop_bits + drop_sub); dK/dV (4 consecutive queries of one
+// key per lane) regenerates per element (drop_z) — same bits, same mask.
+__device__ __forceinline__ uint32_t drop_bits(const Extra& ex, int bh, int q, int k) {
+  return hash3(ex.seed ^ (uint32_t)bh * 0x9E3779B9u, ex.offset + (uint32_t)q, (uint32_t)k >> 2);
+}
+__device__ __forceinline__ float drop_sub(const Extra& ex, uint32_t bits, int sub) {
+  return ((bits >> (8 * sub)) & 0xFFu) < ex.drop_thresh ? 0.f : ex.keep_scale;
+}
 __device__ __forceinline__ float drop_z(const Extra& ex, int bh, int q, int k) {
-  const uint32_t hsh = hash3(ex.seed ^ (uint32_t)bh * 0x9E3779B9u, ex.offset + (uint32_t)q, (uint32_t)k);
-  return hsh < ex.drop_thresh ? 0.f : ex.keep_scale;
+  return drop_sub(ex, drop_bits(ex, bh, q, k), k & 3);
 }
 
 // per-sequence geometry: (q offset, Sq, k offset, Sk, LSE row base) of batch entry b
@@ -410,9 +419,11 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
       if constexpr ((EXT & 4) != 0) {  // dropout after the (undropped) row sum
         const int q = qw0 + 16 * t + (lane & 15);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t bits = drop_bits(ex, b * Hq + h, q, k0 + 16 * j + 4 * g);  // keys 4-aligned
 #pragma unroll
-          for (int r = 0; r < 4; ++r) p[j][r] *= drop_z(ex, b * Hq + h, q, k0 + 16 * j + 4 * g + r);
+          for (int r = 0; r < 4; ++r) p[j][r] *= drop_sub(ex, bits, r);
+        }
       }
       // P^T as B operand: k-step s covers keys 32s..32s+31; element j<4 → (16*(2s)+4g+j), j>=4 → (16*(2s+1)+4g+j-4)
 #pragma unroll
@@ -808,6 +819,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
         float mv[4] = {0.f, 0.f, 0.f, 0.f};
         if constexpr ((EXT & 2) != 0)
           if (myq < Sq) mask_row4<T>(ex, b, h, myq, k0 + 16 * j + 4 * g, Sk, mv);
+        uint32_t dbits = 0;
+        if constexpr ((EXT & 4) != 0) dbits = drop_bits(ex, b * Hq + h, myq, k0 + 16 * j + 4 * g);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = k0 + 16 * j + 4 * g + r;
@@ -820,7 +833,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
           if constexpr ((EXT & 8) != 0)
             if (key < Sk && myq >= row_start(ex, b, h, key)) p = 0.f;
           float z = 1.f;
-          if constexpr ((EXT & 4) != 0) z = drop_z(ex, b * Hq + h, myq, key);
+          if constexpr ((EXT & 4) != 0) z = drop_sub(ex, dbits, r);
           dsb[t][j >> 1][(j & 1) * 4 + r] = f2s<T>(p * (acc_dp[t][j][r] * z - dlt[t]));
         }
       }
@@ -981,9 +994,9 @@ static Extra make_extra(const int* cu_q, const int* cu_k, int total_q, const voi
   e.p_drop = p_drop;
   e.seed = seed;
   e.offset = offset;
-  const double th = (double)p_drop * 4294967296.0;
-  e.drop_thresh = th >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)th;
-  e.keep_scale = p_drop < 1.f ? 1.f / (1.f - p_drop) : 0.f;
+  const int th = (int)((double)p_drop * 256.0 + 0.5);
+  e.drop_thresh = (uint32_t)(th > 256 ? 256 : th);
+  e.keep_scale = e.drop_thresh < 256 ? 256.f / (256.f - (float)e.drop_thresh) : 0.f;
   return e;
 }
 

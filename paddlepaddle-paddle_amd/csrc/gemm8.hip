@@ -159,7 +159,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __r
       if (n >= N) continue;  // N % 8 == 0: a 4-wide group is all in or all out
       if constexpr (EPI == 1) {
         *reinterpret_cast<f32x4*>(ws + (long long)blockIdx.z * M * N + (long long)m * N + n) = acc[i][j];
-      } else if constexpr (EPI == 2) {  // h = alpha*acc + bias -> aux (bf16), C = gelu_tanh(h)
+      } else if constexpr (EPI == 2) {  // h = alpha*acc + bias: C = gelu_tanh(h), aux = gelu_tanh'(h)
         float h[4] = {acc[i][j][0] * alpha, acc[i][j][1] * alpha, acc[i][j][2] * alpha, acc[i][j][3] * alpha};
         if (bias) {
           float bb[4];
@@ -168,18 +168,18 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __r
           for (int r = 0; r < 4; ++r) h[r] += bb[r];
         }
         const long long o = (long long)m * ldc + n;
-        store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(ws) + o, h);
-        float g[4];
+        float g[4], d[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) g[r] = GeluTanh::f(h[r]);
+        for (int r = 0; r < 4; ++r) gelu_tanh_fdf(h[r], g[r], d[r]);
+        store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(ws) + o, d);
         store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(C + o), g);
-      } else if constexpr (EPI == 3) {  // C = alpha*acc * gelu_tanh'(aux)  (aux = saved pre-activation)
+      } else if constexpr (EPI == 3) {  // C = alpha*acc * aux  (aux = the saved gelu_tanh'(h))
         const long long o = (long long)m * ldc + n;
-        float h[4];
-        load_f<bf16_t, 4>(reinterpret_cast<const bf16_t*>(ws) + o, h);
+        float d[4];
+        load_f<bf16_t, 4>(reinterpret_cast<const bf16_t*>(ws) + o, d);
         float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * alpha * GeluTanh::df(h[r]);
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * alpha * d[r];
         store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(C + o), v);
       } else {
         float v[4] = {acc[i][j][0] * alpha, acc[i][j][1] * alpha, acc[i][j][2] * alpha, acc[i][j][3] * alpha};
@@ -219,6 +219,17 @@ __device__ __forceinline__ void epilogue_wide(const f32x4 (&acc)[8][4], uint16_t
     const int n = nb + (upper ? 16 * (2 * p + 1) + 4 * (g - 1) : 16 * (2 * p) + 4 * g);
     float bb[8];
     if (EPI != 3 && bias != nullptr && n < N) load_f<bf16_t, 8>(reinterpret_cast<const bf16_t*>(bias + n), bb);
+    // EPI 3: issue all eight 16-B loads of the saved derivative before any use (one memory round
+    // trip per p instead of eight serialised ones)
+    Pack<bf16_t, 8> hv[8];
+    if constexpr (EPI == 3) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = mb + i * 16 + (lane & 15);
+        if (m < M && n < N)
+          hv[i] = *reinterpret_cast<const Pack<bf16_t, 8>*>(reinterpret_cast<const bf16_t*>(ws) + (long long)m * ldc + n);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float v[8];
@@ -235,10 +246,8 @@ __device__ __forceinline__ void epilogue_wide(const f32x4 (&acc)[8][4], uint16_t
       if (m >= M || n >= N) continue;
       const long long o = (long long)m * ldc + n;
       if constexpr (EPI == 3) {
-        float h[8];
-        load_f<bf16_t, 8>(reinterpret_cast<const bf16_t*>(ws) + o, h);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] *= GeluTanh::df(h[r]);
+        for (int r = 0; r < 8; ++r) v[r] *= (float)hv[i].v[r];
         store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(C + o), v);
       } else {
         if (bias != nullptr) {
@@ -246,9 +255,10 @@ __device__ __forceinline__ void epilogue_wide(const f32x4 (&acc)[8][4], uint16_t
           for (int r = 0; r < 8; ++r) v[r] += bb[r];
         }
         if constexpr (EPI == 2) {
-          store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(ws) + o, v);
+          float d[8];
 #pragma unroll
-          for (int r = 0; r < 8; ++r) v[r] = GeluTanh::f(v[r]);
+          for (int r = 0; r < 8; ++r) gelu_tanh_fdf(v[r], v[r], d[r]);
+          store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(ws) + o, d);
         } else if (beta != 0.f) {
           float old[8];
           load_f<bf16_t, 8>(reinterpret_cast<const bf16_t*>(C + o), old);
@@ -285,8 +295,9 @@ __device__ __forceinline__ void epilogue_z(const f32x4 (&acc)[8][4], uint16_t* _
 }
 
 // EPI 0: bf16 C = alpha*acc (+ beta*C) (+ bias);  EPI 1: raw fp32 split-K slab (ws[z][M][N]);
-// EPI 2: fc1 forward, h = alpha*acc + bias stored to aux (= ws, bf16, ldc) and C = gelu_tanh(h);
-// EPI 3: fc2 dgrad, C = alpha*acc * gelu_tanh'(aux) (aux = the saved h): the bias_act kernels of
+// EPI 2: fc1 forward, h = alpha*acc + bias, C = gelu_tanh(h) and aux (= ws, bf16, ldc) = gelu_tanh'(h);
+// EPI 3: fc2 dgrad, C = alpha*acc * aux (the saved derivative: the epilogue of a 1-block-per-CU
+// GEMM is exposed time, so the tanh work is done once, in the forward): the bias_act kernels of
 // the MLP (reference fusion/gpu/fused_gemm_epilogue_kernel.cu, fused_gemm_epilogue_grad) vanish.
 template <bool AK, bool BKM, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm8_kernel(const char* __restrict__ A, const char* __restrict__ B,
@@ -1043,8 +1054,8 @@ PA_API int pa_gemm8_bf16(const void* A, const void* B, void* C, const void* bias
   return (int)dispatch<1>(transA, transB, A, B, C, (float*)ws, nullptr, M, N, K, lda, ldb, ldc, 1.f, 0.f, splitk, st);
 }
 
-// Fused-epilogue GEMMs of the GPT MLP (A k-contiguous [M][lda], schedule 11).  epi 2: C = gelu(h),
-// aux = h = alpha*A@B + bias;  epi 3: C = alpha*A@B * gelu'(aux).  aux: bf16 [M][ldc].
+// Fused-epilogue GEMMs of the GPT MLP (A k-contiguous [M][lda], schedule 11).  epi 2: h = alpha*A@B +
+// bias, C = gelu(h), aux = gelu'(h);  epi 3: C = alpha*A@B * aux.  aux: bf16 [M][ldc].
 PA_API int pa_gemm8_bf16_epi(const void* A, const void* B, void* C, const void* bias, void* aux, int M, int N, int K,
                              long long lda, long long ldb, long long ldc, int transB, float alpha, int epi,
                              hipStream_t st) {

@@ -89,8 +89,8 @@ def epi_ok(a, b, out_cols):
 def mm_epi(a, b, epi, aux, bias=None, out=None):
     """Fused-epilogue GEMM of the MLP (csrc/gemm8.hip pa_gemm8_bf16_epi, schedule 11).
 
-    epi 2 (fc1 forward): h = a @ b + bias is written to ``aux`` and gelu_tanh(h) is returned;
-    epi 3 (fc2 dgrad):   returns (a @ b) * gelu_tanh'(aux).   a: [M,K] row-major; b: [K,N]
+    epi 2 (fc1 forward): h = a @ b + bias; returns gelu_tanh(h) and writes gelu_tanh'(h) to ``aux``;
+    epi 3 (fc2 dgrad):   returns (a @ b) * aux.   a: [M,K] row-major; b: [K,N]
     (row-major or a transposed view of [N,K]); aux: bf16 [M,N] contiguous."""
     tb, ldb = _op_layout(b)
     M, K = a.shape

@@ -74,9 +74,10 @@ def _grad_b(dy2, bp):
 
 class _MLPGelu(torch.autograd.Function):
     """y = gelu_tanh(x @ W1 + b1) @ W2 + b2 with the activation inside the GEMM epilogues:
-    forward fc1 writes h = x@W1 + b1 and g = gelu(h) in one epilogue (EPI 2), backward's fc2
-    dgrad writes dh = (dy @ W2^T) * gelu'(h) (EPI 3) — no standalone bias+activation kernel
-    either way (reference: fusion/gpu/fused_gemm_epilogue_kernel.cu + its _grad kernel)."""
+    forward fc1 writes g = gelu(h) and gelu'(h) (h = x@W1 + b1) in one epilogue (EPI 2), backward's
+    fc2 dgrad writes dh = (dy @ W2^T) * gelu'(h) (EPI 3, a plain multiply: the tanh work runs once,
+    in the forward) — no standalone bias+activation kernel either way (reference:
+    fusion/gpu/fused_gemm_epilogue_kernel.cu + its _grad kernel)."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, boxes):
@@ -86,7 +87,7 @@ class _MLPGelu(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         M, F_ = x2.shape[0], w1.shape[1]
         wt1 = gemm.kmajor_weight(x2, w1)
-        h = torch.empty(M, F_, dtype=x2.dtype, device=x2.device)
+        h = torch.empty(M, F_, dtype=x2.dtype, device=x2.device)  # gelu'(x@W1 + b1)
         g = gemm.mm_epi(x2, w1 if wt1 is None else wt1.t(), 2, h, bias=b1)
         wt2 = gemm.kmajor_weight(g, w2)
         y = gemm.mm(g, w2 if wt2 is None else wt2.t(), bias=b2)

@@ -483,7 +483,7 @@ def _gelu_tanh(x):
 @pytest.mark.parametrize("kmajor_b", [False, True])
 @pytest.mark.parametrize("M,K,N", [(512, 256, 768), (264, 128, 520), (2048, 1024, 4096)])
 def test_gemm_gelu_epilogues(M, K, N, kmajor_b):
-    """EPI 2 (h = a@b + bias -> aux, C = gelu(h)) and EPI 3 (C = a@b * gelu'(aux)) of csrc/gemm8.hip."""
+    """EPI 2 (h = a@b + bias: C = gelu(h), aux = gelu'(h)) and EPI 3 (C = a@b * aux) of csrc/gemm8.hip."""
     from paddle.ops import gemm
     a = (torch.randn(M, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
     bm = torch.randn(K, N, device=DEV).to(torch.bfloat16)
@@ -493,15 +493,15 @@ def test_gemm_gelu_epilogues(M, K, N, kmajor_b):
     h = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     g = gemm.mm_epi(a, b, 2, h, bias=bias)
     href = a.float() @ bm.float() + bias.float()
-    _close(h, href, 2e-2, 1e-2, 'h')
+    hr = href.clone().requires_grad_()
+    _gelu_tanh(hr).backward(torch.ones_like(hr))
+    _close(h, hr.grad, 2e-2, 1e-2, "gelu'")  # aux = gelu'(h)
     _close(g, _gelu_tanh(href), 2e-2, 1e-2, 'gelu')
     dy = (torch.randn(M, K, device=DEV)).to(torch.bfloat16)
     w2t = torch.randn(N, K, device=DEV).to(torch.bfloat16)  # dgrad operand dy @ W2^T with W2 [N, K]... [K,N] view
     aux = (torch.randn(M, N, device=DEV) * 2).to(torch.bfloat16)
     dh = gemm.mm_epi(dy, w2t.t(), 3, aux)
-    xr = aux.float().requires_grad_()
-    _gelu_tanh(xr).backward(torch.ones_like(xr))
-    ref = (dy.float() @ w2t.float().t()) * xr.grad
+    ref = (dy.float() @ w2t.float().t()) * aux.float()
     _close(dh, ref, 3e-2 * math.sqrt(K) / 8, 2e-2, 'dgelu')
 
 
