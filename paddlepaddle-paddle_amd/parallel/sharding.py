@@ -124,9 +124,16 @@ class _PreBackward(torch.autograd.Function):
 
 class ShardingEngine:
     def __init__(self, model, level='p_g_os', group=None, bucket_mb=256, segment_size=2 ** 20,
-                 release_grads=True, persistent_types=None, persistent_below=None, params=None):
+                 release_grads=True, persistent_types=None, persistent_below=None, params=None, alias=None,
+                 reduce_dtype=None):
         """model: the Layer to shard; or model=None with ``params`` (a parameter list) for stage 1/2
-        (the hybrid-parallel sharding optimizer, which only sees its optimizer's parameters)."""
+        (the hybrid-parallel sharding optimizer, which only sees its optimizer's parameters).
+
+        alias: at world 1 the units alias the optimizer arenas (default); ``alias=False`` (or env
+        PADDLE_AMD_SHARDING_ALIAS=0) runs the multi-rank code path on one rank — release, gather,
+        re-materialise, shard copy — so it can be exercised on a single GPU.
+        reduce_dtype: 'float32' reduce-scatters low-precision gradients in fp32 (fp32 main-grad
+        communication, 2x the bytes) into an fp32 gradient arena; default: the parameter dtype."""
         self.model = model
         self.level = LEVELS[level] if isinstance(level, str) else int(level)
         if model is None and (params is None or self.level == 3):
@@ -137,8 +144,16 @@ class ShardingEngine:
         self.rank = dist.get_rank(self.pg) if dist.is_initialized() else 0
         # one rank: the "shard" is the whole buffer, so units alias the optimizer arenas and
         # nothing is ever released, gathered or copied (no degenerate collectives either)
-        self.alias = self.world == 1
+        if alias is None:
+            import os
+            alias = os.environ.get('PADDLE_AMD_SHARDING_ALIAS', '1') != '0'
+        self.alias = self.world == 1 and bool(alias)
         self.release_grads = release_grads and self.level == 3 and not self.alias
+        rd = str(reduce_dtype).replace('torch.', '').replace('paddle.', '') if reduce_dtype is not None else None
+        if rd not in (None, 'float32', 'bfloat16', 'float16'):
+            raise ValueError(f"reduce_dtype must be float32 / bfloat16 / float16, got {reduce_dtype}")
+        self.reduce_fp32 = rd == 'float32' and not self.alias
+        self._gather_works = []
         from ..nn.layer.common import Embedding
         self.persistent_types = tuple(persistent_types or (Embedding,))
         # units smaller than this stay materialised: gathering them saves nothing, and small
@@ -220,6 +235,9 @@ class ShardingEngine:
                 small = sum(p._t.numel() for p in ps) < self.persistent_below
                 units.append(_Unit(self, ps, layer, persistent or small or self.alias))
 
+        def holds_persistent(layer):
+            return any(isinstance(l, self.persistent_types) for l in layer.sublayers())
+
         def visit(layer):
             n = count(layer)
             if n == 0:
@@ -230,7 +248,9 @@ class ShardingEngine:
             children = [c for c in layer.children() if count(c) > 0]
             from ..nn.layer.container import LayerList, LayerDict
             container = isinstance(layer, (LayerList, LayerDict))  # never called: descend
-            if (n <= limit and not container) or not children:
+            # a subtree holding an embedding is always descended into: the embedding must get its
+            # own persistent unit (its weight is commonly tied to a head used outside the subtree)
+            if (n <= limit and not container and not holds_persistent(layer)) or not children:
                 make(layer, layer.parameters(), False)
                 return
             own = [p for p in layer._parameters.values() if p is not None]
@@ -253,7 +273,8 @@ class ShardingEngine:
             n = a['size']
             dev = a['units'][0].fb.data.device
             a['param'] = torch.empty(n, dtype=dt, device=dev)
-            a['grad'] = torch.zeros(n, dtype=dt, device=dev)
+            gdt = torch.float32 if self.reduce_fp32 else dt
+            a['grad'] = torch.zeros(n, dtype=gdt, device=dev)
             for u in a['units']:
                 if self.alias:
                     u.fb.alias_into(a['param'][u.arena_off:u.arena_off + u.L],
@@ -364,10 +385,12 @@ class ShardingEngine:
             u.rs_work = None
             self._accumulate_shard(u, u.shard(u.fb.grad))
             return
-        out = self.gshard(u) if self.grad_fresh else torch.empty(u.L, dtype=u.fb.grad.dtype, device=u.fb.grad.device)
+        gs = self.gshard(u)
+        out = gs if self.grad_fresh else torch.empty(u.L, dtype=gs.dtype, device=gs.device)
         u._rs_out = out
+        src = u.fb.grad if u.fb.grad.dtype == out.dtype else u.fb.grad.to(out.dtype)  # fp32 main-grad reduce
         op = dist.ReduceOp.AVG if dist.get_backend(self.pg) == 'nccl' else dist.ReduceOp.SUM
-        u.rs_work = dist.reduce_scatter_tensor(out, u.fb.grad, op, group=self.pg, async_op=True)
+        u.rs_work = dist.reduce_scatter_tensor(out, src, op, group=self.pg, async_op=True)
         if self.level == 3:
             u.free_params()
 
@@ -377,7 +400,7 @@ class ShardingEngine:
             if src.data_ptr() != dst.data_ptr():
                 dst.copy_(src)
         else:
-            dst.add_(src)
+            dst.add_(src.to(dst.dtype))
 
     def _finish_backward(self):
         for u in self.units:
@@ -411,13 +434,32 @@ class ShardingEngine:
 
     # ------------------------------------------------------------------ after the update
     def gather_params_after_step(self):
+        """Re-materialise updated parameters.  Stage 1/2 with a model: one ASYNC all-gather per
+        unit, waited for by the model's forward pre-hook (the gathers overlap whatever the host
+        does between step() and the next forward: data loading, logging, LR scheduling);
+        without a model (hybrid-parallel sharding optimizer) the gathers are waited for here."""
         for u in self.units:
             if u.persistent or self.level < 3:
                 if self.world == 1:
-                    u.fb.data[:u.L].copy_(self.pshard(u)) if u.fb.data.data_ptr() != self.pshard(u).data_ptr() else None
+                    if not u.gathered:  # released persistent unit (alias off): plain re-materialise
+                        u.wait_gather()
+                    elif u.fb.data.data_ptr() != self.pshard(u).data_ptr():
+                        u.fb.data[:u.L].copy_(self.pshard(u))
                     continue
-                dist.all_gather_into_tensor(u.fb.data, self.pshard(u), group=self.pg)
+                w = dist.all_gather_into_tensor(u.fb.data, self.pshard(u), group=self.pg, async_op=True)
+                self._gather_works.append(w)
             # stage-3 non-persistent units are gathered lazily by their forward pre-hook
+        if self.model is None or self.level == 3:
+            self.wait_param_gathers()
+        elif not getattr(self, '_gather_hook_installed', False):
+            self.model.register_forward_pre_hook(lambda layer, inputs: self.wait_param_gathers())
+            self._gather_hook_installed = True
+
+    def wait_param_gathers(self):
+        ws, self._gather_works = self._gather_works, []
+        for w in ws:
+            w.wait()
+        return None
 
 
 class ShardedOptimizer:
@@ -646,6 +688,7 @@ class GroupShardedModel:
                 return self._layers.set_state_dict(sd, use_structured_name)
 
             def get_all_parameters(self, convert2cpu=False):
+                engine.wait_param_gathers()
                 for u in engine.units:
                     u.wait_gather()
                 return self._layers.parameters()
@@ -657,6 +700,7 @@ class GroupShardedModel:
 def gathered_state_dict(layer, engine):
     """Full (unsharded) state dict: gathers any released unit, copies, releases again."""
     out = {}
+    engine.wait_param_gathers()
     released = [u for u in engine.units if not u.gathered]
     for u in released:
         u.wait_gather()

@@ -52,10 +52,16 @@ def test_hybrid_parallel_matches_single_device(mode):
     assert out.count(f'{mode} OK') == 2, out[-3000:]
 
 
-@pytest.mark.parametrize("mode", ['os_g', 'p_g_os'])
+@pytest.mark.parametrize("mode", ['os', 'os_g', 'p_g_os'])
 def test_gpt_sharding_matches_single_process(mode):
     out = run_workers('worker_gpt_sharding.py', mode)
     assert out.count(f"gpt {mode} OK") == 2, out[-3000:]
+
+
+def test_gpt_sharding_fp32_reduce_scatter():
+    """fp32 main-grad communication: bf16/fp32 gradients reduce-scattered in fp32 into an fp32 arena."""
+    out = run_workers('worker_gpt_sharding.py', 'p_g_os', 'float32')
+    assert out.count("gpt p_g_os-float32 OK") == 2, out[-3000:]
 
 
 def test_auto_parallel_reshard_and_dist_checkpoint(tmp_path):
