@@ -17,3 +17,9 @@ class dygraph:  # noqa: N801
     def guard(place=None):
         import contextlib
         return contextlib.nullcontext()
+
+
+def create_lod_tensor(data, recursive_seq_lens, place=None):
+    """paddle.base.create_lod_tensor (level-1 LoD on a Tensor; static/sequence.py)."""
+    from .static.sequence import create_lod_tensor as _c
+    return _c(data, recursive_seq_lens, place)

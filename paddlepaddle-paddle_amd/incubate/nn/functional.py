@@ -490,9 +490,10 @@ def variable_length_memory_efficient_attention(query, key, value, seq_lens, kv_s
 def fused_ec_moe(x, gate, bmm0_weight, bmm0_bias, bmm1_weight, bmm1_bias, act_type):
     t, g = _u(x), _u(gate)
     probs = torch.softmax(g.float(), -1)
-    h = torch.einsum('bsd,edf->bsef', t, _u(bmm0_weight)) + _u(bmm0_bias).reshape(1, 1, *_u(bmm0_bias).shape[-2:])
+    E = _u(bmm0_weight).shape[0]
+    h = torch.einsum('bsd,edf->bsef', t, _u(bmm0_weight)) + _u(bmm0_bias).reshape(1, 1, E, -1)
     h = TF.gelu(h) if act_type == 'gelu' else torch.relu(h)
-    o = torch.einsum('bsef,efd->bsed', h, _u(bmm1_weight)) + _u(bmm1_bias).reshape(1, 1, *_u(bmm1_bias).shape[-2:])
+    o = torch.einsum('bsef,efd->bsed', h, _u(bmm1_weight)) + _u(bmm1_bias).reshape(1, 1, E, -1)
     return _w((o * probs.unsqueeze(-1).to(o.dtype)).sum(2))
 
 

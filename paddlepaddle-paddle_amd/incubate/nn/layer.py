@@ -189,3 +189,22 @@ class FusedMultiTransformer(Layer):
             training=self.training, trans_qkvw=self.trans_qkvw, norm_type=self.norm_type,
             use_neox_rotary_style=self.use_neox_rotary_style, gqa_group_size=self.gqa_group_size)
 
+
+
+class FusedEcMoe(Layer):
+    """Reference incubate/nn/layer/fused_ec_moe.py: experts [E, d_model, d_ff] / [E, d_ff, d_model]
+    with [E, 1, d] biases; forward(x [B, S, d_model], gate [B, S, E]) -> [B, S, d_model]."""
+
+    def __init__(self, hidden_size, inter_size, num_experts, act_type, weight_attr=None, bias_attr=None):
+        super().__init__()
+        if act_type not in ('gelu', 'relu'):
+            raise NotImplementedError("Currently only support `gelu`, `relu`. ")
+        self.bmm_weight0 = self.create_parameter([num_experts, hidden_size, inter_size], attr=weight_attr)
+        self.bmm_bias0 = self.create_parameter([num_experts, 1, inter_size], attr=bias_attr, is_bias=True)
+        self.bmm_weight1 = self.create_parameter([num_experts, inter_size, hidden_size], attr=weight_attr)
+        self.bmm_bias1 = self.create_parameter([num_experts, 1, hidden_size], attr=bias_attr, is_bias=True)
+        self.act_type = act_type
+
+    def forward(self, x, gate):
+        return IF.fused_ec_moe(x, gate, self.bmm_weight0, self.bmm_bias0, self.bmm_weight1, self.bmm_bias1,
+                               self.act_type)

@@ -231,7 +231,46 @@ def ctc_loss(log_probs, labels, input_lengths, label_lengths, blank=0, reduction
 
 
 def rnnt_loss(input, label, input_lengths, label_lengths, blank=0, fastemit_lambda=0.001, reduction='mean', name=None):  # noqa: A002
-    raise NotImplementedError("rnnt_loss: transducer loss not provided by this build")
+    """RNN-Transducer loss (reference nn/functional/loss.py:1983 rnnt_loss -> the warprnnt op).
+
+    ``input``: log-probabilities [B, Tmax, Umax+1, V] (used as given, like the reference kernel);
+    ``label`` [B, Umax]; per-sequence lengths.  loss_b = -log sum over alignments of the summed
+    log-probabilities.  Forward variable alpha is vectorised over (B, U) per time step:
+        alpha[t, u] = C[t, u] + logcumsumexp_u'<=u(alpha[t-1, u'] + blank[t-1, u'] - C[t, u'])
+    with C[t, u] = sum_{k<u} emit[t, k] (emission of label k at frame t); gradients by autograd.
+    FastEmit (arXiv 2010.11148): the label-emission gradients are scaled by (1 + lambda), the value
+    is unchanged (the warp-transducer rule).  reduction 'mean' divides the summed loss by B.
+    """
+    lp = _u(input)
+    B, T, U1, V = lp.shape
+    lab = _u(label).long().reshape(B, -1)[:, :U1 - 1].clamp(0, V - 1)
+    tl = _u(input_lengths).long().reshape(B).to(lp.device) if isinstance(input_lengths, Tensor) else \
+        torch.as_tensor(input_lengths, device=lp.device).long().reshape(B)
+    ul = _u(label_lengths).long().reshape(B).to(lp.device) if isinstance(label_lengths, Tensor) else \
+        torch.as_tensor(label_lengths, device=lp.device).long().reshape(B)
+    blank_lp = lp[..., blank]  # [B, T, U1]
+    if U1 > 1:
+        emit = torch.gather(lp[:, :, :U1 - 1, :], 3, lab[:, None, :, None].expand(B, T, U1 - 1, 1)).squeeze(3)
+        if fastemit_lambda:
+            emit = emit * (1.0 + fastemit_lambda) - fastemit_lambda * emit.detach()
+        C = torch.cat([torch.zeros(B, T, 1, dtype=lp.dtype, device=lp.device), torch.cumsum(emit, 2)], 2)
+    else:
+        C = torch.zeros(B, T, 1, dtype=lp.dtype, device=lp.device)
+    alpha = C[:, 0]
+    alphas = [alpha]
+    for t in range(1, T):
+        a_prev = alpha + blank_lp[:, t - 1]
+        alpha = C[:, t] + torch.logcumsumexp(a_prev - C[:, t], 1)
+        alphas.append(alpha)
+    A = torch.stack(alphas, 1)  # [B, T, U1]
+    bi = torch.arange(B, device=lp.device)
+    ll = A[bi, tl - 1, ul] + blank_lp[bi, tl - 1, ul]
+    loss = -ll
+    if reduction == 'mean':
+        return _w(loss.sum() / B)
+    if reduction == 'sum':
+        return _w(loss.sum())
+    return _w(loss)
 
 
 @_amp_op('margin_cross_entropy')
@@ -272,4 +311,38 @@ def hsigmoid_loss(input, label, num_classes, weight, bias=None, path_table=None,
 
 
 def adaptive_log_softmax_with_loss(input, label, head_weight, tail_weights, cutoffs, head_bias=None, name=None):  # noqa: A002
-    raise NotImplementedError("adaptive_log_softmax_with_loss: use nn.AdaptiveLogSoftmaxWithLoss")
+    """Adaptive softmax (reference nn/functional/loss.py:4289): the head scores the shortlist
+    [0, cutoffs[0]) plus one logit per tail cluster; a target in cluster i adds the cluster's
+    own log-softmax (two projections tail_weights[i-1] = (W_proj [in, hsz], W_out [hsz, osz])).
+    Returns (output = log p(label) per row, loss = -mean(output))."""
+    x, y = _u(input), _u(label).long()
+    batched = y.dim() > 0
+    if not batched:
+        x, y = x.unsqueeze(0), y.unsqueeze(0)
+    if x.dim() != 2 or x.shape[0] != y.shape[0]:
+        raise ValueError("input must be [N, in_features] with one label per row")
+    cutoffs = list(cutoffs)
+    head = x @ _u(head_weight)
+    if head_bias is not None:
+        head = head + _u(head_bias)
+    head_lp = torch.log_softmax(head.float() if head.dtype in (torch.float16, torch.bfloat16) else head, -1)
+    short = cutoffs[0]
+    out = torch.zeros(x.shape[0], dtype=head_lp.dtype, device=x.device)
+    in_short = y < short
+    out = torch.where(in_short, head_lp.gather(1, y.clamp(max=short - 1).unsqueeze(1)).squeeze(1), out)
+    bounds = cutoffs + ([] if len(tail_weights) + 1 == len(cutoffs) else [])
+    for i in range(1, len(cutoffs)):
+        lo, hi = cutoffs[i - 1], cutoffs[i]
+        m = (y >= lo) & (y < hi)
+        if not bool(m.any()):
+            continue
+        w0, w1 = tail_weights[i - 1]
+        logits = (x[m] @ _u(w0)) @ _u(w1)
+        lp = torch.log_softmax(logits.to(head_lp.dtype), -1)
+        val = head_lp[m, short + i - 1] + lp.gather(1, (y[m] - lo).unsqueeze(1)).squeeze(1)
+        out = out.masked_scatter(m, val) if False else out.index_put((m.nonzero().squeeze(1),), val)
+    del bounds
+    out = out.to(x.dtype)
+    if not batched:
+        out = out.squeeze(0)
+    return _w(out), _w(-out.mean())

@@ -70,17 +70,48 @@ class HSigmoidLoss(Layer):
 
 
 class AdaptiveLogSoftmaxWithLoss(Layer):
+    """Reference nn/layer/loss.py AdaptiveLogSoftmaxWithLoss: head Linear(in, shortlist + n_clusters)
+    and per cluster i a (Linear(in, in // div_value**(i+1)), Linear(.., cluster size)) tail."""
+
     def __init__(self, in_features, n_classes, cutoffs, div_value=4.0, head_bias=False, name=None):
         super().__init__()
-        import torch
-        from ...core.tensor import Parameter
-        self._m = torch.nn.AdaptiveLogSoftmaxWithLoss(in_features, n_classes, cutoffs, div_value, head_bias)
-        from ...core.place import current_device
-        self._m.to(current_device())
-        for n, p in self._m.named_parameters():
-            self.add_parameter(n.replace('.', '_'), Parameter(p))
+        cutoffs = list(cutoffs)
+        if len(cutoffs) == 0 or cutoffs != sorted(cutoffs) or min(cutoffs) <= 0 or max(cutoffs) > n_classes - 1 \
+                or len(set(cutoffs)) != len(cutoffs):
+            raise ValueError("cutoffs should be a sorted list of unique positive ints < n_classes - 1")
+        self.in_features, self.n_classes, self.div_value = in_features, n_classes, div_value
+        self.cutoffs = cutoffs + [n_classes]
+        self.shortlist_size = self.cutoffs[0]
+        self.n_clusters = len(self.cutoffs) - 1
+        self.head_size = self.shortlist_size + self.n_clusters
+        self.head_weight = self.create_parameter([in_features, self.head_size])
+        self.head_bias = self.create_parameter([self.head_size], is_bias=True) if head_bias else None
+        self.tail_weights = []
+        for i in range(self.n_clusters):
+            hsz = int(in_features // (div_value ** (i + 1)))
+            osz = self.cutoffs[i + 1] - self.cutoffs[i]
+            w0 = self.create_parameter([in_features, hsz])
+            w1 = self.create_parameter([hsz, osz])
+            self.add_parameter(f'tail_{i}_0', w0)
+            self.add_parameter(f'tail_{i}_1', w1)
+            self.tail_weights.append([w0, w1])
 
     def forward(self, input, label):  # noqa: A002
+        return F.adaptive_log_softmax_with_loss(input, label, self.head_weight, self.tail_weights, self.cutoffs,
+                                                self.head_bias)
+
+    def log_prob(self, input):  # noqa: A002
+        import torch
         from ...core.tensor import _wrap
-        r = self._m(input._t, label._t)
-        return _wrap(r.output), _wrap(r.loss)
+        x = input._t
+        head = x @ self.head_weight._t
+        if self.head_bias is not None:
+            head = head + self.head_bias._t
+        hl = torch.log_softmax(head, -1)
+        parts = [hl[:, :self.shortlist_size]]
+        for i, (w0, w1) in enumerate(self.tail_weights):
+            parts.append(torch.log_softmax((x @ w0._t) @ w1._t, -1) + hl[:, self.shortlist_size + i:self.shortlist_size + i + 1])
+        return _wrap(torch.cat(parts, -1))
+
+    def predict(self, input):  # noqa: A002
+        return self.log_prob(input).argmax(-1)

@@ -13,6 +13,9 @@ from .io import (save_inference_model, load_inference_model, serialize_program, 
 from . import nn  # noqa: F401
 from . import amp  # noqa: F401
 from .nn import py_func  # noqa: F401
+from . import sequence as _sequence  # noqa: E402
+from .sequence import create_lod_tensor  # noqa: F401
+_sequence.install_tensor_methods()  # Tensor.set_lod / lod / (set_)recursive_sequence_lengths
 from ..core.tensor import Tensor as Variable  # noqa: F401
 from ..framework.param_attr import ParamAttr, WeightNormParamAttr  # noqa: F401
 

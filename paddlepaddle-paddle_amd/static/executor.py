@@ -191,8 +191,20 @@ def _exec(prog, nodes, env, smap, dev):
             _bind(env, n.outs, [r if r is not None else torch.zeros_like(x) for r, x in zip(res, xs)])
         elif n.kind == 'py':
             args = _resolve(prog, n.args, env, smap, dev)
-            out = n.target(*[_wrap(a) if isinstance(a, torch.Tensor) else a for a in args])
+            ins = []
+            for a in args:
+                if isinstance(a, torch.Tensor):
+                    w = _wrap(a)
+                    if id(a) in _LOD:  # LoD of a fed / produced sequence tensor (static/sequence.py)
+                        w.__dict__['_lod'] = _LOD[id(a)][1]
+                    ins.append(w)
+                else:
+                    ins.append(a)
+            out = n.target(*ins)
             out = out if isinstance(out, (list, tuple)) else [out]
+            for o in out:
+                if isinstance(o, Tensor) and o.__dict__.get('_lod') is not None:
+                    _LOD[id(o._t)] = (o._t, o.__dict__['_lod'])  # keep the tensor alive with its id
             _bind(env, n.outs, [o._t if isinstance(o, Tensor) else o for o in out])
         elif n.kind == 'cond':
             t_nodes, t_refs, f_nodes, f_refs = n.kwargs['branches']
@@ -217,11 +229,15 @@ def _exec(prog, nodes, env, smap, dev):
             raise RuntimeError(f"unknown node kind {n.kind}")
 
 
+_LOD = {}  # id(torch tensor) -> (tensor, level-1 offsets) for LoD values of the running replay
+
+
 def run_program(prog, feed, dev, grad=None):
     """Interpret ``prog``; returns the value env."""
     env = {}
     smap = {}
     feed = feed or {}
+    _LOD.clear()
     for name, (vid, shape, dt) in prog.feeds.items():
         if name not in feed:
             continue
@@ -236,6 +252,9 @@ def run_program(prog, feed, dev, grad=None):
                 elif s != t.shape[i]:
                     raise ValueError(f"feed '{name}' expects shape {shape}, got {list(t.shape)}")
         env[vid] = t
+        lod = feed[name].__dict__.get('_lod') if isinstance(feed[name], Tensor) else None
+        if lod is not None:
+            _LOD[id(t)] = (t, lod)
     needs_grad = grad if grad is not None else any(n.kind in ('minimize', 'backward', 'grad') for n in prog.nodes)
     ctx = contextlib.nullcontext() if needs_grad else torch.no_grad()
     from .amp import autocast_context

@@ -5,6 +5,7 @@ Layer helpers create their parameters eagerly (that is the startup program) and 
 dygraph functional, which the recorder captures.  Control flow traces each branch / the loop
 body into a sub-op-list once; the executor picks the branch (or iterates) at run time.
 """
+import numpy as np
 import torch
 
 from ..core.tensor import Tensor, _wrap, _unwrap
@@ -88,8 +89,173 @@ def prelu(x, mode='all', param_attr=None, data_format="NCHW", name=None):
     return _nn.PReLU(n, weight_attr=param_attr, data_format=data_format)(x)
 
 
-def data_norm(input, *a, **k):  # noqa: A002
-    return F.batch_norm(input, None, None, training=True) if False else layer_norm(input)
+def data_norm(input, act=None, epsilon=1e-05, param_attr=None, data_layout='NCHW', in_place=False, name=None,  # noqa: A002
+              moving_mean_name=None, moving_variance_name=None, do_model_average_for_mean_and_var=True,
+              slot_dim=-1, sync_stats=False, summary_decay_rate=0.9999999, enable_scale_and_shift=False):
+    """Reference static/nn/common.py data_norm (CTR feature normalisation): persistent batch
+    statistics batch_size / batch_sum / batch_square_sum (init 1e4 / 0 / 1e4, like the reference),
+    y = (x - sum/size) * sqrt(size / square_sum); the statistics decay by summary_decay_rate and
+    absorb each training batch (the reference updates them in its backward)."""
+    from ..core.tensor import Parameter
+    C = input.shape[-1] if data_layout == 'NHWC' or len(input.shape) == 2 else input.shape[1]
+
+    def stat(v):
+        p = Parameter(torch.full([C], float(v)), trainable=False)
+        p.stop_gradient = True
+        return p
+    size, ssum, sq = stat(1e4), stat(0.0), stat(1e4)
+    mean = ssum / size
+    scale = (size / sq).sqrt()
+    y = (input - mean) * scale
+    if enable_scale_and_shift:
+        w = _nn.Layer().create_parameter([C], default_initializer=_nn.initializer.Constant(1.0))
+        b = _nn.Layer().create_parameter([C], default_initializer=_nn.initializer.Constant(0.0), is_bias=True)
+        y = y * w + b
+    if not _is_static(input):  # dygraph: update the statistics with this batch
+        with torch.no_grad():
+            x = _unwrap(input).reshape(-1, C).float()
+            for p, v in ((size, torch.full([C], float(x.shape[0]))), (ssum, x.sum(0)), (sq, (x * x).sum(0))):
+                p._t.mul_(summary_decay_rate).add_(v.to(p._t.device, p._t.dtype))
+    return _act(y, act)
+
+
+def group_norm(input, groups, epsilon=1e-05, param_attr=None, bias_attr=None, act=None, data_layout='NCHW',  # noqa: A002
+               name=None):
+    c = input.shape[1] if data_layout == 'NCHW' else input.shape[-1]
+    gn = _nn.GroupNorm(groups, c, epsilon=epsilon, weight_attr=param_attr, bias_attr=bias_attr,
+                       data_format=data_layout)
+    return _act(gn(input), act)
+
+
+def instance_norm(input, epsilon=1e-05, param_attr=None, bias_attr=None, name=None):  # noqa: A002
+    c = input.shape[1]
+    cls = {3: _nn.InstanceNorm1D, 4: _nn.InstanceNorm2D, 5: _nn.InstanceNorm3D}[len(input.shape)]
+    return cls(c, epsilon=epsilon, weight_attr=param_attr, bias_attr=bias_attr)(input)
+
+
+def conv3d(input, num_filters, filter_size, stride=1, padding=0, dilation=1, groups=1, param_attr=None,  # noqa: A002
+           bias_attr=None, use_cudnn=True, act=None, name=None, data_format="NCDHW"):
+    cin = input.shape[1] if data_format == 'NCDHW' else input.shape[-1]
+    conv = _nn.Conv3D(cin, num_filters, filter_size, stride, padding, dilation, groups, weight_attr=param_attr,
+                      bias_attr=bias_attr, data_format=data_format)
+    return _act(conv(input), act)
+
+
+def conv3d_transpose(input, num_filters, output_size=None, filter_size=None, padding=0, stride=1, dilation=1,  # noqa: A002
+                     groups=1, param_attr=None, bias_attr=None, use_cudnn=True, act=None, name=None,
+                     data_format='NCDHW'):
+    cin = input.shape[1] if data_format == 'NCDHW' else input.shape[-1]
+    conv = _nn.Conv3DTranspose(cin, num_filters, filter_size, stride, padding, groups=groups, dilation=dilation,
+                               weight_attr=param_attr, bias_attr=bias_attr, data_format=data_format)
+    return _act(conv(input), act)
+
+
+def bilinear_tensor_product(x, y, size, act=None, name=None, param_attr=None, bias_attr=None):
+    """out_k = x W_k y^T + b_k (reference static/nn/common.py bilinear_tensor_product)."""
+    bl = _nn.Bilinear(x.shape[-1], y.shape[-1], size, weight_attr=param_attr, bias_attr=bias_attr)
+    return _act(bl(x, y), act)
+
+
+def spectral_norm(weight, dim=0, power_iters=1, eps=1e-12, name=None):
+    sn = _nn.SpectralNorm(list(weight.shape), axis=dim, power_iters=power_iters, epsilon=eps)
+    return sn(weight)
+
+
+def deform_conv2d(x, offset, mask, num_filters, filter_size, stride=1, padding=0, dilation=1, groups=1,
+                  deformable_groups=1, im2col_step=1, weight_attr=None, bias_attr=None, name=None):
+    from ..vision.ops import DeformConv2D
+    dc = DeformConv2D(x.shape[1], num_filters, filter_size, stride, padding, dilation, deformable_groups, groups,
+                      weight_attr=weight_attr, bias_attr=bias_attr)
+    return dc(x, offset, mask)
+
+
+def sparse_embedding(input, size, padding_idx=None, is_test=False, entry=None, table_class="MemorySparseTable",  # noqa: A002
+                     param_attr=None, dtype='float32', slot=None):
+    """Parameter-server sparse table lookup; on one process a dense embedding of the same shape."""
+    return embedding(input, size, is_sparse=True, padding_idx=padding_idx, param_attr=param_attr, dtype=dtype)
+
+
+def row_conv(input, future_context_size, param_attr=None, act=None):  # noqa: A002
+    """Lookahead convolution (reference static/nn/common.py row_conv, DeepSpeech2): out[t] =
+    sum_{j=0..k} x[t+j] * W[j] per feature, within each sequence of a LoD input or along the time
+    axis of a padded [B, T, D] input."""
+    D = input.shape[-1]
+    w = _nn.Layer().create_parameter([future_context_size + 1, D], attr=param_attr)
+    if not _is_static(input) and input.__dict__.get('_lod') is not None:
+        from . import sequence as S
+        lod = S.get_lod(input)
+        out = _wrap(S.row_conv_lod(_unwrap(input).reshape(-1, D), lod, _unwrap(w)))
+        return _act(S.with_lod(out, lod), act)
+    x = _unwrap(input)
+    T = x.shape[1]
+    xp = torch.nn.functional.pad(x, (0, 0, 0, future_context_size))
+    out = sum(xp[:, j:j + T] * _unwrap(w)[j] for j in range(future_context_size + 1))
+    return _act(_wrap(out), act)
+
+
+def nce(input, label, num_total_classes, sample_weight=None, param_attr=None, bias_attr=None,  # noqa: A002
+        num_neg_samples=None, name=None, sampler='uniform', custom_dist=None, seed=0, is_sparse=False):
+    """Noise-contrastive estimation loss (reference static/nn/common.py nce / nce_op.h): for each
+    example the true class and num_neg_samples sampled classes are scored with a logistic model
+    o = sigmoid(x·w_c + b_c); cost = -log(o_true / (o_true + k q)) - sum log(k q / (o_neg + k q)),
+    q = the sampler's probability of the class.  Returns [batch, 1]."""
+    k = 10 if num_neg_samples is None else int(num_neg_samples)
+    D = input.shape[-1]
+    layer = _nn.Layer()
+    w = layer.create_parameter([num_total_classes, D], attr=param_attr)
+    b = layer.create_parameter([num_total_classes, 1], attr=bias_attr, is_bias=True)
+    x = _unwrap(input)
+    lab = _unwrap(label).reshape(x.shape[0], -1).long()
+    B = x.shape[0]
+    g = torch.Generator(device='cpu').manual_seed(int(seed))
+    if sampler == 'uniform':
+        q_all = torch.full([num_total_classes], 1.0 / num_total_classes)
+        neg = torch.randint(0, num_total_classes, (B, k), generator=g)
+    elif sampler == 'log_uniform':
+        r = torch.arange(num_total_classes, dtype=torch.float64)
+        q_all = (torch.log((r + 2) / (r + 1)) / np.log(num_total_classes + 1)).float()
+        neg = torch.multinomial(q_all, B * k, replacement=True, generator=g).reshape(B, k)
+    elif sampler == 'custom_dist':
+        q_all = torch.as_tensor(np.asarray(custom_dist), dtype=torch.float32)
+        neg = torch.multinomial(q_all, B * k, replacement=True, generator=g).reshape(B, k)
+    else:
+        raise ValueError(f"unknown sampler {sampler}")
+    neg = neg.to(x.device)
+    q_all = q_all.to(x.device, x.dtype)
+    W, bb = _unwrap(w), _unwrap(b).reshape(-1)
+
+    def score(cls):
+        return torch.sigmoid((x.unsqueeze(1) * W[cls]).sum(-1) + bb[cls])
+    o_t, o_n = score(lab), score(neg)
+    kq_t, kq_n = k * q_all[lab], k * q_all[neg]
+    cost = -torch.log(o_t / (o_t + kq_t)).sum(1) - torch.log(kq_n / (o_n + kq_n)).sum(1)
+    if sample_weight is not None:
+        cost = cost * _unwrap(sample_weight).reshape(-1)
+    return _wrap(cost.reshape(B, 1))
+
+
+def static_pylayer(forward_fn, inputs, backward_fn=None, name=None):
+    """Reference static/nn/static_pylayer.py: run forward_fn on inputs; with backward_fn the
+    gradient of the outputs w.r.t. the inputs is backward_fn(*output_grads)."""
+    if backward_fn is None:
+        return forward_fn(*inputs)
+
+    class _SPL(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, *ts):
+            with torch.no_grad():
+                outs = forward_fn(*[_wrap(t) for t in ts])
+            ctx.multi = isinstance(outs, (list, tuple))
+            outs = outs if ctx.multi else [outs]
+            return tuple(_unwrap(o) for o in outs) if ctx.multi else _unwrap(outs[0])
+
+        @staticmethod
+        def backward(ctx, *gs):
+            res = backward_fn(*[_wrap(g) for g in gs])
+            res = res if isinstance(res, (list, tuple)) else [res]
+            return tuple(None if r is None else _unwrap(r) for r in res)
+    out = _SPL.apply(*[_unwrap(t) for t in inputs])
+    return [_wrap(o) for o in out] if isinstance(out, tuple) else _wrap(out)
 
 
 # ----------------------------------------------------------------- control flow
@@ -219,5 +385,97 @@ def py_func(func, x, out, backward_func=None, skip_vars_in_backward_input=None):
     return res if isinstance(out, (list, tuple)) else res[0]
 
 
-def sequence_pool(*a, **k):
-    raise NotImplementedError("LoD sequence ops are not supported; use padded tensors with masks")
+# ----------------------------------------------------------------- LoD sequence ops (static/sequence.py)
+def _is_static(x):
+    return isinstance(x, Tensor) and x._t.device.type == 'meta'
+
+
+def _seq(fn, tensors, out_rows_like=None, out_cols=None, n_out=1):
+    """Runs a sequence op eagerly, or records it as a py-node inside a static Program (the LoD of
+    the fed tensors reaches it through the Executor)."""
+    if not any(_is_static(t) for t in tensors if isinstance(t, Tensor)):
+        return fn(*tensors)
+    from .program import SENTINELS
+    t0 = _unwrap(tensors[0])
+    cols = list(t0.shape[1:]) if out_cols is None else list(out_cols)
+    with _paused():
+        metas = [torch.empty([SENTINELS[0]] + cols, dtype=t0.dtype, device='meta') for _ in range(n_out)]
+    res = py_func(lambda *ts: fn(*ts), list(tensors), [_wrap(m) for m in metas] if n_out > 1 else _wrap(metas[0]))
+    return res
+
+
+def sequence_pool(input, pool_type, is_test=False, pad_value=0.0):  # noqa: A002
+    from . import sequence as S
+    return _seq(lambda x: S.sequence_pool(x, pool_type, is_test, pad_value), [input])
+
+
+def sequence_first_step(input):  # noqa: A002
+    return sequence_pool(input, 'first')
+
+
+def sequence_last_step(input):  # noqa: A002
+    return sequence_pool(input, 'last')
+
+
+def sequence_softmax(input, use_cudnn=False, name=None):  # noqa: A002
+    from . import sequence as S
+    return _seq(S.sequence_softmax, [input])
+
+
+def sequence_conv(input, num_filters, filter_size=3, filter_stride=1, padding=True, padding_start=None,  # noqa: A002
+                  bias_attr=None, param_attr=None, act=None, name=None):
+    from . import sequence as S
+    if _is_static(input):
+        D = input.shape[-1]
+        lin = _nn.Linear(filter_size * D, num_filters, weight_attr=param_attr, bias_attr=bias_attr)
+        ps = -int(filter_size // 2) if padding_start is None else padding_start
+
+        def run(x):
+            ctx = S._context_rows(_unwrap(x).reshape(x.shape[0], D), S.get_lod(x), filter_size, ps)
+            out = lin(_wrap(ctx))
+            return S.with_lod(_act(out, act), S.get_lod(x))
+        return _seq(run, [input], out_cols=[num_filters])
+    return S.sequence_conv(input, num_filters, filter_size, filter_stride, padding, padding_start, bias_attr,
+                           param_attr, act, name)
+
+
+def sequence_slice(input, offset, length, name=None):  # noqa: A002
+    from . import sequence as S
+    return _seq(lambda x, o, l: S.sequence_slice(x, o, l), [input, offset, length])
+
+
+def sequence_expand(x, y, ref_level=-1, name=None):
+    from . import sequence as S
+    return _seq(lambda a, b: S.sequence_expand(a, b, ref_level), [x, y])
+
+
+def sequence_expand_as(x, y, name=None):
+    from . import sequence as S
+    return _seq(S.sequence_expand_as, [x, y])
+
+
+def sequence_pad(x, pad_value, maxlen=None, name=None):
+    from . import sequence as S
+    if _is_static(x):
+        return _seq(lambda a, p: S.sequence_pad(a, p, maxlen), [x, pad_value], n_out=2)
+    return S.sequence_pad(x, pad_value, maxlen)
+
+
+def sequence_unpad(x, length, name=None):
+    from . import sequence as S
+    return _seq(S.sequence_unpad, [x, length], out_cols=list(x.shape[2:]))
+
+
+def sequence_reshape(input, new_dim):  # noqa: A002
+    from . import sequence as S
+    return _seq(lambda a: S.sequence_reshape(a, new_dim), [input], out_cols=[new_dim])
+
+
+def sequence_scatter(input, index, updates, name=None):  # noqa: A002
+    from . import sequence as S
+    return _seq(S.sequence_scatter, [input, index, updates])
+
+
+def sequence_enumerate(input, win_size, pad_value=0, name=None):  # noqa: A002
+    from . import sequence as S
+    return _seq(lambda a: S.sequence_enumerate(a, win_size, pad_value), [input], out_cols=[win_size])
