@@ -185,9 +185,27 @@ def _fetch_vids(prog, fetch_vars):
     return [_vid_of(prog, v) for v in fetch_vars]
 
 
+def _pd_export(prog, feed_names, fetch_vids):
+    """Reference ProgramDesc bytes (static/pdmodel.py) or None when the program uses an operator
+    outside the exportable set (or PADDLE_AMD_PDMODEL=0): then this framework's IR is written."""
+    if os.environ.get('PADDLE_AMD_PDMODEL', '1') == '0':
+        return None
+    from . import pdmodel
+    try:
+        data, params = pdmodel.export(prog, feed_names, fetch_vids)
+    except pdmodel.Unsupported:
+        prog._pd_params = None
+        return None
+    prog._pd_params = params
+    return data
+
+
 def serialize_program(feed_vars, fetch_vars, program=None, **kw):
     prog = program or default_main_program()
     feed_names = [v.name if isinstance(v, Tensor) else v for v in feed_vars]
+    pd = _pd_export(prog, feed_names, _fetch_vids(prog, fetch_vars))
+    if pd is not None:
+        return pd
     feeds = []
     for name in feed_names:
         vid, shape, dt = prog.feeds[name]
@@ -202,6 +220,12 @@ def serialize_program(feed_vars, fetch_vars, program=None, **kw):
 def serialize_persistables(feed_vars, fetch_vars, executor=None, program=None, **kw):
     from safetensors.torch import save
     prog = program or default_main_program()
+    if getattr(prog, '_pd_params', None) is None and os.environ.get('PADDLE_AMD_PDMODEL', '1') != '0':
+        feed_names = [v.name if isinstance(v, Tensor) else v for v in feed_vars]
+        _pd_export(prog, feed_names, _fetch_vids(prog, fetch_vars))
+    if getattr(prog, '_pd_params', None) is not None:  # reference .pdiparams: LoDTensor streams
+        from .proto import save_combine
+        return save_combine([(n, t.detach()) for n, t in prog._pd_params])
     return save({f"c{cid}": t.detach().contiguous().cpu() for cid, t in prog.consts.items()})
 
 
@@ -222,7 +246,10 @@ class LoadedProgram(Program):
 
 
 def deserialize_program(data, device=None):
+    from . import pdmodel
     with _paused():
+        if isinstance(data, (bytes, bytearray)) and pdmodel.is_program_desc(bytes(data[:1])):
+            return pdmodel.load(bytes(data))
         return _deserialize_program(data, device)
 
 
@@ -254,6 +281,10 @@ def deserialize_persistables(program, data, executor=None, device=None):
     from ..core.place import current_device
     from ..core.tensor import Parameter
     dev = device or current_device()
+    if getattr(program, '_pdmodel', False):
+        from . import pdmodel
+        pdmodel.load_params(program, data, dev)
+        return
     tensors = load(data)
     program._const_owner = {}
     for cid, name in program._const_names.items():
