@@ -390,9 +390,34 @@ def shard_layer(layer, process_mesh, shard_fn=None, input_fn=None, output_fn=Non
 
 
 class _ShardingStageBase:
+    """Reference python/paddle/distributed/auto_parallel/api.py ShardingStage1/2/3: passed to
+    shard_optimizer, it partitions the optimizer state (stage 1), also the gradients (stage 2)
+    and also the parameters (stage 3) over one mesh dimension."""
+    level = None
+
     def __init__(self, mesh=None, sharding_mesh_dim=None):
         self._mesh = mesh
         self._sharding_mesh_dim = sharding_mesh_dim
+
+    def _group(self, params):
+        """Process group of the sharding axis: ``sharding_mesh_dim`` of the mesh (default: the
+        mesh of the first parameter, its dim 0, i.e. the data-parallel axis), or the world."""
+        mesh = self._mesh
+        if mesh is None:
+            for p in params:
+                m = _dist_meta(p)
+                if m is not None:
+                    mesh = m[0]
+                    break
+        if mesh is None or not dist.is_initialized():
+            return None
+        d = self._sharding_mesh_dim
+        if isinstance(d, str):
+            d = mesh.dim_names.index(d)
+        d = 0 if d is None else int(d)
+        _ensure_mesh_groups(mesh)
+        grp, _ = mesh.dim_group(d)
+        return grp
 
 
 class ShardingStage1(_ShardingStageBase):
@@ -408,17 +433,45 @@ class ShardingStage3(_ShardingStageBase):
 
 
 class _ShardOptimizer:
-    """Optimizer whose replicated-parameter gradients are averaged over the data-parallel
-    mesh dim; with a ShardingStage the optimizer states are partitioned by our sharding engine."""
+    """shard_optimizer result.
 
-    def __init__(self, optimizer, shard_fn=None):
+    * no shard_fn: gradients of parameters replicated along a mesh dim are averaged over that
+      dim with ONE coalesced all-reduce per (dim group, dtype) bucket (not one call per
+      parameter), then the wrapped optimizer steps.
+    * ShardingStage1/2: a sharding engine (parallel/sharding.py, the same one as fleet's
+      DygraphShardingOptimizer) over the sharding-axis group owns the optimizer: gradients are
+      reduce-scattered asynchronously as they land in backward, each rank updates its shard of the
+      fp32 master / moments with the fused kernel, parameters are all-gathered after the step.
+    * ShardingStage3: the same, plus the parameters themselves are released between uses when the
+      model is known (dist.to_static / DistModel passes its layer); a bare optimizer gets stage-2
+      behaviour.
+    """
+
+    def __init__(self, optimizer, shard_fn=None, layer=None):
         self._inner_opt = optimizer
         self._shard_fn = shard_fn
         self._engine = None
+        self._sharded = None
+        if shard_fn is not None:
+            if not isinstance(shard_fn, _ShardingStageBase):
+                raise TypeError("shard_fn must be a ShardingStage1/2/3 instance")
+            from ..parallel.sharding import ShardingEngine, ShardedOptimizer
+            params = [p for p in optimizer._parameter_list if not p.stop_gradient]
+            grp = shard_fn._group(params)
+            level = shard_fn.level
+            if level == 'p_g_os' and layer is None:
+                level = 'os_g'
+            if level == 'p_g_os':
+                self._engine = ShardingEngine(layer, level, group=grp)
+            else:
+                self._engine = ShardingEngine(None, level, group=grp, params=params)
+            self._sharded = ShardedOptimizer(optimizer, self._engine)
 
     def _sync_grads(self):
         if not dist.is_initialized() or dist.get_world_size() == 1:
             return
+        from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+        buckets = {}
         for p in self._inner_opt._parameter_list:
             g = p._t.grad
             if g is None:
@@ -426,31 +479,64 @@ class _ShardOptimizer:
             m = _dist_meta(p)
             mesh, pl = (m[0], m[1]) if m else (None, None)
             if mesh is None:
-                dist.all_reduce(g)
-                g.div_(dist.get_world_size())
+                buckets.setdefault((tuple(range(dist.get_world_size())), g.dtype), [None, []])[1].append(g)
                 continue
             for d, pd in enumerate(pl):
                 if isinstance(pd, Replicate) and mesh.shape[d] > 1:
                     grp, ranks = mesh.dim_group(d)
-                    dist.all_reduce(g, group=grp)
-                    g.div_(len(ranks))
+                    b = buckets.setdefault((tuple(ranks), g.dtype), [grp, []])
+                    b[1].append(g)
+        for (ranks, dt), (grp, gs) in buckets.items():
+            flat = _flatten_dense_tensors(gs)
+            dist.all_reduce(flat, group=grp)
+            flat.div_(len(ranks))
+            for g, r in zip(gs, _unflatten_dense_tensors(flat, gs)):
+                g.copy_(r)
 
     def step(self):
+        if self._sharded is not None:
+            return self._sharded.step()
         self._sync_grads()
         self._inner_opt.step()
 
     def clear_grad(self, set_to_zero=True):
+        if self._sharded is not None:
+            return self._sharded.clear_grad()
         self._inner_opt.clear_grad(set_to_zero)
+
+    clear_gradients = clear_grad
+
+    def state_dict(self):
+        return self._sharded.state_dict() if self._sharded is not None else self._inner_opt.state_dict()
+
+    def set_state_dict(self, sd):
+        if self._sharded is not None:
+            return self._sharded.set_state_dict(sd)
+        return self._inner_opt.set_state_dict(sd)
 
     def __getattr__(self, name):
         return getattr(self._inner_opt, name)
 
 
-def shard_optimizer(optimizer, shard_fn=None):
+def shard_optimizer(optimizer, shard_fn=None, gradient_accumulation_steps=1):
     return _ShardOptimizer(optimizer, shard_fn)
 
 
+
 def shard_scaler(scaler):
+    """Reference api.py shard_scaler: the found-inf decision is all-reduced (MAX) over every rank,
+    so ranks holding different shards skip or apply the step together."""
+    def sync(found):
+        v = float(found) if isinstance(found, bool) else float(found.item() > 0)
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            import torch as _t
+            dev = _t.device('cuda', _t.cuda.current_device()) if (_t.cuda.is_available() and
+                                                                 dist.get_backend() == 'nccl') else _t.device('cpu')
+            t = _t.tensor([v], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            v = float(t.item())
+        return v > 0
+    scaler._sync_found_inf = sync
     return scaler
 
 
@@ -495,13 +581,17 @@ class Strategy:
 
     def __init__(self, config=None):
         config = config or {}
-        self.sharding = Strategy._Cfg(enable=False, stage=1, degree=8, **config.get('sharding', {}))
-        self.gradient_merge = Strategy._Cfg(enable=False, k_steps=1, avg=True, **config.get('gradient_merge', {}))
-        self.pipeline = Strategy._Cfg(enable=False, schedule_mode='1F1B', micro_batch_size=1, accumulate_steps=1,
-                                      **config.get('pipeline', {}))
-        self.amp = Strategy._Cfg(enable=False, dtype='bfloat16', level='O2', **config.get('amp', {}))
-        self.recompute = Strategy._Cfg(enable=False, **config.get('recompute', {}))
-        self.fused_passes = Strategy._Cfg(enable=False, fused_passes_list=[], **config.get('fused_passes', {}))
+
+        def cfg(name, **defaults):
+            c = Strategy._Cfg(defaults)
+            c.update(config.get(name, {}))
+            return c
+        self.sharding = cfg('sharding', enable=False, stage=1, degree=8)
+        self.gradient_merge = cfg('gradient_merge', enable=False, k_steps=1, avg=True)
+        self.pipeline = cfg('pipeline', enable=False, schedule_mode='1F1B', micro_batch_size=1, accumulate_steps=1)
+        self.amp = cfg('amp', enable=False, dtype='bfloat16', level='O2')
+        self.recompute = cfg('recompute', enable=False)
+        self.fused_passes = cfg('fused_passes', enable=False, fused_passes_list=[])
 
 
 class DistModel:
@@ -512,8 +602,25 @@ class DistModel:
         self._layer = layer
         self._loader = loader
         self._loss = loss
-        self._opt = optimizer
         self._strategy = strategy or Strategy()
+        st = self._strategy
+        # sharding: optimizer states (and grads / params by stage) over the data-parallel axis
+        if optimizer is not None and st.sharding.get('enable'):
+            inner = optimizer._inner_opt if isinstance(optimizer, _ShardOptimizer) else optimizer
+            stage = {1: ShardingStage1, 2: ShardingStage2, 3: ShardingStage3}[int(st.sharding.get('stage', 1))]()
+            optimizer = _ShardOptimizer(inner, stage, layer=layer)
+        self._opt = optimizer
+        gm = st.gradient_merge
+        self._k = int(gm.get('k_steps', 1)) if gm.get('enable') else 1
+        self._avg = bool(gm.get('avg', True))
+        self._micro = 0
+        if st.recompute.get('enable'):
+            from .fleet.recompute import recompute
+
+            def wrap(f):
+                return lambda *a, **k: recompute(f, *a, **k) if layer.training else f(*a, **k)
+            for _, sub in list(layer.named_children()):
+                sub.forward = wrap(sub.forward)
         self._mode = 'train' if optimizer is not None and loss is not None else 'predict'
 
     def train(self):
@@ -534,12 +641,25 @@ class DistModel:
             with _t.no_grad():
                 return self._layer(*args)
         inputs, labels = args[:-1], args[-1]
-        out = self._layer(*inputs)
-        loss = self._loss(out, labels)
+        amp = self._strategy.amp
+        if amp.get('enable'):
+            from ..amp import auto_cast
+            ctx = auto_cast(True, custom_white_list=amp.get('custom_white_list'),
+                            custom_black_list=amp.get('custom_black_list'), level=amp.get('level', 'O2'),
+                            dtype=amp.get('dtype', 'bfloat16'))
+        else:
+            import contextlib
+            ctx = contextlib.nullcontext()
+        with ctx:
+            out = self._layer(*inputs)
+            loss = self._loss(out, labels)
         if self._mode == 'train':
-            loss.backward()
-            self._opt.step()
-            self._opt.clear_grad()
+            # gradient merge: k micro-steps accumulate before one update ('avg' divides by k)
+            (loss / self._k if (self._k > 1 and self._avg) else loss).backward()
+            self._micro += 1
+            if self._micro % self._k == 0:
+                self._opt.step()
+                self._opt.clear_grad()
         return loss
 
     def state_dict(self, mode='all'):

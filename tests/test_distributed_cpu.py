@@ -70,6 +70,12 @@ def test_auto_parallel_reshard_and_dist_checkpoint(tmp_path):
     assert out.count("auto_parallel OK") == 2, out[-3000:]
 
 
+@pytest.mark.parametrize("mode", ['plain', 'stage1', 'stage2', 'distmodel'])
+def test_auto_parallel_shard_optimizer_matches_single_process(mode):
+    out = run_workers('worker_auto_shard.py', mode)
+    assert out.count(f"auto_shard {mode} OK") == 2, out[-3000:]
+
+
 def test_comm_watchdog_reports_stuck_collective():
     out = run_workers('worker_watchdog.py', timeout=120)
     assert out.count("watchdog OK") == 2, out[-3000:]
