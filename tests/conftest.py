@@ -28,3 +28,13 @@ def static_mode():
     paddle.enable_static()
     yield
     paddle.disable_static()
+
+
+@pytest.fixture(autouse=True)
+def _restore_paddle_device():
+    """A test that switches devices (paddle.set_device) must not leak it into later tests."""
+    import paddle
+    dev = paddle.get_device()
+    yield
+    if paddle.get_device() != dev:
+        paddle.set_device(dev)
