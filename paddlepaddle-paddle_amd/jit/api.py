@@ -1,10 +1,12 @@
 """paddle.jit (reference: python/paddle/jit/api.py — to_static:214, not_to_static:357,
 save:908, load:1480; translated_layer.py TranslatedLayer).
 
-MI355X-first: there is no AST rewriting / tracing compiler.  The eager path already runs the
-hand-written HIP kernels; ``to_static`` keeps dygraph semantics and adds
+MI355X-first: calls are not traced or compiled.  The eager path already runs the hand-written HIP
+kernels; ``to_static`` keeps dygraph semantics and adds
 * a recorded static Program on demand (``concrete_program``) — the same IR ``jit.save``
-  serialises (``static/io.py``);
+  serialises (``static/io.py``).  Recording runs the function after ``dy2static`` has rewritten
+  its tensor-dependent ``if`` / ``while`` / ``for range`` / ``and``/``or``/``not`` into
+  ``cond`` / ``while`` nodes (``jit/dy2static.py``), so the saved program branches per input;
 * HIP-graph replay of the forward for inference-shaped calls (``backend='hip_graph'`` or
   ``build_strategy.use_hip_graph``): launch-bound small-batch decoding collapses into one
   graph launch per call.
@@ -12,12 +14,12 @@ hand-written HIP kernels; ``to_static`` keeps dygraph semantics and adds
 Python class that produced it.
 """
 import functools
-import inspect
 
 import torch
 
 from ..core.tensor import Tensor, _wrap, _unwrap
 from ..nn.layer.layers import Layer
+from .dy2static import convert_function, converted_source
 from ..static.program import (InputSpec, Program, program_guard, data as _data, _start_recording,
                               _stop_recording, _recorder, default_main_program)
 
@@ -41,9 +43,15 @@ def ignore_module(modules):
 
 
 def not_to_static(func=None):
+    def mark(f):
+        try:
+            f._jst_not_to_static = True
+        except (AttributeError, TypeError):
+            pass
+        return f
     if func is None:
-        return lambda f: f
-    return func
+        return mark
+    return mark(func)
 
 
 def _spec_of(x, i):
@@ -77,7 +85,7 @@ def record_program(fn, input_spec):
                 name = s.name or f"x{i}"
                 shape = [(-1 if (d is None or d < 0) else d) for d in s.shape]
                 feeds.append(_data(name, shape, s.dtype))
-            out = fn(*feeds)
+            out = (convert_function(fn) if _to_static_enabled[0] else fn)(*feeds)
     finally:
         if started:
             _stop_recording()
@@ -146,10 +154,7 @@ class StaticFunction:
 
     @property
     def code(self):
-        try:
-            return inspect.getsource(self._fn)
-        except (OSError, TypeError):
-            return ''
+        return converted_source(self._fn)
 
     @property
     def dygraph_function(self):

@@ -610,8 +610,10 @@ def _emit(ex, n):
         if scalar(x) and not scalar(y) and base in ('add', 'mul'):
             x, y = y, x
         if scalar(y):
+            if base == 'div' and float(y) == 0.0:
+                raise Unsupported("division by a zero scalar")
             s, bb = {'add': (1.0, float(y)), 'sub': (1.0, -float(y)), 'mul': (float(y), 0.0),
-                     'div': (1.0 / float(y), 0.0)}[base]
+                     'div': (1.0 / float(y) if base == 'div' else 0.0, 0.0)}[base]
             ex.op('scale', {'X': ex.name_of(x)}, {'Out': out}, scale=s, bias=bb, bias_after_scale=True)
         elif scalar(x):
             raise Unsupported("scalar-first sub/div")
