@@ -191,11 +191,31 @@ class PipelineParallel(Layer):
         self._meta_bwd = None
         self.total_loss = None
         self._sends = []
+        # gradients travel on a second pipe communicator: each (src, dst) channel then carries ONE
+        # kind of message in schedule order, so receives can be posted ahead of the compute that
+        # precedes them without ever being matched against the wrong send (on RCCL every pair
+        # communicator is one stream: a pre-posted activation receive must not sit in front of a
+        # gradient send the peer is waiting for).  Every rank creates every pipe group, in order.
+        self._grad_pg = None
+        topo = hcg.topology()
+        if self.num_stages > 1:
+            for ranks in topo.get_comm_list('pipe'):
+                g = hcg._mk(ranks)
+                if hcg.global_rank in ranks:
+                    self._grad_pg = g
+        self._act_q = []   # posted (work, buffer) activation receives, in micro-batch order
+        self._grad_q = []  # posted (work, buffer) gradient receives
+        self._acts_left = 0
+        self._grads_left = 0
+        self._meta_bwd = None
 
     def forward(self, *a, **k):
         return self._layers(*a, **k)
 
-    # ---- p2p helpers (metadata once, then raw tensors)
+    # ---- p2p helpers (metadata once per batch, then raw tensors; receives posted ahead)
+    def _gpg(self):
+        return None if self._grad_pg is None else getattr(self._grad_pg, 'pg', None)
+
     def _send_meta(self, t, peer):
         meta = torch.tensor([len(t.shape)] + list(t.shape) + [_DT.index(t.dtype)], dtype=torch.int64)
         meta = meta.to(t.device)
@@ -203,10 +223,10 @@ class PipelineParallel(Layer):
         self._isend(n, peer)
         self._isend(meta, peer)
 
-    def _isend(self, t, peer):
+    def _isend(self, t, peer, group=None):
         """Sends never block the schedule: in steady 1F1B a stage sends an activation forward
         while its neighbour sends a gradient back, so blocking sends would deadlock."""
-        self._sends.append((dist.isend(t, peer), t))
+        self._sends.append((dist.isend(t, peer, group=group), t))
 
     def _drain_sends(self):
         for w, _ in self._sends:
@@ -222,6 +242,27 @@ class PipelineParallel(Layer):
         nd = m[0]
         return tuple(m[1:1 + nd]), _DT[m[1 + nd]]
 
+    def _post_act(self, dev):
+        """Posts the receive of the next expected activation (it lands while this stage computes)."""
+        if self._acts_left > 0:
+            shape, dt = self._meta_fwd
+            buf = torch.empty(shape, dtype=dt, device=dev)
+            self._act_q.append((dist.irecv(buf, self._prev), buf))
+            self._acts_left -= 1
+
+    def _post_grad(self, dev):
+        if self._grads_left > 0 and self._meta_bwd is not None:
+            shape, dt = self._meta_bwd
+            buf = torch.empty(shape, dtype=dt, device=dev)
+            self._grad_q.append((dist.irecv(buf, self._next, group=self._gpg()), buf))
+            self._grads_left -= 1
+
+    @staticmethod
+    def _take(q):
+        w, buf = q.pop(0)
+        w.wait()  # RCCL: the compute stream waits on the receive; the host does not block
+        return buf
+
     def _dev(self):
         return torch.device('cuda', torch.cuda.current_device()) if torch.cuda.is_available() else torch.device('cpu')
 
@@ -232,6 +273,14 @@ class PipelineParallel(Layer):
         t = _unwrap(data)
         return [_wrap(c) for c in t.chunk(self.accumulate_steps, 0)]
 
+    def _begin(self, n_fwd, n_bwd):
+        self._sent_meta = False
+        self._meta_fwd = None
+        self._meta_bwd = None
+        self._act_q, self._grad_q = [], []
+        self._acts_left = 0 if self.is_first else n_fwd
+        self._grads_left = 0 if self.is_last else n_bwd
+
     def _fwd_step(self, mb_input, mb_label):
         dev = self._dev()
         if self.is_first:
@@ -239,9 +288,9 @@ class PipelineParallel(Layer):
         else:
             if self._meta_fwd is None:
                 self._meta_fwd = self._recv_meta(self._prev, dev)
-            shape, dt = self._meta_fwd
-            buf = torch.empty(shape, dtype=dt, device=dev)
-            dist.recv(buf, self._prev)
+                self._post_act(dev)
+            buf = self._take(self._act_q)
+            self._post_act(dev)  # prefetch the next micro-batch's activation under this compute
             buf.requires_grad_(True)
             x = _wrap(buf)
         out = self._layers(x)
@@ -254,6 +303,10 @@ class PipelineParallel(Layer):
             self._send_meta(o, self._next)
             self._sent_meta = True
         self._isend(o.detach().contiguous(), self._next)
+        if self._meta_bwd is None and self._grads_left > 0:
+            # the gradient of this stage's output has the output's shape: post its receive now
+            self._meta_bwd = (tuple(o.shape), o.dtype)
+            self._post_grad(dev)
         return x, out
 
     def _bwd_step(self, x, out):
@@ -261,20 +314,19 @@ class PipelineParallel(Layer):
             _unwrap(out).backward()
         else:
             o = _unwrap(out)
-            g = torch.empty_like(o)
-            dist.recv(g, self._next)
+            g = self._take(self._grad_q)
+            self._post_grad(o.device)
             o.backward(g)
         if not self.is_first:
             gx = _unwrap(x).grad
-            self._isend(gx.contiguous(), self._prev)
+            self._isend(gx.contiguous(), self._prev, group=self._gpg())
 
     def train_batch(self, data, optimizer, lr_scheduler=None, scaler=None):
         inputs, labels = data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None)
         mbs_in = self._split(inputs) if self.is_first else [None] * self.accumulate_steps
         mbs_lab = self._split(labels) if (self.is_last and labels is not None) else [None] * self.accumulate_steps
-        self._sent_meta = False
-        self._meta_fwd = None
         n = self.accumulate_steps
+        self._begin(n, n)
         warm = min(self.num_stages - self.stage_id - 1, n)
         pending = []
         losses = []
@@ -294,6 +346,7 @@ class PipelineParallel(Layer):
             self._bwd_step(*pending.pop(0))
         while pending:
             self._bwd_step(*pending.pop(0))
+        assert not (self._act_q or self._grad_q or self._acts_left or self._grads_left), "unmatched pipeline receives"
         self._drain_sends()
         if getattr(optimizer, '_syncs_dp', False) and self._layers._shared_comm:
             # the sharding optimizer reduce-scatters gradients inside backward, before this point
@@ -326,8 +379,7 @@ class PipelineParallel(Layer):
             inputs, labels = data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None)
             mbs_in = self._split(inputs) if self.is_first else [None] * self.accumulate_steps
             mbs_lab = self._split(labels) if (self.is_last and labels is not None) else [None] * self.accumulate_steps
-            self._sent_meta = False
-            self._meta_fwd = None
+            self._begin(self.accumulate_steps, 0)
             outs = []
             for i in range(self.accumulate_steps):
                 _, out = self._fwd_step(mbs_in[i], mbs_lab[i])
@@ -354,14 +406,7 @@ class PipelineParallelWithInterleave(PipelineParallel):
     the schedule is deadlock-free for every P, V (checked by simulation and the gloo tests)."""
 
     def __init__(self, layers, hcg, strategy):
-        super().__init__(layers, hcg, strategy)
-        # a second pipe communicator for gradients (every rank creates every pipe group, in order)
-        self._grad_pg = None
-        topo = hcg.topology()
-        for ranks in topo.get_comm_list('pipe'):
-            g = hcg._mk(ranks)
-            if hcg.global_rank in ranks:
-                self._grad_pg = g
+        super().__init__(layers, hcg, strategy)  # creates the gradient communicator
         self.schedule = 'interleaved_1f1b'
 
     def _peer(self, delta):
