@@ -38,6 +38,22 @@ struct Geom {
   int N, H, W, C, Ho, Wo, Cout, R, S, sh, sw, ph, pw, dh, dw;
 };
 
+// Filter taps of the implicit GEMM (k = (tap, c)): input row/col offsets of each tap, so a kernel
+// can run a SUBSET of the filter (a stride class of the data gradient), and the output pixel
+// mapping y = (oy0 + osy*ho, ox0 + osx*wo) in a [HY, WY] map (a stride class writes every s-th
+// pixel of dX).  Forward: all R*S taps at (r*dh - ph, s*dw - pw), identity mapping.
+constexpr int MAX_TAPS = 64, MAX_CLS = 9;
+struct Taps {
+  short th[MAX_TAPS], tw[MAX_TAPS];
+  int oy0, ox0, osy, osx, HY, WY;
+  long long ldw;  // row stride (elements) of the packed filter [Cout_y][taps][C]
+  // ncls > 0: a multi-class data-gradient launch (class c owns blocks [cls_end[c-1], cls_end[c]))
+  int ncls;
+  int cls_end[MAX_CLS], cls_tap0[MAX_CLS], cls_T[MAX_CLS], cls_a[MAX_CLS], cls_b[MAX_CLS], cls_Hc[MAX_CLS],
+      cls_Wc[MAX_CLS];
+  long long cls_woff[MAX_CLS];
+};
+
 __device__ __forceinline__ f32x4 mfma(s16x8 a, s16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
                                                  0, 0);
@@ -90,11 +106,13 @@ __device__ __forceinline__ void tile_coords(int bid, int nwg, int tm, int tn, in
   nt = in / gm;
 }
 
-template <int BN>
+template <int BN, int WM>
 __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restrict__ X,
                                                          const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y,
-                                                         const uint16_t* __restrict__ bias, Geom g, int M, int K) {
-  constexpr int FN = BN / 64;                 // 16-wide fragments per wave along N
+                                                         const uint16_t* __restrict__ bias, Geom g, Taps tp, int M,
+                                                         int K) {
+  constexpr int WNW = 8 / WM;                 // waves: WM along pixels x WNW along channels
+  constexpr int FM = 16 / WM, FN = BN / (16 * WNW);  // 16x16 fragments per wave
   constexpr int OPA = BM * BK * 2;            // 16 KB
   constexpr int OPB = BN * BK * 2;
   constexpr int SLOT = OPA + OPB;
@@ -106,10 +124,27 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
   constexpr int NSLOT = 4;
   __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
+  const int wr = wave / WNW, wc = wave % WNW;
+  // stride classes of a data gradient share one launch: the block finds its class (tile ranges
+  // are prefix sums) and takes the class's pixel grid, tap range, packed weights and output offset
+  int Ho = g.Ho, Wo = g.Wo, tap0 = 0, oy0 = tp.oy0, ox0 = tp.ox0, bid = blockIdx.x;
+  const uint16_t* Wp = Wt;
+  if (tp.ncls > 0) {
+    int c = 0;
+    while (c + 1 < tp.ncls && bid >= tp.cls_end[c]) ++c;
+    bid -= c ? tp.cls_end[c - 1] : 0;
+    Ho = tp.cls_Hc[c];
+    Wo = tp.cls_Wc[c];
+    tap0 = tp.cls_tap0[c];
+    oy0 = tp.cls_a[c];
+    ox0 = tp.cls_b[c];
+    M = g.N * Ho * Wo;
+    K = tp.cls_T[c] * g.C;
+    Wp = Wt + tp.cls_woff[c];
+  }
   const int tm = (M + BM - 1) / BM, tn = (g.Cout + BN - 1) / BN;
   int mt, ntile;
-  tile_coords(blockIdx.x, tm * tn, tm, tn, mt, ntile);
+  tile_coords(bid, tm * tn, tm, tn, mt, ntile);
   const int m0 = mt * BM, n0 = ntile * BN;
   const int ns = K / BK;
 
@@ -117,7 +152,7 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
   long long xb[2];
   int hb[2], wb[2], lch[2];
   bool mv[2];
-  const int HoWo = g.Ho * g.Wo;
+  const int HoWo = Ho * Wo;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = i * 128 + (tid >> 2);
@@ -125,10 +160,10 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
     mv[i] = m < M;
     const int mm = mv[i] ? m : 0;
     const int n = mm / HoWo, rem = mm - n * HoWo;
-    const int ho = rem / g.Wo, wo = rem - ho * g.Wo;
+    const int ho = rem / Wo, wo = rem - ho * Wo;
     xb[i] = (long long)n * g.H * g.W * g.C;
-    hb[i] = ho * g.sh - g.ph;
-    wb[i] = wo * g.sw - g.pw;
+    hb[i] = ho * g.sh;
+    wb[i] = wo * g.sw;
     lch[i] = (tid & 3) ^ (((row >> 3) & 1) << 1);
   }
   // B (packed weights [Cout][K]) source per DMA
@@ -138,7 +173,7 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
     const int c = (j * NT + tid) % NBC;
     const int row = c >> 2;
     const int l = (c & 3) ^ (((row >> 3) & 1) << 1);
-    bsrc[j] = Wt + (long long)min(n0 + row, g.Cout - 1) * K + l * 8;
+    bsrc[j] = Wp + (long long)min(n0 + row, g.Cout - 1) * tp.ldw + l * 8;
   }
 
   auto stage = [&](int s, int slot) {
@@ -148,10 +183,10 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
     const int kk = s * BK;
     const int tap = kk / g.C;
     const int c0 = kk - tap * g.C;
-    const int r = tap / g.S, q = tap - r * g.S;
+    const int th = tp.th[tap0 + tap], tw = tp.tw[tap0 + tap];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int hi = hb[i] + r * g.dh, wi = wb[i] + q * g.dw;
+      const int hi = hb[i] + th, wi = wb[i] + tw;
       const bool ok = mv[i] && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
       const void* src = ok ? (const void*)(X + xb[i] + ((long long)hi * g.W + wi) * g.C + c0 + lch[i] * 8)
                            : (const void*)g_zero16;
@@ -162,9 +197,9 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
       glds16(bsrc[j] + kk, __builtin_amdgcn_readfirstlane(bbase + ((j * NT + wave * 64) % NBC) * 16));
   };
 
-  f32x4 acc[8][FN];
+  f32x4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -172,11 +207,11 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
   for (int s = 0; s < NSLOT; ++s)
     if (s < ns) stage(s, s);
   wait_barrier<PER_SLOT>(max(min(ns, NSLOT) - 2, 0));
-  s16x8 fa[2][8], fb[2][FN];
+  s16x8 fa[2][FM], fb[2][FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) fb[0][j] = ld_frag(smem + OPA, wc * (16 * FN) + j * 16, lane);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) fa[0][i] = ld_frag(smem, wr * 128 + i * 16, lane);
+  for (int i = 0; i < FM; ++i) fa[0][i] = ld_frag(smem, wr * (16 * FM) + i * 16, lane);
   int slot = 0;
   for (int s = 0; s < ns; s += 2) {
 #pragma unroll
@@ -188,10 +223,10 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
 #pragma unroll
       for (int j = 0; j < FN; ++j) fb[u ^ 1][j] = ld_frag(ia + OPA, wc * (16 * FN) + j * 16, lane);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) fa[u ^ 1][i] = ld_frag(ia, wr * 128 + i * 16, lane);
+      for (int i = 0; i < FM; ++i) fa[u ^ 1][i] = ld_frag(ia, wr * (16 * FM) + i * 16, lane);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma(fb[u][j], fa[u][i], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
@@ -201,10 +236,17 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
   }
 
   const int gq = lane >> 4;
+  const bool ident = tp.osy == 1 && tp.osx == 1 && oy0 == 0 && ox0 == 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wr * (16 * FM) + i * 16 + (lane & 15);
     if (m >= M) continue;
+    long long ym = m;
+    if (!ident) {
+      const int nn = m / HoWo, rem = m - nn * HoWo;
+      const int ho = rem / Wo, wo = rem - ho * Wo;
+      ym = ((long long)nn * tp.HY + oy0 + tp.osy * ho) * tp.WY + ox0 + tp.osx * wo;
+    }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = n0 + wc * (16 * FN) + j * 16 + 4 * gq;
@@ -216,8 +258,228 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] += bb[r];
       }
-      store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(Y + (long long)m * g.Cout + n), v);
+      store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(Y + ym * g.Cout + n), v);
     }
+  }
+}
+
+
+// ============================================================================ filter gradient
+// dW[co, r, s, c] = sum_{n, ho, wo} dY[n, ho, wo, co] * X[n, ho*sh - ph + r*dh, wo*sw - pw + s*dw, c]
+//
+// Implicit GEMM with the PIXELS as the reduction axis: C'[m = (r, s, c)][co] = sum_p A[m][p] B[p][co],
+// A[m][p] = X at pixel p shifted by tap (r, s) (the im2col matrix, never stored), B = dY viewed
+// [P][Cout].  Both operands are m/n-contiguous along their rows (channels are the fastest axis of
+// NHWC), so both are staged as [32 pixels][cols] images and read with ds_read_b64_tr_b16, the
+// hardware transposed LDS read (the layout of the Linear weight-gradient GEMM in csrc/gemm.hip).
+//  * The tap/channel of every 16-B A chunk is fixed per thread (a 256-wide m tile covers whole
+//    8-channel groups of one tap, C % 8 == 0); the pixel advances by 32 per sub-tile, tracked
+//    incrementally as (n, ho, wo) — no division in the loop; taps in the zero padding and pixels
+//    past the split's end DMA a zero block.
+//  * B chunks stride by 32*Cout elements per sub-tile; rows past P are clamped (A is zero there).
+//  * Cout sits on the narrow tile side (BN = 64/128/256 from Cout) so the 64-channel layers do
+//    not waste MFMA work; the many-pixel reduction is split over gridDim.z (fp32 slabs [z][M][Cout]
+//    summed by the caller) to fill the 256 CUs — a 56x56 batch-256 layer has 800k pixels.
+//  * B images narrower than 256 columns use 64-/128-/256-B-row swizzles chosen so the 8 k-rows a
+//    32-lane half of a transposed read touches land on 8 distinct 32-B bank slots.
+template <int WCH>
+__device__ __forceinline__ int swz_w(int r) {
+  if constexpr (WCH >= 16) return ((r & 3) | (((r >> 3) & 1) << 2)) << 1;
+  else return (((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1;
+}
+template <int WCH>
+__device__ __forceinline__ int mn_off(int row, int ch) { return row * (WCH * 16) + ((ch ^ swz_w<WCH>(row)) << 4); }
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// fragment element j of lane (g = lane>>4, i = lane&15) = operand[col0 + i][k = 8g + j]
+template <int WCH>
+__device__ __forceinline__ s16x8 ld_frag_mn(const char* img, int col0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int kr = 8 * g + q;
+  const int ch = (col0 >> 3) + (p >> 1);
+  const int bi = (p & 1) * 8;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + mn_off<WCH>(kr, ch) + bi));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + mn_off<WCH>(kr + 4, ch) + bi));
+  s16x8 v;
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+  v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+  return v;
+}
+
+template <int BN, int WM>
+__global__ __launch_bounds__(NT, 1) void conv_wgrad_kernel(const uint16_t* __restrict__ X,
+                                                           const uint16_t* __restrict__ dY, float* __restrict__ ws,
+                                                           Geom g, int M, int P, int kchunk) {
+  constexpr int WNW = 8 / WM;                 // waves along Cout
+  constexpr int FM = 16 / WM, FN = BN / (16 * WNW);  // 16x16 fragments per wave
+  constexpr int WB = BN / 8;                  // 16-B chunks per B image row
+  constexpr int OPA = 256 * BK * 2;           // 16 KB: [32 pixels][256 (tap, c)]
+  constexpr int OPB = BN * BK * 2;
+  constexpr int SLOT = OPA + OPB;
+  constexpr int NBC = BK * WB;                // chunks of one B sub-tile
+  constexpr int DMA_B = NBC >= NT ? NBC / NT : 1;
+  constexpr int PER_SLOT = 2 + DMA_B;
+  constexpr int NSLOT = 4;
+  __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WNW, wc = wave % WNW;
+  const int tm = (M + 255) / 256, tn = (g.Cout + BN - 1) / BN;
+  int mt, ntile;
+  tile_coords(blockIdx.x, tm * tn, tm, tn, mt, ntile);
+  const int m0 = mt * 256, n0 = ntile * BN;
+  const int kbeg = blockIdx.z * kchunk;
+  const int kend = min(P, kbeg + kchunk);
+  const int ns = (kend - kbeg + BK - 1) / BK;
+
+  // A chunk i: k-row kr = 16 i + tid / 32, logical column chunk (tid % 32) ^ swz(kr)
+  const int HoWo = g.Ho * g.Wo;
+  const int dq = BK / g.Wo, dr = BK - dq * g.Wo;
+  long long xoff[2];
+  int offh[2], offw[2], n_[2], oh_[2], ow_[2], pp[2];
+  bool mv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int kr = 16 * i + (tid >> 5);
+    const int lch = (tid & 31) ^ swz_w<32>(kr);
+    const int m = m0 + lch * 8;
+    mv[i] = m < M;
+    const int mm = mv[i] ? m : 0;
+    const int tap = mm / g.C, c = mm - tap * g.C;
+    const int r = tap / g.S, q = tap - r * g.S;
+    offh[i] = r * g.dh - g.ph;
+    offw[i] = q * g.dw - g.pw;
+    xoff[i] = c;
+    const int p = kbeg + kr;
+    pp[i] = p;
+    const int pc = min(p, P - 1);
+    n_[i] = pc / HoWo;
+    const int rem = pc - n_[i] * HoWo;
+    oh_[i] = rem / g.Wo;
+    ow_[i] = rem - oh_[i] * g.Wo;
+  }
+  // B chunk j: k-row c / WB, logical chunk (c % WB) ^ swz(row)
+  const uint16_t* bsrc[DMA_B];
+  int brow[DMA_B];
+#pragma unroll
+  for (int j = 0; j < DMA_B; ++j) {
+    const int c = (j * NT + tid) % NBC;
+    const int row = c / WB;
+    const int l = (c % WB) ^ swz_w<WB>(row);
+    brow[j] = kbeg + row;
+    bsrc[j] = dY + min(n0 + l * 8, g.Cout - 8);
+  }
+
+  auto stage = [&](int s, int slot) {
+    char* ia = smem + slot * SLOT;
+    const unsigned abase = (unsigned)(size_t)(lds_void*)ia;
+    const unsigned bbase = abase + OPA;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int hi = oh_[i] * g.sh + offh[i], wi = ow_[i] * g.sw + offw[i];
+      const bool ok = mv[i] && pp[i] < kend && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+      const void* src = ok ? (const void*)(X + (((long long)n_[i] * g.H + hi) * g.W + wi) * g.C + xoff[i])
+                           : (const void*)g_zero16;
+      glds16(src, __builtin_amdgcn_readfirstlane(abase + (i * NT + wave * 64) * 16));
+      // advance this chunk's pixel by 32 (sub-tile s+1 of this thread)
+      pp[i] += BK;
+      ow_[i] += dr;
+      oh_[i] += dq;
+      if (ow_[i] >= g.Wo) { ow_[i] -= g.Wo; ++oh_[i]; }
+      while (oh_[i] >= g.Ho) { oh_[i] -= g.Ho; ++n_[i]; }
+    }
+#pragma unroll
+    for (int j = 0; j < DMA_B; ++j) {
+      const int p = min(brow[j] + s * BK, P - 1);
+      glds16(bsrc[j] + (long long)p * g.Cout, __builtin_amdgcn_readfirstlane(bbase + ((j * NT + wave * 64) % NBC) * 16));
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NSLOT; ++s)
+    if (s < ns) stage(s, s);
+  wait_barrier<PER_SLOT>(max(min(ns, NSLOT) - 2, 0));
+  s16x8 fa[2][FM], fb[2][FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) fb[0][j] = ld_frag_mn<WB>(smem + OPA, wc * (16 * FN) + j * 16, lane);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) fa[0][i] = ld_frag_mn<32>(smem, wr * (16 * FM) + i * 16, lane);
+  int slot = 0;
+  for (int s = 0; s < ns; s += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int ss = s + u;
+      const int nslot = slot + 1 == NSLOT ? 0 : slot + 1;
+      if (ss + NSLOT < ns) stage(ss + NSLOT, slot);
+      const char* ia = smem + nslot * SLOT;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[u ^ 1][j] = ld_frag_mn<WB>(ia + OPA, wc * (16 * FN) + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[u ^ 1][i] = ld_frag_mn<32>(ia, wr * (16 * FM) + i * 16, lane);
+      if (ss < ns) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma(fb[u][j], fa[u][i], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      wait_barrier<PER_SLOT>(max(min(ns - 1, ss + NSLOT) - (ss + 2), 0));
+      slot = nslot;
+    }
+  }
+
+  const int gq = lane >> 4;
+  float* slab = ws + (long long)blockIdx.z * M * g.Cout;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wr * (16 * FM) + i * 16 + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wc * (16 * FN) + j * 16 + 4 * gq;
+      if (n >= g.Cout) continue;
+      *reinterpret_cast<f32x4*>(slab + (long long)m * g.Cout + n) = acc[i][j];
+    }
+  }
+}
+
+// fp32 slabs [splits][R*S*C][Cout] -> bf16 OIHW filter gradient [Cout][C][R][S], in two passes:
+// (1) groups of WZ slabs summed with float4 loads over the whole grid (a 56x56 layer has hundreds
+//     of slabs: one thread walking all of them per element would be latency bound),
+// (2) the per-group partials summed and written transposed into the OIHW image.
+constexpr int WZ = 16;
+__global__ __launch_bounds__(256) void wgrad_zsum_kernel(const float* __restrict__ ws, float* __restrict__ part,
+                                                         int splits, long long total4) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= total4) return;
+  const int z0 = blockIdx.y * WZ, z1 = min(splits, z0 + WZ);
+  const float4* src = reinterpret_cast<const float4*>(ws) + e;
+  float4 a = src[(long long)z0 * total4];
+  for (int z = z0 + 1; z < z1; ++z) {
+    const float4 b = src[(long long)z * total4];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  reinterpret_cast<float4*>(part)[(long long)blockIdx.y * total4 + e] = a;
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, uint16_t* __restrict__ dw,
+                                                           int ngroups, int RS, int C, int Cout) {
+  const long long total = (long long)RS * C * Cout;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    // e enumerates the slab order (co fastest): coalesced partial reads
+    const int co = (int)(e % Cout);
+    const long long mc = e / Cout;
+    const int c = (int)(mc % C), rs = (int)(mc / C);
+    float v = 0.f;
+    for (int z = 0; z < ngroups; ++z) v += part[(long long)z * total + e];
+    reinterpret_cast<bf16_t*>(dw)[((long long)co * C + c) * RS + rs] = (bf16_t)v;
   }
 }
 
@@ -232,25 +494,176 @@ PA_API int pa_conv2d_fwd_ok(int C, int Cout, int R, int S) {
   return C > 0 && C % 32 == 0 && (R * S * C) % 64 == 0 && Cout > 0 && Cout % 8 == 0;
 }
 
+// waves along the pixel side per Cout tile width (A/B knob; index 0/1/2 = BN 64/128/256)
+static int g_fwd_wm[3] = {4, 4, 2};  // measured: BN 64 and 128 tiles are LDS-read bound at 2(M)x4(N)
+PA_API int pa_conv2d_set_wm(int bn, int wm) {
+  const int k = bn >= 256 ? 2 : (bn >= 128 ? 1 : 0);
+  const int old = g_fwd_wm[k];
+  if (wm == 2 || wm == 4 || wm == 8) g_fwd_wm[k] = wm;
+  return old;
+}
+
+static void launch_fwd_kernel(int BN, dim3 grid, const uint16_t* xp, const uint16_t* wp, uint16_t* yp,
+                              const uint16_t* bp, const Geom& g, const Taps& tp, int M, int K, hipStream_t st) {
+  if (BN == 256) {
+    if (g_fwd_wm[2] == 4) conv_fwd_kernel<256, 4><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    else conv_fwd_kernel<256, 2><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+  } else if (BN == 128) {
+    if (g_fwd_wm[1] == 4) conv_fwd_kernel<128, 4><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    else conv_fwd_kernel<128, 2><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+  } else {
+    if (g_fwd_wm[0] == 4) conv_fwd_kernel<64, 4><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    else if (g_fwd_wm[0] == 8) conv_fwd_kernel<64, 8><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    else conv_fwd_kernel<64, 2><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+  }
+}
+
+static int launch_fwd(const void* x, const void* wpk, void* y, const void* bias, const Geom& g, const Taps& tp,
+                      int ntaps, hipStream_t st) {
+  const long long Mll = (long long)g.N * g.Ho * g.Wo;
+  if (Mll > (1LL << 30) || Mll <= 0) return (int)hipErrorInvalidValue;
+  const int M = (int)Mll, K = ntaps * g.C;
+  const int BN = g.Cout >= 256 ? 256 : (g.Cout > 64 ? 128 : 64);
+  const int tm = (M + BM - 1) / BM, tn = (g.Cout + BN - 1) / BN;
+  const dim3 grid(tm * tn);
+  const uint16_t *xp = (const uint16_t*)x, *wp = (const uint16_t*)wpk, *bp = (const uint16_t*)bias;
+  uint16_t* yp = (uint16_t*)y;
+  launch_fwd_kernel(BN, grid, xp, wp, yp, bp, g, tp, M, K, st);
+  return (int)hipGetLastError();
+}
+
 PA_API int pa_conv2d_fwd(const void* x, const void* wpk, void* y, const void* bias, int N, int H, int W, int C,
                          int Cout, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw, int Ho, int Wo,
                          hipStream_t st) {
-  if (!pa_conv2d_fwd_ok(C, Cout, R, S) || N <= 0 || Ho <= 0 || Wo <= 0) return (int)hipErrorInvalidValue;
+  if (!pa_conv2d_fwd_ok(C, Cout, R, S) || N <= 0 || Ho <= 0 || Wo <= 0 || R * S > MAX_TAPS)
+    return (int)hipErrorInvalidValue;
   Geom g{N, H, W, C, Ho, Wo, Cout, R, S, sh, sw, ph, pw, dh, dw};
-  const long long Mll = (long long)N * Ho * Wo;
-  if (Mll > (1LL << 30)) return (int)hipErrorInvalidValue;
-  const int M = (int)Mll, K = R * S * C;
-  const int BN = Cout >= 256 ? 256 : (Cout > 64 ? 128 : 64);
-  const int tm = (M + BM - 1) / BM, tn = (Cout + BN - 1) / BN;
-  const dim3 grid(tm * tn);
-  if (BN == 256)
-    conv_fwd_kernel<256><<<grid, NT, 0, st>>>((const uint16_t*)x, (const uint16_t*)wpk, (uint16_t*)y,
-                                              (const uint16_t*)bias, g, M, K);
-  else if (BN == 128)
-    conv_fwd_kernel<128><<<grid, NT, 0, st>>>((const uint16_t*)x, (const uint16_t*)wpk, (uint16_t*)y,
-                                              (const uint16_t*)bias, g, M, K);
-  else
-    conv_fwd_kernel<64><<<grid, NT, 0, st>>>((const uint16_t*)x, (const uint16_t*)wpk, (uint16_t*)y,
-                                             (const uint16_t*)bias, g, M, K);
+  Taps tp{};
+  for (int r = 0; r < R; ++r)
+    for (int q = 0; q < S; ++q) {
+      tp.th[r * S + q] = (short)(r * dh - ph);
+      tp.tw[r * S + q] = (short)(q * dw - pw);
+    }
+  tp.oy0 = tp.ox0 = 0;
+  tp.osy = tp.osx = 1;
+  tp.HY = Ho;
+  tp.WY = Wo;
+  tp.ldw = (long long)R * S * C;
+  return launch_fwd(x, wpk, y, bias, g, tp, R * S, st);
+}
+
+// Data gradient of a strided conv, all stride classes in ONE launch.  Class c = (a, b) covers
+// dX[n, a + s_h*i, b + s_w*j, :] and sees T_c filter taps at dY offsets (th, tw):
+//   dX[n, a + s_h*i, b + s_w*j, c] = sum_t sum_co dY[n, i + th[t], j + tw[t], co] * Wd_c[c][t][co].
+// dy: [N, Hd, Wd, Cout] bf16; wd: packed filter [C][sum_c T_c][Cout] (class c's taps at tap0_c);
+// cls: ncls x {a, b, T}; th/tw: the taps of all classes in class order; dx: [N, H, W, C] (pixels of
+// classes without taps are not written — the caller zero-fills when there are any).
+PA_API int pa_conv2d_dgrad_classes(const void* dy, const void* wd, void* dx, int N, int Hd, int Wd, int Cout, int C,
+                                   int H, int W, int s_h, int s_w, int ncls, const int* cls, const int* th,
+                                   const int* tw, hipStream_t st) {
+  if (ncls <= 0 || ncls > MAX_CLS || s_h <= 0 || s_w <= 0 || Cout % 32 || C % 8 || C <= 0)
+    return (int)hipErrorInvalidValue;
+  Geom g{N, Hd, Wd, Cout, 0, 0, C, 1, 1, 1, 1, 0, 0, 1, 1};
+  Taps tp{};
+  tp.osy = s_h;
+  tp.osx = s_w;
+  tp.HY = H;
+  tp.WY = W;
+  const int BN = C >= 256 ? 256 : (C > 64 ? 128 : 64);
+  const int tn = (C + BN - 1) / BN;
+  int tap = 0, blocks = 0, k = 0;
+  long long woff = 0;
+  for (int c = 0; c < ncls; ++c) {
+    const int a = cls[3 * c], b = cls[3 * c + 1], T = cls[3 * c + 2];
+    const int Hc = (H - a + s_h - 1) / s_h, Wc = (W - b + s_w - 1) / s_w;
+    if (T <= 0 || tap + T > MAX_TAPS || Hc <= 0 || Wc <= 0 || (T * Cout) % 64) return (int)hipErrorInvalidValue;
+    for (int t = 0; t < T; ++t) {
+      tp.th[tap + t] = (short)th[tap + t];
+      tp.tw[tap + t] = (short)tw[tap + t];
+    }
+    const long long Mc = (long long)N * Hc * Wc;
+    if (Mc > (1LL << 30)) return (int)hipErrorInvalidValue;
+    blocks += (int)((Mc + BM - 1) / BM) * tn;
+    tp.cls_end[k] = blocks;
+    tp.cls_tap0[k] = tap;
+    tp.cls_T[k] = T;
+    tp.cls_a[k] = a;
+    tp.cls_b[k] = b;
+    tp.cls_Hc[k] = Hc;
+    tp.cls_Wc[k] = Wc;
+    tp.cls_woff[k] = woff;
+    tap += T;
+    woff += (long long)T * Cout;
+    ++k;
+  }
+  tp.ncls = k;
+  tp.ldw = (long long)tap * Cout;
+  const dim3 grid(blocks);
+  const uint16_t *xp = (const uint16_t*)dy, *wp = (const uint16_t*)wd;
+  uint16_t* yp = (uint16_t*)dx;
+  launch_fwd_kernel(BN, grid, xp, wp, yp, nullptr, g, tp, 0, 0, st);
   return (int)hipGetLastError();
+}
+
+static int g_wgrad_bn_cap = 128;  // widest Cout tile (A/B knob)
+static int g_wgrad_wm = 4;        // waves along the (tap, c) side: 2 / 4 (/ 8 for BN = 64)
+PA_API int pa_conv2d_wgrad_set_wm(int v) {
+  const int old = g_wgrad_wm;
+  if (v == 2 || v == 4 || v == 8) g_wgrad_wm = v;
+  return old;
+}
+PA_API int pa_conv2d_wgrad_set_bncap(int v) {
+  const int old = g_wgrad_bn_cap;
+  if (v > 0) g_wgrad_bn_cap = v;
+  return old;
+}
+
+// Filter gradient.  x: bf16 NHWC [N,H,W,C], dy: bf16 NHWC [N,Ho,Wo,Cout], ws: fp32 scratch of
+// (splits + ceil(splits / 16)) * R*S*C * Cout floats (splits = pa_conv2d_wgrad_splits), dw: bf16 [Cout][C][R][S].  C % 8 == 0, Cout % 8 == 0, kchunk % 32 == 0.
+PA_API int pa_conv2d_wgrad_ok(int C, int Cout) { return C > 0 && C % 8 == 0 && Cout > 0 && Cout % 8 == 0; }
+
+PA_API int pa_conv2d_wgrad(const void* x, const void* dy, void* ws, void* dw, int N, int H, int W, int C, int Cout,
+                           int R, int S, int sh, int sw, int ph, int pw, int dh, int dw_, int Ho, int Wo, int splits,
+                           hipStream_t st) {
+  if (!pa_conv2d_wgrad_ok(C, Cout) || N <= 0 || Ho <= 0 || Wo <= 0 || splits <= 0) return (int)hipErrorInvalidValue;
+  const long long Pll = (long long)N * Ho * Wo;
+  if (Pll > (1LL << 30) || (long long)N * H * W * C > (1LL << 40)) return (int)hipErrorInvalidValue;
+  Geom g{N, H, W, C, Ho, Wo, Cout, R, S, sh, sw, ph, pw, dh, dw_};
+  const int P = (int)Pll, M = R * S * C;
+  int kchunk = (int)(((Pll + splits - 1) / splits + 31) / 32 * 32);
+  splits = (P + kchunk - 1) / kchunk;  // no empty split
+  const int BN = (Cout >= 256 && g_wgrad_bn_cap >= 256) ? 256 : (Cout > 64 && g_wgrad_bn_cap >= 128 ? 128 : 64);
+  const int tm = (M + 255) / 256, tn = (Cout + BN - 1) / BN;
+  const dim3 grid(tm * tn, 1, splits);
+  const uint16_t *xp = (const uint16_t*)x, *dp = (const uint16_t*)dy;
+  float* wsp = (float*)ws;
+  if (BN == 256) {
+    if (g_wgrad_wm == 2) conv_wgrad_kernel<256, 2><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
+    else conv_wgrad_kernel<256, 4><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
+  } else if (BN == 128) {
+    if (g_wgrad_wm == 2) conv_wgrad_kernel<128, 2><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
+    else conv_wgrad_kernel<128, 4><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
+  } else {
+    if (g_wgrad_wm == 2) conv_wgrad_kernel<64, 2><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
+    else if (g_wgrad_wm == 8) conv_wgrad_kernel<64, 8><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
+    else conv_wgrad_kernel<64, 4><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const long long total = (long long)M * Cout;  // Cout % 8 == 0: float4 groups never straddle a row
+  const int ngroups = (splits + WZ - 1) / WZ;
+  float* part = (float*)ws + (long long)splits * total;  // scratch tail: ngroups x total
+  const dim3 zgrid((unsigned)((total / 4 + 255) / 256), ngroups);
+  wgrad_zsum_kernel<<<zgrid, 256, 0, st>>>((const float*)ws, part, splits, total / 4);
+  const long long nb = (total + 255) / 256;
+  const int blocks = (int)(nb < 2048 ? nb : 2048);
+  wgrad_reduce_kernel<<<blocks, 256, 0, st>>>(part, (uint16_t*)dw, ngroups, R * S, C, Cout);
+  return (int)hipGetLastError();
+}
+
+// the split count pa_conv2d_wgrad will actually use (scratch sizing)
+PA_API int pa_conv2d_wgrad_splits(int N, int Ho, int Wo, int splits) {
+  const long long P = (long long)N * Ho * Wo;
+  const long long kchunk = ((P + splits - 1) / splits + 31) / 32 * 32;
+  return (int)((P + kchunk - 1) / kchunk);
 }

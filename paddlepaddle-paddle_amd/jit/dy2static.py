@@ -89,15 +89,17 @@ def _static_cond(pred, true_fn, false_fn, args, names, is_return):
     def as_tensor(v, like=None):
         with _paused():
             if like is not None and (v is UNDEFINED or v is None):
-                return torch.zeros(like.shape, dtype=like.dtype)
+                # placeholder for a variable the branch does not define: never read on that branch,
+                # so a scalar suffices (the node output takes the defined side's meta)
+                return torch.zeros((), dtype=like.dtype)
             if like is not None:
                 return torch.tensor(v, dtype=like.dtype)
             return torch.tensor(v)
 
-    def slot(ta, tb):
+    def slot(ta, tb, like=None):
         t_refs.append(_to_record(prog, ta))
         f_refs.append(_to_record(prog, tb))
-        m = _meta_like(ta)
+        m = _meta_like(ta if like is None else like)
         outs.append(prog._new_value(m))
         return _wrap(m)
 
@@ -116,9 +118,9 @@ def _static_cond(pred, true_fn, false_fn, args, names, is_return):
             return slot(ta, tb)
         num = (bool, int, float)
         if a_t and (isinstance(b, num) or b is UNDEFINED or b is None):
-            return slot(ta, as_tensor(b, ta))
+            return slot(ta, as_tensor(b, ta), ta)
         if b_t and (isinstance(a, num) or a is UNDEFINED or a is None):
-            return slot(as_tensor(a, tb), tb)
+            return slot(as_tensor(a, tb), tb, tb)
         if isinstance(a, num) and isinstance(b, num):
             if a == b and type(a) is type(b):
                 return a

@@ -66,6 +66,13 @@ _SIGS = {
     'pa_gemm_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
     'pa_conv2d_fwd_ok': [I, I, I, I],
     'pa_conv2d_fwd': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
+    'pa_conv2d_wgrad_ok': [I, I],
+    'pa_conv2d_dgrad_classes': [P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
+    'pa_conv2d_wgrad': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
+    'pa_conv2d_wgrad_splits': [I, I, I, I],
+    'pa_conv2d_wgrad_set_bncap': [I],
+    'pa_conv2d_wgrad_set_wm': [I],
+    'pa_conv2d_set_wm': [I, I],
     'pa_gemm_ok': [I, I, I, LL, LL, LL, I],
     'pa_gemm8_ok': [I, I, I, LL, LL, LL, I, I, I],
     'pa_gemm8_set_wide_epi': [I],

@@ -1,12 +1,17 @@
-"""NHWC conv2d forward on the hand-written implicit-GEMM MFMA kernel (csrc/conv.hip).
+"""NHWC conv2d on hand-written implicit-GEMM MFMA kernels (csrc/conv.hip), forward and backward.
 
 Reference: paddle/phi/kernels/gpudnn/conv_kernel.cu (forward), conv_grad_kernel.cu (backward).
-Forward runs csrc/conv.hip (im2col folded into the LDS-DMA source addresses, zero padding via a
-zero block, bias fused); the weight is packed into the [Cout][R][S][C]
-k-contiguous image the kernel stages (re-packed per call).  Backward: the stride-1 data gradient is the same kernel
-run on dY with the flipped, transposed filter; the 1x1 filter gradient is the hand-written GEMM
-(dY^T X, split-K over pixels); strided data gradients and k>1 filter gradients use the storage
-layer's convolution backward (MIOpen NHWC kernels).
+* Forward: im2col folded into the LDS-DMA source addresses, zero padding via a zero block, bias
+  fused; the weight is packed into the [Cout][R][S][C] k-contiguous image the kernel stages
+  (re-packed per call).  Needs C % 32 == 0; the 3-channel stem forward runs on the storage
+  layer's convolution (its backward still comes here).
+* Data gradient (any stride): stride classes of input pixels, each a stride-1 implicit GEMM over
+  dY with the taps that reach it, all classes in one launch (pa_conv2d_dgrad_classes).
+* Filter gradient (any R x S / stride / padding): implicit GEMM with the pixels as the reduction
+  axis, split over the grid (pa_conv2d_wgrad); inputs with C % 8 != 0 (the stem) are zero-padded
+  to 8 channels for it.
+The storage layer's convolution backward (MIOpen) remains only as the fallback for shapes the
+kernels reject (grouped / odd channel counts) or when PADDLE_AMD_HIP_CONV_BWD=0.
 """
 import os
 
@@ -16,9 +21,12 @@ from . import _native as N
 
 _enabled = os.environ.get('PADDLE_AMD_HIP_CONV', '1') != '0'
 _bwd_enabled = os.environ.get('PADDLE_AMD_HIP_CONV_BWD', '1') != '0'
+_wgrad_hip = os.environ.get('PADDLE_AMD_HIP_CONV_WGRAD', '1') != '0'
 
 
 def supported(x, w, groups):
+    """The conv runs through _Conv2dNHWC: a hand-written forward, or (small C, e.g. the RGB stem)
+    the library forward with the hand-written backward."""
     if not _enabled or groups != 1 or x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
         return False
     if x.dim() != 4 or w.dim() != 4 or not x.is_cuda:
@@ -26,7 +34,14 @@ def supported(x, w, groups):
     if N.lib is None and N._load() is None:
         return False
     Cout, C, R, S = w.shape
-    return x.shape[3] == C and bool(N.lib.pa_conv2d_fwd_ok(C, Cout, R, S))
+    if x.shape[3] != C:
+        return False
+    return bool(N.lib.pa_conv2d_fwd_ok(C, Cout, R, S)) or (_bwd_enabled and Cout % 8 == 0 and C < 8)
+
+
+def fwd_ok(w):
+    Cout, C, R, S = w.shape
+    return bool(N.lib.pa_conv2d_fwd_ok(C, Cout, R, S))
 
 
 def _packed(w):
@@ -60,19 +75,6 @@ def conv2d_fwd(x, w, b, stride, pad, dil):
     return _fwd_packed(x, _packed(w), b, stride, pad, dil)
 
 
-def _bwd_wins(dy, x):
-    """Where the hand-written backward beat MIOpen's NHWC backward on MI355X (tools/conv_bench.py,
-    ResNet50 shapes at batch 256): small spatial extents, or 28x28 maps with >= 256 input
-    channels.  The 56x56 / narrow-channel layers stay on MIOpen."""
-    pix = dy.shape[1] * dy.shape[2]
-    return pix <= 196 or (pix <= 784 and x.shape[3] >= 256)
-
-
-def _dgrad_ok(w, stride):
-    Cout, C, R, S = w.shape
-    return _bwd_enabled and tuple(stride) == (1, 1) and bool(N.lib.pa_conv2d_fwd_ok(Cout, C, R, S))
-
-
 def conv2d_dgrad(dy, w, x_hw, pad, dil):
     """Stride-1 data gradient as a forward conv of dy with the spatially flipped, transposed
     filter ([C][R][S][Cout] image) and padding dil*(R-1) - pad (same kernel as the forward)."""
@@ -83,6 +85,69 @@ def conv2d_dgrad(dy, w, x_hw, pad, dil):
         return None
     gx = _fwd_packed(dy, wpk, None, (1, 1), p2, dil)
     return gx if tuple(gx.shape[1:3]) == tuple(x_hw) else None
+
+
+_DGRAD_PLANS = {}
+
+
+def _dgrad_plan(w_shape, x_hw, stride, pad, dil, device):
+    """Stride classes of a data gradient (cached per geometry): ((a, b, T) per class, tap order,
+    dY offsets, whether some input pixels get no tap (zero fill))."""
+    import ctypes
+    key = (tuple(w_shape), tuple(x_hw), tuple(stride), tuple(pad), tuple(dil), str(device))
+    plan = _DGRAD_PLANS.get(key)
+    if plan is not None:
+        return plan
+    Cout, C, R, S = w_shape
+    H, W = x_hw
+    sh, sw = stride
+    classes, empty = [], False
+    for a in range(sh):
+        for b in range(sw):
+            if H - a <= 0 or W - b <= 0:
+                continue
+            taps = [(r * S + q, (a + pad[0] - r * dil[0]) // sh, (b + pad[1] - q * dil[1]) // sw)
+                    for r in range(R) if (a + pad[0] - r * dil[0]) % sh == 0
+                    for q in range(S) if (b + pad[1] - q * dil[1]) % sw == 0]
+            if taps:
+                classes.append((a, b, taps))
+            else:
+                empty = True
+    flat = [t for _, _, taps in classes for t in taps]
+    ok = (0 < len(classes) <= 9 and len(flat) <= 64 and Cout % 32 == 0 and C % 8 == 0
+          and all((len(t) * Cout) % 64 == 0 for _, _, t in classes))
+    order = [t[0] for t in flat]
+    idx = None if order == list(range(R * S)) else torch.tensor(order, device=device)
+    cls = (ctypes.c_int * (3 * max(1, len(classes))))(*[v for a, b, taps in classes for v in (a, b, len(taps))])
+    th = (ctypes.c_int * max(1, len(flat)))(*[t[1] for t in flat])
+    tw = (ctypes.c_int * max(1, len(flat)))(*[t[2] for t in flat])
+    plan = (ok, len(classes), idx, empty, cls, th, tw)
+    _DGRAD_PLANS[key] = plan
+    return plan
+
+
+def conv2d_dgrad_classes(dy, w, x_hw, stride, pad, dil):
+    """Data gradient of any stride: dX splits into stride_h x stride_w classes of input pixels
+    (ih = a + s_h*i, iw = b + s_w*j); each class only sees the filter taps with
+    (a + pad - r*dil) % s == 0, at dY offset (a + pad - r*dil) / s — a stride-1 implicit GEMM over dY
+    with a subset of taps whose output lands on every s-th pixel; all classes run in one launch
+    (csrc/conv.hip pa_conv2d_dgrad_classes).  Stride 1 is the single class with every tap."""
+    import ctypes
+    Cout, C, R, S = w.shape
+    H, W = x_hw
+    ok, ncls, idx, empty, cls, th, tw = _dgrad_plan(w.shape, x_hw, stride, pad, dil, dy.device)
+    if not ok:
+        return None
+    dy = dy.contiguous()
+    Nb, Hd, Wd, _ = dy.shape
+    wt = w.detach().to(torch.bfloat16).permute(1, 2, 3, 0).reshape(C, R * S, Cout)
+    wd = (wt if idx is None else wt.index_select(1, idx)).contiguous()  # [C][taps in class order][Cout]
+    dx = (torch.zeros if empty else torch.empty)(Nb, H, W, C, dtype=torch.bfloat16, device=dy.device)
+    vp = lambda arr: ctypes.cast(arr, ctypes.c_void_p)  # noqa: E731
+    N.check(N.lib.pa_conv2d_dgrad_classes(N.ptr(dy), N.ptr(wd), N.ptr(dx), Nb, Hd, Wd, Cout, C, H, W, stride[0],
+                                          stride[1], ncls, vp(cls), vp(th), vp(tw), N.stream()),
+            'conv2d_dgrad_classes')
+    return dx
 
 
 def conv2d_wgrad_1x1(dy, x):
@@ -101,12 +166,52 @@ def conv2d_wgrad_1x1(dy, x):
     return gemm.hip_mm(a, x2, splitk=sk).view(Cout, C, 1, 1)
 
 
+_WGRAD_TARGET_BLOCKS = 512  # two waves of 256 CUs over (tiles x pixel splits)
+
+
+def wgrad_ok(x, w):
+    Cout, C = w.shape[0], w.shape[1]
+    return _bwd_enabled and bool(N.lib.pa_conv2d_wgrad_ok(C, Cout))
+
+
+def conv2d_wgrad(dy, x, w_shape, stride, pad, dil):
+    """Filter gradient of any R x S / stride / padding / dilation on the implicit-GEMM kernel
+    (pixels are the reduction axis, split over the grid; fp32 slabs folded into the OIHW bf16
+    gradient by a second kernel)."""
+    Cout, C, R, S = w_shape
+    x, dy = x.contiguous(), dy.contiguous()
+    if R == S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0) and C < Cout and Cout % 8 == 0:
+        # 1x1: dW = dY^T X is symmetric in (X, dY) — put the wider channel count on the 256-wide
+        # tile side (a 64-channel input would leave 3/4 of every 256-row tile empty)
+        return conv2d_wgrad(x, dy, (C, Cout, 1, 1), stride, pad, dil).view(C, Cout).t().contiguous().view(Cout, C, 1, 1)
+    Nb, H, W, _ = x.shape
+    _, Ho, Wo, _ = dy.shape
+    M = R * S * C
+    bn = 64 if Cout <= 64 else 128
+    tiles = -(-M // 256) * -(-Cout // bn)
+    P = Nb * Ho * Wo
+    want = max(1, min(_WGRAD_TARGET_BLOCKS // tiles, P // 512))
+    splits = int(N.lib.pa_conv2d_wgrad_splits(Nb, Ho, Wo, want))
+    ws = torch.empty((splits + -(-splits // 16)) * M * Cout, dtype=torch.float32, device=x.device)
+    dw = torch.empty(Cout, C, R, S, dtype=torch.bfloat16, device=x.device)
+    N.check(N.lib.pa_conv2d_wgrad(N.ptr(x), N.ptr(dy), N.ptr(ws), N.ptr(dw), Nb, H, W, C, Cout, R, S, stride[0],
+                                  stride[1], pad[0], pad[1], dil[0], dil[1], Ho, Wo, want, N.stream()), 'conv2d_wgrad')
+    return dw
+
+
+def _lib_conv_fwd(x, w, b, stride, pad, dil):
+    y = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w, b, stride, pad, dil)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, stride, pad, dil):
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, dil, b is not None)
-        return conv2d_fwd(x, w, b, stride, pad, dil)
+        if fwd_ok(w):
+            return conv2d_fwd(x, w, b, stride, pad, dil)
+        return _lib_conv_fwd(x, w, b, stride, pad, dil)
 
     @staticmethod
     def backward(ctx, dy):
@@ -114,17 +219,21 @@ class _Conv2dNHWC(torch.autograd.Function):
         stride, pad, dil, has_b = ctx.cfg
         dy = dy.contiguous()
         gx = gw = gb = None
-        dy_bwd_hip = _bwd_wins(dy, x)
-        if ctx.needs_input_grad[0] and dy_bwd_hip and _dgrad_ok(w, stride):
-            gx = conv2d_dgrad(dy, w, x.shape[1:3], pad, dil)
-        if (ctx.needs_input_grad[1] and dy_bwd_hip and _bwd_enabled and w.shape[2] == w.shape[3] == 1
-                and tuple(stride) == (1, 1) and tuple(pad) == (0, 0)):
-            gw = conv2d_wgrad_1x1(dy, x)
-            gw = gw.to(w.dtype) if gw is not None else None
+        if ctx.needs_input_grad[0] and _bwd_enabled:
+            gx = conv2d_dgrad_classes(dy, w, x.shape[1:3], stride, pad, dil)
+        if ctx.needs_input_grad[1] and _bwd_enabled and _wgrad_hip and w.shape[0] % 8 == 0:
+            C = w.shape[1]
+            if C % 8:  # RGB stem: zero channels do not change the taps of the real ones
+                xp = torch.nn.functional.pad(x, (0, 8 - C % 8))
+                gw = conv2d_wgrad(dy, xp, (w.shape[0], xp.shape[3], w.shape[2], w.shape[3]), stride, pad,
+                                  dil)[:, :C].contiguous()
+            else:
+                gw = conv2d_wgrad(dy, x, tuple(w.shape), stride, pad, dil)
+            gw = gw.to(w.dtype)
         if has_b and ctx.needs_input_grad[2]:
             gb = dy.sum((0, 1, 2), dtype=torch.float32).to(dy.dtype)
         mask = [ctx.needs_input_grad[0] and gx is None, ctx.needs_input_grad[1] and gw is None, False]
-        if any(mask):  # what the hand-written kernels do not cover: MIOpen NHWC backward
+        if any(mask):  # shapes the hand-written kernels reject: MIOpen NHWC backward
             lx, lw, _ = torch.ops.aten.convolution_backward(
                 dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), w, None, list(stride), list(pad), list(dil), False,
                 [0, 0], 1, mask)

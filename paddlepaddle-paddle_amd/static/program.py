@@ -5,7 +5,7 @@ Design: a ``Program`` is a recorded op list (a small IR), not a protobuf desc.  
 mode is on, a ``TorchFunctionMode`` records every tensor operation whose inputs derive from a
 static ``Variable``.  Variables carry *meta* tensors (shape/dtype only, no memory), so building
 a program for a 1.3B model costs nothing.  Dynamic dims (``None``/-1) are given sentinel
-extents (large primes, one per dim position); integer arguments built from them (``B*S``,
+extents (primes just below 2^20, one per dim position); integer arguments built from them (``B*S``,
 ``arange(S)``) are re-specialised at run time by factoring the sentinels out — so user code
 that reads ``x.shape`` and reshapes still runs at any feed shape.
 
@@ -22,8 +22,11 @@ from torch.overrides import TorchFunctionMode
 
 from ..core.tensor import Tensor, _wrap
 
-# one sentinel extent per dynamic-dim position (dim 0 = batch, dim 1 = sequence, ...)
-SENTINELS = (9973, 9967, 9949, 9941, 9931, 9929)
+# one sentinel extent per dynamic-dim position (dim 0 = batch, dim 1 = sequence, ...): the six
+# largest primes below 2^20, so an unrelated recorded integer is a multiple of one with odds of
+# about 1e-6 (meta tensors hold no memory, so the large extents cost nothing; three dynamic dims
+# times a 10^4 feature dim stay far inside int64 numel)
+SENTINELS = (1048573, 1048571, 1048559, 1048549, 1048517, 1048507)
 _SENT_SET = set(SENTINELS)
 
 

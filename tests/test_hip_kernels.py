@@ -798,13 +798,69 @@ def test_hip_conv2d_nhwc(N, H, W, C, Cout, R, stride, pad, dil):
     w = (torch.rand(Cout, C, R, R, device=DEV, generator=g) * 2 - 1).mul(0.1).bfloat16().requires_grad_()
     b = torch.rand(Cout, device=DEV, generator=g).bfloat16().requires_grad_()
     assert conv.supported(x, w, 1)
-    old = conv._bwd_wins
-    conv._bwd_wins = lambda dy, x: True  # exercise the hand-written backward paths on every shape
-    try:
-        y = conv.conv2d_nhwc(x, w, b, (stride, stride), (pad, pad), (dil, dil))
-        _conv_check(y, x, w, b, N, C, Cout, R, stride, pad, dil)
-    finally:
-        conv._bwd_wins = old
+    y = conv.conv2d_nhwc(x, w, b, (stride, stride), (pad, pad), (dil, dil))
+    _conv_check(y, x, w, b, N, C, Cout, R, stride, pad, dil)
+
+
+def test_hip_conv_backward_skips_the_library(monkeypatch):
+    """The ResNet conv shapes (strided 3x3 / 1x1, the RGB stem) never reach MIOpen's backward."""
+    from paddle.ops import conv
+
+    def boom(*a, **k):
+        raise AssertionError("library convolution_backward called")
+    monkeypatch.setattr(torch.ops.aten, 'convolution_backward', boom)
+    for (C, Cout, R, s, p) in [(3, 64, 7, 2, 3), (64, 64, 3, 1, 1), (128, 128, 3, 2, 1), (256, 512, 1, 2, 0)]:
+        x = torch.randn(2, 20, 20, C, device=DEV).bfloat16().requires_grad_(C != 3)
+        w = (torch.randn(Cout, C, R, R, device=DEV) * 0.05).bfloat16().requires_grad_()
+        assert conv.supported(x, w, 1)
+        y = conv.conv2d_nhwc(x, w, None, (s, s), (p, p), (1, 1))
+        y.float().square().sum().backward()
+        xr, wr = x.detach().float().requires_grad_(C != 3), w.detach().float().requires_grad_()
+        yr = torch.nn.functional.conv2d(xr.permute(0, 3, 1, 2), wr, None, s, p)
+        yr.square().sum().backward()
+        _close(w.grad, wr.grad, atol=2.0, rtol=0.03, name=f'dw C{C}')
+        if C != 3:
+            _close(x.grad, xr.grad, atol=0.5, rtol=0.03, name=f'dx C{C}')
+
+
+@pytest.mark.parametrize("N,H,W,C,Cout,R,S,stride,pad,dil", [
+    (4, 56, 56, 64, 64, 3, 3, 1, 1, 1), (3, 29, 31, 128, 128, 3, 3, 2, 1, 1), (2, 16, 16, 256, 64, 1, 1, 2, 0, 1),
+    (2, 40, 40, 8, 64, 7, 7, 2, 3, 1), (1, 11, 13, 64, 200, 3, 5, 1, 2, 2), (5, 7, 7, 512, 512, 3, 3, 1, 1, 1)])
+def test_hip_conv2d_wgrad(N, H, W, C, Cout, R, S, stride, pad, dil):
+    """csrc/conv.hip implicit-GEMM filter gradient (pixels split over the grid) vs fp32."""
+    from paddle.ops import conv
+    g = torch.Generator(device=DEV).manual_seed(C * R + Cout)
+    x = (torch.rand(N, H, W, C, device=DEV, generator=g) * 2 - 1).bfloat16()
+    w_shape = (Cout, C, R, S)
+    Ho = (H + 2 * pad - dil * (R - 1) - 1) // stride + 1
+    Wo = (W + 2 * pad - dil * (S - 1) - 1) // stride + 1
+    dy = torch.randn(N, Ho, Wo, Cout, device=DEV, generator=g).bfloat16()
+    dw = conv.conv2d_wgrad(dy, x, w_shape, (stride, stride), (pad, pad), (dil, dil))
+    ref = torch.ops.aten.convolution_backward(
+        dy.float().permute(0, 3, 1, 2), x.float().permute(0, 3, 1, 2), torch.zeros(w_shape, device=DEV), None,
+        [stride, stride], [pad, pad], [dil, dil], False, [0, 0], 1, [False, True, False])[1]
+    assert dw.shape == ref.shape and dw.dtype == torch.bfloat16
+    _close(dw, ref, atol=0.02 * math.sqrt(N * Ho * Wo) / 8 + 0.02, rtol=0.01, name='conv wgrad')
+
+
+@pytest.mark.parametrize("N,H,W,C,Cout,R,stride,pad,dil", [
+    (2, 56, 56, 128, 128, 3, 2, 1, 1), (3, 15, 13, 64, 256, 3, 2, 1, 1), (2, 28, 28, 256, 512, 1, 2, 0, 1),
+    (2, 14, 14, 64, 64, 3, 1, 1, 1), (1, 17, 19, 64, 128, 3, 2, 2, 2), (2, 12, 12, 96, 64, 2, 2, 0, 1),
+    (1, 10, 10, 64, 128, 5, 3, 2, 1)])
+def test_hip_conv2d_dgrad_classes(N, H, W, C, Cout, R, stride, pad, dil):
+    """Strided data gradient as stride classes on the implicit-GEMM kernel vs fp32."""
+    from paddle.ops import conv
+    g = torch.Generator(device=DEV).manual_seed(C * R + Cout + stride)
+    w = ((torch.rand(Cout, C, R, R, device=DEV, generator=g) * 2 - 1) * 0.1).bfloat16()
+    Ho = (H + 2 * pad - dil * (R - 1) - 1) // stride + 1
+    Wo = (W + 2 * pad - dil * (R - 1) - 1) // stride + 1
+    dy = torch.randn(N, Ho, Wo, Cout, device=DEV, generator=g).bfloat16()
+    dx = conv.conv2d_dgrad_classes(dy, w, (H, W), (stride, stride), (pad, pad), (dil, dil))
+    ref = torch.ops.aten.convolution_backward(
+        dy.float().permute(0, 3, 1, 2), torch.zeros(N, C, H, W, device=DEV), w.float(), None, [stride, stride],
+        [pad, pad], [dil, dil], False, [0, 0], 1, [True, False, False])[0].permute(0, 2, 3, 1)
+    assert dx is not None and dx.shape == ref.shape
+    _close(dx, ref, atol=0.05 * math.sqrt(Cout * R * R) / 8 + 0.05, rtol=0.02, name='conv dgrad classes')
 
 
 def _conv_check(y, x, w, b, N, C, Cout, R, stride, pad, dil):

@@ -9,7 +9,8 @@ from paddle import ops
 def test_op_entry_points_exist():
     for mod, names in [(ops.gemm, ['hip_mm', 'hip_mm_ok', 'wgrad_accumulate', 'hip_fp8_ok', 'hip_fp8_mm',
                                    'fp8_quantize', 'fp8_gemm']),
-                       (ops.conv, ['supported', 'conv2d_fwd', 'conv2d_nhwc', 'conv2d_dgrad', 'conv2d_wgrad_1x1']),
+                       (ops.conv, ['supported', 'conv2d_fwd', 'conv2d_nhwc', 'conv2d_dgrad', 'conv2d_dgrad_classes',
+                                   'conv2d_wgrad', 'conv2d_wgrad_1x1']),
                        (ops.flash_attn, ['flash_attention', 'flash_attention_packed', 'supported'])]:
         for n in names:
             assert hasattr(mod, n), f"{mod.__name__}.{n} missing"

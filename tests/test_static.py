@@ -50,6 +50,21 @@ def test_static_reshape_with_dynamic_dims(static_mode):
     assert nv.tolist() == [0, 1, 2]
 
 
+def test_static_constants_are_not_taken_for_dynamic_dims(static_mode):
+    """Integers in a program that share a factor with small dynamic-dim sentinels (19946 = 2 * 9973,
+    the round-1 batch sentinel) must run unchanged at any feed shape."""
+    main = static.Program()
+    with static.program_guard(main):
+        x = static.data('x', [None, 4], 'float32')
+        n = paddle.arange(0, 19946).sum()
+        y = x.sum() + paddle.ones([9967 * 2, 1]).sum()
+    exe = static.Executor(paddle.CPUPlace())
+    a = np.ones((3, 4), 'float32')
+    nv, yv = exe.run(main, feed={'x': a}, fetch_list=[n, y])
+    assert int(nv) == 19946 * 19945 // 2
+    assert float(yv) == 12.0 + 9967 * 2
+
+
 def test_static_cond_and_while(static_mode):
     main = static.Program()
     with static.program_guard(main):

@@ -31,7 +31,14 @@ def main():
         (28, 512, 256, 1, 1), (28, 256, 256, 3, 2), (14, 256, 1024, 1, 1), (14, 1024, 256, 1, 1),
         (14, 256, 256, 3, 1), (14, 1024, 512, 1, 1), (14, 512, 512, 3, 2), (7, 512, 2048, 1, 1), (7, 2048, 512, 1, 1),
         (7, 512, 512, 3, 1)]
-    tot_h = tot_l = tot_bh = tot_bl = 0.0
+    tot_h = tot_l = tot_bh = tot_bl = tot_wl = tot_wh = tot_dl = tot_dh = 0.0
+    if len(sys.argv) > 1:
+        _native.lib.pa_conv2d_wgrad_set_bncap(int(sys.argv[1]))
+    if len(sys.argv) > 2:
+        _native.lib.pa_conv2d_wgrad_set_wm(int(sys.argv[2]))
+    for i, bn in enumerate((64, 128, 256)):  # forward / data-gradient wave layout per Cout tile width
+        if len(sys.argv) > 3 + i:
+            _native.lib.pa_conv2d_set_wm(bn, int(sys.argv[3 + i]))
     for H, C, Cout, R, s in shapes:
         p = R // 2
         x = torch.randn(B, H, H, C, device='cuda', dtype=torch.bfloat16)
@@ -55,10 +62,25 @@ def main():
         tbh = bench(lambda: torch.autograd.grad(yy, (xg, wg), dy, retain_graph=True))
         tot_bh += tbh
         tot_bl += tbl
+        twl = bench(lambda: torch.ops.aten.convolution_backward(dyc, xc, w, None, [s, s], [p, p], [1, 1], False,
+                                                                [0, 0], 1, [False, True, False]))
+        twh = bench(lambda: conv.conv2d_wgrad(dy, x, tuple(w.shape), (s, s), (p, p), (1, 1)))
+        tdl = bench(lambda: torch.ops.aten.convolution_backward(dyc, xc, w, None, [s, s], [p, p], [1, 1], False,
+                                                                [0, 0], 1, [True, False, False]))
+        tdh = bench(lambda: conv.conv2d_dgrad_classes(dy, w, (H, H), (s, s), (p, p), (1, 1)))
+        tot_dl += tdl
+        tot_dh += tdh
+        print(f"   dgrad MIOpen {tdl*1e6:7.1f} us {fl/tdl/1e12:4.0f} TF | hip {tdh*1e6:7.1f} us {fl/tdh/1e12:4.0f} TF",
+              flush=True)
+        tot_wl += twl
+        tot_wh += twh
+        print(f"   wgrad MIOpen {twl*1e6:7.1f} us {fl/twl/1e12:4.0f} TF | hip {twh*1e6:7.1f} us {fl/twh/1e12:4.0f} TF",
+              flush=True)
         print(f"H{H} C{C} Cout{Cout} R{R} s{s}: fwd MIOpen {tl*1e6:7.1f} us {fl/tl/1e12:4.0f} TF | hip {th*1e6:7.1f} us "
               f"{fl/th/1e12:4.0f} TF || bwd MIOpen {tbl*1e6:7.1f} us | ours {tbh*1e6:7.1f} us", flush=True)
     print(f"sum over shapes: fwd MIOpen {tot_l*1e3:.2f} ms, hip {tot_h*1e3:.2f} ms; bwd MIOpen {tot_bl*1e3:.2f} ms, "
-          f"ours {tot_bh*1e3:.2f} ms", flush=True)
+          f"ours {tot_bh*1e3:.2f} ms; wgrad MIOpen {tot_wl*1e3:.2f} ms, hip {tot_wh*1e3:.2f} ms; "
+          f"dgrad MIOpen {tot_dl*1e3:.2f} ms, hip {tot_dh*1e3:.2f} ms", flush=True)
 
 
 if __name__ == '__main__':
