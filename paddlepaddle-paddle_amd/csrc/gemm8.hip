@@ -954,8 +954,10 @@ __global__ __launch_bounds__(512, 1) void gemm12_kernel(const char* __restrict__
       item_coords(item_of(j), splitk, tm, tn, ksplit, m0, n0, kb, z);
       if constexpr (EPI == 1)
         epilogue_z<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane, z);
+      else if (g_wide_epi)
+        epilogue_wide<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
       else
-        epilogue_z<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane, 0);
+        epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -969,6 +971,7 @@ __global__ __launch_bounds__(512, 1) void gemm12_kernel(const char* __restrict__
 
 
 static int g_sched = 9;
+static int g_epi_sched = 11;  // schedule of the fused-epilogue MLP GEMMs (11 or 12)
 
 template <bool AK, bool BKM, int EPI>
 static hipError_t launch(const void* A, const void* B, void* C, float* ws, const void* bias, int M, int N, int K,
@@ -1013,6 +1016,17 @@ static hipError_t launch_epi(int transB, const void* A, const void* B, void* C, 
                              int N, int K, long long lda, long long ldb, long long ldc, float alpha, hipStream_t st) {
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   dim3 grid(tm * tn, 1, 1);
+  if (g_epi_sched == 12) {  // persistent: the epilogue overlaps the next tile's staging
+    const int items = tm * tn;
+    const int g = items >= 256 ? 256 : (items + 7) / 8 * 8;
+    if (transB)
+      gemm12_kernel<true, true, EPI><<<g, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, (float*)aux,
+                                                        (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, 0.f, K, 1);
+    else
+      gemm12_kernel<true, false, EPI><<<g, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, (float*)aux,
+                                                         (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, 0.f, K, 1);
+    return hipGetLastError();
+  }
   if (transB)
     gemm11_kernel<true, true, EPI><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, (float*)aux,
                                                          (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, 0.f, K);
@@ -1078,5 +1092,12 @@ PA_API int pa_gemm8_set_wide_epi(int v) {
 PA_API int pa_gemm8_set_sched(int v) {
   const int old = pa::g8::g_sched;
   pa::g8::g_sched = v;
+  return old;
+}
+
+// schedule of the fused-epilogue GEMMs (pa_gemm8_bf16_epi): 11 (default) or 12 (persistent)
+PA_API int pa_gemm8_set_epi_sched(int v) {
+  const int old = pa::g8::g_epi_sched;
+  pa::g8::g_epi_sched = v == 12 ? 12 : 11;
   return old;
 }

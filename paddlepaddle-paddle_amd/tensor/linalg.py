@@ -213,6 +213,12 @@ def corrcoef(x, rowvar=True, name=None):
     return _w(torch.corrcoef(t if rowvar else t.t()))
 
 
+def ormqr(x, tau, y, left=True, transpose=False, name=None):
+    """op(Q) @ y (left) or y @ op(Q), Q the product of the Householder reflectors (x, tau) of a QR
+    factorisation, op = transpose (conjugate) when ``transpose`` (reference tensor/linalg.py:5051)."""
+    return _w(torch.ormqr(_u(x), _u(tau), _u(y), left=left, transpose=transpose))
+
+
 def householder_product(x, tau, name=None):
     return _w(torch.linalg.householder_product(_u(x), _u(tau)))
 

@@ -6,5 +6,5 @@ from .resnet import (ResNet, BasicBlock, BottleneckBlock, resnet18, resnet34, re
 from .zoo import (VGG, vgg11, vgg13, vgg16, vgg19, AlexNet, alexnet, MobileNetV1, MobileNetV2, MobileNetV3Small,  # noqa: F401
                   MobileNetV3Large, mobilenet_v1, mobilenet_v2, mobilenet_v3_small, mobilenet_v3_large, SqueezeNet,
                   squeezenet1_0, squeezenet1_1, ShuffleNetV2, shufflenet_v2_x0_5, shufflenet_v2_x1_0,
-                  shufflenet_v2_x2_0, DenseNet, densenet121, densenet161, densenet169, densenet201, densenet264,
+                  shufflenet_v2_x2_0, shufflenet_v2_x0_25, shufflenet_v2_x0_33, shufflenet_v2_x1_5, shufflenet_v2_swish, DenseNet, densenet121, densenet161, densenet169, densenet201, densenet264,
                   GoogLeNet, googlenet, InceptionV3, inception_v3)

@@ -114,7 +114,8 @@ class ConvBNLayer(nn.Layer):
         super().__init__()
         self.conv = nn.Conv2D(cin, cout, k, stride=stride, padding=padding, groups=groups, bias_attr=False)
         self.bn = nn.BatchNorm2D(cout)
-        self.act = {'relu': nn.ReLU(), 'relu6': nn.ReLU6(), 'hardswish': nn.Hardswish(), None: None}[act]
+        self.act = {'relu': nn.ReLU(), 'relu6': nn.ReLU6(), 'hardswish': nn.Hardswish(), 'swish': nn.Swish(),
+                    None: None}[act]
 
     def forward(self, x):
         x = self.bn(self.conv(x))
@@ -412,6 +413,27 @@ def shufflenet_v2_x0_5(pretrained=False, **kw):
 def shufflenet_v2_x2_0(pretrained=False, **kw):
     _no_pretrained(pretrained)
     return ShuffleNetV2(2.0, **kw)
+
+
+def shufflenet_v2_x0_25(pretrained=False, **kw):
+    _no_pretrained(pretrained)
+    return ShuffleNetV2(0.25, **kw)
+
+
+def shufflenet_v2_x0_33(pretrained=False, **kw):
+    _no_pretrained(pretrained)
+    return ShuffleNetV2(0.33, **kw)
+
+
+def shufflenet_v2_x1_5(pretrained=False, **kw):
+    _no_pretrained(pretrained)
+    return ShuffleNetV2(1.5, **kw)
+
+
+def shufflenet_v2_swish(pretrained=False, **kw):
+    """ShuffleNetV2 x1.0 with swish activations (reference vision/models/shufflenetv2.py:541)."""
+    _no_pretrained(pretrained)
+    return ShuffleNetV2(1.0, act='swish', **kw)
 
 
 # ----------------------------------------------------------------------------- DenseNet

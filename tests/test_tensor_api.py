@@ -155,3 +155,22 @@ def test_onnx_export_emits_model_proto(tmp_path):
     assert info['opset'] >= 13 and info['inputs'] == ['img']
     for op in ('Conv', 'Relu', 'Gemm', 'Softmax'):
         assert op in info['ops'], info['ops']
+
+
+def test_linalg_ormqr_reference_docstring():
+    """reference tensor/linalg.py:5075-5083 example values."""
+    import numpy as np
+    import paddle
+    x = paddle.to_tensor([[-114.6, 10.9, 1.1], [-0.304, 38.07, 69.38], [-0.45, -0.17, 62]])
+    tau = paddle.to_tensor([1.55, 1.94, 3.0])
+    out = paddle.linalg.ormqr(x, tau, x)
+    ref = np.array([[63.82712936, -13.82312393, -116.28614044], [-53.65926361, -28.15783691, -70.42700958],
+                    [-79.54292297, 24.00182915, -41.34253311]])
+    np.testing.assert_allclose(out.numpy(), ref, rtol=1e-4, atol=1e-3)
+    # transpose / right multiplication agree with the explicit Q from householder_product
+    q = paddle.linalg.householder_product(x, tau).numpy()
+    y = np.random.RandomState(0).randn(3, 3).astype('float32')
+    np.testing.assert_allclose(paddle.linalg.ormqr(x, tau, paddle.to_tensor(y), transpose=True).numpy(), q.T @ y,
+                               rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(paddle.linalg.ormqr(x, tau, paddle.to_tensor(y), left=False).numpy(), y @ q,
+                               rtol=1e-4, atol=1e-3)

@@ -3,6 +3,8 @@ import gzip
 import os
 import struct
 
+import pytest
+
 import numpy as np
 import torch
 from PIL import Image
@@ -93,3 +95,17 @@ def test_mnist_and_folder(tmp_path):
         Image.fromarray((np.random.rand(8, 8, 3) * 255).astype('uint8')).save(tmp_path / 'f' / c / 'a.png')
     fd = paddle.vision.datasets.DatasetFolder(str(tmp_path / 'f'))
     assert len(fd) == 2 and fd.classes == ['cat', 'dog']
+
+
+@pytest.mark.parametrize('name', ['shufflenet_v2_x0_25', 'shufflenet_v2_x0_33', 'shufflenet_v2_x1_5',
+                                  'shufflenet_v2_swish'])
+def test_shufflenet_variants(name):
+    """The four ShuffleNetV2 builders of reference vision/models/shufflenetv2.py:331-541."""
+    import paddle
+    from paddle.vision import models
+    m = getattr(models, name)(num_classes=7)
+    m.eval()
+    assert m(paddle.randn([2, 3, 64, 64])).shape == [2, 7]
+    last = {'shufflenet_v2_x0_25': 512, 'shufflenet_v2_x0_33': 512, 'shufflenet_v2_x1_5': 1024,
+            'shufflenet_v2_swish': 1024}[name]
+    assert m.fc.weight.shape == [last, 7]
