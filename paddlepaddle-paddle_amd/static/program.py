@@ -247,6 +247,9 @@ class _Recorder(TorchFunctionMode):
         dev_meta = any(isinstance(v, torch.device) and v.type == 'meta' for v in kwargs.values()) or \
             kwargs.get('device') == 'meta'
         static_input = any(t.is_meta and id(t) in prog._val for t in metas)
+        forced = getattr(prog, '_force_record_ids', None)  # decomposition: ops on captured params
+        if forced and not static_input:
+            static_input = any(id(t) in forced for t in metas)
         if not static_input and not dev_meta and not (not metas and (_has_sentinel(list(args)) or
                                                                     _has_sentinel(list(kwargs.values())))):
             if any(t.is_meta for t in metas):
