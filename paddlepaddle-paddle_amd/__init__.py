@@ -97,3 +97,15 @@ def is_compiled_with_ipu():
 
 def get_all_custom_device_type():
     return []
+
+
+def _maybe_native_allocator():
+    """FLAGS_use_native_allocator=1: install csrc/alloc's auto-growth best-fit allocator as the
+    device allocator before anything allocates on the GPU."""
+    import os as _os
+    if _os.environ.get('FLAGS_use_native_allocator', '').lower() in ('1', 'true', 'yes', 'on'):
+        from .device.cuda import allocator as _native_alloc
+        _native_alloc.enable()
+
+
+_maybe_native_allocator()

@@ -5,6 +5,9 @@
   so each TU builds in seconds and the library has no ABI coupling to the torch build).
 * ``_lib/libpaddle_amd_runtime.so`` — ``csrc/runtime/*.cpp`` host code (data-loader
   prefetch ring, host tracer, flags), compiled with g++.
+* ``_lib/libpaddle_amd_alloc.so`` — ``csrc/alloc/allocator.cpp``, the native auto-growth
+  best-fit device allocator (host code over the HIP runtime, compiled with hipcc), loaded by
+  torch's pluggable-allocator hook when enabled.
 
 Incremental: an object is rebuilt only when its source or a header is newer.
 """
@@ -23,6 +26,7 @@ HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 
 KERNEL_LIB = os.path.join(LIB, 'libpaddle_amd_kernels.so')
 RUNTIME_LIB = os.path.join(LIB, 'libpaddle_amd_runtime.so')
+ALLOC_LIB = os.path.join(LIB, 'libpaddle_amd_alloc.so')
 
 
 def _newer(src, dst, deps=()):
@@ -76,10 +80,20 @@ def build_runtime(verbose=False):
     return RUNTIME_LIB
 
 
+def build_alloc(verbose=False):
+    os.makedirs(LIB, exist_ok=True)
+    src = os.path.join(CSRC, 'alloc', 'allocator.cpp')
+    if _newer(src, ALLOC_LIB):
+        _run([HIPCC, '-O2', '-std=c++17', '-fPIC', '-shared', src, '-o', ALLOC_LIB + '.tmp'])
+        os.replace(ALLOC_LIB + '.tmp', ALLOC_LIB)
+    return ALLOC_LIB
+
+
 def build_all(verbose=False):
     k = build_kernels(verbose)
     r = build_runtime(verbose)
-    return k, r
+    a = build_alloc(verbose)
+    return k, r, a
 
 
 if __name__ == '__main__':

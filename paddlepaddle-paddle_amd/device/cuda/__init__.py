@@ -1,6 +1,9 @@
 """paddle.device.cuda (reference: python/paddle/device/cuda/__init__.py): device queries,
-caching-allocator statistics, streams, and HIP graphs (graphs.py)."""
+allocator statistics (torch's caching allocator, or the native auto-growth allocator of
+allocator.py when enabled), streams, and HIP graphs (graphs.py)."""
 import torch
+
+from . import allocator as native_allocator
 
 from .. import Stream, Event, current_stream, synchronize as _sync, stream_guard as _sg, _dev  # noqa: F401
 from .graphs import CUDAGraph, is_cuda_graph_supported, wrap_cuda_graph  # noqa: F401
@@ -15,7 +18,9 @@ def device_count():
 
 
 def empty_cache():
-    if torch.cuda.is_available():
+    if native_allocator.is_enabled():
+        native_allocator.empty_cache(torch.cuda.current_device())
+    elif torch.cuda.is_available():
         torch.cuda.empty_cache()
 
 
@@ -24,22 +29,33 @@ def _idx(device):
 
 
 def max_memory_allocated(device=None):
+    if native_allocator.is_enabled():
+        return native_allocator.stats(_idx(device))['peak_allocated']
     return torch.cuda.max_memory_allocated(_idx(device))
 
 
 def max_memory_reserved(device=None):
+    if native_allocator.is_enabled():
+        return native_allocator.stats(_idx(device))['peak_reserved']
     return torch.cuda.max_memory_reserved(_idx(device))
 
 
 def memory_allocated(device=None):
+    if native_allocator.is_enabled():
+        return native_allocator.stats(_idx(device))['allocated']
     return torch.cuda.memory_allocated(_idx(device))
 
 
 def memory_reserved(device=None):
+    if native_allocator.is_enabled():
+        return native_allocator.stats(_idx(device))['reserved']
     return torch.cuda.memory_reserved(_idx(device))
 
 
 def reset_max_memory_allocated(device=None):
+    if native_allocator.is_enabled():
+        native_allocator.reset_peak(_idx(device))
+        return
     torch.cuda.reset_peak_memory_stats(_idx(device))
 
 

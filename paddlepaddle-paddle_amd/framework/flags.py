@@ -4,7 +4,9 @@ Flags are typed, default-valued, overridable from the environment (``FLAGS_xxx=.
 readable/settable at run time.  Flags that change framework behaviour here:
 ``FLAGS_check_nan_inf`` (op-output NaN/Inf checker, amp/debugging.py),
 ``FLAGS_use_hip_kernels`` (route hot ops to the HIP kernel library),
-``FLAGS_allocator_strategy`` / ``FLAGS_fraction_of_gpu_memory_to_use`` (caching allocator knobs).
+``FLAGS_allocator_strategy`` / ``FLAGS_fraction_of_gpu_memory_to_use`` (caching allocator knobs),
+``FLAGS_use_native_allocator`` / ``FLAGS_auto_growth_chunk_size_in_mb`` (install the native
+auto-growth best-fit device allocator, device/cuda/allocator.py, at import).
 """
 import os
 
@@ -14,6 +16,8 @@ _REGISTRY = {
     'FLAGS_use_hip_kernels': True,
     'FLAGS_allocator_strategy': 'auto_growth',
     'FLAGS_fraction_of_gpu_memory_to_use': 0.92,
+    'FLAGS_use_native_allocator': False,
+    'FLAGS_auto_growth_chunk_size_in_mb': 0,
     'FLAGS_eager_delete_tensor_gb': 0.0,
     'FLAGS_cudnn_deterministic': False,
     'FLAGS_embedding_deterministic': 0,

@@ -10,6 +10,8 @@ Reference: paddle/phi/kernels/gpudnn/conv_kernel.cu (forward), conv_grad_kernel.
 * Filter gradient (any R x S / stride / padding): implicit GEMM with the pixels as the reduction
   axis, split over the grid (pa_conv2d_wgrad); inputs with C % 8 != 0 (the stem) are zero-padded
   to 8 channels for it.
+* 1x1 stride-1 convolutions with wide channel counts: plain GEMMs on the 8-phase MFMA GEMM
+  (forward, data gradient, filter gradient), where measured faster (_pointwise).
 The storage layer's convolution backward (MIOpen) remains only as the fallback for shapes the
 kernels reject (grouped / odd channel counts) or when PADDLE_AMD_HIP_CONV_BWD=0.
 """
@@ -199,6 +201,43 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, dil):
     return dw
 
 
+# 1x1 / stride-1 / unpadded convolutions are plain GEMMs over the N*H*W pixel rows; the 8-phase MFMA
+# GEMM (csrc/gemm8.hip) runs them faster than the implicit-GEMM conv kernel once the GEMM's N side
+# fills its 256-wide tiles (tools/conv1x1_gemm_bench.py, profiles/r2_conv1x1_gemm.log: forward when
+# Cout >= 128, data gradient when C >= 128, filter gradient when C >= 512 and Cout >= C / 2).
+_gemm_1x1 = os.environ.get('PADDLE_AMD_CONV1X1_GEMM', '1') != '0'
+
+
+def _pointwise(w, stride, pad, dil):
+    return (_gemm_1x1 and w.shape[2] == 1 and w.shape[3] == 1 and tuple(stride) == (1, 1)
+            and tuple(pad) == (0, 0))
+
+
+def _gemm_fwd_1x1(x, w, b):
+    from . import gemm
+    Cout, C = w.shape[0], w.shape[1]
+    if Cout < 128:
+        return None
+    x2 = x.contiguous().view(-1, C)
+    wt = w.detach().view(Cout, C).t()  # [C, Cout] view of the k-contiguous [Cout][C] filter
+    bb = b.to(torch.bfloat16).contiguous() if b is not None else None
+    if not gemm.hip_mm_ok(x2, wt):
+        return None
+    return gemm.hip_mm(x2, wt, bias=bb).view(*x.shape[:3], Cout)
+
+
+def _gemm_dgrad_1x1(dy, w):
+    from . import gemm
+    Cout, C = w.shape[0], w.shape[1]
+    if C < 128:
+        return None
+    dy2 = dy.contiguous().view(-1, Cout)
+    w2 = w.detach().view(Cout, C)
+    if not gemm.hip_mm_ok(dy2, w2):
+        return None
+    return gemm.hip_mm(dy2, w2).view(*dy.shape[:3], C)
+
+
 def _lib_conv_fwd(x, w, b, stride, pad, dil):
     y = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w, b, stride, pad, dil)
     return y.permute(0, 2, 3, 1).contiguous()
@@ -209,6 +248,10 @@ class _Conv2dNHWC(torch.autograd.Function):
     def forward(ctx, x, w, b, stride, pad, dil):
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, dil, b is not None)
+        if _pointwise(w, stride, pad, dil) and w.dtype == torch.bfloat16:
+            y = _gemm_fwd_1x1(x, w, b)
+            if y is not None:
+                return y
         if fwd_ok(w):
             return conv2d_fwd(x, w, b, stride, pad, dil)
         return _lib_conv_fwd(x, w, b, stride, pad, dil)
@@ -219,8 +262,12 @@ class _Conv2dNHWC(torch.autograd.Function):
         stride, pad, dil, has_b = ctx.cfg
         dy = dy.contiguous()
         gx = gw = gb = None
+        pw = _pointwise(w, stride, pad, dil)
         if ctx.needs_input_grad[0] and _bwd_enabled:
-            gx = conv2d_dgrad_classes(dy, w, x.shape[1:3], stride, pad, dil)
+            if pw:
+                gx = _gemm_dgrad_1x1(dy, w)
+            if gx is None:
+                gx = conv2d_dgrad_classes(dy, w, x.shape[1:3], stride, pad, dil)
         if ctx.needs_input_grad[1] and _bwd_enabled and _wgrad_hip and w.shape[0] % 8 == 0:
             C = w.shape[1]
             if C % 8:  # RGB stem: zero channels do not change the taps of the real ones
@@ -228,7 +275,10 @@ class _Conv2dNHWC(torch.autograd.Function):
                 gw = conv2d_wgrad(dy, xp, (w.shape[0], xp.shape[3], w.shape[2], w.shape[3]), stride, pad,
                                   dil)[:, :C].contiguous()
             else:
-                gw = conv2d_wgrad(dy, x, tuple(w.shape), stride, pad, dil)
+                if pw and w.shape[1] >= 512 and 2 * w.shape[0] >= w.shape[1]:
+                    gw = conv2d_wgrad_1x1(dy, x)
+                if gw is None:
+                    gw = conv2d_wgrad(dy, x, tuple(w.shape), stride, pad, dil)
             gw = gw.to(w.dtype)
         if has_b and ctx.needs_input_grad[2]:
             gb = dy.sum((0, 1, 2), dtype=torch.float32).to(dy.dtype)

@@ -94,3 +94,6 @@ def run(mode, steps, world, rank):
 if __name__ == '__main__':
     dist.init_parallel_env()
     run(sys.argv[1], 4, dist.get_world_size(), dist.get_rank())
+    # orderly teardown: a rank that exits while gloo's pair threads still run aborts at exit
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
