@@ -70,9 +70,17 @@ def enable(chunk_mb=None, fraction=None):
     return True
 
 
+def _index(device):
+    if isinstance(device, torch.device):
+        return device.index if device.index is not None else (torch.cuda.current_device() if device.type != 'cpu' else 0)
+    if isinstance(device, str):
+        return _index(torch.device(device.replace('gpu', 'cuda')))
+    return int(device or 0)
+
+
 def stats(device=0):
     out = (ctypes.c_longlong * 9)()
-    lib().pa_alloc_stats(int(device), out)
+    lib().pa_alloc_stats(_index(device), out)
     return dict(zip(_STAT_KEYS, list(out)))
 
 
@@ -80,12 +88,12 @@ def empty_cache(device=0):
     """Give fully idle chunks back to the driver (after a device synchronize)."""
     if torch.cuda.is_available():
         torch.cuda.synchronize()
-    return int(lib().pa_alloc_empty_cache(int(device)))
+    return int(lib().pa_alloc_empty_cache(_index(device)))
 
 
 def reset_peak(device=0):
-    lib().pa_alloc_reset_peak(int(device))
+    lib().pa_alloc_reset_peak(_index(device))
 
 
 def largest_free_block(device=0):
-    return int(lib().pa_alloc_largest_free(int(device)))
+    return int(lib().pa_alloc_largest_free(_index(device)))

@@ -323,4 +323,56 @@ class Role:
     SERVER = 2
 
 
+class UtilBase:
+    """fleet.util (reference: python/paddle/distributed/fleet/base/util_factory.py): collective helpers
+    over the worker group plus file sharding for data-parallel input lists."""
+
+    def _t(self, x):
+        import numpy as np
+        import torch
+        return torch.as_tensor(np.asarray(x))
+
+    def all_reduce(self, input, mode="sum", comm_world="worker"):
+        import torch
+        import torch.distributed as tdist
+        t = self._t(input).clone()
+        if tdist.is_available() and tdist.is_initialized() and tdist.get_world_size() > 1:
+            op = {'sum': tdist.ReduceOp.SUM, 'max': tdist.ReduceOp.MAX, 'min': tdist.ReduceOp.MIN}[mode]
+            tdist.all_reduce(t, op=op)
+        return t.numpy()
+
+    def barrier(self, comm_world="worker"):
+        import torch.distributed as tdist
+        if tdist.is_available() and tdist.is_initialized():
+            tdist.barrier()
+
+    def all_gather(self, input, comm_world="worker"):
+        import torch.distributed as tdist
+        if tdist.is_available() and tdist.is_initialized() and tdist.get_world_size() > 1:
+            out = [None] * tdist.get_world_size()
+            tdist.all_gather_object(out, input)
+            return out
+        return [input]
+
+    def get_file_shard(self, files):
+        """This worker's contiguous share of ``files`` (earlier workers take one extra file when
+        the count does not divide)."""
+        if not isinstance(files, list):
+            raise TypeError("files should be a list of file paths")
+        n, i = fleet.worker_num(), fleet.worker_index()
+        base, extra = divmod(len(files), n)
+        start = i * base + min(i, extra)
+        return files[start:start + base + (1 if i < extra else 0)]
+
+    def print_on_rank(self, message, rank_id):
+        if fleet.worker_index() == rank_id:
+            print(message)
+
+
+util = UtilBase()
+Fleet = _Fleet  # the class behind the module-level ``fleet`` singleton (reference fleet/fleet.py)
+from . import data_generator  # noqa: E402,F401
+from .data_generator import MultiSlotDataGenerator, MultiSlotStringDataGenerator  # noqa: E402,F401
+
+
 _ = copy

@@ -4,6 +4,7 @@ import torch
 from . import nn  # noqa: F401
 from . import autotune  # noqa: F401
 from . import asp  # noqa: F401
+from . import autograd  # noqa: F401
 from .optimizer import LookAhead, ModelAverage  # noqa: F401
 from . import optimizer  # noqa: F401
 from ..core.tensor import _wrap, _unwrap

@@ -5,12 +5,38 @@ decorate, calculate_density, set_excluded_layers, utils mask algorithms).
 the input dim, 2 are kept.  ``prune_model`` computes masks (magnitude, 1-D groups) and applies
 them; ``decorate(optimizer)`` re-applies the masks after every step so pruned weights stay 0.
 """
+import re
+
+import numpy as np
 import torch
 
 from ..core.tensor import _unwrap
 
 _excluded = set()
 _masks = {}
+# layer-type name (snake case) -> pruning function (weight ndarray, m, n, mask_algo, param_name)
+# -> (pruned weight, mask); reference incubate/asp/supported_layer_list.py
+_custom_prune = {}
+
+
+def _snake(name):
+    return re.sub(r'(?<!^)(?=[A-Z])', '_', name).lower()
+
+
+def add_supported_layer(layer, pruning_func=None):
+    """Register a layer (name, Layer instance or Layer class) whose parameters ``prune_model``
+    prunes with ``pruning_func(weight_ndarray, m, n, mask_algo, param_name) -> (weight, mask)``
+    (the built-in n:m magnitude mask when None)."""
+    from ..nn.layer.layers import Layer
+    if isinstance(layer, str):
+        name = layer
+    elif isinstance(layer, Layer):
+        name = _snake(type(layer).__name__)
+    elif isinstance(layer, type) and issubclass(layer, Layer):
+        name = _snake(layer.__name__)
+    else:
+        raise TypeError(f"add_supported_layer expects a name or a Layer, got {type(layer)}")
+    _custom_prune[name] = pruning_func
 
 
 def calculate_density(x):
@@ -57,10 +83,24 @@ def _supported(name, p):
 def prune_model(model, n=2, m=4, mask_algo='mask_1d', with_mask=True):
     """Applies n:m masks to every eligible weight (Linear [in, out] is pruned along ``in``)."""
     out = {}
+    owner = {}
+    for lname, layer in model.named_sublayers(include_self=True):
+        for pname, p in layer.named_parameters(include_sublayers=False):
+            owner[id(p)] = _snake(type(layer).__name__)
     for name, p in model.named_parameters():
         if not _supported(name, p):
             continue
         t = _unwrap(p)
+        fn = _custom_prune.get(owner.get(id(p), ''))
+        if fn is not None:  # registered custom pruning function
+            w_np, mask_np = fn(t.detach().float().cpu().numpy(), m, n, mask_algo, name)
+            mask = torch.as_tensor(np.asarray(mask_np), device=t.device)
+            with torch.no_grad():
+                t.copy_(torch.as_tensor(np.asarray(w_np), device=t.device).to(t.dtype))
+            if with_mask:
+                _masks[id(p)] = (p, mask)
+            out[name] = mask
+            continue
         # paddle Linear weights are [in, out]: group along the input dim → transpose for masking
         w = t.t() if t.dim() == 2 else t
         mask = create_mask(w, n, m)

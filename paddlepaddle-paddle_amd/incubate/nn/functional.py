@@ -66,6 +66,32 @@ def fused_dropout_add(x, y, p=0.5, training=True, mode='upscale_in_train', name=
     return _w(TF.dropout(t, p, True) + r)
 
 
+def fused_bias_dropout_residual_layer_norm(x, residual, bias=None, ln_scale=None, ln_bias=None, dropout_rate=0.5,
+                                           ln_epsilon=1e-5, training=True, mode='upscale_in_train', name=None):
+    """y = layer_norm(residual + dropout(x + bias)) (reference incubate/nn/functional/
+    fused_transformer.py fused_bias_dropout_residual_layer_norm).  On the GPU one csrc/norm.hip
+    kernel each way (keep mask regenerated from its counter hash in the backward)."""
+    if mode not in ('upscale_in_train', 'downscale_in_infer'):
+        raise ValueError("mode must be 'upscale_in_train' or 'downscale_in_infer'")
+    t, r = _u(x), _u(residual)
+    p = float(dropout_rate) if training else 0.0
+    w = _u(ln_scale) if ln_scale is not None else None
+    b = _u(ln_bias) if ln_bias is not None else None
+    if (mode == 'upscale_in_train' and ops.use_hip(t) and w is not None and t.shape == r.shape
+            and (bias is None or _u(bias).dtype == t.dtype) and ops.fused.dropout_add_norm_ok(t, w, p)):
+        y, _ = ops.fused.dropout_add_norm(t, bias, r, w, b, float(ln_epsilon), p)
+        return _w(y)
+    h = t + _u(bias) if bias is not None else t
+    if p > 0.0:
+        h = TF.dropout(h, p, True)
+    elif mode == 'downscale_in_infer' and dropout_rate > 0.0 and not training:
+        h = h * (1.0 - dropout_rate)
+    h = h + r
+    y = TF.layer_norm(h.float(), [h.shape[-1]], w.float() if w is not None else None,
+                      b.float() if b is not None else None, ln_epsilon).to(h.dtype)
+    return _w(y)
+
+
 @_amp_op('fused_rotary_position_embedding')
 def fused_rotary_position_embedding(q, k=None, v=None, sin=None, cos=None, position_ids=None,
                                     use_neox_rotary_style=True, time_major=False, rotary_emb_base=10000.0):

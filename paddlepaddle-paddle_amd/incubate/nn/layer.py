@@ -39,8 +39,8 @@ class FusedBiasDropoutResidualLayerNorm(Layer):
         self.p, self.eps = dropout_rate, epsilon
 
     def forward(self, x, residual):
-        h = IF.fused_dropout_add(_wrap(_unwrap(x) + _unwrap(self.linear_bias)), residual, self.p, self.training)
-        return F.layer_norm(h, [_unwrap(h).shape[-1]], self.ln_scale, self.ln_bias, self.eps)
+        return IF.fused_bias_dropout_residual_layer_norm(x, residual, self.linear_bias, self.ln_scale, self.ln_bias,
+                                                         self.p, self.eps, self.training)
 
 
 class FusedMultiHeadAttention(Layer):

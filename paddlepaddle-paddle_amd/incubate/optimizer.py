@@ -87,3 +87,6 @@ class ModelAverage:
             for p in self._params:
                 if id(p) in self._backup:
                     _unwrap(p).copy_(self._backup.pop(id(p)))
+
+
+from ..optimizer.algorithms import LBFGS  # noqa: E402,F401  (reference: incubate/optimizer/lbfgs.py)

@@ -277,3 +277,37 @@ def convert_to_mixed_precision(model_file, params_file, mixed_model_file, mixed_
     shutil.copyfile(model_file, mixed_model_file)
     ts = load_file(params_file)
     save_file({k: (v.to(dt) if v.is_floating_point() else v) for k, v in ts.items()}, mixed_params_file)
+
+
+def get_trt_compile_version():
+    """TensorRT is an NVIDIA engine; this build has none: (0, 0, 0) (reference returns the
+    version the library was compiled against)."""
+    return (0, 0, 0)
+
+
+def get_trt_runtime_version():
+    return (0, 0, 0)
+
+
+class XpuConfig:
+    """Kunlun XPU predictor options (reference inference/wrapper.py); accepted and unused on MI355X."""
+
+    def __init__(self):
+        self.device_id = 0
+        self.l3_size = 0
+        self.l3_ptr = None
+        self.l3_autotune_size = 0
+        self.conv_autotune_level = 0
+        self.fc_autotune_level = 0
+        self.context_gm_size = 0
+        self.transformer_softmax_optimize_level = 0
+        self.transformer_encoder_adaptive_seqlen = True
+        self.quant_post_static_gelu_out_threshold = 10.0
+        self.quant_post_dynamic_activation_method = 0
+        self.quant_post_dynamic_weight_precision = 1
+        self.quant_post_dynamic_op_types = []
+
+
+def _get_phi_kernel_name(fluid_op_name):
+    """Operator name -> kernel name (the same string here: every op is its own kernel entry)."""
+    return fluid_op_name

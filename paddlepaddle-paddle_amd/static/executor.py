@@ -283,6 +283,10 @@ class Executor:
             raise TypeError("Executor.run expects a static Program")
         if program is default_startup_program() or (not program.nodes and not program.feeds):
             return []  # parameters are initialised when their layers are created
+        from ..decomposition import decomp as _decomp
+        if _decomp._prim_config['prim_enabled'] and not getattr(program, '_prim_decomposed', False):
+            _decomp.decompose(program, [])  # incubate.autograd.enable_prim(): run on primitive ops
+            program._prim_decomposed = True
         env = run_program(program, feed, self._dev)
         fetch_list = fetch_list if fetch_list is not None else []
         if not isinstance(fetch_list, (list, tuple)):

@@ -142,3 +142,20 @@ def test_batch_norm_eval_and_custom_rule(static_mode):
         assert calls == [1]
     finally:
         register_decomp('pd_op.silu')(rules.silu)
+
+
+def test_enable_prim_decomposes_on_run(static_mode):
+    from paddle.incubate import autograd as A
+    main, x, out = _build(lambda x: F.softmax(F.gelu(x), -1))
+    exe = paddle.static.Executor()
+    xv = np.random.RandomState(0).randn(4, 16).astype('float32')
+    ref = exe.run(main, feed={'x': xv}, fetch_list=[out])[0]
+    A.enable_prim()
+    try:
+        assert A.prim_enabled()
+        main2, x2, out2 = _build(lambda x: F.softmax(F.gelu(x), -1))
+        got = exe.run(main2, feed={'x': xv}, fetch_list=[out2])[0]
+        assert not any(_names(main2))
+    finally:
+        A.disable_prim()
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)

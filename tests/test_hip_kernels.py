@@ -884,17 +884,23 @@ def test_resnet_conv_routes_to_hip():
     x = paddle.to_tensor(torch.randn(2, 64, 64, 3, device=DEV))
     from paddle.ops import conv
     calls = []
-    orig = conv.conv2d_fwd
+    orig, orig_1x1 = conv.conv2d_fwd, conv._gemm_fwd_1x1
 
     def spy(*a, **k):
         calls.append(a[1].shape)
         return orig(*a, **k)
-    conv.conv2d_fwd = spy
+
+    def spy_1x1(x, w, b):  # 1x1 convolutions with >= 128 output channels run on the GEMM
+        y = orig_1x1(x, w, b)
+        if y is not None:
+            calls.append(w.shape)
+        return y
+    conv.conv2d_fwd, conv._gemm_fwd_1x1 = spy, spy_1x1
     try:
         paddle.amp.decorate(m, level='O2', dtype='bfloat16')
         out = m(paddle.to_tensor(x._t.bfloat16()))
     finally:
-        conv.conv2d_fwd = orig
+        conv.conv2d_fwd, conv._gemm_fwd_1x1 = orig, orig_1x1
     assert out.shape == [2, 1000]
     assert len(calls) >= 50, len(calls)  # every conv but the 3-channel stem
 
