@@ -15,7 +15,7 @@ def _ws(rows, cols, dt, dev):
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, z, gamma, beta, run_mean, run_var, eps, momentum, training, relu):
+    def forward(ctx, x, z, gamma, beta, run_mean, run_var, eps, momentum, training, relu, dz_sink=None):
         C = x.shape[-1]
         x2 = x.contiguous()
         rows = x2.numel() // C
@@ -43,6 +43,7 @@ class _BNAct(torch.autograd.Function):
         ctx.save_for_backward(x2, y if relu else None, mean, rstd, gamma)
         ctx.relu, ctx.has_z, ctx.training = relu, z is not None, training
         ctx.has_beta = beta is not None
+        ctx.dz_sink = dz_sink
         return y
 
     @staticmethod
@@ -61,7 +62,10 @@ class _BNAct(torch.autograd.Function):
         N.check(N.lib.pa_bn_bwd(N.ptr(dy), N.ptr(x), N.ptr(y), N.ptr(mean), N.ptr(rstd), N.ptr(gamma), N.ptr(dx),
                                 N.ptr(dz), N.ptr(dg), N.ptr(db), N.ptr(ws), rows, C, int(ctx.relu), N.dtcode(x.dtype),
                                 N.dtcode(gamma.dtype) if gamma is not None else 0, N.stream()), 'bn_bwd')
-        return dx, dz, dg, db, None, None, None, None, None, None
+        if dz is not None and ctx.dz_sink is not None:
+            ctx.dz_sink.buf = dz  # taken by the consuming conv's dgrad (ops/conv.py GradSink)
+            dz = None
+        return dx, dz, dg, db, None, None, None, None, None, None, None
 
 
 def supported(x, gamma=None):
@@ -76,6 +80,7 @@ def supported(x, gamma=None):
 
 
 def bn_act_nhwc(x, gamma, beta, run_mean, run_var, eps=1e-5, momentum=0.9, training=True, relu=False,
-                residual=None):
-    """act(batch_norm(x) [+ residual]) for a channels-last tensor (channel = last dim)."""
-    return _BNAct.apply(x, residual, gamma, beta, run_mean, run_var, eps, momentum, training, relu)
+                residual=None, dz_sink=None):
+    """act(batch_norm(x) [+ residual]) for a channels-last tensor (channel = last dim).  dz_sink
+    (ops.conv.GradSink): hand the residual gradient to the conv that consumes the residual."""
+    return _BNAct.apply(x, residual, gamma, beta, run_mean, run_var, eps, momentum, training, relu, dz_sink)

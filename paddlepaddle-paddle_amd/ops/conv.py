@@ -226,7 +226,8 @@ def _gemm_fwd_1x1(x, w, b):
     return gemm.hip_mm(x2, wt, bias=bb).view(*x.shape[:3], Cout)
 
 
-def _gemm_dgrad_1x1(dy, w):
+def _gemm_dgrad_1x1(dy, w, acc=None):
+    """dX = dY @ W (+ acc, accumulated in place by the beta = 1 epilogue)."""
     from . import gemm
     Cout, C = w.shape[0], w.shape[1]
     if C < 128:
@@ -235,7 +236,42 @@ def _gemm_dgrad_1x1(dy, w):
     w2 = w.detach().view(Cout, C)
     if not gemm.hip_mm_ok(dy2, w2):
         return None
+    if acc is not None and acc.is_contiguous() and acc.dtype == dy.dtype and acc.numel() == dy2.shape[0] * C:
+        gemm.hip_mm(dy2, w2, out=acc.view(-1, C), beta=1.0)
+        return acc.view(*dy.shape[:3], C)
+    if acc is not None:
+        return None
     return gemm.hip_mm(dy2, w2).view(*dy.shape[:3], C)
+
+
+class GradSink:
+    """Hand-off of a residual-branch gradient to the data-gradient GEMM of the convolution that
+    consumes the same tensor (ResNet identity blocks): the fused BN + add + ReLU backward parks
+    dZ here instead of returning it, and the 1x1 conv's dgrad accumulates into it (beta = 1
+    epilogue), so autograd never runs the separate add of the two branch gradients."""
+    __slots__ = ('buf', 'armed')
+
+    def __init__(self):
+        self.buf = None
+        self.armed = False  # set when a convolution's backward has taken the sink
+
+
+_pending_sink = [None]
+
+
+class dgrad_sink:
+    """Context: the next conv2d_nhwc call adds ``sink.buf`` into its input gradient."""
+
+    def __init__(self, sink):
+        self.sink = sink
+
+    def __enter__(self):
+        _pending_sink[0] = self.sink
+        return self.sink
+
+    def __exit__(self, *exc):
+        _pending_sink[0] = None
+        return False
 
 
 def _lib_conv_fwd(x, w, b, stride, pad, dil):
@@ -245,9 +281,10 @@ def _lib_conv_fwd(x, w, b, stride, pad, dil):
 
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, dil):
+    def forward(ctx, x, w, b, stride, pad, dil, sink=None):
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, dil, b is not None)
+        ctx.sink = sink
         if _pointwise(w, stride, pad, dil) and w.dtype == torch.bfloat16:
             y = _gemm_fwd_1x1(x, w, b)
             if y is not None:
@@ -263,9 +300,14 @@ class _Conv2dNHWC(torch.autograd.Function):
         dy = dy.contiguous()
         gx = gw = gb = None
         pw = _pointwise(w, stride, pad, dil)
+        sink = ctx.sink.buf if ctx.sink is not None else None
+        if ctx.sink is not None:
+            ctx.sink.buf = None
         if ctx.needs_input_grad[0] and _bwd_enabled:
             if pw:
-                gx = _gemm_dgrad_1x1(dy, w)
+                gx = _gemm_dgrad_1x1(dy, w, acc=sink)
+                if gx is not None:
+                    sink = None  # accumulated in the GEMM epilogue
             if gx is None:
                 gx = conv2d_dgrad_classes(dy, w, x.shape[1:3], stride, pad, dil)
         if ctx.needs_input_grad[1] and _bwd_enabled and _wgrad_hip and w.shape[0] % 8 == 0:
@@ -291,8 +333,13 @@ class _Conv2dNHWC(torch.autograd.Function):
                 gx = lx.permute(0, 2, 3, 1)
             if mask[1]:
                 gw = lw
-        return gx, gw, gb, None, None, None
+        if sink is not None:  # residual gradient not taken by a GEMM epilogue: plain add
+            gx = gx + sink if gx is not None else sink
+        return gx, gw, gb, None, None, None, None
 
 
 def conv2d_nhwc(x, w, b, stride, pad, dil):
-    return _Conv2dNHWC.apply(x, w, b, tuple(stride), tuple(pad), tuple(dil))
+    sink, _pending_sink[0] = _pending_sink[0], None
+    if sink is not None:
+        sink.armed = True
+    return _Conv2dNHWC.apply(x, w, b, tuple(stride), tuple(pad), tuple(dil), sink)

@@ -9,15 +9,23 @@ from ... import ops
 from ...core.tensor import _wrap, _unwrap
 
 
-def _bn_act(bn, x, relu=True, residual=None):
+RESIDUAL_GRAD_SINK = True  # identity blocks: conv1's dgrad GEMM accumulates the residual gradient
+
+
+def _fused_bn_ok(bn, t):
+    return (bn.training and bn._data_format[-1] == 'C' and ops.use_hip(t) and isinstance(bn, nn.BatchNorm2D)
+            and bn._use_global_stats is not True and ops.batchnorm.supported(t, None if bn.weight is None else bn.weight._t))
+
+
+def _bn_act(bn, x, relu=True, residual=None, dz_sink=None):
     """act(bn(x) [+ residual]) — one csrc/batchnorm.hip pass each way for channels-last training
     on the GPU (fused_bn_add_activation); the plain layer sequence otherwise."""
     t = _unwrap(x)
-    if (bn.training and bn._data_format[-1] == 'C' and ops.use_hip(t) and isinstance(bn, nn.BatchNorm2D)
-            and bn._use_global_stats is not True and ops.batchnorm.supported(t, None if bn.weight is None else bn.weight._t)):
+    if _fused_bn_ok(bn, t):
         return _wrap(ops.batchnorm.bn_act_nhwc(
             t, None if bn.weight is None else bn.weight._t, None if bn.bias is None else bn.bias._t, bn._mean._t,
-            bn._variance._t, bn._epsilon, bn._momentum, True, relu, None if residual is None else _unwrap(residual)))
+            bn._variance._t, bn._epsilon, bn._momentum, True, relu, None if residual is None else _unwrap(residual),
+            dz_sink))
     y = bn(x)
     if residual is not None:
         y = y + residual
@@ -70,12 +78,21 @@ class BottleneckBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = _bn_act(self.bn1, self.conv1(x))
+        # identity block: the residual gradient is accumulated by conv1's data-gradient GEMM
+        # (ops.conv.GradSink) instead of a separate autograd add of the two branch gradients
+        sink = ops.conv.GradSink() if (RESIDUAL_GRAD_SINK and self.downsample is None
+                                       and _fused_bn_ok(self.bn3, _unwrap(x))) else None
+        if sink is not None:
+            with ops.conv.dgrad_sink(sink):
+                out = self.conv1(x)
+        else:
+            out = self.conv1(x)
+        out = _bn_act(self.bn1, out)
         out = _bn_act(self.bn2, self.conv2(out))
         out = self.conv3(out)
         if self.downsample is not None:
             identity = self.downsample(x)
-        return _bn_act(self.bn3, out, True, identity)
+        return _bn_act(self.bn3, out, True, identity, dz_sink=sink if sink is not None and sink.armed else None)
 
 
 class ResNet(nn.Layer):

@@ -1029,3 +1029,29 @@ def test_hip_kv_cache_write_and_fused_multi_transformer_decode():
     for t in range(S, S + 3):
         o, caches = m(x[:, t:t + 1], caches=caches, time_step=paddle.to_tensor([t]))
         _close(o._t[:, 0], full._t[:, t], atol=4e-2, rtol=4e-2, name=f"fmt decode step {t}")
+
+
+def test_resnet_identity_block_residual_grad_sink():
+    """Identity bottleneck blocks hand the residual gradient to conv1's dgrad GEMM (beta = 1
+    epilogue) instead of an autograd add: input / weight gradients match the add path."""
+    import paddle
+    from paddle.vision.models import resnet as R
+    paddle.set_device('gpu:0')
+    grads = []
+    for on in (False, True):
+        R.RESIDUAL_GRAD_SINK = on
+        try:
+            paddle.seed(3)
+            blk = R.BottleneckBlock(256, 64, data_format='NHWC')
+            blk = paddle.amp.decorate(blk, level='O2', dtype='bfloat16')
+            g = torch.Generator(device=DEV).manual_seed(4)
+            x = paddle.to_tensor(torch.randn(4, 14, 14, 256, device=DEV, generator=g).bfloat16())
+            x.stop_gradient = False
+            y = blk(x)
+            (y.astype('float32') * paddle.to_tensor(torch.randn(4, 14, 14, 256, device=DEV, generator=g))).sum().backward()
+            grads.append((x.grad._t.float().clone(), blk.conv1.weight.grad._t.float().clone(),
+                          blk.conv3.weight.grad._t.float().clone()))
+        finally:
+            R.RESIDUAL_GRAD_SINK = True
+    for a, b, name in zip(grads[0], grads[1], ('dx', 'dw1', 'dw3')):
+        _close(b, a, 0.05 * float(a.abs().max()) + 1e-3, 0.02, name)
