@@ -143,10 +143,14 @@ def main():
     import torch.distributed as dist
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
-    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    # one rank per GPU; the modulo only matters when rehearsing several ranks on fewer GPUs
+    local_rank = int(os.environ.get('LOCAL_RANK', '0')) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+        # RCCL over xGMI; PADDLE_AMD_BENCH_BACKEND=gloo only to rehearse several ranks on one GPU
+        # (RCCL refuses two ranks on one device)
+        be = os.environ.get('PADDLE_AMD_BENCH_BACKEND', 'nccl')
+        dist.init_process_group(be, **({'device_id': torch.device('cuda', local_rank)} if be == 'nccl' else {}))
     import paddle
     paddle.seed(1234 + rank)
     dev = torch.device('cuda', local_rank)
