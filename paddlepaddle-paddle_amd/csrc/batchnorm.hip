@@ -333,7 +333,7 @@ __global__ __launch_bounds__(256) void bwd_partial(const T* __restrict__ dy, con
 template <typename WT>
 __global__ __launch_bounds__(1024) void bwd_finish(const float* __restrict__ p1, const float* __restrict__ p2, int P,
                                                    int cols, const float* __restrict__ rstd, WT* __restrict__ dgamma,
-                                                   WT* __restrict__ dbeta, float* __restrict__ s_out) {
+                                                   WT* __restrict__ dbeta, float* __restrict__ s_out, int accumulate) {
   __shared__ float r1[16][65], r2[16][65];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
@@ -364,8 +364,9 @@ __global__ __launch_bounds__(1024) void bwd_finish(const float* __restrict__ p1,
     for (int i = 0; i < 16; ++i) { s1 += r1[i][lane]; s2 += r2[i][lane]; }
     s_out[c] = s1;
     s_out[cols + c] = s2;
-    if (dbeta != nullptr) dbeta[c] = from_f<WT>(s1);
-    if (dgamma != nullptr) dgamma[c] = from_f<WT>(s2 * rstd[c]);
+    // accumulate: += into the parameters' flat gradient slots (no separate AccumulateGrad add)
+    if (dbeta != nullptr) dbeta[c] = from_f<WT>(s1 + (accumulate ? to_f(dbeta[c]) : 0.f));
+    if (dgamma != nullptr) dgamma[c] = from_f<WT>(s2 * rstd[c] + (accumulate ? to_f(dgamma[c]) : 0.f));
   }
 }
 
@@ -455,7 +456,7 @@ hipError_t fwd(const void* x, const void* z, const void* gamma, const void* beta
 
 template <typename T, typename WT>
 hipError_t bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
-               void* dx, void* dz, void* dgamma, void* dbeta, float* ws, int rows, int cols, int relu,
+               void* dx, void* dz, void* dgamma, void* dbeta, float* ws, int rows, int cols, int relu, int accumulate,
                hipStream_t st) {
   constexpr int E = 16 / sizeof(T);
   const int cb = col_blocks(cols, E);
@@ -471,7 +472,8 @@ hipError_t bwd(const void* dy, const void* x, const void* y, const float* mean, 
     bwd_partial<T, true><<<rgrid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)y, mean, rows, cols, rrb, p1, p2);
   else
     bwd_partial<T, false><<<rgrid, 256, 0, st>>>((const T*)dy, (const T*)x, nullptr, mean, rows, cols, rrb, p1, p2);
-  bwd_finish<WT><<<(cols + 63) / 64, 1024, 0, st>>>(p1, p2, P, cols, rstd, (WT*)dgamma, (WT*)dbeta, sums);
+  bwd_finish<WT><<<(cols + 63) / 64, 1024, 0, st>>>(p1, p2, P, cols, rstd, (WT*)dgamma, (WT*)dbeta, sums,
+                                                    accumulate);
 #define PA_BNB(R, Z) bwd_apply<T, WT, R, Z><<<grid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)y, mean, rstd, \
                                                                  (const WT*)gamma, sums, (T*)dx, (T*)dz, rows, cols, rpb)
   if (relu && dz) PA_BNB(true, true);
@@ -515,10 +517,11 @@ PA_API hipError_t pa_bn_fwd(const void* x, const void* z, const void* gamma, con
 }
 
 // dz (nullable): gradient of the residual input z (= dy masked by ReLU).  y is the saved output
-// (needed only when relu).  dgamma/dbeta in the parameter dtype (nullable).
+// (needed only when relu).  dgamma/dbeta in the parameter dtype (nullable; accumulate != 0: +=).
 PA_API hipError_t pa_bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd,
                             const void* gamma, void* dx, void* dz, void* dgamma, void* dbeta, float* ws, int rows,
-                            int cols, int relu, int xd, int wd, hipStream_t st) {
+                            int cols, int relu, int accumulate, int xd, int wd, hipStream_t st) {
   if (cols % (xd == 0 ? 4 : 8) != 0 || rows < 1) return hipErrorInvalidValue;
-  PA_BN_DISPATCH(xd, wd, (bn::bwd<T, WT>(dy, x, y, mean, rstd, gamma, dx, dz, dgamma, dbeta, ws, rows, cols, relu, st)))
+  PA_BN_DISPATCH(xd, wd, (bn::bwd<T, WT>(dy, x, y, mean, rstd, gamma, dx, dz, dgamma, dbeta, ws, rows, cols, relu,
+                                          accumulate, st)))
 }

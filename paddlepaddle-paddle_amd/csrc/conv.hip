@@ -470,7 +470,7 @@ __global__ __launch_bounds__(256) void wgrad_zsum_kernel(const float* __restrict
 }
 
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, uint16_t* __restrict__ dw,
-                                                           int ngroups, int RS, int C, int Cout) {
+                                                           int ngroups, int RS, int C, int Cout, int accumulate) {
   const long long total = (long long)RS * C * Cout;
   for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
     // e enumerates the slab order (co fastest): coalesced partial reads
@@ -479,7 +479,9 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     const int c = (int)(mc % C), rs = (int)(mc / C);
     float v = 0.f;
     for (int z = 0; z < ngroups; ++z) v += part[(long long)z * total + e];
-    reinterpret_cast<bf16_t*>(dw)[((long long)co * C + c) * RS + rs] = (bf16_t)v;
+    bf16_t* o = reinterpret_cast<bf16_t*>(dw) + ((long long)co * C + c) * RS + rs;
+    if (accumulate) v += (float)*o;  // in place into the flat gradient slot
+    *o = (bf16_t)v;
   }
 }
 
@@ -619,12 +621,13 @@ PA_API int pa_conv2d_wgrad_set_bncap(int v) {
 }
 
 // Filter gradient.  x: bf16 NHWC [N,H,W,C], dy: bf16 NHWC [N,Ho,Wo,Cout], ws: fp32 scratch of
-// (splits + ceil(splits / 16)) * R*S*C * Cout floats (splits = pa_conv2d_wgrad_splits), dw: bf16 [Cout][C][R][S].  C % 8 == 0, Cout % 8 == 0, kchunk % 32 == 0.
+// (splits + ceil(splits / 16)) * R*S*C * Cout floats (splits = pa_conv2d_wgrad_splits), dw: bf16 [Cout][C][R][S]
+// (accumulate != 0: dw += the gradient, in place).  C % 8 == 0, Cout % 8 == 0, kchunk % 32 == 0.
 PA_API int pa_conv2d_wgrad_ok(int C, int Cout) { return C > 0 && C % 8 == 0 && Cout > 0 && Cout % 8 == 0; }
 
 PA_API int pa_conv2d_wgrad(const void* x, const void* dy, void* ws, void* dw, int N, int H, int W, int C, int Cout,
                            int R, int S, int sh, int sw, int ph, int pw, int dh, int dw_, int Ho, int Wo, int splits,
-                           hipStream_t st) {
+                           int accumulate, hipStream_t st) {
   if (!pa_conv2d_wgrad_ok(C, Cout) || N <= 0 || Ho <= 0 || Wo <= 0 || splits <= 0) return (int)hipErrorInvalidValue;
   const long long Pll = (long long)N * Ho * Wo;
   if (Pll > (1LL << 30) || (long long)N * H * W * C > (1LL << 40)) return (int)hipErrorInvalidValue;
@@ -657,7 +660,7 @@ PA_API int pa_conv2d_wgrad(const void* x, const void* dy, void* ws, void* dw, in
   wgrad_zsum_kernel<<<zgrid, 256, 0, st>>>((const float*)ws, part, splits, total / 4);
   const long long nb = (total + 255) / 256;
   const int blocks = (int)(nb < 2048 ? nb : 2048);
-  wgrad_reduce_kernel<<<blocks, 256, 0, st>>>(part, (uint16_t*)dw, ngroups, R * S, C, Cout);
+  wgrad_reduce_kernel<<<blocks, 256, 0, st>>>(part, (uint16_t*)dw, ngroups, R * S, C, Cout, accumulate);
   return (int)hipGetLastError();
 }
 

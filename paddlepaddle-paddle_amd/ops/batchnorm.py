@@ -7,6 +7,7 @@ updated in place with paddle's momentum convention (running = m * running + (1 -
 import torch
 
 from . import _native as N
+from ..parallel.flat_buffer import flat_grad_slot, notify_grad_ready
 
 
 def _ws(rows, cols, dt, dev):
@@ -44,6 +45,7 @@ class _BNAct(torch.autograd.Function):
         ctx.relu, ctx.has_z, ctx.training = relu, z is not None, training
         ctx.has_beta = beta is not None
         ctx.dz_sink = dz_sink
+        ctx.beta_t = beta
         return y
 
     @staticmethod
@@ -56,16 +58,42 @@ class _BNAct(torch.autograd.Function):
         dy = dy.contiguous()
         dx = torch.empty_like(x)
         dz = torch.empty_like(x) if ctx.has_z else None
-        dg = torch.empty_like(gamma) if gamma is not None else None
-        db = torch.empty_like(gamma) if (gamma is not None and ctx.has_beta) else None
+        # gamma / beta gradients straight into their flat-buffer slots (accumulated in place by the
+        # finishing kernel) when both parameters live in flat buffers; fresh tensors otherwise
+        gs, bs, gp, bp = (_slots(gamma, ctx.beta_t) if SLOT_ACCUM and gamma is not None and ctx.has_beta
+                          else (None,) * 4)
+        acc = gs is not None
+        dg = gs if acc else (torch.empty_like(gamma) if gamma is not None else None)
+        db = bs if acc else (torch.empty_like(gamma) if (gamma is not None and ctx.has_beta) else None)
         ws = _ws(rows, C, N.dtcode(x.dtype), x.device)
         N.check(N.lib.pa_bn_bwd(N.ptr(dy), N.ptr(x), N.ptr(y), N.ptr(mean), N.ptr(rstd), N.ptr(gamma), N.ptr(dx),
-                                N.ptr(dz), N.ptr(dg), N.ptr(db), N.ptr(ws), rows, C, int(ctx.relu), N.dtcode(x.dtype),
-                                N.dtcode(gamma.dtype) if gamma is not None else 0, N.stream()), 'bn_bwd')
+                                N.ptr(dz), N.ptr(dg), N.ptr(db), N.ptr(ws), rows, C, int(ctx.relu), int(acc),
+                                N.dtcode(x.dtype), N.dtcode(gamma.dtype) if gamma is not None else 0, N.stream()),
+                'bn_bwd')
+        if acc:
+            notify_grad_ready(gp)
+            notify_grad_ready(bp)
+            dg = db = None
         if dz is not None and ctx.dz_sink is not None:
             ctx.dz_sink.buf = dz  # taken by the consuming conv's dgrad (ops/conv.py GradSink)
             dz = None
         return dx, dz, dg, db, None, None, None, None, None, None, None
+
+
+SLOT_ACCUM = True  # gamma/beta gradients accumulate into flat-buffer slots in place (tests switch it)
+
+
+def _slots(gamma, beta):
+    """(gamma slot, beta slot, gamma param, beta param) when both parameters' gradients live in
+    flat buffers with the parameters' dtype, else Nones."""
+    from ..core.tensor import _PARAMS
+    gp, bp = _PARAMS.get(id(gamma)), _PARAMS.get(id(beta))
+    if gp is None or bp is None or gp._t is not gamma or bp._t is not beta:
+        return None, None, None, None
+    gs, bs = flat_grad_slot(gp), flat_grad_slot(bp)
+    if gs is None or bs is None or gs.dtype != gamma.dtype or bs.dtype != beta.dtype:
+        return None, None, None, None
+    return gs, bs, gp, bp
 
 
 def supported(x, gamma=None):

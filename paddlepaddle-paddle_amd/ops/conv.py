@@ -20,6 +20,17 @@ import os
 import torch
 
 from . import _native as N
+from ..parallel.flat_buffer import flat_grad_slot, notify_grad_ready
+
+
+SLOT_ACCUM = True  # filter gradients accumulate into flat-buffer slots in place (tests switch it)
+
+
+def _param_of(t):
+    """The paddle Parameter whose storage tensor is ``t`` (None for plain tensors)."""
+    from ..core.tensor import _PARAMS
+    p = _PARAMS.get(id(t))
+    return p if p is not None and p._t is t else None
 
 _enabled = os.environ.get('PADDLE_AMD_HIP_CONV', '1') != '0'
 _bwd_enabled = os.environ.get('PADDLE_AMD_HIP_CONV_BWD', '1') != '0'
@@ -152,9 +163,10 @@ def conv2d_dgrad_classes(dy, w, x_hw, stride, pad, dil):
     return dx
 
 
-def conv2d_wgrad_1x1(dy, x):
+def conv2d_wgrad_1x1(dy, x, out=None):
     """1x1 / stride-1 / no-padding filter gradient: dW[co, c] = sum_pixels dY[p, co] X[p, c] on the
-    hand-written GEMM (A = dY^T read with tr_b16; split-K over pixels when the output is small)."""
+    hand-written GEMM (A = dY^T read with tr_b16; split-K over pixels when the output is small).
+    out: bf16 [Cout, C, 1, 1] slot accumulated in place (beta = 1)."""
     from . import gemm
     Cout, C = dy.shape[-1], x.shape[-1]
     dy2, x2 = dy.reshape(-1, Cout), x.reshape(-1, C)
@@ -165,6 +177,8 @@ def conv2d_wgrad_1x1(dy, x):
         sk *= 2
     if not gemm.hip_mm_ok(a, x2, sk):
         return None
+    if out is not None:
+        return gemm.hip_mm(a, x2, out=out.view(Cout, C), beta=1.0, splitk=sk).view(Cout, C, 1, 1)
     return gemm.hip_mm(a, x2, splitk=sk).view(Cout, C, 1, 1)
 
 
@@ -176,13 +190,16 @@ def wgrad_ok(x, w):
     return _bwd_enabled and bool(N.lib.pa_conv2d_wgrad_ok(C, Cout))
 
 
-def conv2d_wgrad(dy, x, w_shape, stride, pad, dil):
+def conv2d_wgrad(dy, x, w_shape, stride, pad, dil, out=None):
     """Filter gradient of any R x S / stride / padding / dilation on the implicit-GEMM kernel
     (pixels are the reduction axis, split over the grid; fp32 slabs folded into the OIHW bf16
-    gradient by a second kernel)."""
+    gradient by a second kernel).  out: a bf16 [Cout, C, R, S] gradient slot the result is
+    ACCUMULATED into (returned); None -> a fresh tensor."""
     Cout, C, R, S = w_shape
     x, dy = x.contiguous(), dy.contiguous()
     if R == S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0) and C < Cout and Cout % 8 == 0:
+        if out is not None:
+            return None  # transposed form below: the caller accumulates
         # 1x1: dW = dY^T X is symmetric in (X, dY) — put the wider channel count on the 256-wide
         # tile side (a 64-channel input would leave 3/4 of every 256-row tile empty)
         return conv2d_wgrad(x, dy, (C, Cout, 1, 1), stride, pad, dil).view(C, Cout).t().contiguous().view(Cout, C, 1, 1)
@@ -195,9 +212,11 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, dil):
     want = max(1, min(_WGRAD_TARGET_BLOCKS // tiles, P // 512))
     splits = int(N.lib.pa_conv2d_wgrad_splits(Nb, Ho, Wo, want))
     ws = torch.empty((splits + -(-splits // 16)) * M * Cout, dtype=torch.float32, device=x.device)
-    dw = torch.empty(Cout, C, R, S, dtype=torch.bfloat16, device=x.device)
+    acc = out is not None
+    dw = out if acc else torch.empty(Cout, C, R, S, dtype=torch.bfloat16, device=x.device)
     N.check(N.lib.pa_conv2d_wgrad(N.ptr(x), N.ptr(dy), N.ptr(ws), N.ptr(dw), Nb, H, W, C, Cout, R, S, stride[0],
-                                  stride[1], pad[0], pad[1], dil[0], dil[1], Ho, Wo, want, N.stream()), 'conv2d_wgrad')
+                                  stride[1], pad[0], pad[1], dil[0], dil[1], Ho, Wo, want, int(acc), N.stream()),
+            'conv2d_wgrad')
     return dw
 
 
@@ -310,21 +329,37 @@ class _Conv2dNHWC(torch.autograd.Function):
                     sink = None  # accumulated in the GEMM epilogue
             if gx is None:
                 gx = conv2d_dgrad_classes(dy, w, x.shape[1:3], stride, pad, dil)
+        slot_used = False
         if ctx.needs_input_grad[1] and _bwd_enabled and _wgrad_hip and w.shape[0] % 8 == 0:
             C = w.shape[1]
+            # the weight's flat-buffer gradient slot: the kernels accumulate into it in place
+            # (no AccumulateGrad add), as the Linear weight gradient does (ops/linear.py)
+            wp = _param_of(w) if SLOT_ACCUM else None
+            slot = flat_grad_slot(wp) if wp is not None else None
+            if slot is not None and (slot.dtype != torch.bfloat16 or not slot.is_contiguous()):
+                slot = None
             if C % 8:  # RGB stem: zero channels do not change the taps of the real ones
                 xp = torch.nn.functional.pad(x, (0, 8 - C % 8))
                 gw = conv2d_wgrad(dy, xp, (w.shape[0], xp.shape[3], w.shape[2], w.shape[3]), stride, pad,
                                   dil)[:, :C].contiguous()
             else:
                 if pw and w.shape[1] >= 512 and 2 * w.shape[0] >= w.shape[1]:
-                    gw = conv2d_wgrad_1x1(dy, x)
+                    gw = conv2d_wgrad_1x1(dy, x, out=slot)
+                    slot_used = gw is not None and slot is not None
                 if gw is None:
-                    gw = conv2d_wgrad(dy, x, tuple(w.shape), stride, pad, dil)
-            gw = gw.to(w.dtype)
+                    gw = conv2d_wgrad(dy, x, tuple(w.shape), stride, pad, dil, out=slot)
+                    slot_used = gw is not None and slot is not None
+                    if gw is None:  # transposed 1x1 form: a fresh tensor
+                        gw = conv2d_wgrad(dy, x, tuple(w.shape), stride, pad, dil)
+            if slot_used:
+                notify_grad_ready(wp)
+                gw = None
+            else:
+                gw = gw.to(w.dtype)
         if has_b and ctx.needs_input_grad[2]:
             gb = dy.sum((0, 1, 2), dtype=torch.float32).to(dy.dtype)
-        mask = [ctx.needs_input_grad[0] and gx is None, ctx.needs_input_grad[1] and gw is None, False]
+        mask = [ctx.needs_input_grad[0] and gx is None, ctx.needs_input_grad[1] and gw is None and not slot_used,
+                False]
         if any(mask):  # shapes the hand-written kernels reject: MIOpen NHWC backward
             lx, lw, _ = torch.ops.aten.convolution_backward(
                 dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), w, None, list(stride), list(pad), list(dil), False,

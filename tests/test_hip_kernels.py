@@ -1055,3 +1055,48 @@ def test_resnet_identity_block_residual_grad_sink():
             R.RESIDUAL_GRAD_SINK = True
     for a, b, name in zip(grads[0], grads[1], ('dx', 'dw1', 'dw3')):
         _close(b, a, 0.05 * float(a.abs().max()) + 1e-3, 0.02, name)
+
+
+def test_conv_bn_param_grads_accumulate_in_flat_slots():
+    """Conv filter gradients (implicit-GEMM wgrad reduce and the 1x1 GEMM wgrad) and BN gamma/beta
+    gradients are accumulated straight into the optimizer's flat-buffer slots: three Momentum
+    steps match the AccumulateGrad path, and no autograd add runs for those parameters."""
+    import paddle
+    from paddle.ops import conv, batchnorm
+    paddle.set_device('gpu:0')
+    nn = paddle.nn
+
+    class Net(nn.Layer):
+        def __init__(self):
+            super().__init__()
+            self.c1 = nn.Conv2D(512, 256, 1, bias_attr=False, data_format='NHWC')   # 1x1 GEMM wgrad
+            self.b1 = nn.BatchNorm2D(256, data_format='NHWC')
+            self.c2 = nn.Conv2D(256, 256, 3, padding=1, bias_attr=False, data_format='NHWC')  # implicit GEMM
+            self.b2 = nn.BatchNorm2D(256, data_format='NHWC')
+
+        def forward(self, x):
+            from paddle.vision.models.resnet import _bn_act
+            return _bn_act(self.b2, self.c2(_bn_act(self.b1, self.c1(x))))
+
+    finals = []
+    for on in (False, True):
+        conv.SLOT_ACCUM = batchnorm.SLOT_ACCUM = on
+        try:
+            paddle.seed(5)
+            net = Net()
+            opt = paddle.optimizer.Momentum(learning_rate=0.05, momentum=0.9, parameters=net.parameters(),
+                                            multi_precision=True)
+            net, opt = paddle.amp.decorate(net, opt, level='O2', dtype='bfloat16')
+            g = torch.Generator(device=DEV).manual_seed(6)
+            x = paddle.to_tensor(torch.randn(8, 14, 14, 512, device=DEV, generator=g).bfloat16())
+            tgt = paddle.to_tensor(torch.randn(8, 14, 14, 256, device=DEV, generator=g).bfloat16())
+            for _ in range(3):
+                loss = ((net(x).astype('float32') - tgt.astype('float32')) ** 2).mean()
+                loss.backward()
+                opt.step()
+                opt.clear_grad()
+            finals.append([p._t.float().clone() for p in net.parameters()])
+        finally:
+            conv.SLOT_ACCUM = batchnorm.SLOT_ACCUM = True
+    for a, b in zip(*finals):
+        _close(b, a, 0.02 * float(a.abs().max()) + 1e-3, 0.02, 'param after 3 steps')
