@@ -1095,7 +1095,7 @@ def test_conv_bn_param_grads_accumulate_in_flat_slots():
                 loss.backward()
                 opt.step()
                 opt.clear_grad()
-            finals.append([p._t.float().clone() for p in net.parameters()])
+            finals.append([p._t.detach().float().clone() for p in net.parameters()])
         finally:
             conv.SLOT_ACCUM = batchnorm.SLOT_ACCUM = True
     for a, b in zip(*finals):
