@@ -338,6 +338,7 @@ struct FusedArgs {  // the fused (bias +) dropout + residual path; drop == false
   void* xbgrad;       // backward: bias gradient (nullable), dtype code xbgd, accumulated if xbaccum
   int xbgd, xbaccum;
   DropSpec dsp;
+  int wacc = 0;       // backward: dw / db accumulated (+=) into the parameters' gradient slots
 };
 
 template <typename T, typename WT, bool RMS>
@@ -411,8 +412,9 @@ hipError_t launch_bwd(const void* dy, const void* x, const void* w, const float*
 #undef PA_NB
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  e = launch_colsum_finish<WT>(dw_part, dw, nparts, cols, 0, st);
-  if (e == hipSuccess && !RMS && db != nullptr) e = launch_colsum_finish<WT>(db_part, db, nparts, cols, 0, st);
+  const int wacc = fa != nullptr ? fa->wacc : 0;
+  e = launch_colsum_finish<WT>(dw_part, dw, nparts, cols, wacc, st);
+  if (e == hipSuccess && !RMS && db != nullptr) e = launch_colsum_finish<WT>(db_part, db, nparts, cols, wacc, st);
   if (e == hipSuccess && xb_part != nullptr)
     e = launch_colsum_finish_dt(xb_part, fa->xbgrad, fa->xbgd, nparts, cols, fa->xbaccum, st);
   if (e != hipSuccess) return e;
@@ -485,11 +487,11 @@ PA_API hipError_t pa_dropout_add_norm_fwd(const void* x, const void* xbias, cons
 // `part` holds 3 * pa_norm_bwd_nparts(rows) * cols floats.
 PA_API hipError_t pa_dropout_add_norm_bwd(const void* dy, const void* s, const void* w, const float* mean,
                                           const float* rstd, const void* dsum, void* dres, void* dx, float* part,
-                                          void* dw, void* db, void* xbgrad, int xbgd, int xbaccum, int rows, int cols,
-                                          int rms, float p, uint32_t seed, uint32_t offset, int xd, int wd,
+                                          void* dw, void* db, void* xbgrad, int xbgd, int xbaccum, int wacc, int rows,
+                                          int cols, int rms, float p, uint32_t seed, uint32_t offset, int xd, int wd,
                                           hipStream_t st) {
   const int np = pa_norm_bwd_nparts(rows);
-  FusedArgs fa{true, nullptr, dx, xbgrad, xbgd, xbaccum, DropSpec{p, seed, offset}};
+  FusedArgs fa{true, nullptr, dx, xbgrad, xbgd, xbaccum, DropSpec{p, seed, offset}, wacc};
   if (rms) {
     PA_NORM_DISPATCH(xd, wd, true,
                      (launch_bwd<T, WT, true>(dy, s, w, nullptr, rstd, dsum, dres, part, dw, nullptr, rows, cols, np,

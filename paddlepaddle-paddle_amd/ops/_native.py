@@ -29,7 +29,7 @@ _SIGS = {
     'pa_rmsnorm_bwd': [P, P, P, P, P, P, P, P, I, I, I, I, P],
     'pa_norm_bwd_nparts': [I],
     'pa_dropout_add_norm_fwd': [P, P, P, P, P, P, P, P, P, I, I, F, I, F, U32, U32, I, I, P],
-    'pa_dropout_add_norm_bwd': [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, U32, U32, I, I, P],
+    'pa_dropout_add_norm_bwd': [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U32, U32, I, I, P],
     'pa_colsum_nparts': [I, I, I],
     'pa_bias_act_bwd_dbias': [I, P, P, P, P, P, P, I, I, I, I, I, P],
     'pa_colsum': [P, P, P, I, I, I, I, I, P],

@@ -126,6 +126,7 @@ class _DropAddNorm(torch.autograd.Function):
         ctx.save_for_backward(s, w, mean, rstd, xb)
         ctx.seed, ctx.off, ctx.p, ctx.rms, ctx.boxes = seed, off, p, rms, boxes
         ctx.has_b, ctx.has_xb = b is not None, xb is not None
+        ctx.b_t = b
         return y, s
 
     @staticmethod
@@ -138,8 +139,15 @@ class _DropAddNorm(torch.autograd.Function):
         dres, dx = torch.empty_like(s), torch.empty_like(s)
         np_ = N.lib.pa_norm_bwd_nparts(rows)
         part = torch.empty(3 * np_ * cols, dtype=torch.float32, device=s.device)
-        dw = torch.empty_like(w)
-        db = torch.empty_like(w) if ctx.has_b and not ctx.rms else None
+        # norm weight / bias gradients accumulate (+=) straight into their flat-buffer slots when the
+        # parameters live there (no AccumulateGrad add per parameter)
+        wslots = _norm_slots(w, ctx.b_t if ctx.has_b and not ctx.rms else None)
+        wacc = wslots is not None
+        if wacc:
+            dw, db = wslots[0], wslots[1]
+        else:
+            dw = torch.empty_like(w)
+            db = torch.empty_like(w) if ctx.has_b and not ctx.rms else None
         xb_box = ctx.boxes[0] if ctx.boxes else None
         xb_out, xb_acc, xb_slot = None, 0, None
         if ctx.has_xb and ctx.needs_input_grad[1]:
@@ -147,9 +155,13 @@ class _DropAddNorm(torch.autograd.Function):
             xb_out, xb_acc = (xb_slot, 1) if xb_slot is not None else (torch.empty_like(xb), 0)
         N.check(N.lib.pa_dropout_add_norm_bwd(N.ptr(dy), N.ptr(s), N.ptr(w), N.ptr(mean), N.ptr(rstd), N.ptr(ds),
                                               N.ptr(dres), N.ptr(dx), N.ptr(part), N.ptr(dw), N.ptr(db), N.ptr(xb_out),
-                                              N.dtcode(xb_out.dtype) if xb_out is not None else 0, xb_acc, rows, cols,
-                                              int(ctx.rms), ctx.p, ctx.seed, ctx.off, N.dtcode(s.dtype),
+                                              N.dtcode(xb_out.dtype) if xb_out is not None else 0, xb_acc, int(wacc),
+                                              rows, cols, int(ctx.rms), ctx.p, ctx.seed, ctx.off, N.dtcode(s.dtype),
                                               N.dtcode(w.dtype), N.stream()), 'dropout_add_norm_bwd')
+        if wacc:
+            for prm in wslots[2]:
+                notify_grad_ready(prm)
+            dw = db = None
         dxb = None
         if xb_out is not None:
             if xb_slot is not None:
@@ -157,6 +169,31 @@ class _DropAddNorm(torch.autograd.Function):
             else:
                 dxb = xb_out
         return dx, dxb, dres, dw, db, None, None, None, None
+
+
+SLOT_ACCUM = True  # norm weight/bias gradients into flat-buffer slots (tests switch it)
+
+
+def _norm_slots(w, b):
+    """(w slot, b slot or None, params) when the norm parameters' gradients live in flat buffers
+    of their own dtype, else None."""
+    if not SLOT_ACCUM:
+        return None
+    from ..core.tensor import _PARAMS
+    out, prms = [], []
+    for t in (w, b):
+        if t is None:
+            out.append(None)
+            continue
+        p = _PARAMS.get(id(t))
+        if p is None or p._t is not t:
+            return None
+        g = flat_grad_slot(p)
+        if g is None or g.dtype != t.dtype or not g.is_contiguous():
+            return None
+        out.append(g)
+        prms.append(p)
+    return out[0], out[1], prms
 
 
 def dropout_add_norm_ok(x, w, p):

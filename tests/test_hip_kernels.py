@@ -1100,3 +1100,35 @@ def test_conv_bn_param_grads_accumulate_in_flat_slots():
             conv.SLOT_ACCUM = batchnorm.SLOT_ACCUM = True
     for a, b in zip(*finals):
         _close(b, a, 0.02 * float(a.abs().max()) + 1e-3, 0.02, 'param after 3 steps')
+
+
+def test_gpt_norm_param_grads_accumulate_in_flat_slots():
+    """LayerNorm weight/bias gradients of the fused dropout+residual+LN backward accumulate into
+    the flat-buffer slots: three AdamW steps of a GPT-tiny match the AccumulateGrad path."""
+    import paddle
+    from paddle.ops import fused
+    from paddle.models.gpt import gpt_config, GPTForPretraining
+    paddle.set_device('gpu:0')
+    finals = []
+    for on in (False, True):
+        fused.SLOT_ACCUM = on
+        try:
+            paddle.seed(11)
+            cfg = gpt_config('gpt-tiny', hidden_dropout_prob=0.1, attention_probs_dropout_prob=0.0)
+            model = GPTForPretraining(cfg)
+            opt = paddle.optimizer.AdamW(learning_rate=1e-3, parameters=model.parameters(), multi_precision=True)
+            model, opt = paddle.amp.decorate(model, opt, level='O2', dtype='bfloat16')
+            paddle.seed(12)
+            ids = paddle.randint(0, cfg.vocab_size, [4, 129])
+            for _ in range(3):
+                loss = model.loss(model(ids[:, :-1]), ids[:, 1:])
+                loss.backward()
+                opt.step()
+                opt.clear_grad()
+            finals.append({n: p._t.detach().float().clone() for n, p in model.named_parameters() if 'norm' in n})
+        finally:
+            fused.SLOT_ACCUM = True
+    assert finals[0]
+    for n in finals[0]:
+        a, b = finals[0][n], finals[1][n]
+        _close(b, a, 1e-2 * float(a.abs().max()) + 1e-4, 1e-2, n)
