@@ -202,7 +202,8 @@ __device__ __forceinline__ void mask_row4(const Extra& ex, int b, int h, int q, 
 // four consecutive keys (8-bit keep test, as the reference's flash-attn kernels quantise p to a
 // uint8 threshold).  The forward and dQ kernels own 4 consecutive keys of one query per lane, so
 // they pay ONE hash per 4 elements (drop_bits + drop_sub); dK/dV (4 consecutive queries of one
-// key per lane) regenerates per element (drop_z) — same bits, same mask.
+// key per lane) hashes one query per lane and shares the words across the key quad with DPP —
+// same bits, same mask (drop_z is the per-element reference form).
 __device__ __forceinline__ uint32_t drop_bits(const Extra& ex, int bh, int q, int k) {
   return hash3(ex.seed ^ (uint32_t)bh * 0x9E3779B9u, ex.offset + (uint32_t)q, (uint32_t)k >> 2);
 }
@@ -638,6 +639,17 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int mykey = kw + 16 * j + (lane & 15);
+        // dropout: the four lanes of a quad hold keys 4c..4c+3 of the same four queries, so each
+        // lane hashes ONE (query 4g + (lane & 3), key quad) and the quad shares the four words
+        // through DPP quad broadcasts (1 hash per lane instead of 4; same bits as drop_z)
+        uint32_t hq[4] = {0u, 0u, 0u, 0u};
+        if constexpr ((EXT & 4) != 0) {
+          const int hmine = (int)drop_bits(ex, b * Hq + h, q0 + 16 * m + 4 * g + (lane & 3), kw + 16 * j + (lane & 12));
+          hq[0] = (uint32_t)__builtin_amdgcn_mov_dpp(hmine, 0x00, 0xF, 0xF, false);
+          hq[1] = (uint32_t)__builtin_amdgcn_mov_dpp(hmine, 0x55, 0xF, 0xF, false);
+          hq[2] = (uint32_t)__builtin_amdgcn_mov_dpp(hmine, 0xAA, 0xF, 0xF, false);
+          hq[3] = (uint32_t)__builtin_amdgcn_mov_dpp(hmine, 0xFF, 0xF, 0xF, false);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = q0 + 16 * m + 4 * g + r;
@@ -660,7 +672,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
           }
           if constexpr ((EXT & 8) != 0) p = q >= rstart[j] ? 0.f : p;
           float z = 1.f;
-          if constexpr ((EXT & 4) != 0) z = drop_z(ex, b * Hq + h, q, mykey);
+          if constexpr ((EXT & 4) != 0) z = drop_sub(ex, hq[r], mykey & 3);
           const float ds = p * (acc_dp[j][m][r] * z - dlv[r]);
           pb[j][m >> 1][(m & 1) * 4 + r] = f2s<T>(p * z);
           db_[j][m >> 1][(m & 1) * 4 + r] = f2s<T>(ds);

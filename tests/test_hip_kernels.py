@@ -437,7 +437,7 @@ def test_dropout_add_norm_fwd_bwd(rms, shape):
     dyb, dsb = dy.to(bf), dsum.to(bf)  # keep both alive across the call (no allocator reuse)
     N.check(N.lib.pa_dropout_add_norm_bwd(N.ptr(dyb), N.ptr(s), N.ptr(w), N.ptr(mean), N.ptr(rstd),
                                           N.ptr(dsb), N.ptr(dres), N.ptr(dx), N.ptr(part), N.ptr(dw),
-                                          N.ptr(db), N.ptr(dxb), 0, 1, rows, cols, int(rms), p, seed, off,
+                                          N.ptr(db), N.ptr(dxb), 0, 1, 0, rows, cols, int(rms), p, seed, off,
                                           N.dtcode(bf), N.dtcode(bf), N.stream()), 'bwd')
     _close(dres, rr.grad, 8e-2, 2e-2, 'dres')
     _close(dx, xr.grad, 8e-2, 2e-2, 'dx')
