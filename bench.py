@@ -34,6 +34,9 @@ def parse():
                     help='attention-probability dropout (in-kernel in csrc/flash_attn.hip)')
     ap.add_argument('--resnet-batch', type=int, default=256)
     ap.add_argument('--no-resnet', action='store_true')
+    ap.add_argument('--graph', action='store_true',
+                    help='replay the whole training step as one captured hipGraph (steps without dropout; '
+                         'device/cuda/graphs.py TrainStepGraph)')
     return ap.parse_args()
 
 
@@ -107,6 +110,17 @@ def build_resnet(args, world, rank, dev):
     return step, B * world, 'samples/sec ResNet50 bf16', 'samples/s', mcfg
 
 
+def _maybe_graph(args, step, cfg):
+    """--graph: the step as one captured hipGraph, captured inside the untimed warmup."""
+    if not args.graph or args.warmup < 2:
+        return step
+    if cfg.get('hidden_dropout', 0) or cfg.get('attention_dropout', 0):
+        return step  # host-drawn dropout seeds cannot be frozen into a graph
+    from paddle.device.cuda.graphs import capture_train_step
+    cfg['hip_graph'] = True
+    return capture_train_step(step, warmup=args.warmup - 1)
+
+
 def measure(step, steps, warmup, world, rank, dev, tag):
     """W untimed warmup steps, then K timed steps bracketed by barrier + device sync; MAX over ranks."""
     import torch
@@ -157,6 +171,7 @@ def main():
 
     build = build_gpt if args.model.startswith('gpt') else build_resnet
     step, work, metric, unit, mcfg = build(args, world, rank, dev)
+    step = _maybe_graph(args, step, mcfg)
     ms, final_loss = measure(step, args.steps, args.warmup, world, rank, dev, args.model)
     value = work / (ms / 1e3)
     out = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": args.steps,
@@ -170,6 +185,7 @@ def main():
         gc.collect()
         torch.cuda.empty_cache()
         rstep, rwork, _, runit, rcfg = build_resnet(args, world, rank, dev)
+        rstep = _maybe_graph(args, rstep, rcfg)
         rms, rloss = measure(rstep, args.steps, args.warmup, world, rank, dev, 'resnet50')
         out["resnet50"] = {"metric": "samples/sec ResNet50 bf16", "value": round(rwork / (rms / 1e3), 2),
                            "unit": runit, "ms_per_step": round(rms, 3), "config": rcfg, "final_loss": round(rloss, 4)}

@@ -6,7 +6,7 @@ import torch
 from . import allocator as native_allocator
 
 from .. import Stream, Event, current_stream, synchronize as _sync, stream_guard as _sg, _dev  # noqa: F401
-from .graphs import CUDAGraph, is_cuda_graph_supported, wrap_cuda_graph  # noqa: F401
+from .graphs import CUDAGraph, is_cuda_graph_supported, wrap_cuda_graph, capture_train_step, TrainStepGraph  # noqa: F401
 
 
 def synchronize(device=None):

@@ -1,10 +1,12 @@
 """HIP graph capture/replay (reference: python/paddle/device/cuda/graphs.py CUDAGraph,
-cuda_graphed_layer.py).
+cuda_graphed_layer.py; the role CINN's whole-graph compilation plays for the reference's
+static training, here done by replaying a captured hipGraph).
 
-Launch-bound inner loops (small decode steps, optimizer sweeps over many tensors) are captured
-once into a hipGraph and replayed with one launch.  Inputs are copied into static buffers; all
-kernels of the captured region (including this framework's ctypes-launched HIP kernels, which
-launch on the current — i.e. capturing — stream) become graph nodes.
+Launch-bound inner loops (small decode steps, optimizer sweeps over many tensors) and whole
+TRAINING STEPS (forward + backward + fused optimizer, ``TrainStepGraph``) are captured once into a
+hipGraph and replayed with one launch.  Inputs are copied into static buffers; all kernels of the
+captured region (including this framework's ctypes-launched HIP kernels, which launch on the
+current — i.e. capturing — stream) become graph nodes.
 """
 import torch
 
@@ -118,3 +120,62 @@ class _Graphed:
 
 def wrap_cuda_graph(function, mode="thread_local", memory_pool="default"):
     return _Graphed(function)
+
+
+class TrainStepGraph:
+    """A whole training step (``step_fn()``: forward, loss, backward, optimizer step, clear_grad,
+    returning the loss) captured into one hipGraph and replayed per call.
+
+    The first ``warmup`` calls run eagerly on a side stream (allocator pools, flat-buffer set-up,
+    library kernel selection and lazily-built optimizer state all happen there, none inside the
+    capture); the next call captures; every later call is ``graph.replay()``.  ``step_fn`` must
+    read its inputs from fixed tensors (copy the next batch into them before calling) and must not
+    synchronise with the host; per-step host values frozen at capture are refused: dropout inside
+    the step raises (its seeds are drawn on the host), and the learning rate must stay constant or
+    live in a device tensor.  Returns the static loss tensor (its value updates on every replay).
+    """
+
+    def __init__(self, step_fn, warmup=3):
+        self.step_fn = step_fn
+        self.warmup = warmup
+        self.calls = 0
+        self.graph = None
+        self.out = None
+
+    def __call__(self):
+        if not torch.cuda.is_available():
+            return self.step_fn()
+        if self.graph is not None:
+            self.graph.replay()
+            return self.out
+        self.calls += 1
+        if self.calls <= self.warmup:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                out = self.step_fn()
+            torch.cuda.current_stream().wait_stream(s)
+            return out
+        torch.cuda.synchronize()
+        g = CUDAGraph()
+        g.capture_begin()
+        try:
+            self.out = self.step_fn()
+        finally:
+            g.capture_end()
+        self.graph = g
+        g.replay()  # the captured step has not executed yet: run it once for this call
+        return self.out
+
+
+def capture_train_step(step_fn, warmup=3):
+    """``TrainStepGraph(step_fn, warmup)``: the training step as one replayable hipGraph."""
+    return TrainStepGraph(step_fn, warmup)
+
+
+def host_rng_guard(what):
+    """Raise when a kernel would freeze a host-drawn dropout seed into a graph being captured."""
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        raise RuntimeError(f"{what}: dropout seeds are drawn on the host and would be frozen into the "
+                           "captured graph (every replay would reuse one mask); capture the step without "
+                           "dropout or run it eagerly")

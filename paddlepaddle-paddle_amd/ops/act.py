@@ -103,6 +103,8 @@ def swiglu(a, b):
 
 def _next_seed(n):
     """(seed, offset) from the paddle.seed-controlled host generator (see ops.fused._next_seed)."""
+    from ..device.cuda.graphs import host_rng_guard
+    host_rng_guard('dropout_add')
     seed, off = torch.randint(0, 2 ** 31 - 1, (2,), device='cpu').tolist()
     return seed, off
 

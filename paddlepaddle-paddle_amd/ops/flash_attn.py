@@ -147,6 +147,8 @@ def _rows_args(rows, B, H, Sk):
 
 
 def _seed():
+    from ..device.cuda.graphs import host_rng_guard
+    host_rng_guard('flash attention dropout')
     return int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
 
 

@@ -106,6 +106,8 @@ def _next_seed():
     """(seed, offset) of one dropout call, both drawn from the host generator, so paddle.seed
     fully determines every keep-mask (reference: the per-op seed/offset pair of the CUDA
     dropout kernels, derived from the paddle.seed-controlled generator)."""
+    from ..device.cuda.graphs import host_rng_guard
+    host_rng_guard('fused dropout + residual + norm')
     s, o = torch.randint(0, 2 ** 31 - 1, (2,), device='cpu').tolist()
     return s, o
 

@@ -1132,3 +1132,45 @@ def test_gpt_norm_param_grads_accumulate_in_flat_slots():
     for n in finals[0]:
         a, b = finals[0][n], finals[1][n]
         _close(b, a, 1e-2 * float(a.abs().max()) + 1e-4, 1e-2, n)
+
+
+def test_train_step_hip_graph_matches_eager():
+    """A whole training step (conv + fused BN + 1x1 GEMM conv + Momentum on flat buffers) captured
+    into one hipGraph replays to the same parameters as eager steps; dropout refuses capture."""
+    import paddle
+    from paddle.device.cuda.graphs import capture_train_step
+    paddle.set_device('gpu:0')
+    nn = paddle.nn
+    finals = []
+    for graphed in (False, True):
+        paddle.seed(21)
+        net = nn.Sequential(nn.Conv2D(64, 128, 3, padding=1, bias_attr=False, data_format='NHWC'),
+                            nn.BatchNorm2D(128, data_format='NHWC'), nn.ReLU(),
+                            nn.Conv2D(128, 256, 1, bias_attr=False, data_format='NHWC'),
+                            nn.AdaptiveAvgPool2D(1, data_format='NHWC'), nn.Flatten(), nn.Linear(256, 10))
+        opt = paddle.optimizer.Momentum(learning_rate=0.05, momentum=0.9, parameters=net.parameters(),
+                                        multi_precision=True)
+        net, opt = paddle.amp.decorate(net, opt, level='O2', dtype='bfloat16')
+        g = torch.Generator(device=DEV).manual_seed(22)
+        x = paddle.to_tensor(torch.randn(16, 16, 16, 64, device=DEV, generator=g).bfloat16())
+        y = paddle.to_tensor(torch.randint(0, 10, (16,), device=DEV, generator=g))
+
+        def step():
+            loss = paddle.nn.functional.cross_entropy(net(x), y)
+            loss.backward()
+            opt.step()
+            opt.clear_grad()
+            return loss
+        run = capture_train_step(step, warmup=2) if graphed else step
+        losses = [float(run()) for _ in range(6)]
+        assert all(l == l for l in losses)
+        finals.append([p._t.detach().float().clone() for p in net.parameters()])
+    for a, b in zip(*finals):
+        _close(b, a, 1e-2 * float(a.abs().max()) + 1e-3, 1e-2, 'graph-replayed params')
+
+    def bad_step():
+        return paddle.incubate.nn.functional.fused_dropout_add(paddle.ones([64, 64]), paddle.ones([64, 64]), 0.5)
+    r = capture_train_step(bad_step, warmup=1)
+    r()
+    with pytest.raises(RuntimeError):
+        r()
