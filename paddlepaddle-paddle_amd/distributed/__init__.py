@@ -30,32 +30,8 @@ def gloo_release():
         _d.destroy_process_group()
 
 
-class _PSOnly:
-    """Parameter-server datasets / sparse-table entries: out of scope for the collective design."""
-
-    def __init__(self, *a, **k):
-        raise NotImplementedError(f"{type(self).__name__} belongs to parameter-server mode, which this "
-                                  "MI355X collective framework does not implement")
-
-
-class InMemoryDataset(_PSOnly):
-    pass
-
-
-class QueueDataset(_PSOnly):
-    pass
-
-
-class CountFilterEntry(_PSOnly):
-    pass
-
-
-class ShowClickEntry(_PSOnly):
-    pass
-
-
-class ProbabilityEntry(_PSOnly):
-    pass
+from .fleet.dataset import (InMemoryDataset, QueueDataset, CountFilterEntry, ProbabilityEntry,  # noqa: E402,F401
+                            ShowClickEntry)
 import importlib as _il
 
 

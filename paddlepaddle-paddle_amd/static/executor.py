@@ -319,8 +319,33 @@ class Executor:
     def close(self):
         pass
 
-    def train_from_dataset(self, *a, **k):
-        raise NotImplementedError("dataset-driven training uses paddle.io.DataLoader + Executor.run")
+    def train_from_dataset(self, program=None, dataset=None, scope=None, thread=0, debug=False, fetch_list=None,
+                           fetch_info=None, print_period=100, fetch_handler=None):
+        """Run ``program`` over every batch of a fleet dataset (reference base/executor.py
+        train_from_dataset): the dataset parses its slot files into feeds of its ``use_var``
+        variables; ``fetch_list`` values are printed every ``print_period`` batches (labelled by
+        ``fetch_info``) and handed to ``fetch_handler.handler`` when given.  Returns the last
+        batch's fetches."""
+        return self._run_from_dataset(program, dataset, fetch_list, fetch_info, print_period, fetch_handler, debug)
+
+    def infer_from_dataset(self, program=None, dataset=None, scope=None, thread=0, debug=False, fetch_list=None,
+                           fetch_info=None, print_period=100, fetch_handler=None):
+        """As train_from_dataset, for a program without an optimizer (reference infer_from_dataset)."""
+        return self._run_from_dataset(program, dataset, fetch_list, fetch_info, print_period, fetch_handler, debug)
+
+    def _run_from_dataset(self, program, dataset, fetch_list, fetch_info, print_period, fetch_handler, debug):
+        if dataset is None:
+            raise RuntimeError("dataset is needed and should be initialized")
+        fetch_list = list(fetch_list or [])
+        fetch_info = list(fetch_info or [getattr(f, 'name', str(i)) for i, f in enumerate(fetch_list)])
+        last = []
+        for bi, feed in enumerate(dataset._iter_batches()):
+            last = self.run(program, feed=feed, fetch_list=fetch_list) if fetch_list else self.run(program, feed=feed)
+            if fetch_list and print_period and (bi + 1) % print_period == 0:
+                print(", ".join(f"{n}: {v}" for n, v in zip(fetch_info, last)), flush=True)
+            if fetch_handler is not None and fetch_list:
+                fetch_handler.handler(dict(zip(fetch_info, last)))
+        return last
 
 
 ParallelExecutor = Executor

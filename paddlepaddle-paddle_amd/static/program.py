@@ -411,6 +411,7 @@ def data(name, shape, dtype=None, lod_level=0):
     prog.feeds[name] = (vid, _static_shape(shape), dt)
     v = _wrap(t)
     v._name = name
+    v.__dict__['_lod_level'] = int(lod_level or 0)
     prog.named_vars[name] = v
     return v
 
