@@ -6,6 +6,7 @@ One process per MI355X: rank/world/local-rank come from the launcher's environme
 RANK / WORLD_SIZE / LOCAL_RANK of torch.distributed.run); the default backend is RCCL
 ("nccl") when a GPU is visible, gloo otherwise.
 """
+import atexit
 import datetime
 import os
 
@@ -71,6 +72,16 @@ class ParallelEnv:
     dev_id = device_id
 
 
+def _destroy_at_exit():
+    """Tear the process group down before interpreter teardown: a rank that exits with gloo's
+    pair threads still joinable dies in std::terminate (exit status -6) after finishing its work."""
+    try:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    except Exception:  # exit path: never mask the program's own status
+        pass
+
+
 def init_parallel_env(backend=None, timeout_s=None):
     """Initialise the global process group (idempotent); returns the global Group."""
     env = ParallelEnv()
@@ -89,6 +100,7 @@ def init_parallel_env(backend=None, timeout_s=None):
             torch.cuda.set_device(env.local_rank % max(torch.cuda.device_count(), 1))
             kw['device_id'] = torch.device('cuda', torch.cuda.current_device())
         dist.init_process_group(be, rank=env.rank, world_size=env.world_size, **kw)
+        atexit.register(_destroy_at_exit)
         from ..core import place
         if be == 'nccl':
             place.set_device(f'gpu:{torch.cuda.current_device()}')
