@@ -263,3 +263,42 @@ def test_ernie_static_executor_amp_o2_gpu(static_mode):
         assert np.isfinite(losses).all() and losses[-1] < losses[0] * 0.6, losses
     finally:
         paddle.set_device('cpu')
+
+
+def test_static_auc_and_ctr_metric_bundle():
+    """static.auc accumulates ROC histograms across Executor runs (global AUC == the dygraph
+    paddle.metric.Auc over all batches; batch AUC over the last slide_steps batches) and
+    ctr_metric_bundle accumulates its six sums."""
+    import numpy as np
+    import paddle
+    paddle.enable_static()
+    try:
+        main, start = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, start):
+            pred = paddle.static.data('pred', [None, 2], 'float32')
+            lab = paddle.static.data('lab', [None, 1], 'int64')
+            auc_out, batch_auc, stats = paddle.static.auc(pred, lab, num_thresholds=255, slide_steps=2)
+            sq, ab, pr, q, pos, ins = paddle.static.ctr_metric_bundle(pred[:, 1:2], lab)
+        exe = paddle.static.Executor()
+        rs = np.random.RandomState(0)
+        ref = paddle.metric.Auc(num_thresholds=255)
+        ref_last2 = []
+        tot = np.zeros(6)
+        for _ in range(4):
+            y = rs.randint(0, 2, (64, 1)).astype('int64')
+            p1 = np.clip(0.5 * y[:, 0] + 0.5 * rs.rand(64), 0, 1).astype('float32')
+            pv = np.stack([1 - p1, p1], 1)
+            a, b, s_sq, s_pos, s_ins = exe.run(main, feed={'pred': pv, 'lab': y},
+                                               fetch_list=[auc_out, batch_auc, sq, pos, ins])
+            ref.update(pv, y)
+            ref_last2 = (ref_last2 + [(pv, y)])[-2:]
+            tot += [((p1 - y[:, 0]) ** 2).sum(), 0, 0, 0, y.sum(), 64]
+        np.testing.assert_allclose(float(a), ref.accumulate(), rtol=1e-5)
+        r2 = paddle.metric.Auc(num_thresholds=255)
+        for pv, y in ref_last2:
+            r2.update(pv, y)
+        np.testing.assert_allclose(float(b), r2.accumulate(), rtol=1e-5)
+        np.testing.assert_allclose(float(s_sq.reshape(-1)[0]), tot[0], rtol=1e-4)
+        assert float(s_pos.reshape(-1)[0]) == tot[4] and float(s_ins.reshape(-1)[0]) == tot[5]
+    finally:
+        paddle.disable_static()
