@@ -258,6 +258,41 @@ def _full_width(cs, D, neox):
     return torch.cat([cs, cs], -1) if neox else cs.repeat_interleave(2, -1)
 
 
+def _quant_out(o, out_scale, out_shift, out_smooth, round_type, max_bound, min_bound):
+    """int8 output quantisation of the fused inference kernels: ((o + shift) * smooth) scaled by
+    max_bound * out_scale, rounded (type 0: half to even, 1: half away from zero) and clipped."""
+    f = o.float()
+    if out_shift is not None:
+        f = f + _u(out_shift).float().reshape(1, -1)
+    if out_smooth is not None:
+        f = f * _u(out_smooth).float().reshape(1, -1)
+    v = f * (max_bound * out_scale)
+    v = torch.round(v) if round_type == 0 else torch.sign(v) * torch.floor(v.abs() + 0.5)
+    return v.clamp(min_bound, max_bound).to(torch.int8)
+
+
+def _compute_dtype(compute_dtype, *likes):
+    m = {'bf16': torch.bfloat16, 'fp16': torch.float16, 'fp32': torch.float32}
+    if compute_dtype in m:
+        return m[compute_dtype]
+    for t in likes:
+        if t is not None and t.is_floating_point():
+            return t.dtype
+    return torch.float32
+
+
+def _beam_gather(cache, beam_off, B, L):
+    """Per-(beam, position) source rows: row b = bi * beam + j reads position p from row
+    bi * beam + beam_off[bi, j, p] (the cache of the beam it descends from)."""
+    nb = _u(beam_off).shape[1]
+    base = (torch.arange(B, device=cache.device) // nb * nb)[:, None]
+    src = base + _u(beam_off).reshape(B, -1)[:, :L].long()                        # [B, L]
+    pos = torch.arange(L, device=cache.device)[None, :].expand(B, L)
+    k = cache[0].permute(0, 2, 1, 3)[src, pos].permute(0, 2, 1, 3).contiguous()  # [B, H, L, D]
+    v = cache[1].permute(0, 2, 1, 3)[src, pos].permute(0, 2, 1, 3).contiguous()
+    return k, v
+
+
 def masked_multihead_attention(x, cache_kv=None, bias=None, src_mask=None, cum_offsets=None, sequence_lengths=None,
                                rotary_tensor=None, beam_cache_offset=None, qkv_out_scale=None, out_shift=None,
                                out_smooth=None, seq_len=1, rotary_emb_dims=0, use_neox_rotary_style=False,
@@ -270,12 +305,18 @@ def masked_multihead_attention(x, cache_kv=None, bias=None, src_mask=None, cum_o
     attends over positions [0, t]).  bias [3, H, D], src_mask additive [B, 1, 1, >= t+1],
     rotary_tensor [2, B, 1|seq, ..., D] (cos, sin).  Returns (out [B, H*D], cache_kv).  The
     attention runs on the split-K HIP decode kernel (csrc/decode_attn.hip); the cache layout is
-    the natural [B, H, L, D] (the reference's CUDA kernel keeps K as [B, H, D/8, L, 8])."""
-    if beam_cache_offset is not None or qkv_out_scale is not None or out_scale > 0:
-        raise NotImplementedError("masked_multihead_attention: beam offsets / int8 quantised paths are not supported")
+    the natural [B, H, L, D] (the reference's CUDA kernel keeps K as [B, H, D/8, L, 8]).
+
+    Quantised serving paths: ``qkv_out_scale`` [3, H, D] dequantises an int32 ``x`` (the int8 QKV
+    GEMM's accumulator); ``out_scale > 0`` quantises the output to int8 after ``out_shift`` /
+    ``out_smooth`` (round type and bounds as the reference).  Beam search: ``beam_cache_offset``
+    [B / beam, beam, L] names, per beam and past position, the beam whose cache row holds that
+    position; the call then returns (out, cache_kv, beam_cache_offset)."""
     t = _u(x)
     cache = _u(cache_kv)
     _, B, H, L, D = cache.shape
+    if qkv_out_scale is not None:  # int32 accumulator -> real values
+        t = (t.float() * _u(qkv_out_scale).float().reshape(1, -1)).to(_compute_dtype(compute_dtype, cache))
     qkv = t.reshape(B, 3, H, D)
     if sequence_lengths is not None:
         step = _u(sequence_lengths).reshape(-1).to(torch.int32)
@@ -304,8 +345,22 @@ def masked_multihead_attention(x, cache_kv=None, bias=None, src_mask=None, cum_o
     mask = None
     if src_mask is not None:
         mask = _u(src_mask).reshape(B, -1).float()
-    o = ops.decode.decode_attention(q, cache[0], cache[1], lens, mask=mask, q_bias=bq)
-    return _w(o.reshape(B, H * D)), _w(cache)
+    if beam_cache_offset is not None:
+        Lu = int(lens.max())
+        kg, vg = _beam_gather(cache, beam_cache_offset, B, Lu)
+        cur = step.long().clamp_min(0)  # the new token's K/V live in its own row
+        ar = torch.arange(B, device=t.device)
+        kg[ar, :, cur] = cache[0][ar, :, cur]
+        vg[ar, :, cur] = cache[1][ar, :, cur]
+        o = ops.decode.decode_attention(q, kg, vg, lens, mask=mask, q_bias=bq)
+    else:
+        o = ops.decode.decode_attention(q, cache[0], cache[1], lens, mask=mask, q_bias=bq)
+    o = o.reshape(B, H * D)
+    if out_scale > 0:
+        o = _quant_out(o, out_scale, out_shift, out_smooth, quant_round_type, quant_max_bound, quant_min_bound)
+    if beam_cache_offset is not None:
+        return _w(o), _w(cache), beam_cache_offset
+    return _w(o), _w(cache)
 
 
 def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq_lens_decoder, seq_lens_this_time,
@@ -324,11 +379,12 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     kernel over the block table).  qkv: [token_num, (Hq + 2 Hkv) * D] unpadded;
     key_cache / value_cache: [num_blocks, Hkv, block_size, D] (updated in place).
     Returns (out [token_num, Hq*D], qkv, key_cache, value_cache)."""
-    if any(a is not None for a in (pre_key_cache, cache_k_quant_scales, qkv_out_scale)) or out_scale > 0 or \
-            use_dynamic_cachekv_quant:
-        raise NotImplementedError("block_multihead_attention: pre-caches / int8 cache quantisation are not supported")
+    if any(a is not None for a in (pre_key_cache, cache_k_quant_scales)) or use_dynamic_cachekv_quant:
+        raise NotImplementedError("block_multihead_attention: pre-caches / int8 KV-cache quantisation are not supported")
     t = _u(qkv)
     kc, vc = _u(key_cache), _u(value_cache)
+    if qkv_out_scale is not None:  # int32 QKV accumulator -> real values
+        t = (t.float() * _u(qkv_out_scale).float().reshape(1, -1)).to(_compute_dtype(compute_dtype, kc))
     _, Hkv, bs, D = kc.shape
     T = t.shape[0]
     Hq = t.shape[1] // D - 2 * Hkv
@@ -371,7 +427,10 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
         lens = dec[dec_b.long()] + 1
         tm = None if tgt_mask is None else _u(tgt_mask).reshape(_u(tgt_mask).shape[0], -1)[dec_b.long()].float()
         out[rows] = ops.decode.decode_attention(q[rows], kc, vc, lens, block_tables=bt[dec_b.long()], mask=tm)
-    return _w(out.reshape(T, Hq * D)), qkv, key_cache, value_cache
+    o = out.reshape(T, Hq * D)
+    if out_scale > 0:
+        o = _quant_out(o, out_scale, out_shift, out_smooth, quant_round_type, quant_max_bound, quant_min_bound)
+    return _w(o), qkv, key_cache, value_cache
 
 
 def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, linear_weights, linear_biases,
@@ -391,9 +450,11 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
     * decode (time_step = t, x [B, 1, E]): the token's K/V are written at position t and it
       attends over [0, t] on the split-K HIP decode kernel (attn_mask: additive [B, 1, 1, t+1]).
     GEMMs go through ops.gemm.mm (hand-written MFMA kernel for large token counts), norms
-    through the fused norm kernels.  Returns out, or (out, cache_kvs) when caches are given."""
-    if beam_offset is not None or pre_caches is not None:
-        raise NotImplementedError("fused_multi_transformer: beam offsets / pre-caches are not supported")
+    through the fused norm kernels.  Returns out, or (out, cache_kvs) when caches are given.
+
+    ``pre_caches[i]`` ([2, B, Hkv, P, D], a shared prefix such as a system prompt) is attended to
+    ahead of the sequence by every query (prefill and decode); ``beam_offset`` [B / beam, beam, L]
+    selects, per beam and past position, the cache row of the beam it descends from (decode)."""
     if ring_id != -1:
         raise NotImplementedError("fused_multi_transformer: use the mpu layers for tensor parallelism (ring_id)")
     h = _u(x)
@@ -467,7 +528,18 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
                 ops.decode.kv_cache_write(k.reshape(B * S, Hkv, D), v.reshape(B * S, Hkv, D), cache[0], cache[1],
                                           pos, seq_of=seq)
             m = _u(attn_mask) if attn_mask is not None else None
-            o = _attend(q, k, v, m, 0.0, m is None, False)
+            if pre_caches is not None:  # prefix keys first: every query sees the whole prefix
+                pc = _u(pre_caches[i])
+                P = pc.shape[3]
+                kk = torch.cat([pc[0].permute(0, 2, 1, 3).to(k.dtype), k], 1)
+                vv = torch.cat([pc[1].permute(0, 2, 1, 3).to(v.dtype), v], 1)
+                if m is None:
+                    qi = torch.arange(S, device=h.device)[:, None]
+                    ki = torch.arange(P + S, device=h.device)[None, :]
+                    m = torch.where(ki <= qi + P, 0.0, float('-inf')).to(torch.float32)[None, None]
+                o = _attend(q, kk, vv, m, 0.0, False, False)
+            else:
+                o = _attend(q, k, v, m, 0.0, m is None, False)
         else:
             if cache is None:
                 raise ValueError("fused_multi_transformer decode (time_step) needs cache_kvs")
@@ -475,7 +547,19 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
             ops.decode.kv_cache_write(k[:, 0], v[:, 0], cache[0], cache[1], pos)
             lens = pos + 1
             m = None if attn_mask is None else _u(attn_mask).reshape(B, -1).float()
-            o = ops.decode.decode_attention(q[:, 0], cache[0], cache[1], lens, mask=m)[:, None]
+            kc, vc = cache[0], cache[1]
+            if beam_offset is not None:
+                kc, vc = _beam_gather(cache, beam_offset, B, step + 1)
+                ar = torch.arange(B, device=h.device)
+                kc[ar, :, step], vc[ar, :, step] = cache[0][ar, :, step], cache[1][ar, :, step]
+            if pre_caches is not None:
+                pc = _u(pre_caches[i])
+                kc = torch.cat([pc[0].to(kc.dtype), kc[:, :, :step + 1]], 2)
+                vc = torch.cat([pc[1].to(vc.dtype), vc[:, :, :step + 1]], 2)
+                lens = lens + pc.shape[3]
+                if m is not None:
+                    m = torch.cat([torch.zeros(B, pc.shape[3], device=m.device), m], 1)
+            o = ops.decode.decode_attention(q[:, 0], kc.contiguous(), vc.contiguous(), lens, mask=m)[:, None]
         if cache is not None:
             caches_out.append(cache_kvs[i])
         o = lin(o.reshape(B, S, Hq * D), linear_weights[i], linear_biases[i] if linear_biases is not None else None)

@@ -151,3 +151,85 @@ def test_fused_multi_transformer_functional_reference_shapes():
     mask = paddle.zeros([2, 1, 3, 3])
     out2 = IF.fused_multi_transformer(x, attn_mask=mask, **args)  # explicit (non-causal) mask
     assert not np.allclose(out.numpy(), out2.numpy())
+
+
+def _mmha_inputs(B, H, L, D, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, 3 * H * D, generator=g)
+    cache = torch.randn(2, B, H, L, D, generator=g)
+    return x, cache
+
+
+def test_mmha_beam_cache_offset_matches_rearranged_cache():
+    """beam_cache_offset: each beam reads past positions from the cache row of its ancestor beam."""
+    import paddle
+    import paddle.incubate.nn.functional as IF
+    B, beam, H, L, D, t = 4, 2, 2, 8, 16, 5
+    x, cache = _mmha_inputs(B, H, L, D, 0)
+    off = torch.randint(0, beam, (B // beam, beam, L), generator=torch.Generator().manual_seed(1))
+    seq = torch.full((B, 1), t, dtype=torch.int32)
+    c1 = cache.clone()
+    out, c1o, off_out = IF.masked_multihead_attention(paddle.to_tensor(x), paddle.to_tensor(c1),
+                                                      sequence_lengths=paddle.to_tensor(seq),
+                                                      beam_cache_offset=paddle.to_tensor(off))
+    # reference: rearrange every row's past positions explicitly, then the plain decode step
+    c2 = cache.clone()
+    for b in range(B):
+        for p in range(t):
+            src = (b // beam) * beam + int(off[b // beam, b % beam, p])
+            c2[:, b, :, p] = cache[:, src, :, p]
+    ref, _ = IF.masked_multihead_attention(paddle.to_tensor(x), paddle.to_tensor(c2),
+                                           sequence_lengths=paddle.to_tensor(seq))
+    np.testing.assert_allclose(out.numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
+    assert off_out is not None
+
+
+def test_mmha_quant_paths():
+    """qkv_out_scale dequantises an int32 qkv; out_scale quantises the output (round half away)."""
+    import paddle
+    import paddle.incubate.nn.functional as IF
+    B, H, L, D, t = 2, 2, 8, 16, 3
+    g = torch.Generator().manual_seed(2)
+    xi = torch.randint(-500, 500, (B, 3 * H * D), generator=g, dtype=torch.int32)
+    sc = torch.rand(3, H, D, generator=g) * 0.01
+    _, cache = _mmha_inputs(B, H, L, D, 3)
+    seq = paddle.to_tensor(torch.full((B, 1), t, dtype=torch.int32))
+    o1, _ = IF.masked_multihead_attention(paddle.to_tensor(xi), paddle.to_tensor(cache.clone()), sequence_lengths=seq,
+                                          qkv_out_scale=paddle.to_tensor(sc), compute_dtype='fp32')
+    xf = xi.float() * sc.reshape(1, -1)
+    o2, _ = IF.masked_multihead_attention(paddle.to_tensor(xf), paddle.to_tensor(cache.clone()), sequence_lengths=seq)
+    np.testing.assert_allclose(o1.numpy(), o2.numpy(), rtol=1e-5, atol=1e-6)
+    oq, _ = IF.masked_multihead_attention(paddle.to_tensor(xf), paddle.to_tensor(cache.clone()), sequence_lengths=seq,
+                                          out_scale=0.5, quant_round_type=1)
+    v = o2.numpy() * 127.0 * 0.5
+    expect = np.clip(np.sign(v) * np.floor(np.abs(v) + 0.5), -127, 127).astype(np.int8)
+    assert oq.numpy().dtype == np.int8
+    np.testing.assert_array_equal(oq.numpy(), expect)
+
+
+def test_fused_multi_transformer_pre_caches_decode():
+    """A pre-cache prefix is attended to ahead of the cached sequence: identical to placing the
+    prefix at the start of the cache and decoding P steps later (no rotary embedding)."""
+    import paddle
+    import paddle.incubate.nn.functional as IF
+    B, S0, E, H, P, L = 2, 3, 32, 2, 4, 16
+    D = E // H
+    g = torch.Generator().manual_seed(4)
+    t = paddle.to_tensor
+    w = lambda *s: t(torch.randn(*s, generator=g) * 0.2)  # noqa: E731
+    params = dict(ln_scales=[t(torch.ones(E))], ln_biases=[t(torch.zeros(E))], qkv_weights=[w(3, H, D, E)],
+                  qkv_biases=[w(3 * H * D)], linear_weights=[w(E, E)], linear_biases=[w(E)],
+                  ffn_ln_scales=[t(torch.ones(E))], ffn_ln_biases=[t(torch.zeros(E))], ffn1_weights=[w(E, 2 * E)],
+                  ffn1_biases=[w(2 * E)], ffn2_weights=[w(2 * E, E)], ffn2_biases=[w(E)])
+    x = w(B, 1, E)
+    pre = torch.randn(2, B, H, P, D, generator=g)
+    hist = torch.randn(2, B, H, L, D, generator=g)
+    c1 = hist.clone()
+    c1[:, :, :, S0 + 1:] = 0
+    o1, _ = IF.fused_multi_transformer(x, cache_kvs=[t(c1)], pre_caches=[t(pre)], time_step=t(torch.tensor([S0])),
+                                       **params)
+    c2 = torch.zeros(2, B, H, L + P, D)
+    c2[:, :, :, :P] = pre
+    c2[:, :, :, P:P + S0] = hist[:, :, :, :S0]
+    o2, _ = IF.fused_multi_transformer(x, cache_kvs=[t(c2)], time_step=t(torch.tensor([S0 + P])), **params)
+    np.testing.assert_allclose(o1.numpy(), o2.numpy(), rtol=1e-4, atol=1e-5)
