@@ -475,6 +475,13 @@ PA_API hipError_t pa_bias_act_bwd_dbias(int act, const void* dy, const void* x, 
   return launch_colsum_finish_dt(part, dbias, odt, (int)grid.y, cols, accum, st);
 }
 
+// out (+)= sum of the nrows fp32 partial rows part[nrows][cols] (partials produced elsewhere, e.g. the
+// fused fc2-dgrad GEMM epilogue's column sums).
+PA_API hipError_t pa_colsum_finish_parts(const float* part, void* out, int odt, int accum, int nrows, int cols,
+                                         hipStream_t st) {
+  return launch_colsum_finish_dt(part, out, odt, nrows, cols, accum, st);
+}
+
 // out (+)= colsum(dy) for dy [rows, cols] with row stride ld == cols (the bias gradient of a Linear).
 PA_API hipError_t pa_colsum(const void* dy, float* part, void* out, int odt, int accum, int rows, int cols, int dt,
                             hipStream_t st) {

@@ -173,7 +173,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __r
         for (int r = 0; r < 4; ++r) gelu_tanh_fdf(h[r], g[r], d[r]);
         store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(ws) + o, d);
         store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(C + o), g);
-      } else if constexpr (EPI == 3) {  // C = alpha*acc * aux  (aux = the saved gelu_tanh'(h))
+      } else if constexpr (EPI == 3 || EPI == 4) {  // C = alpha*acc * aux  (aux = the saved gelu_tanh'(h))
         const long long o = (long long)m * ldc + n;
         float d[4];
         load_f<bf16_t, 4>(reinterpret_cast<const bf16_t*>(ws) + o, d);
@@ -218,11 +218,13 @@ __device__ __forceinline__ void epilogue_wide(const f32x4 (&acc)[8][4], uint16_t
   for (int p = 0; p < 2; ++p) {
     const int n = nb + (upper ? 16 * (2 * p + 1) + 4 * (g - 1) : 16 * (2 * p) + 4 * g);
     float bb[8];
-    if (EPI != 3 && bias != nullptr && n < N) load_f<bf16_t, 8>(reinterpret_cast<const bf16_t*>(bias + n), bb);
+    if (EPI != 3 && EPI != 4 && bias != nullptr && n < N)
+      load_f<bf16_t, 8>(reinterpret_cast<const bf16_t*>(bias + n), bb);
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // EPI 4: column sums of this lane's rows
     // EPI 3: issue all eight 16-B loads of the saved derivative before any use (one memory round
     // trip per p instead of eight serialised ones)
     Pack<bf16_t, 8> hv[8];
-    if constexpr (EPI == 3) {
+    if constexpr (EPI == 3 || EPI == 4) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int m = mb + i * 16 + (lane & 15);
@@ -245,10 +247,14 @@ __device__ __forceinline__ void epilogue_wide(const f32x4 (&acc)[8][4], uint16_t
       const int m = mb + i * 16 + (lane & 15);
       if (m >= M || n >= N) continue;
       const long long o = (long long)m * ldc + n;
-      if constexpr (EPI == 3) {
+      if constexpr (EPI == 3 || EPI == 4) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) v[r] *= (float)hv[i].v[r];
         store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(C + o), v);
+        if constexpr (EPI == 4) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) cs[r] += (float)(bf16_t)v[r];  // the value as stored
+        }
       } else {
         if (bias != nullptr) {
 #pragma unroll
@@ -266,6 +272,23 @@ __device__ __forceinline__ void epilogue_wide(const f32x4 (&acc)[8][4], uint16_t
           for (int r = 0; r < 8; ++r) v[r] += beta * old[r];
         }
         store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(C + o), v);
+      }
+    }
+    if constexpr (EPI == 4) {
+      // bias-gradient fusion: rows of the wave's 128-row slab live in lanes (lane & 15) x i; sum
+      // the 16 lanes of this column group and write one partial row per slab (finished by
+      // pa_colsum_finish_parts into the bias gradient)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        cs[r] += __shfl_xor(cs[r], 1);
+        cs[r] += __shfl_xor(cs[r], 2);
+        cs[r] += __shfl_xor(cs[r], 4);
+        cs[r] += __shfl_xor(cs[r], 8);
+      }
+      if ((lane & 15) == 0 && n < N && mb < M) {
+        float* dst = reinterpret_cast<float*>(const_cast<uint16_t*>(bias)) + (long long)(mb / 128) * N + n;
+        *reinterpret_cast<float4*>(dst) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
       }
     }
   }
@@ -775,6 +798,8 @@ __global__ __launch_bounds__(512, 1) void gemm11_kernel(const char* __restrict__
 
   if constexpr (EPI == 1)
     epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
+  else if constexpr (EPI == 4)
+    epilogue_wide<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
   else if (g_wide_epi)
     epilogue_wide<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
   else
@@ -1016,7 +1041,7 @@ static hipError_t launch_epi(int transB, const void* A, const void* B, void* C, 
                              int N, int K, long long lda, long long ldb, long long ldc, float alpha, hipStream_t st) {
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   dim3 grid(tm * tn, 1, 1);
-  if (g_epi_sched == 12) {  // persistent: the epilogue overlaps the next tile's staging
+  if (g_epi_sched == 12 && EPI != 4) {  // persistent: the epilogue overlaps the next tile's staging
     const int items = tm * tn;
     const int g = items >= 256 ? 256 : (items + 7) / 8 * 8;
     if (transB)
@@ -1077,6 +1102,8 @@ PA_API int pa_gemm8_bf16_epi(const void* A, const void* B, void* C, const void* 
   if (!pa_gemm8_ok(M, N, K, lda, ldb, ldc, 0, transB, 1) || !aux) return (int)hipErrorInvalidValue;
   if (epi == 2) return (int)launch_epi<2>(transB, A, B, C, aux, bias, M, N, K, lda, ldb, ldc, alpha, st);
   if (epi == 3) return (int)launch_epi<3>(transB, A, B, C, aux, nullptr, M, N, K, lda, ldb, ldc, alpha, st);
+  // epi 4: epi 3 + column partial sums of C, one fp32 row per 128-row slab, into bias ([ceil(M/128)][N])
+  if (epi == 4 && bias != nullptr) return (int)launch_epi<4>(transB, A, B, C, aux, bias, M, N, K, lda, ldb, ldc, alpha, st);
   return (int)hipErrorInvalidValue;
 }
 

@@ -43,6 +43,14 @@ def colsum(dy2, out=None, accumulate=False):
     return out
 
 
+def colsum_finish_parts(part, out, nrows, accumulate=True):
+    """out (+)= the sum of the nrows fp32 partial rows in ``part`` ([nrows, cols])."""
+    cols = out.numel()
+    N.check(N.lib.pa_colsum_finish_parts(N.ptr(part), N.ptr(out), N.dtcode(out.dtype), int(bool(accumulate)), nrows,
+                                         cols, N.stream()), 'colsum_finish_parts')
+    return out
+
+
 def _hip(t):
     from . import use_hip
     return use_hip(t)

@@ -86,18 +86,23 @@ def epi_ok(a, b, out_cols):
     return bool(N.lib.pa_gemm8_ok(a.shape[0], out_cols, a.shape[1], lda, ldb, out_cols, 0, tb, 1))
 
 
-def mm_epi(a, b, epi, aux, bias=None, out=None):
+def mm_epi(a, b, epi, aux, bias=None, out=None, colsum_part=None):
     """Fused-epilogue GEMM of the MLP (csrc/gemm8.hip pa_gemm8_bf16_epi, schedule 11).
 
     epi 2 (fc1 forward): h = a @ b + bias; returns gelu_tanh(h) and writes gelu_tanh'(h) to ``aux``;
     epi 3 (fc2 dgrad):   returns (a @ b) * aux.   a: [M,K] row-major; b: [K,N]
-    (row-major or a transposed view of [N,K]); aux: bf16 [M,N] contiguous."""
+    (row-major or a transposed view of [N,K]); aux: bf16 [M,N] contiguous.
+    colsum_part (epi 3 only): fp32 [ceil(M/128) * N] receiving per-128-row-slab column sums of the
+    result (the fc1 bias gradient, finished by fused.colsum_finish_parts)."""
     tb, ldb = _op_layout(b)
     M, K = a.shape
     N_ = b.shape[1]
     if out is None:
         out = torch.empty(M, N_, dtype=torch.bfloat16, device=a.device)
     assert aux.shape == (M, N_) and aux.is_contiguous() and out.is_contiguous()
+    if colsum_part is not None:
+        assert epi == 3 and colsum_part.dtype == torch.float32 and colsum_part.numel() >= -(-M // 128) * N_
+        epi, bias = 4, colsum_part
     N.check(N.lib.pa_gemm8_bf16_epi(N.ptr(a), N.ptr(b), N.ptr(out), N.ptr(bias), N.ptr(aux), M, N_, K, a.stride(0),
                                     ldb, N_, tb, 1.0, int(epi), N.stream()), f'gemm_epi{epi}')
     return out

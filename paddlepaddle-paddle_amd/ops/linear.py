@@ -72,6 +72,9 @@ def _grad_b(dy2, bp):
     return s.to(dy2.dtype)
 
 
+FUSE_DBIAS = True  # fc1 bias gradient from the fc2-dgrad epilogue (tests switch it)
+
+
 class _MLPGelu(torch.autograd.Function):
     """y = gelu_tanh(x @ W1 + b1) @ W2 + b2 with the activation inside the GEMM epilogues:
     forward fc1 writes g = gelu(h) and gelu'(h) (h = x@W1 + b1) in one epilogue (EPI 2), backward's
@@ -102,8 +105,18 @@ class _MLPGelu(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         dw2 = _grad_w(g, dy2, w2p)
         db2 = _grad_b(dy2, b2p) if b2p is not None else None
-        dh = gemm.mm_epi(dy2, w2.t(), 3, h)
-        db1 = _grad_b(dh, b1p)
+        gb1 = flat_grad_slot(b1p) if FUSE_DBIAS else None
+        if gb1 is not None and gb1.is_contiguous():
+            # fc1 bias gradient reduced in the fc2-dgrad GEMM epilogue (per-slab column sums of dh,
+            # finished into the flat slot): no second pass over dh
+            part = torch.empty(-(-dy2.shape[0] // 128) * w2.shape[0], dtype=torch.float32, device=dy2.device)
+            dh = gemm.mm_epi(dy2, w2.t(), 3, h, colsum_part=part)
+            fused.colsum_finish_parts(part, gb1, -(-dy2.shape[0] // 128), accumulate=True)
+            notify_grad_ready(b1p)
+            db1 = None
+        else:
+            dh = gemm.mm_epi(dy2, w2.t(), 3, h)
+            db1 = _grad_b(dh, b1p)
         dw1 = _grad_w(x2, dh, w1p)
         dx = gemm.mm(dh, w1.t()).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
         return dx, dw1, db1, dw2, db2, None

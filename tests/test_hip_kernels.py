@@ -1174,3 +1174,54 @@ def test_train_step_hip_graph_matches_eager():
     r()
     with pytest.raises(RuntimeError):
         r()
+
+
+@pytest.mark.parametrize('M', [1000, 4096])
+def test_gemm_epi3_colsum_partials(M):
+    """fc2-dgrad GEMM epilogue with the fc1 bias-gradient column sums (epi 4): per-128-row-slab
+    partials finished into a gradient slot == colsum of the returned dh (bf16 values)."""
+    from paddle.ops import gemm, fused
+    g = torch.Generator(device=DEV).manual_seed(7)
+    K, N_ = 512, 1024
+    dy = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).bfloat16()
+    w = (torch.rand(N_, K, device=DEV, generator=g) * 2 - 1).bfloat16()  # [fc2 in=N_, out=K]
+    aux = (torch.rand(M, N_, device=DEV, generator=g)).bfloat16()
+    ref = gemm.mm_epi(dy, w.t(), 3, aux)
+    part = torch.full((-(-M // 128) * N_,), float('nan'), device=DEV)
+    dh = gemm.mm_epi(dy, w.t(), 3, aux, colsum_part=part)
+    assert torch.equal(dh, ref)
+    slot = torch.full((N_,), 0.25, device=DEV)
+    fused.colsum_finish_parts(part, slot, -(-M // 128), accumulate=True)
+    expect = dh.float().sum(0) + 0.25
+    _close(slot, expect, 1e-3 * float(expect.abs().max()) + 1e-2, 1e-3, 'epi4 colsum')
+
+
+def test_mlp_fc1_bias_grad_from_dgrad_epilogue():
+    """GPT MLP: the fc1 bias gradient reduced in the fc2-dgrad epilogue trains like the colsum pass."""
+    import paddle
+    from paddle.ops import linear
+    from paddle.models.gpt import gpt_config, GPTForPretraining
+    paddle.set_device('gpu:0')
+    finals = []
+    for on in (False, True):
+        linear.FUSE_DBIAS = on
+        try:
+            paddle.seed(13)
+            cfg = gpt_config('gpt-tiny', hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+            model = GPTForPretraining(cfg)
+            opt = paddle.optimizer.AdamW(learning_rate=1e-3, parameters=model.parameters(), multi_precision=True)
+            model, opt = paddle.amp.decorate(model, opt, level='O2', dtype='bfloat16')
+            paddle.seed(14)
+            ids = paddle.randint(0, cfg.vocab_size, [8, 257])
+            for _ in range(3):
+                loss = model.loss(model(ids[:, :-1]), ids[:, 1:])
+                loss.backward()
+                opt.step()
+                opt.clear_grad()
+            finals.append({n: p._t.detach().float().clone() for n, p in model.named_parameters() if 'fc1' in n})
+        finally:
+            linear.FUSE_DBIAS = True
+    assert any('bias' in n for n in finals[0])
+    for n in finals[0]:
+        a, b = finals[0][n], finals[1][n]
+        _close(b, a, 1e-2 * float(a.abs().max()) + 1e-4, 1e-2, n)
