@@ -378,11 +378,21 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     decode one token at position seq_lens_decoder[b] over their cached prefix (split-K HIP decode
     kernel over the block table).  qkv: [token_num, (Hq + 2 Hkv) * D] unpadded;
     key_cache / value_cache: [num_blocks, Hkv, block_size, D] (updated in place).
-    Returns (out [token_num, Hq*D], qkv, key_cache, value_cache)."""
-    if any(a is not None for a in (pre_key_cache, cache_k_quant_scales)) or use_dynamic_cachekv_quant:
-        raise NotImplementedError("block_multihead_attention: pre-caches / int8 KV-cache quantisation are not supported")
+    Returns (out [token_num, Hq*D], qkv, key_cache, value_cache).
+
+    ``pre_key_cache`` / ``pre_value_cache`` [B, Hkv, P, D]: a per-sequence prefix every query
+    attends to ahead of its own keys (prompts: before the causal prompt block; decode: before the
+    paged prefix).  Static int8 KV caches: with ``cache_k_quant_scales`` / ``cache_v_quant_scales``
+    ([Hkv]) the new K/V are stored as clip(round(x * quant_scale)) in int8 caches and read back as
+    q * dequant_scale (``cache_*_dequant_scales``); the decode rows then attend over the
+    dequantised pages (composite path).  Dynamic per-batch cache quantisation is not implemented."""
+    if use_dynamic_cachekv_quant:
+        raise NotImplementedError("block_multihead_attention: dynamic KV-cache quantisation is not supported")
     t = _u(qkv)
     kc, vc = _u(key_cache), _u(value_cache)
+    qcache = cache_k_quant_scales is not None
+    if qcache and (cache_v_quant_scales is None or cache_k_dequant_scales is None or cache_v_dequant_scales is None):
+        raise ValueError("int8 KV cache needs cache_{k,v}_quant_scales and cache_{k,v}_dequant_scales")
     if qkv_out_scale is not None:  # int32 QKV accumulator -> real values
         t = (t.float() * _u(qkv_out_scale).float().reshape(1, -1)).to(_compute_dtype(compute_dtype, kc))
     _, Hkv, bs, D = kc.shape
@@ -410,8 +420,21 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
         sin = _full_width(cs[1, seq_of.long(), pos.long()], D, use_neox_style)[:, None]
         q = _rope_rows(q, cos, sin, use_neox_style)
         k = _rope_rows(k, cos, sin, use_neox_style)
-    ops.decode.kv_cache_write(k, v, kc, vc, pos, seq_of=seq_of, block_tables=bt)
+    if qcache:  # quantise the new rows into the int8 pages
+        def qz(x, sc):
+            v_ = x.float() * _u(sc).float().reshape(1, -1, 1)
+            v_ = torch.round(v_) if quant_round_type == 0 else torch.sign(v_) * torch.floor(v_.abs() + 0.5)
+            return v_.clamp(quant_min_bound, quant_max_bound).to(kc.dtype)
+        blk = bt[seq_of.long(), (pos // bs).long()].long()
+        off = (pos % bs).long()
+        kc[blk, :, off] = qz(k, cache_k_quant_scales)
+        vc[blk, :, off] = qz(v, cache_v_quant_scales)
+    else:
+        ops.decode.kv_cache_write(k, v, kc, vc, pos, seq_of=seq_of, block_tables=bt)
     out = torch.empty(T, Hq, D, dtype=t.dtype, device=dev)
+    pre_k = _u(pre_key_cache) if pre_key_cache is not None else None
+    pre_v = _u(pre_value_cache) if pre_value_cache is not None else None
+    P = pre_k.shape[2] if pre_k is not None else 0
     enc_l, dec_b = enc.tolist(), ((enc == 0) & (this > 0)).nonzero().reshape(-1)
     # prompts: causal attention over the prompt's own tokens (flash kernel per prompt)
     for b, L in enumerate(enc_l):
@@ -420,13 +443,38 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
         s0 = int(cu[b])
         qb, kb, vb = q[s0:s0 + L][None], k[s0:s0 + L][None], v[s0:s0 + L][None]
         m = None if mask is None else _u(mask)[b:b + 1, :, :L, :L]
-        out[s0:s0 + L] = _attend(qb, kb, vb, m, 0.0, m is None, False)[0]
+        if P:
+            kb = torch.cat([pre_k[b].permute(1, 0, 2)[None].to(kb.dtype), kb], 1)
+            vb = torch.cat([pre_v[b].permute(1, 0, 2)[None].to(vb.dtype), vb], 1)
+            qi = torch.arange(L, device=dev)[:, None]
+            ki = torch.arange(P + L, device=dev)[None, :]
+            causal = torch.where(ki <= qi + P, 0.0, float('-inf')).to(torch.float32)[None, None]
+            m = causal if m is None else torch.cat([torch.zeros(1, m.shape[1], L, P, device=dev), m.float()], -1)
+            out[s0:s0 + L] = _attend(qb, kb, vb, m, 0.0, False, False)[0]
+        else:
+            out[s0:s0 + L] = _attend(qb, kb, vb, m, 0.0, m is None, False)[0]
     # decode tokens: one per sequence, over its paged prefix
     if dec_b.numel():
         rows = cu[:-1][dec_b.long()]
         lens = dec[dec_b.long()] + 1
         tm = None if tgt_mask is None else _u(tgt_mask).reshape(_u(tgt_mask).shape[0], -1)[dec_b.long()].float()
-        out[rows] = ops.decode.decode_attention(q[rows], kc, vc, lens, block_tables=bt[dec_b.long()], mask=tm)
+        if P or qcache:
+            # contiguous copies of the decode rows' pages (dequantised), prefix keys in front
+            nblk = bt.shape[1]
+            pages = bt[dec_b.long()].long()                                   # [n, nblk]
+            kd = kc[pages].permute(0, 2, 1, 3, 4).reshape(len(pages), Hkv, nblk * bs, D)
+            vd = vc[pages].permute(0, 2, 1, 3, 4).reshape(len(pages), Hkv, nblk * bs, D)
+            if qcache:
+                kd = (kd.float() * _u(cache_k_dequant_scales).float().reshape(1, -1, 1, 1)).to(q.dtype)
+                vd = (vd.float() * _u(cache_v_dequant_scales).float().reshape(1, -1, 1, 1)).to(q.dtype)
+            if P:
+                kd = torch.cat([pre_k[dec_b.long()].to(kd.dtype), kd], 2)
+                vd = torch.cat([pre_v[dec_b.long()].to(vd.dtype), vd], 2)
+                if tm is not None:
+                    tm = torch.cat([torch.zeros(tm.shape[0], P, device=dev), tm], 1)
+            out[rows] = ops.decode.decode_attention(q[rows], kd.contiguous(), vd.contiguous(), lens + P, mask=tm)
+        else:
+            out[rows] = ops.decode.decode_attention(q[rows], kc, vc, lens, block_tables=bt[dec_b.long()], mask=tm)
     o = out.reshape(T, Hq * D)
     if out_scale > 0:
         o = _quant_out(o, out_scale, out_shift, out_smooth, quant_round_type, quant_max_bound, quant_min_bound)

@@ -233,3 +233,67 @@ def test_fused_multi_transformer_pre_caches_decode():
     c2[:, :, :, P:P + S0] = hist[:, :, :, :S0]
     o2, _ = IF.fused_multi_transformer(x, cache_kvs=[t(c2)], time_step=t(torch.tensor([S0 + P])), **params)
     np.testing.assert_allclose(o1.numpy(), o2.numpy(), rtol=1e-4, atol=1e-5)
+
+
+def _blha_case(seed, quant=False, pre=0):
+    torch.manual_seed(seed)
+    Hq, Hkv, D, bs, nblk = 4, 2, 8, 4, 24
+    dt = torch.int8 if quant else torch.float32
+    kc = torch.zeros(nblk, Hkv, bs, D, dtype=dt)
+    vc = torch.zeros(nblk, Hkv, bs, D, dtype=dt)
+    enc, dec, this = [5, 0, 3, 0], [0, 6, 0, 9], [5, 1, 3, 1]
+    bt = torch.arange(nblk).reshape(4, 6)
+    qs = torch.tensor([20.0, 30.0])           # quant scales per kv head
+    dq = 1.0 / qs
+    qz = lambda x: torch.clamp(torch.sign(x * qs[None, :, None]) *  # noqa: E731
+                               torch.floor((x * qs[None, :, None]).abs() + 0.5), -127, 127)
+    hist = {1: (torch.randn(6, Hkv, D), torch.randn(6, Hkv, D)), 3: (torch.randn(9, Hkv, D), torch.randn(9, Hkv, D))}
+    for b, (k, v) in hist.items():
+        for p in range(k.shape[0]):
+            kc[bt[b, p // bs], :, p % bs] = (qz(k[p:p + 1])[0] if quant else k[p]).to(dt)
+            vc[bt[b, p // bs], :, p % bs] = (qz(v[p:p + 1])[0] if quant else v[p]).to(dt)
+    T = sum(this)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D)
+    cu = _get_padding_offset(this)
+    pk = torch.randn(4, Hkv, pre, D) if pre else None
+    pv = torch.randn(4, Hkv, pre, D) if pre else None
+    t = paddle.to_tensor
+    kw = {}
+    if quant:
+        kw = dict(cache_k_quant_scales=t(qs), cache_v_quant_scales=t(qs), cache_k_dequant_scales=t(dq),
+                  cache_v_dequant_scales=t(dq))
+    if pre:
+        kw.update(pre_key_cache=t(pk), pre_value_cache=t(pv))
+    out, _, kc2, _ = IF.block_multihead_attention(
+        t(qkv), t(kc), t(vc), t(torch.tensor(enc)[:, None]), t(torch.tensor(dec)[:, None]),
+        t(torch.tensor(this)[:, None]), None, None, t(cu), t(cu), t(bt), block_size=bs, **kw)
+    o = out.numpy()
+    for b in range(4):
+        s0, n = int(cu[b]), this[b]
+        rows = qkv[s0:s0 + n]
+        q = rows[:, :Hq * D].reshape(n, Hq, D)
+        k = rows[:, Hq * D:(Hq + Hkv) * D].reshape(n, Hkv, D)
+        v = rows[:, (Hq + Hkv) * D:].reshape(n, Hkv, D)
+        if b in hist:  # decode rows read everything (incl. their new K/V) back from the cache
+            hk, hv = hist[b]
+            if quant:
+                hk, hv = qz(hk) * dq[None, :, None], qz(hv) * dq[None, :, None]
+                k, v = qz(k) * dq[None, :, None], qz(v) * dq[None, :, None]
+            k, v = torch.cat([hk, k]), torch.cat([hv, v])
+        if pre:
+            k, v = torch.cat([pk[b].permute(1, 0, 2), k]), torch.cat([pv[b].permute(1, 0, 2), v])
+        want = _attn(q, k, v, causal=True)
+        np.testing.assert_allclose(o[s0:s0 + n], want.reshape(n, -1).numpy(), rtol=1e-4, atol=1e-4)
+    return kc2
+
+
+def test_block_multihead_attention_pre_caches():
+    """A per-sequence prefix (pre_key/value_cache) ahead of prompts and decode rows."""
+    _blha_case(5, pre=3)
+
+
+def test_block_multihead_attention_int8_cache():
+    """Static int8 KV cache: new rows quantised into the pages, decode reads dequantised pages."""
+    kc2 = _blha_case(6, quant=True)
+    assert kc2.numpy().dtype == np.int8
+    _blha_case(7, quant=True, pre=2)
