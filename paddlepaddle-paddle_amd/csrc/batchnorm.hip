@@ -268,22 +268,41 @@ __global__ __launch_bounds__(256) void apply_fwd(const T* __restrict__ x, const 
 }
 
 // ---- backward reduce: per channel  s1 = sum g,  s2 = sum g * (x - mean),  g = dy [* (y > 0)]
-template <typename T, bool RELU>
+// XM (ReLU without a residual input): the ReLU mask is recomputed from x with the forward's own
+// affine (a = gamma * rstd, b = beta - mean * a; y > 0 <=> x * a + b > 0, the same fp32 expression
+// as apply_fwd), so y is never read: one activation-sized read less per pass.
+template <typename WT>
+__device__ __forceinline__ void affine_of(const WT* gamma, const WT* beta, const float* mean, const float* rstd, int c,
+                                          float& a, float& b) {
+  const float g = gamma != nullptr ? to_f(gamma[c]) : 1.f;
+  const float bt = beta != nullptr ? to_f(beta[c]) : 0.f;
+  a = g * rstd[c];
+  b = bt - mean[c] * a;
+}
+
+template <typename T, bool RELU, typename WT = float, bool XM = false>
 __global__ __launch_bounds__(256) void bwd_partial(const T* __restrict__ dy, const T* __restrict__ x,
                                                    const T* __restrict__ y, const float* __restrict__ mean, int rows,
-                                                   int cols, int rpb, float* __restrict__ p1, float* __restrict__ p2) {
+                                                   int cols, int rpb, float* __restrict__ p1, float* __restrict__ p2,
+                                                   const WT* __restrict__ gamma = nullptr,
+                                                   const WT* __restrict__ beta = nullptr,
+                                                   const float* __restrict__ rstd = nullptr) {
   constexpr int E = 16 / sizeof(T);
   __shared__ float red[256 * E];
   const Map m = lane_map<E>(cols);
   const int r0 = blockIdx.y * rpb;
   const int r1 = min(rows, r0 + rpb);
-  float mu[E], s1[E], s2[E];
+  float mu[E], s1[E], s2[E], fa[E], fb[E];
 #pragma unroll
-  for (int e = 0; e < E; ++e) { mu[e] = 0.f; s1[e] = 0.f; s2[e] = 0.f; }
+  for (int e = 0; e < E; ++e) { mu[e] = 0.f; s1[e] = 0.f; s2[e] = 0.f; fa[e] = 0.f; fb[e] = 0.f; }
   if (m.active) {
     const int c0 = m.c0, st = m.rpi;
 #pragma unroll
     for (int e = 0; e < E; ++e) mu[e] = mean[c0 + e];
+    if constexpr (XM) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) affine_of<WT>(gamma, beta, mean, rstd, c0 + e, fa[e], fb[e]);
+    }
     int r = r0 + m.sub;
     for (; r + (U - 1) * st < r1; r += U * st) {
       float g[U][E], v[U][E], o[U][E];
@@ -291,14 +310,15 @@ __global__ __launch_bounds__(256) void bwd_partial(const T* __restrict__ dy, con
       for (int u = 0; u < U; ++u) {
         load_f<T, E>(dy + (size_t)(r + u * st) * cols + c0, g[u]);
         load_f<T, E>(x + (size_t)(r + u * st) * cols + c0, v[u]);
-        if constexpr (RELU) load_f<T, E>(y + (size_t)(r + u * st) * cols + c0, o[u]);
+        if constexpr (RELU && !XM) load_f<T, E>(y + (size_t)(r + u * st) * cols + c0, o[u]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           float gg = g[u][e];
-          if constexpr (RELU) gg = o[u][e] > 0.f ? gg : 0.f;
+          if constexpr (XM) gg = (v[u][e] * fa[e] + fb[e]) > 0.f ? gg : 0.f;
+          else if constexpr (RELU) gg = o[u][e] > 0.f ? gg : 0.f;
           s1[e] += gg;
           s2[e] += gg * (v[u][e] - mu[e]);
         }
@@ -307,11 +327,12 @@ __global__ __launch_bounds__(256) void bwd_partial(const T* __restrict__ dy, con
       float g[E], v[E], o[E];
       load_f<T, E>(dy + (size_t)r * cols + c0, g);
       load_f<T, E>(x + (size_t)r * cols + c0, v);
-      if constexpr (RELU) load_f<T, E>(y + (size_t)r * cols + c0, o);
+      if constexpr (RELU && !XM) load_f<T, E>(y + (size_t)r * cols + c0, o);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         float gg = g[e];
-        if constexpr (RELU) gg = o[e] > 0.f ? gg : 0.f;
+        if constexpr (XM) gg = (v[e] * fa[e] + fb[e]) > 0.f ? gg : 0.f;
+        else if constexpr (RELU) gg = o[e] > 0.f ? gg : 0.f;
         s1[e] += gg;
         s2[e] += gg * (v[e] - mu[e]);
       }
@@ -371,12 +392,13 @@ __global__ __launch_bounds__(1024) void bwd_finish(const float* __restrict__ p1,
 }
 
 // dx = gamma * rstd * (g - s1/R - (x - mean) * rstd^2 * s2/R);  dz = g (residual branch)
-template <typename T, typename WT, bool RELU, bool RES>
+template <typename T, typename WT, bool RELU, bool RES, bool XM = false>
 __global__ __launch_bounds__(256) void bwd_apply(const T* __restrict__ dy, const T* __restrict__ x,
                                                  const T* __restrict__ y, const float* __restrict__ mean,
                                                  const float* __restrict__ rstd, const WT* __restrict__ gamma,
                                                  const float* __restrict__ sums, T* __restrict__ dx,
-                                                 T* __restrict__ dz, int rows, int cols, int rpb) {
+                                                 T* __restrict__ dz, int rows, int cols, int rpb,
+                                                 const WT* __restrict__ beta = nullptr) {
   constexpr int E = 16 / sizeof(T);
   const Map m = lane_map<E>(cols);
   if (!m.active) return;
@@ -384,9 +406,10 @@ __global__ __launch_bounds__(256) void bwd_apply(const T* __restrict__ dy, const
   const int r0 = blockIdx.y * rpb;
   const int r1 = min(rows, r0 + rpb);
   const float invR = 1.f / (float)rows;
-  float k1[E], k2[E], k3[E], mu[E];  // dx = k1 * g + k2 * (x - mu) + k3
+  float k1[E], k2[E], k3[E], mu[E], fa[E], fb[E];  // dx = k1 * g + k2 * (x - mu) + k3
 #pragma unroll
   for (int e = 0; e < E; ++e) {
+    if constexpr (XM) affine_of<WT>(gamma, beta, mean, rstd, c0 + e, fa[e], fb[e]);
     const float rs = rstd[c0 + e];
     const float gr = (gamma != nullptr ? to_f(gamma[c0 + e]) : 1.f) * rs;
     mu[e] = mean[c0 + e];
@@ -401,13 +424,14 @@ __global__ __launch_bounds__(256) void bwd_apply(const T* __restrict__ dy, const
     for (int u = 0; u < U; ++u) {
       load_f<T, E>(dy + (size_t)(r + u * st) * cols + c0, g[u]);
       load_f<T, E>(x + (size_t)(r + u * st) * cols + c0, v[u]);
-      if constexpr (RELU) load_f<T, E>(y + (size_t)(r + u * st) * cols + c0, o[u]);
+      if constexpr (RELU && !XM) load_f<T, E>(y + (size_t)(r + u * st) * cols + c0, o[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        if constexpr (RELU) g[u][e] = o[u][e] > 0.f ? g[u][e] : 0.f;
+        if constexpr (XM) g[u][e] = (v[u][e] * fa[e] + fb[e]) > 0.f ? g[u][e] : 0.f;
+        else if constexpr (RELU) g[u][e] = o[u][e] > 0.f ? g[u][e] : 0.f;
         v[u][e] = k1[e] * g[u][e] + k2[e] * (v[u][e] - mu[e]) + k3[e];
       }
       store_f<T, E>(dx + (size_t)(r + u * st) * cols + c0, v[u]);
@@ -418,10 +442,11 @@ __global__ __launch_bounds__(256) void bwd_apply(const T* __restrict__ dy, const
     float g[E], v[E], o[E];
     load_f<T, E>(dy + (size_t)r * cols + c0, g);
     load_f<T, E>(x + (size_t)r * cols + c0, v);
-    if constexpr (RELU) load_f<T, E>(y + (size_t)r * cols + c0, o);
+    if constexpr (RELU && !XM) load_f<T, E>(y + (size_t)r * cols + c0, o);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      if constexpr (RELU) g[e] = o[e] > 0.f ? g[e] : 0.f;
+      if constexpr (XM) g[e] = (v[e] * fa[e] + fb[e]) > 0.f ? g[e] : 0.f;
+      else if constexpr (RELU) g[e] = o[e] > 0.f ? g[e] : 0.f;
       v[e] = k1[e] * g[e] + k2[e] * (v[e] - mu[e]) + k3[e];
     }
     store_f<T, E>(dx + (size_t)r * cols + c0, v);
@@ -456,8 +481,8 @@ hipError_t fwd(const void* x, const void* z, const void* gamma, const void* beta
 
 template <typename T, typename WT>
 hipError_t bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
-               void* dx, void* dz, void* dgamma, void* dbeta, float* ws, int rows, int cols, int relu, int accumulate,
-               hipStream_t st) {
+               const void* beta, void* dx, void* dz, void* dgamma, void* dbeta, float* ws, int rows, int cols, int relu,
+               int accumulate, hipStream_t st) {
   constexpr int E = 16 / sizeof(T);
   const int cb = col_blocks(cols, E);
   const int rpb = rows_per_block(rows, cb);
@@ -468,7 +493,11 @@ hipError_t bwd(const void* dy, const void* x, const void* y, const float* mean, 
   float* p2 = ws + (size_t)P * cols;
   float* sums = ws + (size_t)2 * P * cols;
   const dim3 rgrid(cb, P);
-  if (relu)
+  const bool xm = relu && dz == nullptr;  // ReLU mask from x: y is not read
+  if (xm)
+    bwd_partial<T, true, WT, true><<<rgrid, 256, 0, st>>>((const T*)dy, (const T*)x, nullptr, mean, rows, cols, rrb, p1,
+                                                          p2, (const WT*)gamma, (const WT*)beta, rstd);
+  else if (relu)
     bwd_partial<T, true><<<rgrid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)y, mean, rows, cols, rrb, p1, p2);
   else
     bwd_partial<T, false><<<rgrid, 256, 0, st>>>((const T*)dy, (const T*)x, nullptr, mean, rows, cols, rrb, p1, p2);
@@ -477,7 +506,10 @@ hipError_t bwd(const void* dy, const void* x, const void* y, const float* mean, 
 #define PA_BNB(R, Z) bwd_apply<T, WT, R, Z><<<grid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)y, mean, rstd, \
                                                                  (const WT*)gamma, sums, (T*)dx, (T*)dz, rows, cols, rpb)
   if (relu && dz) PA_BNB(true, true);
-  else if (relu) PA_BNB(true, false);
+  else if (xm)
+    bwd_apply<T, WT, true, false, true><<<grid, 256, 0, st>>>((const T*)dy, (const T*)x, nullptr, mean, rstd,
+                                                              (const WT*)gamma, sums, (T*)dx, nullptr, rows, cols, rpb,
+                                                              (const WT*)beta);
   else if (dz) PA_BNB(false, true);
   else PA_BNB(false, false);
 #undef PA_BNB
@@ -517,11 +549,12 @@ PA_API hipError_t pa_bn_fwd(const void* x, const void* z, const void* gamma, con
 }
 
 // dz (nullable): gradient of the residual input z (= dy masked by ReLU).  y is the saved output
-// (needed only when relu).  dgamma/dbeta in the parameter dtype (nullable; accumulate != 0: +=).
+// (needed only when relu with a residual; ReLU without one recomputes the mask from x, gamma, beta).
+// dgamma/dbeta in the parameter dtype (nullable; accumulate != 0: +=).
 PA_API hipError_t pa_bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd,
-                            const void* gamma, void* dx, void* dz, void* dgamma, void* dbeta, float* ws, int rows,
-                            int cols, int relu, int accumulate, int xd, int wd, hipStream_t st) {
+                            const void* gamma, const void* beta, void* dx, void* dz, void* dgamma, void* dbeta,
+                            float* ws, int rows, int cols, int relu, int accumulate, int xd, int wd, hipStream_t st) {
   if (cols % (xd == 0 ? 4 : 8) != 0 || rows < 1) return hipErrorInvalidValue;
-  PA_BN_DISPATCH(xd, wd, (bn::bwd<T, WT>(dy, x, y, mean, rstd, gamma, dx, dz, dgamma, dbeta, ws, rows, cols, relu,
-                                          accumulate, st)))
+  PA_BN_DISPATCH(xd, wd, (bn::bwd<T, WT>(dy, x, y, mean, rstd, gamma, beta, dx, dz, dgamma, dbeta, ws, rows, cols,
+                                          relu, accumulate, st)))
 }

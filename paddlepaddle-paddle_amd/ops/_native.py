@@ -38,7 +38,7 @@ _SIGS = {
     'pa_maxpool2d_nhwc_bwd': [P, P, P] + [I] * 13 + [P],
     'pa_bn_ws_floats': [I, I, I],
     'pa_bn_fwd': [P, P, P, P, P, P, P, P, P, P, I, I, F, F, I, I, I, I, P],
-    'pa_bn_bwd': [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P],
+    'pa_bn_bwd': [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P],
     'pa_softmax_fwd': [P, P, I, I, I, I, P],
     'pa_softmax_bwd': [P, P, P, I, I, I, P],
     'pa_xent_fwd': [P, P, P, P, I, I, LL, I, P],

@@ -66,7 +66,8 @@ class _BNAct(torch.autograd.Function):
         dg = gs if acc else (torch.empty_like(gamma) if gamma is not None else None)
         db = bs if acc else (torch.empty_like(gamma) if (gamma is not None and ctx.has_beta) else None)
         ws = _ws(rows, C, N.dtcode(x.dtype), x.device)
-        N.check(N.lib.pa_bn_bwd(N.ptr(dy), N.ptr(x), N.ptr(y), N.ptr(mean), N.ptr(rstd), N.ptr(gamma), N.ptr(dx),
+        N.check(N.lib.pa_bn_bwd(N.ptr(dy), N.ptr(x), N.ptr(y), N.ptr(mean), N.ptr(rstd), N.ptr(gamma),
+                                N.ptr(ctx.beta_t), N.ptr(dx),
                                 N.ptr(dz), N.ptr(dg), N.ptr(db), N.ptr(ws), rows, C, int(ctx.relu), int(acc),
                                 N.dtcode(x.dtype), N.dtcode(gamma.dtype) if gamma is not None else 0, N.stream()),
                 'bn_bwd')
