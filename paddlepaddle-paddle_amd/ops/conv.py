@@ -293,6 +293,36 @@ class dgrad_sink:
         return False
 
 
+class SharedDgrad:
+    """Two convolutions reading the same input (a ResNet downsample block's conv1 and shortcut
+    conv): the first backward returns its dX and keeps it; the second accumulates its dX into that
+    tensor in place (the 1x1 dgrad GEMM's beta = 1 epilogue) and returns None, so autograd runs no
+    add of the two branch gradients.  Order-independent; resets for a second backward."""
+    __slots__ = ('buf', 'left')
+
+    def __init__(self):
+        self.buf = None
+        self.left = 2
+
+
+_shared_by_input = {}
+
+
+class shared_dgrad:
+    """Context: conv2d_nhwc calls on ``x`` (same storage and shape) share ``sh``."""
+
+    def __init__(self, x, sh):
+        self.key, self.sh = (x.data_ptr(), tuple(x.shape)), sh
+
+    def __enter__(self):
+        _shared_by_input[self.key] = self.sh
+        return self.sh
+
+    def __exit__(self, *exc):
+        _shared_by_input.pop(self.key, None)
+        return False
+
+
 def _lib_conv_fwd(x, w, b, stride, pad, dil):
     y = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w, b, stride, pad, dil)
     return y.permute(0, 2, 3, 1).contiguous()
@@ -300,10 +330,11 @@ def _lib_conv_fwd(x, w, b, stride, pad, dil):
 
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, dil, sink=None):
+    def forward(ctx, x, w, b, stride, pad, dil, sink=None, shared=None):
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, dil, b is not None)
         ctx.sink = sink
+        ctx.shared = shared
         if _pointwise(w, stride, pad, dil) and w.dtype == torch.bfloat16:
             y = _gemm_fwd_1x1(x, w, b)
             if y is not None:
@@ -322,12 +353,16 @@ class _Conv2dNHWC(torch.autograd.Function):
         sink = ctx.sink.buf if ctx.sink is not None else None
         if ctx.sink is not None:
             ctx.sink.buf = None
+        sh = ctx.shared
+        second = sh is not None and sh.buf is not None and ctx.needs_input_grad[0]
         if ctx.needs_input_grad[0] and _bwd_enabled:
             if pw:
-                gx = _gemm_dgrad_1x1(dy, w, acc=sink)
+                gx = _gemm_dgrad_1x1(dy, w, acc=sh.buf if second else sink)
                 if gx is not None:
                     sink = None  # accumulated in the GEMM epilogue
-            if gx is None:
+                    if second:
+                        gx, second = None, 'done'
+            if gx is None and second != 'done':
                 gx = conv2d_dgrad_classes(dy, w, x.shape[1:3], stride, pad, dil)
         slot_used = False
         if ctx.needs_input_grad[1] and _bwd_enabled and _wgrad_hip and w.shape[0] % 8 == 0:
@@ -358,8 +393,8 @@ class _Conv2dNHWC(torch.autograd.Function):
                 gw = gw.to(w.dtype)
         if has_b and ctx.needs_input_grad[2]:
             gb = dy.sum((0, 1, 2), dtype=torch.float32).to(dy.dtype)
-        mask = [ctx.needs_input_grad[0] and gx is None, ctx.needs_input_grad[1] and gw is None and not slot_used,
-                False]
+        mask = [ctx.needs_input_grad[0] and gx is None and second != 'done',
+                ctx.needs_input_grad[1] and gw is None and not slot_used, False]
         if any(mask):  # shapes the hand-written kernels reject: MIOpen NHWC backward
             lx, lw, _ = torch.ops.aten.convolution_backward(
                 dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), w, None, list(stride), list(pad), list(dil), False,
@@ -370,11 +405,23 @@ class _Conv2dNHWC(torch.autograd.Function):
                 gw = lw
         if sink is not None:  # residual gradient not taken by a GEMM epilogue: plain add
             gx = gx + sink if gx is not None else sink
-        return gx, gw, gb, None, None, None, None
+        if sh is not None and ctx.needs_input_grad[0]:
+            if second == 'done':
+                pass  # this dX went into the first branch's tensor (GEMM beta = 1)
+            elif second:  # this branch's dX came from a non-GEMM kernel: add it to the first's
+                sh.buf.add_(gx)
+                gx = None
+            else:
+                sh.buf = gx  # first branch: keep it for the other branch to accumulate into
+            sh.left -= 1
+            if sh.left == 0:
+                sh.buf, sh.left = None, 2
+        return gx, gw, gb, None, None, None, None, None
 
 
 def conv2d_nhwc(x, w, b, stride, pad, dil):
     sink, _pending_sink[0] = _pending_sink[0], None
     if sink is not None:
         sink.armed = True
-    return _Conv2dNHWC.apply(x, w, b, tuple(stride), tuple(pad), tuple(dil), sink)
+    shared = _shared_by_input.get((x.data_ptr(), tuple(x.shape))) if _shared_by_input else None
+    return _Conv2dNHWC.apply(x, w, b, tuple(stride), tuple(pad), tuple(dil), sink, shared)

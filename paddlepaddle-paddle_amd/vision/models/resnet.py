@@ -82,8 +82,15 @@ class BottleneckBlock(nn.Layer):
         # (ops.conv.GradSink) instead of a separate autograd add of the two branch gradients
         sink = ops.conv.GradSink() if (RESIDUAL_GRAD_SINK and self.downsample is None
                                        and _fused_bn_ok(self.bn3, _unwrap(x))) else None
+        # downsample block: conv1 and the shortcut conv read the same x; their data gradients meet
+        # in one tensor (ops.conv.SharedDgrad) instead of an autograd add
+        shared = ops.conv.SharedDgrad() if (RESIDUAL_GRAD_SINK and self.downsample is not None
+                                            and _fused_bn_ok(self.bn3, _unwrap(x))) else None
         if sink is not None:
             with ops.conv.dgrad_sink(sink):
+                out = self.conv1(x)
+        elif shared is not None:
+            with ops.conv.shared_dgrad(_unwrap(x), shared):
                 out = self.conv1(x)
         else:
             out = self.conv1(x)
@@ -91,7 +98,11 @@ class BottleneckBlock(nn.Layer):
         out = _bn_act(self.bn2, self.conv2(out))
         out = self.conv3(out)
         if self.downsample is not None:
-            identity = self.downsample(x)
+            if shared is not None:
+                with ops.conv.shared_dgrad(_unwrap(x), shared):
+                    identity = self.downsample(x)
+            else:
+                identity = self.downsample(x)
         return _bn_act(self.bn3, out, True, identity, dz_sink=sink if sink is not None and sink.armed else None)
 
 

@@ -1225,3 +1225,38 @@ def test_mlp_fc1_bias_grad_from_dgrad_epilogue():
     for n in finals[0]:
         a, b = finals[0][n], finals[1][n]
         _close(b, a, 1e-2 * float(a.abs().max()) + 1e-4, 1e-2, n)
+
+
+def test_resnet_downsample_block_shared_dgrad():
+    """Downsample bottleneck blocks: conv1's dgrad GEMM accumulates into the shortcut conv's dX
+    (ops.conv.SharedDgrad) — input / weight gradients match the autograd-add path, and a second
+    backward over a retained graph gives the same input gradient again."""
+    import paddle
+    from paddle.vision.models import resnet as R
+    paddle.set_device('gpu:0')
+    grads = []
+    for on in (False, True):
+        R.RESIDUAL_GRAD_SINK = on
+        try:
+            paddle.seed(31)
+            ds = paddle.nn.Sequential(paddle.nn.Conv2D(256, 512, 1, stride=2, bias_attr=False, data_format='NHWC'),
+                                      paddle.nn.BatchNorm2D(512, data_format='NHWC'))
+            blk = R.BottleneckBlock(256, 128, stride=2, downsample=ds, data_format='NHWC')
+            blk = paddle.amp.decorate(blk, level='O2', dtype='bfloat16')
+            g = torch.Generator(device=DEV).manual_seed(32)
+            x = paddle.to_tensor(torch.randn(4, 28, 28, 256, device=DEV, generator=g).bfloat16())
+            x.stop_gradient = False
+            y = blk(x)
+            w = paddle.to_tensor(torch.randn(4, 14, 14, 512, device=DEV, generator=g))
+            (y.astype('float32') * w).sum().backward(retain_graph=True)
+            g1 = x.grad._t.float().clone()
+            x.clear_gradient()
+            (y.astype('float32') * w).sum().backward()
+            g2 = x.grad._t.float().clone()
+            grads.append((g1, g2, blk.conv1.weight.grad._t.float().clone()))
+        finally:
+            R.RESIDUAL_GRAD_SINK = True
+    a, b = grads
+    _close(b[0], a[0], 0.05 * float(a[0].abs().max()) + 1e-3, 0.02, 'dx')
+    _close(b[1], b[0], 1e-6, 0.0, 'dx second backward')
+    _close(b[2], a[2], 0.05 * float(a[2].abs().max()) + 1e-3, 0.02, 'dw1 (twice accumulated)')
