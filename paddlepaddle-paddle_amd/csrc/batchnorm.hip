@@ -20,7 +20,9 @@ namespace pa {
 namespace bn {
 
 constexpr int U = 4;           // rows in flight per lane
-constexpr int kRedBlocks = 512;  // block target of the partial-sum (reduction) passes
+// block target of the partial-sum (reduction) passes (host-side knob pa_bn_tune; the workspace
+// query pa_bn_ws_floats sizes for the current value)
+static int kRedBlocks = 512;
 
 // Lane -> (channel chunk, row phase) map.  Wide rows (>= 256 chunks of E channels): one row per
 // pass, blockIdx.x selects the chunk range.  Narrow rows (C = 64 ... 1024 in ResNet): the block
@@ -557,4 +559,11 @@ PA_API hipError_t pa_bn_bwd(const void* dy, const void* x, const void* y, const 
   if (cols % (xd == 0 ? 4 : 8) != 0 || rows < 1) return hipErrorInvalidValue;
   PA_BN_DISPATCH(xd, wd, (bn::bwd<T, WT>(dy, x, y, mean, rstd, gamma, beta, dx, dz, dgamma, dbeta, ws, rows, cols,
                                           relu, accumulate, st)))
+}
+
+// A/B knob: block target of the BN reduction passes (returns the previous value).
+PA_API int pa_bn_tune(int red_blocks) {
+  const int old = bn::kRedBlocks;
+  if (red_blocks >= 64 && red_blocks <= 8192) bn::kRedBlocks = red_blocks;
+  return old;
 }

@@ -1,0 +1,41 @@
+"""A/B of the BN reduction-pass block target (pa_bn_tune) on the ResNet50 bench step: interleaved
+rounds in one process, ms/step per setting."""
+import os
+import statistics
+import sys
+import types
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+
+def main():
+    import bench
+    import paddle
+    from paddle.ops import _native
+    L = _native._load()
+    paddle.set_device('gpu:0')
+    step, *_ = bench.build_resnet(types.SimpleNamespace(resnet_batch=256), 1, 0, torch.device('cuda', 0))
+    for _ in range(3):
+        step()
+    settings = [int(v) for v in os.environ.get('BN_BLOCKS', '512,1024,2048').split(',')]
+    res = {s: [] for s in settings}
+    for _ in range(4):
+        for s in settings:
+            L.pa_bn_tune(s)
+            step()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                step()
+            e1.record()
+            torch.cuda.synchronize()
+            res[s].append(e0.elapsed_time(e1) / 5)
+    for s in settings:
+        print(f"bn reduction blocks {s:5d}: median {statistics.median(res[s]):.3f} ms/step  min {min(res[s]):.3f}",
+              flush=True)
+
+
+if __name__ == '__main__':
+    main()
