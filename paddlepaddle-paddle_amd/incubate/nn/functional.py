@@ -385,9 +385,12 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     paged prefix).  Static int8 KV caches: with ``cache_k_quant_scales`` / ``cache_v_quant_scales``
     ([Hkv]) the new K/V are stored as clip(round(x * quant_scale)) in int8 caches and read back as
     q * dequant_scale (``cache_*_dequant_scales``); the decode rows then attend over the
-    dequantised pages (composite path).  Dynamic per-batch cache quantisation is not implemented."""
-    if use_dynamic_cachekv_quant:
-        raise NotImplementedError("block_multihead_attention: dynamic KV-cache quantisation is not supported")
+    dequantised pages (composite path).  A uint8 cache stores the value offset by 128 (the
+    reference's layout), an int8 cache stores it as is.  ``use_dynamic_cachekv_quant``: the scales
+    are [B, Hkv] and written here — every prompt sequence of the call gets quant scale
+    max_bound / absmax (per head, over all the call's new K resp. V rows, as the reference's
+    quant_write_cache_int8_kernel does) and dequant scale absmax / max_bound; decode rows
+    quantise and dequantise with their sequence's stored scales."""
     t = _u(qkv)
     kc, vc = _u(key_cache), _u(value_cache)
     qcache = cache_k_quant_scales is not None
@@ -420,11 +423,26 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
         sin = _full_width(cs[1, seq_of.long(), pos.long()], D, use_neox_style)[:, None]
         q = _rope_rows(q, cos, sin, use_neox_style)
         k = _rope_rows(k, cos, sin, use_neox_style)
+    if use_dynamic_cachekv_quant and not qcache:
+        raise ValueError("use_dynamic_cachekv_quant needs the cache_{k,v}_(de)quant_scales tensors ([B, Hkv])")
+    zero_pt = 128.0 if kc.dtype == torch.uint8 else 0.0
     if qcache:  # quantise the new rows into the int8 pages
+        if use_dynamic_cachekv_quant:
+            pre = (enc > 0)
+            if bool(pre.any()):
+                for x_, qs, dqs in ((k, cache_k_quant_scales, cache_k_dequant_scales),
+                                    (v, cache_v_quant_scales, cache_v_dequant_scales)):
+                    amax = x_.float().abs().amax(dim=(0, 2)).clamp_min(1e-30)          # [Hkv]
+                    qv, dv = _u(qs).reshape(B, Hkv), _u(dqs).reshape(B, Hkv)
+                    qv[pre] = (quant_max_bound / amax).to(qv.dtype)
+                    dv[pre] = (amax / quant_max_bound).to(dv.dtype)
+
         def qz(x, sc):
-            v_ = x.float() * _u(sc).float().reshape(1, -1, 1)
+            s_ = _u(sc).float()
+            s_ = s_.reshape(B, Hkv)[seq_of.long()][:, :, None] if use_dynamic_cachekv_quant else s_.reshape(1, -1, 1)
+            v_ = x.float() * s_
             v_ = torch.round(v_) if quant_round_type == 0 else torch.sign(v_) * torch.floor(v_.abs() + 0.5)
-            return v_.clamp(quant_min_bound, quant_max_bound).to(kc.dtype)
+            return (v_.clamp(quant_min_bound, quant_max_bound) + zero_pt).to(kc.dtype)
         blk = bt[seq_of.long(), (pos // bs).long()].long()
         off = (pos % bs).long()
         kc[blk, :, off] = qz(k, cache_k_quant_scales)
@@ -465,8 +483,11 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
             kd = kc[pages].permute(0, 2, 1, 3, 4).reshape(len(pages), Hkv, nblk * bs, D)
             vd = vc[pages].permute(0, 2, 1, 3, 4).reshape(len(pages), Hkv, nblk * bs, D)
             if qcache:
-                kd = (kd.float() * _u(cache_k_dequant_scales).float().reshape(1, -1, 1, 1)).to(q.dtype)
-                vd = (vd.float() * _u(cache_v_dequant_scales).float().reshape(1, -1, 1, 1)).to(q.dtype)
+                def dqz(x_, sc):
+                    s_ = _u(sc).float()
+                    s_ = s_.reshape(B, Hkv)[dec_b.long()] if use_dynamic_cachekv_quant else s_.reshape(1, -1)
+                    return ((x_.float() - zero_pt) * s_[:, :, None, None]).to(q.dtype)
+                kd, vd = dqz(kd, cache_k_dequant_scales), dqz(vd, cache_v_dequant_scales)
             if P:
                 kd = torch.cat([pre_k[dec_b.long()].to(kd.dtype), kd], 2)
                 vd = torch.cat([pre_v[dec_b.long()].to(vd.dtype), vd], 2)

@@ -297,3 +297,49 @@ def test_block_multihead_attention_int8_cache():
     kc2 = _blha_case(6, quant=True)
     assert kc2.numpy().dtype == np.int8
     _blha_case(7, quant=True, pre=2)
+
+
+def test_block_multihead_attention_dynamic_uint8_cache():
+    """Dynamic KV-cache quantisation into uint8 pages (value + 128): a prompt step writes
+    per-(sequence, head) scales max_bound / absmax, a decode step reuses them."""
+    torch.manual_seed(8)
+    Hq, Hkv, D, bs, nblk, B = 2, 2, 8, 4, 8, 2
+    t = paddle.to_tensor
+    kc = torch.zeros(nblk, Hkv, bs, D, dtype=torch.uint8)
+    vc = torch.zeros(nblk, Hkv, bs, D, dtype=torch.uint8)
+    bt = torch.arange(nblk).reshape(B, 4)
+    scales = [torch.zeros(B, Hkv) for _ in range(4)]
+    kw = dict(cache_k_quant_scales=t(scales[0]), cache_v_quant_scales=t(scales[1]),
+              cache_k_dequant_scales=t(scales[2]), cache_v_dequant_scales=t(scales[3]),
+              use_dynamic_cachekv_quant=True)
+    # step 1: sequence 0 is a 5-token prompt, sequence 1 idle
+    qkv1 = torch.randn(5, (Hq + 2 * Hkv) * D)
+    cu1 = _get_padding_offset([5, 0])
+    _, _, kc_t, vc_t = IF.block_multihead_attention(
+        t(qkv1), t(kc), t(vc), t(torch.tensor([[5], [0]])), t(torch.tensor([[0], [0]])), t(torch.tensor([[5], [0]])),
+        None, None, t(cu1), t(cu1), t(bt), block_size=bs, **kw)
+    k1 = qkv1[:, Hq * D:(Hq + Hkv) * D].reshape(5, Hkv, D)
+    v1 = qkv1[:, (Hq + Hkv) * D:].reshape(5, Hkv, D)
+    amax_k, amax_v = k1.abs().amax(dim=(0, 2)), v1.abs().amax(dim=(0, 2))
+    np.testing.assert_allclose(kw['cache_k_quant_scales'].numpy()[0], (127.0 / amax_k).numpy(), rtol=1e-6)
+    np.testing.assert_allclose(kw['cache_v_dequant_scales'].numpy()[0], (amax_v / 127.0).numpy(), rtol=1e-6)
+    assert (kw['cache_k_quant_scales'].numpy()[1] == 0).all()  # the idle sequence keeps its scales
+    kq = kc_t.numpy()[bt[0, 0], :, 0].astype(np.float32) - 128.0
+    np.testing.assert_allclose(kq * (amax_k / 127.0).numpy()[:, None], k1[0].numpy(), atol=float(amax_k.max()) / 127)
+    # step 2: sequence 0 decodes its 6th token against the dequantised prompt
+    qkv2 = torch.randn(1, (Hq + 2 * Hkv) * D)
+    cu2 = _get_padding_offset([1, 0])
+    out, _, _, _ = IF.block_multihead_attention(
+        t(qkv2), kc_t, vc_t, t(torch.tensor([[0], [0]])), t(torch.tensor([[5], [0]])), t(torch.tensor([[1], [0]])),
+        None, None, t(cu2), t(cu2), t(bt), block_size=bs, **kw)
+    qs_k, qs_v = 127.0 / amax_k, 127.0 / amax_v
+
+    def rt(x, s):  # quantise then dequantise, round half away from zero
+        return torch.clamp(torch.sign(x * s[None, :, None]) * torch.floor((x * s[None, :, None]).abs() + 0.5),
+                           -127, 127) / s[None, :, None]
+    k2 = qkv2[:, Hq * D:(Hq + Hkv) * D].reshape(1, Hkv, D)
+    v2 = qkv2[:, (Hq + Hkv) * D:].reshape(1, Hkv, D)
+    kk = torch.cat([rt(k1, qs_k), rt(k2, qs_k)])
+    vv = torch.cat([rt(v1, qs_v), rt(v2, qs_v)])
+    want = _attn(qkv2[:, :Hq * D].reshape(1, Hq, D), kk, vv, causal=False)
+    np.testing.assert_allclose(out.numpy(), want.reshape(1, -1).numpy(), rtol=1e-4, atol=1e-4)
