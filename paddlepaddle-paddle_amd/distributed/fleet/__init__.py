@@ -253,6 +253,14 @@ class HybridParallelOptimizer:
             dist.all_reduce(dist_sq, group=mp.pg)
             sq = dist_sq + rep_sq
         if pp is not None and pp.nranks > 1:
+            # a pipeline-shared weight's copies on later stages are not counted again
+            dup = [p for p in self._inner_opt._parameter_list
+                   if (p.__dict__.get('_pp_shared') or (None, False))[1] and p._t.grad is not None]
+            if dup:
+                d = torch.stack([p._t.grad.float().pow(2).sum() for p in dup]).sum().to(sq.dtype)
+                if mp is not None and mp.nranks > 1 and getattr(dup[0], 'is_distributed', False):
+                    dist.all_reduce(d, group=mp.pg)
+                sq = sq - d
             sq = sq.clone()
             dist.all_reduce(sq, group=pp.pg)
         return sq

@@ -25,6 +25,12 @@ import torch.distributed as dist
 from .....parallel.sharding import ShardingEngine, ShardedOptimizer
 
 
+def _shared_key(p):
+    """Pipeline-shared (SharedLayerDesc) parameters carry (key, duplicate) — see PipelineLayer."""
+    s = p.__dict__.get('_pp_shared')
+    return s[0] if s else None
+
+
 class DygraphShardingOptimizer(ShardedOptimizer):
     _syncs_dp = True  # the pipeline schedule must not all-reduce gradients over dp itself
 
@@ -34,7 +40,7 @@ class DygraphShardingOptimizer(ShardedOptimizer):
         sh = hcg.get_sharding_parallel_group()
         engine = ShardingEngine(None, level=level, group=sh, params=params,
                                 bucket_mb=int(getattr(strategy, 'fuse_grad_size_in_MB', 256) or 256)
-                                if strategy is not None else 256)
+                                if strategy is not None else 256, isolate=_shared_key)
         super().__init__(optimizer, engine)
         self._dist_runs = {dt: self._runs(a, key=lambda p: 1.0 if getattr(p, 'is_distributed', False) else 0.0)
                            for dt, a in engine.arenas.items()}
@@ -51,6 +57,21 @@ class DygraphShardingOptimizer(ShardedOptimizer):
             else:
                 dist.all_reduce(g, group=dp.pg)
                 g.div_(dp.nranks)
+
+    def _shared_units(self):
+        for u in self.engine.units:
+            k = {_shared_key(p) for p in u.params}
+            if len(k) == 1 and None not in k:
+                yield next(iter(k)), u
+
+    @torch.no_grad()
+    def _sync_shared_grads(self, comm):
+        """Sum the gradient shards of each pipeline-shared weight over the stages holding it (its
+        unit has the same parameters, hence the same slicing, on all of them)."""
+        for k, u in self._shared_units():
+            g = comm.get(k)
+            if g is not None:
+                dist.all_reduce(self.engine.gshard(u), group=g.pg)
 
     def _clip_scale(self):
         clip = self._inner._grad_clip
@@ -69,6 +90,11 @@ class DygraphShardingOptimizer(ShardedOptimizer):
                 sq = v if sq is None else sq + v
         if sq is None:
             return None
+        for _, u in self._shared_units():  # a shared weight's copies on later stages: not counted again
+            if u.params[0].__dict__['_pp_shared'][1]:
+                s = self.engine.gshard(u).float().pow(2).sum()
+                isd = 1.0 if getattr(u.params[0], 'is_distributed', False) else 0.0
+                sq = sq - torch.stack([s * isd, s * (1.0 - isd)])
         if self.engine.world > 1:
             dist.all_reduce(sq, group=self.engine.pg)  # shards -> this stage's full local norm
         mp = self._hcg.get_model_parallel_group()

@@ -87,9 +87,9 @@ class PipelineLayer(Layer):
         self._start, self._end = lo, hi
         self.run_function = []
         self._chunks = []
-        self.shared_layers = {}
+        from ....nn.layer.container import LayerDict, LayerList
+        self.shared_layers = LayerDict()  # registered: the optimizer sees the shared weights
         self._shared_descs = {}
-        from ....nn.layer.container import LayerList
         built = []
         for lo_k, hi_k in self._chunk_ranges:
             start = len(self.run_function)
@@ -138,10 +138,22 @@ class PipelineLayer(Layer):
             stages = sorted(stages)
             if len(stages) < 2:
                 continue
-            ranks = [self._hcg.get_rank_from_stage(s) for s in stages]
-            g = new_group(ranks)
+            # one group per pipeline replica (every rank creates every group, in the same order)
+            me = dist.get_rank()
+            for pipe_ranks in self._hcg.topology().get_comm_list('pipe'):
+                ranks = [pipe_ranks[s] for s in stages]
+                g_ = new_group(ranks)
+                if me in ranks:
+                    g = g_
             if self._stage_id in stages:
+                ranks = [self._hcg.get_rank_from_stage(s) for s in stages]
                 comm[k] = g
+                for p in self.shared_layers[k].parameters():
+                    # (key, counted elsewhere): a sharding optimizer gives these their own unit so
+                    # the stages' shards line up, and global-norm clipping counts them on one stage
+                    p.__dict__['_pp_shared'] = (k, self._stage_id != stages[0])
+                    with torch.no_grad():  # every copy starts from the first holder's weights
+                        dist.broadcast(p._t, ranks[0], group=g.pg)
         return comm
 
     def allreduce_shared_weight_gradients(self):
@@ -348,11 +360,12 @@ class PipelineParallel(Layer):
             self._bwd_step(*pending.pop(0))
         assert not (self._act_q or self._grad_q or self._acts_left or self._grads_left), "unmatched pipeline receives"
         self._drain_sends()
-        if getattr(optimizer, '_syncs_dp', False) and self._layers._shared_comm:
-            # the sharding optimizer reduce-scatters gradients inside backward, before this point
-            raise NotImplementedError("pipeline SharedLayerDesc weights with sharding_degree > 1: tie the "
-                                      "weights inside one stage or use sharding_degree 1")
-        self._layers.allreduce_shared_weight_gradients()
+        if getattr(optimizer, '_syncs_dp', False):
+            # the sharding optimizer reduce-scattered the gradients inside backward: sum the shared
+            # weights' shards (own units, identical slicing on every holder) over their stages
+            optimizer._sync_shared_grads(self._layers._shared_comm)
+        else:
+            self._layers.allreduce_shared_weight_gradients()
         if self._dp_group is not None and self._dp_group.nranks > 1 and not getattr(optimizer, '_syncs_dp', False):
             # one coalesced all-reduce per dtype (a sharding optimizer syncs dp on its shards instead)
             from ..utils.hybrid_parallel_util import fused_allreduce_gradients
@@ -491,11 +504,12 @@ class PipelineParallelWithInterleave(PipelineParallel):
                 if not (first_rank and v == 0):
                     self._send(_unwrap(x).grad, prev_rank, 'grad')
         self._drain_sends()
-        if getattr(optimizer, '_syncs_dp', False) and self._layers._shared_comm:
-            # the sharding optimizer reduce-scatters gradients inside backward, before this point
-            raise NotImplementedError("pipeline SharedLayerDesc weights with sharding_degree > 1: tie the "
-                                      "weights inside one stage or use sharding_degree 1")
-        self._layers.allreduce_shared_weight_gradients()
+        if getattr(optimizer, '_syncs_dp', False):
+            # the sharding optimizer reduce-scattered the gradients inside backward: sum the shared
+            # weights' shards (own units, identical slicing on every holder) over their stages
+            optimizer._sync_shared_grads(self._layers._shared_comm)
+        else:
+            self._layers.allreduce_shared_weight_gradients()
         if self._dp_group is not None and self._dp_group.nranks > 1 and not getattr(optimizer, '_syncs_dp', False):
             # one coalesced all-reduce per dtype (a sharding optimizer syncs dp on its shards instead)
             from ..utils.hybrid_parallel_util import fused_allreduce_gradients

@@ -125,7 +125,7 @@ class _PreBackward(torch.autograd.Function):
 class ShardingEngine:
     def __init__(self, model, level='p_g_os', group=None, bucket_mb=256, segment_size=2 ** 20,
                  release_grads=True, persistent_types=None, persistent_below=None, params=None, alias=None,
-                 reduce_dtype=None):
+                 reduce_dtype=None, isolate=None):
         """model: the Layer to shard; or model=None with ``params`` (a parameter list) for stage 1/2
         (the hybrid-parallel sharding optimizer, which only sees its optimizer's parameters).
 
@@ -133,7 +133,10 @@ class ShardingEngine:
         PADDLE_AMD_SHARDING_ALIAS=0) runs the multi-rank code path on one rank — release, gather,
         re-materialise, shard copy — so it can be exercised on a single GPU.
         reduce_dtype: 'float32' reduce-scatters low-precision gradients in fp32 (fp32 main-grad
-        communication, 2x the bytes) into an fp32 gradient arena; default: the parameter dtype."""
+        communication, 2x the bytes) into an fp32 gradient arena; default: the parameter dtype.
+        isolate: stage 1/2 only — ``isolate(p)`` returns a key or None; parameters with the same key
+        form a unit of their own (pipeline-shared weights, whose shards must line up across the
+        stages that hold a copy)."""
         self.model = model
         self.level = LEVELS[level] if isinstance(level, str) else int(level)
         if model is None and (params is None or self.level == 3):
@@ -166,7 +169,7 @@ class ShardingEngine:
         if self.level == 3:
             self.units = self._layer_units(model, segment_size)
         else:
-            self.units = self._bucket_units(params, bucket_mb)
+            self.units = self._bucket_units(params, bucket_mb, isolate)
         for i, u in enumerate(self.units):
             u.index = i
         self._build_arenas()
@@ -195,11 +198,18 @@ class ShardingEngine:
         from .data_parallel import sync_params_buffers
         sync_params_buffers(self.model, self.group)
 
-    def _bucket_units(self, params, bucket_mb):
+    def _bucket_units(self, params, bucket_mb, isolate=None):
         units = []
         by_dt = {}
+        own = {}
         for p in params:
-            by_dt.setdefault(p._t.dtype, []).append(p)
+            k = isolate(p) if isolate is not None else None
+            if k is not None:
+                own.setdefault((k, p._t.dtype), []).append(p)
+            else:
+                by_dt.setdefault(p._t.dtype, []).append(p)
+        for _, ps in sorted(own.items(), key=lambda kv: str(kv[0])):
+            units.append(_Unit(self, ps, None, True))
         cap = bucket_mb * 2 ** 20
         for dt, ps in by_dt.items():
             cur, size = [], 0

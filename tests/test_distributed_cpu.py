@@ -252,3 +252,16 @@ def test_llama_hybrid_tp2_pp2_sharding2_matches_single_device(clip):
 def test_distributed_scaler_agrees_on_overflow():
     out = run_workers('worker_scaler.py')
     assert out.count('scaler OK') == 2, out[-3000:]
+
+
+@pytest.mark.parametrize("clip,shard", [('0', '1'), ('0.05', '1'), ('0.05', '0')])
+def test_pipeline_shared_weight_with_sharding(clip, shard):
+    """SharedLayerDesc (tied embedding / head across two stages) with sharding_degree 2 (or a
+    plain dp axis): the shared weight's gradient is summed over the stages; clipping counts it once."""
+    os.environ['CLIP'], os.environ['SHARD'] = clip, shard
+    try:
+        out = run_workers('worker_pp_shared_sharding.py', nproc=4, timeout=300)
+    finally:
+        os.environ.pop('CLIP', None)
+        os.environ.pop('SHARD', None)
+    assert out.count("shared-weight OK") == 4, out[-3000:]
