@@ -502,6 +502,19 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     return _w(o), qkv, key_cache, value_cache
 
 
+def _ring_group(ring_id):
+    from ...distributed.communication import get_group
+    g = get_group(ring_id) if ring_id else None
+    if g is None:
+        from ...distributed import fleet
+        hcg = fleet.get_hybrid_communicate_group() if hasattr(fleet, 'get_hybrid_communicate_group') else None
+        g = hcg.get_model_parallel_group() if hcg is not None else None
+    if g is None:
+        raise ValueError(f"ring_id {ring_id}: no such communication group (create it with "
+                         "paddle.distributed.new_group or fleet.init)")
+    return g
+
+
 def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, linear_weights, linear_biases,
                             ffn_ln_scales, ffn_ln_biases, ffn1_weights, ffn1_biases, ffn2_weights, ffn2_biases,
                             pre_layer_norm=True, epsilon=1e-05, residual_alpha=1.0, cache_kvs=None, beam_offset=None,
@@ -523,9 +536,20 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
 
     ``pre_caches[i]`` ([2, B, Hkv, P, D], a shared prefix such as a system prompt) is attended to
     ahead of the sequence by every query (prefill and decode); ``beam_offset`` [B / beam, beam, L]
-    selects, per beam and past position, the cache row of the beam it descends from (decode)."""
-    if ring_id != -1:
-        raise NotImplementedError("fused_multi_transformer: use the mpu layers for tensor parallelism (ring_id)")
+    selects, per beam and past position, the cache row of the beam it descends from (decode).
+
+    Tensor parallelism (``ring_id`` != -1): the caller passes this rank's shard — qkv / ffn1 weights
+    split by heads / columns, out-linear / ffn2 weights split by rows — and the partial outputs of
+    the out-linear and ffn2 GEMMs are all-reduced over the group ``ring_id`` (a
+    paddle.distributed group id; the fleet model-parallel group when no such group exists) before
+    their (replicated) biases are added."""
+    tp_group = _ring_group(ring_id) if ring_id != -1 else None
+
+    def row_parallel(t, w, b):
+        o_ = lin(t, w, None)
+        import torch.distributed as tdist
+        tdist.all_reduce(o_, group=tp_group.pg)
+        return o_ + _u(b).reshape(1, -1).to(o_.dtype) if b is not None else o_
     h = _u(x)
     B, S, E = h.shape
     nl = len(qkv_weights)
@@ -631,7 +655,8 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
             o = ops.decode.decode_attention(q[:, 0], kc.contiguous(), vc.contiguous(), lens, mask=m)[:, None]
         if cache is not None:
             caches_out.append(cache_kvs[i])
-        o = lin(o.reshape(B, S, Hq * D), linear_weights[i], linear_biases[i] if linear_biases is not None else None)
+        o = (row_parallel if tp_group is not None else lin)(
+            o.reshape(B, S, Hq * D), linear_weights[i], linear_biases[i] if linear_biases is not None else None)
         h = resid * residual_alpha + o.reshape(B, S, E).to(resid.dtype)
         if not pre_layer_norm:
             h = norm(h, ln_scales[i], ln_biases[i] if ln_biases is not None else None)
@@ -639,7 +664,8 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
         f = norm(h, ffn_ln_scales[i], ffn_ln_biases[i] if ffn_ln_biases is not None else None) if pre_layer_norm \
             else h
         f = act(lin(f, ffn1_weights[i], ffn1_biases[i] if ffn1_biases is not None else None))
-        f = lin(f, ffn2_weights[i], ffn2_biases[i] if ffn2_biases is not None else None)
+        f = (row_parallel if tp_group is not None else lin)(
+            f, ffn2_weights[i], ffn2_biases[i] if ffn2_biases is not None else None)
         h = resid * residual_alpha + f.reshape(B, S, E).to(resid.dtype)
         if not pre_layer_norm:
             h = norm(h, ffn_ln_scales[i], ffn_ln_biases[i] if ffn_ln_biases is not None else None)

@@ -265,3 +265,8 @@ def test_pipeline_shared_weight_with_sharding(clip, shard):
         os.environ.pop('CLIP', None)
         os.environ.pop('SHARD', None)
     assert out.count("shared-weight OK") == 4, out[-3000:]
+
+
+def test_fused_multi_transformer_ring_id_tensor_parallel():
+    out = run_workers('worker_fmt_tp.py', nproc=2, timeout=300)
+    assert out.count("fmt tp OK") == 2, out[-3000:]
