@@ -185,18 +185,34 @@ def fused_bias_act(x, bias=None, dequant_scales=None, shift=None, smooth=None, a
     return _w({'gelu': TF.gelu, 'silu': TF.silu, 'relu': torch.relu}[act_method](t))
 
 
+def _tp_in(h, g):
+    from ...distributed.fleet.layers.mpu.mp_ops import _c_identity
+    return _c_identity(h, group=g)  # identity forward, gradient all-reduced backward
+
+
+def _tp_out(o, bias, g):
+    from ...distributed.fleet.layers.mpu.mp_ops import _mp_allreduce
+    o = _mp_allreduce(o, group=g)
+    return o + bias if bias is not None else o
+
+
 def fused_feedforward(x, linear1_weight, linear2_weight, linear1_bias=None, linear2_bias=None, ln1_scale=None,
                       ln1_bias=None, ln2_scale=None, ln2_bias=None, dropout1_rate=0.5, dropout2_rate=0.5,
                       activation="relu", ln1_epsilon=1e-5, ln2_epsilon=1e-5, pre_layer_norm=False, training=True,
                       mode='upscale_in_train', ring_id=-1, add_residual=True, name=None):
+    """ring_id != -1: tensor parallel over that group — linear1 column-parallel (this rank's
+    columns), linear2 row-parallel (its rows; the partial outputs all-reduced before the bias)."""
     residual = x
     h = x
     if pre_layer_norm:
         h = F.layer_norm(h, [_u(x).shape[-1]], ln1_scale, ln1_bias, ln1_epsilon)
+    g = _ring_group(ring_id) if ring_id != -1 else None
+    if g is not None:
+        h = _tp_in(h, g)
     h = F.linear(h, linear1_weight, linear1_bias)
     h = getattr(F, activation)(h)
     h = F.dropout(h, dropout1_rate, training=training, mode=mode)
-    h = F.linear(h, linear2_weight, linear2_bias)
+    h = F.linear(h, linear2_weight, linear2_bias) if g is None else _tp_out(F.linear(h, linear2_weight), linear2_bias, g)
     if add_residual:
         h = fused_dropout_add(h, residual, dropout2_rate, training, mode)
     else:
@@ -211,19 +227,24 @@ def fused_multi_head_attention(x, qkv_weight, linear_weight, pre_layer_norm=Fals
                                linear_bias=None, cache_kv=None, attn_mask=None, dropout_rate=0.5,
                                attn_dropout_rate=0.5, ln_epsilon=1e-05, training=True, mode='upscale_in_train',
                                ring_id=-1, add_residual=True, num_heads=-1, transpose_qkv_wb=False, name=None):
-    """qkv_weight: [3, H, D, E] (reference layout) or [E, 3E] with transpose_qkv_wb=True."""
+    """qkv_weight: [3, H, D, E] (reference layout) or [E, 3E] with transpose_qkv_wb=True.
+    ring_id != -1: tensor parallel over that group — this rank's heads of qkv_weight / qkv_bias
+    and rows of linear_weight; the out-linear partials are all-reduced before linear_bias."""
     t = _u(x)
     B, S, E = t.shape
     h = x
     if pre_layer_norm:
         h = F.layer_norm(h, [E], pre_ln_scale, pre_ln_bias, pre_ln_epsilon)
+    g = _ring_group(ring_id) if ring_id != -1 else None
+    if g is not None:
+        h = _tp_in(h, g)  # with transpose_qkv_wb, num_heads is this rank's head count
     w = _u(qkv_weight)
     if transpose_qkv_wb:
         qkv = torch.matmul(_u(h), w)
         if qkv_bias is not None:
             qkv = qkv + _u(qkv_bias)
         H = num_heads
-        qkv = qkv.reshape(B, S, 3, H, E // H)
+        qkv = qkv.reshape(B, S, 3, H, qkv.shape[-1] // (3 * H))
     else:
         _, H, D, _ = w.shape
         qkv = torch.einsum('bse,thde->bsthd', _u(h), w)
@@ -232,7 +253,7 @@ def fused_multi_head_attention(x, qkv_weight, linear_weight, pre_layer_norm=Fals
     q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
     o = F.scaled_dot_product_attention(_w(q), _w(k), _w(v), attn_mask, attn_dropout_rate, False, training)
     o = _w(_u(o).reshape(B, S, -1))
-    o = F.linear(o, linear_weight, linear_bias)
+    o = F.linear(o, linear_weight, linear_bias) if g is None else _tp_out(F.linear(o, linear_weight), linear_bias, g)
     if add_residual:
         o = fused_dropout_add(o, x, dropout_rate, training, mode)
     if not pre_layer_norm:

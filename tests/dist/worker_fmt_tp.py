@@ -39,6 +39,34 @@ def main():
     want = IF.fused_multi_transformer(t(x), **wrap(full))
     got = IF.fused_multi_transformer(t(x), ring_id=g.id, **wrap(part))
     np.testing.assert_allclose(got.numpy(), want.numpy(), rtol=1e-4, atol=1e-5)
+    # fused_feedforward / fused_multi_head_attention (training path): outputs and input gradients
+    w1, b1, w2, b2 = rnd(E, F), rnd(F), rnd(F, E), rnd(E)
+    xf = t(x)
+    xf.stop_gradient = False
+    ref = IF.fused_feedforward(xf, t(w1), t(w2), t(b1), t(b2), dropout1_rate=0.0, dropout2_rate=0.0)
+    ref.sum().backward()
+    gref = xf.grad.numpy().copy()
+    xp = t(x)
+    xp.stop_gradient = False
+    out = IF.fused_feedforward(xp, t(w1[:, fs].contiguous()), t(w2[fs].contiguous()), t(b1[fs].contiguous()), t(b2),
+                               dropout1_rate=0.0, dropout2_rate=0.0, ring_id=g.id)
+    out.sum().backward()
+    np.testing.assert_allclose(out.numpy(), ref.numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(xp.grad.numpy(), gref, rtol=1e-4, atol=1e-5)
+    qw, qb, lw, lb = rnd(3, H, D, E), rnd(3 * H * D), rnd(H * D, E), rnd(E)
+    xa = t(x)
+    xa.stop_gradient = False
+    ref = IF.fused_multi_head_attention(xa, t(qw), t(lw), qkv_bias=t(qb), linear_bias=t(lb), dropout_rate=0.0,
+                                        attn_dropout_rate=0.0)
+    ref.sum().backward()
+    xb = t(x)
+    xb.stop_gradient = False
+    out = IF.fused_multi_head_attention(xb, t(qw[:, hs].contiguous()), t(lw[hs.start * D:hs.stop * D].contiguous()),
+                                        qkv_bias=t(qb.reshape(3, H, D)[:, hs].reshape(-1).contiguous()),
+                                        linear_bias=t(lb), dropout_rate=0.0, attn_dropout_rate=0.0, ring_id=g.id)
+    out.sum().backward()
+    np.testing.assert_allclose(out.numpy(), ref.numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(xb.grad.numpy(), xa.grad.numpy(), rtol=1e-4, atol=1e-5)
     print(f"rank{r} fmt tp OK", flush=True)
     dist.barrier()
 
