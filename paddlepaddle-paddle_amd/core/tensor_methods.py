@@ -108,6 +108,10 @@ def install(namespace_funcs):
             '__ifloordiv__': 'floor_divide_', '__imod__': 'remainder_', '__ipow__': 'pow_'}
     for k, m in iops.items():
         setattr(T, k, _ibinop(m))
+    # `a @ b` goes through the AMP-tagged paddle.matmul (matmul_v2 is a white-list op)
+    _mm = namespace_funcs['matmul']
+    T.__matmul__ = lambda self, other: _mm(self, other if isinstance(other, Tensor) else _wrap(torch.as_tensor(other, device=self._t.device)))
+    T.__rmatmul__ = lambda self, other: _mm(other if isinstance(other, Tensor) else _wrap(torch.as_tensor(other, device=self._t.device)), self)
     T.__neg__ = lambda self: _wrap(-self._t)
     T.__pos__ = lambda self: self
     T.__abs__ = lambda self: _wrap(self._t.abs())

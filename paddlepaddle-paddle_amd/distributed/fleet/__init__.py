@@ -257,10 +257,18 @@ class HybridParallelOptimizer:
             dup = [p for p in self._inner_opt._parameter_list
                    if (p.__dict__.get('_pp_shared') or (None, False))[1] and p._t.grad is not None]
             if dup:
-                d = torch.stack([p._t.grad.float().pow(2).sum() for p in dup]).sum().to(sq.dtype)
-                if mp is not None and mp.nranks > 1 and getattr(dup[0], 'is_distributed', False):
-                    dist.all_reduce(d, group=mp.pg)
-                sq = sq - d
+                def _sq(ps):
+                    if not ps:
+                        return torch.zeros_like(sq)
+                    return torch.stack([p._t.grad.float().pow(2).sum() for p in ps]).sum().to(sq.dtype)
+                dup_dist = [p for p in dup if getattr(p, 'is_distributed', False)]
+                dup_rep = [p for p in dup if not getattr(p, 'is_distributed', False)]
+                d_dist = _sq(dup_dist)
+                if mp is not None and mp.nranks > 1:
+                    # tensor-parallel shards of a shared weight were summed over mp above; the
+                    # same ranks hold the same stage, so this collective is uniform over mp
+                    dist.all_reduce(d_dist, group=mp.pg)
+                sq = sq - d_dist - _sq(dup_rep)
             sq = sq.clone()
             dist.all_reduce(sq, group=pp.pg)
         return sq

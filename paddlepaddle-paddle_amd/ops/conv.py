@@ -413,10 +413,18 @@ class _Conv2dNHWC(torch.autograd.Function):
                 gx = None
             else:
                 sh.buf = gx  # first branch: keep it for the other branch to accumulate into
+                # reset at the end of this backward pass whatever happens to the other branch
+                # (it may have run on a library conv, or not at all): a retained-graph second
+                # backward then starts clean
+                torch.autograd.Variable._execution_engine.queue_callback(lambda sh=sh: _reset_shared(sh))
             sh.left -= 1
             if sh.left == 0:
                 sh.buf, sh.left = None, 2
         return gx, gw, gb, None, None, None, None, None
+
+
+def _reset_shared(sh):
+    sh.buf, sh.left = None, 2
 
 
 def conv2d_nhwc(x, w, b, stride, pad, dil):

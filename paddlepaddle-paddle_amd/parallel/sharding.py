@@ -462,8 +462,16 @@ class ShardingEngine:
         if self.model is None or self.level == 3:
             self.wait_param_gathers()
         elif not getattr(self, '_gather_hook_installed', False):
-            self.model.register_forward_pre_hook(lambda layer, inputs: self.wait_param_gathers())
+            # every sublayer waits before it runs or hands out its state dict, so a read through
+            # the original (inner) layer never sees a half-written parameter
+            for layer in self.model.sublayers(include_self=True):
+                layer.register_forward_pre_hook(lambda layer, inputs: self.wait_param_gathers())
+                layer.register_state_dict_hook(self._state_dict_wait)
             self._gather_hook_installed = True
+
+    def _state_dict_wait(self, dest):
+        self.wait_param_gathers()
+        return None
 
     def wait_param_gathers(self):
         ws, self._gather_works = self._gather_works, []
@@ -499,9 +507,14 @@ class ShardedOptimizer:
         if self._kind in ('SGD', 'Momentum'):  # L2 regularisation coefficient (added to the gradient)
             from ..regularizer import L2Decay
             reg = getattr(p, 'regularizer', None) or opt.regularization
+            if reg is None:
+                return 0.0
             if isinstance(reg, (int, float)):
                 return float(reg)
-            return float(reg._coeff) if isinstance(reg, L2Decay) else 0.0
+            if isinstance(reg, L2Decay):
+                return float(reg._coeff)
+            raise NotImplementedError(f"group-sharded {self._kind} supports L2Decay regularisation only, got "
+                                      f"{type(reg).__name__}")
         if not self._decoupled:
             return 0.0
         f = getattr(opt, '_apply_decay_param_fun', None)
@@ -582,11 +595,12 @@ class ShardedOptimizer:
                 g = a['grad'][lo:hi].float()
                 if scale is not None:
                     g = g * scale
+                if mom and rescale != 1.0:
+                    g = g * rescale  # reference momentum: rescale_grad * g + coeff * param
                 if coeff:
                     g = g + coeff * master
                 if mom:
                     v = a['m'][lo:hi]
-                    g = g * rescale
                     v.mul_(mu).add_(g)
                     upd = g + mu * v if nesterov else v
                 else:
@@ -636,6 +650,7 @@ class ShardedOptimizer:
         self.step()
 
     def state_dict(self):
+        self.engine.wait_param_gathers()
         sd = {}
         for dt, a in self.engine.arenas.items():
             key = str(dt).replace('torch.', '')

@@ -89,7 +89,15 @@ def main():
     else:
         model, opt, _ = dist.sharding.group_sharded_parallel(model, opt, level=mode, segment_size=64)
     train(model, opt, rank, world, split=True)
-    got, want = params_of(model), params_of(ref)
+    want = params_of(ref)
+    if mode in ('os', 'os_g'):
+        # read through the ORIGINAL layer right after the last step: the stage-1/2 parameter
+        # all-gathers are asynchronous and must be waited for by the inner state_dict
+        inner = {k: v.numpy().astype(np.float64) for k, v in model._layers.state_dict().items()}
+        for k in want:
+            err = np.abs(inner[k] - want[k]).max()
+            assert err < 2e-5, ('inner', mode, kind, k, err)
+    got = params_of(model)
     for k in want:
         err = np.abs(got[k] - want[k]).max()
         assert err < 2e-5, (mode, kind, k, err)

@@ -133,3 +133,20 @@ def test_check_numerics_abort():
         debugging.check_numerics(t, 'op', 'x')
     stats, vals = debugging.check_numerics(t, 'op', 'x', debugging.DebugMode.CHECK_NAN_INF)
     assert stats.numpy().tolist()[:2] == [1, 0]
+
+
+def test_matmul_operator_follows_amp_lists():
+    """`a @ b` is matmul_v2 (white list): low precision under O1, and a bf16 activation times an fp32
+    weight is cast instead of raising a dtype mismatch."""
+    a, w = _x(4, 8), _x(8, 3)
+    with paddle.amp.auto_cast(level='O1', dtype='bfloat16'):
+        y = a @ w
+        assert y.dtype == paddle.bfloat16
+        h = paddle.nn.Linear(8, 8)(a)                # bf16 activation
+        z = h @ w                                    # fp32 weight
+        assert z.dtype == paddle.bfloat16
+        r = w.t() @ a.t()                            # __matmul__ on the other operand order
+        assert r.dtype == paddle.bfloat16
+    y32 = a @ w
+    assert y32.dtype == paddle.float32
+    np.testing.assert_allclose(y.astype('float32').numpy(), y32.numpy(), rtol=3e-2, atol=3e-2)
