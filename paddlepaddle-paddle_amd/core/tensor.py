@@ -147,6 +147,8 @@ class Tensor:
 
     @property
     def imag(self):
+        if not self._t.is_complex():  # a real tensor's imaginary part is zero
+            return _wrap(torch.zeros_like(self._t))
         return _wrap(torch.imag(self._t))
 
     @property

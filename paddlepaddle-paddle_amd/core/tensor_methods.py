@@ -7,12 +7,11 @@ import torch
 
 from .tensor import Tensor, _wrap, _unwrap
 
-_SKIP = {'to_tensor', 'is_tensor', 'create_parameter', 'create_tensor', 'meshgrid', 'arange', 'linspace', 'logspace',
+_SKIP = {'to_tensor', 'meshgrid', 'arange', 'linspace', 'logspace',
          'eye', 'zeros', 'ones', 'empty', 'full', 'rand', 'randn', 'randint', 'randperm', 'uniform', 'normal',
-         'standard_normal', 'gaussian', 'log_normal', 'tril_indices', 'triu_indices', 'fill_constant', 'broadcast_shape',
-         'shape', 'numel', 'rank', 'is_empty', 'complex', 'polar', 'concat', 'stack', 'hstack', 'vstack', 'dstack',
-         'column_stack', 'row_stack', 'broadcast_tensors', 'add_n', 'einsum', 'block_diag', 'multiplex', 'where',
-         'scatter_nd', 'to_dlpack', 'assign', 'combinations'}
+         'standard_normal', 'gaussian', 'log_normal', 'tril_indices', 'triu_indices', 'fill_constant',
+         'shape', 'numel', 'complex', 'hstack', 'vstack', 'dstack',
+         'column_stack', 'row_stack', 'einsum', 'where', 'to_dlpack', 'assign'}
 _KEEP_NATIVE = {'to', 'astype', 'cast', 'clone', 'detach', 'numpy', 'item', 'tolist', 'cpu', 'cuda', 'backward',
                 'register_hook', 'contiguous', 'is_contiguous', 'dim', 'numel', 'fill_', 'zero_', 'copy_', 'apply',
                 'apply_', 'set_value', 'is_floating_point', 'is_complex', 'is_integer', 'element_size', 'data_ptr'}
@@ -139,3 +138,6 @@ def install(namespace_funcs):
     T.masked_fill = namespace_funcs['masked_fill']
     T.where = lambda self, x=None, y=None, name=None: namespace_funcs['where'](self, x, y)
     T.norm = namespace_funcs['norm']
+    from .. import signal as _signal
+    T.stft = _signal.stft
+    T.istft = _signal.istft

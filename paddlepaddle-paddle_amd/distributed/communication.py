@@ -482,3 +482,20 @@ class stream:
                            use_calc_stream=False: scatter(tensor, tensor_or_tensor_list, src, group, sync_op))
     gather = staticmethod(lambda tensor, gather_list=None, dst=0, group=None, sync_op=True, use_calc_stream=False:
                           gather(tensor, gather_list, dst, group, sync_op))
+
+
+def _register_stream_module():
+    """``paddle.distributed.communication.stream`` as an importable module (reference:
+    python/paddle/distributed/communication/stream/__init__.py)."""
+    import sys
+    import types
+    mod = types.ModuleType(__name__ + '.stream', stream.__doc__)
+    for k, v in vars(stream).items():
+        if not k.startswith('_'):
+            setattr(mod, k, v.__func__ if isinstance(v, staticmethod) else v)
+    mod.__all__ = [k for k in vars(mod) if not k.startswith('_')]
+    sys.modules[mod.__name__] = mod
+    return mod
+
+
+_register_stream_module()

@@ -59,3 +59,12 @@ def identity_loss(x, reduction="none"):
 __all__ = ['LookAhead', 'ModelAverage', 'softmax_mask_fuse_upper_triangle', 'softmax_mask_fuse', 'graph_send_recv',
            'graph_khop_sampler', 'graph_sample_neighbors', 'graph_reindex', 'segment_sum', 'segment_mean',
            'segment_max', 'segment_min', 'identity_loss']
+
+
+def __getattr__(name):
+    if name == 'distributed':  # lazy: pulls in paddle.distributed
+        import importlib
+        m = importlib.import_module('.distributed', __name__)
+        globals()[name] = m
+        return m
+    raise AttributeError(f"module {__name__!r} has no attribute {name!r}")

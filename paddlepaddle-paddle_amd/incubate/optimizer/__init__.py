@@ -4,7 +4,7 @@ import contextlib
 
 import torch
 
-from ..core.tensor import _unwrap
+from ...core.tensor import _unwrap
 
 
 class LookAhead:
@@ -89,4 +89,5 @@ class ModelAverage:
                     _unwrap(p).copy_(self._backup.pop(id(p)))
 
 
-from ..optimizer.algorithms import LBFGS  # noqa: E402,F401  (reference: incubate/optimizer/lbfgs.py)
+from ...optimizer.algorithms import LBFGS  # noqa: E402,F401  (reference: incubate/optimizer/lbfgs.py)
+from . import functional  # noqa: E402,F401

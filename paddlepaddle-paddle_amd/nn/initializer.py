@@ -206,3 +206,18 @@ def set_global_initializer(weight_init, bias_init=None):
 
 def _global_init(is_bias):
     return _global_bias_init if is_bias else _global_weight_init
+
+
+def _register_lazy_init():
+    """``paddle.nn.initializer.lazy_init`` (reference: nn/initializer/lazy_init.py: LazyGuard)."""
+    import sys
+    import types
+    from ..framework import LazyGuard
+    m = types.ModuleType(__name__ + '.lazy_init')
+    m.LazyGuard = LazyGuard
+    m.__all__ = ['LazyGuard']
+    sys.modules[m.__name__] = m
+    return m
+
+
+lazy_init = _register_lazy_init()

@@ -194,6 +194,68 @@ class AbsmaxObserver(ObserverFactory):
         return AbsmaxObserverLayer
 
 
+class GroupWiseWeightObserverLayer(BaseObserver):
+    """Per-group abs-max of a 2-D [in, out] weight: groups of ``group_size`` input rows, one
+    scale per (group, output column) — reference quantization/observers/groupwise.py."""
+
+    def __init__(self, layer=None, quant_bits=8, group_size=128):
+        super().__init__()
+        self._quant_bits = quant_bits
+        self.group_size = group_size
+        self._max = None
+        self._scale = None
+        self._zero_point = None
+
+    def forward(self, inputs):
+        self._max = self._cal_abs_max(inputs)
+        return inputs
+
+    def _cal_abs_max(self, inputs):
+        x = _unwrap(inputs)
+        assert self.group_size in (64, 128), "group_size only support 64 or 128"
+        assert x.dim() == 2, "Currently only support 2D tensor"
+        assert x.shape[0] % self.group_size == 0, "group_size must be a factor of input channels"
+        g = x.detach().t().reshape(x.shape[1], x.shape[0] // self.group_size, self.group_size)
+        m = g.abs().amax(dim=2).float()
+        m = torch.where(m == 0, torch.full_like(m, 1e-8), m)
+        return _wrap(m.t().contiguous())
+
+    def min_value(self):
+        return 0.0
+
+    def max_value(self):
+        return self._max
+
+    def bit_length(self):
+        return self._quant_bits
+
+    def quant_axis(self):
+        return -1
+
+    def cal_thresholds(self):
+        if self._scale is None:
+            self._scale = self._max
+        self._zero_point = _wrap(torch.zeros_like(_unwrap(self._scale)))
+
+    def scales(self):
+        if self._scale is None:
+            self.cal_thresholds()
+        return self._scale
+
+    def zero_points(self):
+        if self._zero_point is None:
+            self.cal_thresholds()
+        return self._zero_point
+
+
+class GroupWiseWeightObserver(ObserverFactory):
+    def __init__(self, quant_bits=8, group_size=128):
+        super().__init__(quant_bits=quant_bits, group_size=group_size)
+
+    def _get_class(self):
+        return GroupWiseWeightObserverLayer
+
+
 class LinearQuanterDequanter(Layer):
     """Frozen quant-dequant with a fixed scale (what ``convert`` leaves in the model)."""
 

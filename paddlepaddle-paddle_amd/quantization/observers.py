@@ -1,2 +1,2 @@
 """paddle.quantization.observers (reference: quantization/observers/__init__.py)."""
-from . import AbsmaxObserver, AbsmaxObserverLayer  # noqa: F401
+from . import AbsmaxObserver, AbsmaxObserverLayer, GroupWiseWeightObserver, GroupWiseWeightObserverLayer  # noqa: F401
