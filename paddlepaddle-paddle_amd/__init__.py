@@ -63,14 +63,14 @@ _LAZY = {
     'sparse': '.sparse', 'text': '.text', 'audio': '.audio', 'geometric': '.geometric',
     'quantization': '.quantization', 'inference': '.inference', 'callbacks': '.hapi.callbacks',
     'onnx': '.onnx', 'sysconfig': '.sysconfig', 'base': '.base', 'decomposition': '.decomposition',
-    'hub': '.hapi.hub', 'batch': '.io.batch', 'reader': '.io.reader', 'dataset': '.io.dataset_zoo',
+    'hub': '.hapi.hub', 'reader': '.reader', 'dataset': '.dataset',
     'cuda': '.device.cuda',
 }
 _LAZY_ATTR = {
     'Model': ('.hapi', 'Model'), 'summary': ('.hapi', 'summary'), 'flops': ('.hapi', 'flops'),
     'DataParallel': ('.distributed', 'DataParallel'), 'set_printoptions': ('.core.printing', 'set_printoptions'),
     'disable_signal_handler': ('.utils', 'disable_signal_handler'), 'get_cudnn_version': ('.device', 'get_cudnn_version'),
-    'check_shape': ('.utils', 'check_shape'), 'grad_fn': ('.autograd', 'grad'), 'iinfo': ('.core.dtype', 'iinfo'),
+    'check_shape': ('.utils', 'check_shape'), 'batch': ('.io.batch', 'batch'), 'grad_fn': ('.autograd', 'grad'), 'iinfo': ('.core.dtype', 'iinfo'),
 }
 
 

@@ -204,8 +204,23 @@ __device__ __forceinline__ void mask_row4(const Extra& ex, int b, int h, int q, 
 // they pay ONE hash per 4 elements (drop_bits + drop_sub); dK/dV (4 consecutive queries of one
 // key per lane) hashes one query per lane and shares the words across the key quad with DPP —
 // same bits, same mask (drop_z is the per-element reference form).
+// The hash input is linear in (query, key quad), so its per-block and per-lane parts hoist out of
+// the tile loops, and the finaliser multiplies with full-rate 24-bit multiplies (v_mul_u32_u24)
+// instead of quarter-rate v_mul_lo_u32: the dropout tiles were VALU-issue bound on the hash.
+// Statistics of the keep bytes (host simulation of this exact function, 1M elements per
+// seed): keep rate within 1e-3 of 230/256 at p = 0.1, adjacent key / row / key+4 correlations
+// |r| < 3e-3, byte histogram chi^2 ~ 255 (255 dof); GPU test test_flash_dropout_statistics.
+__device__ __forceinline__ uint32_t fin24(uint32_t x) {
+  x ^= x >> 16;
+  x = __umul24(x, 0x7FEB35u);
+  x ^= x >> 15;
+  x = __umul24(x, 0x846CA7u);
+  x ^= x >> 16;
+  return x;
+}
 __device__ __forceinline__ uint32_t drop_bits(const Extra& ex, int bh, int q, int k) {
-  return hash3(ex.seed ^ (uint32_t)bh * 0x9E3779B9u, ex.offset + (uint32_t)q, (uint32_t)k >> 2);
+  return fin24((ex.seed ^ (uint32_t)bh * 0x9E3779B9u) + (ex.offset + (uint32_t)q) * 0x85EBCA77u +
+               ((uint32_t)k >> 2) * 0xC2B2AE3Du);
 }
 __device__ __forceinline__ float drop_sub(const Extra& ex, uint32_t bits, int sub) {
   return ((bits >> (8 * sub)) & 0xFFu) < ex.drop_thresh ? 0.f : ex.keep_scale;
@@ -237,9 +252,42 @@ __device__ __forceinline__ Seq seq_of(const Extra& ex, int b, int h, int Hq, int
   return r;
 }
 
+// Block order (speed only; any bijection is correct).  The grid is (Hq, B, NZ): NZ query (or key)
+// blocks per (head, batch) pair, each re-reading the pair's K/V (or Q/dO) rows.  Blocks b and
+// b + 8 of the dispatch order share an XCD and its 4 MB L2.
+//  * G = 0: pair-major rows of the plain grid: all pairs' heaviest blocks first (longest-first over
+//    the whole launch); a pair's blocks run on one XCD but far apart in time, so its rows come from
+//    the Infinity Cache once per block.
+//  * G > 0: each XCD walks its own contiguous range of groups of G pairs, heaviest block first
+//    inside each group: a group's rows (G x 512 KB at S 1024, D 128) stay in that XCD's L2 while
+//    all its blocks run, and the light blocks of one group overlap the heavy ones of the next.
+__constant__ int g_pair_group = 0;
+
+__device__ __forceinline__ void pair_order(int Hq, int B, int NZ, int& h, int& b, int& zi) {
+  const int id = blockIdx.x + Hq * (blockIdx.y + B * blockIdx.z);
+  const int G = g_pair_group;
+  int pair;
+  if (G <= 0) {
+    pair = id % (Hq * B);
+    zi = id / (Hq * B);
+  } else {
+    const int nwg = Hq * B * NZ, P = Hq * B;
+    const int q = nwg >> 3, r = nwg & 7, x = id & 7;
+    const int w = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (id >> 3);
+    const int grp = w / (G * NZ);
+    const int gc = min(G, P - grp * G);  // pairs in this group (the last one may be short)
+    const int rr = w - grp * G * NZ;
+    zi = rr / gc;
+    pair = grp * G + rr % gc;
+  }
+  h = pair % Hq;
+  b = pair / Hq;
+}
+
 // ============================================================================ forward
 // grid: (ceil(Sq/128), Hq, B), block 256 (4 waves x 32 query rows = 2 tiles of 16)
-template <typename T, int D, bool CAUSAL, int EXT = 0>
+// PIPE: K/V tiles double-buffered in LDS, one barrier per key block.
+template <typename T, int D, bool CAUSAL, int EXT = 0, bool PIPE = false>
 __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                      const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
                                                      float* __restrict__ LSE, int Sq_, int Sk_, int Hq, int Hk,
@@ -247,9 +295,8 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
                                                      Extra ex = Extra{}) {
   constexpr int KS = D / 32;   // k-steps over head_dim
   constexpr int DB = D / 16;   // 16-wide d blocks
-  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * D * 2];
-  char* k_lds = smem;
-  char* v_lds = smem + 64 * D * 2;
+  constexpr int STAGE = 2 * 64 * D * 2;  // K and V of one key block
+  __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -258,8 +305,9 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
   // grid (Hq, B, q-blocks): the q-block index is the slowest-dispatched dimension, so every
   // head's heaviest (late, causal) block is issued before any lighter one (longest-first order
   // over the whole grid: the tail of the launch is the short blocks)
-  const int qb = nqb - 1 - (int)blockIdx.z;
-  const int h = blockIdx.x, b = blockIdx.y;
+  int h, b, zi;
+  pair_order(Hq, (int)gridDim.y, nqb, h, b, zi);
+  const int qb = nqb - 1 - zi;
   const int hk = h / (Hq / Hk);
   const Seq sq_ = seq_of<EXT != 0>(ex, b, h, Hq, Sq_, Sk_);
   const int Sq = sq_.sq, Sk = sq_.sk;
@@ -309,18 +357,32 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
     kt.load(0, Sk);
     vt.load(0, Sk);
   }
+  if (PIPE && nkb > 0) {
+    kt.template store<false>(smem);
+    vt.template store<true>(smem + 64 * D * 2);
+    if (nkb > 1) {
+      kt.load(64, Sk);
+      vt.load(64, Sk);
+    }
+    __syncthreads();
+  }
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * 64;
-    __syncthreads();
-    kt.template store<false>(k_lds);
-    vt.template store<true>(v_lds);
-    __syncthreads();
-    if (kb + 1 < nkb) {
-      kt.load(k0 + 64, Sk);
-      vt.load(k0 + 64, Sk);
+    char* st = smem + (PIPE ? (kb & 1) * STAGE : 0);
+    if (!PIPE) {
+      __syncthreads();
+      kt.template store<false>(st);
+      vt.template store<true>(st + 64 * D * 2);
+      __syncthreads();
+      if (kb + 1 < nkb) {
+        kt.load(k0 + 64, Sk);
+        vt.load(k0 + 64, Sk);
+      }
     }
+    const char* k_lds = st;
+    const char* v_lds = st + 64 * D * 2;
     // wave-uniform skip of key blocks fully above this wave's diagonal
-    if (CAUSAL && k0 > qw0 + 31 + off) continue;
+    if (!(CAUSAL && k0 > qw0 + 31 + off)) {
 
     // S^T = K Q^T : acc_s[t][kbk] holds S^T[key 16kbk + 4g + r][query 16t + (lane&15)]
     f32x4 acc_s[2][4];
@@ -446,6 +508,19 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
         acc_o[1][d] = Mfma<T>::run(vf, pf[1][s], acc_o[1][d]);
       }
     }
+    }  // not above the diagonal
+    if (PIPE) {
+      if (kb + 1 < nkb) {
+        char* nx = smem + ((kb + 1) & 1) * STAGE;  // last read in block kb - 1
+        kt.template store<false>(nx);
+        vt.template store<true>(nx + 64 * D * 2);
+        if (kb + 2 < nkb) {
+          kt.load(k0 + 128, Sk);
+          vt.load(k0 + 128, Sk);
+        }
+      }
+      __syncthreads();
+    }
   }
   // epilogue: O = acc / l ; lane holds O[query][16d + 4g + r]
 #pragma unroll
@@ -506,7 +581,10 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const uint16_t* __restri
 // NT = 2 halves the LDS bytes per MFMA (every Q / dO fragment read from LDS feeds two key tiles)
 // at one wave per SIMD (the accumulators of 32 keys x D need the full register file).
 // dK/dV are written per q-head ([B, Sk, Hq, D] strides given by dks/dvs); GQA sums outside.
-template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0>
+// PIPE: Q/dO tiles double-buffered in LDS — one barrier per query block instead of two (tile
+// i+1 is written into the other buffer right after block i's compute; its global loads were
+// issued one block earlier).
+template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0, bool PIPE = false>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
@@ -518,21 +596,19 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
   // ((row & 7) << 1) image, conflict free for both (the row-only swizzle leaves the tr reads
   // 2-way: SQ_LDS_BANK_CONFLICT was 20-27 % of LDS cycles in these kernels)
   constexpr bool BT = (D == 128);
-  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * D * 2 + 2 * 64 * 4];
-  char* q_lds = smem;
-  char* do_lds = smem + 64 * D * 2;
-  float* lse_lds = reinterpret_cast<float*>(smem + 2 * 64 * D * 2);
-  float* dl_lds = lse_lds + 64;
+  constexpr int STAGE = 2 * 64 * D * 2 + 2 * 64 * 4;  // Q, dO, LSE, delta of one query block
+  __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane >> 4;
-  // grid (Hq, B, key-blocks): early key blocks (the most causal queries) dispatched first
-  const int h = blockIdx.x, b = blockIdx.y;
+  // grid (Hq, B, key-blocks): early key blocks (the most causal queries) first within a pair
+  int h, b, zi;
+  pair_order(Hq, (int)gridDim.y, (int)gridDim.z, h, b, zi);
   const int hk = h / (Hq / Hk);
   const Seq sq_ = seq_of<EXT != 0>(ex, b, h, Hq, Sq_, Sk_);
   const int Sq = sq_.sq, Sk = sq_.sk;
-  const int k0 = blockIdx.z * 16 * NT * NW;
+  const int k0 = zi * 16 * NT * NW;
   if (EXT && k0 >= Sk) return;
   const int kw = k0 + wave * 16 * NT;
   const int off = Sk - Sq;
@@ -582,29 +658,52 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
   Tile<D, 64 * NW> qt, dot;
   qt.init(qbase, qs.s);
   dot.init(dobase, dos.s);
-  if (nqb > 0) {
-    qt.load(qstart, Sq);
-    dot.load(qstart, Sq);
+  // the block's LSE / delta rows are prefetched into registers with the Q / dO tile (a load at
+  // the store point would stall every wave of the block on one L2 round trip per query block)
+  float lse_n = 0.f, dl_n = 0.f;
+  auto load_rows = [&](int qq0) {
+    if (threadIdx.x < 64) {
+      const int q = qq0 + threadIdx.x;
+      lse_n = q < Sq ? lse_b[q] : -INFINITY;
+      dl_n = q < Sq ? dl_b[q] : 0.f;
+    }
+  };
+  auto stage_store = [&](char* st) {
+    qt.template store<BT>(st);
+    dot.template store<BT>(st + 64 * D * 2);
+    if (threadIdx.x < 64) {
+      float* l = reinterpret_cast<float*>(st + 2 * 64 * D * 2);
+      // a fully masked row (LSE = -inf) has P = 0: +inf makes every exp2 below vanish
+      l[threadIdx.x] = lse_n == -INFINITY ? INFINITY : lse_n * kLog2e;
+      l[64 + threadIdx.x] = dl_n;
+    }
+  };
+  auto stage_load = [&](int qq0) {
+    qt.load(qq0, Sq);
+    dot.load(qq0, Sq);
+    load_rows(qq0);
+  };
+  if (nqb > 0) stage_load(qstart);
+  if (PIPE && nqb > 0) {
+    stage_store(smem);
+    if (nqb > 1) stage_load(qstart + 64);
+    __syncthreads();
   }
   for (int i = 0; i < nqb; ++i) {
     const int q0 = qstart + i * 64;
-    __syncthreads();
-    qt.template store<BT>(q_lds);
-    dot.template store<BT>(do_lds);
-    if (threadIdx.x < 64) {
-      const int q = q0 + threadIdx.x;
-      // a fully masked row (LSE = -inf) has P = 0: +inf makes every exp2 below vanish
-      const float lv = q < Sq ? lse_b[q] : -INFINITY;
-      lse_lds[threadIdx.x] = lv == -INFINITY ? INFINITY : lv * kLog2e;
-      dl_lds[threadIdx.x] = q < Sq ? dl_b[q] : 0.f;
+    char* st = smem + (PIPE ? (i & 1) * STAGE : 0);
+    if (!PIPE) {
+      __syncthreads();
+      stage_store(st);
+      __syncthreads();
+      if (i + 1 < nqb) stage_load(q0 + 64);
     }
-    __syncthreads();
-    if (i + 1 < nqb) {
-      qt.load(q0 + 64, Sq);
-      dot.load(q0 + 64, Sq);
-    }
-    if (CAUSAL && q0 + 63 + off < kw) continue;  // whole query block above this wave's keys
-
+    const char* q_lds = st;
+    const char* do_lds = st + 64 * D * 2;
+    const float* lse_lds = reinterpret_cast<const float*>(st + 2 * 64 * D * 2);
+    const float* dl_lds = lse_lds + 64;
+    // whole query block above this wave's keys: nothing to compute (still joins the barriers)
+    if (!(CAUSAL && q0 + 63 + off < kw)) {
     // S = Q K^T, dP = dO V^T : acc[j][m] holds [query 16m + 4g + r][key 16j + lane&15]
     f32x4 acc_s[NT][4], acc_dp[NT][4];
 #pragma unroll
@@ -693,6 +792,15 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
         }
       }
     }
+    }  // not above the diagonal
+    if (PIPE) {
+      if (i + 1 < nqb) {
+        // the other buffer was last read in block i - 1, before the barrier that ended it
+        stage_store(smem + ((i + 1) & 1) * STAGE);
+        if (i + 2 < nqb) stage_load(q0 + 128);
+      }
+      __syncthreads();
+    }
   }
   // epilogue: lane holds d[16d + 4g + r][key 16j + lane&15]
 #pragma unroll
@@ -718,7 +826,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
 
 // dQ: grid (ceil(Sq / (16*NT*NW)), Hq, B); NW waves x (16*NT) queries; loop over 64-key blocks
 // (swapped products: lane owns a query).  NT = 2: every K / V fragment read feeds two query tiles.
-template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0>
+// PIPE: K/V tiles double-buffered in LDS, one barrier per key block (as bwd_dkdv_kernel).
+template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0, bool PIPE = false>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
@@ -730,15 +839,15 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
   // ((row & 7) << 1) image, conflict free for both (the row-only swizzle leaves the tr reads
   // 2-way: SQ_LDS_BANK_CONFLICT was 20-27 % of LDS cycles in these kernels)
   constexpr bool BT = (D == 128);
-  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * D * 2];
-  char* k_lds = smem;
-  char* v_lds = smem + 64 * D * 2;
+  constexpr int STAGE = 2 * 64 * D * 2;  // K and V of one key block
+  __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane >> 4;
   const int nqb = (Sq_ + 16 * NT * NW - 1) / (16 * NT * NW);
-  const int qb = nqb - 1 - (int)blockIdx.z;  // grid (Hq, B, q-blocks): heaviest first
-  const int h = blockIdx.x, b = blockIdx.y;
+  int h, b, zi;  // grid (Hq, B, q-blocks): heaviest first within a pair
+  pair_order(Hq, (int)gridDim.y, nqb, h, b, zi);
+  const int qb = nqb - 1 - zi;
   const int hk = h / (Hq / Hk);
   const Seq sq_ = seq_of<EXT != 0>(ex, b, h, Hq, Sq_, Sk_);
   const int Sq = sq_.sq, Sk = sq_.sk;
@@ -789,17 +898,31 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
     kt.load(0, Sk);
     vt.load(0, Sk);
   }
+  if (PIPE && nkb > 0) {
+    kt.template store<BT>(smem);
+    vt.template store<BT>(smem + 64 * D * 2);
+    if (nkb > 1) {
+      kt.load(64, Sk);
+      vt.load(64, Sk);
+    }
+    __syncthreads();
+  }
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * 64;
-    __syncthreads();
-    kt.template store<BT>(k_lds);
-    vt.template store<BT>(v_lds);
-    __syncthreads();
-    if (kb + 1 < nkb) {
-      kt.load(k0 + 64, Sk);
-      vt.load(k0 + 64, Sk);
+    char* st = smem + (PIPE ? (kb & 1) * STAGE : 0);
+    if (!PIPE) {
+      __syncthreads();
+      kt.template store<BT>(st);
+      vt.template store<BT>(st + 64 * D * 2);
+      __syncthreads();
+      if (kb + 1 < nkb) {
+        kt.load(k0 + 64, Sk);
+        vt.load(k0 + 64, Sk);
+      }
     }
-    if (CAUSAL && k0 > qw + 16 * NT - 1 + off) continue;
+    const char* k_lds = st;
+    const char* v_lds = st + 64 * D * 2;
+    if (!(CAUSAL && k0 > qw + 16 * NT - 1 + off)) {
     f32x4 acc_s[NT][4], acc_dp[NT][4];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -860,6 +983,19 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
         for (int t = 0; t < NT; ++t) acc[t][d] = Mfma<T>::run(ka, dsb[t][s], acc[t][d]);
       }
     }
+    }  // not above the diagonal
+    if (PIPE) {
+      if (kb + 1 < nkb) {
+        char* nx = smem + ((kb + 1) & 1) * STAGE;  // last read in block kb - 1
+        kt.template store<BT>(nx);
+        vt.template store<BT>(nx + 64 * D * 2);
+        if (kb + 2 < nkb) {
+          kt.load(k0 + 128, Sk);
+          vt.load(k0 + 128, Sk);
+        }
+      }
+      __syncthreads();
+    }
   }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -894,6 +1030,22 @@ using namespace pa::fa;
   else if (dt == 2 && D == 64 && !causal) { using T = f16_t; constexpr int DD = 64; constexpr bool CC = false; __VA_ARGS__; } \
   else return hipErrorInvalidValue;
 
+// forward K/V double buffering (fwd_kernel PIPE): -2 = not read yet (env PA_FA_FWD_PIPE), else 0/1
+static int g_fwd_pipe = -2;
+static bool fwd_pipe() {
+  if (g_fwd_pipe == -2) {
+    const char* e = getenv("PA_FA_FWD_PIPE");
+    g_fwd_pipe = e ? atoi(e) : 0;
+  }
+  return g_fwd_pipe > 0;
+}
+PA_API int pa_flash_set_fwd_pipe(int v) {
+  fwd_pipe();
+  const int old = g_fwd_pipe;
+  g_fwd_pipe = v;
+  return old;
+}
+
 // strides: [b, s, h] element strides for each tensor (head_dim stride must be 1)
 PA_API hipError_t pa_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int Sq, int Sk,
                                int Hq, int Hk, int D, const long long* qst, const long long* kst, const long long* vst,
@@ -901,10 +1053,17 @@ PA_API hipError_t pa_flash_fwd(const void* q, const void* k, const void* v, void
   if (Hk <= 0 || Hq % Hk != 0) return hipErrorInvalidValue;
   Strides qs{qst[0], qst[1], qst[2]}, ks{kst[0], kst[1], kst[2]}, vs{vst[0], vst[1], vst[2]}, os{ost[0], ost[1], ost[2]};
   dim3 grid(Hq, B, (Sq + 127) / 128);
-  FA_DISPATCH(dt, D, causal,
-              fwd_kernel<T, DD, CC><<<grid, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                                                          (uint16_t*)o, lse, Sq, Sk, Hq, Hk, qs, ks, vs, os,
-                                                          scale * kLog2e));
+  if (fwd_pipe()) {
+    FA_DISPATCH(dt, D, causal,
+                fwd_kernel<T, DD, CC, 0, true><<<grid, 256, 0, st>>>(
+                    (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, Sq, Sk, Hq, Hk, qs,
+                    ks, vs, os, scale * kLog2e));
+  } else {
+    FA_DISPATCH(dt, D, causal,
+                fwd_kernel<T, DD, CC><<<grid, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k,
+                                                            (const uint16_t*)v, (uint16_t*)o, lse, Sq, Sk, Hq, Hk, qs,
+                                                            ks, vs, os, scale * kLog2e));
+  }
   return hipGetLastError();
 }
 
@@ -925,6 +1084,14 @@ static int bwd_variant(int D) {
 }
 
 // v <= 0: automatic; returns the previous setting (-1 = automatic)
+// attention block order (g_pair_group above); returns the previous setting
+PA_API int pa_flash_set_pair_group(int v) {
+  int old = 0;
+  (void)hipMemcpyFromSymbol(&old, HIP_SYMBOL(pa::fa::g_pair_group), sizeof(int));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(pa::fa::g_pair_group), &v, sizeof(int));
+  return old;
+}
+
 PA_API int pa_flash_set_bwd_variant(int v) {
   bwd_variant(128);
   const int old = g_bwd_variant;
@@ -948,7 +1115,16 @@ PA_API hipError_t pa_flash_bwd(const void* q, const void* k, const void* v, cons
   FA_DISPATCH(dt, D, causal, {
     bwd_delta_kernel<T, DD><<<(int)((nrows + 15) / 16), 256, 0, st>>>((const uint16_t*)dout, (const uint16_t*)o, delta,
                                                                       B, Sq, Hq, dos, os);
-    if (bwd_variant(D) == 3) {
+    if (bwd_variant(D) == 4) {
+      dim3 g1(Hq, B, (Sk + 127) / 128);
+      bwd_dkdv_kernel<T, DD, CC, 1, 8, 0, true><<<g1, 512, 0, st>>>(
+          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+          (uint16_t*)dk, (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs, scale);
+      dim3 g2(Hq, B, (Sq + 127) / 128);
+      bwd_dq_kernel<T, DD, CC, 1, 8, 0, true><<<g2, 512, 0, st>>>(
+          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+          (uint16_t*)dq, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, scale);
+    } else if (bwd_variant(D) == 3) {
       dim3 g1(Hq, B, (Sk + 127) / 128);
       bwd_dkdv_kernel<T, DD, CC, 1, 8><<<g1, 512, 0, st>>>((const uint16_t*)q, (const uint16_t*)k,
                                                            (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
@@ -1025,9 +1201,14 @@ PA_API hipError_t pa_flash_fwd_ex(const void* q, const void* k, const void* v, v
   dim3 grid(Hq, B, (Sq + 127) / 128);
   const int feat = 1 | (mask ? 2 : 0) | (p_drop > 0.f ? 4 : 0) | (rows ? 8 : 0);
 #define FA_FWD_EX(F)                                                                                            \
-  fwd_kernel<T, DD, CC, F><<<grid, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,    \
-                                                 (uint16_t*)o, lse, Sq, Sk, Hq, Hk, qs, ks, vs, os, scale * kLog2e, \
-                                                 ex)
+  if (fwd_pipe())                                                                                               \
+    fwd_kernel<T, DD, CC, F, true><<<grid, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k,                \
+                                                         (const uint16_t*)v, (uint16_t*)o, lse, Sq, Sk, Hq, Hk, \
+                                                         qs, ks, vs, os, scale * kLog2e, ex);                   \
+  else                                                                                                          \
+    fwd_kernel<T, DD, CC, F><<<grid, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,  \
+                                                   (uint16_t*)o, lse, Sq, Sk, Hq, Hk, qs, ks, vs, os,           \
+                                                   scale * kLog2e, ex)
   FA_DISPATCH(dt, D, causal, {
     switch (feat) {
       case 1: FA_FWD_EX(1); break;
@@ -1049,6 +1230,17 @@ static void bwd_ex(const void* q, const void* k, const void* v, const void* dout
                    Strides vs, Strides dos, Strides dqs, Strides dks, Strides dvs, float scale, const Extra& ex,
                    hipStream_t st) {
   constexpr int NW = DD == 128 ? 8 : 4;
+  if (bwd_variant(DD) == 4) {  // double-buffered tiles
+    dim3 g1(Hq, B, (Sk + 16 * NW - 1) / (16 * NW));
+    bwd_dkdv_kernel<T, DD, CC, 1, NW, F, true><<<g1, 64 * NW, 0, st>>>(
+        (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk,
+        (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs, scale, ex);
+    dim3 g2(Hq, B, (Sq + 16 * NW - 1) / (16 * NW));
+    bwd_dq_kernel<T, DD, CC, 1, NW, F, true><<<g2, 64 * NW, 0, st>>>(
+        (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dq,
+        Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, scale, ex);
+    return;
+  }
   dim3 g1(Hq, B, (Sk + 16 * NW - 1) / (16 * NW));
   bwd_dkdv_kernel<T, DD, CC, 1, NW, F><<<g1, 64 * NW, 0, st>>>(
       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk,

@@ -58,9 +58,13 @@ def on_change(name, fn):
 
 
 def set_flags(flags):
+    if not isinstance(flags, dict):
+        raise TypeError("flags in set_flags should be a dict")
     for k, v in flags.items():
         if not k.startswith('FLAGS_'):
             k = 'FLAGS_' + k
+        if k not in _REGISTRY:
+            raise ValueError(f"Flag {k} cannot set its value through this function.")
         _REGISTRY[k] = v
         for fn in _hooks.get(k, []):
             fn(v)

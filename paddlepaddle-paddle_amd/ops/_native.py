@@ -60,6 +60,8 @@ _SIGS = {
     'pa_act_fwd_tune': [I, I],
     'pa_act_cs_tune': [I],
     'pa_flash_set_bwd_variant': [I],
+    'pa_flash_set_pair_group': [I],
+    'pa_flash_set_fwd_pipe': [I],
     'pa_gemm_fp8_ok': [I, I, I, LL, LL, LL],
     'pa_fp8_cast_transpose': [P, I, I, LL, P, P, P, I, I, P, I, F, P],
     'pa_fp8_amax': [P, I, I, LL, P, P],

@@ -50,67 +50,8 @@ class ViterbiDecoder(Layer):
         return viterbi_decode(potentials, self.transitions, lengths, self.include_bos_eos_tag)
 
 
-class _LocalTextDataset(Dataset):
-    """Line-oriented local dataset (the reference downloads; we only read ``data_file``)."""
-
-    def __init__(self, data_file=None, mode='train', **kw):
-        if data_file is None:
-            raise RuntimeError(f"{type(self).__name__}: no network access; pass data_file= pointing at a local copy")
-        with open(data_file, encoding='utf-8', errors='ignore') as f:
-            self.lines = [ln.rstrip('\n') for ln in f if ln.strip()]
-        self.mode = mode
-
-    def __getitem__(self, i):
-        return self.lines[i]
-
-    def __len__(self):
-        return len(self.lines)
-
-
-class UCIHousing(Dataset):
-    """Boston housing regression (13 features → price) from a local whitespace table."""
-
-    def __init__(self, data_file=None, mode='train', download=False):
-        import numpy as np
-        if data_file is None:
-            raise RuntimeError("UCIHousing: no network access; pass data_file=housing.data")
-        data = np.loadtxt(data_file).astype('float32')
-        mx, mn, avg = data.max(0), data.min(0), data.mean(0)
-        feats = (data[:, :-1] - avg[:-1]) / (mx[:-1] - mn[:-1])
-        n = int(len(data) * 0.8)
-        sl = slice(0, n) if mode == 'train' else slice(n, None)
-        self.x, self.y = feats[sl], data[sl, -1:]
-
-    def __getitem__(self, i):
-        return self.x[i], self.y[i]
-
-    def __len__(self):
-        return len(self.x)
-
-
-class Imdb(_LocalTextDataset):
-    pass
-
-
-class Imikolov(_LocalTextDataset):
-    pass
-
-
-class Movielens(_LocalTextDataset):
-    pass
-
-
-class Conll05st(_LocalTextDataset):
-    pass
-
-
-class WMT14(_LocalTextDataset):
-    pass
-
-
-class WMT16(_LocalTextDataset):
-    pass
-
+from . import datasets  # noqa: E402,F401
+from .datasets import Conll05st, Imdb, Imikolov, Movielens, UCIHousing, WMT14, WMT16  # noqa: E402,F401
 
 __all__ = ['Conll05st', 'Imdb', 'Imikolov', 'Movielens', 'UCIHousing', 'WMT14', 'WMT16', 'ViterbiDecoder',
            'viterbi_decode']

@@ -176,35 +176,120 @@ class ImageFolder(Dataset):
         return len(self.samples)
 
 
-class Flowers(DatasetFolder):
+def _backend(backend):
+    if backend is None:
+        from ..image import get_image_backend
+        backend = get_image_backend()
+    if backend not in ('pil', 'cv2'):
+        raise ValueError(f"Expected backend are one of ['pil', 'cv2'], but got {backend}")
+    return backend
+
+
+class Flowers(Dataset):
+    """Oxford 102 Flowers from the published files: ``102flowers.tgz`` (jpg/image_NNNNN.jpg; read
+    in place, not extracted), ``imagelabels.mat`` and ``setid.mat`` (scipy.io.loadmat: MATLAB
+    arrays, nothing executed).  As the reference, 'train' uses the large 'tstid' split and
+    'test' the small 'trnid' one."""
+
+    _FLAG = {'train': 'tstid', 'test': 'trnid', 'valid': 'valid'}
+
     def __init__(self, data_file=None, label_file=None, setid_file=None, mode='train', transform=None,
                  download=True, backend=None):
-        if data_file is None:
+        m = mode.lower()
+        assert m in self._FLAG, f"mode should be 'train', 'valid' or 'test', but got {mode}"
+        if not data_file or not label_file or not setid_file:
             _no_download('Flowers')
-        super().__init__(data_file, transform=transform)
+        self.backend, self.transform = _backend(backend), transform
+        import scipy.io as scio
+        self.labels = scio.loadmat(label_file)['labels'][0]
+        self.indexes = scio.loadmat(setid_file)[self._FLAG[m]][0]
+        self.data_file = data_file
+        self._tar = None
+
+    def _image_bytes(self, name):
+        if os.path.isdir(self.data_file):
+            with open(os.path.join(self.data_file, name), 'rb') as f:
+                return f.read()
+        if self._tar is None:
+            self._tar = tarfile.open(self.data_file)
+            self._members = {m.name.lstrip('./'): m for m in self._tar.getmembers()}
+        return self._tar.extractfile(self._members[name]).read()
+
+    def __getitem__(self, idx):
+        import io as _io
+        from PIL import Image
+        index = int(self.indexes[idx])
+        label = np.array([self.labels[index - 1]]).astype('int64')
+        image = Image.open(_io.BytesIO(self._image_bytes("jpg/image_%05d.jpg" % index)))
+        if self.backend == 'cv2':
+            image = np.array(image)
+        if self.transform is not None:
+            image = self.transform(image)
+        if self.backend == 'cv2':
+            image = np.asarray(image).astype('float32')
+        return image, label
+
+    def __len__(self):
+        return len(self.indexes)
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d['_tar'] = None  # reopened lazily in each worker
+        return d
 
 
 class VOC2012(Dataset):
+    """PASCAL VOC2012 segmentation from ``VOCtrainval_11-May-2012.tar`` (or its extracted root):
+    (image, class-index mask).  Split map as the reference: train -> trainval, test -> train,
+    valid -> val."""
+
+    _FLAG = {'train': 'trainval', 'test': 'train', 'valid': 'val'}
+    _SET, _IMG, _LAB = ('VOCdevkit/VOC2012/ImageSets/Segmentation/{}.txt', 'VOCdevkit/VOC2012/JPEGImages/{}.jpg',
+                        'VOCdevkit/VOC2012/SegmentationClass/{}.png')
+
     def __init__(self, data_file=None, mode='train', transform=None, download=True, backend=None):
+        m = mode.lower()
+        assert m in self._FLAG, f"mode should be 'train', 'valid' or 'test', but got {mode}"
         if data_file is None:
             _no_download('VOC2012')
-        root = data_file
-        split = {'train': 'train', 'valid': 'val', 'test': 'val'}[mode]
-        with open(os.path.join(root, 'ImageSets', 'Segmentation', split + '.txt')) as f:
-            self.ids = [ln.strip() for ln in f if ln.strip()]
-        self.root, self.transform = root, transform
+        self.backend, self.transform, self.data_file = _backend(backend), transform, data_file
+        self._tar = None
+        ids = self._read(self._SET.format(self._FLAG[m])).decode('utf-8').split()
+        self.data = [self._IMG.format(i) for i in ids]
+        self.labels = [self._LAB.format(i) for i in ids]
+
+    def _read(self, name):
+        if os.path.isdir(self.data_file):
+            root = self.data_file
+            if not os.path.exists(os.path.join(root, name)) and name.startswith('VOCdevkit/VOC2012/'):
+                name = name[len('VOCdevkit/VOC2012/'):]  # the extracted VOC2012 directory itself
+            with open(os.path.join(root, name), 'rb') as f:
+                return f.read()
+        if self._tar is None:
+            self._tar = tarfile.open(self.data_file)
+            self._members = {mm.name: mm for mm in self._tar.getmembers()}
+        return self._tar.extractfile(self._members[name]).read()
 
     def __getitem__(self, idx):
+        import io as _io
         from PIL import Image
-        i = self.ids[idx]
-        img = Image.open(os.path.join(self.root, 'JPEGImages', i + '.jpg')).convert('RGB')
-        lab = np.array(Image.open(os.path.join(self.root, 'SegmentationClass', i + '.png')))
+        img = Image.open(_io.BytesIO(self._read(self.data[idx])))
+        lab = Image.open(_io.BytesIO(self._read(self.labels[idx])))
+        if self.backend == 'cv2':
+            img, lab = np.array(img), np.array(lab)
         if self.transform is not None:
             img = self.transform(img)
-        return img, lab
+        if self.backend == 'cv2':
+            return np.asarray(img).astype('float32'), np.asarray(lab)
+        return img, np.array(lab)
 
     def __len__(self):
-        return len(self.ids)
+        return len(self.data)
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d['_tar'] = None
+        return d
 
 
 __all__ = ['DatasetFolder', 'ImageFolder', 'MNIST', 'FashionMNIST', 'Flowers', 'Cifar10', 'Cifar100', 'VOC2012']

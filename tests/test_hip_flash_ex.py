@@ -130,6 +130,25 @@ def test_flash_dropout(causal, D):
     _grads_vs_ref(o2, r, (qq, kk, vv), ri, 6e-2, 'dropout')
 
 
+@pytest.mark.parametrize("p", [0.1, 0.5])
+def test_flash_dropout_statistics(p):
+    """Keep mask recovered from the kernel (one-hot V): keep rate, and no correlation between
+    neighbouring keys, key quads or queries (the hash must not leak structure into the mask)."""
+    B, S, H, D = 1, 128, 8, 128
+    _, _, _, _, z = _dropout_mask(B, S, H, D, False, p, seed=7)
+    keep = (z > 0).float().reshape(-1, S, S)  # [H, Sq, Sk]
+    n = keep.numel()
+    assert abs(keep.mean().item() - (1 - p)) < 4 * (p * (1 - p) / n) ** 0.5 + 2 / 256, keep.mean().item()
+
+    def corr(a, b):
+        a, b = a.reshape(-1) - a.mean(), b.reshape(-1) - b.mean()
+        return (a @ b / (a.norm() * b.norm())).item()
+    tol = 5 / (n ** 0.5)
+    for name, (a, b) in {'key': (keep[..., :-1], keep[..., 1:]), 'key+4': (keep[..., :-4], keep[..., 4:]),
+                         'query': (keep[:, :-1], keep[:, 1:]), 'head': (keep[:-1], keep[1:])}.items():
+        assert abs(corr(a, b)) < tol, (name, corr(a, b))
+
+
 def test_flash_dropout_packed_matches_unpacked():
     B, S, H, D, p = 2, 256, 4, 128, 0.1
     qkv = _leaf(B, S, 3, H, D)
