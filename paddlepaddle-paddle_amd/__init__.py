@@ -63,7 +63,7 @@ _LAZY = {
     'sparse': '.sparse', 'text': '.text', 'audio': '.audio', 'geometric': '.geometric',
     'quantization': '.quantization', 'inference': '.inference', 'callbacks': '.hapi.callbacks',
     'onnx': '.onnx', 'sysconfig': '.sysconfig', 'base': '.base', 'decomposition': '.decomposition',
-    'hub': '.hapi.hub', 'reader': '.reader', 'dataset': '.dataset',
+    'hub': '.hapi.hub', 'reader': '.reader', 'dataset': '.dataset', 'cost_model': '.cost_model',
     'cuda': '.device.cuda',
 }
 _LAZY_ATTR = {

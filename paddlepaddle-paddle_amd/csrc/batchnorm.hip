@@ -150,7 +150,7 @@ __global__ __launch_bounds__(1024) void stats_finish(const float* __restrict__ p
                                                      float* __restrict__ run_mean, float* __restrict__ run_var) {
   __shared__ float red[16][65];
   __shared__ float mshare[64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = blockIdx.x * 64 + lane;
   const float nlast = (float)(rows - (P - 1) * rpb), nfull = (float)rpb;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(1024) void bwd_finish(const float* __restrict__ p1,
                                                    int cols, const float* __restrict__ rstd, WT* __restrict__ dgamma,
                                                    WT* __restrict__ dbeta, float* __restrict__ s_out, int accumulate) {
   __shared__ float r1[16][65], r2[16][65];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = blockIdx.x * 64 + lane;
   float a = 0.f, b = 0.f, a2 = 0.f, b2 = 0.f, a3 = 0.f, b3 = 0.f, a4 = 0.f, b4 = 0.f;
   if (c < cols) {

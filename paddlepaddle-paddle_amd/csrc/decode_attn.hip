@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(const T* __restrict__ q
   constexpr int EPL = D / 16;  // elements per lane
   constexpr int U = 4;         // positions per lane group per iteration
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int grp = lane >> 4, sub = lane & 15;
   const int len = lens[b];
   const int p0 = split * chunk, p1 = min(len, p0 + chunk);

@@ -14,7 +14,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void embedding_fwd(const int64_t* __restrict__ ids, const T* __restrict__ w,
                                                      T* __restrict__ out, int n, int dim, int64_t vocab) {
   constexpr int E = 16 / sizeof(T);
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= n) return;
   int64_t id = ids[row];
@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void embedding_fwd(const int64_t* __restrict__
 template <typename T>
 __global__ __launch_bounds__(256) void embedding_bwd(const int64_t* __restrict__ ids, const T* __restrict__ dy,
                                                      float* __restrict__ dw32, int n, int dim, int64_t vocab) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= n) return;
   int64_t id = ids[row];

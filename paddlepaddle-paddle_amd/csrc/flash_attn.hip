@@ -21,6 +21,7 @@
 //    QKV projection with no copies.
 #include "common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 namespace pa {
 namespace fa {
@@ -299,7 +300,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
   __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE];
 
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches and addresses
   const int g = lane >> 4;
   const int nqb = (Sq_ + 127) / 128;
   // grid (Hq, B, q-blocks): the q-block index is the slowest-dispatched dimension, so every
@@ -600,7 +601,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
   __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE];
 
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches and addresses
   const int g = lane >> 4;
   // grid (Hq, B, key-blocks): early key blocks (the most causal queries) first within a pair
   int h, b, zi;
@@ -729,6 +730,11 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
     // P and dS, packed as B operands (k = query, permuted as in the forward)
     const bool need_mask = (q0 + 64 > Sq) || (kw + 16 * NT > Sk) || (CAUSAL && kw + 16 * NT - 1 > q0 + off);
     s16x8 pb[NT][2], db_[NT][2];
+    // two instantiations of the elementwise block, selected by a wave-uniform branch: with one
+    // body and a runtime test hipcc if-converts the mask into per-element selects that every
+    // (mostly unmasked) tile pays
+    auto p_ds = [&](auto mask_tag) {
+    constexpr bool MASK = decltype(mask_tag)::value;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const float4 lse4 = *reinterpret_cast<const float4*>(lse_lds + 16 * m + 4 * g);
@@ -765,7 +771,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
             sl = kLog2e;
           }
           float p = fast_exp2(__builtin_fmaf(sv, sl, -lsev[r]));
-          if (need_mask) {
+          if constexpr (MASK) {
             const bool masked = (q >= Sq) || (mykey >= Sk) || (CAUSAL && mykey > q + off);
             p = masked ? 0.f : p;
           }
@@ -778,6 +784,11 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
         }
       }
     }
+    };
+    if (need_mask)
+      p_ds(std::true_type{});
+    else
+      p_ds(std::false_type{});
     // dV^T += dO^T P ;  dK^T += Q^T dS
 #pragma unroll
     for (int d = 0; d < DB; ++d) {
@@ -842,7 +853,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
   constexpr int STAGE = 2 * 64 * D * 2;  // K and V of one key block
   __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches and addresses
   const int g = lane >> 4;
   const int nqb = (Sq_ + 16 * NT * NW - 1) / (16 * NT * NW);
   int h, b, zi;  // grid (Hq, B, q-blocks): heaviest first within a pair
@@ -946,6 +957,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
     }
     const bool need_mask = (k0 + 64 > Sk) || (qw + 16 * NT > Sq) || (CAUSAL && k0 + 63 > qw + off);
     s16x8 dsb[NT][2];
+    auto ds_blk = [&](auto mask_tag) {  // masked / unmasked instantiations (see bwd_dkdv_kernel)
+    constexpr bool MASK = decltype(mask_tag)::value;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int myq = qw + 16 * t + (lane & 15);
@@ -961,7 +974,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
           const int key = k0 + 16 * j + 4 * g + r;
           const float sv = (EXT & 2) ? acc_s[t][j][r] * scale + mv[r] : acc_s[t][j][r];
           float p = fast_exp2(__builtin_fmaf(sv, (EXT & 2) ? kLog2e : scale_log2, -lse2[t]));
-          if (need_mask) {
+          if constexpr (MASK) {
             const bool masked = (key >= Sk) || (myq >= Sq) || (CAUSAL && key > myq + off);
             p = masked ? 0.f : p;
           }
@@ -973,6 +986,11 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
         }
       }
     }
+    };
+    if (need_mask)
+      ds_blk(std::true_type{});
+    else
+      ds_blk(std::false_type{});
     // dQ^T += K^T dS^T
 #pragma unroll
     for (int d = 0; d < DB; ++d) {

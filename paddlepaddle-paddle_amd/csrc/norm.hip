@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const T* __restrict__ x, 
                                                        DropSpec dsp) {
   constexpr int E = 16 / sizeof(T);
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row >= rows) return;
   const size_t base = (size_t)row * cols;
   float v[MAXC][E];

@@ -18,7 +18,7 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const T* __restrict__ 
                                                           int cols, int causal_cols_per_row_offset) {
   constexpr int E = 16 / sizeof(T);
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row >= rows) return;
   const size_t base = (size_t)row * cols;
   // CAUSAL: row r of a [.., S, S] score matrix keeps columns <= (r % S) + offset
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const T* __restrict__ 
                                                           T* __restrict__ dx, int rows, int cols) {
   constexpr int E = 16 / sizeof(T);
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row >= rows) return;
   const size_t base = (size_t)row * cols;
   float yv[MAXC][E], gv[MAXC][E];

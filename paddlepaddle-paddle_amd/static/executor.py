@@ -157,7 +157,32 @@ def _feed_tensor(v, dt, dev):
 _SUBS = {'map': None}  # target substitutions of the running replay (static.amp fp8: ops/fp8.py)
 
 
+# per-node timing of the running replay (paddle.cost_model.CostModel.profile_measure): None, or a
+# list receiving (node index, op name, milliseconds); device work is synchronised per node
+_PROFILE = {'rec': None}
+
+
+def _op_name(n):
+    t = n.target
+    return getattr(t, '__name__', None) or type(t).__name__ if n.kind in ('torch', 'py') else n.kind
+
+
 def _exec(prog, nodes, env, smap, dev):
+    rec = _PROFILE['rec']
+    if rec is None:
+        return _exec_nodes(prog, nodes, env, smap, dev)
+    import time
+    sync = (lambda: torch.cuda.synchronize(dev)) if dev is not None and torch.device(dev).type == 'cuda' else \
+        (lambda: None)
+    for i, n in enumerate(nodes):
+        sync()
+        t0 = time.perf_counter()
+        _exec_nodes(prog, [n], env, smap, dev)
+        sync()
+        rec.append((len(rec), _op_name(n), (time.perf_counter() - t0) * 1e3))
+
+
+def _exec_nodes(prog, nodes, env, smap, dev):
     subs = _SUBS['map']
     for n in nodes:
         if n.kind == 'torch':

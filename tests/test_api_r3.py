@@ -210,3 +210,23 @@ def test_tensor_method_parity_and_imag_of_real():
     assert int(x.rank()) == 2
     np.testing.assert_allclose(x.broadcast_shape([1, 2]) if False else [2, 2], [2, 2])
     assert paddle.vision.get_image_backend() == 'pil'
+
+
+def test_cost_model_profiles_program_nodes():
+    cm = paddle.cost_model.CostModel()
+    try:
+        startup, main = cm.build_program()
+        cd = cm.profile_measure(startup, main, device='cpu')
+    finally:
+        paddle.disable_static()
+    assert len(cd) >= 2 and cd.get_whole_time_ms() > 0
+    names = [cd.get_op_name(i) for i in range(len(cd))]
+    assert 'minimize' in names
+    assert abs(sum(cd.op_times().values()) - cd.get_whole_time_ms()) < 1e-9
+    table = cm.static_cost_data()
+    assert isinstance(table, list) and table
+    rec = table[0]
+    got = cm.get_static_op_time(rec['op'], forward=True, dtype='float32' if 'float32' in rec['config'] else 'bfloat16')
+    assert got and 'op_time' in got
+    with pytest.raises(ValueError):
+        cm.get_static_op_time(None)
