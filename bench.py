@@ -34,6 +34,10 @@ def parse():
                     help='attention-probability dropout (in-kernel in csrc/flash_attn.hip)')
     ap.add_argument('--resnet-batch', type=int, default=256)
     ap.add_argument('--no-resnet', action='store_true')
+    ap.add_argument('--cpu', action='store_true',
+                    help='rehearsal only (tests): run the same bench path on the CPU with gloo, e.g. with '
+                         '--model gpt-tiny --resnet-model resnet18; the numbers mean nothing')
+    ap.add_argument('--resnet-model', default='resnet50', help=argparse.SUPPRESS)
     ap.add_argument('--graph', action='store_true',
                     help='replay the whole training step as one captured hipGraph (steps without dropout; '
                          'device/cuda/graphs.py TrainStepGraph)')
@@ -87,14 +91,17 @@ def build_resnet(args, world, rank, dev):
     from paddle.vision.models import resnet50
     paddle.seed(1234)
     B = args.resnet_batch
-    model = resnet50(data_format='NHWC')
+    from paddle.vision import models as _vm
+    model = resnet50(data_format='NHWC') if args.resnet_model == 'resnet50' else \
+        getattr(_vm, args.resnet_model)(data_format='NHWC')
     opt = paddle.optimizer.Momentum(learning_rate=0.1, momentum=0.9, parameters=model.parameters(),
                                     weight_decay=1e-4, multi_precision=True)
     model, opt = paddle.amp.decorate(model, opt, level='O2', dtype='bfloat16')
     if world > 1:
         model = pdist.DataParallel(model)
     g = torch.Generator(device=dev).manual_seed(rank)
-    img = paddle.to_tensor(torch.randn(B, 224, 224, 3, device=dev, dtype=torch.bfloat16, generator=g))
+    res = 224 if args.resnet_model == 'resnet50' else 32
+    img = paddle.to_tensor(torch.randn(B, res, res, 3, device=dev, dtype=torch.bfloat16, generator=g))
     lab = paddle.to_tensor(torch.randint(0, 1000, (B,), device=dev, generator=g))
 
     def step():
@@ -105,7 +112,7 @@ def build_resnet(args, world, rank, dev):
         opt.clear_grad()
         return loss
 
-    mcfg = {'model': 'resnet50', 'global_batch': B * world, 'image': '224x224 NHWC', 'parallelism': f"dp{world}",
+    mcfg = {'model': args.resnet_model, 'global_batch': B * world, 'image': f'{res}x{res} NHWC', 'parallelism': f"dp{world}",
             'optimizer': 'Momentum'}
     return step, B * world, 'samples/sec ResNet50 bf16', 'samples/s', mcfg
 
@@ -125,6 +132,8 @@ def measure(step, steps, warmup, world, rank, dev, tag):
     """W untimed warmup steps, then K timed steps bracketed by barrier + device sync; MAX over ranks."""
     import torch
     import torch.distributed as dist
+    if dev.type != 'cuda':  # --cpu rehearsal
+        torch.cuda.synchronize = lambda *a, **k: None
     loss = None
     for i in range(warmup):
         loss = step()
@@ -152,11 +161,12 @@ def measure(step, steps, warmup, world, rank, dev, tag):
 
 def main():
     args = parse()
-    import gc
     import torch
     import torch.distributed as dist
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
+    if args.cpu:
+        return _main_cpu(args, world, rank)
     # one rank per GPU; the modulo only matters when rehearsing several ranks on fewer GPUs
     local_rank = int(os.environ.get('LOCAL_RANK', '0')) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
@@ -168,6 +178,25 @@ def main():
     import paddle
     paddle.seed(1234 + rank)
     dev = torch.device('cuda', local_rank)
+    _run(args, world, rank, dev)
+
+
+def _main_cpu(args, world, rank):
+    """--cpu: the identical bench flow on the CPU over gloo (multi-rank rehearsal in tests)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group('gloo')
+    import paddle
+    paddle.set_device('cpu')
+    paddle.seed(1234 + rank)
+    _run(args, world, rank, torch.device('cpu'))
+
+
+def _run(args, world, rank, dev):
+    import gc
+    import torch
+    import torch.distributed as dist
 
     build = build_gpt if args.model.startswith('gpt') else build_resnet
     step, work, metric, unit, mcfg = build(args, world, rank, dev)

@@ -20,6 +20,57 @@ from ..parallel.flat_buffer import flat_grad_slot, notify_grad_ready
 from . import fused, gemm
 
 
+import os
+
+# Weight-gradient / data-gradient overlap: the wgrad GEMM of a Linear is launched on a side HIP
+# stream right before its dgrad GEMM on the compute stream, so the two (independent) GEMMs share
+# the chip; the compute stream joins the side stream before the gradient is announced ready.
+# Pays where a GEMM leaves CUs idle (the QKV weight gradient: 192 256x256 tiles on 256 CUs).
+WGRAD_OVERLAP = os.environ.get('PADDLE_AMD_WGRAD_OVERLAP', '0') == '1'
+OVERLAP_MIN_TILES = 128
+_side_streams = {}
+
+
+def _side_stream(dev):
+    s = _side_streams.get(dev)
+    if s is None:
+        s = _side_streams[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def _wgrad_async(x2, dy2, wp):
+    """Launch W.grad += x2^T dy2 on the side stream; returns a join token, or None when the
+    gradient does not live in a flat slot / overlap is off (caller uses _grad_w)."""
+    if not WGRAD_OVERLAP or not x2.is_cuda:
+        return None
+    gw = flat_grad_slot(wp)
+    if gw is None or not gemm.hip_mm_ok(x2.t(), dy2, 1) or gw.dtype != torch.bfloat16 or not gw.is_contiguous():
+        return None
+    # only a wgrad that leaves CUs idle in its single round of 256x256 tiles (the QKV weight
+    # gradient, 192 tiles): two full-chip GEMMs side by side measured slower (cache / XCD-order
+    # interference, profiles/r3_wgrad_overlap_ab.log)
+    tiles = -(-gw.shape[0] // 256) * -(-gw.shape[1] // 256)
+    if not (OVERLAP_MIN_TILES <= tiles < 256):
+        return None
+    main = torch.cuda.current_stream(x2.device)
+    side = _side_stream(x2.device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        gemm.wgrad_accumulate(x2, dy2, gw)
+    x2.record_stream(side)
+    dy2.record_stream(side)
+    done = torch.cuda.Event()
+    done.record(side)
+    return done, wp
+
+
+def _wgrad_join(tok):
+    done, wp = tok
+    torch.cuda.current_stream().wait_event(done)
+    notify_grad_ready(wp)
+    return None
+
+
 class _LinearAccum(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, box):
@@ -38,8 +89,9 @@ class _LinearAccum(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         wp, bp = ctx.box
         dy2 = dy.reshape(-1, dy.shape[-1])
+        tok = _wgrad_async(x2, dy2, wp)
         dx = gemm.mm(dy2, w.t()).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
-        dw = _grad_w(x2, dy2, wp)
+        dw = _wgrad_join(tok) if tok is not None else _grad_w(x2, dy2, wp)
         db = _grad_b(dy2, bp) if bp is not None else None
         return dx, dw, db, None
 
@@ -103,7 +155,8 @@ class _MLPGelu(torch.autograd.Function):
         x2, w1, w2, h, g = ctx.saved_tensors
         w1p, b1p, w2p, b2p = ctx.boxes
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dw2 = _grad_w(g, dy2, w2p)
+        tok2 = _wgrad_async(g, dy2, w2p)  # fc2 wgrad beside the fc2 dgrad
+        dw2 = None if tok2 is not None else _grad_w(g, dy2, w2p)
         db2 = _grad_b(dy2, b2p) if b2p is not None else None
         gb1 = flat_grad_slot(b1p) if FUSE_DBIAS else None
         if gb1 is not None and gb1.is_contiguous():
@@ -117,8 +170,13 @@ class _MLPGelu(torch.autograd.Function):
         else:
             dh = gemm.mm_epi(dy2, w2.t(), 3, h)
             db1 = _grad_b(dh, b1p)
-        dw1 = _grad_w(x2, dh, w1p)
+        if tok2 is not None:
+            _wgrad_join(tok2)
+        tok1 = _wgrad_async(x2, dh, w1p)  # fc1 wgrad beside the fc1 dgrad
+        dw1 = None if tok1 is not None else _grad_w(x2, dh, w1p)
         dx = gemm.mm(dh, w1.t()).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
+        if tok1 is not None:
+            _wgrad_join(tok1)
         return dx, dw1, db1, dw2, db2, None
 
 

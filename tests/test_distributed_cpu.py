@@ -270,3 +270,23 @@ def test_pipeline_shared_weight_with_sharding(clip, shard):
 def test_fused_multi_transformer_ring_id_tensor_parallel():
     out = run_workers('worker_fmt_tp.py', nproc=2, timeout=300)
     assert out.count("fmt tp OK") == 2, out[-3000:]
+
+
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_bench_multi_rank_path_rehearsal(nproc):
+    """bench.py's N-rank flow (one process per device, sharding-3 GPT + data-parallel ResNet,
+    barrier-bracketed timing, MAX over ranks, one JSON line from rank 0) on gloo with tiny models."""
+    import json
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES='', HIP_VISIBLE_DEVICES='', PYTHONPATH=ROOT, OMP_NUM_THREADS='1')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={nproc}',
+           '--master-addr=127.0.0.1', f'--master-port={_port()}', os.path.join(ROOT, 'bench.py'), '--cpu',
+           '--model', 'gpt-tiny', '--steps', '2', '--warmup', '1', '--resnet-model', 'resnet18', '--resnet-batch', '2',
+           '--micro-batch', '2', '--seq', '64', '--gpus', str(nproc)]
+    r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == nproc and d['config']['parallelism'] == f'sharding-3x{nproc}'
+    assert d['config']['global_batch'] == 2 * nproc and d['resnet50']['config']['parallelism'] == f'dp{nproc}'
+    assert d['value'] > 0 and abs(d['value'] - 2 * 64 * nproc / (d['ms_per_step'] / 1e3)) < 1e-2 * d['value']

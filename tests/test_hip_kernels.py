@@ -1260,3 +1260,36 @@ def test_resnet_downsample_block_shared_dgrad():
     _close(b[0], a[0], 0.05 * float(a[0].abs().max()) + 1e-3, 0.02, 'dx')
     _close(b[1], b[0], 1e-6, 0.0, 'dx second backward')
     _close(b[2], a[2], 0.05 * float(a[2].abs().max()) + 1e-3, 0.02, 'dw1 (twice accumulated)')
+
+
+def test_wgrad_side_stream_overlap_is_exact():
+    """GPT-tiny trained with every Linear weight gradient on the side stream (ops.linear
+    WGRAD_OVERLAP: wgrad beside dgrad, joined before the gradient is announced) gives bitwise
+    the same parameters as the serial order: same kernels, same inputs, only the stream differs."""
+    import paddle
+    from paddle.ops import linear
+    from paddle.models.gpt import gpt_config, GPTForPretraining
+    paddle.set_device('gpu:0')
+    finals = []
+    old = linear.WGRAD_OVERLAP
+    for on in (False, True):
+        linear.WGRAD_OVERLAP = on
+        try:
+            paddle.seed(21)
+            cfg = gpt_config('gpt-tiny', hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+            model = GPTForPretraining(cfg)
+            opt = paddle.optimizer.AdamW(learning_rate=1e-3, parameters=model.parameters(), multi_precision=True)
+            model, opt = paddle.amp.decorate(model, opt, level='O2', dtype='bfloat16')
+            paddle.seed(22)
+            ids = paddle.randint(0, cfg.vocab_size, [8, 257])
+            for _ in range(3):
+                loss = model.loss(model(ids[:, :-1]), ids[:, 1:])
+                loss.backward()
+                opt.step()
+                opt.clear_grad()
+            torch.cuda.synchronize()
+            finals.append({n: p._t.detach().float().clone() for n, p in model.named_parameters()})
+        finally:
+            linear.WGRAD_OVERLAP = old
+    for n in finals[0]:
+        assert torch.equal(finals[0][n], finals[1][n]), n
