@@ -529,19 +529,39 @@ __device__ __forceinline__ void wait_vm_n(int n) {  // n in {0, 4, 8, 12}, wave-
   else wait_vm<0>();
 }
 
-template <bool AK, bool BKM, int EPI>
+// Second problem of a grouped launch (GRP): blocks [tiles of problem 0, +tiles of problem 1) take
+// it.  Same K, layout, alpha / beta and epilogue as problem 0.  Used to run two weight gradients
+// whose tile counts add up to one full round of the chip (the GPT QKV and out-projection weight
+// gradients: 192 + 64 = 256 tiles) as one launch instead of a partly idle round plus a split-K.
+struct Prob {
+  const char* A;
+  const char* B;
+  uint16_t* C;
+  int M, N;
+  long long lda, ldb, ldc;
+};
+
+template <bool AK, bool BKM, int EPI, bool GRP = false>
 __global__ __launch_bounds__(512, 1) void gemm9_kernel(const char* __restrict__ A, const char* __restrict__ B,
                                                        uint16_t* __restrict__ C, float* __restrict__ ws,
                                                        const uint16_t* __restrict__ bias, int M, int N, int K,
                                                        long long lda, long long ldb, long long ldc, float alpha,
-                                                       float beta, int ksplit) {
+                                                       float beta, int ksplit, Prob p1 = Prob{}) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3, wq = wave & 3;
+  int bid = blockIdx.x;
+  if constexpr (GRP) {
+    const int t0 = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    if (bid >= t0) {  // block-uniform: this block computes a tile of problem 1
+      A = p1.A, B = p1.B, C = p1.C, M = p1.M, N = p1.N, lda = p1.lda, ldb = p1.ldb, ldc = p1.ldc;
+      bid -= t0;
+    }
+  }
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   int mt, ntile;
-  tile_coords(blockIdx.x, tm * tn, tm, tn, mt, ntile);
+  tile_coords(bid, tm * tn, tm, tn, mt, ntile);
   const int m0 = mt * BM, n0 = ntile * BN;
   const int kbeg = blockIdx.z * ksplit;
   const int nt = ksplit / BK;
@@ -1105,6 +1125,24 @@ PA_API int pa_gemm8_bf16_epi(const void* A, const void* B, void* C, const void* 
   // epi 4: epi 3 + column partial sums of C, one fp32 row per 128-row slab, into bias ([ceil(M/128)][N])
   if (epi == 4 && bias != nullptr) return (int)launch_epi<4>(transB, A, B, C, aux, bias, M, N, K, lda, ldb, ldc, alpha, st);
   return (int)hipErrorInvalidValue;
+}
+
+// Two weight gradients in one launch (schedule 9, both operands m/n-contiguous as the Linear
+// weight gradient reads them: A = X^T [K][M], B = dY [K][N]), C_i = alpha * A_i @ B_i + beta * C_i,
+// shared K.  Returns hipErrorInvalidValue outside the kernel contract.
+PA_API int pa_gemm8_wgrad_grouped2(const void* A0, const void* B0, void* C0, int M0, int N0, long long lda0,
+                                   long long ldb0, long long ldc0, const void* A1, const void* B1, void* C1, int M1,
+                                   int N1, long long lda1, long long ldb1, long long ldc1, int K, float alpha,
+                                   float beta, hipStream_t st) {
+  using namespace pa::g8;
+  if (!pa_gemm8_ok(M0, N0, K, lda0, ldb0, ldc0, 1, 0, 1) || !pa_gemm8_ok(M1, N1, K, lda1, ldb1, ldc1, 1, 0, 1))
+    return (int)hipErrorInvalidValue;
+  const int t0 = ((M0 + BM - 1) / BM) * ((N0 + BN - 1) / BN), t1 = ((M1 + BM - 1) / BM) * ((N1 + BN - 1) / BN);
+  Prob p1{(const char*)A1, (const char*)B1, (uint16_t*)C1, M1, N1, lda1, ldb1, ldc1};
+  gemm9_kernel<false, false, 0, true><<<t0 + t1, 512, 0, st>>>((const char*)A0, (const char*)B0, (uint16_t*)C0,
+                                                               nullptr, nullptr, M0, N0, K, lda0, ldb0, ldc0, alpha,
+                                                               beta, K, p1);
+  return (int)hipGetLastError();
 }
 
 PA_API int pa_gemm8_set_wide_epi(int v) {

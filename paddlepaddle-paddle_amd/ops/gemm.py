@@ -152,6 +152,30 @@ def wgrad_accumulate(x2, dy2, gw):
     return True
 
 
+def wgrad_tiles(gw):
+    """256x256 output tiles of a weight gradient."""
+    return -(-gw.shape[0] // 256) * -(-gw.shape[1] // 256)
+
+
+def wgrad_grouped_ok(x2, dy2, gw):
+    return (_hip_gemm and x2.is_cuda and gw.dtype == torch.bfloat16 and gw.is_contiguous() and
+            hip_mm_ok(x2.t(), dy2, 1) and _op_layout(x2.t())[0] == 1 and _op_layout(dy2)[0] == 0)
+
+
+def wgrad_accumulate_grouped2(a, b):
+    """Two weight gradients gw += x^T @ dy (a, b: (x2, dy2, gw), the same token count) in ONE
+    launch of the weight-gradient GEMM (csrc/gemm8.hip pa_gemm8_wgrad_grouped2): their tiles fill
+    one round of the chip together where each alone would leave CUs idle or need split-K."""
+    (xa, da, ga), (xb, db, gb) = a, b
+    K = xa.shape[0]
+    assert xb.shape[0] == K and da.shape[0] == K and db.shape[0] == K
+    at, bt = xa.t(), xb.t()
+    N.check(N.lib.pa_gemm8_wgrad_grouped2(
+        N.ptr(at), N.ptr(da), N.ptr(ga), ga.shape[0], ga.shape[1], _op_layout(at)[1], _op_layout(da)[1], ga.stride(0),
+        N.ptr(bt), N.ptr(db), N.ptr(gb), gb.shape[0], gb.shape[1], _op_layout(bt)[1], _op_layout(db)[1],
+        gb.stride(0), K, 1.0, 1.0, N.stream()), 'gemm_wgrad_grouped2')
+
+
 def transpose2d(x):
     """x^T materialised (csrc/act.hip ``pa_transpose2d``: 64x64 LDS tiles, 16-byte loads/stores)."""
     R, C = x.shape

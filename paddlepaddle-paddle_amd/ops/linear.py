@@ -14,13 +14,14 @@ buffers (inside the training engines); everything else takes the ordinary autogr
 
 Reference analogue: paddle/phi/kernels/fusion/gpu/fused_linear_param_grad_add_kernel.cu.
 """
+import os
+
 import torch
 
-from ..parallel.flat_buffer import flat_grad_slot, notify_grad_ready
+from ..parallel.flat_buffer import (flat_grad_slot, notify_grad_ready, defer_grad, complete_deferred,
+                                    register_pre_finish)
 from . import fused, gemm
 
-
-import os
 
 # Weight-gradient / data-gradient overlap: the wgrad GEMM of a Linear is launched on a side HIP
 # stream right before its dgrad GEMM on the compute stream, so the two (independent) GEMMs share
@@ -71,6 +72,60 @@ def _wgrad_join(tok):
     return None
 
 
+# Grouped weight gradients: a Linear weight gradient too small to fill the chip (fewer than 128
+# 256x256 tiles: the GPT out-projection, 64 tiles, which otherwise runs split-K 4 + a reduce pass) is
+# deferred until the next Linear weight gradient of the same token count whose tiles complete one
+# round with it (the QKV projection, 192 tiles): both then run as ONE launch of the weight-gradient
+# GEMM (ops.gemm.wgrad_accumulate_grouped2).  Its grad-ready hooks are held meanwhile
+# (parallel.flat_buffer.defer_grad) and anything still pending is flushed before the engines'
+# end-of-backward work (register_pre_finish) or by an end-of-backward callback.
+GROUP_WGRAD = os.environ.get('PADDLE_AMD_GROUP_WGRAD', '1') == '1'
+_pending = []          # [(x2, dy2, wparam, grad slot)] — at most one deferred weight gradient
+_cb_armed = [False]
+
+
+def _flush_pending():
+    while _pending:
+        x2, dy2, wp, gw = _pending.pop()
+        if not gemm.wgrad_accumulate(x2, dy2, gw):
+            gw.addmm_(x2.t(), dy2)
+        complete_deferred(wp)
+
+
+def _end_of_backward():
+    _cb_armed[0] = False
+    _flush_pending()
+
+
+register_pre_finish(_flush_pending)
+
+
+def _grad_w_grouped(x2, dy2, wp):
+    gw = flat_grad_slot(wp)
+    if not GROUP_WGRAD or gw is None or not x2.is_cuda or not gemm.wgrad_grouped_ok(x2, dy2, gw):
+        _flush_pending()
+        return _grad_w(x2, dy2, wp)
+    t = gemm.wgrad_tiles(gw)
+    if _pending:
+        px, pd, pw, pg = _pending[0]
+        both = t + gemm.wgrad_tiles(pg)
+        if px.shape[0] == x2.shape[0] and 224 <= both <= 256:
+            _pending.clear()
+            gemm.wgrad_accumulate_grouped2((x2, dy2, gw), (px, pd, pg))
+            complete_deferred(pw)
+            notify_grad_ready(wp)
+            return None
+        _flush_pending()
+    if t < 128:
+        defer_grad(wp)
+        _pending.append((x2, dy2, wp, gw))
+        if not _cb_armed[0]:
+            _cb_armed[0] = True
+            torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
+        return None
+    return _grad_w(x2, dy2, wp)
+
+
 class _LinearAccum(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, box):
@@ -91,7 +146,7 @@ class _LinearAccum(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         tok = _wgrad_async(x2, dy2, wp)
         dx = gemm.mm(dy2, w.t()).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
-        dw = _wgrad_join(tok) if tok is not None else _grad_w(x2, dy2, wp)
+        dw = _wgrad_join(tok) if tok is not None else _grad_w_grouped(x2, dy2, wp)
         db = _grad_b(dy2, bp) if bp is not None else None
         return dx, dw, db, None
 

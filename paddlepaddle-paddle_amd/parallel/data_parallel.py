@@ -125,6 +125,8 @@ class GradAllReducer:
             b.work = dist.all_reduce(g, dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     def _finish(self):
+        from .flat_buffer import run_pre_finish
+        run_pre_finish()  # deferred gradient kernels land before any bucket is treated as final
         for b in self.buckets:
             if b.work is None and b.pending != len(b.params):
                 self._launch(b)  # partially-touched bucket (unused params): reduce what we have

@@ -117,7 +117,9 @@ def register_grad_ready(p, fn):
     weight-gradient GEMM, which bypasses AccumulateGrad).  Returns a removable handle."""
     lst = p.__dict__.setdefault('_grad_ready', [])
     lst.append(fn)
-    h = p._t.register_post_accumulate_grad_hook(lambda t: fn())
+    # a gradient whose kernel was deferred (ops.linear grouped weight gradients) is not complete
+    # when autograd accumulates its (undefined) value: complete_deferred() fires the hooks later
+    h = p._t.register_post_accumulate_grad_hook(lambda t: None if p.__dict__.get('_grad_deferred') else fn())
 
     class _Handle:
         def remove(self):
@@ -158,6 +160,35 @@ def notify_grad_ready(p):
     if _HOOKS_FIRE:
         return
     for fn in p.__dict__.get('_grad_ready', ()):
+        fn()
+
+
+def defer_grad(p):
+    """Mark p's flat-slot gradient as still being computed (its kernel is deferred past the
+    autograd node): grad-ready hooks are held until complete_deferred(p)."""
+    p.__dict__['_grad_deferred'] = True
+
+
+def complete_deferred(p):
+    """The deferred gradient of p has been written: fire its grad-ready hooks now."""
+    if p.__dict__.pop('_grad_deferred', None):
+        for fn in list(p.__dict__.get('_grad_ready', ())):
+            fn()
+
+
+# Called by the training engines at the start of their end-of-backward callbacks (and by a
+# callback of their own when no engine runs), before any bucket / unit is treated as final:
+# producers of deferred gradients flush them here.
+_PRE_FINISH = []
+
+
+def register_pre_finish(fn):
+    if fn not in _PRE_FINISH:
+        _PRE_FINISH.append(fn)
+
+
+def run_pre_finish():
+    for fn in list(_PRE_FINISH):
         fn()
 
 

@@ -31,7 +31,7 @@ import torch
 import torch.distributed as dist
 
 from ..core.tensor import Tensor, Parameter, _wrap, _unwrap
-from .flat_buffer import FlatBuffer, ALIGN, register_grad_ready
+from .flat_buffer import FlatBuffer, ALIGN, register_grad_ready, run_pre_finish
 from .. import ops
 
 LEVELS = {'os': 1, 'os_g': 2, 'p_g_os': 3}
@@ -413,6 +413,7 @@ class ShardingEngine:
             dst.add_(src.to(dst.dtype))
 
     def _finish_backward(self):
+        run_pre_finish()  # deferred gradient kernels (ops.linear grouped weight gradients) land first
         for u in self.units:
             if u.pending > 0 and u.rs_work is None:
                 if not u.grad_live:

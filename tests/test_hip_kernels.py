@@ -1293,3 +1293,59 @@ def test_wgrad_side_stream_overlap_is_exact():
             linear.WGRAD_OVERLAP = old
     for n in finals[0]:
         assert torch.equal(finals[0][n], finals[1][n]), n
+
+
+def test_wgrad_grouped2_matches_fp32_reference():
+    """Two weight gradients (the GPT QKV 2048x6144 and out-projection 2048x2048 shapes: 192 + 64
+    tiles) in one grouped launch: gw_i += x_i^T dy_i, beta = 1, against fp32 torch."""
+    from paddle.ops import gemm
+    torch.manual_seed(0)
+    K = 1024
+    xa, da = (torch.randn(K, 2048, device='cuda') * 0.5).bfloat16(), (torch.randn(K, 6144, device='cuda') * 0.5).bfloat16()
+    xb, db = (torch.randn(K, 2048, device='cuda') * 0.5).bfloat16(), (torch.randn(K, 2048, device='cuda') * 0.5).bfloat16()
+    ga, gb = torch.randn(2048, 6144, device='cuda').bfloat16(), torch.randn(2048, 2048, device='cuda').bfloat16()
+    ra = ga.float() + xa.float().t() @ da.float()
+    rb = gb.float() + xb.float().t() @ db.float()
+    assert gemm.wgrad_grouped_ok(xa, da, ga) and gemm.wgrad_grouped_ok(xb, db, gb)
+    gemm.wgrad_accumulate_grouped2((xa, da, ga), (xb, db, gb))
+    torch.cuda.synchronize()
+    _close(ga, ra, 2e-2 * float(ra.abs().max()), 1e-2, 'grouped wgrad A')
+    _close(gb, rb, 2e-2 * float(rb.abs().max()), 1e-2, 'grouped wgrad B')
+
+
+def test_gpt_grouped_wgrad_trains_like_separate():
+    """A hidden-2048 GPT layer: the out-projection weight gradient deferred into the QKV one
+    (ops.linear GROUP_WGRAD, one grouped launch) trains like the separate launches."""
+    import paddle
+    from paddle.ops import linear
+    from paddle.models.gpt import gpt_config, GPTForPretraining
+    paddle.set_device('gpu:0')
+    finals = []
+    old = linear.GROUP_WGRAD
+    for on in (False, True):
+        linear.GROUP_WGRAD = on
+        try:
+            paddle.seed(31)
+            cfg = gpt_config('gpt-tiny', hidden_size=2048, num_attention_heads=16, intermediate_size=4096,
+                             num_hidden_layers=1, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+            model = GPTForPretraining(cfg)
+            opt = paddle.optimizer.AdamW(learning_rate=1e-4, parameters=model.parameters(), multi_precision=True)
+            model, opt = paddle.amp.decorate(model, opt, level='O2', dtype='bfloat16')
+            model, opt, _ = paddle.distributed.sharding.group_sharded_parallel(model, opt, level='p_g_os')
+            inner = model._layers
+            paddle.seed(32)
+            ids = paddle.randint(0, cfg.vocab_size, [8, 129])
+            for _ in range(2):
+                loss = inner.loss(model(ids[:, :-1]), ids[:, 1:])
+                loss.backward()
+                assert not linear._pending  # flushed by the end of every backward
+                opt.step()
+                opt.clear_grad()
+            finals.append({n: p._t.detach().float().clone() for n, p in inner.named_parameters()
+                           if 'out_proj' in n or 'qkv' in n})
+        finally:
+            linear.GROUP_WGRAD = old
+    assert any('out_proj' in n for n in finals[0])
+    for n in finals[0]:
+        a, b = finals[0][n], finals[1][n]
+        _close(b, a, 2e-2 * float(a.abs().max()) + 1e-4, 2e-2, n)
