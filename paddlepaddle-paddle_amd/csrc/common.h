@@ -103,6 +103,24 @@ __device__ __forceinline__ void gelu_tanh_fdf(float x, float& f, float& df) {
   df = 0.5f * (1.f + t) + hx * (1.f - t * t) * 0.79788456080286536f * (1.f + 3.f * 0.044715f * x2);
 }
 
+// gelu_tanh and its derivative for a PAIR of values in the sigmoid form (packed-f32 VALU, one
+// v_exp_f32 + one v_rcp_f32 per value): gelu_tanh(x) = x s, s = sigmoid(2u) = 1 / (1 + 2^z),
+// z = -2 log2(e) u, u = c (x + a x^3);  gelu_tanh'(x) = s + x s (1 - s) 2c (1 + 3 a x^2)
+// (= 0.5 (1 + t) + 0.5 x (1 - t^2) u' with t = 2s - 1).  Saturates cleanly: 2^z = inf -> s = 0.
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void gelu_tanh_fdf2(f32x2_t x, f32x2_t& f, f32x2_t& df) {
+  constexpr float c = 0.79788456080286536f, a = 0.044715f, l2e = 1.4426950408889634f;
+  constexpr float k1 = -2.f * l2e * c, k2 = -2.f * l2e * c * a, m1 = 2.f * c, m2 = 6.f * a * c;
+  const f32x2_t x2 = x * x;
+  const f32x2_t z = x * __builtin_elementwise_fma(x2, f32x2_t{k2, k2}, f32x2_t{k1, k1});
+  f32x2_t d = f32x2_t{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)} + 1.f;
+  const f32x2_t sg = f32x2_t{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f = x * sg;
+  const f32x2_t w = x * __builtin_elementwise_fma(x2, f32x2_t{m2, m2}, f32x2_t{m1, m1});
+  const f32x2_t k = __builtin_elementwise_fma(-sg, sg, sg);  // s (1 - s)
+  df = __builtin_elementwise_fma(w, k, sg);
+}
+
 struct GeluTanh {
   static __device__ __forceinline__ float f(float x) {
     const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
@@ -172,6 +190,66 @@ inline hipError_t launch_colsum_finish(const float* part, void* out, int P, int 
   colsum_finish<OT><<<(cols + 63) / 64, 1024, 0, st>>>(part, (OT*)out, P, cols, accum);
   return hipGetLastError();
 }
+
+// Up to three column-sum finishes over partial matrices of one shape [P, cols] in ONE launch
+// (blockIdx.y = job): the gamma / beta / bias gradients of a fused norm backward, each with its own
+// output dtype (0 fp32, 1 bf16, 2 fp16) and accumulate flag.  Same summation order as colsum_finish.
+struct FinishJob {
+  const float* part;
+  void* out;
+  int odt;
+  int accum;
+};
+struct FinishJobs {
+  FinishJob j[3];
+};
+
+template <typename OT>
+__device__ __forceinline__ void finish_store(void* out, int c, float t, int accum) {
+  OT* o = reinterpret_cast<OT*>(out);
+  o[c] = from_f<OT>(accum ? to_f(o[c]) + t : t);
+}
+
+static __global__ __launch_bounds__(1024) void colsum_finish_multi(FinishJobs jobs, int P, int cols) {
+  __shared__ float red[16][65];
+  const int y = blockIdx.y;
+  const FinishJob jb = y == 0 ? jobs.j[0] : (y == 1 ? jobs.j[1] : jobs.j[2]);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const float* __restrict__ part = jb.part;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < cols) {
+    int p = w;
+    for (; p + 48 < P; p += 64) {
+      s0 += part[(size_t)p * cols + c];
+      s1 += part[(size_t)(p + 16) * cols + c];
+      s2 += part[(size_t)(p + 32) * cols + c];
+      s3 += part[(size_t)(p + 48) * cols + c];
+    }
+    for (; p < P; p += 16) s0 += part[(size_t)p * cols + c];
+  }
+  red[w][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (w == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][lane];
+    if (jb.odt == 0) finish_store<float>(jb.out, c, t, jb.accum);
+    else if (jb.odt == 1) finish_store<bf16_t>(jb.out, c, t, jb.accum);
+    else finish_store<f16_t>(jb.out, c, t, jb.accum);
+  }
+}
+
+inline hipError_t launch_colsum_finish_multi(const FinishJobs& jobs, int njobs, int P, int cols, hipStream_t st) {
+  if (njobs <= 0) return hipSuccess;
+  colsum_finish_multi<<<dim3((cols + 63) / 64, njobs), 1024, 0, st>>>(jobs, P, cols);
+  return hipGetLastError();
+}
+
+template <typename T> constexpr int dtcode_of();
+template <> constexpr int dtcode_of<float>() { return 0; }
+template <> constexpr int dtcode_of<bf16_t>() { return 1; }
+template <> constexpr int dtcode_of<f16_t>() { return 2; }
 
 // dtype-coded output (0 fp32, 1 bf16, 2 fp16)
 inline hipError_t launch_colsum_finish_dt(const float* part, void* out, int odt, int P, int cols, int accum,

@@ -47,6 +47,7 @@ constexpr int BM = 256, BN = 256, BK = 64;
 // A/B switch for the 16-B-wide epilogue of schedule 11 (pa_gemm8_set_wide_epi); read by every
 // block, set only between launches.
 __constant__ int g_wide_epi = 1;
+
 constexpr int HALF = 128 * BK * 2;  // one 128-row (or 128-col) half of an operand tile: 16 KB
 constexpr int OPB = 2 * HALF;       // 32 KB
 constexpr int BUF = 2 * OPB;        // A + B of one K-tile: 64 KB
@@ -208,10 +209,15 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __r
 // 16 B per lane (each instruction: 16 rows x 64 contiguous bytes) instead of 32 stores of 8 B
 // (16 rows x 32 B) — the K = 2048 GEMMs of the step are epilogue-store-issue bound at the tail
 // (cdna_hip_programming T21).  Bias / beta / aux reads become 16-B loads too.
-template <int EPI>
+// Diagnostic variants (pa_gemm8_diag only): EPI 10 + e runs epilogue e's arithmetic but skips its
+// global stores (a data-dependent never-true guard keeps the math alive) — the epilogue's store
+// cost is the time difference to EPI e.
+template <int EPI_>
 __device__ __forceinline__ void epilogue_wide(const f32x4 (&acc)[8][4], uint16_t* __restrict__ C,
                                               float* __restrict__ ws, const uint16_t* __restrict__ bias, int M, int N,
                                               long long ldc, float alpha, float beta, int mb, int nb, int lane) {
+  constexpr int EPI = EPI_ % 10;
+  constexpr bool NOSTORE = EPI_ >= 10;
   const int g = lane >> 4;
   const bool upper = (g & 1) != 0;
 #pragma unroll
@@ -263,15 +269,22 @@ __device__ __forceinline__ void epilogue_wide(const f32x4 (&acc)[8][4], uint16_t
         if constexpr (EPI == 2) {
           float d[8];
 #pragma unroll
-          for (int r = 0; r < 8; ++r) gelu_tanh_fdf(v[r], v[r], d[r]);
-          store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(ws) + o, d);
+          for (int r = 0; r < 8; r += 2) {
+            f32x2_t fv, dv;
+            gelu_tanh_fdf2(f32x2_t{v[r], v[r + 1]}, fv, dv);
+            v[r] = fv.x;
+            v[r + 1] = fv.y;
+            d[r] = dv.x;
+            d[r + 1] = dv.y;
+          }
+          if (!NOSTORE || d[0] == 1234567.f) store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(ws) + o, d);
         } else if (beta != 0.f) {
           float old[8];
           load_f<bf16_t, 8>(reinterpret_cast<const bf16_t*>(C + o), old);
 #pragma unroll
           for (int r = 0; r < 8; ++r) v[r] += beta * old[r];
         }
-        store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(C + o), v);
+        if (!NOSTORE || v[0] == 1234567.f) store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(C + o), v);
       }
     }
     if constexpr (EPI == 4) {
@@ -1165,4 +1178,24 @@ PA_API int pa_gemm8_set_epi_sched(int v) {
   const int old = pa::g8::g_epi_sched;
   pa::g8::g_epi_sched = v == 12 ? 12 : 11;
   return old;
+}
+
+// Diagnostic: schedule-11 GEMM (A, B k-contiguous) with epilogue variant epi (0, 2, 10, 12; see
+// epilogue_wide).  aux: bf16 [M][ldc] for the GELU forms.
+PA_API int pa_gemm8_diag(const void* A, const void* B, void* C, const void* bias, void* aux, int M, int N, int K,
+                         int epi, hipStream_t st) {
+  using namespace pa::g8;
+  if (!pa_gemm8_ok(M, N, K, K, K, N, 0, 1, 1)) return (int)hipErrorInvalidValue;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  dim3 grid(tm * tn, 1, 1);
+#define PA_DIAG(E)                                                                                              \
+  gemm11_kernel<true, true, E><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, (float*)aux, \
+                                                     (const uint16_t*)bias, M, N, K, K, K, N, 1.f, 0.f, K)
+  if (epi == 0) PA_DIAG(0);
+  else if (epi == 2) PA_DIAG(2);
+  else if (epi == 10) PA_DIAG(10);
+  else if (epi == 12) PA_DIAG(12);
+  else return (int)hipErrorInvalidValue;
+#undef PA_DIAG
+  return (int)hipGetLastError();
 }

@@ -412,13 +412,14 @@ hipError_t launch_bwd(const void* dy, const void* x, const void* w, const float*
 #undef PA_NB
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  // gamma / beta / input-bias gradient finishes: one launch
   const int wacc = fa != nullptr ? fa->wacc : 0;
-  e = launch_colsum_finish<WT>(dw_part, dw, nparts, cols, wacc, st);
-  if (e == hipSuccess && !RMS && db != nullptr) e = launch_colsum_finish<WT>(db_part, db, nparts, cols, wacc, st);
-  if (e == hipSuccess && xb_part != nullptr)
-    e = launch_colsum_finish_dt(xb_part, fa->xbgrad, fa->xbgd, nparts, cols, fa->xbaccum, st);
-  if (e != hipSuccess) return e;
-  return hipGetLastError();
+  FinishJobs jobs{};
+  int nj = 0;
+  jobs.j[nj++] = FinishJob{dw_part, dw, dtcode_of<WT>(), wacc};
+  if (!RMS && db != nullptr) jobs.j[nj++] = FinishJob{db_part, db, dtcode_of<WT>(), wacc};
+  if (xb_part != nullptr) jobs.j[nj++] = FinishJob{xb_part, fa->xbgrad, fa->xbgd, fa->xbaccum};
+  return launch_colsum_finish_multi(jobs, nj, nparts, cols, st);
 }
 
 }  // namespace pa

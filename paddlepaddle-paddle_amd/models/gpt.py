@@ -15,6 +15,7 @@ MI355X mapping (per decoder block):
   LM head + loss        → hand-written GEMMs (tied, E.grad accumulated in place) + csrc/softmax_xent.hip
 """
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -58,6 +59,11 @@ def gpt_config(name, **overrides):
     d = dict(GPT_CONFIGS[name])
     d.update(overrides)
     return GPTConfig(**d)
+
+
+# fc2 bias handed to the next fused dropout + residual + LayerNorm (its gradient reduced in that
+# kernel's backward pass) instead of a GEMM bias epilogue + a column-sum pass (tests switch it)
+DEFER_FC2_BIAS = os.environ.get('PADDLE_AMD_DEFER_FC2_BIAS', '1') == '1'
 
 
 def _normal(std):
@@ -122,8 +128,25 @@ class GPTDecoderLayer(nn.Layer):
             ops.fused.bias_act_ok(_unwrap(x), self.mlp.fc1.bias)
 
     def forward(self, x, residual=None):
+        out, h, ob = self.forward_deferred(x, residual)
+        if ob is not None:
+            out = _wrap(_unwrap(out) + ob._t)
+        return out, h
+
+    def forward_deferred(self, x, residual=None, x_bias=None):
+        """forward() whose fc2 bias may be left to the consumer: returns (out, residual, out_bias)
+        with out_bias a Parameter still to be added to ``out`` (None when already applied).  The
+        GPT model hands it to the next fused dropout + residual + LayerNorm kernel, which adds it
+        and reduces its gradient in its own pass (no separate column-sum over the MLP output).
+        ``x_bias``: the previous block's deferred bias for ``x``."""
         if self._fused(x):
-            return self._forward_fused(x, residual)
+            return self._forward_fused(x, residual, x_bias)
+        if x_bias is not None:
+            x = _wrap(_unwrap(x) + x_bias._t)
+        out, h = self._forward_plain(x, residual)
+        return out, h, None
+
+    def _forward_plain(self, x, residual):
         if residual is None:
             a, h = self.ln1(x), x
         else:
@@ -133,26 +156,33 @@ class GPTDecoderLayer(nn.Layer):
         b, h = IF.fused_layer_norm(self._drop(attn), self.ln2.weight, self.ln2.bias, self.ln2._epsilon, residual=h)
         return self.mlp(b), h
 
-    def _forward_fused(self, x, residual):
+    def _forward_fused(self, x, residual, x_bias=None):
         """Training path on the HIP kernels: dropout + residual add + LayerNorm is one kernel each
-        way, the out-projection and fc1 biases are applied (and their gradients reduced) inside
-        the consuming kernels, so those two GEMMs run without a bias epilogue."""
+        way, the out-projection, fc1 and fc2 biases are applied (and their gradients reduced) inside
+        the consuming kernels, so those GEMMs run without a bias epilogue.  Returns
+        (out, residual, out_bias) — the fc2 bias is deferred to the next norm (forward_deferred)."""
         fz = ops.fused
         if residual is None:
+            if x_bias is not None:
+                x = _wrap(_unwrap(x) + x_bias._t)
             a, h = self.ln1(x), x
         else:
-            a, h = fz.dropout_add_norm(_unwrap(x), None, _unwrap(residual), self.ln1.weight._t, self.ln1.bias._t,
+            a, h = fz.dropout_add_norm(_unwrap(x), x_bias, _unwrap(residual), self.ln1.weight._t, self.ln1.bias._t,
                                        self.ln1._epsilon, self.p)
             a, h = _wrap(a), _wrap(h)
         o = F.linear(self.attn.core(a), self.attn.out_proj.weight, None)
         b, h = fz.dropout_add_norm(_unwrap(o), self.attn.out_proj.bias, _unwrap(h), self.ln2.weight._t,
                                    self.ln2.bias._t, self.ln2._epsilon, self.p)
         m = self.mlp
+        ob = m.fc2.bias if DEFER_FC2_BIAS else None
         if ops.linear.mlp_gelu_ok(b, m.fc1.weight, m.fc1.bias, m.fc2.weight):  # GELU in the GEMM epilogues
-            return _wrap(ops.linear.mlp_gelu(b, m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias)), _wrap(h)
+            y = ops.linear.mlp_gelu(b, m.fc1.weight, m.fc1.bias, m.fc2.weight, None if ob is not None else m.fc2.bias)
+            return _wrap(y), _wrap(h), ob
         z = F.linear(_wrap(b), m.fc1.weight, None)
         g = fz.bias_act(_unwrap(z), m.fc1.bias, 'gelu_tanh')
-        return m.fc2(_wrap(g)), _wrap(h)
+        if ob is not None:
+            return F.linear(_wrap(g), m.fc2.weight, None), _wrap(h), ob
+        return m.fc2(_wrap(g)), _wrap(h), None
 
 
 class GPTEmbeddings(nn.Layer):
@@ -183,17 +213,21 @@ class GPTModel(nn.Layer):
 
     def forward(self, input_ids, position_ids=None):
         x = self.embeddings(input_ids, position_ids)
-        out, res = x, None
+        out, res, ob = x, None, None  # ob: the previous block's deferred fc2 bias (forward_deferred)
         for layer in self.layers:
             if self.config.use_recompute and self.training:
                 from ..distributed.fleet.recompute import recompute
+                if ob is not None:
+                    out, ob = _wrap(_unwrap(out) + ob._t), None
                 out, res = recompute(layer, out, res)
             else:
-                out, res = layer(out, res)
+                out, res, ob = layer.forward_deferred(out, res, ob)
         if res is not None and self.training and ops.fused.dropout_add_norm_ok(_unwrap(out), None, self.p):
-            y, _ = ops.fused.dropout_add_norm(_unwrap(out), None, _unwrap(res), self.final_norm.weight._t,
+            y, _ = ops.fused.dropout_add_norm(_unwrap(out), ob, _unwrap(res), self.final_norm.weight._t,
                                               self.final_norm.bias._t, self.final_norm._epsilon, self.p)
             return _wrap(y)
+        if ob is not None:
+            out = _wrap(_unwrap(out) + ob._t)
         if self.p > 0:
             out = F.dropout(out, self.p, training=self.training)
         y, _ = IF.fused_layer_norm(out, self.final_norm.weight, self.final_norm.bias, self.final_norm._epsilon,

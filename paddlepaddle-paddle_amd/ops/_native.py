@@ -79,6 +79,7 @@ _SIGS = {
     'pa_gemm8_ok': [I, I, I, LL, LL, LL, I, I, I],
     'pa_gemm8_set_wide_epi': [I],
     'pa_gemm8_set_epi_sched': [I],
+    'pa_gemm8_diag': [P, P, P, P, P, I, I, I, I, P],
     'pa_bn_tune': [I],
     'pa_colsum_finish_parts': [P, P, I, I, I, I, P],
     'pa_gemm8_bf16_epi': [P, P, P, P, P, I, I, I, LL, LL, LL, I, F, I, P],

@@ -480,15 +480,17 @@ def _gelu_tanh(x):
     return 0.5 * x * (1 + torch.tanh(0.7978845608028654 * (x + 0.044715 * x ** 3)))
 
 
+@pytest.mark.parametrize("bscale", [1.0, 12.0])
 @pytest.mark.parametrize("kmajor_b", [False, True])
 @pytest.mark.parametrize("M,K,N", [(512, 256, 768), (264, 128, 520), (2048, 1024, 4096)])
-def test_gemm_gelu_epilogues(M, K, N, kmajor_b):
-    """EPI 2 (h = a@b + bias: C = gelu(h), aux = gelu'(h)) and EPI 3 (C = a@b * aux) of csrc/gemm8.hip."""
+def test_gemm_gelu_epilogues(M, K, N, kmajor_b, bscale):
+    """EPI 2 (h = a@b + bias: C = gelu(h), aux = gelu'(h)) and EPI 3 (C = a@b * aux) of csrc/gemm8.hip;
+    bscale 12 drives h deep into both saturated tails (sigmoid-form GELU: 2^z overflows to inf)."""
     from paddle.ops import gemm
     a = (torch.randn(M, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
     bm = torch.randn(K, N, device=DEV).to(torch.bfloat16)
     b = bm.t().contiguous().t() if kmajor_b else bm
-    bias = torch.randn(N, device=DEV).to(torch.bfloat16)
+    bias = (torch.randn(N, device=DEV) * bscale).to(torch.bfloat16)
     assert gemm.epi_ok(a, b, N)
     h = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     g = gemm.mm_epi(a, b, 2, h, bias=bias)
@@ -497,6 +499,7 @@ def test_gemm_gelu_epilogues(M, K, N, kmajor_b):
     _gelu_tanh(hr).backward(torch.ones_like(hr))
     _close(h, hr.grad, 2e-2, 1e-2, "gelu'")  # aux = gelu'(h)
     _close(g, _gelu_tanh(href), 2e-2, 1e-2, 'gelu')
+    assert torch.isfinite(g.float()).all() and torch.isfinite(h.float()).all()
     dy = (torch.randn(M, K, device=DEV)).to(torch.bfloat16)
     w2t = torch.randn(N, K, device=DEV).to(torch.bfloat16)  # dgrad operand dy @ W2^T with W2 [N, K]... [K,N] view
     aux = (torch.randn(M, N, device=DEV) * 2).to(torch.bfloat16)
@@ -1225,6 +1228,45 @@ def test_mlp_fc1_bias_grad_from_dgrad_epilogue():
     for n in finals[0]:
         a, b = finals[0][n], finals[1][n]
         _close(b, a, 1e-2 * float(a.abs().max()) + 1e-4, 1e-2, n)
+
+
+def test_gpt_fc2_bias_deferred_to_next_norm():
+    """GPT blocks hand the fc2 bias to the next fused dropout + residual + LayerNorm kernel (bias
+    added there, its gradient reduced in that kernel's backward): the loss and every parameter
+    gradient (fc2 biases included) match the GEMM-epilogue bias + column-sum path (same dropout
+    masks: same host seed sequence)."""
+    import paddle
+    from paddle.models import gpt as gpt_mod
+    from paddle.models.gpt import gpt_config, GPTForPretraining
+    from paddle.parallel.flat_buffer import flat_grad_slot
+    paddle.set_device('gpu:0')
+    grads, losses = [], []
+    for on in (False, True):
+        gpt_mod.DEFER_FC2_BIAS = on
+        try:
+            paddle.seed(23)
+            cfg = gpt_config('gpt-tiny', hidden_dropout_prob=0.1, attention_probs_dropout_prob=0.0)
+            model = GPTForPretraining(cfg)
+            opt = paddle.optimizer.AdamW(learning_rate=1e-3, parameters=model.parameters(), multi_precision=True)
+            model, opt = paddle.amp.decorate(model, opt, level='O2', dtype='bfloat16')
+            paddle.seed(24)
+            ids = paddle.randint(0, cfg.vocab_size, [8, 257])
+            loss = model.loss(model(ids[:, :-1]), ids[:, 1:])
+            loss.backward()
+            losses.append(float(loss))
+            g = {}
+            for n, p in model.named_parameters():
+                t = flat_grad_slot(p)
+                t = t if t is not None else p._t.grad
+                g[n] = t.detach().float().clone()
+            grads.append(g)
+        finally:
+            gpt_mod.DEFER_FC2_BIAS = True
+    assert abs(losses[0] - losses[1]) < 1e-2 * abs(losses[0]), losses
+    assert any('fc2.bias' in n for n in grads[0])
+    for n in grads[0]:
+        a, b = grads[0][n], grads[1][n]
+        _close(b, a, 3e-2 * float(a.abs().max()) + 1e-6, 0.0, n)
 
 
 def test_resnet_downsample_block_shared_dgrad():
