@@ -44,7 +44,7 @@ class ParallelMode:
 
 
 _LAZY = {'fleet': '.fleet', 'launch': '.launch', 'auto_parallel': '.auto_parallel', 'checkpoint': '.checkpoint',
-         'utils': '.utils', 'io': '.io', 'rpc': '.rpc'}
+         'utils': '.utils', 'io': '.io', 'rpc': '.rpc', 'passes': '.passes'}
 _AUTO = ('ProcessMesh', 'DistAttr', 'shard_tensor', 'dtensor_from_fn', 'reshard', 'shard_layer', 'shard_dataloader',
          'ReduceType', 'Placement', 'Shard', 'Replicate', 'Partial', 'shard_optimizer', 'shard_scaler',
          'ShardingStage1', 'ShardingStage2', 'ShardingStage3', 'to_static', 'Strategy', 'DistModel',

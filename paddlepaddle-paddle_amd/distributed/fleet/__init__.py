@@ -182,6 +182,9 @@ class _Fleet:
         if not self._is_collective:
             from ..ps import PSOptimizer
             return PSOptimizer(optimizer, self._ps, self._strategy)
+        from ...framework import in_dynamic_mode
+        if not in_dynamic_mode():  # static Program + Executor: collective data parallelism
+            return StaticCollectiveOptimizer(optimizer, self._hcg, self._strategy or DistributedStrategy())
         hcg = self._hcg
         if hcg is None:
             return optimizer
@@ -215,6 +218,86 @@ class _Fleet:
     @property
     def util(self):
         return utils
+
+
+class StaticCollectiveOptimizer:
+    """``fleet.distributed_optimizer`` in static mode (reference: fleet/meta_optimizers/
+    raw_program_optimizer.py + amp / gradient_merge meta optimizers, which rewrite the program
+    with c_broadcast of the parameters in the startup program and c_allreduce_sum of every
+    gradient).  ``minimize`` records the backward/update node and installs its step policy
+    (static/minimize.py): strategy.amp -> static AMP (amp_configs), strategy.gradient_merge ->
+    k-step merge, data-parallel gradient averaging over the data (x sharding) ranks in
+    ``fuse_grad_size_in_MB`` buckets.  Parameters are broadcast from the group's first rank when
+    the program is built, so every rank starts from the same weights.  Static tensor/pipeline
+    parallel program rewriting is not provided (mp/pp degree must be 1 here)."""
+
+    def __init__(self, optimizer, hcg, strategy):
+        self._inner_opt = optimizer
+        self._hcg = hcg
+        self._strategy = strategy
+        self._policy = None
+
+    def __getattr__(self, name):
+        return getattr(self.__dict__['_inner_opt'], name)
+
+    def _dp_group(self):
+        hcg = self._hcg
+        if hcg is None:
+            return None
+        if hcg.get_model_parallel_world_size() > 1 or hcg.get_pipe_parallel_world_size() > 1:
+            raise NotImplementedError("static-mode fleet: tensor / pipeline parallel program rewriting is not "
+                                      "supported (use dygraph fleet.distributed_model for mp/pp)")
+        if hcg.get_sharding_parallel_world_size() > 1:
+            # static sharding trains like data parallelism over data x sharding ranks (the reference's
+            # static sharding pass shards the optimizer state; the update is the same)
+            from ..communication import new_group
+            return new_group(list(range(dist.get_world_size())))
+        g = hcg.get_data_parallel_group()
+        return g if g is not None and g.nranks > 1 else None
+
+    def minimize(self, loss, startup_program=None, parameter_list=None, no_grad_set=None):
+        from ...static.program import _static_minimize
+        from ...static.minimize import step_policy
+        from ...static.program import default_main_program
+        s = self._strategy
+        opt = self._inner_opt
+        if s.amp:
+            from ...static import amp as samp
+            c = s.amp_configs
+            pure = bool(c.get('use_pure_fp16') or c.get('use_pure_bf16'))
+            dtype = 'bfloat16' if (c.get('use_pure_bf16') or c.get('use_bf16') or c.get('dtype') == 'bfloat16') \
+                else 'float16'
+            lists = samp.AutoMixedPrecisionLists(custom_white_list=c.get('custom_white_list') or None,
+                                                 custom_black_list=c.get('custom_black_list') or None, dtype=dtype)
+            opt = samp.decorate(opt, amp_lists=lists, level='O2' if pure else 'O1', dtype=dtype,
+                                init_loss_scaling=c.get('init_loss_scaling', 32768.0),
+                                use_dynamic_loss_scaling=c.get('use_dynamic_loss_scaling', None),
+                                incr_every_n_steps=c.get('incr_every_n_steps', 1000),
+                                decr_every_n_nan_or_inf=c.get('decr_every_n_nan_or_inf', 2),
+                                incr_ratio=c.get('incr_ratio', 2.0), decr_ratio=c.get('decr_ratio', 0.8))
+            res = opt.minimize(loss, startup_program, parameter_list, no_grad_set)
+        else:
+            res = _static_minimize(opt, loss, parameter_list, no_grad_set)
+        prog = default_main_program()
+        pol = step_policy(prog)
+        if s.gradient_merge:
+            pol.k_steps = max(1, int(s.gradient_merge_configs.get('k_steps', 1)))
+            pol.avg = bool(s.gradient_merge_configs.get('avg', True))
+        pol.dp_group = self._dp_group()
+        pol.fuse_grad_size_in_MB = s.fuse_grad_size_in_MB
+        if pol.dp_group is not None:
+            _broadcast_params(pol._params(), pol.dp_group)
+        self._policy = pol
+        return res
+
+
+def _broadcast_params(params, group):
+    """Parameters from the group's first rank (the reference's startup-program c_broadcast)."""
+    pg = getattr(group, 'pg', None)
+    src = group.ranks[0] if getattr(group, 'ranks', None) else 0
+    with torch.no_grad():
+        for p in params:
+            dist.broadcast(p._t.data, src=src, group=pg)
 
 
 class HybridParallelOptimizer:

@@ -151,26 +151,41 @@ class OptimizerWithMixedPrecision:
 
     # ---- executed by the Executor for the recorded minimize node
     def _static_minimize_exec(self, loss):
-        params = [p._t for p in (self._params or []) if p._t.requires_grad]
-        if not self._use_scaling:
+        self._scaled_backward(loss)
+        self._apply_update()
+
+    def _scaled_backward(self, loss, div=1.0):
+        """backward of loss * scale / div (gradients accumulate; static.minimize.StaticMinimize
+        splits the step so gradient merge / data-parallel reduction run in between)."""
+        if not self._use_scaling and div == 1.0:
             loss.backward()
+            return
+        (loss.float() * (self._scale / div)).backward()
+
+    def _apply_update(self, sync_found_inf=None):
+        """Unscale, check for inf/nan (``sync_found_inf``: a callable reducing the flag over the
+        data-parallel ranks), step unless found, clear, update the dynamic loss scale."""
+        if not self._use_scaling:
             self._optimizer.step()
             self._optimizer.clear_grad()
             return
-        (loss.float() * self._scale).backward()
+        params = [p._t for p in (self._params or []) if p._t.requires_grad]
         inv = 1.0 / self._scale
-        finite = torch.ones((), dtype=torch.bool, device=loss.device)
+        finite = None
         for t in params:
             if t.grad is not None:
                 t.grad.mul_(inv)
-                finite &= torch.isfinite(t.grad).all()
-        ok = bool(finite.item())
-        self.found_inf = not ok
-        if ok:
+                f = torch.isfinite(t.grad).all()
+                finite = f if finite is None else finite & f
+        found = False if finite is None else not bool(finite.item())
+        if sync_found_inf is not None:
+            found = sync_found_inf(found)
+        self.found_inf = found
+        if not found:
             self._optimizer.step()
         self._optimizer.clear_grad()
         if self._dynamic:
-            if ok:
+            if not found:
                 self._good += 1
                 self._bad = 0
                 if self._good == self._incr_every:

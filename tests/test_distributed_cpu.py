@@ -290,3 +290,9 @@ def test_bench_multi_rank_path_rehearsal(nproc):
     assert d['n_gpus'] == nproc and d['config']['parallelism'] == f'sharding-3x{nproc}'
     assert d['config']['global_batch'] == 2 * nproc and d['resnet50']['config']['parallelism'] == f'dp{nproc}'
     assert d['value'] > 0 and abs(d['value'] - 2 * 64 * nproc / (d['ms_per_step'] / 1e3)) < 1e-2 * d['value']
+
+
+@pytest.mark.parametrize("mode", ['fleet', 'fleet_merge', 'pass'])
+def test_static_collective_data_parallel_matches_full_batch(mode):
+    out = run_workers('worker_static_dp.py', mode)
+    assert out.count(f'static dp {mode} OK') == 2, out[-3000:]
