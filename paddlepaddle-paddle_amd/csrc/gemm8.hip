@@ -211,13 +211,16 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __r
 // (cdna_hip_programming T21).  Bias / beta / aux reads become 16-B loads too.
 // Diagnostic variants (pa_gemm8_diag only): EPI 10 + e runs epilogue e's arithmetic but skips its
 // global stores (a data-dependent never-true guard keeps the math alive) — the epilogue's store
-// cost is the time difference to EPI e.
+// cost is the time difference to EPI e; EPI 20 stores the same bytes with every store instruction
+// covering 1 KiB of consecutive addresses (a block's tile as one 128 KiB run; wrong layout, timing
+// only) — what full-line stores would buy over the tile's 16 rows x 64 B per instruction.
 template <int EPI_>
 __device__ __forceinline__ void epilogue_wide(const f32x4 (&acc)[8][4], uint16_t* __restrict__ C,
                                               float* __restrict__ ws, const uint16_t* __restrict__ bias, int M, int N,
                                               long long ldc, float alpha, float beta, int mb, int nb, int lane) {
   constexpr int EPI = EPI_ % 10;
-  constexpr bool NOSTORE = EPI_ >= 10;
+  constexpr bool NOSTORE = EPI_ >= 10 && EPI_ < 20;
+  constexpr bool LINEAR = EPI_ >= 20;  // diagnostic: same bytes, each store 1 KiB contiguous
   const int g = lane >> 4;
   const bool upper = (g & 1) != 0;
 #pragma unroll
@@ -284,7 +287,12 @@ __device__ __forceinline__ void epilogue_wide(const f32x4 (&acc)[8][4], uint16_t
 #pragma unroll
           for (int r = 0; r < 8; ++r) v[r] += beta * old[r];
         }
-        if (!NOSTORE || v[0] == 1234567.f) store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(C + o), v);
+        if constexpr (LINEAR) {
+          const long long lo = (long long)blockIdx.x * 65536 + (threadIdx.x >> 6) * 8192 + p * 4096 + i * 512 + lane * 8;
+          store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(C + lo), v);
+        } else if (!NOSTORE || v[0] == 1234567.f) {
+          store_f<bf16_t, 8>(reinterpret_cast<bf16_t*>(C + o), v);
+        }
       }
     }
     if constexpr (EPI == 4) {
@@ -304,6 +312,208 @@ __device__ __forceinline__ void epilogue_wide(const f32x4 (&acc)[8][4], uint16_t
         *reinterpret_cast<float4*>(dst + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
       }
     }
+  }
+}
+
+// LDS-staged epilogue (schedule 11): the block's 256 x 256 bf16 output tile is assembled in the
+// (then idle) 128 KiB of LDS and written back in whole rows — every store instruction covers two
+// rows x 512 contiguous bytes (full 128-B lines) instead of 16 rows x 64 B.  Measured on the
+// GPT-3 1.3B shapes: the register-fragment stores cost 8-13 % of a K = 2048 GEMM, the same bytes
+// as 1 KiB runs almost nothing (tools/gemm_epi_cost.py EPI 20, profiles/r3s2_gemm_epilogue_cost*).
+// Inputs of the epilogue (the saved GELU derivative of EPI 3/4, the old C of beta != 0) come in
+// the same way: row-contiguous loads into the LDS tile, fragment reads out of it.
+// Tile layout: row r (0..255) at r * 512 B, 16-B chunk c (0..31) at slot c ^ (r & 31): the
+// fragment writes / reads (16 rows x one chunk per 16 lanes) and the row reads / writes (one
+// row's 32 chunks per 32 lanes) are both bank-conflict free.
+__device__ __forceinline__ int stile(int r, int c) { return r * 512 + ((c ^ (r & 31)) << 4); }
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) char lds_char;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+
+// global [rows of the tile] -> LDS tile.  Wave w moves rows 32w .. 32w + 31, two per instruction.
+__device__ __forceinline__ void tile_in(const uint16_t* __restrict__ src, long long ld, int m0, int n0, int M, int N,
+                                        lds_char* lds, int wave, int lane) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    u32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = wave * 32 + 2 * (8 * h + j) + (lane >> 5), c = lane & 31;
+      // clamped, branch-free (rows / chunks past the edge load an in-bounds neighbour that is
+      // never stored back; a per-load branch here makes the register allocator spill the
+      // accumulators inside the main loop)
+      const int m = min(m0 + r, M - 1), n = min(n0 + c * 8, N - 8);
+      v[j] = *reinterpret_cast<const u32x4*>(src + (long long)m * ld + n);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = wave * 32 + 2 * (8 * h + j) + (lane >> 5), c = lane & 31;
+      *(lds_u32x4*)(lds + stile(r, c)) = v[j];
+    }
+  }
+}
+
+// LDS tile -> global rows (bounds-checked per 16-B chunk: N % 8 == 0).
+__device__ __forceinline__ void tile_out(uint16_t* __restrict__ dst, long long ld, int m0, int n0, int M, int N,
+                                         const lds_char* lds, int wave, int lane) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    u32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = wave * 32 + 2 * (8 * h + j) + (lane >> 5), c = lane & 31;
+      v[j] = *(const lds_u32x4*)(lds + stile(r, c));
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = wave * 32 + 2 * (8 * h + j) + (lane >> 5), c = lane & 31;
+      const int m = m0 + r, n = n0 + c * 8;
+      if (m < M && n < N) *reinterpret_cast<u32x4*>(dst + (long long)m * ld + n) = v[j];
+    }
+  }
+}
+
+__device__ __forceinline__ u32x4 pack_bf16x8(const float (&v)[8]) {
+  Pack<bf16_t, 8> pk;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) pk.v[r] = (bf16_t)v[r];
+  return __builtin_bit_cast(u32x4, pk);
+}
+
+template <int EPI>
+__device__ __forceinline__ void epilogue_staged(const f32x4 (&acc)[8][4], uint16_t* __restrict__ C,
+                                                float* __restrict__ ws, const uint16_t* __restrict__ bias, int M,
+                                                int N, long long ldc, float alpha, float beta, int m0, int n0,
+                                                int wr, int wc, int lane, lds_char* lds) {
+  static_assert(EPI == 0 || EPI == 2 || EPI == 3 || EPI == 4, "staged epilogue: EPI 0/2/3/4");
+  // opaque lane id: every address below depends on it, so none of them is hoisted above the main
+  // loop (the compiler otherwise precomputes ~80 registers of epilogue addresses there and spills)
+  asm volatile("" : "+v"(lane));
+  const int wave = wr * 4 + wc;
+  const int g = lane >> 4;
+  const bool upper = (g & 1) != 0;
+  const int mb = m0 + wr * 128, nb = n0 + wc * 64;
+  constexpr bool AUX_IN = EPI == 3 || EPI == 4;
+  const bool old_in = EPI == 0 && beta != 0.f;
+  // (no barrier first: the main loop's closing barriers already order every wave's last fragment
+  // reads before this point)
+  if (AUX_IN) tile_in(reinterpret_cast<const uint16_t*>(ws), ldc, m0, n0, M, N, lds, wave, lane);
+  else if (old_in) tile_in(C, ldc, m0, n0, M, N, lds, wave, lane);
+  if (AUX_IN || old_in) __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int n = nb + (upper ? 16 * (2 * p + 1) + 4 * (g - 1) : 16 * (2 * p) + 4 * g);
+    const int ch = (n - n0) >> 3;
+    float bb[8];
+    if (!AUX_IN && bias != nullptr && n < N) load_f<bf16_t, 8>(reinterpret_cast<const bf16_t*>(bias + n), bb);
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float lo = acc[i][2 * p][e], hi = acc[i][2 * p + 1][e];
+        asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(lo), "+v"(hi));
+        v[e] = lo * alpha;
+        v[4 + e] = hi * alpha;
+      }
+      const int r = wr * 128 + i * 16 + (lane & 15);
+      lds_char* slot = lds + stile(r, ch);
+      const bool valid = m0 + r < M && n < N;
+      if constexpr (AUX_IN) {
+        const Pack<bf16_t, 8> hv = __builtin_bit_cast(Pack<bf16_t, 8>, *(const lds_u32x4*)slot);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= (float)hv.v[e];
+        if constexpr (EPI == 4) {
+          if (valid) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cs[e] += (float)(bf16_t)v[e];  // the value as stored
+          }
+        }
+      } else {
+        if (bias != nullptr) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bb[e];
+        }
+        if constexpr (EPI == 2) {
+          float d[8];
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            f32x2_t fv, dv;
+            gelu_tanh_fdf2(f32x2_t{v[e], v[e + 1]}, fv, dv);
+            v[e] = fv.x;
+            v[e + 1] = fv.y;
+            d[e] = dv.x;
+            d[e + 1] = dv.y;
+          }
+          (void)d;  // gelu'(h) is recomputed from the accumulators after C has left the tile
+        } else if (old_in) {
+          float old[8];
+          const Pack<bf16_t, 8> ov = __builtin_bit_cast(Pack<bf16_t, 8>, *(const lds_u32x4*)slot);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) old[e] = (float)ov.v[e];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += beta * old[e];
+        }
+      }
+      // in place: this lane is the only reader / writer of its (row, chunk) slots
+      *(lds_u32x4*)slot = pack_bf16x8(v);
+    }
+    if constexpr (EPI == 4) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        cs[e] += __shfl_xor(cs[e], 1);
+        cs[e] += __shfl_xor(cs[e], 2);
+        cs[e] += __shfl_xor(cs[e], 4);
+        cs[e] += __shfl_xor(cs[e], 8);
+      }
+      if ((lane & 15) == 0 && n < N && mb < M) {
+        float* dst = reinterpret_cast<float*>(const_cast<uint16_t*>(bias)) + (long long)(mb / 128) * N + n;
+        *reinterpret_cast<float4*>(dst) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
+      }
+    }
+  }
+  __syncthreads();
+  tile_out(C, ldc, m0, n0, M, N, lds, wave, lane);
+  if constexpr (EPI == 2) {
+    // second tile: gelu'(h), recomputed from the accumulators (holding it packed through the C
+    // pass would cost 64 registers and spill the main loop)
+    __syncthreads();  // every wave has read its C rows out of the tile
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int n = nb + (upper ? 16 * (2 * p + 1) + 4 * (g - 1) : 16 * (2 * p) + 4 * g);
+      const int ch = (n - n0) >> 3;
+      float bb[8];
+      if (bias != nullptr && n < N) load_f<bf16_t, 8>(reinterpret_cast<const bf16_t*>(bias + n), bb);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float lo = acc[i][2 * p][e], hi = acc[i][2 * p + 1][e];
+          asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(lo), "+v"(hi));
+          v[e] = lo * alpha;
+          v[4 + e] = hi * alpha;
+        }
+        if (bias != nullptr) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bb[e];
+        }
+        float d[8];
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          f32x2_t fv, dv;
+          gelu_tanh_fdf2(f32x2_t{v[e], v[e + 1]}, fv, dv);
+          d[e] = dv.x;
+          d[e + 1] = dv.y;
+        }
+        *(lds_u32x4*)(lds + stile(wr * 128 + i * 16 + (lane & 15), ch)) = pack_bf16x8(d);
+      }
+    }
+    __syncthreads();
+    tile_out(reinterpret_cast<uint16_t*>(ws), ldc, m0, n0, M, N, lds, wave, lane);
   }
 }
 
@@ -831,6 +1041,8 @@ __global__ __launch_bounds__(512, 1) void gemm11_kernel(const char* __restrict__
 
   if constexpr (EPI == 1)
     epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
+  else if constexpr (EPI >= 100)  // LDS-staged epilogue of EPI - 100 (its own instantiation)
+    epilogue_staged<EPI - 100>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0, n0, wr, wc, lane, (lds_char*)smem);
   else if constexpr (EPI == 4)
     epilogue_wide<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
   else if (g_wide_epi)
@@ -1029,6 +1241,12 @@ __global__ __launch_bounds__(512, 1) void gemm12_kernel(const char* __restrict__
 
 
 static int g_sched = 9;
+// LDS-staged epilogue of schedule 11 (pa_gemm8_set_staged_epi), launched as the EPI + 100
+// instantiation.  1 (default): the GELU-derivative GEMMs (EPI 3/4: the staged aux-tile READ is
+// what pays, fc2 dgrad 543 -> 496 us); 2: also EPI 0/2 (measured 0-1.5 % faster on the K = 2048
+// shapes, 4 % slower at K = 8192 / two tile rounds, and EPI 2 loses to its derivative recompute:
+// profiles/r3s2_gemm_epilogue_cost_staged.log); 0: off.
+static int g_staged = 1;
 static int g_epi_sched = 11;  // schedule of the fused-epilogue MLP GEMMs (11 or 12)
 
 template <bool AK, bool BKM, int EPI>
@@ -1043,10 +1261,19 @@ static hipError_t launch(const void* A, const void* B, void* C, float* ws, const
     gemm12_kernel<AK, BKM, EPI><<<g, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                    (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
                                                    K / splitk, splitk);
-  } else if (g_sched == 11)
+  } else if (g_sched == 11) {
+    if constexpr (EPI == 0) {
+      if (g_staged == 2) {
+        gemm11_kernel<AK, BKM, 100><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
+                                                          (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
+                                                          K / splitk);
+        return hipGetLastError();
+      }
+    }
     gemm11_kernel<AK, BKM, EPI><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                       (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
                                                       K / splitk);
+  }
   else if (g_sched == 9)
     gemm9_kernel<AK, BKM, EPI><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                      (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
@@ -1083,6 +1310,17 @@ static hipError_t launch_epi(int transB, const void* A, const void* B, void* C, 
     else
       gemm12_kernel<true, false, EPI><<<g, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, (float*)aux,
                                                          (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, 0.f, K, 1);
+    return hipGetLastError();
+  }
+  if (g_staged == 2 || (g_staged == 1 && EPI != 2)) {
+    if (transB)
+      gemm11_kernel<true, true, EPI + 100><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C,
+                                                                 (float*)aux, (const uint16_t*)bias, M, N, K, lda, ldb,
+                                                                 ldc, alpha, 0.f, K);
+    else
+      gemm11_kernel<true, false, EPI + 100><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C,
+                                                                  (float*)aux, (const uint16_t*)bias, M, N, K, lda,
+                                                                  ldb, ldc, alpha, 0.f, K);
     return hipGetLastError();
   }
   if (transB)
@@ -1158,6 +1396,12 @@ PA_API int pa_gemm8_wgrad_grouped2(const void* A0, const void* B0, void* C0, int
   return (int)hipGetLastError();
 }
 
+PA_API int pa_gemm8_set_staged_epi(int v) {
+  const int old = pa::g8::g_staged;
+  pa::g8::g_staged = v < 0 ? 0 : (v > 2 ? 2 : v);
+  return old;
+}
+
 PA_API int pa_gemm8_set_wide_epi(int v) {
   int old = 1;
   (void)hipMemcpyFromSymbol(&old, HIP_SYMBOL(pa::g8::g_wide_epi), sizeof(int));
@@ -1195,6 +1439,9 @@ PA_API int pa_gemm8_diag(const void* A, const void* B, void* C, const void* bias
   else if (epi == 2) PA_DIAG(2);
   else if (epi == 10) PA_DIAG(10);
   else if (epi == 12) PA_DIAG(12);
+  else if (epi == 20) PA_DIAG(20);
+  else if (epi == 100) PA_DIAG(100);
+  else if (epi == 102) PA_DIAG(102);
   else return (int)hipErrorInvalidValue;
 #undef PA_DIAG
   return (int)hipGetLastError();

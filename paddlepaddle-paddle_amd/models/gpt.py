@@ -106,6 +106,15 @@ class GPTMLP(nn.Layer):
         return self.fc2(F.gelu(self.fc1(x), approximate=True))
 
 
+class DeferredBias:
+    """A bias Parameter still to be added to a block's output (deliberately not a Tensor, so layer
+    hooks that act on tensor outputs — e.g. the sharding engine's — leave it alone)."""
+    __slots__ = ('param',)
+
+    def __init__(self, param):
+        self.param = param
+
+
 class GPTDecoderLayer(nn.Layer):
     """Pre-LN block.  ``forward(x, residual)`` takes the *un-added* sublayer output of the
     previous block and the residual stream, so every residual add is fused into the next
@@ -127,24 +136,26 @@ class GPTDecoderLayer(nn.Layer):
         return self.training and ops.fused.dropout_add_norm_ok(_unwrap(x), None, self.p) and \
             ops.fused.bias_act_ok(_unwrap(x), self.mlp.fc1.bias)
 
-    def forward(self, x, residual=None):
-        out, h, ob = self.forward_deferred(x, residual)
+    def forward(self, x, residual=None, x_bias=None, defer_bias=False):
+        """Returns (out, residual_stream); with ``defer_bias=True`` (the GPT model's own loop)
+        (out, residual_stream, DeferredBias or None): the fc2 bias may be left to the consumer,
+        which hands it to the next fused dropout + residual + LayerNorm kernel (bias added there,
+        its gradient reduced in that kernel's backward: no separate column-sum over the MLP
+        output).  ``x_bias``: the previous block's DeferredBias for ``x``.  Not deferred when the
+        bias can be released after this block's forward (sharding stage-3 units)."""
+        xb = x_bias.param if x_bias is not None else None
+        if self._fused(x):
+            out, h, ob = self._forward_fused(x, residual, xb)
+        else:
+            if xb is not None:
+                x = _wrap(_unwrap(x) + xb._t)
+            out, h = self._forward_plain(x, residual)
+            ob = None
+        if defer_bias:
+            return out, h, (DeferredBias(ob) if ob is not None else None)
         if ob is not None:
             out = _wrap(_unwrap(out) + ob._t)
         return out, h
-
-    def forward_deferred(self, x, residual=None, x_bias=None):
-        """forward() whose fc2 bias may be left to the consumer: returns (out, residual, out_bias)
-        with out_bias a Parameter still to be added to ``out`` (None when already applied).  The
-        GPT model hands it to the next fused dropout + residual + LayerNorm kernel, which adds it
-        and reduces its gradient in its own pass (no separate column-sum over the MLP output).
-        ``x_bias``: the previous block's deferred bias for ``x``."""
-        if self._fused(x):
-            return self._forward_fused(x, residual, x_bias)
-        if x_bias is not None:
-            x = _wrap(_unwrap(x) + x_bias._t)
-        out, h = self._forward_plain(x, residual)
-        return out, h, None
 
     def _forward_plain(self, x, residual):
         if residual is None:
@@ -174,7 +185,8 @@ class GPTDecoderLayer(nn.Layer):
         b, h = fz.dropout_add_norm(_unwrap(o), self.attn.out_proj.bias, _unwrap(h), self.ln2.weight._t,
                                    self.ln2.bias._t, self.ln2._epsilon, self.p)
         m = self.mlp
-        ob = m.fc2.bias if DEFER_FC2_BIAS else None
+        ob = m.fc2.bias if (DEFER_FC2_BIAS and m.fc2.bias is not None
+                            and not m.fc2.bias.__dict__.get('_releasable', False)) else None
         if ops.linear.mlp_gelu_ok(b, m.fc1.weight, m.fc1.bias, m.fc2.weight):  # GELU in the GEMM epilogues
             y = ops.linear.mlp_gelu(b, m.fc1.weight, m.fc1.bias, m.fc2.weight, None if ob is not None else m.fc2.bias)
             return _wrap(y), _wrap(h), ob
@@ -218,16 +230,17 @@ class GPTModel(nn.Layer):
             if self.config.use_recompute and self.training:
                 from ..distributed.fleet.recompute import recompute
                 if ob is not None:
-                    out, ob = _wrap(_unwrap(out) + ob._t), None
+                    out, ob = _wrap(_unwrap(out) + ob.param._t), None
                 out, res = recompute(layer, out, res)
             else:
-                out, res, ob = layer.forward_deferred(out, res, ob)
+                out, res, ob = layer(out, res, ob, defer_bias=True)
         if res is not None and self.training and ops.fused.dropout_add_norm_ok(_unwrap(out), None, self.p):
-            y, _ = ops.fused.dropout_add_norm(_unwrap(out), ob, _unwrap(res), self.final_norm.weight._t,
-                                              self.final_norm.bias._t, self.final_norm._epsilon, self.p)
+            y, _ = ops.fused.dropout_add_norm(_unwrap(out), ob.param if ob is not None else None, _unwrap(res),
+                                              self.final_norm.weight._t, self.final_norm.bias._t,
+                                              self.final_norm._epsilon, self.p)
             return _wrap(y)
         if ob is not None:
-            out = _wrap(_unwrap(out) + ob._t)
+            out = _wrap(_unwrap(out) + ob.param._t)
         if self.p > 0:
             out = F.dropout(out, self.p, training=self.training)
         y, _ = IF.fused_layer_norm(out, self.final_norm.weight, self.final_norm.bias, self.final_norm._epsilon,

@@ -80,6 +80,7 @@ _SIGS = {
     'pa_gemm8_set_wide_epi': [I],
     'pa_gemm8_set_epi_sched': [I],
     'pa_gemm8_diag': [P, P, P, P, P, I, I, I, I, P],
+    'pa_gemm8_set_staged_epi': [I],
     'pa_bn_tune': [I],
     'pa_colsum_finish_parts': [P, P, I, I, I, I, P],
     'pa_gemm8_bf16_epi': [P, P, P, P, P, I, I, I, LL, LL, LL, I, F, I, P],
@@ -116,6 +117,9 @@ def _load():
             fn.argtypes = args
             fn.restype = None if name in _VOID_RET else (ctypes.c_longlong if name in _LL_RET else ctypes.c_int)
         lib = l
+        st = os.environ.get('PADDLE_AMD_GEMM_STAGED')  # A/B: LDS-staged GEMM epilogue level (0/1/2)
+        if st is not None:
+            l.pa_gemm8_set_staged_epi(int(st))
     except OSError as e:  # pragma: no cover
         load_error = str(e)
     return lib

@@ -56,6 +56,12 @@ class _Unit:
         self.gather_work = None
         self.rs_work = None
         self.pending = sum(1 for p in self.params if p._t.requires_grad)
+        # stage-3 parameters that are released after their layer's forward: consumers outside the
+        # layer must not hold on to them (models/gpt.py defers a bias to the next block only when
+        # this is False)
+        releasable = engine.level == 3 and not persistent
+        for p in self.params:
+            p.__dict__['_releasable'] = releasable
         self.arena_off = None  # set by engine
         self.index = -1
 

@@ -607,8 +607,15 @@ def test_sharding_stage3_alias_off_matches_alias_on_gpu(reduce_dtype):
             losses.append(float(loss))
         return losses, {k: v.astype('float32').numpy() for k, v in model.state_dict().items()}, eng
 
-    l1, s1, e1 = train(True)
-    l0, s0, e0 = train(False)
+    # the fc2 bias is deferred into the next block's norm only where its unit stays resident (alias
+    # on), which changes the rounding: compare the engines with the same bias placement
+    from paddle.models import gpt as gpt_mod
+    gpt_mod.DEFER_FC2_BIAS = False
+    try:
+        l1, s1, e1 = train(True)
+        l0, s0, e0 = train(False)
+    finally:
+        gpt_mod.DEFER_FC2_BIAS = True
     assert e1.alias and not e0.alias and any(not u.persistent for u in e0.units)
     if reduce_dtype is None:
         assert l0 == l1, (l0, l1)
@@ -757,6 +764,46 @@ def _gemm_case(gemm, ta, tb, M, N, K, splitk):
     want = 0.5 * ref + c.float() + bias.float()
     gemm.hip_mm(a, b, out=c, bias=bias, alpha=0.5, beta=1.0, splitk=splitk)
     _close(c, want, atol=0.02 * math.sqrt(K) / 8 + 0.05, rtol=0.01, name=f"gemm acc {ta}{tb}")
+
+
+@pytest.mark.parametrize("tb", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(512, 768, 512), (328, 264, 384), (1000, 1032, 256), (2048, 4096, 1024)])
+def test_gemm_staged_epilogue_bitwise(M, N, K, tb):
+    """Schedule 11 with the LDS-staged epilogue (whole-row stores through the LDS tile) writes
+    exactly what the register-fragment epilogue writes: plain, bias + beta accumulate, and the
+    fused MLP epilogues (gelu + gelu', x aux, x aux + column sums), ragged edges included."""
+    from paddle.ops import gemm
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N + K)
+    a = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).bfloat16()
+    b32 = torch.rand(K, N, device=DEV, generator=g) * 2 - 1
+    b = b32.bfloat16() if tb == 0 else b32.t().contiguous().bfloat16().t()
+    c0 = (torch.rand(M, N, device=DEV, generator=g) - 0.5).bfloat16()
+    bias = torch.rand(N, device=DEV, generator=g).bfloat16()
+    aux_in = (torch.randn(M, N, device=DEV, generator=g) * 2).bfloat16()
+    old_v = _native.lib.pa_gemm_set_variant(11)
+    outs = []
+    try:
+        for staged in (0, 2):
+            _native.lib.pa_gemm8_set_staged_epi(staged)
+            r = {'plain': gemm.hip_mm(a, b)}
+            c = c0.clone()
+            gemm.hip_mm(a, b, out=c, bias=bias, alpha=0.5, beta=1.0)
+            r['acc'] = c
+            h = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            r['gelu'] = gemm.mm_epi(a, b, 2, h, bias=bias)
+            r['gelu_d'] = h
+            r['dgelu'] = gemm.mm_epi(a, b, 3, aux_in)
+            part = torch.zeros(-(-M // 128) * N, dtype=torch.float32, device=DEV)
+            r['dgelu_cs'] = gemm.mm_epi(a, b, 3, aux_in, colsum_part=part)
+            r['colsum'] = part
+            outs.append(r)
+    finally:
+        _native.lib.pa_gemm8_set_staged_epi(1)
+        _native.lib.pa_gemm_set_variant(old_v)
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+    ref = a.float() @ b.float()
+    _close(outs[1]['plain'], ref, atol=0.02 * math.sqrt(K) / 8 + 0.05, rtol=0.01, name='staged plain')
 
 
 @pytest.mark.parametrize("fmt", [(torch.float8_e4m3fn, torch.float8_e4m3fn), (torch.float8_e4m3fn, torch.float8_e5m2)])

@@ -23,7 +23,7 @@ def timeit(fn, n=10):
 
 def main():
     import paddle  # noqa: F401
-    from paddle.ops import _native as NT
+    from paddle.ops import _native as NT, gemm
     L = NT._load()
     M, dev, bf = 16 * 1024, 'cuda', torch.bfloat16
     rnd = lambda *s: torch.rand(*s, device=dev, dtype=bf) * 2 - 1
@@ -37,12 +37,23 @@ def main():
     for r in range(R):
         for name, K, N in shapes:
             a, b, c, aux, bias = data[name]
-            epis = (0, 10, 2, 12) if name == 'fc1' else (0, 10)
+            epis = (0, 10, 20, 100, 2, 12, 102) if name == 'fc1' else (0, 10, 100)
             for e in epis:
                 for st in (0,):
                     fn = lambda e=e: NT.check(L.pa_gemm8_diag(NT.ptr(a), NT.ptr(b), NT.ptr(c), NT.ptr(bias),
                                                               NT.ptr(aux), M, N, K, e, NT.stream()), 'diag')
                     res.setdefault((name, e, st, 2.0 * M * N * K), []).append(timeit(fn))
+        # fused MLP epilogues through the production entry (fc2 dgrad x gelu' with the fc1 bias
+        # column sums = EPI 4), register-fragment vs LDS-staged epilogue
+        a, b, c, aux, bias = data['fc1']
+        part = torch.empty(M // 128 * 8192, device=dev, dtype=torch.float32)
+        for stg in (0, 2):
+            L.pa_gemm8_set_staged_epi(stg)
+            res.setdefault(('fc2dgrad-epi4', 4 + 100 * stg, 0, 2.0 * M * 8192 * 2048), []).append(
+                timeit(lambda: gemm.mm_epi(a, b.t(), 3, aux, out=c, colsum_part=part)))
+            res.setdefault(('fc1fwd-epi2', 2 + 100 * stg, 0, 2.0 * M * 8192 * 2048), []).append(
+                timeit(lambda: gemm.mm_epi(a, b.t(), 2, aux, bias=bias, out=c)))
+        L.pa_gemm8_set_staged_epi(1)
         print(f'round {r} done', flush=True)
     for (name, e, st, fl), ts in res.items():
         med = statistics.median(ts)
