@@ -517,6 +517,143 @@ __device__ __forceinline__ void epilogue_staged(const f32x4 (&acc)[8][4], uint16
   }
 }
 
+// Wave-local staged epilogue (schedule 11): no block barrier.  Each wave owns 16 KiB of the (then
+// idle) LDS and its 128 x 64 output slice goes out in two 64-row halves: the fragments of a half
+// are written to the wave's region ([64 rows][128 B], 16-B chunk c of row r at c ^ ((r >> 1) & 7):
+// conflict-free both ways), read back row-wise and stored as whole 128-B lines (8 rows x 128 B
+// per store instruction instead of 16 rows x 64 B).  EPI 2 keeps both outputs of a half in the
+// region (C in the first 8 KiB, gelu' in the second); EPI 3/4 and beta != 0 bring their input tile
+// in row-wise the same way.  LDS accesses of one wave complete in order, so no waits are needed
+// between the writes and the reads of other lanes' rows; wave_barrier keeps the compiler from
+// reordering them.
+__device__ __forceinline__ int wtile(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+template <int EPI>
+__device__ __forceinline__ void epilogue_wstaged(const f32x4 (&acc)[8][4], uint16_t* __restrict__ C,
+                                                 float* __restrict__ ws, const uint16_t* __restrict__ bias, int M,
+                                                 int N, long long ldc, float alpha, float beta, int mb, int nb,
+                                                 int lane, lds_char* region) {
+  static_assert(EPI == 0 || EPI == 2 || EPI == 3 || EPI == 4, "staged epilogue: EPI 0/2/3/4");
+  const int g = lane >> 4;
+  const bool upper = (g & 1) != 0;
+  constexpr bool AUX_IN = EPI == 3 || EPI == 4;
+  const bool old_in = EPI == 0 && beta != 0.f;
+  lds_char* reg_c = region;          // [64][128 B] output half (EPI 2: C)
+  lds_char* reg_a = region + 8192;   // EPI 2: gelu' half
+  const uint16_t* src_in = AUX_IN ? reinterpret_cast<const uint16_t*>(ws) : C;
+  float cs[2][8];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[p][e] = 0.f;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int rb = mb + half * 64;  // first row of this half
+    if (AUX_IN || old_in) {
+      // input half, row-wise: 8 rows x 128 B per load (clamped at the edges: never stored back)
+      u32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = 8 * j + (lane >> 3), c = lane & 7;
+        const int m = min(rb + r, M - 1), n = min(nb + c * 8, N - 8);
+        v[j] = *reinterpret_cast<const u32x4*>(src_in + (long long)m * ldc + n);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) *(lds_u32x4*)(reg_c + wtile(8 * j + (lane >> 3), lane & 7)) = v[j];
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int n = nb + (upper ? 16 * (2 * p + 1) + 4 * (g - 1) : 16 * (2 * p) + 4 * g);
+      const int ch = (n - nb) >> 3;
+      float bb[8];
+      if (!AUX_IN && bias != nullptr && n < N) load_f<bf16_t, 8>(reinterpret_cast<const bf16_t*>(bias + n), bb);
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int i = half * 4 + ii;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float lo = acc[i][2 * p][e], hi = acc[i][2 * p + 1][e];
+          asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(lo), "+v"(hi));
+          v[e] = lo * alpha;
+          v[4 + e] = hi * alpha;
+        }
+        const int r = ii * 16 + (lane & 15);  // row within the half
+        lds_char* slot = reg_c + wtile(r, ch);
+        if constexpr (AUX_IN) {
+          const Pack<bf16_t, 8> hv = __builtin_bit_cast(Pack<bf16_t, 8>, *(const lds_u32x4*)slot);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= (float)hv.v[e];
+          if constexpr (EPI == 4) {
+            if (rb + r < M && n < N) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) cs[p][e] += (float)(bf16_t)v[e];  // the value as stored
+            }
+          }
+        } else {
+          if (bias != nullptr) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += bb[e];
+          }
+          if constexpr (EPI == 2) {
+            float d[8];
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+              f32x2_t fv, dv;
+              gelu_tanh_fdf2(f32x2_t{v[e], v[e + 1]}, fv, dv);
+              v[e] = fv.x;
+              v[e + 1] = fv.y;
+              d[e] = dv.x;
+              d[e + 1] = dv.y;
+            }
+            *(lds_u32x4*)(reg_a + wtile(r, ch)) = pack_bf16x8(d);
+          } else if (old_in) {
+            const Pack<bf16_t, 8> ov = __builtin_bit_cast(Pack<bf16_t, 8>, *(const lds_u32x4*)slot);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += beta * (float)ov.v[e];
+          }
+        }
+        *(lds_u32x4*)slot = pack_bf16x8(v);  // in place: only this lane touches this slot
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // the half, row-wise: 8 rows x 128 B per store
+#pragma unroll
+    for (int o = 0; o < (EPI == 2 ? 2 : 1); ++o) {
+      const lds_char* rg = o == 0 ? reg_c : reg_a;
+      uint16_t* dst = o == 0 ? C : reinterpret_cast<uint16_t*>(ws);
+      u32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = *(const lds_u32x4*)(rg + wtile(8 * j + (lane >> 3), lane & 7));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = rb + 8 * j + (lane >> 3), n = nb + (lane & 7) * 8;
+        if (m < M && n < N) *reinterpret_cast<u32x4*>(dst + (long long)m * ldc + n) = v[j];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the next half overwrites the region after these reads
+  }
+  if constexpr (EPI == 4) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int n = nb + (upper ? 16 * (2 * p + 1) + 4 * (g - 1) : 16 * (2 * p) + 4 * g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        cs[p][e] += __shfl_xor(cs[p][e], 1);
+        cs[p][e] += __shfl_xor(cs[p][e], 2);
+        cs[p][e] += __shfl_xor(cs[p][e], 4);
+        cs[p][e] += __shfl_xor(cs[p][e], 8);
+      }
+      if ((lane & 15) == 0 && n < N && mb < M) {
+        float* dst = reinterpret_cast<float*>(const_cast<uint16_t*>(bias)) + (long long)(mb / 128) * N + n;
+        *reinterpret_cast<float4*>(dst) = make_float4(cs[p][0], cs[p][1], cs[p][2], cs[p][3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(cs[p][4], cs[p][5], cs[p][6], cs[p][7]);
+      }
+    }
+  }
+}
+
 // same, with an explicit split-K slab index (persistent kernels: blockIdx.z is not the slice)
 template <int EPI>
 __device__ __forceinline__ void epilogue_z(const f32x4 (&acc)[8][4], uint16_t* __restrict__ C,
@@ -1041,7 +1178,10 @@ __global__ __launch_bounds__(512, 1) void gemm11_kernel(const char* __restrict__
 
   if constexpr (EPI == 1)
     epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
-  else if constexpr (EPI >= 100)  // LDS-staged epilogue of EPI - 100 (its own instantiation)
+  else if constexpr (EPI >= 200)  // wave-local staged epilogue of EPI - 200 (its own instantiation)
+    epilogue_wstaged<EPI - 200>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane,
+                                (lds_char*)smem + (wr * 4 + wc) * 16384);
+  else if constexpr (EPI >= 100)  // block-staged epilogue of EPI - 100 (its own instantiation)
     epilogue_staged<EPI - 100>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0, n0, wr, wc, lane, (lds_char*)smem);
   else if constexpr (EPI == 4)
     epilogue_wide<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
@@ -1241,12 +1381,16 @@ __global__ __launch_bounds__(512, 1) void gemm12_kernel(const char* __restrict__
 
 
 static int g_sched = 9;
-// LDS-staged epilogue of schedule 11 (pa_gemm8_set_staged_epi), launched as the EPI + 100
-// instantiation.  1 (default): the GELU-derivative GEMMs (EPI 3/4: the staged aux-tile READ is
+// LDS-staged epilogue of schedule 11 (pa_gemm8_set_staged_epi).  4 (default): the wave-local
+// staged epilogue (EPI + 200 instantiation, no block barrier, whole 128-B lines) for EPI 0/2/3/4 —
+// faster than the register-fragment stores on every GPT-3 1.3B shape (fc1 + GELU 525 -> 486 us,
+// fc2 dgrad x gelu' 550 -> 482, qkv 319 -> 309: profiles/r3s2_gemm_epilogue_cost_wstaged.log).
+// The block-staged form (EPI + 100, one block barrier, 512-B rows): 1: the GELU-derivative GEMMs (EPI 3/4: the staged aux-tile READ is
 // what pays, fc2 dgrad 543 -> 496 us); 2: also EPI 0/2 (measured 0-1.5 % faster on the K = 2048
 // shapes, 4 % slower at K = 8192 / two tile rounds, and EPI 2 loses to its derivative recompute:
-// profiles/r3s2_gemm_epilogue_cost_staged.log); 0: off.
-static int g_staged = 1;
+// profiles/r3s2_gemm_epilogue_cost_staged.log); 3: the wave-local staged epilogue (EPI + 200,
+// no block barrier) for EPI 3/4; 4: wave-local for EPI 0/2/3/4; 0: off.
+static int g_staged = 4;
 static int g_epi_sched = 11;  // schedule of the fused-epilogue MLP GEMMs (11 or 12)
 
 template <bool AK, bool BKM, int EPI>
@@ -1265,6 +1409,12 @@ static hipError_t launch(const void* A, const void* B, void* C, float* ws, const
     if constexpr (EPI == 0) {
       if (g_staged == 2) {
         gemm11_kernel<AK, BKM, 100><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
+                                                          (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
+                                                          K / splitk);
+        return hipGetLastError();
+      }
+      if (g_staged == 4) {
+        gemm11_kernel<AK, BKM, 200><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                           (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
                                                           K / splitk);
         return hipGetLastError();
@@ -1310,6 +1460,17 @@ static hipError_t launch_epi(int transB, const void* A, const void* B, void* C, 
     else
       gemm12_kernel<true, false, EPI><<<g, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, (float*)aux,
                                                          (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, 0.f, K, 1);
+    return hipGetLastError();
+  }
+  if (g_staged == 4 || (g_staged == 3 && EPI != 2)) {
+    if (transB)
+      gemm11_kernel<true, true, EPI + 200><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C,
+                                                                 (float*)aux, (const uint16_t*)bias, M, N, K, lda, ldb,
+                                                                 ldc, alpha, 0.f, K);
+    else
+      gemm11_kernel<true, false, EPI + 200><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C,
+                                                                  (float*)aux, (const uint16_t*)bias, M, N, K, lda,
+                                                                  ldb, ldc, alpha, 0.f, K);
     return hipGetLastError();
   }
   if (g_staged == 2 || (g_staged == 1 && EPI != 2)) {
@@ -1398,7 +1559,7 @@ PA_API int pa_gemm8_wgrad_grouped2(const void* A0, const void* B0, void* C0, int
 
 PA_API int pa_gemm8_set_staged_epi(int v) {
   const int old = pa::g8::g_staged;
-  pa::g8::g_staged = v < 0 ? 0 : (v > 2 ? 2 : v);
+  pa::g8::g_staged = v < 0 ? 0 : (v > 4 ? 4 : v);
   return old;
 }
 
@@ -1442,6 +1603,8 @@ PA_API int pa_gemm8_diag(const void* A, const void* B, void* C, const void* bias
   else if (epi == 20) PA_DIAG(20);
   else if (epi == 100) PA_DIAG(100);
   else if (epi == 102) PA_DIAG(102);
+  else if (epi == 200) PA_DIAG(200);
+  else if (epi == 202) PA_DIAG(202);
   else return (int)hipErrorInvalidValue;
 #undef PA_DIAG
   return (int)hipGetLastError();

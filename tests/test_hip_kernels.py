@@ -783,7 +783,7 @@ def test_gemm_staged_epilogue_bitwise(M, N, K, tb):
     old_v = _native.lib.pa_gemm_set_variant(11)
     outs = []
     try:
-        for staged in (0, 2):
+        for staged in (0, 2, 4):
             _native.lib.pa_gemm8_set_staged_epi(staged)
             r = {'plain': gemm.hip_mm(a, b)}
             c = c0.clone()
@@ -798,10 +798,11 @@ def test_gemm_staged_epilogue_bitwise(M, N, K, tb):
             r['colsum'] = part
             outs.append(r)
     finally:
-        _native.lib.pa_gemm8_set_staged_epi(1)
+        _native.lib.pa_gemm8_set_staged_epi(4)
         _native.lib.pa_gemm_set_variant(old_v)
-    for k in outs[0]:
-        assert torch.equal(outs[0][k], outs[1][k]), k
+    for o in outs[1:]:
+        for k in outs[0]:
+            assert torch.equal(outs[0][k], o[k]), k
     ref = a.float() @ b.float()
     _close(outs[1]['plain'], ref, atol=0.02 * math.sqrt(K) / 8 + 0.05, rtol=0.01, name='staged plain')
 

@@ -37,7 +37,7 @@ def main():
     for r in range(R):
         for name, K, N in shapes:
             a, b, c, aux, bias = data[name]
-            epis = (0, 10, 20, 100, 2, 12, 102) if name == 'fc1' else (0, 10, 100)
+            epis = (0, 10, 20, 100, 200, 2, 12, 102, 202) if name == 'fc1' else (0, 10, 100, 200)
             for e in epis:
                 for st in (0,):
                     fn = lambda e=e: NT.check(L.pa_gemm8_diag(NT.ptr(a), NT.ptr(b), NT.ptr(c), NT.ptr(bias),
@@ -47,13 +47,13 @@ def main():
         # column sums = EPI 4), register-fragment vs LDS-staged epilogue
         a, b, c, aux, bias = data['fc1']
         part = torch.empty(M // 128 * 8192, device=dev, dtype=torch.float32)
-        for stg in (0, 2):
+        for stg in (0, 1, 3, 4):
             L.pa_gemm8_set_staged_epi(stg)
             res.setdefault(('fc2dgrad-epi4', 4 + 100 * stg, 0, 2.0 * M * 8192 * 2048), []).append(
                 timeit(lambda: gemm.mm_epi(a, b.t(), 3, aux, out=c, colsum_part=part)))
             res.setdefault(('fc1fwd-epi2', 2 + 100 * stg, 0, 2.0 * M * 8192 * 2048), []).append(
                 timeit(lambda: gemm.mm_epi(a, b.t(), 2, aux, bias=bias, out=c)))
-        L.pa_gemm8_set_staged_epi(1)
+        L.pa_gemm8_set_staged_epi(4)
         print(f'round {r} done', flush=True)
     for (name, e, st, fl), ts in res.items():
         med = statistics.median(ts)
