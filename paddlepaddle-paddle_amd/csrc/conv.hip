@@ -106,7 +106,25 @@ __device__ __forceinline__ void tile_coords(int bid, int nwg, int tm, int tn, in
   nt = in / gm;
 }
 
-template <int BN, int WM>
+typedef __attribute__((address_space(3))) char lds_char;
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+
+// Staged store of one wave's (16 FM) x (16 FN) output tile: the 8-B fragments go to the wave's
+// own LDS region ([rows][32 FN bytes], 16-B chunk c of row r at c ^ ((r / rows-per-256-B) % chunks))
+// and come back row-wise, 16 B per lane, so every store instruction writes whole 64-256-B row
+// segments instead of 16 rows x 8 B (each lane's 4 columns) — the same measure as the GEMM's
+// wave-local staged epilogue (csrc/gemm8.hip epilogue_wstaged).  No block barrier: a wave's LDS
+// accesses complete in order; wave_barrier only stops the compiler from reordering them.
+template <int FM, int FN>
+__device__ __forceinline__ int cstage_off(int r, int c) {
+  constexpr int RB = 32 * FN, CPR = RB / 16, RPL = RB >= 256 ? 1 : 256 / RB;
+  return r * RB + ((c ^ ((r / RPL) & (CPR - 1))) << 4);
+}
+
+template <int BN, int WM, bool STG = true>
 __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restrict__ X,
                                                          const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y,
                                                          const uint16_t* __restrict__ bias, Geom g, Taps tp, int M,
@@ -237,6 +255,55 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
 
   const int gq = lane >> 4;
   const bool ident = tp.osy == 1 && tp.osx == 1 && oy0 == 0 && ox0 == 0;
+  if constexpr (STG) {
+    constexpr int RB = 32 * FN, CPR = RB / 16, RPI = 64 / CPR;  // row bytes, 16-B chunks per row, rows per read
+    lds_char* reg = (lds_char*)smem + wave * (16 * FM * RB);
+    float bb[FN][4];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wc * (16 * FN) + j * 16 + 4 * gq;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bb[j][r] = 0.f;
+      if (bias && n < g.Cout) load_f<bf16_t, 4>(reinterpret_cast<const bf16_t*>(bias + n), bb[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int r = i * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        Pack<bf16_t, 4> pk;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk.v[e] = (bf16_t)(acc[i][j][e] + bb[j][e]);
+        const int cb = j * 32 + gq * 8;  // byte column within the wave's row
+        *(lds_u32x2*)(reg + cstage_off<FM, FN>(r, cb >> 4) + (cb & 15)) = __builtin_bit_cast(u32x2, pk);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    constexpr int NRD = 16 * FM / RPI;  // row-read instructions per wave
+#pragma unroll
+    for (int q = 0; q < NRD; q += 8) {
+      u32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (q + u < NRD) v[u] = *(const lds_u32x4*)(reg + cstage_off<FM, FN>((q + u) * RPI + lane / CPR, lane % CPR));
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (q + u >= NRD) continue;
+        const int r = (q + u) * RPI + lane / CPR;
+        const int m = m0 + wr * (16 * FM) + r;
+        const int n = n0 + wc * (16 * FN) + (lane % CPR) * 8;
+        if (m >= M || n >= g.Cout) continue;
+        long long ym = m;
+        if (!ident) {
+          const int nn = m / HoWo, rem = m - nn * HoWo;
+          const int ho = rem / Wo, wo = rem - ho * Wo;
+          ym = ((long long)nn * tp.HY + oy0 + tp.osy * ho) * tp.WY + ox0 + tp.osx * wo;
+        }
+        *reinterpret_cast<u32x4*>(Y + ym * g.Cout + n) = v[u];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int m = m0 + wr * (16 * FM) + i * 16 + (lane & 15);
@@ -307,7 +374,7 @@ __device__ __forceinline__ s16x8 ld_frag_mn(const char* img, int col0, int lane)
   return v;
 }
 
-template <int BN, int WM>
+template <int BN, int WM, bool STG = true>
 __global__ __launch_bounds__(NT, 1) void conv_wgrad_kernel(const uint16_t* __restrict__ X,
                                                            const uint16_t* __restrict__ dY, float* __restrict__ ws,
                                                            Geom g, int M, int P, int kchunk) {
@@ -437,6 +504,32 @@ __global__ __launch_bounds__(NT, 1) void conv_wgrad_kernel(const uint16_t* __res
 
   const int gq = lane >> 4;
   float* slab = ws + (long long)blockIdx.z * M * g.Cout;
+  if constexpr (STG) {
+    // fp32 slab rows leave whole: per 16-row fragment band, the wave's 16 x (16 FN) fp32 go to its
+    // own 16 x 64 FN-byte LDS region and come back row-wise (16 B per lane, 64 FN-byte row
+    // segments per store) instead of 16 rows x 64 B per store instruction
+    constexpr int RB = 64 * FN, CPR = RB / 16, RPI = 64 / CPR, RPL = RB >= 256 ? 1 : 256 / RB;
+    lds_char* reg = (lds_char*)smem + wave * (16 * RB);
+    auto off = [&](int r, int c) { return r * RB + ((c ^ ((r / RPL) & (CPR - 1))) << 4); };
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        *(lds_u32x4*)(reg + off(lane & 15, j * 4 + gq)) = __builtin_bit_cast(u32x4, acc[i][j]);
+      __builtin_amdgcn_wave_barrier();
+      u32x4 v[16 / RPI];
+#pragma unroll
+      for (int u = 0; u < 16 / RPI; ++u) v[u] = *(const lds_u32x4*)(reg + off(u * RPI + lane / CPR, lane % CPR));
+#pragma unroll
+      for (int u = 0; u < 16 / RPI; ++u) {
+        const int m = m0 + wr * (16 * FM) + i * 16 + u * RPI + lane / CPR;
+        const int n = n0 + wc * (16 * FN) + (lane % CPR) * 4;
+        if (m < M && n < g.Cout) *reinterpret_cast<u32x4*>(slab + (long long)m * g.Cout + n) = v[u];
+      }
+      __builtin_amdgcn_wave_barrier();  // the next band overwrites the region after these reads
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int m = m0 + wr * (16 * FM) + i * 16 + (lane & 15);
@@ -490,6 +583,14 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 
 using namespace pa::conv;
 
+// staged (row-segment) output stores of the forward / data-gradient and filter-gradient kernels (A/B knob pa_conv2d_set_staged; default on)
+static int g_conv_staged = 1;
+PA_API int pa_conv2d_set_staged(int v) {
+  const int old = g_conv_staged;
+  g_conv_staged = v ? 1 : 0;
+  return old;
+}
+
 // Contract: bf16 NHWC input [N,H,W,C], packed weight [Cout][R][S][C], output [N,Ho,Wo,Cout];
 // C % 32 == 0, (R*S*C) % 64 == 0, Cout % 8 == 0 (checked; Python falls back to MIOpen otherwise).
 PA_API int pa_conv2d_fwd_ok(int C, int Cout, int R, int S) {
@@ -505,19 +606,27 @@ PA_API int pa_conv2d_set_wm(int bn, int wm) {
   return old;
 }
 
+
+template <bool STG>
+static void launch_fwd_kernel_t(int BN, dim3 grid, const uint16_t* xp, const uint16_t* wp, uint16_t* yp,
+                                const uint16_t* bp, const Geom& g, const Taps& tp, int M, int K, hipStream_t st) {
+  if (BN == 256) {
+    if (g_fwd_wm[2] == 4) conv_fwd_kernel<256, 4, STG><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    else conv_fwd_kernel<256, 2, STG><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+  } else if (BN == 128) {
+    if (g_fwd_wm[1] == 4) conv_fwd_kernel<128, 4, STG><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    else conv_fwd_kernel<128, 2, STG><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+  } else {
+    if (g_fwd_wm[0] == 4) conv_fwd_kernel<64, 4, STG><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    else if (g_fwd_wm[0] == 8) conv_fwd_kernel<64, 8, STG><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    else conv_fwd_kernel<64, 2, STG><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+  }
+}
+
 static void launch_fwd_kernel(int BN, dim3 grid, const uint16_t* xp, const uint16_t* wp, uint16_t* yp,
                               const uint16_t* bp, const Geom& g, const Taps& tp, int M, int K, hipStream_t st) {
-  if (BN == 256) {
-    if (g_fwd_wm[2] == 4) conv_fwd_kernel<256, 4><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
-    else conv_fwd_kernel<256, 2><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
-  } else if (BN == 128) {
-    if (g_fwd_wm[1] == 4) conv_fwd_kernel<128, 4><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
-    else conv_fwd_kernel<128, 2><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
-  } else {
-    if (g_fwd_wm[0] == 4) conv_fwd_kernel<64, 4><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
-    else if (g_fwd_wm[0] == 8) conv_fwd_kernel<64, 8><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
-    else conv_fwd_kernel<64, 2><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
-  }
+  if (g_conv_staged) launch_fwd_kernel_t<true>(BN, grid, xp, wp, yp, bp, g, tp, M, K, st);
+  else launch_fwd_kernel_t<false>(BN, grid, xp, wp, yp, bp, g, tp, M, K, st);
 }
 
 static int launch_fwd(const void* x, const void* wpk, void* y, const void* bias, const Geom& g, const Taps& tp,
@@ -620,6 +729,22 @@ PA_API int pa_conv2d_wgrad_set_bncap(int v) {
   return old;
 }
 
+template <bool STG>
+static void launch_wgrad_kernel(int BN, dim3 grid, const uint16_t* xp, const uint16_t* dp, float* wsp, const Geom& g,
+                                int M, int P, int kchunk, hipStream_t st) {
+  if (BN == 256) {
+    if (g_wgrad_wm == 2) conv_wgrad_kernel<256, 2, STG><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
+    else conv_wgrad_kernel<256, 4, STG><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
+  } else if (BN == 128) {
+    if (g_wgrad_wm == 2) conv_wgrad_kernel<128, 2, STG><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
+    else conv_wgrad_kernel<128, 4, STG><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
+  } else {
+    if (g_wgrad_wm == 2) conv_wgrad_kernel<64, 2, STG><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
+    else if (g_wgrad_wm == 8) conv_wgrad_kernel<64, 8, STG><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
+    else conv_wgrad_kernel<64, 4, STG><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
+  }
+}
+
 // Filter gradient.  x: bf16 NHWC [N,H,W,C], dy: bf16 NHWC [N,Ho,Wo,Cout], ws: fp32 scratch of
 // (splits + ceil(splits / 16)) * R*S*C * Cout floats (splits = pa_conv2d_wgrad_splits), dw: bf16 [Cout][C][R][S]
 // (accumulate != 0: dw += the gradient, in place).  C % 8 == 0, Cout % 8 == 0, kchunk % 32 == 0.
@@ -640,17 +765,8 @@ PA_API int pa_conv2d_wgrad(const void* x, const void* dy, void* ws, void* dw, in
   const dim3 grid(tm * tn, 1, splits);
   const uint16_t *xp = (const uint16_t*)x, *dp = (const uint16_t*)dy;
   float* wsp = (float*)ws;
-  if (BN == 256) {
-    if (g_wgrad_wm == 2) conv_wgrad_kernel<256, 2><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
-    else conv_wgrad_kernel<256, 4><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
-  } else if (BN == 128) {
-    if (g_wgrad_wm == 2) conv_wgrad_kernel<128, 2><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
-    else conv_wgrad_kernel<128, 4><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
-  } else {
-    if (g_wgrad_wm == 2) conv_wgrad_kernel<64, 2><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
-    else if (g_wgrad_wm == 8) conv_wgrad_kernel<64, 8><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
-    else conv_wgrad_kernel<64, 4><<<grid, NT, 0, st>>>(xp, dp, wsp, g, M, P, kchunk);
-  }
+  if (g_conv_staged) launch_wgrad_kernel<true>(BN, grid, xp, dp, wsp, g, M, P, kchunk, st);
+  else launch_wgrad_kernel<false>(BN, grid, xp, dp, wsp, g, M, P, kchunk, st);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const long long total = (long long)M * Cout;  // Cout % 8 == 0: float4 groups never straddle a row

@@ -1040,7 +1040,11 @@ __global__ __launch_bounds__(512, 1) void gemm9_kernel(const char* __restrict__ 
   if (wr == 0) bar();  // match waves 4-7's barrier count
 
   // (the 16-B epilogue measured neutral here: weight gradients, K = 16384, beta = 1)
-  epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
+  if constexpr (EPI >= 200)  // wave-local staged epilogue (its own instantiation)
+    epilogue_wstaged<EPI - 200>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane,
+                                (lds_char*)smem + (wr * 4 + wc) * 16384);
+  else
+    epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
 }
 
 
@@ -1391,6 +1395,8 @@ static int g_sched = 9;
 // profiles/r3s2_gemm_epilogue_cost_staged.log); 3: the wave-local staged epilogue (EPI + 200,
 // no block barrier) for EPI 3/4; 4: wave-local for EPI 0/2/3/4; 0: off.
 static int g_staged = 4;
+// wave-local staged epilogue in schedule 9 (the weight-gradient GEMM, beta = 1 accumulate)
+static int g_staged9 = 1;
 static int g_epi_sched = 11;  // schedule of the fused-epilogue MLP GEMMs (11 or 12)
 
 template <bool AK, bool BKM, int EPI>
@@ -1424,10 +1430,19 @@ static hipError_t launch(const void* A, const void* B, void* C, float* ws, const
                                                       (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
                                                       K / splitk);
   }
-  else if (g_sched == 9)
+  else if (g_sched == 9) {
+    if constexpr (EPI == 0) {
+      if (g_staged9) {
+        gemm9_kernel<AK, BKM, 200><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
+                                                         (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
+                                                         K / splitk);
+        return hipGetLastError();
+      }
+    }
     gemm9_kernel<AK, BKM, EPI><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                      (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
                                                      K / splitk);
+  }
   else
     gemm8_kernel<AK, BKM, EPI><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                      (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
@@ -1551,6 +1566,12 @@ PA_API int pa_gemm8_wgrad_grouped2(const void* A0, const void* B0, void* C0, int
     return (int)hipErrorInvalidValue;
   const int t0 = ((M0 + BM - 1) / BM) * ((N0 + BN - 1) / BN), t1 = ((M1 + BM - 1) / BM) * ((N1 + BN - 1) / BN);
   Prob p1{(const char*)A1, (const char*)B1, (uint16_t*)C1, M1, N1, lda1, ldb1, ldc1};
+  if (g_staged9) {
+    gemm9_kernel<false, false, 200, true><<<t0 + t1, 512, 0, st>>>((const char*)A0, (const char*)B0, (uint16_t*)C0,
+                                                                   nullptr, nullptr, M0, N0, K, lda0, ldb0, ldc0,
+                                                                   alpha, beta, K, p1);
+    return (int)hipGetLastError();
+  }
   gemm9_kernel<false, false, 0, true><<<t0 + t1, 512, 0, st>>>((const char*)A0, (const char*)B0, (uint16_t*)C0,
                                                                nullptr, nullptr, M0, N0, K, lda0, ldb0, ldc0, alpha,
                                                                beta, K, p1);
@@ -1560,6 +1581,12 @@ PA_API int pa_gemm8_wgrad_grouped2(const void* A0, const void* B0, void* C0, int
 PA_API int pa_gemm8_set_staged_epi(int v) {
   const int old = pa::g8::g_staged;
   pa::g8::g_staged = v < 0 ? 0 : (v > 4 ? 4 : v);
+  return old;
+}
+
+PA_API int pa_gemm8_set_staged9(int v) {
+  const int old = pa::g8::g_staged9;
+  pa::g8::g_staged9 = v ? 1 : 0;
   return old;
 }
 

@@ -75,12 +75,14 @@ _SIGS = {
     'pa_conv2d_wgrad_set_bncap': [I],
     'pa_conv2d_wgrad_set_wm': [I],
     'pa_conv2d_set_wm': [I, I],
+    'pa_conv2d_set_staged': [I],
     'pa_gemm_ok': [I, I, I, LL, LL, LL, I],
     'pa_gemm8_ok': [I, I, I, LL, LL, LL, I, I, I],
     'pa_gemm8_set_wide_epi': [I],
     'pa_gemm8_set_epi_sched': [I],
     'pa_gemm8_diag': [P, P, P, P, P, I, I, I, I, P],
     'pa_gemm8_set_staged_epi': [I],
+    'pa_gemm8_set_staged9': [I],
     'pa_bn_tune': [I],
     'pa_colsum_finish_parts': [P, P, I, I, I, I, P],
     'pa_gemm8_bf16_epi': [P, P, P, P, P, I, I, I, LL, LL, LL, I, F, I, P],
@@ -120,6 +122,12 @@ def _load():
         st = os.environ.get('PADDLE_AMD_GEMM_STAGED')  # A/B: LDS-staged GEMM epilogue level (0/1/2)
         if st is not None:
             l.pa_gemm8_set_staged_epi(int(st))
+        cst = os.environ.get('PADDLE_AMD_CONV_STAGED')  # A/B: staged conv output stores
+        if cst is not None:
+            l.pa_conv2d_set_staged(int(cst))
+        st9 = os.environ.get('PADDLE_AMD_GEMM_STAGED9')  # A/B: staged weight-gradient epilogue
+        if st9 is not None:
+            l.pa_gemm8_set_staged9(int(st9))
     except OSError as e:  # pragma: no cover
         load_error = str(e)
     return lib

@@ -807,6 +807,73 @@ def test_gemm_staged_epilogue_bitwise(M, N, K, tb):
     _close(outs[1]['plain'], ref, atol=0.02 * math.sqrt(K) / 8 + 0.05, rtol=0.01, name='staged plain')
 
 
+@pytest.mark.parametrize("M,N,K", [(512, 768, 1024), (328, 264, 384), (2048, 6144, 2048)])
+def test_wgrad_staged_epilogue_bitwise(M, N, K):
+    """Schedule 9 (weight gradient: both operands m/n-contiguous, beta = 1 accumulate) with the
+    wave-local staged epilogue == the register epilogue, single and grouped launches."""
+    from paddle.ops import gemm
+    g = torch.Generator(device=DEV).manual_seed(M + 3 * N + K)
+    x = (torch.rand(K, M, device=DEV, generator=g) * 2 - 1).bfloat16()    # tokens x in
+    dy = (torch.rand(K, N, device=DEV, generator=g) * 2 - 1).bfloat16()   # tokens x out
+    x2 = (torch.rand(K, 256, device=DEV, generator=g) * 2 - 1).bfloat16()
+    dy2 = (torch.rand(K, 512, device=DEV, generator=g) * 2 - 1).bfloat16()
+    g0 = (torch.rand(M, N, device=DEV, generator=g) - 0.5).bfloat16()
+    h0 = (torch.rand(256, 512, device=DEV, generator=g) - 0.5).bfloat16()
+    outs = []
+    try:
+        for st in (0, 1):
+            _native.lib.pa_gemm8_set_staged9(st)
+            gw, gh = g0.clone(), h0.clone()
+            assert gemm.wgrad_accumulate(x, dy, gw)
+            gw2, gh2 = g0.clone(), h0.clone()
+            gemm.wgrad_accumulate_grouped2((x, dy, gw2), (x2, dy2, gh2))
+            outs.append((gw, gw2, gh2))
+    finally:
+        _native.lib.pa_gemm8_set_staged9(1)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    ref = g0.float() + x.float().t() @ dy.float()
+    _close(outs[1][0], ref, atol=0.02 * math.sqrt(K) / 8 + 0.05, rtol=0.01, name='staged wgrad')
+
+
+@pytest.mark.parametrize("wm", [2, 4, 8])
+@pytest.mark.parametrize("N,H,C,Cout,R,stride", [(2, 14, 64, 64, 3, 1), (3, 9, 128, 128, 3, 2), (2, 8, 64, 256, 3, 1),
+                                                 (1, 7, 256, 192, 3, 2), (2, 10, 64, 136, 1, 1)])
+def test_conv_staged_stores_bitwise(N, H, C, Cout, R, stride, wm):
+    """csrc/conv.hip forward / data-gradient / filter-gradient kernels with the staged row-segment
+    stores write exactly what the per-fragment stores write (every tile width / wave split, ragged pixel and channel
+    edges, stride-2 data-gradient classes)."""
+    from paddle.ops import conv
+    g = torch.Generator(device=DEV).manual_seed(N * 100 + H + C + Cout)
+    x = (torch.rand(N, H, H, C, device=DEV, generator=g) * 2 - 1).bfloat16()
+    w = (torch.rand(Cout, C, R, R, device=DEV, generator=g) * 2 - 1).bfloat16() / math.sqrt(C * R * R)
+    b = torch.rand(Cout, device=DEV, generator=g).bfloat16()
+    pad = (R // 2, R // 2)
+    bn = 256 if Cout >= 256 else (128 if Cout > 64 else 64)
+    if wm == 8 and bn != 64:
+        pytest.skip("wave split 8 only exists for 64-wide tiles")
+    old_wm = _native.lib.pa_conv2d_set_wm(bn, wm)
+    outs = []
+    try:
+        for st in (0, 1):
+            _native.lib.pa_conv2d_set_staged(st)
+            y = conv.conv2d_fwd(x, w, b, (stride, stride), pad, (1, 1))
+            dy = torch.ones_like(y) * 0.5 + y * 0.25
+            gx = conv.conv2d_dgrad_classes(dy, w, (H, H), (stride, stride), pad, (1, 1))
+            gw = conv.conv2d_wgrad(dy, x, tuple(w.shape), (stride, stride), pad, (1, 1)) if conv.wgrad_ok(x, w) \
+                else None
+            outs.append((y, gx, gw))
+    finally:
+        _native.lib.pa_conv2d_set_staged(1)
+        _native.lib.pa_conv2d_set_wm(bn, old_wm)
+    assert torch.equal(outs[0][0], outs[1][0])
+    for k in (1, 2):
+        if outs[0][k] is not None:
+            assert torch.equal(outs[0][k], outs[1][k]), k
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w.float(), b.float(), stride, pad)
+    _close(outs[1][0].permute(0, 3, 1, 2), ref, 0.05, 0.02, 'staged conv fwd')
+
+
 @pytest.mark.parametrize("fmt", [(torch.float8_e4m3fn, torch.float8_e4m3fn), (torch.float8_e4m3fn, torch.float8_e5m2)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 1024), (328, 264, 384), (1000, 1024, 2048)])
 def test_hip_fp8_gemm(fmt, M, N, K):
