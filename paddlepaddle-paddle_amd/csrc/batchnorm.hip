@@ -214,6 +214,34 @@ __global__ __launch_bounds__(1024) void stats_finish(const float* __restrict__ p
   }
 }
 
+// ---- Chan merge of G consecutive slab statistics (mean, M2 over rpb rows each, the last slab of
+// all P possibly short) into one (mean, M2) per group of G slabs: the epilogue-produced statistics
+// of a convolution / GEMM (thousands of 64-128-row slabs) brought down to a few hundred chunks
+// of G * rpb rows for stats_finish.  grid (ceil(cols / 256), ceil(P / G)), one column per thread.
+__global__ __launch_bounds__(256) void stats_merge(const float* __restrict__ pmean, const float* __restrict__ pm2,
+                                                   int P, int rows, int rpb, int cols, int G,
+                                                   float* __restrict__ omean, float* __restrict__ om2, int P2) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const int p0 = blockIdx.y * G, p1 = min(P, p0 + G);
+  const float nfull = (float)rpb, nlast = (float)(rows - (P - 1) * rpb);
+  float n = 0.f, s = 0.f;
+  for (int p = p0; p < p1; ++p) {
+    const float np = p == P - 1 ? nlast : nfull;
+    s += np * pmean[(size_t)p * cols + c];
+    n += np;
+  }
+  const float mu = s / n;
+  float m2 = 0.f;
+  for (int p = p0; p < p1; ++p) {
+    const float np = p == P - 1 ? nlast : nfull;
+    const float d = pmean[(size_t)p * cols + c] - mu;
+    m2 += pm2[(size_t)p * cols + c] + np * d * d;
+  }
+  omean[(size_t)blockIdx.y * cols + c] = mu;
+  om2[(size_t)blockIdx.y * cols + c] = m2;
+}
+
 // ---- y = act(x * a + b [+ z]),  a = gamma * rstd, b = beta - mean * a  (per channel)
 template <typename T, typename WT, bool RELU, bool RES>
 __global__ __launch_bounds__(256) void apply_fwd(const T* __restrict__ x, const T* __restrict__ z,
@@ -481,6 +509,41 @@ hipError_t fwd(const void* x, const void* z, const void* gamma, const void* beta
   return hipGetLastError();
 }
 
+// forward from slab statistics produced by the producer's epilogue (parts: fp32 [2][P][cols],
+// slabs of rpb rows, the last possibly short); ws: 2 * min(P, 512) * cols floats
+template <typename T, typename WT>
+hipError_t fwd_parts(const void* x, const void* z, const void* gamma, const void* beta, void* y, float* mean,
+                     float* rstd, float* run_mean, float* run_var, const float* parts, int P, int prpb, float* ws,
+                     int rows, int cols, float eps, float momentum, int relu, hipStream_t st) {
+  constexpr int E = 16 / sizeof(T);
+  const int cb = col_blocks(cols, E);
+  const int rpb = rows_per_block(rows, cb);
+  const dim3 grid(cb, (rows + rpb - 1) / rpb);
+  const float* pm = parts;
+  const float* pq = parts + (size_t)P * cols;
+  int Pf = P, rf = prpb;
+  if (P > 512) {  // merge groups of G slabs first (the finisher's per-lane loop is serial)
+    const int G = (P + 511) / 512;
+    const int P2 = (P + G - 1) / G;
+    stats_merge<<<dim3((cols + 255) / 256, P2), 256, 0, st>>>(pm, pq, P, rows, prpb, cols, G, ws,
+                                                               ws + (size_t)P2 * cols, P2);
+    pm = ws;
+    pq = ws + (size_t)P2 * cols;
+    Pf = P2;
+    rf = prpb * G;
+  }
+  stats_finish<<<(cols + 63) / 64, 1024, 0, st>>>(pm, pq, Pf, rows, rf, cols, eps, momentum, mean, rstd, run_mean,
+                                                  run_var);
+#define PA_BNF(R, Z) apply_fwd<T, WT, R, Z><<<grid, 256, 0, st>>>((const T*)x, (const T*)z, mean, rstd, \
+                                                                 (const WT*)gamma, (const WT*)beta, (T*)y, rows, cols, rpb)
+  if (relu && z) PA_BNF(true, true);
+  else if (relu) PA_BNF(true, false);
+  else if (z) PA_BNF(false, true);
+  else PA_BNF(false, false);
+#undef PA_BNF
+  return hipGetLastError();
+}
+
 template <typename T, typename WT>
 hipError_t bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
                const void* beta, void* dx, void* dz, void* dgamma, void* dbeta, float* ws, int rows, int cols, int relu,
@@ -548,6 +611,20 @@ PA_API hipError_t pa_bn_fwd(const void* x, const void* z, const void* gamma, con
   if (cols % (xd == 0 ? 4 : 8) != 0 || rows < 1) return hipErrorInvalidValue;
   PA_BN_DISPATCH(xd, wd, (bn::fwd<T, WT>(x, z, gamma, beta, y, mean, rstd, run_mean, run_var, ws, rows, cols, eps,
                                           momentum, training, relu, st)))
+}
+
+// Training forward whose batch statistics come from the producing kernel's epilogue (parts: fp32
+// [2][P][cols] slab means then M2s, slabs of rpb rows, only the last one short — csrc/conv.hip
+// pa_conv2d_fwd_stats, csrc/gemm8.hip epi 5); ws: >= 2 * 512 * cols floats.
+PA_API hipError_t pa_bn_fwd_parts(const void* x, const void* z, const void* gamma, const void* beta, void* y,
+                                  float* mean, float* rstd, float* run_mean, float* run_var, const float* parts, int P,
+                                  int rpb, float* ws, int rows, int cols, float eps, float momentum, int relu, int xd,
+                                  int wd, hipStream_t st) {
+  if (cols % (xd == 0 ? 4 : 8) != 0 || rows < 1 || P < 1 || rpb < 1 || (long long)(P - 1) * rpb >= rows ||
+      (long long)P * rpb < rows)
+    return hipErrorInvalidValue;
+  PA_BN_DISPATCH(xd, wd, (bn::fwd_parts<T, WT>(x, z, gamma, beta, y, mean, rstd, run_mean, run_var, parts, P, rpb, ws,
+                                                rows, cols, eps, momentum, relu, st)))
 }
 
 // dz (nullable): gradient of the residual input z (= dy masked by ReLU).  y is the saved output

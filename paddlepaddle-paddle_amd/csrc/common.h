@@ -87,6 +87,58 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return r;
 }
 
+// Per-column batch-norm statistics of one wave's output slab, computed in the producing GEMM /
+// convolution epilogue (fused_bn statistics: the standalone column pass over the activation is
+// skipped).  Swapped-MFMA layout: the lane holds rows 16 i + (lane & 15) (i < FM) of columns
+// 16 j + 4 (lane >> 4) + e (j < FN, e < 4) in acc[i][j][e]; rows at or past `nvalid` are excluded.
+// Two-pass in registers (sum -> mean -> sum of squared deviations: no E[x^2] - E[x]^2
+// cancellation), each pass reduced over the 16 lanes of a column group by xor shuffles.  The
+// slab's (mean, M2) over its nvalid rows go to pmean[col], pm2[col] (lanes with lane & 15 == 0;
+// cols >= ncols skipped, ncols % 4 == 0).  `add` (nullable, 4 FN values per lane, e.g. the bias)
+// is added to every value first.
+template <int FM, int FN, typename V>
+__device__ __forceinline__ void wave_col_stats(const V (&acc)[FM][FN], const float (*add)[4], int nvalid, int col0,
+                                               int ncols, float* __restrict__ pmean, float* __restrict__ pm2) {
+  if (nvalid <= 0) return;
+  const int lane = threadIdx.x & 63, r16 = lane & 15;
+  const float inv_n = 1.f / (float)nvalid;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const bool ok = 16 * i + r16 < nvalid;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[e] += ok ? acc[i][j][e] + (add ? add[j][e] : 0.f) : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) s[e] += __shfl_xor(s[e], o, 64);
+      s[e] *= inv_n;  // the slab mean, in every lane of the group
+    }
+    float q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const bool ok = 16 * i + r16 < nvalid;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = acc[i][j][e] + (add ? add[j][e] : 0.f) - s[e];
+        q[e] += ok ? d * d : 0.f;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) q[e] += __shfl_xor(q[e], o, 64);
+    const int c = col0 + 16 * j + 4 * (lane >> 4);
+    if (r16 == 0 && c < ncols) {
+      *reinterpret_cast<float4*>(pmean + c) = make_float4(s[0], s[1], s[2], s[3]);
+      *reinterpret_cast<float4*>(pm2 + c) = make_float4(q[0], q[1], q[2], q[3]);
+    }
+  }
+}
+
 // tanh(u) = 1 - 2 / (1 + e^{2u}) on the v_exp_f32 path (libm tanhf is a long polynomial
 // branch ladder: it made the GeLU kernels VALU-bound instead of HBM-bound).  Saturates
 // correctly at both ends (e^{2u} -> inf gives 1, -> 0 gives -1); |error| ~ 1e-7.

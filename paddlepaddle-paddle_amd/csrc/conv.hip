@@ -52,6 +52,9 @@ struct Taps {
   int cls_end[MAX_CLS], cls_tap0[MAX_CLS], cls_T[MAX_CLS], cls_a[MAX_CLS], cls_b[MAX_CLS], cls_Hc[MAX_CLS],
       cls_Wc[MAX_CLS];
   long long cls_woff[MAX_CLS];
+  // forward launches only (nullable): batch-norm column statistics of every 16*FM-row wave slab,
+  // fp32 [2][ceil(M / (16 FM))][Cout] (slab means, then M2s) — fused_bn statistics in the epilogue
+  float* stats;
 };
 
 __device__ __forceinline__ f32x4 mfma(s16x8 a, s16x8 b, f32x4 c) {
@@ -255,6 +258,13 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
 
   const int gq = lane >> 4;
   const bool ident = tp.osy == 1 && tp.osx == 1 && oy0 == 0 && ox0 == 0;
+  if (tp.stats != nullptr) {  // wave-uniform: forward launches without bias (host contract)
+    constexpr int RW = 16 * FM;
+    const int mw = m0 + wr * RW;
+    const long long P = (M + RW - 1) / RW;
+    wave_col_stats<FM, FN>(acc, nullptr, min(RW, M - mw), n0 + wc * (16 * FN), g.Cout,
+                           tp.stats + (long long)(mw / RW) * g.Cout, tp.stats + (P + mw / RW) * g.Cout);
+  }
   if constexpr (STG) {
     constexpr int RB = 32 * FN, CPR = RB / 16, RPI = 64 / CPR;  // row bytes, 16-B chunks per row, rows per read
     lds_char* reg = (lds_char*)smem + wave * (16 * FM * RB);
@@ -643,9 +653,35 @@ static int launch_fwd(const void* x, const void* wpk, void* y, const void* bias,
   return (int)hipGetLastError();
 }
 
+// rows per batch-norm statistics slab of a forward launch with Cout output channels (16 x the
+// fragments per wave along the pixels: 256 / WM of the tile width the launcher picks)
+PA_API int pa_conv2d_fwd_stat_rows(int Cout) {
+  const int BN = Cout >= 256 ? 256 : (Cout > 64 ? 128 : 64);
+  return 256 / g_fwd_wm[BN >= 256 ? 2 : (BN >= 128 ? 1 : 0)];
+}
+
+static int conv2d_fwd_impl(const void* x, const void* wpk, void* y, const void* bias, float* stats, int N, int H,
+                           int W, int C, int Cout, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw,
+                           int Ho, int Wo, hipStream_t st);
+
 PA_API int pa_conv2d_fwd(const void* x, const void* wpk, void* y, const void* bias, int N, int H, int W, int C,
                          int Cout, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw, int Ho, int Wo,
                          hipStream_t st) {
+  return conv2d_fwd_impl(x, wpk, y, bias, nullptr, N, H, W, C, Cout, R, S, sh, sw, ph, pw, dh, dw, Ho, Wo, st);
+}
+
+// forward + batch-norm column statistics (stats: fp32 [2][ceil(N*Ho*Wo / rows)][Cout], rows =
+// pa_conv2d_fwd_stat_rows(Cout)); no bias
+PA_API int pa_conv2d_fwd_stats(const void* x, const void* wpk, void* y, float* stats, int N, int H, int W, int C,
+                               int Cout, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw, int Ho, int Wo,
+                               hipStream_t st) {
+  if (stats == nullptr) return (int)hipErrorInvalidValue;
+  return conv2d_fwd_impl(x, wpk, y, nullptr, stats, N, H, W, C, Cout, R, S, sh, sw, ph, pw, dh, dw, Ho, Wo, st);
+}
+
+static int conv2d_fwd_impl(const void* x, const void* wpk, void* y, const void* bias, float* stats, int N, int H,
+                           int W, int C, int Cout, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw,
+                           int Ho, int Wo, hipStream_t st) {
   if (!pa_conv2d_fwd_ok(C, Cout, R, S) || N <= 0 || Ho <= 0 || Wo <= 0 || R * S > MAX_TAPS)
     return (int)hipErrorInvalidValue;
   Geom g{N, H, W, C, Ho, Wo, Cout, R, S, sh, sw, ph, pw, dh, dw};
@@ -660,6 +696,7 @@ PA_API int pa_conv2d_fwd(const void* x, const void* wpk, void* y, const void* bi
   tp.HY = Ho;
   tp.WY = Wo;
   tp.ldw = (long long)R * S * C;
+  tp.stats = stats;
   return launch_fwd(x, wpk, y, bias, g, tp, R * S, st);
 }
 
@@ -748,6 +785,54 @@ static void launch_wgrad_kernel(int BN, dim3 grid, const uint16_t* xp, const uin
 // Filter gradient.  x: bf16 NHWC [N,H,W,C], dy: bf16 NHWC [N,Ho,Wo,Cout], ws: fp32 scratch of
 // (splits + ceil(splits / 16)) * R*S*C * Cout floats (splits = pa_conv2d_wgrad_splits), dw: bf16 [Cout][C][R][S]
 // (accumulate != 0: dw += the gradient, in place).  C % 8 == 0, Cout % 8 == 0, kchunk % 32 == 0.
+// im2col of an NHWC input for convolutions whose channel count the implicit-GEMM kernel does not
+// take (the 3-channel RGB stem): out [M = N*Ho*Wo][Kp] bf16, k = (r, s, c) with c fastest, zeros for
+// taps in the padding and for k >= R*S*C (Kp % 8 == 0).  One 16-B store per thread; the input
+// rows it gathers from stay in L2 across the neighbouring output pixels.  The convolution is then
+// a 1 x 1 convolution of this matrix on conv_fwd_kernel.
+__global__ __launch_bounds__(256) void im2col_kernel(const uint16_t* __restrict__ X, uint16_t* __restrict__ out,
+                                                     Geom g, int M, int Kp) {
+  const int cpr = Kp >> 3;
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long m = t / cpr;
+  if (m >= M) return;
+  const int k0 = (int)(t - m * cpr) * 8;
+  const int HoWo = g.Ho * g.Wo;
+  const int n = (int)(m / HoWo), rem = (int)(m - (long long)n * HoWo);
+  const int ho = rem / g.Wo, wo = rem - ho * g.Wo;
+  const int KK = g.R * g.S * g.C;
+  uint16_t v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = k0 + e;
+    uint16_t val = 0;
+    if (k < KK) {
+      const int c = k % g.C, rs = k / g.C;
+      const int q = rs % g.S, r = rs / g.S;
+      const int hi = ho * g.sh - g.ph + r * g.dh, wi = wo * g.sw - g.pw + q * g.dw;
+      if ((unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W)
+        val = X[(((long long)n * g.H + hi) * g.W + wi) * g.C + c];
+    }
+    v[e] = val;
+  }
+  uint4 pk;
+  pk.x = v[0] | ((unsigned)v[1] << 16);
+  pk.y = v[2] | ((unsigned)v[3] << 16);
+  pk.z = v[4] | ((unsigned)v[5] << 16);
+  pk.w = v[6] | ((unsigned)v[7] << 16);
+  *reinterpret_cast<uint4*>(out + m * Kp + k0) = pk;
+}
+
+PA_API int pa_im2col_nhwc(const void* x, void* out, int N, int H, int W, int C, int R, int S, int sh, int sw, int ph,
+                          int pw, int dh, int dw, int Ho, int Wo, int Kp, hipStream_t st) {
+  const long long M = (long long)N * Ho * Wo;
+  if (M <= 0 || M > (1LL << 30) || Kp % 8 || Kp < R * S * C || C <= 0) return (int)hipErrorInvalidValue;
+  Geom g{N, H, W, C, Ho, Wo, 0, R, S, sh, sw, ph, pw, dh, dw};
+  const long long threads = M * (Kp / 8);
+  im2col_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, st>>>((const uint16_t*)x, (uint16_t*)out, g, (int)M, Kp);
+  return (int)hipGetLastError();
+}
+
 PA_API int pa_conv2d_wgrad_ok(int C, int Cout) { return C > 0 && C % 8 == 0 && Cout > 0 && Cout % 8 == 0; }
 
 PA_API int pa_conv2d_wgrad(const void* x, const void* dy, void* ws, void* dw, int N, int H, int W, int C, int Cout,

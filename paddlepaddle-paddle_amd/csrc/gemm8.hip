@@ -201,6 +201,9 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __r
       }
     }
   }
+  if constexpr (EPI == 5)  // + batch-norm column statistics of the 128-row slab (ws: [2][ceil(M/128)][N])
+    wave_col_stats<8, 4>(acc, nullptr, min(128, M - mb), nb, N, ws + (long long)(mb / 128) * N,
+                         ws + ((long long)((M + 127) / 128) + mb / 128) * N);
 }
 
 // 16-B-wide epilogue (CDNA4 v_permlane16_swap): lanes of 16-lane rows g and g^1 hold adjacent
@@ -533,7 +536,7 @@ __device__ __forceinline__ void epilogue_wstaged(const f32x4 (&acc)[8][4], uint1
                                                  float* __restrict__ ws, const uint16_t* __restrict__ bias, int M,
                                                  int N, long long ldc, float alpha, float beta, int mb, int nb,
                                                  int lane, lds_char* region) {
-  static_assert(EPI == 0 || EPI == 2 || EPI == 3 || EPI == 4, "staged epilogue: EPI 0/2/3/4");
+  static_assert(EPI == 0 || EPI == 2 || EPI == 3 || EPI == 4 || EPI == 5, "staged epilogue: EPI 0/2/3/4/5");
   const int g = lane >> 4;
   const bool upper = (g & 1) != 0;
   constexpr bool AUX_IN = EPI == 3 || EPI == 4;
@@ -634,6 +637,9 @@ __device__ __forceinline__ void epilogue_wstaged(const f32x4 (&acc)[8][4], uint1
     }
     __builtin_amdgcn_wave_barrier();  // the next half overwrites the region after these reads
   }
+  if constexpr (EPI == 5)  // EPI 0 + batch-norm column statistics of the slab (ws: [2][ceil(M/128)][N])
+    wave_col_stats<8, 4>(acc, nullptr, min(128, M - mb), nb, N, ws + (long long)(mb / 128) * N,
+                         ws + ((long long)((M + 127) / 128) + mb / 128) * N);
   if constexpr (EPI == 4) {
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
@@ -1187,6 +1193,8 @@ __global__ __launch_bounds__(512, 1) void gemm11_kernel(const char* __restrict__
                                 (lds_char*)smem + (wr * 4 + wc) * 16384);
   else if constexpr (EPI >= 100)  // block-staged epilogue of EPI - 100 (its own instantiation)
     epilogue_staged<EPI - 100>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0, n0, wr, wc, lane, (lds_char*)smem);
+  else if constexpr (EPI == 5)  // batch-norm statistics: the register epilogue carries them
+    epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
   else if constexpr (EPI == 4)
     epilogue_wide<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
   else if (g_wide_epi)
@@ -1466,7 +1474,7 @@ static hipError_t launch_epi(int transB, const void* A, const void* B, void* C, 
                              int N, int K, long long lda, long long ldb, long long ldc, float alpha, hipStream_t st) {
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   dim3 grid(tm * tn, 1, 1);
-  if (g_epi_sched == 12 && EPI != 4) {  // persistent: the epilogue overlaps the next tile's staging
+  if (g_epi_sched == 12 && EPI != 4 && EPI != 5) {  // persistent: the epilogue overlaps the next tile's staging
     const int items = tm * tn;
     const int g = items >= 256 ? 256 : (items + 7) / 8 * 8;
     if (transB)
@@ -1488,15 +1496,15 @@ static hipError_t launch_epi(int transB, const void* A, const void* B, void* C, 
                                                                   ldb, ldc, alpha, 0.f, K);
     return hipGetLastError();
   }
-  if (g_staged == 2 || (g_staged == 1 && EPI != 2)) {
+  if (EPI != 5 && (g_staged == 2 || (g_staged == 1 && EPI != 2))) {
     if (transB)
-      gemm11_kernel<true, true, EPI + 100><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C,
+      gemm11_kernel<true, true, EPI == 5 ? 100 : EPI + 100><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C,
                                                                  (float*)aux, (const uint16_t*)bias, M, N, K, lda, ldb,
                                                                  ldc, alpha, 0.f, K);
     else
-      gemm11_kernel<true, false, EPI + 100><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C,
-                                                                  (float*)aux, (const uint16_t*)bias, M, N, K, lda,
-                                                                  ldb, ldc, alpha, 0.f, K);
+      gemm11_kernel<true, false, EPI == 5 ? 100 : EPI + 100><<<grid, 512, 0, st>>>(
+          (const char*)A, (const char*)B, (uint16_t*)C, (float*)aux, (const uint16_t*)bias, M, N, K, lda, ldb, ldc,
+          alpha, 0.f, K);
     return hipGetLastError();
   }
   if (transB)
@@ -1551,6 +1559,9 @@ PA_API int pa_gemm8_bf16_epi(const void* A, const void* B, void* C, const void* 
   if (epi == 3) return (int)launch_epi<3>(transB, A, B, C, aux, nullptr, M, N, K, lda, ldb, ldc, alpha, st);
   // epi 4: epi 3 + column partial sums of C, one fp32 row per 128-row slab, into bias ([ceil(M/128)][N])
   if (epi == 4 && bias != nullptr) return (int)launch_epi<4>(transB, A, B, C, aux, bias, M, N, K, lda, ldb, ldc, alpha, st);
+  // epi 5: plain C = alpha*A@B + batch-norm column statistics (mean, M2) of every 128-row slab into
+  // aux (fp32 [2][ceil(M/128)][N]: means, then M2s), finished by pa_bn_fwd_parts; no bias
+  if (epi == 5 && bias == nullptr) return (int)launch_epi<5>(transB, A, B, C, aux, nullptr, M, N, K, lda, ldb, ldc, alpha, st);
   return (int)hipErrorInvalidValue;
 }
 

@@ -38,6 +38,7 @@ _SIGS = {
     'pa_maxpool2d_nhwc_bwd': [P, P, P] + [I] * 13 + [P],
     'pa_bn_ws_floats': [I, I, I],
     'pa_bn_fwd': [P, P, P, P, P, P, P, P, P, P, I, I, F, F, I, I, I, I, P],
+    'pa_bn_fwd_parts': [P, P, P, P, P, P, P, P, P, P, I, I, P, I, I, F, F, I, I, I, P],
     'pa_bn_bwd': [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P],
     'pa_softmax_fwd': [P, P, I, I, I, I, P],
     'pa_softmax_bwd': [P, P, P, I, I, I, P],
@@ -68,6 +69,9 @@ _SIGS = {
     'pa_gemm_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
     'pa_conv2d_fwd_ok': [I, I, I, I],
     'pa_conv2d_fwd': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
+    'pa_conv2d_fwd_stats': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
+    'pa_conv2d_fwd_stat_rows': [I],
+    'pa_im2col_nhwc': [P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
     'pa_conv2d_wgrad_ok': [I, I],
     'pa_conv2d_dgrad_classes': [P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     'pa_conv2d_wgrad': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],

@@ -32,10 +32,21 @@ class _BNAct(torch.autograd.Function):
             rstd = torch.rsqrt(run_var.float() + eps)
         rm = run_mean if (training and run_mean is not None and run_mean.dtype == torch.float32) else None
         rv = run_var if rm is not None else None
-        ws = _ws(rows, C, dt, x.device)
-        N.check(N.lib.pa_bn_fwd(N.ptr(x2), N.ptr(z2), N.ptr(gamma), N.ptr(beta), N.ptr(y), N.ptr(mean), N.ptr(rstd),
-                                N.ptr(rm), N.ptr(rv), N.ptr(ws), rows, C, float(eps), float(momentum), int(training),
-                                int(relu), dt, wd, N.stream()), 'bn_fwd')
+        parts = None
+        if training and (run_mean is None or rm is not None):
+            from .conv import take_bn_parts
+            parts = take_bn_parts(x)  # slab statistics written by the producing conv / GEMM epilogue
+        if parts is not None:
+            pbuf, P, prpb = parts
+            ws = torch.empty(2 * min(P, 512) * C, dtype=torch.float32, device=x.device)
+            N.check(N.lib.pa_bn_fwd_parts(N.ptr(x2), N.ptr(z2), N.ptr(gamma), N.ptr(beta), N.ptr(y), N.ptr(mean),
+                                          N.ptr(rstd), N.ptr(rm), N.ptr(rv), N.ptr(pbuf), P, prpb, N.ptr(ws), rows, C,
+                                          float(eps), float(momentum), int(relu), dt, wd, N.stream()), 'bn_fwd_parts')
+        else:
+            ws = _ws(rows, C, dt, x.device)
+            N.check(N.lib.pa_bn_fwd(N.ptr(x2), N.ptr(z2), N.ptr(gamma), N.ptr(beta), N.ptr(y), N.ptr(mean),
+                                    N.ptr(rstd), N.ptr(rm), N.ptr(rv), N.ptr(ws), rows, C, float(eps), float(momentum),
+                                    int(training), int(relu), dt, wd, N.stream()), 'bn_fwd')
         if training and run_mean is not None and rm is None:  # non-fp32 running buffers
             with torch.no_grad():
                 xv = x2.reshape(rows, C).float()

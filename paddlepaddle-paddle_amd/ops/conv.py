@@ -3,8 +3,10 @@
 Reference: paddle/phi/kernels/gpudnn/conv_kernel.cu (forward), conv_grad_kernel.cu (backward).
 * Forward: im2col folded into the LDS-DMA source addresses, zero padding via a zero block, bias
   fused; the weight is packed into the [Cout][R][S][C] k-contiguous image the kernel stages
-  (re-packed per call).  Needs C % 32 == 0; the 3-channel stem forward runs on the storage
-  layer's convolution (its backward still comes here).
+  (re-packed per call).  Needs C % 32 == 0; few-channel inputs (the 3-channel RGB stem) go
+  through an explicit im2col matrix (pa_im2col_nhwc, K padded to 64) and a 1x1 convolution.
+* Batch-norm statistics (fused_bn_stats): the forward epilogue can also emit per-slab channel
+  (mean, M2) for the batch norm that consumes the output (ops/batchnorm.py).
 * Data gradient (any stride): stride classes of input pixels, each a stride-1 implicit GEMM over
   dY with the taps that reach it, all classes in one launch (pa_conv2d_dgrad_classes).
 * Filter gradient (any R x S / stride / padding): implicit GEMM with the pixels as the reduction
@@ -70,6 +72,53 @@ def _out_hw(H, W, R, S, stride, pad, dil):
             (W + 2 * pad[1] - dil[1] * (S - 1) - 1) // stride[1] + 1)
 
 
+# ---- batch-norm statistics from the convolution epilogue (fused_bn statistics)
+# Inside ``fused_bn_stats()`` (the ResNet forward), every forward convolution without bias that runs
+# on a hand-written kernel also writes the per-channel (mean, M2) of each 64-256-row slab of its
+# output (csrc/conv.hip pa_conv2d_fwd_stats, csrc/gemm8.hip epi 5).  The training batch norm that
+# consumes that output (ops/batchnorm.py) takes them instead of re-reading the activation for its
+# statistics pass.  Entries are keyed by the output tensor object (weak reference) and popped by
+# the consumer.
+_stats_mode = [0]
+_bn_parts = {}  # id(y) -> (weakref(y), parts [2][P][C] fp32, P, rows per slab)
+
+
+class fused_bn_stats:
+    """Context: forward convolutions also emit batch-norm slab statistics of their outputs."""
+
+    def __enter__(self):
+        _stats_mode[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _stats_mode[0] -= 1
+        if _stats_mode[0] == 0:
+            _bn_parts.clear()
+        return False
+
+
+def _want_stats(b):
+    return _stats_mode[0] > 0 and b is None and _stats_enabled
+
+
+_stats_enabled = os.environ.get('PADDLE_AMD_CONV_BN_STATS', '1') != '0'
+
+
+def _stash_parts(y, parts, P, rpb):
+    import weakref
+    for k in [k for k, v in _bn_parts.items() if v[0]() is None]:
+        del _bn_parts[k]
+    _bn_parts[id(y)] = (weakref.ref(y), parts, P, rpb)
+
+
+def take_bn_parts(x):
+    """(parts, P, rows per slab) of a tensor produced under fused_bn_stats(), or None."""
+    e = _bn_parts.pop(id(x), None)
+    if e is None or e[0]() is not x:
+        return None
+    return e[1], e[2], e[3]
+
+
 def _fwd_packed(x, wpk, b, stride, pad, dil):
     """x: [N,H,W,C] bf16, wpk: packed [Cout][R][S][C] -> y [N,Ho,Wo,Cout]."""
     x = x.contiguous()
@@ -77,6 +126,15 @@ def _fwd_packed(x, wpk, b, stride, pad, dil):
     Cout, R, S, _ = wpk.shape
     Ho, Wo = _out_hw(H, W, R, S, stride, pad, dil)
     y = torch.empty(Nb, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
+    if _want_stats(b):
+        rpb = int(N.lib.pa_conv2d_fwd_stat_rows(Cout))
+        P = -(-(Nb * Ho * Wo) // rpb)
+        parts = torch.empty(2 * P * Cout, dtype=torch.float32, device=x.device)
+        N.check(N.lib.pa_conv2d_fwd_stats(N.ptr(x), N.ptr(wpk), N.ptr(y), N.ptr(parts), Nb, H, W, C, Cout, R, S,
+                                          stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], Ho, Wo, N.stream()),
+                'conv2d_fwd_stats')
+        _stash_parts(y, parts, P, rpb)
+        return y
     bb = b.to(torch.bfloat16).contiguous() if b is not None else None
     N.check(N.lib.pa_conv2d_fwd(N.ptr(x), N.ptr(wpk), N.ptr(y), N.ptr(bb), Nb, H, W, C, Cout, R, S, stride[0],
                                 stride[1], pad[0], pad[1], dil[0], dil[1], Ho, Wo, N.stream()), 'conv2d_fwd')
@@ -86,6 +144,39 @@ def _fwd_packed(x, wpk, b, stride, pad, dil):
 def conv2d_fwd(x, w, b, stride, pad, dil):
     """x: [N,H,W,C] bf16 (NHWC), w: [Cout,C,R,S] (paddle OIHW) -> y [N,Ho,Wo,Cout]."""
     return _fwd_packed(x, _packed(w), b, stride, pad, dil)
+
+
+_im2col_fwd = os.environ.get('PADDLE_AMD_CONV_IM2COL', '1') != '0'
+
+
+def im2col_ok(x, w):
+    """Few-channel convolutions (the RGB stem): im2col + a 1x1 convolution on the MFMA kernel."""
+    Cout, C, R, S = w.shape
+    return _im2col_fwd and C % 32 != 0 and R * S * C <= 1024 and Cout % 8 == 0
+
+
+def conv2d_fwd_im2col(x, w, b, stride, pad, dil):
+    """y = conv(x, w) as im2col(x) [M, Kp] (Kp = R*S*C rounded up to 64, zero columns) times the
+    [Cout][Kp] filter image, the second step being a 1 x 1 convolution on conv_fwd_kernel (so the
+    batch-norm statistics epilogue applies as for any other forward)."""
+    x = x.contiguous()
+    Nb, H, W, C = x.shape
+    Cout, _, R, S = w.shape
+    Ho, Wo = _out_hw(H, W, R, S, stride, pad, dil)
+    K = R * S * C
+    Kp = -(-K // 64) * 64
+    M = Nb * Ho * Wo
+    cols = torch.empty(M, Kp, dtype=torch.bfloat16, device=x.device)
+    N.check(N.lib.pa_im2col_nhwc(N.ptr(x), N.ptr(cols), Nb, H, W, C, R, S, stride[0], stride[1], pad[0], pad[1],
+                                 dil[0], dil[1], Ho, Wo, Kp, N.stream()), 'im2col_nhwc')
+    wpk = torch.zeros(Cout, 1, 1, Kp, dtype=torch.bfloat16, device=x.device)
+    wpk[:, 0, 0, :K] = w.detach().permute(0, 2, 3, 1).reshape(Cout, K)
+    y4 = _fwd_packed(cols.view(1, M, 1, Kp), wpk, b, (1, 1), (0, 0), (1, 1))
+    y = y4.view(Nb, Ho, Wo, Cout)
+    e = take_bn_parts(y4)
+    if e is not None:  # statistics were stashed under the [1, M, 1, Cout] output: re-key them to y
+        _stash_parts(y, *e)
+    return y
 
 
 def conv2d_dgrad(dy, w, x_hw, pad, dil):
@@ -242,6 +333,11 @@ def _gemm_fwd_1x1(x, w, b):
     bb = b.to(torch.bfloat16).contiguous() if b is not None else None
     if not gemm.hip_mm_ok(x2, wt):
         return None
+    if _want_stats(b) and gemm.epi_ok(x2, wt, Cout):
+        y, parts, P = gemm.mm_bn_stats(x2, wt)
+        y = y.view(*x.shape[:3], Cout)
+        _stash_parts(y, parts, P, 128)
+        return y
     return gemm.hip_mm(x2, wt, bias=bb).view(*x.shape[:3], Cout)
 
 
@@ -341,6 +437,8 @@ class _Conv2dNHWC(torch.autograd.Function):
                 return y
         if fwd_ok(w):
             return conv2d_fwd(x, w, b, stride, pad, dil)
+        if im2col_ok(x, w) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
+            return conv2d_fwd_im2col(x, w, b, stride, pad, dil)
         return _lib_conv_fwd(x, w, b, stride, pad, dil)
 
     @staticmethod

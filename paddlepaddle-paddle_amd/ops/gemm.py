@@ -108,6 +108,20 @@ def mm_epi(a, b, epi, aux, bias=None, out=None, colsum_part=None):
     return out
 
 
+def mm_bn_stats(a, b):
+    """out = a @ b on the fused-epilogue GEMM (epi 5) plus the batch-norm column statistics of
+    every 128-row slab of out: returns (out, parts fp32 [2][P][N] (slab means, then M2s), P)."""
+    tb, ldb = _op_layout(b)
+    M, K = a.shape
+    N_ = b.shape[1]
+    out = torch.empty(M, N_, dtype=torch.bfloat16, device=a.device)
+    P = -(-M // 128)
+    parts = torch.empty(2 * P * N_, dtype=torch.float32, device=a.device)
+    N.check(N.lib.pa_gemm8_bf16_epi(N.ptr(a), N.ptr(b), N.ptr(out), None, N.ptr(parts), M, N_, K, a.stride(0),
+                                    ldb, N_, tb, 1.0, 5, N.stream()), 'gemm_epi5')
+    return out, parts, P
+
+
 def _splitk_for(M, N_, K):
     """Split-K factor for outputs with too few 256x256 tiles to fill 256 CUs (the 2048x2048
     out-projection weight gradient: 64 tiles x 4 slices, profiles/r2_gemm_sched.log)."""

@@ -4,6 +4,8 @@ Same sublayer names as the reference (conv1/bn1/layer1..4/fc, blocks conv1..3/bn
 so reference checkpoints map 1:1.  ``data_format='NHWC'`` keeps activations channels-last, the
 layout MIOpen's fast convolution paths want on CDNA.
 """
+from contextlib import nullcontext as _nullctx
+
 from ... import nn
 from ... import ops
 from ...core.tensor import _wrap, _unwrap
@@ -145,8 +147,11 @@ class ResNet(nn.Layer):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        # every convolution here feeds a batch norm: in training, the conv epilogues also emit the
+        # norm's batch statistics (ops.conv.fused_bn_stats), so the norms skip their statistics pass
+        with ops.conv.fused_bn_stats() if self.training else _nullctx():
+            x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+            x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if self.with_pool:
             x = self.avgpool(x)
         if self.num_classes > 0:

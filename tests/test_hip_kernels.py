@@ -666,6 +666,151 @@ def test_batchnorm_nhwc_fused(dt, shape, mode):
         _close(z.grad, zr.grad, tol * 2, 1e-2, 'bn dz')
 
 
+# ---- batch-norm statistics from the conv / GEMM epilogue (ops.conv.fused_bn_stats) ----
+
+def _slab_ref(y2, rpb):
+    """(means, M2s) [P, C] of every rpb-row slab of y2 [M, C] (fp64 reference)."""
+    M, C = y2.shape
+    P = -(-M // rpb)
+    pad = P * rpb - M
+    yd = y2.double()
+    means, m2s = [], []
+    for p in range(P):
+        blk = yd[p * rpb:min(M, (p + 1) * rpb)]
+        mu = blk.mean(0)
+        means.append(mu)
+        m2s.append(((blk - mu) ** 2).sum(0))
+    return torch.stack(means), torch.stack(m2s)
+
+
+@pytest.mark.parametrize("shape,cout,k,stride", [((4, 14, 14, 64), 64, 3, 1), ((2, 28, 28, 128), 128, 3, 2),
+                                                 ((2, 9, 9, 256), 256, 3, 1), ((3, 7, 7, 64), 256, 1, 2)])
+def test_conv_fwd_bn_stats_parts(shape, cout, k, stride):
+    """pa_conv2d_fwd_stats: the output equals the plain forward bitwise; the slab (mean, M2) of
+    the epilogue match an fp64 reference over the fp32 products (rows per slab from the launcher)."""
+    from paddle.ops import conv
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(*shape, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(cout, shape[-1], k, k, device=DEV, generator=g) * 0.05).to(torch.bfloat16)
+    pad = (k // 2, k // 2)
+    y0 = conv.conv2d_fwd(x, w, None, (stride, stride), pad, (1, 1))
+    with conv.fused_bn_stats():
+        y1 = conv.conv2d_fwd(x, w, None, (stride, stride), pad, (1, 1))
+        parts = conv.take_bn_parts(y1)
+    assert parts is not None
+    pbuf, P, rpb = parts
+    assert torch.equal(y0, y1)
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float(), None, stride, pad).permute(0, 2, 3, 1)
+    y2 = ref.reshape(-1, cout)
+    rm, rq = _slab_ref(y2, rpb)
+    assert P == rm.shape[0]
+    pm = pbuf[:P * cout].view(P, cout).double()
+    pq = pbuf[P * cout:].view(P, cout).double()
+    _close(pm, rm, 2e-3, 2e-3, 'slab means')
+    _close(pq, rq, 2e-2 * rpb ** 0.5, 2e-3, 'slab M2')
+
+
+@pytest.mark.parametrize("shape,cout,k,stride,pad", [((4, 32, 32, 3), 64, 7, 2, 3), ((2, 17, 19, 3), 64, 7, 2, 3),
+                                                     ((2, 16, 16, 5), 32, 3, 1, 1)])
+def test_conv_stem_im2col(shape, cout, k, stride, pad):
+    """Few-channel (RGB stem) forward: pa_im2col_nhwc + the 1x1 MFMA convolution == fp32 conv; its
+    batch-norm slab statistics are re-keyed to the NHWC output."""
+    from paddle.ops import conv
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randn(*shape, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(cout, shape[-1], k, k, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float(), None, stride, pad).permute(0, 2, 3, 1)
+    y = conv.conv2d_fwd_im2col(x, w, None, (stride, stride), (pad, pad), (1, 1))
+    _close(y.float(), ref, 3e-2, 1e-2, 'stem conv')
+    with conv.fused_bn_stats():
+        y2 = conv.conv2d_fwd_im2col(x, w, None, (stride, stride), (pad, pad), (1, 1))
+        parts = conv.take_bn_parts(y2)
+    assert parts is not None and torch.equal(y, y2)
+    pbuf, P, rpb = parts
+    rm, _ = _slab_ref(ref.reshape(-1, cout), rpb)
+    _close(pbuf[:P * cout].view(P, cout).double(), rm, 3e-3, 3e-3, 'stem slab means')
+
+
+@pytest.mark.parametrize("M,C,N", [(1024, 256, 512), (328, 128, 256), (2048, 512, 2048)])
+def test_gemm_epi5_bn_stats(M, C, N):
+    """csrc/gemm8.hip epi 5: C = A @ B^T bitwise-equal to the plain GEMM, 128-row slab statistics
+    vs an fp64 reference."""
+    from paddle.ops import gemm
+    g = torch.Generator(device=DEV).manual_seed(5)
+    a = torch.randn(M, C, device=DEV, generator=g).to(torch.bfloat16)
+    wt = (torch.randn(N, C, device=DEV, generator=g) * 0.05).to(torch.bfloat16)
+    b = wt.t()
+    y0 = gemm.hip_mm(a, b)
+    y1, parts, P = gemm.mm_bn_stats(a, b)
+    assert torch.equal(y0, y1)
+    rm, rq = _slab_ref(a.float() @ b.float(), 128)
+    _close(parts[:P * N].view(P, N).double(), rm, 2e-3, 2e-3, 'slab means')
+    _close(parts[P * N:].view(P, N).double(), rq, 2e-2 * 128 ** 0.5, 2e-3, 'slab M2')
+
+
+@pytest.mark.parametrize("rows_per_slab,P", [(64, 700), (128, 98), (64, 12544 // 16)])
+def test_bn_fwd_from_parts_matches_stats_pass(rows_per_slab, P):
+    """pa_bn_fwd_parts (merge + finish + apply from slab statistics) == the statistics-pass forward."""
+    from paddle.ops import batchnorm, conv
+    C = 128
+    rows = rows_per_slab * P - 7  # short last slab
+    g = torch.Generator(device=DEV).manual_seed(7)
+    x = (torch.randn(rows, C, device=DEV, generator=g) * 3 + 1).to(torch.bfloat16)
+    gam = 1 + 0.1 * torch.randn(C, device=DEV, generator=g)
+    bet = 0.1 * torch.randn(C, device=DEV, generator=g)
+    m, q = _slab_ref(x.float(), rows_per_slab)
+    parts = torch.cat([m.float().reshape(-1), q.float().reshape(-1)])
+    outs = []
+    for use_parts in (False, True):
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        if use_parts:
+            conv._stash_parts(x, parts, P, rows_per_slab)
+        y = batchnorm.bn_act_nhwc(x, gam, bet, rm, rv, 1e-5, 0.9, True, True)
+        outs.append((y.float(), rm, rv))
+    (y0, m0, v0), (y1, m1, v1) = outs
+    _close(y1, y0, 2e-2, 1e-2, 'bn y')
+    _close(m1, m0, 1e-4, 1e-4, 'running mean')
+    _close(v1, v0, 1e-4, 1e-4, 'running var')
+
+
+def test_resnet_fused_bn_stats_matches_unfused(monkeypatch):
+    """ResNet50 NHWC bf16 O2 forward+backward with the conv/GEMM-epilogue statistics == the
+    statistics-pass path (loss, a conv weight gradient, running stats), and the epilogue path is
+    really taken (every conv under the model feeds its BN its slab statistics)."""
+    import paddle
+    from paddle.vision.models import resnet50
+    from paddle.ops import conv
+    paddle.set_device('gpu:0')
+    taken = []
+    orig = conv.take_bn_parts
+
+    def spy(x):
+        r = orig(x)
+        taken.append(r is not None)
+        return r
+    monkeypatch.setattr(conv, 'take_bn_parts', spy)
+    res = []
+    for on in (False, True):
+        monkeypatch.setattr(conv, '_stats_enabled', on)
+        paddle.seed(0)
+        model = resnet50(data_format='NHWC', num_classes=10)
+        model = paddle.amp.decorate(model, level='O2', dtype='bfloat16')
+        g = torch.Generator(device=DEV).manual_seed(1)
+        img = paddle.to_tensor(torch.randn(16, 64, 64, 3, device=DEV, generator=g).to(torch.bfloat16))
+        lab = paddle.to_tensor(torch.randint(0, 10, (16,), device=DEV, generator=g))
+        taken.clear()
+        loss = paddle.nn.functional.cross_entropy(model(img), lab)
+        loss.backward()
+        w = model.layer2[0].conv2.weight
+        res.append((float(loss), w.grad._t.float().clone(), model.layer3[1].bn2._mean._t.float().clone()))
+        if on:
+            assert sum(taken) >= 52, (sum(taken), len(taken))  # all but the 3-channel stem
+    (l0, g0, m0), (l1, g1, m1) = res
+    assert abs(l0 - l1) < 2e-2 * max(1.0, abs(l0)), (l0, l1)
+    _close(m1, m0, 2e-2, 2e-2, 'running mean')
+    assert torch.nn.functional.cosine_similarity(g0.reshape(1, -1), g1.reshape(1, -1)).item() > 0.98
+
+
 def test_resnet50_nhwc_train_step_uses_fused_bn():
     """ResNet50 (NHWC) trains through the fused HIP batch-norm: every BN layer takes the kernel,
     fp32 loss decreases; bf16 O2 steps stay finite (a random-init 50-layer net at batch 8 is too
