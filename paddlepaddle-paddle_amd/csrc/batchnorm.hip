@@ -217,15 +217,16 @@ __global__ __launch_bounds__(1024) void stats_finish(const float* __restrict__ p
 // ---- Chan merge of G consecutive slab statistics (mean, M2 over rpb rows each, the last slab of
 // all P possibly short) into one (mean, M2) per group of G slabs: the epilogue-produced statistics
 // of a convolution / GEMM (thousands of 64-128-row slabs) brought down to a few hundred chunks
-// of G * rpb rows for stats_finish.  grid (ceil(cols / 256), ceil(P / G)), one column per thread.
+// of G * rpb rows for stats_finish.  grid (ceil(cols / blockDim), ceil(P / G)), one column per thread.
 __global__ __launch_bounds__(256) void stats_merge(const float* __restrict__ pmean, const float* __restrict__ pm2,
                                                    int P, int rows, int rpb, int cols, int G,
                                                    float* __restrict__ omean, float* __restrict__ om2, int P2) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= cols) return;
   const int p0 = blockIdx.y * G, p1 = min(P, p0 + G);
   const float nfull = (float)rpb, nlast = (float)(rows - (P - 1) * rpb);
   float n = 0.f, s = 0.f;
+#pragma unroll 8
   for (int p = p0; p < p1; ++p) {
     const float np = p == P - 1 ? nlast : nfull;
     s += np * pmean[(size_t)p * cols + c];
@@ -233,6 +234,7 @@ __global__ __launch_bounds__(256) void stats_merge(const float* __restrict__ pme
   }
   const float mu = s / n;
   float m2 = 0.f;
+#pragma unroll 8
   for (int p = p0; p < p1; ++p) {
     const float np = p == P - 1 ? nlast : nfull;
     const float d = pmean[(size_t)p * cols + c] - mu;
@@ -525,7 +527,8 @@ hipError_t fwd_parts(const void* x, const void* z, const void* gamma, const void
   if (P > 512) {  // merge groups of G slabs first (the finisher's per-lane loop is serial)
     const int G = (P + 511) / 512;
     const int P2 = (P + G - 1) / G;
-    stats_merge<<<dim3((cols + 255) / 256, P2), 256, 0, st>>>(pm, pq, P, rows, prpb, cols, G, ws,
+    const int bt = cols >= 256 ? 256 : (cols + 63) / 64 * 64;  // narrow rows: one wave per block
+    stats_merge<<<dim3((cols + bt - 1) / bt, P2), bt, 0, st>>>(pm, pq, P, rows, prpb, cols, G, ws,
                                                                ws + (size_t)P2 * cols, P2);
     pm = ws;
     pq = ws + (size_t)P2 * cols;

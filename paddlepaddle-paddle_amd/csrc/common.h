@@ -87,12 +87,23 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return r;
 }
 
+// Sum over the 16 lanes of a DPP row (lanes 16k .. 16k+15), result in every lane of the row: DPP
+// quad_perm xor 1 / xor 2, then row_half_mirror and row_mirror (once a quad / half-row holds one
+// value in every lane, mirroring adds the other quad / half): VALU only, no LDS crossbar traffic.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, true));
+  return v;
+}
+
 // Per-column batch-norm statistics of one wave's output slab, computed in the producing GEMM /
 // convolution epilogue (fused_bn statistics: the standalone column pass over the activation is
 // skipped).  Swapped-MFMA layout: the lane holds rows 16 i + (lane & 15) (i < FM) of columns
 // 16 j + 4 (lane >> 4) + e (j < FN, e < 4) in acc[i][j][e]; rows at or past `nvalid` are excluded.
 // Two-pass in registers (sum -> mean -> sum of squared deviations: no E[x^2] - E[x]^2
-// cancellation), each pass reduced over the 16 lanes of a column group by xor shuffles.  The
+// cancellation), each pass reduced over the 16 lanes of a column group by DPP (row16_sum).  The
 // slab's (mean, M2) over its nvalid rows go to pmean[col], pm2[col] (lanes with lane & 15 == 0;
 // cols >= ncols skipped, ncols % 4 == 0).  `add` (nullable, 4 FN values per lane, e.g. the bias)
 // is added to every value first.
@@ -113,9 +124,7 @@ __device__ __forceinline__ void wave_col_stats(const V (&acc)[FM][FN], const flo
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) s[e] += __shfl_xor(s[e], o, 64);
-      s[e] *= inv_n;  // the slab mean, in every lane of the group
+      s[e] = row16_sum(s[e]) * inv_n;  // the slab mean, in every lane of the group
     }
     float q[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -128,9 +137,7 @@ __device__ __forceinline__ void wave_col_stats(const V (&acc)[FM][FN], const flo
       }
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) q[e] += __shfl_xor(q[e], o, 64);
+    for (int e = 0; e < 4; ++e) q[e] = row16_sum(q[e]);
     const int c = col0 + 16 * j + 4 * (lane >> 4);
     if (r16 == 0 && c < ncols) {
       *reinterpret_cast<float4*>(pmean + c) = make_float4(s[0], s[1], s[2], s[3]);

@@ -36,6 +36,7 @@ __device__ uint4 g_zero16[4];
 
 struct Geom {
   int N, H, W, C, Ho, Wo, Cout, R, S, sh, sw, ph, pw, dh, dw;
+  long long total;  // input elements (im2col bounds; 0 elsewhere)
 };
 
 // Filter taps of the implicit GEMM (k = (tap, c)): input row/col offsets of each tap, so a kernel
@@ -786,50 +787,100 @@ static void launch_wgrad_kernel(int BN, dim3 grid, const uint16_t* xp, const uin
 // (splits + ceil(splits / 16)) * R*S*C * Cout floats (splits = pa_conv2d_wgrad_splits), dw: bf16 [Cout][C][R][S]
 // (accumulate != 0: dw += the gradient, in place).  C % 8 == 0, Cout % 8 == 0, kchunk % 32 == 0.
 // im2col of an NHWC input for convolutions whose channel count the implicit-GEMM kernel does not
-// take (the 3-channel RGB stem): out [M = N*Ho*Wo][Kp] bf16, k = (r, s, c) with c fastest, zeros for
-// taps in the padding and for k >= R*S*C (Kp % 8 == 0).  One 16-B store per thread; the input
-// rows it gathers from stay in L2 across the neighbouring output pixels.  The convolution is then
-// a 1 x 1 convolution of this matrix on conv_fwd_kernel.
-__global__ __launch_bounds__(256) void im2col_kernel(const uint16_t* __restrict__ X, uint16_t* __restrict__ out,
-                                                     Geom g, int M, int Kp) {
-  const int cpr = Kp >> 3;
-  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long m = t / cpr;
-  if (m >= M) return;
-  const int k0 = (int)(t - m * cpr) * 8;
-  const int HoWo = g.Ho * g.Wo;
-  const int n = (int)(m / HoWo), rem = (int)(m - (long long)n * HoWo);
-  const int ho = rem / g.Wo, wo = rem - ho * g.Wo;
-  const int KK = g.R * g.S * g.C;
+// take (the 3-channel RGB stem).  Row-segment layout: k = r * RK + s * C + c with RK = S*C rounded
+// up to 8, so each filter row's S*C taps are one contiguous run of the input (channels fastest,
+// then w) and one 16-B-aligned run of the output row; out [M = N*Ho*Wo][Kp] bf16, zeros for taps
+// in the padding, for the RK - S*C slots of each filter row and for k >= R*RK (Kp % 8 == 0).  One
+// thread per 16-B output chunk, consecutive lanes on consecutive chunks (whole-row stores), 8
+// 2-byte gathers each with constant-divisor tap math (a thread per pixel writing 24 chunks at a
+// 384-B lane stride measured 0.81 ms on the ResNet50 stem; per-element runtime divisions 1.24 ms).
+// The convolution is then a 1 x 1 convolution of this matrix on conv_fwd_kernel with the filter
+// packed in the same k order.
+template <int S, int C>
+__global__ __launch_bounds__(256) void im2col_rows_kernel(const uint16_t* __restrict__ X, uint16_t* __restrict__ out,
+                                                          Geom g, int M, int Kp) {
+  constexpr int SC = S * C, RK = (SC + 7) / 8 * 8, CPR = RK / 8;  // 16-B chunks per filter row
+  const int cpo = Kp >> 3;                                         // 16-B chunks per output row
+  // 32-bit index math (host: M * Kp / 8 < 2^31): 64-bit divisions are software sequences of ~150
+  // instructions, which made this gather kernel VALU-bound
+  const unsigned t = blockIdx.x * 256u + threadIdx.x;  // consecutive lanes: consecutive chunks
+  const unsigned m = t / (unsigned)cpo;
+  if (m >= (unsigned)M) return;
+  const int q = (int)(t - m * (unsigned)cpo);
+  const int r = q / CPR, t0 = (q - r * CPR) * 8;
   uint16_t v[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int k = k0 + e;
-    uint16_t val = 0;
-    if (k < KK) {
-      const int c = k % g.C, rs = k / g.C;
-      const int q = rs % g.S, r = rs / g.S;
-      const int hi = ho * g.sh - g.ph + r * g.dh, wi = wo * g.sw - g.pw + q * g.dw;
-      if ((unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W)
-        val = X[(((long long)n * g.H + hi) * g.W + wi) * g.C + c];
+  for (int e = 0; e < 8; ++e) v[e] = 0;
+  if (r < g.R) {
+    const unsigned HoWo = (unsigned)(g.Ho * g.Wo);
+    const unsigned n = m / HoWo, rem = m - n * HoWo;
+    const int ho = (int)(rem / (unsigned)g.Wo), wo = (int)rem - ho * g.Wo;
+    const int hi = ho * g.sh - g.ph + r * g.dh;
+    if ((unsigned)hi < (unsigned)g.H) {
+      const long long row0 = ((long long)n * g.H + hi) * g.W * C;  // element index of the input row
+      const int wi0 = wo * g.sw - g.pw;
+      // with unit dilation the S*C taps of a filter row are ONE contiguous run of the input row, so
+      // a chunk's 8 values are 8 consecutive elements: two aligned 16-B loads + a 2-byte-granular
+      // funnel shift instead of 8 scattered 2-byte gathers (which were TA-bound)
+      const long long b0 = row0 + (long long)wi0 * C + t0;
+      const long long a0 = b0 >= 0 ? (b0 & ~7LL) : -1;
+      if (g.dw == 1 && a0 >= 0 && a0 + 16 <= g.total) {
+        const uint4 lo = *reinterpret_cast<const uint4*>(X + a0);
+        const uint4 hi4 = *reinterpret_cast<const uint4*>(X + a0 + 8);
+        const unsigned w[8] = {lo.x, lo.y, lo.z, lo.w, hi4.x, hi4.y, hi4.z, hi4.w};
+        const int sh2 = (int)(b0 - a0) * 2;  // byte shift 0..14
+        const int wq = sh2 >> 2, bq = sh2 & 3;
+        unsigned o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          // words wq + j and wq + j + 1 of the window (wq <= 3): 4-way selects, no dynamic indexing
+          const unsigned x0 = wq == 0 ? w[j] : wq == 1 ? w[j + 1] : wq == 2 ? w[j + 2] : w[j + 3];
+          const unsigned x1 = wq == 0 ? w[j + 1] : wq == 1 ? w[j + 2] : wq == 2 ? w[j + 3] : w[j + 4];
+          o[j] = __builtin_amdgcn_alignbyte(x1, x0, bq);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int tt = t0 + e;
+          const int wi = wi0 + tt / C;
+          const uint16_t val = (uint16_t)(o[e >> 1] >> ((e & 1) * 16));
+          v[e] = (tt < SC && (unsigned)wi < (unsigned)g.W) ? val : 0;
+        }
+      } else {
+        const uint16_t* xr = X + row0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int tt = t0 + e;  // (s, c) = (tt / C, tt % C): constant divisors
+          const int sidx = tt / C, c = tt - sidx * C;
+          const int wi = wi0 + sidx * g.dw;
+          if (tt < SC && (unsigned)wi < (unsigned)g.W) v[e] = xr[(long long)wi * C + c];
+        }
+      }
     }
-    v[e] = val;
   }
   uint4 pk;
   pk.x = v[0] | ((unsigned)v[1] << 16);
   pk.y = v[2] | ((unsigned)v[3] << 16);
   pk.z = v[4] | ((unsigned)v[5] << 16);
   pk.w = v[6] | ((unsigned)v[7] << 16);
-  *reinterpret_cast<uint4*>(out + m * Kp + k0) = pk;
+  *reinterpret_cast<uint4*>(out + (long long)m * Kp + q * 8) = pk;
 }
+
+// returns hipErrorInvalidValue for (S, C) pairs without an instantiation (the caller falls back)
+PA_API int pa_im2col_rows_ok(int S, int C) { return (S == 7 && C == 3) || (S == 3 && C == 3) || (S == 3 && C == 5); }
 
 PA_API int pa_im2col_nhwc(const void* x, void* out, int N, int H, int W, int C, int R, int S, int sh, int sw, int ph,
                           int pw, int dh, int dw, int Ho, int Wo, int Kp, hipStream_t st) {
   const long long M = (long long)N * Ho * Wo;
-  if (M <= 0 || M > (1LL << 30) || Kp % 8 || Kp < R * S * C || C <= 0) return (int)hipErrorInvalidValue;
-  Geom g{N, H, W, C, Ho, Wo, 0, R, S, sh, sw, ph, pw, dh, dw};
-  const long long threads = M * (Kp / 8);
-  im2col_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, st>>>((const uint16_t*)x, (uint16_t*)out, g, (int)M, Kp);
+  const int RK = (S * C + 7) / 8 * 8;
+  if (M <= 0 || M * (Kp / 8) >= (1LL << 31) || Kp % 8 || Kp < R * RK || C <= 0 || !pa_im2col_rows_ok(S, C))
+    return (int)hipErrorInvalidValue;
+  Geom g{N, H, W, C, Ho, Wo, 0, R, S, sh, sw, ph, pw, dh, dw, (long long)N * H * W * C};
+  const unsigned blocks = (unsigned)((M * (Kp / 8) + 255) / 256);
+  const uint16_t* xp = (const uint16_t*)x;
+  uint16_t* op = (uint16_t*)out;
+  if (S == 7 && C == 3) im2col_rows_kernel<7, 3><<<blocks, 256, 0, st>>>(xp, op, g, (int)M, Kp);
+  else if (S == 3 && C == 3) im2col_rows_kernel<3, 3><<<blocks, 256, 0, st>>>(xp, op, g, (int)M, Kp);
+  else im2col_rows_kernel<3, 5><<<blocks, 256, 0, st>>>(xp, op, g, (int)M, Kp);
   return (int)hipGetLastError();
 }
 

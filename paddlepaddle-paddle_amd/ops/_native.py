@@ -72,6 +72,7 @@ _SIGS = {
     'pa_conv2d_fwd_stats': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
     'pa_conv2d_fwd_stat_rows': [I],
     'pa_im2col_nhwc': [P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
+    'pa_im2col_rows_ok': [I, I],
     'pa_conv2d_wgrad_ok': [I, I],
     'pa_conv2d_dgrad_classes': [P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     'pa_conv2d_wgrad': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],

@@ -3,8 +3,9 @@
 Reference: paddle/phi/kernels/gpudnn/conv_kernel.cu (forward), conv_grad_kernel.cu (backward).
 * Forward: im2col folded into the LDS-DMA source addresses, zero padding via a zero block, bias
   fused; the weight is packed into the [Cout][R][S][C] k-contiguous image the kernel stages
-  (re-packed per call).  Needs C % 32 == 0; few-channel inputs (the 3-channel RGB stem) go
-  through an explicit im2col matrix (pa_im2col_nhwc, K padded to 64) and a 1x1 convolution.
+  (re-packed per call).  Needs C % 32 == 0; the 3-channel RGB stem forward stays on the storage
+  layer's direct convolution (an explicit im2col + 1x1 MFMA path, pa_im2col_nhwc, is available
+  behind PADDLE_AMD_CONV_IM2COL=1 but measured slower there).
 * Batch-norm statistics (fused_bn_stats): the forward epilogue can also emit per-slab channel
   (mean, M2) for the batch norm that consumes the output (ops/batchnorm.py).
 * Data gradient (any stride): stride classes of input pixels, each a stride-1 implicit GEMM over
@@ -146,31 +147,38 @@ def conv2d_fwd(x, w, b, stride, pad, dil):
     return _fwd_packed(x, _packed(w), b, stride, pad, dil)
 
 
-_im2col_fwd = os.environ.get('PADDLE_AMD_CONV_IM2COL', '1') != '0'
+# Off by default: on the ResNet50 stem (256 x 224 x 224 x 3, 7x7/2) the im2col matrix is
+# [3.2M, 192] = 1.23 GB written and read back; im2col 0.54 ms + the 1x1 conv 0.12 ms lose to the
+# library's direct convolution (0.36 ms): 8.23k vs 8.37k img/s (profiles/r3s3_im2col_ab.log).
+_im2col_fwd = os.environ.get('PADDLE_AMD_CONV_IM2COL', '0') != '0'
 
 
 def im2col_ok(x, w):
     """Few-channel convolutions (the RGB stem): im2col + a 1x1 convolution on the MFMA kernel."""
     Cout, C, R, S = w.shape
-    return _im2col_fwd and C % 32 != 0 and R * S * C <= 1024 and Cout % 8 == 0
+    return (_im2col_fwd and C % 32 != 0 and Cout % 8 == 0 and N.lib is not None
+            and bool(N.lib.pa_im2col_rows_ok(S, C)))
 
 
 def conv2d_fwd_im2col(x, w, b, stride, pad, dil):
-    """y = conv(x, w) as im2col(x) [M, Kp] (Kp = R*S*C rounded up to 64, zero columns) times the
-    [Cout][Kp] filter image, the second step being a 1 x 1 convolution on conv_fwd_kernel (so the
-    batch-norm statistics epilogue applies as for any other forward)."""
+    """y = conv(x, w) as im2col(x) [M, Kp] times the [Cout][Kp] filter image, the second step a
+    1 x 1 convolution on conv_fwd_kernel (so the batch-norm statistics epilogue applies as for
+    any other forward).  k = r * RK + s * C + c (RK = S*C rounded up to 8: each filter row one
+    contiguous input run and one aligned output run), Kp = R*RK rounded up to 64, zero slots."""
     x = x.contiguous()
     Nb, H, W, C = x.shape
     Cout, _, R, S = w.shape
     Ho, Wo = _out_hw(H, W, R, S, stride, pad, dil)
-    K = R * S * C
-    Kp = -(-K // 64) * 64
+    RK = -(-(S * C) // 8) * 8
+    Kp = -(-(R * RK) // 64) * 64
     M = Nb * Ho * Wo
     cols = torch.empty(M, Kp, dtype=torch.bfloat16, device=x.device)
     N.check(N.lib.pa_im2col_nhwc(N.ptr(x), N.ptr(cols), Nb, H, W, C, R, S, stride[0], stride[1], pad[0], pad[1],
                                  dil[0], dil[1], Ho, Wo, Kp, N.stream()), 'im2col_nhwc')
+    wimg = torch.zeros(Cout, R, RK, dtype=torch.bfloat16, device=x.device)
+    wimg[:, :, :S * C] = w.detach().permute(0, 2, 3, 1).reshape(Cout, R, S * C)
     wpk = torch.zeros(Cout, 1, 1, Kp, dtype=torch.bfloat16, device=x.device)
-    wpk[:, 0, 0, :K] = w.detach().permute(0, 2, 3, 1).reshape(Cout, K)
+    wpk[:, 0, 0, :R * RK] = wimg.reshape(Cout, R * RK)
     y4 = _fwd_packed(cols.view(1, M, 1, Kp), wpk, b, (1, 1), (0, 0), (1, 1))
     y = y4.view(Nb, Ho, Wo, Cout)
     e = take_bn_parts(y4)
