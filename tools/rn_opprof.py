@@ -10,7 +10,7 @@ import torch
 
 def main():
     import bench
-    args = types.SimpleNamespace(resnet_batch=int(os.environ.get('RN_BATCH', '256')))
+    args = types.SimpleNamespace(resnet_batch=int(os.environ.get('RN_BATCH', '256')), resnet_model='resnet50')
     dev = torch.device('cuda', 0)
     import paddle
     paddle.set_device('gpu:0')
