@@ -39,8 +39,8 @@ def parse():
                          '--model gpt-tiny --resnet-model resnet18; the numbers mean nothing')
     ap.add_argument('--resnet-model', default='resnet50', help=argparse.SUPPRESS)
     ap.add_argument('--graph', action='store_true',
-                    help='replay the whole training step as one captured hipGraph (steps without dropout; '
-                         'device/cuda/graphs.py TrainStepGraph)')
+                    help='replay the whole training step as one captured hipGraph (dropout re-randomised per '
+                         'replay by a device generation counter; device/cuda/graphs.py TrainStepGraph)')
     return ap.parse_args()
 
 
@@ -121,8 +121,6 @@ def _maybe_graph(args, step, cfg):
     """--graph: the step as one captured hipGraph, captured inside the untimed warmup."""
     if not args.graph or args.warmup < 2:
         return step
-    if cfg.get('hidden_dropout', 0) or cfg.get('attention_dropout', 0):
-        return step  # host-drawn dropout seeds cannot be frozen into a graph
     from paddle.device.cuda.graphs import capture_train_step
     cfg['hip_graph'] = True
     return capture_train_step(step, warmup=args.warmup - 1)

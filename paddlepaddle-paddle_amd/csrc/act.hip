@@ -245,6 +245,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void dropout_add_fwd(const T* __restrict__ x, const T* __restrict__ residual,
                                                        T* __restrict__ y, long long n, float p, uint32_t seed,
                                                        uint32_t offset) {
+  seed = rng_mix(seed);  // graph-captured steps: per-replay stream
   constexpr int E = 16 / sizeof(T);
   const float scale = 1.f / (1.f - p);
   const long long nv = n / E;
@@ -279,6 +280,7 @@ __global__ __launch_bounds__(256) void dropout_add_fwd(const T* __restrict__ x, 
 template <typename T>
 __global__ __launch_bounds__(256) void dropout_bwd(const T* __restrict__ dy, T* __restrict__ dx, long long n, float p,
                                                    uint32_t seed, uint32_t offset) {
+  seed = rng_mix(seed);  // graph-captured steps: per-replay stream
   constexpr int E = 16 / sizeof(T);
   const float scale = 1.f / (1.f - p);
   const long long nv = n / E;
@@ -497,4 +499,9 @@ PA_API hipError_t pa_colsum(const void* dy, float* part, void* out, int odt, int
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return launch_colsum_finish_dt(part, out, odt, (int)grid.y, cols, accum, st);
+}
+
+// graph-safe dropout streams (common.h rng_mix): generation counter of this module's kernels
+PA_API int pa_act_set_rng_gen(const void* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(pa::g_rng_gen), &p, sizeof(p));
 }

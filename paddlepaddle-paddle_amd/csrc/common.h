@@ -192,6 +192,18 @@ struct GeluTanh {
   }
 };
 
+// Graph-safe dropout streams: an optional device-resident generation counter mixed into every
+// dropout seed once at kernel entry.  Eager steps leave it unset (the seed as drawn on the host);
+// a captured training step (device/cuda/graphs.py TrainStepGraph) advances the counter as the
+// first node of every replay, so the host seeds frozen into the graph still give a fresh keep-mask
+// per step, and a step's backward regenerates its forward's masks (same counter value).  One
+// pointer per translation unit (static), set by that file's pa_*_set_rng_gen.
+static __constant__ const uint32_t* g_rng_gen = nullptr;
+__device__ __forceinline__ uint32_t rng_mix(uint32_t seed) {
+  const uint32_t* p = g_rng_gen;
+  return p ? seed ^ (*p * 0x9E3779B1u) : seed;
+}
+
 // Counter-based RNG (for dropout): a cheap stateless hash of (seed, offset, index) → uniform [0,1).
 __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
   // murmur3-style finaliser chain

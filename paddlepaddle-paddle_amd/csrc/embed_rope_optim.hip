@@ -77,7 +77,8 @@ __global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, T* _
 //   p *= (1 - lr * wd);  m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2
 //   p -= lr * sqrt(1-b2^t)/(1-b1^t) * m / (sqrt(v) + eps * sqrt(1-b2^t))
 // grad may be bf16/fp16/fp32; `lowp` (optional) receives the updated param in the model dtype.
-// lr/b1pow/b2pow are read from device scalars so a captured hipGraph replays with fresh values.
+// lr and (b1pow, b2pow) may be read from device scalars (lr_ptr, pows) so a captured hipGraph
+// replays with fresh values.
 typedef int nt_i4 __attribute__((ext_vector_type(4)));
 
 // 16-byte streaming (nontemporal: no reuse, keep the caches for the rest) load / store of N
@@ -151,7 +152,12 @@ __global__ __launch_bounds__(256) void adamw_scalar_kernel(float* __restrict__ p
                                                            P* __restrict__ lowp, long long n,
                                                            const float* __restrict__ lr_ptr, float lr_host, float b1,
                                                            float b2, float eps, float wd, float b1pow, float b2pow,
-                                                           const float* __restrict__ grad_scale) {
+                                                           const float* __restrict__ grad_scale,
+    const float* __restrict__ pows) {
+  if (pows != nullptr) {  // device-resident beta powers (graph-captured steps advance them)
+    b1pow = pows[0];
+    b2pow = pows[1];
+  }
   const float lr = lr_ptr != nullptr ? *lr_ptr : lr_host;
   const float gs = grad_scale != nullptr ? *grad_scale : 1.f;
   const float bc2 = sqrtf(1.f - b2pow);
@@ -179,7 +185,12 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
                                                     float* __restrict__ m, float* __restrict__ v, P* __restrict__ lowp,
                                                     long long n, const float* __restrict__ lr_ptr, float lr_host,
                                                     float b1, float b2, float eps, float wd, float b1pow, float b2pow,
-                                                    const float* __restrict__ grad_scale) {
+                                                    const float* __restrict__ grad_scale,
+    const float* __restrict__ pows) {
+  if (pows != nullptr) {  // device-resident beta powers (graph-captured steps advance them)
+    b1pow = pows[0];
+    b2pow = pows[1];
+  }
   const float lr = lr_ptr != nullptr ? *lr_ptr : lr_host;
   const float gs = grad_scale != nullptr ? *grad_scale : 1.f;
   const float bc2 = sqrtf(1.f - b2pow);
@@ -333,7 +344,7 @@ PA_API void pa_adamw_tune(int nt, int blocks_per_cu) {
 // gd = grad dtype, pd = low-precision param copy dtype (-1 = none)
 PA_API hipError_t pa_adamw(float* p, const void* g, float* m, float* v, void* lowp, long long n, const float* lr_ptr,
                            float lr, float b1, float b2, float eps, float wd, float b1pow, float b2pow,
-                           const float* grad_scale, int gd, int pd, hipStream_t st) {
+                           const float* grad_scale, const float* pows, int gd, int pd, hipStream_t st) {
   const int grid = grid_for(n / 16 + 1, 256, 256 * g_adamw_bpc);
   // every 8-element access is a 16-byte vector (or two): all five streams must be 16-byte aligned
   const bool aligned = ((((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g | (uintptr_t)lowp) & 15) == 0);
@@ -341,13 +352,13 @@ PA_API hipError_t pa_adamw(float* p, const void* g, float* m, float* v, void* lo
   do {                                                                                                         \
     if (aligned && g_adamw_nt)                                                                                 \
       adamw_kernel<G, P, true><<<grid, 256, 0, st>>>(p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1, b2, eps, \
-                                                     wd, b1pow, b2pow, grad_scale);                            \
+                                                     wd, b1pow, b2pow, grad_scale, pows);                      \
     else if (aligned)                                                                                          \
       adamw_kernel<G, P, false><<<grid, 256, 0, st>>>(p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1, b2,   \
-                                                      eps, wd, b1pow, b2pow, grad_scale);                      \
+                                                      eps, wd, b1pow, b2pow, grad_scale, pows);                \
     else                                                                                                       \
       adamw_scalar_kernel<G, P><<<grid_for(n, 256, 256 * 8), 256, 0, st>>>(                                    \
-          p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1, b2, eps, wd, b1pow, b2pow, grad_scale);          \
+          p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1, b2, eps, wd, b1pow, b2pow, grad_scale, pows);    \
   } while (0)
   if (pd < 0) lowp = nullptr;
   const int pp = pd < 0 ? 0 : pd;

@@ -294,6 +294,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
                                                      float* __restrict__ LSE, int Sq_, int Sk_, int Hq, int Hk,
                                                      Strides qs, Strides ks_, Strides vs, Strides os, float scale_log2,
                                                      Extra ex = Extra{}) {
+  if constexpr ((EXT & 4) != 0) ex.seed = rng_mix(ex.seed);  // graph-captured steps: per-replay stream
   constexpr int KS = D / 32;   // k-steps over head_dim
   constexpr int DB = D / 16;   // 16-wide d blocks
   constexpr int STAGE = 2 * 64 * D * 2;  // K and V of one key block
@@ -591,6 +592,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq_, int Sk_, int Hq, int Hk, Strides qs, Strides ks_,
     Strides vs, Strides dos, Strides dks, Strides dvs, float scale, Extra ex = Extra{}) {
+  if constexpr ((EXT & 4) != 0) ex.seed = rng_mix(ex.seed);  // graph-captured steps: per-replay stream
   constexpr int KS = D / 32;
   constexpr int DB = D / 16;
   // D = 128: tiles read both by rows (ds_read_b128) and by columns (tr_b16) use the chunk ^
@@ -844,6 +846,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     uint16_t* __restrict__ dQ, int Sq_, int Sk_, int Hq, int Hk, Strides qs, Strides ks_, Strides vs, Strides dos,
     Strides dqs, float scale, Extra ex = Extra{}) {
+  if constexpr ((EXT & 4) != 0) ex.seed = rng_mix(ex.seed);  // graph-captured steps: per-replay stream
   constexpr int KS = D / 32;
   constexpr int DB = D / 16;
   // D = 128: tiles read both by rows (ds_read_b128) and by columns (tr_b16) use the chunk ^
@@ -1301,4 +1304,9 @@ PA_API hipError_t pa_flash_bwd_ex(const void* q, const void* k, const void* v, c
     }
   });
   return hipGetLastError();
+}
+
+// graph-safe dropout streams (common.h rng_mix): generation counter of this module's kernels
+PA_API int pa_flash_set_rng_gen(const void* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(pa::g_rng_gen), &p, sizeof(p));
 }

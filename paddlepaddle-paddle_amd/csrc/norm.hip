@@ -43,6 +43,7 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const T* __restrict__ x, 
                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                        int rows, int cols, float eps, const T* __restrict__ xbias,
                                                        DropSpec dsp) {
+  dsp.seed = rng_mix(dsp.seed);  // graph-captured steps: per-replay stream
   constexpr int E = 16 / sizeof(T);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -177,6 +178,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dy,
                                                        float* __restrict__ db_part, int rows, int cols,
                                                        T* __restrict__ dxd, float* __restrict__ xb_part,
                                                        DropSpec dsp) {
+  dsp.seed = rng_mix(dsp.seed);  // graph-captured steps: per-replay stream
   constexpr int E = 16 / sizeof(T);
   __shared__ float red[8];
   const int tid = threadIdx.x;
@@ -500,4 +502,9 @@ PA_API hipError_t pa_dropout_add_norm_bwd(const void* dy, const void* s, const v
   }
   PA_NORM_DISPATCH(xd, wd, false,
                    (launch_bwd<T, WT, false>(dy, s, w, mean, rstd, dsum, dres, part, dw, db, rows, cols, np, st, &fa)))
+}
+
+// graph-safe dropout streams (common.h rng_mix): generation counter of this module's kernels
+PA_API int pa_norm_set_rng_gen(const void* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(pa::g_rng_gen), &p, sizeof(p));
 }

@@ -131,8 +131,11 @@ class TrainStepGraph:
     capture); the next call captures; every later call is ``graph.replay()``.  ``step_fn`` must
     read its inputs from fixed tensors (copy the next batch into them before calling) and must not
     synchronise with the host; per-step host values frozen at capture are refused: dropout inside
-    the step raises (its seeds are drawn on the host), and the learning rate must stay constant or
-    live in a device tensor.  Returns the static loss tensor (its value updates on every replay).
+    the step is graph-safe: the HIP dropout kernels mix a device-resident generation counter into
+    their host-drawn seeds (csrc/common.h rng_mix), and the captured graph advances that counter as
+    its first node, so every replay draws fresh keep-masks (a step's backward still regenerates its
+    forward's); the learning rate must stay constant or live in a device tensor.  Returns the
+    static loss tensor (its value updates on every replay).
     """
 
     def __init__(self, step_fn, warmup=3):
@@ -156,10 +159,13 @@ class TrainStepGraph:
                 out = self.step_fn()
             torch.cuda.current_stream().wait_stream(s)
             return out
+        gen = install_rng_generation()
         torch.cuda.synchronize()
         g = CUDAGraph()
         g.capture_begin()
         try:
+            if gen is not None:
+                gen.add_(1)  # first node of every replay: a fresh dropout stream per step
             self.out = self.step_fn()
         finally:
             g.capture_end()
@@ -173,9 +179,36 @@ def capture_train_step(step_fn, warmup=3):
     return TrainStepGraph(step_fn, warmup)
 
 
+_RNG_GEN = {}  # device index -> int32 [1] generation counter read by the HIP dropout kernels
+
+
+def install_rng_generation(device=None):
+    """The device-resident dropout generation counter (created and handed to the norm / activation
+    / flash-attention kernel modules on first use; 0 until a captured step advances it, so eager
+    steps keep their host-drawn streams).  None when the HIP kernel library is not loaded."""
+    from ...ops import _native as N
+    if N._load() is None:
+        return None
+    dev = torch.device('cuda', torch.cuda.current_device() if device is None else device)
+    gen = _RNG_GEN.get(dev.index)
+    if gen is None:
+        gen = torch.zeros(1, dtype=torch.int32, device=dev)
+        for fn in ('pa_norm_set_rng_gen', 'pa_act_set_rng_gen', 'pa_flash_set_rng_gen'):
+            N.check(getattr(N.lib, fn)(N.ptr(gen)), fn)
+        _RNG_GEN[dev.index] = gen
+    return gen
+
+
+def rng_generation(device=None):
+    """The generation counter tensor of ``device`` (None before the first captured step)."""
+    return _RNG_GEN.get(torch.cuda.current_device() if device is None else device)
+
+
 def host_rng_guard(what):
-    """Raise when a kernel would freeze a host-drawn dropout seed into a graph being captured."""
-    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+    """Raise when a kernel would freeze a host-drawn dropout seed into a graph being captured
+    without the device generation counter (install_rng_generation) that re-randomises it."""
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing() and \
+            _RNG_GEN.get(torch.cuda.current_device()) is None:
         raise RuntimeError(f"{what}: dropout seeds are drawn on the host and would be frozen into the "
                            "captured graph (every replay would reuse one mask); capture the step without "
                            "dropout or run it eagerly")

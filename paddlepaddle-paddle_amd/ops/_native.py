@@ -52,7 +52,7 @@ _SIGS = {
     'pa_embedding_fwd': [P, P, P, I, I, LL, I, P],
     'pa_embedding_bwd': [P, P, P, P, I, I, LL, I, I, P],
     'pa_rope': [P, P, P, P, P, I, I, I, I, I, F, I, P],
-    'pa_adamw': [P, P, P, P, P, LL, P, F, F, F, F, F, F, F, P, I, I, P],
+    'pa_adamw': [P, P, P, P, P, LL, P, F, F, F, F, F, F, F, P, P, I, I, P],
     'pa_sumsq': [P, LL, P, I, P],
     'pa_momentum': [P, P, P, P, LL, P, F, F, F, F, I, P, I, I, P],
     'pa_sumsq_parts': [],
@@ -73,6 +73,9 @@ _SIGS = {
     'pa_conv2d_fwd_stat_rows': [I],
     'pa_im2col_nhwc': [P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
     'pa_im2col_rows_ok': [I, I],
+    'pa_norm_set_rng_gen': [P],
+    'pa_act_set_rng_gen': [P],
+    'pa_flash_set_rng_gen': [P],
     'pa_conv2d_wgrad_ok': [I, I],
     'pa_conv2d_dgrad_classes': [P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     'pa_conv2d_wgrad': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],

@@ -10,13 +10,15 @@ from . import _native as N
 
 
 def adamw_flat(master, grad, m, v, lowp, lr, beta1, beta2, eps, weight_decay, beta1_pow, beta2_pow, lr_tensor=None,
-               grad_scale=None):
+               grad_scale=None, pows=None):
+    """pows (optional): device fp32 [beta1_pow, beta2_pow] read by the kernel instead of the host
+    values (the caller advances it on the device, so a captured step replays with fresh powers)."""
     n = master.numel()
     assert grad.numel() == n and m.numel() == n and v.numel() == n
     pd = -1 if lowp is None else N.dtcode(lowp.dtype)
     N.check(N.lib.pa_adamw(N.ptr(master), N.ptr(grad), N.ptr(m), N.ptr(v), N.ptr(lowp), n, N.ptr(lr_tensor),
                            float(lr), beta1, beta2, eps, weight_decay, float(beta1_pow), float(beta2_pow),
-                           N.ptr(grad_scale), N.dtcode(grad.dtype), pd, N.stream()), 'adamw')
+                           N.ptr(grad_scale), N.ptr(pows), N.dtcode(grad.dtype), pd, N.stream()), 'adamw')
 
 
 def sumsq(x):

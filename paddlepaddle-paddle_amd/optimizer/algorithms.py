@@ -240,15 +240,20 @@ class Adam(Optimizer):
                     return super().step()
                 fb.sync_grads()
             scale = self._clip_flat()
+            capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
             for ent in self._flat:
                 fb = ent['fb']
                 glr = lr * self._param_groups[ent['group']].get('learning_rate', 1.0)
                 lowp = fb.data if fb.dtype != torch.float32 else None
+                pows = _device_pows(ent, self._beta1, self._beta2, fb.device, capturing)
                 ops.optim.adamw_flat(ent['master'], fb.grad, ent['m1'], ent['m2'], lowp, glr, self._beta1,
                                      self._beta2, self._epsilon, ent['coeff'], ent['b1p'], ent['b2p'],
-                                     grad_scale=scale)
+                                     grad_scale=scale, pows=pows if capturing else None)
                 ent['b1p'] *= self._beta1
                 ent['b2p'] *= self._beta2
+                if pows is not None:
+                    pows.mul_(ent['betas'])
+                    ent['graph_stepped'] = ent.get('graph_stepped', False) or capturing
         self._global_step += 1
 
     def _clip_flat(self):
@@ -292,9 +297,11 @@ class Adam(Optimizer):
         sd = super().state_dict()
         if self._flat is not None:
             for ent in self._flat:
+                # a graph-replayed step advances only the device copy of the powers
+                b1p, b2p = ent['pows'].tolist() if ent.get('graph_stepped') else (ent['b1p'], ent['b2p'])
                 for p in ent['fb'].params:
-                    sd[f"{p.name}_beta1_pow_acc_0"] = _wrap(torch.tensor([ent['b1p']]))
-                    sd[f"{p.name}_beta2_pow_acc_0"] = _wrap(torch.tensor([ent['b2p']]))
+                    sd[f"{p.name}_beta1_pow_acc_0"] = _wrap(torch.tensor([b1p]))
+                    sd[f"{p.name}_beta2_pow_acc_0"] = _wrap(torch.tensor([b2p]))
         return sd
 
     def _on_state_loaded(self):
@@ -320,6 +327,21 @@ class Adam(Optimizer):
                     b2 = self._accumulators['beta2_pow_acc'].get(p.name)
                     if b2 is not None:
                         ent['b2p'] = float(b2.reshape(-1)[0])
+                if ent.get('pows') is not None:
+                    ent['pows'].copy_(torch.tensor([ent['b1p'], ent['b2p']]))
+
+
+def _device_pows(ent, b1, b2, device, capturing):
+    """Device copy [beta1^t, beta2^t] of a flat entry's bias-correction powers, advanced on the
+    device after every update (eager steps keep reading the host values): a training step captured
+    into a hipGraph (device/cuda/graphs.py TrainStepGraph) reads and advances it, so replays see
+    the powers of their own step instead of the ones frozen at capture.  Created on the first
+    eager step (never inside a capture)."""
+    pows = ent.get('pows')
+    if pows is None and not capturing and str(device).startswith('cuda'):
+        pows = ent['pows'] = torch.tensor([ent['b1p'], ent['b2p']], dtype=torch.float32, device=device)
+        ent['betas'] = torch.tensor([b1, b2], dtype=torch.float32, device=device)
+    return pows
 
 
 class AdamW(Adam):

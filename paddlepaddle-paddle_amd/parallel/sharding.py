@@ -629,6 +629,14 @@ class ShardedOptimizer:
             return
         b1, b2, eps = opt._beta1, opt._beta2, opt._epsilon
         b1p, b2p = b1 ** self._step, b2 ** self._step
+        # device copy of the powers for steps captured into a hipGraph (the host values would be
+        # frozen at capture); created on an eager step, advanced on the device after each update
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        pows = getattr(self, '_pows', None)
+        if pows is None and not capturing and any(ops.use_hip(a['master']) for a in self.engine.arenas.values()):
+            dev = next(iter(self.engine.arenas.values()))['master'].device
+            pows = self._pows = torch.tensor([b1p, b2p], dtype=torch.float32, device=dev)
+            self._betas = torch.tensor([b1, b2], dtype=torch.float32, device=dev)
         for dt, a in self.engine.arenas.items():
             g = a['grad']
             if scale is not None and not ops.use_hip(g):
@@ -640,10 +648,12 @@ class ShardedOptimizer:
                 if ops.use_hip(a['master']):
                     ops.optim.adamw_flat(a['master'][lo:hi], g[lo:hi], a['m'][lo:hi], a['v'][lo:hi],
                                          None if lowp is None else lowp[lo:hi], lr, b1, b2, eps, coeff, b1p, b2p,
-                                         grad_scale=scale)
+                                         grad_scale=scale, pows=pows if capturing else None)
                 else:
                     _adamw_ref(a['master'][lo:hi], g[lo:hi], a['m'][lo:hi], a['v'][lo:hi],
                                None if lowp is None else lowp[lo:hi], lr, b1, b2, eps, coeff, b1p, b2p)
+        if pows is not None:
+            pows.mul_(self._betas)
         self.engine.gather_params_after_step()
         opt._global_step += 1
 
@@ -679,6 +689,7 @@ class ShardedOptimizer:
             if dt != torch.float32:
                 a['param'].copy_(a['master'].to(dt))
         self._step = int(sd.get('@step@', self._step))
+        self._pows = None  # re-derived from the loaded step on the next eager step
         if 'LR_Scheduler' in sd and hasattr(self._inner._learning_rate, 'set_state_dict'):
             self._inner._learning_rate.set_state_dict(sd['LR_Scheduler'])
         self.engine.gather_params_after_step()

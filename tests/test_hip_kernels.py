@@ -1422,7 +1422,8 @@ def test_gpt_norm_param_grads_accumulate_in_flat_slots():
 
 def test_train_step_hip_graph_matches_eager():
     """A whole training step (conv + fused BN + 1x1 GEMM conv + Momentum on flat buffers) captured
-    into one hipGraph replays to the same parameters as eager steps; dropout refuses capture."""
+    into one hipGraph replays to the same parameters as eager steps; dropout in a captured step
+    draws a fresh mask per replay."""
     import paddle
     from paddle.device.cuda.graphs import capture_train_step
     paddle.set_device('gpu:0')
@@ -1454,12 +1455,71 @@ def test_train_step_hip_graph_matches_eager():
     for a, b in zip(*finals):
         _close(b, a, 1e-2 * float(a.abs().max()) + 1e-3, 1e-2, 'graph-replayed params')
 
-    def bad_step():
-        return paddle.incubate.nn.functional.fused_dropout_add(paddle.ones([64, 64]), paddle.ones([64, 64]), 0.5)
-    r = capture_train_step(bad_step, warmup=1)
+    # dropout inside a captured step: the graph advances the device generation counter per replay,
+    # so consecutive replays draw different keep-masks
+    def drop_step():
+        return paddle.incubate.nn.functional.fused_dropout_add(paddle.ones([64, 64]), paddle.zeros([64, 64]), 0.5)
+    r = capture_train_step(drop_step, warmup=1)
     r()
-    with pytest.raises(RuntimeError):
-        r()
+    a = r()._t.clone()
+    b = r()._t.clone()
+    assert not torch.equal(a, b)
+    assert set(a.unique().tolist()) <= {0.0, 2.0}
+
+
+def test_train_step_graph_dropout_adamw_gpt():
+    """GPT-tiny with hidden + attention dropout and AdamW (fp32 masters, global-norm clip) as one
+    captured hipGraph: every replay draws fresh dropout masks (device generation counter), its
+    backward regenerates the same masks as its forward (an eager step run with the replay's
+    generation and host seeds reproduces the replay's loss), the bias-correction powers advance on
+    the device, and training proceeds (loss falls)."""
+    import paddle
+    from paddle.models.gpt import gpt_config, GPTForPretraining
+    from paddle.device.cuda.graphs import capture_train_step, rng_generation
+    paddle.set_device('gpu:0')
+
+    def build(lr):
+        paddle.seed(0)
+        cfg = gpt_config('gpt-tiny', hidden_dropout_prob=0.1, attention_probs_dropout_prob=0.1)
+        model = GPTForPretraining(cfg)
+        opt = paddle.optimizer.AdamW(learning_rate=lr, parameters=model.parameters(), multi_precision=True,
+                                     grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
+        model, opt = paddle.amp.decorate(model, opt, level='O2', dtype='bfloat16')
+        ids = paddle.randint(0, cfg.vocab_size, [4, 129])
+        x, y = ids[:, :-1], ids[:, 1:]
+
+        def step():
+            loss = model.loss(model(x), y)
+            loss.backward()
+            opt.step()
+            opt.clear_grad()
+            return loss
+        return step, opt
+
+    # lr = 0: parameters fixed, so losses differ only through the dropout masks
+    step, _ = build(0.0)
+    g = capture_train_step(step, warmup=1)
+    g()
+    paddle.seed(123)
+    l1 = float(g())  # capture + replay 1
+    l2 = float(g())  # replay 2
+    gen = rng_generation()
+    assert gen is not None and l1 != l2
+    n = int(gen.item())
+    gen.fill_(n)
+    paddle.seed(123)  # the host seeds the capture drew
+    le = float(step())
+    assert abs(le - l2) <= 1e-5 * abs(l2), (le, l2)
+    # training: AdamW bias correction on the device, loss falls over replays
+    step, opt = build(2e-3)
+    g = capture_train_step(step, warmup=2)
+    losses = [float(g()) for _ in range(12)]
+    assert all(l == l for l in losses), losses
+    assert sum(losses[-3:]) < sum(losses[:3]), losses
+    ent = opt._flat[0] if getattr(opt, '_flat', None) else None
+    if ent is not None and ent.get('pows') is not None:
+        b1p = float(ent['pows'][0])
+        assert abs(b1p - 0.9 ** 13) < 1e-5, b1p  # 12 updates so far, powers for the 13th
 
 
 @pytest.mark.parametrize('M', [1000, 4096])
