@@ -194,16 +194,28 @@ def flash_attention_with_sparse_mask(query, key, value, attn_mask_start_row_indi
 
 def sparse_attention(query, key, value, sparse_csr_offset, sparse_csr_columns, key_padding_mask=None, attn_mask=None,
                      name=None):
+    """Attention restricted to a CSR sparsity pattern per (batch, head) (reference:
+    python/paddle/nn/functional/sparse_attention.py): row i of (b, h) attends to the key columns
+    ``sparse_csr_columns[b, h, offset[b, h, i]:offset[b, h, i + 1]]``.  ``key_padding_mask``
+    ([batch, seq]) and ``attn_mask`` ([seq, seq]) zero entries mask positions out as well.
+    The CSR pattern is expanded to a dense boolean mask on the device in one scatter (row of every
+    stored entry by a batched searchsorted over the offsets) — no host loop."""
     q, k, v = _u(query), _u(key), _u(value)  # [b, h, s, d]
-    off, cols = _u(sparse_csr_offset), _u(sparse_csr_columns)
+    off, cols = _u(sparse_csr_offset).long(), _u(sparse_csr_columns).long()
     B, H, S, D = q.shape
-    mask = torch.zeros(B, H, S, S, dtype=torch.bool, device=q.device)
-    for b in range(B):
-        for h in range(H):
-            o = off[b, h].tolist()
-            c = cols[b, h]
-            for i in range(S):
-                mask[b, h, i, c[o[i]:o[i + 1]]] = True
+    Sk = k.shape[2]
+    nnz = cols.shape[-1]
+    idx = torch.arange(nnz, device=q.device).expand(B, H, nnz).contiguous()
+    rows = torch.searchsorted(off[..., 1:].contiguous(), idx, right=True)  # row of every stored entry
+    valid = idx < off[..., -1:]
+    bi = torch.arange(B, device=q.device).view(B, 1, 1).expand(B, H, nnz)
+    hi = torch.arange(H, device=q.device).view(1, H, 1).expand(B, H, nnz)
+    mask = torch.zeros(B, H, S, Sk, dtype=torch.bool, device=q.device)
+    mask[bi[valid], hi[valid], rows.clamp_max(S - 1)[valid], cols[valid]] = True
+    if key_padding_mask is not None:
+        mask &= (_u(key_padding_mask) != 0).view(B, 1, 1, Sk)
+    if attn_mask is not None:
+        mask &= (_u(attn_mask) != 0).view(1, 1, S, Sk)
     return _w(TF.scaled_dot_product_attention(q, k, v, attn_mask=mask))
 
 

@@ -230,3 +230,43 @@ def test_cost_model_profiles_program_nodes():
     assert got and 'op_time' in got
     with pytest.raises(ValueError):
         cm.get_static_op_time(None)
+
+
+def test_sparse_attention_csr_matches_dense_mask():
+    """nn.functional.sparse_attention: the CSR pattern (plus key_padding_mask / attn_mask zeros)
+    expanded on the device equals attention under the equivalent dense boolean mask."""
+    import torch
+    import paddle
+    import paddle.nn.functional as F
+    g = torch.Generator().manual_seed(0)
+    B, H, S, D = 2, 3, 7, 4
+    q, k, v = (torch.randn(B, H, S, D, generator=g) for _ in range(3))
+    dense = torch.zeros(B, H, S, S, dtype=torch.bool)
+    offs, colss = [], []
+    for b in range(B):
+        for h in range(H):
+            o, c = [0], []
+            for i in range(S):
+                cs = sorted(set(torch.randint(0, S, (3,), generator=g).tolist()) | {i})
+                c += cs
+                o.append(len(c))
+                dense[b, h, i, cs] = True
+            offs.append(o)
+            colss.append(c)
+    nmax = max(len(c) for c in colss)
+    off = torch.tensor(offs, dtype=torch.int32).view(B, H, S + 1)
+    cols = torch.tensor([c + [0] * (nmax - len(c)) for c in colss], dtype=torch.int32).view(B, H, nmax)
+    T = paddle.to_tensor
+    out = F.sparse_attention(T(q), T(k), T(v), T(off), T(cols))
+    ref = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=dense)
+    assert torch.allclose(out._t, ref, atol=1e-6)
+    kpm = torch.ones(B, S)
+    kpm[:, -1] = 0
+    am = torch.ones(S, S)
+    am[:, 0] = 0
+    am[0, 0] = 1
+    out2 = F.sparse_attention(T(q), T(k), T(v), T(off), T(cols), key_padding_mask=T(kpm), attn_mask=T(am))
+    m2 = dense & (kpm != 0).view(B, 1, 1, S) & (am != 0).view(1, 1, S, S)
+    ref2 = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=m2)
+    ok = m2.any(-1, keepdim=True).expand_as(ref2)  # rows with no allowed key are undefined
+    assert torch.allclose(out2._t[ok], ref2[ok], atol=1e-6)
