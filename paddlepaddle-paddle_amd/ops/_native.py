@@ -74,6 +74,9 @@ _SIGS = {
     'pa_im2col_nhwc': [P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
     'pa_im2col_rows_ok': [I, I],
     'pa_norm_set_rng_gen': [P],
+    'pa_skinny_ok': [I, I, I, LL, LL],
+    'pa_skinny_ws_floats': [I, I, I],
+    'pa_skinny_gemm': [P, P, P, P, P, I, I, I, LL, LL, LL, I, P],
     'pa_act_set_rng_gen': [P],
     'pa_flash_set_rng_gen': [P],
     'pa_conv2d_wgrad_ok': [I, I],
@@ -109,7 +112,7 @@ _SIGS = {
                      P],
 }
 
-_LL_RET = {'pa_bn_ws_floats'}
+_LL_RET = {'pa_bn_ws_floats', 'pa_skinny_ws_floats'}
 _VOID_RET = {'pa_adamw_tune', 'pa_act_fwd_tune', 'pa_act_cs_tune'}
 
 

@@ -134,9 +134,59 @@ def _splitk_for(M, N_, K):
     return 1
 
 
+_skinny = os.environ.get('PADDLE_AMD_SKINNY_GEMM', '1') != '0'
+
+
+def skinny_ok(a, b):
+    """Decode-shaped GEMM contract (csrc/skinny_gemm.hip): a [M<=64, K] k-contiguous, b [K, N]
+    row-major or a transposed view of [N, K]."""
+    if not (_skinny and a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2
+            and b.dim() == 2 and a.stride(1) == 1 and a.shape[1] == b.shape[0]):
+        return False
+    if b.stride(1) == 1:
+        ldw = b.stride(0)
+    elif b.stride(0) == 1:
+        ldw = b.stride(1)
+    else:
+        return False
+    if a.data_ptr() % 16 or b.data_ptr() % 16 or N._load() is None:
+        return False
+    return bool(N.lib.pa_skinny_ok(a.shape[0], b.shape[1], a.shape[1], a.stride(0), ldw))
+
+
+def skinny_mm(a, b, bias=None, out=None):
+    """out[M, N] = a @ b (+ bias) for M <= 64 (decode steps) on the weight-streaming MFMA kernel:
+    in-register 8x8 transposes of n-major weight blocks feed v_mfma_f32_16x16x32_bf16 directly,
+    K split over ~2 blocks per CU with an fp32 partial sum (csrc/skinny_gemm.hip)."""
+    M, K = a.shape
+    N_ = b.shape[1]
+    kmaj = b.stride(1) != 1
+    ldw = b.stride(1) if kmaj else b.stride(0)
+    if out is None:
+        out = torch.empty(M, N_, dtype=torch.bfloat16, device=a.device)
+    assert out.stride(1) == 1 and out.stride(0) % 8 == 0
+    bb = bias.to(torch.bfloat16).contiguous() if bias is not None else None
+    ws = _workspace(int(N.lib.pa_skinny_ws_floats(M, N_, K)), a.device)
+    N.check(N.lib.pa_skinny_gemm(N.ptr(a), N.ptr(b), N.ptr(bb), N.ptr(out), N.ptr(ws), M, N_, K, a.stride(0), ldw,
+                                 out.stride(0), int(kmaj), N.stream()), 'skinny_gemm')
+    return out
+
+
+def _skinny_wins(M, N_, K):
+    """Where the skinny kernel beats the library (profiles/r3s3_decode_gemm.log, Llama-2-13B layer
+    shapes): every shape at M <= 16 (out 22.9 -> 16.8 us, ffn2 53.3 -> 26.1, ffn1 59 -> 48, qkv
+    even); at 16 < M <= 64 only the deep-K shapes (ffn2: 60 -> 33 us at M 32, 75 -> 46 at M 64)."""
+    return M <= 16 or (M <= 64 and K >= 2 * N_)
+
+
 def mm(a, b, out=None, bias=None, beta=0.0):
-    """out = a @ b (+ beta*out) (+ bias) on the hand-written kernel when the operands fit its
-    contract, else on the library (torch).  a: [M,K], b: [K,N] (either may be a transposed view)."""
+    """out = a @ b (+ beta*out) (+ bias) on the hand-written kernels when the operands fit their
+    contract (M <= 64: the decode-shaped skinny GEMM; else the 8-phase MFMA GEMM), else on the
+    library (torch).  a: [M,K], b: [K,N] (either may be a transposed view)."""
+    if a.is_cuda and _skinny_wins(a.shape[0], b.shape[1], a.shape[1]) and beta == 0.0 and skinny_ok(a, b) and (
+            out is None or (
+            out.dtype == torch.bfloat16 and out.stride(1) == 1 and out.stride(0) % 8 == 0)):
+        return skinny_mm(a, b, bias=bias, out=out)
     if _hip_gemm and a.is_cuda and hip_mm_ok(a, b, 1) and (bias is None or (
             bias.dtype == torch.bfloat16 and bias.is_contiguous())) and (out is None or (
             out.dtype == torch.bfloat16 and out.stride(1) == 1)):

@@ -1734,3 +1734,26 @@ def test_gpt_grouped_wgrad_trains_like_separate():
     for n in finals[0]:
         a, b = finals[0][n], finals[1][n]
         _close(b, a, 2e-2 * float(a.abs().max()) + 1e-4, 2e-2, n)
+
+
+@pytest.mark.parametrize("kmajor", [False, True])
+@pytest.mark.parametrize("M,K,N", [(1, 5120, 5120), (5, 96, 520), (16, 13824, 5120), (17, 2048, 2056),
+                                   (33, 512, 1024), (64, 5120, 15360), (3, 32, 8)])
+def test_skinny_gemm_decode_shapes(M, K, N, kmajor):
+    """csrc/skinny_gemm.hip (M <= 64): n-major weights (in-register 8x8 transposes) and k-major
+    weights, bias epilogue, partial 128-column tiles, vs an fp32 reference; ops.gemm.mm routes
+    small-M GEMMs to it."""
+    from paddle.ops import gemm
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N)
+    a = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    if kmajor:
+        w = (torch.randn(N, K, device=DEV, generator=g) * 0.05).to(torch.bfloat16).t()  # [K, N] view
+    else:
+        w = (torch.randn(K, N, device=DEV, generator=g) * 0.05).to(torch.bfloat16)
+    bias = (torch.randn(N, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    assert gemm.skinny_ok(a, w)
+    ref = a.float() @ w.float() + bias.float()
+    y = gemm.skinny_mm(a, w, bias=bias)
+    _close(y.float(), ref, 2e-2 * math.sqrt(K / 512) + 1e-2, 1e-2, 'skinny gemm')
+    if gemm._skinny_wins(M, N, K):  # the shapes ops.gemm.mm sends to it
+        assert torch.equal(y, gemm.mm(a, w, bias=bias))

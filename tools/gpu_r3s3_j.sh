@@ -1,0 +1,6 @@
+#!/bin/bash
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python tools/decode_gemm_bench.py > gpurun_out/r3s3_decode_gemm.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/r3s3_decode_gemm.log; exit 1; }
+grep -v amdgpu gpurun_out/r3s3_decode_gemm.log
