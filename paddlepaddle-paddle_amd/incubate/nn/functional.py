@@ -585,34 +585,58 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
     def lin(t, w, b, trans=False):
         t2 = t.reshape(-1, t.shape[-1])
         wt = _u(w)
-        y = ops.gemm.mm(t2, wt.t() if trans else wt, bias=None)
-        if b is not None:
-            y = y + _u(b).reshape(1, -1)
+        wt = wt.t() if trans else wt
+        bb = None if b is None else _u(b).reshape(-1)
+        if bb is not None and bb.dtype == t2.dtype and ops.gemm._skinny_wins(t2.shape[0], wt.shape[1], t2.shape[1]):
+            return ops.gemm.mm(t2, wt, bias=bb)  # decode GEMM: the bias is added in its finishing pass
+        y = ops.gemm.mm(t2, wt, bias=None)
+        if bb is not None:
+            y = y + bb.reshape(1, -1)
         return y
+
+    # pre-LN with unit residual scale: every residual add is fused into the following norm kernel
+    # (fused_layer_norm / fused_rms_norm with residual=), carried as (pending delta, stream)
+    fuse_res = pre_layer_norm and residual_alpha == 1.0
+
+    def norm_add(delta, stream, w, b):
+        if norm_type == 'rmsnorm':
+            y, s_ = fused_rms_norm(_w(delta), w, b, epsilon, residual=_w(stream))
+        else:
+            y, s_ = fused_layer_norm(_w(delta), w, b, epsilon, residual=_w(stream))
+        return _u(y), _u(s_)
 
     def act(t):
         if activation == 'gelu':
             return TF.gelu(t)
         if activation == 'relu':
             return torch.relu(t)
+        if activation == 'swiglu' and t.is_cuda:
+            return _u(swiglu(_w(t)))  # one fused kernel over the two halves (no silu + mul pair)
         if activation in ('swiglu', 'geglu'):
             a, g = t.chunk(2, -1)
             return (TF.silu(a) if activation == 'swiglu' else TF.gelu(a)) * g
         raise ValueError(f"unsupported activation {activation}")
 
     caches_out = []
+    pending = None  # fuse_res: the previous block's ffn2 output, not yet added to the stream h
+    if step is not None:  # decode: one position per sequence, the same for every layer
+        pos_step = torch.full((B,), step, dtype=torch.int32, device=h.device)
+        lens_step = pos_step + 1
     for i in range(nl):
+        if pending is not None:
+            a, h = norm_add(pending, h, ln_scales[i], ln_biases[i] if ln_biases is not None else None)
+            pending = None
+        else:
+            a = norm(h, ln_scales[i], ln_biases[i] if ln_biases is not None else None) if pre_layer_norm else h
         resid = h
-        a = norm(h, ln_scales[i], ln_biases[i] if ln_biases is not None else None) if pre_layer_norm else h
         w = _u(qkv_weights[i])
+        qb = qkv_biases[i] if qkv_biases is not None else None
         if trans_qkvw:
             Wm = w.reshape(-1, E)                                  # [(Hq + 2 Hkv) * D, E]
-            qkv = lin(a, Wm, None, trans=True)
+            qkv = lin(a, Wm, qb, trans=True)
         else:
             Wm = w.reshape(E, -1)
-            qkv = lin(a, Wm, None)
-        if qkv_biases is not None and qkv_biases[i] is not None:
-            qkv = qkv + _u(qkv_biases[i]).reshape(1, -1)
+            qkv = lin(a, Wm, qb)
         if gqa_group_size > 0:
             D = w.shape[-2] if trans_qkvw else w.shape[-1]
             Hkv = gqa_group_size
@@ -657,9 +681,9 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
         else:
             if cache is None:
                 raise ValueError("fused_multi_transformer decode (time_step) needs cache_kvs")
-            pos = torch.full((B,), step, dtype=torch.int32, device=h.device)
+            pos = pos_step
             ops.decode.kv_cache_write(k[:, 0], v[:, 0], cache[0], cache[1], pos)
-            lens = pos + 1
+            lens = lens_step
             m = None if attn_mask is None else _u(attn_mask).reshape(B, -1).float()
             kc, vc = cache[0], cache[1]
             if beam_offset is not None:
@@ -678,18 +702,27 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
             caches_out.append(cache_kvs[i])
         o = (row_parallel if tp_group is not None else lin)(
             o.reshape(B, S, Hq * D), linear_weights[i], linear_biases[i] if linear_biases is not None else None)
-        h = resid * residual_alpha + o.reshape(B, S, E).to(resid.dtype)
-        if not pre_layer_norm:
-            h = norm(h, ln_scales[i], ln_biases[i] if ln_biases is not None else None)
+        if fuse_res:
+            f, h = norm_add(o.reshape(B, S, E).to(resid.dtype), resid, ffn_ln_scales[i],
+                            ffn_ln_biases[i] if ffn_ln_biases is not None else None)
+        else:
+            h = resid * residual_alpha + o.reshape(B, S, E).to(resid.dtype)
+            if not pre_layer_norm:
+                h = norm(h, ln_scales[i], ln_biases[i] if ln_biases is not None else None)
+            f = norm(h, ffn_ln_scales[i], ffn_ln_biases[i] if ffn_ln_biases is not None else None) \
+                if pre_layer_norm else h
         resid = h
-        f = norm(h, ffn_ln_scales[i], ffn_ln_biases[i] if ffn_ln_biases is not None else None) if pre_layer_norm \
-            else h
         f = act(lin(f, ffn1_weights[i], ffn1_biases[i] if ffn1_biases is not None else None))
         f = (row_parallel if tp_group is not None else lin)(
             f, ffn2_weights[i], ffn2_biases[i] if ffn2_biases is not None else None)
+        if fuse_res:
+            pending = f.reshape(B, S, E).to(resid.dtype)
+            continue
         h = resid * residual_alpha + f.reshape(B, S, E).to(resid.dtype)
         if not pre_layer_norm:
             h = norm(h, ffn_ln_scales[i], ffn_ln_biases[i] if ffn_ln_biases is not None else None)
+    if pending is not None:
+        h = h + pending
     out = _w(h)
     return (out, caches_out) if cache_kvs is not None else out
 

@@ -176,7 +176,7 @@ def _skinny_wins(M, N_, K):
     """Where the skinny kernel beats the library (profiles/r3s3_decode_gemm.log, Llama-2-13B layer
     shapes): every shape at M <= 16 (out 22.9 -> 16.8 us, ffn2 53.3 -> 26.1, ffn1 59 -> 48, qkv
     even); at 16 < M <= 64 only the deep-K shapes (ffn2: 60 -> 33 us at M 32, 75 -> 46 at M 64)."""
-    return M <= 16 or (M <= 64 and K >= 2 * N_)
+    return _skinny and (M <= 16 or (M <= 64 and K >= 2 * N_))
 
 
 def mm(a, b, out=None, bias=None, beta=0.0):
