@@ -212,3 +212,49 @@ def host_rng_guard(what):
         raise RuntimeError(f"{what}: dropout seeds are drawn on the host and would be frozen into the "
                            "captured graph (every replay would reuse one mask); capture the step without "
                            "dropout or run it eagerly")
+
+
+class DecodeStepGraph:
+    """One generation (decode) step of a cached model captured into a hipGraph and replayed per
+    token — the launch-bound small-batch decode loop becomes one graph launch.
+
+    ``step_fn(x, time_step)`` runs the model on the new tokens ``x`` at position ``time_step`` (a
+    device int tensor, e.g. ``FusedMultiTransformer(x, caches=..., time_step=...)``) and returns its
+    output; KV caches are updated in place by the model.  The graph reads ``x`` from a static
+    buffer and ``time_step`` from a device counter it advances by one as its last node, so each
+    call is ``copy new tokens -> replay`` with no host-side position bookkeeping.  ``warmup``
+    eager steps run first (allocator pools, kernel selection); the first captured call also
+    produces that step's output.  Host-side cache features (beam_offset, pre_caches) are refused.
+    """
+
+    def __init__(self, step_fn, x_example, start_step, warmup=1):
+        self.step_fn = step_fn
+        self.x = x_example.clone()
+        self.time_step = torch.tensor([int(start_step)], dtype=torch.int32, device=self.x.device)
+        self.warmup = warmup
+        self.graph = None
+        self.out = None
+
+    def __call__(self, x_new):
+        from ...core.tensor import Tensor, _wrap
+        xt = x_new._t if isinstance(x_new, Tensor) else x_new
+        self.x.copy_(xt)
+        if self.graph is not None:
+            self.graph.replay()
+            return self.out
+        if self.warmup > 0:
+            self.warmup -= 1
+            out = self.step_fn(_wrap(self.x), _wrap(self.time_step))
+            self.time_step.add_(1)
+            return out
+        torch.cuda.synchronize()
+        g = CUDAGraph()  # captures on its own side stream
+        g.capture_begin()
+        try:
+            self.out = self.step_fn(_wrap(self.x), _wrap(self.time_step))
+            self.time_step.add_(1)
+        finally:
+            g.capture_end()
+        self.graph = g
+        g.replay()
+        return self.out

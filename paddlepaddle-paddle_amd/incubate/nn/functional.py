@@ -574,8 +574,17 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
     h = _u(x)
     B, S, E = h.shape
     nl = len(qkv_weights)
-    step = None if time_step is None else int(_u(time_step).reshape(-1)[0]) if isinstance(time_step, Tensor) or \
-        torch.is_tensor(time_step) else (None if time_step is None else int(time_step))
+    # a device-resident time_step inside a hipGraph capture (DecodeStepGraph) stays on the device:
+    # positions / lengths / the rotary row are derived from it there (no host read)
+    ts_t = _u(time_step) if isinstance(time_step, Tensor) or torch.is_tensor(time_step) else None
+    dev_step = ts_t is not None and ts_t.is_cuda and torch.cuda.is_current_stream_capturing()
+    if dev_step:
+        if beam_offset is not None or pre_caches is not None:
+            raise ValueError("fused_multi_transformer: beam_offset / pre_caches need a host time_step "
+                             "(not supported inside a captured decode step)")
+        step = -1  # decode, position on the device
+    else:
+        step = None if time_step is None else int(ts_t.reshape(-1)[0]) if ts_t is not None else int(time_step)
 
     def norm(t, w, b):
         if norm_type == 'rmsnorm':
@@ -619,7 +628,10 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
 
     caches_out = []
     pending = None  # fuse_res: the previous block's ffn2 output, not yet added to the stream h
-    if step is not None:  # decode: one position per sequence, the same for every layer
+    if dev_step:
+        pos_step = ts_t.reshape(-1)[:1].to(torch.int32).expand(B).contiguous()
+        lens_step = pos_step + 1
+    elif step is not None:  # decode: one position per sequence, the same for every layer
         pos_step = torch.full((B,), step, dtype=torch.int32, device=h.device)
         lens_step = pos_step + 1
     for i in range(nl):
@@ -650,6 +662,9 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
             re = _u(rotary_embs).float().reshape(2, B, -1, D)      # [2, B, seq, D]
             if step is None:
                 cos, sin = re[0][:, :S, None], re[1][:, :S, None]
+            elif dev_step:
+                idx = pos_step[:1].long().clamp_max(re.shape[2] - 1)
+                cos, sin = re[0].index_select(1, idx)[:, :, None], re[1].index_select(1, idx)[:, :, None]
             else:
                 idx = min(step, re.shape[2] - 1)
                 cos, sin = re[0][:, idx:idx + 1, None], re[1][:, idx:idx + 1, None]

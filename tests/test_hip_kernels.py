@@ -1757,3 +1757,39 @@ def test_skinny_gemm_decode_shapes(M, K, N, kmajor):
     _close(y.float(), ref, 2e-2 * math.sqrt(K / 512) + 1e-2, 1e-2, 'skinny gemm')
     if gemm._skinny_wins(M, N, K):  # the shapes ops.gemm.mm sends to it
         assert torch.equal(y, gemm.mm(a, w, bias=bias))
+
+
+def test_fused_multi_transformer_decode_step_graph():
+    """FusedMultiTransformer decode steps replayed from one captured hipGraph (DecodeStepGraph:
+    device-resident time_step advanced by the graph, KV caches updated in place) == eager decode
+    steps from the same prefill."""
+    import paddle
+    from paddle.incubate.nn import FusedMultiTransformer
+    from paddle.device.cuda.graphs import DecodeStepGraph
+    paddle.set_device('gpu:0')
+    E, H, F_, nl, B, S, L = 256, 4, 512, 2, 3, 5, 32
+    paddle.seed(0)
+    m = FusedMultiTransformer(E, H, F_, num_layers=nl, norm_type='rmsnorm', activation='swiglu')
+    m.eval()
+    m.to(dtype='bfloat16')
+    D = E // H
+    x = (paddle.randn([B, S + 6, E]) * 0.5).astype('bfloat16')
+    outs = []
+    for graphed in (False, True):
+        caches = [paddle.zeros([2, B, H, L, D], dtype='bfloat16') for _ in range(nl)]
+        with paddle.no_grad():
+            m(x[:, :S], caches=caches)  # prefill
+            res = []
+            if graphed:
+                g = DecodeStepGraph(lambda xx, ts: m(xx, caches=caches, time_step=ts)[0], x[:, S:S + 1]._t, S,
+                                    warmup=1)
+                for t in range(S, S + 6):
+                    res.append(g(x[:, t:t + 1])._t.float().clone())
+                assert g.graph is not None and int(g.time_step.item()) == S + 6
+            else:
+                for t in range(S, S + 6):
+                    o, _ = m(x[:, t:t + 1], caches=caches, time_step=paddle.to_tensor([t]))
+                    res.append(o._t.float().clone())
+        outs.append(res)
+    for a, b in zip(*outs):
+        _close(b, a, 2e-2, 2e-2, 'graph-replayed decode step')

@@ -37,8 +37,21 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
             res.append(e0.elapsed_time(e1) / 20 / nl)
+        # the same decode step replayed from one captured hipGraph (device time_step)
+        from paddle.device.cuda.graphs import DecodeStepGraph
+        with paddle.no_grad():
+            gs = DecodeStepGraph(lambda xx, t: m(xx, caches=caches, time_step=t)[0], x._t, L - 40, warmup=1)
+            for _ in range(3):
+                gs(x)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(20):
+                gs(x)
+            e1.record()
+            torch.cuda.synchronize()
+        res.append(e0.elapsed_time(e1) / 20 / nl)
         print(f"B {B:3d} L {L}: {res[0]:.3f} ms/layer (library GEMMs) -> {res[1]:.3f} ms/layer (skinny GEMMs)"
-              f"  [{res[0] / res[1]:.2f}x]")
+              f"  [{res[0] / res[1]:.2f}x]; decode step as one hipGraph: {res[2]:.3f} ms/layer")
     gemm._skinny = True
 
 
