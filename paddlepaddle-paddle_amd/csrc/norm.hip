@@ -24,14 +24,19 @@ struct DropSpec {
   uint32_t seed, offset;
 };
 
+// Each 32-bit hash gives two 16-bit uniforms (one hash per PAIR of elements: the per-element hash
+// made this VALU the larger half of the fused norm kernels' issue); p is applied at 1/65536
+// resolution and the keep scale matches the quantised rate exactly.
 template <int E>
 __device__ __forceinline__ void drop_mask(const DropSpec& d, size_t vec_index, float (&m)[E]) {
-  const float scale = 1.f / (1.f - d.p);
+  const uint32_t thr = (uint32_t)(d.p * 65536.f + 0.5f);
+  const float scale = 65536.f / (float)(65536u - min(thr, 65535u));
   const uint32_t h0 = hash3(d.seed, d.offset, (uint32_t)vec_index);
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
+  for (int e = 0; e < E; e += 2) {
     const uint32_t h = (e == 0) ? h0 : hash3(h0, (uint32_t)e, 0x2545F491u);
-    m[e] = uniform01(h) >= d.p ? scale : 0.f;
+    m[e] = (h & 0xFFFFu) >= thr ? scale : 0.f;
+    if (e + 1 < E) m[e + 1] = (h >> 16) >= thr ? scale : 0.f;
   }
 }
 
