@@ -8,14 +8,16 @@ from ...parallel.sharding import ShardingEngine, ShardedOptimizer, GroupShardedM
 
 def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, offload=False, sync_buffers=False,
                            buffer_max_size=2 ** 23, segment_size=2 ** 20, sync_comm=False, dp_group=None,
-                           exclude_layer=None, reduce_dtype=None, alias=None):
+                           exclude_layer=None, reduce_dtype=None, alias=None, reshard_after_forward=None):
     """level: 'os' (stage 1), 'os_g' (stage 2), 'p_g_os' (stage 3). Returns (model, optimizer, scaler).
 
     MI355X extensions: ``reduce_dtype='float32'`` reduce-scatters gradients in fp32 (main-grad
-    precision at 8 ranks); ``alias=False`` runs the multi-rank path at world size 1."""
+    precision at 8 ranks); ``alias=False`` runs the multi-rank path at world size 1;
+    ``reshard_after_forward`` (stage 3): see parallel.sharding.ShardingEngine (None: keep the
+    gathered parameters from forward to backward when the model is small against the HBM)."""
     assert level in ('os', 'os_g', 'p_g_os'), f"unknown sharding level {level}"
     engine = ShardingEngine(model, level, group=group, segment_size=segment_size, reduce_dtype=reduce_dtype,
-                            alias=alias)
+                            alias=alias, reshard_after_forward=reshard_after_forward)
     wrapped = GroupShardedModel(model, engine)
     opt = ShardedOptimizer(optimizer, engine)
     return wrapped, opt, scaler

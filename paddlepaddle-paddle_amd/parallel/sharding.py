@@ -131,7 +131,7 @@ class _PreBackward(torch.autograd.Function):
 class ShardingEngine:
     def __init__(self, model, level='p_g_os', group=None, bucket_mb=256, segment_size=2 ** 20,
                  release_grads=True, persistent_types=None, persistent_below=None, params=None, alias=None,
-                 reduce_dtype=None, isolate=None):
+                 reduce_dtype=None, isolate=None, reshard_after_forward=None):
         """model: the Layer to shard; or model=None with ``params`` (a parameter list) for stage 1/2
         (the hybrid-parallel sharding optimizer, which only sees its optimizer's parameters).
 
@@ -142,7 +142,13 @@ class ShardingEngine:
         communication, 2x the bytes) into an fp32 gradient arena; default: the parameter dtype.
         isolate: stage 1/2 only — ``isolate(p)`` returns a key or None; parameters with the same key
         form a unit of their own (pipeline-shared weights, whose shards must line up across the
-        stages that hold a copy)."""
+        stages that hold a copy).
+        reshard_after_forward (stage 3): release a unit's gathered parameters after its forward
+        and all-gather them again for its backward (True), or keep them until the unit's gradient
+        reduce-scatter (False: one all-gather per unit and step instead of two, the parameters of
+        the whole model materialised at the forward/backward turn).  None: False on a GPU when the
+        model's parameters take at most 1/16 of the device memory (288 GB HBM: e.g. GPT-3 1.3B's
+        2.6 GB), else True; always True on the CPU."""
         self.model = model
         self.level = LEVELS[level] if isinstance(level, str) else int(level)
         if model is None and (params is None or self.level == 3):
@@ -158,6 +164,8 @@ class ShardingEngine:
             alias = os.environ.get('PADDLE_AMD_SHARDING_ALIAS', '1') != '0'
         self.alias = self.world == 1 and bool(alias)
         self.release_grads = release_grads and self.level == 3 and not self.alias
+        self.reshard_after_forward = self._auto_reshard(model, params) if reshard_after_forward is None \
+            else bool(reshard_after_forward)
         rd = str(reduce_dtype).replace('torch.', '').replace('paddle.', '') if reduce_dtype is not None else None
         if rd not in (None, 'float32', 'bfloat16', 'float16'):
             raise ValueError(f"reduce_dtype must be float32 / bfloat16 / float16, got {reduce_dtype}")
@@ -302,6 +310,14 @@ class ShardingEngine:
             a['v'] = torch.zeros(n, dtype=torch.float32, device=dev)
             a['b1p'] = None
 
+    def _auto_reshard(self, model, params):
+        ps = list(params) if params is not None else (list(model.parameters()) if model is not None else [])
+        if not ps or not ps[0]._t.is_cuda:
+            return True
+        nbytes = sum(p._t.numel() * p._t.element_size() for p in ps)
+        total = torch.cuda.get_device_properties(ps[0]._t.device).total_memory
+        return nbytes * 16 > total
+
     def pshard(self, u):
         return self.arenas[u.dtype]['param'][u.arena_off:u.arena_off + u.L]
 
@@ -370,7 +386,10 @@ class ShardingEngine:
                     for i, r in zip(idx, res):
                         new[i] = _wrap(r)
                     outputs = tuple(new) if isinstance(outputs, tuple) else new[0]
-            u.free_params()
+                if self.reshard_after_forward:
+                    u.free_params()  # else kept until its gradient reduce-scatter (no backward re-gather)
+            else:
+                u.free_params()
             return outputs
         return hook
 

@@ -86,8 +86,14 @@ def main():
     opt = make_opt(kind, model.parameters())
     if mode == 'dp':
         model = paddle.DataParallel(model)
+    elif mode == 'p_g_os_keep':  # stage 3 without the backward re-gather (reshard_after_forward=False)
+        model, opt, _ = dist.sharding.group_sharded_parallel(model, opt, level='p_g_os', segment_size=64,
+                                                             reshard_after_forward=False)
+        assert not model._engine.reshard_after_forward
     else:
         model, opt, _ = dist.sharding.group_sharded_parallel(model, opt, level=mode, segment_size=64)
+        if mode == 'p_g_os':
+            assert model._engine.reshard_after_forward  # CPU default
     train(model, opt, rank, world, split=True)
     want = params_of(ref)
     if mode in ('os', 'os_g'):

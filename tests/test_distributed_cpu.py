@@ -28,7 +28,7 @@ def run_workers(script, *args, nproc=2, timeout=300):
     return r.stdout
 
 
-@pytest.mark.parametrize("mode", ['dp', 'os', 'os_g', 'p_g_os'])
+@pytest.mark.parametrize("mode", ['dp', 'os', 'os_g', 'p_g_os', 'p_g_os_keep'])
 def test_dp_and_sharding_match_single_process(mode):
     out = run_workers('worker_dp_sharding.py', mode)
     assert out.count(f'{mode} OK') == 2
