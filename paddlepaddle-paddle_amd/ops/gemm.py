@@ -179,6 +179,42 @@ def _skinny_wins(M, N_, K):
     return _skinny and (M <= 16 or (M <= 64 and K >= 2 * N_))
 
 
+def _round_split(a, b, out, beta=0.0):
+    """Few-round GEMMs whose last round of 256x256 tiles leaves most CUs idle (the tied LM-head
+    weight gradient: 197 x 8 = 1576 tiles = 6 full rounds + 40 tiles): the rows of the full rounds
+    run as one GEMM and the remaining tile rows as a split-K GEMM (4x the work items at 1/4 the
+    depth), so the tail costs about a quarter round instead of a whole one.  beta (accumulate
+    into ``out``) is honoured by both parts.  None when it does not apply."""
+    M, K = a.shape
+    N_ = b.shape[1]
+    tm, tn = -(-M // 256), -(-N_ // 256)
+    tiles = tm * tn
+    full = tiles // 256
+    tail = tiles - full * 256
+    if full == 0 or full > 12 or tail == 0 or tail * 10 > 256 * 3:
+        return None  # many rounds (the tail is a small share) or a well-filled last round
+    m1 = (full * 256 // tn) * 256  # rows covered by whole tile rows inside the full rounds
+    if m1 <= 0 or m1 >= M:
+        return None
+    rest_tiles = -(-(M - m1) // 256) * tn
+    sk = 1
+    for s_ in (8, 4, 2):
+        if rest_tiles * s_ <= 256 and K % (64 * s_) == 0 and K // s_ >= 512:
+            sk = s_
+            break
+    if sk == 1:
+        return None
+    a1, a2 = a[:m1], a[m1:]
+    if not (hip_mm_ok(a1, b, 1) and hip_mm_ok(a2, b, sk)):
+        return None
+    if out is None:
+        out = torch.empty(M, N_, dtype=torch.bfloat16, device=a.device)
+        beta = 0.0
+    hip_mm(a1, b, out=out[:m1], beta=beta)
+    hip_mm(a2, b, out=out[m1:], beta=beta, splitk=sk)  # beta applied by the split-K reduce
+    return out
+
+
 def mm(a, b, out=None, bias=None, beta=0.0):
     """out = a @ b (+ beta*out) (+ bias) on the hand-written kernels when the operands fit their
     contract (M <= 64: the decode-shaped skinny GEMM; else the 8-phase MFMA GEMM), else on the
@@ -193,6 +229,10 @@ def mm(a, b, out=None, bias=None, beta=0.0):
         sk = _splitk_for(a.shape[0], b.shape[1], a.shape[1]) if bias is None else 1
         if sk > 1 and not hip_mm_ok(a, b, sk):
             sk = 1
+        if sk == 1 and bias is None:
+            r = _round_split(a, b, out, beta if out is not None else 0.0)
+            if r is not None:
+                return r
         return hip_mm(a, b, out=out, bias=bias, beta=beta if out is not None else 0.0, splitk=sk)
     if out is None:
         return torch.addmm(bias, a, b) if bias is not None else torch.mm(a, b)

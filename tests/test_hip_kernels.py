@@ -1793,3 +1793,22 @@ def test_fused_multi_transformer_decode_step_graph():
         outs.append(res)
     for a, b in zip(*outs):
         _close(b, a, 2e-2, 2e-2, 'graph-replayed decode step')
+
+
+def test_gemm_round_split_tail():
+    """ops.gemm.mm on a few-round GEMM with a thin last round (LM-head weight-gradient shape class:
+    6 full rounds of 256x256 tiles + 40 tiles) runs the tail rows split-K; result vs fp32."""
+    from paddle.ops import gemm
+    g = torch.Generator(device=DEV).manual_seed(9)
+    M, K, N = 50304, 1024, 2048
+    a = torch.randn(K, M, device=DEV, generator=g).to(torch.bfloat16).t()  # transposed view, as dlogits^T
+    b = (torch.randn(K, N, device=DEV, generator=g) * 0.05).to(torch.bfloat16)
+    assert gemm._round_split(a, b, None) is not None
+    y = gemm.mm(a, b)
+    ref = a.float() @ b.float()
+    _close(y.float(), ref, 3e-2, 1e-2, 'round-split gemm')
+    # accumulate form (the weight-gradient slot, beta = 1)
+    acc = (torch.randn(M, N, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    ref2 = acc.float() + ref
+    gemm.mm(a, b, out=acc, beta=1.0)
+    _close(acc.float(), ref2, 3e-2, 1e-2, 'round-split gemm, beta = 1')
