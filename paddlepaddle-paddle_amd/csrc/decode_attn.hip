@@ -70,11 +70,27 @@ __device__ __forceinline__ float row_sum16(float v) {
   return v;
 }
 
+// cache element -> float: bf16 / fp16 as is; int8 caches store round(x * quant_scale), uint8 ones
+// the same offset by 128 (the reference's layout); the dequant scale is folded in elsewhere
+__device__ __forceinline__ float cvt(bf16_t v) { return (float)v; }
+__device__ __forceinline__ float cvt(f16_t v) { return (float)v; }
+__device__ __forceinline__ float cvt(int8_t v) { return (float)v; }
+__device__ __forceinline__ float cvt(uint8_t v) { return (float)v - 128.f; }
+
 template <typename T, int N>
 __device__ __forceinline__ void unpack(const Pack<T, N>& p, float (&o)[N]) {
 #pragma unroll
-  for (int i = 0; i < N; ++i) o[i] = to_f(p.v[i]);
+  for (int i = 0; i < N; ++i) o[i] = cvt(p.v[i]);
 }
+
+// Dequantisation of an 8-bit KV cache: per KV head (static, sb = 0) or per (sequence, KV head)
+// (dynamic, sb = Hkv) scales.  The K scale is folded into the query (q . (s k) = s (q . k)); the V
+// scale multiplies the merged accumulator (constant over the positions of a (sequence, head)).
+struct Deq {
+  const float* ks = nullptr;
+  const float* vs = nullptr;
+  long long sb = 0;
+};
 
 // grid (nsplit, Hkv, B), 256 threads.  G = query heads per KV head (GQA group size), D head dim.
 // q: [B, Hq*D] rows of stride q_stride (elements) (+ optional q bias [Hq*D]).
@@ -86,14 +102,15 @@ __device__ __forceinline__ void unpack(const Pack<T, N>& p, float (&o)[N]) {
 // base + 16u + 4*wave + grp.  Raw K/V stay packed in registers until used; the softmax of a lane
 // group is updated once per iteration (one max / rescale per head for its U positions).
 // Paged caches with block_size % (16*U) == 0 and an aligned chunk look the block id up once per
-// iteration (a wave-uniform scalar load) instead of once per position.
-template <typename T, int D, int G, bool PAGED>
+// iteration (a wave-uniform scalar load) instead of once per position.  8-bit caches issue the
+// loads of iteration i+1 before the math of iteration i (two register sets of raw K/V).
+template <typename T, int D, int G, bool PAGED, typename CT = T>
 __global__ __launch_bounds__(256) void attn_split_kernel(const T* __restrict__ q, long long q_stride,
                                                          const T* __restrict__ q_bias, Cache cache,
                                                          const int* __restrict__ lens, const float* __restrict__ mask,
                                                          long long mask_stride, T* __restrict__ out,
                                                          long long out_stride, float* __restrict__ ws, int Hq, int Hkv,
-                                                         int nsplit, int chunk, float scale) {
+                                                         int nsplit, int chunk, float scale, Deq dq = Deq{}) {
   constexpr int EPL = D / 16;  // elements per lane
   constexpr int U = 4;         // positions per lane group per iteration
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
@@ -114,9 +131,11 @@ __global__ __launch_bounds__(256) void attn_split_kernel(const T* __restrict__ q
 #pragma unroll
       for (int e = 0; e < EPL; ++e) qf[g][e] += bb[e];
     }
+    const float ksc = dq.ks != nullptr ? dq.ks[(long long)b * dq.sb + hk] : 1.f;  // 8-bit cache: K dequant
 #pragma unroll
-    for (int e = 0; e < EPL; ++e) qf[g][e] *= sl2;  // scores come out in log2 units
+    for (int e = 0; e < EPL; ++e) qf[g][e] *= sl2 * ksc;  // scores come out in log2 units
   }
+  const float vsc = dq.vs != nullptr ? dq.vs[(long long)b * dq.sb + hk] : 1.f;  // 8-bit cache: V dequant
   float m[G], l[G], acc[G][EPL];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -125,15 +144,14 @@ __global__ __launch_bounds__(256) void attn_split_kernel(const T* __restrict__ q
 #pragma unroll
     for (int e = 0; e < EPL; ++e) acc[g][e] = 0.f;
   }
-  const T* kc = reinterpret_cast<const T*>(cache.k);
-  const T* vc = reinterpret_cast<const T*>(cache.v);
-  typedef Pack<T, EPL> PK;
+  const CT* kc = reinterpret_cast<const CT*>(cache.k);
+  const CT* vc = reinterpret_cast<const CT*>(cache.v);
+  typedef Pack<CT, EPL> PK;
   const bool blk_aligned = PAGED && (cache.block_size % (16 * U) == 0) && (chunk % (16 * U) == 0);
-  for (int base = p0; base < p1; base += 16 * U) {
-    PK kr[U], vr[U];
-    bool ok[U];
+  // K/V of iteration `base` -> registers (lanes past p1 load nothing)
+  auto load = [&](int base, PK (&kr)[U], PK (&vr)[U], bool (&ok)[U]) {
     long long o0 = 0;
-    if (PAGED && blk_aligned) {
+    if (PAGED && blk_aligned && base < p1) {
       const int blk = cache.block_tables[(long long)b * cache.max_blocks + base / cache.block_size];
       o0 = (((long long)blk * Hkv + hk) * cache.block_size + (base % cache.block_size)) * D;
     }
@@ -148,11 +166,14 @@ __global__ __launch_bounds__(256) void attn_split_kernel(const T* __restrict__ q
         vr[u] = *reinterpret_cast<const PK*>(vc + o);
       }
     }
+  };
+  // one iteration's math on raw K/V registers (positions base + 16u + 4*wave + grp)
+  auto step = [&](int base, const PK (&kr)[U], const PK (&vr)[U], const bool (&ok)[U]) {
     float sc[G][U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       float kf[EPL];
-      unpack<T, EPL>(kr[u], kf);
+      unpack<CT, EPL>(kr[u], kf);
       const float mk = (mask && ok[u]) ? mask[(long long)b * mask_stride + base + 16 * u + 4 * wave + grp] * kLog2e
                                        : 0.f;
 #pragma unroll
@@ -181,11 +202,36 @@ __global__ __launch_bounds__(256) void attn_split_kernel(const T* __restrict__ q
         l[g] += pr;
         if (ok[u]) {
           float vf[EPL];
-          unpack<T, EPL>(vr[u], vf);
+          unpack<CT, EPL>(vr[u], vf);
 #pragma unroll
           for (int e = 0; e < EPL; ++e) acc[g][e] += pr * vf[e];
         }
       }
+    }
+  };
+  PK kr[U], vr[U];
+  bool ok[U];
+  if constexpr (sizeof(CT) == 1) {
+    // 8-bit caches: software pipeline, the next iteration's K/V in flight while this one computes
+    // (half-size raw registers; measured 1.1-1.2x on the int8 path, a loss for 16-bit caches,
+    // whose larger register sets cost occupancy)
+    load(p0, kr, vr, ok);
+    for (int base = p0; base < p1; base += 16 * U) {
+      PK kn[U], vn[U];
+      bool okn[U];
+      load(base + 16 * U, kn, vn, okn);
+      step(base, kr, vr, ok);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        kr[u] = kn[u];
+        vr[u] = vn[u];
+        ok[u] = okn[u];
+      }
+    }
+  } else {
+    for (int base = p0; base < p1; base += 16 * U) {
+      load(base, kr, vr, ok);
+      step(base, kr, vr, ok);
     }
   }
 
@@ -216,6 +262,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(const T* __restrict__ q
         A += red[i][g][d] * w;
       }
     }
+    A *= vsc;
     const int h = hk * G + g;
     if (nsplit == 1) {
       out[(long long)b * out_stride + (long long)h * D + d] = from_f<T>(L > 0.f ? A / L : 0.f);
@@ -275,28 +322,34 @@ __global__ void kv_write_kernel(const T* __restrict__ knew, const T* __restrict_
   }
 }
 
-template <typename T, int D, int G, bool PAGED>
+template <typename T, int D, int G, bool PAGED, typename CT = T>
 static hipError_t launch_attn(const void* q, long long q_stride, const void* q_bias, const Cache& c, const int* lens,
                               const float* mask, long long mask_stride, void* out, long long out_stride, float* ws,
-                              int B, int Hq, int Hkv, int max_len, int nsplit, float scale, hipStream_t st) {
+                              int B, int Hq, int Hkv, int max_len, int nsplit, float scale, hipStream_t st,
+                              const Deq& dq = Deq{}) {
+  if constexpr (D * G > 1024) {
+    return hipErrorInvalidValue;  // outside pa_decode_ok (not instantiated)
+  } else {
   int chunk = (max_len + nsplit - 1) / nsplit;
   chunk = (chunk + 63) / 64 * 64;  // whole 64-position iterations (aligned paged lookups)
   dim3 grid(nsplit, Hkv, B);
-  attn_split_kernel<T, D, G, PAGED><<<grid, 256, 0, st>>>((const T*)q, q_stride, (const T*)q_bias, c, lens, mask,
-                                                          mask_stride, (T*)out, out_stride, ws, Hq, Hkv, nsplit,
-                                                          chunk, scale);
+  attn_split_kernel<T, D, G, PAGED, CT><<<grid, 256, 0, st>>>((const T*)q, q_stride, (const T*)q_bias, c, lens, mask,
+                                                              mask_stride, (T*)out, out_stride, ws, Hq, Hkv, nsplit,
+                                                              chunk, scale, dq);
   if (nsplit > 1) combine_kernel<T, D><<<B * Hq, D, 0, st>>>(ws, (T*)out, out_stride, Hq, nsplit);
   return hipGetLastError();
+  }
 }
 
-template <typename T, int D, bool PAGED>
+template <typename T, int D, bool PAGED, typename CT = T>
 static hipError_t dispatch_g(int G, const void* q, long long q_stride, const void* q_bias, const Cache& c,
                              const int* lens, const float* mask, long long mask_stride, void* out, long long out_stride,
-                             float* ws, int B, int Hq, int Hkv, int max_len, int nsplit, float scale, hipStream_t st) {
-#define PA_DEC_G(GG)                                                                                              \
-  case GG:                                                                                                        \
-    return launch_attn<T, D, GG, PAGED>(q, q_stride, q_bias, c, lens, mask, mask_stride, out, out_stride, ws, B, \
-                                        Hq, Hkv, max_len, nsplit, scale, st);
+                             float* ws, int B, int Hq, int Hkv, int max_len, int nsplit, float scale, hipStream_t st,
+                             const Deq& dq = Deq{}) {
+#define PA_DEC_G(GG)                                                                                                 \
+  case GG:                                                                                                           \
+    return launch_attn<T, D, GG, PAGED, CT>(q, q_stride, q_bias, c, lens, mask, mask_stride, out, out_stride, ws, B, \
+                                            Hq, Hkv, max_len, nsplit, scale, st, dq);
   switch (G) {
     PA_DEC_G(1)
     PA_DEC_G(2)
@@ -357,6 +410,43 @@ PA_API int pa_decode_attn(int dtype, const void* q, long long q_stride, const vo
     PA_DEC_D(pa::f16_t, 256)
   }
 #undef PA_DEC_D
+  return (int)hipErrorInvalidValue;
+}
+
+// Decode over an 8-bit KV cache (cdt 3: int8 q = round(x * quant_scale); 4: uint8 = that + 128),
+// dequantised in the kernel: kscale / vscale [Hkv] (static) or [B, Hkv] (dynamic: scale_b_stride
+// = Hkv).  bf16 queries / outputs, D in {64, 128}; otherwise as pa_decode_attn.
+PA_API int pa_decode_attn_q8(int cdt, const void* q, long long q_stride, const void* q_bias, const void* kc,
+                             const void* vc, const int* block_tables, int max_blocks, int block_size,
+                             long long max_len, const int* lens, const float* mask, long long mask_stride, void* out,
+                             long long out_stride, float* ws, int B, int Hq, int Hkv, int D, int nsplit, float scale,
+                             const float* kscale, const float* vscale, long long scale_b_stride, hipStream_t st) {
+  if (Hkv <= 0 || Hq % Hkv || (cdt != 3 && cdt != 4) || !kscale || !vscale) return (int)hipErrorInvalidValue;
+  const int G = Hq / Hkv;
+  if (!pa_decode_ok(1, D, G) || D == 256 || (nsplit > 1 && !ws)) return (int)hipErrorInvalidValue;
+  Cache c{kc, vc, block_tables, max_blocks, block_size, max_len};
+  Deq dq;
+  dq.ks = kscale;
+  dq.vs = vscale;
+  dq.sb = scale_b_stride;
+  const int span = block_tables ? max_blocks * block_size : (int)max_len;
+  const bool paged = block_tables != nullptr;
+#define PA_DEC_Q(CT, DD)                                                                                             \
+  if (D == DD) {                                                                                                    \
+    if (paged)                                                                                                      \
+      return (int)dispatch_g<pa::bf16_t, DD, true, CT>(G, q, q_stride, q_bias, c, lens, mask, mask_stride, out,      \
+                                                       out_stride, ws, B, Hq, Hkv, span, nsplit, scale, st, dq);     \
+    return (int)dispatch_g<pa::bf16_t, DD, false, CT>(G, q, q_stride, q_bias, c, lens, mask, mask_stride, out,       \
+                                                      out_stride, ws, B, Hq, Hkv, span, nsplit, scale, st, dq);      \
+  }
+  if (cdt == 3) {
+    PA_DEC_Q(int8_t, 64)
+    PA_DEC_Q(int8_t, 128)
+  } else {
+    PA_DEC_Q(uint8_t, 64)
+    PA_DEC_Q(uint8_t, 128)
+  }
+#undef PA_DEC_Q
   return (int)hipErrorInvalidValue;
 }
 

@@ -405,9 +405,9 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     attends to ahead of its own keys (prompts: before the causal prompt block; decode: before the
     paged prefix).  Static int8 KV caches: with ``cache_k_quant_scales`` / ``cache_v_quant_scales``
     ([Hkv]) the new K/V are stored as clip(round(x * quant_scale)) in int8 caches and read back as
-    q * dequant_scale (``cache_*_dequant_scales``); the decode rows then attend over the
-    dequantised pages (composite path).  A uint8 cache stores the value offset by 128 (the
-    reference's layout), an int8 cache stores it as is.  ``use_dynamic_cachekv_quant``: the scales
+    q * dequant_scale (``cache_*_dequant_scales``); the decode rows read the 8-bit pages directly
+    and dequantise inside the HIP decode kernel (a dequantised copy only with pre-caches).  A uint8
+    cache stores the value offset by 128 (the reference's layout), an int8 cache stores it as is.  ``use_dynamic_cachekv_quant``: the scales
     are [B, Hkv] and written here — every prompt sequence of the call gets quant scale
     max_bound / absmax (per head, over all the call's new K resp. V rows, as the reference's
     quant_write_cache_int8_kernel does) and dequant scale absmax / max_bound; decode rows
@@ -497,7 +497,15 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
         rows = cu[:-1][dec_b.long()]
         lens = dec[dec_b.long()] + 1
         tm = None if tgt_mask is None else _u(tgt_mask).reshape(_u(tgt_mask).shape[0], -1)[dec_b.long()].float()
-        if P or qcache:
+        if qcache and not P:
+            # 8-bit pages dequantised inside the decode kernel (scales per KV head or per sequence)
+            def dsc(sc):
+                s_ = _u(sc).float()
+                return s_.reshape(B, Hkv)[dec_b.long()] if use_dynamic_cachekv_quant else s_.reshape(Hkv)
+            out[rows] = ops.decode.decode_attention(q[rows], kc, vc, lens, block_tables=bt[dec_b.long()], mask=tm,
+                                                    k_dequant=dsc(cache_k_dequant_scales),
+                                                    v_dequant=dsc(cache_v_dequant_scales))
+        elif P or qcache:
             # contiguous copies of the decode rows' pages (dequantised), prefix keys in front
             nblk = bt.shape[1]
             pages = bt[dec_b.long()].long()                                   # [n, nblk]

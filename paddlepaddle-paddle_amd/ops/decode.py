@@ -105,15 +105,49 @@ def decode_attention_ref(q, cache_k, cache_v, lens, block_tables=None, mask=None
     return out.to(q.dtype)
 
 
-def decode_attention(q, cache_k, cache_v, lens, block_tables=None, mask=None, q_bias=None, scale=None):
+def _dequant_cache(cache, sc, zero_pt, dtype):
+    """8-bit cache -> (x - zero_pt) * scale; sc [Hkv] or [B, Hkv] (contiguous caches only)."""
+    s_ = sc.float().reshape(-1, cache.shape[1]) if sc.dim() > 1 else sc.float().reshape(1, -1)
+    return ((cache.float() - zero_pt) * s_[:, :, None, None]).to(dtype)
+
+
+def decode_attention(q, cache_k, cache_v, lens, block_tables=None, mask=None, q_bias=None, scale=None,
+                     k_dequant=None, v_dequant=None):
     """One decode step: q [B, Hq, D] (rows may be strided views of a fused qkv) over the cache.
-    lens: int [B] positions to attend (new token included); mask: additive [B, >= max_len] fp32."""
+    lens: int [B] positions to attend (new token included); mask: additive [B, >= max_len] fp32.
+    8-bit caches (int8: round(x * quant_scale); uint8: that + 128) take fp32 dequant scales
+    k_dequant / v_dequant of shape [Hkv] (static) or [B, Hkv] (dynamic, per sequence) and are
+    dequantised inside the kernel (bf16 queries, D 64 / 128)."""
     B, Hq, D = q.shape
     Hkv = cache_k.shape[1]
     scale = 1.0 / math.sqrt(D) if scale is None else float(scale)
     G = Hq // Hkv if Hkv else 0
-    if not (_hip(q, cache_k, cache_v) and Hq % Hkv == 0 and cache_k.is_contiguous() and cache_v.is_contiguous()
-            and q.dtype == cache_k.dtype and N.lib.pa_decode_ok(N.dtcode(q.dtype), D, G)):
+    q8 = cache_k.dtype in (torch.int8, torch.uint8)
+    if q8:
+        if k_dequant is None or v_dequant is None:
+            raise ValueError("an 8-bit KV cache needs k_dequant / v_dequant scales")
+        ks = k_dequant.float().contiguous()
+        vs = v_dequant.float().contiguous()
+        if ks.numel() not in (Hkv, B * Hkv) or vs.numel() != ks.numel():
+            raise ValueError(f"dequant scales must have {Hkv} or {B}x{Hkv} entries, got {ks.numel()} / {vs.numel()}")
+        zp = 128.0 if cache_k.dtype == torch.uint8 else 0.0
+        hip_ok = (_hip(q, cache_k, cache_v, ks, vs) and Hq % Hkv == 0 and cache_k.is_contiguous()
+                  and cache_v.is_contiguous() and cache_v.dtype == cache_k.dtype and q.dtype == torch.bfloat16
+                  and D in (64, 128) and N.lib.pa_decode_ok(N.dtcode(q.dtype), D, G))
+        if not hip_ok:
+            if block_tables is not None:  # gather the pages first, then dequantise
+                nb, bs = block_tables.shape[1], cache_k.shape[2]
+                pg = block_tables.long()
+                cache_k = cache_k[pg].permute(0, 2, 1, 3, 4).reshape(B, Hkv, nb * bs, D)
+                cache_v = cache_v[pg].permute(0, 2, 1, 3, 4).reshape(B, Hkv, nb * bs, D)
+                block_tables = None
+            kd = _dequant_cache(cache_k, ks.reshape(-1, Hkv) if ks.numel() > Hkv else ks, zp, q.dtype)
+            vd = _dequant_cache(cache_v, vs.reshape(-1, Hkv) if vs.numel() > Hkv else vs, zp, q.dtype)
+            if kd.shape[0] != B:
+                kd, vd = kd.expand(B, -1, -1, -1), vd.expand(B, -1, -1, -1)
+            return decode_attention_ref(q, kd, vd, lens, None, mask, q_bias, scale)
+    elif not (_hip(q, cache_k, cache_v) and Hq % Hkv == 0 and cache_k.is_contiguous() and cache_v.is_contiguous()
+              and q.dtype == cache_k.dtype and N.lib.pa_decode_ok(N.dtcode(q.dtype), D, G)):
         return decode_attention_ref(q, cache_k, cache_v, lens, block_tables, mask, q_bias, scale)
     qr, qs = _rows(q)
     lens = lens.to(torch.int32).contiguous()
@@ -123,9 +157,14 @@ def decode_attention(q, cache_k, cache_v, lens, block_tables=None, mask=None, q_
     nsplit = N.lib.pa_decode_nsplit(B, Hkv, span)
     out = torch.empty(B, Hq, D, dtype=q.dtype, device=q.device)
     ws = _ws(B * Hq * nsplit * (D + 2), q.device) if nsplit > 1 else None
-    N.check(N.lib.pa_decode_attn(N.dtcode(q.dtype), N.ptr(qr), qs, N.ptr(None if q_bias is None else q_bias.contiguous()),
-                                 N.ptr(cache_k), N.ptr(cache_v), N.ptr(bt), 0 if bt is None else bt.shape[1],
-                                 cache_k.shape[2], 0 if bt is not None else cache_k.shape[2], N.ptr(lens), N.ptr(msk),
-                                 0 if msk is None else msk.stride(0), N.ptr(out), Hq * D, N.ptr(ws), B, Hq, Hkv, D,
-                                 nsplit, scale, N.stream()), 'decode_attn')
+    qb = N.ptr(None if q_bias is None else q_bias.contiguous())
+    common = (N.ptr(cache_k), N.ptr(cache_v), N.ptr(bt), 0 if bt is None else bt.shape[1], cache_k.shape[2],
+              0 if bt is not None else cache_k.shape[2], N.ptr(lens), N.ptr(msk),
+              0 if msk is None else msk.stride(0), N.ptr(out), Hq * D, N.ptr(ws), B, Hq, Hkv, D, nsplit, scale)
+    if q8:
+        N.check(N.lib.pa_decode_attn_q8(3 if cache_k.dtype == torch.int8 else 4, N.ptr(qr), qs, qb, *common,
+                                        N.ptr(ks), N.ptr(vs), Hkv if ks.numel() > Hkv else 0, N.stream()),
+                'decode_attn_q8')
+    else:
+        N.check(N.lib.pa_decode_attn(N.dtcode(q.dtype), N.ptr(qr), qs, qb, *common, N.stream()), 'decode_attn')
     return out

@@ -70,6 +70,36 @@ def test_decode_attention_paged_equals_contiguous():
     np.testing.assert_allclose(a.numpy(), p.numpy(), rtol=1e-5, atol=1e-6)
 
 
+def test_decode_attention_int8_cache_matches_dequantised():
+    """8-bit caches (int8 / uint8 with zero point 128; static [Hkv] and per-sequence [B, Hkv]
+    dequant scales, paged and contiguous) == attention over the dequantised bf16 / fp32 cache."""
+    torch.manual_seed(3)
+    B, Hq, Hkv, D, bs, L = 2, 4, 2, 8, 4, 12
+    for cdt, zp in ((torch.int8, 0), (torch.uint8, 128)):
+        for dyn in (False, True):
+            kq = torch.randint(-127, 128, (B, Hkv, L, D))
+            vq = torch.randint(-127, 128, (B, Hkv, L, D))
+            ks = torch.rand((B, Hkv) if dyn else (Hkv,)) * 0.05 + 0.01
+            vs = torch.rand((B, Hkv) if dyn else (Hkv,)) * 0.05 + 0.01
+            q = torch.randn(B, Hq, D)
+            lens = torch.tensor([5, 12])
+            kd = kq.float() * ks.reshape(-1, Hkv)[:, :, None, None]
+            vd = vq.float() * vs.reshape(-1, Hkv)[:, :, None, None]
+            want = decode.decode_attention_ref(q, kd.expand(B, -1, -1, -1), vd.expand(B, -1, -1, -1), lens)
+            got = decode.decode_attention(q, (kq + zp).to(cdt), (vq + zp).to(cdt), lens, k_dequant=ks, v_dequant=vs)
+            np.testing.assert_allclose(got.numpy(), want.numpy(), rtol=1e-5, atol=1e-6)
+            nblk = B * L // bs
+            bt = torch.randperm(nblk).reshape(B, L // bs)
+            kp = torch.empty(nblk, Hkv, bs, D, dtype=cdt)
+            vp = torch.empty(nblk, Hkv, bs, D, dtype=cdt)
+            for b in range(B):
+                for j in range(L // bs):
+                    kp[bt[b, j]] = (kq[b, :, j * bs:(j + 1) * bs] + zp).to(cdt)
+                    vp[bt[b, j]] = (vq[b, :, j * bs:(j + 1) * bs] + zp).to(cdt)
+            got = decode.decode_attention(q, kp, vp, lens, block_tables=bt, k_dequant=ks, v_dequant=vs)
+            np.testing.assert_allclose(got.numpy(), want.numpy(), rtol=1e-5, atol=1e-6)
+
+
 def _get_padding_offset(this):
     cu = torch.zeros(len(this) + 1, dtype=torch.int32)
     cu[1:] = torch.cumsum(torch.tensor(this), 0)

@@ -1295,6 +1295,41 @@ def test_hip_decode_attention(dt, D, Hq, Hkv, paged):
     _close(out, ref, atol=2e-2, rtol=2e-2, name=f"decode D{D} G{Hq // Hkv} paged={paged}")
 
 
+@pytest.mark.parametrize("cdt", [torch.int8, torch.uint8])
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 8, 8), (128, 32, 8), (64, 16, 2)])
+@pytest.mark.parametrize("paged,dynamic", [(False, False), (True, False), (True, True)])
+def test_hip_decode_attention_int8_cache(cdt, D, Hq, Hkv, paged, dynamic):
+    """pa_decode_attn_q8: 8-bit KV caches dequantised inside the decode kernel (K scale folded into
+    the query, V scale on the merged accumulator; uint8 zero point 128), static [Hkv] and dynamic
+    [B, Hkv] scales, vs the fp32 reference over the dequantised cache."""
+    from paddle.ops import decode
+    g = torch.Generator(device=DEV).manual_seed(D * 7 + Hq + Hkv)
+    B, L, bs = 4, 900, 64
+    lens = torch.tensor([1, 300, 900, 129], device=DEV, dtype=torch.int32)
+    zp = 128 if cdt == torch.uint8 else 0
+    shape = (B * ((L + bs - 1) // bs) + 4, Hkv, bs, D) if paged else (B, Hkv, L, D)
+    kc = (torch.randint(-127, 128, shape, device=DEV, generator=g) + zp).to(cdt)
+    vc = (torch.randint(-127, 128, shape, device=DEV, generator=g) + zp).to(cdt)
+    bt = (torch.randperm(shape[0], device=DEV, generator=g)[:B * ((L + bs - 1) // bs)].reshape(B, -1).int()
+          if paged else None)
+    sshape = (B, Hkv) if dynamic else (Hkv,)
+    ks = torch.rand(sshape, device=DEV, generator=g) * 0.02 + 0.005
+    vs = torch.rand(sshape, device=DEV, generator=g) * 0.02 + 0.005
+    q = torch.randn(B, Hq, D, device=DEV, generator=g).bfloat16()
+    mask = torch.where(torch.rand(B, L, device=DEV, generator=g) < 0.1, -1e4, 0.0).float()
+    out = decode.decode_attention(q, kc, vc, lens, block_tables=bt, mask=mask, k_dequant=ks, v_dequant=vs)
+
+    def deq(c, s_):
+        s_ = s_.reshape(-1, Hkv)
+        if paged:  # per-sequence scales: dequantise each sequence's gathered pages
+            pg = bt.long()
+            c = c[pg].permute(0, 2, 1, 3, 4).reshape(B, Hkv, -1, D)
+        return (c.float() - zp) * s_[:, :, None, None]
+    ref = decode.decode_attention_ref(q, deq(kc, ks).expand(B, -1, -1, -1), deq(vc, vs).expand(B, -1, -1, -1),
+                                      lens, mask=mask)
+    _close(out, ref, atol=2e-2, rtol=2e-2, name=f"decode q8 {cdt} D{D} G{Hq // Hkv} paged={paged} dyn={dynamic}")
+
+
 def test_hip_kv_cache_write_and_fused_multi_transformer_decode():
     """pa_kv_cache_write + the HIP decode kernel inside fused_multi_transformer: incremental decode on
     the GPU matches the full causal forward."""
