@@ -322,6 +322,33 @@ __global__ void kv_write_kernel(const T* __restrict__ knew, const T* __restrict_
   }
 }
 
+// Quantising variant for 8-bit caches: q = clip(round(x * quant_scale), qmin, qmax) (+128 for
+// uint8), quant scales per KV head (sb = 0) or per (sequence, head) (sb = Hkv).  round_type 0:
+// half to even (rint), 1: half away from zero.
+template <typename T, bool PAGED, typename CT>
+__global__ void kv_write_q8_kernel(const T* __restrict__ knew, const T* __restrict__ vnew, long long kv_stride,
+                                   Cache cache, const int* __restrict__ seq_of, const int* __restrict__ pos, int Hkv,
+                                   int D, const float* __restrict__ kqs, const float* __restrict__ vqs, long long sb,
+                                   int round_type, float qmax, float qmin) {
+  const int r = blockIdx.x, hk = blockIdx.y;
+  const int b = seq_of ? seq_of[r] : r;
+  const int p = pos[r];
+  if (p < 0) return;
+  const long long o = pos_off<PAGED>(cache, b, hk, Hkv, p, D);
+  CT* kc = reinterpret_cast<CT*>(const_cast<void*>(cache.k));
+  CT* vc = reinterpret_cast<CT*>(const_cast<void*>(cache.v));
+  const float ks = kqs[(long long)b * sb + hk], vs = vqs[(long long)b * sb + hk];
+  const float zp = sizeof(CT) == 1 && CT(-1) > CT(0) ? 128.f : 0.f;  // unsigned cache: offset by 128
+  auto qz = [&](float x) {
+    const float y = round_type == 0 ? rintf(x) : roundf(x);
+    return CT(fminf(fmaxf(y, qmin), qmax) + zp);
+  };
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    kc[o + d] = qz(to_f(knew[(long long)r * kv_stride + (long long)hk * D + d]) * ks);
+    vc[o + d] = qz(to_f(vnew[(long long)r * kv_stride + (long long)hk * D + d]) * vs);
+  }
+}
+
 template <typename T, int D, int G, bool PAGED, typename CT = T>
 static hipError_t launch_attn(const void* q, long long q_stride, const void* q_bias, const Cache& c, const int* lens,
                               const float* mask, long long mask_stride, void* out, long long out_stride, float* ws,
@@ -411,6 +438,39 @@ PA_API int pa_decode_attn(int dtype, const void* q, long long q_stride, const vo
   }
 #undef PA_DEC_D
   return (int)hipErrorInvalidValue;
+}
+
+// Quantising cache write into an 8-bit cache (cdt 3: int8, 4: uint8 with zero point 128): rows of
+// knew / vnew (dtype 1 bf16 / 2 fp16, stride kv_stride) at pos[r] of sequence seq_of[r];
+// quant scales kqs / vqs [Hkv] (scale_b_stride 0) or [B, Hkv] (scale_b_stride Hkv).
+PA_API int pa_kv_cache_write_q8(int dtype, int cdt, const void* knew, const void* vnew, long long kv_stride, void* kc,
+                                void* vc, const int* block_tables, int max_blocks, int block_size, long long max_len,
+                                const int* seq_of, const int* pos, int R, int Hkv, int D, const float* kqs,
+                                const float* vqs, long long scale_b_stride, int round_type, float qmax, float qmin,
+                                hipStream_t st) {
+  if (R <= 0) return 0;
+  if ((dtype != 1 && dtype != 2) || (cdt != 3 && cdt != 4) || !kqs || !vqs || Hkv <= 0 || D <= 0)
+    return (int)hipErrorInvalidValue;
+  Cache c{kc, vc, block_tables, max_blocks, block_size, max_len};
+  dim3 grid(R, Hkv);
+  const int th = D >= 256 ? 256 : (D + 63) / 64 * 64;
+#define PA_KVQ(TT, CT, PG)                                                                                      \
+  kv_write_q8_kernel<TT, PG, CT><<<grid, th, 0, st>>>((const TT*)knew, (const TT*)vnew, kv_stride, c, seq_of, pos, \
+                                                       Hkv, D, kqs, vqs, scale_b_stride, round_type, qmax, qmin)
+#define PA_KVQ_T(TT)                                                           \
+  if (cdt == 3) {                                                              \
+    if (block_tables) PA_KVQ(TT, int8_t, true); else PA_KVQ(TT, int8_t, false);  \
+  } else {                                                                     \
+    if (block_tables) PA_KVQ(TT, uint8_t, true); else PA_KVQ(TT, uint8_t, false); \
+  }
+  if (dtype == 1) {
+    PA_KVQ_T(pa::bf16_t)
+  } else {
+    PA_KVQ_T(pa::f16_t)
+  }
+#undef PA_KVQ_T
+#undef PA_KVQ
+  return (int)hipGetLastError();
 }
 
 // Decode over an 8-bit KV cache (cdt 3: int8 q = round(x * quant_scale); 4: uint8 = that + 128),

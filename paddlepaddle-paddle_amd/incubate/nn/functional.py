@@ -458,16 +458,9 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
                     qv[pre] = (quant_max_bound / amax).to(qv.dtype)
                     dv[pre] = (amax / quant_max_bound).to(dv.dtype)
 
-        def qz(x, sc):
-            s_ = _u(sc).float()
-            s_ = s_.reshape(B, Hkv)[seq_of.long()][:, :, None] if use_dynamic_cachekv_quant else s_.reshape(1, -1, 1)
-            v_ = x.float() * s_
-            v_ = torch.round(v_) if quant_round_type == 0 else torch.sign(v_) * torch.floor(v_.abs() + 0.5)
-            return (v_.clamp(quant_min_bound, quant_max_bound) + zero_pt).to(kc.dtype)
-        blk = bt[seq_of.long(), (pos // bs).long()].long()
-        off = (pos % bs).long()
-        kc[blk, :, off] = qz(k, cache_k_quant_scales)
-        vc[blk, :, off] = qz(v, cache_v_quant_scales)
+        ops.decode.kv_cache_write_q8(k, v, kc, vc, pos, _u(cache_k_quant_scales), _u(cache_v_quant_scales),
+                                     seq_of=seq_of, block_tables=bt, round_type=quant_round_type,
+                                     qmax=quant_max_bound, qmin=quant_min_bound)
     else:
         ops.decode.kv_cache_write(k, v, kc, vc, pos, seq_of=seq_of, block_tables=bt)
     out = torch.empty(T, Hq, D, dtype=t.dtype, device=dev)

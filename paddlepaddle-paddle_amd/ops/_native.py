@@ -108,6 +108,7 @@ _SIGS = {
     'pa_decode_attn': [I, P, LL, P, P, P, P, I, I, LL, P, P, LL, P, LL, P, I, I, I, I, I, F, P],
     'pa_decode_attn_q8': [I, P, LL, P, P, P, P, I, I, LL, P, P, LL, P, LL, P, I, I, I, I, I, F, P, P, LL, P],
     'pa_kv_cache_write': [I, P, P, LL, P, P, P, P, P, I, I, LL, P, P, I, I, I, P],
+    'pa_kv_cache_write_q8': [I, I, P, P, LL, P, P, P, I, I, LL, P, P, I, I, I, P, P, LL, I, F, F, P],
     'pa_flash_fwd': [P, P, P, P, P, I, I, I, I, I, I, LLP, LLP, LLP, LLP, F, I, I, P],
     'pa_flash_bwd': [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, LLP, LLP, LLP, LLP, LLP, LLP, LLP, LLP, F, I, I,
                      P],

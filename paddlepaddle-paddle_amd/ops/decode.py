@@ -74,6 +74,53 @@ def kv_cache_write(k_new, v_new, cache_k, cache_v, pos, seq_of=None, block_table
             cache_v[blk, :, p % bs] = vb[r].to(cache_v.dtype)
 
 
+def kv_cache_write_q8(k_new, v_new, cache_k, cache_v, pos, k_quant, v_quant, seq_of=None, block_tables=None,
+                      round_type=0, qmax=127.0, qmin=-127.0):
+    """Quantising cache write into an int8 / uint8 cache: clip(round(x * quant_scale), qmin, qmax)
+    (+128 for uint8).  k_quant / v_quant: [Hkv] (static) or [B, Hkv] (per sequence, indexed by
+    seq_of[r]).  round_type 0 rounds half to even, 1 half away from zero."""
+    R, Hkv, D = k_new.shape
+    pos = pos.to(torch.int32).contiguous()
+    seq_of = None if seq_of is None else seq_of.to(torch.int32).contiguous()
+    kq, vq = k_quant.float().contiguous(), v_quant.float().contiguous()
+    dyn = kq.numel() > Hkv
+    if _hip(k_new, v_new, cache_k, cache_v, kq, vq) and cache_k.is_contiguous() and cache_v.is_contiguous() and \
+            k_new.dtype in (torch.bfloat16, torch.float16) and cache_k.dtype in (torch.int8, torch.uint8) and \
+            cache_v.dtype == cache_k.dtype:
+        kn, ks = _rows(k_new)
+        vn, vs = _rows(v_new)
+        if ks != vs:
+            kn, vn = kn.contiguous(), vn.contiguous()
+            ks = kn.stride(0)
+        bt = None if block_tables is None else block_tables.to(torch.int32).contiguous()
+        N.check(N.lib.pa_kv_cache_write_q8(N.dtcode(kn.dtype), 3 if cache_k.dtype == torch.int8 else 4, N.ptr(kn),
+                                           N.ptr(vn), ks, N.ptr(cache_k), N.ptr(cache_v), N.ptr(bt),
+                                           0 if bt is None else bt.shape[1], cache_k.shape[2],
+                                           0 if bt is not None else cache_k.shape[2], N.ptr(seq_of), N.ptr(pos), R,
+                                           Hkv, D, N.ptr(kq), N.ptr(vq), Hkv if dyn else 0, int(round_type),
+                                           float(qmax), float(qmin), N.stream()), 'kv_cache_write_q8')
+        return
+    zp = 128.0 if cache_k.dtype == torch.uint8 else 0.0
+    sq = (torch.arange(R, device=k_new.device) if seq_of is None else seq_of).long()
+
+    def qz(x, sc):
+        s_ = sc.reshape(-1, Hkv)[sq][:, :, None] if dyn else sc.reshape(1, Hkv, 1)
+        y = x.float() * s_
+        y = torch.round(y) if round_type == 0 else torch.sign(y) * torch.floor(y.abs() + 0.5)
+        return (y.clamp(qmin, qmax) + zp).to(cache_k.dtype)
+    kk, vv = qz(k_new, kq), qz(v_new, vq)
+    ok = pos >= 0
+    p_, b_ = pos.long()[ok], sq[ok]
+    if block_tables is None:
+        cache_k[b_, :, p_] = kk[ok]
+        cache_v[b_, :, p_] = vv[ok]
+    else:
+        bs = cache_k.shape[2]
+        blk = block_tables.long()[b_, p_ // bs]
+        cache_k[blk, :, p_ % bs] = kk[ok]
+        cache_v[blk, :, p_ % bs] = vv[ok]
+
+
 def _gather_cache(cache, b, L, block_tables):
     """[Hkv, L, D] view of sequence b's first L positions."""
     if block_tables is None:

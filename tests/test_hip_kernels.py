@@ -1330,6 +1330,35 @@ def test_hip_decode_attention_int8_cache(cdt, D, Hq, Hkv, paged, dynamic):
     _close(out, ref, atol=2e-2, rtol=2e-2, name=f"decode q8 {cdt} D{D} G{Hq // Hkv} paged={paged} dyn={dynamic}")
 
 
+@pytest.mark.parametrize("cdt", [torch.int8, torch.uint8])
+@pytest.mark.parametrize("paged,dynamic,rt", [(True, False, 0), (True, True, 1), (False, False, 1)])
+def test_hip_kv_cache_write_q8(cdt, paged, dynamic, rt):
+    """pa_kv_cache_write_q8 (quantising write into an 8-bit cache) == the torch composite, exactly."""
+    from paddle.ops import decode
+    g = torch.Generator(device=DEV).manual_seed(11)
+    R, Hkv, D, bs, B = 37, 4, 128, 16, 3
+    k = (torch.randn(R, Hkv, D, device=DEV, generator=g) * 3).bfloat16()
+    v = (torch.randn(R, Hkv, D, device=DEV, generator=g) * 3).bfloat16()
+    seq = torch.randint(0, B, (R,), device=DEV, generator=g).int()
+    pos = torch.randperm(64, device=DEV, generator=g)[:R].int()
+    pos[5] = -1
+    if paged:
+        shape, bt = (B * 4 + 2, Hkv, bs, D), torch.randperm(B * 4 + 2, device=DEV, generator=g)[:B * 4].reshape(B, 4).int()
+    else:
+        shape, bt = (B, Hkv, 64, D), None
+    sshape = (B, Hkv) if dynamic else (Hkv,)
+    kq = torch.rand(sshape, device=DEV, generator=g) * 40 + 1
+    vq = torch.rand(sshape, device=DEV, generator=g) * 40 + 1
+    kc = torch.zeros(shape, dtype=cdt, device=DEV)
+    vc = torch.zeros(shape, dtype=cdt, device=DEV)
+    kr, vr = kc.cpu(), vc.cpu()
+    decode.kv_cache_write_q8(k, v, kc, vc, pos, kq, vq, seq_of=seq, block_tables=bt, round_type=rt)
+    decode.kv_cache_write_q8(k.cpu(), v.cpu(), kr, vr, pos.cpu(), kq.cpu(), vq.cpu(), seq_of=seq.cpu(),
+                             block_tables=None if bt is None else bt.cpu(), round_type=rt)
+    assert torch.equal(kc.cpu(), kr) and torch.equal(vc.cpu(), vr)
+    assert int((kr != (128 if cdt == torch.uint8 else 0)).sum()) > 0
+
+
 def test_hip_kv_cache_write_and_fused_multi_transformer_decode():
     """pa_kv_cache_write + the HIP decode kernel inside fused_multi_transformer: incremental decode on
     the GPU matches the full causal forward."""
