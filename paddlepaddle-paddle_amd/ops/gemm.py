@@ -296,10 +296,11 @@ _kmajor_fwd = os.environ.get('PADDLE_AMD_KMAJOR_FWD', '1') != '0'
 def kmajor_weight(x2, w):
     """K-major copy W^T ([out, in]) of a paddle [in, out] weight for the forward GEMM, or None.
 
-    hipBLASLt runs y = x @ W (B operand N-major) at 1.06-1.39 PF/s on the GPT-3 1.3B shapes but
-    y = x @ (W^T)^T (both operands K-major, the dgrad layout) at 1.25-1.59 PF/s
-    (tools/fwd_layout_bench.py, profiles/fwd_layout_r1.log); the transpose of a 2048x8192 weight
-    costs ~15 us, so the copy pays off once the token count is large (training micro-batches).
+    Both operands K-major is the hand-written GEMM's fastest layout (an LDS-staged N-major B tile
+    needs a transposing read); the transpose of a 2048x8192 weight costs ~15 us, so the copy pays
+    off once the token count is large (training micro-batches): GPT-3 1.3B step 129.1-129.5 ms with
+    the copies vs 130.2-130.5 ms reading W directly (profiles/r3s3_kmajor_fwd_ab.log; round 1's
+    hipBLASLt measurement: profiles/fwd_layout_r1.log).
     """
     if not _kmajor_fwd or x2.shape[0] < 4096 or w.dtype not in (torch.bfloat16, torch.float16):
         return None
