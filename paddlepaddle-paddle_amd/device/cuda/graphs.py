@@ -134,8 +134,10 @@ class TrainStepGraph:
     the step is graph-safe: the HIP dropout kernels mix a device-resident generation counter into
     their host-drawn seeds (csrc/common.h rng_mix), and the captured graph advances that counter as
     its first node, so every replay draws fresh keep-masks (a step's backward still regenerates its
-    forward's); the learning rate must stay constant or live in a device tensor.  Returns the
-    static loss tensor (its value updates on every replay).
+    forward's).  The fused optimizers read their learning rate from a device scalar that an
+    ``on_replay`` hook refills from ``get_lr()`` before each replay (LR schedulers stepped on the
+    host between calls take effect), and their host step counters advance after each replay.
+    Returns the static loss tensor (its value updates on every replay).
     """
 
     def __init__(self, step_fn, warmup=3):
@@ -144,12 +146,25 @@ class TrainStepGraph:
         self.calls = 0
         self.graph = None
         self.out = None
+        self.hooks = []  # (pre, post) host callbacks registered through on_replay() during capture
+        self.replays = 0
+
+    def _pre(self):
+        for pre, _ in self.hooks:
+            if pre is not None:
+                pre()
 
     def __call__(self):
+        global _CAPTURE_HOOKS
         if not torch.cuda.is_available():
             return self.step_fn()
         if self.graph is not None:
+            self._pre()
             self.graph.replay()
+            self.replays += 1
+            for _, post in self.hooks:
+                if post is not None:
+                    post()
             return self.out
         self.calls += 1
         if self.calls <= self.warmup:
@@ -162,6 +177,7 @@ class TrainStepGraph:
         gen = install_rng_generation()
         torch.cuda.synchronize()
         g = CUDAGraph()
+        hooks, _CAPTURE_HOOKS = [], []
         g.capture_begin()
         try:
             if gen is not None:
@@ -169,9 +185,34 @@ class TrainStepGraph:
             self.out = self.step_fn()
         finally:
             g.capture_end()
+            hooks, _CAPTURE_HOOKS = _CAPTURE_HOOKS, None
+        self.hooks = hooks
         self.graph = g
-        g.replay()  # the captured step has not executed yet: run it once for this call
+        # the captured step has not executed yet: run it once for this call (its host-side
+        # bookkeeping already ran during the capture, so no post hooks for this one)
+        self._pre()
+        g.replay()
+        self.replays = 1
         return self.out
+
+
+_CAPTURE_HOOKS = None  # list while a TrainStepGraph captures, else None
+
+
+def on_replay(pre=None, post=None):
+    """Register host callbacks with the TrainStepGraph being captured.
+
+    ``pre()`` runs before every replay and refreshes device-resident scalars from host state (the
+    optimizers fill their device learning rate from ``get_lr()``, so an LR scheduler stepped on the
+    host between replays takes effect); ``post()`` runs after every replay but the first and
+    advances host counters whose update the captured step's Python code performed once, at capture
+    (optimizer step counts, host copies of the bias-correction powers).  Returns True when a
+    capture took the hooks; False (nothing registered) outside a TrainStepGraph capture, where a
+    caller keeps its host values (frozen into a raw ``CUDAGraph``)."""
+    if _CAPTURE_HOOKS is None:
+        return False
+    _CAPTURE_HOOKS.append((pre, post))
+    return True
 
 
 def capture_train_step(step_fn, warmup=3):

@@ -28,11 +28,13 @@ def sumsq(x):
     return parts.sum()
 
 
-def momentum_flat(master, grad, velocity, lowp, lr, mu, l2=0.0, rescale=1.0, nesterov=False, grad_scale=None):
-    """Fused momentum over flat buffers (csrc/embed_rope_optim.hip momentum_kernel)."""
+def momentum_flat(master, grad, velocity, lowp, lr, mu, l2=0.0, rescale=1.0, nesterov=False, grad_scale=None,
+                  lr_tensor=None):
+    """Fused momentum over flat buffers (csrc/embed_rope_optim.hip momentum_kernel).  ``lr_tensor``: a
+    device fp32 [1] learning rate read by the kernel instead of ``lr`` (captured steps)."""
     n = master.numel()
     assert grad.numel() == n and velocity.numel() == n
     pd = -1 if lowp is None else N.dtcode(lowp.dtype)
-    N.check(N.lib.pa_momentum(N.ptr(master), N.ptr(grad), N.ptr(velocity), N.ptr(lowp), n, None, float(lr), float(mu),
+    N.check(N.lib.pa_momentum(N.ptr(master), N.ptr(grad), N.ptr(velocity), N.ptr(lowp), n, N.ptr(lr_tensor), float(lr), float(mu),
                               float(l2), float(rescale), int(bool(nesterov)), N.ptr(grad_scale), N.dtcode(grad.dtype),
                               pd, N.stream()), 'momentum')

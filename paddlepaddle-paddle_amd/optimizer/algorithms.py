@@ -117,11 +117,16 @@ class Momentum(Optimizer):
                 if clip is not None:
                     clip(self._params_grads(group))
             lr = self.get_lr()
+            dev_lr = _graph_lr(self, self._flat, self._advance_host_step)
             for ent in self._flat:
                 fb = ent['fb']
                 glr = lr * self._param_groups[ent['group']].get('learning_rate', 1.0)
                 ops.optim.momentum_flat(ent['master'], fb.grad, ent['v'], fb.data if fb.dtype != torch.float32 else None,
-                                        glr, self._momentum, ent['l2'], self._rescale, self._use_nesterov)
+                                        glr, self._momentum, ent['l2'], self._rescale, self._use_nesterov,
+                                        lr_tensor=ent['lr_dev'] if dev_lr else None)
+        self._global_step += 1
+
+    def _advance_host_step(self):
         self._global_step += 1
 
     def clear_grad(self, set_to_zero=True):
@@ -241,6 +246,7 @@ class Adam(Optimizer):
                 fb.sync_grads()
             scale = self._clip_flat()
             capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+            dev_lr = _graph_lr(self, self._flat, self._advance_host_step)
             for ent in self._flat:
                 fb = ent['fb']
                 glr = lr * self._param_groups[ent['group']].get('learning_rate', 1.0)
@@ -248,12 +254,20 @@ class Adam(Optimizer):
                 pows = _device_pows(ent, self._beta1, self._beta2, fb.device, capturing)
                 ops.optim.adamw_flat(ent['master'], fb.grad, ent['m1'], ent['m2'], lowp, glr, self._beta1,
                                      self._beta2, self._epsilon, ent['coeff'], ent['b1p'], ent['b2p'],
+                                     lr_tensor=ent['lr_dev'] if dev_lr else None,
                                      grad_scale=scale, pows=pows if capturing else None)
                 ent['b1p'] *= self._beta1
                 ent['b2p'] *= self._beta2
                 if pows is not None:
                     pows.mul_(ent['betas'])
                     ent['graph_stepped'] = ent.get('graph_stepped', False) or capturing
+        self._global_step += 1
+
+    def _advance_host_step(self):
+        # a replay of a captured step: the device powers advanced in the graph, the host copies here
+        for ent in self._flat or ():
+            ent['b1p'] *= self._beta1
+            ent['b2p'] *= self._beta2
         self._global_step += 1
 
     def _clip_flat(self):
@@ -329,6 +343,34 @@ class Adam(Optimizer):
                         ent['b2p'] = float(b2.reshape(-1)[0])
                 if ent.get('pows') is not None:
                     ent['pows'].copy_(torch.tensor([ent['b1p'], ent['b2p']]))
+
+
+def _graph_lr(opt, ents, post):
+    """Learning rate as a device scalar for a step being captured by a TrainStepGraph
+    (device/cuda/graphs.py on_replay): each flat-buffer entry holds an fp32 [1] ``lr_dev`` that the
+    graph's pre-replay hook refills from ``opt.get_lr()`` (times the group multiplier), so a host
+    LR scheduler keeps working across replays; ``post`` advances the optimizer's host counters
+    after each replay.  False (use the host value) when nothing is being captured that way.
+
+    ``lr_dev`` is allocated on an eager step, never inside the capture: a block taken from the
+    graph's private pool may be one a temporary earlier in the same step used, which the replay
+    would overwrite after the pre-replay fill."""
+    if not torch.cuda.is_available():
+        return False
+    if not torch.cuda.is_current_stream_capturing():
+        for ent in ents:
+            if ent.get('lr_dev') is None and ent['fb'].device.type == 'cuda':
+                ent['lr_dev'] = torch.zeros(1, dtype=torch.float32, device=ent['fb'].device)
+        return False
+    if any(ent.get('lr_dev') is None for ent in ents):
+        return False  # captured without an eager step first: host value (frozen)
+    from ..device.cuda.graphs import on_replay
+
+    def pre():
+        lr = opt.get_lr()
+        for ent in ents:
+            ent['lr_dev'].fill_(lr * opt._param_groups[ent['group']].get('learning_rate', 1.0))
+    return on_replay(pre=pre, post=post)
 
 
 def _device_pows(ent, b1, b2, device, capturing):

@@ -631,7 +631,7 @@ class ShardedOptimizer:
                     upd = g + mu * v if nesterov else v
                 else:
                     upd = g
-                master.sub_(lr * upd)
+                master.sub_(upd * lr if torch.is_tensor(lr) else lr * upd)
                 if lowp is not None:
                     lowp[lo:hi].copy_(master.to(dt))
 
@@ -640,9 +640,10 @@ class ShardedOptimizer:
         opt = self._inner
         self._step += 1
         lr = opt.get_lr()
+        lr_dev = self._graph_lr()
         scale = self._clip_scale()
         if self._kind in ('SGD', 'Momentum'):
-            self._step_sgd_momentum(lr, scale)
+            self._step_sgd_momentum(lr if lr_dev is None else lr_dev, scale)
             self.engine.gather_params_after_step()
             opt._global_step += 1
             return
@@ -667,7 +668,7 @@ class ShardedOptimizer:
                 if ops.use_hip(a['master']):
                     ops.optim.adamw_flat(a['master'][lo:hi], g[lo:hi], a['m'][lo:hi], a['v'][lo:hi],
                                          None if lowp is None else lowp[lo:hi], lr, b1, b2, eps, coeff, b1p, b2p,
-                                         grad_scale=scale, pows=pows if capturing else None)
+                                         lr_tensor=lr_dev, grad_scale=scale, pows=pows if capturing else None)
                 else:
                     _adamw_ref(a['master'][lo:hi], g[lo:hi], a['m'][lo:hi], a['v'][lo:hi],
                                None if lowp is None else lowp[lo:hi], lr, b1, b2, eps, coeff, b1p, b2p)
@@ -675,6 +676,31 @@ class ShardedOptimizer:
             pows.mul_(self._betas)
         self.engine.gather_params_after_step()
         opt._global_step += 1
+
+    def _graph_lr(self):
+        """Device fp32 [1] learning rate while a TrainStepGraph captures this step: refilled from
+        the inner optimizer's get_lr() before every replay; the host step counters advance after
+        each replay (device/cuda/graphs.py on_replay).  None otherwise (host value).  Allocated on
+        an eager step, not from the capture's private pool (a block an earlier temporary of the
+        captured step used would be overwritten by the replay after the pre-replay fill)."""
+        if not torch.cuda.is_available():
+            return None
+        lr_dev = getattr(self, '_lr_dev', None)
+        if not torch.cuda.is_current_stream_capturing():
+            if lr_dev is None and self.engine.arenas:
+                dev = next(iter(self.engine.arenas.values()))['master'].device
+                if dev.type == 'cuda':
+                    self._lr_dev = torch.zeros(1, dtype=torch.float32, device=dev)
+            return None
+        if lr_dev is None:
+            return None
+        from ..device.cuda.graphs import on_replay
+        opt = self._inner
+
+        def post():
+            self._step += 1
+            opt._global_step += 1
+        return lr_dev if on_replay(pre=lambda: lr_dev.fill_(opt.get_lr()), post=post) else None
 
     def clear_grad(self, set_to_zero=True):
         self.engine.zero_grad()
