@@ -550,32 +550,8 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const uint16_t* __restrict_
 }
 
 // ============================================================================ backward
-// delta[b, h, q] = sum_d dO[q, d] * O[q, d]   (one 16-lane group per row)
-template <typename T, int D>
-__global__ __launch_bounds__(256) void bwd_delta_kernel(const uint16_t* __restrict__ dO, const uint16_t* __restrict__ O,
-                                                        float* __restrict__ delta, int B, int Sq, int Hq, Strides dos,
-                                                        Strides os) {
-  const int rid = blockIdx.x * 16 + (threadIdx.x >> 4);
-  const int sub = threadIdx.x & 15;
-  const long long nrows = (long long)B * Hq * Sq;
-  if (rid >= nrows) return;
-  const int q = rid % Sq;
-  const int h = (rid / Sq) % Hq;
-  const int b = rid / (Sq * Hq);
-  const uint16_t* dp = dO + b * dos.b + h * dos.h + (long long)q * dos.s;
-  const uint16_t* op = O + b * os.b + h * os.h + (long long)q * os.s;
-  float s = 0.f;
-  for (int j = sub * 8; j < D; j += 128) {
-    float a[8], c[8];
-    load_f<T, 8>((const T*)(dp + j), a);
-    load_f<T, 8>((const T*)(op + j), c);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s += a[e] * c[e];
-  }
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
-  if (sub == 0) delta[rid] = s;
-}
+// delta[b, h, q] = sum_d dO[q, d] * O[q, d] is computed inside bwd_dq_kernel (launched before the
+// dK/dV kernel, which reads the stored rows); there is no separate delta pass.
 
 // dK/dV: grid (ceil(Sk / (16*NT*NW)), Hq, B); NW waves x (16*NT) keys; loop over 64-query blocks.
 // NW = 8 doubles the keys that share each staged Q/dO tile (halving the Q/dO re-reads from
@@ -843,9 +819,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dkdv_kernel
 template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0, bool PIPE = false>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
-    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
     uint16_t* __restrict__ dQ, int Sq_, int Sk_, int Hq, int Hk, Strides qs, Strides ks_, Strides vs, Strides dos,
-    Strides dqs, float scale, Extra ex = Extra{}) {
+    Strides dqs, float scale, Extra ex = Extra{}, const uint16_t* __restrict__ O = nullptr, Strides os = Strides{}) {
   if constexpr ((EXT & 4) != 0) ex.seed = rng_mix(ex.seed);  // graph-captured steps: per-replay stream
   constexpr int KS = D / 32;
   constexpr int DB = D / 16;
@@ -873,8 +849,13 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
   const bool vl = EXT && ex.cu_q;
   Q += (vl ? 0 : b * qs.b) + sq_.qo * qs.s;
   dO += (vl ? 0 : b * dos.b) + sq_.qo * dos.s;
+  // O != null: delta = rowsum(dO * O) is computed here from the dO fragments this kernel holds
+  // anyway (lane: 8 * KS elements of its query row; the 4 lane groups reduced by shuffles) and
+  // stored for the dK/dV kernel launched after this one (no separate delta pass)
+  const bool fuse_delta = O != nullptr;
+  if (fuse_delta) O += (vl ? 0 : b * os.b) + sq_.qo * os.s;
 
-  s16x8 qf[NT][KS], dof[NT][KS];
+  s16x8 qf[NT][KS], dof[NT][KS], of[NT][KS];
   float lse2[NT], dlt[NT];
   const long long lrow = sq_.lrow;
 #pragma unroll
@@ -892,7 +873,14 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
     }
     const float lv = myq < Sq ? LSE[lrow + myq] : -INFINITY;
     lse2[t] = lv == -INFINITY ? INFINITY : lv * kLog2e;
-    dlt[t] = myq < Sq ? Delta[lrow + myq] : 0.f;
+    if (fuse_delta) {  // O fragments issued now, reduced after the first K/V tile loads are in flight
+#pragma unroll
+      for (int k = 0; k < KS; ++k)
+        of[t][k] = myq < Sq ? *reinterpret_cast<const s16x8*>(O + h * os.h + (long long)myq * os.s + 32 * k + 8 * g)
+                            : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    } else {
+      dlt[t] = myq < Sq ? Delta[lrow + myq] : 0.f;
+    }
   }
   f32x4 acc[NT][DB];
 #pragma unroll
@@ -911,6 +899,22 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 3 - NT) void bwd_dq_kernel(
   if (nkb > 0) {
     kt.load(0, Sk);
     vt.load(0, Sk);
+  }
+  if (fuse_delta) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float ds = 0.f;
+#pragma unroll
+      for (int k = 0; k < KS; ++k)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          ds += to_f(__builtin_bit_cast(T, (short)dof[t][k][e])) * to_f(__builtin_bit_cast(T, (short)of[t][k][e]));
+      ds += __shfl_xor(ds, 16);
+      ds += __shfl_xor(ds, 32);
+      dlt[t] = ds;
+      const int myq = qw + 16 * t + (lane & 15);
+      if (g == 0 && myq < Sq) Delta[lrow + myq] = ds;
+    }
   }
   if (PIPE && nkb > 0) {
     kt.template store<BT>(smem);
@@ -1132,49 +1136,48 @@ PA_API hipError_t pa_flash_bwd(const void* q, const void* k, const void* v, cons
   Strides qs{qst[0], qst[1], qst[2]}, ks{kst[0], kst[1], kst[2]}, vs{vst[0], vst[1], vst[2]},
       os{ost[0], ost[1], ost[2]}, dos{dost[0], dost[1], dost[2]}, dqs{dqst[0], dqst[1], dqst[2]},
       dks{dkst[0], dkst[1], dkst[2]}, dvs{dvst[0], dvst[1], dvst[2]};
-  const long long nrows = (long long)B * Hq * Sq;
+  // dQ runs first in every variant: it computes the delta rows (rowsum dO * O) from its own dO
+  // fragments and stores them for the dK/dV kernel that follows on the same stream
   FA_DISPATCH(dt, D, causal, {
-    bwd_delta_kernel<T, DD><<<(int)((nrows + 15) / 16), 256, 0, st>>>((const uint16_t*)dout, (const uint16_t*)o, delta,
-                                                                      B, Sq, Hq, dos, os);
     if (bwd_variant(D) == 4) {
+      dim3 g2(Hq, B, (Sq + 127) / 128);
+      bwd_dq_kernel<T, DD, CC, 1, 8, 0, true><<<g2, 512, 0, st>>>(
+          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+          (uint16_t*)dq, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, scale, Extra{}, (const uint16_t*)o, os);
       dim3 g1(Hq, B, (Sk + 127) / 128);
       bwd_dkdv_kernel<T, DD, CC, 1, 8, 0, true><<<g1, 512, 0, st>>>(
           (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
           (uint16_t*)dk, (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs, scale);
-      dim3 g2(Hq, B, (Sq + 127) / 128);
-      bwd_dq_kernel<T, DD, CC, 1, 8, 0, true><<<g2, 512, 0, st>>>(
-          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-          (uint16_t*)dq, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, scale);
     } else if (bwd_variant(D) == 3) {
+      dim3 g2(Hq, B, (Sq + 127) / 128);
+      bwd_dq_kernel<T, DD, CC, 1, 8><<<g2, 512, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                                                         (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk,
+                                                         Hq, Hk, qs, ks, vs, dos, dqs, scale, Extra{}, (const uint16_t*)o, os);
       dim3 g1(Hq, B, (Sk + 127) / 128);
       bwd_dkdv_kernel<T, DD, CC, 1, 8><<<g1, 512, 0, st>>>((const uint16_t*)q, (const uint16_t*)k,
                                                            (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
                                                            (uint16_t*)dk, (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs,
                                                            dos, dks, dvs, scale);
-      dim3 g2(Hq, B, (Sq + 127) / 128);
-      bwd_dq_kernel<T, DD, CC, 1, 8><<<g2, 512, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                                                         (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk,
-                                                         Hq, Hk, qs, ks, vs, dos, dqs, scale);
     } else if (bwd_variant(D) == 2) {
+      dim3 g2(Hq, B, (Sq + 127) / 128);
+      bwd_dq_kernel<T, DD, CC, 2><<<g2, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                                                      (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk, Hq,
+                                                      Hk, qs, ks, vs, dos, dqs, scale, Extra{}, (const uint16_t*)o, os);
       dim3 g1(Hq, B, (Sk + 127) / 128);
       bwd_dkdv_kernel<T, DD, CC, 2><<<g1, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                                                         (const uint16_t*)dout, lse, delta, (uint16_t*)dk,
                                                         (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs,
                                                         scale);
-      dim3 g2(Hq, B, (Sq + 127) / 128);
-      bwd_dq_kernel<T, DD, CC, 2><<<g2, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                                                      (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk, Hq,
-                                                      Hk, qs, ks, vs, dos, dqs, scale);
     } else {
+      dim3 g2(Hq, B, (Sq + 63) / 64);
+      bwd_dq_kernel<T, DD, CC, 1><<<g2, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                                                      (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk, Hq,
+                                                      Hk, qs, ks, vs, dos, dqs, scale, Extra{}, (const uint16_t*)o, os);
       dim3 g1(Hq, B, (Sk + 63) / 64);
       bwd_dkdv_kernel<T, DD, CC, 1><<<g1, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                                                         (const uint16_t*)dout, lse, delta, (uint16_t*)dk,
                                                         (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs,
                                                         scale);
-      dim3 g2(Hq, B, (Sq + 63) / 64);
-      bwd_dq_kernel<T, DD, CC, 1><<<g2, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                                                      (const uint16_t*)dout, lse, delta, (uint16_t*)dq, Sq, Sk, Hq,
-                                                      Hk, qs, ks, vs, dos, dqs, scale);
     }
   });
   return hipGetLastError();
@@ -1246,31 +1249,30 @@ PA_API hipError_t pa_flash_fwd_ex(const void* q, const void* k, const void* v, v
 
 // dK/dV + dQ launches of one feature set (D = 128: 8-wave blocks, D = 64: 4-wave blocks)
 template <typename T, int DD, bool CC, int F>
-static void bwd_ex(const void* q, const void* k, const void* v, const void* dout, const float* lse, float* delta,
-                   void* dq, void* dk, void* dv, int B, int Sq, int Sk, int Hq, int Hk, Strides qs, Strides ks,
-                   Strides vs, Strides dos, Strides dqs, Strides dks, Strides dvs, float scale, const Extra& ex,
-                   hipStream_t st) {
+static void bwd_ex(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
+                   float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int Hq, int Hk, Strides qs,
+                   Strides ks, Strides vs, Strides os, Strides dos, Strides dqs, Strides dks, Strides dvs, float scale,
+                   const Extra& ex, hipStream_t st) {
+  // dQ first: it computes the delta rows from its own dO fragments (o != null) and stores them
+  // for the dK/dV kernel that follows on the same stream
   constexpr int NW = DD == 128 ? 8 : 4;
+  dim3 g1(Hq, B, (Sk + 16 * NW - 1) / (16 * NW));
+  dim3 g2(Hq, B, (Sq + 16 * NW - 1) / (16 * NW));
   if (bwd_variant(DD) == 4) {  // double-buffered tiles
-    dim3 g1(Hq, B, (Sk + 16 * NW - 1) / (16 * NW));
+    bwd_dq_kernel<T, DD, CC, 1, NW, F, true><<<g2, 64 * NW, 0, st>>>(
+        (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dq,
+        Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, scale, ex, (const uint16_t*)o, os);
     bwd_dkdv_kernel<T, DD, CC, 1, NW, F, true><<<g1, 64 * NW, 0, st>>>(
         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk,
         (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs, scale, ex);
-    dim3 g2(Hq, B, (Sq + 16 * NW - 1) / (16 * NW));
-    bwd_dq_kernel<T, DD, CC, 1, NW, F, true><<<g2, 64 * NW, 0, st>>>(
-        (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dq,
-        Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, scale, ex);
     return;
   }
-  dim3 g1(Hq, B, (Sk + 16 * NW - 1) / (16 * NW));
+  bwd_dq_kernel<T, DD, CC, 1, NW, F><<<g2, 64 * NW, 0, st>>>(
+      (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dq,
+      Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, scale, ex, (const uint16_t*)o, os);
   bwd_dkdv_kernel<T, DD, CC, 1, NW, F><<<g1, 64 * NW, 0, st>>>(
       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk,
       (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs, scale, ex);
-  dim3 g2(Hq, B, (Sq + 16 * NW - 1) / (16 * NW));
-  bwd_dq_kernel<T, DD, CC, 1, NW, F><<<g2, 64 * NW, 0, st>>>((const uint16_t*)q, (const uint16_t*)k,
-                                                             (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-                                                             (uint16_t*)dq, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs,
-                                                             scale, ex);
 }
 
 PA_API hipError_t pa_flash_bwd_ex(const void* q, const void* k, const void* v, const void* o, const void* dout,
@@ -1288,19 +1290,16 @@ PA_API hipError_t pa_flash_bwd_ex(const void* q, const void* k, const void* v, c
   if (mask && rows) return hipErrorInvalidValue;  // one mask form per call
   const Extra ex = make_extra(cu_q, cu_k, total_q, mask, mb, mh, mq, mask_f32, p_drop, seed, offset, rows, rb, rh);
   // delta rows: [B, Hq, Sq] or, varlen, [Hq, total_q] (one "batch" of total_q packed rows)
-  const int dB = cu_q ? 1 : B, dS = cu_q ? total_q : Sq;
-  const long long nrows = (long long)dB * Hq * dS;
+  // (written by the dQ kernel, which runs first)
   FA_DISPATCH(dt, D, causal, {
-    bwd_delta_kernel<T, DD><<<(int)((nrows + 15) / 16), 256, 0, st>>>((const uint16_t*)dout, (const uint16_t*)o, delta,
-                                                                      dB, dS, Hq, dos, os);
     const int feat = 1 | (mask ? 2 : 0) | (p_drop > 0.f ? 4 : 0) | (rows ? 8 : 0);
     switch (feat) {
-      case 1: bwd_ex<T, DD, CC, 1>(q, k, v, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, dks, dvs, scale, ex, st); break;
-      case 3: bwd_ex<T, DD, CC, 3>(q, k, v, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, dks, dvs, scale, ex, st); break;
-      case 5: bwd_ex<T, DD, CC, 5>(q, k, v, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, dks, dvs, scale, ex, st); break;
-      case 7: bwd_ex<T, DD, CC, 7>(q, k, v, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, dks, dvs, scale, ex, st); break;
-      case 9: bwd_ex<T, DD, CC, 9>(q, k, v, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, dks, dvs, scale, ex, st); break;
-      default: bwd_ex<T, DD, CC, 13>(q, k, v, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dqs, dks, dvs, scale, ex, st); break;
+      case 1: bwd_ex<T, DD, CC, 1>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, os, dos, dqs, dks, dvs, scale, ex, st); break;
+      case 3: bwd_ex<T, DD, CC, 3>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, os, dos, dqs, dks, dvs, scale, ex, st); break;
+      case 5: bwd_ex<T, DD, CC, 5>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, os, dos, dqs, dks, dvs, scale, ex, st); break;
+      case 7: bwd_ex<T, DD, CC, 7>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, os, dos, dqs, dks, dvs, scale, ex, st); break;
+      case 9: bwd_ex<T, DD, CC, 9>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, os, dos, dqs, dks, dvs, scale, ex, st); break;
+      default: bwd_ex<T, DD, CC, 13>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, qs, ks, vs, os, dos, dqs, dks, dvs, scale, ex, st); break;
     }
   });
   return hipGetLastError();
