@@ -335,6 +335,53 @@ __global__ __launch_bounds__(256) void transpose2d_b16(const uint16_t* __restric
   }
 }
 
+// Wide form for cols % 128 == 0: a block transposes two side-by-side 64x64 tiles (four 16-byte
+// loads in flight per thread instead of two), element pairs go to LDS as one dword (the even
+// 66-element pitch keeps (2j, 2j + 1) in one dword), and each thread builds the 16-byte chunks of
+// two adjacent output rows from eight dword reads (low halves -> row c, high halves -> row c + 1),
+// a quarter of the LDS instructions of the 16-bit form.
+__global__ __launch_bounds__(256) void transpose2d_b16_w(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                         int rows, int cols) {
+  __shared__ uint32_t tile[2][64][33];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 128;
+  const int lr = tid >> 3, ch = tid & 7;
+  uint4 v[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      v[t][p] = *reinterpret_cast<const uint4*>(x + (long long)(r0 + lr + 32 * p) * cols + c0 + 64 * t + 8 * ch);
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      uint32_t* row = &tile[t][lr + 32 * p][4 * ch];
+      row[0] = v[t][p].x;
+      row[1] = v[t][p].y;
+      row[2] = v[t][p].z;
+      row[3] = v[t][p].w;
+    }
+  __syncthreads();
+  const int c = 2 * (tid >> 3);  // output rows c, c + 1 of each tile (input columns)
+  const int e0 = 8 * ch;         // output elements e0 .. e0 + 7 (input rows)
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    uint32_t d[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = tile[t][e0 + i][c >> 1];
+    uint32_t a[4], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a[j] = (d[2 * j] & 0xffffu) | (d[2 * j + 1] << 16);
+      b[j] = (d[2 * j] >> 16) | (d[2 * j + 1] & 0xffff0000u);
+    }
+    const long long yc = c0 + 64 * t + c;
+    *reinterpret_cast<uint4*>(y + yc * rows + r0 + e0) = make_uint4(a[0], a[1], a[2], a[3]);
+    *reinterpret_cast<uint4*>(y + (yc + 1) * rows + r0 + e0) = make_uint4(b[0], b[1], b[2], b[3]);
+  }
+}
+
 int cs_rows_per_block(int rows, int colblocks);
 
 // forward bias+activation launch shape (A/B knob: pa_act_fwd_tune)
@@ -400,7 +447,10 @@ PA_API void pa_act_fwd_tune(int target_blocks, int unroll) {
 PA_API hipError_t pa_transpose2d(const void* x, void* y, int rows, int cols, int elem_bytes, hipStream_t st) {
   if (elem_bytes != 2 || rows % 64 != 0 || cols % 64 != 0 || rows <= 0 || cols <= 0 || rows / 64 > 65535)
     return hipErrorInvalidValue;
-  transpose2d_b16<<<dim3(cols / 64, rows / 64), 256, 0, st>>>((const uint16_t*)x, (uint16_t*)y, rows, cols);
+  if (cols % 128 == 0)
+    transpose2d_b16_w<<<dim3(cols / 128, rows / 64), 256, 0, st>>>((const uint16_t*)x, (uint16_t*)y, rows, cols);
+  else
+    transpose2d_b16<<<dim3(cols / 64, rows / 64), 256, 0, st>>>((const uint16_t*)x, (uint16_t*)y, rows, cols);
   return hipGetLastError();
 }
 

@@ -1212,9 +1212,10 @@ def test_conv_sees_in_place_optimizer_updates():
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("R,C", [(64, 64), (2048, 8192), (8192, 2048), (192, 320)])
+@pytest.mark.parametrize("R,C", [(64, 64), (2048, 8192), (8192, 2048), (192, 320), (128, 384), (2048, 6144)])
 def test_hip_transpose2d(dt, R, C):
-    """csrc/act.hip pa_transpose2d (64x64 LDS tiles) is an exact transpose."""
+    """csrc/act.hip pa_transpose2d is an exact transpose (64x64 LDS tiles; the wide two-tile form
+    with dword LDS traffic when cols % 128 == 0)."""
     from paddle.ops import gemm
     x = torch.randn(R, C, device=DEV).to(dt)
     assert torch.equal(gemm.transpose2d(x), x.t().contiguous())
