@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B: captured Momentum step, host LR (old) vs device LR refilled per replay (new), twice each
+# A/B run during development: captured Momentum step, host LR (PA_AB_HOST_LR, a temporary knob since removed) vs device LR; found the capture-pool aliasing fixed in optimizer/algorithms.py _graph_lr
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
