@@ -10,7 +10,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_HERE, '_lib', 'libpaddle_amd_kernels.so')
+# PADDLE_AMD_KERNEL_LIB: another build of the kernel library (same-box A/B of two kernel versions)
+LIB_PATH = os.environ.get('PADDLE_AMD_KERNEL_LIB') or os.path.join(_HERE, '_lib', 'libpaddle_amd_kernels.so')
 
 lib = None
 load_error = None
