@@ -182,8 +182,10 @@ class TrainStepGraph:
         try:
             if gen is not None:
                 gen.add_(1)  # first node of every replay: a fresh dropout stream per step
+                _RNG_CAPTURE.add(torch.cuda.current_device())
             self.out = self.step_fn()
         finally:
+            _RNG_CAPTURE.discard(torch.cuda.current_device())
             g.capture_end()
             hooks, _CAPTURE_HOOKS = _CAPTURE_HOOKS, None
         self.hooks = hooks
@@ -221,6 +223,9 @@ def capture_train_step(step_fn, warmup=3):
 
 
 _RNG_GEN = {}  # device index -> int32 [1] generation counter read by the HIP dropout kernels
+# devices whose graph being captured advances that counter as its first node (a TrainStepGraph
+# capture): only there is a host-drawn dropout seed safe to freeze into the graph
+_RNG_CAPTURE = set()
 
 
 def install_rng_generation(device=None):
@@ -247,9 +252,11 @@ def rng_generation(device=None):
 
 def host_rng_guard(what):
     """Raise when a kernel would freeze a host-drawn dropout seed into a graph being captured
-    without the device generation counter (install_rng_generation) that re-randomises it."""
+    without a per-replay advance of the device generation counter (install_rng_generation).  Only a
+    TrainStepGraph capture adds that advance; a raw CUDAGraph / wrap_cuda_graph / DecodeStepGraph
+    capture raises even after a TrainStepGraph created the counter on this device."""
     if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing() and \
-            _RNG_GEN.get(torch.cuda.current_device()) is None:
+            torch.cuda.current_device() not in _RNG_CAPTURE:
         raise RuntimeError(f"{what}: dropout seeds are drawn on the host and would be frozen into the "
                            "captured graph (every replay would reuse one mask); capture the step without "
                            "dropout or run it eagerly")
@@ -266,6 +273,9 @@ class DecodeStepGraph:
     call is ``copy new tokens -> replay`` with no host-side position bookkeeping.  ``warmup``
     eager steps run first (allocator pools, kernel selection); the first captured call also
     produces that step's output.  Host-side cache features (beam_offset, pre_caches) are refused.
+    Any other per-step tensor ``step_fn`` uses (an attention mask, rotary tables, sequence
+    lengths) is captured by address: keep it in a static buffer and refill it in place before the
+    call — a new tensor created per step is not seen by the replay.
     """
 
     def __init__(self, step_fn, x_example, start_step, warmup=1):

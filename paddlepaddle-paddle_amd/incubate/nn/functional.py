@@ -564,7 +564,13 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
     split by heads / columns, out-linear / ffn2 weights split by rows — and the partial outputs of
     the out-linear and ffn2 GEMMs are all-reduced over the group ``ring_id`` (a
     paddle.distributed group id; the fleet model-parallel group when no such group exists) before
-    their (replicated) biases are added."""
+    their (replicated) biases are added.
+
+    Inside a captured decode step (``DecodeStepGraph``: a device ``time_step`` during capture)
+    only ``time_step`` is re-read per replay as a value; ``attn_mask``, ``rotary_embs`` and
+    ``seq_lens`` are graph inputs by ADDRESS — the replay reads whatever their storage holds, so
+    they must be static buffers the caller refills in place (``buf.copy_(new)``) before each
+    replay; a freshly allocated tensor per step would be silently ignored."""
     tp_group = _ring_group(ring_id) if ring_id != -1 else None
 
     def row_parallel(t, w, b):

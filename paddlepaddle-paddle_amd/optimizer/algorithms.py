@@ -311,8 +311,10 @@ class Adam(Optimizer):
         sd = super().state_dict()
         if self._flat is not None:
             for ent in self._flat:
-                # a graph-replayed step advances only the device copy of the powers
-                b1p, b2p = ent['pows'].tolist() if ent.get('graph_stepped') else (ent['b1p'], ent['b2p'])
+                # the fp64 host powers: advanced by every eager step and, through the replay hook
+                # (_advance_host_step), by every graph replay too — one checkpoint precision
+                # whether or not the run replayed (the fp32 device copy is for the kernel only)
+                b1p, b2p = ent['b1p'], ent['b2p']
                 for p in ent['fb'].params:
                     sd[f"{p.name}_beta1_pow_acc_0"] = _wrap(torch.tensor([b1p]))
                     sd[f"{p.name}_beta2_pow_acc_0"] = _wrap(torch.tensor([b2p]))

@@ -484,7 +484,15 @@ class ShardingEngine:
                     continue
                 w = dist.all_gather_into_tensor(u.fb.data, self.pshard(u), group=self.pg, async_op=True)
                 self._gather_works.append(w)
-            # stage-3 non-persistent units are gathered lazily by their forward pre-hook
+            else:
+                # stage-3 non-persistent units are gathered lazily by their forward pre-hook; one
+                # still holding (or prefetching) pre-step weights — e.g. gathered by a grad-enabled
+                # forward after the last backward — is released so the next forward re-gathers
+                if u.gather_work is not None:
+                    u.gather_work.wait()
+                    u.gather_work = None
+                    u.gathered = True
+                u.free_params()
         if self.model is None or self.level == 3:
             self.wait_param_gathers()
         elif not getattr(self, '_gather_hook_installed', False):
@@ -734,7 +742,13 @@ class ShardedOptimizer:
             if dt != torch.float32:
                 a['param'].copy_(a['master'].to(dt))
         self._step = int(sd.get('@step@', self._step))
-        self._pows = None  # re-derived from the loaded step on the next eager step
+        pows = getattr(self, '_pows', None)
+        if pows is not None and self._kind not in ('SGD', 'Momentum'):
+            # in place: a TrainStepGraph captured before the load keeps reading this tensor (powers
+            # of the NEXT update, step + 1)
+            b1, b2 = self._inner._beta1, self._inner._beta2
+            nxt = self._step + 1
+            pows.copy_(torch.tensor([b1 ** nxt, b2 ** nxt], dtype=torch.float32))
         if 'LR_Scheduler' in sd and hasattr(self._inner._learning_rate, 'set_state_dict'):
             self._inner._learning_rate.set_state_dict(sd['LR_Scheduler'])
         self.engine.gather_params_after_step()

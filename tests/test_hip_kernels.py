@@ -1530,6 +1530,19 @@ def test_train_step_hip_graph_matches_eager():
     b = r()._t.clone()
     assert not torch.equal(a, b)
     assert set(a.unique().tolist()) <= {0.0, 2.0}
+    # the generation counter now exists on this device, but a raw CUDAGraph capture does not
+    # advance it per replay: host-drawn dropout seeds must still be refused there
+    from paddle.device.cuda.graphs import CUDAGraph
+    x1, x0 = paddle.ones([64, 64]), paddle.zeros([64, 64])
+    torch.cuda.synchronize()
+    cg = CUDAGraph()
+    cg.capture_begin()
+    try:
+        with pytest.raises(RuntimeError, match='frozen'):
+            paddle.incubate.nn.functional.fused_dropout_add(x1, x0, 0.5)
+    finally:
+        cg.capture_end()
+    torch.cuda.synchronize()
 
 
 def test_train_step_graph_dropout_adamw_gpt():
@@ -1634,6 +1647,46 @@ def test_train_step_graph_lr_scheduler(kind):
     # a frozen learning rate would leave the replayed parameters far from the eager ones: the
     # schedule drops the rate 64x over the 8 steps, so a sanity bound on the first layer's drift
     assert all(torch.isfinite(t).all() for t in finals[1])
+
+
+def test_train_step_graph_sharded_state_reload():
+    """Loading a sharded-AdamW state dict into a run whose step is already captured: the replayed
+    steps after the load use the bias-correction powers of the loaded step count (the device powers
+    tensor the graph reads is refilled in place), so they reproduce the steps that followed the save."""
+    import paddle
+    from paddle.core.tensor import _wrap
+    from paddle.device.cuda.graphs import capture_train_step
+    paddle.set_device('gpu:0')
+    nn = paddle.nn
+    paddle.seed(9)
+    net = nn.Sequential(nn.Linear(128, 256), nn.GELU(), nn.Linear(256, 10))
+    opt = paddle.optimizer.AdamW(learning_rate=1e-2, parameters=net.parameters(), multi_precision=True)
+    net, opt = paddle.amp.decorate(net, opt, level='O2', dtype='bfloat16')
+    net, opt, _ = paddle.distributed.sharding.group_sharded_parallel(net, opt, level='p_g_os')
+    g = torch.Generator(device=DEV).manual_seed(10)
+    x = paddle.to_tensor(torch.randn(64, 128, device=DEV, generator=g).bfloat16())
+    y = paddle.to_tensor(torch.randint(0, 10, (64,), device=DEV, generator=g))
+
+    def step():
+        loss = paddle.nn.functional.cross_entropy(net(x), y)
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        return loss
+    run = capture_train_step(step, warmup=1)
+    for _ in range(4):
+        run()
+    sd = {k: (_wrap(v._t.clone()) if hasattr(v, '_t') else v) for k, v in opt.state_dict().items()}
+    for _ in range(3):
+        run()
+    after = [p._t.detach().float().clone() for p in net.parameters()]
+    for _ in range(3):
+        run()
+    opt.set_state_dict(sd)
+    for _ in range(3):
+        run()
+    for a, b in zip(after, [p._t.detach().float() for p in net.parameters()]):
+        _close(b, a, 1e-3 * float(a.abs().max()) + 1e-5, 1e-3, 'replayed steps after a state reload')
 
 
 @pytest.mark.parametrize('M', [1000, 4096])
