@@ -1,0 +1,123 @@
+// Extra instantiations of the 8-phase MFMA GEMM (gemm8_impl.h) in their own translation unit, so
+// the tuned bf16 training-step kernels of gemm8.hip keep their register allocation (co-compiled
+// template variants perturb each other's codegen):
+//
+//  * pa_gemmx: general bf16 / fp16 GEMM, optionally BATCHED (blockIdx.y = batch index, per-operand
+//    element strides, stride 0 = broadcast) — the hand-written path behind paddle.matmul / mm / bmm /
+//    einsum contractions and Linear outside the training engines (eval, no_grad, inference).
+//    Reference semantics: paddle/phi/kernels/impl/matmul_kernel_impl.h (MatMulFunction, batched
+//    broadcast) over funcs/blas/blaslt_impl.cu.h.
+//  * pa_gemm8_fp8: OCP fp8 (e4m3 / e5m2) x fp8 -> bf16 on the same schedule (schedule 11, both
+//    operands k-contiguous), one v_mfma_scale_f32_16x16x128_f8f6f4 per 16x16 fragment and 128-byte
+//    k-tile: the bf16 kernel's LDS images, DMA pipeline and epilogue unchanged, twice the FLOPs per
+//    matrix-pipe cycle.  Per-tensor dequant scales are device scalars (delayed scaling, no host
+//    sync).  Reference: paddle/phi/kernels/fusion/fp8_gemm, python/paddle/static/amp/decorator.py:755.
+#define PA_G8_EXTRA_TU 1
+#include "gemm8_impl.h"
+
+namespace pa {
+namespace g8 {
+
+template <typename T, bool BAT>
+static hipError_t launchx(int transA, int transB, const void* A, const void* B, void* C, const void* bias, int M,
+                          int N, int K, long long lda, long long ldb, long long ldc, int batch, long long sA,
+                          long long sB, long long sC, float alpha, float beta, hipStream_t st) {
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  dim3 grid(tm * tn, batch, 1);
+  const long long bA = sA * 2, bB = sB * 2;  // byte strides
+  const char* a = (const char*)A;
+  const char* b = (const char*)B;
+  uint16_t* c = (uint16_t*)C;
+  const uint16_t* bi = (const uint16_t*)bias;
+  // k-contiguous A: schedule 11 (row-half staging, full 128-B DMA lines); m-contiguous A: schedule 9
+  // (k-half staging) — the same per-layout choice as the bf16 training GEMMs (pa_gemm_bf16)
+  if (transA == 0) {
+    if (transB)
+      gemm11_kernel<true, true, 200, T, BAT><<<grid, 512, 0, st>>>(a, b, c, nullptr, bi, M, N, K, lda, ldb, ldc,
+                                                                   alpha, beta, K, bA, bB, sC);
+    else
+      gemm11_kernel<true, false, 200, T, BAT><<<grid, 512, 0, st>>>(a, b, c, nullptr, bi, M, N, K, lda, ldb, ldc,
+                                                                    alpha, beta, K, bA, bB, sC);
+  } else {
+    if (transB)
+      gemm9_kernel<false, true, 200, false, T, BAT><<<grid, 512, 0, st>>>(a, b, c, nullptr, bi, M, N, K, lda, ldb,
+                                                                          ldc, alpha, beta, K, Prob{}, bA, bB, sC);
+    else
+      gemm9_kernel<false, false, 200, false, T, BAT><<<grid, 512, 0, st>>>(a, b, c, nullptr, bi, M, N, K, lda, ldb,
+                                                                           ldc, alpha, beta, K, Prob{}, bA, bB, sC);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace g8
+}  // namespace pa
+
+static bool spanx_ok(int transX, int rows, int K, long long ld) {
+  const long long span = transX == 0 ? ((long long)rows * ld) * 2 : ((long long)K * ld) * 2;
+  return span < (1LL << 32);
+}
+
+// Contract (else the caller falls back to the library): K % 64 == 0, M, N, lda, ldb, ldc % 8 == 0,
+// 16-B aligned operands (and batch strides % 8 == 0), each operand matrix spanning < 4 GiB (32-bit
+// DMA offsets; the batch offset is added to the 64-bit base).  dt: 1 = bf16, 2 = fp16.
+PA_API int pa_gemmx_ok(int M, int N, int K, long long lda, long long ldb, long long ldc, int transA, int transB,
+                       int dt) {
+  if (M <= 0 || N <= 0 || K <= 0 || (dt != 1 && dt != 2)) return 0;
+  if (K % 64 || M % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8) return 0;
+  return spanx_ok(transA, M, K, lda) && spanx_ok(transB != 0 ? 0 : 1, N, K, ldb);
+}
+
+// C[b] = alpha * op(A[b]) @ op(B[b]) (+ beta * C[b]) (+ bias), b < batch.  transA == 0: A[b] is
+// [M][lda] (k contiguous), else [K][lda]; transB != 0: B[b] is [N][ldb], else [K][ldb].  Strides in
+// elements between consecutive batch matrices (0 = the same matrix for every b).
+PA_API int pa_gemmx(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, long long lda,
+                    long long ldb, long long ldc, int transA, int transB, int batch, long long sA, long long sB,
+                    long long sC, int dt, float alpha, float beta, hipStream_t st) {
+  using namespace pa::g8;
+  if (!pa_gemmx_ok(M, N, K, lda, ldb, ldc, transA, transB, dt) || batch < 1 || batch > 65535 || sA % 8 ||
+      sB % 8 || sC % 8)
+    return (int)hipErrorInvalidValue;
+  if (dt == 1) {
+    if (batch == 1)
+      return (int)launchx<pa::bf16_t, false>(transA, transB, A, B, C, bias, M, N, K, lda, ldb, ldc, 1, 0, 0, 0, alpha,
+                                             beta, st);
+    return (int)launchx<pa::bf16_t, true>(transA, transB, A, B, C, bias, M, N, K, lda, ldb, ldc, batch, sA, sB, sC,
+                                          alpha, beta, st);
+  }
+  if (batch == 1)
+    return (int)launchx<pa::f16_t, false>(transA, transB, A, B, C, bias, M, N, K, lda, ldb, ldc, 1, 0, 0, 0, alpha,
+                                          beta, st);
+  return (int)launchx<pa::f16_t, true>(transA, transB, A, B, C, bias, M, N, K, lda, ldb, ldc, batch, sA, sB, sC, alpha,
+                                       beta, st);
+}
+
+// fp8 contract: K % 128 == 0, M % 8 == 0, N % 8 == 0, lda / ldw % 16 (bytes), ldc % 8, both operands
+// k-contiguous (A [M][lda], W [N][ldw], the fp8 Linear layout), spans < 4 GiB.
+PA_API int pa_gemm8_fp8_ok(int M, int N, int K, long long lda, long long ldw, long long ldc) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % 128 || M % 8 || N % 8 || lda % 16 || ldw % 16 || ldc % 8) return 0;
+  return (long long)M * lda < (1LL << 32) && (long long)N * ldw < (1LL << 32);
+}
+
+// C[M,N] (bf16) = alpha * scale_a * scale_b * A @ W^T (+ beta * C) (+ bias); fmt 0 = e4m3, 1 = e5m2.
+PA_API int pa_gemm8_fp8(const void* A, const void* W, void* C, const void* bias, const void* scale_a,
+                        const void* scale_b, int M, int N, int K, long long lda, long long ldw, long long ldc,
+                        float alpha, float beta, int fmtA, int fmtB, hipStream_t st) {
+  using namespace pa::g8;
+  if (!pa_gemm8_fp8_ok(M, N, K, lda, ldw, ldc) || fmtA < 0 || fmtA > 1 || fmtB < 0 || fmtB > 1)
+    return (int)hipErrorInvalidValue;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  dim3 grid(tm * tn, 1, 1);
+  // the kernel counts k and leading dims in 2-byte units: fp8 bytes / 2
+  const int K2 = K / 2;
+  const long long la = lda / 2, lw = ldw / 2;
+  auto go = [&](auto kern) {
+    kern<<<grid, 512, 0, st>>>((const char*)A, (const char*)W, (uint16_t*)C, nullptr, (const uint16_t*)bias, M, N, K2,
+                               la, lw, ldc, alpha, beta, K2, 0LL, 0LL, 0LL, (const float*)scale_a,
+                               (const float*)scale_b);
+  };
+  if (fmtA == 0 && fmtB == 0) go(gemm11_kernel<true, true, 200, F8<0, 0>, false>);
+  else if (fmtA == 0) go(gemm11_kernel<true, true, 200, F8<0, 1>, false>);
+  else if (fmtB == 0) go(gemm11_kernel<true, true, 200, F8<1, 0>, false>);
+  else go(gemm11_kernel<true, true, 200, F8<1, 1>, false>);
+  return (int)hipGetLastError();
+}

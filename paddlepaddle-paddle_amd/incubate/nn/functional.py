@@ -152,9 +152,9 @@ def fused_matmul_bias(x, y, bias=None, transpose_x=False, transpose_y=False, nam
         a = a.transpose(-1, -2)
     if transpose_y:
         b = b.transpose(-1, -2)
-    if bias is not None and a.dim() == 2:
-        return _w(torch.addmm(_u(bias), a, b))
-    out = torch.matmul(a, b)
+    if bias is not None and a.dim() == 2 and b.dim() == 2:
+        return _w(ops.matmul.linear(a, b, _u(bias)))  # bias in the GEMM epilogue
+    out = ops.matmul.matmul(a, b)
     return _w(out + _u(bias) if bias is not None else out)
 
 
@@ -240,7 +240,7 @@ def fused_multi_head_attention(x, qkv_weight, linear_weight, pre_layer_norm=Fals
         h = _tp_in(h, g)  # with transpose_qkv_wb, num_heads is this rank's head count
     w = _u(qkv_weight)
     if transpose_qkv_wb:
-        qkv = torch.matmul(_u(h), w)
+        qkv = ops.matmul.matmul(_u(h), w)
         if qkv_bias is not None:
             qkv = qkv + _u(qkv_bias)
         H = num_heads

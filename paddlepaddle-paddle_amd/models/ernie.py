@@ -177,7 +177,7 @@ class ErnieForPretraining(nn.Layer):
         if masked_positions is not None:
             t = t.reshape(-1, t.shape[-1])[_unwrap(masked_positions).reshape(-1)]
         z = self.transform_ln(F.gelu(self.transform(_wrap(t))))
-        logits = torch.matmul(_unwrap(z), _unwrap(self.ernie.embeddings.word_embeddings.weight).t()) + \
+        logits = ops.matmul.matmul(_unwrap(z), _unwrap(self.ernie.embeddings.word_embeddings.weight).t()) + \
             _unwrap(self.decoder_bias)
         return _wrap(logits), self.nsp(pooled)
 

@@ -261,7 +261,7 @@ class GPTForPretraining(nn.Layer):
         if t.is_cuda and ops.use_hip(t) and t.dtype == torch.bfloat16 and _unwrap(w).dtype == torch.bfloat16:
             from ..ops.linear import tied_head  # hand-written GEMMs, in-place E.grad accumulate
             return _wrap(tied_head(t, w))
-        return _wrap(torch.matmul(t, _unwrap(w).t()))  # tied LM head
+        return _wrap(ops.matmul.matmul(t, _unwrap(w).t()))  # tied LM head
 
     def loss(self, logits, labels):
         lg = _unwrap(logits)

@@ -166,7 +166,7 @@ class LlamaForCausalLM(nn.Layer):
     def forward(self, input_ids, position_ids=None):
         h = self.llama(input_ids, position_ids)
         if self.config.tie_word_embeddings:
-            return _wrap(torch.matmul(_unwrap(h), _unwrap(self.llama.embed_tokens.weight).t()))
+            return _wrap(ops.matmul.matmul(_unwrap(h), _unwrap(self.llama.embed_tokens.weight).t()))
         return self.lm_head(h)
 
     def loss(self, logits, labels, ignore_index=-100):

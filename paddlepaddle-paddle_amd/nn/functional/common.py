@@ -22,12 +22,9 @@ def linear(x, weight, bias=None, name=None):
     if isinstance(weight, Tensor) and '_flat' in weight.__dict__ and ops.linear.eligible(weight) and \
             (bias is None or '_flat' in bias.__dict__):
         return _w(ops.linear.linear_accum(t, weight, bias))
-    if t.dim() == 2:
-        return _w(torch.addmm(b, t, w) if b is not None else torch.mm(t, w))
-    if b is not None:
-        out = torch.addmm(b, t.reshape(-1, t.shape[-1]), w)
-        return _w(out.reshape(*t.shape[:-1], w.shape[-1]))
-    return _w(torch.matmul(t, w))
+    # everything else (eval / no_grad / inference, weights outside flat buffers): all three GEMMs on
+    # the hand-written kernel for bf16 / fp16 GPU operands (ops/matmul.py), else torch
+    return _w(ops.matmul.linear(t, w, b))
 
 
 def bilinear(x1, x2, weight, bias=None, name=None):

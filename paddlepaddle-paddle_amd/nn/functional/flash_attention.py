@@ -23,7 +23,7 @@ def masked_attention_bhsd(q, k, v, mask, dropout_p=0.0, scale=None):
     records cleanly into static Programs.  Bool masks: True = keep; float masks are additive.
     """
     sc = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
-    s = torch.matmul(q, k.transpose(-1, -2)).float() * sc
+    s = ops.matmul.matmul(q, k.transpose(-1, -2)).float() * sc
     if mask is not None:
         if mask.dtype == torch.bool:
             s = s.masked_fill(~mask, -1e30)
@@ -32,7 +32,7 @@ def masked_attention_bhsd(q, k, v, mask, dropout_p=0.0, scale=None):
     p = torch.softmax(s, -1)
     if dropout_p > 0.0:
         p = TF.dropout(p, dropout_p)
-    return torch.matmul(p.to(v.dtype), v)
+    return ops.matmul.matmul(p.to(v.dtype), v)
 
 
 def _sdpa_reference(q, k, v, mask, dropout_p, causal, scale=None):

@@ -37,3 +37,4 @@ def native_loaded():
 from . import norm, softmax, act, xent, embedding, rope, optim, flash_attn, gemm, linear, fused, batchnorm, conv, pool  # noqa: E402,F401,E501
 from . import decode  # noqa: E402,F401
 from . import fp8  # noqa: E402,F401
+from . import matmul  # noqa: E402,F401

@@ -68,6 +68,10 @@ _SIGS = {
     'pa_fp8_cast_transpose': [P, I, I, LL, P, P, P, I, I, P, I, F, P],
     'pa_fp8_amax': [P, I, I, LL, P, P],
     'pa_gemm_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
+    'pa_gemm8_fp8_ok': [I, I, I, LL, LL, LL],
+    'pa_gemm8_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
+    'pa_gemmx_ok': [I, I, I, LL, LL, LL, I, I, I],
+    'pa_gemmx': [P, P, P, P, I, I, I, LL, LL, LL, I, I, I, LL, LL, LL, I, F, F, P],
     'pa_conv2d_fwd_ok': [I, I, I, I],
     'pa_conv2d_fwd': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
     'pa_conv2d_fwd_stats': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],

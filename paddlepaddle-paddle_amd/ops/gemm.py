@@ -312,6 +312,9 @@ def kmajor_weight(x2, w):
 
 
 _FP8_FMT = {torch.float8_e4m3fn: 0, torch.float8_e5m2: 1}
+# fp8 GEMM schedule: the 8-phase kernel (csrc/gemm8x.hip pa_gemm8_fp8, default) or the round-1
+# two-stage kernel (csrc/gemm.hip pa_gemm_fp8; PADDLE_AMD_FP8_8PHASE=0, A/B only)
+_fp8_8phase = os.environ.get('PADDLE_AMD_FP8_8PHASE', '1') != '0'
 
 
 def hip_fp8_ok(a, w):
@@ -327,7 +330,8 @@ def hip_fp8_ok(a, w):
 
 def hip_fp8_mm(a, w, scale_a=None, scale_b=None, bias=None, out=None, alpha=1.0, beta=0.0):
     """out[M,N] (bf16) = alpha * scale_a * scale_b * a @ w^T (+ beta*out) (+ bias) on the
-    hand-written CDNA4 fp8 kernel (v_mfma_scale_f32_16x16x128_f8f6f4, csrc/gemm.hip).
+    hand-written CDNA4 fp8 kernel (v_mfma_scale_f32_16x16x128_f8f6f4 on the 8-phase ping-pong
+    schedule, csrc/gemm8x.hip; the older two-stage kernel of csrc/gemm.hip for A/B).
     scale_a / scale_b: device fp32 scalars (dequant scales), read on the GPU (no host sync)."""
     M, K = a.shape
     N_ = w.shape[0]
@@ -337,6 +341,12 @@ def hip_fp8_mm(a, w, scale_a=None, scale_b=None, bias=None, out=None, alpha=1.0,
     assert out.dtype == torch.bfloat16 and out.stride(1) == 1 and out.shape == (M, N_)
     sa = scale_a.float().reshape(1) if scale_a is not None else None
     sb = scale_b.float().reshape(1) if scale_b is not None else None
+    if _fp8_8phase and N.lib.pa_gemm8_fp8_ok(M, N_, K, a.stride(0), w.stride(0), out.stride(0)):
+        # the 8-phase ping-pong schedule of the bf16 GEMM with one scaled fp8 MFMA per 128-byte k-tile
+        N.check(N.lib.pa_gemm8_fp8(N.ptr(a), N.ptr(w), N.ptr(out), N.ptr(bias), N.ptr(sa), N.ptr(sb), M, N_, K,
+                                   a.stride(0), w.stride(0), out.stride(0), float(alpha), float(beta),
+                                   _FP8_FMT[a.dtype], _FP8_FMT[w.dtype], N.stream()), 'gemm8_fp8')
+        return out
     N.check(N.lib.pa_gemm_fp8(N.ptr(a), N.ptr(w), N.ptr(out), N.ptr(bias), N.ptr(sa), N.ptr(sb), M, N_, K, a.stride(0),
                               w.stride(0), out.stride(0), float(alpha), float(beta), _FP8_FMT[a.dtype],
                               _FP8_FMT[w.dtype], N.stream()), 'gemm_fp8')

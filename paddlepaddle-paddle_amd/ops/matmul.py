@@ -1,0 +1,342 @@
+"""Dense matmul family on the hand-written MFMA GEMM (csrc/gemm8.hip + gemm8x.hip).
+
+Every bf16 / fp16 ``paddle.matmul`` / ``mm`` / ``bmm`` / ``@`` / two-operand ``einsum``
+contraction, ``F.linear`` outside the training engines (eval, ``no_grad``, inference predictors,
+layers whose weights are not in flat buffers), ``addmm``, and the static-graph / inference replay of
+recorded ``torch.matmul``-family nodes lands here:
+
+* 2-D (and N-D x 2-D with flattenable leading dims): ``gemm.mm`` — the training-step kernels for
+  bf16 (decode-shaped M <= 64 on the weight-streaming skinny kernel), ``pa_gemmx`` for fp16;
+* batched with broadcasting (``[..., M, K] @ [..., K, N]``): ONE launch of ``pa_gemmx`` with the
+  batch on ``blockIdx.y`` and per-operand element strides (stride 0 = a broadcast operand, so a
+  shared weight is never materialised per batch);
+* transposes are free: each matrix is read as it sits (k-contiguous or m/n-contiguous images).
+
+Reference: paddle/phi/kernels/impl/matmul_kernel_impl.h:960 (MatMulFunction: broadcasting, batched
+strides, vector cases), python/paddle/tensor/linalg.py:177 (matmul), :2133 (bmm).  Shapes outside
+the kernel contract (K % 64, odd dims, fp32, vectors, CPU / meta tensors) take torch's library path.
+"""
+import os
+
+import torch
+
+from . import _native as N
+from . import gemm
+
+_DT = {torch.bfloat16: 1, torch.float16: 2}
+_enabled = os.environ.get('PADDLE_AMD_HIP_MATMUL', '1') != '0'
+
+
+def _use(*ts):
+    """All operands on the GPU, one dtype of the kernel (bf16 / fp16), HIP library on."""
+    if not _enabled or not gemm._hip_gemm:
+        return False
+    t0 = ts[0]
+    if not isinstance(t0, torch.Tensor) or t0.device.type != 'cuda' or t0.dtype not in _DT:
+        return False
+    for t in ts[1:]:
+        if not isinstance(t, torch.Tensor) or t.device != t0.device or t.dtype != t0.dtype:
+            return False
+    from . import use_hip
+    return use_hip(t0)
+
+
+def _layout(t):
+    """(trans, ld) of the last two dims: 0 = row-major (k or n contiguous), 1 = column-major."""
+    r, c = t.shape[-2], t.shape[-1]
+    s0, s1 = t.stride(-2), t.stride(-1)
+    if s1 == 1 and (s0 >= c or r == 1):
+        return 0, (s0 if r > 1 else c)
+    if s0 == 1 and (s1 >= r or c == 1):
+        return 1, (s1 if c > 1 else r)
+    return None, None
+
+
+def _bstride(t, nb):
+    """Single element stride of the (collapsed) leading nb batch dims, or None when they do not
+    collapse to one stride (then the operand is made contiguous)."""
+    if nb == 0:
+        return 0
+    sizes, strides = t.shape[:nb], t.stride()[:nb]
+    st = None
+    # innermost non-unit batch dim sets the stride; every outer one must continue it
+    expect = None
+    for sz, s in zip(reversed(sizes), reversed(strides)):
+        if sz == 1:
+            continue
+        if st is None:
+            st, expect = s, s * sz
+            continue
+        if s != expect:
+            return None
+        expect = s * sz
+    return 0 if st is None else st
+
+
+def _mm2d(a, b, bias=None, alpha=1.0):
+    """a [M,K] @ b [K,N] (+ bias) for bf16 / fp16 on the hand-written kernels; None if outside."""
+    if a.data_ptr() % 16 or b.data_ptr() % 16:
+        return None
+    if a.dtype == torch.bfloat16 and alpha == 1.0:
+        if gemm._skinny_wins(a.shape[0], b.shape[1], a.shape[1]) and gemm.skinny_ok(a, b):
+            return gemm.skinny_mm(a, b, bias=bias)
+        if gemm.hip_mm_ok(a, b, 1) and (bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous())):
+            return gemm.mm(a, b, bias=bias)
+        return None
+    r = _gemmx(a.unsqueeze(0), b.unsqueeze(0), 1, bias=bias, alpha=alpha)
+    return None if r is None else r[0]
+
+
+def _gemmx(a3, b3, batch, bias=None, alpha=1.0, out=None, beta=0.0):
+    """[batch] x (a3 [.., M, K] @ b3 [.., K, N]) in one pa_gemmx launch.  a3 / b3 carry one batch
+    dim (size 1 or batch; stride 0 = broadcast).  Returns out [batch, M, N] or None."""
+    ta, lda = _layout(a3)
+    tb, ldb = _layout(b3)
+    if ta is None or tb is None:
+        return None
+    M, K = a3.shape[-2], a3.shape[-1]
+    N_ = b3.shape[-1]
+    if N._load() is None or not N.lib.pa_gemmx_ok(M, N_, K, lda, ldb, N_, ta, 1 - tb, _DT[a3.dtype]):
+        return None
+    sa = a3.stride(0) if a3.shape[0] > 1 else 0
+    sb = b3.stride(0) if b3.shape[0] > 1 else 0
+    if sa % 8 or sb % 8 or a3.data_ptr() % 16 or b3.data_ptr() % 16 or batch > 65535:
+        return None
+    if bias is not None and (bias.dtype != a3.dtype or not bias.is_contiguous() or bias.numel() != N_):
+        return None
+    if out is None:
+        out = torch.empty(batch, M, N_, dtype=a3.dtype, device=a3.device)
+        beta = 0.0
+    N.check(N.lib.pa_gemmx(N.ptr(a3), N.ptr(b3), N.ptr(out), N.ptr(bias), M, N_, K, lda, ldb, N_, ta, 1 - tb, batch,
+                           sa, sb, M * N_, _DT[a3.dtype], float(alpha), float(beta), N.stream()), 'gemmx')
+    return out
+
+
+def _matmul_raw(a, b):
+    """a [..., M, K] @ b [..., K, N] (both >= 2-D, same bf16 / fp16 dtype, GPU), no autograd.
+    Returns None when the shapes are outside the kernel contract."""
+    K = a.shape[-1]
+    if b.shape[-2] != K:
+        return None
+    M, N_ = a.shape[-2], b.shape[-1]
+    if b.dim() == 2:
+        # [..., M, K] @ [K, N]: the leading dims fold into M when they are a view
+        try:
+            a2 = a.view(-1, K) if a.dim() > 2 else a
+        except RuntimeError:
+            a2 = None
+        if a2 is not None:
+            y = _mm2d(a2, b)
+            return None if y is None else y.view(*a.shape[:-1], N_)
+    bs = torch.broadcast_shapes(a.shape[:-2], b.shape[:-2])
+    nb = len(bs)
+    batch = 1
+    for s in bs:
+        batch *= s
+    if batch == 1:
+        y = _mm2d(a.reshape(M, K), b.reshape(K, N_))
+        return None if y is None else y.view(*bs, M, N_)
+    ae = a.expand(*bs, M, K)
+    be = b.expand(*bs, K, N_)
+    sa, sb_ = _bstride(ae, nb), _bstride(be, nb)
+    if sa is None:
+        ae = ae.contiguous()
+        sa = M * K
+    if sb_ is None:
+        be = be.contiguous()
+        sb_ = K * N_
+    a3 = ae.as_strided((batch if sa else 1, M, K), (sa if sa else 0, ae.stride(-2), ae.stride(-1)))
+    b3 = be.as_strided((batch if sb_ else 1, K, N_), (sb_ if sb_ else 0, be.stride(-2), be.stride(-1)))
+    y = _gemmx(a3, b3, batch)
+    return None if y is None else y.view(*bs, M, N_)
+
+
+def _reduce_to(g, shape):
+    """Sum the broadcast dims of a gradient back to ``shape``."""
+    if tuple(g.shape) == tuple(shape):
+        return g
+    lead = g.dim() - len(shape)
+    if lead > 0:
+        g = g.sum(dim=tuple(range(lead)))
+    dims = tuple(i for i, s in enumerate(shape) if s == 1 and g.shape[i] != 1)
+    if dims:
+        g = g.sum(dim=dims, keepdim=True)
+    return g.reshape(shape)
+
+
+def _mt(x):
+    return x.transpose(-1, -2)
+
+
+class _MatmulFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        y = _matmul_raw(a, b)
+        if y is None:
+            y = torch.matmul(a, b)
+        ctx.save_for_backward(a, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        da = db = None
+        if ctx.needs_input_grad[0]:
+            da = _reduce_to(matmul(g, _mt(b)), a.shape)
+        if ctx.needs_input_grad[1]:
+            if b.dim() == 2 and a.dim() > 2:
+                K = a.shape[-1]
+                a2 = a.reshape(-1, K)
+                g2 = g.reshape(-1, g.shape[-1])
+                db = matmul(a2.t(), g2)
+            else:
+                db = _reduce_to(matmul(_mt(a), g), b.shape)
+        return da, db
+
+
+def matmul(a, b):
+    """torch-semantics matmul of two torch tensors on the hand-written GEMM where it applies."""
+    if a.dim() < 2 or b.dim() < 2 or not _use(a, b):
+        return torch.matmul(a, b)
+    if torch.is_grad_enabled() and (a.requires_grad or b.requires_grad):
+        return _MatmulFn.apply(a, b)
+    y = _matmul_raw(a, b)
+    return torch.matmul(a, b) if y is None else y
+
+
+class _LinearFn(torch.autograd.Function):
+    """y = x @ W + b (W [in, out]) with all three GEMMs hand-written (the training-engine form,
+    ops.linear, accumulates into flat gradient buffers; this one returns gradients)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias):
+        x2 = x.reshape(-1, x.shape[-1])
+        y = _mm2d(x2, w, bias=bias)
+        if y is None:
+            y = torch.addmm(bias, x2, w) if bias is not None else torch.mm(x2, w)
+        ctx.save_for_backward(x2, w)
+        ctx.xshape = x.shape
+        ctx.has_bias = bias is not None
+        return y.view(*x.shape[:-1], w.shape[1])
+
+    @staticmethod
+    def backward(ctx, g):
+        x2, w = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1])
+        dx = matmul(g2, w.t()).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dw = matmul(x2.t(), g2) if ctx.needs_input_grad[1] else None
+        db = g2.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def linear(x, w, bias=None):
+    """paddle F.linear (W stored [in, out]) outside the training engines."""
+    if w.dim() != 2 or x.dim() < 1 or not _use(x, w) or (bias is not None and not _use(x, bias)):
+        if x.dim() == 2:
+            return torch.addmm(bias, x, w) if bias is not None else torch.mm(x, w)
+        if bias is not None:
+            return torch.addmm(bias, x.reshape(-1, x.shape[-1]), w).reshape(*x.shape[:-1], w.shape[-1])
+        return torch.matmul(x, w)
+    b = bias.reshape(-1) if bias is not None else None
+    if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad or (b is not None and b.requires_grad)):
+        return _LinearFn.apply(x, w, b)
+    x2 = x.reshape(-1, x.shape[-1])
+    y = _mm2d(x2, w, bias=b)
+    if y is None:
+        y = torch.addmm(b, x2, w) if b is not None else torch.mm(x2, w)
+    return y.view(*x.shape[:-1], w.shape[1])
+
+
+def addmm(inp, x, y, beta=1.0, alpha=1.0):
+    """beta * inp + alpha * (x @ y)."""
+    if not _use(x, y) or torch.is_grad_enabled() and any(t.requires_grad for t in (inp, x, y)):
+        return torch.addmm(inp, x, y, beta=beta, alpha=alpha)
+    if x.dim() == 2 and y.dim() == 2 and inp.dtype == x.dtype and inp.is_cuda:
+        if inp.dim() == 1 and inp.numel() == y.shape[1] and beta == 1.0 and alpha == 1.0:
+            r = _mm2d(x, y, bias=inp.contiguous())
+            if r is not None:
+                return r
+        out = inp.expand(x.shape[0], y.shape[1]).contiguous()
+        r = _gemmx(x.unsqueeze(0), y.unsqueeze(0), 1, alpha=alpha, out=out.unsqueeze(0), beta=beta)
+        if r is not None:
+            return out
+    return torch.addmm(inp, x, y, beta=beta, alpha=alpha)
+
+
+def _parse(eq, nops):
+    eq = eq.replace(' ', '')
+    if '.' in eq:
+        return None
+    if '->' in eq:
+        lhs, out = eq.split('->')
+    else:
+        lhs = eq
+        cnt = {}
+        for c in lhs.replace(',', ''):
+            cnt[c] = cnt.get(c, 0) + 1
+        out = ''.join(sorted(c for c, n in cnt.items() if n == 1))
+    ins = lhs.split(',')
+    if len(ins) != nops:
+        return None
+    return ins, out
+
+
+def einsum(eq, *operands):
+    """Two-operand einsum contractions as one (batched) GEMM: operands permuted to
+    [batch, free, contracted] / [batch, contracted, free] (a copy only where the labels are not
+    already in that order), contracted on the hand-written kernel, result permuted to the output
+    labels.  Other forms (ellipsis, repeated labels, 1 or 3+ operands) take torch.einsum."""
+    if len(operands) != 2 or not _use(*operands):
+        return torch.einsum(eq, *operands)
+    p = _parse(eq, 2)
+    if p is None:
+        return torch.einsum(eq, *operands)
+    (lx, ly), lo = p
+    x, y = operands
+    if len(set(lx)) != len(lx) or len(set(ly)) != len(ly) or len(set(lo)) != len(lo) or \
+            x.dim() != len(lx) or y.dim() != len(ly) or any(c not in lx + ly for c in lo):
+        return torch.einsum(eq, *operands)
+    # labels summed away in only one operand: reduce them first
+    sx = [i for i, c in enumerate(lx) if c not in ly and c not in lo]
+    sy = [i for i, c in enumerate(ly) if c not in lx and c not in lo]
+    if sx:
+        x = x.sum(dim=sx)
+        lx = ''.join(c for i, c in enumerate(lx) if i not in sx)
+    if sy:
+        y = y.sum(dim=sy)
+        ly = ''.join(c for i, c in enumerate(ly) if i not in sy)
+    size = {c: x.shape[i] for i, c in enumerate(lx)}
+    for i, c in enumerate(ly):
+        if c in size and size[c] != y.shape[i]:
+            return torch.einsum(eq, *operands)
+        size[c] = y.shape[i]
+    bat = [c for c in lo if c in lx and c in ly]
+    con = [c for c in lx if c in ly and c not in lo]
+    fx = [c for c in lo if c in lx and c not in ly]
+    fy = [c for c in lo if c in ly and c not in lx]
+    if not con:
+        return torch.einsum(eq, *operands)
+
+    def prod(cs):
+        r = 1
+        for c in cs:
+            r *= size[c]
+        return r
+    xp = x.permute(*[lx.index(c) for c in bat + fx + con]).reshape(prod(bat), prod(fx), prod(con))
+    yp = y.permute(*[ly.index(c) for c in bat + con + fy]).reshape(prod(bat), prod(con), prod(fy))
+    r = matmul(xp, yp).reshape(*[size[c] for c in bat + fx + fy])
+    cur = bat + fx + fy
+    return r.permute(*[cur.index(c) for c in lo]) if cur != list(lo) else r
+
+
+def _tensor_matmul(self, other):
+    return matmul(self, other)
+
+
+def static_substitutions():
+    """Replay-time substitutes for recorded torch GEMM nodes (static Executor, jit.load, predictor):
+    the recorded program keeps plain torch targets; replay on the GPU runs them here."""
+    return {torch.matmul: matmul, torch.mm: matmul, torch.bmm: matmul,
+            torch.Tensor.matmul: _tensor_matmul, torch.Tensor.__matmul__: _tensor_matmul,
+            torch.addmm: addmm, torch.einsum: einsum,
+            torch.nn.functional.linear: lambda x, w, b=None: linear(x, w.t(), b)}

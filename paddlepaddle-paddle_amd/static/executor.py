@@ -182,8 +182,21 @@ def _exec(prog, nodes, env, smap, dev):
         rec.append((len(rec), _op_name(n), (time.perf_counter() - t0) * 1e3))
 
 
+_GEMM_SUBS = {}
+
+
+def _gemm_subs():
+    """Recorded torch GEMM targets (matmul / mm / bmm / addmm / einsum / linear) -> the hand-written
+    MFMA GEMM routing of ops/matmul.py (torch itself for CPU / fp32 / out-of-contract shapes)."""
+    if not _GEMM_SUBS:
+        from ..ops import matmul as _hm
+        _GEMM_SUBS.update(_hm.static_substitutions())
+    return _GEMM_SUBS
+
+
 def _exec_nodes(prog, nodes, env, smap, dev):
     subs = _SUBS['map']
+    gsubs = _gemm_subs()
     for n in nodes:
         if n.kind == 'torch':
             args = _resolve(prog, n.args, env, smap, dev)
@@ -191,6 +204,10 @@ def _exec_nodes(prog, nodes, env, smap, dev):
             if n.meta.get('factory') and 'device' in kwargs and kwargs['device'] is None:
                 kwargs['device'] = dev
             fn = subs.get(n.target, n.target) if subs else n.target
+            try:
+                fn = gsubs.get(fn, fn)
+            except TypeError:  # unhashable target
+                pass
             _bind(env, n.outs, fn(*args, **kwargs))
         elif n.kind == 'minimize':
             loss = env[n.args[0].vid]

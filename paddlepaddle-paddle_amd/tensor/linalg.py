@@ -1,12 +1,14 @@
 """paddle linalg API (reference: python/paddle/tensor/linalg.py, python/paddle/linalg.py).
 
-``matmul`` is the dense GEMM entry point: bf16/fp16 GEMMs go to hipBLASLt (the plain-
-library path); fused GEMM epilogues used by the models live in ``ops/``.
+``matmul`` / ``mm`` / ``bmm`` / two-operand ``einsum`` are the dense GEMM entry points: bf16 / fp16
+operands on the GPU run the hand-written MFMA GEMM (ops/matmul.py: batched with broadcasting,
+transposes read in place); other dtypes / devices / shapes outside the kernel contract use torch.
 """
 import torch
 
 from ._helpers import _w, _u, _axis, Tensor
 from ..core.amp_dispatch import amp_op as _amp_op
+from ..ops import matmul as _hm
 
 
 @_amp_op('matmul_v2')
@@ -16,17 +18,20 @@ def matmul(x, y, transpose_x=False, transpose_y=False, name=None):
         a = a.transpose(-1, -2) if a.dim() > 1 else a
     if transpose_y:
         b = b.transpose(-1, -2) if b.dim() > 1 else b
-    return _w(torch.matmul(a, b))
+    return _w(_hm.matmul(a, b))
 
 
 @_amp_op('matmul_v2')
 def mm(input, mat2, name=None):  # noqa: A002
-    return _w(torch.matmul(_u(input), _u(mat2)))
+    return _w(_hm.matmul(_u(input), _u(mat2)))
 
 
 @_amp_op('matmul_v2')
 def bmm(x, y, name=None):
-    return _w(torch.bmm(_u(x), _u(y)))
+    a, b = _u(x), _u(y)
+    if a.dim() != 3 or b.dim() != 3 or a.shape[0] != b.shape[0]:
+        return _w(torch.bmm(a, b))  # torch's error for mismatched shapes
+    return _w(_hm.matmul(a, b))
 
 
 def dot(x, y, name=None):
@@ -44,7 +49,7 @@ def mv(x, vec, name=None):
 def einsum(equation, *operands):
     if len(operands) == 1 and isinstance(operands[0], (list, tuple)):
         operands = operands[0]
-    return _w(torch.einsum(equation, *[_u(o) for o in operands]))
+    return _w(_hm.einsum(equation, *[_u(o) for o in operands]))
 
 
 @_amp_op('pnorm')

@@ -202,7 +202,8 @@ def add_n(inputs, name=None):
 
 
 def addmm(input, x, y, beta=1.0, alpha=1.0, name=None):  # noqa: A002
-    return _w(torch.addmm(_u(input), _u(x), _u(y), beta=beta, alpha=alpha))
+    from ..ops import matmul as _hm
+    return _w(_hm.addmm(_u(input), _u(x), _u(y), beta=beta, alpha=alpha))
 
 
 def addmm_(input, x, y, beta=1.0, alpha=1.0, name=None):  # noqa: A002

@@ -59,8 +59,13 @@ def main():
         f1 = 2.0 * M * K * N
         tl = bench(lambda: torch._scaled_mm(a, bt.t(), scale_a=one, scale_b=one, out_dtype=bf))
         th = bench(lambda: gemm.hip_fp8_mm(a, bt, scale_a=one, scale_b=one))
-        print(f"  fp8 gemm {name}: torch._scaled_mm {tl*1e6:8.1f} us {f1/tl/1e12:6.0f} TF | hip {th*1e6:8.1f} us "
-              f"{f1/th/1e12:6.0f} TF", flush=True)
+        gemm._fp8_8phase = False
+        t2 = bench(lambda: gemm.hip_fp8_mm(a, bt, scale_a=one, scale_b=one))
+        gemm._fp8_8phase = True
+        th2 = bench(lambda: gemm.hip_fp8_mm(a, bt, scale_a=one, scale_b=one))
+        print(f"  fp8 gemm {name}: torch._scaled_mm {tl*1e6:8.1f} us {f1/tl/1e12:6.0f} TF | hip 8-phase "
+              f"{th*1e6:8.1f} / {th2*1e6:8.1f} us {f1/min(th, th2)/1e12:6.0f} TF | hip 2-stage {t2*1e6:8.1f} us "
+              f"{f1/t2/1e12:6.0f} TF", flush=True)
         m = F8.FP8Meta(F8.E4M3, 16, 0, dev)
         xb = x.detach()
         tc = bench(lambda: m.cast(xb))
