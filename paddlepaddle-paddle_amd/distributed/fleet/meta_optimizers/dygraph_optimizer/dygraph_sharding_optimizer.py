@@ -50,12 +50,18 @@ class DygraphShardingOptimizer(ShardedOptimizer):
         dp = self._hcg.get_data_parallel_group()
         if dp is None or dp.nranks <= 1:
             return
+        # one async all-reduce per arena, all in flight together, then one wait each (RCCL
+        # pipelines them on its stream; the gradient shards are final only after the last
+        # micro-batch's reduce-scatter, so this runs once per step, after backward)
+        nccl = dist.get_backend(dp.pg) == 'nccl'
+        works = []
         for a in self.engine.arenas.values():
             g = a['grad']
-            if dist.get_backend(dp.pg) == 'nccl':
-                dist.all_reduce(g, dist.ReduceOp.AVG, group=dp.pg)
-            else:
-                dist.all_reduce(g, group=dp.pg)
+            works.append((g, dist.all_reduce(g, dist.ReduceOp.AVG if nccl else dist.ReduceOp.SUM, group=dp.pg,
+                                             async_op=True)))
+        for g, w in works:
+            w.wait()
+            if not nccl:
                 g.div_(dp.nranks)
 
     def _shared_units(self):
@@ -95,7 +101,7 @@ class DygraphShardingOptimizer(ShardedOptimizer):
                 s = self.engine.gshard(u).float().pow(2).sum()
                 isd = 1.0 if getattr(u.params[0], 'is_distributed', False) else 0.0
                 sq = sq - torch.stack([s * isd, s * (1.0 - isd)])
-        if self.engine.world > 1:
+        if self.engine.collectives:
             dist.all_reduce(sq, group=self.engine.pg)  # shards -> this stage's full local norm
         mp = self._hcg.get_model_parallel_group()
         if mp is not None and mp.nranks > 1:

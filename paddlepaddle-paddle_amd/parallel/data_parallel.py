@@ -158,7 +158,9 @@ class DataParallel(Layer):
         self.find_unused_parameters = find_unused_parameters
         self.group = group
         self._strategy = strategy
-        ready = dist.is_available() and dist.is_initialized() and dist.get_world_size(_pg(group)) > 1
+        import os
+        force = os.environ.get('PADDLE_AMD_FORCE_COLLECTIVES', '0') == '1'  # 1-rank RCCL rehearsal
+        ready = dist.is_available() and dist.is_initialized() and (dist.get_world_size(_pg(group)) > 1 or force)
         self._reducer = None
         if ready:
             sync_params_buffers(layers, group)

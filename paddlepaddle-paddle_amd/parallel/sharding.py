@@ -83,7 +83,7 @@ class _Unit:
         st = self.fb.data.untyped_storage()
         st.resize_(self.fb.numel * self.fb.data.element_size())
         src = self.engine.pshard(self)
-        if self.engine.world == 1:
+        if not self.engine.collectives:
             self.fb.data.copy_(src)
             self.gathered = True
             return
@@ -157,12 +157,20 @@ class ShardingEngine:
         self.pg = _pg(group)
         self.world = dist.get_world_size(self.pg) if dist.is_initialized() else 1
         self.rank = dist.get_rank(self.pg) if dist.is_initialized() else 0
+        # collectives: False only for a single rank with no forced collectives.  Forcing them
+        # (PADDLE_AMD_FORCE_COLLECTIVES=1 with an initialised process group, e.g. a 1-rank RCCL
+        # group) runs the real all-gather / reduce-scatter / all-reduce calls at world 1, so the
+        # multi-GPU stream ordering is exercised on one GPU (the gradients then equal the world-1
+        # result bit for bit: a 1-rank AVG / SUM is the identity).
+        import os
+        force = os.environ.get('PADDLE_AMD_FORCE_COLLECTIVES', '0') == '1' and dist.is_initialized()
+        self.collectives = self.world > 1 or force
         # one rank: the "shard" is the whole buffer, so units alias the optimizer arenas and
         # nothing is ever released, gathered or copied (no degenerate collectives either)
         if alias is None:
             import os
             alias = os.environ.get('PADDLE_AMD_SHARDING_ALIAS', '1') != '0'
-        self.alias = self.world == 1 and bool(alias)
+        self.alias = not self.collectives and bool(alias)
         self.release_grads = release_grads and self.level == 3 and not self.alias
         self.reshard_after_forward = self._auto_reshard(model, params) if reshard_after_forward is None \
             else bool(reshard_after_forward)
@@ -201,7 +209,7 @@ class ShardingEngine:
 
     # ------------------------------------------------------------------ construction
     def _broadcast_params(self):
-        if self.world == 1:
+        if not self.collectives:
             return
         if self.model is None:  # replicas of every parameter start equal: broadcast from rank 0
             src = self.group.ranks[0] if self.group is not None and hasattr(self.group, 'ranks') else 0
@@ -416,7 +424,7 @@ class ShardingEngine:
         if self.alias:
             u.rs_work = None  # gradients already live in the arena
             return
-        if self.world == 1:
+        if not self.collectives:
             u.rs_work = None
             self._accumulate_shard(u, u.shard(u.fb.grad))
             return
@@ -476,7 +484,7 @@ class ShardingEngine:
         without a model (hybrid-parallel sharding optimizer) the gathers are waited for here."""
         for u in self.units:
             if u.persistent or self.level < 3:
-                if self.world == 1:
+                if not self.collectives:
                     if not u.gathered:  # released persistent unit (alias off): plain re-materialise
                         u.wait_gather()
                     elif u.fb.data.data_ptr() != self.pshard(u).data_ptr():
@@ -608,7 +616,7 @@ class ShardedOptimizer:
             sq = s if sq is None else sq + s
         if clip._extra_sq_norm_fn is not None:
             sq = clip._extra_sq_norm_fn(sq)
-        if self.engine.world > 1:
+        if self.engine.collectives:
             dist.all_reduce(sq, group=self.engine.pg)
         norm = sq.sqrt()
         return torch.clamp(clip.clip_norm / torch.clamp(norm, min=clip.clip_norm), max=1.0)

@@ -9,3 +9,5 @@ timeout -k 10 300 python -u tools/matmul_bench.py > gpurun_out/r4a_matmul_bench.
 cat gpurun_out/r4a_matmul_bench.log
 timeout -k 10 300 python -u tools/fp8_bench.py > gpurun_out/r4a_fp8_bench.log 2>&1 || { echo "fp8 bench failed"; tail -30 gpurun_out/r4a_fp8_bench.log; exit 1; }
 cat gpurun_out/r4a_fp8_bench.log
+timeout -k 10 300 python -u -m pytest tests/test_rccl_world1.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r4a_rccl.log 2>&1 || { echo "rccl tests failed"; tail -40 gpurun_out/r4a_rccl.log; exit 1; }
+tail -2 gpurun_out/r4a_rccl.log
