@@ -33,7 +33,9 @@ def rms_norm(x, normalized_shape, weight=None, epsilon=1e-05, name=None):
     tf = t.float() if t.dtype in (torch.float16, torch.bfloat16) else t
     var = tf.pow(2).mean(-1, keepdim=True)
     y = (tf * torch.rsqrt(var + epsilon)).to(t.dtype)
-    return _w(y * w if w is not None else y)
+    # output in the input's dtype (an fp32 weight under AMP-O2 must not promote a bf16 activation,
+    # matching the HIP kernel path)
+    return _w(y * w.to(t.dtype) if w is not None else y)
 
 
 def batch_norm(x, running_mean, running_var, weight=None, bias=None, training=False, momentum=0.9, epsilon=1e-05,
