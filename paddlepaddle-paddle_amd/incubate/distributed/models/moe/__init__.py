@@ -7,6 +7,14 @@ one ``all_to_all_single`` over the expert-parallel group (RCCL over xGMI; every 
 direct link on an 8-GPU node).  Each rank runs its local experts on contiguous segments, then
 the reverse all-to-all returns outputs which are combined with the gate weights by one
 ``index_add``.  The exchange is an autograd Function whose backward is the reverse exchange.
+
+Expert compute: when the experts are homogeneous two-layer FFNs (same class, one Linear d -> f and
+one Linear f -> d, an elementwise activation between them — the ExpertLayer form of the reference's
+MoE tests and PaddleNLP), the local experts run as TWO batched GEMM launches over all experts
+(ops/matmul.py: [E, capacity, d] @ [E, d, f], blockIdx.y = expert) instead of a Python loop of
+per-expert Linears (reference kernel: paddle/phi/kernels/fusion/cutlass/moe_kernel.cu).  The
+structure is verified once numerically against expert 0's own forward (activation identified
+among relu / gelu / gelu-tanh / silu); anything else keeps the per-expert loop.
 """
 import math
 
@@ -153,6 +161,82 @@ class SwitchGate(NaiveGate):
         return _wrap(s.to(lg.dtype)), _wrap(i)
 
 
+# ----------------------------------------------------------------- grouped experts
+_ACTS = {
+    'relu': torch.relu,
+    'gelu': lambda t: TF.gelu(t),
+    'gelu_tanh': lambda t: TF.gelu(t, approximate='tanh'),
+    'silu': TF.silu,
+}
+
+
+def _ffn_linears(expert):
+    lins = [l for l in expert.sublayers() if isinstance(l, Linear)]
+    if len(lins) != 2 or len(expert.parameters()) != sum(len(l.parameters()) for l in lins):
+        return None
+    return lins
+
+
+def _detect_grouped(experts, d_model):
+    """(order, act) when every expert is x -> lin2(act(lin1(x))) with matching shapes, else None.
+    Verified numerically on expert 0 with a random probe (fp32, on the experts' device)."""
+    e0 = experts[0]
+    lins = _ffn_linears(e0)
+    if lins is None or any(type(e) is not type(e0) for e in experts):
+        return None
+    a, b = lins
+    if a.weight.shape[0] != d_model:
+        a, b = b, a
+    if a.weight.shape[0] != d_model or b.weight.shape[1] != d_model or a.weight.shape[1] != b.weight.shape[0]:
+        return None
+    for e in experts[1:]:
+        l2 = _ffn_linears(e)
+        if l2 is None or sorted(tuple(l.weight.shape) for l in l2) != sorted((tuple(a.weight.shape),
+                                                                              tuple(b.weight.shape))):
+            return None
+    first = 0 if lins[0] is a else 1
+    w = a.weight._t
+    g = torch.Generator(device=w.device).manual_seed(0)
+    probe = torch.randn(4, d_model, generator=g, device=w.device).to(w.dtype)
+    with torch.no_grad():
+        ref = _unwrap(e0(_wrap(probe))).float()
+        h = probe.float() @ a.weight._t.float() + (a.bias._t.float() if a.bias is not None else 0.0)
+        for name, fn in _ACTS.items():
+            out = fn(h).to(w.dtype).float() @ b.weight._t.float() + (b.bias._t.float() if b.bias is not None else 0.0)
+            tol = 1e-4 if w.dtype == torch.float32 else 3e-2
+            if torch.allclose(out, ref, atol=tol * (ref.abs().max().item() + 1e-3), rtol=tol):
+                return first, name
+    return None
+
+
+def _grouped_ffn(experts, spec, per_exp, d_model):
+    """All experts' FFNs as two batched GEMMs over a [E, cap, d] zero-padded token block."""
+    from ..... import ops
+    first, act = spec
+    E = len(experts)
+    lins = [_ffn_linears(e) for e in experts]
+    l1 = [l[first] for l in lins]
+    l2 = [l[1 - first] for l in lins]
+    counts = [c.shape[0] for c in per_exp]
+    cap = max(max(counts), 1)
+    cap = -(-cap // 8) * 8  # the GEMM's row contract
+    x = per_exp[0]
+    blk = x.new_zeros(E, cap, d_model)
+    rows = torch.cat([torch.arange(c, device=x.device) + j * cap for j, c in enumerate(counts)])
+    blk = blk.view(E * cap, d_model).index_copy(0, rows, torch.cat(per_exp, 0)).view(E, cap, d_model)
+    w1 = torch.stack([l.weight._t for l in l1])  # [E, d, f]
+    w2 = torch.stack([l.weight._t for l in l2])  # [E, f, d]
+    h = ops.matmul.matmul(blk, w1)
+    if l1[0].bias is not None:
+        h = h + torch.stack([l.bias._t for l in l1]).unsqueeze(1)
+    h = _ACTS[act](h)
+    y = ops.matmul.matmul(h, w2)
+    if l2[0].bias is not None:
+        y = y + torch.stack([l.bias._t for l in l2]).unsqueeze(1)
+    flat = y.reshape(E * cap, -1).index_select(0, rows)
+    return list(flat.split(counts, 0))
+
+
 # ----------------------------------------------------------------- layer
 class MoELayer(Layer):
     def __init__(self, d_model, experts, gate=None, moe_group=None, mp_group=None, recompute_interval=0,
@@ -178,6 +262,7 @@ class MoELayer(Layer):
                 raise ValueError(f"unknown gate type {typ}")
         self.gate = gate
         self.top_k = getattr(gate, 'top_k', 1)
+        self._grouped = None  # (order, act) once verified; False = per-expert loop
 
     def forward(self, inp):
         t = _unwrap(inp)
@@ -209,12 +294,17 @@ class MoELayer(Layer):
                        for j in range(self.num_expert)]
         else:
             per_exp = list(send.split(counts.tolist(), 0))
-        outs = []
-        for j, chunk in enumerate(per_exp):
-            if chunk.shape[0] == 0:
-                outs.append(chunk.new_zeros((0, self.d_model)))
-                continue
-            outs.append(_unwrap(self.experts[j](_wrap(chunk))))
+        if self._grouped is None:
+            self._grouped = _detect_grouped(list(self.experts), self.d_model) or False
+        if self._grouped and self.num_expert > 1:
+            outs = _grouped_ffn(list(self.experts), self._grouped, per_exp, self.d_model)
+        else:
+            outs = []
+            for j, chunk in enumerate(per_exp):
+                if chunk.shape[0] == 0:
+                    outs.append(chunk.new_zeros((0, self.d_model)))
+                    continue
+                outs.append(_unwrap(self.experts[j](_wrap(chunk))))
         if self.world_size > 1:
             rc = recv_counts.view(self.world_size, self.num_expert)
             pieces = [o.split(rc[:, j].tolist(), 0) for j, o in enumerate(outs)]

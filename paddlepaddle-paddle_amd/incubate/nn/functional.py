@@ -769,13 +769,21 @@ def variable_length_memory_efficient_attention(query, key, value, seq_lens, kv_s
 
 
 def fused_ec_moe(x, gate, bmm0_weight, bmm0_bias, bmm1_weight, bmm1_bias, act_type):
+    """Every token through every expert, combined with the softmaxed gate (reference
+    incubate/nn/functional/fused_ec_moe.py:18, kernel fusion/cutlass/moe_kernel.cu).  The expert
+    FFNs are two batched GEMMs over the experts (ops/matmul.py: the token matrix broadcast to every
+    expert at batch stride 0, blockIdx.y = expert) — no per-expert loop, no weight copies."""
     t, g = _u(x), _u(gate)
-    probs = torch.softmax(g.float(), -1)
-    E = _u(bmm0_weight).shape[0]
-    h = torch.einsum('bsd,edf->bsef', t, _u(bmm0_weight)) + _u(bmm0_bias).reshape(1, 1, E, -1)
+    B, S, D = t.shape
+    probs = torch.softmax(g.float(), -1)                       # [B, S, E]
+    w0, w1 = _u(bmm0_weight), _u(bmm1_weight)                  # [E, D, F], [E, F, D]
+    E = w0.shape[0]
+    t2 = t.reshape(1, B * S, D)
+    h = ops.matmul.matmul(t2, w0) + _u(bmm0_bias).reshape(E, 1, -1).to(t.dtype)   # [E, T, F]
     h = TF.gelu(h) if act_type == 'gelu' else torch.relu(h)
-    o = torch.einsum('bsef,efd->bsed', h, _u(bmm1_weight)) + _u(bmm1_bias).reshape(1, 1, E, -1)
-    return _w((o * probs.unsqueeze(-1).to(o.dtype)).sum(2))
+    o = ops.matmul.matmul(h, w1) + _u(bmm1_bias).reshape(E, 1, -1).to(t.dtype)    # [E, T, D]
+    pr = probs.reshape(B * S, E).t().unsqueeze(-1).to(o.dtype)                     # [E, T, 1]
+    return _w((o * pr).sum(0).reshape(B, S, D))
 
 
 def blha_get_max_len(seq_lens_encoder, seq_lens_decoder, batch_size):
