@@ -163,6 +163,12 @@ class _Fleet:
         mode = hcg.get_parallel_mode()
         if mode == ParallelMode.PIPELINE_PARALLEL:
             if getattr(model, 'get_num_virtual_stages', lambda: 1)() > 1:
+                cfg = getattr(self._strategy, 'pipeline_configs', {}) or {}
+                acc, pp = int(cfg.get('accumulate_steps', 1)), hcg.get_pipe_parallel_world_size()
+                if pp <= acc < 2 * pp:  # the reference's choice (fleet/model.py:168)
+                    return meta_parallel.PipelineParallelWithInterleaveFthenB(model, hcg, self._strategy)
+                if acc < pp:
+                    raise ValueError(f"The accumulate_steps({acc}) should be greater than or equal to pp_degree({pp})")
                 return meta_parallel.PipelineParallelWithInterleave(model, hcg, self._strategy)
             return meta_parallel.PipelineParallel(model, hcg, self._strategy)
         if mode == ParallelMode.TENSOR_PARALLEL or mode == ParallelMode.SEGMENT_PARALLEL:

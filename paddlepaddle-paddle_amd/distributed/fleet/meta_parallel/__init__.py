@@ -1,6 +1,7 @@
 """paddle.distributed.fleet.meta_parallel (reference: .../fleet/meta_parallel/__init__.py)."""
 from .pipeline import (LayerDesc, SharedLayerDesc, SegmentLayers, PipelineLayer, PipelineParallel,  # noqa: F401
-                       PipelineParallelWithInterleave)
+                       PipelineParallelWithInterleave, PipelineParallelWithInterleaveFthenB)
+from . import sharding  # noqa: F401,E402
 from ..layers.mpu import (VocabParallelEmbedding, ColumnParallelLinear, RowParallelLinear,  # noqa: F401
                           ParallelCrossEntropy, get_rng_state_tracker, model_parallel_random_seed)
 from ....nn.layer.layers import Layer as _Layer

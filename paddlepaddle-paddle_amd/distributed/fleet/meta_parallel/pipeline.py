@@ -530,4 +530,26 @@ class PipelineParallelWithInterleave(PipelineParallel):
         return self.total_loss
 
 
+
+class PipelineParallelWithInterleaveFthenB(PipelineParallelWithInterleave):
+    """Virtual pipeline stages with the forward-then-backward order (reference:
+    pipeline_parallel.py:1831 PipelineParallelWithInterleaveFthenB; fleet.distributed_model picks
+    it when pp_degree <= accumulate_steps < 2 * pp_degree): every forward unit of the interleaved
+    order first, then every backward unit in reverse — the interleaved 1F1B schedule without its
+    steady state, which needs fewer micro-batches (P) than 1F1B's warm-up (2P) at the cost of
+    holding all micro-batches' activations.  Sends are asynchronous and receives block in one
+    global order per channel, so the schedule is deadlock-free like the 1F1B one."""
+
+    def _units(self, n, V, P, r):
+        total = n * V
+        fch = lambda k: (k % (P * V)) // P  # noqa: E731
+        mb = lambda k: (k // (P * V)) * P + k % P  # noqa: E731
+        if n % P != 0:
+            self.schedule = 'breadth_first'
+            return ([('F', v, m) for v in range(V) for m in range(n)] +
+                    [('B', v, m) for v in reversed(range(V)) for m in range(n)])
+        self.schedule = 'interleaved_fthenb'
+        return ([('F', fch(k), mb(k)) for k in range(total)] +
+                [('B', V - 1 - fch(k), mb(k)) for k in range(total)])
+
 _DT = [torch.float32, torch.float16, torch.bfloat16, torch.float64, torch.int64, torch.int32, torch.bool]

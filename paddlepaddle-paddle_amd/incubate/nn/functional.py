@@ -768,6 +768,89 @@ def variable_length_memory_efficient_attention(query, key, value, seq_lens, kv_s
     return _w(torch.einsum('bhqk,bhkd->bhqd', p, v.float()).to(q.dtype))
 
 
+def fused_dot_product_attention(q, k, v, mask, scaling_factor, dropout_prob, is_training, is_causal_masking,
+                                use_workspace_opt=None, return_softmax=False):
+    """Scaled dot-product attention on BSHD bf16 / fp16 (reference
+    incubate/nn/functional/fused_dot_product_attention.py:22, a cuDNN fused kernel there): the
+    hand-written flash-attention kernel (csrc/flash_attn.hip) with the int / bool keep-mask
+    [B, 1, Sq, Sk] (1 = attend) or causal masking, in-kernel dropout and ``scaling_factor``.
+    ``return_softmax`` additionally returns the [B, H, Sq, Sk] probabilities (recomputed)."""
+    qt, kt, vt = _u(q), _u(k), _u(v)
+    B, Sq, Sk = qt.shape[0], qt.shape[1], kt.shape[1]
+    m = None
+    if mask is not None and not is_causal_masking:
+        mt = _u(mask)
+        if tuple(mt.shape) != (B, 1, Sq, Sk):
+            raise ValueError(f"mask shape must be [batch_size, 1, q_seqlen, k_seqlen], got {list(mt.shape)}")
+        m = mt.bool() if mt.dtype != torch.bool else mt
+        if bool(m.all()):
+            m = None  # the reference's all-ones default
+    p = float(dropout_prob) if is_training else 0.0
+    out = _attend(qt, kt, vt, m, p, bool(is_causal_masking), bool(is_training), scale=float(scaling_factor))
+    if not return_softmax:
+        return _w(out)
+    s = torch.einsum('bqhd,bkhd->bhqk', qt.float(), kt.float()) * float(scaling_factor)
+    if is_causal_masking:
+        s = s.masked_fill(torch.ones(Sq, Sk, dtype=torch.bool, device=s.device).tril(Sk - Sq).logical_not(),
+                          float('-inf'))
+    elif m is not None:
+        s = s.masked_fill(~m, float('-inf'))
+    return _w(out), _w(torch.softmax(s, -1).to(qt.dtype))
+
+
+def fused_gate_attention(query, key=None, query_weight=None, key_weight=None, value_weight=None, qkv_weight=None,
+                         gate_linear_weight=None, gate_linear_bias=None, out_linear_weight=None,
+                         out_linear_bias=None, nonbatched_bias=None, attn_mask=None, has_gating=True,
+                         merge_qkv=True, use_flash_attn=False):
+    """AlphaFold-style gated self-attention over [batch, msa_len, res_len, q_dim] (reference
+    incubate/nn/functional/fused_gate_attention.py:19):
+      q, k, v = projections (packed qkv_weight [3, H, c, q_dim], or separate [dim, H, c] weights)
+      logits  = q k^T * c^-0.5 + attn_mask [B, msa, 1, 1, m] (+ nonbatched_bias [B, 1, H, res, m])
+      o       = softmax(logits) v  (* sigmoid(query @ gate_w + gate_b) when has_gating)
+      out     = o @ out_linear_weight [H, c, q_dim] + out_linear_bias.
+    Every projection and both attention products are two-operand contractions on the hand-written
+    (batched) GEMM for bf16 / fp16 GPU operands (ops/matmul.py); the softmax runs in fp32."""
+    qd = _u(query)
+    if merge_qkv:
+        if qkv_weight is None:
+            raise ValueError("fused_gate_attention: merge_qkv=True needs qkv_weight [3, H, c, q_dim]")
+        w = _u(qkv_weight)
+        H, c = w.shape[1], w.shape[2]
+        qkv = ops.matmul.matmul(qd.reshape(-1, qd.shape[-1]), w.reshape(3 * H * c, -1).t().to(qd.dtype))
+        qkv = qkv.reshape(*qd.shape[:-1], 3, H, c)
+        q, k, v = qkv[..., 0, :, :], qkv[..., 1, :, :], qkv[..., 2, :, :]
+    else:
+        md = _u(key) if key is not None else qd
+        qw, kw, vw = _u(query_weight), _u(key_weight), _u(value_weight)
+        H, c = qw.shape[1], qw.shape[2]
+        q = ops.matmul.matmul(qd.reshape(-1, qd.shape[-1]), qw.reshape(qw.shape[0], -1).to(qd.dtype))
+        k = ops.matmul.matmul(md.reshape(-1, md.shape[-1]), kw.reshape(kw.shape[0], -1).to(qd.dtype))
+        v = ops.matmul.matmul(md.reshape(-1, md.shape[-1]), vw.reshape(vw.shape[0], -1).to(qd.dtype))
+        q = q.reshape(*qd.shape[:-1], H, c)
+        k = k.reshape(*md.shape[:-1], H, c)
+        v = v.reshape(*md.shape[:-1], H, c)
+    q = q * (c ** -0.5)
+    # [n, b, q, h, c] -> [n, b, h, q, c]
+    qh, kh, vh = q.permute(0, 1, 3, 2, 4), k.permute(0, 1, 3, 2, 4), v.permute(0, 1, 3, 2, 4)
+    logits = ops.matmul.matmul(qh, kh.transpose(-1, -2)).float()          # [n, b, h, q, m]
+    if attn_mask is not None:
+        logits = logits + _u(attn_mask).float()
+    if nonbatched_bias is not None:
+        logits = logits + _u(nonbatched_bias).float()
+    wts = torch.softmax(logits, -1).to(vh.dtype)
+    o = ops.matmul.matmul(wts, vh).permute(0, 1, 3, 2, 4)                  # [n, b, q, h, c]
+    if has_gating:
+        gw, gb = _u(gate_linear_weight), _u(gate_linear_bias)
+        gv = ops.matmul.matmul(qd.reshape(-1, qd.shape[-1]), gw.reshape(gw.shape[0], -1).to(qd.dtype))
+        gv = gv.reshape(*qd.shape[:-1], H, c) + gb.to(gv.dtype)
+        o = o * torch.sigmoid(gv.float()).to(o.dtype)
+    ow = _u(out_linear_weight)
+    out = ops.matmul.matmul(o.reshape(-1, H * c), ow.reshape(H * c, -1).to(o.dtype))
+    if out_linear_bias is not None:
+        out = out + _u(out_linear_bias).to(out.dtype)
+    return _w(out.reshape(*qd.shape[:-1], -1))
+
+
 def fused_ec_moe(x, gate, bmm0_weight, bmm0_bias, bmm1_weight, bmm1_bias, act_type):
     """Every token through every expert, combined with the softmaxed gate (reference
     incubate/nn/functional/fused_ec_moe.py:18, kernel fusion/cutlass/moe_kernel.cu).  The expert

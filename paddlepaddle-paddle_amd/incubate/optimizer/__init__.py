@@ -91,3 +91,5 @@ class ModelAverage:
 
 from ...optimizer.algorithms import LBFGS  # noqa: E402,F401  (reference: incubate/optimizer/lbfgs.py)
 from . import functional  # noqa: E402,F401
+
+from .distributed_fused_lamb import DistributedFusedLamb  # noqa: E402,F401

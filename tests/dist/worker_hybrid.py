@@ -135,11 +135,11 @@ class Block(nn.Layer):
         return paddle.tanh(self.fc(x))
 
 
-def pp_test(virtual=1):
+def pp_test(virtual=1, acc=4):
     world = int(os.environ['WORLD_SIZE'])
     s = fleet.DistributedStrategy()
     s.hybrid_configs = {'dp_degree': 1, 'mp_degree': 1, 'pp_degree': world}
-    s.pipeline_configs = {'accumulate_steps': 4, 'micro_batch_size': 2}
+    s.pipeline_configs = {'accumulate_steps': acc, 'micro_batch_size': 8 // acc}
     fleet.init(is_collective=True, strategy=s)
     d = 6
     nblk = 2 * world * virtual
@@ -163,25 +163,29 @@ def pp_test(virtual=1):
     x = paddle.to_tensor(np.random.RandomState(0).randn(8, d).astype('float32'))
     y = paddle.to_tensor(np.random.RandomState(1).randn(8, d).astype('float32'))
     loss = model.train_batch([x, y], opt)
-    # reference: same 4 micro-batches, mean of per-micro-batch losses
+    # reference: same micro-batches, mean of per-micro-batch losses
     ropt = paddle.optimizer.SGD(learning_rate=0.1, parameters=[p for b in full for p in b.parameters()])
     tot = 0.0
-    for mb in range(4):
-        h = x[mb * 2:(mb + 1) * 2]
+    mbs = 8 // acc
+    for mb in range(acc):
+        h = x[mb * mbs:(mb + 1) * mbs]
         for b in full:
             h = b(h)
-        l = loss_fn(h, y[mb * 2:(mb + 1) * 2]) / 4
+        l = loss_fn(h, y[mb * mbs:(mb + 1) * mbs]) / acc
         l.backward()
         tot += float(l)
     ropt.step()
     assert abs(float(loss) - tot) < 1e-5, (float(loss), tot)
     for blk, gi in zip(pl.run_function, owned):
         np.testing.assert_allclose(blk.fc.weight.numpy(), full[gi].fc.weight.numpy(), atol=1e-5)
-    tag = 'pp' if virtual == 1 else 'vpp'
+    tag = 'pp' if virtual == 1 else ('vpp' if acc < 2 * world else 'vpp8')
     if virtual > 1:
-        assert model.schedule == 'interleaved_1f1b', model.schedule
+        # the reference's choice (fleet/model.py:168): FthenB for pp <= acc < 2 pp, else 1F1B
+        want = 'interleaved_fthenb' if acc < 2 * world else 'interleaved_1f1b'
+        assert model.schedule == want, (model.schedule, want)
     print(f"rank{dist.get_rank()} {tag} OK stage{stage}", flush=True)
 
 
 if __name__ == '__main__':
-    {'tp': tp_test, 'sp': sp_test, 'pp': pp_test, 'vpp': lambda: pp_test(2), 'tpdp': tpdp_test}[sys.argv[1]]()
+    {'tp': tp_test, 'sp': sp_test, 'pp': pp_test, 'vpp': lambda: pp_test(2), 'vpp8': lambda: pp_test(2, 8),
+     'tpdp': tpdp_test}[sys.argv[1]]()

@@ -1,0 +1,116 @@
+"""Round-4 API surface: DistributedFusedLamb, fleet.utils.mix_precision_utils, the
+fleet.meta_parallel.sharding module path (GroupShardedOptimizerStage2 / GroupShardedStage2 /
+GroupShardedStage3) — each against the plain single-process computation it must equal."""
+import numpy as np
+import pytest
+import torch
+
+import paddle
+
+nn = paddle.nn
+
+
+def _train(model, opt, steps=4, accumulate=1, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    xs = [paddle.to_tensor(torch.randn(16, 8, generator=g)) for _ in range(steps * accumulate)]
+    losses = []
+    for i, x in enumerate(xs):
+        loss = (model(x) ** 2).mean()
+        loss.backward()
+        if (i + 1) % accumulate == 0:
+            opt.step()
+            opt.clear_grad()
+        losses.append(float(loss))
+    return losses
+
+
+def test_distributed_fused_lamb_matches_lamb():
+    from paddle.incubate.optimizer import DistributedFusedLamb
+    res = []
+    for kind in ('ref', 'dfl'):
+        paddle.seed(0)
+        m = nn.Sequential(nn.Linear(8, 16), nn.Tanh(), nn.Linear(16, 4))
+        excl = lambda p: p.name.endswith('b_0') or 'bias' in p.name  # noqa: E731
+        clip = nn.ClipGradByGlobalNorm(0.5)
+        if kind == 'ref':
+            opt = paddle.optimizer.Lamb(1e-2, parameters=m.parameters(), lamb_weight_decay=0.05, grad_clip=clip,
+                                        exclude_from_weight_decay_fn=excl)
+        else:
+            opt = DistributedFusedLamb(1e-2, parameters=m.parameters(), lamb_weight_decay=0.05, grad_clip=clip,
+                                       exclude_from_weight_decay_fn=excl)
+        res.append((_train(m, opt), [p.numpy() for p in m.parameters()]))
+    (la, pa), (lb, pb) = res
+    np.testing.assert_allclose(la, lb, rtol=1e-5)
+    for a, b in zip(pa, pb):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_distributed_fused_lamb_gradient_accumulation():
+    """gradient_accumulation_steps=2 over micro-batches == Lamb on the mean gradient."""
+    from paddle.incubate.optimizer import DistributedFusedLamb
+    paddle.seed(0)
+    m = nn.Linear(8, 4)
+    opt = DistributedFusedLamb(1e-2, parameters=m.parameters(), gradient_accumulation_steps=2)
+    g = torch.Generator().manual_seed(3)
+    xs = [paddle.to_tensor(torch.randn(16, 8, generator=g)) for _ in range(4)]
+    for x in xs:
+        (m(x) ** 2).mean().backward()
+        opt.step()
+        opt.clear_grad()
+    paddle.seed(0)
+    m2 = nn.Linear(8, 4)
+    opt2 = paddle.optimizer.Lamb(1e-2, parameters=m2.parameters())
+    for i in range(0, 4, 2):
+        ((m2(xs[i]) ** 2).mean() * 0.5 + (m2(xs[i + 1]) ** 2).mean() * 0.5).backward()
+        opt2.step()
+        opt2.clear_grad()
+    np.testing.assert_allclose(m.weight.numpy(), m2.weight.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_mix_precision_main_grad():
+    """bf16 model + MixPrecisionLayer/Optimizer: gradients accumulate in an fp32 main_grad (the
+    bf16 .grad is released) and the update equals AdamW on the fp32 main gradients."""
+    from paddle.distributed.fleet.utils import mix_precision_utils as mpu
+    paddle.seed(0)
+    m = nn.Linear(8, 4)
+    m.to(dtype='bfloat16')
+    mm = mpu.MixPrecisionLayer(m, dtype='bfloat16')
+    opt = mpu.MixPrecisionOptimizer(paddle.optimizer.AdamW(1e-2, parameters=m.parameters(), multi_precision=True))
+    x = paddle.to_tensor(torch.randn(16, 8).bfloat16())
+    for _ in range(2):  # two micro-batches accumulate into main_grad
+        (mm(x).astype('float32') ** 2).mean().backward()
+    w = m.weight
+    assert w.grad is None and w.main_grad is not None and w.main_grad.dtype == paddle.float32
+    mg = w.main_grad.numpy().copy()
+    w0 = w._t.float().clone()
+    opt.step()
+    opt.clear_grad()
+    assert float(w.main_grad.abs().sum()) == 0.0
+    # reference: one AdamW step on the fp32 master with gradient mg
+    ref = paddle.optimizer.AdamW(1e-2, parameters=[paddle.create_parameter([8, 4], 'float32')])
+    p = ref._parameter_list[0]
+    p._t.data.copy_(w0)
+    p._t.grad = torch.from_numpy(mg)
+    ref.step()
+    np.testing.assert_allclose(w._t.detach().float().numpy(), p._t.detach().bfloat16().float().numpy(), atol=1e-2)
+
+
+@pytest.mark.parametrize('stage', [2, 3])
+def test_meta_parallel_sharding_module_path(stage):
+    from paddle.distributed.fleet.meta_parallel.sharding import (GroupShardedOptimizerStage2, GroupShardedStage2,
+                                                                  GroupShardedStage3, GroupShardedScaler)
+    res = []
+    for wrap in (False, True):
+        paddle.seed(0)
+        m = nn.Sequential(nn.Linear(8, 32), nn.ReLU(), nn.Linear(32, 4))
+        opt = paddle.optimizer.AdamW(1e-2, parameters=m.parameters())
+        model, o = m, opt
+        if wrap and stage == 2:
+            o = GroupShardedOptimizerStage2(m.parameters(), opt)
+            model = GroupShardedStage2(m, o)
+        elif wrap:
+            model = GroupShardedStage3(m, opt)
+        res.append(_train(model, o))
+    np.testing.assert_allclose(res[0], res[1], rtol=1e-5)
+    s = paddle.amp.GradScaler()
+    assert GroupShardedScaler(s) is s

@@ -104,9 +104,10 @@ def test_rpc_sync_async_between_workers():
     assert out.count("rpc OK") == 2, out[-3000:]
 
 
-@pytest.mark.parametrize("mode", ['pp', 'vpp'])
+@pytest.mark.parametrize("mode", ['pp', 'vpp', 'vpp8'])
 def test_pipeline_four_stages(mode):
-    """4 ranks: 1F1B and the interleaved 1F1B virtual-stage schedule match single-device SGD."""
+    """4 ranks: 1F1B, the interleaved forward-then-backward (accumulate 4 = pp) and the interleaved
+    1F1B (accumulate 8 = 2 pp) virtual-stage schedules match single-device SGD."""
     out = run_workers('worker_hybrid.py', mode, nproc=4)
     assert out.count(f'{mode} OK') == 4, out[-3000:]
 
