@@ -49,6 +49,8 @@ from . import nn  # noqa: E402,F401
 from . import optimizer  # noqa: E402,F401
 from . import regularizer  # noqa: E402,F401
 from . import ops  # noqa: E402,F401
+from . import _C_ops  # noqa: E402,F401
+from . import pir  # noqa: E402,F401
 from .tensor.linalg import (matmul, bmm, mm, dot, mv, einsum, norm as _norm, cdist, pdist, histogram,  # noqa: E402,F401
                             histogramdd, bincount, cross)
 from .tensor.math import prod  # noqa: E402,F401

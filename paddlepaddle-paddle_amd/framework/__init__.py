@@ -96,3 +96,5 @@ def _current_expected_place():
 
 
 _ = os
+
+from .. import core  # noqa: E402,F401  (paddle.framework.core: reference C++ module surface)

@@ -30,6 +30,9 @@ _REGISTRY = {
     'FLAGS_selected_gpus': '0',
     'FLAGS_comm_timeout_seconds': 1800,
     'FLAGS_enable_async_trace': False,
+    'FLAGS_prim_all': False,
+    'FLAGS_prim_forward': False,
+    'FLAGS_prim_backward': False,
 }
 
 
@@ -84,3 +87,23 @@ def get_flags(flags):
 
 def get(name, default=None):
     return _REGISTRY.get(name, default)
+
+
+class _FlagsView:
+    """core.globals(): dict-style access to the registry (setting goes through set_flags)."""
+
+    def __getitem__(self, k):
+        return get_flags([k])[k]
+
+    def __setitem__(self, k, v):
+        set_flags({k: v})
+
+    def __contains__(self, k):
+        return (k if k.startswith('FLAGS_') else 'FLAGS_' + k) in _REGISTRY
+
+    def keys(self):
+        return list(_REGISTRY.keys())
+
+    def get(self, k, default=None):
+        return self[k] if k in self else default
+

@@ -56,10 +56,13 @@ def get_num_bytes_of_data_type(dtype):
 
 class Config:
     def __init__(self, model_file=None, params_file=None):
-        if model_file is not None and params_file is None and not str(model_file).endswith('.pdmodel'):
-            self._prefix = str(model_file).rstrip('/') + '/inference'  # model_dir form
-        elif model_file is not None:
-            self._prefix = str(model_file)[:-len('.pdmodel')] if str(model_file).endswith('.pdmodel') else model_file
+        mf = str(model_file) if model_file is not None else None
+        ext = next((e for e in ('.pdmodel', '.json') if mf is not None and mf.endswith(e)), None)
+        if mf is not None and params_file is None and ext is None:
+            self._prefix = mf.rstrip('/') + '/inference'  # model_dir form
+        elif mf is not None:
+            # <prefix>.pdmodel (ProgramDesc / this framework's IR) or <prefix>.json (the reference's PIR)
+            self._prefix = mf[:-len(ext)] if ext else mf
         else:
             self._prefix = None
         self._use_gpu = torch.cuda.is_available()
@@ -77,6 +80,9 @@ class Config:
         return self._prefix
 
     def prog_file(self):
+        import os
+        if not os.path.exists(self._prefix + '.pdmodel') and os.path.exists(self._prefix + '.json'):
+            return self._prefix + '.json'
         return self._prefix + '.pdmodel'
 
     def params_file(self):

@@ -235,6 +235,8 @@ def save_inference_model(path_prefix, feed_vars, fetch_vars, executor=None, prog
     d = os.path.dirname(path_prefix)
     if d:
         os.makedirs(d, exist_ok=True)
+    if _pir_mode(kwargs) and save_pir(feed_vars, fetch_vars, path_prefix, program):
+        return
     with open(path_prefix + '.pdmodel', 'wb') as f:
         f.write(serialize_program(feed_vars, fetch_vars, program))
     with open(path_prefix + '.pdiparams', 'wb') as f:
@@ -246,11 +248,46 @@ class LoadedProgram(Program):
 
 
 def deserialize_program(data, device=None):
-    from . import pdmodel
+    from . import pdmodel, pir_json
     with _paused():
         if isinstance(data, (bytes, bytearray)) and pdmodel.is_program_desc(bytes(data[:1])):
             return pdmodel.load(bytes(data))
+        if pir_json.is_pir_json(data):  # the reference's PIR .json program (save_pir)
+            return pir_json.load(data)
         return _deserialize_program(data, device)
+
+
+def _pir_mode(kwargs):
+    """Write the reference's PIR .json program instead of a ProgramDesc: format='pir' /
+    FLAGS_enable_pir_api (the reference 3.x default) / PADDLE_AMD_PIR=1."""
+    fmt = kwargs.get('format')
+    if fmt is not None:
+        return str(fmt).lower() in ('pir', 'json')
+    if os.environ.get('PADDLE_AMD_PIR') is not None:
+        return os.environ['PADDLE_AMD_PIR'] == '1'
+    try:
+        from ..framework.flags import get_flags
+        return bool(get_flags(['FLAGS_enable_pir_api']).get('FLAGS_enable_pir_api', False))
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def save_pir(feed_vars, fetch_vars, path_prefix, program=None):
+    """<prefix>.json (PIR program) + <prefix>.pdiparams; returns False when the program uses an
+    operator outside the lowered set (the caller then writes the other format)."""
+    from . import pdmodel, pir_json
+    prog = program or default_main_program()
+    feed_names = [v.name if isinstance(v, Tensor) else v for v in feed_vars]
+    try:
+        data, params = pir_json.export(prog, feed_names, _fetch_vids(prog, fetch_vars))
+    except pdmodel.Unsupported:
+        return False
+    from .proto import save_combine
+    with open(path_prefix + '.json', 'wb') as f:
+        f.write(data)
+    with open(path_prefix + '.pdiparams', 'wb') as f:
+        f.write(save_combine([(n, t.detach()) for n, t in params]))
+    return True
 
 
 def _deserialize_program(data, device=None):
@@ -302,7 +339,9 @@ def load_inference_model(path_prefix, executor=None, **kwargs):
     """Returns [program, feed_target_names, fetch_targets]."""
     from ..core.place import to_device
     dev = executor._dev if executor is not None and hasattr(executor, '_dev') else to_device(None)
-    with open(path_prefix + '.pdmodel', 'rb') as f:
+    model = path_prefix + '.json' if os.path.exists(path_prefix + '.json') and \
+        not os.path.exists(path_prefix + '.pdmodel') else path_prefix + '.pdmodel'
+    with open(model, 'rb') as f:
         prog = deserialize_program(f.read(), dev)
     with open(path_prefix + '.pdiparams', 'rb') as f:
         deserialize_persistables(prog, f.read(), executor, dev)

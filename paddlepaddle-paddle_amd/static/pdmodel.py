@@ -164,12 +164,13 @@ def _layer_norm(ins, at):
 
 
 def _matmul_v2(ins, at):
+    from ..ops import matmul as _hm  # bf16 / fp16 GPU operands: the hand-written GEMM
     x, y = _one(ins, 'X'), _one(ins, 'Y')
     if at.get('trans_x', False):
         x = x.transpose(-1, -2) if x.dim() > 1 else x
     if at.get('trans_y', False):
         y = y.transpose(-1, -2) if y.dim() > 1 else y
-    return {'Out': [torch.matmul(x, y)]}
+    return {'Out': [_hm.matmul(x, y)]}
 
 
 def _matmul_v1(ins, at):
@@ -258,6 +259,264 @@ def _dropout(ins, at):
     return {'Out': [x * (1.0 - p) if impl == 'downgrade_in_infer' else x]}
 
 
+# ---- widened set: the operators the reference's jit.save / save_inference_model write for the
+# vision zoo (interp, pad, conv transpose, group / instance norm, prelu, fc), ERNIE / GPT
+# (fill_constant, shape, stack, gather, where, tril_triu, split, expand_v2, range, comparisons,
+# cumsum, top_k_v2, one_hot_v2, index_select) — legacy slot / attribute names of
+# paddle/phi/api/yaml/op_compat.yaml.
+def _fill_constant(ins, at):
+    shape = at.get('shape', [])
+    st = ins.get('ShapeTensor') or []
+    if st:
+        shape = [int(v) for v in st[0].reshape(-1).tolist()]
+    val = at.get('value', 0.0)
+    if at.get('str_value'):
+        val = float(at['str_value'])
+    vt = ins.get('ValueTensor') or []
+    if vt:
+        val = vt[0].reshape(-1)[0].item()
+    return {'Out': [torch.full(list(shape), val, dtype=P.torch_dtype(at.get('dtype', 5)))]}
+
+
+def _stack(ins, at):
+    return {'Y': [torch.stack(ins['X'], at.get('axis', 0))]}
+
+
+def _gather(ins, at):
+    x, idx = _one(ins, 'X'), _one(ins, 'Index')
+    ax = at.get('axis', 0)
+    if ins.get('Axis'):
+        ax = int(ins['Axis'][0].reshape(-1)[0])
+    return {'Out': [torch.index_select(x, ax, idx.reshape(-1).long()).reshape(
+        list(x.shape[:ax]) + list(idx.shape) + list(x.shape[ax + 1:]) if idx.dim() != 1 else
+        list(x.shape[:ax]) + [idx.shape[0]] + list(x.shape[ax + 1:]))]}
+
+
+def _split(ins, at):
+    x = _one(ins, 'X')
+    ax = at.get('axis', 0)
+    if ins.get('AxisTensor'):
+        ax = int(ins['AxisTensor'][0].reshape(-1)[0])
+    ax %= x.dim()
+    sec = at.get('sections', [])
+    if sec:
+        sec = list(sec)
+        if -1 in sec:
+            sec[sec.index(-1)] = x.shape[ax] - (sum(sec) + 1)
+        return {'Out': list(torch.split(x, sec, ax))}
+    return {'Out': list(torch.chunk(x, at.get('num', 1), ax))}
+
+
+def _expand_v2(ins, at):
+    x = _one(ins, 'X')
+    shape = list(at.get('shape', []))
+    if ins.get('Shape'):
+        shape = [int(v) for v in ins['Shape'][0].reshape(-1).tolist()]
+    lead = len(shape) - x.dim()
+    shape = [x.shape[i - lead] if s == -1 else s for i, s in enumerate(shape)]
+    return {'Out': [x.expand(shape)]}
+
+
+def _cmp(fn):
+    return lambda ins, at: {'Out': [fn(_one(ins, 'X'), _one(ins, 'Y'))]}
+
+
+def _cumsum(ins, at):
+    x = _one(ins, 'X')
+    if at.get('flatten', False):
+        x = x.reshape(-1)
+    ax = at.get('axis', -1)
+    if at.get('reverse', False):
+        x = x.flip(ax)
+    y = x.cumsum(ax)
+    if at.get('exclusive', False):
+        y = y - x
+    return {'Out': [y.flip(ax) if at.get('reverse', False) else y]}
+
+
+def _top_k_v2(ins, at):
+    x = _one(ins, 'X')
+    k = at.get('k', 1)
+    if ins.get('K'):
+        k = int(ins['K'][0].reshape(-1)[0])
+    v, i = torch.topk(x, k, at.get('axis', -1), largest=at.get('largest', True), sorted=at.get('sorted', True))
+    return {'Out': [v], 'Indices': [i]}
+
+
+def _interp(mode):
+    def f(ins, at):
+        x = _one(ins, 'X')
+        nhwc = at.get('data_layout', 'NCHW') == 'NHWC'
+        if nhwc:
+            x = x.permute(0, 3, 1, 2)
+        oh, ow = at.get('out_h', -1), at.get('out_w', -1)
+        if ins.get('OutSize'):
+            oh, ow = [int(v) for v in ins['OutSize'][0].reshape(-1).tolist()]
+        sc = at.get('scale', [])
+        kw = {}
+        if oh > 0 and ow > 0:
+            kw['size'] = (oh, ow)
+        else:
+            kw['scale_factor'] = tuple(sc) if len(sc) == 2 else (sc[0], sc[0])
+        if mode == 'nearest':
+            y = TF.interpolate(x, mode='nearest', **kw)
+        else:
+            y = TF.interpolate(x, mode=mode, align_corners=at.get('align_corners', False), **kw)
+        return {'Out': [y.permute(0, 2, 3, 1) if nhwc else y]}
+    return f
+
+
+def _pad3d(ins, at):
+    x = _one(ins, 'X')
+    p = at.get('paddings', [0] * 6)  # [left, right, top, bottom, front, back]
+    mode = at.get('mode', 'constant')
+    ndhwc = at.get('data_format', 'NCDHW') == 'NDHWC'
+    if ndhwc:
+        x = x.permute(0, 4, 1, 2, 3)
+    y = TF.pad(x, list(p), mode=mode, value=at.get('value', 0.0)) if mode == 'constant' else TF.pad(x, list(p), mode=mode)
+    return {'Out': [y.permute(0, 2, 3, 4, 1) if ndhwc else y]}
+
+
+def _conv2d_transpose(ins, at):
+    x, w = _one(ins, 'Input'), _one(ins, 'Filter')
+    nhwc = at.get('data_format', 'NCHW') == 'NHWC'
+    if nhwc:
+        x = x.permute(0, 3, 1, 2)
+    p = at.get('paddings', [0, 0])
+    pad = (p[0], p[2]) if len(p) == 4 else tuple(p)
+    op = at.get('output_padding', []) or [0, 0]
+    y = TF.conv_transpose2d(x, w, None, at.get('strides', [1, 1]), pad, tuple(op), at.get('groups', 1),
+                            at.get('dilations', [1, 1]))
+    return {'Output': [y.permute(0, 2, 3, 1) if nhwc else y]}
+
+
+def _group_norm(ins, at):
+    x = _one(ins, 'X')
+    nhwc = at.get('data_layout', 'NCHW') == 'NHWC'
+    xt = x.movedim(-1, 1) if nhwc else x
+    y = TF.group_norm(xt, at.get('groups', 1), _one(ins, 'Scale'), _one(ins, 'Bias'), at.get('epsilon', 1e-5))
+    return {'Y': [y.movedim(1, -1) if nhwc else y]}
+
+
+def _instance_norm(ins, at):
+    x = _one(ins, 'X')
+    return {'Y': [TF.instance_norm(x, weight=_one(ins, 'Scale'), bias=_one(ins, 'Bias'), eps=at.get('epsilon', 1e-5))]}
+
+
+def _prelu(ins, at):
+    x, a = _one(ins, 'X'), _one(ins, 'Alpha')
+    mode = at.get('mode', 'all')
+    if mode == 'channel':
+        shp = [1, -1] + [1] * (x.dim() - 2) if at.get('data_format', 'NCHW') == 'NCHW' else [1] * (x.dim() - 1) + [-1]
+        a = a.reshape(shp)
+    elif mode == 'element':
+        a = a.reshape([1] + list(x.shape[1:]))
+    return {'Out': [torch.where(x >= 0, x, a * x)]}
+
+
+def _fc(ins, at):
+    from ..ops import matmul as _hm
+    x, w, b = _one(ins, 'Input'), _one(ins, 'W'), _one(ins, 'Bias')
+    n = at.get('in_num_col_dims', 1)
+    x2 = x.reshape(int(math.prod(x.shape[:n])), -1)
+    y = _hm.matmul(x2, w)
+    if b is not None:
+        y = y + b.reshape(1, -1)
+    if at.get('activation_type', '') == 'relu':
+        y = torch.relu(y)
+    return {'Out': [y.reshape(*x.shape[:n], -1)]}
+
+
+def _p_norm(ins, at):
+    x = _one(ins, 'X')
+    p = at.get('porder', 2.0)
+    if at.get('asvector', False):
+        return {'Out': [torch.linalg.vector_norm(x.reshape(-1), p)]}
+    return {'Out': [torch.linalg.vector_norm(x, p, dim=at.get('axis', -1), keepdim=at.get('keepdim', False))]}
+
+
+def _assign_value(ins, at):
+    dt = P.torch_dtype(at.get('dtype', 5))
+    for k in ('fp32_values', 'int32_values', 'int64_values', 'bool_values', 'fp64_values'):
+        if at.get(k):
+            return {'Out': [torch.tensor(at[k], dtype=dt).reshape(at.get('shape', [-1]))]}
+    vals = at.get('values', [])
+    return {'Out': [torch.tensor(vals, dtype=dt).reshape(at.get('shape', [-1]))]}
+
+
+def _fold(x, dims, keep, fn):
+    """A one-axis reduction applied over several axes (highest first, so indices stay valid)."""
+    for d in sorted(dims, reverse=True):
+        x = fn(x, d, keepdim=keep)
+    return x
+
+
+def _arange(ins, at):
+    s, e, st = (_one(ins, k).reshape(-1)[0].item() for k in ('Start', 'End', 'Step'))
+    return {'Out': [torch.arange(s, e, st, dtype=_one(ins, 'Start').dtype)]}
+
+
+OPS_EXTRA = {
+    'fill_constant': _fill_constant,
+    'shape': lambda ins, at: {'Out': [torch.tensor(list(_one(ins, 'Input').shape), dtype=torch.int32)]},
+    'stack': _stack, 'gather': _gather,
+    'where': lambda ins, at: {'Out': [torch.where(_one(ins, 'Condition').bool(), _one(ins, 'X'), _one(ins, 'Y'))]},
+    'tril_triu': lambda ins, at: {'Out': [(torch.tril if at.get('lower', True) else torch.triu)(
+        _one(ins, 'X'), at.get('diagonal', 0))]},
+    'split': _split, 'expand_v2': _expand_v2,
+    'tile': lambda ins, at: {'Out': [_one(ins, 'X').repeat(*(
+        [1] * (len(at['repeat_times']) - _one(ins, 'X').dim()) + list(at['repeat_times'])))]},
+    'range': _arange,
+    'equal': _cmp(torch.eq), 'not_equal': _cmp(torch.ne), 'less_than': _cmp(torch.lt),
+    'less_equal': _cmp(torch.le), 'greater_than': _cmp(torch.gt), 'greater_equal': _cmp(torch.ge),
+    'logical_and': _cmp(torch.logical_and), 'logical_or': _cmp(torch.logical_or),
+    'logical_xor': _cmp(torch.logical_xor),
+    'logical_not': lambda ins, at: {'Out': [torch.logical_not(_one(ins, 'X'))]},
+    'cumsum': _cumsum, 'top_k_v2': _top_k_v2,
+    'one_hot_v2': lambda ins, at: {'Out': [TF.one_hot(_one(ins, 'X').long(), at['depth']).float()]},
+    'index_select': lambda ins, at: {'Out': [torch.index_select(_one(ins, 'X'), at.get('dim', 0),
+                                                                _one(ins, 'Index').long())]},
+    'sin': _act(lambda x, a: torch.sin(x)), 'cos': _act(lambda x, a: torch.cos(x)),
+    'log': _act(lambda x, a: torch.log(x)), 'square': _act(lambda x, a: x * x),
+    'sign': _act(lambda x, a: torch.sign(x)), 'floor': _act(lambda x, a: torch.floor(x)),
+    'ceil': _act(lambda x, a: torch.ceil(x)), 'round': _act(lambda x, a: torch.round(x)),
+    'reciprocal': _act(lambda x, a: torch.reciprocal(x)), 'erf': _act(lambda x, a: torch.erf(x)),
+    'softplus': _act(lambda x, a: TF.softplus(x, a.get('beta', 1.0), a.get('threshold', 20.0))),
+    'mish': _act(lambda x, a: TF.mish(x)), 'elu': _act(lambda x, a: TF.elu(x, a.get('alpha', 1.0))),
+    'selu': _act(lambda x, a: TF.selu(x)), 'celu': _act(lambda x, a: TF.celu(x, a.get('alpha', 1.0))),
+    'pow': _act(lambda x, a: torch.pow(x, a.get('factor', 1.0))),
+    'elementwise_floordiv': _ew(torch.floor_divide), 'elementwise_mod': _ew(torch.remainder),
+    'reduce_min': _reduce(lambda x, d, k: x.amin(d, keepdim=k)),
+    'reduce_prod': _reduce(lambda x, d, k: _fold(x, d, k, torch.prod)),
+    'reduce_any': _reduce(lambda x, d, k: _fold(x.bool(), d, k, torch.any)),
+    'reduce_all': _reduce(lambda x, d, k: _fold(x.bool(), d, k, torch.all)),
+    'p_norm': _p_norm,
+    'bilinear_interp_v2': _interp('bilinear'), 'nearest_interp_v2': _interp('nearest'),
+    'bicubic_interp_v2': _interp('bicubic'),
+    'pad3d': _pad3d, 'conv2d_transpose': _conv2d_transpose, 'group_norm': _group_norm,
+    'instance_norm': _instance_norm, 'prelu': _prelu, 'fc': _fc,
+    'argsort': lambda ins, at: dict(zip(('Out', 'Indices'), ([t] for t in torch.sort(
+        _one(ins, 'X'), at.get('axis', -1), descending=at.get('descending', False))))),
+    'arg_min': lambda ins, at: {'Out': [torch.argmin(_one(ins, 'X'), at.get('axis', -1),
+                                                     keepdim=at.get('keepdims', False))]},
+    'flip': lambda ins, at: {'Out': [torch.flip(_one(ins, 'X'), list(at.get('axis', [0])))]},
+    'roll': lambda ins, at: {'Out': [torch.roll(_one(ins, 'X'), list(at.get('shifts', [0])),
+                                                list(at.get('axis', [])) or None)]},
+    'unstack': lambda ins, at: {'Y': list(torch.unbind(_one(ins, 'X'), at.get('axis', 0)))},
+    'sum': lambda ins, at: {'Out': [sum(ins['X'][1:], ins['X'][0])]},
+    'bmm': lambda ins, at: _matmul_v2(ins, {}),
+    'fill_any_like': lambda ins, at: {'Out': [torch.full_like(
+        _one(ins, 'X'), at.get('value', 0.0), dtype=None if at.get('dtype', -1) in (-1, None) else
+        P.torch_dtype(at['dtype']))]},
+    'fill_zeros_like': lambda ins, at: {'Out': [torch.zeros_like(_one(ins, 'X'))]},
+    'assign_value': _assign_value,
+    'lookup_table': _lookup,
+    'swish': _act(lambda x, a: x * torch.sigmoid(a.get('beta', 1.0) * x)),
+    'hard_sigmoid_': None,
+}
+OPS_EXTRA.pop('hard_sigmoid_')
+
+
 OPS = {
     'conv2d': _conv2d, 'depthwise_conv2d': _conv2d, 'pool2d': _pool2d, 'batch_norm': _batch_norm,
     'layer_norm': _layer_norm, 'matmul_v2': _matmul_v2, 'matmul': _matmul_v1, 'mul': _mul,
@@ -291,6 +550,7 @@ OPS = {
     'arg_max': lambda ins, at: {'Out': [torch.argmax(_one(ins, 'X'), at.get('axis', -1),
                                                      keepdim=at.get('keepdims', False))]},
 }
+OPS.update(OPS_EXTRA)
 
 
 class _OpCall:
@@ -393,6 +653,9 @@ def load_params(prog, data, device):
         p = Parameter(t, trainable=t.is_floating_point(), name=name)
         prog.consts[cid] = p._t
         prog._const_owner[cid] = p
+    for cid, t in list(prog.consts.items()):  # literal constants of the program (PIR full ops)
+        if cid not in prog._const_names and isinstance(t, torch.Tensor):
+            prog.consts[cid] = t.to(device)
 
 
 # ============================================================================ export

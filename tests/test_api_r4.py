@@ -114,3 +114,56 @@ def test_meta_parallel_sharding_module_path(stage):
     np.testing.assert_allclose(res[0], res[1], rtol=1e-5)
     s = paddle.amp.GradScaler()
     assert GroupShardedScaler(s) is s
+
+
+def test_c_ops_surface():
+    """paddle._C_ops entry points (ops.yaml argument order) equal the paddle API / reference math."""
+    C = paddle._C_ops
+    g = torch.Generator().manual_seed(0)
+    x = paddle.to_tensor(torch.randn(4, 8, generator=g))
+    y = paddle.to_tensor(torch.randn(3, 8, generator=g))
+    np.testing.assert_allclose(C.matmul(x, y, False, True).numpy(), x.numpy() @ y.numpy().T, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(C.add(x, x).numpy(), 2 * x.numpy(), rtol=1e-6)
+    np.testing.assert_allclose(C.scale(x, 2.0, 1.0, True).numpy(), 2 * x.numpy() + 1, rtol=1e-6)
+    out, mean, var = C.layer_norm(x, None, None, 1e-5, 1)
+    np.testing.assert_allclose(mean.numpy(), x.numpy().mean(1), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(var.numpy(), x.numpy().var(1), rtol=1e-4, atol=1e-6)
+    assert C.relu(x).shape == [4, 8] and C.elementwise_mul(x, x).shape == [4, 8]
+    with pytest.raises(AttributeError):
+        C.definitely_not_an_op
+    # adamw_: in-place single-parameter update == AdamW reference formula
+    p = paddle.to_tensor(torch.randn(5, generator=g))
+    gr = paddle.to_tensor(torch.randn(5, generator=g))
+    m1, m2 = paddle.zeros([5]), paddle.zeros([5])
+    b1p, b2p = paddle.to_tensor([0.9]), paddle.to_tensor([0.999])
+    p0 = p.numpy().copy()
+    C.adamw_(p, gr, paddle.to_tensor([0.01]), m1, m2, None, b1p, b2p, None, None, 0.9, 0.999, 1e-8, 1.0, 0.01, True)
+    gg = gr.numpy()
+    mh, vh = (0.1 * gg) / 0.1, (0.001 * gg * gg) / 0.001
+    ref = p0 * (1 - 0.01 * 0.01) - 0.01 * mh / (np.sqrt(vh) + 1e-8)
+    np.testing.assert_allclose(p.numpy(), ref, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(b1p.numpy(), [0.81], rtol=1e-6)
+
+
+def test_base_core_and_pir_namespaces(static_mode, tmp_path):
+    from paddle.base import core
+    assert core.VarDesc.VarType.FP32 == 5 and core.VarDesc.VarType.BF16 == 22
+    assert core.DataType.FLOAT32 == 10
+    assert core.is_compiled_with_rocm() and not core.is_compiled_with_xpu()
+    assert core.eager.Tensor is paddle.Tensor
+    assert core.globals()['FLAGS_enable_pir_api'] in (True, False)
+    assert paddle.framework.core is core
+    main = paddle.static.Program()
+    with paddle.static.program_guard(main):
+        x = paddle.static.data('x', [None, 4], 'float32')
+        y = paddle.nn.functional.relu(paddle.static.nn.fc(x, 3))
+    ops = paddle.pir.ops_of(main)
+    assert ops and all(o.name() for o in ops)
+    exe = paddle.static.Executor(paddle.CPUPlace())
+    xs = np.random.rand(2, 4).astype('float32')
+    ref, = exe.run(main, feed={'x': xs}, fetch_list=[y])
+    path = str(tmp_path / 'm')
+    paddle.pir.save(main, path, [x], [y])
+    prog = paddle.pir.load(path + '.json')
+    got, = exe.run(prog, feed={'x': xs}, fetch_list=prog._fetch_vars)
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
