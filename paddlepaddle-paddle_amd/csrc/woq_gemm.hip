@@ -1,0 +1,317 @@
+// Weight-only int8 / int4 decode GEMM for gfx950 (W8A16 / W4A16): Y[M, N] = X[M, K] @ dequant(Wq)^T
+// (+ bias), M <= 32 new tokens.  The weight is streamed from HBM once in its quantised form (1 or
+// 0.5 byte per element instead of 2) and dequantised in registers, straight into MFMA B fragments.
+//
+// Reference semantics: paddle/phi/kernels/gpu/weight_only_linear_kernel.cu (CUTLASS fpA_intB GEMV /
+// GEMM), python/paddle/nn/quant/quantized_linear.py:151 weight_only_linear, with this framework's
+// weight layout (nn/quant/quantized_linear.py weight_quantize): int8 [N][K] (k contiguous), int4
+// packed two signed nibbles per byte along k ([N][K/2], low nibble = even k), symmetric scales per
+// output channel ([N]) or per k-group of 64 / 128 ([K/G][N]).
+//
+// CDNA4 design (the k-major path of skinny_gemm.hip, widened per byte):
+//  * A wave owns 128 output columns: lane (g = lane>>4, i = lane&15) handles columns n0 + 16c + i
+//    (c = 0..7).  Per k chunk it loads ONE 16-B piece per column: int8 -> 16 k values (chunk 64),
+//    int4 -> 32 k values (chunk 128), so a chunk is 8 x 16 B per lane like the bf16 kernel's 32-k
+//    step, but covers 2x / 4x the k.
+//  * k order inside a chunk is permuted identically for both operands: lane group g takes k values
+//    [16g, 16g+16) (int8) or [32g, 32g+32) (int4) and splits them into 2 / 4 MFMA steps of 8; the
+//    activation fragment of step s is X[m][k0 + 16g + 8s .. +8] (int8) / X[m][k0 + 32g + 8s ..]
+//    (int4) — 16-B loads of contiguous bf16, no shuffles.  Every k appears exactly once, so the
+//    dot products are exact sums in a different order.
+//  * Dequant: a byte u (int8 xor 0x80, int4 nibble xor 0x8) becomes the fp32 2^23 + u with one
+//    v_perm_b32 (exponent byte 0x4B, two zero bytes, u), minus (2^23 + 128 / 8) gives the signed
+//    integer exactly; bf16 holds every integer |v| <= 256 exactly, so per-channel scales are applied
+//    to the fp32 accumulator at the end (no per-element multiply); group scales multiply in fp32
+//    before the bf16 pack.
+//  * Up to 2 row tiles of 16 (M <= 32) share each dequantised fragment; NST register stages keep the
+//    next chunks' weight loads in flight; the 4 waves of a block split its K range and are summed
+//    through LDS; K splits across blocks go to an fp32 partial buffer summed by the finish kernel
+//    (+ per-channel scale, + bias).
+#include "common.h"
+
+namespace pa {
+namespace woq {
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma(s16x8 a, s16x8 b, f32x4 c) {
+  if constexpr (__is_same(T, f16_t))
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                  0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+}
+
+// byte b (0..3) of d as the fp32 2^23 + byte
+__device__ __forceinline__ float magic(unsigned d, int b) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B000000u, d, 0x07040400u | (unsigned)b));
+}
+
+template <typename T>
+__device__ __forceinline__ unsigned pack2(float a, float b) {
+  Pack<T, 2> p;
+  p.v[0] = (T)a;
+  p.v[1] = (T)b;
+  return __builtin_bit_cast(unsigned, p);
+}
+
+// 8 signed values (exact integers, or * s when SCALE) of one MFMA fragment.
+// int8: bytes q[0..7] of the two dwords lo, hi (k order = byte order).
+template <typename T, bool SCALE>
+__device__ __forceinline__ s16x8 frag_i8(unsigned lo, unsigned hi, float s) {
+  lo ^= 0x80808080u;
+  hi ^= 0x80808080u;
+  constexpr float off = 8388608.0f + 128.0f;
+  float v[8];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    v[b] = magic(lo, b) - off;
+    v[4 + b] = magic(hi, b) - off;
+  }
+  if constexpr (SCALE) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= s;
+  }
+  return __builtin_bit_cast(s16x8, make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
+                                              pack2<T>(v[6], v[7])));
+}
+
+// int4: one dword = 8 nibbles, k = 2b (low nibble of byte b), 2b + 1 (high nibble)
+template <typename T, bool SCALE>
+__device__ __forceinline__ s16x8 frag_i4(unsigned d, float s) {
+  const unsigned ev = (d & 0x0F0F0F0Fu) ^ 0x08080808u;         // k = 0, 2, 4, 6
+  const unsigned od = ((d >> 4) & 0x0F0F0F0Fu) ^ 0x08080808u;  // k = 1, 3, 5, 7
+  constexpr float off = 8388608.0f + 8.0f;
+  float v[8];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    v[2 * b] = magic(ev, b) - off;
+    v[2 * b + 1] = magic(od, b) - off;
+  }
+  if constexpr (SCALE) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= s;
+  }
+  return __builtin_bit_cast(s16x8, make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
+                                              pack2<T>(v[6], v[7])));
+}
+
+// grid (ceil(N / 128), KS), 256 threads.  part: fp32 [KS][M][N].  BITS 8 / 4; G = group size (0 =
+// per channel: the scale is applied by the finish kernel).
+template <typename T, int BITS, int MT, int NST, bool GRP>
+__global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X, long long ldx,
+                                                  const uint8_t* __restrict__ Wq, long long ldw_bytes,
+                                                  const float* __restrict__ gscale, int group,
+                                                  float* __restrict__ part, int M, int N, int K, int kchunk) {
+  constexpr int KC = BITS == 8 ? 64 : 128;  // k per chunk
+  constexpr int NS = KC / 32;                // MFMA steps per chunk
+  __shared__ float red[3][MT * 8 * 4][64];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n0 = blockIdx.x * 128;
+  const int kw = kchunk / 4;  // per wave, a multiple of KC
+  const int kbeg = blockIdx.y * kchunk + w * kw;
+  const int kend = min(K, kbeg + kw);
+  const int g = lane >> 4, i = lane & 15;
+  f32x4 acc[MT][8];
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int cols[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) cols[c] = min(n0 + 16 * c + i, N - 1);  // clamped columns are never stored
+  uint4 rw[NST][8];
+  s16x8 rx[NST][MT][NS];
+  auto load_stage = [&](int st, int k0) {
+    const long long kb = BITS == 8 ? (long long)(k0 + 16 * g) : (long long)(k0 / 2 + 16 * g);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) rw[st][c] = *reinterpret_cast<const uint4*>(Wq + (long long)cols[c] * ldw_bytes + kb);
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int m = 16 * t + i;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const int kk = k0 + (BITS == 8 ? 16 : 32) * g + 8 * s;
+        rx[st][t][s] = m < M ? *reinterpret_cast<const s16x8*>(X + (long long)m * ldx + kk)
+                             : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+  };
+#pragma unroll
+  for (int st = 0; st < NST; ++st)
+    if (kbeg + KC * st < kend) load_stage(st, kbeg + KC * st);
+  for (int base = kbeg; base < kend; base += KC * NST) {
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      const int k0 = base + KC * st;
+      if (k0 >= kend) break;
+      float sc[8];
+      if constexpr (GRP) {
+        // this lane's k range [k0 + 16g, +16) / [k0 + 32g, +32) lies inside one group (group >= 64)
+        const int gi = (k0 + (BITS == 8 ? 16 : 32) * g) / group;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) sc[c] = gscale[(long long)gi * N + cols[c]];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) sc[c] = 1.f;
+      }
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint4 q = rw[st][c];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          s16x8 bf;
+          if constexpr (BITS == 8) {
+            bf = s == 0 ? frag_i8<T, GRP>(q.x, q.y, sc[c]) : frag_i8<T, GRP>(q.z, q.w, sc[c]);
+          } else {
+            const unsigned d = s == 0 ? q.x : s == 1 ? q.y : s == 2 ? q.z : q.w;
+            bf = frag_i4<T, GRP>(d, sc[c]);
+          }
+#pragma unroll
+          for (int t = 0; t < MT; ++t) acc[t][c] = mfma<T>(rx[st][t][s], bf, acc[t][c]);
+        }
+      }
+      if (k0 + KC * NST < kend) load_stage(st, k0 + KC * NST);
+    }
+  }
+  if (w > 0) {
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[w - 1][(t * 8 + c) * 4 + r][lane] = acc[t][c][r];
+  }
+  __syncthreads();
+  if (w != 0) return;
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        acc[t][c][r] += red[0][(t * 8 + c) * 4 + r][lane] + red[1][(t * 8 + c) * 4 + r][lane] +
+                        red[2][(t * 8 + c) * 4 + r][lane];
+  // lane holds C[m = 16t + 4g + r][column n0 + 16c + i]
+  float* out = part + (long long)blockIdx.y * M * N;
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = 16 * t + 4 * g + r;
+      if (m >= M) continue;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int col = n0 + 16 * c + i;
+        if (col < N) out[(long long)m * N + col] = acc[t][c][r];
+      }
+    }
+}
+
+// Y[m, n] = (sum_s part[s][m][n]) * (cscale ? cscale[n] : 1) (+ bias[n]), 8 columns per thread
+template <typename T>
+__global__ __launch_bounds__(256) void woq_finish(const float* __restrict__ part, int KS, int M, int N,
+                                                  const float* __restrict__ cscale, const uint16_t* __restrict__ bias,
+                                                  uint16_t* __restrict__ Y, long long ldy) {
+  const long long e = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (e >= (long long)M * N) return;
+  const int m = (int)(e / N), n = (int)(e - (long long)m * N);
+  float v[8];
+  {
+    const float4 a = *reinterpret_cast<const float4*>(part + e), b = *reinterpret_cast<const float4*>(part + e + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  for (int s = 1; s < KS; ++s) {
+    const float* p = part + (long long)s * M * N + e;
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+  }
+  if (cscale != nullptr) {
+    const float4 a = *reinterpret_cast<const float4*>(cscale + n), b = *reinterpret_cast<const float4*>(cscale + n + 4);
+    v[0] *= a.x; v[1] *= a.y; v[2] *= a.z; v[3] *= a.w; v[4] *= b.x; v[5] *= b.y; v[6] *= b.z; v[7] *= b.w;
+  }
+  if (bias != nullptr) {
+    float bb[8];
+    load_f<T, 8>(reinterpret_cast<const T*>(bias + n), bb);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] += bb[q];
+  }
+  store_f<T, 8>(reinterpret_cast<T*>(Y + (long long)m * ldy + n), v);
+}
+
+// K splits: ~2 blocks per CU over the 128-column tiles; each split a multiple of 4 waves x chunk
+static void plan(int N, int K, int bits, int& KS, int& kchunk) {
+  const int unit = 4 * (bits == 8 ? 64 : 128);
+  const int tiles = (N + 127) / 128;
+  int ks = (512 + tiles - 1) / tiles;
+  const int kmax = (K + unit - 1) / unit;
+  ks = ks < 1 ? 1 : (ks > kmax ? kmax : ks);
+  kchunk = ((K + ks - 1) / ks + unit - 1) / unit * unit;
+  KS = (K + kchunk - 1) / kchunk;
+}
+
+template <typename T, int BITS, bool GRP>
+static void launch(const void* X, long long ldx, const void* Wq, long long ldwb, const float* gscale, int group,
+                   float* ws, int M, int N, int K, int KS, int kchunk, hipStream_t st) {
+  const dim3 grid((N + 127) / 128, KS);
+  const uint16_t* x = (const uint16_t*)X;
+  const uint8_t* w = (const uint8_t*)Wq;
+  // (a 4-row-tile variant for M <= 64 spills at 256 VGPRs: M > 32 takes the dequantise + GEMM path)
+  if (M <= 16)
+    woq_kernel<T, BITS, 1, 3, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk);
+  else
+    woq_kernel<T, BITS, 2, 2, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk);
+}
+
+}  // namespace woq
+}  // namespace pa
+
+// Contract: 1 <= M <= 32; bits 8: K % 64 == 0, bits 4: K % 128 == 0; N % 8 == 0; X rows k-contiguous
+// (ldx % 8 == 0, 16-B aligned); Wq [N][ldw_bytes] with ldw_bytes % 16 == 0; group 0 (per-channel
+// scale [N]) or 64 / 128 (scale [K / group][N]); dt 1 = bf16, 2 = fp16 activations / output.
+PA_API int pa_woq_ok(int M, int N, int K, long long ldx, long long ldw_bytes, int bits, int group, int dt) {
+  if (M < 1 || M > 32 || N < 8 || N % 8 || ldx % 8 || ldw_bytes % 16 || (dt != 1 && dt != 2)) return 0;
+  if (bits == 8 && K % 64) return 0;
+  if (bits == 4 && K % 128) return 0;
+  if (bits != 8 && bits != 4) return 0;
+  if (group != 0 && group != 64 && group != 128) return 0;
+  if (group && K % group) return 0;
+  return 1;
+}
+
+PA_API long long pa_woq_ws_floats(int M, int N, int K, int bits) {
+  int KS, kc;
+  pa::woq::plan(N, K, bits, KS, kc);
+  return (long long)KS * M * N;
+}
+
+PA_API int pa_woq_gemm(const void* X, const void* Wq, const float* scale, const void* bias, void* Y, float* ws, int M,
+                       int N, int K, long long ldx, long long ldw_bytes, long long ldy, int bits, int group, int dt,
+                       hipStream_t st) {
+  using namespace pa::woq;
+  if (!pa_woq_ok(M, N, K, ldx, ldw_bytes, bits, group, dt) || ws == nullptr || scale == nullptr || ldy % 8)
+    return (int)hipErrorInvalidValue;
+  int KS, kchunk;
+  plan(N, K, bits, KS, kchunk);
+  const bool grp = group != 0;
+#define WOQ_DISPATCH(T)                                                                                        \
+  do {                                                                                                         \
+    if (bits == 8 && grp) launch<T, 8, true>(X, ldx, Wq, ldw_bytes, scale, group, ws, M, N, K, KS, kchunk, st);  \
+    else if (bits == 8) launch<T, 8, false>(X, ldx, Wq, ldw_bytes, scale, 0, ws, M, N, K, KS, kchunk, st);       \
+    else if (grp) launch<T, 4, true>(X, ldx, Wq, ldw_bytes, scale, group, ws, M, N, K, KS, kchunk, st);          \
+    else launch<T, 4, false>(X, ldx, Wq, ldw_bytes, scale, 0, ws, M, N, K, KS, kchunk, st);                      \
+    const long long groups = ((long long)M * N + 7) / 8;                                                       \
+    woq_finish<T><<<(unsigned)((groups + 255) / 256), 256, 0, st>>>(ws, KS, M, N, grp ? nullptr : scale,       \
+                                                                     (const uint16_t*)bias, (uint16_t*)Y, ldy); \
+  } while (0)
+  if (dt == 1) WOQ_DISPATCH(pa::bf16_t);
+  else WOQ_DISPATCH(pa::f16_t);
+#undef WOQ_DISPATCH
+  return (int)hipGetLastError();
+}

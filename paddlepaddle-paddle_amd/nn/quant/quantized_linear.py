@@ -5,8 +5,10 @@ Layout (ours, documented; the reference's is a CUTLASS-arch-specific interleave)
 weight quantises to int8 ``[n, k]`` (k contiguous) — int4 packs two signed nibbles per byte along
 k into ``[n, k // 2]`` (low nibble = even k) — with symmetric absmax scales: per output channel
 ``[n]`` (group_size -1) or per k-group ``[k // group_size, n]``.  ``arch`` is accepted for API
-compatibility (the MI355X path does not depend on it).  Matmuls dequantise to the activation dtype
-and run on the framework GEMM (the hand-written MFMA kernel for bf16 on the GPU).
+compatibility (the MI355X path does not depend on it).  On the GPU, decode-shaped calls (<= 32 token
+rows, bf16 / fp16) run the weight-only kernel csrc/woq_gemm.hip (quantised weight streamed once,
+dequantised in registers into MFMA fragments); larger token counts dequantise once and run the
+hand-written GEMM.
 """
 import torch
 
@@ -93,6 +95,15 @@ def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="in
         raise ValueError("weight_only_linear needs weight_scale")
     t = _u(x)
     algo = 'weight_only_int4' if weight_dtype == 'int4' else 'weight_only_int8'
+    from ... import ops
+    x2 = t.reshape(-1, t.shape[-1])
+    wq = _u(weight)
+    bits, grp = (4 if weight_dtype == 'int4' else 8), (0 if group_size == -1 else group_size)
+    if ops.use_hip(x2) and ops.woq.woq_ok(x2.contiguous(), wq, bits, grp):
+        # decode-shaped: stream the quantised weight once, dequantise in registers (csrc/woq_gemm.hip)
+        y = ops.woq.woq_linear(x2.contiguous(), wq, _u(weight_scale), bits, grp,
+                               None if bias is None else _u(bias))
+        return _w(y.reshape(*t.shape[:-1], y.shape[-1]))
     w = _dequant(weight, weight_scale, algo, group_size).to(t.dtype)
     from ...tensor.linalg import matmul
     y = matmul(_w(t), _w(w.contiguous()))

@@ -38,3 +38,4 @@ from . import norm, softmax, act, xent, embedding, rope, optim, flash_attn, gemm
 from . import decode  # noqa: E402,F401
 from . import fp8  # noqa: E402,F401
 from . import matmul  # noqa: E402,F401
+from . import woq  # noqa: E402,F401

@@ -71,6 +71,9 @@ _SIGS = {
     'pa_gemm8_fp8_ok': [I, I, I, LL, LL, LL],
     'pa_gemm8_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
     'pa_gemmx_ok': [I, I, I, LL, LL, LL, I, I, I],
+    'pa_woq_ok': [I, I, I, LL, LL, I, I, I],
+    'pa_woq_ws_floats': [I, I, I, I],
+    'pa_woq_gemm': [P, P, P, P, P, P, I, I, I, LL, LL, LL, I, I, I, P],
     'pa_gemmx': [P, P, P, P, I, I, I, LL, LL, LL, I, I, I, LL, LL, LL, I, F, F, P],
     'pa_conv2d_fwd_ok': [I, I, I, I],
     'pa_conv2d_fwd': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
@@ -119,7 +122,7 @@ _SIGS = {
                      P],
 }
 
-_LL_RET = {'pa_bn_ws_floats', 'pa_skinny_ws_floats'}
+_LL_RET = {'pa_bn_ws_floats', 'pa_skinny_ws_floats', 'pa_woq_ws_floats'}
 _VOID_RET = {'pa_adamw_tune', 'pa_act_fwd_tune', 'pa_act_cs_tune'}
 
 

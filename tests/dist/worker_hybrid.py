@@ -135,7 +135,7 @@ class Block(nn.Layer):
         return paddle.tanh(self.fc(x))
 
 
-def pp_test(virtual=1, acc=4):
+def pp_test(virtual=1, acc=4, tag=None):
     world = int(os.environ['WORLD_SIZE'])
     s = fleet.DistributedStrategy()
     s.hybrid_configs = {'dp_degree': 1, 'mp_degree': 1, 'pp_degree': world}
@@ -178,7 +178,7 @@ def pp_test(virtual=1, acc=4):
     assert abs(float(loss) - tot) < 1e-5, (float(loss), tot)
     for blk, gi in zip(pl.run_function, owned):
         np.testing.assert_allclose(blk.fc.weight.numpy(), full[gi].fc.weight.numpy(), atol=1e-5)
-    tag = 'pp' if virtual == 1 else ('vpp' if acc < 2 * world else 'vpp8')
+    tag = tag or ('pp' if virtual == 1 else 'vpp')
     if virtual > 1:
         # the reference's choice (fleet/model.py:168): FthenB for pp <= acc < 2 pp, else 1F1B
         want = 'interleaved_fthenb' if acc < 2 * world else 'interleaved_1f1b'
@@ -187,5 +187,5 @@ def pp_test(virtual=1, acc=4):
 
 
 if __name__ == '__main__':
-    {'tp': tp_test, 'sp': sp_test, 'pp': pp_test, 'vpp': lambda: pp_test(2), 'vpp8': lambda: pp_test(2, 8),
+    {'tp': tp_test, 'sp': sp_test, 'pp': pp_test, 'vpp': lambda: pp_test(2), 'vpp8': lambda: pp_test(2, 8, 'vpp8'),
      'tpdp': tpdp_test}[sys.argv[1]]()

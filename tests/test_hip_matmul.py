@@ -207,3 +207,33 @@ def test_fp8_8phase_gemm(M, N, K, fmts):
     # accumulate: out2 = 0.5 * a @ w^T * scales + 1.0 * out
     out2 = gemm.hip_fp8_mm(a, w, scale_a=sa, scale_b=sb, out=out.clone(), alpha=0.5, beta=1.0)
     _close(out2, ref + (a.float() @ w.float().t()) * 0.0625, 1.5e-2, 'fp8 beta=1')
+
+
+@pytest.mark.parametrize('bits,group', [(8, -1), (8, 64), (8, 128), (4, -1), (4, 64), (4, 128)])
+@pytest.mark.parametrize('M', [1, 7, 16, 32])
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16])
+def test_weight_only_linear_kernel(bits, group, M, dt):
+    """weight_only_linear on the W8A16 / W4A16 decode kernel (csrc/woq_gemm.hip) vs the fp32 product
+    with the dequantised weight (Llama-2-13B-like widths scaled down)."""
+    from paddle.nn.quant import weight_quantize, weight_only_linear
+    g = torch.Generator(device=DEV).manual_seed(11)
+    K, N_ = 2560, 1152
+    w = (torch.randn(K, N_, device=DEV, generator=g) * 0.05)
+    x = torch.randn(M, K, device=DEV, generator=g).to(dt)
+    b = torch.randn(N_, device=DEV, generator=g).to(dt)
+    algo = 'weight_only_int4' if bits == 4 else 'weight_only_int8'
+    q, s = weight_quantize(paddle.to_tensor(w), algo=algo, group_size=group)
+    from paddle.nn.quant.quantized_linear import _dequant
+    wd = _dequant(q, s, algo, group)  # [K, N] fp32
+    ref = x.float() @ wd + b.float()
+    from paddle.ops import woq
+    calls = []
+    orig = woq.woq_linear
+    woq.woq_linear = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]
+    try:
+        y = weight_only_linear(paddle.to_tensor(x), q, paddle.to_tensor(b), s,
+                               weight_dtype='int4' if bits == 4 else 'int8', group_size=group)._t
+    finally:
+        woq.woq_linear = orig
+    assert calls, 'weight-only kernel did not run'
+    _close(y, ref, 2e-2, f'woq bits={bits} group={group} M={M}')

@@ -1,0 +1,46 @@
+"""Weight-only int8 / int4 decode GEMM (csrc/woq_gemm.hip) vs the bf16 skinny decode GEMM and the
+library on Llama-2-13B layer shapes, M <= 16, random operands; also reports the quantised-weight
+streaming bandwidth."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+
+def bench(fn, n=50):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 1e3 / n
+
+
+def main():
+    import paddle  # noqa: F401
+    from paddle.ops import woq, gemm
+    from paddle.nn.quant import weight_quantize
+    dev = 'cuda'
+    for name, K, N in [('qkv', 5120, 15360), ('out', 5120, 5120), ('ffn1', 5120, 27648), ('ffn2', 13824, 5120)]:
+        w = torch.randn(K, N, device=dev) * 0.02
+        wb = w.bfloat16()
+        q8, s8 = (t._t for t in weight_quantize(paddle.to_tensor(w), 'weight_only_int8'))
+        q4, s4 = (t._t for t in weight_quantize(paddle.to_tensor(w), 'weight_only_int4'))
+        for M in (1, 8, 16):
+            x = torch.randn(M, K, device=dev).bfloat16()
+            tb = bench(lambda: gemm.skinny_mm(x, wb))
+            tl = bench(lambda: torch.mm(x, wb))
+            t8 = bench(lambda: woq.woq_linear(x, q8, s8, 8, 0))
+            t4 = bench(lambda: woq.woq_linear(x, q4, s4, 4, 0))
+            print(f"{name:5s} K={K:5d} N={N:5d} M={M:2d}: bf16 skinny {tb*1e6:7.1f} us ({K*N*2/tb/1e12:4.2f} TB/s) | "
+                  f"library {tl*1e6:7.1f} | int8 {t8*1e6:7.1f} us ({K*N/t8/1e12:4.2f} TB/s, {tb/t8:4.2f}x) | "
+                  f"int4 {t4*1e6:7.1f} us ({K*N/2/t4/1e12:4.2f} TB/s, {tb/t4:4.2f}x)", flush=True)
+
+
+if __name__ == '__main__':
+    main()
