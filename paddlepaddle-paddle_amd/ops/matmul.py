@@ -91,12 +91,12 @@ def _gemmx(a3, b3, batch, bias=None, alpha=1.0, out=None, beta=0.0):
     """[batch] x (a3 [.., M, K] @ b3 [.., K, N]) in one pa_gemmx launch.  a3 / b3 carry one batch
     dim (size 1 or batch; stride 0 = broadcast).  Returns out [batch, M, N] or None."""
     ta, lda = _layout(a3)
-    tb, ldb = _layout(b3)
+    tb, ldb = _layout(b3)  # tb = 1: b3 is a transposed view of [N][K] (k contiguous), the kernel's transB
     if ta is None or tb is None:
         return None
     M, K = a3.shape[-2], a3.shape[-1]
     N_ = b3.shape[-1]
-    if N._load() is None or not N.lib.pa_gemmx_ok(M, N_, K, lda, ldb, N_, ta, 1 - tb, _DT[a3.dtype]):
+    if N._load() is None or not N.lib.pa_gemmx_ok(M, N_, K, lda, ldb, N_, ta, tb, _DT[a3.dtype]):
         return None
     sa = a3.stride(0) if a3.shape[0] > 1 else 0
     sb = b3.stride(0) if b3.shape[0] > 1 else 0
@@ -107,7 +107,7 @@ def _gemmx(a3, b3, batch, bias=None, alpha=1.0, out=None, beta=0.0):
     if out is None:
         out = torch.empty(batch, M, N_, dtype=a3.dtype, device=a3.device)
         beta = 0.0
-    N.check(N.lib.pa_gemmx(N.ptr(a3), N.ptr(b3), N.ptr(out), N.ptr(bias), M, N_, K, lda, ldb, N_, ta, 1 - tb, batch,
+    N.check(N.lib.pa_gemmx(N.ptr(a3), N.ptr(b3), N.ptr(out), N.ptr(bias), M, N_, K, lda, ldb, N_, ta, tb, batch,
                            sa, sb, M * N_, _DT[a3.dtype], float(alpha), float(beta), N.stream()), 'gemmx')
     return out
 

@@ -25,6 +25,8 @@ def main():
     import paddle  # noqa: F401
     from paddle.ops import woq, gemm
     from paddle.nn.quant import weight_quantize
+    from paddle.ops import _native
+    assert _native._load() is not None, _native.load_error
     dev = 'cuda'
     for name, K, N in [('qkv', 5120, 15360), ('out', 5120, 5120), ('ffn1', 5120, 27648), ('ffn2', 13824, 5120)]:
         w = torch.randn(K, N, device=dev) * 0.02
