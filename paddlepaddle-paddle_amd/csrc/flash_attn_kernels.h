@@ -1,0 +1,1073 @@
+// Flash attention forward + backward on MFMA (gfx950, bf16 / fp16, head_dim 64 or 128).
+//
+// Reference semantics: paddle/phi/kernels/gpu/flash_attn_kernel.cu, flash_attn_grad_kernel.cu
+// (python/paddle/nn/functional/flash_attention.py): layout [batch, seq, heads, head_dim] (BSHD),
+// causal mask aligned bottom-right (key <= query + Sk - Sq), GQA (Hq % Hk == 0), softmax_lse
+// saved as fp32 [B, Hq, Sq] for the backward.
+//
+// CDNA4 design (not a translation of the CUDA kernel):
+//  * 64-wide waves, v_mfma_f32_16x16x32_{bf16,f16}.  Forward uses the *swapped* product
+//    S^T = K·Q^T so a lane owns one query row (query = lane & 15) in every accumulator:
+//    row max / row sum need only 2 cross-lane shuffles and the rescale of O is lane-local.
+//    P stays in registers and feeds P·V directly as the MFMA B operand (K-permutation trick:
+//    element j of lane group g is key 4g+j / 16+4g+j-4, matched by the V operand).
+//  * V is consumed column-wise with ds_read_b64_tr_b16 (hardware transposed LDS read), so V
+//    is staged row-major exactly as it sits in HBM.
+//  * K/V tiles XOR-swizzled in LDS (16-byte chunk ^ f(row)) → conflict-free ds_read_b128 and
+//    tr reads; register-staged prefetch of tile t+1 is issued before computing tile t.
+//  * Backward = dK/dV kernel (keys stationary per wave, non-swapped products) + dQ kernel
+//    (queries stationary, swapped products).  No float atomics: dQ is deterministic.
+//  * Strided q/k/v/o (element strides for batch/seq/head) so q, k, v can be slices of a fused
+//    QKV projection with no copies.
+#pragma once
+#include "common.h"
+#include <stdlib.h>
+#include <type_traits>
+
+// the block-order switch is a per-module __constant__: flash_attn.hip defines it with external linkage
+// (its kernels' codegen depends on that), the wide-head-dim module gets a static copy
+#ifndef PA_FA_PAIR_GROUP_DECL
+#define PA_FA_PAIR_GROUP_DECL __constant__
+#endif
+
+namespace pa {
+namespace fa {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+template <typename T> struct Mfma;
+template <> struct Mfma<bf16_t> {
+  static __device__ __forceinline__ f32x4 run(s16x8 a, s16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mfma<f16_t> {
+  static __device__ __forceinline__ f32x4 run(s16x8 a, s16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  }
+};
+
+template <typename T>
+__device__ __forceinline__ short f2s(float v) {
+  return __builtin_bit_cast(short, from_f<T>(v));
+}
+
+// LDS row pitch (elements) of a [rows][D] tile: D itself, except D = 96, whose 12-chunk rows are
+// laid out in 16-chunk (D = 128) rows so the XOR swizzles below stay inside the row (the four
+// spare chunks are never written or read; no zero padding of the operands themselves).
+template <int D> constexpr int fa_pitch() { return D == 96 ? 128 : D; }
+// 16-byte-chunk swizzles (see header comment). pitch >= 128 → >= 256-B rows (D 96/128/256: banks
+// repeat every 256 B), pitch 64 → 128-B rows.
+template <int D> __device__ __forceinline__ int swz_b128(int row) { return fa_pitch<D>() >= 128 ? (row & 15) : ((row >> 1) & 7); }
+template <int D> __device__ __forceinline__ int swz_tr(int row) { return fa_pitch<D>() >= 128 ? ((row & 7) << 1) : (((row >> 1) & 3) << 1); }
+
+// LDS byte offset of 16-byte chunk `ch` of row `row` in a [rows][D] 16-bit tile.
+template <int D, bool TR>
+__device__ __forceinline__ int lds_off(int row, int ch) {
+  return row * (fa_pitch<D>() * 2) + ((ch ^ (TR ? swz_tr<D>(row) : swz_b128<D>(row))) << 4);
+}
+
+// Stage helpers: a [64][D] tile of 16-bit elements, 256 threads, NLD 16-byte chunks per thread.
+// The per-thread address is computed once (init); a tile load adds one wave-uniform offset and,
+// for full tiles, skips the per-row bounds checks entirely.
+template <int D, int NTHR = 256, bool FLAT = (NTHR % (D / 8)) != 0>
+struct Tile {
+  static constexpr int CH = D / 8;               // 16-byte chunks per row
+  static constexpr int NLD = 64 * CH / NTHR;     // chunks per thread
+  static constexpr int RPL = NTHR / CH;          // rows covered by one pass of the block
+  static_assert(NLD * NTHR == 64 * CH, "tile chunks must split evenly over the block");
+  uint4 r[NLD];
+  const uint16_t* p;
+  long long rs;
+  int row_in;
+  __device__ __forceinline__ void init(const uint16_t* base, long long row_stride) {
+    row_in = threadIdx.x / CH;
+    rs = row_stride;
+    p = base + (long long)row_in * row_stride + (threadIdx.x % CH) * 8;
+  }
+  __device__ __forceinline__ void load(int row0, int nrows) {
+    if constexpr (FLAT) {  // CH does not divide the block (D = 96): chunk c = tid + NTHR * i
+      const uint16_t* q = p - (long long)row_in * rs - (threadIdx.x % CH) * 8 + (long long)row0 * rs;
+#pragma unroll
+      for (int i = 0; i < NLD; ++i) {
+        const int c = threadIdx.x + NTHR * i, row = c / CH;
+        r[i] = (row0 + row < nrows) ? *reinterpret_cast<const uint4*>(q + (long long)row * rs + (c % CH) * 8)
+                                    : make_uint4(0, 0, 0, 0);
+      }
+      return;
+    }
+    const uint16_t* q = p + (long long)row0 * rs;
+    if (row0 + 64 <= nrows) {
+#pragma unroll
+      for (int i = 0; i < NLD; ++i) r[i] = *reinterpret_cast<const uint4*>(q + (long long)(RPL * i) * rs);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NLD; ++i)
+        r[i] = (row0 + row_in + RPL * i < nrows) ? *reinterpret_cast<const uint4*>(q + (long long)(RPL * i) * rs)
+                                                  : make_uint4(0, 0, 0, 0);
+    }
+  }
+  template <bool TR>
+  __device__ __forceinline__ void store(char* lds) const {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + NTHR * i;
+      const int row = c / CH, ch = c % CH;
+      *reinterpret_cast<uint4*>(lds + lds_off<D, TR>(row, ch)) = r[i];
+    }
+  }
+};
+
+// raw v_exp_f32 (2^x): exp2(-inf) = 0; no denormal range fix-up (inputs are <= ~8 here)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// lazy rescale threshold (log2 units): the running max used as the exponent base is only moved
+// when a row's new max exceeds it by more than this, so most tiles skip the O/l rescale.
+constexpr float kRescaleTau = 8.0f;
+
+// A/B operand read: row `row`, d-range [32ks + 8g, +8) → 8 x 16-bit
+template <int D, bool TR>
+__device__ __forceinline__ s16x8 ld_row8(const char* lds, int row, int ks, int g) {
+  return *reinterpret_cast<const s16x8*>(lds + lds_off<D, TR>(row, 4 * ks + g));
+}
+
+// Transposed operand: lane (16g + i) gets column (16db + i) of rows {r0+4g+q} (elements 0..3) and
+// {r0+16+4g+q} (elements 4..7).  Lane 16g+4q+p supplies the address of row r0+4g+q, col 16db+4p.
+template <int D, bool TR>
+__device__ __forceinline__ s16x8 ld_tr8(const char* lds, int r0, int db, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int ch = 2 * db + (p >> 1);
+  const int byte_in = (p & 1) * 8;
+  const int rowa = r0 + 4 * g + q, rowb = rowa + 16;
+  typedef __attribute__((address_space(3))) s16x4 lds_v4;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(lds + lds_off<D, TR>(rowa, ch) + byte_in));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(lds + lds_off<D, TR>(rowb, ch) + byte_in));
+  s16x8 r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
+struct Strides {
+  long long b, s, h;
+};
+
+// Optional features (EXT kernels; the plain instantiations compile none of this):
+//  * varlen: cu_q / cu_k [B+1] token offsets of packed [total, H, D] tensors (batch strides
+//    ignored); per-sequence lengths, bottom-right causal alignment per sequence; LSE / delta
+//    laid out [Hq, total_q];
+//  * additive mask (fp32, or the activation dtype) at mask[b*mb + h*mh + q*mq + k] (broadcast
+//    dims have stride 0); -inf entries mask;
+//  * dropout on the normalised probabilities: keep(b, h, q, k) = hash(seed, offset, element)
+//    regenerated bit-identically by the backward kernels; the softmax statistics (LSE) are those
+//    of the undropped probabilities;
+//  * flashmask start-row indices (int32, rows[b*rb + h*rh + key]): key k is masked for queries
+//    q >= rows[k] (python/paddle/nn/functional/flash_attention.py:844
+//    flash_attention_with_sparse_mask), O(S) memory instead of a dense [S, S] mask.
+struct Extra {
+  const int* cu_q;
+  const int* cu_k;
+  int total_q;
+  const void* mask;
+  long long mb, mh, mq;
+  int mask_f32;
+  float p_drop;
+  uint32_t seed, offset;
+  uint32_t drop_thresh;  // drop when the element's random byte < drop_thresh (= round(p_drop * 256))
+  float keep_scale;      // 256 / (256 - drop_thresh): unbiased for the quantised keep probability
+  const int* rows;       // flashmask: key k masked for queries q >= rows[b*rb + h*rh + k]
+  long long rb, rh;
+};
+
+// flashmask column test (EXT & 8): true when (q, key) is masked by the start-row indices
+__device__ __forceinline__ int row_start(const Extra& ex, int b, int h, int key) {
+  return ex.rows[(long long)b * ex.rb + (long long)h * ex.rh + key];
+}
+
+template <typename T>
+__device__ __forceinline__ void mask4(const Extra& ex, int b, int h, int q, int k, float (&o)[4]) {
+  const long long i = (long long)b * ex.mb + (long long)h * ex.mh + (long long)q * ex.mq + k;
+  if (ex.mask_f32) {
+    const float* m = reinterpret_cast<const float*>(ex.mask) + i;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = m[r];
+  } else {
+    const T* m = reinterpret_cast<const T*>(ex.mask) + i;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = to_f(m[r]);
+  }
+}
+
+// mask values of keys k..k+3 (vector load when all four are in range, else per element)
+template <typename T>
+__device__ __forceinline__ void mask_row4(const Extra& ex, int b, int h, int q, int k, int Sk, float (&o)[4]) {
+  if (k + 3 < Sk) {
+    mask4<T>(ex, b, h, q, k, o);
+    return;
+  }
+  const long long i = (long long)b * ex.mb + (long long)h * ex.mh + (long long)q * ex.mq + k;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    o[r] = (k + r < Sk) ? (ex.mask_f32 ? reinterpret_cast<const float*>(ex.mask)[i + r]
+                                       : to_f(reinterpret_cast<const T*>(ex.mask)[i + r]))
+                        : 0.f;
+}
+
+// Dropout keep mask: one 32-bit counter hash per (bh, q, key quad k>>2) gives the random bytes of
+// four consecutive keys (8-bit keep test, as the reference's flash-attn kernels quantise p to a
+// uint8 threshold).  The forward and dQ kernels own 4 consecutive keys of one query per lane, so
+// they pay ONE hash per 4 elements (drop_bits + drop_sub); dK/dV (4 consecutive queries of one
+// key per lane) hashes one query per lane and shares the words across the key quad with DPP —
+// same bits, same mask (drop_z is the per-element reference form).
+// The hash input is linear in (query, key quad), so its per-block and per-lane parts hoist out of
+// the tile loops, and the finaliser multiplies with full-rate 24-bit multiplies (v_mul_u32_u24)
+// instead of quarter-rate v_mul_lo_u32: the dropout tiles were VALU-issue bound on the hash.
+// Statistics of the keep bytes (host simulation of this exact function, 1M elements per
+// seed): keep rate within 1e-3 of 230/256 at p = 0.1, adjacent key / row / key+4 correlations
+// |r| < 3e-3, byte histogram chi^2 ~ 255 (255 dof); GPU test test_flash_dropout_statistics.
+__device__ __forceinline__ uint32_t fin24(uint32_t x) {
+  x ^= x >> 16;
+  x = __umul24(x, 0x7FEB35u);
+  x ^= x >> 15;
+  x = __umul24(x, 0x846CA7u);
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t drop_bits(const Extra& ex, int bh, int q, int k) {
+  return fin24((ex.seed ^ (uint32_t)bh * 0x9E3779B9u) + (ex.offset + (uint32_t)q) * 0x85EBCA77u +
+               ((uint32_t)k >> 2) * 0xC2B2AE3Du);
+}
+__device__ __forceinline__ float drop_sub(const Extra& ex, uint32_t bits, int sub) {
+  return ((bits >> (8 * sub)) & 0xFFu) < ex.drop_thresh ? 0.f : ex.keep_scale;
+}
+__device__ __forceinline__ float drop_z(const Extra& ex, int bh, int q, int k) {
+  return drop_sub(ex, drop_bits(ex, bh, q, k), k & 3);
+}
+
+// per-sequence geometry: (q offset, Sq, k offset, Sk, LSE row base) of batch entry b
+struct Seq {
+  long long qo, ko, lrow;
+  int sq, sk;
+};
+template <bool EXT>
+__device__ __forceinline__ Seq seq_of(const Extra& ex, int b, int h, int Hq, int Sq, int Sk) {
+  Seq r;
+  if (EXT && ex.cu_q) {
+    r.qo = ex.cu_q[b];
+    r.ko = ex.cu_k[b];
+    r.sq = ex.cu_q[b + 1] - ex.cu_q[b];
+    r.sk = ex.cu_k[b + 1] - ex.cu_k[b];
+    r.lrow = (long long)h * ex.total_q + r.qo;
+  } else {
+    r.qo = r.ko = 0;
+    r.sq = Sq;
+    r.sk = Sk;
+    r.lrow = ((long long)b * Hq + h) * Sq;
+  }
+  return r;
+}
+
+// Block order (speed only; any bijection is correct).  The grid is (Hq, B, NZ): NZ query (or key)
+// blocks per (head, batch) pair, each re-reading the pair's K/V (or Q/dO) rows.  Blocks b and
+// b + 8 of the dispatch order share an XCD and its 4 MB L2.
+//  * G = 0: pair-major rows of the plain grid: all pairs' heaviest blocks first (longest-first over
+//    the whole launch); a pair's blocks run on one XCD but far apart in time, so its rows come from
+//    the Infinity Cache once per block.
+//  * G > 0: each XCD walks its own contiguous range of groups of G pairs, heaviest block first
+//    inside each group: a group's rows (G x 512 KB at S 1024, D 128) stay in that XCD's L2 while
+//    all its blocks run, and the light blocks of one group overlap the heavy ones of the next.
+PA_FA_PAIR_GROUP_DECL int g_pair_group = 0;
+
+__device__ __forceinline__ void pair_order(int Hq, int B, int NZ, int& h, int& b, int& zi) {
+  const int id = blockIdx.x + Hq * (blockIdx.y + B * blockIdx.z);
+  const int G = g_pair_group;
+  int pair;
+  if (G <= 0) {
+    pair = id % (Hq * B);
+    zi = id / (Hq * B);
+  } else {
+    const int nwg = Hq * B * NZ, P = Hq * B;
+    const int q = nwg >> 3, r = nwg & 7, x = id & 7;
+    const int w = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (id >> 3);
+    const int grp = w / (G * NZ);
+    const int gc = min(G, P - grp * G);  // pairs in this group (the last one may be short)
+    const int rr = w - grp * G * NZ;
+    zi = rr / gc;
+    pair = grp * G + rr % gc;
+  }
+  h = pair % Hq;
+  b = pair / Hq;
+}
+
+// ============================================================================ forward
+// grid: (Hq, B, ceil(Sq / (64 QT))), block 256 (4 waves x QT tiles of 16 query rows; QT = 2, 1 at D = 256)
+// PIPE: K/V tiles double-buffered in LDS, one barrier per key block.
+template <typename T, int D, bool CAUSAL, int EXT = 0, bool PIPE = false>
+__global__ __launch_bounds__(256, D > 128 ? 1 : 2) void fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+                                                     const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
+                                                     float* __restrict__ LSE, int Sq_, int Sk_, int Hq, int Hk,
+                                                     Strides qs, Strides ks_, Strides vs, Strides os, float scale_log2,
+                                                     Extra ex = Extra{}) {
+  if constexpr ((EXT & 4) != 0) ex.seed = rng_mix(ex.seed);  // graph-captured steps: per-replay stream
+  constexpr int KS = D / 32;   // k-steps over head_dim
+  constexpr int DB = D / 16;   // 16-wide d blocks
+  constexpr int STAGE = 2 * 64 * fa_pitch<D>() * 2;  // K and V of one key block
+  // query tiles of 16 rows per wave: 2 (32 rows, 128-row blocks); D = 256 keeps 1 (64-row blocks)
+  // so its O accumulators and Q fragments fit the register file
+  constexpr int QT = D > 128 ? 1 : 2;
+  __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches and addresses
+  const int g = lane >> 4;
+  const int nqb = (Sq_ + 64 * QT - 1) / (64 * QT);
+  // grid (Hq, B, q-blocks): the q-block index is the slowest-dispatched dimension, so every
+  // head's heaviest (late, causal) block is issued before any lighter one (longest-first order
+  // over the whole grid: the tail of the launch is the short blocks)
+  int h, b, zi;
+  pair_order(Hq, (int)gridDim.y, nqb, h, b, zi);
+  const int qb = nqb - 1 - zi;
+  const int hk = h / (Hq / Hk);
+  const Seq sq_ = seq_of<EXT != 0>(ex, b, h, Hq, Sq_, Sk_);
+  const int Sq = sq_.sq, Sk = sq_.sk;
+  const int q0 = qb * 64 * QT;
+  if (EXT && q0 >= Sq) return;  // varlen: this sequence is shorter
+  const int qw0 = q0 + wave * 16 * QT;
+  const int off = Sk - Sq;  // bottom-right causal alignment
+  // EXT: scores are brought to natural units (+ mask) right after QK^T, then exponentiated in
+  // base 2 with log2(e)
+  const float sl2 = (EXT & 2) ? kLog2e : scale_log2;
+  const float scale_n = scale_log2 / kLog2e;
+
+  const uint16_t* qbase = Q + (EXT && ex.cu_q ? 0 : b * qs.b) + sq_.qo * qs.s + h * qs.h;
+  const uint16_t* kbase = K + (EXT && ex.cu_q ? 0 : b * ks_.b) + sq_.ko * ks_.s + hk * ks_.h;
+  const uint16_t* vbase = V + (EXT && ex.cu_q ? 0 : b * vs.b) + sq_.ko * vs.s + hk * vs.h;
+
+  // Q fragments (B operand of S^T = K Q^T): lane holds Q[qw0 + 16t + (lane&15)][32ks + 8g .. +8]
+  s16x8 qf[QT][KS];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int q = qw0 + 16 * t + (lane & 15);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      if (q < Sq)
+        qf[t][k] = *reinterpret_cast<const s16x8*>(qbase + (long long)q * qs.s + 32 * k + 8 * g);
+      else
+        qf[t][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+
+  f32x4 acc_o[QT][DB];
+#pragma unroll
+  for (int t = 0; t < QT; ++t)
+#pragma unroll
+    for (int d = 0; d < DB; ++d) acc_o[t][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run[2] = {-INFINITY, -INFINITY};  // [QT] used (sized 2 for both: same code at QT = 2)
+  float l_run[2] = {0.f, 0.f};
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + 64 * QT + off);
+  const int nkb = kend > 0 ? (kend + 63) / 64 : 0;
+
+  Tile<D> kt, vt;
+  kt.init(kbase, ks_.s);
+  vt.init(vbase, vs.s);
+  if (nkb > 0) {
+    kt.load(0, Sk);
+    vt.load(0, Sk);
+  }
+  if (PIPE && nkb > 0) {
+    kt.template store<false>(smem);
+    vt.template store<true>(smem + 64 * fa_pitch<D>() * 2);
+    if (nkb > 1) {
+      kt.load(64, Sk);
+      vt.load(64, Sk);
+    }
+    __syncthreads();
+  }
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * 64;
+    char* st = smem + (PIPE ? (kb & 1) * STAGE : 0);
+    if (!PIPE) {
+      __syncthreads();
+      kt.template store<false>(st);
+      vt.template store<true>(st + 64 * fa_pitch<D>() * 2);
+      __syncthreads();
+      if (kb + 1 < nkb) {
+        kt.load(k0 + 64, Sk);
+        vt.load(k0 + 64, Sk);
+      }
+    }
+    const char* k_lds = st;
+    const char* v_lds = st + 64 * fa_pitch<D>() * 2;
+    // wave-uniform skip of key blocks fully above this wave's diagonal
+    if (!(CAUSAL && k0 > qw0 + 16 * QT - 1 + off)) {
+
+    // S^T = K Q^T : acc_s[t][kbk] holds S^T[key 16kbk + 4g + r][query 16t + (lane&15)]
+    f32x4 acc_s[QT][4];
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc_s[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const s16x8 kf = ld_row8<D, false>(k_lds, 16 * j + (lane & 15), k, g);
+        acc_s[0][j] = Mfma<T>::run(kf, qf[0][k], acc_s[0][j]);
+        if constexpr (QT == 2) acc_s[1][j] = Mfma<T>::run(kf, qf[1][k], acc_s[1][j]);
+      }
+    }
+    if constexpr ((EXT & 2) != 0) {
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        const int q = qw0 + 16 * t + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float mv[4] = {0.f, 0.f, 0.f, 0.f};
+          if (q < Sq) mask_row4<T>(ex, b, h, q, k0 + 16 * j + 4 * g, Sk, mv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc_s[t][j][r] = acc_s[t][j][r] * scale_n + mv[r];
+        }
+      }
+    }
+    if constexpr ((EXT & 8) != 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 16 * j + 4 * g + r;
+          const int rs = key < Sk ? row_start(ex, b, h, key) : 0;
+#pragma unroll
+          for (int t = 0; t < QT; ++t)
+            if (qw0 + 16 * t + (lane & 15) >= rs) acc_s[t][j][r] = -INFINITY;
+        }
+    }
+    // online softmax in the log2 domain.  Masking only on tiles that touch the diagonal or the
+    // ragged end (wave-uniform test); the scale is folded into the exponent's FMA; the running
+    // max moves lazily (kRescaleTau) so the O/l rescale is skipped on most tiles.
+    const bool need_mask = (k0 + 64 > Sk) || (CAUSAL && k0 + 63 > qw0 + off);
+    if (need_mask) {
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        const int q = qw0 + 16 * t + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = k0 + 16 * j + 4 * g + r;
+            if ((key >= Sk) || (CAUSAL && key > q + off)) acc_s[t][j][r] = -INFINITY;
+          }
+      }
+    }
+    float mnew[QT];
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      float mx = acc_s[t][0][0];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc_s[t][j][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mnew[t] = mx * sl2;
+    }
+    bool bump;
+    if constexpr (QT == 2)
+      bump = (mnew[0] > m_run[0] + kRescaleTau) || (mnew[1] > m_run[1] + kRescaleTau);
+    else
+      bump = mnew[0] > m_run[0] + kRescaleTau;
+    if (__ballot(bump) != 0ull) {
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        const float m_upd = fmaxf(m_run[t], mnew[t]);
+        const float alpha = (m_upd == -INFINITY) ? 1.f : fast_exp2(m_run[t] - m_upd);
+        m_run[t] = m_upd;
+        l_run[t] *= alpha;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) acc_o[t][d] *= alpha;
+      }
+    }
+    s16x8 pf[QT][2];
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      const float neg_m = (m_run[t] == -INFINITY) ? 0.f : -m_run[t];
+      float ls = 0.f;
+      float p[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          p[j][r] = fast_exp2(__builtin_fmaf(acc_s[t][j][r], sl2, neg_m));
+          ls += p[j][r];
+        }
+      l_run[t] += ls;
+      if constexpr ((EXT & 4) != 0) {  // dropout after the (undropped) row sum
+        const int q = qw0 + 16 * t + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t bits = drop_bits(ex, b * Hq + h, q, k0 + 16 * j + 4 * g);  // keys 4-aligned
+#pragma unroll
+          for (int r = 0; r < 4; ++r) p[j][r] *= drop_sub(ex, bits, r);
+        }
+      }
+      // P^T as B operand: k-step s covers keys 32s..32s+31; element j<4 → (16*(2s)+4g+j), j>=4 → (16*(2s+1)+4g+j-4)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pf[t][s][r] = f2s<T>(p[2 * s][r]);
+          pf[t][s][4 + r] = f2s<T>(p[2 * s + 1][r]);
+        }
+      }
+    }
+    // O^T += V^T P^T
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const s16x8 vf = ld_tr8<D, true>(v_lds, 32 * s, d, lane);
+        acc_o[0][d] = Mfma<T>::run(vf, pf[0][s], acc_o[0][d]);
+        if constexpr (QT == 2) acc_o[1][d] = Mfma<T>::run(vf, pf[1][s], acc_o[1][d]);
+      }
+    }
+    }  // not above the diagonal
+    if (PIPE) {
+      if (kb + 1 < nkb) {
+        char* nx = smem + ((kb + 1) & 1) * STAGE;  // last read in block kb - 1
+        kt.template store<false>(nx);
+        vt.template store<true>(nx + 64 * fa_pitch<D>() * 2);
+        if (kb + 2 < nkb) {
+          kt.load(k0 + 128, Sk);
+          vt.load(k0 + 128, Sk);
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // epilogue: O = acc / l ; lane holds O[query][16d + 4g + r]
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    float l = l_run[t];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int q = qw0 + 16 * t + (lane & 15);
+    if (q < Sq) {
+      uint16_t* orow = O + (EXT && ex.cu_q ? 0 : b * os.b) + h * os.h + (sq_.qo + q) * os.s;
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        s16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2s<T>(acc_o[t][d][r] * inv);
+        *reinterpret_cast<s16x4*>(orow + 16 * d + 4 * g) = o;
+      }
+      if (g == 0) {
+        const float mm = (m_run[t] == -INFINITY) ? 0.f : m_run[t];
+        LSE[sq_.lrow + q] = l > 0.f ? (mm + log2f(l)) * kLn2 : -INFINITY;
+      }
+    }
+  }
+}
+
+// ============================================================================ backward
+// delta[b, h, q] = sum_d dO[q, d] * O[q, d] is computed inside bwd_dq_kernel (launched before the
+// dK/dV kernel, which reads the stored rows); there is no separate delta pass.
+
+// dK/dV: grid (ceil(Sk / (16*NT*NW)), Hq, B); NW waves x (16*NT) keys; loop over 64-query blocks.
+// NW = 8 doubles the keys that share each staged Q/dO tile (halving the Q/dO re-reads from
+// L2/HBM, which bound the 4-wave form) at the same 2 waves/SIMD.
+// NT = 2 halves the LDS bytes per MFMA (every Q / dO fragment read from LDS feeds two key tiles)
+// at one wave per SIMD (the accumulators of 32 keys x D need the full register file).
+// dK/dV are written per q-head ([B, Sk, Hq, D] strides given by dks/dvs); GQA sums outside.
+// PIPE: Q/dO tiles double-buffered in LDS — one barrier per query block instead of two (tile
+// i+1 is written into the other buffer right after block i's compute; its global loads were
+// issued one block earlier).
+template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0, bool PIPE = false>
+// (D = 96 with an additive mask needs more than 256 registers: one wave per SIMD there too)
+__global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 2) != 0)) ? 1 : 3 - NT) void bwd_dkdv_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
+    uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq_, int Sk_, int Hq, int Hk, Strides qs, Strides ks_,
+    Strides vs, Strides dos, Strides dks, Strides dvs, float scale, Extra ex = Extra{}) {
+  if constexpr ((EXT & 4) != 0) ex.seed = rng_mix(ex.seed);  // graph-captured steps: per-replay stream
+  constexpr int KS = D / 32;
+  constexpr int DB = D / 16;
+  // D = 128: tiles read both by rows (ds_read_b128) and by columns (tr_b16) use the chunk ^
+  // ((row & 7) << 1) image, conflict free for both (the row-only swizzle leaves the tr reads
+  // 2-way: SQ_LDS_BANK_CONFLICT was 20-27 % of LDS cycles in these kernels)
+  constexpr bool BT = (fa_pitch<D>() >= 128);
+  constexpr int STAGE = 2 * 64 * fa_pitch<D>() * 2 + 2 * 64 * 4;  // Q, dO, LSE, delta of one query block
+  __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches and addresses
+  const int g = lane >> 4;
+  // grid (Hq, B, key-blocks): early key blocks (the most causal queries) first within a pair
+  int h, b, zi;
+  pair_order(Hq, (int)gridDim.y, (int)gridDim.z, h, b, zi);
+  const int hk = h / (Hq / Hk);
+  const Seq sq_ = seq_of<EXT != 0>(ex, b, h, Hq, Sq_, Sk_);
+  const int Sq = sq_.sq, Sk = sq_.sk;
+  const int k0 = zi * 16 * NT * NW;
+  if (EXT && k0 >= Sk) return;
+  const int kw = k0 + wave * 16 * NT;
+  const int off = Sk - Sq;
+  const float scale_log2 = scale * kLog2e;
+  const bool vl = EXT && ex.cu_q;
+
+  const uint16_t* qbase = Q + (vl ? 0 : b * qs.b) + sq_.qo * qs.s + h * qs.h;
+  const uint16_t* dobase = dO + (vl ? 0 : b * dos.b) + sq_.qo * dos.s + h * dos.h;
+  K += (vl ? 0 : b * ks_.b) + sq_.ko * ks_.s;
+  V += (vl ? 0 : b * vs.b) + sq_.ko * vs.s;
+  // K, V of this wave's keys as B operands: lane holds K[key][32ks + 8g .. +8]
+  s16x8 kf[NT][KS], vf[NT][KS];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int key = kw + 16 * j + (lane & 15);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      if (key < Sk) {
+        kf[j][k] = *reinterpret_cast<const s16x8*>(K + hk * ks_.h + (long long)key * ks_.s + 32 * k + 8 * g);
+        vf[j][k] = *reinterpret_cast<const s16x8*>(V + hk * vs.h + (long long)key * vs.s + 32 * k + 8 * g);
+      } else {
+        kf[j][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        vf[j][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+  }
+  f32x4 acc_dk[NT][DB], acc_dv[NT][DB];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+      acc_dk[j][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc_dv[j][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  int rstart[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int key = kw + 16 * j + (lane & 15);
+    rstart[j] = ((EXT & 8) != 0 && key < Sk) ? row_start(ex, b, h, key) : 0x7fffffff;
+  }
+  int qstart = 0;
+  if (CAUSAL) qstart = max(0, (k0 - off) / 64 * 64);
+  const int nqb = (Sq - qstart + 63) / 64;
+  const float* lse_b = LSE + sq_.lrow;
+  const float* dl_b = Delta + sq_.lrow;
+
+  Tile<D, 64 * NW> qt, dot;
+  qt.init(qbase, qs.s);
+  dot.init(dobase, dos.s);
+  // the block's LSE / delta rows are prefetched into registers with the Q / dO tile (a load at
+  // the store point would stall every wave of the block on one L2 round trip per query block)
+  float lse_n = 0.f, dl_n = 0.f;
+  auto load_rows = [&](int qq0) {
+    if (threadIdx.x < 64) {
+      const int q = qq0 + threadIdx.x;
+      lse_n = q < Sq ? lse_b[q] : -INFINITY;
+      dl_n = q < Sq ? dl_b[q] : 0.f;
+    }
+  };
+  auto stage_store = [&](char* st) {
+    qt.template store<BT>(st);
+    dot.template store<BT>(st + 64 * fa_pitch<D>() * 2);
+    if (threadIdx.x < 64) {
+      float* l = reinterpret_cast<float*>(st + 2 * 64 * fa_pitch<D>() * 2);
+      // a fully masked row (LSE = -inf) has P = 0: +inf makes every exp2 below vanish
+      l[threadIdx.x] = lse_n == -INFINITY ? INFINITY : lse_n * kLog2e;
+      l[64 + threadIdx.x] = dl_n;
+    }
+  };
+  auto stage_load = [&](int qq0) {
+    qt.load(qq0, Sq);
+    dot.load(qq0, Sq);
+    load_rows(qq0);
+  };
+  if (nqb > 0) stage_load(qstart);
+  if (PIPE && nqb > 0) {
+    stage_store(smem);
+    if (nqb > 1) stage_load(qstart + 64);
+    __syncthreads();
+  }
+  for (int i = 0; i < nqb; ++i) {
+    const int q0 = qstart + i * 64;
+    char* st = smem + (PIPE ? (i & 1) * STAGE : 0);
+    if (!PIPE) {
+      __syncthreads();
+      stage_store(st);
+      __syncthreads();
+      if (i + 1 < nqb) stage_load(q0 + 64);
+    }
+    const char* q_lds = st;
+    const char* do_lds = st + 64 * fa_pitch<D>() * 2;
+    const float* lse_lds = reinterpret_cast<const float*>(st + 2 * 64 * fa_pitch<D>() * 2);
+    const float* dl_lds = lse_lds + 64;
+    // whole query block above this wave's keys: nothing to compute (still joins the barriers)
+    if (!(CAUSAL && q0 + 63 + off < kw)) {
+    // S = Q K^T, dP = dO V^T : acc[j][m] holds [query 16m + 4g + r][key 16j + lane&15]
+    f32x4 acc_s[NT][4], acc_dp[NT][4];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        acc_s[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc_dp[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const s16x8 qa = ld_row8<D, BT>(q_lds, 16 * m + (lane & 15), k, g);
+        const s16x8 da = ld_row8<D, BT>(do_lds, 16 * m + (lane & 15), k, g);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          acc_s[j][m] = Mfma<T>::run(qa, kf[j][k], acc_s[j][m]);
+          acc_dp[j][m] = Mfma<T>::run(da, vf[j][k], acc_dp[j][m]);
+        }
+      }
+    }
+    // P and dS, packed as B operands (k = query, permuted as in the forward)
+    const bool need_mask = (q0 + 64 > Sq) || (kw + 16 * NT > Sk) || (CAUSAL && kw + 16 * NT - 1 > q0 + off);
+    s16x8 pb[NT][2], db_[NT][2];
+    // two instantiations of the elementwise block, selected by a wave-uniform branch: with one
+    // body and a runtime test hipcc if-converts the mask into per-element selects that every
+    // (mostly unmasked) tile pays
+    auto p_ds = [&](auto mask_tag) {
+    constexpr bool MASK = decltype(mask_tag)::value;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const float4 lse4 = *reinterpret_cast<const float4*>(lse_lds + 16 * m + 4 * g);
+      const float4 dl4 = *reinterpret_cast<const float4*>(dl_lds + 16 * m + 4 * g);
+      const float lsev[4] = {lse4.x, lse4.y, lse4.z, lse4.w};
+      const float dlv[4] = {dl4.x, dl4.y, dl4.z, dl4.w};
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int mykey = kw + 16 * j + (lane & 15);
+        // dropout: the four lanes of a quad hold keys 4c..4c+3 of the same four queries, so each
+        // lane hashes ONE (query 4g + (lane & 3), key quad) and the quad shares the four words
+        // through DPP quad broadcasts (1 hash per lane instead of 4; same bits as drop_z)
+        uint32_t hq[4] = {0u, 0u, 0u, 0u};
+        if constexpr ((EXT & 4) != 0) {
+          const int hmine = (int)drop_bits(ex, b * Hq + h, q0 + 16 * m + 4 * g + (lane & 3), kw + 16 * j + (lane & 12));
+          hq[0] = (uint32_t)__builtin_amdgcn_mov_dpp(hmine, 0x00, 0xF, 0xF, false);
+          hq[1] = (uint32_t)__builtin_amdgcn_mov_dpp(hmine, 0x55, 0xF, 0xF, false);
+          hq[2] = (uint32_t)__builtin_amdgcn_mov_dpp(hmine, 0xAA, 0xF, 0xF, false);
+          hq[3] = (uint32_t)__builtin_amdgcn_mov_dpp(hmine, 0xFF, 0xF, 0xF, false);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = q0 + 16 * m + 4 * g + r;
+          float sv = acc_s[j][m][r];
+          float sl = scale_log2;
+          if constexpr ((EXT & 2) != 0) {  // natural units + mask, then base-2
+            float mv = 0.f;
+            if (q < Sq && mykey < Sk) {
+              const long long mi = (long long)b * ex.mb + (long long)h * ex.mh + (long long)q * ex.mq + mykey;
+              mv = ex.mask_f32 ? reinterpret_cast<const float*>(ex.mask)[mi]
+                               : to_f(reinterpret_cast<const T*>(ex.mask)[mi]);
+            }
+            sv = sv * scale + mv;
+            sl = kLog2e;
+          }
+          float p = fast_exp2(__builtin_fmaf(sv, sl, -lsev[r]));
+          if constexpr (MASK) {
+            const bool masked = (q >= Sq) || (mykey >= Sk) || (CAUSAL && mykey > q + off);
+            p = masked ? 0.f : p;
+          }
+          if constexpr ((EXT & 8) != 0) p = q >= rstart[j] ? 0.f : p;
+          float z = 1.f;
+          if constexpr ((EXT & 4) != 0) z = drop_sub(ex, hq[r], mykey & 3);
+          const float ds = p * (acc_dp[j][m][r] * z - dlv[r]);
+          pb[j][m >> 1][(m & 1) * 4 + r] = f2s<T>(p * z);
+          db_[j][m >> 1][(m & 1) * 4 + r] = f2s<T>(ds);
+        }
+      }
+    }
+    };
+    if (need_mask)
+      p_ds(std::true_type{});
+    else
+      p_ds(std::false_type{});
+    // dV^T += dO^T P ;  dK^T += Q^T dS
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const s16x8 doa = ld_tr8<D, BT>(do_lds, 32 * s, d, lane);
+        const s16x8 qa = ld_tr8<D, BT>(q_lds, 32 * s, d, lane);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          acc_dv[j][d] = Mfma<T>::run(doa, pb[j][s], acc_dv[j][d]);
+          acc_dk[j][d] = Mfma<T>::run(qa, db_[j][s], acc_dk[j][d]);
+        }
+      }
+    }
+    }  // not above the diagonal
+    if (PIPE) {
+      if (i + 1 < nqb) {
+        // the other buffer was last read in block i - 1, before the barrier that ended it
+        stage_store(smem + ((i + 1) & 1) * STAGE);
+        if (i + 2 < nqb) stage_load(q0 + 128);
+      }
+      __syncthreads();
+    }
+  }
+  // epilogue: lane holds d[16d + 4g + r][key 16j + lane&15]
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int mykey = kw + 16 * j + (lane & 15);
+    if (mykey < Sk) {
+      uint16_t* dkrow = dK + (vl ? 0 : b * dks.b) + h * dks.h + (sq_.ko + mykey) * dks.s;
+      uint16_t* dvrow = dV + (vl ? 0 : b * dvs.b) + h * dvs.h + (sq_.ko + mykey) * dvs.s;
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        s16x4 a, c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          a[r] = f2s<T>(acc_dk[j][d][r] * scale);
+          c[r] = f2s<T>(acc_dv[j][d][r]);
+        }
+        *reinterpret_cast<s16x4*>(dkrow + 16 * d + 4 * g) = a;
+        *reinterpret_cast<s16x4*>(dvrow + 16 * d + 4 * g) = c;
+      }
+    }
+  }
+}
+
+// dQ: grid (ceil(Sq / (16*NT*NW)), Hq, B); NW waves x (16*NT) queries; loop over 64-key blocks
+// (swapped products: lane owns a query).  NT = 2: every K / V fragment read feeds two query tiles.
+// PIPE: K/V tiles double-buffered in LDS, one barrier per key block (as bwd_dkdv_kernel).
+template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0, bool PIPE = false>
+__global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128) ? 1 : 3 - NT) void bwd_dq_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
+    uint16_t* __restrict__ dQ, int Sq_, int Sk_, int Hq, int Hk, Strides qs, Strides ks_, Strides vs, Strides dos,
+    Strides dqs, float scale, Extra ex = Extra{}, const uint16_t* __restrict__ O = nullptr, Strides os = Strides{}) {
+  if constexpr ((EXT & 4) != 0) ex.seed = rng_mix(ex.seed);  // graph-captured steps: per-replay stream
+  constexpr int KS = D / 32;
+  constexpr int DB = D / 16;
+  // D = 128: tiles read both by rows (ds_read_b128) and by columns (tr_b16) use the chunk ^
+  // ((row & 7) << 1) image, conflict free for both (the row-only swizzle leaves the tr reads
+  // 2-way: SQ_LDS_BANK_CONFLICT was 20-27 % of LDS cycles in these kernels)
+  constexpr bool BT = (fa_pitch<D>() >= 128);
+  constexpr int STAGE = 2 * 64 * fa_pitch<D>() * 2;  // K and V of one key block
+  __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches and addresses
+  const int g = lane >> 4;
+  const int nqb = (Sq_ + 16 * NT * NW - 1) / (16 * NT * NW);
+  int h, b, zi;  // grid (Hq, B, q-blocks): heaviest first within a pair
+  pair_order(Hq, (int)gridDim.y, nqb, h, b, zi);
+  const int qb = nqb - 1 - zi;
+  const int hk = h / (Hq / Hk);
+  const Seq sq_ = seq_of<EXT != 0>(ex, b, h, Hq, Sq_, Sk_);
+  const int Sq = sq_.sq, Sk = sq_.sk;
+  const int q0 = qb * 16 * NT * NW;
+  if (EXT && q0 >= Sq) return;
+  const int qw = q0 + wave * 16 * NT;
+  const int off = Sk - Sq;
+  const float scale_log2 = scale * kLog2e;
+  const bool vl = EXT && ex.cu_q;
+  Q += (vl ? 0 : b * qs.b) + sq_.qo * qs.s;
+  dO += (vl ? 0 : b * dos.b) + sq_.qo * dos.s;
+  // O != null: delta = rowsum(dO * O) is computed here from the dO fragments this kernel holds
+  // anyway (lane: 8 * KS elements of its query row; the 4 lane groups reduced by shuffles) and
+  // stored for the dK/dV kernel launched after this one (no separate delta pass)
+  const bool fuse_delta = O != nullptr;
+  if (fuse_delta) O += (vl ? 0 : b * os.b) + sq_.qo * os.s;
+
+  s16x8 qf[NT][KS], dof[NT][KS], of[NT][KS];
+  float lse2[NT], dlt[NT];
+  const long long lrow = sq_.lrow;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int myq = qw + 16 * t + (lane & 15);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      if (myq < Sq) {
+        qf[t][k] = *reinterpret_cast<const s16x8*>(Q + h * qs.h + (long long)myq * qs.s + 32 * k + 8 * g);
+        dof[t][k] = *reinterpret_cast<const s16x8*>(dO + h * dos.h + (long long)myq * dos.s + 32 * k + 8 * g);
+      } else {
+        qf[t][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        dof[t][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+    const float lv = myq < Sq ? LSE[lrow + myq] : -INFINITY;
+    lse2[t] = lv == -INFINITY ? INFINITY : lv * kLog2e;
+    if (fuse_delta) {  // O fragments issued now, reduced after the first K/V tile loads are in flight
+#pragma unroll
+      for (int k = 0; k < KS; ++k)
+        of[t][k] = myq < Sq ? *reinterpret_cast<const s16x8*>(O + h * os.h + (long long)myq * os.s + 32 * k + 8 * g)
+                            : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    } else {
+      dlt[t] = myq < Sq ? Delta[lrow + myq] : 0.f;
+    }
+  }
+  f32x4 acc[NT][DB];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int d = 0; d < DB; ++d) acc[t][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const uint16_t* kbase = K + (vl ? 0 : b * ks_.b) + sq_.ko * ks_.s + hk * ks_.h;
+  const uint16_t* vbase = V + (vl ? 0 : b * vs.b) + sq_.ko * vs.s + hk * vs.h;
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + 16 * NT * NW + off);
+  const int nkb = kend > 0 ? (kend + 63) / 64 : 0;
+  Tile<D, 64 * NW> kt, vt;
+  kt.init(kbase, ks_.s);
+  vt.init(vbase, vs.s);
+  if (nkb > 0) {
+    kt.load(0, Sk);
+    vt.load(0, Sk);
+  }
+  if (fuse_delta) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float ds = 0.f;
+#pragma unroll
+      for (int k = 0; k < KS; ++k)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          ds += to_f(__builtin_bit_cast(T, (short)dof[t][k][e])) * to_f(__builtin_bit_cast(T, (short)of[t][k][e]));
+      ds += __shfl_xor(ds, 16);
+      ds += __shfl_xor(ds, 32);
+      dlt[t] = ds;
+      const int myq = qw + 16 * t + (lane & 15);
+      if (g == 0 && myq < Sq) Delta[lrow + myq] = ds;
+    }
+  }
+  if (PIPE && nkb > 0) {
+    kt.template store<BT>(smem);
+    vt.template store<BT>(smem + 64 * fa_pitch<D>() * 2);
+    if (nkb > 1) {
+      kt.load(64, Sk);
+      vt.load(64, Sk);
+    }
+    __syncthreads();
+  }
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * 64;
+    char* st = smem + (PIPE ? (kb & 1) * STAGE : 0);
+    if (!PIPE) {
+      __syncthreads();
+      kt.template store<BT>(st);
+      vt.template store<BT>(st + 64 * fa_pitch<D>() * 2);
+      __syncthreads();
+      if (kb + 1 < nkb) {
+        kt.load(k0 + 64, Sk);
+        vt.load(k0 + 64, Sk);
+      }
+    }
+    const char* k_lds = st;
+    const char* v_lds = st + 64 * fa_pitch<D>() * 2;
+    if (!(CAUSAL && k0 > qw + 16 * NT - 1 + off)) {
+    f32x4 acc_s[NT][4], acc_dp[NT][4];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc_s[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc_dp[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const s16x8 ka = ld_row8<D, BT>(k_lds, 16 * j + (lane & 15), k, g);
+        const s16x8 va = ld_row8<D, BT>(v_lds, 16 * j + (lane & 15), k, g);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          acc_s[t][j] = Mfma<T>::run(ka, qf[t][k], acc_s[t][j]);
+          acc_dp[t][j] = Mfma<T>::run(va, dof[t][k], acc_dp[t][j]);
+        }
+      }
+    }
+    const bool need_mask = (k0 + 64 > Sk) || (qw + 16 * NT > Sq) || (CAUSAL && k0 + 63 > qw + off);
+    s16x8 dsb[NT][2];
+    auto ds_blk = [&](auto mask_tag) {  // masked / unmasked instantiations (see bwd_dkdv_kernel)
+    constexpr bool MASK = decltype(mask_tag)::value;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int myq = qw + 16 * t + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float mv[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr ((EXT & 2) != 0)
+          if (myq < Sq) mask_row4<T>(ex, b, h, myq, k0 + 16 * j + 4 * g, Sk, mv);
+        uint32_t dbits = 0;
+        if constexpr ((EXT & 4) != 0) dbits = drop_bits(ex, b * Hq + h, myq, k0 + 16 * j + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 16 * j + 4 * g + r;
+          const float sv = (EXT & 2) ? acc_s[t][j][r] * scale + mv[r] : acc_s[t][j][r];
+          float p = fast_exp2(__builtin_fmaf(sv, (EXT & 2) ? kLog2e : scale_log2, -lse2[t]));
+          if constexpr (MASK) {
+            const bool masked = (key >= Sk) || (myq >= Sq) || (CAUSAL && key > myq + off);
+            p = masked ? 0.f : p;
+          }
+          if constexpr ((EXT & 8) != 0)
+            if (key < Sk && myq >= row_start(ex, b, h, key)) p = 0.f;
+          float z = 1.f;
+          if constexpr ((EXT & 4) != 0) z = drop_sub(ex, dbits, r);
+          dsb[t][j >> 1][(j & 1) * 4 + r] = f2s<T>(p * (acc_dp[t][j][r] * z - dlt[t]));
+        }
+      }
+    }
+    };
+    if (need_mask)
+      ds_blk(std::true_type{});
+    else
+      ds_blk(std::false_type{});
+    // dQ^T += K^T dS^T
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const s16x8 ka = ld_tr8<D, BT>(k_lds, 32 * s, d, lane);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t][d] = Mfma<T>::run(ka, dsb[t][s], acc[t][d]);
+      }
+    }
+    }  // not above the diagonal
+    if (PIPE) {
+      if (kb + 1 < nkb) {
+        char* nx = smem + ((kb + 1) & 1) * STAGE;  // last read in block kb - 1
+        kt.template store<BT>(nx);
+        vt.template store<BT>(nx + 64 * fa_pitch<D>() * 2);
+        if (kb + 2 < nkb) {
+          kt.load(k0 + 128, Sk);
+          vt.load(k0 + 128, Sk);
+        }
+      }
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int myq = qw + 16 * t + (lane & 15);
+    if (myq < Sq) {
+      uint16_t* row = dQ + (vl ? 0 : b * dqs.b) + h * dqs.h + (sq_.qo + myq) * dqs.s;
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        s16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2s<T>(acc[t][d][r] * scale);
+        *reinterpret_cast<s16x4*>(row + 16 * d + 4 * g) = o;
+      }
+    }
+  }
+}
+
+}  // namespace fa
+}  // namespace pa

@@ -1,7 +1,9 @@
 """paddle.nn.functional conv / pooling (reference: python/paddle/nn/functional/{conv,pooling}.py).
 
-Convolutions run on MIOpen through the storage layer (library path); channels-last
-(NHWC) input is kept channels-last in memory, which is MIOpen's fast layout on CDNA.
+bf16 2-D convolutions (NCHW or NHWC) run on the hand-written implicit-GEMM kernels of csrc/conv.hip
+channels-last; NCHW tensors are carried as NCHW views with channels-last strides, so a default
+``data_format='NCHW'`` network pays no layout copies between layers.  Depthwise convolutions run
+on csrc/dwconv.hip.  Shapes the kernels reject fall back to the storage layer (MIOpen).
 """
 import numpy as np
 import torch
@@ -79,9 +81,17 @@ def _conv(x, weight, bias, stride, padding, dilation, groups, data_format, nd, f
     p, extra = _resolve_padding(padding, nd, list(t.shape[2:]), list(w.shape[2:]), s, d)
     if extra is not None:
         t = TF.pad(t, extra)
-    if cl and nd == 2 and ops.use_hip(t) and ops.conv.supported(t.permute(0, 2, 3, 1), w, groups):
-        # NHWC conv2d forward on the hand-written implicit-GEMM kernel (csrc/conv.hip)
-        return _w(ops.conv.conv2d_nhwc(t.permute(0, 2, 3, 1), w, b, s, p, d))
+    if nd == 2 and ops.use_hip(t) and ops.conv.supported(t.permute(0, 2, 3, 1), w, groups):
+        # conv2d on the hand-written implicit-GEMM kernels (csrc/conv.hip), which run channels-last.
+        # NCHW (paddle's default) is served transparently: the NHWC result is returned as an NCHW
+        # view with channels-last strides, which the next conv / batch norm / max pool takes
+        # without a copy (only a genuinely NCHW-contiguous input, e.g. the image, is repacked once).
+        y = ops.conv.conv2d_nhwc(t.permute(0, 2, 3, 1).contiguous(), w, b, s, p, d)
+        return _w(y if cl else y.permute(0, 3, 1, 2))
+    if nd == 2 and ops.use_hip(t) and ops.conv.dw_supported(t.permute(0, 2, 3, 1), w, groups):
+        # depthwise (groups == C_in == C_out) on csrc/dwconv.hip, channels-last as above
+        y = ops.conv.dwconv2d_nhwc(t.permute(0, 2, 3, 1).contiguous(), w, b, s, p, d)
+        return _w(y if cl else y.permute(0, 3, 1, 2))
     out = fn(t, w, b, s, p, d, groups)
     if cl:
         out = out.permute(0, *range(2, nd + 2), 1)
@@ -154,10 +164,13 @@ def _pool(x, kernel_size, stride, padding, ceil_mode, data_format, nd, fn, extra
     if pre is not None:
         t = TF.pad(t, pre, value=float('-inf') if fn in (TF.max_pool1d, TF.max_pool2d, TF.max_pool3d) else 0.0)
     kw = dict(extra or {})
-    if cl and nd == 2 and fn is TF.max_pool2d and not return_mask and pre is None and ops.use_hip(t) and \
-            ops.pool.supported(_u(x), k, s, p):
-        # NHWC max pool on csrc/pool.hip (one-byte argmax, atomics-free gather backward)
-        return _w(ops.pool.max_pool2d_nhwc(_u(x), k, s, p, ceil_mode))
+    if nd == 2 and fn is TF.max_pool2d and not return_mask and pre is None and ops.use_hip(t):
+        # NHWC max pool on csrc/pool.hip (one-byte argmax, atomics-free gather backward); an NCHW
+        # tensor with channels-last strides (the output of a routed conv2d) is the same memory
+        xn = _u(x) if cl else t.permute(0, 2, 3, 1)
+        if (cl or xn.is_contiguous()) and ops.pool.supported(xn, k, s, p):
+            y = ops.pool.max_pool2d_nhwc(xn, k, s, p, ceil_mode)
+            return _w(y if cl else y.permute(0, 3, 1, 2))
     if return_mask:
         out, mask = fn(t, k, s, p, ceil_mode=ceil_mode, return_indices=True, **kw)
         if cl:

@@ -54,10 +54,10 @@ def _sdpa_reference(q, k, v, mask, dropout_p, causal, scale=None):
 
 
 def _pad_head(q, k, v):
-    """Head dims the kernels do not tile (e.g. 80, 96) are zero-padded to the next tiled one
-    (64 / 128): the extra q·k terms are 0 and the extra output columns are sliced off."""
+    """Head dims the kernels do not tile (e.g. 80, 192) are zero-padded to the next tiled one
+    (64 / 96 / 128 / 256): the extra q·k terms are 0 and the extra output columns are sliced off."""
     D = q.shape[-1]
-    Dp = 64 if D <= 64 else 128 if D <= 128 else D
+    Dp = ops.flash_attn.tiled_head_dim(D) or D
     if Dp == D:
         return q, k, v, D
     return (TF.pad(q, (0, Dp - D)), TF.pad(k, (0, Dp - D)), TF.pad(v, (0, Dp - D)), D)
@@ -67,10 +67,10 @@ def _hip_ok(q, k, v):
     if not ops.use_hip(q):
         return False
     D = q.shape[-1]
-    Dp = 64 if D <= 64 else 128 if D <= 128 else D
+    Dp = ops.flash_attn.tiled_head_dim(D)
     # shape/dtype contract of the kernels, checked on the (padded) operand geometry
     return (q.dtype in (torch.bfloat16, torch.float16) and k.dtype == q.dtype and v.dtype == q.dtype
-            and Dp in (64, 128) and k.shape[-1] == D and v.shape[-1] == D and k.shape == v.shape
+            and Dp is not None and k.shape[-1] == D and v.shape[-1] == D and k.shape == v.shape
             and k.shape[-2] > 0 and q.shape[-2] % k.shape[-2] == 0)
 
 

@@ -44,10 +44,20 @@ def batch_norm(x, running_mean, running_var, weight=None, bias=None, training=Fa
     cl = data_format[-1] == 'C' and t.dim() > 2
     use_batch = training if use_global_stats is None else not use_global_stats
     rm, rv = _u(running_mean), _u(running_var)
-    if cl and use_batch and ops.use_hip(t) and ops.batchnorm.supported(t, None if weight is None else _u(weight)):
+    g = None if weight is None else _u(weight)
+    if cl and use_batch and ops.use_hip(t) and ops.batchnorm.supported(t, g):
         # channels-last activation = [rows, C] matrix: column-blocked HIP statistics + apply kernels
-        return _w(ops.batchnorm.bn_act_nhwc(t, None if weight is None else _u(weight),
-                                            None if bias is None else _u(bias), rm, rv, epsilon, momentum, True))
+        return _w(ops.batchnorm.bn_act_nhwc(t, g, None if bias is None else _u(bias), rm, rv, epsilon, momentum,
+                                            True))
+    if not cl and t.dim() == 4 and ops.use_hip(t) and t.is_contiguous(memory_format=torch.channels_last) \
+            and ops.batchnorm.supported(t.permute(0, 2, 3, 1), g) \
+            and (use_batch or not (torch.is_grad_enabled() and any(
+                v is not None and v.requires_grad for v in (t, g, None if bias is None else _u(bias))))):
+        # NCHW view with channels-last strides (a routed conv2d output): the same kernels on the
+        # NHWC image (inference with running statistics included: no backward needed there)
+        y = ops.batchnorm.bn_act_nhwc(t.permute(0, 2, 3, 1), g, None if bias is None else _u(bias), rm, rv, epsilon,
+                                      momentum, bool(use_batch))
+        return _w(y.permute(0, 3, 1, 2))
     if cl:
         t = t.permute(0, t.dim() - 1, *range(1, t.dim() - 1))
     out = TF.batch_norm(t, rm, rv, None if weight is None else _u(weight), None if bias is None else _u(bias),

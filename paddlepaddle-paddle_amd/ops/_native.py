@@ -36,6 +36,15 @@ _SIGS = {
     'pa_colsum': [P, P, P, I, I, I, I, I, P],
     'pa_transpose2d': [P, P, I, I, I, P],
     'pa_maxpool2d_nhwc_fwd': [P, P, P] + [I] * 13 + [P],
+    'pa_dwconv_ok': [I] * 15,
+    'pa_conv_stem_ok': [I] * 6,
+    'pa_conv_stem_kp': [I, I, I],
+    'pa_conv_stem_rk': [I, I],
+    'pa_conv_stem_fwd': [P, P, P, P] + [I] * 14 + [P],
+    'pa_dwconv_fwd': [P, P, P, P] + [I] * 15 + [P],
+    'pa_dwconv_dgrad': [P, P, P] + [I] * 15 + [P],
+    'pa_dwconv_wgrad_splits': [I] * 6,
+    'pa_dwconv_wgrad': [P, P, P, P] + [I] * 17 + [P],
     'pa_maxpool2d_nhwc_bwd': [P, P, P] + [I] * 13 + [P],
     'pa_bn_ws_floats': [I, I, I],
     'pa_bn_fwd': [P, P, P, P, P, P, P, P, P, P, I, I, F, F, I, I, I, I, P],

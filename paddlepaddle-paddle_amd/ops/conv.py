@@ -81,7 +81,7 @@ def _out_hw(H, W, R, S, stride, pad, dil):
 # statistics pass.  Entries are keyed by the output tensor object (weak reference) and popped by
 # the consumer.
 _stats_mode = [0]
-_bn_parts = {}  # id(y) -> (weakref(y), parts [2][P][C] fp32, P, rows per slab)
+_bn_parts = {}  # (data_ptr, numel) of y -> (weakref(y), parts [2][P][C] fp32, P, rows per slab)
 
 
 class fused_bn_stats:
@@ -105,17 +105,27 @@ def _want_stats(b):
 _stats_enabled = os.environ.get('PADDLE_AMD_CONV_BN_STATS', '1') != '0'
 
 
+def _parts_key(t):
+    # keyed by memory, not by tensor object: an NCHW conv2d returns its NHWC output as a permuted
+    # view (ops reached through nn.functional see a different tensor object with the same storage)
+    return (t.data_ptr(), t.numel())
+
+
 def _stash_parts(y, parts, P, rpb):
     import weakref
     for k in [k for k, v in _bn_parts.items() if v[0]() is None]:
         del _bn_parts[k]
-    _bn_parts[id(y)] = (weakref.ref(y), parts, P, rpb)
+    _bn_parts[_parts_key(y)] = (weakref.ref(y), parts, P, rpb, y._version)
 
 
 def take_bn_parts(x):
-    """(parts, P, rows per slab) of a tensor produced under fused_bn_stats(), or None."""
-    e = _bn_parts.pop(id(x), None)
-    if e is None or e[0]() is not x:
+    """(parts, P, rows per slab) of a tensor produced under fused_bn_stats() (or a view of it with
+    the same memory), or None."""
+    e = _bn_parts.pop(_parts_key(x), None)
+    if e is None:
+        return None
+    y = e[0]()
+    if y is None or x._version != e[4]:  # freed, or modified in place since the epilogue wrote them
         return None
     return e[1], e[2], e[3]
 
@@ -183,7 +193,7 @@ def conv2d_fwd_im2col(x, w, b, stride, pad, dil):
     y = y4.view(Nb, Ho, Wo, Cout)
     e = take_bn_parts(y4)
     if e is not None:  # statistics were stashed under the [1, M, 1, Cout] output: re-key them to y
-        _stash_parts(y, *e)
+        _stash_parts(y, *e[:3])
     return y
 
 
@@ -427,6 +437,33 @@ class shared_dgrad:
         return False
 
 
+_stem_enabled = os.environ.get('PADDLE_AMD_CONV_STEM', '1') != '0'
+
+
+def stem_ok(x, w, stride, dil):
+    """Few-channel forward (the RGB stem) on csrc/conv_stem.hip."""
+    Cout, C, R, S = w.shape
+    return (_stem_enabled and tuple(dil) == (1, 1) and x.dtype == w.dtype and x.dtype in (torch.bfloat16, torch.float16)
+            and N.lib is not None and bool(N.lib.pa_conv_stem_ok(C, Cout, R, S, stride[0], stride[1])))
+
+
+def conv2d_fwd_stem(x, w, b, stride, pad):
+    """y = conv(x, w) for C <= 8: the R input-row segments of an output-row segment staged once in
+    LDS, MFMA over k = (filter row, s*C + c) with the [Cout][Kp] filter image below."""
+    x = x.contiguous()
+    Nb, H, W, C = x.shape
+    Cout, _, R, S = w.shape
+    Ho, Wo = _out_hw(H, W, R, S, stride, pad, (1, 1))
+    RK, Kp = int(N.lib.pa_conv_stem_rk(C, S)), int(N.lib.pa_conv_stem_kp(C, R, S))
+    wimg = torch.zeros(Cout, Kp, dtype=x.dtype, device=x.device)
+    wimg[:, :R * RK].view(Cout, R, RK)[:, :, :S * C] = w.detach().to(x.dtype).permute(0, 2, 3, 1).reshape(Cout, R, S * C)
+    y = torch.empty(Nb, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
+    bb = b.to(x.dtype).contiguous() if b is not None else None
+    N.check(N.lib.pa_conv_stem_fwd(N.ptr(x), N.ptr(wimg), N.ptr(bb), N.ptr(y), Nb, H, W, C, Cout, R, S, stride[0],
+                                   stride[1], pad[0], pad[1], Ho, Wo, N.dtcode(x.dtype), N.stream()), 'conv_stem_fwd')
+    return y
+
+
 def _lib_conv_fwd(x, w, b, stride, pad, dil):
     y = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w, b, stride, pad, dil)
     return y.permute(0, 2, 3, 1).contiguous()
@@ -447,6 +484,8 @@ class _Conv2dNHWC(torch.autograd.Function):
             return conv2d_fwd(x, w, b, stride, pad, dil)
         if im2col_ok(x, w) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
             return conv2d_fwd_im2col(x, w, b, stride, pad, dil)
+        if stem_ok(x, w, stride, dil):
+            return conv2d_fwd_stem(x, w, b, stride, pad)
         return _lib_conv_fwd(x, w, b, stride, pad, dil)
 
     @staticmethod
@@ -539,3 +578,79 @@ def conv2d_nhwc(x, w, b, stride, pad, dil):
         sink.armed = True
     shared = _shared_by_input.get((x.data_ptr(), tuple(x.shape))) if _shared_by_input else None
     return _Conv2dNHWC.apply(x, w, b, tuple(stride), tuple(pad), tuple(dil), sink, shared)
+
+
+# ---- depthwise convolution (groups == C_in == C_out) on csrc/dwconv.hip
+_dw_enabled = os.environ.get('PADDLE_AMD_HIP_DWCONV', '1') != '0'
+
+
+def dw_supported(x, w, groups):
+    """x: NHWC view; w: [C, 1, R, S] with groups == C (channel multiplier 1), 16-bit dtypes."""
+    if not _dw_enabled or x.dim() != 4 or w.dim() != 4 or not x.is_cuda:
+        return False
+    C = x.shape[3]
+    if groups != C or groups == 1 or w.shape[0] != C or w.shape[1] != 1 or C % 8:
+        return False
+    if x.dtype not in (torch.bfloat16, torch.float16) or w.dtype != x.dtype:
+        return False
+    return N.lib is not None or N._load() is not None
+
+
+def _dw_geo(x, w, stride, pad, dil):
+    Nb, H, W, C = x.shape
+    R, S = w.shape[2], w.shape[3]
+    Ho, Wo = _out_hw(H, W, R, S, stride, pad, dil)
+    return (Nb, H, W, C, Ho, Wo, R, S, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1])
+
+
+def _dw_taps(w):
+    """[C, 1, R, S] filter -> the tap-major [R*S][C] image the kernels read."""
+    C, _, R, S = w.shape
+    return w.detach().reshape(C, R * S).t().contiguous()
+
+
+class _DWConvNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, dil):
+        x = x.contiguous()
+        g = _dw_geo(x, w, stride, pad, dil)
+        Nb, H, W, C, Ho, Wo = g[:6]
+        dt = N.dtcode(x.dtype)
+        y = torch.empty(Nb, Ho, Wo, C, dtype=x.dtype, device=x.device)
+        bb = b.to(x.dtype).contiguous() if b is not None else None
+        N.check(N.lib.pa_dwconv_fwd(N.ptr(x), N.ptr(_dw_taps(w)), N.ptr(bb), N.ptr(y), *g, dt, N.stream()),
+                'dwconv_fwd')
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, pad, dil, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pad, dil, has_b = ctx.cfg
+        dy = dy.contiguous()
+        g = _dw_geo(x, w, stride, pad, dil)
+        Nb, H, W, C, Ho, Wo, R, S = g[:8]
+        dt = N.dtcode(x.dtype)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x)
+            N.check(N.lib.pa_dwconv_dgrad(N.ptr(dy), N.ptr(_dw_taps(w)), N.ptr(gx), *g, dt, N.stream()),
+                    'dwconv_dgrad')
+        if ctx.needs_input_grad[1]:
+            splits = int(N.lib.pa_dwconv_wgrad_splits(Nb, Ho, Wo, C, R, S))
+            ws = torch.empty(splits * R * S * C, dtype=torch.float32, device=x.device)
+            gw = torch.empty(C, 1, R, S, dtype=x.dtype, device=x.device)
+            N.check(N.lib.pa_dwconv_wgrad(N.ptr(x), N.ptr(dy), N.ptr(ws), N.ptr(gw), *g, splits, 0, dt, N.stream()),
+                    'dwconv_wgrad')
+            gw = gw.to(w.dtype)
+        if has_b and ctx.needs_input_grad[2]:
+            gb = dy.sum((0, 1, 2), dtype=torch.float32).to(dy.dtype)
+        return gx, gw, gb, None, None, None
+
+
+def dwconv2d_nhwc(x, w, b, stride, pad, dil):
+    """Depthwise conv2d of an NHWC tensor: x [N,H,W,C], w [C,1,R,S] -> y [N,Ho,Wo,C]."""
+    if N._load() is None:
+        raise RuntimeError("dwconv2d_nhwc: HIP kernel library not loaded: " + str(N.load_error))
+    return _DWConvNHWC.apply(x, w, b, tuple(stride), tuple(pad), tuple(dil))

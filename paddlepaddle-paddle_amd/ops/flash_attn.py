@@ -9,6 +9,18 @@ import torch
 from . import _native as N
 
 
+# head dims with native tiles: 64 / 128 (csrc/flash_attn.hip), 96 / 256 (csrc/flash_attn_wide.hip)
+HEAD_DIMS = (64, 96, 128, 256)
+
+
+def tiled_head_dim(D):
+    """The smallest natively tiled head dim >= D (operands are zero-padded to it), or None."""
+    for t in HEAD_DIMS:
+        if D <= t:
+            return t
+    return None
+
+
 def supported_ex(q, k, v):
     """The extended kernels (mask / dropout / varlen) take the same operand contract."""
     return supported(q, k, v)
@@ -16,7 +28,7 @@ def supported_ex(q, k, v):
 
 def supported(q, k, v):
     return (q.dim() == 4 and q.dtype in (torch.bfloat16, torch.float16) and k.dtype == q.dtype and v.dtype == q.dtype
-            and q.shape[-1] in (64, 128) and k.shape[-1] == q.shape[-1] and v.shape[-1] == q.shape[-1]
+            and q.shape[-1] in HEAD_DIMS and k.shape[-1] == q.shape[-1] and v.shape[-1] == q.shape[-1]
             and q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1
             and k.shape[2] > 0 and q.shape[2] % k.shape[2] == 0 and k.shape == v.shape
             and all(s % 8 == 0 for t in (q, k, v) for s in t.stride()[:3]))

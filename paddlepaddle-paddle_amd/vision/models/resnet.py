@@ -1,10 +1,12 @@
 """ResNet / ResNeXt / Wide-ResNet (reference: python/paddle/vision/models/resnet.py).
 
 Same sublayer names as the reference (conv1/bn1/layer1..4/fc, blocks conv1..3/bn1..3/downsample)
-so reference checkpoints map 1:1.  ``data_format='NHWC'`` keeps activations channels-last, the
-layout MIOpen's fast convolution paths want on CDNA.
+so reference checkpoints map 1:1.  Both data formats run the channels-last HIP kernels: NHWC
+directly, NCHW as NCHW views with channels-last strides (nn/functional/conv.py).
 """
 from contextlib import nullcontext as _nullctx
+
+import torch
 
 from ... import nn
 from ... import ops
@@ -14,20 +16,38 @@ from ...core.tensor import _wrap, _unwrap
 RESIDUAL_GRAD_SINK = True  # identity blocks: conv1's dgrad GEMM accumulates the residual gradient
 
 
+def _nhwc(bn, t):
+    """The channels-last image of an activation: itself for NHWC layers, the NHWC view of an
+    NCHW tensor with channels-last strides (what a routed NCHW conv2d returns), else None."""
+    if bn._data_format[-1] == 'C':
+        return t
+    if t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last):
+        return t.permute(0, 2, 3, 1)
+    return None
+
+
 def _fused_bn_ok(bn, t):
-    return (bn.training and bn._data_format[-1] == 'C' and ops.use_hip(t) and isinstance(bn, nn.BatchNorm2D)
-            and bn._use_global_stats is not True and ops.batchnorm.supported(t, None if bn.weight is None else bn.weight._t))
+    if not (bn.training and isinstance(bn, nn.BatchNorm2D) and bn._use_global_stats is not True and ops.use_hip(t)):
+        return False
+    tn = _nhwc(bn, t)
+    return tn is not None and ops.batchnorm.supported(tn, None if bn.weight is None else bn.weight._t)
 
 
 def _bn_act(bn, x, relu=True, residual=None, dz_sink=None):
     """act(bn(x) [+ residual]) — one csrc/batchnorm.hip pass each way for channels-last training
-    on the GPU (fused_bn_add_activation); the plain layer sequence otherwise."""
+    on the GPU (fused_bn_add_activation); the plain layer sequence otherwise.  NCHW layers run the
+    same kernels on the channels-last image (ops.conv returns NCHW views with NHWC strides)."""
     t = _unwrap(x)
     if _fused_bn_ok(bn, t):
-        return _wrap(ops.batchnorm.bn_act_nhwc(
-            t, None if bn.weight is None else bn.weight._t, None if bn.bias is None else bn.bias._t, bn._mean._t,
-            bn._variance._t, bn._epsilon, bn._momentum, True, relu, None if residual is None else _unwrap(residual),
-            dz_sink))
+        r = None
+        if residual is not None:
+            r = _nhwc(bn, _unwrap(residual))
+            if r is None:  # an NCHW-contiguous residual: repack it once
+                r = _unwrap(residual).permute(0, 2, 3, 1).contiguous()
+        y = ops.batchnorm.bn_act_nhwc(
+            _nhwc(bn, t), None if bn.weight is None else bn.weight._t, None if bn.bias is None else bn.bias._t,
+            bn._mean._t, bn._variance._t, bn._epsilon, bn._momentum, True, relu, r, dz_sink)
+        return _wrap(y if bn._data_format[-1] == 'C' else y.permute(0, 3, 1, 2))
     y = bn(x)
     if residual is not None:
         y = y + residual
@@ -84,6 +104,7 @@ class BottleneckBlock(nn.Layer):
         # (ops.conv.GradSink) instead of a separate autograd add of the two branch gradients
         sink = ops.conv.GradSink() if (RESIDUAL_GRAD_SINK and self.downsample is None
                                        and _fused_bn_ok(self.bn3, _unwrap(x))) else None
+        xk = _nhwc(self.bn3, _unwrap(x))  # the tensor conv2d_nhwc sees (shared-dgrad key)
         # downsample block: conv1 and the shortcut conv read the same x; their data gradients meet
         # in one tensor (ops.conv.SharedDgrad) instead of an autograd add
         shared = ops.conv.SharedDgrad() if (RESIDUAL_GRAD_SINK and self.downsample is not None
@@ -92,7 +113,7 @@ class BottleneckBlock(nn.Layer):
             with ops.conv.dgrad_sink(sink):
                 out = self.conv1(x)
         elif shared is not None:
-            with ops.conv.shared_dgrad(_unwrap(x), shared):
+            with ops.conv.shared_dgrad(xk, shared):
                 out = self.conv1(x)
         else:
             out = self.conv1(x)
@@ -101,7 +122,7 @@ class BottleneckBlock(nn.Layer):
         out = self.conv3(out)
         if self.downsample is not None:
             if shared is not None:
-                with ops.conv.shared_dgrad(_unwrap(x), shared):
+                with ops.conv.shared_dgrad(xk, shared):
                     identity = self.downsample(x)
             else:
                 identity = self.downsample(x)

@@ -1,0 +1,165 @@
+"""Convolution everywhere: depthwise kernels (csrc/dwconv.hip), the few-channel stem forward
+(csrc/conv_stem.hip) and the transparent NCHW -> channels-last routing of paddle.nn.functional
+conv2d / batch_norm / max_pool2d, each against a plain PyTorch fp32 reference; the default NCHW
+resnet50() must run without a single MIOpen kernel."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import paddle  # noqa: E402
+from paddle.ops import _native  # noqa: E402
+
+DEV = 'cuda'
+
+
+def setup_module(m):
+    torch.manual_seed(0)
+    assert _native._load() is not None, _native.load_error
+
+
+def _close(a, b, atol, rtol=0.0, name=''):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    tol = atol + rtol * b.abs().max().item()
+    assert err <= tol, f"{name}: max err {err} > {tol}"
+
+
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize('N,H,W,C,k,s,p,d', [
+    (4, 28, 28, 64, 3, 1, 1, 1), (2, 29, 31, 96, 3, 2, 1, 1), (2, 14, 14, 40, 5, 1, 2, 1),
+    (2, 17, 17, 32, 7, 2, 3, 1), (2, 20, 20, 48, 3, 1, 2, 2), (1, 9, 9, 1024, 3, 1, 1, 1)])
+@pytest.mark.parametrize('bias', [False, True])
+def test_dwconv_fwd_bwd(dt, N, H, W, C, k, s, p, d, bias):
+    from paddle.ops import conv
+    x = torch.randn(N, H, W, C, device=DEV, dtype=dt)
+    w = (0.3 * torch.randn(C, 1, k, k, device=DEV)).to(dt)
+    b = (0.1 * torch.randn(C, device=DEV)).to(dt) if bias else None
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    wr = w.detach().float().requires_grad_()
+    br = b.detach().float().requires_grad_() if bias else None
+    yr = torch.nn.functional.conv2d(xr, wr, br, s, p, d, groups=C).permute(0, 2, 3, 1)
+    xh, wh = x.clone().requires_grad_(), w.clone().requires_grad_()
+    bh = b.clone().requires_grad_() if bias else None
+    y = conv.dwconv2d_nhwc(xh, wh, bh, (s, s), (p, p), (d, d))
+    assert y.shape == yr.shape
+    _close(y, yr, 3e-2, 1e-2, 'dw fwd')
+    g = torch.randn_like(yr)
+    y.backward(g.to(dt))
+    yr.backward(g)
+    _close(xh.grad, xr.grad.permute(0, 2, 3, 1), 3e-2, 1e-2, 'dw dgrad')
+    _close(wh.grad, wr.grad, 5e-2, 2e-2, 'dw wgrad')
+    if bias:
+        _close(bh.grad, br.grad, 5e-2, 2e-2, 'dw dbias')
+
+
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize('N,H,W,C,Cout,k,s,p', [
+    (2, 64, 64, 3, 64, 7, 2, 3), (2, 224, 224, 3, 64, 7, 2, 3), (3, 33, 45, 4, 128, 3, 1, 1),
+    (2, 40, 40, 1, 64, 5, 2, 2), (1, 300, 300, 3, 64, 3, 2, 1)])
+@pytest.mark.parametrize('bias', [False, True])
+def test_conv_stem_fwd(dt, N, H, W, C, Cout, k, s, p, bias):
+    from paddle.ops import conv
+    x = torch.randn(N, H, W, C, device=DEV, dtype=dt)
+    w = (0.2 * torch.randn(Cout, C, k, k, device=DEV)).to(dt)
+    b = (0.1 * torch.randn(Cout, device=DEV)).to(dt) if bias else None
+    assert conv.stem_ok(x, w, (s, s), (1, 1))
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float(), None if b is None else b.float(), s,
+                                     p).permute(0, 2, 3, 1)
+    y = conv.conv2d_fwd_stem(x, w, b, (s, s), (p, p))
+    assert y.shape == ref.shape
+    _close(y, ref, 3e-2, 1e-2, 'stem fwd')
+
+
+def _miopen_kernels(fn):
+    """Names of the library (MIOpen) convolution / batch-norm / pooling kernels ``fn`` launches."""
+    from torch.profiler import profile, ProfilerActivity
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        fn()
+        torch.cuda.synchronize()
+    names = {e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA}
+    bad = ('miopen', 'igemm', 'naive_conv', 'batchnorm', 'im2col', 'col2im', 'conv_fwd', 'conv_bwd', 'gridwise',
+           'winograd', 'pooling', 'xdlops', 'subsample', 'sp3asm', 'mlo')
+    ours = ('pa::', 'pa_')
+    return sorted(n for n in names if any(b in n.lower() for b in bad) and not any(o in n for o in ours))
+
+
+def test_nchw_conv_bn_pool_routed():
+    """NCHW conv2d / batch_norm / max_pool2d on bf16 GPU tensors run the channels-last kernels:
+    outputs are NCHW views with channels-last strides, values match fp32 torch, and the profiler
+    sees no library convolution kernels."""
+    F = paddle.nn.functional
+    x = torch.randn(4, 32, 20, 20, device=DEV).bfloat16()
+    w = (0.1 * torch.randn(64, 32, 3, 3, device=DEV)).bfloat16()
+    gamma = torch.ones(64, device=DEV)
+    beta = torch.zeros(64, device=DEV)
+    rm, rv = torch.zeros(64, device=DEV), torch.ones(64, device=DEV)
+    out = {}
+
+    def run():
+        y = F.conv2d(paddle.to_tensor(x), paddle.to_tensor(w), padding=1)
+        z = F.batch_norm(y, paddle.to_tensor(rm), paddle.to_tensor(rv), paddle.to_tensor(gamma),
+                         paddle.to_tensor(beta), training=True)
+        out['y'], out['z'] = y._t, z._t
+        out['p'] = F.max_pool2d(z, 3, 2, 1)._t
+
+    assert _miopen_kernels(run) == []
+    y, z, pool = out['y'], out['z'], out['p']
+    assert y.shape == (4, 64, 20, 20) and y.is_contiguous(memory_format=torch.channels_last)
+    yr = torch.nn.functional.conv2d(x.float(), w.float(), None, 1, 1)
+    _close(y, yr, 3e-2, 1e-2, 'nchw conv')
+    zr = torch.nn.functional.batch_norm(yr, None, None, gamma, beta, True, 0.1, 1e-5)
+    _close(z, zr, 5e-2, 2e-2, 'nchw bn')
+    _close(pool, torch.nn.functional.max_pool2d(z.float(), 3, 2, 1), 1e-6, 0, 'nchw pool')
+
+
+def test_nchw_depthwise_routed():
+    F = paddle.nn.functional
+    x = torch.randn(2, 64, 16, 16, device=DEV).bfloat16()
+    w = (0.3 * torch.randn(64, 1, 3, 3, device=DEV)).bfloat16()
+    out = {}
+
+    def run():
+        out['y'] = F.conv2d(paddle.to_tensor(x), paddle.to_tensor(w), stride=2, padding=1, groups=64)._t
+
+    assert _miopen_kernels(run) == []
+    ref = torch.nn.functional.conv2d(x.float(), w.float(), None, 2, 1, groups=64)
+    _close(out['y'], ref, 3e-2, 1e-2, 'nchw dw')
+
+
+def test_resnet50_nchw_default_no_miopen():
+    """paddle.vision.models.resnet50() with its default data_format='NCHW', AMP-O2 bf16 training
+    step: no MIOpen kernel in forward + backward, and the loss equals the NHWC model's with the
+    same weights (same kernels, only the layout bookkeeping differs)."""
+    from paddle.vision.models import resnet50
+    losses = {}
+    for df in ('NCHW', 'NHWC'):
+        paddle.seed(7)
+        net = resnet50(num_classes=10, data_format=df)
+        opt = paddle.optimizer.Momentum(learning_rate=0.01, momentum=0.9, parameters=net.parameters(),
+                                        multi_precision=True)
+        net, opt = paddle.amp.decorate(net, opt, level='O2', dtype='bfloat16')
+        g = torch.Generator(device=DEV).manual_seed(3)
+        img = torch.randn(4, 3, 64, 64, device=DEV, generator=g).bfloat16()
+        lab = torch.randint(0, 10, (4,), device=DEV, generator=g)
+        xin = paddle.to_tensor(img if df == 'NCHW' else img.permute(0, 2, 3, 1).contiguous())
+        y = paddle.to_tensor(lab)
+        vals = []
+
+        def step():
+            loss = paddle.nn.functional.cross_entropy(net(xin), y)
+            loss.backward()
+            opt.step()
+            opt.clear_grad()
+            vals.append(float(loss))
+
+        step()  # warm-up (first-call packing / plans)
+        if df == 'NCHW':
+            bad = _miopen_kernels(step)
+            assert bad == [], bad
+        else:
+            step()
+        losses[df] = vals
+    assert all(v == v for v in losses['NCHW'])
+    for a, b in zip(losses['NCHW'], losses['NHWC']):
+        assert abs(a - b) <= 2e-2 * abs(b) + 1e-3, losses

@@ -53,8 +53,10 @@ def main():
 
 
 def run():
-    for (B, S, H, D, causal) in [(16, 1024, 16, 128, True), (4, 4096, 16, 128, True), (16, 1024, 16, 128, False),
-                                 (8, 2048, 32, 64, True)]:
+    shapes = [(16, 1024, 16, 128, True), (4, 4096, 16, 128, True), (16, 1024, 16, 128, False), (8, 2048, 32, 64, True)]
+    if os.environ.get('FA_SHAPES') == 'wide':  # native head_dim 96 / 256 (csrc/flash_attn_wide.hip)
+        shapes = [(8, 2048, 16, 96, True), (8, 2048, 16, 96, False), (4, 2048, 8, 256, True), (4, 2048, 8, 256, False)]
+    for (B, S, H, D, causal) in shapes:
         qkv = torch.randn(B, S, 3, H, D, device='cuda', dtype=torch.bfloat16, requires_grad=True)
         flops = 4 * B * H * S * S * D * (0.5 if causal else 1.0)
         o = ops.flash_attn.flash_attention_packed(qkv, causal)
