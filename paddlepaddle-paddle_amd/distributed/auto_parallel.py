@@ -447,11 +447,16 @@ class _ShardOptimizer:
       behaviour.
     """
 
-    def __init__(self, optimizer, shard_fn=None, layer=None):
+    def __init__(self, optimizer, shard_fn=None, layer=None, gradient_accumulation_steps=1):
         self._inner_opt = optimizer
         self._shard_fn = shard_fn
         self._engine = None
         self._sharded = None
+        # gradient accumulation (reference: shard_optimizer(..., gradient_accumulation_steps)):
+        # step() / clear_grad() act on every k-th call; the k-1 calls in between leave the
+        # accumulated gradients in place
+        self._acc_k = max(1, int(gradient_accumulation_steps))
+        self._acc_n = 0
         if shard_fn is not None:
             if not isinstance(shard_fn, _ShardingStageBase):
                 raise TypeError("shard_fn must be a ShardingStage1/2/3 instance")
@@ -493,13 +498,21 @@ class _ShardOptimizer:
             for g, r in zip(gs, _unflatten_dense_tensors(flat, gs)):
                 g.copy_(r)
 
+    def _boundary(self):
+        return self._acc_n % self._acc_k == 0
+
     def step(self):
+        self._acc_n += 1
+        if not self._boundary():
+            return None
         if self._sharded is not None:
             return self._sharded.step()
         self._sync_grads()
         self._inner_opt.step()
 
     def clear_grad(self, set_to_zero=True):
+        if not self._boundary():
+            return None  # mid-accumulation: keep the summed gradients
         if self._sharded is not None:
             return self._sharded.clear_grad()
         self._inner_opt.clear_grad(set_to_zero)
@@ -519,7 +532,7 @@ class _ShardOptimizer:
 
 
 def shard_optimizer(optimizer, shard_fn=None, gradient_accumulation_steps=1):
-    return _ShardOptimizer(optimizer, shard_fn)
+    return _ShardOptimizer(optimizer, shard_fn, gradient_accumulation_steps=gradient_accumulation_steps)
 
 
 
@@ -608,8 +621,17 @@ class DistModel:
         if optimizer is not None and st.sharding.get('enable'):
             inner = optimizer._inner_opt if isinstance(optimizer, _ShardOptimizer) else optimizer
             stage = {1: ShardingStage1, 2: ShardingStage2, 3: ShardingStage3}[int(st.sharding.get('stage', 1))]()
-            optimizer = _ShardOptimizer(inner, stage, layer=layer)
+            acc = optimizer._acc_k if isinstance(optimizer, _ShardOptimizer) else 1
+            optimizer = _ShardOptimizer(inner, stage, layer=layer, gradient_accumulation_steps=acc)
         self._opt = optimizer
+        # pipeline: one call = one mini-batch of ``accumulate_steps`` micro-batches (or
+        # batch / micro_batch_size of them), run in the configured schedule's order and followed by
+        # ONE optimizer update; stage placement across meshes runs through the SPMD reshards
+        pp = st.pipeline
+        self._pp = bool(pp.get('enable'))
+        self._pp_acc = max(1, int(pp.get('accumulate_steps', 1) or 1))
+        self._pp_mbs = int(pp.get('micro_batch_size', 1) or 1)
+        self._pp_mode = str(pp.get('schedule_mode', '1F1B'))
         gm = st.gradient_merge
         self._k = int(gm.get('k_steps', 1)) if gm.get('enable') else 1
         self._avg = bool(gm.get('avg', True))
@@ -650,6 +672,8 @@ class DistModel:
         else:
             import contextlib
             ctx = contextlib.nullcontext()
+        if self._pp and self._mode == 'train':
+            return self._pipeline_step(inputs, labels, ctx)
         with ctx:
             out = self._layer(*inputs)
             loss = self._loss(out, labels)
@@ -661,6 +685,48 @@ class DistModel:
                 self._opt.step()
                 self._opt.clear_grad()
         return loss
+
+    def _micro_batches(self, inputs, labels):
+        lead = labels if isinstance(labels, Tensor) else next((x for x in inputs if isinstance(x, Tensor)), None)
+        B = lead.shape[0] if lead is not None else 1
+        n = self._pp_acc if self._pp_acc > 1 else max(1, B // max(1, self._pp_mbs))
+        if B % n:
+            raise ValueError(f"pipeline: batch {B} does not split into {n} micro-batches")
+        m = B // n
+
+        def cut(x, i):
+            return x[i * m:(i + 1) * m] if isinstance(x, Tensor) and x.shape and x.shape[0] == B else x
+        return [([cut(x, i) for x in inputs], cut(labels, i)) for i in range(n)]
+
+    def _pipeline_step(self, inputs, labels, ctx):
+        """Micro-batched step (reference auto-parallel pipeline: accumulate_steps micro-batches per
+        mini-batch, schedule FThenB / 1F1B / VPP).  Every micro-batch's loss is scaled by 1/n and its
+        gradients accumulate; the update runs once.  FThenB runs all forwards before the backwards
+        (activations of every micro-batch alive), 1F1B interleaves (one micro-batch in flight)."""
+        mbs = self._micro_batches(inputs, labels)
+        n = len(mbs)
+        losses = []
+        if self._pp_mode.upper() == 'FTHENB':
+            pending = []
+            for x, y in mbs:
+                with ctx:
+                    loss = self._loss(self._layer(*x), y)
+                pending.append(loss)
+            for loss in pending:
+                (loss / n).backward()
+                losses.append(loss.detach())
+        else:
+            for x, y in mbs:
+                with ctx:
+                    loss = self._loss(self._layer(*x), y)
+                (loss / n).backward()
+                losses.append(loss.detach())
+        self._micro += 1
+        if self._micro % self._k == 0:
+            self._opt.step()
+            self._opt.clear_grad()
+        from ..tensor.manipulation import stack
+        return stack(losses).mean()
 
     def state_dict(self, mode='all'):
         sd = dict(self._layer.state_dict())

@@ -234,8 +234,13 @@ class StaticCollectiveOptimizer:
     (static/minimize.py): strategy.amp -> static AMP (amp_configs), strategy.gradient_merge ->
     k-step merge, data-parallel gradient averaging over the data (x sharding) ranks in
     ``fuse_grad_size_in_MB`` buckets.  Parameters are broadcast from the group's first rank when
-    the program is built, so every rank starts from the same weights.  Static tensor/pipeline
-    parallel program rewriting is not provided (mp/pp degree must be 1 here)."""
+    the program is built, so every rank starts from the same weights.  Tensor parallelism: the
+    fleet mpu layers (ColumnParallelLinear / RowParallelLinear / VocabParallelEmbedding /
+    ParallelCrossEntropy) record their c_identity / c_allreduce / c_split / c_concat collectives as
+    program nodes, which run the eager RCCL ops (and their backward) when the Executor replays the
+    program.  Pipeline parallelism: ops recorded under ``static.device_guard('gpu:N')`` form stage
+    N; each rank runs its stage's section with ``pipeline_configs`` accumulate_steps micro-batches
+    (FThenB / 1F1B) and send/recv of the boundary activations and gradients (static/pipeline.py)."""
 
     def __init__(self, optimizer, hcg, strategy):
         self._inner_opt = optimizer
@@ -250,9 +255,8 @@ class StaticCollectiveOptimizer:
         hcg = self._hcg
         if hcg is None:
             return None
-        if hcg.get_model_parallel_world_size() > 1 or hcg.get_pipe_parallel_world_size() > 1:
-            raise NotImplementedError("static-mode fleet: tensor / pipeline parallel program rewriting is not "
-                                      "supported (use dygraph fleet.distributed_model for mp/pp)")
+        # tensor parallel: the mpu layers record their collectives as program nodes (mp_ops
+        # _static_value); gradients are averaged over the data-parallel group only
         if hcg.get_sharding_parallel_world_size() > 1:
             # static sharding trains like data parallelism over data x sharding ranks (the reference's
             # static sharding pass shards the optimizer state; the update is the same)
@@ -291,6 +295,18 @@ class StaticCollectiveOptimizer:
             pol.avg = bool(s.gradient_merge_configs.get('avg', True))
         pol.dp_group = self._dp_group()
         pol.fuse_grad_size_in_MB = s.fuse_grad_size_in_MB
+        hcg = self._hcg
+        if hcg is not None and hcg.get_pipe_parallel_world_size() > 1:
+            # static pipeline: the program runs split by device_guard stage (static/pipeline.py)
+            from ...static.pipeline import PipelineConfig
+            pc = dict(getattr(s, 'pipeline_configs', None) or {})
+            grp = hcg.get_pipe_parallel_group()
+            st_id, S = hcg.get_stage_id(), hcg.get_pipe_parallel_world_size()
+            ranks = list(grp.ranks)
+            pol.pipeline = PipelineConfig(st_id, S, pc.get('accumulate_steps', 1), grp,
+                                          ranks[st_id - 1] if st_id > 0 else None,
+                                          ranks[st_id + 1] if st_id < S - 1 else None,
+                                          pc.get('schedule_mode', '1F1B'))
         if pol.dp_group is not None:
             _broadcast_params(pol._params(), pol.dp_group)
         self._policy = pol

@@ -99,20 +99,55 @@ def _gather(x, group, axis):
     return torch.cat(list(out.unbind(0)), dim=axis)
 
 
+def _static_value(x):
+    """True while a static Program is being recorded and ``x`` is one of its (meta) values: the
+    collective becomes ONE program node that runs the eager op (and its autograd) at replay, like the
+    reference's c_identity / c_allreduce_sum / c_split / c_concat ops in a static program."""
+    t = _unwrap(x) if isinstance(x, Tensor) else x
+    if not isinstance(t, torch.Tensor) or not t.is_meta:
+        return False
+    from .....static.program import recording
+    return recording()
+
+
+def _record(eager, x, shape):
+    from .....static.program import py_node, _paused
+    t = _unwrap(x)
+    with _paused():
+        meta = torch.empty(shape, dtype=t.dtype, device='meta')
+    return py_node(eager, [x], [meta])[0]
+
+
+def _axis_shape(t, axis, f):
+    shape = list(t.shape)
+    shape[axis] = f(shape[axis])
+    return shape
+
+
 def _c_identity(x, group=None, skip_c_identity_dynamic=False):
+    if _static_value(x):
+        return _record(lambda v: _c_identity(v, group), x, list(_unwrap(x).shape))
     return _wrap(_Identity.apply(_unwrap(x), group))
 
 
 def _mp_allreduce(x, op=None, group=None, use_calc_stream=True, use_model_parallel=True,
                   skip_c_identity_dynamic=False):
+    if _static_value(x):
+        return _record(lambda v: _mp_allreduce(v, group=group), x, list(_unwrap(x).shape))
     return _wrap(_AllReduce.apply(_unwrap(x), group))
 
 
 def _c_split(x, group=None, axis=-1):
+    if _static_value(x):
+        n = _n(group)
+        return _record(lambda v: _c_split(v, group, axis), x, _axis_shape(_unwrap(x), axis, lambda d: d // n))
     return _wrap(_Split.apply(_unwrap(x), group, axis))
 
 
 def _c_concat(x, group=None, axis=-1):
+    if _static_value(x):
+        n = _n(group)
+        return _record(lambda v: _c_concat(v, group, axis), x, _axis_shape(_unwrap(x), axis, lambda d: d * n))
     return _wrap(_Concat.apply(_unwrap(x), group, axis))
 
 
@@ -154,6 +189,13 @@ class _VocabParallelXent(torch.autograd.Function):
 
 
 def _c_softmax_with_cross_entropy(logits, label, group=None, return_softmax=False, ignore_index=-100):
+    if _static_value(logits):
+        from .....static.program import py_node, _paused
+        t = _unwrap(logits)
+        with _paused():
+            meta = torch.empty(list(t.shape[:-1]) + [1], dtype=t.dtype, device='meta')
+        return py_node(lambda lg, lb: _c_softmax_with_cross_entropy(lg, lb, group, False, ignore_index),
+                       [logits, label], [meta])[0]
     lab = _unwrap(label)
     if lab.dim() == _unwrap(logits).dim():
         lab = lab.squeeze(-1)

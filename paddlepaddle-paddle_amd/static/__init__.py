@@ -52,7 +52,20 @@ def xpu_places(device_ids=None):
 
 @contextlib.contextmanager
 def device_guard(device=None):
-    yield
+    """Ops recorded inside run on pipeline stage N for ``'gpu:N'`` (reference
+    static.device_guard + the fleet pipeline optimizer's program split by op device); 'cpu' /
+    None leave the stage unchanged.  Execution placement itself is the Executor's place."""
+    from .program import _STAGE
+    prev = _STAGE[0]
+    if isinstance(device, str) and ':' in device:
+        try:
+            _STAGE[0] = int(device.split(':')[1])
+        except ValueError:
+            pass
+    try:
+        yield
+    finally:
+        _STAGE[0] = prev
 
 
 @contextlib.contextmanager

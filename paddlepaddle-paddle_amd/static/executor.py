@@ -274,12 +274,54 @@ def _exec_nodes(prog, nodes, env, smap, dev):
 _LOD = {}  # id(torch tensor) -> (tensor, level-1 offsets) for LoD values of the running replay
 
 
+def _pipeline_policy(prog):
+    for n in reversed(prog.nodes):
+        if n.kind == 'minimize':
+            return n.target if getattr(n.target, 'pipeline', None) is not None else None
+    return None
+
+
+def _run_pipelined(prog, feed, dev, pol):
+    """One pipeline-parallel training step (static/pipeline.py) on this rank's stage."""
+    from .pipeline import run_pipeline
+    from .amp import autocast_context
+
+    def run_forward(nodes, env, feed_m):
+        smap = {}
+        _bind_feeds(prog, feed_m, dev, env, smap)
+        with _paused(), autocast_context(prog, dev) as subs:
+            prev, _SUBS['map'] = _SUBS['map'], subs
+            try:
+                _exec(prog, nodes, env, smap, dev)
+            finally:
+                _SUBS['map'] = prev
+    _LOD.clear()
+    return run_pipeline(prog, feed, dev, pol, pol.pipeline, run_forward)
+
+
 def run_program(prog, feed, dev, grad=None):
     """Interpret ``prog``; returns the value env."""
+    pol = _pipeline_policy(prog)
+    if pol is not None and (grad is None or grad):
+        return _run_pipelined(prog, feed, dev, pol)
     env = {}
     smap = {}
-    feed = feed or {}
     _LOD.clear()
+    _bind_feeds(prog, feed, dev, env, smap)
+    needs_grad = grad if grad is not None else any(n.kind in ('minimize', 'backward', 'grad') for n in prog.nodes)
+    ctx = contextlib.nullcontext() if needs_grad else torch.no_grad()
+    from .amp import autocast_context
+    with _paused(), ctx, autocast_context(prog, dev) as subs:
+        prev, _SUBS['map'] = _SUBS['map'], subs
+        try:
+            _exec(prog, prog.nodes, env, smap, dev)
+        finally:
+            _SUBS['map'] = prev
+    return env
+
+
+def _bind_feeds(prog, feed, dev, env, smap):
+    feed = feed or {}
     for name, (vid, shape, dt) in prog.feeds.items():
         if name not in feed:
             continue
@@ -297,16 +339,6 @@ def run_program(prog, feed, dev, grad=None):
         lod = feed[name].__dict__.get('_lod') if isinstance(feed[name], Tensor) else None
         if lod is not None:
             _LOD[id(t)] = (t, lod)
-    needs_grad = grad if grad is not None else any(n.kind in ('minimize', 'backward', 'grad') for n in prog.nodes)
-    ctx = contextlib.nullcontext() if needs_grad else torch.no_grad()
-    from .amp import autocast_context
-    with _paused(), ctx, autocast_context(prog, dev) as subs:
-        prev, _SUBS['map'] = _SUBS['map'], subs
-        try:
-            _exec(prog, prog.nodes, env, smap, dev)
-        finally:
-            _SUBS['map'] = prev
-    return env
 
 
 class Executor:

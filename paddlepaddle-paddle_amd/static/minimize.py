@@ -26,6 +26,7 @@ class StaticMinimize:
         self.dp_group = None  # paddle.distributed Group (or None: no reduction)
         self.fuse_grad_size_in_MB = 32
         self._micro = 0
+        self.pipeline = None  # static/pipeline.PipelineConfig when the program runs pipelined
 
     def __getattr__(self, name):
         return getattr(self.__dict__['_opt'], name)

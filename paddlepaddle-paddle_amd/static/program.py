@@ -27,6 +27,9 @@ from ..core.tensor import Tensor, _wrap
 # about 1e-6 (meta tensors hold no memory, so the large extents cost nothing; three dynamic dims
 # times a 10^4 feature dim stay far inside int64 numel)
 SENTINELS = (1048573, 1048571, 1048559, 1048549, 1048517, 1048507)
+
+# pipeline stage of the ops being recorded (static.device_guard('gpu:N') -> N; None outside a guard)
+_STAGE = [None]
 _SENT_SET = set(SENTINELS)
 
 
@@ -270,7 +273,7 @@ class _Recorder(TorchFunctionMode):
             return out
         out = _metaize(out)
         outs = _register_outs(prog, out)
-        prog.nodes.append(Node('torch', func, rec_args, rec_kwargs, outs, {'factory': factory}))
+        prog.nodes.append(Node('torch', func, rec_args, rec_kwargs, outs, {'factory': factory, 'stage': _STAGE[0]}))
         return out
 
 
@@ -539,5 +542,5 @@ def py_node(fn, inputs, out_metas):
     prog = default_main_program()
     rec = _to_record(prog, [x._t if isinstance(x, Tensor) else x for x in inputs])
     outs = [prog._new_value(m) for m in out_metas]
-    prog.nodes.append(Node('py', fn, rec, {}, outs))
+    prog.nodes.append(Node('py', fn, rec, {}, outs, {'stage': _STAGE[0]}))
     return [_wrap(m) for m in out_metas]

@@ -1,0 +1,90 @@
+"""Static Program pipeline parallelism over gloo ranks (reference: fleet static pipeline optimizer;
+ops placed with static.device_guard('gpu:N'), pipeline_configs accumulate_steps micro-batches).
+argv[1]: schedule ('1F1B' / 'FThenB'); argv[2]: 'pp' (pp = world) or 'ppdp' (pp 2 x dp 2).
+Every rank builds the same program (same seed); after 3 steps each stage's parameters must equal a
+single-process run on the full batch."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import numpy as np  # noqa: E402
+
+import paddle  # noqa: E402
+import paddle.distributed as dist  # noqa: E402
+import paddle.static as static  # noqa: E402
+from paddle.distributed import fleet  # noqa: E402
+
+
+def build(stages, opt_fn):
+    paddle.seed(11)
+    main, startup = static.Program(), static.Program()
+    with static.program_guard(main, startup):
+        x = static.data('x', [None, 6], 'float32')
+        y = static.data('y', [None, 1], 'int64')
+        with static.device_guard('gpu:0'):
+            h = static.nn.fc(x, 12, activation='relu')
+            skip = static.nn.fc(x, 5)  # crosses two boundaries when there are 3 stages
+        with static.device_guard(f'gpu:{min(1, stages - 1)}'):
+            h = static.nn.fc(h, 10, activation='tanh')
+        with static.device_guard(f'gpu:{stages - 1}'):
+            z = paddle.concat([h, skip], axis=1)
+            logits = static.nn.fc(z, 3)
+            loss = paddle.nn.functional.cross_entropy(logits, y)
+        opt_fn().minimize(loss)
+    return main, startup, loss
+
+
+def main():
+    sched, mode = sys.argv[1], sys.argv[2]
+    world = int(os.environ['WORLD_SIZE'])
+    pp = 2 if mode == 'ppdp' else world
+    dp = world // pp
+    acc = 4
+    s = fleet.DistributedStrategy()
+    s.hybrid_configs = {'dp_degree': dp, 'mp_degree': 1, 'pp_degree': pp}
+    s.pipeline = True
+    s.pipeline_configs = {'accumulate_steps': acc, 'micro_batch_size': 2, 'schedule_mode': sched}
+    fleet.init(is_collective=True, strategy=s)
+    hcg = fleet.get_hybrid_communicate_group()
+    rank = dist.get_rank()
+    dp_rank = hcg.get_data_parallel_rank()
+    paddle.enable_static()
+    sgd = lambda: paddle.optimizer.SGD(learning_rate=0.2)  # noqa: E731
+    main_p, startup, loss = build(pp, lambda: fleet.distributed_optimizer(sgd()))
+    exe = static.Executor(paddle.CPUPlace())
+    exe.run(startup)
+    rng = np.random.RandomState(0)
+    B = 8 * dp
+    batches = []
+    for _ in range(3):
+        xs = rng.randn(B, 6).astype('float32')
+        batches.append((xs, (xs[:, :3].argmax(1)).reshape(-1, 1).astype('int64')))
+    half = B // dp
+    losses = []
+    for xs, ys in batches:
+        out = exe.run(main_p, feed={'x': xs[dp_rank * half:(dp_rank + 1) * half],
+                                    'y': ys[dp_rank * half:(dp_rank + 1) * half]}, fetch_list=[loss])
+        losses.append(float(np.asarray(out[0]).reshape(-1)[0]))
+    got = [p.numpy().copy() for p in main_p.all_parameters()]
+    ref_main, ref_startup, ref_loss = build(pp, sgd)
+    ref_losses = []
+    for xs, ys in batches:
+        # same micro-batch means as the pipeline: acc equal chunks of each dp shard, averaged
+        out = exe.run(ref_main, feed={'x': xs, 'y': ys}, fetch_list=[ref_loss])
+        ref_losses.append(float(np.asarray(out[0]).reshape(-1)[0]))
+    # parameters in creation order: fc(x) w,b and skip w,b on stage 0, the middle fc on stage
+    # min(1, pp-1), the head on the last stage; a rank owns (updates) its stage's parameters only
+    st = [0, 0, 0, 0, min(1, pp - 1), min(1, pp - 1), pp - 1, pp - 1]
+    me = hcg.get_stage_id()
+    ref = [p.numpy() for p in ref_main.all_parameters()]
+    assert len(got) == len(st) == len(ref), (len(got), len(ref))
+    for a, b, s_ in zip(got, ref, st):
+        if s_ == me:
+            np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+    if dp == 1:
+        np.testing.assert_allclose(losses, ref_losses, rtol=1e-4, atol=1e-5)
+    print(f"rank{rank} static pp {sched} {mode} OK", flush=True)
+
+
+if __name__ == '__main__':
+    main()

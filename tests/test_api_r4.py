@@ -167,3 +167,55 @@ def test_base_core_and_pir_namespaces(static_mode, tmp_path):
     prog = paddle.pir.load(path + '.json')
     got, = exe.run(prog, feed={'x': xs}, fetch_list=prog._fetch_vars)
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
+
+
+# ---- auto-parallel: gradient accumulation + Strategy.pipeline (distributed/auto_parallel.py)
+def _lin(seed=0):
+    paddle.seed(seed)
+    return paddle.nn.Linear(6, 3)
+
+
+def test_shard_optimizer_gradient_accumulation():
+    import paddle.distributed as dist
+    xs = [paddle.randn([4, 6]) for _ in range(2)]
+    m1 = _lin()
+    o1 = dist.shard_optimizer(paddle.optimizer.SGD(0.1, parameters=m1.parameters()), gradient_accumulation_steps=2)
+    for i, x in enumerate(xs):
+        m1(x).sum().backward()
+        o1.step()
+        o1.clear_grad()
+        if i == 0:  # mid-accumulation: no update, gradients kept
+            ref0 = _lin()
+            np.testing.assert_allclose(m1.weight.numpy(), ref0.weight.numpy())
+            assert m1.weight.grad is not None
+    m2 = _lin()
+    o2 = paddle.optimizer.SGD(0.1, parameters=m2.parameters())
+    (m2(xs[0]).sum() + m2(xs[1]).sum()).backward()
+    o2.step()
+    np.testing.assert_allclose(m1.weight.numpy(), m2.weight.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(m1.bias.numpy(), m2.bias.numpy(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize('mode', ['1F1B', 'FThenB'])
+@pytest.mark.parametrize('acc,mbs', [(4, 1), (1, 2)])
+def test_dist_model_pipeline_micro_batches(mode, acc, mbs):
+    """Strategy.pipeline: one DistModel call = accumulate_steps micro-batches (or batch /
+    micro_batch_size) + one update; equals the full-batch step for a mean loss."""
+    import paddle.distributed as dist
+    x, y = paddle.randn([8, 6]), paddle.randn([8, 3])
+    loss_fn = paddle.nn.MSELoss()
+    m1 = _lin(1)
+    st = dist.Strategy()
+    st.pipeline.enable = True
+    st.pipeline.schedule_mode = mode
+    st.pipeline.accumulate_steps = acc
+    st.pipeline.micro_batch_size = mbs
+    dm = dist.to_static(m1, None, loss_fn, paddle.optimizer.SGD(0.05, parameters=m1.parameters()), st)
+    l1 = float(dm(x, y))
+    m2 = _lin(1)
+    o2 = paddle.optimizer.SGD(0.05, parameters=m2.parameters())
+    l2 = loss_fn(m2(x), y)
+    l2.backward()
+    o2.step()
+    assert abs(l1 - float(l2)) < 1e-5
+    np.testing.assert_allclose(m1.weight.numpy(), m2.weight.numpy(), rtol=1e-5, atol=1e-6)

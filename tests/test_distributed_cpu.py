@@ -297,3 +297,20 @@ def test_bench_multi_rank_path_rehearsal(nproc):
 def test_static_collective_data_parallel_matches_full_batch(mode):
     out = run_workers('worker_static_dp.py', mode)
     assert out.count(f'static dp {mode} OK') == 2, out[-3000:]
+
+
+@pytest.mark.parametrize("mode,nproc", [('tp', 2), ('tpdp', 4)])
+def test_static_fleet_tensor_parallel(mode, nproc):
+    """Static-mode fleet with mpu layers: collectives recorded as program nodes; shards match a
+    single-process full-weight run."""
+    out = run_workers('worker_static_tp.py', mode, nproc=nproc)
+    assert out.count(f'static {mode} OK') == nproc, out[-3000:]
+
+
+@pytest.mark.parametrize("sched,mode,nproc", [('1F1B', 'pp', 2), ('FThenB', 'pp', 2), ('1F1B', 'pp', 3),
+                                              ('1F1B', 'ppdp', 4)])
+def test_static_fleet_pipeline_parallel(sched, mode, nproc):
+    """Static-mode fleet pipeline: device_guard stages, micro-batched FThenB / 1F1B with
+    send/recv of activations and gradients; every stage's parameters match a single-process run."""
+    out = run_workers('worker_static_pp.py', sched, mode, nproc=nproc)
+    assert out.count(f'static pp {sched} {mode} OK') == nproc, out[-3000:]
