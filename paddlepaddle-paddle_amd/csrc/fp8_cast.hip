@@ -140,6 +140,91 @@ __global__ __launch_bounds__(256) void cast_transpose_kernel(const bf16_t* __res
   }
 }
 
+// Full-tile variant (R, C multiples of 128): every global access a wave makes is contiguous.
+//  * row pass: chunk k = tid + 256 i (i < 8) of the tile = 16 B of bf16 at row k / 16, column
+//    8 (k % 16): one load instruction covers 4 rows x 256 B; its 8 fp8 bytes go to q (4 rows x
+//    128 B per store instruction) and, as two dwords, to the LDS tile (pitch 132 B: the 32 lanes
+//    of a ds_write_b32 half touch 2 rows x 16 chunks on distinct banks);
+//  * column pass: lane (rg = lane / 8, cg = lane % 8) of wave w reads 16 rows x 4 bytes
+//    (ds_read_b32, rows 16 rg .. +15, columns 4 (8 w + cg) .. +3 — conflict free: bank =
+//    16 rg + cg + const within each 32-lane half), transposes the 16 x 4 bytes in registers and
+//    stores four 16-B q^T chunks; 8 lanes cover one 128-B q^T row segment per store instruction.
+// The old kernel's 2-lanes-per-row mapping gave 64 scattered 16-B segments per load / store
+// instruction (2.3 TB/s on [16384, 2048]).
+constexpr int P2 = T + 4;
+
+template <int FMT>
+__global__ __launch_bounds__(256) void cast_transpose_full_kernel(const bf16_t* __restrict__ x, int R, int C,
+                                                                  long long ldx, uint8_t* __restrict__ q,
+                                                                  uint8_t* __restrict__ qt, float* __restrict__ hist,
+                                                                  int L, int cur, float* __restrict__ scale_inv,
+                                                                  float margin_mul) {
+  __shared__ __attribute__((aligned(16))) uint8_t tile[T * P2];
+  __shared__ float red[4];
+  const float fmax = fmax_of<FMT>();
+  const float s = scale_from_hist(hist, L, cur, fmax, margin_mul);
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.y * T, c0 = blockIdx.x * T;
+  float am = 0.f;
+  float v[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {  // all eight 16-B loads in flight before any use
+    const int k = tid + 256 * i, row = k >> 4, ch = k & 15;
+    load_f<bf16_t, 8>(x + (long long)(r0 + row) * ldx + c0 + 8 * ch, v[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int k = tid + 256 * i, row = k >> 4, ch = k & 15;
+    uint32_t w[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      am = fmaxf(am, fmaxf(fmaxf(fabsf(v[i][4 * j]), fabsf(v[i][4 * j + 1])),
+                           fmaxf(fabsf(v[i][4 * j + 2]), fabsf(v[i][4 * j + 3]))));
+      w[j] = cvt2<FMT>(v[i][4 * j] * s, v[i][4 * j + 1] * s) | (cvt2<FMT>(v[i][4 * j + 2] * s, v[i][4 * j + 3] * s) << 16);
+    }
+    if (q) *reinterpret_cast<uint2*>(q + (long long)(r0 + row) * C + c0 + 8 * ch) = make_uint2(w[0], w[1]);
+    if (qt) {
+      uint32_t* t32 = reinterpret_cast<uint32_t*>(tile + row * P2 + 8 * ch);
+      t32[0] = w[0];
+      t32[1] = w[1];
+    }
+  }
+  if (qt) {
+    __syncthreads();
+    const int lane = tid & 63, wave = tid >> 6;
+    const int rg = lane >> 3, cgl = lane & 7;
+    {  // 4 waves x 8 column groups of 4 = the tile's 128 columns; 8 row groups of 16 = its 128 rows
+      const int cg = wave * 8 + cgl;  // column group: input columns 4 cg .. 4 cg + 3
+      uint32_t rw[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) rw[i] = *reinterpret_cast<const uint32_t*>(tile + (16 * rg + i) * P2 + 4 * cg);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // q^T row (input column) c0 + 4 cg + j, bytes of rows 16 rg ..
+        uint32_t o[4];
+#pragma unroll
+        for (int kq = 0; kq < 4; ++kq) {
+          const uint32_t a = (rw[4 * kq] >> (8 * j)) & 0xFFu, b = (rw[4 * kq + 1] >> (8 * j)) & 0xFFu;
+          const uint32_t c = (rw[4 * kq + 2] >> (8 * j)) & 0xFFu, d = (rw[4 * kq + 3] >> (8 * j)) & 0xFFu;
+          o[kq] = a | (b << 8) | (c << 16) | (d << 24);
+        }
+        *reinterpret_cast<uint4*>(qt + (long long)(c0 + 4 * cg + j) * R + r0 + 16 * rg) =
+            make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    }
+  }
+  am = wave_max(am);
+  if ((tid & 63) == 0) red[tid >> 6] = am;
+  __syncthreads();
+  if (tid == 0) {
+    const float b = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomic_max_pos(hist + cur, b);
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+      hist[(cur + 1) % L] = 0.f;
+      scale_inv[0] = 1.f / s;
+    }
+  }
+}
+
 // amax of a bf16 [R, C] tensor folded into *out (first use of a tensor: seeds the history)
 __global__ __launch_bounds__(256) void amax_kernel(const bf16_t* __restrict__ x, int R, int C, long long ldx,
                                                    float* __restrict__ out) {
@@ -164,6 +249,13 @@ __global__ __launch_bounds__(256) void amax_kernel(const bf16_t* __restrict__ x,
 
 using namespace pa;
 
+static int g_cast_full = 1;  // A/B switch: full-tile kernel for 128-multiple shapes
+PA_API int pa_fp8_set_cast_full(int v) {
+  const int old = g_cast_full;
+  g_cast_full = v;
+  return old;
+}
+
 // x: bf16 [R, C] (row stride ldx, 16-B aligned rows), q: [R, C] fp8 or null, qt: [C, R] fp8 or null.
 // fmt 0 = e4m3fn, 1 = e5m2.  C % 8 == 0.
 PA_API int pa_fp8_cast_transpose(const void* x, int R, int C, long long ldx, void* q, void* qt, void* hist, int L,
@@ -172,6 +264,15 @@ PA_API int pa_fp8_cast_transpose(const void* x, int R, int C, long long ldx, voi
     return (int)hipErrorInvalidValue;
   dim3 grid((C + f8::T - 1) / f8::T, (R + f8::T - 1) / f8::T);
   if (grid.y > 65535) return (int)hipErrorInvalidValue;
+  if (R % f8::T == 0 && C % f8::T == 0 && ldx % 8 == 0 && g_cast_full) {
+    if (fmt == 0)
+      f8::cast_transpose_full_kernel<0><<<grid, 256, 0, st>>>((const bf16_t*)x, R, C, ldx, (uint8_t*)q, (uint8_t*)qt,
+                                                                (float*)hist, L, cur, (float*)scale_inv, margin_mul);
+    else
+      f8::cast_transpose_full_kernel<1><<<grid, 256, 0, st>>>((const bf16_t*)x, R, C, ldx, (uint8_t*)q, (uint8_t*)qt,
+                                                                (float*)hist, L, cur, (float*)scale_inv, margin_mul);
+    return (int)hipGetLastError();
+  }
   if (fmt == 0)
     f8::cast_transpose_kernel<0><<<grid, 256, 0, st>>>((const bf16_t*)x, R, C, ldx, (uint8_t*)q, (uint8_t*)qt,
                                                          (float*)hist, L, cur, (float*)scale_inv, margin_mul);

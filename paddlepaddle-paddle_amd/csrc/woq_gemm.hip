@@ -245,11 +245,14 @@ __global__ __launch_bounds__(256) void woq_finish(const float* __restrict__ part
   store_f<T, 8>(reinterpret_cast<T*>(Y + (long long)m * ldy + n), v);
 }
 
-// K splits: ~2 blocks per CU over the 128-column tiles; each split a multiple of 4 waves x chunk
+// tuning knobs (pa_woq_tune): target blocks of the K-split plan, register stages of the M <= 16 kernel
+static int g_target_blocks = 512, g_nst = 3;
+
+// K splits: ~g_target_blocks blocks over the 128-column tiles; each split a multiple of 4 waves x chunk
 static void plan(int N, int K, int bits, int& KS, int& kchunk) {
   const int unit = 4 * (bits == 8 ? 64 : 128);
   const int tiles = (N + 127) / 128;
-  int ks = (512 + tiles - 1) / tiles;
+  int ks = (g_target_blocks + tiles - 1) / tiles;
   const int kmax = (K + unit - 1) / unit;
   ks = ks < 1 ? 1 : (ks > kmax ? kmax : ks);
   kchunk = ((K + ks - 1) / ks + unit - 1) / unit * unit;
@@ -263,7 +266,11 @@ static void launch(const void* X, long long ldx, const void* Wq, long long ldwb,
   const uint16_t* x = (const uint16_t*)X;
   const uint8_t* w = (const uint8_t*)Wq;
   // (a 4-row-tile variant for M <= 64 spills at 256 VGPRs: M > 32 takes the dequantise + GEMM path)
-  if (M <= 16)
+  if (M <= 16 && g_nst == 2)
+    woq_kernel<T, BITS, 1, 2, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk);
+  else if (M <= 16 && g_nst == 4)
+    woq_kernel<T, BITS, 1, 4, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk);
+  else if (M <= 16)
     woq_kernel<T, BITS, 1, 3, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk);
   else
     woq_kernel<T, BITS, 2, 2, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk);
@@ -283,6 +290,15 @@ PA_API int pa_woq_ok(int M, int N, int K, long long ldx, long long ldw_bytes, in
   if (group != 0 && group != 64 && group != 128) return 0;
   if (group && K % group) return 0;
   return 1;
+}
+
+// A/B knobs: target block count of the K-split plan (default 512), register stages (2 / 3 / 4) of the
+// M <= 16 kernel (default 3); <= 0 keeps a value.  Returns the previous target.
+PA_API int pa_woq_tune(int target_blocks, int nst) {
+  const int old = pa::woq::g_target_blocks;
+  if (target_blocks > 0) pa::woq::g_target_blocks = target_blocks;
+  if (nst > 0) pa::woq::g_nst = nst;
+  return old;
 }
 
 PA_API long long pa_woq_ws_floats(int M, int N, int K, int bits) {

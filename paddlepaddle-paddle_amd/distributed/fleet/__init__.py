@@ -493,6 +493,7 @@ class UtilBase:
 util = UtilBase()
 Fleet = _Fleet  # the class behind the module-level ``fleet`` singleton (reference fleet/fleet.py)
 from . import data_generator  # noqa: E402,F401
+from . import auto  # noqa: E402,F401
 from .data_generator import MultiSlotDataGenerator, MultiSlotStringDataGenerator  # noqa: E402,F401
 
 

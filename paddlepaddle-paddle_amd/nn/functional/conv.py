@@ -100,6 +100,17 @@ def _conv(x, weight, bias, stride, padding, dilation, groups, data_format, nd, f
 
 @_amp_op('conv2d')
 def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format='NCL', name=None):
+    t, w = _u(x), _u(weight)
+    if ops.use_hip(t) and t.dim() == 3 and w.dim() == 3 and not isinstance(padding, str) and groups == 1:
+        # a 1-D convolution is a 2-D one over a height-1 image: the channels-last HIP kernels
+        cl = data_format[-1] == 'C'
+        xn = (t if cl else t.permute(0, 2, 1)).unsqueeze(1)  # [N, 1, L, C]
+        w4 = w.unsqueeze(2)
+        pd = _ntuple(padding, 1)
+        if len(pd) == 1 and ops.conv.supported(xn, w4, 1):
+            y = ops.conv.conv2d_nhwc(xn.contiguous(), w4, None if bias is None else _u(bias), (1, _ntuple(stride, 1)[0]),
+                                     (0, pd[0]), (1, _ntuple(dilation, 1)[0]))[:, 0]  # [N, Lo, Cout]
+            return _w(y if cl else y.permute(0, 2, 1))
     return _conv(x, weight, bias, stride, padding, dilation, groups, data_format, 1, TF.conv1d)
 
 
@@ -128,6 +139,13 @@ def _conv_t(x, weight, bias, stride, padding, output_padding, dilation, groups, 
     if output_size is not None:
         osz = _ntuple(output_size, nd) if not isinstance(output_size, int) else (output_size,) * nd
         op = tuple(osz[i] - ((t.shape[2 + i] - 1) * s[i] - 2 * p[i] + d[i] * (w.shape[2 + i] - 1) + 1) for i in range(nd))
+    if nd == 2 and ops.use_hip(t):
+        ohw = tuple((t.shape[2 + i] - 1) * s[i] - 2 * p[i] + d[i] * (w.shape[2 + i] - 1) + op[i] + 1 for i in range(2))
+        xn = t.permute(0, 2, 3, 1)
+        if ops.conv.convt_supported(xn, w, groups, s, p, d, ohw):
+            # transposed conv on the stride-class data-gradient kernel (channels-last, NCHW as views)
+            y = ops.conv.conv_transpose2d_nhwc(xn.contiguous(), w, b, s, p, d, ohw)
+            return _w(y if cl else y.permute(0, 3, 1, 2))
     out = fn(t, w, b, s, p, op, groups, d)
     if cl:
         out = out.permute(0, *range(2, nd + 2), 1)

@@ -76,6 +76,8 @@ _SIGS = {
     'pa_gemm_fp8_ok': [I, I, I, LL, LL, LL],
     'pa_fp8_cast_transpose': [P, I, I, LL, P, P, P, I, I, P, I, F, P],
     'pa_fp8_amax': [P, I, I, LL, P, P],
+    'pa_fp8_set_cast_full': [I],
+    'pa_woq_tune': [I, I],
     'pa_gemm_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
     'pa_gemm8_fp8_ok': [I, I, I, LL, LL, LL],
     'pa_gemm8_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],

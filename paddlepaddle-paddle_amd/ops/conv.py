@@ -654,3 +654,55 @@ def dwconv2d_nhwc(x, w, b, stride, pad, dil):
     if N._load() is None:
         raise RuntimeError("dwconv2d_nhwc: HIP kernel library not loaded: " + str(N.load_error))
     return _DWConvNHWC.apply(x, w, b, tuple(stride), tuple(pad), tuple(dil))
+
+
+# ---- transposed convolution (reference gpudnn conv_transpose_kernel.cu) on the same kernels
+# conv_transpose2d(x, w) IS the data gradient of conv2d(., w) evaluated at dY = x: the stride-class
+# data-gradient kernel computes it; its input gradient is the conv2d forward of dOut with w and its
+# filter gradient the conv filter-gradient kernel with the roles of input and output swapped.
+def convt_supported(x, w, groups, stride, pad, dil, out_hw):
+    """x: NHWC view [N, H, W, Cin]; w: [Cin, Cout, R, S] (paddle's transposed-conv layout)."""
+    if not (_enabled and _bwd_enabled) or groups != 1 or x.dim() != 4 or w.dim() != 4 or not x.is_cuda:
+        return False
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or x.shape[3] != w.shape[0]:
+        return False
+    if N.lib is None and N._load() is None:
+        return False
+    Cin, Cout, R, S = w.shape
+    if not bool(N.lib.pa_conv2d_fwd_ok(Cout, Cin, R, S)) or not bool(N.lib.pa_conv2d_wgrad_ok(Cout, Cin)):
+        return False
+    ok = _dgrad_plan((Cin, Cout, R, S), tuple(out_hw), tuple(stride), tuple(pad), tuple(dil), x.device)[0]
+    return bool(ok)
+
+
+class _ConvT2dNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, dil, out_hw):
+        x = x.contiguous()
+        y = conv2d_dgrad_classes(x, w, out_hw, stride, pad, dil)
+        if y is None:
+            raise RuntimeError("conv_transpose2d: geometry rejected by the data-gradient kernel")
+        if b is not None:
+            y = y + b.to(y.dtype)
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, pad, dil, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pad, dil, has_b = ctx.cfg
+        dy = dy.contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:  # conv2d forward of dOut with the same filter
+            gx = conv2d_fwd(dy, w, None, stride, pad, dil)
+        if ctx.needs_input_grad[1]:  # filter gradient of that conv: its input is dOut, its dY is x
+            gw = conv2d_wgrad(x, dy, tuple(w.shape), stride, pad, dil).to(w.dtype)
+        if has_b and ctx.needs_input_grad[2]:
+            gb = dy.sum((0, 1, 2), dtype=torch.float32).to(dy.dtype)
+        return gx, gw, gb, None, None, None, None
+
+
+def conv_transpose2d_nhwc(x, w, b, stride, pad, dil, out_hw):
+    """Transposed conv2d of an NHWC tensor: x [N,H,W,Cin], w [Cin,Cout,R,S] -> [N,Ho,Wo,Cout]."""
+    return _ConvT2dNHWC.apply(x, w, b, tuple(stride), tuple(pad), tuple(dil), tuple(out_hw))

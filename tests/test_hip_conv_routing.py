@@ -89,8 +89,8 @@ def test_nchw_conv_bn_pool_routed():
     outputs are NCHW views with channels-last strides, values match fp32 torch, and the profiler
     sees no library convolution kernels."""
     F = paddle.nn.functional
-    x = torch.randn(4, 32, 20, 20, device=DEV).bfloat16()
-    w = (0.1 * torch.randn(64, 32, 3, 3, device=DEV)).bfloat16()
+    x = torch.randn(4, 64, 20, 20, device=DEV).bfloat16()
+    w = (0.1 * torch.randn(64, 64, 3, 3, device=DEV)).bfloat16()
     gamma = torch.ones(64, device=DEV)
     beta = torch.zeros(64, device=DEV)
     rm, rv = torch.zeros(64, device=DEV), torch.ones(64, device=DEV)
@@ -163,3 +163,55 @@ def test_resnet50_nchw_default_no_miopen():
     assert all(v == v for v in losses['NCHW'])
     for a, b in zip(losses['NCHW'], losses['NHWC']):
         assert abs(a - b) <= 2e-2 * abs(b) + 1e-3, losses
+
+
+@pytest.mark.parametrize('N,Cin,Cout,H,k,s,p,op,cl', [
+    (2, 64, 32, 9, 4, 2, 1, 0, False), (2, 128, 64, 7, 3, 2, 1, 1, False), (1, 64, 64, 12, 3, 1, 1, 0, True),
+    (2, 256, 128, 5, 2, 2, 0, 0, False)])
+def test_conv_transpose2d_routed(N, Cin, Cout, H, k, s, p, op, cl):
+    """conv2d_transpose on the stride-class data-gradient kernel: forward and all three gradients
+    vs fp32 torch, no MIOpen kernels."""
+    F = paddle.nn.functional
+    x = torch.randn(N, Cin, H, H + 1, device=DEV).bfloat16()
+    w = (0.1 * torch.randn(Cin, Cout, k, k, device=DEV)).bfloat16()
+    b = (0.1 * torch.randn(Cout, device=DEV)).bfloat16()
+    xs = x.permute(0, 2, 3, 1).contiguous() if cl else x
+    xp, wp, bp = (paddle.to_tensor(t.clone()) for t in (xs, w, b))
+    for t in (xp, wp, bp):
+        t.stop_gradient = False
+    out = {}
+
+    def run():
+        y = F.conv2d_transpose(xp, wp, bp, stride=s, padding=p, output_padding=op,
+                               data_format='NHWC' if cl else 'NCHW')
+        out['y'] = y
+        (y * y).sum().backward()
+
+    assert _miopen_kernels(run) == []
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.conv_transpose2d(xr, wr, br, s, p, op)
+    (yr * yr).sum().backward()
+    y = out['y']._t
+    _close(y.permute(0, 3, 1, 2) if cl else y, yr, 5e-2, 1e-2, 'convT fwd')
+    gx = xp.grad._t
+    _close(gx.permute(0, 3, 1, 2) if cl else gx, xr.grad, 0.3, 3e-2, 'convT dx')
+    _close(wp.grad._t, wr.grad, 0.5, 3e-2, 'convT dw')
+    _close(bp.grad._t, br.grad, 0.5, 3e-2, 'convT db')
+
+
+@pytest.mark.parametrize('cl', [False, True])
+def test_conv1d_routed(cl):
+    F = paddle.nn.functional
+    x = torch.randn(4, 64, 50, device=DEV).bfloat16()
+    w = (0.1 * torch.randn(128, 64, 3, device=DEV)).bfloat16()
+    xs = x.permute(0, 2, 1).contiguous() if cl else x
+    out = {}
+
+    def run():
+        out['y'] = F.conv1d(paddle.to_tensor(xs), paddle.to_tensor(w), padding=1, stride=2,
+                            data_format='NLC' if cl else 'NCL')._t
+
+    assert _miopen_kernels(run) == []
+    ref = torch.nn.functional.conv1d(x.float(), w.float(), None, 2, 1)
+    y = out['y']
+    _close(y.permute(0, 2, 1) if cl else y, ref, 3e-2, 1e-2, 'conv1d')

@@ -44,5 +44,41 @@ def main():
                   f"int4 {t4*1e6:7.1f} us ({K*N/2/t4/1e12:4.2f} TB/s, {tb/t4:4.2f}x)", flush=True)
 
 
+def sweep():
+    """WOQ_SWEEP=1: K-split target blocks x register stages (pa_woq_tune) on the same shapes."""
+    import paddle  # noqa: F401
+    from paddle.ops import woq, gemm, _native
+    from paddle.nn.quant import weight_quantize
+    assert _native._load() is not None, _native.load_error
+    L = _native.lib
+    dev = 'cuda'
+    for name, K, N in [('qkv', 5120, 15360), ('out', 5120, 5120), ('ffn1', 5120, 27648), ('ffn2', 13824, 5120)]:
+        w = torch.randn(K, N, device=dev) * 0.02
+        wb = w.bfloat16()
+        q8, s8 = (t._t for t in weight_quantize(paddle.to_tensor(w), 'weight_only_int8'))
+        q4, s4 = (t._t for t in weight_quantize(paddle.to_tensor(w), 'weight_only_int4'))
+        for M in (1, 16):
+            x = torch.randn(M, K, device=dev).bfloat16()
+            tb = bench(lambda: gemm.skinny_mm(x, wb))
+            best = {}
+            for tgt in (128, 256, 512, 1024, 2048):
+                for nst in (2, 3, 4):
+                    L.pa_woq_tune(tgt, nst)
+                    t8 = bench(lambda: woq.woq_linear(x, q8, s8, 8, 0))
+                    t4 = bench(lambda: woq.woq_linear(x, q4, s4, 4, 0))
+                    print(f"{name:5s} M={M:2d} target {tgt:5d} nst {nst}: int8 {t8*1e6:6.1f} us ({tb/t8:4.2f}x) "
+                          f"int4 {t4*1e6:6.1f} us ({tb/t4:4.2f}x)", flush=True)
+                    for b, t in ((8, t8), (4, t4)):
+                        if b not in best or t < best[b][0]:
+                            best[b] = (t, tgt, nst)
+            print(f"{name:5s} M={M:2d} bf16 {tb*1e6:6.1f} us | best int8 {best[8][0]*1e6:6.1f} us ({tb/best[8][0]:4.2f}x, "
+                  f"target {best[8][1]} nst {best[8][2]}) | best int4 {best[4][0]*1e6:6.1f} us "
+                  f"({tb/best[4][0]:4.2f}x, target {best[4][1]} nst {best[4][2]})", flush=True)
+    L.pa_woq_tune(512, 3)
+
+
 if __name__ == '__main__':
-    main()
+    if os.environ.get('WOQ_SWEEP') == '1':
+        sweep()
+    else:
+        main()
