@@ -592,13 +592,16 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void fwd_kernel(const uint16_
 // PIPE: Q/dO tiles double-buffered in LDS — one barrier per query block instead of two (tile
 // i+1 is written into the other buffer right after block i's compute; its global loads were
 // issued one block earlier).
-template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0, bool PIPE = false>
+// WDS: also store dS^T (bf16/f16, [key][query] rows of ``dsld`` elements per (b, h) at
+// dsT + b * dsb + h * dsh) for the dQ-from-dS kernel (flash_attn_ds.hip).
+template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0, bool PIPE = false, bool WDS = false>
 // (D = 96 with an additive mask needs more than 256 registers: one wave per SIMD there too)
 __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 2) != 0)) ? 1 : 3 - NT) void bwd_dkdv_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq_, int Sk_, int Hq, int Hk, Strides qs, Strides ks_,
-    Strides vs, Strides dos, Strides dks, Strides dvs, float scale, Extra ex = Extra{}) {
+    Strides vs, Strides dos, Strides dks, Strides dvs, float scale, Extra ex = Extra{},
+    uint16_t* __restrict__ dsT = nullptr, long long dsb = 0, long long dsh = 0, int dsld = 0) {
   if constexpr ((EXT & 4) != 0) ex.seed = rng_mix(ex.seed);  // graph-captured steps: per-replay stream
   constexpr int KS = D / 32;
   constexpr int DB = D / 16;
@@ -798,6 +801,24 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 
       p_ds(std::true_type{});
     else
       p_ds(std::false_type{});
+    if constexpr (WDS) {
+      // dS^T rows (keys) x 64 queries of this block: lane (g, i) holds key kw + 16j + i, queries
+      // q0 + 32s + 4g + (0..3) (elements 0..3) and q0 + 32s + 16 + 4g + (0..3) (elements 4..7)
+      uint16_t* dsbase = dsT + (long long)b * dsb + (long long)h * dsh;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int key = kw + 16 * j + (lane & 15);
+        if (key < Sk) {
+          uint16_t* row = dsbase + (long long)key * dsld + q0 + 4 * g;
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const s16x8 d8 = db_[j][s2];
+            *reinterpret_cast<s16x4*>(row + 32 * s2) = s16x4{d8[0], d8[1], d8[2], d8[3]};
+            *reinterpret_cast<s16x4*>(row + 32 * s2 + 16) = s16x4{d8[4], d8[5], d8[6], d8[7]};
+          }
+        }
+      }
+    }
     // dV^T += dO^T P ;  dK^T += Q^T dS
 #pragma unroll
     for (int d = 0; d < DB; ++d) {

@@ -239,7 +239,7 @@ def install_rng_generation(device=None):
     gen = _RNG_GEN.get(dev.index)
     if gen is None:
         gen = torch.zeros(1, dtype=torch.int32, device=dev)
-        for fn in ('pa_norm_set_rng_gen', 'pa_act_set_rng_gen', 'pa_flash_set_rng_gen'):
+        for fn in ('pa_norm_set_rng_gen', 'pa_act_set_rng_gen', 'pa_flash_set_rng_gen', 'pa_flash_ds_set_rng_gen'):
             N.check(getattr(N.lib, fn)(N.ptr(gen)), fn)
         _RNG_GEN[dev.index] = gen
     return gen

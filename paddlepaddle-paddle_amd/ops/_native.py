@@ -98,6 +98,9 @@ _SIGS = {
     'pa_skinny_gemm': [P, P, P, P, P, I, I, I, LL, LL, LL, I, P],
     'pa_act_set_rng_gen': [P],
     'pa_flash_set_rng_gen': [P],
+    'pa_flash_ds_set_rng_gen': [P],
+    'pa_flash_ds_ld': [I],
+    'pa_flash_bwd_ds': [P] * 11 + [I] * 6 + [LLP] * 8 + [F, I, I, P, P, I, P, LL, LL, LL, I, F, U32, U32, P, LL, LL, P],
     'pa_conv2d_wgrad_ok': [I, I],
     'pa_conv2d_dgrad_classes': [P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     'pa_conv2d_wgrad': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],

@@ -3,6 +3,7 @@
 Reference: paddle/phi/kernels/gpu/flash_attn_kernel.cu / flash_attn_grad_kernel.cu.
 """
 import math
+import os
 
 import torch
 
@@ -32,6 +33,58 @@ def supported(q, k, v):
             and q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1
             and k.shape[2] > 0 and q.shape[2] % k.shape[2] == 0 and k.shape == v.shape
             and all(s % 8 == 0 for t in (q, k, v) for s in t.stride()[:3]))
+
+
+# Backward with a materialised dS (csrc/flash_attn_ds.hip): delta pass, dK/dV kernel that also
+# stores dS^T, dQ = dS K from it — instead of a second kernel recomputing S and dP.  The dS^T
+# workspace (B * Hq * Sk * ceil(Sq / 128) * 128 elements, 0.5 GB for GPT-3 1.3B's attention) is
+# kept per device and reused by every layer.  PADDLE_AMD_FA_DS_BWD=1 selects it (set_ds_backward).
+_ds_bwd = [os.environ.get('PADDLE_AMD_FA_DS_BWD', '0') != '0']
+_DS_WS = {}
+
+
+def set_ds_backward(on):
+    old = _ds_bwd[0]
+    _ds_bwd[0] = bool(on)
+    return old
+
+
+def _ds_ok(D, dt):
+    return _ds_bwd[0] and D in (64, 128) and dt in (torch.bfloat16, torch.float16)
+
+
+def _ds_ws(B, Hq, Sq, Sk, dtype, device):
+    n = B * Hq * Sk * int(N.lib.pa_flash_ds_ld(Sq))
+    key = (str(device), dtype)
+    t = _DS_WS.get(key)
+    if t is None or t.numel() < n:
+        _DS_WS[key] = t = torch.empty(n, dtype=dtype, device=device)
+    return t
+
+
+def _bwd_call(q, k, v, o, do, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, D, scale, causal, cu_q=None, cu_k=None,
+              total=0, m=None, mb=0, mh=0, mq=0, mf=0, p_drop=0.0, seed=0, rows=None, rb=0, rh=0, ex=False):
+    """The backward launch sequence: dS path when enabled, else the recompute kernels
+    (pa_flash_bwd, or pa_flash_bwd_ex when any extended feature is in use)."""
+    st = (N.strides3(q), N.strides3(k), N.strides3(v), N.strides3(o), N.strides3(do), N.strides3(dq),
+          N.strides3(dk), N.strides3(dv))
+    if _ds_ok(D, q.dtype):
+        ws = _ds_ws(B, Hq, Sq, Sk, q.dtype, q.device)
+        N.check(N.lib.pa_flash_bwd_ds(N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse), N.ptr(delta),
+                                      N.ptr(dq), N.ptr(dk), N.ptr(dv), N.ptr(ws), B, Sq, Sk, Hq, Hk, D, *st, scale,
+                                      int(causal), N.dtcode(q.dtype), N.ptr(cu_q), N.ptr(cu_k), total, N.ptr(m), mb,
+                                      mh, mq, mf, float(p_drop), seed & 0xFFFFFFFF, 0, N.ptr(rows), rb, rh,
+                                      N.stream()), 'flash_bwd_ds')
+    elif ex:
+        N.check(N.lib.pa_flash_bwd_ex(N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse), N.ptr(delta),
+                                      N.ptr(dq), N.ptr(dk), N.ptr(dv), B, Sq, Sk, Hq, Hk, D, *st, scale, int(causal),
+                                      N.dtcode(q.dtype), N.ptr(cu_q), N.ptr(cu_k), total, N.ptr(m), mb, mh, mq, mf,
+                                      float(p_drop), seed & 0xFFFFFFFF, 0, N.ptr(rows), rb, rh, N.stream()),
+                'flash_bwd_ex')
+    else:
+        N.check(N.lib.pa_flash_bwd(N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse), N.ptr(delta),
+                                   N.ptr(dq), N.ptr(dk), N.ptr(dv), B, Sq, Sk, Hq, Hk, D, *st, scale, int(causal),
+                                   N.dtcode(q.dtype), N.stream()), 'flash_bwd')
 
 
 def _fwd(q, k, v, causal, scale):
@@ -64,11 +117,7 @@ class _FlashAttn(torch.autograd.Function):
         dk = torch.empty(B, Sk, Hq, D, dtype=q.dtype, device=q.device)
         dv = torch.empty(B, Sk, Hq, D, dtype=q.dtype, device=q.device)
         delta = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
-        N.check(N.lib.pa_flash_bwd(N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse), N.ptr(delta),
-                                   N.ptr(dq), N.ptr(dk), N.ptr(dv), B, Sq, Sk, Hq, Hk, D, N.strides3(q), N.strides3(k),
-                                   N.strides3(v), N.strides3(o), N.strides3(do), N.strides3(dq), N.strides3(dk),
-                                   N.strides3(dv), ctx.scale, int(ctx.causal), N.dtcode(q.dtype), N.stream()),
-                'flash_bwd')
+        _bwd_call(q, k, v, o, do, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, D, ctx.scale, ctx.causal)
         if Hq != Hk:  # GQA: sum the per-q-head dK/dV over each kv group
             dk = dk.view(B, Sk, Hk, Hq // Hk, D).sum(3)
             dv = dv.view(B, Sk, Hk, Hq // Hk, D).sum(3)
@@ -98,11 +147,7 @@ class _FlashAttnPacked(torch.autograd.Function):
         dqkv = torch.empty(B, S, 3, H, D, dtype=qkv.dtype, device=qkv.device)
         dq, dk, dv = dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2]
         delta = torch.empty(B, H, S, dtype=torch.float32, device=q.device)
-        N.check(N.lib.pa_flash_bwd(N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse), N.ptr(delta),
-                                   N.ptr(dq), N.ptr(dk), N.ptr(dv), B, S, S, H, H, D, N.strides3(q), N.strides3(k),
-                                   N.strides3(v), N.strides3(o), N.strides3(do), N.strides3(dq), N.strides3(dk),
-                                   N.strides3(dv), ctx.scale, int(ctx.causal), N.dtcode(q.dtype), N.stream()),
-                'flash_bwd')
+        _bwd_call(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, S, H, H, D, ctx.scale, ctx.causal)
         return dqkv, None, None
 
 
@@ -227,13 +272,8 @@ class _FlashAttnEx(torch.autograd.Function):
         qv, kv, vv, ov, dov, dqv, dkv, dvv = views
         m, mb, mh, mq, mf = _mask_args(mask, B, Hq, Sq, Sk, q.dtype)
         rows, rb, rh = _rows_args(rows, B, Hq, Sk)
-        N.check(N.lib.pa_flash_bwd_ex(N.ptr(qv), N.ptr(kv), N.ptr(vv), N.ptr(ov), N.ptr(dov), N.ptr(lse),
-                                      N.ptr(delta), N.ptr(dqv), N.ptr(dkv), N.ptr(dvv), B, Sq, Sk, Hq, Hk, D,
-                                      N.strides3(qv), N.strides3(kv), N.strides3(vv), N.strides3(ov),
-                                      N.strides3(dov), N.strides3(dqv), N.strides3(dkv), N.strides3(dvv), scale,
-                                      int(causal), N.dtcode(q.dtype), N.ptr(cu_q), N.ptr(cu_k), total, N.ptr(m), mb,
-                                      mh, mq, mf, float(p_drop), seed & 0xFFFFFFFF, 0, N.ptr(rows), rb, rh, N.stream()),
-                'flash_bwd_ex')
+        _bwd_call(qv, kv, vv, ov, dov, lse, delta, dqv, dkv, dvv, B, Sq, Sk, Hq, Hk, D, scale, causal, cu_q, cu_k, total,
+                  m, mb, mh, mq, mf, p_drop, seed, rows, rb, rh, ex=True)
         if Hq != Hk:
             dk = dk.unflatten(-2, (Hk, Hq // Hk)).sum(-2)
             dv = dv.unflatten(-2, (Hk, Hq // Hk)).sum(-2)
@@ -284,12 +324,8 @@ class _FlashAttnPackedEx(torch.autograd.Function):
         dq, dk, dv = dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2]
         delta = torch.empty(B, H, S, dtype=torch.float32, device=q.device)
         m, mb, mh, mq, mf = _mask_args(mask, B, H, S, S, q.dtype)
-        N.check(N.lib.pa_flash_bwd_ex(N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse), N.ptr(delta),
-                                      N.ptr(dq), N.ptr(dk), N.ptr(dv), B, S, S, H, H, D, N.strides3(q), N.strides3(k),
-                                      N.strides3(v), N.strides3(o), N.strides3(do), N.strides3(dq), N.strides3(dk),
-                                      N.strides3(dv), scale, int(causal), N.dtcode(q.dtype), None, None, 0, N.ptr(m),
-                                      mb, mh, mq, mf, float(p_drop), seed & 0xFFFFFFFF, 0, None, 0, 0, N.stream()),
-                'flash_bwd_ex')
+        _bwd_call(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, S, H, H, D, scale, causal, None, None, 0, m, mb, mh, mq,
+                  mf, p_drop, seed, None, 0, 0, ex=True)
         return dqkv, None, None, None, None
 
 

@@ -46,6 +46,12 @@ def timeit(fn, n=10):
 
 
 def main():
+    if os.environ.get('FA_DS_AB') == '1':  # recompute backward vs materialised-dS backward
+        for on in (False, True):
+            ops.flash_attn.set_ds_backward(on)
+            print(f"-- dS backward {'on' if on else 'off'}", flush=True)
+            run()
+        return
     for var in [int(x) for x in os.environ.get('FA_VARIANTS', '1').split(',')]:
         _native.lib.pa_flash_set_bwd_variant(var)
         print(f"-- backward variant {var}", flush=True)
