@@ -610,7 +610,11 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 
   // 2-way: SQ_LDS_BANK_CONFLICT was 20-27 % of LDS cycles in these kernels)
   constexpr bool BT = (fa_pitch<D>() >= 128);
   constexpr int STAGE = 2 * 64 * fa_pitch<D>() * 2 + 2 * 64 * 4;  // Q, dO, LSE, delta of one query block
-  __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE];
+  // D > 128: the wave's K / V rows live in LDS (read per k-step) instead of 2 x 8 fragments of
+  // registers each, which with the dK / dV accumulators exceeded the 512-entry register file
+  constexpr bool KVL = D > 128;
+  constexpr int KVW = KVL ? NT * 16 * D * 2 : 0;  // bytes of one wave's K (or V) rows
+  __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE + 2 * NW * KVW];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches and addresses
@@ -633,18 +637,35 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 
   K += (vl ? 0 : b * ks_.b) + sq_.ko * ks_.s;
   V += (vl ? 0 : b * vs.b) + sq_.ko * vs.s;
   // K, V of this wave's keys as B operands: lane holds K[key][32ks + 8g .. +8]
-  s16x8 kf[NT][KS], vf[NT][KS];
+  s16x8 kf[NT][KVL ? 1 : KS], vf[NT][KVL ? 1 : KS];
+  char* kv_lds = smem + (PIPE ? 2 : 1) * STAGE + wave * 2 * KVW;  // KVL: [NT*16][D] K rows, then V rows
+  if constexpr (KVL) {
+    constexpr int CH = D / 8, NCH = NT * 16 * CH / 64;  // 16-B chunks per row / per lane
 #pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int key = kw + 16 * j + (lane & 15);
-#pragma unroll
-    for (int k = 0; k < KS; ++k) {
+    for (int i = 0; i < NCH; ++i) {
+      const int c = lane + 64 * i, row = c / CH, ch = c % CH;
+      const int key = kw + row;
+      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
       if (key < Sk) {
-        kf[j][k] = *reinterpret_cast<const s16x8*>(K + hk * ks_.h + (long long)key * ks_.s + 32 * k + 8 * g);
-        vf[j][k] = *reinterpret_cast<const s16x8*>(V + hk * vs.h + (long long)key * vs.s + 32 * k + 8 * g);
-      } else {
-        kf[j][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        vf[j][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        kv = *reinterpret_cast<const uint4*>(K + hk * ks_.h + (long long)key * ks_.s + 8 * ch);
+        vv = *reinterpret_cast<const uint4*>(V + hk * vs.h + (long long)key * vs.s + 8 * ch);
+      }
+      *reinterpret_cast<uint4*>(kv_lds + lds_off<D, false>(row, ch)) = kv;
+      *reinterpret_cast<uint4*>(kv_lds + KVW + lds_off<D, false>(row, ch)) = vv;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int key = kw + 16 * j + (lane & 15);
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        if (key < Sk) {
+          kf[j][k] = *reinterpret_cast<const s16x8*>(K + hk * ks_.h + (long long)key * ks_.s + 32 * k + 8 * g);
+          vf[j][k] = *reinterpret_cast<const s16x8*>(V + hk * vs.h + (long long)key * vs.s + 32 * k + 8 * g);
+        } else {
+          kf[j][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+          vf[j][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
       }
     }
   }
@@ -726,6 +747,27 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 
         acc_s[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
         acc_dp[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
+    if constexpr (KVL) {
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        s16x8 kk[NT], vv[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          kk[j] = ld_row8<D, false>(kv_lds, 16 * j + (lane & 15), k, g);
+          vv[j] = ld_row8<D, false>(kv_lds + KVW, 16 * j + (lane & 15), k, g);
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const s16x8 qa = ld_row8<D, BT>(q_lds, 16 * m + (lane & 15), k, g);
+          const s16x8 da = ld_row8<D, BT>(do_lds, 16 * m + (lane & 15), k, g);
+#pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            acc_s[j][m] = Mfma<T>::run(qa, kk[j], acc_s[j][m]);
+            acc_dp[j][m] = Mfma<T>::run(da, vv[j], acc_dp[j][m]);
+          }
+        }
+      }
+    } else {
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
 #pragma unroll
@@ -738,6 +780,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 
           acc_dp[j][m] = Mfma<T>::run(da, vf[j][k], acc_dp[j][m]);
         }
       }
+    }
     }
     // P and dS, packed as B operands (k = query, permuted as in the forward)
     const bool need_mask = (q0 + 64 > Sq) || (kw + 16 * NT > Sk) || (CAUSAL && kw + 16 * NT - 1 > q0 + off);

@@ -38,19 +38,27 @@ def supported(q, k, v):
 # Backward with a materialised dS (csrc/flash_attn_ds.hip): delta pass, dK/dV kernel that also
 # stores dS^T, dQ = dS K from it — instead of a second kernel recomputing S and dP.  The dS^T
 # workspace (B * Hq * Sk * ceil(Sq / 128) * 128 elements, 0.5 GB for GPT-3 1.3B's attention) is
-# kept per device and reused by every layer.  PADDLE_AMD_FA_DS_BWD=1 selects it (set_ds_backward).
-_ds_bwd = [os.environ.get('PADDLE_AMD_FA_DS_BWD', '0') != '0']
+# kept per device and reused by every layer.  Default: head_dim 128 (B16 S1024 H16 causal
+# fwd+bwd 0.720 -> 0.651 ms, GPT-3 1.3B step 124.4k -> 125.7k tok/s, profiles/r4e_attn_ds_ab.log);
+# head_dim 64 stays on the recompute pair (1.04 -> 1.24 ms there: its dQ recompute is cheaper than
+# the dS round trip).  PADDLE_AMD_FA_DS_BWD=0 / 1: off / also for head_dim 64.
+_ds_env = os.environ.get('PADDLE_AMD_FA_DS_BWD')
+_ds_bwd = [None if _ds_env is None else _ds_env != '0']  # None: automatic (head_dim 128)
 _DS_WS = {}
 
 
 def set_ds_backward(on):
+    """True: every supported head dim, False: off, None: automatic (head_dim 128).  Returns the old."""
     old = _ds_bwd[0]
-    _ds_bwd[0] = bool(on)
+    _ds_bwd[0] = None if on is None else bool(on)
     return old
 
 
 def _ds_ok(D, dt):
-    return _ds_bwd[0] and D in (64, 128) and dt in (torch.bfloat16, torch.float16)
+    if dt not in (torch.bfloat16, torch.float16):
+        return False
+    on = _ds_bwd[0]
+    return D == 128 if on is None else (on and D in (64, 128))
 
 
 def _ds_ws(B, Hq, Sq, Sk, dtype, device):
