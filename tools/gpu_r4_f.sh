@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 300 python -u tools/resnet_layout_act_diff.py > gpurun_out/r4f_resnet_act_diff.log 2>&1 || { echo "act diff failed"; tail -30 gpurun_out/r4f_resnet_act_diff.log; exit 1; }
 grep -v amdgpu.ids gpurun_out/r4f_resnet_act_diff.log
-timeout -k 10 900 python -u -m pytest tests/test_hip_flash_ds.py tests/test_hip_flash_wide.py tests/test_hip_flash_ex.py tests/test_fp8.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r4f_flash_tests.log 2>&1 || { echo "flash tests failed"; tail -60 gpurun_out/r4f_flash_tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_hip_flash_ds.py tests/test_hip_flash_wide.py tests/test_hip_flash_ex.py tests/test_fp8.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r4f_flash_tests.log 2>&1 || { echo "flash tests failed"; tail -60 gpurun_out/r4f_flash_tests.log; exit 1; }
 tail -3 gpurun_out/r4f_flash_tests.log
 timeout -k 10 300 python -u tools/fp8_bench.py > gpurun_out/r4f_fp8_bench.log 2>&1 || { echo "fp8 bench failed"; tail -30 gpurun_out/r4f_fp8_bench.log; exit 1; }
 grep -v amdgpu.ids gpurun_out/r4f_fp8_bench.log
