@@ -604,8 +604,15 @@ PA_API int pa_conv2d_set_staged(int v) {
 
 // Contract: bf16 NHWC input [N,H,W,C], packed weight [Cout][R][S][C], output [N,Ho,Wo,Cout];
 // C % 32 == 0, (R*S*C) % 64 == 0, Cout % 8 == 0 (checked; Python falls back to MIOpen otherwise).
+// Zero taps appended to the filter so that K = taps * C is a multiple of the 64-deep main loop
+// (C % 64 == 32 with an odd tap count, e.g. a 3x3 conv over 32 channels): the extra tap reads the
+// zero block (offset far outside the image) against zero filter columns.  The packed filter of
+// pa_conv2d_fwd / _stats is [Cout][R*S + pa_conv2d_fwd_pad_taps(C, R, S)][C].
+PA_API int pa_conv2d_fwd_pad_taps(int C, int R, int S) { return ((long long)R * S * C) % 64 != 0 ? 1 : 0; }
+
 PA_API int pa_conv2d_fwd_ok(int C, int Cout, int R, int S) {
-  return C > 0 && C % 32 == 0 && (R * S * C) % 64 == 0 && Cout > 0 && Cout % 8 == 0;
+  return C > 0 && C % 32 == 0 && R > 0 && S > 0 && R * S + pa_conv2d_fwd_pad_taps(C, R, S) <= MAX_TAPS && Cout > 0 &&
+         Cout % 8 == 0;
 }
 
 // waves along the pixel side per Cout tile width (A/B knob; index 0/1/2 = BN 64/128/256)
@@ -683,7 +690,7 @@ PA_API int pa_conv2d_fwd_stats(const void* x, const void* wpk, void* y, float* s
 static int conv2d_fwd_impl(const void* x, const void* wpk, void* y, const void* bias, float* stats, int N, int H,
                            int W, int C, int Cout, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw,
                            int Ho, int Wo, hipStream_t st) {
-  if (!pa_conv2d_fwd_ok(C, Cout, R, S) || N <= 0 || Ho <= 0 || Wo <= 0 || R * S > MAX_TAPS)
+  if (!pa_conv2d_fwd_ok(C, Cout, R, S) || N <= 0 || Ho <= 0 || Wo <= 0 || H >= 16384 || W >= 16384)
     return (int)hipErrorInvalidValue;
   Geom g{N, H, W, C, Ho, Wo, Cout, R, S, sh, sw, ph, pw, dh, dw};
   Taps tp{};
@@ -692,13 +699,15 @@ static int conv2d_fwd_impl(const void* x, const void* wpk, void* y, const void* 
       tp.th[r * S + q] = (short)(r * dh - ph);
       tp.tw[r * S + q] = (short)(q * dw - pw);
     }
+  const int ntaps = R * S + pa_conv2d_fwd_pad_taps(C, R, S);
+  for (int t = R * S; t < ntaps; ++t) tp.th[t] = tp.tw[t] = (short)-30000;  // always outside: zero block
   tp.oy0 = tp.ox0 = 0;
   tp.osy = tp.osx = 1;
   tp.HY = Ho;
   tp.WY = Wo;
-  tp.ldw = (long long)R * S * C;
+  tp.ldw = (long long)ntaps * C;
   tp.stats = stats;
-  return launch_fwd(x, wpk, y, bias, g, tp, R * S, st);
+  return launch_fwd(x, wpk, y, bias, g, tp, ntaps, st);
 }
 
 // Data gradient of a strided conv, all stride classes in ONE launch.  Class c = (a, b) covers

@@ -66,7 +66,12 @@ __global__ __launch_bounds__(256, 2) void dq_from_ds_kernel(const uint16_t* __re
   constexpr int DB = D / 16;
   constexpr bool BT = (fa_pitch<D>() >= 128);
   constexpr int KT = 64 * fa_pitch<D>() * 2;  // K tile bytes
-  __shared__ __attribute__((aligned(16))) char smem[KT + 64 * QB * 2];
+  constexpr int STG = KT + 64 * QB * 2;  // one K tile + one dS^T tile
+  // Two LDS stages and two register stages: key block kb + 3 is requested right after block
+  // kb + 1 is written to LDS, so a tile has ~2 key blocks of compute to arrive (one block of
+  // compute is far shorter than the HBM latency: with a single register stage the kernel ran at
+  // 2.9 TB/s; a third register set spilled).
+  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
@@ -92,59 +97,84 @@ __global__ __launch_bounds__(256, 2) void dq_from_ds_kernel(const uint16_t* __re
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int d = 0; d < DB; ++d) acc[t][d] = f32x4{0.f, 0.f, 0.f, 0.f};
-  Tile<D, 256> kt;
-  Tile<128, 256> st;  // the dS^T tile: 64 key rows x 128 queries (D = 128 image)
-  kt.init(kbase, ks_.s);
-  st.init(dsbase, dsld);
+  Tile<D, 256> kt0, kt1;
+  Tile<128, 256> st0, st1;  // dS^T tiles: 64 key rows x 128 queries (D = 128 image)
+  kt0.init(kbase, ks_.s);
+  kt1.init(kbase, ks_.s);
+  st0.init(dsbase, dsld);
+  st1.init(dsbase, dsld);
+  // every tile load below is unconditional (index clamped to the last key block, rows to Sk):
+  // guarded loads made the compiler's counted waits drain the whole queue at the join points
+  const int last = max(nkb - 1, 0) * 64;
   if (nkb > 0) {
-    kt.load(0, Sk);
-    st.load(0, Sk);
+    kt0.load_clamped(0, Sk);
+    st0.load_clamped(0, Sk);
+    kt1.load_clamped(min(64, last), Sk);
+    st1.load_clamped(min(64, last), Sk);
+    kt0.template store<BT>(smem);
+    st0.template store<true>(smem + KT);
+    kt0.load_clamped(min(128, last), Sk);
+    st0.load_clamped(min(128, last), Sk);
+    __syncthreads();
   }
-  char* k_lds = smem;
-  char* s_lds = smem + KT;
-  for (int kb = 0; kb < nkb; ++kb) {
+  // key block kb from LDS stage kb & 1; then block kb + 1 (register set (kb + 1) % 2) into the
+  // other stage (unused after the last block) and block kb + 3 requested into that set
+  auto compute = [&](int kb) {
     const int k0 = kb * 64;
-    __syncthreads();
-    kt.template store<BT>(k_lds);
-    st.template store<true>(s_lds);
-    __syncthreads();
-    if (kb + 1 < nkb) {
-      kt.load(k0 + 64, Sk);
-      st.load(k0 + 64, Sk);
-    }
-    if (CAUSAL && k0 > qw + 16 * NT - 1 + off) continue;  // whole key block above this wave's rows
-    // dS^T fragments: lane (g, i) of tile t, step s: keys k0 + 32s + 4g + (0..3) / + 16, query qw + 16t + i
-    s16x8 dsf[NT][2];
+    const char* k_lds = smem + (kb & 1) * STG;
+    const char* s_lds = k_lds + KT;
+    if (!(CAUSAL && k0 > qw + 16 * NT - 1 + off)) {  // else: whole key block above this wave's rows
+      // dS^T fragments: lane (g, i) of tile t, step s: keys k0 + 32s + 4g + (0..3) / + 16, query qw + 16t + i
+      s16x8 dsf[NT][2];
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) dsf[t][s] = ld_tr8<128, true>(s_lds, 32 * s, (qw - q0) / 16 + t, lane);
-    const bool need_mask = (k0 + 64 > Sk) || (CAUSAL && k0 + 63 > qw + off);
-    if (need_mask) {
+        for (int s = 0; s < 2; ++s) dsf[t][s] = ld_tr8<128, true>(s_lds, 32 * s, (qw - q0) / 16 + t, lane);
+      const bool need_mask = (k0 + 64 > Sk) || (CAUSAL && k0 + 63 > qw + off);
+      if (need_mask) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int q = qw + 16 * t + (lane & 15);
+        for (int t = 0; t < NT; ++t) {
+          const int q = qw + 16 * t + (lane & 15);
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+          for (int s = 0; s < 2; ++s)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int key = k0 + 32 * s + 4 * g + (e & 3) + (e >= 4 ? 16 : 0);
-            const bool masked = (key >= Sk) || (CAUSAL && key > q + off);
-            dsf[t][s][e] = masked ? (short)0 : dsf[t][s][e];
-          }
+            for (int e = 0; e < 8; ++e) {
+              const int key = k0 + 32 * s + 4 * g + (e & 3) + (e >= 4 ? 16 : 0);
+              const bool masked = (key >= Sk) || (CAUSAL && key > q + off);
+              dsf[t][s][e] = masked ? (short)0 : dsf[t][s][e];
+            }
+        }
       }
-    }
-    // dQ^T += K^T dS^T
+      // dQ^T += K^T dS^T
 #pragma unroll
-    for (int d = 0; d < DB; ++d) {
+      for (int d = 0; d < DB; ++d) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const s16x8 ka = ld_tr8<D, BT>(k_lds, 32 * s, d, lane);
+        for (int s = 0; s < 2; ++s) {
+          const s16x8 ka = ld_tr8<D, BT>(k_lds, 32 * s, d, lane);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t][d] = Mfma<T>::run(ka, dsf[t][s], acc[t][d]);
+          for (int t = 0; t < NT; ++t) acc[t][d] = Mfma<T>::run(ka, dsf[t][s], acc[t][d]);
+        }
       }
-    }
+    }  // not above the diagonal
+  };
+  // (a macro, not a lambda over Tile references: those pushed the register sets to scratch)
+#define PA_DQ_STEP(KB, KN, SN)                                                   \
+  do {                                                                           \
+    compute(KB);                                                                 \
+    char* nx = smem + (((KB) + 1) & 1) * STG;                                    \
+    KN.template store<BT>(nx);                                                   \
+    SN.template store<true>(nx + KT);                                            \
+    KN.load_clamped(min((KB) * 64 + 192, last), Sk);                             \
+    SN.load_clamped(min((KB) * 64 + 192, last), Sk);                             \
+    __syncthreads();                                                             \
+  } while (0)
+  int kb = 0;
+  for (; kb + 2 <= nkb; kb += 2) {
+    PA_DQ_STEP(kb, kt1, st1);
+    PA_DQ_STEP(kb + 1, kt0, st0);
   }
+  if (kb < nkb) PA_DQ_STEP(kb, kt1, st1);
+#undef PA_DQ_STEP
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int myq = qw + 16 * t + (lane & 15);

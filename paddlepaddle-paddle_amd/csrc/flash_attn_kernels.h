@@ -114,6 +114,21 @@ struct Tile {
                                                   : make_uint4(0, 0, 0, 0);
     }
   }
+  // branch-free load (nrows >= 1): rows past nrows re-read row nrows - 1 (finite data the
+  // consumer masks), so the compiler can keep several tiles' loads in flight with counted waits
+  __device__ __forceinline__ void load_clamped(int row0, int nrows) {
+    static_assert(!FLAT, "clamped loads use the row-per-thread mapping");
+    const uint16_t* q = p + (long long)row0 * rs;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int dr = min(RPL * i, nrows - 1 - row0 - row_in);
+      // through a plain vector type: a uint4 struct copy stayed a memcpy and pinned the register
+      // sets to scratch
+      typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(q + (long long)dr * rs);
+      r[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  }
   template <bool TR>
   __device__ __forceinline__ void store(char* lds) const {
 #pragma unroll

@@ -40,7 +40,9 @@ _SIGS = {
     'pa_conv_stem_ok': [I] * 6,
     'pa_conv_stem_kp': [I, I, I],
     'pa_conv_stem_rk': [I, I],
-    'pa_conv_stem_fwd': [P, P, P, P] + [I] * 14 + [P],
+    'pa_conv_stem_fwd': [P] * 5 + [I] * 14 + [P],
+    'pa_conv_stem_stat_rows': [I],
+    'pa_conv2d_fwd_pad_taps': [I, I, I],
     'pa_dwconv_fwd': [P, P, P, P] + [I] * 15 + [P],
     'pa_dwconv_dgrad': [P, P, P] + [I] * 15 + [P],
     'pa_dwconv_wgrad_splits': [I] * 6,

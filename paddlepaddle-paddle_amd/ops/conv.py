@@ -81,7 +81,10 @@ def _out_hw(H, W, R, S, stride, pad, dil):
 # statistics pass.  Entries are keyed by the output tensor object (weak reference) and popped by
 # the consumer.
 _stats_mode = [0]
-_bn_parts = {}  # (data_ptr, numel) of y -> (weakref(y), parts [2][P][C] fp32, P, rows per slab)
+# (data_ptr, numel) of y -> (y, parts [2][P][C] fp32, P, rows per slab, y._version).  y is held
+# strongly, for the fused_bn_stats() scope only: a weak reference died with the NHWC tensor object
+# when an NCHW conv2d handed back only its permuted view, and its norm then recomputed statistics
+_bn_parts = {}
 
 
 class fused_bn_stats:
@@ -112,10 +115,7 @@ def _parts_key(t):
 
 
 def _stash_parts(y, parts, P, rpb):
-    import weakref
-    for k in [k for k, v in _bn_parts.items() if v[0]() is None]:
-        del _bn_parts[k]
-    _bn_parts[_parts_key(y)] = (weakref.ref(y), parts, P, rpb, y._version)
+    _bn_parts[_parts_key(y)] = (y, parts, P, rpb, y._version)
 
 
 def take_bn_parts(x):
@@ -124,8 +124,9 @@ def take_bn_parts(x):
     e = _bn_parts.pop(_parts_key(x), None)
     if e is None:
         return None
-    y = e[0]()
-    if y is None or x._version != e[4]:  # freed, or modified in place since the epilogue wrote them
+    if x._version != e[4] or x.shape[-1] != e[0].shape[-1]:
+        # modified in place since the epilogue wrote them (views share the version counter), or
+        # another channel view of the same memory
         return None
     return e[1], e[2], e[3]
 
@@ -136,6 +137,9 @@ def _fwd_packed(x, wpk, b, stride, pad, dil):
     Nb, H, W, C = x.shape
     Cout, R, S, _ = wpk.shape
     Ho, Wo = _out_hw(H, W, R, S, stride, pad, dil)
+    pt = int(N.lib.pa_conv2d_fwd_pad_taps(C, R, S))
+    if pt:  # K = taps * C made a multiple of 64 with zero taps (e.g. 3x3 over 32 channels)
+        wpk = torch.cat([wpk.reshape(Cout, R * S * C), wpk.new_zeros(Cout, pt * C)], 1)
     y = torch.empty(Nb, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
     if _want_stats(b):
         rpb = int(N.lib.pa_conv2d_fwd_stat_rows(Cout))
@@ -235,15 +239,19 @@ def _dgrad_plan(w_shape, x_hw, stride, pad, dil, device):
                 classes.append((a, b, taps))
             else:
                 empty = True
+    # a class whose K = taps * Cout is an odd multiple of 32 gets a zero tap (filter slot R*S holds
+    # zeros; its dY offset lies far outside, so the kernel reads the zero block)
+    classes = [(a, b, taps + ([(R * S, -30000, -30000)] if (len(taps) * Cout) % 64 else []))
+               for a, b, taps in classes]
     flat = [t for _, _, taps in classes for t in taps]
-    ok = (0 < len(classes) <= 9 and len(flat) <= 64 and Cout % 32 == 0 and C % 8 == 0
+    ok = (0 < len(classes) <= 9 and len(flat) <= 64 and Cout % 32 == 0 and C % 8 == 0 and H < 16384 and W < 16384
           and all((len(t) * Cout) % 64 == 0 for _, _, t in classes))
     order = [t[0] for t in flat]
     idx = None if order == list(range(R * S)) else torch.tensor(order, device=device)
     cls = (ctypes.c_int * (3 * max(1, len(classes))))(*[v for a, b, taps in classes for v in (a, b, len(taps))])
     th = (ctypes.c_int * max(1, len(flat)))(*[t[1] for t in flat])
     tw = (ctypes.c_int * max(1, len(flat)))(*[t[2] for t in flat])
-    plan = (ok, len(classes), idx, empty, cls, th, tw)
+    plan = (ok, len(classes), idx, empty, cls, th, tw, R * S in order)
     _DGRAD_PLANS[key] = plan
     return plan
 
@@ -257,12 +265,14 @@ def conv2d_dgrad_classes(dy, w, x_hw, stride, pad, dil):
     import ctypes
     Cout, C, R, S = w.shape
     H, W = x_hw
-    ok, ncls, idx, empty, cls, th, tw = _dgrad_plan(w.shape, x_hw, stride, pad, dil, dy.device)
+    ok, ncls, idx, empty, cls, th, tw, zpad = _dgrad_plan(w.shape, x_hw, stride, pad, dil, dy.device)
     if not ok:
         return None
     dy = dy.contiguous()
     Nb, Hd, Wd, _ = dy.shape
     wt = w.detach().to(torch.bfloat16).permute(1, 2, 3, 0).reshape(C, R * S, Cout)
+    if zpad:  # zero-tap slot
+        wt = torch.cat([wt, wt.new_zeros(C, 1, Cout)], 1)
     wd = (wt if idx is None else wt.index_select(1, idx)).contiguous()  # [C][taps in class order][Cout]
     dx = (torch.zeros if empty else torch.empty)(Nb, H, W, C, dtype=torch.bfloat16, device=dy.device)
     vp = lambda arr: ctypes.cast(arr, ctypes.c_void_p)  # noqa: E731
@@ -448,8 +458,9 @@ def stem_ok(x, w, stride, dil):
 
 
 def conv2d_fwd_stem(x, w, b, stride, pad):
-    """y = conv(x, w) for C <= 8: the R input-row segments of an output-row segment staged once in
-    LDS, MFMA over k = (filter row, s*C + c) with the [Cout][Kp] filter image below."""
+    """y = conv(x, w) for C <= 8: the input rows of RB output rows staged once in LDS, MFMA over
+    k = (filter row, s*C + c) with the [Cout][Kp] filter image below; under fused_bn_stats() the
+    epilogue also writes the batch-norm slab statistics (one slab per output-row segment)."""
     x = x.contiguous()
     Nb, H, W, C = x.shape
     Cout, _, R, S = w.shape
@@ -459,8 +470,16 @@ def conv2d_fwd_stem(x, w, b, stride, pad):
     wimg[:, :R * RK].view(Cout, R, RK)[:, :, :S * C] = w.detach().to(x.dtype).permute(0, 2, 3, 1).reshape(Cout, R, S * C)
     y = torch.empty(Nb, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
     bb = b.to(x.dtype).contiguous() if b is not None else None
-    N.check(N.lib.pa_conv_stem_fwd(N.ptr(x), N.ptr(wimg), N.ptr(bb), N.ptr(y), Nb, H, W, C, Cout, R, S, stride[0],
-                                   stride[1], pad[0], pad[1], Ho, Wo, N.dtcode(x.dtype), N.stream()), 'conv_stem_fwd')
+    rpb = int(N.lib.pa_conv_stem_stat_rows(Wo)) if _want_stats(b) else 0
+    parts = None
+    if rpb:
+        P = Nb * Ho * (-(-Wo // 128))
+        parts = torch.empty(2 * P * Cout, dtype=torch.float32, device=x.device)
+    N.check(N.lib.pa_conv_stem_fwd(N.ptr(x), N.ptr(wimg), N.ptr(bb), N.ptr(y), N.ptr(parts), Nb, H, W, C, Cout, R, S,
+                                   stride[0], stride[1], pad[0], pad[1], Ho, Wo, N.dtcode(x.dtype), N.stream()),
+            'conv_stem_fwd')
+    if parts is not None:
+        _stash_parts(y, parts, P, rpb)
     return y
 
 

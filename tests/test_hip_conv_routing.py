@@ -71,6 +71,61 @@ def test_conv_stem_fwd(dt, N, H, W, C, Cout, k, s, p, bias):
     _close(y, ref, 3e-2, 1e-2, 'stem fwd')
 
 
+@pytest.mark.parametrize('N,H,W,C,Cout,k,s,p', [
+    (2, 224, 224, 3, 64, 7, 2, 3), (3, 64, 64, 3, 64, 7, 2, 3), (2, 33, 45, 4, 128, 3, 1, 1),
+    (1, 512, 512, 3, 64, 7, 2, 3)])
+def test_conv_stem_bn_stats(N, H, W, C, Cout, k, s, p):
+    """Under fused_bn_stats() the stem epilogue's slab (mean, M2) merge to the batch statistics of
+    the fp32 convolution (one slab per output-row segment)."""
+    from paddle.ops import conv
+    x = torch.randn(N, H, W, C, device=DEV).bfloat16()
+    w = (0.2 * torch.randn(Cout, C, k, k, device=DEV)).bfloat16()
+    with conv.fused_bn_stats():
+        y = conv.conv2d_fwd_stem(x, w, None, (s, s), (p, p))
+        e = conv.take_bn_parts(y)
+    assert e is not None
+    parts, P, rpb = e
+    M = y.numel() // Cout
+    assert P * rpb == M
+    pm, pq = parts.view(2, P, Cout)
+    mean = pm.mean(0)  # equal slabs
+    m2 = pq.sum(0) + rpb * ((pm - mean) ** 2).sum(0)
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float(), None, s, p).permute(0, 2, 3, 1)
+    ref = ref.reshape(M, Cout)
+    _close(mean, ref.mean(0), 1e-3, 1e-3, 'stem bn mean')
+    _close(m2 / M, ref.var(0, unbiased=False), 1e-3, 1e-2, 'stem bn var')
+    _close(y, ref.view_as(y), 3e-2, 1e-2, 'stem fwd (stats launch)')
+
+
+@pytest.mark.parametrize('C,Cout,k,s,p', [(32, 32, 3, 1, 1), (32, 64, 3, 2, 1), (96, 32, 3, 2, 1), (32, 32, 5, 1, 2)])
+def test_conv_zero_tap_padding(C, Cout, k, s, p):
+    """K = taps * C an odd multiple of 32 (3x3 over 32 channels): forward and stride-1 / strided
+    data gradients run the implicit-GEMM kernels with a zero tap appended; fp32 torch reference,
+    and no library convolution kernel in forward + backward."""
+    from paddle.ops import conv
+    x = torch.randn(2, 19, 21, C, device=DEV).bfloat16()
+    w = (0.1 * torch.randn(Cout, C, k, k, device=DEV)).bfloat16()
+    assert conv.supported(x, w, 1) and conv.fwd_ok(w)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_()
+    wr = w.float().requires_grad_()
+    yr = torch.nn.functional.conv2d(xr, wr, None, s, p).permute(0, 2, 3, 1)
+    xh, wh = x.clone().requires_grad_(), w.clone().requires_grad_()
+    g = torch.randn_like(yr)
+
+    def run():
+        y = conv.conv2d_nhwc(xh, wh, None, (s, s), (p, p), (1, 1))
+        y.backward(g.bfloat16())
+        return y
+    bad = _miopen_kernels(run)
+    assert bad == [], bad
+    xh.grad = wh.grad = None
+    y = run()
+    yr.backward(g)
+    _close(y, yr, 3e-2, 1e-2, 'fwd')
+    _close(xh.grad, xr.grad.permute(0, 2, 3, 1), 3e-2, 1e-2, 'dgrad')
+    _close(wh.grad, wr.grad, 5e-2, 2e-2, 'wgrad')
+
+
 def _miopen_kernels(fn):
     """Names of the library (MIOpen) convolution / batch-norm / pooling kernels ``fn`` launches."""
     from torch.profiler import profile, ProfilerActivity

@@ -37,14 +37,28 @@ def run(df):
                 t.register_hook(g)
         return f
     for name, sub in net.named_sublayers():
-        if name.count('.') <= 2:
+        if name.count('.') <= 3 and name.startswith(('conv1', 'maxpool', 'layer1.0', 'layer1.1')):
             sub.register_forward_post_hook(hook(name))
+        elif name.count('.') <= 2:
+            sub.register_forward_post_hook(hook(name))
+    from paddle.ops import conv as C, batchnorm as BNM
+    hits = []
+    orig = C.take_bn_parts
+
+    def spy(x):
+        r = orig(x)
+        hits.append(r is not None)
+        return r
+    C.take_bn_parts = spy
+    BNM_take = getattr(BNM, 'take_bn_parts', None)
     g = torch.Generator(device='cuda').manual_seed(3)
     img = torch.randn(4, 3, 64, 64, device='cuda', generator=g).bfloat16()
     lab = torch.randint(0, 10, (4,), device='cuda', generator=g)
     xin = paddle.to_tensor(img if df == 'NCHW' else img.permute(0, 2, 3, 1).contiguous())
     loss = paddle.nn.functional.cross_entropy(net(xin), paddle.to_tensor(lab))
     loss.backward()
+    C.take_bn_parts = orig
+    print(df, 'bn parts hits:', ''.join('1' if h else '0' for h in hits), flush=True)
     return acts, grads, order
 
 
