@@ -92,6 +92,10 @@ def _conv(x, weight, bias, stride, padding, dilation, groups, data_format, nd, f
         # depthwise (groups == C_in == C_out) on csrc/dwconv.hip, channels-last as above
         y = ops.conv.dwconv2d_nhwc(t.permute(0, 2, 3, 1).contiguous(), w, b, s, p, d)
         return _w(y if cl else y.permute(0, 3, 1, 2))
+    if nd == 2 and ops.use_hip(t) and ops.conv.gconv_supported(t.permute(0, 2, 3, 1), w, groups, s, p, d):
+        # grouped (1 < groups < C_in: ResNeXt) on csrc/gconv.hip, channels-last as above
+        y = ops.conv.gconv2d_nhwc(t.permute(0, 2, 3, 1).contiguous(), w, b, groups, s, p, d)
+        return _w(y if cl else y.permute(0, 3, 1, 2))
     out = fn(t, w, b, s, p, d, groups)
     if cl:
         out = out.permute(0, *range(2, nd + 2), 1)

@@ -43,6 +43,11 @@ _SIGS = {
     'pa_conv_stem_fwd': [P] * 5 + [I] * 14 + [P],
     'pa_conv_stem_stat_rows': [I],
     'pa_conv2d_fwd_pad_taps': [I, I, I],
+    'pa_gconv_ok': [I] * 17,
+    'pa_gconv_fwd': [P] * 4 + [I] * 17 + [P],
+    'pa_gconv_dgrad': [P] * 3 + [I] * 17 + [P],
+    'pa_gconv_wgrad_splits': [I] * 8,
+    'pa_gconv_wgrad': [P] * 4 + [I] * 19 + [P],
     'pa_dwconv_fwd': [P, P, P, P] + [I] * 15 + [P],
     'pa_dwconv_dgrad': [P, P, P] + [I] * 15 + [P],
     'pa_dwconv_wgrad_splits': [I] * 6,

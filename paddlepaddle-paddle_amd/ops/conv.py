@@ -675,6 +675,79 @@ def dwconv2d_nhwc(x, w, b, stride, pad, dil):
     return _DWConvNHWC.apply(x, w, b, tuple(stride), tuple(pad), tuple(dil))
 
 
+# ---- grouped convolution (1 < groups < C_in, ResNeXt / ShuffleNet-v1) on csrc/gconv.hip
+_gc_enabled = os.environ.get('PADDLE_AMD_HIP_GCONV', '1') != '0'
+
+
+def _gc_geo(x, w, groups, stride, pad, dil):
+    Nb, H, W, C = x.shape
+    Cout, _, R, S = w.shape
+    Ho, Wo = _out_hw(H, W, R, S, stride, pad, dil)
+    return (Nb, H, W, C, Ho, Wo, Cout, groups, R, S, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1])
+
+
+def gconv_supported(x, w, groups, stride=(1, 1), pad=(0, 0), dil=(1, 1)):
+    """x: NHWC view; w: [Cout, C / groups, R, S], 1 < groups < C, C / groups % 4 == 0 and
+    Cout / groups % 8 == 0, 16-bit dtypes."""
+    if not _gc_enabled or x.dim() != 4 or w.dim() != 4 or not x.is_cuda or groups <= 1:
+        return False
+    C = x.shape[3]
+    if groups >= C or C % groups or w.shape[1] * groups != C or w.shape[0] % groups:
+        return False
+    if x.dtype not in (torch.bfloat16, torch.float16) or w.dtype != x.dtype:
+        return False
+    if N.lib is None and N._load() is None:
+        return False
+    return bool(N.lib.pa_gconv_ok(*_gc_geo(x, w, groups, stride, pad, dil), N.dtcode(x.dtype)))
+
+
+class _GConvNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, groups, stride, pad, dil):
+        x = x.contiguous()
+        g = _gc_geo(x, w, groups, stride, pad, dil)
+        Nb, H, W, C, Ho, Wo, Cout = g[:7]
+        dt = N.dtcode(x.dtype)
+        y = torch.empty(Nb, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
+        bb = b.to(x.dtype).contiguous() if b is not None else None
+        wf = w.detach().permute(2, 3, 1, 0).contiguous()  # [R][S][Cg][Cout]
+        N.check(N.lib.pa_gconv_fwd(N.ptr(x), N.ptr(wf), N.ptr(bb), N.ptr(y), *g, dt, N.stream()), 'gconv_fwd')
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (groups, stride, pad, dil, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        groups, stride, pad, dil, has_b = ctx.cfg
+        dy = dy.contiguous()
+        g = _gc_geo(x, w, groups, stride, pad, dil)
+        Nb, H, W, C, Ho, Wo, Cout, _, R, S = g[:10]
+        dt = N.dtcode(x.dtype)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x)
+            wd = w.detach().permute(2, 3, 0, 1).contiguous()  # [R][S][Cout][Cg]
+            N.check(N.lib.pa_gconv_dgrad(N.ptr(dy), N.ptr(wd), N.ptr(gx), *g, dt, N.stream()), 'gconv_dgrad')
+        if ctx.needs_input_grad[1]:
+            splits = int(N.lib.pa_gconv_wgrad_splits(Nb, Ho, Wo, Cout, groups, R, S, C))
+            ws = torch.empty(splits * R * S * Cout * (C // groups), dtype=torch.float32, device=x.device)
+            gw = torch.empty(Cout, C // groups, R, S, dtype=x.dtype, device=x.device)
+            N.check(N.lib.pa_gconv_wgrad(N.ptr(x), N.ptr(dy), N.ptr(ws), N.ptr(gw), *g, splits, 0, dt, N.stream()),
+                    'gconv_wgrad')
+            gw = gw.to(w.dtype)
+        if has_b and ctx.needs_input_grad[2]:
+            gb = dy.sum((0, 1, 2), dtype=torch.float32).to(dy.dtype)
+        return gx, gw, gb, None, None, None, None
+
+
+def gconv2d_nhwc(x, w, b, groups, stride, pad, dil):
+    """Grouped conv2d of an NHWC tensor: x [N,H,W,C], w [Cout, C/groups, R, S] -> y [N,Ho,Wo,Cout]."""
+    if N._load() is None:
+        raise RuntimeError("gconv2d_nhwc: HIP kernel library not loaded: " + str(N.load_error))
+    return _GConvNHWC.apply(x, w, b, int(groups), tuple(stride), tuple(pad), tuple(dil))
+
+
 # ---- transposed convolution (reference gpudnn conv_transpose_kernel.cu) on the same kernels
 # conv_transpose2d(x, w) IS the data gradient of conv2d(., w) evaluated at dY = x: the stride-class
 # data-gradient kernel computes it; its input gradient is the conv2d forward of dOut with w and its

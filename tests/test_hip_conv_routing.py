@@ -126,6 +126,51 @@ def test_conv_zero_tap_padding(C, Cout, k, s, p):
     _close(wh.grad, wr.grad, 5e-2, 2e-2, 'wgrad')
 
 
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize('N,H,W,C,Cout,G,k,s,p', [
+    (2, 14, 14, 128, 128, 32, 3, 1, 1), (2, 15, 13, 256, 256, 32, 3, 2, 1), (1, 9, 9, 1024, 1024, 32, 3, 1, 1),
+    (2, 12, 12, 96, 48, 3, 1, 1, 0), (2, 10, 11, 64, 128, 8, 5, 1, 2)])
+@pytest.mark.parametrize('bias', [False, True])
+def test_gconv_fwd_bwd(dt, N, H, W, C, Cout, G, k, s, p, bias):
+    """Grouped conv (csrc/gconv.hip) vs fp32 torch: forward, data and filter gradients (and bias)."""
+    from paddle.ops import conv
+    x = torch.randn(N, H, W, C, device=DEV, dtype=dt)
+    w = (0.2 * torch.randn(Cout, C // G, k, k, device=DEV)).to(dt)
+    b = (0.1 * torch.randn(Cout, device=DEV)).to(dt) if bias else None
+    assert conv.gconv_supported(x, w, G, (s, s), (p, p), (1, 1))
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    wr = w.detach().float().requires_grad_()
+    br = b.detach().float().requires_grad_() if bias else None
+    yr = torch.nn.functional.conv2d(xr, wr, br, s, p, 1, groups=G).permute(0, 2, 3, 1)
+    xh, wh = x.clone().requires_grad_(), w.clone().requires_grad_()
+    bh = b.clone().requires_grad_() if bias else None
+    y = conv.gconv2d_nhwc(xh, wh, bh, G, (s, s), (p, p), (1, 1))
+    assert y.shape == yr.shape
+    _close(y, yr, 3e-2, 1e-2, 'gconv fwd')
+    g = torch.randn_like(yr)
+    y.backward(g.to(dt))
+    yr.backward(g)
+    _close(xh.grad, xr.grad.permute(0, 2, 3, 1), 3e-2, 1e-2, 'gconv dgrad')
+    _close(wh.grad, wr.grad, 5e-2, 2e-2, 'gconv wgrad')
+    if bias:
+        _close(bh.grad, br.grad, 5e-2, 2e-2, 'gconv dbias')
+
+
+def test_resnext_block_nchw_no_miopen():
+    """paddle.nn.functional.conv2d with groups=32 (ResNeXt's grouped 3x3) on NCHW bf16: routed to
+    the grouped kernels, no library convolution kernel forward or backward."""
+    F = paddle.nn.functional
+    x = paddle.to_tensor(torch.randn(4, 128, 16, 16, device=DEV).bfloat16())
+    x.stop_gradient = False
+    w = paddle.to_tensor((0.1 * torch.randn(128, 4, 3, 3, device=DEV)).bfloat16())
+    w.stop_gradient = False
+
+    def run():
+        y = F.conv2d(x, w, padding=1, groups=32)
+        y.sum().backward()
+    assert _miopen_kernels(run) == []
+
+
 def _miopen_kernels(fn):
     """Names of the library (MIOpen) convolution / batch-norm / pooling kernels ``fn`` launches."""
     from torch.profiler import profile, ProfilerActivity
