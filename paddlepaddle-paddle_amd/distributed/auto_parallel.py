@@ -644,6 +644,121 @@ class DistModel:
             for _, sub in list(layer.named_children()):
                 sub.forward = wrap(sub.forward)
         self._mode = 'train' if optimizer is not None and loss is not None else 'predict'
+        # static form: the step is recorded once per (mode, input signature) into a static
+        # Program and replayed by the Executor (reference: to_static builds the distributed
+        # program); the eager step remains for what the program form does not cover
+        self._static_reason = self._static_blocker(layer, optimizer, st)
+        self._progs = {}
+        self._exe = None
+
+    @staticmethod
+    def _static_blocker(layer, optimizer, st):
+        """None when the step can run as a static Program, else why it runs eagerly."""
+        import os
+        if os.environ.get('PADDLE_AMD_DIST_TO_STATIC', '1') == '0':
+            return 'disabled by PADDLE_AMD_DIST_TO_STATIC=0'
+        if st.pipeline.get('enable'):
+            return 'pipeline schedules run eagerly'
+        if st.sharding.get('enable') or isinstance(optimizer, _ShardOptimizer):
+            return 'sharded optimizer states run eagerly'
+        if st.recompute.get('enable'):
+            return 'recompute runs eagerly'
+        if any(is_dist_tensor(p) for p in layer.parameters()):
+            return 'parameters with dist attributes run on the SPMD-propagated eager path'
+        return None
+
+    @property
+    def is_static(self):
+        return self._static_reason is None
+
+    def _dp_of(self, args):
+        """Data-parallel group of the step: the mesh dim the inputs' batch axis is sharded on."""
+        for a in args:
+            m = _dist_meta(a)
+            if m is None:
+                continue
+            mesh, placements, _ = m
+            for d, p in enumerate(placements):
+                if isinstance(p, Shard) and p.dim == 0 and mesh.shape[d] > 1:
+                    _ensure_mesh_groups(mesh)
+                    rank = dist.get_rank() if dist.is_initialized() else 0
+                    c = mesh.coord(rank)
+                    sl = [c[i] if i != d else slice(None) for i in range(mesh.ndim)]
+                    ranks = mesh.mesh[tuple(sl)].reshape(-1).tolist()
+                    import types
+                    return types.SimpleNamespace(pg=_subgroup(ranks), nranks=len(ranks))
+        return None
+
+    def _build_static(self, mode, args):
+        import torch as _t
+        from .. import static as _st
+        from ..static.program import _static_minimize
+        from ..static.minimize import step_policy
+        from .. import framework as _fw
+        vals = [_unwrap(a) if isinstance(a, Tensor) else _t.as_tensor(a) for a in args]
+        was_dynamic = _fw.in_dynamic_mode()
+        if was_dynamic:
+            _fw.enable_static()
+        try:
+            main, startup = _st.Program(), _st.Program()
+            with _st.program_guard(main, startup):
+                dt_name = {_t.float32: 'float32', _t.float16: 'float16', _t.bfloat16: 'bfloat16', _t.int64: 'int64',
+                           _t.int32: 'int32', _t.float64: 'float64', _t.bool: 'bool', _t.uint8: 'uint8'}
+                feeds = [_st.data(f'dm_input_{i}', [-1] + list(v.shape[1:]), dt_name[v.dtype])
+                         for i, v in enumerate(vals)]
+                amp = self._strategy.amp
+                import contextlib
+                if amp.get('enable') and mode != 'train':
+                    from ..amp import auto_cast
+                    ctx = auto_cast(True, level=amp.get('level', 'O2'), dtype=amp.get('dtype', 'bfloat16'))
+                else:
+                    ctx = contextlib.nullcontext()
+                if mode == 'predict':
+                    with ctx:
+                        fetch = self._layer(*feeds)
+                else:
+                    with ctx:
+                        out = self._layer(*feeds[:-1])
+                        fetch = self._loss(out, feeds[-1])
+                    if mode == 'train':
+                        opt = self._opt
+                        if amp.get('enable'):
+                            from ..static import amp as samp
+                            dtype = amp.get('dtype', 'bfloat16')
+                            lists = samp.AutoMixedPrecisionLists(custom_white_list=amp.get('custom_white_list'),
+                                                                 custom_black_list=amp.get('custom_black_list'),
+                                                                 dtype=dtype)
+                            opt = samp.decorate(opt, amp_lists=lists, level=amp.get('level', 'O2'), dtype=dtype)
+                            opt.minimize(fetch)
+                        else:
+                            _static_minimize(opt, fetch)
+                        pol = step_policy(main)
+                        pol.k_steps, pol.avg = self._k, self._avg
+                        pol.dp_group = self._dp_of(args)
+        finally:
+            if was_dynamic:
+                _fw.disable_static()
+        if self._exe is None:
+            self._exe = _st.Executor()
+        plan = (main, [f'dm_input_{i}' for i in range(len(vals))], fetch, self._dp_of(args))
+        return plan
+
+    def _static_call(self, args):
+        import torch as _t
+        key = (self._mode, tuple((tuple(_unwrap(a).shape[1:]), _unwrap(a).dtype) if isinstance(a, Tensor)
+                                 else (type(a),) for a in args))
+        plan = self._progs.get(key)
+        if plan is None:
+            plan = self._progs[key] = self._build_static(self._mode, args)
+        prog, names, fetch, dp = plan
+        feed = {n: (_unwrap(a).detach() if isinstance(a, Tensor) else a) for n, a in zip(names, args)}
+        res = self._exe.run(prog, feed=feed, fetch_list=[fetch], return_numpy=False)[0]
+        if self._mode != 'predict' and dp is not None:
+            # the loss of the global batch: the mean of the data-parallel ranks' local losses
+            r = _unwrap(res).detach().float().clone()
+            dist.all_reduce(r, group=dp.pg)
+            res = _wrap((r / dp.nranks).to(_unwrap(res).dtype))
+        return res
 
     def train(self):
         self._mode = 'train'
@@ -658,6 +773,8 @@ class DistModel:
         self._layer.eval()
 
     def __call__(self, *args):
+        if self._static_reason is None:
+            return self._static_call(args)
         if self._mode == 'predict':
             import torch as _t
             with _t.no_grad():

@@ -314,3 +314,11 @@ def test_static_fleet_pipeline_parallel(sched, mode, nproc):
     send/recv of activations and gradients; every stage's parameters match a single-process run."""
     out = run_workers('worker_static_pp.py', sched, mode, nproc=nproc)
     assert out.count(f'static pp {sched} {mode} OK') == nproc, out[-3000:]
+
+
+@pytest.mark.parametrize('k', [1, 2])
+def test_dist_to_static_program_data_parallel(k):
+    """dist.to_static records the step into a static Program; batch-sharded inputs on 2 ranks
+    give the single-process full-batch result (gradient merge k = 2 too)."""
+    out = run_workers('worker_dist_static.py', str(k))
+    assert out.count(f'dist static k{k} OK') == 2, out[-3000:]

@@ -13,3 +13,7 @@ timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_INSTS_LDS SQ_INSTS_VALU SQ
 python3 tools/pmc_summary.py gpurun_out/pmc_attn > gpurun_out/r4h_attn_pmc.txt 2>&1
 cat gpurun_out/r4h_attn_pmc.txt | head -80
 find gpurun_out/pmc_attn -name "*.csv" -size +2M -delete
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum SQ_WAVES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d gpurun_out/pmc_attn/p3 -o p3 --output-format csv -- python3 tools/attn_pmc.py > gpurun_out/pmc_attn/p3.log 2>&1 || { echo "pass3 failed"; tail -20 gpurun_out/pmc_attn/p3.log; exit 1; }
+python3 tools/pmc_summary.py gpurun_out/pmc_attn > gpurun_out/r4h_attn_pmc.txt 2>&1
+cat gpurun_out/r4h_attn_pmc.txt | head -120
+find gpurun_out/pmc_attn -name "*.csv" -size +2M -delete
