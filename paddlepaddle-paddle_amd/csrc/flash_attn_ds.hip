@@ -66,12 +66,7 @@ __global__ __launch_bounds__(256, 2) void dq_from_ds_kernel(const uint16_t* __re
   constexpr int DB = D / 16;
   constexpr bool BT = (fa_pitch<D>() >= 128);
   constexpr int KT = 64 * fa_pitch<D>() * 2;  // K tile bytes
-  constexpr int STG = KT + 64 * QB * 2;  // one K tile + one dS^T tile
-  // Two LDS stages and two register stages: key block kb + 3 is requested right after block
-  // kb + 1 is written to LDS, so a tile has ~2 key blocks of compute to arrive (one block of
-  // compute is far shorter than the HBM latency: with a single register stage the kernel ran at
-  // 2.9 TB/s; a third register set spilled).
-  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+  __shared__ __attribute__((aligned(16))) char smem[KT + 64 * QB * 2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
@@ -88,7 +83,9 @@ __global__ __launch_bounds__(256, 2) void dq_from_ds_kernel(const uint16_t* __re
   const int off = Sk - Sq;
   const bool vl = EXT && ex.cu_q;
   const uint16_t* kbase = K + (vl ? 0 : (long long)b * ks_.b) + sq_.ko * ks_.s + (long long)hk * ks_.h;
-  const uint16_t* dsbase = dsT + (long long)b * dsb + (long long)h * dsh + q0;
+  // dS^T tiles [64 keys][128 queries] of this query block: tile kb at dshead + kb * tstride
+  const uint16_t* dshead = dsT + (long long)b * dsb + (long long)h * dsh + (long long)qb * 8192;
+  const long long tstride = (long long)(dsld >> 7) * 8192;
   int kend = Sk;
   if (CAUSAL) kend = min(Sk, q0 + QB + off);
   const int nkb = kend > 0 ? (kend + 63) / 64 : 0;
@@ -97,84 +94,60 @@ __global__ __launch_bounds__(256, 2) void dq_from_ds_kernel(const uint16_t* __re
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int d = 0; d < DB; ++d) acc[t][d] = f32x4{0.f, 0.f, 0.f, 0.f};
-  Tile<D, 256> kt0, kt1;
-  Tile<128, 256> st0, st1;  // dS^T tiles: 64 key rows x 128 queries (D = 128 image)
-  kt0.init(kbase, ks_.s);
-  kt1.init(kbase, ks_.s);
-  st0.init(dsbase, dsld);
-  st1.init(dsbase, dsld);
-  // every tile load below is unconditional (index clamped to the last key block, rows to Sk):
-  // guarded loads made the compiler's counted waits drain the whole queue at the join points
-  const int last = max(nkb - 1, 0) * 64;
+  Tile<D, 256> kt;
+  Tile<128, 256> st;  // the dS^T tile: 64 key rows x 128 queries (D = 128 image)
+  kt.init(kbase, ks_.s);
+  st.init(dshead, 128);
   if (nkb > 0) {
-    kt0.load_clamped(0, Sk);
-    st0.load_clamped(0, Sk);
-    kt1.load_clamped(min(64, last), Sk);
-    st1.load_clamped(min(64, last), Sk);
-    kt0.template store<BT>(smem);
-    st0.template store<true>(smem + KT);
-    kt0.load_clamped(min(128, last), Sk);
-    st0.load_clamped(min(128, last), Sk);
-    __syncthreads();
+    kt.load(0, Sk);
+    st.load(0, Sk);
   }
-  // key block kb from LDS stage kb & 1; then block kb + 1 (register set (kb + 1) % 2) into the
-  // other stage (unused after the last block) and block kb + 3 requested into that set
-  auto compute = [&](int kb) {
+  char* k_lds = smem;
+  char* s_lds = smem + KT;
+  for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * 64;
-    const char* k_lds = smem + (kb & 1) * STG;
-    const char* s_lds = k_lds + KT;
-    if (!(CAUSAL && k0 > qw + 16 * NT - 1 + off)) {  // else: whole key block above this wave's rows
-      // dS^T fragments: lane (g, i) of tile t, step s: keys k0 + 32s + 4g + (0..3) / + 16, query qw + 16t + i
-      s16x8 dsf[NT][2];
+    __syncthreads();
+    kt.template store<BT>(k_lds);
+    st.template store<true>(s_lds);
+    __syncthreads();
+    if (kb + 1 < nkb) {
+      kt.load(k0 + 64, Sk);
+      st.init(dshead + (kb + 1) * tstride, 128);
+      st.load(0, Sk - (k0 + 64));
+    }
+    if (CAUSAL && k0 > qw + 16 * NT - 1 + off) continue;  // whole key block above this wave's rows
+    // dS^T fragments: lane (g, i) of tile t, step s: keys k0 + 32s + 4g + (0..3) / + 16, query qw + 16t + i
+    s16x8 dsf[NT][2];
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) dsf[t][s] = ld_tr8<128, true>(s_lds, 32 * s, (qw - q0) / 16 + t, lane);
-      const bool need_mask = (k0 + 64 > Sk) || (CAUSAL && k0 + 63 > qw + off);
-      if (need_mask) {
+      for (int s = 0; s < 2; ++s) dsf[t][s] = ld_tr8<128, true>(s_lds, 32 * s, (qw - q0) / 16 + t, lane);
+    const bool need_mask = (k0 + 64 > Sk) || (CAUSAL && k0 + 63 > qw + off);
+    if (need_mask) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const int q = qw + 16 * t + (lane & 15);
+      for (int t = 0; t < NT; ++t) {
+        const int q = qw + 16 * t + (lane & 15);
 #pragma unroll
-          for (int s = 0; s < 2; ++s)
+        for (int s = 0; s < 2; ++s)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const int key = k0 + 32 * s + 4 * g + (e & 3) + (e >= 4 ? 16 : 0);
-              const bool masked = (key >= Sk) || (CAUSAL && key > q + off);
-              dsf[t][s][e] = masked ? (short)0 : dsf[t][s][e];
-            }
-        }
+          for (int e = 0; e < 8; ++e) {
+            const int key = k0 + 32 * s + 4 * g + (e & 3) + (e >= 4 ? 16 : 0);
+            const bool masked = (key >= Sk) || (CAUSAL && key > q + off);
+            dsf[t][s][e] = masked ? (short)0 : dsf[t][s][e];
+          }
       }
-      // dQ^T += K^T dS^T
+    }
+    // dQ^T += K^T dS^T
 #pragma unroll
-      for (int d = 0; d < DB; ++d) {
+    for (int d = 0; d < DB; ++d) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const s16x8 ka = ld_tr8<D, BT>(k_lds, 32 * s, d, lane);
+      for (int s = 0; s < 2; ++s) {
+        const s16x8 ka = ld_tr8<D, BT>(k_lds, 32 * s, d, lane);
 #pragma unroll
-          for (int t = 0; t < NT; ++t) acc[t][d] = Mfma<T>::run(ka, dsf[t][s], acc[t][d]);
-        }
+        for (int t = 0; t < NT; ++t) acc[t][d] = Mfma<T>::run(ka, dsf[t][s], acc[t][d]);
       }
-    }  // not above the diagonal
-  };
-  // (a macro, not a lambda over Tile references: those pushed the register sets to scratch)
-#define PA_DQ_STEP(KB, KN, SN)                                                   \
-  do {                                                                           \
-    compute(KB);                                                                 \
-    char* nx = smem + (((KB) + 1) & 1) * STG;                                    \
-    KN.template store<BT>(nx);                                                   \
-    SN.template store<true>(nx + KT);                                            \
-    KN.load_clamped(min((KB) * 64 + 192, last), Sk);                             \
-    SN.load_clamped(min((KB) * 64 + 192, last), Sk);                             \
-    __syncthreads();                                                             \
-  } while (0)
-  int kb = 0;
-  for (; kb + 2 <= nkb; kb += 2) {
-    PA_DQ_STEP(kb, kt1, st1);
-    PA_DQ_STEP(kb + 1, kt0, st0);
+    }
   }
-  if (kb < nkb) PA_DQ_STEP(kb, kt1, st1);
-#undef PA_DQ_STEP
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int myq = qw + 16 * t + (lane & 15);
@@ -208,8 +181,12 @@ using namespace pa::fa;
   else if (dt == 2 && D == 64 && !causal) { using T = f16_t; constexpr int DD = 64; constexpr bool CC = false; __VA_ARGS__; }    \
   else return hipErrorInvalidValue;
 
-// dS^T workspace geometry: per (b, h) Sk rows of dsld = ceil(Sq / 128) * 128 elements
+// dS^T workspace geometry: per (b, h) ceil(Sk / 64) x ceil(Sq / 128) tiles of [64][128] elements
+// (dsld = ceil(Sq / 128) * 128 elements per 64-key tile row)
 PA_API int pa_flash_ds_ld(int Sq) { return (Sq + 127) / 128 * 128; }
+PA_API long long pa_flash_ds_ws_elems(int B, int Hq, int Sq, int Sk) {
+  return (long long)B * Hq * ((Sk + 63) / 64 * 64) * pa_flash_ds_ld(Sq);
+}
 
 template <typename T, int DD, bool CC, int F>
 static void bwd_ds(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
@@ -218,7 +195,7 @@ static void bwd_ds(const void* q, const void* k, const void* v, const void* o, c
                    float scale, const Extra& ex, hipStream_t st) {
   constexpr int NW = DD == 128 ? 8 : 4;
   const int dsld = pa_flash_ds_ld(Sq);
-  const long long dsh = (long long)Sk * dsld, dsb = (long long)Hq * dsh;
+  const long long dsh = (long long)((Sk + 63) / 64 * 64) * dsld, dsb = (long long)Hq * dsh;
   delta_kernel<T, DD, F><<<dim3(Hq, B, (Sq + 63) / 64), 256, 0, st>>>((const uint16_t*)o, (const uint16_t*)dout,
                                                                       delta, Sq, Sk, Hq, os, dos, ex);
   bwd_dkdv_kernel<T, DD, CC, 1, NW, F, false, true><<<dim3(Hq, B, (Sk + 16 * NW - 1) / (16 * NW)), 64 * NW, 0, st>>>(
@@ -229,7 +206,7 @@ static void bwd_ds(const void* q, const void* k, const void* v, const void* o, c
 }
 
 // Same contract as pa_flash_bwd_ex (cu_q == null: dense; mask / dropout / flashmask rows optional)
-// plus the dS^T workspace: B * Hq * Sk * pa_flash_ds_ld(Sq) elements of the activation dtype
+// plus the dS^T workspace: pa_flash_ds_ws_elems(B, Hq, Sq, Sk) elements of the activation dtype
 // (varlen: B sequences, Sq / Sk the maximum lengths).
 PA_API hipError_t pa_flash_bwd_ds(const void* q, const void* k, const void* v, const void* o, const void* dout,
                                   const float* lse, float* delta, void* dq, void* dk, void* dv, void* dsT, int B,

@@ -114,21 +114,6 @@ struct Tile {
                                                   : make_uint4(0, 0, 0, 0);
     }
   }
-  // branch-free load (nrows >= 1): rows past nrows re-read row nrows - 1 (finite data the
-  // consumer masks), so the compiler can keep several tiles' loads in flight with counted waits
-  __device__ __forceinline__ void load_clamped(int row0, int nrows) {
-    static_assert(!FLAT, "clamped loads use the row-per-thread mapping");
-    const uint16_t* q = p + (long long)row0 * rs;
-#pragma unroll
-    for (int i = 0; i < NLD; ++i) {
-      const int dr = min(RPL * i, nrows - 1 - row0 - row_in);
-      // through a plain vector type: a uint4 struct copy stayed a memcpy and pinned the register
-      // sets to scratch
-      typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(q + (long long)dr * rs);
-      r[i] = make_uint4(v[0], v[1], v[2], v[3]);
-    }
-  }
   template <bool TR>
   __device__ __forceinline__ void store(char* lds) const {
 #pragma unroll
@@ -607,8 +592,10 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void fwd_kernel(const uint16_
 // PIPE: Q/dO tiles double-buffered in LDS — one barrier per query block instead of two (tile
 // i+1 is written into the other buffer right after block i's compute; its global loads were
 // issued one block earlier).
-// WDS: also store dS^T (bf16/f16, [key][query] rows of ``dsld`` elements per (b, h) at
-// dsT + b * dsb + h * dsh) for the dQ-from-dS kernel (flash_attn_ds.hip).
+// WDS: also store dS^T (bf16/f16) for the dQ-from-dS kernel (flash_attn_ds.hip), per (b, h) at
+// dsT + b * dsb + h * dsh as contiguous [64 keys][128 queries] tiles, tile (key / 64, query / 128) at
+// ((key / 64) * (dsld / 128) + query / 128) * 8192 elements: the dQ kernel reads each tile as one
+// 16 KiB run (row-major [key][dsld] rows 2 KiB apart streamed at 2.5 TB/s).
 template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0, bool PIPE = false, bool WDS = false>
 // (D = 96 with an additive mask needs more than 256 registers: one wave per SIMD there too)
 __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 2) != 0)) ? 1 : 3 - NT) void bwd_dkdv_kernel(
@@ -867,7 +854,8 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 
       for (int j = 0; j < NT; ++j) {
         const int key = kw + 16 * j + (lane & 15);
         if (key < Sk) {
-          uint16_t* row = dsbase + (long long)key * dsld + q0 + 4 * g;
+          uint16_t* row = dsbase + ((long long)(key >> 6) * (dsld >> 7) + (q0 >> 7)) * 8192 + (key & 63) * 128 +
+                          (q0 & 64) + 4 * g;
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) {
             const s16x8 d8 = db_[j][s2];

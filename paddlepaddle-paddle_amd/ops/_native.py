@@ -107,6 +107,7 @@ _SIGS = {
     'pa_flash_set_rng_gen': [P],
     'pa_flash_ds_set_rng_gen': [P],
     'pa_flash_ds_ld': [I],
+    'pa_flash_ds_ws_elems': [I, I, I, I],
     'pa_flash_bwd_ds': [P] * 11 + [I] * 6 + [LLP] * 8 + [F, I, I, P, P, I, P, LL, LL, LL, I, F, U32, U32, P, LL, LL, P],
     'pa_conv2d_wgrad_ok': [I, I],
     'pa_conv2d_dgrad_classes': [P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
@@ -143,7 +144,7 @@ _SIGS = {
                      P],
 }
 
-_LL_RET = {'pa_bn_ws_floats', 'pa_skinny_ws_floats', 'pa_woq_ws_floats'}
+_LL_RET = {'pa_bn_ws_floats', 'pa_skinny_ws_floats', 'pa_woq_ws_floats', 'pa_flash_ds_ws_elems'}
 _VOID_RET = {'pa_adamw_tune', 'pa_act_fwd_tune', 'pa_act_cs_tune'}
 
 

@@ -62,7 +62,7 @@ def _ds_ok(D, dt):
 
 
 def _ds_ws(B, Hq, Sq, Sk, dtype, device):
-    n = B * Hq * Sk * int(N.lib.pa_flash_ds_ld(Sq))
+    n = int(N.lib.pa_flash_ds_ws_elems(B, Hq, Sq, Sk))
     key = (str(device), dtype)
     t = _DS_WS.get(key)
     if t is None or t.numel() < n:
