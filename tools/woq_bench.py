@@ -76,7 +76,7 @@ def sweep():
             x = torch.randn(M, K, device=dev).bfloat16()
             tb = bench(lambda: gemm.skinny_mm(x, wb))
             best = {}
-            for tgt in (128, 256, 512, 1024, 2048):
+            for tgt in (256, 512, 1024, 2048, 4096):
                 for nst in (2, 3, 4):
                     L.pa_woq_tune(tgt, nst)
                     t8 = bench(lambda: woq.woq_linear(x, q8, s8, 8, 0))
