@@ -244,3 +244,42 @@ def test_auto_parallel_engine_fit_evaluate_predict_save_load(tmp_path):
     net[0].weight.set_value(paddle.zeros_like(net[0].weight))
     eng.load(str(tmp_path / 'm'))
     np.testing.assert_allclose(net[0].weight.numpy(), w)
+
+
+def test_dist_to_static_program_matches_eager(monkeypatch):
+    """dist.to_static records train / eval / predict steps into static Programs (one per mode and
+    input signature, Executor replay); losses, predictions and the trained weights equal the eager
+    DistModel's (gradient merge k = 2, ragged batch sizes re-specialise the batch dim)."""
+    import numpy as np
+    import paddle.distributed as dist
+
+    def run(static):
+        monkeypatch.setenv('PADDLE_AMD_DIST_TO_STATIC', '1' if static else '0')
+        paddle.seed(3)
+        net = paddle.nn.Sequential(paddle.nn.Linear(8, 16), paddle.nn.ReLU(), paddle.nn.Linear(16, 4))
+        opt = paddle.optimizer.AdamW(0.01, parameters=net.parameters())
+        st = dist.Strategy()
+        st.gradient_merge.enable = True
+        st.gradient_merge.k_steps = 2
+        dm = dist.to_static(net, None, paddle.nn.CrossEntropyLoss(), opt, st)
+        assert dm.is_static == static
+        rng = np.random.RandomState(0)
+        out = []
+        for i in range(6):
+            n = 5 + (i % 2)
+            x = paddle.to_tensor(rng.randn(n, 8).astype('float32'))
+            y = paddle.to_tensor(rng.randint(0, 4, (n,)).astype('int64'))
+            out.append(float(dm(x, y)))
+        dm.eval()
+        x = paddle.to_tensor(rng.randn(3, 8).astype('float32'))
+        y = paddle.to_tensor(rng.randint(0, 4, (3,)).astype('int64'))
+        out.append(float(dm(x, y)))
+        dm.predict()
+        pred = dm(x).numpy()
+        return out, pred, [p.numpy().copy() for p in net.parameters()]
+
+    a, b = run(True), run(False)
+    np.testing.assert_allclose(a[0], b[0], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(a[1], b[1], rtol=1e-6, atol=1e-7)
+    for p, q in zip(a[2], b[2]):
+        np.testing.assert_allclose(p, q, rtol=1e-6, atol=1e-7)
