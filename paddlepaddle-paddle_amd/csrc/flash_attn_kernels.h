@@ -59,6 +59,20 @@ __device__ __forceinline__ short f2s(float v) {
   return __builtin_bit_cast(short, from_f<T>(v));
 }
 
+// two floats -> one dword of two 16-bit values in ONE v_cvt_pk_{bf16,f16}_f32 (per-element
+// conversions compile to two single converts plus a pack: 3 VALU per pair in the softmax loops)
+typedef float fa_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 fa_bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 fa_f16x2 __attribute__((ext_vector_type(2)));
+template <typename T>
+__device__ __forceinline__ unsigned f2s2(float a, float b) {
+  const fa_f32x2 v = {a, b};
+  if constexpr (__is_same(T, f16_t))
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(v, fa_f16x2));
+  else
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(v, fa_bf16x2));
+}
+
 // LDS row pitch (elements) of a [rows][D] tile: D itself, except D = 96, whose 12-chunk rows are
 // laid out in 16-chunk (D = 128) rows so the XOR swizzles below stay inside the row (the four
 // spare chunks are never written or read; no zero padding of the operands themselves).
@@ -522,13 +536,11 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void fwd_kernel(const uint16_
       }
       // P^T as B operand: k-step s covers keys 32s..32s+31; element j<4 → (16*(2s)+4g+j), j>=4 → (16*(2s+1)+4g+j-4)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pf[t][s][r] = f2s<T>(p[2 * s][r]);
-          pf[t][s][4 + r] = f2s<T>(p[2 * s + 1][r]);
-        }
-      }
+      for (int s = 0; s < 2; ++s)
+        pf[t][s] = __builtin_bit_cast(s16x8, make_uint4(f2s2<T>(p[2 * s][0], p[2 * s][1]),
+                                                        f2s2<T>(p[2 * s][2], p[2 * s][3]),
+                                                        f2s2<T>(p[2 * s + 1][0], p[2 * s + 1][1]),
+                                                        f2s2<T>(p[2 * s + 1][2], p[2 * s + 1][3])));
     }
     // O^T += V^T P^T
 #pragma unroll
@@ -812,6 +824,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 
           hq[2] = (uint32_t)__builtin_amdgcn_mov_dpp(hmine, 0xAA, 0xF, 0xF, false);
           hq[3] = (uint32_t)__builtin_amdgcn_mov_dpp(hmine, 0xFF, 0xF, 0xF, false);
         }
+        float pz[4], dsv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = q0 + 16 * m + 4 * g + r;
@@ -835,10 +848,24 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 
           if constexpr ((EXT & 8) != 0) p = q >= rstart[j] ? 0.f : p;
           float z = 1.f;
           if constexpr ((EXT & 4) != 0) z = drop_sub(ex, hq[r], mykey & 3);
-          const float ds = p * (acc_dp[j][m][r] * z - dlv[r]);
-          pb[j][m >> 1][(m & 1) * 4 + r] = f2s<T>(p * z);
-          db_[j][m >> 1][(m & 1) * 4 + r] = f2s<T>(ds);
+          pz[r] = p * z;
+          dsv[r] = p * (acc_dp[j][m][r] * z - dlv[r]);
         }
+        // elements (m & 1) * 4 + 0..3 of the fragments = dwords (m & 1) * 2, + 1
+        uint4 pu = __builtin_bit_cast(uint4, pb[j][m >> 1]), du = __builtin_bit_cast(uint4, db_[j][m >> 1]);
+        if ((m & 1) == 0) {
+          pu.x = f2s2<T>(pz[0], pz[1]);
+          pu.y = f2s2<T>(pz[2], pz[3]);
+          du.x = f2s2<T>(dsv[0], dsv[1]);
+          du.y = f2s2<T>(dsv[2], dsv[3]);
+        } else {
+          pu.z = f2s2<T>(pz[0], pz[1]);
+          pu.w = f2s2<T>(pz[2], pz[3]);
+          du.z = f2s2<T>(dsv[0], dsv[1]);
+          du.w = f2s2<T>(dsv[2], dsv[3]);
+        }
+        pb[j][m >> 1] = __builtin_bit_cast(s16x8, pu);
+        db_[j][m >> 1] = __builtin_bit_cast(s16x8, du);
       }
     }
     };
@@ -1074,6 +1101,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128) ? 1 : 3 - NT) void bw
           if (myq < Sq) mask_row4<T>(ex, b, h, myq, k0 + 16 * j + 4 * g, Sk, mv);
         uint32_t dbits = 0;
         if constexpr ((EXT & 4) != 0) dbits = drop_bits(ex, b * Hq + h, myq, k0 + 16 * j + 4 * g);
+        float dsv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = k0 + 16 * j + 4 * g + r;
@@ -1087,8 +1115,17 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128) ? 1 : 3 - NT) void bw
             if (key < Sk && myq >= row_start(ex, b, h, key)) p = 0.f;
           float z = 1.f;
           if constexpr ((EXT & 4) != 0) z = drop_sub(ex, dbits, r);
-          dsb[t][j >> 1][(j & 1) * 4 + r] = f2s<T>(p * (acc_dp[t][j][r] * z - dlt[t]));
+          dsv[r] = p * (acc_dp[t][j][r] * z - dlt[t]);
         }
+        uint4 du = __builtin_bit_cast(uint4, dsb[t][j >> 1]);
+        if ((j & 1) == 0) {
+          du.x = f2s2<T>(dsv[0], dsv[1]);
+          du.y = f2s2<T>(dsv[2], dsv[3]);
+        } else {
+          du.z = f2s2<T>(dsv[0], dsv[1]);
+          du.w = f2s2<T>(dsv[2], dsv[3]);
+        }
+        dsb[t][j >> 1] = __builtin_bit_cast(s16x8, du);
       }
     }
     };

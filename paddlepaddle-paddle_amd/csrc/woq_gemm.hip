@@ -24,7 +24,7 @@
 //    to the fp32 accumulator at the end (no per-element multiply); group scales multiply in fp32
 //    before the bf16 pack.
 //  * Up to 2 row tiles of 16 (M <= 32) share each dequantised fragment; NST register stages keep the
-//    next chunks' weight loads in flight; the 4 waves of a block split its K range and are summed
+//    next chunks' weight loads in flight (all loads unconditional, so the waits are counted); the 4 waves of a block split its K range and are summed
 //    through LDS; K splits across blocks go to an fp32 partial buffer summed by the finish kernel
 //    (+ per-channel scale, + bias).
 #include "common.h"
@@ -52,12 +52,19 @@ __device__ __forceinline__ float magic(unsigned d, int b) {
   return __builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B000000u, d, 0x07040400u | (unsigned)b));
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// two floats -> one packed 16-bit pair in ONE v_cvt_pk_{bf16,f16}_f32 (element-wise conversions
+// compiled to two converts plus a pack)
 template <typename T>
 __device__ __forceinline__ unsigned pack2(float a, float b) {
-  Pack<T, 2> p;
-  p.v[0] = (T)a;
-  p.v[1] = (T)b;
-  return __builtin_bit_cast(unsigned, p);
+  const f32x2 v = {a, b};
+  if constexpr (__is_same(T, f16_t))
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(v, f16x2));
+  else
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
 }
 
 // 8 signed values (exact integers, or * s when SCALE) of one MFMA fragment.
@@ -101,13 +108,48 @@ __device__ __forceinline__ s16x8 frag_i4(unsigned d, float s) {
                                               pack2<T>(v[6], v[7])));
 }
 
+// Per-channel-scale path (no group scales): the MFMA runs on the UNSIGNED codes u = q + 128
+// (int8) / q + 8 (int4), exact in bf16 / fp16 (integers <= 256), converted with one
+// v_cvt_f32_ubyte per element (the backend's byte -> float instruction) and one pack per pair: 12
+// VALU per 8 int8 elements instead of 22 with the magic-number form (the kernel was VALU-issue
+// bound: SQ_WAIT_INST_ANY 50 %, profiles/r4j_woq_pmc.txt).  The offset comes back out exactly in
+// the finish kernel: y = s * (sum_k x_k u_k - off * sum_k x_k), from per-row sums of X.
+template <typename T>
+__device__ __forceinline__ s16x8 frag_u8(unsigned lo, unsigned hi) {
+  lo ^= 0x80808080u;  // two's-complement byte q -> unsigned code q + 128
+  hi ^= 0x80808080u;
+  float v[8];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    v[b] = (float)((lo >> (8 * b)) & 0xFFu);
+    v[4 + b] = (float)((hi >> (8 * b)) & 0xFFu);
+  }
+  return __builtin_bit_cast(s16x8, make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
+                                              pack2<T>(v[6], v[7])));
+}
+
+template <typename T>
+__device__ __forceinline__ s16x8 frag_u4(unsigned d) {
+  const unsigned ev = (d & 0x0F0F0F0Fu) ^ 0x08080808u;         // k = 0, 2, 4, 6 (code q + 8)
+  const unsigned od = ((d >> 4) & 0x0F0F0F0Fu) ^ 0x08080808u;  // k = 1, 3, 5, 7
+  float v[8];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    v[2 * b] = (float)((ev >> (8 * b)) & 0xFFu);
+    v[2 * b + 1] = (float)((od >> (8 * b)) & 0xFFu);
+  }
+  return __builtin_bit_cast(s16x8, make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
+                                              pack2<T>(v[6], v[7])));
+}
+
 // grid (ceil(N / 128), KS), 256 threads.  part: fp32 [KS][M][N].  BITS 8 / 4; G = group size (0 =
 // per channel: the scale is applied by the finish kernel).
 template <typename T, int BITS, int MT, int NST, bool GRP>
 __global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X, long long ldx,
                                                   const uint8_t* __restrict__ Wq, long long ldw_bytes,
                                                   const float* __restrict__ gscale, int group,
-                                                  float* __restrict__ part, int M, int N, int K, int kchunk) {
+                                                  float* __restrict__ part, int M, int N, int K, int kchunk,
+                                                  float* __restrict__ xsum) {
   constexpr int KC = BITS == 8 ? 64 : 128;  // k per chunk
   constexpr int NS = KC / 32;                // MFMA steps per chunk
   __shared__ float red[3][MT * 8 * 4][64];
@@ -128,56 +170,90 @@ __global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X
   for (int c = 0; c < 8; ++c) cols[c] = min(n0 + 16 * c + i, N - 1);  // clamped columns are never stored
   uint4 rw[NST][8];
   s16x8 rx[NST][MT][NS];
-  auto load_stage = [&](int st, int k0) {
+  float rs[NST][GRP ? 8 : 1];  // group scales of the stage's k range (GRP)
+  // every load below is unconditional: chunk indices past the wave's range are clamped to its last
+  // chunk (re-read, never used), so the compiler's counted waits retire exactly one stage (guarded
+  // loads made it wait for vmcnt(0) and the register stages never overlapped)
+  const int nch = (kend - kbeg) / KC;  // kbeg..kend is a whole number of chunks
+  auto load_stage = [&](int st, int j) {
+    const int k0 = kbeg + KC * min(j, max(nch - 1, 0));
     const long long kb = BITS == 8 ? (long long)(k0 + 16 * g) : (long long)(k0 / 2 + 16 * g);
 #pragma unroll
     for (int c = 0; c < 8; ++c) rw[st][c] = *reinterpret_cast<const uint4*>(Wq + (long long)cols[c] * ldw_bytes + kb);
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
-      const int m = 16 * t + i;
+      const int m = min(16 * t + i, M - 1);  // rows past M are never stored
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         const int kk = k0 + (BITS == 8 ? 16 : 32) * g + 8 * s;
-        rx[st][t][s] = m < M ? *reinterpret_cast<const s16x8*>(X + (long long)m * ldx + kk)
-                             : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        rx[st][t][s] = *reinterpret_cast<const s16x8*>(X + (long long)m * ldx + kk);
+      }
+    }
+    if constexpr (GRP) {
+      // this lane's k range [k0 + 16g, +16) / [k0 + 32g, +32) lies inside one group (group >= 64)
+      const int gi = (k0 + (BITS == 8 ? 16 : 32) * g) / group;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) rs[st][c] = gscale[(long long)gi * N + cols[c]];
+    }
+  };
+  // !GRP: per-row sums of the X fragments this wave multiplies (column tile 0 only), for the
+  // finish kernel's offset correction
+  float xs[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) xs[t] = 0.f;
+  const bool want_xs = !GRP && blockIdx.x == 0;
+  auto compute = [&](int st) {
+    if (!GRP && want_xs) {
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xs[t] += to_f(__builtin_bit_cast(T, (uint16_t)rx[st][t][s][e]));
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const uint4 q = rw[st][c];
+      const float sc = GRP ? rs[st][GRP ? c : 0] : 1.f;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        s16x8 bf;
+        if constexpr (BITS == 8 && GRP) {
+          bf = s == 0 ? frag_i8<T, GRP>(q.x, q.y, sc) : frag_i8<T, GRP>(q.z, q.w, sc);
+        } else if constexpr (BITS == 8) {
+          bf = s == 0 ? frag_u8<T>(q.x, q.y) : frag_u8<T>(q.z, q.w);
+        } else if constexpr (GRP) {
+          const unsigned d = s == 0 ? q.x : s == 1 ? q.y : s == 2 ? q.z : q.w;
+          bf = frag_i4<T, GRP>(d, sc);
+        } else {
+          const unsigned d = s == 0 ? q.x : s == 1 ? q.y : s == 2 ? q.z : q.w;
+          bf = frag_u4<T>(d);
+        }
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[t][c] = mfma<T>(rx[st][t][s], bf, acc[t][c]);
       }
     }
   };
+  if (nch > 0) {
 #pragma unroll
-  for (int st = 0; st < NST; ++st)
-    if (kbeg + KC * st < kend) load_stage(st, kbeg + KC * st);
-  for (int base = kbeg; base < kend; base += KC * NST) {
+    for (int st = 0; st < NST; ++st) load_stage(st, st);
+  }
+  for (int j = 0; j < nch; j += NST) {
 #pragma unroll
     for (int st = 0; st < NST; ++st) {
-      const int k0 = base + KC * st;
-      if (k0 >= kend) break;
-      float sc[8];
-      if constexpr (GRP) {
-        // this lane's k range [k0 + 16g, +16) / [k0 + 32g, +32) lies inside one group (group >= 64)
-        const int gi = (k0 + (BITS == 8 ? 16 : 32) * g) / group;
+      if (j + st < nch) compute(st);  // wave-uniform; no loads inside
+      load_stage(st, j + st + NST);
+    }
+  }
+  __shared__ float xred[4][MT * 16];
+  if (want_xs) {
+    // lanes (g, i) of row 16t + i: sum over the 4 k-slice groups, then over the 4 waves
 #pragma unroll
-        for (int c = 0; c < 8; ++c) sc[c] = gscale[(long long)gi * N + cols[c]];
-      } else {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) sc[c] = 1.f;
-      }
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const uint4 q = rw[st][c];
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          s16x8 bf;
-          if constexpr (BITS == 8) {
-            bf = s == 0 ? frag_i8<T, GRP>(q.x, q.y, sc[c]) : frag_i8<T, GRP>(q.z, q.w, sc[c]);
-          } else {
-            const unsigned d = s == 0 ? q.x : s == 1 ? q.y : s == 2 ? q.z : q.w;
-            bf = frag_i4<T, GRP>(d, sc[c]);
-          }
-#pragma unroll
-          for (int t = 0; t < MT; ++t) acc[t][c] = mfma<T>(rx[st][t][s], bf, acc[t][c]);
-        }
-      }
-      if (k0 + KC * NST < kend) load_stage(st, k0 + KC * NST);
+    for (int t = 0; t < MT; ++t) {
+      float v = xs[t];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g == 0) xred[w][t * 16 + i] = v;
     }
   }
   if (w > 0) {
@@ -198,6 +274,9 @@ __global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X
       for (int r = 0; r < 4; ++r)
         acc[t][c][r] += red[0][(t * 8 + c) * 4 + r][lane] + red[1][(t * 8 + c) * 4 + r][lane] +
                         red[2][(t * 8 + c) * 4 + r][lane];
+  if (want_xs && lane < MT * 16 && lane < M) {
+    xsum[(long long)blockIdx.y * M + lane] = xred[0][lane] + xred[1][lane] + xred[2][lane] + xred[3][lane];
+  }
   // lane holds C[m = 16t + 4g + r][column n0 + 16c + i]
   float* out = part + (long long)blockIdx.y * M * N;
 #pragma unroll
@@ -215,10 +294,12 @@ __global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X
 }
 
 // Y[m, n] = (sum_s part[s][m][n]) * (cscale ? cscale[n] : 1) (+ bias[n]), 8 columns per thread
+// (xsum != null: the partials are of the unsigned codes; subtract off * sum_s xsum[s][m] first)
 template <typename T>
 __global__ __launch_bounds__(256) void woq_finish(const float* __restrict__ part, int KS, int M, int N,
                                                   const float* __restrict__ cscale, const uint16_t* __restrict__ bias,
-                                                  uint16_t* __restrict__ Y, long long ldy) {
+                                                  uint16_t* __restrict__ Y, long long ldy,
+                                                  const float* __restrict__ xsum, float off) {
   const long long e = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
   if (e >= (long long)M * N) return;
   const int m = (int)(e / N), n = (int)(e - (long long)m * N);
@@ -231,6 +312,12 @@ __global__ __launch_bounds__(256) void woq_finish(const float* __restrict__ part
     const float* p = part + (long long)s * M * N + e;
     const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
     v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+  }
+  if (xsum != nullptr) {
+    float xs = 0.f;
+    for (int s = 0; s < KS; ++s) xs += xsum[(long long)s * M + m];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] -= off * xs;
   }
   if (cscale != nullptr) {
     const float4 a = *reinterpret_cast<const float4*>(cscale + n), b = *reinterpret_cast<const float4*>(cscale + n + 4);
@@ -246,13 +333,17 @@ __global__ __launch_bounds__(256) void woq_finish(const float* __restrict__ part
 }
 
 // tuning knobs (pa_woq_tune): target blocks of the K-split plan, register stages of the M <= 16 kernel
-static int g_target_blocks = 512, g_nst = 3;
+// (graph-timed sweep, profiles/r4n_woq_sweep.log: 2 register stages everywhere; ~256 blocks for wide
+// outputs (>= 100 column tiles: qkv / ffn1 of Llama-2-13B), ~512 for narrow ones; g_target_blocks
+// > 0 overrides both)
+static int g_target_blocks = 0, g_nst = 2;
 
 // K splits: ~g_target_blocks blocks over the 128-column tiles; each split a multiple of 4 waves x chunk
 static void plan(int N, int K, int bits, int& KS, int& kchunk) {
   const int unit = 4 * (bits == 8 ? 64 : 128);
   const int tiles = (N + 127) / 128;
-  int ks = (g_target_blocks + tiles - 1) / tiles;
+  const int target = g_target_blocks > 0 ? g_target_blocks : (tiles >= 100 ? 256 : 512);
+  int ks = (target + tiles - 1) / tiles;
   const int kmax = (K + unit - 1) / unit;
   ks = ks < 1 ? 1 : (ks > kmax ? kmax : ks);
   kchunk = ((K + ks - 1) / ks + unit - 1) / unit * unit;
@@ -261,19 +352,19 @@ static void plan(int N, int K, int bits, int& KS, int& kchunk) {
 
 template <typename T, int BITS, bool GRP>
 static void launch(const void* X, long long ldx, const void* Wq, long long ldwb, const float* gscale, int group,
-                   float* ws, int M, int N, int K, int KS, int kchunk, hipStream_t st) {
+                   float* ws, int M, int N, int K, int KS, int kchunk, float* xsum, hipStream_t st) {
   const dim3 grid((N + 127) / 128, KS);
   const uint16_t* x = (const uint16_t*)X;
   const uint8_t* w = (const uint8_t*)Wq;
   // (a 4-row-tile variant for M <= 64 spills at 256 VGPRs: M > 32 takes the dequantise + GEMM path)
   if (M <= 16 && g_nst == 2)
-    woq_kernel<T, BITS, 1, 2, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk);
+    woq_kernel<T, BITS, 1, 2, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
   else if (M <= 16 && g_nst == 4)
-    woq_kernel<T, BITS, 1, 4, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk);
+    woq_kernel<T, BITS, 1, 4, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
   else if (M <= 16)
-    woq_kernel<T, BITS, 1, 3, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk);
+    woq_kernel<T, BITS, 1, 3, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
   else
-    woq_kernel<T, BITS, 2, 2, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk);
+    woq_kernel<T, BITS, 2, 2, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
 }
 
 }  // namespace woq
@@ -292,11 +383,13 @@ PA_API int pa_woq_ok(int M, int N, int K, long long ldx, long long ldw_bytes, in
   return 1;
 }
 
-// A/B knobs: target block count of the K-split plan (default 512), register stages (2 / 3 / 4) of the
-// M <= 16 kernel (default 3); <= 0 keeps a value.  Returns the previous target.
+// A/B knobs: target block count of the K-split plan (default 0 = by output width), register stages
+// (2 / 3 / 4) of the M <= 16 kernel (default 2); target < 0 restores the width rule, 0 keeps the
+// value, nst <= 0 keeps it.  Returns the previous target.
 PA_API int pa_woq_tune(int target_blocks, int nst) {
   const int old = pa::woq::g_target_blocks;
   if (target_blocks > 0) pa::woq::g_target_blocks = target_blocks;
+  else if (target_blocks < 0) pa::woq::g_target_blocks = 0;
   if (nst > 0) pa::woq::g_nst = nst;
   return old;
 }
@@ -304,7 +397,7 @@ PA_API int pa_woq_tune(int target_blocks, int nst) {
 PA_API long long pa_woq_ws_floats(int M, int N, int K, int bits) {
   int KS, kc;
   pa::woq::plan(N, K, bits, KS, kc);
-  return (long long)KS * M * N;
+  return (long long)KS * M * N + (long long)KS * M;  // partials + per-split row sums of X
 }
 
 PA_API int pa_woq_gemm(const void* X, const void* Wq, const float* scale, const void* bias, void* Y, float* ws, int M,
@@ -316,15 +409,18 @@ PA_API int pa_woq_gemm(const void* X, const void* Wq, const float* scale, const 
   int KS, kchunk;
   plan(N, K, bits, KS, kchunk);
   const bool grp = group != 0;
+  float* xsum = ws + (long long)KS * M * N;
 #define WOQ_DISPATCH(T)                                                                                        \
   do {                                                                                                         \
-    if (bits == 8 && grp) launch<T, 8, true>(X, ldx, Wq, ldw_bytes, scale, group, ws, M, N, K, KS, kchunk, st);  \
-    else if (bits == 8) launch<T, 8, false>(X, ldx, Wq, ldw_bytes, scale, 0, ws, M, N, K, KS, kchunk, st);       \
-    else if (grp) launch<T, 4, true>(X, ldx, Wq, ldw_bytes, scale, group, ws, M, N, K, KS, kchunk, st);          \
-    else launch<T, 4, false>(X, ldx, Wq, ldw_bytes, scale, 0, ws, M, N, K, KS, kchunk, st);                      \
+    if (bits == 8 && grp) launch<T, 8, true>(X, ldx, Wq, ldw_bytes, scale, group, ws, M, N, K, KS, kchunk, xsum, st); \
+    else if (bits == 8) launch<T, 8, false>(X, ldx, Wq, ldw_bytes, scale, 0, ws, M, N, K, KS, kchunk, xsum, st);      \
+    else if (grp) launch<T, 4, true>(X, ldx, Wq, ldw_bytes, scale, group, ws, M, N, K, KS, kchunk, xsum, st);         \
+    else launch<T, 4, false>(X, ldx, Wq, ldw_bytes, scale, 0, ws, M, N, K, KS, kchunk, xsum, st);                     \
     const long long groups = ((long long)M * N + 7) / 8;                                                       \
     woq_finish<T><<<(unsigned)((groups + 255) / 256), 256, 0, st>>>(ws, KS, M, N, grp ? nullptr : scale,       \
-                                                                     (const uint16_t*)bias, (uint16_t*)Y, ldy); \
+                                                                     (const uint16_t*)bias, (uint16_t*)Y, ldy,  \
+                                                                     grp ? nullptr : xsum,                      \
+                                                                     bits == 8 ? 128.f : 8.f);                  \
   } while (0)
   if (dt == 1) WOQ_DISPATCH(pa::bf16_t);
   else WOQ_DISPATCH(pa::f16_t);

@@ -89,7 +89,7 @@ def sweep():
             print(f"{name:5s} M={M:2d} bf16 {tb*1e6:6.1f} us | best int8 {best[8][0]*1e6:6.1f} us ({tb/best[8][0]:4.2f}x, "
                   f"target {best[8][1]} nst {best[8][2]}) | best int4 {best[4][0]*1e6:6.1f} us "
                   f"({tb/best[4][0]:4.2f}x, target {best[4][1]} nst {best[4][2]})", flush=True)
-    L.pa_woq_tune(512, 3)
+    L.pa_woq_tune(-1, 2)
 
 
 if __name__ == '__main__':
