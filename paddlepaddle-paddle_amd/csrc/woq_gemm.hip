@@ -144,7 +144,7 @@ __device__ __forceinline__ s16x8 frag_u4(unsigned d) {
 
 // grid (ceil(N / 128), KS), 256 threads.  part: fp32 [KS][M][N].  BITS 8 / 4; G = group size (0 =
 // per channel: the scale is applied by the finish kernel).
-template <typename T, int BITS, int MT, int NST, bool GRP>
+template <typename T, int BITS, int MT, int NST, bool GRP, int CT = 8>
 __global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X, long long ldx,
                                                   const uint8_t* __restrict__ Wq, long long ldw_bytes,
                                                   const float* __restrict__ gscale, int group,
@@ -152,25 +152,25 @@ __global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X
                                                   float* __restrict__ xsum) {
   constexpr int KC = BITS == 8 ? 64 : 128;  // k per chunk
   constexpr int NS = KC / 32;                // MFMA steps per chunk
-  __shared__ float red[3][MT * 8 * 4][64];
+  __shared__ float red[3][MT * CT * 4][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int n0 = blockIdx.x * 128;
+  const int n0 = blockIdx.x * 16 * CT;
   const int kw = kchunk / 4;  // per wave, a multiple of KC
   const int kbeg = blockIdx.y * kchunk + w * kw;
   const int kend = min(K, kbeg + kw);
   const int g = lane >> 4, i = lane & 15;
-  f32x4 acc[MT][8];
+  f32x4 acc[MT][CT];
 #pragma unroll
   for (int t = 0; t < MT; ++t)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int cols[8];
+    for (int c = 0; c < CT; ++c) acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int cols[CT];
 #pragma unroll
-  for (int c = 0; c < 8; ++c) cols[c] = min(n0 + 16 * c + i, N - 1);  // clamped columns are never stored
-  uint4 rw[NST][8];
+  for (int c = 0; c < CT; ++c) cols[c] = min(n0 + 16 * c + i, N - 1);  // clamped columns are never stored
+  uint4 rw[NST][CT];
   s16x8 rx[NST][MT][NS];
-  float rs[NST][GRP ? 8 : 1];  // group scales of the stage's k range (GRP)
+  float rs[NST][GRP ? CT : 1];  // group scales of the stage's k range (GRP)
   // every load below is unconditional: chunk indices past the wave's range are clamped to its last
   // chunk (re-read, never used), so the compiler's counted waits retire exactly one stage (guarded
   // loads made it wait for vmcnt(0) and the register stages never overlapped)
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X
     const int k0 = kbeg + KC * min(j, max(nch - 1, 0));
     const long long kb = BITS == 8 ? (long long)(k0 + 16 * g) : (long long)(k0 / 2 + 16 * g);
 #pragma unroll
-    for (int c = 0; c < 8; ++c) rw[st][c] = *reinterpret_cast<const uint4*>(Wq + (long long)cols[c] * ldw_bytes + kb);
+    for (int c = 0; c < CT; ++c) rw[st][c] = *reinterpret_cast<const uint4*>(Wq + (long long)cols[c] * ldw_bytes + kb);
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const int m = min(16 * t + i, M - 1);  // rows past M are never stored
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X
       // this lane's k range [k0 + 16g, +16) / [k0 + 32g, +32) lies inside one group (group >= 64)
       const int gi = (k0 + (BITS == 8 ? 16 : 32) * g) / group;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) rs[st][c] = gscale[(long long)gi * N + cols[c]];
+      for (int c = 0; c < CT; ++c) rs[st][c] = gscale[(long long)gi * N + cols[c]];
     }
   };
   // !GRP: per-row sums of the X fragments this wave multiplies (column tile 0 only), for the
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X
           for (int e = 0; e < 8; ++e) xs[t] += to_f(__builtin_bit_cast(T, (uint16_t)rx[st][t][s][e]));
     }
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < CT; ++c) {
       const uint4 q = rw[st][c];
       const float sc = GRP ? rs[st][GRP ? c : 0] : 1.f;
 #pragma unroll
@@ -260,20 +260,20 @@ __global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X
 #pragma unroll
     for (int t = 0; t < MT; ++t)
 #pragma unroll
-      for (int c = 0; c < 8; ++c)
+      for (int c = 0; c < CT; ++c)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) red[w - 1][(t * 8 + c) * 4 + r][lane] = acc[t][c][r];
+        for (int r = 0; r < 4; ++r) red[w - 1][(t * CT + c) * 4 + r][lane] = acc[t][c][r];
   }
   __syncthreads();
   if (w != 0) return;
 #pragma unroll
   for (int t = 0; t < MT; ++t)
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
+    for (int c = 0; c < CT; ++c)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        acc[t][c][r] += red[0][(t * 8 + c) * 4 + r][lane] + red[1][(t * 8 + c) * 4 + r][lane] +
-                        red[2][(t * 8 + c) * 4 + r][lane];
+        acc[t][c][r] += red[0][(t * CT + c) * 4 + r][lane] + red[1][(t * CT + c) * 4 + r][lane] +
+                        red[2][(t * CT + c) * 4 + r][lane];
   if (want_xs && lane < MT * 16 && lane < M) {
     xsum[(long long)blockIdx.y * M + lane] = xred[0][lane] + xred[1][lane] + xred[2][lane] + xred[3][lane];
   }
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X
       const int m = 16 * t + 4 * g + r;
       if (m >= M) continue;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
+      for (int c = 0; c < CT; ++c) {
         const int col = n0 + 16 * c + i;
         if (col < N) out[(long long)m * N + col] = acc[t][c][r];
       }
@@ -339,9 +339,13 @@ __global__ __launch_bounds__(256) void woq_finish(const float* __restrict__ part
 static int g_target_blocks = 0, g_nst = 2;
 
 // K splits: ~g_target_blocks blocks over the 128-column tiles; each split a multiple of 4 waves x chunk
-static void plan(int N, int K, int bits, int& KS, int& kchunk) {
+static int g_ct = 8;  // 16-column tiles per wave of the M <= 16 kernel (8 = 128 columns per block, 4 = 64)
+static int eff_ct(int M) { return M <= 16 ? g_ct : 8; }
+
+static void plan(int N, int K, int bits, int M, int& KS, int& kchunk) {
   const int unit = 4 * (bits == 8 ? 64 : 128);
-  const int tiles = (N + 127) / 128;
+  const int ct = eff_ct(M);
+  const int tiles = (N + 16 * ct - 1) / (16 * ct);
   const int target = g_target_blocks > 0 ? g_target_blocks : (tiles >= 100 ? 256 : 512);
   int ks = (target + tiles - 1) / tiles;
   const int kmax = (K + unit - 1) / unit;
@@ -353,11 +357,17 @@ static void plan(int N, int K, int bits, int& KS, int& kchunk) {
 template <typename T, int BITS, bool GRP>
 static void launch(const void* X, long long ldx, const void* Wq, long long ldwb, const float* gscale, int group,
                    float* ws, int M, int N, int K, int KS, int kchunk, float* xsum, hipStream_t st) {
-  const dim3 grid((N + 127) / 128, KS);
+  const dim3 grid((N + 16 * eff_ct(M) - 1) / (16 * eff_ct(M)), KS);
   const uint16_t* x = (const uint16_t*)X;
   const uint8_t* w = (const uint8_t*)Wq;
   // (a 4-row-tile variant for M <= 64 spills at 256 VGPRs: M > 32 takes the dequantise + GEMM path)
-  if (M <= 16 && g_nst == 2)
+  if (M <= 16 && g_ct == 4 && g_nst == 4)
+    woq_kernel<T, BITS, 1, 4, GRP, 4><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
+  else if (M <= 16 && g_ct == 4 && g_nst == 3)
+    woq_kernel<T, BITS, 1, 3, GRP, 4><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
+  else if (M <= 16 && g_ct == 4)
+    woq_kernel<T, BITS, 1, 2, GRP, 4><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
+  else if (M <= 16 && g_nst == 2)
     woq_kernel<T, BITS, 1, 2, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
   else if (M <= 16 && g_nst == 4)
     woq_kernel<T, BITS, 1, 4, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
@@ -394,9 +404,16 @@ PA_API int pa_woq_tune(int target_blocks, int nst) {
   return old;
 }
 
+// A/B knob: 16-column tiles per wave of the M <= 16 kernel (4 or 8); returns the previous value
+PA_API int pa_woq_set_ct(int ct) {
+  const int old = pa::woq::g_ct;
+  if (ct == 4 || ct == 8) pa::woq::g_ct = ct;
+  return old;
+}
+
 PA_API long long pa_woq_ws_floats(int M, int N, int K, int bits) {
   int KS, kc;
-  pa::woq::plan(N, K, bits, KS, kc);
+  pa::woq::plan(N, K, bits, M, KS, kc);
   return (long long)KS * M * N + (long long)KS * M;  // partials + per-split row sums of X
 }
 
@@ -407,7 +424,7 @@ PA_API int pa_woq_gemm(const void* X, const void* Wq, const float* scale, const 
   if (!pa_woq_ok(M, N, K, ldx, ldw_bytes, bits, group, dt) || ws == nullptr || scale == nullptr || ldy % 8)
     return (int)hipErrorInvalidValue;
   int KS, kchunk;
-  plan(N, K, bits, KS, kchunk);
+  plan(N, K, bits, M, KS, kchunk);
   const bool grp = group != 0;
   float* xsum = ws + (long long)KS * M * N;
 #define WOQ_DISPATCH(T)                                                                                        \

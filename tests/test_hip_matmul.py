@@ -212,9 +212,19 @@ def test_fp8_8phase_gemm(M, N, K, fmts):
 @pytest.mark.parametrize('bits,group', [(8, -1), (8, 64), (8, 128), (4, -1), (4, 64), (4, 128)])
 @pytest.mark.parametrize('M', [1, 7, 16, 32])
 @pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16])
-def test_weight_only_linear_kernel(bits, group, M, dt):
+@pytest.mark.parametrize('ct', [8, 4])
+def test_weight_only_linear_kernel(bits, group, M, dt, ct):
     """weight_only_linear on the W8A16 / W4A16 decode kernel (csrc/woq_gemm.hip) vs the fp32 product
-    with the dequantised weight (Llama-2-13B-like widths scaled down)."""
+    with the dequantised weight (Llama-2-13B-like widths scaled down); both column-tile widths."""
+    from paddle.ops import _native
+    old_ct = _native.lib.pa_woq_set_ct(ct)
+    try:
+        _woq_case(bits, group, M, dt)
+    finally:
+        _native.lib.pa_woq_set_ct(old_ct)
+
+
+def _woq_case(bits, group, M, dt):
     from paddle.nn.quant import weight_quantize, weight_only_linear
     g = torch.Generator(device=DEV).manual_seed(11)
     K, N_ = 2560, 1152

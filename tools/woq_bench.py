@@ -76,20 +76,23 @@ def sweep():
             x = torch.randn(M, K, device=dev).bfloat16()
             tb = bench(lambda: gemm.skinny_mm(x, wb))
             best = {}
-            for tgt in (256, 512, 1024, 2048, 4096):
-                for nst in (2, 3, 4):
+            for ct, tgt, nst in [(8, t, n) for t in (256, 512, 1024) for n in (2, 3)] + \
+                    [(4, t, n) for t in (256, 512, 1024) for n in (2, 3, 4)]:
+                L.pa_woq_set_ct(ct)
+                if True:
                     L.pa_woq_tune(tgt, nst)
                     t8 = bench(lambda: woq.woq_linear(x, q8, s8, 8, 0))
                     t4 = bench(lambda: woq.woq_linear(x, q4, s4, 4, 0))
-                    print(f"{name:5s} M={M:2d} target {tgt:5d} nst {nst}: int8 {t8*1e6:6.1f} us ({tb/t8:4.2f}x) "
+                    print(f"{name:5s} M={M:2d} ct {ct} target {tgt:5d} nst {nst}: int8 {t8*1e6:6.1f} us ({tb/t8:4.2f}x) "
                           f"int4 {t4*1e6:6.1f} us ({tb/t4:4.2f}x)", flush=True)
                     for b, t in ((8, t8), (4, t4)):
                         if b not in best or t < best[b][0]:
-                            best[b] = (t, tgt, nst)
+                            best[b] = (t, f'{ct}/{tgt}', nst)
             print(f"{name:5s} M={M:2d} bf16 {tb*1e6:6.1f} us | best int8 {best[8][0]*1e6:6.1f} us ({tb/best[8][0]:4.2f}x, "
                   f"target {best[8][1]} nst {best[8][2]}) | best int4 {best[4][0]*1e6:6.1f} us "
                   f"({tb/best[4][0]:4.2f}x, target {best[4][1]} nst {best[4][2]})", flush=True)
     L.pa_woq_tune(-1, 2)
+    L.pa_woq_set_ct(8)
 
 
 if __name__ == '__main__':
