@@ -333,20 +333,23 @@ __global__ __launch_bounds__(256) void woq_finish(const float* __restrict__ part
 }
 
 // tuning knobs (pa_woq_tune): target blocks of the K-split plan, register stages of the M <= 16 kernel
-// (graph-timed sweep, profiles/r4n_woq_sweep.log: 2 register stages everywhere; ~256 blocks for wide
-// outputs (>= 100 column tiles: qkv / ffn1 of Llama-2-13B), ~512 for narrow ones; g_target_blocks
-// > 0 overrides both)
+// (graph-timed sweeps, profiles/r4n_woq_sweep.log / r4p_woq_sweep.log: 2 register stages and ~256
+// blocks at M <= 16; for the M <= 32 kernel ~256 blocks on wide outputs (>= 100 column tiles), ~512 on
+// narrow ones; g_target_blocks > 0 overrides)
 static int g_target_blocks = 0, g_nst = 2;
 
 // K splits: ~g_target_blocks blocks over the 128-column tiles; each split a multiple of 4 waves x chunk
-static int g_ct = 8;  // 16-column tiles per wave of the M <= 16 kernel (8 = 128 columns per block, 4 = 64)
+// 16-column tiles per wave of the M <= 16 kernel (8 = 128 columns per block, 4 = 64, 2 = 32): narrower
+// tiles mean fewer registers per wave, more waves and more independent dequant chains in flight —
+// 4 beat 8 on every Llama-2-13B shape (int8 ffn1 1.60x vs 1.42x the bf16 skinny GEMM, profiles/r4p_woq_sweep.log)
+static int g_ct = 4;
 static int eff_ct(int M) { return M <= 16 ? g_ct : 8; }
 
 static void plan(int N, int K, int bits, int M, int& KS, int& kchunk) {
   const int unit = 4 * (bits == 8 ? 64 : 128);
   const int ct = eff_ct(M);
   const int tiles = (N + 16 * ct - 1) / (16 * ct);
-  const int target = g_target_blocks > 0 ? g_target_blocks : (tiles >= 100 ? 256 : 512);
+  const int target = g_target_blocks > 0 ? g_target_blocks : (M <= 16 ? 256 : (tiles >= 100 ? 256 : 512));
   int ks = (target + tiles - 1) / tiles;
   const int kmax = (K + unit - 1) / unit;
   ks = ks < 1 ? 1 : (ks > kmax ? kmax : ks);
@@ -361,7 +364,9 @@ static void launch(const void* X, long long ldx, const void* Wq, long long ldwb,
   const uint16_t* x = (const uint16_t*)X;
   const uint8_t* w = (const uint8_t*)Wq;
   // (a 4-row-tile variant for M <= 64 spills at 256 VGPRs: M > 32 takes the dequantise + GEMM path)
-  if (M <= 16 && g_ct == 4 && g_nst == 4)
+  if (M <= 16 && g_ct == 2)
+    woq_kernel<T, BITS, 1, 2, GRP, 2><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
+  else if (M <= 16 && g_ct == 4 && g_nst == 4)
     woq_kernel<T, BITS, 1, 4, GRP, 4><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
   else if (M <= 16 && g_ct == 4 && g_nst == 3)
     woq_kernel<T, BITS, 1, 3, GRP, 4><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
@@ -407,7 +412,7 @@ PA_API int pa_woq_tune(int target_blocks, int nst) {
 // A/B knob: 16-column tiles per wave of the M <= 16 kernel (4 or 8); returns the previous value
 PA_API int pa_woq_set_ct(int ct) {
   const int old = pa::woq::g_ct;
-  if (ct == 4 || ct == 8) pa::woq::g_ct = ct;
+  if (ct == 2 || ct == 4 || ct == 8) pa::woq::g_ct = ct;
   return old;
 }
 

@@ -76,8 +76,7 @@ def sweep():
             x = torch.randn(M, K, device=dev).bfloat16()
             tb = bench(lambda: gemm.skinny_mm(x, wb))
             best = {}
-            for ct, tgt, nst in [(8, t, n) for t in (256, 512, 1024) for n in (2, 3)] + \
-                    [(4, t, n) for t in (256, 512, 1024) for n in (2, 3, 4)]:
+            for ct, tgt, nst in [(4, t, 2) for t in (256, 512)] + [(2, t, 2) for t in (128, 256, 512, 1024)]:
                 L.pa_woq_set_ct(ct)
                 if True:
                     L.pa_woq_tune(tgt, nst)
@@ -92,7 +91,7 @@ def sweep():
                   f"target {best[8][1]} nst {best[8][2]}) | best int4 {best[4][0]*1e6:6.1f} us "
                   f"({tb/best[4][0]:4.2f}x, target {best[4][1]} nst {best[4][2]})", flush=True)
     L.pa_woq_tune(-1, 2)
-    L.pa_woq_set_ct(8)
+    L.pa_woq_set_ct(4)
 
 
 if __name__ == '__main__':
