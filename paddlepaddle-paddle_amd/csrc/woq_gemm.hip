@@ -340,16 +340,18 @@ static int g_target_blocks = 0, g_nst = 2;
 
 // K splits: ~g_target_blocks blocks over the 128-column tiles; each split a multiple of 4 waves x chunk
 // 16-column tiles per wave of the M <= 16 kernel (8 = 128 columns per block, 4 = 64, 2 = 32): narrower
-// tiles mean fewer registers per wave, more waves and more independent dequant chains in flight —
-// 4 beat 8 on every Llama-2-13B shape (int8 ffn1 1.60x vs 1.42x the bf16 skinny GEMM, profiles/r4p_woq_sweep.log)
-static int g_ct = 4;
-static int eff_ct(int M) { return M <= 16 ? g_ct : 8; }
+// tiles mean fewer registers per wave, more waves and more independent dequant chains in flight.
+// Automatic (g_ct = 0): 2 at M <= 4, 4 at M <= 16 — graph-timed on the Llama-2-13B shapes, M = 1
+// int8 1.38-1.60x / int4 1.50-2.07x the bf16 skinny GEMM (profiles/r4q_woq_sweep.log).
+static int g_ct = 0;
+static int eff_ct(int M) { return M > 16 ? 8 : (g_ct ? g_ct : (M <= 4 ? 2 : 4)); }
 
 static void plan(int N, int K, int bits, int M, int& KS, int& kchunk) {
   const int unit = 4 * (bits == 8 ? 64 : 128);
   const int ct = eff_ct(M);
   const int tiles = (N + 16 * ct - 1) / (16 * ct);
-  const int target = g_target_blocks > 0 ? g_target_blocks : (M <= 16 ? 256 : (tiles >= 100 ? 256 : 512));
+  const int target = g_target_blocks > 0 ? g_target_blocks
+                                          : (M <= 4 ? (K > 8192 ? 512 : 128) : (M <= 16 || tiles >= 100 ? 256 : 512));
   int ks = (target + tiles - 1) / tiles;
   const int kmax = (K + unit - 1) / unit;
   ks = ks < 1 ? 1 : (ks > kmax ? kmax : ks);
@@ -364,13 +366,14 @@ static void launch(const void* X, long long ldx, const void* Wq, long long ldwb,
   const uint16_t* x = (const uint16_t*)X;
   const uint8_t* w = (const uint8_t*)Wq;
   // (a 4-row-tile variant for M <= 64 spills at 256 VGPRs: M > 32 takes the dequantise + GEMM path)
-  if (M <= 16 && g_ct == 2)
+  const int ct = eff_ct(M);
+  if (M <= 16 && ct == 2)
     woq_kernel<T, BITS, 1, 2, GRP, 2><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
-  else if (M <= 16 && g_ct == 4 && g_nst == 4)
+  else if (M <= 16 && ct == 4 && g_nst == 4)
     woq_kernel<T, BITS, 1, 4, GRP, 4><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
-  else if (M <= 16 && g_ct == 4 && g_nst == 3)
+  else if (M <= 16 && ct == 4 && g_nst == 3)
     woq_kernel<T, BITS, 1, 3, GRP, 4><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
-  else if (M <= 16 && g_ct == 4)
+  else if (M <= 16 && ct == 4)
     woq_kernel<T, BITS, 1, 2, GRP, 4><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
   else if (M <= 16 && g_nst == 2)
     woq_kernel<T, BITS, 1, 2, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
@@ -409,10 +412,11 @@ PA_API int pa_woq_tune(int target_blocks, int nst) {
   return old;
 }
 
-// A/B knob: 16-column tiles per wave of the M <= 16 kernel (4 or 8); returns the previous value
+// A/B knob: 16-column tiles per wave of the M <= 16 kernel (2 / 4 / 8; 0 = automatic by M); returns
+// the previous value
 PA_API int pa_woq_set_ct(int ct) {
   const int old = pa::woq::g_ct;
-  if (ct == 2 || ct == 4 || ct == 8) pa::woq::g_ct = ct;
+  if (ct == 0 || ct == 2 || ct == 4 || ct == 8) pa::woq::g_ct = ct;
   return old;
 }
 

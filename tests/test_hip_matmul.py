@@ -212,7 +212,7 @@ def test_fp8_8phase_gemm(M, N, K, fmts):
 @pytest.mark.parametrize('bits,group', [(8, -1), (8, 64), (8, 128), (4, -1), (4, 64), (4, 128)])
 @pytest.mark.parametrize('M', [1, 7, 16, 32])
 @pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize('ct', [8, 4, 2])
+@pytest.mark.parametrize('ct', [0, 8, 4, 2])
 def test_weight_only_linear_kernel(bits, group, M, dt, ct):
     """weight_only_linear on the W8A16 / W4A16 decode kernel (csrc/woq_gemm.hip) vs the fp32 product
     with the dequantised weight (Llama-2-13B-like widths scaled down); both column-tile widths."""

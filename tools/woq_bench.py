@@ -91,7 +91,7 @@ def sweep():
                   f"target {best[8][1]} nst {best[8][2]}) | best int4 {best[4][0]*1e6:6.1f} us "
                   f"({tb/best[4][0]:4.2f}x, target {best[4][1]} nst {best[4][2]})", flush=True)
     L.pa_woq_tune(-1, 2)
-    L.pa_woq_set_ct(4)
+    L.pa_woq_set_ct(0)
 
 
 if __name__ == '__main__':
