@@ -181,6 +181,15 @@ using namespace pa::fa;
   else if (dt == 2 && D == 64 && !causal) { using T = f16_t; constexpr int DD = 64; constexpr bool CC = false; __VA_ARGS__; }    \
   else return hipErrorInvalidValue;
 
+// block order of this module's kernels (pair_order's G; the module has its own copy of the
+// constant): returns the previous value
+PA_API int pa_flash_ds_set_pair_group(int v) {
+  int old = 0;
+  (void)hipMemcpyFromSymbol(&old, HIP_SYMBOL(pa::fa::g_pair_group), sizeof(int));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(pa::fa::g_pair_group), &v, sizeof(int));
+  return old;
+}
+
 // dS^T workspace geometry: per (b, h) ceil(Sk / 64) x ceil(Sq / 128) tiles of [64][128] elements
 // (dsld = ceil(Sq / 128) * 128 elements per 64-key tile row)
 PA_API int pa_flash_ds_ld(int Sq) { return (Sq + 127) / 128 * 128; }

@@ -109,6 +109,7 @@ _SIGS = {
     'pa_flash_ds_set_rng_gen': [P],
     'pa_flash_ds_ld': [I],
     'pa_flash_ds_ws_elems': [I, I, I, I],
+    'pa_flash_ds_set_pair_group': [I],
     'pa_flash_bwd_ds': [P] * 11 + [I] * 6 + [LLP] * 8 + [F, I, I, P, P, I, P, LL, LL, LL, I, F, U32, U32, P, LL, LL, P],
     'pa_conv2d_wgrad_ok': [I, I],
     'pa_conv2d_dgrad_classes': [P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P, P],

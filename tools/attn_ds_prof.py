@@ -14,6 +14,8 @@ def main():
     from paddle.ops import _native
     _native._load()
     ops.flash_attn.set_ds_backward(sys.argv[1] == 'ds')
+    if len(sys.argv) > 2:  # block-order group of the dS module (pair_order G)
+        _native.lib.pa_flash_ds_set_pair_group(int(sys.argv[2]))
     qkv = torch.randn(16, 1024, 3, 16, 128, device='cuda', dtype=torch.bfloat16, requires_grad=True)
     g = torch.randn(16, 1024, 16, 128, device='cuda', dtype=torch.bfloat16)
     for _ in range(12):
