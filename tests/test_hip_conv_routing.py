@@ -315,3 +315,31 @@ def test_conv1d_routed(cl):
     ref = torch.nn.functional.conv1d(x.float(), w.float(), None, 2, 1)
     y = out['y']
     _close(y.permute(0, 2, 1) if cl else y, ref, 3e-2, 1e-2, 'conv1d')
+
+
+def test_resnext50_nchw_training_step_no_miopen():
+    """paddle.vision.models.resnext50_32x4d() (default NCHW, grouped 3x3 convolutions with 4..32
+    channels per group) trains an AMP-O2 bf16 step with no library convolution / batch-norm /
+    pooling kernel, and its loss is finite."""
+    from paddle.vision.models import resnext50_32x4d
+    paddle.seed(5)
+    net = resnext50_32x4d(num_classes=10)
+    opt = paddle.optimizer.Momentum(learning_rate=0.01, momentum=0.9, parameters=net.parameters(),
+                                    multi_precision=True)
+    net, opt = paddle.amp.decorate(net, opt, level='O2', dtype='bfloat16')
+    g = torch.Generator(device=DEV).manual_seed(3)
+    xin = paddle.to_tensor(torch.randn(2, 3, 64, 64, device=DEV, generator=g).bfloat16())
+    y = paddle.to_tensor(torch.randint(0, 10, (2,), device=DEV, generator=g))
+    vals = []
+
+    def step():
+        loss = paddle.nn.functional.cross_entropy(net(xin), y)
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        vals.append(float(loss))
+
+    step()
+    bad = _miopen_kernels(step)
+    assert bad == [], bad
+    assert all(v == v and abs(v) < 1e4 for v in vals), vals
