@@ -37,6 +37,9 @@ __device__ uint4 g_zero16[4];
 struct Geom {
   int N, H, W, C, Ho, Wo, Cout, R, S, sh, sw, ph, pw, dh, dw;
   long long total;  // input elements (im2col bounds; 0 elsewhere)
+  // forward only: channels as STORED in X when the K decomposition uses C padded to a multiple of
+  // 32 (C % 32 != 0, C % 8 == 0: the padded 8-channel chunks read the zero block); 0 = C
+  int Cs;
 };
 
 // Filter taps of the implicit GEMM (k = (tap, c)): input row/col offsets of each tap, so a kernel
@@ -128,7 +131,7 @@ __device__ __forceinline__ int cstage_off(int r, int c) {
   return r * RB + ((c ^ ((r / RPL) & (CPR - 1))) << 4);
 }
 
-template <int BN, int WM, bool STG = true>
+template <int BN, int WM, bool STG = true, bool PADC = false>
 __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restrict__ X,
                                                          const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y,
                                                          const uint16_t* __restrict__ bias, Geom g, Taps tp, int M,
@@ -147,6 +150,7 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
   __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WNW, wc = wave % WNW;
+  const int Cs = PADC ? g.Cs : g.C;  // channels per stored input pixel
   // stride classes of a data gradient share one launch: the block finds its class (tile ranges
   // are prefix sums) and takes the class's pixel grid, tap range, packed weights and output offset
   int Ho = g.Ho, Wo = g.Wo, tap0 = 0, oy0 = tp.oy0, ox0 = tp.ox0, bid = blockIdx.x;
@@ -183,7 +187,7 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
     const int mm = mv[i] ? m : 0;
     const int n = mm / HoWo, rem = mm - n * HoWo;
     const int ho = rem / Wo, wo = rem - ho * Wo;
-    xb[i] = (long long)n * g.H * g.W * g.C;
+    xb[i] = (long long)n * g.H * g.W * Cs;
     hb[i] = ho * g.sh;
     wb[i] = wo * g.sw;
     lch[i] = (tid & 3) ^ (((row >> 3) & 1) << 1);
@@ -204,13 +208,14 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_kernel(const uint16_t* __restr
     const unsigned bbase = abase + OPA;
     const int kk = s * BK;
     const int tap = kk / g.C;
-    const int c0 = kk - tap * g.C;
+    const int c0 = kk - tap * g.C;  // g.C: the (padded) channels of the K decomposition
     const int th = tp.th[tap0 + tap], tw = tp.tw[tap0 + tap];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int hi = hb[i] + th, wi = wb[i] + tw;
-      const bool ok = mv[i] && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-      const void* src = ok ? (const void*)(X + xb[i] + ((long long)hi * g.W + wi) * g.C + c0 + lch[i] * 8)
+      const bool ok = mv[i] && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W &&
+                      (PADC == false || c0 + lch[i] * 8 < Cs);
+      const void* src = ok ? (const void*)(X + xb[i] + ((long long)hi * g.W + wi) * Cs + c0 + lch[i] * 8)
                            : (const void*)g_zero16;
       glds16(src, __builtin_amdgcn_readfirstlane(abase + (i * NT + wave * 64) * 16));
     }
@@ -610,9 +615,15 @@ PA_API int pa_conv2d_set_staged(int v) {
 // pa_conv2d_fwd / _stats is [Cout][R*S + pa_conv2d_fwd_pad_taps(C, R, S)][C].
 PA_API int pa_conv2d_fwd_pad_taps(int C, int R, int S) { return ((long long)R * S * C) % 64 != 0 ? 1 : 0; }
 
+// Channels of the K decomposition for C stored input channels: C itself when C % 32 == 0, else C
+// rounded up to 32 (C % 8 == 0): the padded 8-channel chunks of every tap read the zero block and
+// meet zero filter columns (packed filter [Cout][taps][pa_conv2d_fwd_cpad(C)]).
+PA_API int pa_conv2d_fwd_cpad(int C) { return (C + 31) / 32 * 32; }
+
 PA_API int pa_conv2d_fwd_ok(int C, int Cout, int R, int S) {
-  return C > 0 && C % 32 == 0 && R > 0 && S > 0 && R * S + pa_conv2d_fwd_pad_taps(C, R, S) <= MAX_TAPS && Cout > 0 &&
-         Cout % 8 == 0;
+  if (C <= 0 || C % 8 != 0) return 0;
+  const int Cp = pa_conv2d_fwd_cpad(C);
+  return R > 0 && S > 0 && R * S + pa_conv2d_fwd_pad_taps(Cp, R, S) <= MAX_TAPS && Cout > 0 && Cout % 8 == 0;
 }
 
 // waves along the pixel side per Cout tile width (A/B knob; index 0/1/2 = BN 64/128/256)
@@ -625,25 +636,26 @@ PA_API int pa_conv2d_set_wm(int bn, int wm) {
 }
 
 
-template <bool STG>
+template <bool STG, bool PADC = false>
 static void launch_fwd_kernel_t(int BN, dim3 grid, const uint16_t* xp, const uint16_t* wp, uint16_t* yp,
                                 const uint16_t* bp, const Geom& g, const Taps& tp, int M, int K, hipStream_t st) {
   if (BN == 256) {
-    if (g_fwd_wm[2] == 4) conv_fwd_kernel<256, 4, STG><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
-    else conv_fwd_kernel<256, 2, STG><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    if (g_fwd_wm[2] == 4) conv_fwd_kernel<256, 4, STG, PADC><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    else conv_fwd_kernel<256, 2, STG, PADC><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
   } else if (BN == 128) {
-    if (g_fwd_wm[1] == 4) conv_fwd_kernel<128, 4, STG><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
-    else conv_fwd_kernel<128, 2, STG><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    if (g_fwd_wm[1] == 4) conv_fwd_kernel<128, 4, STG, PADC><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    else conv_fwd_kernel<128, 2, STG, PADC><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
   } else {
-    if (g_fwd_wm[0] == 4) conv_fwd_kernel<64, 4, STG><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
-    else if (g_fwd_wm[0] == 8) conv_fwd_kernel<64, 8, STG><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
-    else conv_fwd_kernel<64, 2, STG><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    if (g_fwd_wm[0] == 4) conv_fwd_kernel<64, 4, STG, PADC><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    else if (g_fwd_wm[0] == 8) conv_fwd_kernel<64, 8, STG, PADC><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
+    else conv_fwd_kernel<64, 2, STG, PADC><<<grid, NT, 0, st>>>(xp, wp, yp, bp, g, tp, M, K);
   }
 }
 
 static void launch_fwd_kernel(int BN, dim3 grid, const uint16_t* xp, const uint16_t* wp, uint16_t* yp,
                               const uint16_t* bp, const Geom& g, const Taps& tp, int M, int K, hipStream_t st) {
-  if (g_conv_staged) launch_fwd_kernel_t<true>(BN, grid, xp, wp, yp, bp, g, tp, M, K, st);
+  if (g.Cs > 0 && g.Cs != g.C) launch_fwd_kernel_t<true, true>(BN, grid, xp, wp, yp, bp, g, tp, M, K, st);
+  else if (g_conv_staged) launch_fwd_kernel_t<true>(BN, grid, xp, wp, yp, bp, g, tp, M, K, st);
   else launch_fwd_kernel_t<false>(BN, grid, xp, wp, yp, bp, g, tp, M, K, st);
 }
 
@@ -692,7 +704,9 @@ static int conv2d_fwd_impl(const void* x, const void* wpk, void* y, const void* 
                            int Ho, int Wo, hipStream_t st) {
   if (!pa_conv2d_fwd_ok(C, Cout, R, S) || N <= 0 || Ho <= 0 || Wo <= 0 || H >= 16384 || W >= 16384)
     return (int)hipErrorInvalidValue;
-  Geom g{N, H, W, C, Ho, Wo, Cout, R, S, sh, sw, ph, pw, dh, dw};
+  const int Cs = C;
+  C = pa_conv2d_fwd_cpad(Cs);  // K decomposition channels (filter packed with this many)
+  Geom g{N, H, W, C, Ho, Wo, Cout, R, S, sh, sw, ph, pw, dh, dw, 0, Cs};
   Taps tp{};
   for (int r = 0; r < R; ++r)
     for (int q = 0; q < S; ++q) {

@@ -43,6 +43,7 @@ _SIGS = {
     'pa_conv_stem_fwd': [P] * 5 + [I] * 14 + [P],
     'pa_conv_stem_stat_rows': [I],
     'pa_conv2d_fwd_pad_taps': [I, I, I],
+    'pa_conv2d_fwd_cpad': [I],
     'pa_gconv_ok': [I] * 17,
     'pa_gconv_fwd': [P] * 4 + [I] * 17 + [P],
     'pa_gconv_dgrad': [P] * 3 + [I] * 17 + [P],

@@ -137,9 +137,12 @@ def _fwd_packed(x, wpk, b, stride, pad, dil):
     Nb, H, W, C = x.shape
     Cout, R, S, _ = wpk.shape
     Ho, Wo = _out_hw(H, W, R, S, stride, pad, dil)
-    pt = int(N.lib.pa_conv2d_fwd_pad_taps(C, R, S))
+    Cp = int(N.lib.pa_conv2d_fwd_cpad(C))
+    if Cp != C:  # C % 32 != 0: zero filter channels up to the padded K decomposition
+        wpk = torch.cat([wpk, wpk.new_zeros(Cout, R, S, Cp - C)], 3)
+    pt = int(N.lib.pa_conv2d_fwd_pad_taps(Cp, R, S))
     if pt:  # K = taps * C made a multiple of 64 with zero taps (e.g. 3x3 over 32 channels)
-        wpk = torch.cat([wpk.reshape(Cout, R * S * C), wpk.new_zeros(Cout, pt * C)], 1)
+        wpk = torch.cat([wpk.reshape(Cout, R * S * Cp), wpk.new_zeros(Cout, pt * Cp)], 1)
     y = torch.empty(Nb, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
     if _want_stats(b):
         rpb = int(N.lib.pa_conv2d_fwd_stat_rows(Cout))
@@ -528,6 +531,10 @@ class _Conv2dNHWC(torch.autograd.Function):
                         gx, second = None, 'done'
             if gx is None and second != 'done':
                 gx = conv2d_dgrad_classes(dy, w, x.shape[1:3], stride, pad, dil)
+                if gx is None and tuple(stride) == (1, 1) and fwd_ok(w.transpose(0, 1)):
+                    # C_out % 32 != 0 (MobileNet pointwise): the stride-1 data gradient as a forward
+                    # conv of dY, whose K decomposition pads the channels to 32
+                    gx = conv2d_dgrad(dy, w, x.shape[1:3], pad, dil)
         slot_used = False
         if ctx.needs_input_grad[1] and _bwd_enabled and _wgrad_hip and w.shape[0] % 8 == 0:
             C = w.shape[1]

@@ -171,6 +171,36 @@ def test_resnext_block_nchw_no_miopen():
     assert _miopen_kernels(run) == []
 
 
+@pytest.mark.parametrize('C,Cout,k,s,p', [(24, 144, 1, 1, 0), (144, 24, 1, 1, 0), (16, 96, 1, 1, 0),
+                                         (24, 64, 3, 1, 1), (40, 32, 3, 1, 1), (72, 48, 1, 1, 0)])
+def test_conv_channel_padding(C, Cout, k, s, p):
+    """Input channels C % 32 != 0 (C % 8 == 0, MobileNet pointwise / 3x3 convs): the implicit-GEMM
+    forward pads the K decomposition to 32 channels (zero-block chunks x zero filter columns);
+    forward, data and filter gradients vs fp32 torch, no library convolution kernel."""
+    from paddle.ops import conv
+    x = torch.randn(2, 15, 17, C, device=DEV).bfloat16()
+    w = (0.1 * torch.randn(Cout, C, k, k, device=DEV)).bfloat16()
+    assert conv.supported(x, w, 1) and conv.fwd_ok(w)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_()
+    wr = w.float().requires_grad_()
+    yr = torch.nn.functional.conv2d(xr, wr, None, s, p).permute(0, 2, 3, 1)
+    xh, wh = x.clone().requires_grad_(), w.clone().requires_grad_()
+    g = torch.randn_like(yr)
+
+    def run():
+        y = conv.conv2d_nhwc(xh, wh, None, (s, s), (p, p), (1, 1))
+        y.backward(g.bfloat16())
+        return y
+    bad = _miopen_kernels(run)
+    assert bad == [], bad
+    xh.grad = wh.grad = None
+    y = run()
+    yr.backward(g)
+    _close(y, yr, 3e-2, 1e-2, 'fwd')
+    _close(xh.grad, xr.grad.permute(0, 2, 3, 1), 3e-2, 1e-2, 'dgrad')
+    _close(wh.grad, wr.grad, 5e-2, 2e-2, 'wgrad')
+
+
 def _miopen_kernels(fn):
     """Names of the library (MIOpen) convolution / batch-norm / pooling kernels ``fn`` launches."""
     from torch.profiler import profile, ProfilerActivity
