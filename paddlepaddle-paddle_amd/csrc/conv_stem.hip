@@ -125,6 +125,9 @@ __global__ __launch_bounds__(256) void fwd_kernel(const uint16_t* __restrict__ x
 #pragma unroll
   for (int m = 0; m < 2; ++m) pq[m] = off + (32 * wave + 16 * m + l16) * g.sw * g.C;
   const int nvw = max(0, min(32, g.Wo - ow0 - 32 * wave));  // valid pixels of this wave
+  // Cout % 16 == 0: a lane's 16 channels co0 + 16 g4 .. + 15 are all valid or none (not stored)
+  const bool cvalid = co0 + 16 * g4 < g.Cout;
+  const int cbase = min(co0 + 16 * g4, g.Cout - 16);  // in-bounds bias reads either way
   float* wst = reinterpret_cast<float*>(rows + g.NR * g.SEGP);  // STATS: [RB][4 waves][2][64]
   __syncthreads();
 
@@ -169,12 +172,12 @@ __global__ __launch_bounds__(256) void fwd_kernel(const uint16_t* __restrict__ x
     for (int i = 0; i < 16; ++i) bv[i] = 0.f;
     if (bias != nullptr) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) bv[i] = to_f(bias[co0 + 16 * g4 + i]);
+      for (int i = 0; i < 16; ++i) bv[i] = to_f(bias[cbase + i]);
     }
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const int ow = ow0 + 32 * wave + 16 * m + l16;
-      if (ow >= g.Wo) continue;
+      if (ow >= g.Wo || !cvalid) continue;
       uint16_t* dst = y + (nh * g.Wo + ow) * g.Cout + co0 + 16 * g4;
       float v0[8], v1[8];
 #pragma unroll
@@ -221,7 +224,7 @@ __global__ __launch_bounds__(256) void fwd_kernel(const uint16_t* __restrict__ x
     for (int idx = tid; idx < g.RB * CT; idx += 256) {
       const int rb = idx >> 6, c = idx & 63;
       const int oh = oh0 + rb;
-      if (oh >= g.Ho) continue;
+      if (oh >= g.Ho || co0 + c >= g.Cout) continue;
       float cnt = 0.f, mean = 0.f, m2 = 0.f;
 #pragma unroll
       for (int w = 0; w < 4; ++w) {  // Chan merge of the wave slabs
@@ -249,7 +252,9 @@ using namespace pa;
 static bool stem_geo(int N, int H, int W, int C, int Ho, int Wo, int Cout, int R, int S, int sh, int sw, int ph,
                      int pw, bool stats, pa::stem::Geo& g) {
   using namespace pa::stem;
-  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C > 8 || Ho <= 0 || Wo <= 0 || Cout <= 0 || Cout % CT != 0) return false;
+  // Cout % 16: the last block's missing channels have zero filter rows (the host pads the image to
+  // a multiple of 64 rows) and are not stored
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C > 8 || Ho <= 0 || Wo <= 0 || Cout <= 0 || Cout % 16 != 0) return false;
   if (R <= 0 || S <= 0 || R > 11 || S > 11 || sh <= 0 || sw <= 0 || sh > 4 || sw > 4 || ph < 0 || pw < 0) return false;
   if ((long long)W * C >= (1LL << 30)) return false;
   const int RK = (S * C + 7) / 8 * 8;
@@ -288,7 +293,8 @@ PA_API int pa_conv_stem_stat_rows(int Wo) {
   return Wo > 0 && (Wo <= PT || Wo % PT == 0) ? (Wo < PT ? Wo : PT) : 0;
 }
 
-// x [N,H,W,C] (16-bit), wimg [Cout][Kp], bias [Cout] or null -> y [N,Ho,Wo,Cout]; dilation 1.
+// x [N,H,W,C] (16-bit), wimg [ceil(Cout / 64) * 64][Kp] (rows past Cout zero), bias [Cout] or null ->
+// y [N,Ho,Wo,Cout]; Cout % 16 == 0; dilation 1.
 // stats (nullable, no bias): fp32 [2][N*Ho*ceil(Wo/128)][Cout] slab means then M2s.
 PA_API hipError_t pa_conv_stem_fwd(const void* x, const void* wimg, const void* bias, void* y, float* stats, int N,
                                    int H, int W, int C, int Cout, int R, int S, int sh, int sw, int ph, int pw, int Ho,
@@ -300,7 +306,7 @@ PA_API hipError_t pa_conv_stem_fwd(const void* x, const void* wimg, const void* 
   const long long gy = (long long)N * g.HB;
   if (gy > 2147483647LL || (long long)N * H * W * C >= (1LL << 46)) return hipErrorInvalidValue;
   g.vec = ((W * C) % 8 == 0 && ((uintptr_t)x & 15) == 0) ? 1 : 0;
-  const dim3 grid((Wo + pa::stem::PT - 1) / pa::stem::PT, (unsigned)gy, Cout / pa::stem::CT);
+  const dim3 grid((Wo + pa::stem::PT - 1) / pa::stem::PT, (unsigned)gy, (Cout + pa::stem::CT - 1) / pa::stem::CT);
   const size_t lds = stem_lds(g, wst);
   const int ks = g.Kp / 32;
 #define PA_STEM_LAUNCH(T, K)                                                                               \

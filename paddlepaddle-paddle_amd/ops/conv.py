@@ -469,8 +469,8 @@ def conv2d_fwd_stem(x, w, b, stride, pad):
     Cout, _, R, S = w.shape
     Ho, Wo = _out_hw(H, W, R, S, stride, pad, (1, 1))
     RK, Kp = int(N.lib.pa_conv_stem_rk(C, S)), int(N.lib.pa_conv_stem_kp(C, R, S))
-    wimg = torch.zeros(Cout, Kp, dtype=x.dtype, device=x.device)
-    wimg[:, :R * RK].view(Cout, R, RK)[:, :, :S * C] = w.detach().to(x.dtype).permute(0, 2, 3, 1).reshape(Cout, R, S * C)
+    wimg = torch.zeros(-(-Cout // 64) * 64, Kp, dtype=x.dtype, device=x.device)  # rows past Cout stay zero
+    wimg[:Cout, :R * RK].view(Cout, R, RK)[:, :, :S * C] = w.detach().to(x.dtype).permute(0, 2, 3, 1).reshape(Cout, R, S * C)
     y = torch.empty(Nb, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
     bb = b.to(x.dtype).contiguous() if b is not None else None
     rpb = int(N.lib.pa_conv_stem_stat_rows(Wo)) if _want_stats(b) else 0

@@ -56,7 +56,8 @@ def test_dwconv_fwd_bwd(dt, N, H, W, C, k, s, p, d, bias):
 @pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize('N,H,W,C,Cout,k,s,p', [
     (2, 64, 64, 3, 64, 7, 2, 3), (2, 224, 224, 3, 64, 7, 2, 3), (3, 33, 45, 4, 128, 3, 1, 1),
-    (2, 40, 40, 1, 64, 5, 2, 2), (1, 300, 300, 3, 64, 3, 2, 1)])
+    (2, 40, 40, 1, 64, 5, 2, 2), (1, 300, 300, 3, 64, 3, 2, 1), (2, 96, 96, 3, 32, 3, 2, 1),
+    (2, 50, 52, 3, 80, 3, 2, 1)])
 @pytest.mark.parametrize('bias', [False, True])
 def test_conv_stem_fwd(dt, N, H, W, C, Cout, k, s, p, bias):
     from paddle.ops import conv
@@ -73,7 +74,7 @@ def test_conv_stem_fwd(dt, N, H, W, C, Cout, k, s, p, bias):
 
 @pytest.mark.parametrize('N,H,W,C,Cout,k,s,p', [
     (2, 224, 224, 3, 64, 7, 2, 3), (3, 64, 64, 3, 64, 7, 2, 3), (2, 33, 45, 4, 128, 3, 1, 1),
-    (1, 512, 512, 3, 64, 7, 2, 3)])
+    (1, 512, 512, 3, 64, 7, 2, 3), (2, 96, 96, 3, 32, 3, 2, 1)])
 def test_conv_stem_bn_stats(N, H, W, C, Cout, k, s, p):
     """Under fused_bn_stats() the stem epilogue's slab (mean, M2) merge to the batch statistics of
     the fp32 convolution (one slab per output-row segment)."""
@@ -359,6 +360,34 @@ def test_resnext50_nchw_training_step_no_miopen():
     net, opt = paddle.amp.decorate(net, opt, level='O2', dtype='bfloat16')
     g = torch.Generator(device=DEV).manual_seed(3)
     xin = paddle.to_tensor(torch.randn(2, 3, 64, 64, device=DEV, generator=g).bfloat16())
+    y = paddle.to_tensor(torch.randint(0, 10, (2,), device=DEV, generator=g))
+    vals = []
+
+    def step():
+        loss = paddle.nn.functional.cross_entropy(net(xin), y)
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        vals.append(float(loss))
+
+    step()
+    bad = _miopen_kernels(step)
+    assert bad == [], bad
+    assert all(v == v and abs(v) < 1e4 for v in vals), vals
+
+
+def test_mobilenet_v2_nchw_training_step_no_miopen():
+    """paddle.vision.models.mobilenet_v2() (default NCHW: 3 -> 32 stem, depthwise 3x3, pointwise
+    convs over 16 / 24 / 144 / ... channels) trains an AMP-O2 bf16 step with no library
+    convolution / batch-norm / pooling kernel, and its loss is finite."""
+    from paddle.vision.models import mobilenet_v2
+    paddle.seed(5)
+    net = mobilenet_v2(num_classes=10)
+    opt = paddle.optimizer.Momentum(learning_rate=0.01, momentum=0.9, parameters=net.parameters(),
+                                    multi_precision=True)
+    net, opt = paddle.amp.decorate(net, opt, level='O2', dtype='bfloat16')
+    g = torch.Generator(device=DEV).manual_seed(3)
+    xin = paddle.to_tensor(torch.randn(2, 3, 96, 96, device=DEV, generator=g).bfloat16())
     y = paddle.to_tensor(torch.randint(0, 10, (2,), device=DEV, generator=g))
     vals = []
 
