@@ -58,6 +58,14 @@ def batch_norm(x, running_mean, running_var, weight=None, bias=None, training=Fa
         y = ops.batchnorm.bn_act_nhwc(t.permute(0, 2, 3, 1), g, None if bias is None else _u(bias), rm, rv, epsilon,
                                       momentum, bool(use_batch))
         return _w(y.permute(0, 3, 1, 2))
+    if use_batch and ops.use_hip(t) and t.dim() == 4 and (cl or t.is_contiguous(memory_format=torch.channels_last)) \
+            and ops.batchnorm.channel_pad_ok(t, g):
+        # channel count off the kernels' 16-byte grain (ShuffleNetV2 58/116/232): zero-padded copy
+        b = None if bias is None else _u(bias)
+        if cl:
+            return _w(ops.batchnorm.bn_nhwc_cpad(t, g, b, rm, rv, epsilon, momentum, True))
+        y = ops.batchnorm.bn_nhwc_cpad(t.permute(0, 2, 3, 1), g, b, rm, rv, epsilon, momentum, True)
+        return _w(y.permute(0, 3, 1, 2))
     if cl:
         t = t.permute(0, t.dim() - 1, *range(1, t.dim() - 1))
     out = TF.batch_norm(t, rm, rv, None if weight is None else _u(weight), None if bias is None else _u(bias),

@@ -119,6 +119,40 @@ def supported(x, gamma=None):
     return N._load() is not None
 
 
+def channel_pad_ok(x, gamma=None):
+    """The HIP kernels need C * elem_size % 16 == 0; a channel count off that grain (ShuffleNetV2's
+    58/116/232) runs them on a zero-padded copy instead (``bn_nhwc_cpad``)."""
+    if not x.is_cuda or x.dim() < 2 or x.dtype not in (torch.bfloat16, torch.float16, torch.float32):
+        return False
+    if gamma is not None and gamma.dtype not in (torch.float32, x.dtype):
+        return False
+    return N._load() is not None
+
+
+def bn_nhwc_cpad(x, gamma, beta, run_mean, run_var, eps=1e-5, momentum=0.9, training=True):
+    """batch_norm of a channels-last tensor whose channel count the kernels cannot vectorise: pad the
+    channel dim to the 16-byte grain with zeros (their statistics are 0 / 0 and their outputs are
+    sliced away, so gamma 1 / beta 0 there), run ``bn_act_nhwc``, slice back.  Gradients flow
+    through the pad / slice; the padded running statistics are written back into the caller's."""
+    C = x.shape[-1]
+    v = 16 // x.element_size()
+    Cp = -(-C // v) * v
+    pc = Cp - C
+    xp = torch.nn.functional.pad(x, (0, pc))
+    gp = torch.cat([gamma, gamma.new_ones(pc)]) if gamma is not None else None
+    bp = torch.cat([beta, beta.new_zeros(pc)]) if beta is not None else None
+    rmp = torch.cat([run_mean, run_mean.new_zeros(pc)]) if run_mean is not None else None
+    rvp = torch.cat([run_var, run_var.new_ones(pc)]) if run_var is not None else None
+    y = bn_act_nhwc(xp, gp, bp, rmp, rvp, eps, momentum, training)
+    if training:
+        with torch.no_grad():
+            if run_mean is not None:
+                run_mean.copy_(rmp[:C])
+            if run_var is not None:
+                run_var.copy_(rvp[:C])
+    return y[..., :C].contiguous()
+
+
 def bn_act_nhwc(x, gamma, beta, run_mean, run_var, eps=1e-5, momentum=0.9, training=True, relu=False,
                 residual=None, dz_sink=None):
     """act(batch_norm(x) [+ residual]) for a channels-last tensor (channel = last dim).  dz_sink

@@ -402,3 +402,32 @@ def test_mobilenet_v2_nchw_training_step_no_miopen():
     bad = _miopen_kernels(step)
     assert bad == [], bad
     assert all(v == v and abs(v) < 1e4 for v in vals), vals
+
+
+@pytest.mark.parametrize('C', [58, 116, 3])
+def test_bn_channel_pad_matches_torch(C):
+    """Batch norm over a channel count off the 16-byte grain runs the HIP kernels on a zero-padded
+    copy: output, input / gamma / beta gradients and running statistics match the fp32 reference."""
+    from paddle.ops import batchnorm as BN
+    g = torch.Generator(device=DEV).manual_seed(C)
+    x = torch.randn(4, 7, 9, C, device=DEV, generator=g).bfloat16().requires_grad_()
+    gam = (torch.rand(C, device=DEV, generator=g) + 0.5).requires_grad_()
+    bet = torch.randn(C, device=DEV, generator=g).requires_grad_()
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    assert not BN.supported(x, gam) and BN.channel_pad_ok(x, gam)
+    y = BN.bn_nhwc_cpad(x, gam, bet, rm, rv, 1e-5, 0.9, True)
+    dy = torch.randn(y.shape, device=DEV, generator=g).bfloat16()
+    y.backward(dy)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    gr, br = gam.detach().clone().requires_grad_(), bet.detach().clone().requires_grad_()
+    rmr, rvr = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    yr = torch.nn.functional.batch_norm(xr, rmr, rvr, gr, br, True, 0.1, 1e-5)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    assert y.shape == x.shape
+    torch.testing.assert_close(y.float(), yr.permute(0, 2, 3, 1), atol=4e-2, rtol=2e-2)
+    torch.testing.assert_close(x.grad.float(), xr.grad.permute(0, 2, 3, 1), atol=6e-2, rtol=3e-2)
+    torch.testing.assert_close(gam.grad, gr.grad, atol=5e-1, rtol=2e-2)
+    torch.testing.assert_close(bet.grad, br.grad, atol=5e-1, rtol=2e-2)
+    torch.testing.assert_close(rm, rmr, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(rv, rvr, atol=2e-3, rtol=2e-3)
+
