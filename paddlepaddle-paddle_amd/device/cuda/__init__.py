@@ -18,6 +18,8 @@ def device_count():
 
 
 def empty_cache():
+    from ...ops.workspace import release_all
+    release_all()  # kernel scratch (dS^T, split-K partials) no captured graph still addresses
     if native_allocator.is_enabled():
         native_allocator.empty_cache(torch.cuda.current_device())
     elif torch.cuda.is_available():

@@ -170,8 +170,19 @@ _ACTS = {
 }
 
 
+# sublayers an expert may hold besides its two Linears: parameterless, deterministic and
+# mode-independent (a Dropout — or any unknown layer — keeps the expert on the per-expert loop, since
+# the one-off numeric probe cannot see train/eval-dependent behaviour)
+_PASSIVE = ('ReLU', 'GELU', 'Silu', 'SiLU', 'Swish', 'Sequential', 'LayerList')
+
+
 def _ffn_linears(expert):
-    lins = [l for l in expert.sublayers() if isinstance(l, Linear)]
+    lins = []
+    for l in expert.sublayers():
+        if isinstance(l, Linear):
+            lins.append(l)
+        elif type(l).__name__ not in _PASSIVE:
+            return None
     if len(lins) != 2 or len(expert.parameters()) != sum(len(l.parameters()) for l in lins):
         return None
     return lins
@@ -262,7 +273,7 @@ class MoELayer(Layer):
                 raise ValueError(f"unknown gate type {typ}")
         self.gate = gate
         self.top_k = getattr(gate, 'top_k', 1)
-        self._grouped = None  # (order, act) once verified; False = per-expert loop
+        self._grouped = {}  # training flag -> (order, act) once verified, or False (per-expert loop)
 
     def forward(self, inp):
         t = _unwrap(inp)
@@ -294,10 +305,12 @@ class MoELayer(Layer):
                        for j in range(self.num_expert)]
         else:
             per_exp = list(send.split(counts.tolist(), 0))
-        if self._grouped is None:
-            self._grouped = _detect_grouped(list(self.experts), self.d_model) or False
-        if self._grouped and self.num_expert > 1:
-            outs = _grouped_ffn(list(self.experts), self._grouped, per_exp, self.d_model)
+        mode = bool(self.training)
+        if mode not in self._grouped:  # probed per mode: train/eval behaviour may differ
+            self._grouped[mode] = _detect_grouped(list(self.experts), self.d_model) or False
+        spec = self._grouped[mode]
+        if spec and self.num_expert > 1:
+            outs = _grouped_ffn(list(self.experts), spec, per_exp, self.d_model)
         else:
             outs = []
             for j, chunk in enumerate(per_exp):

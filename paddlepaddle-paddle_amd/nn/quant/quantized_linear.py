@@ -99,7 +99,8 @@ def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="in
     x2 = t.reshape(-1, t.shape[-1])
     wq = _u(weight)
     bits, grp = (4 if weight_dtype == 'int4' else 8), (0 if group_size == -1 else group_size)
-    if ops.use_hip(x2) and ops.woq.woq_ok(x2.contiguous(), wq, bits, grp):
+    needs_grad = torch.is_grad_enabled() and (t.requires_grad or (bias is not None and _u(bias).requires_grad))
+    if not needs_grad and ops.use_hip(x2) and ops.woq.woq_ok(x2.contiguous(), wq, bits, grp):
         # decode-shaped: stream the quantised weight once, dequantise in registers (csrc/woq_gemm.hip)
         y = ops.woq.woq_linear(x2.contiguous(), wq, _u(weight_scale), bits, grp,
                                None if bias is None else _u(bias))

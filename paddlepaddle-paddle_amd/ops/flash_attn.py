@@ -44,7 +44,9 @@ def supported(q, k, v):
 # the dS round trip).  PADDLE_AMD_FA_DS_BWD=0 / 1: off / also for head_dim 64.
 _ds_env = os.environ.get('PADDLE_AMD_FA_DS_BWD')
 _ds_bwd = [None if _ds_env is None else _ds_env != '0']  # None: automatic (head_dim 128)
-_DS_WS = {}
+# bounded: a dS^T image above PADDLE_AMD_FA_DS_WS_MB (default 8 GiB) takes the recompute kernels
+from .workspace import workspace as _workspace
+_DS_WS = _workspace('flash_ds', int(os.environ.get('PADDLE_AMD_FA_DS_WS_MB', '8192')) << 20)
 
 
 def set_ds_backward(on):
@@ -62,12 +64,11 @@ def _ds_ok(D, dt):
 
 
 def _ds_ws(B, Hq, Sq, Sk, dtype, device):
+    """The shared dS^T workspace, or None when it would exceed the bound."""
     n = int(N.lib.pa_flash_ds_ws_elems(B, Hq, Sq, Sk))
-    key = (str(device), dtype)
-    t = _DS_WS.get(key)
-    if t is None or t.numel() < n:
-        _DS_WS[key] = t = torch.empty(n, dtype=dtype, device=device)
-    return t
+    if not _DS_WS.fits(n, dtype):
+        return None
+    return _DS_WS.get(n, dtype, device)
 
 
 def _bwd_call(q, k, v, o, do, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, D, scale, causal, cu_q=None, cu_k=None,
@@ -76,8 +77,8 @@ def _bwd_call(q, k, v, o, do, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, D, scal
     (pa_flash_bwd, or pa_flash_bwd_ex when any extended feature is in use)."""
     st = (N.strides3(q), N.strides3(k), N.strides3(v), N.strides3(o), N.strides3(do), N.strides3(dq),
           N.strides3(dk), N.strides3(dv))
-    if _ds_ok(D, q.dtype):
-        ws = _ds_ws(B, Hq, Sq, Sk, q.dtype, q.device)
+    ws = _ds_ws(B, Hq, Sq, Sk, q.dtype, q.device) if _ds_ok(D, q.dtype) else None
+    if ws is not None:
         N.check(N.lib.pa_flash_bwd_ds(N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse), N.ptr(delta),
                                       N.ptr(dq), N.ptr(dk), N.ptr(dv), N.ptr(ws), B, Sq, Sk, Hq, Hk, D, *st, scale,
                                       int(causal), N.dtcode(q.dtype), N.ptr(cu_q), N.ptr(cu_k), total, N.ptr(m), mb,

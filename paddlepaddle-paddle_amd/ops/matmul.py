@@ -256,7 +256,10 @@ def addmm(inp, x, y, beta=1.0, alpha=1.0):
             r = _mm2d(x, y, bias=inp.contiguous())
             if r is not None:
                 return r
-        out = inp.expand(x.shape[0], y.shape[1]).contiguous()
+        # always a fresh buffer: .contiguous() of an already-contiguous [M, N] input would alias
+        # the caller's tensor, and the beta-accumulating kernel writes its result in place
+        out = torch.empty(x.shape[0], y.shape[1], dtype=x.dtype, device=x.device)
+        out.copy_(inp.expand(x.shape[0], y.shape[1]))
         r = _gemmx(x.unsqueeze(0), y.unsqueeze(0), 1, alpha=alpha, out=out.unsqueeze(0), beta=beta)
         if r is not None:
             return out

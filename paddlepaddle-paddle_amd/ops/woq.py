@@ -20,7 +20,8 @@ def woq_ok(x2, wq, bits, group):
     return bool(N.lib.pa_woq_ok(M, wq.shape[0], K, x2.stride(0), wq.stride(0), bits, group, _DT[x2.dtype]))
 
 
-_ws = {}
+from .workspace import workspace as _workspace
+_ws = _workspace('woq')
 
 
 def woq_linear(x2, wq, scale, bits, group, bias=None):
@@ -29,9 +30,7 @@ def woq_linear(x2, wq, scale, bits, group, bias=None):
     Nn = wq.shape[0]
     out = torch.empty(M, Nn, dtype=x2.dtype, device=x2.device)
     need = int(N.lib.pa_woq_ws_floats(M, Nn, K, bits))
-    ws = _ws.get(x2.device)
-    if ws is None or ws.numel() < need:
-        ws = _ws[x2.device] = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=x2.device)
+    ws = _ws.get(need, torch.float32, x2.device, min_numel=1 << 20)
     sc = scale.float().contiguous()
     b = None if bias is None else bias.to(x2.dtype).contiguous()
     N.check(N.lib.pa_woq_gemm(N.ptr(x2), N.ptr(wq), N.ptr(sc), N.ptr(b), N.ptr(out), N.ptr(ws), M, Nn, K,

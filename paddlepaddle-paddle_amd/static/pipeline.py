@@ -146,6 +146,19 @@ def _split_feed(prog, feed, acc):
     return parts
 
 
+def _found_inf_sync(pol, cfg, dev):
+    """found-inf flag MAX-reduced over the pipe group (each stage checks only its own parameters)
+    and the data-parallel group, so every rank of the step skips or applies the update together."""
+    def sync(found):
+        t = torch.tensor([1.0 if found else 0.0], device=dev)
+        if cfg.group is not None and cfg.nstages > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=cfg.group.pg)
+        if pol._nranks() > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=getattr(pol.dp_group, 'pg', None))
+        return bool(t.item() > 0)
+    return sync
+
+
 def run_pipeline(prog, feed, dev, pol, cfg, run_forward):
     """Execute one pipelined training step of ``prog`` on this rank's stage.  ``run_forward(nodes,
     env, feed)`` binds the feeds into ``env`` and interprets ``nodes`` (executor internals)."""
@@ -176,12 +189,20 @@ def run_pipeline(prog, feed, dev, pol, cfg, run_forward):
             sent[m] = sv
         envs[m], recvd[m] = env, rv
 
+    amp = pol._amp()
+    merge = pol.k_steps if pol.k_steps > 1 else 1
+    div = float(acc * (merge if pol.avg else 1))
+
     def backward(m):
         env = envs[m]
         if s == S - 1:
             loss = env[plan.loss_vid]
             losses.append(loss.detach().float().reshape(-1)[0])
-            (loss / acc).backward()
+            if amp is not None:
+                # loss scaling: the scaled gradient flows back through every stage's boundary sends
+                amp._scaled_backward(loss, div)
+            else:
+                (loss / div).backward()
         else:
             ts, gs = [], []
             for v in plan.cross[s + 1]:
@@ -219,12 +240,18 @@ def run_pipeline(prog, feed, dev, pol, cfg, run_forward):
             b += 1
     for w, _ in works:
         w.wait()
-    # the update: data-parallel reduction + optimizer (params of other stages have no gradient)
-    if pol._nranks() > 1:
-        pol._allreduce_grads()
-    opt = pol._plain()
-    opt.step()
-    opt.clear_grad()
+    # the update (every k-th run under gradient merge): data-parallel reduction, then the AMP
+    # unscale / finite check / skip-or-step / scale update or the plain optimizer step
+    pol._micro += 1
+    if pol._micro % merge == 0:
+        if pol._nranks() > 1:
+            pol._allreduce_grads()
+        if amp is not None:
+            amp._apply_update(_found_inf_sync(pol, cfg, comm_dev))
+        else:
+            opt = pol._plain()
+            opt.step()
+            opt.clear_grad()
     # mean micro-batch loss on every stage of the pipe group (src: the last stage)
     val = torch.stack(losses).mean() if losses else torch.zeros((), dtype=torch.float32)
     val = val.to(comm_dev)

@@ -1,6 +1,8 @@
 """Static Program pipeline parallelism over gloo ranks (reference: fleet static pipeline optimizer;
 ops placed with static.device_guard('gpu:N'), pipeline_configs accumulate_steps micro-batches).
-argv[1]: schedule ('1F1B' / 'FThenB'); argv[2]: 'pp' (pp = world) or 'ppdp' (pp 2 x dp 2).
+argv[1]: schedule ('1F1B' / 'FThenB'); argv[2]: 'pp' (pp = world), 'ppdp' (pp 2 x dp 2), 'ppamp'
+(pp = world + static AMP fp16 with dynamic loss scaling whose first step overflows: every stage must
+skip it together) or 'ppgm' (pp = world + gradient merge k_steps 2: one update per two runs).
 Every rank builds the same program (same seed); after 3 steps each stage's parameters must equal a
 single-process run on the full batch."""
 import os
@@ -40,7 +42,15 @@ def main():
     pp = 2 if mode == 'ppdp' else world
     dp = world // pp
     acc = 4
+    amp_cfg = dict(init_loss_scaling=2.0 ** 24, use_dynamic_loss_scaling=True, incr_every_n_steps=1000,
+                   decr_every_n_nan_or_inf=1, decr_ratio=2.0 ** -12)
     s = fleet.DistributedStrategy()
+    if mode == 'ppamp':
+        s.amp = True
+        s.amp_configs = dict(amp_cfg)
+    if mode == 'ppgm':
+        s.gradient_merge = True
+        s.gradient_merge_configs = {'k_steps': 2, 'avg': True}
     s.hybrid_configs = {'dp_degree': dp, 'mp_degree': 1, 'pp_degree': pp}
     s.pipeline = True
     s.pipeline_configs = {'accumulate_steps': acc, 'micro_batch_size': 2, 'schedule_mode': sched}
@@ -56,7 +66,7 @@ def main():
     rng = np.random.RandomState(0)
     B = 8 * dp
     batches = []
-    for _ in range(3):
+    for _ in range(4 if mode == 'ppgm' else 3):
         xs = rng.randn(B, 6).astype('float32')
         batches.append((xs, (xs[:, :3].argmax(1)).reshape(-1, 1).astype('int64')))
     half = B // dp
@@ -66,8 +76,16 @@ def main():
                                     'y': ys[dp_rank * half:(dp_rank + 1) * half]}, fetch_list=[loss])
         losses.append(float(np.asarray(out[0]).reshape(-1)[0]))
     got = [p.numpy().copy() for p in main_p.all_parameters()]
-    ref_main, ref_startup, ref_loss = build(pp, sgd)
+    if mode == 'ppamp':
+        import paddle.static.amp as samp
+        ref_opt = lambda: samp.decorate(sgd(), level='O1', dtype='float16', **amp_cfg)  # noqa: E731
+    else:
+        ref_opt = sgd
+    ref_main, ref_startup, ref_loss = build(pp, ref_opt)
     ref_losses = []
+    if mode == 'ppgm':  # the merged step == one full-batch step over both runs' samples
+        batches = [(np.concatenate([batches[i][0], batches[i + 1][0]]),
+                    np.concatenate([batches[i][1], batches[i + 1][1]])) for i in (0, 2)]
     for xs, ys in batches:
         # same micro-batch means as the pipeline: acc equal chunks of each dp shard, averaged
         out = exe.run(ref_main, feed={'x': xs, 'y': ys}, fetch_list=[ref_loss])
@@ -80,8 +98,13 @@ def main():
     assert len(got) == len(st) == len(ref), (len(got), len(ref))
     for a, b, s_ in zip(got, ref, st):
         if s_ == me:
-            np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
-    if dp == 1:
+            tol = 2e-3 if mode == 'ppamp' else 1e-4
+            np.testing.assert_allclose(a, b, rtol=tol, atol=tol / 10)
+    if mode == 'ppamp':
+        pol = main_p.nodes[-1].target
+        scale = pol._amp()._scale
+        assert scale == 2.0 ** 12, scale  # the overflowing first step was skipped on every stage
+    if dp == 1 and mode not in ('ppgm', 'ppamp'):
         np.testing.assert_allclose(losses, ref_losses, rtol=1e-4, atol=1e-5)
     print(f"rank{rank} static pp {sched} {mode} OK", flush=True)
 

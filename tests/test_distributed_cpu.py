@@ -308,7 +308,7 @@ def test_static_fleet_tensor_parallel(mode, nproc):
 
 
 @pytest.mark.parametrize("sched,mode,nproc", [('1F1B', 'pp', 2), ('FThenB', 'pp', 2), ('1F1B', 'pp', 3),
-                                              ('1F1B', 'ppdp', 4)])
+                                              ('1F1B', 'ppdp', 4), ('1F1B', 'ppamp', 2), ('FThenB', 'ppgm', 2)])
 def test_static_fleet_pipeline_parallel(sched, mode, nproc):
     """Static-mode fleet pipeline: device_guard stages, micro-batched FThenB / 1F1B with
     send/recv of activations and gradients; every stage's parameters match a single-process run."""

@@ -110,3 +110,59 @@ def test_ds_dropout_matches_recompute(D):
             FA.set_ds_backward(old)
     for a, b, n in zip(grads[0], grads[1], 'qkv'):
         _close(b, a, 3e-2, 1e-2, f'dropout d{n} ds vs recompute')
+
+
+def test_ds_llama_bench_shape_strided_qkv():
+    """The llama2_13b bench key's attention: B2 S4096 H40 D128 causal, q/k/v strided views of one
+    [B, S, 3H, D] projection, through the dS backward (default at D = 128) vs fp32."""
+    assert FA._ds_ok(128, torch.bfloat16)
+    B, S, H, D = 2, 4096, 40, 128
+    qkv = _leaf(B, S, 3 * H, D)
+    q, k, v = qkv[:, :, :H], qkv[:, :, H:2 * H], qkv[:, :, 2 * H:]
+    o = FA.flash_attention(q, k, v, True)
+    ri = qkv.detach().float().requires_grad_()
+    r = _ref(ri[:, :, :H], ri[:, :, H:2 * H], ri[:, :, 2 * H:], True)
+    _close(o, r, 2e-2, name='llama fwd')
+    g = torch.randn_like(r)
+    o.backward(g.bfloat16())
+    r.backward(g)
+    for i, n in enumerate('qkv'):
+        sl = slice(i * H, (i + 1) * H)
+        _close(qkv.grad[:, :, sl], ri.grad[:, :, sl], 5e-2, 2e-2, f'llama d{n}')
+    del r, ri
+    torch.cuda.empty_cache()
+
+
+def test_ds_workspace_survives_growth_after_capture(ds_on):
+    """A graph captured with the dS backward keeps its workspace: an eager call at a larger shape
+    grows the workspace, the replay must still produce the captured shape's gradients."""
+    B, S, H, D = 2, 256, 4, 128
+    q, k, v = _leaf(B, S, H, D), _leaf(B, S, H, D), _leaf(B, S, H, D)
+    g = torch.randn(B, S, H, D, device=DEV).bfloat16()
+    FA._DS_WS.release()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm-up on the capture stream
+        for t in (q, k, v):
+            t.grad = None
+        FA.flash_attention(q, k, v, True).backward(g)
+    torch.cuda.current_stream().wait_stream(s)
+    ref = [t.grad.clone() for t in (q, k, v)]
+    graph = torch.cuda.CUDAGraph()
+    for t in (q, k, v):
+        t.grad = torch.zeros_like(t)
+    with torch.cuda.graph(graph):
+        o = FA.flash_attention(q, k, v, True)
+        o.backward(g)
+    # larger eager shape: grows (replaces) the workspace
+    big = [_leaf(4, 2048, 8, D) for _ in range(3)]
+    FA.flash_attention(*big, True).backward(torch.randn(4, 2048, 8, D, device=DEV).bfloat16())
+    assert FA._DS_WS.nbytes() >= 4 * 8 * 2048 * 2048 * 2
+    keep = torch.full((64 << 20,), 7.0, device=DEV)  # recycle freed memory into live tensors
+    for t in (q, k, v):
+        t.grad.zero_()
+    graph.replay()
+    torch.cuda.synchronize()
+    for a, b, n in zip((q, k, v), ref, 'qkv'):
+        _close(a.grad, b, 1e-2, name=f'replay d{n}')
+    assert bool((keep == 7.0).all())

@@ -169,6 +169,34 @@ def test_addmm_and_skinny_decode_shape():
     _close(out, 0.5 * full.float() + 2.0 * (x2.float() @ y.float()), 1e-2, 'addmm beta/alpha')
 
 
+def test_addmm_leaves_input_unchanged():
+    """addmm with a contiguous [M, N] input must not write its result into the input's storage."""
+    g = torch.Generator(device=DEV).manual_seed(16)
+    inp = _rand(256, 512, g=g)
+    keep = inp.clone()
+    x, y = _rand(256, 1024, g=g), _rand(1024, 512, g=g)
+    with torch.no_grad():
+        out = hm.addmm(inp, x, y, beta=0.5, alpha=2.0)
+    assert torch.equal(inp, keep), 'addmm overwrote its input'
+    assert out.data_ptr() != inp.data_ptr()
+    _close(out, 0.5 * keep.float() + 2.0 * (x.float() @ y.float()), 1e-2, 'addmm fresh out')
+
+
+def test_weight_only_linear_grad_reaches_x():
+    """Decode-shaped weight_only_linear with x requiring grad takes the differentiable path."""
+    from paddle.nn.quant import weight_quantize, weight_only_linear
+    from paddle.nn.quant.quantized_linear import _dequant
+    g = torch.Generator(device=DEV).manual_seed(17)
+    w = torch.randn(512, 256, device=DEV, generator=g) * 0.05
+    q, s = weight_quantize(paddle.to_tensor(w), algo='weight_only_int8')
+    x = paddle.to_tensor(torch.randn(4, 512, device=DEV, generator=g).bfloat16())
+    x.stop_gradient = False
+    y = weight_only_linear(x, q, weight_scale=s, weight_dtype='int8')
+    y.sum().backward()
+    wd = _dequant(q, s, 'weight_only_int8', -1)
+    _close(x.grad._t, wd.sum(1).expand(4, -1), 3e-2, 'woq dx')
+
+
 def test_static_executor_replays_on_hip_gemm(static_mode):
     """A static Program with fc layers run by the Executor on the GPU: the recorded torch GEMM nodes
     replay on the hand-written kernel."""

@@ -41,13 +41,13 @@ def test_grouped_experts_match_loop(act, name):
         experts = [FFN(d, f, act) for _ in range(E)]
         layer = MoELayer(d, experts, gate=NaiveGate(d, E, 1, topk=2))
         if not grouped:
-            layer._grouped = False
+            layer._grouped = {True: False, False: False}
         x = paddle.to_tensor(torch.randn(3, 7, d, generator=torch.Generator().manual_seed(2)))
         x.stop_gradient = False
         y = layer(x)
         (y ** 2).sum().backward()
         if grouped:
-            assert layer._grouped == (0, name)
+            assert layer._grouped[True] == (0, name)
         res.append((y.numpy(), x.grad.numpy(), [e.htoh4.weight.grad.numpy() for e in experts]))
     (ya, ga, wa), (yb, gb, wb) = res
     assert abs(ya - yb).max() < 1e-5
@@ -60,7 +60,33 @@ def test_detection_rejects_non_ffn():
     paddle.seed(0)
     layer = MoELayer(8, [Odd(8) for _ in range(2)], gate=NaiveGate(8, 2, 1, topk=1))
     layer(paddle.randn([2, 3, 8]))
-    assert layer._grouped is False
+    assert layer._grouped[True] is False
+
+
+class FFNDrop(paddle.nn.Layer):
+    def __init__(self, d, f):
+        super().__init__()
+        self.fc1 = paddle.nn.Linear(d, f)
+        self.drop = paddle.nn.Dropout(0.5)
+        self.fc2 = paddle.nn.Linear(f, d)
+
+    def forward(self, x):
+        return self.fc2(self.drop(paddle.nn.functional.relu(self.fc1(x))))
+
+
+def test_detection_rejects_dropout_expert_probed_in_eval():
+    """An expert with a Dropout between its Linears matches the FFN formula in eval mode; the
+    grouped path must not be taken (it would skip the dropout once the layer trains)."""
+    paddle.seed(0)
+    experts = [FFNDrop(8, 16) for _ in range(2)]
+    layer = MoELayer(8, experts, gate=NaiveGate(8, 2, 1, topk=1))
+    layer.eval()
+    layer(paddle.randn([2, 3, 8]))
+    assert layer._grouped[False] is False
+    layer.train()
+    x = paddle.randn([4, 8, 8])
+    y1, y2 = layer(x).numpy(), layer(x).numpy()
+    assert abs(y1 - y2).max() > 0  # dropout is live in training forwards
 
 
 def test_fused_ec_moe_dense_formula():
