@@ -311,10 +311,12 @@ def run_program(prog, feed, dev, grad=None):
     needs_grad = grad if grad is not None else any(n.kind in ('minimize', 'backward', 'grad') for n in prog.nodes)
     ctx = contextlib.nullcontext() if needs_grad else torch.no_grad()
     from .amp import autocast_context
+    from .ir_passes import ir_nodes
+    nodes = ir_nodes(prog, dev)  # the fusion-pass rewrite (static/ir_passes.py) on GPU programs
     with _paused(), ctx, autocast_context(prog, dev) as subs:
         prev, _SUBS['map'] = _SUBS['map'], subs
         try:
-            _exec(prog, prog.nodes, env, smap, dev)
+            _exec(prog, nodes, env, smap, dev)
         finally:
             _SUBS['map'] = prev
     return env

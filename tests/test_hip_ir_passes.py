@@ -1,0 +1,94 @@
+"""IR fusion passes on the GPU: a static ERNIE program (AMP-O2 bf16) run by the Executor with the
+fused nodes (flash attention with the padding mask and in-kernel dropout, fused add + LayerNorm on
+csrc/norm.hip) vs the same program unfused (fusion off: the recorded torch ops)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import paddle  # noqa: E402
+from paddle import static  # noqa: E402
+from paddle.static import ir_passes as IP  # noqa: E402
+from paddle.ops import flash_attn as FA, norm as NORM, fused as FUSED  # noqa: E402
+
+from test_ir_passes import _build, _feed  # noqa: E402
+
+
+def _run(train, drop, mode, steps=3):
+    old = IP.set_mode(mode)
+    try:
+        paddle.set_device('gpu:0')
+        paddle.seed(5)
+        main, loss, logits = _build(train, drop, hidden=128, heads=2)
+        static.amp.cast_model_to_fp16(main, dest_type='bfloat16', level='O1')  # autocast replay
+        paddle.enable_static()
+        try:
+            exe = static.Executor(paddle.CUDAPlace(0))
+            outs = [exe.run(main, feed=_feed(), fetch_list=[loss, logits]) for _ in range(steps)]
+        finally:
+            paddle.disable_static()
+        return outs, IP.fusion_stats(main)
+    finally:
+        IP.set_mode(old)
+
+
+class _Count:
+    def __init__(self, mod, name):
+        self.mod, self.name, self.n = mod, name, 0
+
+    def __enter__(self):
+        self.orig = getattr(self.mod, self.name)
+
+        def f(*a, **k):
+            self.n += 1
+            return self.orig(*a, **k)
+        setattr(self.mod, self.name, f)
+        return self
+
+    def __exit__(self, *a):
+        setattr(self.mod, self.name, self.orig)
+
+
+def test_ernie_static_fused_kernels_match_unfused_program():
+    ref, _ = _run(False, 0.0, '0', steps=1)
+    with _Count(FA, 'flash_attention_ex') as ca, _Count(NORM, 'add_layer_norm') as cn:
+        out, stats = _run(False, 0.0, 'auto', steps=1)
+    assert stats.get('multihead_matmul_fuse_pass_v2') == 2, stats
+    assert ca.n == 2 and cn.n == 5, (ca.n, cn.n)
+    np.testing.assert_allclose(out[0][1], ref[0][1], rtol=5e-2, atol=5e-2)
+    np.testing.assert_allclose(out[0][0], ref[0][0], rtol=3e-2, atol=3e-2)
+
+
+def test_ernie_static_amp_bf16_training_fused():
+    """AMP-O2 bf16 training with dropout: the fused program takes the flash kernel (mask + dropout)
+    and the fused dropout + add + LayerNorm kernels, and trains (finite, decreasing loss)."""
+    old = IP.set_mode('auto')
+    try:
+        paddle.set_device('gpu:0')
+        paddle.seed(5)
+        paddle.enable_static()
+        try:
+            from paddle.models import ernie_config, ErnieForSequenceClassification
+            cfg = ernie_config('ernie-tiny', hidden_size=128, num_attention_heads=2)
+            main, startup = static.Program(), static.Program()
+            with static.program_guard(main, startup):
+                ids = static.data('ids', [None, 32], 'int64')
+                lab = static.data('lab', [None], 'int64')
+                model = ErnieForSequenceClassification(cfg, num_classes=2)
+                loss = paddle.nn.functional.cross_entropy(model(ids), lab)
+                opt = static.amp.decorate(paddle.optimizer.AdamW(learning_rate=1e-3, parameters=model.parameters()),
+                                          level='O2', dtype='bfloat16')
+                opt.minimize(loss)
+            exe = static.Executor(paddle.CUDAPlace(0))
+            opt.amp_init(paddle.CUDAPlace(0))
+            with _Count(FA, 'flash_attention_ex') as ca, _Count(FUSED, 'dropout_add_norm') as cd:
+                losses = [float(np.asarray(exe.run(main, feed=_feed(), fetch_list=[loss])[0]).reshape(-1)[0])
+                          for _ in range(8)]
+        finally:
+            paddle.disable_static()
+    finally:
+        IP.set_mode(old)
+    assert ca.n == 16 and cd.n == 32, (ca.n, cd.n)
+    assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
+    assert torch.cuda.is_available()

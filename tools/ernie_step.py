@@ -1,0 +1,42 @@
+"""Run the bench's ERNIE-3.0 static AMP-O2 step alone (fp8 or bf16) for rocprofv3.
+
+usage: python tools/ernie_step.py fp8|bf16 [steps] [warmup]
+Prints ms/step (wall, synchronized) on stderr-free stdout.
+"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    mode = sys.argv[1]
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    warm = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    sys.argv = [sys.argv[0]]
+    args = bench.parse()
+    torch.cuda.set_device(0)
+    dev = torch.device('cuda', 0)
+    step, work, *_ = bench.build_ernie_static(args, 1, 0, dev, mode == 'fp8')
+    for _ in range(warm):
+        step()
+        if os.environ.get('STEP_MARKER'):
+            torch.cuda._sleep(10)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+        if os.environ.get('STEP_MARKER'):
+            torch.cuda._sleep(10)  # one 'spin_kernel' per step: the rocprof step boundary
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    print(f"ernie {mode}: {ms:.3f} ms/step, {work / ms * 1e3:.0f} tok/s")
+
+
+if __name__ == '__main__':
+    main()
