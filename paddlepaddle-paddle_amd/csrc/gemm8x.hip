@@ -121,3 +121,71 @@ PA_API int pa_gemm8_fp8(const void* A, const void* W, void* C, const void* bias,
   else go(gemm11_kernel<true, true, 200, F8<1, 1>, false>);
   return (int)hipGetLastError();
 }
+
+// Split-K fp8 GEMM (the fp8 Linear weight gradient X^T dY: M x N = in x out features, K = tokens —
+// e.g. 768 x 2304 x 32768 is 27 output tiles for 256 CUs, so the K range is split over gridDim.z
+// slices writing fp32 slabs ws[z][M][N], folded by fp8_splitk_reduce with the dequant scales).
+// Contract: pa_gemm8_fp8_ok and K % (128 * splitk) == 0; ws holds splitk * M * N floats.
+namespace pa {
+namespace g8 {
+__global__ __launch_bounds__(256) void fp8_splitk_reduce(const float* __restrict__ ws, uint16_t* __restrict__ C,
+                                                         const uint16_t* __restrict__ bias, int M, int N,
+                                                         long long ldc, int S, float alpha, float beta,
+                                                         const float* __restrict__ sa, const float* __restrict__ sb) {
+  const long long idx = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const long long MN = (long long)M * N;
+  if (idx >= MN) return;
+  float a = alpha;
+  if (sa) a *= sa[0];
+  if (sb) a *= sb[0];
+  const int m = (int)(idx / N), n = (int)(idx - (long long)m * N);
+  f32x4 s = *reinterpret_cast<const f32x4*>(ws + idx);
+  for (int k = 1; k < S; ++k) s += *reinterpret_cast<const f32x4*>(ws + k * MN + idx);
+  float v[4] = {s[0] * a, s[1] * a, s[2] * a, s[3] * a};
+  uint16_t* dst = C + (long long)m * ldc + n;
+  if (beta != 0.f) {
+    float o[4];
+    load_f<bf16_t, 4>(reinterpret_cast<const bf16_t*>(dst), o);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += beta * o[r];
+  }
+  if (bias) {
+    float bb[4];
+    load_f<bf16_t, 4>(reinterpret_cast<const bf16_t*>(bias + n), bb);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += bb[r];
+  }
+  store_f<bf16_t, 4>(reinterpret_cast<bf16_t*>(dst), v);
+}
+}  // namespace g8
+}  // namespace pa
+
+PA_API int pa_gemm8_fp8_splitk(const void* A, const void* W, void* C, const void* bias, const void* scale_a,
+                               const void* scale_b, void* ws, int M, int N, int K, long long lda, long long ldw,
+                               long long ldc, float alpha, float beta, int fmtA, int fmtB, int splitk,
+                               hipStream_t st) {
+  using namespace pa::g8;
+  if (splitk < 2 || !ws || K % (128 * splitk) || !pa_gemm8_fp8_ok(M, N, K, lda, ldw, ldc) || fmtA < 0 || fmtA > 1 ||
+      fmtB < 0 || fmtB > 1)
+    return (int)hipErrorInvalidValue;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  dim3 grid(tm * tn, 1, splitk);
+  const int K2 = K / 2;
+  const long long la = lda / 2, lw = ldw / 2;
+  auto go = [&](auto kern) {
+    kern<<<grid, 512, 0, st>>>((const char*)A, (const char*)W, nullptr, (float*)ws, nullptr, M, N, K2, la, lw, N,
+                               1.f, 0.f, K2 / splitk, 0LL, 0LL, 0LL, nullptr, nullptr);
+  };
+  if (fmtA == 0 && fmtB == 0) go(gemm11_kernel<true, true, 1, F8<0, 0>, false>);
+  else if (fmtA == 0) go(gemm11_kernel<true, true, 1, F8<0, 1>, false>);
+  else if (fmtB == 0) go(gemm11_kernel<true, true, 1, F8<1, 0>, false>);
+  else go(gemm11_kernel<true, true, 1, F8<1, 1>, false>);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const long long MN = (long long)M * N;
+  fp8_splitk_reduce<<<(unsigned)((MN / 4 + 255) / 256), 256, 0, st>>>((const float*)ws, (uint16_t*)C,
+                                                                       (const uint16_t*)bias, M, N, ldc, splitk,
+                                                                       alpha, beta, (const float*)scale_a,
+                                                                       (const float*)scale_b);
+  return (int)hipGetLastError();
+}

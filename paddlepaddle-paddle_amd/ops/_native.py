@@ -90,6 +90,7 @@ _SIGS = {
     'pa_gemm_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
     'pa_gemm8_fp8_ok': [I, I, I, LL, LL, LL],
     'pa_gemm8_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
+    'pa_gemm8_fp8_splitk': [P, P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, I, P],
     'pa_gemmx_ok': [I, I, I, LL, LL, LL, I, I, I],
     'pa_woq_ok': [I, I, I, LL, LL, I, I, I],
     'pa_woq_ws_floats': [I, I, I, I],

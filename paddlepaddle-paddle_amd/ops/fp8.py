@@ -130,6 +130,16 @@ def fp8_mm(a, b, sa, sb, bias=None, out_dtype=torch.bfloat16):
     return out.to(out_dtype)
 
 
+def _colsum(dy2):
+    """fp32 column sums of a bf16 [rows, N] gradient (the bias gradient) — one HIP pass, no fp32
+    copy of dy (csrc/act.hip colsum) on the GPU."""
+    if dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16):
+        from . import fused
+        if fused.colsum_ok(dy2):
+            return fused.colsum(dy2)
+    return dy2.float().sum(0)
+
+
 class FP8State:
     """The three metas of one fp8 Linear (kept on the weight Parameter)."""
 
@@ -169,7 +179,7 @@ class _FP8Linear(torch.autograd.Function):
         if need_dw:
             dw = fp8_mm(xqt, gqt, sx, sg).to(ctx.wdt)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = dy2.float().sum(0).to(ctx.bdt)
+            db = _colsum(dy2).to(ctx.bdt)
         return dx, dw, db, None
 
 

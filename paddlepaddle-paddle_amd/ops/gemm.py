@@ -317,6 +317,23 @@ _FP8_FMT = {torch.float8_e4m3fn: 0, torch.float8_e5m2: 1}
 _fp8_8phase = os.environ.get('PADDLE_AMD_FP8_8PHASE', '1') != '0'
 
 
+from .workspace import workspace as _workspace  # noqa: E402
+_FP8_WS = _workspace('fp8_splitk')
+
+
+def _fp8_splitk(M, N_, K):
+    """Split-K factor of an fp8 GEMM whose 256x256 output tiles cannot fill the chip (the fp8 Linear
+    weight gradient: in x out features over a token-count K): slices of >= 1024 k each, at most
+    ~2 rounds of blocks."""
+    tiles = -(-M // 256) * -(-N_ // 256)
+    if tiles >= 128:
+        return 1
+    for s in (16, 8, 4, 2):
+        if K % (128 * s) == 0 and K // s >= 1024 and tiles * s <= 384:
+            return s
+    return 1
+
+
 def hip_fp8_ok(a, w):
     """a: [M,K] fp8 row-major; w: [N,K] fp8 row-major (the weight of an fp8 Linear)."""
     if a.dtype not in _FP8_FMT or w.dtype not in _FP8_FMT or a.dim() != 2 or w.dim() != 2:
@@ -341,6 +358,15 @@ def hip_fp8_mm(a, w, scale_a=None, scale_b=None, bias=None, out=None, alpha=1.0,
     assert out.dtype == torch.bfloat16 and out.stride(1) == 1 and out.shape == (M, N_)
     sa = scale_a.float().reshape(1) if scale_a is not None else None
     sb = scale_b.float().reshape(1) if scale_b is not None else None
+    sk = _fp8_splitk(M, N_, K)
+    if _fp8_8phase and sk > 1 and N.lib.pa_gemm8_fp8_ok(M, N_, K, a.stride(0), w.stride(0), out.stride(0)):
+        # few output tiles over a deep K (the fp8 weight gradient): K split over the grid, fp32 slabs
+        ws = _FP8_WS.get(sk * M * N_, torch.float32, a.device)
+        N.check(N.lib.pa_gemm8_fp8_splitk(N.ptr(a), N.ptr(w), N.ptr(out), N.ptr(bias), N.ptr(sa), N.ptr(sb), N.ptr(ws),
+                                          M, N_, K, a.stride(0), w.stride(0), out.stride(0), float(alpha),
+                                          float(beta), _FP8_FMT[a.dtype], _FP8_FMT[w.dtype], sk, N.stream()),
+                'gemm8_fp8_splitk')
+        return out
     if _fp8_8phase and N.lib.pa_gemm8_fp8_ok(M, N_, K, a.stride(0), w.stride(0), out.stride(0)):
         # the 8-phase ping-pong schedule of the bf16 GEMM with one scaled fp8 MFMA per 128-byte k-tile
         N.check(N.lib.pa_gemm8_fp8(N.ptr(a), N.ptr(w), N.ptr(out), N.ptr(bias), N.ptr(sa), N.ptr(sb), M, N_, K,

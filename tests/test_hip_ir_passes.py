@@ -55,7 +55,9 @@ def test_ernie_static_fused_kernels_match_unfused_program():
     with _Count(FA, 'flash_attention_ex') as ca, _Count(NORM, 'add_layer_norm') as cn:
         out, stats = _run(False, 0.0, 'auto', steps=1)
     assert stats.get('multihead_matmul_fuse_pass_v2') == 2, stats
-    assert ca.n == 2 and cn.n == 5, (ca.n, cn.n)
+    # 4 of the 5 add + LayerNorm sites: the embedding sum stays fp32 under O1 autocast (embedding
+    # lookups are not autocast ops), so that one takes the composite
+    assert ca.n == 2 and cn.n == 4, (ca.n, cn.n)
     np.testing.assert_allclose(out[0][1], ref[0][1], rtol=5e-2, atol=5e-2)
     np.testing.assert_allclose(out[0][0], ref[0][0], rtol=3e-2, atol=3e-2)
 

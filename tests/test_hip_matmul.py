@@ -217,9 +217,11 @@ def test_static_executor_replays_on_hip_gemm(static_mode):
     _close(torch.from_numpy(np.asarray(out, dtype=np.float32)), ref, 1e-2, 'static replay')
 
 
-@pytest.mark.parametrize('M,N,K', [(4096, 6144, 2048), (4096, 2048, 8192), (1000, 1024, 512), (256, 4096, 1024)])
+@pytest.mark.parametrize('M,N,K', [(4096, 6144, 2048), (4096, 2048, 8192), (1000, 1024, 512), (256, 4096, 1024),
+                                   (768, 2304, 8192), (512, 768, 4096)])
 @pytest.mark.parametrize('fmts', [(torch.float8_e4m3fn, torch.float8_e4m3fn), (torch.float8_e5m2, torch.float8_e4m3fn)])
 def test_fp8_8phase_gemm(M, N, K, fmts):
+    """(768 x 2304 x 8192 and 512 x 768 x 4096: the split-K path of the fp8 weight gradient)"""
     """The 8-phase fp8 GEMM (one scaled MFMA per 128-byte k-tile, device scales, bias, beta) vs the
     fp32 product of the dequantised operands."""
     g = torch.Generator(device=DEV).manual_seed(7)
