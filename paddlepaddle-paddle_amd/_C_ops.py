@@ -232,12 +232,69 @@ _ALIASES = {'elementwise_add': 'add', 'elementwise_sub': 'subtract', 'elementwis
             'lookup_table_v2': 'embedding', 'fill_constant': 'full'}
 
 
+def check_finite_and_unscale_(x, scale, found_inf):
+    """xs *= 1/scale in place, found_inf set on any inf/nan (csrc/amp.hip, one launch per 48)."""
+    from .core.tensor import _unwrap
+    from .ops.amp import check_finite_and_unscale_ as _k
+    import torch
+    xs = [_unwrap(t) for t in x]
+    f = _unwrap(found_inf)
+    ft = torch.zeros(1, dtype=torch.float32, device=f.device)
+    _k(xs, _unwrap(scale).float().reshape(1), ft)
+    f.copy_((ft.reshape(f.shape) != 0).to(f.dtype))
+    return x, found_inf
+
+
+def update_loss_scaling_(x, found_inf, prev_loss_scaling, in_good_steps, in_bad_steps, incr_every_n_steps,
+                         decr_every_n_nan_or_inf, incr_ratio, decr_ratio, stop_update=False):
+    """Dynamic loss-scale update on device scalars; gradients zeroed when found_inf (reference
+    update_loss_scaling op semantics)."""
+    from .core.tensor import _unwrap
+    from .ops.amp import update_loss_scaling_ as _k
+    import torch
+    f = _unwrap(found_inf)
+    ff = f.float().reshape(1)
+    for t in x:
+        tt = _unwrap(t)
+        tt.mul_(torch.where(ff != 0, torch.zeros_like(ff), torch.ones_like(ff)).to(tt.dtype))
+    if stop_update:
+        return x, prev_loss_scaling, in_good_steps, in_bad_steps
+    sc, g, b = _unwrap(prev_loss_scaling), _unwrap(in_good_steps), _unwrap(in_bad_steps)
+    s32, g32, b32 = sc.float().reshape(1).clone(), g.float().reshape(1).clone(), b.float().reshape(1).clone()
+    _k(ff, s32, g32, b32, incr_every_n_steps, decr_every_n_nan_or_inf, incr_ratio, decr_ratio)
+    sc.copy_(s32.reshape(sc.shape).to(sc.dtype))
+    g.copy_(g32.reshape(g.shape).to(g.dtype))
+    b.copy_(b32.reshape(b.shape).to(b.dtype))
+    return x, prev_loss_scaling, in_good_steps, in_bad_steps
+
+
+def _inplace_of(fn, name):
+    """An in-place ``name`` built from its out-of-place op: the result is written back into the
+    first argument's storage (same shape and dtype required), which is returned."""
+    def f(x, *a, **k):
+        from .core.tensor import _unwrap
+        out = fn(x, *a, **k)
+        xt, ot = _unwrap(x), _unwrap(out)
+        if tuple(ot.shape) != tuple(xt.shape):
+            raise ValueError(f"paddle._C_ops.{name}: result shape {tuple(ot.shape)} != input {tuple(xt.shape)}")
+        xt.copy_(ot.to(xt.dtype))
+        return x
+    f.__name__ = name
+    return f
+
+
 def __getattr__(name):
     if name in _ALIASES:
         return globals()[_ALIASES[name]]
-    base = name[:-1] if name.endswith('_') else name
+    inplace = name.endswith('_') and not name.endswith('__')
+    base = name[:-1] if inplace else name
     for mod in (_P(), _F()):
-        fn = getattr(mod, name, None) or getattr(mod, base, None)
+        fn = getattr(mod, name, None)
         if callable(fn):
             return fn
+    if inplace:  # no in-place function: keep the in-place contract explicitly
+        for mod in (_P(), _F()):
+            fn = getattr(mod, base, None)
+            if callable(fn):
+                return _inplace_of(fn, name)
     raise AttributeError(f"paddle._C_ops has no operator '{name}'")

@@ -107,7 +107,9 @@ class OptimizerWithMixedPrecision:
             use_dynamic_loss_scaling = is_fp16
         self._use_scaling = is_fp16 or bool(use_dynamic_loss_scaling)
         self._dynamic = bool(use_dynamic_loss_scaling)
-        self._scale = float(init_loss_scaling) if self._use_scaling else 1.0
+        self._scale_host = float(init_loss_scaling) if self._use_scaling else 1.0
+        self._scale_t = None   # device-resident loss scale (+ good / bad step counters), created
+        self._counts_t = None  # on the first scaled backward, updated by csrc/amp.hip
         self._incr_every = incr_every_n_steps
         self._decr_every = decr_every_n_nan_or_inf
         self._incr_ratio = incr_ratio
@@ -123,8 +125,26 @@ class OptimizerWithMixedPrecision:
     def __getattr__(self, name):  # get_lr, set_lr_scheduler, state_dict, ...
         return getattr(self.__dict__['_optimizer'], name)
 
+    @property
+    def _scale(self):
+        if self._scale_t is not None:
+            return float(self._scale_t.item())
+        return self._scale_host
+
+    @_scale.setter
+    def _scale(self, v):
+        self._scale_host = float(v)
+        if self._scale_t is not None:
+            self._scale_t.fill_(float(v))
+
     def get_loss_scaling(self):
         return torch.tensor([self._scale], dtype=torch.float32)
+
+    def _state(self, dev):
+        if self._scale_t is None or self._scale_t.device != dev:
+            self._scale_t = torch.full((1,), self._scale_host, dtype=torch.float32, device=dev)
+            self._counts_t = torch.tensor([float(self._good), float(self._bad)], dtype=torch.float32, device=dev)
+        return self._scale_t
 
     def _cast_params(self):
         if self._level == 'O2' and not self._casted and self._program is not None:
@@ -160,7 +180,11 @@ class OptimizerWithMixedPrecision:
         if not self._use_scaling and div == 1.0:
             loss.backward()
             return
-        (loss.float() * (self._scale / div)).backward()
+        if not self._use_scaling:
+            (loss.float() / div).backward()
+            return
+        sc = self._state(loss.device)  # device scale: no host read
+        (loss.float() * (sc / div)).backward()
 
     def _apply_update(self, sync_found_inf=None):
         """Unscale, check for inf/nan (``sync_found_inf``: a callable reducing the flag over the
@@ -170,33 +194,30 @@ class OptimizerWithMixedPrecision:
             self._optimizer.clear_grad()
             return
         params = [p._t for p in (self._params or []) if p._t.requires_grad]
-        inv = 1.0 / self._scale
-        finite = None
-        for t in params:
-            if t.grad is not None:
-                t.grad.mul_(inv)
-                f = torch.isfinite(t.grad).all()
-                finite = f if finite is None else finite & f
-        found = False if finite is None else not bool(finite.item())
+        grads = [t.grad for t in params if t.grad is not None]
+        dev = grads[0].device if grads else (params[0].device if params else torch.device('cpu'))
+        from ..ops.amp import check_finite_and_unscale_, update_loss_scaling_
+        sc = self._state(dev)
+        found_t = torch.zeros(1, dtype=torch.float32, device=dev)
+        # one multi-tensor launch per 48 gradients (csrc/amp.hip): unscale + inf/nan flag on device
+        check_finite_and_unscale_(grads, sc, found_t)
+        found = bool(found_t.item() != 0)  # the one host read of the step: skip-or-step
         if sync_found_inf is not None:
             found = sync_found_inf(found)
+            found_t.fill_(1.0 if found else 0.0)
         self.found_inf = found
         if not found:
             self._optimizer.step()
         self._optimizer.clear_grad()
         if self._dynamic:
-            if not found:
-                self._good += 1
-                self._bad = 0
-                if self._good == self._incr_every:
-                    self._scale *= self._incr_ratio
-                    self._good = 0
+            cnt = self._counts_t
+            update_loss_scaling_(found_t, sc, cnt[0:1], cnt[1:2], self._incr_every, self._decr_every,
+                                 self._incr_ratio, self._decr_ratio)
+            # host mirrors of the counters (state_dict / tests); the scale itself stays on device
+            if found:
+                self._good, self._bad = 0, (self._bad + 1) % max(1, self._decr_every)
             else:
-                self._bad += 1
-                self._good = 0
-                if self._bad == self._decr_every:
-                    self._scale = max(self._scale * self._decr_ratio, 1.0)
-                    self._bad = 0
+                self._bad, self._good = 0, (self._good + 1) % max(1, self._incr_every)
 
 
 def decorate(optimizer, amp_lists=None, level='O1', dtype='float16', master_weight=None, master_grad=False,

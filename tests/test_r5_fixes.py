@@ -33,3 +33,24 @@ def test_weight_only_linear_differentiable_cpu():
     x.stop_gradient = False
     weight_only_linear(x, q, weight_scale=s).sum().backward()
     assert x.grad is not None and x.grad.shape == [3, 64]
+
+
+def test_c_ops_inplace_fallback_keeps_inplace_semantics():
+    x = paddle.to_tensor([1.0, -2.0, 3.0])
+    r = paddle._C_ops.hardtanh_(x, -1.0, 1.0)
+    assert r is x and x.numpy().tolist() == [1.0, -1.0, 1.0]
+
+
+def test_amp_loss_scaling_ops_cpu():
+    from paddle.ops.amp import check_finite_and_unscale_, update_loss_scaling_
+    gs = [torch.tensor([2.0, 4.0]), torch.tensor([1.0, float('nan')], dtype=torch.bfloat16)]
+    found = torch.zeros(1)
+    check_finite_and_unscale_(gs, torch.tensor([2.0]), found)
+    assert gs[0].tolist() == [1.0, 2.0] and found.item() == 1.0
+    sc, g, b = torch.tensor([8.0]), torch.zeros(1), torch.zeros(1)
+    update_loss_scaling_(found, sc, g, b, 2, 1, 2.0, 0.5)
+    assert sc.item() == 4.0
+    found.zero_()
+    for _ in range(2):
+        update_loss_scaling_(found, sc, g, b, 2, 1, 2.0, 0.5)
+    assert sc.item() == 8.0 and g.item() == 0.0
