@@ -11,15 +11,15 @@ import torch
 
 from . import _native as N
 
-_ws_cache = {}
+from .workspace import workspace as _new_workspace
+
+_DEC_WS = _new_workspace('decode_partials')
 
 
 def _ws(n, dev):
-    w = _ws_cache.get(dev)
-    if w is None or w.numel() < n:
-        w = torch.empty(max(n, 1 << 16), dtype=torch.float32, device=dev)
-        _ws_cache[dev] = w
-    return w
+    """fp32 split-K partials of the decode kernels (capture-safe: DecodeStepGraph replays keep
+    the buffer they captured, ops/workspace.py)."""
+    return _DEC_WS.get(n, torch.float32, dev, min_numel=1 << 16)
 
 
 def _hip(*ts):

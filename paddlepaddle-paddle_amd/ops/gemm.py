@@ -14,6 +14,9 @@ import os
 import torch
 
 from . import _native as N
+from .workspace import workspace as _new_workspace
+
+_GEMM_WS = _new_workspace('gemm_partials')
 
 
 def _op_layout(t):
@@ -25,15 +28,9 @@ def _op_layout(t):
     return None, None
 
 
-_ws_cache = {}
-
-
 def _workspace(n, device):
-    w = _ws_cache.get(device)
-    if w is None or w.numel() < n:
-        w = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=device)
-        _ws_cache[device] = w
-    return w
+    """fp32 split-K / skinny-GEMM partials (capture-safe, ops/workspace.py)."""
+    return _GEMM_WS.get(n, torch.float32, device, min_numel=1 << 20)
 
 
 def hip_mm_ok(a, b, splitk=1):
@@ -317,8 +314,7 @@ _FP8_FMT = {torch.float8_e4m3fn: 0, torch.float8_e5m2: 1}
 _fp8_8phase = os.environ.get('PADDLE_AMD_FP8_8PHASE', '1') != '0'
 
 
-from .workspace import workspace as _workspace  # noqa: E402
-_FP8_WS = _workspace('fp8_splitk')
+_FP8_WS = _new_workspace('fp8_splitk')
 
 
 def _fp8_splitk(M, N_, K):
