@@ -77,6 +77,12 @@ template <int FA, int FB>
 struct F8 {
   static constexpr int fa = FA, fb = FB;
 };
+// int8 operands (signed), int32 accumulation, bf16 out with per-row x per-column dequant scales:
+// like fp8, the bf16 byte images are reused unchanged — a 64-element bf16 k-half (64 bytes) is 64
+// int8 k values, exactly one v_mfma_i32_16x16x64_i8 per fragment pair (the lane -> byte mapping of
+// the 16x16x64 i8 operand equals the 16x16x32 bf16 one; a k permutation shared by A and B leaves
+// the dot products exact).  The int32 sums live in the f32x4 accumulator registers as raw bits.
+struct I8T {};
 template <typename T>
 struct is_f8 { static constexpr bool value = false; };
 template <int FA, int FB>
@@ -89,9 +95,15 @@ struct OutT<f16_t> { using type = f16_t; };
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
 template <typename T>
 __device__ __forceinline__ f32x4 mfmaT(s16x8 a, s16x8 b, f32x4 c) {
-  if constexpr (__is_same(T, f16_t))
+  if constexpr (__is_same(T, I8T))
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, a),
+                                                                           __builtin_bit_cast(i32x4, b),
+                                                                           __builtin_bit_cast(i32x4, c), 0, 0, 0));
+  else if constexpr (__is_same(T, f16_t))
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
                                                   0);
   else
@@ -1296,6 +1308,25 @@ __global__ __launch_bounds__(512, 1) void gemm11_kernel(const char* __restrict__
   }
   if (wr == 0) bar();
 
+  if constexpr (__is_same(T, I8T)) {
+    // int32 sums -> fp32 with the dequant scales: sa = per-row (token) scales [M], sb = per-column
+    // (output channel) scales [N]; lane owns C[mb + 16i + (lane & 15)][nb + 16j + 4(lane >> 4) + r]
+    const int mb = m0 + wr * 128, nb = n0 + wc * 64;
+    float cs[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[j][r] = sb ? sb[min(nb + 16 * j + 4 * (lane >> 4) + r, N - 1)] : 1.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float rs = sa ? sa[min(mb + 16 * i + (lane & 15), M - 1)] : 1.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[i][j][r] = (float)__builtin_bit_cast(int, acc[i][j][r]) * rs * cs[j][r];
+    }
+  }
   if constexpr (EPI == 1)
     epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
   else if constexpr (EPI >= 200)  // wave-local staged epilogue of EPI - 200 (its own instantiation)

@@ -189,3 +189,26 @@ PA_API int pa_gemm8_fp8_splitk(const void* A, const void* W, void* C, const void
                                                                        (const float*)scale_b);
   return (int)hipGetLastError();
 }
+
+// int8 GEMM (LLM.int8 / W8A8): C[M,N] (bf16) = (A @ W^T) * row_scale[m] * col_scale[n] (+ beta * C)
+// (+ bias), A int8 [M][lda], W int8 [N][ldw] (both k-contiguous), int32 accumulation in
+// v_mfma_i32_16x16x64_i8 (2x the bf16 MFMA rate).  Reference: paddle/phi/kernels/gpu/
+// llm_int8_linear_kernel.cu (python/paddle/nn/quant/quantized_linear.py:239).
+// Contract: K % 128 == 0, M, N % 8 == 0, lda / ldw % 16, ldc % 8, spans < 4 GiB.
+PA_API int pa_gemm8_i8_ok(int M, int N, int K, long long lda, long long ldw, long long ldc) {
+  return pa_gemm8_fp8_ok(M, N, K, lda, ldw, ldc);
+}
+
+PA_API int pa_gemm8_i8(const void* A, const void* W, void* C, const void* bias, const float* row_scale,
+                       const float* col_scale, int M, int N, int K, long long lda, long long ldw, long long ldc,
+                       float beta, hipStream_t st) {
+  using namespace pa::g8;
+  if (!pa_gemm8_i8_ok(M, N, K, lda, ldw, ldc)) return (int)hipErrorInvalidValue;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  dim3 grid(tm * tn, 1, 1);
+  const int K2 = K / 2;  // the kernel counts k and leading dims in 2-byte units
+  gemm11_kernel<true, true, 200, I8T, false><<<grid, 512, 0, st>>>(
+      (const char*)A, (const char*)W, (uint16_t*)C, nullptr, (const uint16_t*)bias, M, N, K2, lda / 2, ldw / 2, ldc,
+      1.f, beta, K2, 0LL, 0LL, 0LL, row_scale, col_scale);
+  return (int)hipGetLastError();
+}

@@ -113,28 +113,79 @@ def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="in
     return y
 
 
+# outlier-column capacity of the GPU path (a multiple of 64: the 16-bit outlier GEMM's K)
+LLM_INT8_OUTLIER_CAP = 128
+
+
 def llm_int8_linear(x, weight, bias=None, weight_scale=None, threshold=6.0):
-    """LLM.int8 (reference quantized_linear.py llm_int8_linear): input feature columns holding any
+    """LLM.int8 (reference quantized_linear.py:239 llm_int8_linear): input feature columns holding any
     |x| > threshold are multiplied in floating point with the dequantised weight rows; the rest are
     quantised per token (absmax, int8) and multiplied against the int8 weight, rescaled by both
-    scales."""
+    scales.
+
+    On the GPU (bf16 / fp16 x, K % 128 == 0, N % 8 == 0) there is no host synchronisation: the
+    outlier columns are compacted on the device into a fixed-capacity set (``LLM_INT8_OUTLIER_CAP``
+    columns, outliers first by a stable device sort) whose 16-bit product runs on the hand-written
+    GEMM with the bias, then the int8 MFMA GEMM (csrc/gemm8x.hip pa_gemm8_i8, int32 accumulation,
+    per-token x per-channel dequant in its epilogue) accumulates onto it (beta = 1).  Should more
+    columns than the capacity exceed the threshold, the surplus ones stay on the int8 path (their
+    rows are then quantised with a larger scale) — exact LLM.int8 up to the capacity, graceful past
+    it.  Elsewhere: the exact composite."""
     if weight_scale is None:
         raise ValueError("llm_int8_linear needs weight_scale")
     t = _u(x)
     lead = t.shape[:-1]
-    a = t.reshape(-1, t.shape[-1]).float()
-    qw = _u(weight).float()                                                  # [n, k] int8 values
-    ws = _u(weight_scale).float()                                            # [n]
+    qw_i8 = _u(weight)
+    ws = _u(weight_scale)
+    K = t.shape[-1]
+    a16 = t.reshape(-1, K)
+    from ... import ops
+    if (a16.is_cuda and a16.dtype in (torch.bfloat16, torch.float16) and ops.use_hip(a16) and K % 128 == 0
+            and qw_i8.dtype == torch.int8 and qw_i8.dim() == 2 and qw_i8.shape[1] == K and qw_i8.shape[0] % 8 == 0):
+        y = _llm_int8_gpu(a16.contiguous(), qw_i8.contiguous(), ws, None if bias is None else _u(bias), threshold)
+        if y is not None:
+            return _w(y.to(t.dtype).reshape(*lead, -1))
+    a = a16.float()
+    qw = qw_i8.float()                                                       # [n, k] int8 values
+    wsf = ws.float()                                                         # [n]
     outl = (a.abs() > threshold).any(0)                                      # [k]
     a_in = a.masked_fill(outl[None, :], 0.0)
     sx = a_in.abs().amax(1, keepdim=True).clamp_min(1e-12) / 127.0           # [m, 1]
     qa = torch.round(a_in / sx).clamp(-127, 127)
-    y = (qa @ qw.t()) * sx * ws[None, :]
-    if bool(outl.any()):
-        y = y + a[:, outl] @ (qw[:, outl] * ws[:, None]).t()
+    y = (qa @ qw.t()) * sx * wsf[None, :]
+    y = y + (a * outl[None, :].float()) @ (qw * wsf[:, None]).t()            # outlier columns, fp32
     if bias is not None:
         y = y + _u(bias).float()
     return _w(y.to(t.dtype).reshape(*lead, -1))
+
+
+def _llm_int8_gpu(a, qw, ws, bias, threshold):
+    from ...ops import int8 as I8, matmul as hm
+    M, K = a.shape
+    Nn = qw.shape[0]
+    M8 = -(-M // 8) * 8
+    if not I8.quant_rows_ok(a):
+        return None
+    cap = min(K, LLM_INT8_OUTLIER_CAP)
+    outl = (a.abs() > threshold).any(0)                                      # [K] bool, device
+    order = torch.argsort((~outl).to(torch.int8), stable=True)               # outlier columns first
+    idx = order[:cap]
+    sel = outl.index_select(0, idx)                                          # which of them are outliers
+    excl = torch.zeros(K, dtype=torch.uint8, device=a.device)
+    excl.index_copy_(0, idx, sel.to(torch.uint8))
+    qa, sx = I8.quant_rows(a, excl, rows=M8)                                 # int8 [M8, K], fp32 [M8]
+    # 16-bit outlier product (+ bias) first: [M, cap] @ [cap, N]
+    a_o = a.index_select(1, idx) * sel.to(a.dtype)
+    w_o = (qw.index_select(1, idx).float() * ws.float()[:, None]).to(a.dtype).t().contiguous()
+    a_o8 = a_o if M8 == M else torch.cat([a_o, a_o.new_zeros(M8 - M, cap)])
+    b = None if bias is None else bias.to(a.dtype)
+    out = hm.linear(a_o8, w_o, b)
+    if out.dtype != torch.bfloat16:
+        out = out.to(torch.bfloat16)
+    if not I8.i8_mm_ok(qa, qw):
+        return None
+    out = I8.i8_mm(qa, qw, sx, ws, out=out.contiguous(), beta=1.0)
+    return out[:M]
 
 
 def apply_per_channel_scale(x, scales):

@@ -277,3 +277,56 @@ def _woq_case(bits, group, M, dt):
         woq.woq_linear = orig
     assert calls, 'weight-only kernel did not run'
     _close(y, ref, 2e-2, f'woq bits={bits} group={group} M={M}')
+
+
+@pytest.mark.parametrize('M,N,K', [(512, 768, 1024), (1000, 4096, 2048), (8, 256, 128), (4096, 2048, 4096)])
+def test_int8_mfma_gemm(M, N, K):
+    """pa_gemm8_i8 (v_mfma_i32_16x16x64_i8): exact int32 sums, per-row x per-column dequant, bias,
+    beta accumulate — vs the fp32 product of the int8 values."""
+    from paddle.ops import int8 as I8
+    g = torch.Generator(device=DEV).manual_seed(21)
+    a = torch.randint(-127, 128, (M, K), device=DEV, generator=g, dtype=torch.int32).to(torch.int8)
+    w = torch.randint(-127, 128, (N, K), device=DEV, generator=g, dtype=torch.int32).to(torch.int8)
+    rs = torch.rand(M, device=DEV, generator=g) * 0.01
+    cs = torch.rand(N, device=DEV, generator=g) * 0.01
+    bias = _rand(N, g=g)
+    assert I8.i8_mm_ok(a, w)
+    out = I8.i8_mm(a, w, rs, cs, bias=bias)
+    exact = (a.double() @ w.double().t())
+    ref = (exact * rs.double()[:, None] * cs.double()[None, :]).float() + bias.float()
+    _close(out, ref, 1e-2, f'int8 {M}x{N}x{K}')
+    out2 = I8.i8_mm(a, w, rs, cs, out=out.clone(), beta=1.0)
+    _close(out2, ref + (exact * rs.double()[:, None] * cs.double()[None, :]).float(), 1.5e-2, 'int8 beta')
+
+
+@pytest.mark.parametrize('M', [1, 7, 100, 512])
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16])
+def test_llm_int8_linear_gpu(M, dt):
+    """llm_int8_linear on the int8 MFMA GEMM + the 16-bit outlier GEMM (no host sync) vs the fp32
+    LLM.int8 formula; outlier columns planted."""
+    from paddle.nn.quant import weight_quantize, llm_int8_linear
+    from paddle.ops import int8 as I8
+    g = torch.Generator(device=DEV).manual_seed(22)
+    K, N_ = 1024, 768
+    w = torch.randn(K, N_, device=DEV, generator=g) * 0.05
+    q, s = weight_quantize(paddle.to_tensor(w), algo='llm.int8')
+    x = torch.randn(M, K, device=DEV, generator=g)
+    x[:, [5, 77, 900]] *= 30.0
+    x = x.to(dt)
+    b = torch.randn(N_, device=DEV, generator=g).to(dt)
+    calls = []
+    orig = I8.i8_mm
+    I8.i8_mm = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]
+    try:
+        y = llm_int8_linear(paddle.to_tensor(x), q, paddle.to_tensor(b), s, threshold=6.0)._t
+    finally:
+        I8.i8_mm = orig
+    assert calls, 'int8 kernel did not run'
+    a = x.float()
+    outl = (a.abs() > 6.0).any(0)
+    a_in = a.masked_fill(outl[None, :], 0.0)
+    sx = a_in.abs().amax(1, keepdim=True).clamp_min(1e-12) / 127.0
+    qa = torch.round(a_in / sx).clamp(-127, 127)
+    qw, ws = q._t.float(), s._t.float()
+    ref = (qa @ qw.t()) * sx * ws[None, :] + (a * outl.float()) @ (qw * ws[:, None]).t() + b.float()
+    _close(y, ref, 3e-2, f'llm.int8 M={M} {dt}')

@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r5c
-timeout -k 10 400 python -u -m pytest -x -q -m gpu --timeout 200 --timeout-method thread tests/test_hip_matmul.py -k "fp8 or amp" tests/test_fp8.py tests/test_hip_amp.py > gpurun_out/r5c/tests.log 2>&1 || { echo "tests failed"; tail -60 gpurun_out/r5c/tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest -x -q -m gpu --timeout 200 --timeout-method thread tests/test_hip_matmul.py -k "fp8 or amp or int8" tests/test_fp8.py tests/test_hip_amp.py > gpurun_out/r5c/tests.log 2>&1 || { echo "tests failed"; tail -60 gpurun_out/r5c/tests.log; exit 1; }
 tail -2 gpurun_out/r5c/tests.log
 timeout -k 10 300 python tools/ernie_gemm_ab.py > gpurun_out/r5c/gemm_ab.log 2>&1 || { echo "gemm ab failed"; tail -30 gpurun_out/r5c/gemm_ab.log; exit 1; }
 grep -v amdgpu.ids gpurun_out/r5c/gemm_ab.log
