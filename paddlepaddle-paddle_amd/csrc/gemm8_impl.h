@@ -97,12 +97,19 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
+// accumulator register type per operand tag: int32 sums for int8 (kept as i32x4 through the whole
+// loop — carrying them in f32x4 registers through bit casts miscompiles on ROCm 7.2: only element
+// 0 of a bit-cast MFMA result survives, tools/probe/i8_mfma_probe.hip)
 template <typename T>
-__device__ __forceinline__ f32x4 mfmaT(s16x8 a, s16x8 b, f32x4 c) {
+struct AccOf { using type = f32x4; };
+template <>
+struct AccOf<I8T> { using type = i32x4; };
+
+template <typename T, typename A>
+__device__ __forceinline__ A mfmaT(s16x8 a, s16x8 b, A c) {
   if constexpr (__is_same(T, I8T))
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, a),
-                                                                           __builtin_bit_cast(i32x4, b),
-                                                                           __builtin_bit_cast(i32x4, c), 0, 0, 0));
+    return __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, a), __builtin_bit_cast(i32x4, b), c, 0, 0,
+                                                 0);
   else if constexpr (__is_same(T, f16_t))
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
                                                   0);
@@ -1147,6 +1154,30 @@ __global__ __launch_bounds__(512, 1) void gemm9_kernel(const char* __restrict__ 
 }
 
 
+// epilogue dispatch of schedule 11 (shared by the float and the int8 accumulator forms)
+template <int EPI, typename T>
+__device__ __forceinline__ void gemm11_epilogue(const f32x4 (&acc)[8][4], uint16_t* __restrict__ C,
+                                                float* __restrict__ ws, const uint16_t* __restrict__ bias, int M, int N,
+                                                long long ldc, float alpha, float beta, int m0, int n0, int wr, int wc,
+                                                int lane, char* smem) {
+  if constexpr (EPI == 1)
+    epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
+  else if constexpr (EPI >= 200)  // wave-local staged epilogue of EPI - 200 (its own instantiation)
+    epilogue_wstaged<EPI - 200, typename OutT<T>::type>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128,
+                                                        n0 + wc * 64, lane, (lds_char*)smem + (wr * 4 + wc) * 16384);
+  else if constexpr (EPI >= 100)  // block-staged epilogue of EPI - 100 (its own instantiation)
+    epilogue_staged<EPI - 100>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0, n0, wr, wc, lane, (lds_char*)smem);
+  else if constexpr (EPI == 5)  // batch-norm statistics: the register epilogue carries them
+    epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
+  else if constexpr (EPI == 4)
+    epilogue_wide<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
+  else if (g_wide_epi)
+    epilogue_wide<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
+  else
+    epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
+}
+
+
 // ---------------------------------------------------------------------------------------------
 // Schedule 11: schedule 8's images (row halves, full 128-B lines for k-contiguous operands) with
 // 32 MFMAs per segment instead of 16, halving the barriers per K-tile (4 per wave):
@@ -1211,11 +1242,11 @@ __global__ __launch_bounds__(512, 1) void gemm11_kernel(const char* __restrict__
     for (int u = 0; u < 4; ++u) glds(base, offB[u], d + u * 1024);
   };
 
-  f32x4 acc[8][4];
+  typename AccOf<T>::type acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) acc[i][j] = typename AccOf<T>::type{0, 0, 0, 0};
 
   // prologue in the steady-state issue order
   if (wr == 0) {
@@ -1317,32 +1348,21 @@ __global__ __launch_bounds__(512, 1) void gemm11_kernel(const char* __restrict__
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) cs[j][r] = sb ? sb[min(nb + 16 * j + 4 * (lane >> 4) + r, N - 1)] : 1.f;
+    f32x4 accf[8][4];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float rs = sa ? sa[min(mb + 16 * i + (lane & 15), M - 1)] : 1.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          acc[i][j][r] = (float)__builtin_bit_cast(int, acc[i][j][r]) * rs * cs[j][r];
+        for (int r = 0; r < 4; ++r) accf[i][j][r] = (float)acc[i][j][r] * rs * cs[j][r];
     }
+    gemm11_epilogue<EPI, T>(accf, C, ws, bias, M, N, ldc, alpha, beta, m0, n0, wr, wc, lane, smem);
+  } else {
+    gemm11_epilogue<EPI, T>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0, n0, wr, wc, lane, smem);
   }
-  if constexpr (EPI == 1)
-    epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
-  else if constexpr (EPI >= 200)  // wave-local staged epilogue of EPI - 200 (its own instantiation)
-    epilogue_wstaged<EPI - 200, typename OutT<T>::type>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128,
-                                                        n0 + wc * 64, lane, (lds_char*)smem + (wr * 4 + wc) * 16384);
-  else if constexpr (EPI >= 100)  // block-staged epilogue of EPI - 100 (its own instantiation)
-    epilogue_staged<EPI - 100>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0, n0, wr, wc, lane, (lds_char*)smem);
-  else if constexpr (EPI == 5)  // batch-norm statistics: the register epilogue carries them
-    epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
-  else if constexpr (EPI == 4)
-    epilogue_wide<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
-  else if (g_wide_epi)
-    epilogue_wide<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
-  else
-    epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
 }
+
 
 
 // ---------------------------------------------------------------------------------------------

@@ -225,7 +225,10 @@ class _LinearFn(torch.autograd.Function):
         g2 = g.reshape(-1, g.shape[-1])
         dx = matmul(g2, w.t()).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
         dw = matmul(x2.t(), g2) if ctx.needs_input_grad[1] else None
-        db = g2.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        db = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            from . import fused
+            db = fused.colsum(g2.contiguous()).to(g2.dtype) if fused.colsum_ok(g2.contiguous()) else g2.sum(0)
         return dx, dw, db
 
 
@@ -249,7 +252,15 @@ def linear(x, w, bias=None):
 
 def addmm(inp, x, y, beta=1.0, alpha=1.0):
     """beta * inp + alpha * (x @ y)."""
-    if not _use(x, y) or torch.is_grad_enabled() and any(t.requires_grad for t in (inp, x, y)):
+    if not _use(x, y):
+        return torch.addmm(inp, x, y, beta=beta, alpha=alpha)
+    if torch.is_grad_enabled() and any(t.requires_grad for t in (inp, x, y)):
+        # a Linear with its bias (the recorded form of nn.Linear in static programs): all three
+        # GEMMs on the hand-written kernels (ERNIE-base shapes fwd + dgrad + wgrad 1.01-1.23x the
+        # library, profiles/r5c_ernie_gemm_ab.log)
+        if (beta == 1.0 and alpha == 1.0 and x.dim() == 2 and y.dim() == 2 and inp.dim() == 1
+                and inp.numel() == y.shape[1] and _use(x, inp)):
+            return _LinearFn.apply(x, y, inp)
         return torch.addmm(inp, x, y, beta=beta, alpha=alpha)
     if x.dim() == 2 and y.dim() == 2 and inp.dtype == x.dtype and inp.is_cuda:
         if inp.dim() == 1 and inp.numel() == y.shape[1] and beta == 1.0 and alpha == 1.0:

@@ -100,6 +100,24 @@ def fused_attention(q, k, v, mask=None, scale=1.0, dropout=0.0, mask_mode=None, 
     return torch.matmul(p.to(v.dtype), v)
 
 
+def fused_attention_packed(qkv, mask=None, scale=1.0, dropout=0.0, mask_mode=None, fill=-1e30):
+    """The same attention with q / k / v the three [B, S, H, D] slices of one packed [B, S, 3, H, D]
+    projection (dim 2): the packed flash path writes dQ / dK / dV straight into one packed gradient
+    (no per-slice zero-filled gradient buffers and adds).  Returns [B, H, S, D]."""
+    if (qkv.dim() == 5 and qkv.shape[2] == 3 and qkv.dtype in (torch.bfloat16, torch.float16) and _hip(qkv)
+            and (mask is None or (isinstance(mask, torch.Tensor) and mask.device == qkv.device and mask.dim() <= 4))):
+        from ..ops import flash_attn as FA
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        if FA.supported(q, k, v):
+            m = _attn_mask(mask, mask_mode, fill, qkv.dtype)
+            if m is not None and m.dim() < 4:
+                m = m.reshape((1,) * (4 - m.dim()) + tuple(m.shape))
+            o = FA.flash_attention_packed_ex(qkv, scale=float(scale), mask=m, dropout=float(dropout))
+            return o.transpose(1, 2)
+    q, k, v = (qkv[:, :, i].transpose(1, 2) for i in range(3))
+    return fused_attention(q, k, v, mask, scale, dropout, mask_mode, False, fill)
+
+
 def _norm_ok(x, w, b):
     C = x.shape[-1]
     return (_hip(x) and w is not None and b is not None and w.dim() == 1 and w.numel() == C and b.numel() == C
@@ -168,7 +186,7 @@ def fused_softmax(x, dim=-1):
     return torch.softmax(x, dim)
 
 
-FUSED_TARGETS = (fused_attention, fused_layer_norm, fused_dropout_add_layer_norm, fused_linear, fused_softmax)
+FUSED_TARGETS = (fused_attention, fused_attention_packed, fused_layer_norm, fused_dropout_add_layer_norm, fused_linear, fused_softmax)
 
 
 # ============================================================================ node vocabulary
@@ -194,6 +212,7 @@ def _init_kinds():
         'reshape': [T.reshape, T.view, torch.reshape],
         'gelu': [TF.gelu],
         'relu': [torch.relu, TF.relu, T.relu],
+        'getitem': [T.__getitem__],
     }
     for k, fs in table.items():
         for f in fs:
@@ -505,6 +524,20 @@ def _attention(g, i):
     for r_ in (q_ref, k_ref, v_ref):
         if g.rank(r_) not in (None, 4):
             return None
+    # q / k / v as transposed slices 0 / 1 / 2 of one packed [B, S, 3, H, D] projection
+    packed = None
+    if not k_transposed:
+        srcs = [_packed_slice(g, r_, idx, i) for idx, r_ in enumerate((q_ref, k_ref, v_ref))]
+        if all(sr is not None for sr in srcs) and len({sr[0].vid for sr in srcs}) == 1 and \
+                g.rank(srcs[0][0]) in (None, 5):
+            body = sorted(set(chain + [j_ for sr in srcs for j_ in sr[1]]))
+            if g.private(body, users=(i,)):
+                packed = srcs[0][0]
+    if packed is not None:
+        node = Node('torch', fused_attention_packed, [packed, mask],
+                    {'scale': scale, 'dropout': drop, 'mask_mode': mode, 'fill': fill},
+                    n.outs, dict(n.meta or {}, fused='multihead_matmul_fuse_pass_v2'))
+        return body + [i], {i: node}
     body = sorted(set(chain))
     if not g.private(body, users=(i,)):
         return None
@@ -512,6 +545,24 @@ def _attention(g, i):
                 {'scale': scale, 'dropout': drop, 'mask_mode': mode, 'k_transposed': k_transposed, 'fill': fill},
                 n.outs, dict(n.meta or {}, fused='multihead_matmul_fuse_pass_v2'))
     return body + [i], {i: node}
+
+
+def _packed_slice(g, ref, idx, before):
+    """(P, [node indices]) when ``ref`` = P[:, :, idx].transpose(1, 2), else None."""
+    tj = g.producer(ref.vid, before)
+    tn = g.node(tj)
+    if _kind(tn) != 'transpose' or len(tn.args) != 3 or not isinstance(tn.args[0], Ref) or \
+            {tn.args[1], tn.args[2]} != {1, 2}:
+        return None
+    gj = g.producer(tn.args[0].vid, tj)
+    gn = g.node(gj)
+    if _kind(gn) != 'getitem' or len(gn.args) != 2 or not isinstance(gn.args[0], Ref):
+        return None
+    key = gn.args[1]
+    full = slice(None, None, None)
+    if not (isinstance(key, tuple) and len(key) == 3 and key[0] == full and key[1] == full and key[2] == idx):
+        return None
+    return gn.args[0], [tj, gj]
 
 
 def _ln_args(n):

@@ -52,9 +52,9 @@ class _Count:
 
 def test_ernie_static_fused_kernels_match_unfused_program():
     ref, _ = _run(False, 0.0, '0', steps=1)
-    with _Count(FA, 'flash_attention_ex') as ca, _Count(NORM, 'add_layer_norm') as cn:
+    with _Count(FA, 'flash_attention_packed_ex') as ca, _Count(NORM, 'add_layer_norm') as cn:
         out, stats = _run(False, 0.0, 'auto', steps=1)
-    assert stats.get('multihead_matmul_fuse_pass_v2') == 2, stats
+    assert stats.get('multihead_matmul_fuse_pass_v2') == 2, stats  # packed q / k / v slices of the qkv GEMM
     # 4 of the 5 add + LayerNorm sites: the embedding sum stays fp32 under O1 autocast (embedding
     # lookups are not autocast ops), so that one takes the composite
     assert ca.n == 2 and cn.n == 4, (ca.n, cn.n)
@@ -84,7 +84,7 @@ def test_ernie_static_amp_bf16_training_fused():
                 opt.minimize(loss)
             exe = static.Executor(paddle.CUDAPlace(0))
             opt.amp_init(paddle.CUDAPlace(0))
-            with _Count(FA, 'flash_attention_ex') as ca, _Count(FUSED, 'dropout_add_norm') as cd:
+            with _Count(FA, 'flash_attention_packed_ex') as ca, _Count(FUSED, 'dropout_add_norm') as cd:
                 losses = [float(np.asarray(exe.run(main, feed=_feed(), fetch_list=[loss])[0]).reshape(-1)[0])
                           for _ in range(8)]
         finally:

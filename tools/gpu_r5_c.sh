@@ -16,3 +16,5 @@ trace=$(find gpurun_out/r5c/prof_fp8 -name "*kernel_trace.csv" | head -1)
 python3 tools/prof_steady.py "$trace" spin_kernel 3 30 > gpurun_out/r5c/ernie_fp8_steady.txt 2>&1
 head -36 gpurun_out/r5c/ernie_fp8_steady.txt
 rm -f "$trace"
+timeout -k 10 300 python tools/matmul_bench.py > gpurun_out/r5c/matmul_bench.log 2>&1 || { echo "matmul bench failed"; tail -20 gpurun_out/r5c/matmul_bench.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/r5c/matmul_bench.log
