@@ -110,6 +110,16 @@ class Config:
     def switch_ir_optim(self, x=True):
         self._ir_optim = x
 
+    def pass_builder(self):
+        """The IR fusion pass list applied to the loaded program (reference
+        paddle_pass_builder.h PassStrategy: passes / delete_pass / append_pass / insert_pass)."""
+        if getattr(self, '_pass_builder', None) is None:
+            self._pass_builder = PassStrategy()
+        return self._pass_builder
+
+    def delete_pass(self, name):
+        self.pass_builder().delete_pass(name)
+
     def ir_optim(self):
         return self._ir_optim
 
@@ -142,6 +152,41 @@ class Config:
     def summary(self):
         return (f"model: {self._prefix}\nuse_gpu: {self._use_gpu} (device {self._device_id})\n"
                 f"precision: {self._precision.name}\nhip_graph: {self._hip_graph}")
+
+
+class PassStrategy:
+    """Ordered IR pass names (static/ir_passes.py); unknown names are kept but ignored."""
+
+    def __init__(self, passes=None):
+        from ..static.ir_passes import DEFAULT_PASSES
+        self._passes = list(DEFAULT_PASSES if passes is None else passes)
+        self._debug = False
+
+    def passes(self):
+        return list(self._passes)
+
+    def all_passes(self):
+        return self.passes()
+
+    def delete_pass(self, name):
+        self._passes = [p for p in self._passes if p != name]
+
+    def append_pass(self, name):
+        self._passes.append(name)
+
+    def insert_pass(self, idx, name):
+        self._passes.insert(idx, name)
+
+    def clear_passes(self):
+        self._passes = []
+
+    def turn_on_debug(self):
+        self._debug = True
+
+    def _known(self):
+        from ..static.ir_passes import pass_names
+        known = set(pass_names())
+        return [p for p in self._passes if p in known]
 
 
 class Tensor:
@@ -206,6 +251,12 @@ class Predictor:
             for cid, t in list(self._program.consts.items()):
                 if t.is_floating_point():
                     self._program.consts[cid] = t.to(dt)
+        # IR fusion passes (static/ir_passes.py) on the loaded program: switch_ir_optim(False) turns
+        # them off, pass_builder() edits the list
+        self._program._ir_optim = bool(config._ir_optim)
+        pb = getattr(config, '_pass_builder', None)
+        if pb is not None:
+            self._program._ir_passes = tuple(pb._known())
         self._out_names = [f"fetch_{i}" for i in range(len(self._fetch))]
         self._inputs = {}
         self._outputs = {}

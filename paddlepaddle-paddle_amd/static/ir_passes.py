@@ -125,8 +125,22 @@ def _norm_ok(x, w, b):
             and w.is_cuda)
 
 
-def fused_layer_norm(x, weight=None, bias=None, eps=1e-5):
-    """layer_norm over the last dim on csrc/norm.hip (composite otherwise)."""
+def _ln_composite(x, weight, bias, eps, axis):
+    ns = list(x.shape[axis:])
+    w = None if weight is None else weight.reshape(ns)
+    b = None if bias is None else bias.reshape(ns)
+    return TF.layer_norm(x, ns, w, b, eps)
+
+
+def _last_axis(x, axis):
+    return axis is None or axis in (-1, x.dim() - 1)
+
+
+def fused_layer_norm(x, weight=None, bias=None, eps=1e-5, begin_axis=None):
+    """layer_norm over the last dim on csrc/norm.hip (composite otherwise); ``begin_axis``: an
+    imported layer_norm's begin_norm_axis (normalises dims [begin_axis:])."""
+    if not _last_axis(x, begin_axis):
+        return _ln_composite(x, weight, bias, eps, begin_axis)
     if _norm_ok(x, weight, bias):
         from ..ops import norm
         return norm.layer_norm(x, weight, bias, float(eps))
@@ -135,9 +149,13 @@ def fused_layer_norm(x, weight=None, bias=None, eps=1e-5):
     return TF.layer_norm(x, [x.shape[-1]], w, b, eps)
 
 
-def fused_dropout_add_layer_norm(x, res, weight=None, bias=None, eps=1e-5, p=0.0):
+def fused_dropout_add_layer_norm(x, res, weight=None, bias=None, eps=1e-5, p=0.0, begin_axis=None):
     """[layer_norm(dropout(x, p) + res), dropout(x, p) + res] — one kernel each way on the GPU.
     Under AMP a float32 residual stream is carried in x's 16-bit dtype (the reference's O2)."""
+    if not _last_axis(x, begin_axis):
+        h = TF.dropout(x, p, True) if p > 0.0 else x
+        s = h + res
+        return [_ln_composite(s, weight, bias, eps, begin_axis), s]
     if (_norm_ok(x, weight, bias) and isinstance(res, torch.Tensor) and res.shape == x.shape
             and x.dtype in (torch.bfloat16, torch.float16)):
         from ..ops import norm, fused
@@ -246,6 +264,15 @@ def _num(v):
     return isinstance(v, (int, float)) and not isinstance(v, bool)
 
 
+def _one_out(n):
+    """The output of a single-output node as the executor binds it (imported operators keep a
+    one-element list of vids)."""
+    o = n.outs
+    if isinstance(o, (list, tuple)) and len(o) == 1 and isinstance(o[0], int):
+        return o[0]
+    return o
+
+
 def _pd_in(n, slot, i=0):
     """i-th argument of input slot ``slot`` of an imported-operator node (None if absent)."""
     pos = 0
@@ -336,9 +363,20 @@ class _Graph:
         if not isinstance(ref, Ref):
             return None
         j = self.producer(ref.vid, before)
-        while j is not None and _kind(self.nodes[j]) == 'cast' and self._pure_cast(self.nodes[j]):
+        while j is not None:
+            nj = self.nodes[j]
+            k = _kind(nj)
+            if k == 'cast' and self._pure_cast(nj):
+                inner = nj.args[0]
+            elif k in ('pd.cast', 'pd.assign') or (k == 'pd.dropout' and nj.target.attrs.get('is_test', False) and
+                                                   nj.target.attrs.get('dropout_implementation') ==
+                                                   'upscale_in_train'):
+                inner = _pd_in(nj, 'X')
+                if len(_outs_of(nj.outs, [])) != 1:
+                    return None
+            else:
+                break
             chain.append(j)
-            inner = self.nodes[j].args[0]
             if not isinstance(inner, Ref):
                 return None
             j = self.producer(inner.vid, j)
@@ -471,6 +509,25 @@ def _attention(g, i):
             mask, mode = m, 'drop'
         chain.append(j)
         j = g.src(x, j, chain)
+    elif kj == 'pd.where':
+        cond, xv, yv = _pd_in(nj, 'Condition'), _pd_in(nj, 'X'), _pd_in(nj, 'Y')
+        fj = g.producer(xv.vid, j) if isinstance(xv, Ref) else None
+        fn = g.node(fj)
+        if _kind(fn) != 'pd.fill_constant' or _pd_in(fn, 'ShapeTensor') is not None or \
+                float(fn.target.attrs.get('value', 0.0)) > -1e4 or not isinstance(cond, Ref):
+            return None
+        fill = float(fn.target.attrs.get('value'))
+        chain.append(fj)
+        mj = g.producer(cond.vid, j)
+        mn = g.node(mj)
+        if _kind(mn) == 'pd.logical_not' and isinstance(_pd_in(mn, 'X'), Ref) and cond.vid not in g.external and \
+                g.uses.get(cond.vid, set()) <= {j}:
+            mask, mode = _pd_in(mn, 'X'), 'keep'
+            chain.append(mj)
+        else:
+            mask, mode = cond, 'drop'
+        chain.append(j)
+        j = g.src(yv, j, chain)
     elif kj in ('add', 'pd.elementwise_add'):
         a, b = (nj.args[0], nj.args[1]) if kj == 'add' else (_pd_in(nj, 'X'), _pd_in(nj, 'Y'))
         if kj == 'add' and (len(nj.args) != 2 or nj.kwargs):
@@ -536,14 +593,14 @@ def _attention(g, i):
     if packed is not None:
         node = Node('torch', fused_attention_packed, [packed, mask],
                     {'scale': scale, 'dropout': drop, 'mask_mode': mode, 'fill': fill},
-                    n.outs, dict(n.meta or {}, fused='multihead_matmul_fuse_pass_v2'))
+                    _one_out(n), dict(n.meta or {}, fused='multihead_matmul_fuse_pass_v2'))
         return body + [i], {i: node}
     body = sorted(set(chain))
     if not g.private(body, users=(i,)):
         return None
     node = Node('torch', fused_attention, [q_ref, k_ref, v_ref, mask],
                 {'scale': scale, 'dropout': drop, 'mask_mode': mode, 'k_transposed': k_transposed, 'fill': fill},
-                n.outs, dict(n.meta or {}, fused='multihead_matmul_fuse_pass_v2'))
+                _one_out(n), dict(n.meta or {}, fused='multihead_matmul_fuse_pass_v2'))
     return body + [i], {i: node}
 
 
@@ -586,11 +643,18 @@ def _ln_args(n):
 
 
 def _ln_rank_ok(g, n, x):
+    """An imported layer_norm whose rank is known must normalise the last dim; with the rank
+    unknown (ProgramDesc values carry no shapes here) the fused node checks begin_norm_axis at run
+    time and takes the composite otherwise."""
     if _kind(n) == 'pd.layer_norm':
         r = g.rank(x)
         ax = n.target.attrs.get('begin_norm_axis', 1)
-        return r is not None and ax in (-1, r - 1)
+        return r is None or ax in (-1, r - 1)
     return True
+
+
+def _ln_axis(n):
+    return n.target.attrs.get('begin_norm_axis', 1) if _kind(n) == 'pd.layer_norm' else None
 
 
 def _ln_out(n):
@@ -651,7 +715,8 @@ def _add_ln(g, i, with_dropout):
         if any(isinstance(t, Ref) and (g.producer(t.vid, i) or -1) > aj for t in (w, b)):
             return None
         ln_out = _ln_out(n)
-        node = Node('torch', fused_dropout_add_layer_norm, [src, res, w, b], {'eps': eps, 'p': p},
+        node = Node('torch', fused_dropout_add_layer_norm, [src, res, w, b], {'eps': eps, 'p': p,
+                                                                            'begin_axis': _ln_axis(n)},
                     [ln_out, add_out[0]], dict(n.meta or {},
                                                fused='fused_dropout_add_layernorm' if with_dropout else
                                                'skip_layernorm_fuse_pass'))
@@ -669,7 +734,7 @@ def _layer_norm(g, i):
     if any(v in g.external or g.uses.get(v) for v in extra):
         return None
     x, w, b, eps = la
-    node = Node('torch', fused_layer_norm, [x, w, b], {'eps': eps}, _ln_out(n),
+    node = Node('torch', fused_layer_norm, [x, w, b], {'eps': eps, 'begin_axis': _ln_axis(n)}, _ln_out(n),
                 dict(n.meta or {}, fused='layer_norm_fuse_pass'))
     return [i], {i: node}
 
@@ -738,7 +803,7 @@ def _softmax(g, i):
         x = _pd_in(n, 'X')
     else:
         return None
-    return [i], {i: Node('torch', fused_softmax, [x], {}, n.outs, dict(n.meta or {}, fused='softmax_fuse_pass'))}
+    return [i], {i: Node('torch', fused_softmax, [x], {}, _one_out(n), dict(n.meta or {}, fused='softmax_fuse_pass'))}
 
 
 _PASSES = {
@@ -797,7 +862,8 @@ def ir_nodes(prog, dev):
     program version and pass list), or prog.nodes itself when fusion is off."""
     if not _enabled(prog, dev) or not prog.nodes:
         return prog.nodes
-    passes = tuple(getattr(prog, '_ir_passes', None) or DEFAULT_PASSES)
+    passes = getattr(prog, '_ir_passes', None)
+    passes = tuple(DEFAULT_PASSES if passes is None else passes)
     key = (len(prog.nodes), id(prog.nodes[-1]), passes)
     c = getattr(prog, '_ir_cache', None)
     if c is not None and c[0] == key:

@@ -545,6 +545,8 @@ OPS = {
     'reduce_max': _reduce(lambda x, d, k: x.amax(d, keepdim=k)),
     'mean': lambda ins, at: {'Out': [_one(ins, 'X').mean()]},
     'lookup_table_v2': _lookup, 'dropout': _dropout,
+    'expand_as_v2': lambda ins, at: {'Out': [_one(ins, 'X').expand_as(_one(ins, 'Y')) if ins.get('Y') else
+                                             _one(ins, 'X').expand(at['target_shape'])]},
     'assign': lambda ins, at: {'Out': [_one(ins, 'X')]},
     'clip': lambda ins, at: {'Out': [torch.clamp(_one(ins, 'X'), at.get('min'), at.get('max'))]},
     'arg_max': lambda ins, at: {'Out': [torch.argmax(_one(ins, 'X'), at.get('axis', -1),
@@ -883,8 +885,17 @@ def _emit(ex, n):
         else:
             ex.op('elementwise_' + base, {'X': ex.name_of(x), 'Y': ex.name_of(y)}, {'Out': out}, axis=-1)
     elif t in ('reshape', 'view'):
-        shape = a[1:] if len(a) > 2 else a[1]
-        ex.op('reshape2', {'X': X()}, {'Out': out, 'XShape': ex.new_tmp()}, shape=_ints(shape))
+        shape = list(a[1:] if len(a) > 2 else a[1])
+        xm = ex.meta.get(a[0].vid) if isinstance(a[0], Ref) else None
+        tgt = []
+        for i, v in enumerate(shape):
+            # a dynamic (sentinel) extent kept in place is reshape2's 0 ("copy input dim i"), so at
+            # most one -1 is left to infer
+            if xm is not None and i < xm.dim() and isinstance(v, int) and v == xm.shape[i] and v in _SENT:
+                tgt.append(0)
+            else:
+                tgt.append(_lit_int(v))
+        ex.op('reshape2', {'X': X()}, {'Out': out, 'XShape': ex.new_tmp()}, shape=tgt)
     elif t == 'permute':
         dims = a[1:] if len(a) > 2 else a[1]
         ex.op('transpose2', {'X': X()}, {'Out': out, 'XShape': ex.new_tmp()}, axis=[int(d) for d in dims])
@@ -925,6 +936,70 @@ def _emit(ex, n):
             raise Unsupported("to() without dtype")
         ex.op('cast', {'X': X()}, {'Out': out}, in_dtype=P.dtype_code(ex.meta[a[0].vid].dtype)
               if isinstance(a[0], Ref) and a[0].vid in ex.meta else 5, out_dtype=P.dtype_code(dt))
+    elif t in ('ne', 'eq', 'lt', 'le', 'gt', 'ge', '__ne__', '__eq__', '__lt__', '__le__', '__gt__', '__ge__') \
+            and len(a) == 2:
+        typ = {'ne': 'not_equal', 'eq': 'equal', 'lt': 'less_than', 'le': 'less_equal', 'gt': 'greater_than',
+               'ge': 'greater_equal'}[t.strip('_')]
+        y = a[1]
+        if scalar(y):
+            c = ex.new_tmp()
+            xm = ex.meta.get(a[0].vid) if isinstance(a[0], Ref) else None
+            ex.op('fill_constant', {}, {'Out': c}, shape=[1], value=float(y),
+                  dtype=P.dtype_code(xm.dtype if xm is not None else torch.float32))
+            yname = c
+        else:
+            yname = ex.name_of(y)
+        ex.op(typ, {'X': X(), 'Y': yname}, {'Out': out}, axis=-1)
+    elif t == 'arange' and len(a) == 1 and scalar(a[0]):
+        n_ = _lit_int(a[0])
+        if n_ < 0:
+            raise Unsupported("arange over a dynamic dim")
+        ex.op('assign_value', {}, {'Out': out}, shape=[n_], dtype=P.dtype_code(torch.int64),
+              int64_values=list(range(n_)))
+    elif t == 'expand_as':
+        ex.op('expand_as_v2', {'X': X(), 'Y': ex.name_of(a[1])}, {'Out': out})
+    elif t in ('zeros_like', 'ones_like'):
+        dt = k.get('dtype') or (ex.meta[a[0].vid].dtype if isinstance(a[0], Ref) and a[0].vid in ex.meta else None)
+        ex.op('fill_any_like', {'X': X()}, {'Out': out}, value=0.0 if t == 'zeros_like' else 1.0,
+              dtype=P.dtype_code(dt) if dt is not None else -1)
+    elif t == 'bool':
+        ex.op('cast', {'X': X()}, {'Out': out}, in_dtype=P.dtype_code(ex.meta[a[0].vid].dtype)
+              if isinstance(a[0], Ref) and a[0].vid in ex.meta else 3, out_dtype=P.dtype_code(torch.bool))
+    elif t in ('__invert__', 'logical_not', 'bitwise_not'):
+        xm = ex.meta.get(a[0].vid) if isinstance(a[0], Ref) else None
+        if xm is not None and xm.dtype != torch.bool:
+            raise Unsupported("bitwise not of a non-bool tensor")
+        ex.op('logical_not', {'X': X()}, {'Out': out})
+    elif t == 'masked_fill' and len(a) == 3 and scalar(a[2]):
+        c = ex.new_tmp()
+        xm = ex.meta.get(a[0].vid) if isinstance(a[0], Ref) else None
+        ex.op('fill_constant', {}, {'Out': c}, shape=[1], value=float(a[2]),
+              dtype=P.dtype_code(xm.dtype if xm is not None else torch.float32))
+        ex.op('where', {'Condition': ex.name_of(a[1]), 'X': c, 'Y': X()}, {'Out': out})
+    elif t == '__getitem__':
+        key = a[1] if isinstance(a[1], tuple) else (a[1],)
+        axes, starts, ends, dec = [], [], [], []
+        for ax, kk in enumerate(key):
+            if isinstance(kk, slice):
+                if kk.step not in (None, 1):
+                    raise Unsupported("strided slice")
+                if kk.start is None and kk.stop is None:
+                    continue
+                axes.append(ax)
+                starts.append(_lit_int(kk.start or 0))
+                ends.append(_lit_int(kk.stop) if kk.stop is not None else 2 ** 31 - 1)
+            elif isinstance(kk, int) and not isinstance(kk, bool) and kk >= 0:
+                axes.append(ax)
+                starts.append(kk)
+                ends.append(kk + 1)
+                dec.append(ax)
+            else:
+                raise Unsupported(f"index {kk!r}")
+        if not axes:
+            ex.op('assign', {'X': X()}, {'Out': out})
+        else:
+            ex.op('slice', {'Input': X()}, {'Out': out}, axes=axes, starts=starts, ends=ends, decrease_axis=dec,
+                  infer_flags=[1] * len(axes))
     elif t in ('clamp', 'clip'):
         lo = a[1] if len(a) > 1 else k.get('min')
         hi = a[2] if len(a) > 2 else k.get('max')

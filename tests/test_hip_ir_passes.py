@@ -94,3 +94,25 @@ def test_ernie_static_amp_bf16_training_fused():
     assert ca.n == 16 and cd.n == 32, (ca.n, cd.n)
     assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
     assert torch.cuda.is_available()
+
+
+def test_programdesc_predictor_bf16_fused_vs_unfused(tmp_path):
+    """An ERNIE ProgramDesc run by the bf16 Predictor with the IR passes (flash attention, fused
+    add + LayerNorm, GEMM + bias) vs the same model with switch_ir_optim(False)."""
+    from paddle import inference as I
+    from test_ir_passes import _ernie_inference_model
+    prefix, feed, _ = _ernie_inference_model(tmp_path)
+
+    def pred(ir):
+        c = I.Config(prefix + '.pdmodel', prefix + '.pdiparams')
+        c.enable_use_gpu(256, 0, I.PrecisionType.Bfloat16)
+        c.switch_ir_optim(ir)
+        return I.create_predictor(c)
+    x = paddle.to_tensor(feed, place=paddle.CUDAPlace(0))
+    ref = pred(False).run([x])[0].numpy()
+    p = pred(True)
+    with _Count(FA, 'flash_attention_ex') as ca, _Count(NORM, 'add_layer_norm') as cn:
+        out = p.run([x])[0].numpy()
+    assert IP.fusion_stats(p._program).get('multihead_matmul_fuse_pass_v2') == 2
+    assert ca.n == 2 and cn.n == 5, (ca.n, cn.n)
+    np.testing.assert_allclose(out, ref, rtol=5e-2, atol=5e-2)

@@ -119,3 +119,45 @@ def test_shared_mask_invert_not_claimed(fusion_mode):
     nodes, stats = IP.apply_passes(main)
     assert stats.get('multihead_matmul_fuse_pass_v2') == 2
     assert any(IP._kind(n) == 'invert' for n in nodes)
+
+
+def _ernie_inference_model(tmp_path, hidden=128, heads=2):
+    import os
+    paddle.seed(0)
+    paddle.enable_static()
+    try:
+        cfg = ernie_config('ernie-tiny', hidden_size=hidden, num_attention_heads=heads)
+        main, startup = static.Program(), static.Program()
+        with static.program_guard(main, startup):
+            ids = static.data('ids', [None, 32], 'int64')
+            model = ErnieForSequenceClassification(cfg, num_classes=2)
+            model.eval()
+            logits = model(ids)
+        exe = static.Executor(paddle.CPUPlace())
+        prefix = os.path.join(str(tmp_path), 'ernie')
+        static.save_inference_model(prefix, [ids], [logits], exe, program=main)
+        feed = _feed()['ids'][:3]
+        ref = exe.run(main, feed={'ids': feed}, fetch_list=[logits])[0]
+    finally:
+        paddle.disable_static()
+    return prefix, feed, ref
+
+
+def test_programdesc_ernie_predictor_fused(tmp_path, fusion_mode):
+    """ERNIE exported as a reference ProgramDesc (.pdmodel) and run by the inference Predictor: the
+    imported-operator passes (matmul_v2 / scale / where / softmax / matmul_v2 attention, add +
+    layer_norm, matmul_v2 + elementwise_add fc) rewrite it, and it computes the recorded program's
+    outputs exactly."""
+    from paddle import inference as I
+    prefix, feed, ref = _ernie_inference_model(tmp_path)
+    pred = I.create_predictor(I.Config(prefix + '.pdmodel', prefix + '.pdiparams'))
+    assert getattr(pred._program, '_pdmodel', False)  # really the ProgramDesc import
+    out = pred.run([paddle.to_tensor(feed)])[0].numpy()
+    assert IP.fusion_stats(pred._program) == {'multihead_matmul_fuse_pass_v2': 2, 'skip_layernorm_fuse_pass': 5,
+                                              'fc_fuse_pass': 10}
+    np.testing.assert_array_equal(out, ref)
+    cfg = I.Config(prefix + '.pdmodel', prefix + '.pdiparams')
+    cfg.switch_ir_optim(False)
+    pred2 = I.create_predictor(cfg)
+    np.testing.assert_array_equal(pred2.run([paddle.to_tensor(feed)])[0].numpy(), ref)
+    assert IP.fusion_stats(pred2._program) == {}
