@@ -55,3 +55,86 @@ def quant_rows(x, excl=None, rows=None):
 def quant_rows_ok(x):
     return (x.is_cuda and x.dim() == 2 and x.stride(1) == 1 and x.dtype in (torch.bfloat16, torch.float16, torch.float32)
             and x.shape[1] % 8 == 0 and x.stride(0) % 8 == 0 and x.data_ptr() % 32 == 0 and _lib() is not None)
+
+
+# ----------------------------------------------------------------------------- static int8 programs
+def quantize_static(x, scale, bits=8):
+    """int8 q = clamp(round(x / step)) with a per-tensor (activation) step = scale / qmax."""
+    qmax = float(2 ** (bits - 1) - 1)
+    s = scale.to(x.device) if isinstance(scale, torch.Tensor) else torch.tensor(float(scale), device=x.device)
+    step = s.float().reshape(()) / qmax
+    return torch.round(x.float() / step).clamp_(-qmax, qmax).to(torch.int8)
+
+
+def quant_linear(x, qw, w_scale, act_scale, bias=None, bits=8, weight_bits=8):
+    """A frozen quantised Linear (paddle.static.quantization): y = dequant(quant(x)) @ dequant(qw)^T
+    (+ bias) with x quantised per tensor by the calibrated ``act_scale`` (abs-max threshold) and the
+    int8 weight ``qw`` [N, K] (k-contiguous) by per-output-channel ``w_scale`` [N] thresholds.
+    On the GPU: the int8 MFMA GEMM (pa_gemm8_i8) with the two dequant steps in its epilogue."""
+    qmax_a = float(2 ** (bits - 1) - 1)
+    qmax_w = float(2 ** (weight_bits - 1) - 1)
+    K = x.shape[-1]
+    x2 = x.reshape(-1, K)
+    M, Nn = x2.shape[0], qw.shape[0]
+    ws = w_scale.to(device=x.device, dtype=torch.float32).reshape(-1) / qmax_w   # per-channel dequant step
+    a_step = (act_scale.to(device=x.device, dtype=torch.float32) if isinstance(act_scale, torch.Tensor) else
+              torch.tensor(float(act_scale), device=x.device)).reshape(()) / qmax_a
+    if (x2.is_cuda and bits == 8 and weight_bits == 8 and K % 128 == 0 and Nn % 8 == 0 and qw.dtype == torch.int8
+            and _lib() is not None):
+        M8 = -(-M // 8) * 8
+        qa = quantize_static(x2, act_scale, bits)
+        if M8 != M:
+            qa = torch.cat([qa, qa.new_zeros(M8 - M, K)])
+        if i8_mm_ok(qa, qw.contiguous()):
+            y = i8_mm(qa, qw.contiguous(), a_step.expand(M8).contiguous(), ws,
+                      bias=None if bias is None else bias.reshape(-1))
+            return y[:M].to(x.dtype if x.is_floating_point() else torch.bfloat16).reshape(*x.shape[:-1], Nn)
+    xq = quantize_static(x2, act_scale, bits).float() * a_step
+    y = xq @ (qw.to(x.device).float() * ws[:, None]).t()
+    if bias is not None:
+        y = y + bias.to(x.device).float()
+    return y.to(x.dtype).reshape(*x.shape[:-1], Nn)
+
+
+class _FakeQuant(torch.autograd.Function):
+    """quant -> dequant with a straight-through gradient (inside the clip range)."""
+
+    @staticmethod
+    def forward(ctx, x, step, qmax):
+        q = torch.round(x / step).clamp(-qmax, qmax)
+        ctx.save_for_backward(x, step)
+        ctx.qmax = qmax
+        return q * step
+
+    @staticmethod
+    def backward(ctx, g):
+        x, step = ctx.saved_tensors
+        keep = (x.abs() <= step * ctx.qmax).to(g.dtype)
+        return g * keep, None, None
+
+
+def fake_quant_dequant(x, scale, bits=8, axis=None):
+    """Quantise-dequantise x with abs-max threshold ``scale`` (per tensor, or per channel along
+    ``axis``), straight-through gradient.  The QAT node of QuantizationTransformPass."""
+    qmax = float(2 ** (bits - 1) - 1)
+    s = scale.to(x.dtype) if isinstance(scale, torch.Tensor) else torch.tensor(float(scale), dtype=x.dtype,
+                                                                              device=x.device)
+    if axis is not None and s.dim() == 1:
+        shape = [1] * x.dim()
+        shape[axis] = -1
+        s = s.reshape(shape)
+    step = torch.clamp(s / qmax, min=1e-12)
+    return _FakeQuant.apply(x, step, qmax)
+
+
+def moving_average_abs_max(x, state, accum, moving_rate, training):
+    """Activation fake quant of QAT (reference fake_quantize_dequantize_moving_average_abs_max):
+    in training the threshold is the moving average accum / state of the batch abs-max, updated in
+    place on the device; returns quant-dequant(x)."""
+    if training:
+        with torch.no_grad():
+            cur = x.detach().abs().amax().float()
+            state.mul_(moving_rate).add_(1.0)
+            accum.mul_(moving_rate).add_(cur)
+    scale = (accum / state.clamp(min=1e-12)).to(x.dtype)
+    return fake_quant_dequant(x, scale)

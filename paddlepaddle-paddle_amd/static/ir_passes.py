@@ -23,6 +23,8 @@ Passes (names follow the reference where one exists):
   layer_norm_fuse_pass            layer_norm                           ==> csrc/norm.hip
   fc_fuse_pass                    x @ W + b (-> relu / gelu)           ==> GEMM (+ bias + act kernel)
   softmax_fuse_pass               standalone last-dim softmax           ==> csrc/softmax_xent.hip
+  quant_linear_fuse_pass          quantize_linear -> dequantize_linear (activation) + dequantize_linear
+                                  (int8 weight) -> matmul_v2 (+ bias)  ==> the int8 MFMA GEMM
 
 The Executor and the inference Predictor run programs through ``ir_nodes(program, device)``: the
 rewritten node list is built once per program version and cached; ``program.nodes`` itself is never
@@ -36,7 +38,7 @@ import torch.nn.functional as TF
 
 from .program import Node, Ref, Const
 
-DEFAULT_PASSES = ('multihead_matmul_fuse_pass_v2', 'fused_dropout_add_layernorm', 'skip_layernorm_fuse_pass',
+DEFAULT_PASSES = ('quant_linear_fuse_pass', 'multihead_matmul_fuse_pass_v2', 'fused_dropout_add_layernorm', 'skip_layernorm_fuse_pass',
                   'layer_norm_fuse_pass', 'fc_fuse_pass', 'softmax_fuse_pass')
 
 # FLAGS_static_ir_fusion: 'auto' (default: GPU programs), '1' / 'always' (every device, used by the
@@ -806,7 +808,53 @@ def _softmax(g, i):
     return [i], {i: Node('torch', fused_softmax, [x], {}, _one_out(n), dict(n.meta or {}, fused='softmax_fuse_pass'))}
 
 
+def _quant_linear(g, i):
+    """An imported onnx-format int8 GEMM (the reference's quantised inference models and this
+    framework's saved PTQ / QAT models) as one paddle.ops.int8.quant_linear node."""
+    n = g.nodes[i]
+    if _kind(n) != 'pd.matmul_v2' or n.target.attrs.get('trans_x'):
+        return None
+    xd, wd = _pd_in(n, 'X'), _pd_in(n, 'Y')
+    if not isinstance(xd, Ref) or not isinstance(wd, Ref):
+        return None
+    dj, wj = g.producer(xd.vid, i), g.producer(wd.vid, i)
+    dn, wn = g.node(dj), g.node(wj)
+    if _kind(dn) != 'pd.dequantize_linear' or _kind(wn) != 'pd.dequantize_linear':
+        return None
+    qv = _pd_in(dn, 'X')
+    qj = g.producer(qv.vid, dj) if isinstance(qv, Ref) else None
+    qn = g.node(qj)
+    if _kind(qn) != 'pd.quantize_linear' or qn.target.attrs.get('quant_axis', -1) not in (-1, None) or \
+            dn.target.attrs.get('quant_axis', -1) not in (-1, None):
+        return None
+    x, acs = _pd_in(qn, 'X'), _pd_in(qn, 'Scale')
+    wq, ws = _pd_in(wn, 'X'), _pd_in(wn, 'Scale')
+    if not isinstance(x, Ref) or not isinstance(wq, Const) or not isinstance(ws, Const) or acs is None:
+        return None
+    trans = bool(n.target.attrs.get('trans_y'))
+    if wn.target.attrs.get('quant_axis', 0) != (0 if trans else 1):
+        return None
+    body, tail, bias = [qj, dj, wj, i], i, None
+    out_v = _outs_of(n.outs, [])
+    uj = list(g.uses.get(out_v[0], ()))
+    if len(uj) == 1 and out_v[0] not in g.external:
+        an = g.nodes[uj[0]]
+        if _kind(an) == 'pd.elementwise_add' and getattr(_pd_in(an, 'X'), 'vid', None) == out_v[0] and \
+                isinstance(_pd_in(an, 'Y'), Const):
+            bias, tail = _pd_in(an, 'Y'), uj[0]
+            body.append(uj[0])
+            out_v = _outs_of(an.outs, [])
+    if not trans or len(out_v) != 1 or not g.private(body[:-1] if tail != i else [qj, dj, wj], users=(i, tail)):
+        return None
+    from ..ops.int8 import quant_linear
+    node = Node('torch', quant_linear, [x, wq, ws, acs, bias], {'bits': qn.target.attrs.get('bit_length', 8),
+                                                                 'weight_bits': wn.target.attrs.get('bit_length', 8)},
+                out_v[0], dict(n.meta or {}, fused='quant_linear_fuse_pass'))
+    return body, {tail: node}
+
+
 _PASSES = {
+    'quant_linear_fuse_pass': _quant_linear,
     'multihead_matmul_fuse_pass_v2': _attention,
     'fused_dropout_add_layernorm': lambda g, i: _add_ln(g, i, True),
     'skip_layernorm_fuse_pass': lambda g, i: _add_ln(g, i, False),

@@ -252,6 +252,25 @@ def _lookup(ins, at):
     return {'Out': [out]}
 
 
+def _quant_linear_op(ins, at, quant):
+    """quantize_linear / dequantize_linear (reference onnx_format int8 models): abs-max ``Scale``
+    (per tensor, or per channel along quant_axis), symmetric (zero point 0).  quantize returns the
+    integer grid values (in X's float dtype), dequantize maps them back."""
+    x, sc = _one(ins, 'X'), _one(ins, 'Scale')
+    qmax = float(2 ** (at.get('bit_length', 8) - 1) - 1)
+    axis = at.get('quant_axis', -1)
+    s = sc.to(x.device).float()
+    if axis is not None and axis >= 0 and s.numel() > 1:
+        shape = [1] * x.dim()
+        shape[axis] = -1
+        s = s.reshape(shape)
+    step = s / qmax
+    if quant:
+        return torch.round(x.float() / step).clamp(-qmax, qmax).to(x.dtype if x.is_floating_point() else torch.float32)
+    out = x.float() * step
+    return out
+
+
 def _dropout(ins, at):
     x = _one(ins, 'X')
     p = at.get('dropout_prob', 0.5)
@@ -545,6 +564,8 @@ OPS = {
     'reduce_max': _reduce(lambda x, d, k: x.amax(d, keepdim=k)),
     'mean': lambda ins, at: {'Out': [_one(ins, 'X').mean()]},
     'lookup_table_v2': _lookup, 'dropout': _dropout,
+    'quantize_linear': lambda ins, at: {'Y': [_quant_linear_op(ins, at, True)]},
+    'dequantize_linear': lambda ins, at: {'Y': [_quant_linear_op(ins, at, False)]},
     'expand_as_v2': lambda ins, at: {'Out': [_one(ins, 'X').expand_as(_one(ins, 'Y')) if ins.get('Y') else
                                              _one(ins, 'X').expand(at['target_shape'])]},
     'assign': lambda ins, at: {'Out': [_one(ins, 'X')]},
@@ -758,8 +779,61 @@ def _pair(v):
                                                                               else [v, v])
 
 
+def _emit_opcall(ex, n):
+    """An imported operator node re-emitted as the operator it came from."""
+    t = n.target
+    o = ex.blk.ops.add()
+    o.type = t.type
+    pos = 0
+    for slot, cnt in t.slots:
+        v = o.inputs.add()
+        v.parameter = slot
+        v.arguments.extend([ex.name_of(a) for a in n.args[pos:pos + cnt]])
+        pos += cnt
+    outs = n.outs if isinstance(n.outs, (list, tuple)) else [n.outs]
+    pos = 0
+    for slot, cnt in t.out_slots:
+        v = o.outputs.add()
+        v.parameter = slot
+        v.arguments.extend([ex.name_of(Ref(vid)) if vid is not None else ex.new_tmp() for vid in outs[pos:pos + cnt]])
+        pos += cnt
+    for k, val in t.attrs.items():
+        if val is None:
+            continue
+        _set_attr(o, k, val)
+
+
+def _emit_quant_linear(ex, n):
+    """A frozen int8 GEMM (paddle.ops.int8.quant_linear) as the reference's onnx-format ops:
+    quantize_linear -> dequantize_linear on the activation (per-tensor threshold), the int8 weight
+    ([N, K] stored, dequantize_linear along quant_axis 0) consumed by matmul_v2(trans_y), + bias."""
+    x, qw, ws, acs = n.args[0], n.args[1], n.args[2], n.args[3]
+    bias = n.args[4] if len(n.args) > 4 else None
+    bits = n.kwargs.get('bits', 8)
+    wbits = n.kwargs.get('weight_bits', 8)
+    out = ex.name_of(Ref(n.outs))
+    zp_a, zp_w = ex.new_tmp(), ex.new_tmp()
+    ex.op('fill_constant', {}, {'Out': zp_a}, shape=[1], value=0.0, dtype=P.dtype_code(torch.float32))
+    ex.op('fill_constant', {}, {'Out': zp_w}, shape=[1], value=0.0, dtype=P.dtype_code(torch.float32))
+    xq, xd, wd = ex.new_tmp(), ex.new_tmp(), ex.new_tmp()
+    ex.op('quantize_linear', {'X': ex.name_of(x), 'Scale': ex.name_of(acs), 'ZeroPoint': zp_a}, {'Y': xq},
+          bit_length=bits, quant_axis=-1)
+    ex.op('dequantize_linear', {'X': xq, 'Scale': ex.name_of(acs), 'ZeroPoint': zp_a}, {'Y': xd},
+          bit_length=bits, quant_axis=-1)
+    ex.op('dequantize_linear', {'X': ex.name_of(qw), 'Scale': ex.name_of(ws), 'ZeroPoint': zp_w}, {'Y': wd},
+          bit_length=wbits, quant_axis=0)
+    dst = out if bias is None else ex.new_tmp()
+    ex.op('matmul_v2', {'X': xd, 'Y': wd}, {'Out': dst}, trans_x=False, trans_y=True)
+    if bias is not None:
+        ex.op('elementwise_add', {'X': dst, 'Y': ex.name_of(bias)}, {'Out': out}, axis=-1)
+
+
 def _emit(ex, n):
+    if type(n.target).__name__ == '_OpCall':
+        return _emit_opcall(ex, n)
     t = getattr(n.target, '__name__', str(n.target))
+    if t == 'quant_linear' and getattr(n.target, '__module__', '').endswith('ops.int8'):
+        return _emit_quant_linear(ex, n)
     a, k = list(n.args), dict(n.kwargs)
     out = ex.name_of(Ref(n.outs)) if isinstance(n.outs, int) else None
 
@@ -1034,7 +1108,7 @@ def export(prog, feed_names, fetch_vids):
     for n in prog.nodes:
         if n.kind != 'torch':
             raise Unsupported(f"node kind {n.kind}")
-        if not isinstance(n.outs, int):
+        if not isinstance(n.outs, int) and type(n.target).__name__ != '_OpCall':
             raise Unsupported("multi-output node")
         _emit(ex, n)
     for i, vid in enumerate(fetch_vids):

@@ -123,6 +123,7 @@ def test_shared_mask_invert_not_claimed(fusion_mode):
 
 def _ernie_inference_model(tmp_path, hidden=128, heads=2):
     import os
+    paddle.set_device('cpu')  # the model is built and exported on the CPU (GPU boxes included)
     paddle.seed(0)
     paddle.enable_static()
     try:
