@@ -44,25 +44,23 @@ class DygraphShardingOptimizer(ShardedOptimizer):
         super().__init__(optimizer, engine)
         self._dist_runs = {dt: self._runs(a, key=lambda p: 1.0 if getattr(p, 'is_distributed', False) else 0.0)
                            for dt, a in engine.arenas.items()}
+        dp = hcg.get_data_parallel_group()
+        if dp is not None and dp.nranks > 1:
+            engine.dp_pg = dp.pg  # overlapped gradient-shard all-reduce over the dp replicas
+            # pipeline-shared weights are summed over their stages after backward: their dp
+            # all-reduce waits for step() (two in-place collectives must not race on one shard)
+            engine.dp_defer = {u.index for u in engine.units if any(_shared_key(p) is not None for p in u.params)}
 
     # ---- gradient synchronisation across the data-parallel replicas of every sharding group
     def _dp_sync(self):
+        """Gradient shards averaged over the data-parallel replicas.  The all-reduce of each unit
+        was launched during backward the moment its shard was final (ShardingEngine._launch_dp:
+        chained behind the unit's reduce-scatter on the device, overlapping the remaining backward);
+        here the few not yet launched go out and every one is waited for."""
         dp = self._hcg.get_data_parallel_group()
         if dp is None or dp.nranks <= 1:
             return
-        # one async all-reduce per arena, all in flight together, then one wait each (RCCL
-        # pipelines them on its stream; the gradient shards are final only after the last
-        # micro-batch's reduce-scatter, so this runs once per step, after backward)
-        nccl = dist.get_backend(dp.pg) == 'nccl'
-        works = []
-        for a in self.engine.arenas.values():
-            g = a['grad']
-            works.append((g, dist.all_reduce(g, dist.ReduceOp.AVG if nccl else dist.ReduceOp.SUM, group=dp.pg,
-                                             async_op=True)))
-        for g, w in works:
-            w.wait()
-            if not nccl:
-                g.div_(dp.nranks)
+        self.engine.finish_dp_sync(dp.nranks)
 
     def _shared_units(self):
         for u in self.engine.units:

@@ -321,6 +321,11 @@ class PipelineParallel(Layer):
             self._post_grad(dev)
         return x, out
 
+    def _set_dp_final(self, optimizer, final):
+        eng = getattr(optimizer, 'engine', None)
+        if eng is not None and hasattr(eng, 'dp_final'):
+            eng.dp_final = bool(final)
+
     def _bwd_step(self, x, out):
         if self.is_last:
             _unwrap(out).backward()
@@ -349,15 +354,21 @@ class PipelineParallel(Layer):
             if self.is_last:
                 losses.append(_unwrap(out).detach())
             fi += 1
+        bi = 0
         for _ in range(n - warm):
             x, out = self._fwd_step(mbs_in[fi], mbs_lab[fi])
             pending.append((x, out))
             if self.is_last:
                 losses.append(_unwrap(out).detach())
             fi += 1
+            self._set_dp_final(optimizer, bi == n - 1)  # dp all-reduce overlap on the last micro-batch
             self._bwd_step(*pending.pop(0))
+            bi += 1
         while pending:
+            self._set_dp_final(optimizer, bi == n - 1)
             self._bwd_step(*pending.pop(0))
+            bi += 1
+        self._set_dp_final(optimizer, True)
         assert not (self._act_q or self._grad_q or self._acts_left or self._grads_left), "unmatched pipeline receives"
         self._drain_sends()
         if getattr(optimizer, '_syncs_dp', False):

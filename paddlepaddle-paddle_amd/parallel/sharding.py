@@ -206,6 +206,17 @@ class ShardingEngine:
         self._fwd_order = []
         self._recording = True
         self.grad_fresh = True
+        # data-parallel replicas of the sharding group (hybrid parallelism): the gradient shard of
+        # a unit is all-reduced over dp_pg as soon as it is final — on RCCL chained on the device
+        # behind the unit's reduce-scatter (a side stream waits for it, the all-reduce is issued
+        # from there), overlapping the rest of backward; dp_final is cleared by pipeline schedules
+        # for every micro-batch but the last
+        self.dp_pg = None
+        self.dp_final = True
+        self.dp_defer = set()  # units whose dp all-reduce waits for step() (pipeline-shared weights)
+        self._dp_works = []
+        self._dp_done = set()
+        self._dp_stream = None
 
     # ------------------------------------------------------------------ construction
     def _broadcast_params(self):
@@ -434,8 +445,49 @@ class ShardingEngine:
         src = u.fb.grad if u.fb.grad.dtype == out.dtype else u.fb.grad.to(out.dtype)  # fp32 main-grad reduce
         op = dist.ReduceOp.AVG if dist.get_backend(self.pg) == 'nccl' else dist.ReduceOp.SUM
         u.rs_work = dist.reduce_scatter_tensor(out, src, op, group=self.pg, async_op=True)
+        if self.dp_pg is not None and self.dp_final and self.grad_fresh and dist.get_backend(self.pg) == 'nccl':
+            self._launch_dp(u)  # out IS the shard: chain the dp all-reduce behind the reduce-scatter
         if self.level == 3:
             u.free_params()
+
+    def _launch_dp(self, u):
+        """Async all-reduce (average) of unit u's gradient shard over the data-parallel group."""
+        if self.dp_pg is None or u.index in self._dp_done:
+            return
+        if u.index in self.dp_defer and not getattr(self, '_dp_flush', False):
+            return
+        gs = self.gshard(u)
+        nccl = dist.get_backend(self.dp_pg) == 'nccl'
+        op = dist.ReduceOp.AVG if nccl else dist.ReduceOp.SUM
+        if nccl and gs.is_cuda and u.rs_work is not None:
+            if self._dp_stream is None:
+                self._dp_stream = torch.cuda.Stream(device=gs.device)
+            side = self._dp_stream
+            side.wait_stream(torch.cuda.current_stream(gs.device))
+            with torch.cuda.stream(side):
+                u.rs_work.wait()  # device-side: the side stream waits for the reduce-scatter
+                w = dist.all_reduce(gs, op, group=self.dp_pg, async_op=True)
+        else:
+            w = dist.all_reduce(gs, op, group=self.dp_pg, async_op=True)
+        self._dp_works.append((gs, w, nccl))
+        self._dp_done.add(u.index)
+
+    def finish_dp_sync(self, dp_nranks):
+        """Launch the dp all-reduce of every unit not yet launched, then wait for all of them."""
+        if self.dp_pg is None:
+            return
+        self._dp_flush = True
+        try:
+            for u in self.units:
+                self._launch_dp(u)
+        finally:
+            self._dp_flush = False
+        for gs, w, nccl in self._dp_works:
+            w.wait()
+            if not nccl:
+                gs.div_(dp_nranks)
+        self._dp_works = []
+        self._dp_done = set()
 
     def _accumulate_shard(self, u, src):
         dst = self.gshard(u)
@@ -465,6 +517,8 @@ class ShardingEngine:
                 u.fb.grad.zero_()
             u.free_grads()
             u.free_params()
+            if self.dp_pg is not None and self.dp_final:
+                self._launch_dp(u)  # shard final (accumulated / CPU path): its dp all-reduce goes now
         self.grad_fresh = False
         if self._recording and self._fwd_order:
             self._recording = False
@@ -475,6 +529,8 @@ class ShardingEngine:
         for a in self.arenas.values():
             a['grad'].zero_()
         self.grad_fresh = True
+        self._dp_works = []
+        self._dp_done = set()
 
     # ------------------------------------------------------------------ after the update
     def gather_params_after_step(self):

@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r5f
-timeout -k 10 300 python -u -m pytest -x -q -m gpu --timeout 200 --timeout-method thread tests/test_hip_ir_passes.py > gpurun_out/r5f/tests.log 2>&1 || { echo "tests failed"; tail -60 gpurun_out/r5f/tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q -m gpu --timeout 200 --timeout-method thread tests/test_hip_ir_passes.py tests/test_hip_quant.py > gpurun_out/r5f/tests.log 2>&1 || { echo "tests failed"; tail -60 gpurun_out/r5f/tests.log; exit 1; }
 tail -2 gpurun_out/r5f/tests.log
 timeout -k 10 300 python tools/ernie_predictor.py --no-ir > gpurun_out/r5f/pred_noir.log 2>&1 || { echo "pred noir failed"; tail -30 gpurun_out/r5f/pred_noir.log; exit 1; }
 grep ir= gpurun_out/r5f/pred_noir.log

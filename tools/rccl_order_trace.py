@@ -13,7 +13,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(steps=3):
+def run(steps=3, model_name='gpt-tiny', batch=4, seq=128):
     import socket
     import torch
     import torch.distributed as dist
@@ -28,7 +28,8 @@ def run(steps=3):
     import paddle
     from paddle.models.gpt import gpt_config, GPTForPretraining
     paddle.seed(0)
-    cfg = gpt_config('gpt-tiny', hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    cfg = gpt_config(model_name, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0,
+                     max_position_embeddings=max(seq, 1024))
     model = GPTForPretraining(cfg)
     opt = paddle.optimizer.AdamW(learning_rate=1e-3, parameters=model.parameters(), multi_precision=True,
                                  grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
@@ -36,7 +37,7 @@ def run(steps=3):
     model, opt, _ = paddle.distributed.sharding.group_sharded_parallel(model, opt, level='p_g_os')
     assert opt.engine.collectives
     inner = model._layers if hasattr(model, '_layers') else model
-    ids = paddle.to_tensor(torch.randint(0, cfg.vocab_size, (4, 129), device='cuda'))
+    ids = paddle.to_tensor(torch.randint(0, cfg.vocab_size, (batch, seq + 1), device='cuda'))
     x, y = ids[:, :-1], ids[:, 1:]
     for i in range(steps):
         torch.cuda.synchronize()
@@ -79,8 +80,45 @@ def report(path):
                   f'(+{gap:.1f} us after its end)')
 
 
+def overlap(path):
+    """Share of RCCL kernel time that runs while a compute kernel of another queue runs (last
+    step: after the last step-marker fill), from a rocprofv3 kernel trace."""
+    rows = list(csv.DictReader(open(path)))
+    key = 'Kernel_Name' if 'Kernel_Name' in rows[0] else 'Kernel-Name'
+    rows.sort(key=lambda r: int(r['Start_Timestamp']))
+    is_rccl = lambda n: 'nccl' in n.lower() or 'rccl' in n.lower()  # noqa: E731
+    marks = [i for i, r in enumerate(rows) if 'FillFunctor' in r[key] or 'fill' in r[key].lower()]
+    t0 = int(rows[marks[-1]]['Start_Timestamp']) if marks else 0
+    sel = [r for r in rows if int(r['Start_Timestamp']) >= t0]
+    comm = [(int(r['Start_Timestamp']), int(r['End_Timestamp'])) for r in sel if is_rccl(r[key])]
+    comp = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp'])) for r in sel if not is_rccl(r[key]))
+    merged = []
+    for a, b in comp:
+        if merged and a <= merged[-1][1]:
+            merged[-1][1] = max(merged[-1][1], b)
+        else:
+            merged.append([a, b])
+    tot = sum(b - a for a, b in comm)
+    ov = 0
+    for a, b in comm:
+        for c, d in merged:
+            if d <= a:
+                continue
+            if c >= b:
+                break
+            ov += min(b, d) - max(a, c)
+    span = (max(b for _, b in comm + comp) - min(a for a, _ in comm + comp)) / 1e6 if comm else 0
+    n_comm = len(comm)
+    print(f"last step: {n_comm} RCCL kernels, {tot / 1e6:.3f} ms RCCL kernel time, {ov / 1e6:.3f} ms of it "
+          f"({100.0 * ov / max(tot, 1):.1f} %) concurrent with compute kernels; step span {span:.2f} ms")
+
+
 if __name__ == '__main__':
     if len(sys.argv) > 2 and sys.argv[1] == '--report':
         report(sys.argv[2])
+    elif len(sys.argv) > 2 and sys.argv[1] == '--overlap':
+        overlap(sys.argv[2])
+    elif len(sys.argv) > 1 and sys.argv[1] == '--gpt13':
+        run(steps=3, model_name='gpt3-1.3b', batch=4, seq=1024)
     else:
         run()
