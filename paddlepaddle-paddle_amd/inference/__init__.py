@@ -248,9 +248,17 @@ class Predictor:
         self._program, self._feeds, self._fetch = load_inference_model(config._prefix, _Exe())
         if config._precision in (PrecisionType.Half, PrecisionType.Bfloat16):
             dt = torch.float16 if config._precision == PrecisionType.Half else torch.bfloat16
+            owners = getattr(self._program, '_const_owner', None) or {}
             for cid, t in list(self._program.consts.items()):
-                if t.is_floating_point():
-                    self._program.consts[cid] = t.to(dt)
+                o = owners.get(cid)  # a loaded parameter resolves through its owner (executor._resolve)
+                src = o._t if o is not None else t
+                if isinstance(src, torch.Tensor) and src.is_floating_point():
+                    self._program.consts[cid] = src.to(dt)
+                    if o is not None:
+                        o._t = self._program.consts[cid]
+            if getattr(self._program, '_pdmodel', False):
+                from ..static.pdmodel import set_float_dtype
+                set_float_dtype(self._program, dt)
         # IR fusion passes (static/ir_passes.py) on the loaded program: switch_ir_optim(False) turns
         # them off, pass_builder() edits the list
         self._program._ir_optim = bool(config._ir_optim)
@@ -282,8 +290,13 @@ class Predictor:
 
     def run(self, inputs=None):
         if inputs is not None:
+            from ..core.tensor import Tensor as PT
             for n, x in zip(self._feeds, inputs):
-                self.get_input_handle(n).copy_from_cpu(x.numpy() if hasattr(x, 'numpy') else x)
+                t = x._t if isinstance(x, PT) else x
+                if isinstance(t, torch.Tensor) and t.device == self._dev:
+                    self.get_input_handle(n).share_external_data(t)  # already resident: no round trip
+                else:
+                    self.get_input_handle(n).copy_from_cpu(x.numpy() if hasattr(x, 'numpy') else x)
         feeds = {n: self._inputs[n] for n in self._feeds}
         if self._config._hip_graph and self._dev.type == 'cuda':
             if self._graph is None:

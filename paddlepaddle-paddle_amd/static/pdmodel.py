@@ -576,6 +576,25 @@ OPS = {
 OPS.update(OPS_EXTRA)
 
 
+# operators whose outputs are made from attributes alone: built on the program's device
+_FACTORY_OPS = frozenset({'fill_constant', 'assign_value', 'gaussian_random', 'uniform_random'})
+
+
+# operators that (re)type values from attributes: under a 16-bit Predictor their fp32 outputs take
+# the model dtype (the role of the reference's convert_to_mixed_precision retyping,
+# paddle/fluid/inference/analysis/passes/convert_to_mixed_precision.cc)
+_RETYPE_OPS = _FACTORY_OPS | {'cast'}
+
+
+def set_float_dtype(prog, dtype):
+    """Make the attribute-typed float values of an imported program (fill_constant, assign_value,
+    cast to fp32, ...) ``dtype`` — the whole-program 16-bit mode of the Predictor."""
+    for n in prog.nodes:
+        if isinstance(n.target, _OpCall) and n.target.type in _RETYPE_OPS:
+            n.kwargs = dict(n.kwargs, float_dtype=dtype)
+    prog._version = getattr(prog, '_version', 0) + 1
+
+
 class _OpCall:
     """A node target: runs one reference operator on torch tensors (inputs by slot)."""
 
@@ -583,7 +602,22 @@ class _OpCall:
         self.type, self.slots, self.out_slots, self.attrs = typ, slots, out_slots, attrs
         self.__name__ = typ
 
-    def __call__(self, *args):
+    def __call__(self, *args, device=None, float_dtype=None):
+        if device is not None and not any(isinstance(a, torch.Tensor) for a in args):
+            # an attribute-only value (fill_constant / assign_value): made once per device and dtype,
+            # a constant of every later run (no operator of this runtime writes its inputs in place)
+            key = (str(device), float_dtype)
+            c = self.__dict__.setdefault('_const', {})
+            if key not in c:
+                c[key] = self._run(args, device, float_dtype)
+            return list(c[key])
+        return self._run(args, device, float_dtype)
+
+    def _run(self, args, device, float_dtype):
+        dev = next((a.device for a in args if isinstance(a, torch.Tensor) and a.device.type != 'cpu'), None)
+        if dev is not None:  # host-made values (shapes, constants of an older export) meet device ones
+            args = [a.to(dev, non_blocking=True) if isinstance(a, torch.Tensor) and a.device.type == 'cpu' else a
+                    for a in args]
         ins, i = {}, 0
         for slot, n in self.slots:
             ins[slot] = list(args[i:i + n])
@@ -593,6 +627,11 @@ class _OpCall:
         for slot, n in self.out_slots:
             vals = outs.get(slot, [])
             res.extend(vals[:n] + [None] * (n - len(vals)))
+        if device is not None:
+            res = [r.to(device) if isinstance(r, torch.Tensor) else r for r in res]
+        if float_dtype is not None:  # 16-bit inference: fp32 constants / casts follow the model dtype
+            res = [r.to(float_dtype) if isinstance(r, torch.Tensor) and r.dtype in (torch.float32, torch.float64)
+                   else r for r in res]
         return res
 
 
@@ -642,7 +681,11 @@ def load(data):
         args = [ref(a) for v in op.inputs for a in v.arguments]
         out_slots = [(v.parameter, len(v.arguments)) for v in op.outputs]
         outs = [ref(a).vid if isinstance(ref(a), Ref) else None for v in op.outputs for a in v.arguments]
-        prog.nodes.append(Node('torch', _OpCall(op.type, slots, out_slots, at), args, {}, outs))
+        if op.type in _FACTORY_OPS:  # created on the executor's device (static/executor.py 'factory')
+            prog.nodes.append(Node('torch', _OpCall(op.type, slots, out_slots, at), args, {'device': None}, outs,
+                                   {'factory': True}))
+        else:
+            prog.nodes.append(Node('torch', _OpCall(op.type, slots, out_slots, at), args, {}, outs))
     for _, name in sorted(feeds):
         v = vdesc[name]
         td = v.type.lod_tensor.tensor

@@ -5,6 +5,7 @@ three AdamW training steps with dropout; the rewrite counts pin what matched.  T
 (kernels inside the fused nodes vs the unfused program) is tests/test_hip_ir_passes.py."""
 import numpy as np
 import pytest
+import torch
 
 import paddle
 from paddle import static
@@ -162,3 +163,21 @@ def test_programdesc_ernie_predictor_fused(tmp_path, fusion_mode):
     pred2 = I.create_predictor(cfg)
     np.testing.assert_array_equal(pred2.run([paddle.to_tensor(feed)])[0].numpy(), ref)
     assert IP.fusion_stats(pred2._program) == {}
+
+
+def test_programdesc_bf16_predictor_casts_parameters(tmp_path):
+    """A bf16 Predictor over a ProgramDesc model runs its loaded parameters (resolved through their
+    owners) in bf16, so the fused entry points see 16-bit operands."""
+    from paddle import inference as I
+    prefix, feed, _ = _ernie_inference_model(tmp_path)
+    c = I.Config(prefix + '.pdmodel', prefix + '.pdiparams')
+    c.enable_use_gpu(256, 0, I.PrecisionType.Bfloat16)
+    p = I.create_predictor(c)
+    prog = p._program
+    owners = prog._const_owner
+    assert owners
+    for cid, o in owners.items():
+        if o._t.is_floating_point():
+            assert o._t.dtype == torch.bfloat16 and prog.consts[cid] is o._t
+    out = p.run([paddle.to_tensor(feed)])[0]
+    assert np.isfinite(out.numpy()).all()

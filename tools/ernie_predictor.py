@@ -68,8 +68,8 @@ def main():
     from paddle.static import ir_passes as IP
     print(f"ir={'off' if a.no_ir else 'on'} {ms:.3f} ms/run  passes {IP.fusion_stats(p._program)}", flush=True)
     if not a.no_ir and not a.no_ref:
-        ref = predictor(prefix, False).run([x])[0].numpy()
-        print(f"max |fused - unfused| logits {np.abs(out.numpy() - ref).max():.4g} (|logits| max "
+        ref = predictor(prefix, False).run([x])[0].astype('float32').numpy()
+        print(f"max |fused - unfused| logits {np.abs(out.astype('float32').numpy() - ref).max():.4g} (|logits| max "
               f"{np.abs(ref).max():.3g})", flush=True)
 
 
