@@ -216,6 +216,10 @@ def mm(a, b, out=None, bias=None, beta=0.0):
     """out = a @ b (+ beta*out) (+ bias) on the hand-written kernels when the operands fit their
     contract (M <= 64: the decode-shaped skinny GEMM; else the 8-phase MFMA GEMM), else on the
     library (torch).  a: [M,K], b: [K,N] (either may be a transposed view)."""
+    if a.is_cuda and b.dim() == 2 and b.shape[1] < 8 and out is None and beta == 0.0:
+        r = _tiny_n(a, b, bias)
+        if r is not None:
+            return r
     if a.is_cuda and _skinny_wins(a.shape[0], b.shape[1], a.shape[1]) and beta == 0.0 and skinny_ok(a, b) and (
             out is None or (
             out.dtype == torch.bfloat16 and out.stride(1) == 1 and out.stride(0) % 8 == 0)):
@@ -240,6 +244,26 @@ def mm(a, b, out=None, bias=None, beta=0.0):
     if bias is not None:
         out.add_(bias)
     return out
+
+
+def _tiny_n(a, b, bias):
+    """A GEMM with fewer than 8 output columns (a classifier head: [M, K] @ [K, 2]) as its transpose
+    y^T = b^T @ a^T on the decode-shaped skinny kernel: b^T's < 8 rows are its short side (padded to
+    8 with zero rows), the M activation rows its N.  None when the operands do not fit."""
+    M, K = a.shape
+    n = b.shape[1]
+    if not _skinny or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or M % 8 or M < 8 or a.stride(1) != 1:
+        return None
+    wt = torch.zeros(8, K, dtype=torch.bfloat16, device=a.device)
+    wt[:n].copy_(b.t())
+    at = a.t()  # [K, M]: a transposed view of the k-contiguous [M, K]
+    if not skinny_ok(wt, at):
+        return None
+    yt = skinny_mm(wt, at)  # [8, M]
+    y = yt[:n].t()
+    if bias is not None:
+        y = y + bias.to(y.dtype)
+    return y.contiguous()
 
 
 def wgrad_accumulate(x2, dy2, gw):

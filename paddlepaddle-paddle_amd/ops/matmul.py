@@ -80,6 +80,10 @@ def _mm2d(a, b, bias=None, alpha=1.0):
     if a.dtype == torch.bfloat16 and alpha == 1.0:
         if gemm._skinny_wins(a.shape[0], b.shape[1], a.shape[1]) and gemm.skinny_ok(a, b):
             return gemm.skinny_mm(a, b, bias=bias)
+        if b.shape[1] < 8 and a.is_cuda:  # classifier heads: the transposed problem on the skinny kernel
+            r = gemm._tiny_n(a, b, bias)
+            if r is not None:
+                return r
         if gemm.hip_mm_ok(a, b, 1) and (bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous())):
             return gemm.mm(a, b, bias=bias)
         return None

@@ -774,9 +774,19 @@ def _fc(g, i):
             body.append(uj[0])
             out_v = _outs_of(an.outs, [])
     act = None
+    view = None  # a reshape2 between the bias add and the activation (the 3-D Linear export)
     if len(out_v) == 1:
         uj = list(g.uses.get(out_v[0], ()))
-        if len(uj) == 1 and out_v[0] not in g.external:
+        if len(uj) == 1 and out_v[0] not in g.external and _kind(g.nodes[uj[0]]) == 'pd.reshape2':
+            rn = g.nodes[uj[0]]
+            r_out = rn.outs[0] if isinstance(rn.outs, list) and rn.outs else None
+            xs = rn.outs[1] if isinstance(rn.outs, list) and len(rn.outs) > 1 else None
+            uk = list(g.uses.get(r_out, ())) if r_out is not None else []
+            if (r_out is not None and r_out not in g.external and len(uk) == 1 and
+                    (xs is None or not g.uses.get(xs)) and _kind(g.nodes[uk[0]]) in ('pd.relu', 'pd.gelu')):
+                view = uj[0]
+                uj = uk
+        if len(uj) == 1 and (view is not None or out_v[0] not in g.external):
             cn = g.nodes[uj[0]]
             kc = _kind(cn)
             if kc == 'pd.relu':
@@ -784,11 +794,27 @@ def _fc(g, i):
             elif kc == 'pd.gelu':
                 act = 'gelu_tanh' if cn.target.attrs.get('approximate', False) else 'gelu'
             if act is not None:
+                if view is not None:
+                    body.append(view)
                 body.append(uj[0])
                 tail = uj[0]
-                out_v = _outs_of(cn.outs, [])
+                act_out = _outs_of(cn.outs, [])
+                if view is None:
+                    out_v = act_out
+            elif view is not None:
+                view = None
     if len(body) == 1 or len(out_v) != 1 or not g.private(body[:-1], users=body[-1:]):
         return None  # a bare matmul already runs on the hand-written GEMM
+    if view is not None:
+        # act(x @ W + b) on the 2-D product, then the reshape re-targeted to the activation's output
+        if len(act_out) != 1:
+            return None
+        rn = g.nodes[view]
+        lin = Node('torch', fused_linear, [x, w, bias], {'act': act, 'trans_w': trans}, out_v[0],
+                   dict(n.meta or {}, fused='fc_fuse_pass'))
+        rs = Node(rn.kind, rn.target, list(rn.args), dict(rn.kwargs),
+                  [act_out[0]] + [None] * (len(rn.outs) - 1), dict(rn.meta or {}))
+        return body, {body[1]: lin, tail: rs}
     node = Node('torch', fused_linear, [x, w, bias], {'act': act, 'trans_w': trans}, out_v[0],
                 dict(n.meta or {}, fused='fc_fuse_pass'))
     return body, {tail: node}

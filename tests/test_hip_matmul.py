@@ -330,3 +330,26 @@ def test_llm_int8_linear_gpu(M, dt):
     qw, ws = q._t.float(), s._t.float()
     ref = (qa @ qw.t()) * sx * ws[None, :] + (a * outl.float()) @ (qw * ws[:, None]).t() + b.float()
     _close(y, ref, 3e-2, f'llm.int8 M={M} {dt}')
+
+
+@pytest.mark.parametrize('M,K,n', [(32, 768, 2), (96, 1024, 3), (64, 256, 7)])
+def test_tiny_n_head_on_transposed_skinny(M, K, n):
+    """[M, K] @ [K, n < 8] (+ bias): the classifier-head GEMM runs as its transpose on the skinny
+    kernel (csrc/skinny_gemm.hip) instead of the library."""
+    g = torch.Generator(device=DEV).manual_seed(40 + n)
+    x, w, b = _rand(M, K, g=g), _rand(K, n, g=g), _rand(n, g=g)
+    calls = []
+    orig = gemm.skinny_mm
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+    gemm.skinny_mm = spy
+    try:
+        with torch.no_grad():
+            y = hm.linear(x, w, b)
+    finally:
+        gemm.skinny_mm = orig
+    assert calls, 'tiny-N GEMM did not reach the skinny kernel'
+    assert y.shape == (M, n)
+    _close(y, x.float() @ w.float() + b.float(), 2e-2, 'tiny-n')
