@@ -16,8 +16,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from ..core.tensor import Tensor, _wrap, _unwrap
-from ..nn.layer.layers import Layer
+from ...core.tensor import Tensor, _wrap, _unwrap
+from ...nn.layer.layers import Layer
 
 
 # ----------------------------------------------------------------- placements
@@ -215,7 +215,7 @@ def _attach(t, mesh, placements, global_shape):
     w.__dict__['is_dist'] = lambda: True
     # the torch storage carries the dist attr too: ops see it through the SPMD mode
     # (auto_parallel_spmd: per-op sharding propagation + differentiable reshards)
-    from . import auto_parallel_spmd as spmd
+    from .. import auto_parallel_spmd as spmd
     spmd.tag(w._t, mesh, placements, global_shape)
     if dist.is_initialized():
         spmd.enable()
@@ -228,7 +228,7 @@ def _dist_meta(t):
         return None
     if 'process_mesh' in t.__dict__:
         return t.__dict__['process_mesh'], t.__dict__['placements'], t.__dict__['_global_shape']
-    from . import auto_parallel_spmd as spmd
+    from .. import auto_parallel_spmd as spmd
     return spmd.meta(t._t)
 
 
@@ -258,7 +258,7 @@ _install_tensor_props()
 
 def shard_tensor(data, mesh, placements, dtype=None, place=None, stop_gradient=None):
     """``data`` is the global value (identical on every rank); returns this rank's local piece."""
-    from ..core.tensor import to_tensor
+    from ...core.tensor import to_tensor
     t = data if isinstance(data, Tensor) else to_tensor(data, dtype=dtype)
     _ensure_mesh_groups(mesh)
     g = _unwrap(t)
@@ -269,7 +269,7 @@ def shard_tensor(data, mesh, placements, dtype=None, place=None, stop_gradient=N
             local = torch.zeros_like(local)  # partial: value lives on coordinate 0 of that dim
     out = _wrap(local.detach().clone().requires_grad_(g.requires_grad))
     if isinstance(t, Tensor) and hasattr(t, 'trainable'):
-        from ..core.tensor import Parameter
+        from ...core.tensor import Parameter
         out = Parameter(out._t, trainable=not t.stop_gradient, name=t.name)
     if stop_gradient is not None:
         out.stop_gradient = stop_gradient
@@ -303,7 +303,7 @@ def reshard(dist_tensor, mesh, placements):
     gshape = list(m[2]) if m else list(t.shape)
     if src_mesh == mesh and t.requires_grad and torch.is_grad_enabled():
         # differentiable path: conjugate collectives in backward
-        from . import auto_parallel_spmd as spmd
+        from .. import auto_parallel_spmd as spmd
         _ensure_mesh_groups(mesh)
         return _attach(_wrap(spmd._reshard_local(t, mesh, src, list(placements))), mesh, placements, gshape)
     if src_mesh != mesh:
@@ -338,7 +338,7 @@ def reshard(dist_tensor, mesh, placements):
                 # Shard(i) -> Shard(j): all-to-all
                 ins = [c.contiguous() for c in cur.chunk(n, dst.dim)]
                 outs = [torch.empty_like(ins[0]) for _ in range(n)]
-                from .communication import all_to_all_tensors
+                from ..communication import all_to_all_tensors
                 all_to_all_tensors(outs, ins, grp)
                 cur = torch.cat(outs, s.dim)
             else:  # Shard -> Partial: keep on coordinate 0 after gathering
@@ -447,7 +447,7 @@ class _ShardOptimizer:
       behaviour.
     """
 
-    def __init__(self, optimizer, shard_fn=None, layer=None, gradient_accumulation_steps=1):
+    def __init__(self, optimizer, shard_fn=None, layer=None, gradient_accumulation_steps=1, engine_kwargs=None):
         self._inner_opt = optimizer
         self._shard_fn = shard_fn
         self._engine = None
@@ -460,14 +460,15 @@ class _ShardOptimizer:
         if shard_fn is not None:
             if not isinstance(shard_fn, _ShardingStageBase):
                 raise TypeError("shard_fn must be a ShardingStage1/2/3 instance")
-            from ..parallel.sharding import ShardingEngine, ShardedOptimizer
+            from ...parallel.sharding import ShardingEngine, ShardedOptimizer
             params = [p for p in optimizer._parameter_list if not p.stop_gradient]
             grp = shard_fn._group(params)
             level = shard_fn.level
             if level == 'p_g_os' and layer is None:
                 level = 'os_g'
+            kw = dict(engine_kwargs or {})
             if level == 'p_g_os':
-                self._engine = ShardingEngine(layer, level, group=grp)
+                self._engine = ShardingEngine(layer, level, group=grp, **kw)
             else:
                 self._engine = ShardingEngine(None, level, group=grp, params=params)
             self._sharded = ShardedOptimizer(optimizer, self._engine)
@@ -622,7 +623,10 @@ class DistModel:
             inner = optimizer._inner_opt if isinstance(optimizer, _ShardOptimizer) else optimizer
             stage = {1: ShardingStage1, 2: ShardingStage2, 3: ShardingStage3}[int(st.sharding.get('stage', 1))]()
             acc = optimizer._acc_k if isinstance(optimizer, _ShardOptimizer) else 1
-            optimizer = _ShardOptimizer(inner, stage, layer=layer, gradient_accumulation_steps=acc)
+            kw = {}
+            if st.sharding.get('segment_size') is not None:  # stage 3: units below this stay materialised
+                kw['segment_size'] = int(st.sharding.get('segment_size'))
+            optimizer = _ShardOptimizer(inner, stage, layer=layer, gradient_accumulation_steps=acc, engine_kwargs=kw)
         self._opt = optimizer
         # pipeline: one call = one mini-batch of ``accumulate_steps`` micro-batches (or
         # batch / micro_batch_size of them), run in the configured schedule's order and followed by
@@ -637,13 +641,17 @@ class DistModel:
         self._avg = bool(gm.get('avg', True))
         self._micro = 0
         if st.recompute.get('enable'):
-            from .fleet.recompute import recompute
+            from ..fleet.recompute import recompute
 
             def wrap(f):
                 return lambda *a, **k: recompute(f, *a, **k) if layer.training else f(*a, **k)
             for _, sub in list(layer.named_children()):
                 sub.forward = wrap(sub.forward)
         self._mode = 'train' if optimizer is not None and loss is not None else 'predict'
+        # pipeline stages from the process meshes the parameters were placed on (shard_layer /
+        # shard_tensor with Replicate placements, one mesh per stage, in forward order)
+        self._pp_plan = self._pipeline_plan(layer) if self._pp else None
+        self._pp_stale = False
         # static form: the step is recorded once per (mode, input signature) into a static
         # Program and replayed by the Executor (reference: to_static builds the distributed
         # program); the eager step remains for what the program form does not cover
@@ -657,15 +665,85 @@ class DistModel:
         import os
         if os.environ.get('PADDLE_AMD_DIST_TO_STATIC', '1') == '0':
             return 'disabled by PADDLE_AMD_DIST_TO_STATIC=0'
+        sharded = isinstance(optimizer, _ShardOptimizer) and optimizer._sharded is not None
         if st.pipeline.get('enable'):
-            return 'pipeline schedules run eagerly'
-        if st.sharding.get('enable') or isinstance(optimizer, _ShardOptimizer):
-            return 'sharded optimizer states run eagerly'
+            if DistModel._pipeline_plan(layer) is None:
+                return 'pipeline stages need the parameters placed on one process mesh per stage'
+            if sharded:
+                return 'sharding inside pipeline stages runs eagerly'
+        if sharded and st.amp.get('enable'):
+            return 'AMP over a sharded optimizer runs eagerly'
         if st.recompute.get('enable'):
             return 'recompute runs eagerly'
-        if any(is_dist_tensor(p) for p in layer.parameters()):
-            return 'parameters with dist attributes run on the SPMD-propagated eager path'
+        for p in layer.parameters():
+            m = _dist_meta(p)
+            if m is not None and any(not isinstance(x, Replicate) for x in m[1]):
+                return 'tensor-parallel placements run on the SPMD-propagated eager path'
+            if m is not None and not st.pipeline.get('enable'):
+                return 'parameters with dist attributes run on the SPMD-propagated eager path'
         return None
+
+    @staticmethod
+    def _pipeline_plan(layer):
+        """{'meshes': stage meshes, 'layer_stage': {id(sublayer): stage}} from the parameters'
+        process meshes (Replicate placements only), or None when fewer than two stages are marked
+        or the stage meshes differ in size."""
+        meshes, layer_stage = [], {}
+        for sub in layer.sublayers(include_self=True):
+            own = [q for q in sub._parameters.values() if q is not None]
+            for q in own:
+                m = _dist_meta(q)
+                if m is None:
+                    continue
+                if any(not isinstance(x, Replicate) for x in m[1]):
+                    return None
+                if m[0] not in meshes:
+                    meshes.append(m[0])
+                layer_stage[id(sub)] = meshes.index(m[0])
+                break
+        if len(meshes) < 2 or len({len(m.process_ids) for m in meshes}) != 1:
+            return None
+        return {'meshes': meshes, 'layer_stage': layer_stage}
+
+    def _pipeline_config(self):
+        """static/pipeline.PipelineConfig of this rank (stage = the mesh holding it; the j-th
+        rank of every stage mesh forms one pipe; the ranks of a stage mesh are its data-parallel
+        replicas) and the data-parallel group of the stage."""
+        import types
+        from ...static.pipeline import PipelineConfig
+        meshes = self._pp_plan['meshes']
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        stage = next(k for k, m in enumerate(meshes) if rank in m)
+        j = meshes[stage].process_ids.index(rank)
+        pipe = [m.process_ids[j] for m in meshes]
+        for m in meshes:  # every rank creates the same groups in the same order (new_group is collective)
+            _subgroup(m.process_ids)
+        for jj in range(len(meshes[0].process_ids)):
+            _subgroup([m.process_ids[jj] for m in meshes])
+        grp = types.SimpleNamespace(ranks=pipe, pg=_subgroup(pipe))
+        S = len(meshes)
+        cfg = PipelineConfig(stage, S, self._pp_acc, grp, pipe[stage - 1] if stage > 0 else None,
+                             pipe[stage + 1] if stage < S - 1 else None, self._pp_mode)
+        dpr = meshes[stage].process_ids
+        dp = types.SimpleNamespace(pg=_subgroup(dpr), nranks=len(dpr), ranks=dpr) if len(dpr) > 1 else None
+        return cfg, dp
+
+    def _sync_stage_params(self):
+        """Every stage's parameters from the first rank of its mesh to all ranks (each rank updates
+        only its own stage's copy in training; a whole-model eval / predict needs all of them)."""
+        if not self._pp_stale or not dist.is_initialized():
+            return
+        import torch as _t
+        meshes, ls = self._pp_plan['meshes'], self._pp_plan['layer_stage']
+        with _t.no_grad():
+            for sub in self._layer.sublayers(include_self=True):
+                if id(sub) not in ls:
+                    continue
+                src = meshes[ls[id(sub)]].process_ids[0]
+                for q in sub._parameters.values():
+                    if q is not None:
+                        dist.broadcast(_unwrap(q), src)
+        self._pp_stale = False
 
     @property
     def is_static(self):
@@ -691,14 +769,27 @@ class DistModel:
 
     def _build_static(self, mode, args):
         import torch as _t
-        from .. import static as _st
-        from ..static.program import _static_minimize
-        from ..static.minimize import step_policy
-        from .. import framework as _fw
+        from ... import static as _st
+        from ...static.program import _static_minimize
+        from ...static.minimize import step_policy
+        from ... import framework as _fw
+        from ...static import program as _prog
         vals = [_unwrap(a) if isinstance(a, Tensor) else _t.as_tensor(a) for a in args]
         was_dynamic = _fw.in_dynamic_mode()
         if was_dynamic:
             _fw.enable_static()
+        pp = self._pp_plan if (mode == 'train' and self._pp_plan is not None) else None
+        hooks = []
+        if pp is not None:  # ops recorded inside a stage's sublayers run on that stage
+            for sub in self._layer.sublayers(include_self=True):
+                k = pp['layer_stage'].get(id(sub))
+                if k is not None:
+                    hooks.append(sub.register_forward_pre_hook(
+                        lambda lyr, inp, _k=k: _prog._STAGE.__setitem__(0, _k)))
+        prev_stage = _prog._STAGE[0]
+        eng = self._opt._engine if isinstance(self._opt, _ShardOptimizer) else None
+        if eng is not None:
+            eng.hooks_off = True  # stage 3: recording gathers nothing; the replay is gathered up front
         try:
             main, startup = _st.Program(), _st.Program()
             with _st.program_guard(main, startup):
@@ -709,7 +800,7 @@ class DistModel:
                 amp = self._strategy.amp
                 import contextlib
                 if amp.get('enable') and mode != 'train':
-                    from ..amp import auto_cast
+                    from ...amp import auto_cast
                     ctx = auto_cast(True, level=amp.get('level', 'O2'), dtype=amp.get('dtype', 'bfloat16'))
                 else:
                     ctx = contextlib.nullcontext()
@@ -719,11 +810,15 @@ class DistModel:
                 else:
                     with ctx:
                         out = self._layer(*feeds[:-1])
+                        if pp is not None:
+                            _prog._STAGE[0] = len(pp['meshes']) - 1  # the loss: last stage
                         fetch = self._loss(out, feeds[-1])
                     if mode == 'train':
                         opt = self._opt
+                        if isinstance(opt, _ShardOptimizer):
+                            opt = opt._sharded if opt._sharded is not None else opt._inner_opt
                         if amp.get('enable'):
-                            from ..static import amp as samp
+                            from ...static import amp as samp
                             dtype = amp.get('dtype', 'bfloat16')
                             lists = samp.AutoMixedPrecisionLists(custom_white_list=amp.get('custom_white_list'),
                                                                  custom_black_list=amp.get('custom_black_list'),
@@ -733,9 +828,19 @@ class DistModel:
                         else:
                             _static_minimize(opt, fetch)
                         pol = step_policy(main)
-                        pol.k_steps, pol.avg = self._k, self._avg
-                        pol.dp_group = self._dp_of(args)
+                        acc = self._opt._acc_k if isinstance(self._opt, _ShardOptimizer) else 1
+                        pol.k_steps, pol.avg = self._k * acc, (self._avg if acc == 1 or self._k > 1 else False)
+                        # a sharded optimizer averages its gradients in its reduce-scatter
+                        sharded = isinstance(self._opt, _ShardOptimizer) and self._opt._sharded is not None
+                        pol.dp_group = None if sharded else self._dp_of(args)
+                        if pp is not None:
+                            pol.pipeline, pol.dp_group = self._pipeline_config()
         finally:
+            _prog._STAGE[0] = prev_stage
+            for h in hooks:
+                h.remove()
+            if eng is not None:
+                eng.hooks_off = False
             if was_dynamic:
                 _fw.disable_static()
         if self._exe is None:
@@ -752,8 +857,24 @@ class DistModel:
             plan = self._progs[key] = self._build_static(self._mode, args)
         prog, names, fetch, dp = plan
         feed = {n: (_unwrap(a).detach() if isinstance(a, Tensor) else a) for n, a in zip(names, args)}
+        eng = self._opt._engine if isinstance(self._opt, _ShardOptimizer) else None
+        if eng is not None and eng.level == 3:
+            # stage 3 in the program form: every unit is gathered for the step (its gradient
+            # reduce-scattered as it completes in backward) and released again after it
+            for u in eng.units:
+                u.wait_gather()
+                if self._mode == 'train':
+                    u.alloc_grads()
+        if self._pp_plan is not None:
+            if self._mode == 'train':
+                self._pp_stale = True
+            else:
+                self._sync_stage_params()
         res = self._exe.run(prog, feed=feed, fetch_list=[fetch], return_numpy=False)[0]
-        if self._mode != 'predict' and dp is not None:
+        if eng is not None and eng.level == 3 and self._mode != 'train':
+            for u in eng.units:
+                u.free_params()
+        if self._mode != 'predict' and dp is not None and self._pp_plan is None:
             # the loss of the global batch: the mean of the data-parallel ranks' local losses
             r = _unwrap(res).detach().float().clone()
             dist.all_reduce(r, group=dp.pg)
@@ -782,7 +903,7 @@ class DistModel:
         inputs, labels = args[:-1], args[-1]
         amp = self._strategy.amp
         if amp.get('enable'):
-            from ..amp import auto_cast
+            from ...amp import auto_cast
             ctx = auto_cast(True, custom_white_list=amp.get('custom_white_list'),
                             custom_black_list=amp.get('custom_black_list'), level=amp.get('level', 'O2'),
                             dtype=amp.get('dtype', 'bfloat16'))
@@ -842,10 +963,18 @@ class DistModel:
         if self._micro % self._k == 0:
             self._opt.step()
             self._opt.clear_grad()
-        from ..tensor.manipulation import stack
+        from ...tensor.manipulation import stack
         return stack(losses).mean()
 
+    def _materialize(self):
+        """Stage 3: gather every released unit (the parameters a state dict reads)."""
+        eng = self._opt._engine if isinstance(self._opt, _ShardOptimizer) else None
+        if eng is not None and eng.level == 3:
+            for u in eng.units:
+                u.wait_gather()
+
     def state_dict(self, mode='all'):
+        self._materialize()
         sd = dict(self._layer.state_dict())
         if mode in ('all', 'opt') and self._opt is not None:
             sd.update(self._opt.state_dict())
@@ -862,181 +991,9 @@ def to_static(layer, loader=None, loss=None, optimizer=None, strategy=None, inpu
 _ = (copy, Layer)
 
 
-# ----------------------------------------------------------------- high-level Engine
-class Engine:
-    """Auto-parallel high-level API (reference: distributed/auto_parallel/static/engine.py:68,
-    ``from paddle.distributed.fleet import auto; auto.Engine``): ``fit`` / ``evaluate`` /
-    ``predict`` / ``save`` / ``load`` over a DistModel (strategy: sharding, gradient merge,
-    pipeline micro-batching, AMP, recompute).  The reference compiles a distributed static
-    program; here the step runs eagerly on the SPMD-propagated dist tensors, so the placements
-    given with shard_tensor / shard_layer drive the collectives.  Data: each rank reads its
-    data-parallel share of every batch (DistributedBatchSampler over the world) unless the
-    dataset is already split."""
-
-    def __init__(self, model=None, loss=None, optimizer=None, metrics=None, cluster=None, strategy=None):
-        self._model = model
-        self._loss = loss
-        self._optimizer = optimizer
-        self._metrics = [] if metrics is None else (list(metrics) if isinstance(metrics, (list, tuple)) else [metrics])
-        self._strategy = strategy if strategy is not None else Strategy()
-        self._dm = None
-        self._mode = 'train'
-        self.history = None
-
-    # -- plumbing
-    def _dist_model(self):
-        if self._dm is None:
-            self._dm = DistModel(self._model, None, self._loss, self._optimizer, self._strategy)
-        return self._dm
-
-    def _loader(self, data, batch_size, collate_fn, shuffle=False):
-        from ..io import DataLoader, Dataset, DistributedBatchSampler
-        if data is None:
-            return None
-        if not isinstance(data, Dataset):
-            return data  # an iterable of ready batches
-        if batch_size is None:
-            return data
-        if dist.is_initialized() and dist.get_world_size() > 1:
-            bs = DistributedBatchSampler(data, batch_size=batch_size, shuffle=shuffle, drop_last=True)
-            return DataLoader(data, batch_sampler=bs, collate_fn=collate_fn)
-        return DataLoader(data, batch_size=batch_size, shuffle=shuffle, collate_fn=collate_fn, drop_last=False)
-
-    @staticmethod
-    def _split(batch, split):
-        items = list(batch) if isinstance(batch, (list, tuple)) else [batch]
-        k = split if split is not None else (len(items) - 1 if len(items) > 1 else len(items))
-        return items[:k], items[k:]
-
-    def _update_metrics(self, out, labels):
-        res = {}
-        for m in self._metrics:
-            r = m.compute(out, *labels) if hasattr(m, 'compute') else out
-            m.update(*(r if isinstance(r, (list, tuple)) else [r]))
-            acc = m.accumulate()
-            names = m.name() if callable(getattr(m, 'name', None)) else [type(m).__name__]
-            names = names if isinstance(names, (list, tuple)) else [names]
-            vals = acc if isinstance(acc, (list, tuple)) else [acc]
-            res.update(dict(zip(names, vals)))
-        return res
-
-    # -- public API
-    def prepare(self, inputs_spec=None, labels_spec=None, inputs=None, labels=None, main_program=None,
-                startup_program=None, mode='train', init_parameters=True):
-        self._mode = mode
-        self._dist_model()
-
-    def to_mode(self, mode):
-        assert mode in ('train', 'eval', 'predict'), mode
-        self._mode = mode
-
-    def fit(self, train_data, train_sample_split=None, batch_size=1, epochs=1, steps_per_epoch=None, log_freq=10,
-            save_dir=None, save_freq=1, valid_data=None, valid_sample_split=None, valid_freq=1, valid_steps=None,
-            collate_fn=None, callbacks=None, verbose=2, nvprof_range=(-1, -1)):
-        dm = self._dist_model()
-        loader = self._loader(train_data, batch_size, collate_fn, shuffle=False)
-        history = {'loss': []}
-        for epoch in range(epochs):
-            dm.train()
-            for m in self._metrics:
-                m.reset()
-            for step, batch in enumerate(loader):
-                if steps_per_epoch is not None and step >= steps_per_epoch:
-                    break
-                ins, labels = self._split(batch, train_sample_split)
-                loss = dm(*ins, *labels)
-                history['loss'].append(float(loss))
-                if verbose and log_freq and step % log_freq == 0 and (not dist.is_initialized() or dist.get_rank() == 0):
-                    print(f"[Engine] epoch {epoch} step {step} loss {history['loss'][-1]:.6f}", flush=True)
-            if save_dir is not None and save_freq and (epoch + 1) % save_freq == 0:
-                import os
-                self.save(os.path.join(save_dir, f'epoch{epoch}'), training=True)
-            if valid_data is not None and valid_freq and (epoch + 1) % valid_freq == 0:
-                res = self.evaluate(valid_data, valid_sample_split, batch_size, valid_steps, log_freq, collate_fn,
-                                    verbose=0)
-                for k, v in res.items():
-                    history.setdefault('eval_' + k, []).append(v)
-        self.history = history
-        return history
-
-    def evaluate(self, valid_data, valid_sample_split=None, batch_size=1, steps=None, log_freq=10, collate_fn=None,
-                 callbacks=None, verbose=2):
-        import torch as _t
-        loader = self._loader(valid_data, batch_size, collate_fn)
-        self._model.eval()
-        for m in self._metrics:
-            m.reset()
-        losses, res = [], {}
-        with _t.no_grad():
-            for step, batch in enumerate(loader):
-                if steps is not None and step >= steps:
-                    break
-                ins, labels = self._split(batch, valid_sample_split)
-                out = self._model(*ins)
-                if self._loss is not None and labels:
-                    losses.append(float(self._loss(out, *labels)))
-                if self._metrics and labels:
-                    res = self._update_metrics(out, labels)
-        self._model.train()
-        out = {'loss': sum(losses) / len(losses)} if losses else {}
-        out.update(res)
-        return out
-
-    def predict(self, test_data, test_sample_split=None, batch_size=1, steps=None, collate_fn=None, callbacks=None,
-                verbose=2):
-        import torch as _t
-        loader = self._loader(test_data, batch_size, collate_fn)
-        self._model.eval()
-        outs = []
-        with _t.no_grad():
-            for step, batch in enumerate(loader):
-                if steps is not None and step >= steps:
-                    break
-                items = list(batch) if isinstance(batch, (list, tuple)) else [batch]
-                k = test_sample_split if test_sample_split is not None else len(items)
-                outs.append(self._model(*items[:k]))
-        self._model.train()
-        return outs
-
-    def run(self, data=None, feed=None, fetch_list=None, mode=None):
-        """One step on an already-collated batch ``data`` (inputs..., labels...)."""
-        mode = mode or self._mode
-        ins, labels = self._split(data, None)
-        if mode == 'train':
-            return {'loss': float(self._dist_model()(*ins, *labels))}
-        import torch as _t
-        with _t.no_grad():
-            return {'outputs': self._model(*ins)}
-
-    def dataloader(self, dataset, batch_size=1, shuffle=False, drop_last=False, collate_fn=None, num_workers=0,
-                   use_buffer_reader=True, use_shared_memory=True, timeout=0, worker_init_fn=None, epochs=1,
-                   steps_per_epoch=None, sample_split=1, mode=None):
-        return self._loader(dataset, batch_size, collate_fn, shuffle=shuffle)
-
-    def save(self, path, training=True):
-        from ..framework.io import save
-        save(self._model.state_dict(), path + '.pdparams')
-        if training and self._optimizer is not None:
-            save(self._optimizer.state_dict(), path + '.pdopt')
-
-    def load(self, path, strict=True, load_optimizer=True):
-        import os
-        from ..framework.io import load
-        self._model.set_state_dict(load(path + '.pdparams'))
-        if load_optimizer and self._optimizer is not None and os.path.exists(path + '.pdopt'):
-            self._optimizer.set_state_dict(load(path + '.pdopt'))
-
-    def cost(self, inputs_spec=None, labels_spec=None, mode=None):
-        return None  # the reference's static cost model; eager steps are timed with paddle.profiler
-
-    @property
-    def main_program(self):
-        return None
-
-    @property
-    def startup_program(self):
-        return None
-
-    @property
-    def optimizer(self):
-        return self._optimizer
+# the high-level Engine lives in auto_parallel/static/engine.py (reference layout)
+def __getattr__(name):
+    if name == 'Engine':
+        from .static.engine import Engine
+        return Engine
+    raise AttributeError(name)

@@ -202,6 +202,7 @@ class ShardingEngine:
             for u in self.units:
                 u.free_params()
                 u.free_grads()
+        self.hooks_off = False
         self._armed = False
         self._fwd_order = []
         self._recording = True
@@ -371,6 +372,8 @@ class ShardingEngine:
         self.model.register_forward_pre_hook(self._root_pre)
 
     def _root_pre(self, layer, inputs):
+        if self.hooks_off:
+            return None
         for u in self.units:
             if u.persistent or u.layer is None:
                 u.wait_gather()
@@ -380,6 +383,8 @@ class ShardingEngine:
 
     def _fwd_pre(self, u):
         def hook(layer, inputs):
+            if self.hooks_off:
+                return None
             if self._recording and torch.is_grad_enabled():
                 self._fwd_order.append(u)
             u.wait_gather()
@@ -394,6 +399,8 @@ class ShardingEngine:
 
     def _fwd_post(self, u):
         def hook(layer, inputs, outputs):
+            if self.hooks_off:  # static recording (dist.to_static): the replay gathers up front
+                return outputs
             if torch.is_grad_enabled():
                 outs = outputs if isinstance(outputs, tuple) else (outputs,)
                 idx = [i for i, o in enumerate(outs) if isinstance(o, Tensor) and o._t.requires_grad]

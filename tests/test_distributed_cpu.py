@@ -322,3 +322,11 @@ def test_dist_to_static_program_data_parallel(k):
     give the single-process full-batch result (gradient merge k = 2 too)."""
     out = run_workers('worker_dist_static.py', str(k))
     assert out.count(f'dist static k{k} OK') == 2, out[-3000:]
+
+
+@pytest.mark.parametrize("mode", ['shard1', 'shard2', 'shard3', 'pp_1F1B', 'pp_FThenB', 'engine'])
+def test_dist_to_static_sharded_and_pipelined_programs(mode):
+    """dist.to_static / auto.Engine with sharding stage 1/2/3 or a 2-stage pipeline run as static
+    Programs and equal single-process training (tests/dist/worker_dist_static_sp.py)."""
+    out = run_workers('worker_dist_static_sp.py', mode)
+    assert out.count(f'dist static {mode} OK') == 2, out[-3000:]
