@@ -35,6 +35,7 @@ _SIGS = {
     'pa_rt_trace_count': ([], _LL),
     'pa_rt_trace_collect': ([_LLP, _LL], _LL),
     'pa_rt_trace_clear': ([], None),
+    'pa_rt_adamw': ([_P, _P, _I, _P, _P, _P, _I, _LL] + [ctypes.c_float] * 8, _I),
 }
 
 

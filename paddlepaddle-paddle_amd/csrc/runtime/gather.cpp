@@ -7,6 +7,7 @@
 // `prefetch_factor` batches per worker) and paddle/fluid/operators/reader/
 // blocking_queue.h + buffered_reader.cc (double-buffered host->device staging).
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -200,4 +201,105 @@ PA_RT int pa_rt_queue_size(void* h) {
   auto* q = static_cast<Queue*>(h);
   std::lock_guard<std::mutex> g(q->mu);
   return static_cast<int>(q->q.size());
+}
+
+// ---------------------------------------------------------------------------------------------
+// Offloaded optimizer update (group-sharded training with offload=True; reference
+// python/paddle/distributed/fleet/meta_parallel/sharding/group_sharded_stage3.py:98-127 and the
+// CPU adam kernel it runs): the fp32 master / moments of this rank's shard live in host memory,
+// the reduce-scattered gradient shard arrives by an async D2H copy into a pinned buffer, and the
+// update runs here on the worker pool (one contiguous slice per thread, vectorised loop), writing
+// the new master in place and the 16-bit parameter image (bf16 / fp16, round to nearest even)
+// for the H2D copy back.  gdt / odt: 0 fp32, 1 bf16, 2 fp16 (grad / low-precision out, odt -1 = none).
+namespace {
+inline float bf16_to_f(uint16_t h) {
+  uint32_t u = static_cast<uint32_t>(h) << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+inline uint16_t f_to_bf16(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return static_cast<uint16_t>((u >> 16) | 0x40);  // NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+inline float f16_to_f(uint16_t h) {
+  const uint32_t s = (h & 0x8000u) << 16, e = (h >> 10) & 0x1f, m = h & 0x3ff;
+  uint32_t u;
+  if (e == 0) {
+    if (m == 0) {
+      u = s;
+    } else {  // subnormal
+      int ee = -1;
+      uint32_t mm = m;
+      do {
+        ++ee;
+        mm <<= 1;
+      } while (!(mm & 0x400));
+      u = s | ((127 - 15 - ee) << 23) | ((mm & 0x3ff) << 13);
+    }
+  } else if (e == 31) {
+    u = s | 0x7f800000u | (m << 13);
+  } else {
+    u = s | ((e + 127 - 15) << 23) | (m << 13);
+  }
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+inline uint16_t f_to_f16(float f) {  // round to nearest even, overflow to inf, NaN kept
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  const uint32_t s = (u >> 16) & 0x8000u;
+  const uint32_t a = u & 0x7fffffffu;
+  if (a >= 0x7f800000u) return static_cast<uint16_t>(s | 0x7c00u | (a > 0x7f800000u ? 0x200u : 0u));
+  if (a >= 0x477ff000u) return static_cast<uint16_t>(s | 0x7c00u);  // rounds past 65504
+  if (a < 0x38800000u) {  // subnormal half (or zero)
+    if (a < 0x33000000u) return static_cast<uint16_t>(s);
+    const uint32_t e = a >> 23, mant = (a & 0x7fffffu) | 0x800000u;
+    const uint32_t sh = 126 - e;  // 14 - (e - 127) + 13 - 1 ... shift to the 10-bit field
+    uint32_t r = mant >> (sh);
+    const uint32_t rem = mant & ((1u << sh) - 1), half = 1u << (sh - 1);
+    if (rem > half || (rem == half && (r & 1u))) ++r;
+    return static_cast<uint16_t>(s | r);
+  }
+  uint32_t r = a - 0x38000000u;  // rebias exponent 127 -> 15
+  r += 0xfffu + ((r >> 13) & 1u);
+  return static_cast<uint16_t>(s | (r >> 13));
+}
+}  // namespace
+
+PA_RT int pa_rt_adamw(float* master, const void* grad, int gdt, float* m, float* v, void* out, int odt, int64_t n,
+                      float lr, float b1, float b2, float eps, float wd, float b1p, float b2p, float grad_scale) {
+  if (n <= 0) return 0;
+  if (gdt < 0 || gdt > 2 || odt < -1 || odt > 2) return 1;
+  const float bc2 = std::sqrt(1.f - b2p);
+  const float step = lr * bc2 / (1.f - b1p);
+  const float epsc = eps * bc2;
+  const float decay = 1.f - lr * wd;
+  const int64_t chunk = 1 << 16;
+  const int parts = static_cast<int>((n + chunk - 1) / chunk);
+  pool().parallel_for(parts, [&](int part) {
+    const int64_t lo = part * chunk, hi = std::min(n, lo + chunk);
+    for (int64_t i = lo; i < hi; ++i) {
+      float g;
+      if (gdt == 0) g = static_cast<const float*>(grad)[i];
+      else if (gdt == 1) g = bf16_to_f(static_cast<const uint16_t*>(grad)[i]);
+      else g = f16_to_f(static_cast<const uint16_t*>(grad)[i]);
+      g *= grad_scale;
+      float p = master[i] * decay;
+      const float mi = m[i] * b1 + (1.f - b1) * g;
+      const float vi = v[i] * b2 + (1.f - b2) * g * g;
+      p -= step * mi / (std::sqrt(vi) + epsc);
+      m[i] = mi;
+      v[i] = vi;
+      master[i] = p;
+      if (odt == 1) static_cast<uint16_t*>(out)[i] = f_to_bf16(p);
+      else if (odt == 2) static_cast<uint16_t*>(out)[i] = f_to_f16(p);
+      else if (odt == 0) static_cast<float*>(out)[i] = p;
+    }
+  });
+  return 0;
 }

@@ -9,15 +9,12 @@ inner optimizer is used as is."""
 class GroupShardedOptimizerStage2:
     def __init__(self, params, optim, group=None, offload=False, device="gpu", pretrain_sync_models=True,
                  dp_group=None, **kw):
-        if offload:
-            raise NotImplementedError("GroupShardedOptimizerStage2(offload=True): the MI355X build keeps the "
-                                      "optimizer state in HBM (288 GB per GPU)")
         self._optim = optim
         self._params = list(params) if params is not None else list(optim._parameter_list)
         self._group = group
         self._dp_group = dp_group
         self._sharded = None  # parallel.sharding.ShardedOptimizer, set by GroupShardedStage2
-        self.offload = False
+        self.offload = bool(offload)  # read by GroupShardedStage2 when it builds the engine
 
     def _bind(self, sharded):
         self._sharded = sharded

@@ -13,7 +13,8 @@ class GroupShardedStage2(Layer):
         opts = sharding_optimizer if isinstance(sharding_optimizer, list) else [sharding_optimizer]
         self._sharding_optimizers = opts
         engine = ShardingEngine(layer, 'os_g', group=group,
-                                bucket_mb=max(1, int(buffer_max_size * 2 // 2 ** 20)) if buffer_max_size else 256)
+                                bucket_mb=max(1, int(buffer_max_size * 2 // 2 ** 20)) if buffer_max_size else 256,
+                                offload=any(getattr(o, 'offload', False) for o in opts))
         self.__dict__['_engine'] = engine
         for o in opts:
             inner = o._optim if hasattr(o, '_bind') else o

@@ -11,11 +11,10 @@ class GroupShardedStage3(Layer):
     def __init__(self, layer, optimizer, group=None, sync_buffers=False, device="gpu", segment_size=2 ** 20,
                  pretrain_sync_models=True, offload=False, sync_comm=False, dp_group=None, exclude_layer=None):
         super().__init__()
-        if offload:
-            raise NotImplementedError("GroupShardedStage3(offload=True): the MI355X build keeps parameters and "
-                                      "optimizer state in HBM (288 GB per GPU)")
         self._layer = layer
-        engine = ShardingEngine(layer, 'p_g_os', group=group, segment_size=segment_size)
+        # offload: the shard's fp32 master + Adam moments in pinned host memory, updated by the host
+        # runtime (parallel/sharding.py ShardingEngine offload)
+        engine = ShardingEngine(layer, 'p_g_os', group=group, segment_size=segment_size, offload=offload)
         self.__dict__['_engine'] = engine
         inner = optimizer._optim if hasattr(optimizer, '_bind') else optimizer
         sharded = ShardedOptimizer(inner, engine)

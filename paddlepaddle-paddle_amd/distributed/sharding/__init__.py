@@ -14,10 +14,12 @@ def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, off
     MI355X extensions: ``reduce_dtype='float32'`` reduce-scatters gradients in fp32 (main-grad
     precision at 8 ranks); ``alias=False`` runs the multi-rank path at world size 1;
     ``reshard_after_forward`` (stage 3): see parallel.sharding.ShardingEngine (None: keep the
-    gathered parameters from forward to backward when the model is small against the HBM)."""
+    gathered parameters from forward to backward when the model is small against the HBM).
+    ``offload=True``: optimizer state of the shard in pinned host memory, updated by the host
+    runtime (ShardingEngine offload)."""
     assert level in ('os', 'os_g', 'p_g_os'), f"unknown sharding level {level}"
     engine = ShardingEngine(model, level, group=group, segment_size=segment_size, reduce_dtype=reduce_dtype,
-                            alias=alias, reshard_after_forward=reshard_after_forward)
+                            alias=alias, reshard_after_forward=reshard_after_forward, offload=offload)
     wrapped = GroupShardedModel(model, engine)
     opt = ShardedOptimizer(optimizer, engine)
     return wrapped, opt, scaler

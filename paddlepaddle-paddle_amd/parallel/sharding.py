@@ -131,7 +131,7 @@ class _PreBackward(torch.autograd.Function):
 class ShardingEngine:
     def __init__(self, model, level='p_g_os', group=None, bucket_mb=256, segment_size=2 ** 20,
                  release_grads=True, persistent_types=None, persistent_below=None, params=None, alias=None,
-                 reduce_dtype=None, isolate=None, reshard_after_forward=None):
+                 reduce_dtype=None, isolate=None, reshard_after_forward=None, offload=False):
         """model: the Layer to shard; or model=None with ``params`` (a parameter list) for stage 1/2
         (the hybrid-parallel sharding optimizer, which only sees its optimizer's parameters).
 
@@ -148,7 +148,11 @@ class ShardingEngine:
         reduce-scatter (False: one all-gather per unit and step instead of two, the parameters of
         the whole model materialised at the forward/backward turn).  None: False on a GPU when the
         model's parameters take at most 1/16 of the device memory (288 GB HBM: e.g. GPT-3 1.3B's
-        2.6 GB), else True; always True on the CPU."""
+        2.6 GB), else True; always True on the CPU.
+        offload: the fp32 master weights and Adam moments of this rank's shard live in pinned host
+        memory (12 bytes per shard element off the device); the step copies the gradient shard
+        down, updates on the host runtime's worker pool (csrc/runtime pa_rt_adamw) and copies the
+        16-bit parameter shard back (reference group_sharded_stage3.py:98-127 offload)."""
         self.model = model
         self.level = LEVELS[level] if isinstance(level, str) else int(level)
         if model is None and (params is None or self.level == 3):
@@ -178,6 +182,7 @@ class ShardingEngine:
         if rd not in (None, 'float32', 'bfloat16', 'float16'):
             raise ValueError(f"reduce_dtype must be float32 / bfloat16 / float16, got {reduce_dtype}")
         self.reduce_fp32 = rd == 'float32' and not self.alias
+        self.offload = bool(offload)
         self._gather_works = []
         from ..nn.layer.common import Embedding
         self.persistent_types = tuple(persistent_types or (Embedding,))
@@ -325,9 +330,18 @@ class ShardingEngine:
                                     a['grad'][u.arena_off:u.arena_off + u.L])
                 else:
                     a['param'][u.arena_off:u.arena_off + u.L].copy_(u.shard(u.fb.data))
-            a['master'] = a['param'].float().clone() if dt != torch.float32 else a['param']
-            a['m'] = torch.zeros(n, dtype=torch.float32, device=dev)
-            a['v'] = torch.zeros(n, dtype=torch.float32, device=dev)
+            if self.offload:  # optimizer state in (pinned) host memory, staging buffers for the step
+                pin = dev.type == 'cuda'
+                a['master'] = torch.empty(n, dtype=torch.float32, pin_memory=pin)
+                a['master'].copy_(a['param'].float())
+                a['m'] = torch.zeros(n, dtype=torch.float32, pin_memory=pin)
+                a['v'] = torch.zeros(n, dtype=torch.float32, pin_memory=pin)
+                a['grad_host'] = torch.empty(n, dtype=a['grad'].dtype, pin_memory=pin)
+                a['param_host'] = torch.empty(n, dtype=dt, pin_memory=pin)
+            else:
+                a['master'] = a['param'].float().clone() if dt != torch.float32 else a['param']
+                a['m'] = torch.zeros(n, dtype=torch.float32, device=dev)
+                a['v'] = torch.zeros(n, dtype=torch.float32, device=dev)
             a['b1p'] = None
 
     def _auto_reshard(self, model, params):
@@ -685,19 +699,22 @@ class ShardedOptimizer:
         return torch.clamp(clip.clip_norm / torch.clamp(norm, min=clip.clip_norm), max=1.0)
 
     @torch.no_grad()
-    def _step_sgd_momentum(self, lr, scale):
+    def _step_sgd_momentum(self, lr, scale, offload=False):
         opt = self._inner
         mom = self._kind == 'Momentum'
         mu = float(getattr(opt, '_momentum', 0.0))
         nesterov = bool(getattr(opt, '_use_nesterov', False))
         rescale = float(getattr(opt, '_rescale', 1.0))
         for dt, a in self.engine.arenas.items():
-            lowp = a['param'] if dt != torch.float32 else None
+            if offload:  # host master / velocity, the gradient shard already copied down
+                lowp, grad = a['param_host'], a['grad_host']
+            else:
+                lowp, grad = (a['param'] if dt != torch.float32 else None), a['grad']
             for lo, hi, coeff in self._coeff_runs[dt]:
                 if hi <= lo:
                     continue
                 master = a['master'][lo:hi]
-                g = a['grad'][lo:hi].float()
+                g = grad[lo:hi].float()
                 if scale is not None:
                     g = g * scale
                 if mom and rescale != 1.0:
@@ -714,8 +731,52 @@ class ShardedOptimizer:
                 if lowp is not None:
                     lowp[lo:hi].copy_(master.to(dt))
 
+    _DTC = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+    @torch.no_grad()
+    def _step_offload(self):
+        """The update with the optimizer state in host memory: per arena one async D2H of the
+        gradient shard, the native host AdamW (or the SGD / Momentum rule) over the worker pool,
+        one H2D of the updated parameter shard."""
+        from .. import _runtime as R
+        opt = self._inner
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("sharding offload cannot run inside a captured step graph")
+        self._step += 1
+        lr = float(opt.get_lr())
+        scale = self._clip_scale()
+        gs = 1.0 if scale is None else float(scale)
+        for a in self.engine.arenas.values():
+            a['grad_host'].copy_(a['grad'], non_blocking=True)
+        if any(a['grad'].is_cuda for a in self.engine.arenas.values()):
+            torch.cuda.current_stream().synchronize()
+        if self._kind in ('SGD', 'Momentum'):
+            self._step_sgd_momentum(lr, None if scale is None else gs, offload=True)
+        else:
+            b1, b2, eps = opt._beta1, opt._beta2, opt._epsilon
+            b1p, b2p = b1 ** self._step, b2 ** self._step
+            L = R.lib()
+            for dt, a in self.engine.arenas.items():
+                gh, ph = a['grad_host'], a['param_host']
+                for lo, hi, coeff in self._coeff_runs[dt]:
+                    if hi <= lo:
+                        continue
+                    es = a['master'].element_size()
+                    rc = L.pa_rt_adamw(a['master'].data_ptr() + lo * es, gh.data_ptr() + lo * gh.element_size(),
+                                       self._DTC[gh.dtype], a['m'].data_ptr() + lo * es, a['v'].data_ptr() + lo * es,
+                                       ph.data_ptr() + lo * ph.element_size(), self._DTC[ph.dtype], hi - lo, lr,
+                                       b1, b2, eps, float(coeff), b1p, b2p, gs)
+                    if rc:
+                        raise RuntimeError(f"pa_rt_adamw failed ({rc})")
+        for a in self.engine.arenas.values():
+            a['param'].copy_(a['param_host'], non_blocking=True)
+        self.engine.gather_params_after_step()
+        opt._global_step += 1
+
     @torch.no_grad()
     def step(self):
+        if self.engine.offload:
+            return self._step_offload()
         opt = self._inner
         self._step += 1
         lr = opt.get_lr()
@@ -810,7 +871,7 @@ class ShardedOptimizer:
                 v = sd.get(f'shard_{nm}_{key}')
                 if v is not None:
                     buf.copy_(_unwrap(v).to(buf.device))
-            if dt != torch.float32:
+            if dt != torch.float32 or self.engine.offload:
                 a['param'].copy_(a['master'].to(dt))
         self._step = int(sd.get('@step@', self._step))
         pows = getattr(self, '_pows', None)

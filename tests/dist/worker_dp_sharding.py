@@ -90,6 +90,12 @@ def main():
         model, opt, _ = dist.sharding.group_sharded_parallel(model, opt, level='p_g_os', segment_size=64,
                                                              reshard_after_forward=False)
         assert not model._engine.reshard_after_forward
+    elif mode.endswith('_offload'):  # optimizer state in host memory, host-runtime update
+        level = mode[:-len('_offload')]
+        model, opt, _ = dist.sharding.group_sharded_parallel(model, opt, level=level, segment_size=64, offload=True)
+        eng = model._engine
+        assert eng.offload and all(not a['m'].is_cuda and not a['master'].is_cuda for a in eng.arenas.values())
+        mode = level
     else:
         model, opt, _ = dist.sharding.group_sharded_parallel(model, opt, level=mode, segment_size=64)
         if mode == 'p_g_os':
@@ -107,7 +113,7 @@ def main():
     for k in want:
         err = np.abs(got[k] - want[k]).max()
         assert err < 2e-5, (mode, kind, k, err)
-    print(f"rank{rank} {mode} OK", flush=True)
+    print(f"rank{rank} {sys.argv[1]} OK", flush=True)
 
 
 if __name__ == '__main__':

@@ -28,7 +28,7 @@ def run_workers(script, *args, nproc=2, timeout=300):
     return r.stdout
 
 
-@pytest.mark.parametrize("mode", ['dp', 'os', 'os_g', 'p_g_os', 'p_g_os_keep'])
+@pytest.mark.parametrize("mode", ['dp', 'os', 'os_g', 'p_g_os', 'p_g_os_keep', 'os_g_offload', 'p_g_os_offload'])
 def test_dp_and_sharding_match_single_process(mode):
     out = run_workers('worker_dp_sharding.py', mode)
     assert out.count(f'{mode} OK') == 2
@@ -40,7 +40,7 @@ def test_tensor_parallel_with_data_parallel_syncs_gradients():
 
 
 @pytest.mark.parametrize("kind", ['momentum', 'sgd'])
-@pytest.mark.parametrize("mode", ['os', 'p_g_os'])
+@pytest.mark.parametrize("mode", ['os', 'p_g_os', 'p_g_os_offload'])
 def test_sharded_momentum_sgd_match_single_process(mode, kind):
     out = run_workers('worker_dp_sharding.py', mode, kind)
     assert out.count(f'{mode} OK') == 2, out[-3000:]
