@@ -31,7 +31,13 @@ def _index(item):
 
 
 def _getitem(self, item):
-    return _wrap(self._t[_index(item)])
+    out = _wrap(self._t[_index(item)])
+    sv = self.__dict__.get('_static_value')
+    if sv is not None and isinstance(item, int):
+        # a static-mode shape tensor (paddle.shape): its elements keep their record-time extents
+        # (a dynamic dim's sentinel) for the shape inference of consumers such as reshape
+        out.__dict__['_static_value'] = sv[item]
+    return out
 
 
 def _setitem(self, item, value):

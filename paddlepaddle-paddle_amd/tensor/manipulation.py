@@ -24,8 +24,49 @@ def _paddle_shape(t, shape):
     return shape
 
 
+def _is_var(v):
+    return isinstance(v, Tensor) and v._t.is_meta
+
+
+def _runtime_reshape(x, *dims):
+    shp = []
+    for d in dims:
+        if isinstance(d, Tensor):
+            shp.extend(int(v) for v in d._t.reshape(-1).tolist())
+        else:
+            shp.append(int(d))
+    return _w(x._t.reshape(_paddle_shape(x._t, shp)))
+
+
+def _static_reshape(x, shape):
+    """reshape whose target shape holds static-mode tensors (paddle.shape results, their elements,
+    a shape Variable): a recorded node that reads the extents at run time (the reference's
+    ShapeTensor / ShapeTensorList inputs of reshape2).  The recorded output extents: each tensor
+    element's record-time value (a dynamic dim's sentinel) when known, else -1."""
+    from ..static.program import py_node
+    t = _u(x)
+    items = list(shape) if isinstance(shape, (list, tuple)) else [shape]
+    rec = []
+    for d in items:
+        if isinstance(d, Tensor):
+            sv = d.__dict__.get('_static_value')
+            if sv is None:
+                if d._t.dim() == 0 or d._t.numel() == 1:
+                    rec.append(-1)
+                else:
+                    raise ValueError("reshape: a shape tensor needs its record-time extents (paddle.shape)")
+            else:
+                rec.extend(sv if isinstance(sv, (list, tuple)) else [sv])
+        else:
+            rec.append(int(d))
+    meta = torch.empty(t.reshape(_paddle_shape(t, rec)).shape, dtype=t.dtype, device='meta')
+    return py_node(_runtime_reshape, [x, *items], [meta])[0]
+
+
 def reshape(x, shape, name=None):
     t = _u(x)
+    if t.is_meta and (_is_var(shape) or (isinstance(shape, (list, tuple)) and any(_is_var(d) for d in shape))):
+        return _static_reshape(x, shape)
     return _w(t.reshape(_paddle_shape(t, shape)))
 
 
@@ -539,8 +580,20 @@ def tensordot(x, y, axes=2, name=None):
     return _w(torch.tensordot(_u(x), _u(y), dims=axes))
 
 
+def _runtime_shape(x):
+    return _w(torch.tensor(list(x._t.shape), dtype=torch.int32))
+
+
 def shape(input):  # noqa: A002
-    return _w(torch.tensor(list(_u(input).shape), dtype=torch.int32))
+    t = _u(input)
+    if t.is_meta:
+        # static mode: a recorded node producing the run-time extents (dynamic dims included), its
+        # record-time value kept for the shape inference of consumers
+        from ..static.program import py_node
+        out = py_node(_runtime_shape, [input], [torch.empty(t.dim(), dtype=torch.int32, device='meta')])[0]
+        out.__dict__['_static_value'] = list(t.shape)
+        return out
+    return _w(torch.tensor(list(t.shape), dtype=torch.int32))
 
 
 def resize_(x, shape, fill_zero=False):
