@@ -49,6 +49,22 @@ PA_API int pa_flash_set_fwd_pipe(int v) {
   return old;
 }
 
+// software-pipelined forward (fwd_sp_kernel): -2 = not read yet (env PA_FA_FWD_SP), else 0/1
+static int g_fwd_sp = -2;
+static bool fwd_sp() {
+  if (g_fwd_sp == -2) {
+    const char* e = getenv("PA_FA_FWD_SP");
+    g_fwd_sp = e ? atoi(e) : 0;
+  }
+  return g_fwd_sp > 0;
+}
+PA_API int pa_flash_set_fwd_sp(int v) {
+  fwd_sp();
+  const int old = g_fwd_sp;
+  g_fwd_sp = v;
+  return old;
+}
+
 // strides: [b, s, h] element strides for each tensor (head_dim stride must be 1)
 PA_API hipError_t pa_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int Sq, int Sk,
                                int Hq, int Hk, int D, const long long* qst, const long long* kst, const long long* vst,
@@ -57,7 +73,12 @@ PA_API hipError_t pa_flash_fwd(const void* q, const void* k, const void* v, void
   Strides qs{qst[0], qst[1], qst[2]}, ks{kst[0], kst[1], kst[2]}, vs{vst[0], vst[1], vst[2]}, os{ost[0], ost[1], ost[2]};
   if (wide_d(D)) return wide_fwd(q, k, v, o, lse, B, Sq, Sk, Hq, Hk, D, qs, ks, vs, os, scale, causal, dt, nullptr, st);
   dim3 grid(Hq, B, (Sq + 127) / 128);
-  if (fwd_pipe()) {
+  if (fwd_sp() && D == 64) {
+    FA_DISPATCH(dt, D, causal, if constexpr (DD == 64) {
+      fwd_sp_kernel<T, DD, CC><<<grid, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                                                     (uint16_t*)o, lse, Sq, Sk, Hq, Hk, qs, ks, vs, os, scale * kLog2e);
+    });
+  } else if (fwd_pipe()) {
     FA_DISPATCH(dt, D, causal,
                 fwd_kernel<T, DD, CC, 0, true><<<grid, 256, 0, st>>>(
                     (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, Sq, Sk, Hq, Hk, qs,
@@ -209,6 +230,14 @@ PA_API hipError_t pa_flash_fwd_ex(const void* q, const void* k, const void* v, v
   dim3 grid(Hq, B, (Sq + 127) / 128);
   const int feat = 1 | (mask ? 2 : 0) | (p_drop > 0.f ? 4 : 0) | (rows ? 8 : 0);
 #define FA_FWD_EX(F)                                                                                            \
+  if constexpr (DD == 64) {                                                                                     \
+    if (fwd_sp()) {                                                                                             \
+      fwd_sp_kernel<T, DD, CC, F><<<grid, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k,                 \
+                                                        (const uint16_t*)v, (uint16_t*)o, lse, Sq, Sk, Hq, Hk,  \
+                                                        qs, ks, vs, os, scale * kLog2e, ex);                    \
+      break;                                                                                                    \
+    }                                                                                                           \
+  }                                                                                                             \
   if (fwd_pipe())                                                                                               \
     fwd_kernel<T, DD, CC, F, true><<<grid, 256, 0, st>>>((const uint16_t*)q, (const uint16_t*)k,                \
                                                          (const uint16_t*)v, (uint16_t*)o, lse, Sq, Sk, Hq, Hk, \

@@ -591,6 +591,337 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void fwd_kernel(const uint16_
   }
 }
 
+// One 16-B-per-lane LDS-DMA (global_load_lds_dwordx4): global saddr base + per-lane 32-bit byte
+// offset -> LDS (M0 base + 16 * lane).  Inline asm so the compiler neither counts it nor drains it
+// at every LDS read; retired by an explicit vmcnt before the barrier that publishes the tile.
+__device__ __forceinline__ void fa_glds(const void* base, unsigned off, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(off), "s"(base), "s"(lds_dst)
+      : "memory");
+}
+
+// LDS-DMA fill of a [64][D] tile in the swizzled image of lds_off<D, TR>: each wave-instruction
+// writes 1 KiB lane-linearly (4 rows of 256 B at D = 128, 8 rows of 128 B at D = 64), so the
+// swizzle is folded into each lane's SOURCE chunk.  Rows past `rows` (the ragged end) re-read the
+// last valid row: finite values whose scores are masked.  4 waves x NI instructions per tile.
+template <int D, bool TR>
+struct DmaTile {
+  static constexpr int RB = fa_pitch<D>() * 2;      // row bytes
+  static constexpr int RPI = 1024 / RB;             // rows per wave-instruction
+  static constexpr int NI = 64 / RPI / 4;           // instructions per wave per tile
+  static_assert(D == 64 || D == 128, "LDS-DMA tiles: head_dim 64 / 128");
+  unsigned row_l[NI], ch_l[NI];
+  __device__ __forceinline__ void init(int wave, int lane) {
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int r = (wave * NI + u) * RPI + lane / (RB / 16);
+      const int pc = lane % (RB / 16);
+      row_l[u] = r;
+      ch_l[u] = pc ^ (TR ? swz_tr<D>(r) : swz_b128<D>(r));
+    }
+  }
+  // rows [row0, row0 + 64) of the tensor at base (element row stride rs); valid rows < rows
+  __device__ __forceinline__ void issue(const uint16_t* base, long long rs, int row0, int rows, char* lds,
+                                        int wave) const {
+    const uint16_t* tb = base + (long long)row0 * rs;
+    const unsigned dst = (unsigned)(size_t)(__attribute__((address_space(3))) char*)lds;
+    const int last = rows - 1 - row0;
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int r = min((int)row_l[u], last);
+      fa_glds(tb, (unsigned)((long long)r * rs * 2 + ch_l[u] * 16), dst + (wave * NI + u) * 1024);
+    }
+  }
+};
+
+// ============================================================================ forward, software-pipelined
+// Same contract, grid and numerics as fwd_kernel, restructured so the matrix pipe never waits on
+// the softmax of its own wave: key block kb+1's scores S(kb+1) = K Q^T are issued while the
+// softmax of S(kb) runs (independent instruction streams in one basic block), then P(kb) V(kb).
+// K and V live in separate two-slot LDS rings one block apart — at the start of iteration kb,
+// K(kb+1) and V(kb) are resident; K(kb+2) and V(kb+1) are LDS-DMA'd (no register staging) into
+// the slots of K(kb) and V(kb-1) during the iteration and retired before its ONE barrier.  Two
+// score accumulator sets (+32 VGPRs at QT = 2), none for staging.
+template <typename T, int D, bool CAUSAL, int EXT = 0, int QT = 2>
+__global__ __launch_bounds__(256, 2) void fwd_sp_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+                                                        const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
+                                                        float* __restrict__ LSE, int Sq_, int Sk_, int Hq, int Hk,
+                                                        Strides qs, Strides ks_, Strides vs, Strides os,
+                                                        float scale_log2, Extra ex = Extra{}) {
+  // head_dim 64 (the BERT / ERNIE attention): 2 query tiles of 16 rows per wave, 2 waves per SIMD,
+  // ~200 VGPRs.  (At 128 the second score set does not fit beside O: fwd_kernel serves it.)
+  static_assert(D == 64 && QT == 2, "software-pipelined forward: head_dim 64");
+  if constexpr ((EXT & 4) != 0) ex.seed = rng_mix(ex.seed);
+  constexpr int KS = D / 32;
+  constexpr int DB = D / 16;
+  constexpr int TILE = 64 * fa_pitch<D>() * 2;  // one [64][D] 16-bit tile
+  // [K slot 0][K slot 1][V slot 0][V slot 1]
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int nqb = (Sq_ + 64 * QT - 1) / (64 * QT);
+  int h, b, zi;
+  pair_order(Hq, (int)gridDim.y, nqb, h, b, zi);
+  const int qb = nqb - 1 - zi;
+  const int hk = h / (Hq / Hk);
+  const Seq sq_ = seq_of<EXT != 0>(ex, b, h, Hq, Sq_, Sk_);
+  const int Sq = sq_.sq, Sk = sq_.sk;
+  const int q0 = qb * 64 * QT;
+  if (EXT && q0 >= Sq) return;
+  const int qw0 = q0 + wave * 16 * QT;
+  const int off = Sk - Sq;
+  const float sl2 = (EXT & 2) ? kLog2e : scale_log2;
+  const float scale_n = scale_log2 / kLog2e;
+
+  const uint16_t* qbase = Q + (EXT && ex.cu_q ? 0 : b * qs.b) + sq_.qo * qs.s + h * qs.h;
+  const uint16_t* kbase = K + (EXT && ex.cu_q ? 0 : b * ks_.b) + sq_.ko * ks_.s + hk * ks_.h;
+  const uint16_t* vbase = V + (EXT && ex.cu_q ? 0 : b * vs.b) + sq_.ko * vs.s + hk * vs.h;
+
+  s16x8 qf[QT][KS];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int q = qw0 + 16 * t + (lane & 15);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      if (q < Sq)
+        qf[t][k] = *reinterpret_cast<const s16x8*>(qbase + (long long)q * qs.s + 32 * k + 8 * g);
+      else
+        qf[t][k] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  auto qfrag = [&](int t, int k) -> s16x8 { return qf[t][k]; };
+
+  f32x4 acc_o[QT][DB];
+#pragma unroll
+  for (int t = 0; t < QT; ++t)
+#pragma unroll
+    for (int d = 0; d < DB; ++d) acc_o[t][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run[QT], l_run[QT];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    m_run[t] = -INFINITY;
+    l_run[t] = 0.f;
+  }
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + 64 * QT + off);
+  const int nkb = kend > 0 ? (kend + 63) / 64 : 0;
+
+  auto kslot = [&](int i) { return smem + i * TILE; };
+  auto vslot = [&](int i) { return smem + (2 + i) * TILE; };
+
+  // S^T(kb) = K(kb) Q^T from a K slot
+  auto scores = [&](const char* k_lds, f32x4 (&acc)[QT][4]) {
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const s16x8 kf = ld_row8<D, false>(k_lds, 16 * j + (lane & 15), k, g);
+#pragma unroll
+        for (int t = 0; t < QT; ++t) acc[t][j] = Mfma<T>::run(kf, qfrag(t, k), acc[t][j]);
+      }
+    }
+  };
+
+  DmaTile<D, false> kd;
+  DmaTile<D, true> vd;
+  kd.init(wave, lane);
+  vd.init(wave, lane);
+  f32x4 s_cur[QT][4], s_nxt[QT][4];
+  if (nkb > 0) {
+    // prologue: K(0), V(0), K(1) resident before the first scores
+    kd.issue(kbase, ks_.s, 0, Sk, kslot(0), wave);
+    vd.issue(vbase, vs.s, 0, Sk, vslot(0), wave);
+    if (nkb > 1) kd.issue(kbase, ks_.s, 64, Sk, kslot(1), wave);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    scores(kslot(0), s_cur);
+  }
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * 64;
+    const bool nxt = kb + 1 < nkb;
+    // K(kb+2) into K(kb)'s slot (read as S(kb) in the previous iteration), V(kb+1) into V(kb-1)'s:
+    // in flight through this iteration's matrix work, retired before its closing barrier
+    if (kb + 2 < nkb) kd.issue(kbase, ks_.s, k0 + 128, Sk, kslot(kb & 1), wave);
+    if (nxt) vd.issue(vbase, vs.s, k0 + 64, Sk, vslot((kb + 1) & 1), wave);
+    const bool skip = CAUSAL && k0 > qw0 + 16 * QT - 1 + off;  // wave-uniform: tile above the diagonal
+    const char* knext = kslot((kb + 1) & 1);  // (stale on the last block: scores computed, never used)
+    auto qk_step = [&](int k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const s16x8 kf = ld_row8<D, false>(knext, 16 * j + (lane & 15), k, g);
+#pragma unroll
+        for (int t = 0; t < QT; ++t) s_nxt[t][j] = Mfma<T>::run(kf, qfrag(t, k), s_nxt[t][j]);
+      }
+    };
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s_nxt[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (skip) {
+#pragma unroll
+      for (int k = 0; k < KS; ++k) qk_step(k);
+    } else {
+      // phase A: k-step 0 of S(kb+1) | masks + row maxima of S(kb)
+      qk_step(0);
+      if constexpr ((EXT & 2) != 0) {
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
+          const int q = qw0 + 16 * t + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float mv[4] = {0.f, 0.f, 0.f, 0.f};
+            if (q < Sq) mask_row4<T>(ex, b, h, q, k0 + 16 * j + 4 * g, Sk, mv);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s_cur[t][j][r] = s_cur[t][j][r] * scale_n + mv[r];
+          }
+        }
+      }
+      if constexpr ((EXT & 8) != 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = k0 + 16 * j + 4 * g + r;
+            const int rs = key < Sk ? row_start(ex, b, h, key) : 0;
+#pragma unroll
+            for (int t = 0; t < QT; ++t)
+              if (qw0 + 16 * t + (lane & 15) >= rs) s_cur[t][j][r] = -INFINITY;
+          }
+      }
+      const bool need_mask = (k0 + 64 > Sk) || (CAUSAL && k0 + 63 > qw0 + off);
+      if (need_mask) {
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
+          const int q = qw0 + 16 * t + (lane & 15);
+          const int lim = CAUSAL ? min(Sk - 1, q + off) : Sk - 1;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (k0 + 16 * j + 4 * g + r > lim) s_cur[t][j][r] = -INFINITY;
+        }
+      }
+      float mnew[QT];
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        float mx = s_cur[t][0][0];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s_cur[t][j][r]);
+        mnew[t] = mx;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // phase B: k-step 1 | cross-lane maxima, lazy rescale
+      if constexpr (KS > 1) qk_step(1);
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        float mx = mnew[t];
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mnew[t] = mx * sl2;
+      }
+      bool bump = false;
+#pragma unroll
+      for (int t = 0; t < QT; ++t) bump = bump || (mnew[t] > m_run[t] + kRescaleTau);
+      if (__ballot(bump) != 0ull) {
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
+          const float m_upd = fmaxf(m_run[t], mnew[t]);
+          const float alpha = (m_upd == -INFINITY) ? 1.f : fast_exp2(m_run[t] - m_upd);
+          m_run[t] = m_upd;
+          l_run[t] *= alpha;
+#pragma unroll
+          for (int d = 0; d < DB; ++d) acc_o[t][d] *= alpha;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // phases C / D: k-steps 2 / 3 | exponentials, row sums, dropout, 16-bit P of query tile t
+      s16x8 pf[QT][2];
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        if (KS > 2 && t < KS - 2) qk_step(2 + t);
+        const float neg_m = (m_run[t] == -INFINITY) ? 0.f : -m_run[t];
+        float ls = 0.f;
+        float p[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            p[j][r] = fast_exp2(__builtin_fmaf(s_cur[t][j][r], sl2, neg_m));
+            ls += p[j][r];
+          }
+        l_run[t] += ls;
+        if constexpr ((EXT & 4) != 0) {
+          const int q = qw0 + 16 * t + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t bits = drop_bits(ex, b * Hq + h, q, k0 + 16 * j + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) p[j][r] *= drop_sub(ex, bits, r);
+          }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          pf[t][s2] = __builtin_bit_cast(s16x8, make_uint4(f2s2<T>(p[2 * s2][0], p[2 * s2][1]),
+                                                           f2s2<T>(p[2 * s2][2], p[2 * s2][3]),
+                                                           f2s2<T>(p[2 * s2 + 1][0], p[2 * s2 + 1][1]),
+                                                           f2s2<T>(p[2 * s2 + 1][2], p[2 * s2 + 1][3])));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // --- O^T += V^T P^T from V(kb)
+      const char* v_lds = vslot(kb & 1);
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const s16x8 vf = ld_tr8<D, true>(v_lds, 32 * s, d, lane);
+#pragma unroll
+          for (int t = 0; t < QT; ++t) acc_o[t][d] = Mfma<T>::run(vf, pf[t][s], acc_o[t][d]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s_cur[t][j] = s_nxt[t][j];
+  }
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    float l = l_run[t];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int q = qw0 + 16 * t + (lane & 15);
+    if (q < Sq) {
+      uint16_t* orow = O + (EXT && ex.cu_q ? 0 : b * os.b) + h * os.h + (sq_.qo + q) * os.s;
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        s16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2s<T>(acc_o[t][d][r] * inv);
+        *reinterpret_cast<s16x4*>(orow + 16 * d + 4 * g) = o;
+      }
+      if (g == 0) {
+        const float mm = (m_run[t] == -INFINITY) ? 0.f : m_run[t];
+        LSE[sq_.lrow + q] = l > 0.f ? (mm + log2f(l)) * kLn2 : -INFINITY;
+      }
+    }
+  }
+}
+
 // ============================================================================ backward
 // delta[b, h, q] = sum_d dO[q, d] * O[q, d] is computed inside bwd_dq_kernel (launched before the
 // dK/dV kernel, which reads the stored rows); there is no separate delta pass.

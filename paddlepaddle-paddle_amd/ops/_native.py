@@ -81,6 +81,7 @@ _SIGS = {
     'pa_flash_set_bwd_variant': [I],
     'pa_flash_set_pair_group': [I],
     'pa_flash_set_fwd_pipe': [I],
+    'pa_flash_set_fwd_sp': [I],
     'pa_gemm_fp8_ok': [I, I, I, LL, LL, LL],
     'pa_fp8_cast_transpose': [P, I, I, LL, P, P, P, I, I, P, I, F, P],
     'pa_fp8_amax': [P, I, I, LL, P, P],
