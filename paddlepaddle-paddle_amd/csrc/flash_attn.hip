@@ -221,11 +221,13 @@ PA_API hipError_t pa_flash_fwd_ex(const void* q, const void* k, const void* v, v
                                   const long long* vst, const long long* ost, float scale, int causal, int dt,
                                   const int* cu_q, const int* cu_k, int total_q, const void* mask, long long mb,
                                   long long mh, long long mq, int mask_f32, float p_drop, unsigned seed,
-                                  unsigned offset, const int* rows, long long rb, long long rh, hipStream_t st) {
+                                  unsigned offset, const int* rows, long long rb, long long rh, const int* mask_all,
+                                  hipStream_t st) {
   if (Hk <= 0 || Hq % Hk != 0 || (cu_q == nullptr) != (cu_k == nullptr)) return hipErrorInvalidValue;
   Strides qs{qst[0], qst[1], qst[2]}, ks{kst[0], kst[1], kst[2]}, vs{vst[0], vst[1], vst[2]}, os{ost[0], ost[1], ost[2]};
   if (mask && rows) return hipErrorInvalidValue;  // one mask form per call
-  const Extra ex = make_extra(cu_q, cu_k, total_q, mask, mb, mh, mq, mask_f32, p_drop, seed, offset, rows, rb, rh);
+  Extra ex = make_extra(cu_q, cu_k, total_q, mask, mb, mh, mq, mask_f32, p_drop, seed, offset, rows, rb, rh);
+  ex.mask_all = mask ? mask_all : nullptr;
   if (wide_d(D)) return wide_fwd(q, k, v, o, lse, B, Sq, Sk, Hq, Hk, D, qs, ks, vs, os, scale, causal, dt, &ex, st);
   dim3 grid(Hq, B, (Sq + 127) / 128);
   const int feat = 1 | (mask ? 2 : 0) | (p_drop > 0.f ? 4 : 0) | (rows ? 8 : 0);
@@ -295,13 +297,15 @@ PA_API hipError_t pa_flash_bwd_ex(const void* q, const void* k, const void* v, c
                                   const long long* dqst, const long long* dkst, const long long* dvst, float scale,
                                   int causal, int dt, const int* cu_q, const int* cu_k, int total_q, const void* mask,
                                   long long mb, long long mh, long long mq, int mask_f32, float p_drop, unsigned seed,
-                                  unsigned offset, const int* rows, long long rb, long long rh, hipStream_t st) {
+                                  unsigned offset, const int* rows, long long rb, long long rh, const int* mask_all,
+                                  hipStream_t st) {
   if (Hk <= 0 || Hq % Hk != 0 || (cu_q == nullptr) != (cu_k == nullptr)) return hipErrorInvalidValue;
   Strides qs{qst[0], qst[1], qst[2]}, ks{kst[0], kst[1], kst[2]}, vs{vst[0], vst[1], vst[2]},
       os{ost[0], ost[1], ost[2]}, dos{dost[0], dost[1], dost[2]}, dqs{dqst[0], dqst[1], dqst[2]},
       dks{dkst[0], dkst[1], dkst[2]}, dvs{dvst[0], dvst[1], dvst[2]};
   if (mask && rows) return hipErrorInvalidValue;  // one mask form per call
-  const Extra ex = make_extra(cu_q, cu_k, total_q, mask, mb, mh, mq, mask_f32, p_drop, seed, offset, rows, rb, rh);
+  Extra ex = make_extra(cu_q, cu_k, total_q, mask, mb, mh, mq, mask_f32, p_drop, seed, offset, rows, rb, rh);
+  ex.mask_all = mask ? mask_all : nullptr;
   // delta rows: [B, Hq, Sq] or, varlen, [Hq, total_q] (one "batch" of total_q packed rows)
   // (written by the dQ kernel, which runs first)
   if (wide_d(D))

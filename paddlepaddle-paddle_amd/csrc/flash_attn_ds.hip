@@ -224,7 +224,8 @@ PA_API hipError_t pa_flash_bwd_ds(const void* q, const void* k, const void* v, c
                                   const long long* dqst, const long long* dkst, const long long* dvst, float scale,
                                   int causal, int dt, const int* cu_q, const int* cu_k, int total_q, const void* mask,
                                   long long mb, long long mh, long long mq, int mask_f32, float p_drop, unsigned seed,
-                                  unsigned offset, const int* rows, long long rb, long long rh, hipStream_t st) {
+                                  unsigned offset, const int* rows, long long rb, long long rh, const int* mask_all,
+                                  hipStream_t st) {
   if (Hk <= 0 || Hq % Hk != 0 || (cu_q == nullptr) != (cu_k == nullptr) || dsT == nullptr) return hipErrorInvalidValue;
   if (mask && rows) return hipErrorInvalidValue;
   Strides qs{qst[0], qst[1], qst[2]}, ks{kst[0], kst[1], kst[2]}, vs{vst[0], vst[1], vst[2]},
@@ -242,6 +243,7 @@ PA_API hipError_t pa_flash_bwd_ds(const void* q, const void* k, const void* v, c
   ex.mh = mh;
   ex.mq = mq;
   ex.mask_f32 = mask_f32;
+  ex.mask_all = mask ? mask_all : nullptr;
   ex.p_drop = p_drop;
   ex.seed = seed;
   ex.offset = offset;

@@ -200,6 +200,9 @@ struct Extra {
   float keep_scale;      // 256 / (256 - drop_thresh): unbiased for the quantised keep probability
   const int* rows;       // flashmask: key k masked for queries q >= rows[b*rb + h*rh + k]
   long long rb, rh;
+  // [B] int32 (optional): nonzero = the dense mask keeps every key of batch entry b (a padding
+  // mask of an unpadded sequence) — its per-element loads are skipped for that entry
+  const int* mask_all = nullptr;
 };
 
 // flashmask column test (EXT & 8): true when (q, key) is masked by the start-row indices
@@ -271,10 +274,12 @@ __device__ __forceinline__ float drop_z(const Extra& ex, int bh, int q, int k) {
 struct Seq {
   long long qo, ko, lrow;
   int sq, sk;
+  bool mask;  // the dense mask must be read for this batch entry
 };
 template <bool EXT>
 __device__ __forceinline__ Seq seq_of(const Extra& ex, int b, int h, int Hq, int Sq, int Sk) {
   Seq r;
+  r.mask = !(EXT && ex.mask_all && ex.mask_all[b] != 0);
   if (EXT && ex.cu_q) {
     r.qo = ex.cu_q[b];
     r.ko = ex.cu_k[b];
@@ -448,7 +453,7 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void fwd_kernel(const uint16_
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           float mv[4] = {0.f, 0.f, 0.f, 0.f};
-          if (q < Sq) mask_row4<T>(ex, b, h, q, k0 + 16 * j + 4 * g, Sk, mv);
+          if (q < Sq && sq_.mask) mask_row4<T>(ex, b, h, q, k0 + 16 * j + 4 * g, Sk, mv);
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc_s[t][j][r] = acc_s[t][j][r] * scale_n + mv[r];
         }
@@ -780,7 +785,7 @@ __global__ __launch_bounds__(256, 2) void fwd_sp_kernel(const uint16_t* __restri
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             float mv[4] = {0.f, 0.f, 0.f, 0.f};
-            if (q < Sq) mask_row4<T>(ex, b, h, q, k0 + 16 * j + 4 * g, Sk, mv);
+            if (q < Sq && sq_.mask) mask_row4<T>(ex, b, h, q, k0 + 16 * j + 4 * g, Sk, mv);
 #pragma unroll
             for (int r = 0; r < 4; ++r) s_cur[t][j][r] = s_cur[t][j][r] * scale_n + mv[r];
           }
@@ -1163,7 +1168,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 
           float sl = scale_log2;
           if constexpr ((EXT & 2) != 0) {  // natural units + mask, then base-2
             float mv = 0.f;
-            if (q < Sq && mykey < Sk) {
+            if (q < Sq && mykey < Sk && sq_.mask) {
               const long long mi = (long long)b * ex.mb + (long long)h * ex.mh + (long long)q * ex.mq + mykey;
               mv = ex.mask_f32 ? reinterpret_cast<const float*>(ex.mask)[mi]
                                : to_f(reinterpret_cast<const T*>(ex.mask)[mi]);
@@ -1429,7 +1434,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128) ? 1 : 3 - NT) void bw
       for (int j = 0; j < 4; ++j) {
         float mv[4] = {0.f, 0.f, 0.f, 0.f};
         if constexpr ((EXT & 2) != 0)
-          if (myq < Sq) mask_row4<T>(ex, b, h, myq, k0 + 16 * j + 4 * g, Sk, mv);
+          if (myq < Sq && sq_.mask) mask_row4<T>(ex, b, h, myq, k0 + 16 * j + 4 * g, Sk, mv);
         uint32_t dbits = 0;
         if constexpr ((EXT & 4) != 0) dbits = drop_bits(ex, b * Hq + h, myq, k0 + 16 * j + 4 * g);
         float dsv[4];

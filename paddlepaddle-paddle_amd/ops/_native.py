@@ -118,7 +118,8 @@ _SIGS = {
     'pa_flash_ds_ld': [I],
     'pa_flash_ds_ws_elems': [I, I, I, I],
     'pa_flash_ds_set_pair_group': [I],
-    'pa_flash_bwd_ds': [P] * 11 + [I] * 6 + [LLP] * 8 + [F, I, I, P, P, I, P, LL, LL, LL, I, F, U32, U32, P, LL, LL, P],
+    'pa_flash_bwd_ds': [P] * 11 + [I] * 6 + [LLP] * 8 + [F, I, I, P, P, I, P, LL, LL, LL, I, F, U32, U32, P, LL, LL, P,
+                                                         P],
     'pa_conv2d_wgrad_ok': [I, I],
     'pa_conv2d_dgrad_classes': [P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     'pa_conv2d_wgrad': [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
@@ -140,9 +141,9 @@ _SIGS = {
     'pa_gemm8_wgrad_grouped2': [P, P, P, I, I, LL, LL, LL, P, P, P, I, I, LL, LL, LL, I, F, F, P],
     'pa_gemm_bf16': [P, P, P, P, P, I, I, I, LL, LL, LL, I, I, F, F, I, P],
     'pa_flash_fwd_ex': [P, P, P, P, P, I, I, I, I, I, I, LLP, LLP, LLP, LLP, F, I, I, P, P, I, P, LL, LL, LL, I, F,
-                        U32, U32, P, LL, LL, P],
+                        U32, U32, P, LL, LL, P, P],
     'pa_flash_bwd_ex': [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, LLP, LLP, LLP, LLP, LLP, LLP, LLP, LLP, F, I,
-                        I, P, P, I, P, LL, LL, LL, I, F, U32, U32, P, LL, LL, P],
+                        I, P, P, I, P, LL, LL, LL, I, F, U32, U32, P, LL, LL, P, P],
     'pa_decode_nsplit': [I, I, I],
     'pa_decode_ok': [I, I, I],
     'pa_decode_attn': [I, P, LL, P, P, P, P, I, I, LL, P, P, LL, P, LL, P, I, I, I, I, I, F, P],

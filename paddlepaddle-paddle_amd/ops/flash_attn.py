@@ -73,6 +73,7 @@ def _ds_ws(B, Hq, Sq, Sk, dtype, device):
 
 def _bwd_call(q, k, v, o, do, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, D, scale, causal, cu_q=None, cu_k=None,
               total=0, m=None, mb=0, mh=0, mq=0, mf=0, p_drop=0.0, seed=0, rows=None, rb=0, rh=0, ex=False):
+    mall = _mask_all(m, mh, mq)
     """The backward launch sequence: dS path when enabled, else the recompute kernels
     (pa_flash_bwd, or pa_flash_bwd_ex when any extended feature is in use)."""
     st = (N.strides3(q), N.strides3(k), N.strides3(v), N.strides3(o), N.strides3(do), N.strides3(dq),
@@ -83,13 +84,13 @@ def _bwd_call(q, k, v, o, do, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, D, scal
                                       N.ptr(dq), N.ptr(dk), N.ptr(dv), N.ptr(ws), B, Sq, Sk, Hq, Hk, D, *st, scale,
                                       int(causal), N.dtcode(q.dtype), N.ptr(cu_q), N.ptr(cu_k), total, N.ptr(m), mb,
                                       mh, mq, mf, float(p_drop), seed & 0xFFFFFFFF, 0, N.ptr(rows), rb, rh,
-                                      N.stream()), 'flash_bwd_ds')
+                                      N.ptr(mall), N.stream()), 'flash_bwd_ds')
     elif ex:
         N.check(N.lib.pa_flash_bwd_ex(N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse), N.ptr(delta),
                                       N.ptr(dq), N.ptr(dk), N.ptr(dv), B, Sq, Sk, Hq, Hk, D, *st, scale, int(causal),
                                       N.dtcode(q.dtype), N.ptr(cu_q), N.ptr(cu_k), total, N.ptr(m), mb, mh, mq, mf,
-                                      float(p_drop), seed & 0xFFFFFFFF, 0, N.ptr(rows), rb, rh, N.stream()),
-                'flash_bwd_ex')
+                                      float(p_drop), seed & 0xFFFFFFFF, 0, N.ptr(rows), rb, rh, N.ptr(mall),
+                                      N.stream()), 'flash_bwd_ex')
     else:
         N.check(N.lib.pa_flash_bwd(N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse), N.ptr(delta),
                                    N.ptr(dq), N.ptr(dk), N.ptr(dv), B, Sq, Sk, Hq, Hk, D, *st, scale, int(causal),
@@ -199,6 +200,15 @@ def _mask_args(mask, B, H, Sq, Sk, dtype):
     return m, st[0], st[1], st[2], int(m.dtype == torch.float32)
 
 
+def _mask_all(m, mh, mq):
+    """[B] int32 device flags for a key-only mask (constant over heads and queries): 1 where the
+    mask keeps every key of the batch entry (an unpadded sequence), so the kernels skip its
+    per-element loads; None for other masks.  No host synchronisation."""
+    if m is None or mh != 0 or mq != 0:
+        return None
+    return (m[:, 0, 0, :] == 0).all(-1).to(torch.int32)
+
+
 def _rows_args(rows, B, H, Sk):
     """(tensor, rb, rh) for flashmask start-row indices broadcastable to [B, H, Sk] (int32)."""
     if rows is None:
@@ -236,10 +246,12 @@ def _fwd_ex(q, k, v, causal, scale, mask, p_drop, seed, cu_q, cu_k, max_q, max_k
         qv, kv, vv, ov = q.unsqueeze(0), k.unsqueeze(0), v.unsqueeze(0), o.unsqueeze(0)
     m, mb, mh, mq, mf = _mask_args(mask, B, Hq, Sq, Sk, q.dtype)
     rows, rb, rh = _rows_args(rows, B, Hq, Sk)
+    mall = _mask_all(m, mh, mq)
     N.check(N.lib.pa_flash_fwd_ex(N.ptr(qv), N.ptr(kv), N.ptr(vv), N.ptr(ov), N.ptr(lse), B, Sq, Sk, Hq, Hk, D,
                                   N.strides3(qv), N.strides3(kv), N.strides3(vv), N.strides3(ov), scale, int(causal),
                                   N.dtcode(q.dtype), N.ptr(cu_q), N.ptr(cu_k), total, N.ptr(m), mb, mh, mq, mf,
-                                  float(p_drop), seed & 0xFFFFFFFF, 0, N.ptr(rows), rb, rh, N.stream()), 'flash_fwd_ex')
+                                  float(p_drop), seed & 0xFFFFFFFF, 0, N.ptr(rows), rb, rh, N.ptr(mall), N.stream()),
+            'flash_fwd_ex')
     return o, lse
 
 

@@ -102,3 +102,27 @@ def test_sp_forward_grad_through_classic_backward():
     _ref(qr, kr, vr, True).backward(g.float())
     for a, b_, n in ((q.grad, qr.grad, 'dq'), (k.grad, kr.grad, 'dk'), (v.grad, vr.grad, 'dv')):
         assert (a.float() - b_).abs().max().item() < 5e-2, n
+
+
+@pytest.mark.parametrize('sp', [0, 1])
+@pytest.mark.parametrize('D', [64, 128])
+def test_key_padding_mask_mixed_batch_fwd_bwd(sp, D):
+    """A key-only padding mask where some batch entries are unpadded (their per-element mask loads
+    are skipped through the per-batch all-keep flags) and others padded: forward and gradients vs
+    fp32, through both forward kernels."""
+    torch.manual_seed(21 + D)
+    B, S, H = 4, 320, 4
+    q, k, v = (torch.randn(B, S, H, D, device=DEV).to(torch.bfloat16).requires_grad_() for _ in range(3))
+    keep = torch.ones(B, 1, 1, S, dtype=torch.bool, device=DEV)
+    keep[1, ..., 250:] = False
+    keep[2, ..., 7:] = False
+    with _SP(bool(sp)):
+        o = FA.flash_attention_ex(q, k, v, mask=keep)
+    g = torch.randn_like(o)
+    o.backward(g)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    ref = _ref(qr, kr, vr, False, keep)
+    ref.backward(g.float())
+    assert (o.float() - ref).abs().max().item() < 2e-2
+    for a, b_, n in ((q.grad, qr.grad, 'dq'), (k.grad, kr.grad, 'dk'), (v.grad, vr.grad, 'dv')):
+        assert (a.float() - b_).abs().max().item() < 6e-2, n

@@ -41,6 +41,8 @@ def main():
     fl = 4 * B * H * S * S * D
     cases.append(('ernie mask+drop B64 S512 H12', lambda: FA.flash_attention_ex(q, k, v, mask=keep, dropout=0.1), fl))
     cases.append(('ernie mask      B64 S512 H12', lambda: FA.flash_attention_ex(q, k, v, mask=keep), fl))
+    allk = torch.ones(B, 1, 1, S, dtype=torch.bool, device='cuda')
+    cases.append(('all-keep mask+drop B64 S512', lambda: FA.flash_attention_ex(q, k, v, mask=allk, dropout=0.1), fl))
     cases.append(('plain           B64 S512 H12', lambda: FA.flash_attention(q, k, v, False), fl))
     B2, S2, H2 = 8, 2048, 16
     q2, k2, v2 = (torch.randn(B2, S2, H2, D, device='cuda', dtype=torch.bfloat16) for _ in range(3))
@@ -54,6 +56,20 @@ def main():
                 for sp in (0, 1):
                     _native.lib.pa_flash_set_fwd_sp(sp)
                     res.setdefault((name, sp), []).append(timed(fn))
+    # forward + backward of the ERNIE attention (bench shape: an all-keep padding mask + dropout)
+    qg, kg, vg = (t.clone().requires_grad_() for t in (q, k, v))
+    gout = torch.randn_like(q)
+
+    def fb(mask):
+        def f():
+            o = FA.flash_attention_ex(qg, kg, vg, mask=mask, dropout=0.1)
+            o.backward(gout)
+        return f
+    for nm, mk in (('fwd+bwd all-keep mask', allk), ('fwd+bwd no mask     ', None), ('fwd+bwd padded mask ', keep)):
+        for sp in (0, 1):
+            _native.lib.pa_flash_set_fwd_sp(sp)
+            t = timed(fb(mk), it=15)
+            print(f"{nm} sp={sp}: {t:8.1f} us ({3.5 * fl / t / 1e6:6.0f} TF-equiv)", flush=True)
     for name, fn, f in cases:
         a = sorted(res[(name, 0)])[1]
         b = sorted(res[(name, 1)])[1]
