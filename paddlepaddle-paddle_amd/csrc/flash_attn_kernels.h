@@ -331,7 +331,7 @@ __device__ __forceinline__ void pair_order(int Hq, int B, int NZ, int& h, int& b
 // grid: (Hq, B, ceil(Sq / (64 QT))), block 256 (4 waves x QT tiles of 16 query rows; QT = 2, 1 at D = 256)
 // PIPE: K/V tiles double-buffered in LDS, one barrier per key block.
 template <typename T, int D, bool CAUSAL, int EXT = 0, bool PIPE = false>
-__global__ __launch_bounds__(256, D > 128 ? 1 : 2) void fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+__device__ __forceinline__ void fwd_impl(char* smem_p, const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                      const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
                                                      float* __restrict__ LSE, int Sq_, int Sk_, int Hq, int Hk,
                                                      Strides qs, Strides ks_, Strides vs, Strides os, float scale_log2,
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void fwd_kernel(const uint16_
   // query tiles of 16 rows per wave: 2 (32 rows, 128-row blocks); D = 256 keeps 1 (64-row blocks)
   // so its O accumulators and Q fragments fit the register file
   constexpr int QT = D > 128 ? 1 : 2;
-  __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE];
+  char* const smem = smem_p;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches and addresses
@@ -594,6 +594,29 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void fwd_kernel(const uint16_
       }
     }
   }
+}
+
+// Entry point: a block whose batch entry has an all-keep mask (Extra::mask_all) runs the mask-free
+// instantiation — no mask branches or natural-unit rescaling in its loop (the mask path costs
+// ~30 % at D = 64 even with its loads skipped).  Both forms share this kernel's LDS.
+template <typename T, int D, bool CAUSAL, int EXT = 0, bool PIPE = false>
+__global__ __launch_bounds__(256, D > 128 ? 1 : 2) void fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+                                                     const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
+                                                     float* __restrict__ LSE, int Sq_, int Sk_, int Hq, int Hk,
+                                                     Strides qs, Strides ks_, Strides vs, Strides os, float scale_log2,
+                                                     Extra ex = Extra{}) {
+  constexpr int STAGE = 2 * 64 * fa_pitch<D>() * 2;
+  __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE];
+  if constexpr ((EXT & 2) != 0) {
+    constexpr int QT = D > 128 ? 1 : 2;
+    int h_, b_, z_;
+    pair_order(Hq, (int)gridDim.y, (Sq_ + 64 * QT - 1) / (64 * QT), h_, b_, z_);
+    if (ex.mask_all && !ex.cu_q && ex.mask_all[b_] != 0) {
+      fwd_impl<T, D, CAUSAL, (EXT & ~2), PIPE>(smem, Q, K, V, O, LSE, Sq_, Sk_, Hq, Hk, qs, ks_, vs, os, scale_log2, ex);
+      return;
+    }
+  }
+  fwd_impl<T, D, CAUSAL, EXT, PIPE>(smem, Q, K, V, O, LSE, Sq_, Sk_, Hq, Hk, qs, ks_, vs, os, scale_log2, ex);
 }
 
 // One 16-B-per-lane LDS-DMA (global_load_lds_dwordx4): global saddr base + per-lane 32-bit byte
@@ -945,8 +968,7 @@ __global__ __launch_bounds__(256, 2) void fwd_sp_kernel(const uint16_t* __restri
 // ((key / 64) * (dsld / 128) + query / 128) * 8192 elements: the dQ kernel reads each tile as one
 // 16 KiB run (row-major [key][dsld] rows 2 KiB apart streamed at 2.5 TB/s).
 template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0, bool PIPE = false, bool WDS = false>
-// (D = 96 with an additive mask needs more than 256 registers: one wave per SIMD there too)
-__global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 2) != 0)) ? 1 : 3 - NT) void bwd_dkdv_kernel(
+__device__ __forceinline__ void bwd_dkdv_impl(char* smem_p,
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq_, int Sk_, int Hq, int Hk, Strides qs, Strides ks_,
@@ -964,7 +986,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 
   // registers each, which with the dK / dV accumulators exceeded the 512-entry register file
   constexpr bool KVL = D > 128;
   constexpr int KVW = KVL ? NT * 16 * D * 2 : 0;  // bytes of one wave's K (or V) rows
-  __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE + 2 * NW * KVW];
+  char* const smem = smem_p;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches and addresses
@@ -1274,11 +1296,38 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 
   }
 }
 
+// Entry point (as fwd_kernel): all-keep batch entries run the mask-free instantiation.
+template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0, bool PIPE = false, bool WDS = false>
+// (D = 96 with an additive mask needs more than 256 registers: one wave per SIMD there too)
+__global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128 || (D == 96 && (EXT & 2) != 0)) ? 1 : 3 - NT) void bwd_dkdv_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
+    uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq_, int Sk_, int Hq, int Hk, Strides qs, Strides ks_,
+    Strides vs, Strides dos, Strides dks, Strides dvs, float scale, Extra ex = Extra{},
+    uint16_t* __restrict__ dsT = nullptr, long long dsb = 0, long long dsh = 0, int dsld = 0) {
+  constexpr int STAGE = 2 * 64 * fa_pitch<D>() * 2 + 2 * 64 * 4;
+  constexpr bool KVL = D > 128;
+  constexpr int KVW = KVL ? NT * 16 * D * 2 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE + 2 * NW * KVW];
+  if constexpr ((EXT & 2) != 0) {
+    int h_, b_, z_;
+    pair_order(Hq, (int)gridDim.y, (int)gridDim.z, h_, b_, z_);
+    if (ex.mask_all && !ex.cu_q && ex.mask_all[b_] != 0) {
+      bwd_dkdv_impl<T, D, CAUSAL, NT, NW, (EXT & ~2), PIPE, WDS>(smem, Q, K, V, dO, LSE, Delta, dK, dV, Sq_, Sk_, Hq,
+                                                                   Hk, qs, ks_, vs, dos, dks, dvs, scale, ex, dsT, dsb,
+                                                                   dsh, dsld);
+      return;
+    }
+  }
+  bwd_dkdv_impl<T, D, CAUSAL, NT, NW, EXT, PIPE, WDS>(smem, Q, K, V, dO, LSE, Delta, dK, dV, Sq_, Sk_, Hq, Hk, qs, ks_,
+                                                      vs, dos, dks, dvs, scale, ex, dsT, dsb, dsh, dsld);
+}
+
 // dQ: grid (ceil(Sq / (16*NT*NW)), Hq, B); NW waves x (16*NT) queries; loop over 64-key blocks
 // (swapped products: lane owns a query).  NT = 2: every K / V fragment read feeds two query tiles.
 // PIPE: K/V tiles double-buffered in LDS, one barrier per key block (as bwd_dkdv_kernel).
 template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0, bool PIPE = false>
-__global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128) ? 1 : 3 - NT) void bwd_dq_kernel(
+__device__ __forceinline__ void bwd_dq_impl(char* smem_p,
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
     uint16_t* __restrict__ dQ, int Sq_, int Sk_, int Hq, int Hk, Strides qs, Strides ks_, Strides vs, Strides dos,
@@ -1291,7 +1340,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128) ? 1 : 3 - NT) void bw
   // 2-way: SQ_LDS_BANK_CONFLICT was 20-27 % of LDS cycles in these kernels)
   constexpr bool BT = (fa_pitch<D>() >= 128);
   constexpr int STAGE = 2 * 64 * fa_pitch<D>() * 2;  // K and V of one key block
-  __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE];
+  char* const smem = smem_p;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches and addresses
   const int g = lane >> 4;
@@ -1507,6 +1556,28 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128) ? 1 : 3 - NT) void bw
       }
     }
   }
+}
+
+// Entry point (as fwd_kernel): all-keep batch entries run the mask-free instantiation.
+template <typename T, int D, bool CAUSAL, int NT, int NW = 4, int EXT = 0, bool PIPE = false>
+__global__ __launch_bounds__(64 * NW, (NW == 8 || D > 128) ? 1 : 3 - NT) void bwd_dq_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
+    uint16_t* __restrict__ dQ, int Sq_, int Sk_, int Hq, int Hk, Strides qs, Strides ks_, Strides vs, Strides dos,
+    Strides dqs, float scale, Extra ex = Extra{}, const uint16_t* __restrict__ O = nullptr, Strides os = Strides{}) {
+  constexpr int STAGE = 2 * 64 * fa_pitch<D>() * 2;
+  __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 2 : 1) * STAGE];
+  if constexpr ((EXT & 2) != 0) {
+    int h_, b_, z_;
+    pair_order(Hq, (int)gridDim.y, (Sq_ + 16 * NT * NW - 1) / (16 * NT * NW), h_, b_, z_);
+    if (ex.mask_all && !ex.cu_q && ex.mask_all[b_] != 0) {
+      bwd_dq_impl<T, D, CAUSAL, NT, NW, (EXT & ~2), PIPE>(smem, Q, K, V, dO, LSE, Delta, dQ, Sq_, Sk_, Hq, Hk, qs, ks_,
+                                                          vs, dos, dqs, scale, ex, O, os);
+      return;
+    }
+  }
+  bwd_dq_impl<T, D, CAUSAL, NT, NW, EXT, PIPE>(smem, Q, K, V, dO, LSE, Delta, dQ, Sq_, Sk_, Hq, Hk, qs, ks_, vs, dos,
+                                               dqs, scale, ex, O, os);
 }
 
 }  // namespace fa
