@@ -246,6 +246,13 @@ PA_API int pa_gemm8_set_staged9(int v) {
   return old;
 }
 
+PA_API int pa_gemm8_set_nt_store(int v) {
+  int old = 0;
+  (void)hipMemcpyFromSymbol(&old, HIP_SYMBOL(pa::g8::g_nt_store), sizeof(int));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(pa::g8::g_nt_store), &v, sizeof(int));
+  return old;
+}
+
 PA_API int pa_gemm8_set_wide_epi(int v) {
   int old = 1;
   (void)hipMemcpyFromSymbol(&old, HIP_SYMBOL(pa::g8::g_wide_epi), sizeof(int));

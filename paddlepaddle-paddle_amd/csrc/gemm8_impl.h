@@ -52,8 +52,11 @@ constexpr int BM = 256, BN = 256, BK = 64;
 // block, set only between launches.
 #ifndef PA_G8_EXTRA_TU
 __constant__ int g_wide_epi = 1;
+// A/B switch (pa_gemm8_set_nt_store): the wave-staged epilogue's row stores non-temporal
+__constant__ int g_nt_store = 0;
 #else
 static __constant__ int g_wide_epi = 1;  // gemm8x.hip: a private copy (its kernels do not read it)
+static __constant__ int g_nt_store = 0;
 #endif
 
 constexpr int HALF = 128 * BK * 2;  // one 128-row (or 128-col) half of an operand tile: 16 KB
@@ -721,10 +724,17 @@ __device__ __forceinline__ void epilogue_wstaged(const f32x4 (&acc)[8][4], uint1
       u32x4 v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = *(const lds_u32x4*)(rg + wtile(8 * j + (lane >> 3), lane & 7));
+      const bool nt = g_nt_store != 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int m = rb + 8 * j + (lane >> 3), n = nb + (lane & 7) * 8;
-        if (m < M && n < N) *reinterpret_cast<u32x4*>(dst + (long long)m * ldc + n) = v[j];
+        if (m < M && n < N) {
+          u32x4* ptr = reinterpret_cast<u32x4*>(dst + (long long)m * ldc + n);
+          if (nt)
+            __builtin_nontemporal_store(v[j], ptr);
+          else
+            *ptr = v[j];
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();  // the next half overwrites the region after these reads

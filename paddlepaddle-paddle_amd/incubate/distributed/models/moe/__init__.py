@@ -222,19 +222,48 @@ def _detect_grouped(experts, d_model):
 
 def _grouped_ffn(experts, spec, per_exp, d_model):
     """All experts' FFNs as two batched GEMMs over a [E, cap, d] zero-padded token block."""
+    counts = [c.shape[0] for c in per_exp]
+    cap = -(-max(max(counts), 1) // 8) * 8  # the GEMM's row contract
+    x = per_exp[0]
+    rows = torch.cat([torch.arange(c, device=x.device) + j * cap for j, c in enumerate(counts)])
+    flat = _grouped_ffn_rows(experts, spec, torch.cat(per_exp, 0), rows, cap, d_model)
+    return list(flat.split(counts, 0))
+
+
+def _ep_regroup_index(rc, E, cap, device):
+    """Expert-parallel regroup as ONE index: row i of the all-to-all receive buffer (grouped by
+    source rank, then local expert; rc[r][j] rows each) goes to slot j * cap + (rows of expert j
+    from ranks < r) + its position inside its segment of the [E, cap] expert-major block.  The
+    same index maps the block's outputs back to receive order (the return all-to-all's layout),
+    so neither direction loops over (rank, expert) pieces."""
+    W = len(rc)
+    seg_len = [rc[r][j] for r in range(W) for j in range(E)]
+    n = sum(seg_len)
+    seg_start, acc = [], 0
+    for c in seg_len:
+        seg_start.append(acc)
+        acc += c
+    base, run = [], [0] * E
+    for r in range(W):
+        for j in range(E):
+            base.append(j * cap + run[j])
+            run[j] += rc[r][j]
+    lens = torch.tensor(seg_len, device=device)
+    seg = torch.repeat_interleave(torch.arange(W * E, device=device), lens, output_size=n)
+    local = torch.arange(n, device=device) - torch.tensor(seg_start, device=device)[seg]
+    return torch.tensor(base, device=device)[seg] + local
+
+
+def _grouped_ffn_rows(experts, spec, x_rows, dst, cap, d_model):
+    """Two batched GEMMs over the [E, cap, d] block filled by ``x_rows`` at slots ``dst``; returns
+    the output rows in the order of ``x_rows``."""
     from ..... import ops
     first, act = spec
     E = len(experts)
     lins = [_ffn_linears(e) for e in experts]
     l1 = [l[first] for l in lins]
     l2 = [l[1 - first] for l in lins]
-    counts = [c.shape[0] for c in per_exp]
-    cap = max(max(counts), 1)
-    cap = -(-cap // 8) * 8  # the GEMM's row contract
-    x = per_exp[0]
-    blk = x.new_zeros(E, cap, d_model)
-    rows = torch.cat([torch.arange(c, device=x.device) + j * cap for j, c in enumerate(counts)])
-    blk = blk.view(E * cap, d_model).index_copy(0, rows, torch.cat(per_exp, 0)).view(E, cap, d_model)
+    blk = x_rows.new_zeros(E * cap, d_model).index_copy(0, dst, x_rows).view(E, cap, d_model)
     w1 = torch.stack([l.weight._t for l in l1])  # [E, d, f]
     w2 = torch.stack([l.weight._t for l in l2])  # [E, f, d]
     h = ops.matmul.matmul(blk, w1)
@@ -244,8 +273,7 @@ def _grouped_ffn(experts, spec, per_exp, d_model):
     y = ops.matmul.matmul(h, w2)
     if l2[0].bias is not None:
         y = y + torch.stack([l.bias._t for l in l2]).unsqueeze(1)
-    flat = y.reshape(E * cap, -1).index_select(0, rows)
-    return list(flat.split(counts, 0))
+    return y.reshape(E * cap, -1).index_select(0, dst)
 
 
 # ----------------------------------------------------------------- layer
@@ -298,6 +326,23 @@ class MoELayer(Layer):
             in_splits = counts.view(self.world_size, self.num_expert).sum(1).tolist()
             out_splits = recv_counts.view(self.world_size, self.num_expert).sum(1).tolist()
             recv = _AllToAll.apply(send, out_splits, in_splits, self.group)
+        mode = bool(self.training)
+        if mode not in self._grouped:  # probed per mode: train/eval behaviour may differ
+            self._grouped[mode] = _detect_grouped(list(self.experts), self.d_model) or False
+        spec = self._grouped[mode]
+        if self.world_size > 1 and spec and self.num_expert > 1:
+            # grouped experts: the receive buffer goes straight into the expert-major block and the
+            # block's outputs straight back into receive order (one index each way)
+            rc = recv_counts.view(self.world_size, self.num_expert).tolist()
+            cap = -(-max(max(sum(rc[r][j] for r in range(self.world_size)) for j in range(self.num_expert)), 1)
+                    // 8) * 8
+            dst = _ep_regroup_index(rc, self.num_expert, cap, recv.device)
+            back_in = _grouped_ffn_rows(list(self.experts), spec, recv, dst, cap, self.d_model)
+            ret = _AllToAll.apply(back_in, in_splits, out_splits, self.group)
+            y = torch.zeros(T, ret.shape[-1], dtype=ret.dtype, device=ret.device)
+            y = y.index_add(0, tok, ret * sf.unsqueeze(-1).to(ret.dtype))
+            return _wrap(y.reshape(shape[:-1] + (ret.shape[-1],)))
+        if self.world_size > 1:
             # recv is grouped by source rank, then local expert; regroup by local expert
             rc = recv_counts.view(self.world_size, self.num_expert)
             seg = list(recv.split(rc.reshape(-1).tolist(), 0))
@@ -305,10 +350,6 @@ class MoELayer(Layer):
                        for j in range(self.num_expert)]
         else:
             per_exp = list(send.split(counts.tolist(), 0))
-        mode = bool(self.training)
-        if mode not in self._grouped:  # probed per mode: train/eval behaviour may differ
-            self._grouped[mode] = _detect_grouped(list(self.experts), self.d_model) or False
-        spec = self._grouped[mode]
         if spec and self.num_expert > 1:
             outs = _grouped_ffn(list(self.experts), spec, per_exp, self.d_model)
         else:

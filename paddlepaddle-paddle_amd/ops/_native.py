@@ -131,6 +131,7 @@ _SIGS = {
     'pa_gemm_ok': [I, I, I, LL, LL, LL, I],
     'pa_gemm8_ok': [I, I, I, LL, LL, LL, I, I, I],
     'pa_gemm8_set_wide_epi': [I],
+    'pa_gemm8_set_nt_store': [I],
     'pa_gemm8_set_epi_sched': [I],
     'pa_gemm8_diag': [P, P, P, P, P, I, I, I, I, P],
     'pa_gemm8_set_staged_epi': [I],

@@ -1,5 +1,6 @@
 """Expert-parallel MoE (world 2, 2 local experts each) equals a single-process MoE holding all 4
-experts with the same gate, forward and input gradients."""
+experts with the same gate, forward and input gradients.  argv[1] == 'ffn': Linear-GELU-Linear
+experts, which run as batched GEMMs with the one-index receive-buffer regroup."""
 import os
 import sys
 
@@ -20,11 +21,22 @@ class Expert(paddle.nn.Layer):
         return paddle.nn.functional.relu(self.fc(x))
 
 
+class FFN(paddle.nn.Layer):
+    def __init__(self, d):
+        super().__init__()
+        self.fc1 = paddle.nn.Linear(d, 2 * d)
+        self.fc2 = paddle.nn.Linear(2 * d, d)
+
+    def forward(self, x):
+        return self.fc2(paddle.nn.functional.gelu(self.fc1(x)))
+
+
 def main():
+    ffn = len(sys.argv) > 1 and sys.argv[1] == 'ffn'
     dist.init_parallel_env()
     r, W, d = dist.get_rank(), 2, 8
     paddle.seed(0)
-    all_exp = [Expert(d) for _ in range(4)]
+    all_exp = [(FFN if ffn else Expert)(d) for _ in range(4)]
     gate = NaiveGate(d, 4, 1, topk=2)
     ref = MoELayer(d, all_exp, gate=gate)
     group = dist.new_group([0, 1])
@@ -39,6 +51,8 @@ def main():
     x2.stop_gradient = False
     y2 = ref(x2)
     assert float((y - y2).abs().max()) < 1e-5, float((y - y2).abs().max())
+    if ffn:
+        assert local._grouped.get(True), local._grouped  # the batched-GEMM path ran
     y.sum().backward()
     y2.sum().backward()
     assert float((x.grad - x2.grad).abs().max()) < 1e-5

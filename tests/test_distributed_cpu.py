@@ -94,8 +94,9 @@ def test_launch_module_spawns_workers(tmp_path):
     assert 'worker 1 2 1' in (tmp_path / 'log' / 'workerlog.1').read_text()
 
 
-def test_moe_expert_parallel_matches_single_process():
-    out = run_workers('worker_moe.py')
+@pytest.mark.parametrize("kind", ['linear', 'ffn'])
+def test_moe_expert_parallel_matches_single_process(kind):
+    out = run_workers('worker_moe.py', kind)
     assert out.count("moe OK") == 2, out[-3000:]
 
 
