@@ -88,6 +88,17 @@ def _conv(x, weight, bias, stride, padding, dilation, groups, data_format, nd, f
         # without a copy (only a genuinely NCHW-contiguous input, e.g. the image, is repacked once).
         y = ops.conv.conv2d_nhwc(t.permute(0, 2, 3, 1).contiguous(), w, b, s, p, d)
         return _w(y if cl else y.permute(0, 3, 1, 2))
+    if nd == 2 and groups == 1 and w.dim() == 4 and w.shape[0] % 8 and ops.use_hip(t):
+        # C_out off the 8-channel grain (a 10-class 1x1 head): zero filters pad C_out, the extra
+        # output channels are sliced away (their gradients are zero); autograd maps the padded
+        # filter / bias gradients back
+        cp = -(-w.shape[0] // 8) * 8 - w.shape[0]
+        wp = TF.pad(w, (0, 0, 0, 0, 0, 0, 0, cp))
+        if ops.conv.supported(t.permute(0, 2, 3, 1), wp, 1):
+            bp = None if b is None else TF.pad(b, (0, cp))
+            y = ops.conv.conv2d_nhwc(t.permute(0, 2, 3, 1).contiguous(), wp, bp, s, p, d)[..., :w.shape[0]]
+            y = y.contiguous()
+            return _w(y if cl else y.permute(0, 3, 1, 2))
     if nd == 2 and ops.use_hip(t) and ops.conv.dw_supported(t.permute(0, 2, 3, 1), w, groups):
         # depthwise (groups == C_in == C_out) on csrc/dwconv.hip, channels-last as above
         y = ops.conv.dwconv2d_nhwc(t.permute(0, 2, 3, 1).contiguous(), w, b, s, p, d)

@@ -431,3 +431,38 @@ def test_bn_channel_pad_matches_torch(C):
     torch.testing.assert_close(rm, rmr, atol=1e-3, rtol=1e-3)
     torch.testing.assert_close(rv, rvr, atol=2e-3, rtol=2e-3)
 
+
+
+@pytest.mark.parametrize('C,Cout,k,p,bias', [(512, 10, 1, 0, True), (64, 10, 3, 1, False), (128, 3, 3, 1, True)])
+def test_conv_cout_padding(C, Cout, k, p, bias):
+    """C_out % 8 != 0 (SqueezeNet's 10-class 1x1 head): paddle.nn.functional.conv2d pads C_out with
+    zero filters onto the implicit-GEMM kernels and slices the output; forward, data / filter / bias
+    gradients vs fp32 torch, no library convolution kernel."""
+    F = paddle.nn.functional
+    x = torch.randn(2, C, 13, 15, device=DEV).bfloat16()
+    w = (0.05 * torch.randn(Cout, C, k, k, device=DEV)).bfloat16()
+    b = torch.randn(Cout, device=DEV).bfloat16() if bias else None
+    xr = x.float().requires_grad_()
+    wr = w.float().requires_grad_()
+    br = b.float().requires_grad_() if bias else None
+    yr = torch.nn.functional.conv2d(xr, wr, br, 1, p)
+    g = torch.randn_like(yr)
+    xp = paddle.to_tensor(x, stop_gradient=False)
+    wp = paddle.to_tensor(w, stop_gradient=False)
+    bp = paddle.to_tensor(b, stop_gradient=False) if bias else None
+    out = []
+
+    def run():
+        y = F.conv2d(xp, wp, bp, 1, p)
+        y.backward(paddle.to_tensor(g.bfloat16()))
+        out.append(y)
+    bad = _miopen_kernels(run)
+    assert bad == [], bad
+    yr.backward(g)
+    y = out[0]._t if hasattr(out[0], '_t') else out[0]
+    assert tuple(y.shape) == tuple(yr.shape)
+    _close(y, yr, 3e-2, 1e-2, 'fwd')
+    _close(xp.grad._t, xr.grad, 3e-2, 1e-2, 'dgrad')
+    _close(wp.grad._t, wr.grad, 5e-2, 2e-2, 'wgrad')
+    if bias:
+        _close(bp.grad._t, br.grad, 5e-2, 2e-2, 'bgrad')
