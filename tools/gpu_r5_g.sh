@@ -6,6 +6,6 @@ mkdir -p gpurun_out/r5g
 timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r5g/rccl -o run -- python3 tools/rccl_order_trace.py --gpt13 > gpurun_out/r5g/rccl.log 2>&1 || { echo "trace failed"; tail -30 gpurun_out/r5g/rccl.log; exit 1; }
 trace=$(find gpurun_out/r5g/rccl -name "*kernel_trace.csv" | head -1)
 python3 tools/rccl_order_trace.py --overlap "$trace" | tee gpurun_out/r5g/overlap.txt
-python3 tools/rccl_order_trace.py --report "$trace" | tail -25 > gpurun_out/r5g/order.txt
+python3 tools/rccl_order_trace.py --report "$trace" > gpurun_out/r5g/order.txt || true
 head -25 gpurun_out/r5g/order.txt
-rm -f "$trace"
+cp "$trace" gpurun_out/r5g/trace_keep.csv 2>/dev/null; rm -f "$trace"

@@ -41,8 +41,8 @@ def run(steps=3, model_name='gpt-tiny', batch=4, seq=128):
     x, y = ids[:, :-1], ids[:, 1:]
     for i in range(steps):
         torch.cuda.synchronize()
-        # step marker kernel: a named fill the report splits steps on
-        torch.full((1,), float(i), device='cuda')
+        # step marker: a spin kernel the reports split steps on
+        torch.cuda._sleep(1000)
         loss = inner.loss(model(x), y)
         loss.backward()
         opt.step()
@@ -81,17 +81,25 @@ def report(path):
 
 
 def overlap(path):
-    """Share of RCCL kernel time that runs while a compute kernel of another queue runs (last
-    step: after the last step-marker fill), from a rocprofv3 kernel trace."""
+    """The last step (after the last spin marker) of a rocprofv3 kernel trace: the compute queue is
+    the one running the most kernels; every kernel on another queue is collective work (RCCL
+    kernels, or — for a 1-rank group, where RCCL turns a reduce-scatter / all-gather into a device
+    copy — its copies on the RCCL stream).  Prints those kernels by name and the share of their time
+    that runs concurrently with compute-queue kernels."""
+    from collections import Counter
     rows = list(csv.DictReader(open(path)))
     key = 'Kernel_Name' if 'Kernel_Name' in rows[0] else 'Kernel-Name'
+    qk = 'Queue_Id' if 'Queue_Id' in rows[0] else ('Stream_Id' if 'Stream_Id' in rows[0] else None)
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
-    is_rccl = lambda n: 'nccl' in n.lower() or 'rccl' in n.lower()  # noqa: E731
-    marks = [i for i, r in enumerate(rows) if 'FillFunctor' in r[key] or 'fill' in r[key].lower()]
-    t0 = int(rows[marks[-1]]['Start_Timestamp']) if marks else 0
+    marks = [i for i, r in enumerate(rows) if 'spin' in r[key].lower() or 'sleep' in r[key].lower()]
+    t0 = int(rows[marks[-1]]['End_Timestamp']) if marks else 0
     sel = [r for r in rows if int(r['Start_Timestamp']) >= t0]
-    comm = [(int(r['Start_Timestamp']), int(r['End_Timestamp'])) for r in sel if is_rccl(r[key])]
-    comp = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp'])) for r in sel if not is_rccl(r[key]))
+    qs = Counter(r[qk] for r in sel) if qk else Counter()
+    cq = qs.most_common(1)[0][0] if qs else None
+    is_comm = lambda r: ('nccl' in r[key].lower() or 'rccl' in r[key].lower() or  # noqa: E731
+                         (qk is not None and r[qk] != cq))
+    comm = [(int(r['Start_Timestamp']), int(r['End_Timestamp'])) for r in sel if is_comm(r)]
+    comp = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp'])) for r in sel if not is_comm(r))
     merged = []
     for a, b in comp:
         if merged and a <= merged[-1][1]:
@@ -108,9 +116,12 @@ def overlap(path):
                 break
             ov += min(b, d) - max(a, c)
     span = (max(b for _, b in comm + comp) - min(a for a, _ in comm + comp)) / 1e6 if comm else 0
-    n_comm = len(comm)
-    print(f"last step: {n_comm} RCCL kernels, {tot / 1e6:.3f} ms RCCL kernel time, {ov / 1e6:.3f} ms of it "
-          f"({100.0 * ov / max(tot, 1):.1f} %) concurrent with compute kernels; step span {span:.2f} ms")
+    print(f"queues in the last step (kernels): {dict(qs)}; compute queue {cq}")
+    names = Counter(r[key][:90] for r in sel if is_comm(r))
+    for n, c in names.most_common(12):
+        print(f"  collective-queue kernel x{c}: {n}")
+    print(f"last step: {len(comm)} collective-queue kernels, {tot / 1e6:.3f} ms, {ov / 1e6:.3f} ms of it "
+          f"({100.0 * ov / max(tot, 1):.1f} %) concurrent with compute-queue kernels; step span {span:.2f} ms")
 
 
 if __name__ == '__main__':
