@@ -61,6 +61,14 @@ static hipError_t launch(const void* A, const void* B, void* C, float* ws, const
   if (g_sched == 12) {
     const int items = tm * tn * splitk;
     const int g = items >= 256 ? 256 : (items + 7) / 8 * 8;  // one block per CU, a multiple of 8 (XCDs)
+    if constexpr (EPI == 0) {
+      if (g_staged == 4 && splitk == 1) {  // the quarter-tile wave-staged epilogue (EPI 300)
+        gemm12_kernel<AK, BKM, 300><<<g, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
+                                                       (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
+                                                       K, 1);
+        return hipGetLastError();
+      }
+    }
     gemm12_kernel<AK, BKM, EPI><<<g, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                    (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
                                                    K / splitk, splitk);

@@ -762,6 +762,77 @@ __device__ __forceinline__ void epilogue_wstaged(const f32x4 (&acc)[8][4], uint1
   }
 }
 
+// Quarter-tile wave-staged epilogue of the persistent schedule 12 (EPI 0): the operand LDS is busy
+// with the next work item's first K-tiles, so each wave stages its 128 x 64 slice through its own
+// 4 KiB of the spare LDS above them (32 rows per round, four rounds) and stores whole 128-B lines
+// as epilogue_wstaged does — the store tail overlaps the next item's staging DMA instead of a
+// block exit + prologue.
+template <typename OT = bf16_t>
+__device__ __forceinline__ void epilogue_wq(const f32x4 (&acc)[8][4], uint16_t* __restrict__ C,
+                                            const uint16_t* __restrict__ bias, int M, int N, long long ldc,
+                                            float alpha, float beta, int mb, int nb, int lane, lds_char* region) {
+  const int g = lane >> 4;
+  const bool upper = (g & 1) != 0;
+  const bool old_in = beta != 0.f;
+#pragma unroll
+  for (int qr = 0; qr < 4; ++qr) {
+    const int rb = mb + qr * 32;  // first row of this quarter
+    if (old_in) {
+      u32x4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 8 * j + (lane >> 3), c = lane & 7;
+        const int m = min(rb + r, M - 1), n = min(nb + c * 8, N - 8);
+        v[j] = *reinterpret_cast<const u32x4*>(C + (long long)m * ldc + n);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *(lds_u32x4*)(region + wtile(8 * j + (lane >> 3), lane & 7)) = v[j];
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int n = nb + (upper ? 16 * (2 * p + 1) + 4 * (g - 1) : 16 * (2 * p) + 4 * g);
+      const int ch = (n - nb) >> 3;
+      float bb[8];
+      if (bias != nullptr && n < N) load_f<OT, 8>(reinterpret_cast<const OT*>(bias + n), bb);
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = qr * 2 + ii;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float lo = acc[i][2 * p][e], hi = acc[i][2 * p + 1][e];
+          asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(lo), "+v"(hi));
+          v[e] = lo * alpha;
+          v[4 + e] = hi * alpha;
+        }
+        const int r = ii * 16 + (lane & 15);
+        lds_char* slot = region + wtile(r, ch);
+        if (bias != nullptr) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bb[e];
+        }
+        if (old_in) {
+          const Pack<OT, 8> ov = __builtin_bit_cast(Pack<OT, 8>, *(const lds_u32x4*)slot);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += beta * (float)ov.v[e];
+        }
+        *(lds_u32x4*)slot = pack8<OT>(v);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    u32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = *(const lds_u32x4*)(region + wtile(8 * j + (lane >> 3), lane & 7));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = rb + 8 * j + (lane >> 3), n = nb + (lane & 7) * 8;
+      if (m < M && n < N) *reinterpret_cast<u32x4*>(C + (long long)m * ldc + n) = v[j];
+    }
+    __builtin_amdgcn_wave_barrier();  // the next quarter overwrites the region after these reads
+  }
+}
+
 // same, with an explicit split-K slab index (persistent kernels: blockIdx.z is not the slice)
 template <int EPI>
 __device__ __forceinline__ void epilogue_z(const f32x4 (&acc)[8][4], uint16_t* __restrict__ C,
@@ -1399,13 +1470,15 @@ __device__ __forceinline__ void item_coords(int item, int splitk, int tm, int tn
   kb = z * ksplit;
 }
 
+// EPI 300: EPI 0 with the quarter-tile wave-staged epilogue (epilogue_wq) in the 32 KiB of LDS above
+// the operand buffers (its own instantiation: 160 KiB of LDS)
 template <bool AK, bool BKM, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm12_kernel(const char* __restrict__ A, const char* __restrict__ B,
                                                         uint16_t* __restrict__ C, float* __restrict__ ws,
                                                         const uint16_t* __restrict__ bias, int M, int N, int K,
                                                         long long lda, long long ldb, long long ldc, float alpha,
                                                         float beta, int ksplit, int splitk) {
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES + (EPI == 300 ? 32768 : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3, wq = wave & 3;
@@ -1545,7 +1618,10 @@ __global__ __launch_bounds__(512, 1) void gemm12_kernel(const char* __restrict__
     if (++kt == nt) {  // item j complete: epilogue from registers, then a fresh accumulator
       int m0, n0, kb, z;
       item_coords(item_of(j), splitk, tm, tn, ksplit, m0, n0, kb, z);
-      if constexpr (EPI == 1)
+      if constexpr (EPI == 300)
+        epilogue_wq(acc, C, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane,
+                    (lds_char*)smem + LDS_BYTES + wave * 4096);
+      else if constexpr (EPI == 1)
         epilogue_z<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane, z);
       else if (g_wide_epi)
         epilogue_wide<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);

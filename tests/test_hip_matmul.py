@@ -353,3 +353,30 @@ def test_tiny_n_head_on_transposed_skinny(M, K, n):
     assert calls, 'tiny-N GEMM did not reach the skinny kernel'
     assert y.shape == (M, n)
     _close(y, x.float() @ w.float() + b.float(), 2e-2, 'tiny-n')
+
+
+@pytest.mark.parametrize('M,K,N,kmaj,beta,bias', [(16384, 2048, 6144, True, 0.0, False), (1000, 512, 776, True, 0.0, True),
+                                                (4096, 1024, 2048, True, 1.0, False), (2048, 4096, 1024, False, 1.0, False),
+                                                (520, 256, 264, False, 0.0, False)])
+def test_persistent_schedule_staged_epilogue_matches(M, K, N, kmaj, beta, bias):
+    """Schedule 12 (persistent, the quarter-tile wave-staged epilogue in the spare LDS) equals the
+    default schedules bit for bit (same per-tile accumulation order), incl. ragged edges, bias and
+    the beta = 1 weight-gradient accumulate."""
+    g = torch.Generator(device=DEV).manual_seed(M + N)
+    a = _rand(M, K, g=g) if kmaj else _rand(K, M, g=g).t()
+    b = _rand(N, K, g=g).t()
+    bb = _rand(N, g=g) if bias else None
+    init = _rand(M, N, g=g)
+    outs = []
+    for v in (0, 12):
+        old = _native.lib.pa_gemm_set_variant(v)
+        try:
+            out = init.clone()
+            gemm.hip_mm(a, b, out=out, bias=bb, beta=beta)
+            torch.cuda.synchronize()
+        finally:
+            _native.lib.pa_gemm_set_variant(old)
+        outs.append(out)
+    ref = a.float() @ b.float() + (beta * init.float()) + (bb.float() if bias else 0.0)
+    _close(outs[1], ref, 2e-2, 'sched12')
+    assert torch.equal(outs[0], outs[1])
