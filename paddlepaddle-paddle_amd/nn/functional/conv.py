@@ -99,6 +99,10 @@ def _conv(x, weight, bias, stride, padding, dilation, groups, data_format, nd, f
             y = ops.conv.conv2d_nhwc(t.permute(0, 2, 3, 1).contiguous(), wp, bp, s, p, d)[..., :w.shape[0]]
             y = y.contiguous()
             return _w(y if cl else y.permute(0, 3, 1, 2))
+    if nd == 3 and groups == 1 and ops.use_hip(t) and w.dim() == 5:
+        y = _conv3d_depth_taps(t, w, b, s, p, d)
+        if y is not None:
+            return _w(y if cl else y.permute(0, 4, 1, 2, 3))
     if nd == 2 and ops.use_hip(t) and ops.conv.dw_supported(t.permute(0, 2, 3, 1), w, groups):
         # depthwise (groups == C_in == C_out) on csrc/dwconv.hip, channels-last as above
         y = ops.conv.dwconv2d_nhwc(t.permute(0, 2, 3, 1).contiguous(), w, b, s, p, d)
@@ -111,6 +115,32 @@ def _conv(x, weight, bias, stride, padding, dilation, groups, data_format, nd, f
     if cl:
         out = out.permute(0, *range(2, nd + 2), 1)
     return _w(out)
+
+
+def _conv3d_depth_taps(t, w, b, s, p, d):
+    """conv3d on the 2-D implicit-GEMM kernels: for every depth tap z of the filter, the input depth
+    slices that tap reads (stride s[0], dilation d[0], zero depth padding p[0]) are folded into the
+    batch — [N * D_out, H, W, C] channels-last — and convolved with the tap's 2-D filter w[:, :, z];
+    the kd partial outputs add up.  Differentiable through the 2-D kernels' backward.  Returns the
+    NDHWC output, or None when a 2-D sub-problem is outside the kernels' contract."""
+    N, C, D, H, W = t.shape
+    kd = w.shape[2]
+    Do = (D + 2 * p[0] - d[0] * (kd - 1) - 1) // s[0] + 1
+    if Do <= 0:
+        return None
+    xn = t.permute(0, 2, 3, 4, 1)  # NDHWC view
+    if p[0]:
+        xn = TF.pad(xn, (0, 0, 0, 0, 0, 0, p[0], p[0]))
+    y = None
+    for z in range(kd):
+        lo = z * d[0]
+        xz = xn[:, lo:lo + (Do - 1) * s[0] + 1:s[0]].reshape(N * Do, H, W, C)
+        wz = w[:, :, z]
+        if not ops.conv.supported(xz, wz, 1):
+            return None
+        yz = ops.conv.conv2d_nhwc(xz.contiguous(), wz.contiguous(), b if z == 0 else None, s[1:], p[1:], d[1:])
+        y = yz if y is None else y + yz
+    return y.reshape(N, Do, y.shape[1], y.shape[2], y.shape[3])
 
 
 @_amp_op('conv2d')

@@ -466,3 +466,40 @@ def test_conv_cout_padding(C, Cout, k, p, bias):
     _close(wp.grad._t, wr.grad, 5e-2, 2e-2, 'wgrad')
     if bias:
         _close(bp.grad._t, br.grad, 5e-2, 2e-2, 'bgrad')
+
+
+@pytest.mark.parametrize('C,Cout,D,k,s,p,fmt', [(32, 64, 8, 3, 1, 1, 'NCDHW'), (64, 32, 9, 3, 2, 1, 'NCDHW'),
+                                               (16, 32, 6, 1, 1, 0, 'NDHWC'), (32, 32, 7, 3, 1, 0, 'NDHWC')])
+def test_conv3d_depth_taps_on_hip_kernels(C, Cout, D, k, s, p, fmt):
+    """conv3d folded onto the 2-D implicit-GEMM kernels (one batched 2-D convolution per depth tap):
+    forward, data / filter / bias gradients vs fp32 torch, no library convolution kernel."""
+    F = paddle.nn.functional
+    x = torch.randn(2, C, D, 10, 12, device=DEV).bfloat16()
+    w = (0.05 * torch.randn(Cout, C, k, k, k, device=DEV)).bfloat16()
+    b = torch.randn(Cout, device=DEV).bfloat16()
+    xr, wr, br = (t.float().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.conv3d(xr, wr, br, s, p)
+    g = torch.randn_like(yr)
+    xin = x if fmt == 'NCDHW' else x.permute(0, 2, 3, 4, 1).contiguous()
+    xp = paddle.to_tensor(xin, stop_gradient=False)
+    wp = paddle.to_tensor(w, stop_gradient=False)
+    bp = paddle.to_tensor(b, stop_gradient=False)
+    out = []
+
+    def run():
+        y = F.conv3d(xp, wp, bp, s, p, data_format=fmt)
+        gg = g if fmt == 'NCDHW' else g.permute(0, 2, 3, 4, 1)
+        y.backward(paddle.to_tensor(gg.bfloat16().contiguous()))
+        out.append(y)
+    bad = _miopen_kernels(run)
+    assert bad == [], bad
+    yr.backward(g)
+    y = out[0]._t
+    if fmt == 'NDHWC':
+        y = y.permute(0, 4, 1, 2, 3)
+    assert tuple(y.shape) == tuple(yr.shape)
+    _close(y, yr, 3e-2, 1e-2, 'fwd')
+    dx = xp.grad._t if fmt == 'NCDHW' else xp.grad._t.permute(0, 4, 1, 2, 3)
+    _close(dx, xr.grad, 3e-2, 1e-2, 'dgrad')
+    _close(wp.grad._t, wr.grad, 5e-2, 2e-2, 'wgrad')
+    _close(bp.grad._t, br.grad, 5e-2, 2e-2, 'bgrad')
