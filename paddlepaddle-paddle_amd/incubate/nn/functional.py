@@ -543,7 +543,10 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
                             pre_caches=None, seq_lens=None, rotary_embs=None, time_step=None, attn_mask=None,
                             dropout_rate=0.0, rotary_emb_dims=0, activation="gelu", training=False,
                             mode='upscale_in_train', trans_qkvw=True, ring_id=-1, norm_type="layernorm",
-                            use_neox_rotary_style=False, gqa_group_size=-1, name=None):
+                            use_neox_rotary_style=False, gqa_group_size=-1, name=None,
+                            qkv_out_scales=None, out_linear_out_scales=None, ffn1_out_scales=None,
+                            ffn2_out_scales=None, qkv_in_scale=None, out_linear_in_scale=None, ffn1_in_scale=None,
+                            ffn2_in_scale=None, quant_round_type=1, quant_max_bound=127.0, quant_min_bound=-127.0):
     """A stack of transformer blocks in one call (reference incubate/nn/functional/
     fused_transformer.py:964).  Per layer: (pre-)norm -> fused QKV GEMM -> attention -> out proj
     -> residual -> (pre-)norm -> FFN1 -> activation -> FFN2 -> residual.
@@ -570,11 +573,25 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
     only ``time_step`` is re-read per replay as a value; ``attn_mask``, ``rotary_embs`` and
     ``seq_lens`` are graph inputs by ADDRESS — the replay reads whatever their storage holds, so
     they must be static buffers the caller refills in place (``buf.copy_(new)``) before each
-    replay; a freshly allocated tensor per step would be silently ignored."""
-    tp_group = _ring_group(ring_id) if ring_id != -1 else None
+    replay; a freshly allocated tensor per step would be silently ignored.
 
-    def row_parallel(t, w, b):
-        o_ = lin(t, w, None)
+    int8 weights (``fused_multi_transformer_int8``, reference fused_multi_transformer_int8_op.cu):
+    a Linear whose weight is int8 — laid out [out, in] (qkv [3, H, D, E] with trans_qkvw) — runs
+    quantise (per-layer calibrated ``*_in_scale``) -> int8 GEMM -> dequantise by the per-channel
+    ``*_out_scales`` [N] + bias on ops.int8.static_int8_linear (int8 MFMA GEMM / W8A16 decode
+    kernel on the GPU)."""
+    tp_group = _ring_group(ring_id) if ring_id != -1 else None
+    qcfg = dict(round_type=quant_round_type, max_bound=quant_max_bound, min_bound=quant_min_bound)
+
+    def qsc(ins, outs, i):
+        if outs is None:
+            return None
+        if ins is None:
+            raise ValueError("fused_multi_transformer: int8 weights need the *_in_scale of every Linear")
+        return float(ins[i]), _u(outs[i])
+
+    def row_parallel(t, w, b, q=None):
+        o_ = lin(t, w, None, q=q)
         import torch.distributed as tdist
         tdist.all_reduce(o_, group=tp_group.pg)
         return o_ + _u(b).reshape(1, -1).to(o_.dtype) if b is not None else o_
@@ -598,9 +615,15 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
             return _u(fused_rms_norm(_w(t), w, b, epsilon))
         return _u(F.layer_norm(_w(t), [E], w, b, epsilon))
 
-    def lin(t, w, b, trans=False):
+    def lin(t, w, b, trans=False, q=None, i8_kn=False):
         t2 = t.reshape(-1, t.shape[-1])
         wt = _u(w)
+        if wt.dtype == torch.int8:  # [N, K] int8; i8_kn: the qkv weight [K, N] without trans_qkvw
+            if q is None:
+                raise ValueError("fused_multi_transformer: int8 weights need *_out_scales and *_in_scale")
+            wq = wt.t() if i8_kn else wt
+            return ops.int8.static_int8_linear(t2, wq.contiguous(), q[1], q[0],
+                                               None if b is None else _u(b).reshape(-1), **qcfg)
         wt = wt.t() if trans else wt
         bb = None if b is None else _u(b).reshape(-1)
         if bb is not None and bb.dtype == t2.dtype and ops.gemm._skinny_wins(t2.shape[0], wt.shape[1], t2.shape[1]):
@@ -652,10 +675,10 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
         qb = qkv_biases[i] if qkv_biases is not None else None
         if trans_qkvw:
             Wm = w.reshape(-1, E)                                  # [(Hq + 2 Hkv) * D, E]
-            qkv = lin(a, Wm, qb, trans=True)
+            qkv = lin(a, Wm, qb, trans=True, q=qsc(qkv_in_scale, qkv_out_scales, i))
         else:
             Wm = w.reshape(E, -1)
-            qkv = lin(a, Wm, qb)
+            qkv = lin(a, Wm, qb, q=qsc(qkv_in_scale, qkv_out_scales, i), i8_kn=True)
         if gqa_group_size > 0:
             D = w.shape[-2] if trans_qkvw else w.shape[-1]
             Hkv = gqa_group_size
@@ -723,7 +746,8 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
         if cache is not None:
             caches_out.append(cache_kvs[i])
         o = (row_parallel if tp_group is not None else lin)(
-            o.reshape(B, S, Hq * D), linear_weights[i], linear_biases[i] if linear_biases is not None else None)
+            o.reshape(B, S, Hq * D), linear_weights[i], linear_biases[i] if linear_biases is not None else None,
+            q=qsc(out_linear_in_scale, out_linear_out_scales, i))
         if fuse_res:
             f, h = norm_add(o.reshape(B, S, E).to(resid.dtype), resid, ffn_ln_scales[i],
                             ffn_ln_biases[i] if ffn_ln_biases is not None else None)
@@ -734,9 +758,11 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
             f = norm(h, ffn_ln_scales[i], ffn_ln_biases[i] if ffn_ln_biases is not None else None) \
                 if pre_layer_norm else h
         resid = h
-        f = act(lin(f, ffn1_weights[i], ffn1_biases[i] if ffn1_biases is not None else None))
+        f = act(lin(f, ffn1_weights[i], ffn1_biases[i] if ffn1_biases is not None else None,
+                    q=qsc(ffn1_in_scale, ffn1_out_scales, i)))
         f = (row_parallel if tp_group is not None else lin)(
-            f, ffn2_weights[i], ffn2_biases[i] if ffn2_biases is not None else None)
+            f, ffn2_weights[i], ffn2_biases[i] if ffn2_biases is not None else None,
+            q=qsc(ffn2_in_scale, ffn2_out_scales, i))
         if fuse_res:
             pending = f.reshape(B, S, E).to(resid.dtype)
             continue
@@ -747,6 +773,32 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
         h = h + pending
     out = _w(h)
     return (out, caches_out) if cache_kvs is not None else out
+
+
+def fused_multi_transformer_int8(x, ln_scales, ln_biases, qkv_weights, qkv_biases, linear_weights, linear_biases,
+                                 ffn_ln_scales, ffn_ln_biases, ffn1_weights, ffn1_biases, ffn2_weights, ffn2_biases,
+                                 pre_layer_norm=True, epsilon=1e-05, cache_kvs=None, time_step=None, attn_mask=None,
+                                 dropout_rate=0.0, activation="gelu", training=False, mode='upscale_in_train',
+                                 trans_qkvw=True, ring_id=-1, name=None, qkv_out_scales=None,
+                                 out_linear_out_scales=None, ffn1_out_scales=None, ffn2_out_scales=None, num_head=0,
+                                 dim_head=0, dim_ffn=0, qkv_in_scale=(), out_linear_in_scale=(), ffn1_in_scale=(),
+                                 ffn2_in_scale=(), quant_round_type=1, quant_max_bound=127.0, quant_min_bound=-127.0):
+    """The int8 FusedMultiTransformer (reference paddle/fluid/operators/fused/
+    fused_multi_transformer_int8_op.cc; API as in test/legacy_test/test_fused_multi_transformer_int8_op.py:32):
+    int8 weights [out, in] (qkv [3, H, D, E]), per-layer calibrated activation scales ``*_in_scale``
+    (floats) and per-output-channel dequant scales ``*_out_scales`` ([N] fp32).  Every Linear runs
+    quantise -> int8 GEMM -> dequantise + bias (ops.int8.static_int8_linear); norms, attention and
+    the KV cache are the 16-bit fused_multi_transformer path.  num_head / dim_head / dim_ffn are
+    implied by the weight shapes."""
+    return fused_multi_transformer(
+        x, ln_scales, ln_biases, qkv_weights, qkv_biases, linear_weights, linear_biases, ffn_ln_scales,
+        ffn_ln_biases, ffn1_weights, ffn1_biases, ffn2_weights, ffn2_biases, pre_layer_norm=pre_layer_norm,
+        epsilon=epsilon, cache_kvs=cache_kvs, time_step=time_step, attn_mask=attn_mask, dropout_rate=dropout_rate,
+        activation=activation, training=training, mode=mode, trans_qkvw=trans_qkvw, ring_id=ring_id,
+        qkv_out_scales=qkv_out_scales, out_linear_out_scales=out_linear_out_scales, ffn1_out_scales=ffn1_out_scales,
+        ffn2_out_scales=ffn2_out_scales, qkv_in_scale=qkv_in_scale, out_linear_in_scale=out_linear_in_scale,
+        ffn1_in_scale=ffn1_in_scale, ffn2_in_scale=ffn2_in_scale, quant_round_type=quant_round_type,
+        quant_max_bound=quant_max_bound, quant_min_bound=quant_min_bound)
 
 
 def variable_length_memory_efficient_attention(query, key, value, seq_lens, kv_seq_lens, mask=None, scale=None,

@@ -39,3 +39,4 @@ from . import decode  # noqa: E402,F401
 from . import fp8  # noqa: E402,F401
 from . import matmul  # noqa: E402,F401
 from . import woq  # noqa: E402,F401
+from . import int8  # noqa: E402,F401

@@ -94,6 +94,7 @@ _SIGS = {
     'pa_gemm8_i8_ok': [I, I, I, LL, LL, LL],
     'pa_gemm8_i8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, P],
     'pa_i8_quant_rows': [P, I, I, LL, P, P, LL, P, I, P],
+    'pa_i8_quant_static': [P, I, I, I, LL, P, LL, F, F, F, I, I, I, P],
     'pa_amp_check_unscale': [P, P, P, I, P, P, P],
     'pa_amp_update_scale': [P, P, P, P, I, I, F, F, F, P],
     'pa_gemm8_fp8_splitk': [P, P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, I, P],

@@ -23,14 +23,14 @@ def i8_mm_ok(a, w):
 
 def i8_mm(a, w, row_scale, col_scale, bias=None, out=None, beta=0.0, out_dtype=torch.bfloat16):
     """out[M, N] = (a @ w^T) * row_scale[m] * col_scale[n] (+ beta * out) (+ bias), int32 accumulation;
-    row_scale fp32 [M] (per token), col_scale fp32 [N] (per output channel)."""
+    row_scale fp32 [M] (per token; None = 1), col_scale fp32 [N] (per output channel)."""
     M, K = a.shape
     Nn = w.shape[0]
     if out is None:
         out = torch.empty(M, Nn, dtype=out_dtype, device=a.device)
         beta = 0.0
     assert out.dtype == torch.bfloat16 and out.stride(1) == 1 and out.shape == (M, Nn)
-    rs = row_scale.float().contiguous()
+    rs = None if row_scale is None else row_scale.float().contiguous()
     cs = col_scale.float().contiguous()
     b = None if bias is None else bias.to(torch.bfloat16).contiguous()
     N.check(N.lib.pa_gemm8_i8(N.ptr(a), N.ptr(w), N.ptr(out), N.ptr(b), N.ptr(rs), N.ptr(cs), M, Nn, K, a.stride(0),
@@ -55,6 +55,62 @@ def quant_rows(x, excl=None, rows=None):
 def quant_rows_ok(x):
     return (x.is_cuda and x.dim() == 2 and x.stride(1) == 1 and x.dtype in (torch.bfloat16, torch.float16, torch.float32)
             and x.shape[1] % 8 == 0 and x.stride(0) % 8 == 0 and x.data_ptr() % 32 == 0 and _lib() is not None)
+
+
+def quant_static(x, mul, rows=None, out_dtype=torch.int8, round_type=1, max_bound=127.0, min_bound=-127.0):
+    """q = clip(round(x * mul), min_bound, max_bound) of x [M, K] (csrc/int8_quant.hip
+    pa_i8_quant_static; round_type 1 rounds half away from zero, 0 half to even) into int8 — or bf16
+    holding the same integers — [rows or M, K], padding rows zero."""
+    M, K = x.shape
+    R = rows or M
+    q = torch.empty(R, K, dtype=out_dtype, device=x.device)
+    N.check(_lib().pa_i8_quant_static(N.ptr(x), M, R, K, x.stride(0), N.ptr(q), K, float(mul), float(min_bound),
+                                     float(max_bound), int(round_type), N.dtcode(x.dtype),
+                                     0 if out_dtype == torch.int8 else 1, N.stream()), 'i8_quant_static')
+    return q
+
+
+def _round_ref(v, round_type):
+    return torch.round(v) if round_type == 0 else torch.sign(v) * torch.floor(v.abs() + 0.5)
+
+
+def static_int8_linear(x, qw, out_scale, in_scale, bias=None, round_type=1, max_bound=127.0, min_bound=-127.0):
+    """The int8 Linear of fused_multi_transformer_int8 (reference fused_multi_transformer_int8_op.cu:
+    quantise -> int8 GEMM -> dequantise + bias): x [..., K] is quantised per tensor with the
+    calibrated ``in_scale`` (q = clip(round(max_bound * in_scale * x))), multiplied by the int8
+    weight ``qw`` [N, K] in int32 and dequantised per output channel by ``out_scale`` [N]
+    (y = acc * out_scale[n] + bias[n]).
+
+    GPU: decode-shaped token counts (M <= 32) quantise into bf16 integers and stream the int8 weight
+    once through the W8A16 decode kernel (csrc/woq_gemm.hip; integer products, fp32 sums; quantising
+    inside that kernel's loads measured slower: every column block redoes it on its critical path); larger
+    ones quantise into int8 rows (padded to 8) for the v_mfma_i32_16x16x64_i8 GEMM
+    (csrc/gemm8x.hip pa_gemm8_i8) with the dequant scale and bias in its epilogue.  Output bf16 on
+    the GPU (the model's activation dtype), x.dtype on the CPU composite."""
+    from . import woq
+    K = x.shape[-1]
+    x2 = x.reshape(-1, K)
+    M, Nn = x2.shape[0], qw.shape[0]
+    mul = float(max_bound) * float(in_scale)
+    osc = out_scale.to(device=x.device, dtype=torch.float32).reshape(-1)
+    if x2.is_cuda and qw.dtype == torch.int8 and _lib() is not None and K % 8 == 0:
+        x2 = x2.contiguous()
+        if M <= 32:
+            qb = quant_static(x2, mul, out_dtype=torch.bfloat16, round_type=round_type, max_bound=max_bound,
+                              min_bound=min_bound)
+            if woq.woq_ok(qb, qw, 8, 0):
+                y = woq.woq_linear(qb, qw, osc, 8, 0, None if bias is None else bias.reshape(-1))
+                return y.reshape(*x.shape[:-1], Nn)
+        M8 = -(-M // 8) * 8
+        qa = quant_static(x2, mul, rows=M8, round_type=round_type, max_bound=max_bound, min_bound=min_bound)
+        if i8_mm_ok(qa, qw):
+            y = i8_mm(qa, qw, None, osc, bias=None if bias is None else bias.reshape(-1))
+            return y[:M].reshape(*x.shape[:-1], Nn)
+    q = _round_ref(x2.float() * mul, round_type).clamp_(min_bound, max_bound)
+    y = (q.double() @ qw.to(x.device).double().t()).float() * osc
+    if bias is not None:
+        y = y + bias.to(x.device).float().reshape(1, -1)
+    return y.to(x.dtype if x.is_floating_point() else torch.float32).reshape(*x.shape[:-1], Nn)
 
 
 # ----------------------------------------------------------------------------- static int8 programs
