@@ -104,15 +104,20 @@ __global__ __launch_bounds__(256) void fwd_kernel(const uint16_t* __restrict__ x
 
   const int g4 = lane >> 4, l16 = lane & 15;
   const int SC = g.S * g.C;
-  // the wave's filter slice for all K steps, rows permuted (see the header)
-  s16x8 wf[KSTEPS][4];
-  {
-    const uint16_t* wb = wimg + (long long)(co0 + 16 * (l16 >> 2) + (l16 & 3)) * g.Kp + 8 * g4;
+  // the wave's filter slice for all K steps, rows permuted (see the header).  Up to 8 K steps it
+  // stays in registers for all RB rows; the deep filters (AlexNet's 11x11: Kp = 448, 14 steps,
+  // instantiated as KSTEPS 16 with the live count g.Kp / 32) re-read it per step from L1/L2
+  // (64 x Kp x 2 bytes, shared by every block of the launch) instead of holding 224 VGPRs.
+  constexpr bool WREG = KSTEPS <= 8;
+  const uint16_t* wb = wimg + (long long)(co0 + 16 * (l16 >> 2) + (l16 & 3)) * g.Kp + 8 * g4;
+  s16x8 wf[WREG ? KSTEPS : 1][4];
+  if constexpr (WREG) {
 #pragma unroll
     for (int ks = 0; ks < KSTEPS; ++ks)
 #pragma unroll
       for (int t = 0; t < 4; ++t) wf[ks][t] = *reinterpret_cast<const s16x8*>(wb + (long long)4 * t * g.Kp + ks * 32);
   }
+  const int nks = WREG ? KSTEPS : g.Kp / 32;
   // this lane's (filter row, run offset) per K step
   int kr[KSTEPS], kj[KSTEPS];
 #pragma unroll
@@ -141,6 +146,11 @@ __global__ __launch_bounds__(256) void fwd_kernel(const uint16_t* __restrict__ x
       for (int t = 0; t < 4; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KSTEPS; ++ks) {
+      if (!WREG && ks >= nks) break;  // block-uniform
+      s16x8 wk[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        wk[t] = WREG ? wf[WREG ? ks : 0][t] : *reinterpret_cast<const s16x8*>(wb + (long long)4 * t * g.Kp + ks * 32);
       const int r = kr[ks], j0 = kj[ks];
       const bool live = r < g.R;
       const uint16_t* rowp = rows + (rb * g.sh + (live ? r : 0)) * g.SEGP;
@@ -162,7 +172,7 @@ __global__ __launch_bounds__(256) void fwd_kernel(const uint16_t* __restrict__ x
         }
         xf = __builtin_bit_cast(s16x8, d);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[m][t] = mfma<T>(wf[ks][t], xf, acc[m][t]);
+        for (int t = 0; t < 4; ++t) acc[m][t] = mfma<T>(wk[t], xf, acc[m][t]);
       }
     }
     // lane: channels co0 + 16 g4 + 4 t + e (acc[m][t][e]) of pixel ow0 + 32 wave + 16 m + l16
@@ -259,7 +269,7 @@ static bool stem_geo(int N, int H, int W, int C, int Ho, int Wo, int Cout, int R
   if ((long long)W * C >= (1LL << 30)) return false;
   const int RK = (S * C + 7) / 8 * 8;
   const int Kp = (R * RK + 31) / 32 * 32;
-  if (Kp > 256) return false;
+  if (Kp > 512) return false;  // > 256: the streamed-filter instantiation
   // staged segment: columns (ow0*sw - pw) .. ((ow0+PT-1)*sw - pw + S - 1), plus up to 7 elements
   // of round-down slack in front and the last fragment's read-ahead (RK - S*C + the 5th dword)
   const int SEGP = ((((PT - 1) * sw + S) * C + RK + 16) + 7) / 8 * 8;
@@ -328,7 +338,7 @@ PA_API hipError_t pa_conv_stem_fwd(const void* x, const void* wimg, const void* 
     case 6: PA_STEM_LAUNCH(T, 6); break;        \
     case 7: PA_STEM_LAUNCH(T, 7); break;        \
     case 8: PA_STEM_LAUNCH(T, 8); break;        \
-    default: return hipErrorInvalidValue;       \
+    default: PA_STEM_LAUNCH(T, 16); break;      \
   }
   if (dt == 1) {
     PA_STEM_KS(bf16_t)

@@ -99,6 +99,14 @@ def _conv(x, weight, bias, stride, padding, dilation, groups, data_format, nd, f
             y = ops.conv.conv2d_nhwc(t.permute(0, 2, 3, 1).contiguous(), wp, bp, s, p, d)[..., :w.shape[0]]
             y = y.contiguous()
             return _w(y if cl else y.permute(0, 3, 1, 2))
+    if (nd == 2 and w.dim() == 4 and t.shape[1] >= 8 and t.shape[1] % 8 and (groups == 1 or groups == t.shape[1])
+            and ops.use_hip(t)):
+        # C_in off the 8-channel grain (ShuffleNet's 58 / 116-channel branches): the channels-last
+        # input is zero-padded to the grain (one copy) with zero filter taps for the extra channels
+        # (plain conv: extra input channels; depthwise: extra channels sliced off the output)
+        y = _conv_cin_pad(t, w, b, s, p, d, groups)
+        if y is not None:
+            return _w(y if cl else y.permute(0, 3, 1, 2))
     if nd == 3 and groups == 1 and ops.use_hip(t) and w.dim() == 5:
         y = _conv3d_depth_taps(t, w, b, s, p, d)
         if y is not None:
@@ -115,6 +123,28 @@ def _conv(x, weight, bias, stride, padding, dilation, groups, data_format, nd, f
     if cl:
         out = out.permute(0, *range(2, nd + 2), 1)
     return _w(out)
+
+
+def _conv_cin_pad(t, w, b, s, p, d, groups):
+    """conv2d / depthwise conv2d of an NCHW(-viewed) t whose channel count C is not a multiple of 8,
+    on the hand-written channels-last kernels over a zero-padded copy; returns NHWC or None."""
+    C = t.shape[1]
+    cp = -(-C // 8) * 8 - C
+    xp = TF.pad(t.permute(0, 2, 3, 1), (0, cp))                     # NHWC, channels padded, contiguous
+    if groups == 1:
+        co = w.shape[0]
+        cop = -(-co // 8) * 8 - co
+        wp = TF.pad(w, (0, 0, 0, 0, 0, cp, 0, cop))                  # zero taps: extra in / out channels
+        bp = None if b is None else TF.pad(b, (0, cop))
+        if not ops.conv.supported(xp, wp, 1):
+            return None
+        y = ops.conv.conv2d_nhwc(xp, wp, bp, s, p, d)
+        return y[..., :co].contiguous() if cop else y
+    wp = TF.pad(w, (0, 0, 0, 0, 0, 0, 0, cp))                        # [C + cp, 1, R, S]
+    bp = None if b is None else TF.pad(b, (0, cp))
+    if not ops.conv.dw_supported(xp, wp, C + cp):
+        return None
+    return ops.conv.dwconv2d_nhwc(xp, wp, bp, s, p, d)[..., :C].contiguous()
 
 
 def _conv3d_depth_taps(t, w, b, s, p, d):

@@ -457,23 +457,30 @@ def stem_ok(x, w, stride, dil):
     """Few-channel forward (the RGB stem) on csrc/conv_stem.hip."""
     Cout, C, R, S = w.shape
     return (_stem_enabled and tuple(dil) == (1, 1) and x.dtype == w.dtype and x.dtype in (torch.bfloat16, torch.float16)
-            and N.lib is not None and bool(N.lib.pa_conv_stem_ok(C, Cout, R, S, stride[0], stride[1])))
+            and N.lib is not None and bool(N.lib.pa_conv_stem_ok(C, -(-Cout // 16) * 16, R, S, stride[0], stride[1])))
 
 
-def conv2d_fwd_stem(x, w, b, stride, pad):
+def conv2d_fwd_stem(x, w, b, stride, pad, stats=True):
     """y = conv(x, w) for C <= 8: the input rows of RB output rows staged once in LDS, MFMA over
     k = (filter row, s*C + c) with the [Cout][Kp] filter image below; under fused_bn_stats() the
-    epilogue also writes the batch-norm slab statistics (one slab per output-row segment)."""
+    epilogue also writes the batch-norm slab statistics (one slab per output-row segment).
+    C_out % 16 != 0 (ShuffleNet's 3 -> 24 stem): computed over zero filter rows up to the 16-channel
+    grain and sliced (no statistics epilogue then)."""
     x = x.contiguous()
     Nb, H, W, C = x.shape
     Cout, _, R, S = w.shape
+    if Cout % 16:
+        c16 = -(-Cout // 16) * 16
+        wp = torch.cat([w, w.new_zeros(c16 - Cout, C, R, S)])
+        bp = None if b is None else torch.cat([b, b.new_zeros(c16 - Cout)])
+        return conv2d_fwd_stem(x, wp, bp, stride, pad, stats=False)[..., :Cout].contiguous()
     Ho, Wo = _out_hw(H, W, R, S, stride, pad, (1, 1))
     RK, Kp = int(N.lib.pa_conv_stem_rk(C, S)), int(N.lib.pa_conv_stem_kp(C, R, S))
     wimg = torch.zeros(-(-Cout // 64) * 64, Kp, dtype=x.dtype, device=x.device)  # rows past Cout stay zero
     wimg[:Cout, :R * RK].view(Cout, R, RK)[:, :, :S * C] = w.detach().to(x.dtype).permute(0, 2, 3, 1).reshape(Cout, R, S * C)
     y = torch.empty(Nb, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
     bb = b.to(x.dtype).contiguous() if b is not None else None
-    rpb = int(N.lib.pa_conv_stem_stat_rows(Wo)) if _want_stats(b) else 0
+    rpb = int(N.lib.pa_conv_stem_stat_rows(Wo)) if stats and _want_stats(b) else 0
     parts = None
     if rpb:
         P = Nb * Ho * (-(-Wo // 128))

@@ -6,6 +6,7 @@ import torch
 
 import paddle
 from paddle.nn.functional import conv as C
+C_ = C
 
 
 def _nhwc_conv2d(x, w, b, s, p, d):
@@ -32,3 +33,31 @@ def test_depth_taps_match_conv3d(monkeypatch, D, k, s, p, dil):
     torch.testing.assert_close(gx, rx)
     torch.testing.assert_close(gw, rw)
     torch.testing.assert_close(gb, rb)
+
+
+def _nhwc_dwconv2d(x, w, b, s, p, d):
+    y = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w, b, s, p, d, groups=x.shape[3])
+    return y.permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize('C,Cout,groups,k,s', [(58, 58, 1, 1, 1), (58, 29, 1, 3, 2), (58, 58, 58, 3, 1),
+                                                (116, 116, 116, 3, 2)])
+def test_cin_padding_matches_conv2d(monkeypatch, C, Cout, groups, k, s):
+    """C_in % 8 != 0 (nn/functional/conv.py _conv_cin_pad): zero channels / zero taps on the padded
+    channels-last copy reproduce torch's conv2d, forward and gradients (torch convs stand in for the
+    HIP kernels)."""
+    monkeypatch.setattr(C_.ops.conv, 'supported', lambda x, w, g: x.shape[3] % 8 == 0 and w.shape[0] % 8 == 0)
+    monkeypatch.setattr(C_.ops.conv, 'dw_supported', lambda x, w, g: x.shape[3] % 8 == 0)
+    monkeypatch.setattr(C_.ops.conv, 'conv2d_nhwc', _nhwc_conv2d)
+    monkeypatch.setattr(C_.ops.conv, 'dwconv2d_nhwc', _nhwc_dwconv2d)
+    torch.manual_seed(C + k)
+    x = torch.randn(2, C, 9, 10, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(Cout, C // groups, k, k, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(Cout, dtype=torch.float64, requires_grad=True)
+    p = k // 2
+    y = C_._conv_cin_pad(x, w, b, (s, s), (p, p), (1, 1), groups).permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv2d(x, w, b, s, p, 1, groups)
+    torch.testing.assert_close(y, ref)
+    g = torch.randn_like(ref)
+    for a, r in zip(torch.autograd.grad(y, (x, w, b), g), torch.autograd.grad(ref, (x, w, b), g)):
+        torch.testing.assert_close(a, r)

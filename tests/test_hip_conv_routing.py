@@ -57,7 +57,11 @@ def test_dwconv_fwd_bwd(dt, N, H, W, C, k, s, p, d, bias):
 @pytest.mark.parametrize('N,H,W,C,Cout,k,s,p', [
     (2, 64, 64, 3, 64, 7, 2, 3), (2, 224, 224, 3, 64, 7, 2, 3), (3, 33, 45, 4, 128, 3, 1, 1),
     (2, 40, 40, 1, 64, 5, 2, 2), (1, 300, 300, 3, 64, 3, 2, 1), (2, 96, 96, 3, 32, 3, 2, 1),
-    (2, 50, 52, 3, 80, 3, 2, 1)])
+    (2, 50, 52, 3, 80, 3, 2, 1),
+    # deep filters on the streamed-filter instantiation: AlexNet's 11x11/4 stem (Kp 448), a 9x9 (Kp 288)
+    (2, 224, 224, 3, 64, 11, 4, 2), (2, 67, 61, 3, 96, 11, 4, 2), (2, 41, 37, 3, 48, 9, 2, 4),
+    # C_out off the 16-channel grain (ShuffleNet v2's 3 -> 24 stem): zero filter rows, sliced output
+    (2, 64, 64, 3, 24, 3, 2, 1), (2, 30, 30, 3, 8, 5, 1, 2)])
 @pytest.mark.parametrize('bias', [False, True])
 def test_conv_stem_fwd(dt, N, H, W, C, Cout, k, s, p, bias):
     from paddle.ops import conv
@@ -74,7 +78,7 @@ def test_conv_stem_fwd(dt, N, H, W, C, Cout, k, s, p, bias):
 
 @pytest.mark.parametrize('N,H,W,C,Cout,k,s,p', [
     (2, 224, 224, 3, 64, 7, 2, 3), (3, 64, 64, 3, 64, 7, 2, 3), (2, 33, 45, 4, 128, 3, 1, 1),
-    (1, 512, 512, 3, 64, 7, 2, 3), (2, 96, 96, 3, 32, 3, 2, 1)])
+    (1, 512, 512, 3, 64, 7, 2, 3), (2, 96, 96, 3, 32, 3, 2, 1), (2, 224, 224, 3, 64, 11, 4, 2)])
 def test_conv_stem_bn_stats(N, H, W, C, Cout, k, s, p):
     """Under fused_bn_stats() the stem epilogue's slab (mean, M2) merge to the batch statistics of
     the fp32 convolution (one slab per output-row segment)."""
@@ -466,6 +470,37 @@ def test_conv_cout_padding(C, Cout, k, p, bias):
     _close(wp.grad._t, wr.grad, 5e-2, 2e-2, 'wgrad')
     if bias:
         _close(bp.grad._t, br.grad, 5e-2, 2e-2, 'bgrad')
+
+
+@pytest.mark.parametrize('C,Cout,k,s,p,groups', [(58, 58, 1, 1, 0, 1), (116, 232, 1, 1, 0, 1), (58, 64, 3, 2, 1, 1),
+                                                  (58, 58, 3, 1, 1, 58), (58, 58, 3, 2, 1, 58), (116, 116, 3, 2, 1, 116)])
+def test_conv_cin_padding(C, Cout, k, s, p, groups):
+    """C_in % 8 != 0 (ShuffleNet v2's 58 / 116-channel branches): plain and depthwise conv2d run on
+    the hand-written kernels over a zero-padded channels-last copy; forward, data / filter / bias
+    gradients vs fp32 torch, no library convolution kernel."""
+    F = paddle.nn.functional
+    x = torch.randn(2, C, 14, 13, device=DEV).bfloat16()
+    w = (0.1 * torch.randn(Cout, C // groups, k, k, device=DEV)).bfloat16()
+    b = torch.randn(Cout, device=DEV).bfloat16()
+    xr, wr, br = (v.float().requires_grad_() for v in (x, w, b))
+    yr = torch.nn.functional.conv2d(xr, wr, br, s, p, 1, groups)
+    g = torch.randn_like(yr)
+    xp, wp, bp = (paddle.to_tensor(v, stop_gradient=False) for v in (x, w, b))
+    out = []
+
+    def run():
+        y = F.conv2d(xp, wp, bp, s, p, groups=groups)
+        y.backward(paddle.to_tensor(g.bfloat16()))
+        out.append(y)
+    bad = _miopen_kernels(run)
+    assert bad == [], bad
+    yr.backward(g)
+    y = out[0]._t
+    assert tuple(y.shape) == tuple(yr.shape)
+    _close(y, yr, 3e-2, 1e-2, 'fwd')
+    _close(xp.grad._t, xr.grad, 3e-2, 1e-2, 'dgrad')
+    _close(wp.grad._t, wr.grad, 5e-2, 2e-2, 'wgrad')
+    _close(bp.grad._t, br.grad, 5e-2, 2e-2, 'bgrad')
 
 
 @pytest.mark.parametrize('C,Cout,D,k,s,p,fmt', [(32, 64, 8, 3, 1, 1, 'NCDHW'), (64, 32, 9, 3, 2, 1, 'NCDHW'),

@@ -26,7 +26,10 @@ def main():
              ('vgg16', 224), ('alexnet', 224), ('mobilenet_v1', 224), ('mobilenet_v2', 224),
              ('mobilenet_v3_small', 224), ('mobilenet_v3_large', 224), ('shufflenet_v2_x1_0', 224),
              ('squeezenet1_1', 224), ('densenet121', 224), ('googlenet', 224), ('inception_v3', 299)]
+    only = set(sys.argv[1:])
     for name, hw in cases:
+        if only and name not in only:
+            continue
         if not hasattr(M, name):
             print(f'{name:22s} (not in paddle.vision.models)', flush=True)
             continue
