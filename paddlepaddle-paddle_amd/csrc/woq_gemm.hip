@@ -5,7 +5,8 @@
 // Reference semantics: paddle/phi/kernels/gpu/weight_only_linear_kernel.cu (CUTLASS fpA_intB GEMV /
 // GEMM), python/paddle/nn/quant/quantized_linear.py:151 weight_only_linear, with this framework's
 // weight layout (nn/quant/quantized_linear.py weight_quantize): int8 [N][K] (k contiguous), int4
-// packed two signed nibbles per byte along k ([N][K/2], low nibble = even k), symmetric scales per
+// packed two signed nibbles per byte along k ([N][K/2]; per 8 k: byte b = k b low nibble, k 4 + b high
+// nibble), symmetric scales per
 // output channel ([N]) or per k-group of 64 / 128 ([K/G][N]).
 //
 // CDNA4 design (the k-major path of skinny_gemm.hip, widened per byte):
@@ -18,11 +19,12 @@
 //    activation fragment of step s is X[m][k0 + 16g + 8s .. +8] (int8) / X[m][k0 + 32g + 8s ..]
 //    (int4) — 16-B loads of contiguous bf16, no shuffles.  Every k appears exactly once, so the
 //    dot products are exact sums in a different order.
-//  * Dequant: a byte u (int8 xor 0x80, int4 nibble xor 0x8) becomes the fp32 2^23 + u with one
-//    v_perm_b32 (exponent byte 0x4B, two zero bytes, u), minus (2^23 + 128 / 8) gives the signed
-//    integer exactly; bf16 holds every integer |v| <= 256 exactly, so per-channel scales are applied
-//    to the fp32 accumulator at the end (no per-element multiply); group scales multiply in fp32
-//    before the bf16 pack.
+//  * Dequant, group scales: a byte u (int8 xor 0x80, int4 nibble xor 0x8) becomes the fp32 2^23 + u
+//    with one v_perm_b32 (exponent byte 0x4B, two zero bytes, u), minus (2^23 + 128 / 8) gives the
+//    signed integer exactly; the group scale multiplies in fp32 before the 16-bit pack.  Per-channel
+//    scales: the MFMA runs on unsigned codes held exactly in 16 bits (frag_u8 / frag_u4, the
+//    constant offset removed in the epilogue with per-row sums of X) and the scale is applied to
+//    the fp32 accumulator at the end.
 //  * Up to 2 row tiles of 16 (M <= 32) share each dequantised fragment; NST register stages keep the
 //    next chunks' weight loads in flight (all loads unconditional, so the waits are counted); the 4 waves of a block split its K range and are summed
 //    through LDS; K splits across blocks go to an fp32 partial buffer summed by the finish kernel
@@ -67,6 +69,24 @@ __device__ __forceinline__ unsigned pack2(float a, float b) {
     return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
 }
 
+// acc + the sum of the 8 16-bit values of a fragment: 4 v_dot2c_f32_{bf16,f16} against (1, 1)
+template <typename T>
+__device__ __forceinline__ float rowsum8(s16x8 f, float acc) {
+  const uint4 u = __builtin_bit_cast(uint4, f);
+  const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if constexpr (__is_same(T, f16_t)) {
+      const f16x2 one = {(_Float16)1.f, (_Float16)1.f};
+      acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, w[j]), one, acc, false);
+    } else {
+      const bf16x2 one = {(__bf16)1.f, (__bf16)1.f};
+      acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, w[j]), one, acc, false);
+    }
+  }
+  return acc;
+}
+
 // 8 signed values (exact integers, or * s when SCALE) of one MFMA fragment.
 // int8: bytes q[0..7] of the two dwords lo, hi (k order = byte order).
 template <typename T, bool SCALE>
@@ -88,17 +108,17 @@ __device__ __forceinline__ s16x8 frag_i8(unsigned lo, unsigned hi, float s) {
                                               pack2<T>(v[6], v[7])));
 }
 
-// int4: one dword = 8 nibbles, k = 2b (low nibble of byte b), 2b + 1 (high nibble)
+// int4: one dword = 8 nibbles, k = b (low nibble of byte b), 4 + b (high nibble)
 template <typename T, bool SCALE>
 __device__ __forceinline__ s16x8 frag_i4(unsigned d, float s) {
-  const unsigned ev = (d & 0x0F0F0F0Fu) ^ 0x08080808u;         // k = 0, 2, 4, 6
-  const unsigned od = ((d >> 4) & 0x0F0F0F0Fu) ^ 0x08080808u;  // k = 1, 3, 5, 7
+  const unsigned lo = (d & 0x0F0F0F0Fu) ^ 0x08080808u;         // k = 0, 1, 2, 3
+  const unsigned hi = ((d >> 4) & 0x0F0F0F0Fu) ^ 0x08080808u;  // k = 4, 5, 6, 7
   constexpr float off = 8388608.0f + 8.0f;
   float v[8];
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
-    v[2 * b] = magic(ev, b) - off;
-    v[2 * b + 1] = magic(od, b) - off;
+    v[b] = magic(lo, b) - off;
+    v[4 + b] = magic(hi, b) - off;
   }
   if constexpr (SCALE) {
 #pragma unroll
@@ -118,6 +138,14 @@ template <typename T>
 __device__ __forceinline__ s16x8 frag_u8(unsigned lo, unsigned hi) {
   lo ^= 0x80808080u;  // two's-complement byte q -> unsigned code q + 128
   hi ^= 0x80808080u;
+  if constexpr (__is_same(T, f16_t)) {
+    // fp16 holds 1024 + u exactly (10 mantissa bits): one byte permute per pair, as frag_u4
+    constexpr unsigned E = 0x64646464u;
+    return __builtin_bit_cast(s16x8, make_uint4(__builtin_amdgcn_perm(E, lo, 0x04010400u),
+                                                __builtin_amdgcn_perm(E, lo, 0x04030402u),
+                                                __builtin_amdgcn_perm(E, hi, 0x04010400u),
+                                                __builtin_amdgcn_perm(E, hi, 0x04030402u)));
+  }
   float v[8];
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
@@ -128,18 +156,23 @@ __device__ __forceinline__ s16x8 frag_u8(unsigned lo, unsigned hi) {
                                               pack2<T>(v[6], v[7])));
 }
 
+// int4, per-channel scale: the byte codes u = q + 8 (0..15) of a dword's low nibbles (k 0..3) and
+// high nibbles (k 4..7) become 16-bit operands with ONE v_perm_b32 per pair: each code is placed
+// under a constant exponent byte — bf16 0x43:u = 128 + u (exact, 7 mantissa bits), fp16 0x64:u =
+// 1024 + u — so 8 values cost 4 extract + 4 permute VALU (was 16 with byte -> float -> pack).  The
+// constant comes back out in the epilogue with the row sums: y = s * (sum x v - off * sum x),
+// off = 136 (bf16) / 1032 (fp16).
 template <typename T>
 __device__ __forceinline__ s16x8 frag_u4(unsigned d) {
-  const unsigned ev = (d & 0x0F0F0F0Fu) ^ 0x08080808u;         // k = 0, 2, 4, 6 (code q + 8)
-  const unsigned od = ((d >> 4) & 0x0F0F0F0Fu) ^ 0x08080808u;  // k = 1, 3, 5, 7
-  float v[8];
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    v[2 * b] = (float)((ev >> (8 * b)) & 0xFFu);
-    v[2 * b + 1] = (float)((od >> (8 * b)) & 0xFFu);
-  }
-  return __builtin_bit_cast(s16x8, make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
-                                              pack2<T>(v[6], v[7])));
+  const unsigned t = d ^ 0x88888888u;                 // two's-complement nibble q -> code q + 8
+  const unsigned lo = t & 0x0F0F0F0Fu;                // k = 0, 1, 2, 3
+  const unsigned hi = (t >> 4) & 0x0F0F0F0Fu;         // k = 4, 5, 6, 7
+  constexpr unsigned E = __is_same(T, f16_t) ? 0x64646464u : 0x43434343u;
+  // v_perm_b32(src0 = E, src1 = x, sel): selector 0..3 = byte of x, 4 = the exponent byte
+  return __builtin_bit_cast(s16x8, make_uint4(__builtin_amdgcn_perm(E, lo, 0x04010400u),
+                                              __builtin_amdgcn_perm(E, lo, 0x04030402u),
+                                              __builtin_amdgcn_perm(E, hi, 0x04010400u),
+                                              __builtin_amdgcn_perm(E, hi, 0x04030402u)));
 }
 
 // grid (ceil(N / 128), KS), 256 threads.  part: fp32 [KS][M][N].  BITS 8 / 4; G = group size (0 =
@@ -149,7 +182,8 @@ __global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X
                                                   const uint8_t* __restrict__ Wq, long long ldw_bytes,
                                                   const float* __restrict__ gscale, int group,
                                                   float* __restrict__ part, int M, int N, int K, int kchunk,
-                                                  float* __restrict__ xsum) {
+                                                  float* __restrict__ xsum, uint16_t* __restrict__ Y, long long ldy,
+                                                  const uint16_t* __restrict__ bias, float off) {
   constexpr int KC = BITS == 8 ? 64 : 128;  // k per chunk
   constexpr int NS = KC / 32;                // MFMA steps per chunk
   __shared__ float red[3][MT * CT * 4][64];
@@ -201,15 +235,15 @@ __global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X
   float xs[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) xs[t] = 0.f;
-  const bool want_xs = !GRP && blockIdx.x == 0;
+  // fused epilogue (Y != null, the K range is not split across blocks): every block needs its rows'
+  // sums for the offset correction
+  const bool want_xs = !GRP && (Y != nullptr || blockIdx.x == 0);
   auto compute = [&](int st) {
     if (!GRP && want_xs) {
 #pragma unroll
       for (int t = 0; t < MT; ++t)
 #pragma unroll
-        for (int s = 0; s < NS; ++s)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) xs[t] += to_f(__builtin_bit_cast(T, (uint16_t)rx[st][t][s][e]));
+        for (int s = 0; s < NS; ++s) xs[t] = rowsum8<T>(rx[st][t][s], xs[t]);
     }
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
@@ -274,6 +308,28 @@ __global__ __launch_bounds__(256) void woq_kernel(const uint16_t* __restrict__ X
       for (int r = 0; r < 4; ++r)
         acc[t][c][r] += red[0][(t * CT + c) * 4 + r][lane] + red[1][(t * CT + c) * 4 + r][lane] +
                         red[2][(t * CT + c) * 4 + r][lane];
+  if (Y != nullptr) {
+    // fused finish (one K split): y = (acc - off * rowsum) * cscale + bias, straight to Y; the lane
+    // holds C[m = 16t + 4g + r][column n0 + 16c + i]
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * t + 4 * g + r;
+        if (m >= M) continue;
+        const float xr = GRP ? 0.f : xred[0][m] + xred[1][m] + xred[2][m] + xred[3][m];
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          const int col = n0 + 16 * c + i;
+          if (col >= N) continue;
+          float v = acc[t][c][r];
+          if constexpr (!GRP) v = (v - off * xr) * gscale[col];
+          if (bias != nullptr) v += to_f(__builtin_bit_cast(T, bias[col]));
+          Y[(long long)m * ldy + col] = __builtin_bit_cast(uint16_t, from_f<T>(v));
+        }
+      }
+    return;
+  }
   if (want_xs && lane < MT * 16 && lane < M) {
     xsum[(long long)blockIdx.y * M + lane] = xred[0][lane] + xred[1][lane] + xred[2][lane] + xred[3][lane];
   }
@@ -337,21 +393,32 @@ __global__ __launch_bounds__(256) void woq_finish(const float* __restrict__ part
 // blocks at M <= 16; for the M <= 32 kernel ~256 blocks on wide outputs (>= 100 column tiles), ~512 on
 // narrow ones; g_target_blocks > 0 overrides)
 static int g_target_blocks = 0, g_nst = 2;
+// A/B switch (pa_woq_set_fused_finish): single-split launches finish in the main kernel (default on)
+static int g_fused_finish = 1;
 
 // K splits: ~g_target_blocks blocks over the 128-column tiles; each split a multiple of 4 waves x chunk
 // 16-column tiles per wave of the M <= 16 kernel (8 = 128 columns per block, 4 = 64, 2 = 32): narrower
 // tiles mean fewer registers per wave, more waves and more independent dequant chains in flight.
 // Automatic (g_ct = 0): 2 at M <= 4, 4 at M <= 16 — graph-timed on the Llama-2-13B shapes, M = 1
 // int8 1.38-1.60x / int4 1.50-2.07x the bf16 skinny GEMM (profiles/r4q_woq_sweep.log).
+// Since the single-split launches finish in the main kernel (no finish pass), the sweep after the
+// byte-permute int4 dequant (profiles/r5v_woq_sweep.log) favours one K split with 32-column waves
+// wherever that still gives >= 128 blocks: M <= 4 always (ffn2 K = 13824: int8 21.5 -> 18.5 us, int4
+// 15.0 -> 12.4); 5 <= M <= 16 unless the output is wide (N >= 16384) or deep (K > 2N), where 64-column
+// waves split over ~256 blocks stay ahead (ffn1 25.9 vs 33.3 us int4).
 static int g_ct = 0;
-static int eff_ct(int M) { return M > 16 ? 8 : (g_ct ? g_ct : (M <= 4 ? 2 : 4)); }
+static bool wide_or_deep(int N, int K) { return N >= 16384 || K > 2 * N; }
+static int eff_ct(int M, int N, int K) {
+  return M > 16 ? 8 : (g_ct ? g_ct : (M <= 4 || !wide_or_deep(N, K) ? 2 : 4));
+}
 
 static void plan(int N, int K, int bits, int M, int& KS, int& kchunk) {
   const int unit = 4 * (bits == 8 ? 64 : 128);
-  const int ct = eff_ct(M);
+  const int ct = eff_ct(M, N, K);
   const int tiles = (N + 16 * ct - 1) / (16 * ct);
-  const int target = g_target_blocks > 0 ? g_target_blocks
-                                          : (M <= 4 ? (K > 8192 ? 512 : 128) : (M <= 16 || tiles >= 100 ? 256 : 512));
+  const int target = g_target_blocks > 0
+                         ? g_target_blocks
+                         : (M <= 4 || (M <= 16 && !wide_or_deep(N, K)) ? 128 : (M <= 16 || tiles >= 100 ? 256 : 512));
   int ks = (target + tiles - 1) / tiles;
   const int kmax = (K + unit - 1) / unit;
   ks = ks < 1 ? 1 : (ks > kmax ? kmax : ks);
@@ -361,28 +428,29 @@ static void plan(int N, int K, int bits, int M, int& KS, int& kchunk) {
 
 template <typename T, int BITS, bool GRP>
 static void launch(const void* X, long long ldx, const void* Wq, long long ldwb, const float* gscale, int group,
-                   float* ws, int M, int N, int K, int KS, int kchunk, float* xsum, hipStream_t st) {
-  const dim3 grid((N + 16 * eff_ct(M) - 1) / (16 * eff_ct(M)), KS);
+                   float* ws, int M, int N, int K, int KS, int kchunk, float* xsum, uint16_t* Y, long long ldy,
+                   const uint16_t* bias, float off, hipStream_t st) {
+  const dim3 grid((N + 16 * eff_ct(M, N, K) - 1) / (16 * eff_ct(M, N, K)), KS);
   const uint16_t* x = (const uint16_t*)X;
   const uint8_t* w = (const uint8_t*)Wq;
   // (a 4-row-tile variant for M <= 64 spills at 256 VGPRs: M > 32 takes the dequantise + GEMM path)
-  const int ct = eff_ct(M);
+  const int ct = eff_ct(M, N, K);
   if (M <= 16 && ct == 2)
-    woq_kernel<T, BITS, 1, 2, GRP, 2><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
+    woq_kernel<T, BITS, 1, 2, GRP, 2><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum, Y, ldy, bias, off);
   else if (M <= 16 && ct == 4 && g_nst == 4)
-    woq_kernel<T, BITS, 1, 4, GRP, 4><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
+    woq_kernel<T, BITS, 1, 4, GRP, 4><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum, Y, ldy, bias, off);
   else if (M <= 16 && ct == 4 && g_nst == 3)
-    woq_kernel<T, BITS, 1, 3, GRP, 4><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
+    woq_kernel<T, BITS, 1, 3, GRP, 4><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum, Y, ldy, bias, off);
   else if (M <= 16 && ct == 4)
-    woq_kernel<T, BITS, 1, 2, GRP, 4><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
+    woq_kernel<T, BITS, 1, 2, GRP, 4><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum, Y, ldy, bias, off);
   else if (M <= 16 && g_nst == 2)
-    woq_kernel<T, BITS, 1, 2, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
+    woq_kernel<T, BITS, 1, 2, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum, Y, ldy, bias, off);
   else if (M <= 16 && g_nst == 4)
-    woq_kernel<T, BITS, 1, 4, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
+    woq_kernel<T, BITS, 1, 4, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum, Y, ldy, bias, off);
   else if (M <= 16)
-    woq_kernel<T, BITS, 1, 3, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
+    woq_kernel<T, BITS, 1, 3, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum, Y, ldy, bias, off);
   else
-    woq_kernel<T, BITS, 2, 2, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum);
+    woq_kernel<T, BITS, 2, 2, GRP><<<grid, 256, 0, st>>>(x, ldx, w, ldwb, gscale, group, ws, M, N, K, kchunk, xsum, Y, ldy, bias, off);
 }
 
 }  // namespace woq
@@ -420,6 +488,12 @@ PA_API int pa_woq_set_ct(int ct) {
   return old;
 }
 
+PA_API int pa_woq_set_fused_finish(int on) {
+  const int old = pa::woq::g_fused_finish;
+  if (on >= 0) pa::woq::g_fused_finish = on ? 1 : 0;
+  return old;
+}
+
 PA_API long long pa_woq_ws_floats(int M, int N, int K, int bits) {
   int KS, kc;
   pa::woq::plan(N, K, bits, M, KS, kc);
@@ -436,17 +510,25 @@ PA_API int pa_woq_gemm(const void* X, const void* Wq, const float* scale, const 
   plan(N, K, bits, M, KS, kchunk);
   const bool grp = group != 0;
   float* xsum = ws + (long long)KS * M * N;
+  // one K split: the main kernel finishes the tile itself (scale, offset, bias, 16-bit store)
+  const bool fused = KS == 1 && g_fused_finish;
+  uint16_t* Yf = fused ? (uint16_t*)Y : nullptr;
+  const uint16_t* bf = fused ? (const uint16_t*)bias : nullptr;
+  // unsigned-code offsets of the per-channel paths (frag_u8: u = q + 128; frag_u4: 128 + q + 8 /
+  // 1024 + q + 8)
+  const float off = bits == 8 ? (dt == 1 ? 128.f : 1152.f) : (dt == 1 ? 136.f : 1032.f);
 #define WOQ_DISPATCH(T)                                                                                        \
   do {                                                                                                         \
-    if (bits == 8 && grp) launch<T, 8, true>(X, ldx, Wq, ldw_bytes, scale, group, ws, M, N, K, KS, kchunk, xsum, st); \
-    else if (bits == 8) launch<T, 8, false>(X, ldx, Wq, ldw_bytes, scale, 0, ws, M, N, K, KS, kchunk, xsum, st);      \
-    else if (grp) launch<T, 4, true>(X, ldx, Wq, ldw_bytes, scale, group, ws, M, N, K, KS, kchunk, xsum, st);         \
-    else launch<T, 4, false>(X, ldx, Wq, ldw_bytes, scale, 0, ws, M, N, K, KS, kchunk, xsum, st);                     \
+    if (bits == 8 && grp) launch<T, 8, true>(X, ldx, Wq, ldw_bytes, scale, group, ws, M, N, K, KS, kchunk, xsum, Yf, ldy, bf, off, st); \
+    else if (bits == 8) launch<T, 8, false>(X, ldx, Wq, ldw_bytes, scale, 0, ws, M, N, K, KS, kchunk, xsum, Yf, ldy, bf, off, st);      \
+    else if (grp) launch<T, 4, true>(X, ldx, Wq, ldw_bytes, scale, group, ws, M, N, K, KS, kchunk, xsum, Yf, ldy, bf, off, st);         \
+    else launch<T, 4, false>(X, ldx, Wq, ldw_bytes, scale, 0, ws, M, N, K, KS, kchunk, xsum, Yf, ldy, bf, off, st);                     \
+    if (fused) break;                                                                                          \
     const long long groups = ((long long)M * N + 7) / 8;                                                       \
     woq_finish<T><<<(unsigned)((groups + 255) / 256), 256, 0, st>>>(ws, KS, M, N, grp ? nullptr : scale,       \
                                                                      (const uint16_t*)bias, (uint16_t*)Y, ldy,  \
                                                                      grp ? nullptr : xsum,                      \
-                                                                     bits == 8 ? 128.f : 8.f);                  \
+                                                                     off);                                      \
   } while (0)
   if (dt == 1) WOQ_DISPATCH(pa::bf16_t);
   else WOQ_DISPATCH(pa::f16_t);

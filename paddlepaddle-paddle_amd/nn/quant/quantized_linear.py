@@ -3,7 +3,7 @@ python/paddle/nn/quant/quantized_linear.py).
 
 Layout (ours, documented; the reference's is a CUTLASS-arch-specific interleave): a [k, n] float
 weight quantises to int8 ``[n, k]`` (k contiguous) — int4 packs two signed nibbles per byte along
-k into ``[n, k // 2]`` (low nibble = even k) — with symmetric absmax scales: per output channel
+k into ``[n, k // 2]`` (per 8 k: byte b = k b low nibble, k 4 + b high nibble) — with symmetric absmax scales: per output channel
 ``[n]`` (group_size -1) or per k-group ``[k // group_size, n]``.  ``arch`` is accepted for API
 compatibility (the MI355X path does not depend on it).  On the GPU, decode-shaped calls (<= 32 token
 rows, bf16 / fp16) run the weight-only kernel csrc/woq_gemm.hip (quantised weight streamed once,
@@ -46,11 +46,13 @@ def weight_quantize(x, algo="weight_only_int8", arch=None, group_size=-1):
         q = torch.round(wg / scale[:, None, :]).clamp(-qm, qm).reshape(k, n)
     q = q.to(torch.int8).t().contiguous()                                   # [n, k]
     if algo == 'weight_only_int4':
-        if k % 2:
-            raise ValueError("int4 packing needs an even k")
-        lo = q[:, 0::2].to(torch.int16) & 0xF
-        hi = q[:, 1::2].to(torch.int16) & 0xF
-        q = (lo | (hi << 4)).to(torch.uint8).view(torch.int8)               # [n, k/2]
+        if k % 8:
+            raise ValueError("int4 packing needs k % 8 == 0")
+        # per 8 consecutive k (one 32-bit word): byte b holds k 8w + b (low nibble) and 8w + 4 + b
+        # (high nibble) — the decode kernel turns a word's low / high nibbles into two 4-element runs
+        # of MFMA operand with one byte permute per pair (csrc/woq_gemm.hip frag_u4)
+        q8 = q.to(torch.int16).reshape(n, k // 8, 2, 4) & 0xF
+        q = (q8[:, :, 0] | (q8[:, :, 1] << 4)).reshape(n, k // 2).to(torch.uint8).view(torch.int8)  # [n, k/2]
     return _w(q), _w(scale.float())
 
 
@@ -62,7 +64,8 @@ def _unpack(q, algo):
     lo, hi = b & 0xF, (b >> 4) & 0xF
     lo = torch.where(lo > 7, lo - 16, lo)
     hi = torch.where(hi > 7, hi - 16, hi)
-    return torch.stack([lo, hi], -1).reshape(q.shape[0], -1).float()        # [n, k]
+    n = q.shape[0]
+    return torch.stack([lo.reshape(n, -1, 4), hi.reshape(n, -1, 4)], 2).reshape(n, -1).float()  # [n, k]
 
 
 def _dequant(q, scale, algo, group_size):

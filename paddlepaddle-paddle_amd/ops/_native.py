@@ -88,6 +88,7 @@ _SIGS = {
     'pa_fp8_set_cast_full': [I],
     'pa_woq_tune': [I, I],
     'pa_woq_set_ct': [I],
+    'pa_woq_set_fused_finish': [I],
     'pa_gemm_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
     'pa_gemm8_fp8_ok': [I, I, I, LL, LL, LL],
     'pa_gemm8_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],

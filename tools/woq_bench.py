@@ -52,11 +52,15 @@ def main():
             x = torch.randn(M, K, device=dev).bfloat16()
             tb = bench(lambda: gemm.skinny_mm(x, wb))
             tl = bench(lambda: torch.mm(x, wb))
-            t8 = bench(lambda: woq.woq_linear(x, q8, s8, 8, 0))
-            t4 = bench(lambda: woq.woq_linear(x, q4, s4, 4, 0))
-            print(f"{name:5s} K={K:5d} N={N:5d} M={M:2d}: bf16 skinny {tb*1e6:7.1f} us ({K*N*2/tb/1e12:4.2f} TB/s) | "
-                  f"library {tl*1e6:7.1f} | int8 {t8*1e6:7.1f} us ({K*N/t8/1e12:4.2f} TB/s, {tb/t8:4.2f}x) | "
-                  f"int4 {t4*1e6:7.1f} us ({K*N/2/t4/1e12:4.2f} TB/s, {tb/t4:4.2f}x)", flush=True)
+            for fused in ((1, 0) if os.environ.get('WOQ_FUSED_AB') == '1' else (1,)):
+                _native.lib.pa_woq_set_fused_finish(fused)
+                t8 = bench(lambda: woq.woq_linear(x, q8, s8, 8, 0))
+                t4 = bench(lambda: woq.woq_linear(x, q4, s4, 4, 0))
+                tag = '' if os.environ.get('WOQ_FUSED_AB') != '1' else (' [fused finish]' if fused else ' [finish kernel]')
+                print(f"{name:5s} K={K:5d} N={N:5d} M={M:2d}: bf16 skinny {tb*1e6:7.1f} us ({K*N*2/tb/1e12:4.2f} TB/s) | "
+                      f"library {tl*1e6:7.1f} | int8 {t8*1e6:7.1f} us ({K*N/t8/1e12:4.2f} TB/s, {tb/t8:4.2f}x) | "
+                      f"int4 {t4*1e6:7.1f} us ({K*N/2/t4/1e12:4.2f} TB/s, {tb/t4:4.2f}x){tag}", flush=True)
+            _native.lib.pa_woq_set_fused_finish(1)
 
 
 def sweep():
