@@ -218,6 +218,33 @@ PA_API int pa_gemm8_bf16_epi(const void* A, const void* B, void* C, const void* 
   return (int)hipErrorInvalidValue;
 }
 
+// Inference epilogues: C = act(alpha * A @ B + bias) with act 6 relu, 7 gelu (erf), 8 gelu (tanh) in
+// the wave-staged epilogue of schedule 11; no aux output (imported programs' fc_fuse_pass).
+PA_API int pa_gemm8_bf16_act(const void* A, const void* B, void* C, const void* bias, int M, int N, int K,
+                             long long lda, long long ldb, long long ldc, int transB, float alpha, int act,
+                             hipStream_t st) {
+  using namespace pa::g8;
+  if (!pa_gemm8_ok(M, N, K, lda, ldb, ldc, 0, transB, 1) || act < 6 || act > 8) return (int)hipErrorInvalidValue;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  dim3 grid(tm * tn, 1, 1);
+#define PA_G8_ACT(E)                                                                                                \
+  do {                                                                                                             \
+    if (transB)                                                                                                    \
+      gemm11_kernel<true, true, E + 200><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C,        \
+                                                               nullptr, (const uint16_t*)bias, M, N, K, lda, ldb,  \
+                                                               ldc, alpha, 0.f, K);                                \
+    else                                                                                                           \
+      gemm11_kernel<true, false, E + 200><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C,       \
+                                                                nullptr, (const uint16_t*)bias, M, N, K, lda, ldb, \
+                                                                ldc, alpha, 0.f, K);                               \
+  } while (0)
+  if (act == 6) PA_G8_ACT(6);
+  else if (act == 7) PA_G8_ACT(7);
+  else PA_G8_ACT(8);
+#undef PA_G8_ACT
+  return (int)hipGetLastError();
+}
+
 // Two weight gradients in one launch (schedule 9, both operands m/n-contiguous as the Linear
 // weight gradient reads them: A = X^T [K][M], B = dY [K][N]), C_i = alpha * A_i @ B_i + beta * C_i,
 // shared K.  Returns hipErrorInvalidValue outside the kernel contract.

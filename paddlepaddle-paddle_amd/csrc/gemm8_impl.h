@@ -631,7 +631,10 @@ __device__ __forceinline__ void epilogue_wstaged(const f32x4 (&acc)[8][4], uint1
                                                  float* __restrict__ ws, const uint16_t* __restrict__ bias, int M,
                                                  int N, long long ldc, float alpha, float beta, int mb, int nb,
                                                  int lane, lds_char* region) {
-  static_assert(EPI == 0 || EPI == 2 || EPI == 3 || EPI == 4 || EPI == 5, "staged epilogue: EPI 0/2/3/4/5");
+  // EPI 6 / 7 / 8: inference activations after the bias (relu / gelu erf / gelu tanh), no aux
+  // output — the fc_fuse_pass epilogue of imported programs (static/ir_passes.py fused_linear)
+  static_assert(EPI == 0 || EPI == 2 || EPI == 3 || EPI == 4 || EPI == 5 || EPI == 6 || EPI == 7 || EPI == 8,
+                "staged epilogue: EPI 0/2/3/4/5/6/7/8");
   const int g = lane >> 4;
   const bool upper = (g & 1) != 0;
   constexpr bool AUX_IN = EPI == 3 || EPI == 4;
@@ -706,6 +709,20 @@ __device__ __forceinline__ void epilogue_wstaged(const f32x4 (&acc)[8][4], uint1
               d[e + 1] = dv.y;
             }
             *(lds_u32x4*)(reg_a + wtile(r, ch)) = pack_bf16x8(d);
+          } else if constexpr (EPI == 6) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+          } else if constexpr (EPI == 7) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+          } else if constexpr (EPI == 8) {
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+              f32x2_t fv, dv;
+              gelu_tanh_fdf2(f32x2_t{v[e], v[e + 1]}, fv, dv);
+              v[e] = fv.x;
+              v[e + 1] = fv.y;
+            }
           } else if (old_in) {
             const Pack<OT, 8> ov = __builtin_bit_cast(Pack<OT, 8>, *(const lds_u32x4*)slot);
 #pragma unroll

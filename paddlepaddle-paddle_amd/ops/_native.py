@@ -141,6 +141,7 @@ _SIGS = {
     'pa_bn_tune': [I],
     'pa_colsum_finish_parts': [P, P, I, I, I, I, P],
     'pa_gemm8_bf16_epi': [P, P, P, P, P, I, I, I, LL, LL, LL, I, F, I, P],
+    'pa_gemm8_bf16_act': [P, P, P, P, I, I, I, LL, LL, LL, I, F, I, P],
     'pa_gemm8_wgrad_grouped2': [P, P, P, I, I, LL, LL, LL, P, P, P, I, I, LL, LL, LL, I, F, F, P],
     'pa_gemm_bf16': [P, P, P, P, P, I, I, I, LL, LL, LL, I, I, F, F, I, P],
     'pa_flash_fwd_ex': [P, P, P, P, P, I, I, I, I, I, I, LLP, LLP, LLP, LLP, F, I, I, P, P, I, P, LL, LL, LL, I, F,

@@ -73,9 +73,9 @@ def _ds_ws(B, Hq, Sq, Sk, dtype, device):
 
 def _bwd_call(q, k, v, o, do, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, D, scale, causal, cu_q=None, cu_k=None,
               total=0, m=None, mb=0, mh=0, mq=0, mf=0, p_drop=0.0, seed=0, rows=None, rb=0, rh=0, ex=False):
-    mall = _mask_all(m, mh, mq)
     """The backward launch sequence: dS path when enabled, else the recompute kernels
     (pa_flash_bwd, or pa_flash_bwd_ex when any extended feature is in use)."""
+    mall = _mask_all(m, mh, mq)
     st = (N.strides3(q), N.strides3(k), N.strides3(v), N.strides3(o), N.strides3(do), N.strides3(dq),
           N.strides3(dk), N.strides3(dv))
     ws = _ds_ws(B, Hq, Sq, Sk, q.dtype, q.device) if _ds_ok(D, q.dtype) else None

@@ -105,6 +105,24 @@ def mm_epi(a, b, epi, aux, bias=None, out=None, colsum_part=None):
     return out
 
 
+_ACT_EPI = {'relu': 6, 'gelu': 7, 'gelu_tanh': 8}
+
+
+def mm_act(a, b, bias, act):
+    """act(a @ b + bias) with the bias and the activation (relu / gelu erf / gelu tanh) in the
+    GEMM's wave-staged epilogue (csrc/gemm8.hip pa_gemm8_bf16_act) — the inference fc_fuse_pass
+    form: no derivative output, no separate activation pass.  a: [M, K] k-contiguous bf16; b: [K, N]
+    (row-major or a transposed view of [N, K]); contract: ``epi_ok(a, b, N)``."""
+    tb, ldb = _op_layout(b)
+    M, K = a.shape
+    N_ = b.shape[1]
+    out = torch.empty(M, N_, dtype=torch.bfloat16, device=a.device)
+    bb = None if bias is None else bias.to(torch.bfloat16).contiguous()
+    N.check(N.lib.pa_gemm8_bf16_act(N.ptr(a), N.ptr(b), N.ptr(out), N.ptr(bb), M, N_, K, a.stride(0), ldb, N_, tb,
+                                    1.0, _ACT_EPI[act], N.stream()), f'gemm_act_{act}')
+    return out
+
+
 def mm_bn_stats(a, b):
     """out = a @ b on the fused-epilogue GEMM (epi 5) plus the batch-norm column statistics of
     every 128-row slab of out: returns (out, parts fp32 [2][P][N] (slab means, then M2s), P)."""

@@ -179,15 +179,20 @@ _ACT = {None: None, 'relu': torch.relu, 'gelu': lambda t: TF.gelu(t), 'gelu_tanh
 
 def fused_linear(x, w, bias=None, act=None, trans_w=False):
     """act(x @ W + bias) (W [in, out], or [out, in] with ``trans_w``): the GEMM on the hand-written
-    kernel (ops/matmul.py routing) with the bias in its epilogue, the activation in one pass over
-    the output (csrc/act.hip); composite otherwise."""
+    kernel (ops/matmul.py routing) with the bias in its epilogue; bf16 inputs of >= 1024 rows also
+    take the activation in the epilogue (ops.gemm.mm_act), others run it as one pass over the
+    output (csrc/act.hip); composite otherwise."""
     from ..ops import matmul as hm
     W = w.t() if trans_w else w
     if act in (None, 'relu', 'gelu', 'gelu_tanh') and _hip(x) and x.dtype in (torch.bfloat16, torch.float16) \
             and W.dtype == x.dtype and (bias is None or bias.dtype == x.dtype):
-        from ..ops import act as A
+        from ..ops import act as A, gemm as G
         if act is None:
             return hm.linear(x, W, bias)
+        x2 = x.reshape(-1, x.shape[-1])
+        if (x.dtype == torch.bfloat16 and x2.shape[0] >= 1024 and not torch.is_grad_enabled()
+                and G.epi_ok(x2, W, W.shape[1])):
+            return G.mm_act(x2, W, bias, act).reshape(*x.shape[:-1], W.shape[1])
         y = hm.linear(x, W, None)
         if act == 'relu':
             return A.bias_relu(y, bias)

@@ -380,3 +380,23 @@ def test_persistent_schedule_staged_epilogue_matches(M, K, N, kmaj, beta, bias):
     ref = a.float() @ b.float() + (beta * init.float()) + (bb.float() if bias else 0.0)
     _close(outs[1], ref, 2e-2, 'sched12')
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('act', ['relu', 'gelu', 'gelu_tanh'])
+@pytest.mark.parametrize('M,K,N,trans', [(1024, 768, 3072, False), (1304, 512, 768, True), (2048, 1024, 640, False)])
+def test_gemm_act_epilogue(act, M, K, N, trans):
+    """Inference fc epilogue (pa_gemm8_bf16_act): act(x @ W + b) in the GEMM's staged epilogue vs fp32."""
+    from paddle.ops import gemm as G
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device='cuda').bfloat16()
+    w = (torch.randn(N, K, device='cuda') * 0.05).bfloat16() if trans else (torch.randn(K, N, device='cuda') * 0.05).bfloat16()
+    W = w.t() if trans else w
+    b = torch.randn(N, device='cuda').bfloat16()
+    assert G.epi_ok(x, W, N)
+    y = G.mm_act(x, W, b, act)
+    h = x.float() @ W.float() + b.float()
+    ref = {'relu': torch.relu(h), 'gelu': torch.nn.functional.gelu(h),
+           'gelu_tanh': torch.nn.functional.gelu(h, approximate='tanh')}[act]
+    err = (y.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2, err
