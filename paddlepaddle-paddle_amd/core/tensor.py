@@ -468,7 +468,14 @@ class Parameter(Tensor):
 EagerParamBase = Parameter
 
 
-def _fast_wrap(t, _new=object.__new__, _T=Tensor):
+# [True] while a bytecode-translated (jit/sot.py) function runs: the tracer-visible paths below are
+# taken only then (a list read instead of torch.compiler.is_compiling() on every wrap)
+SOT_ACTIVE = [False]
+
+
+def _fast_wrap(t, _new=object.__new__, _T=Tensor, _sot=SOT_ACTIVE, _compiling=torch.compiler.is_compiling):
+    if _sot[0] and _compiling():  # inside a bytecode translation: a constructor the tracer follows
+        return _T(t)
     o = _new(_T)
     o._t = t
     o._name = None

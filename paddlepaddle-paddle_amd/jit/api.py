@@ -9,7 +9,10 @@ kernels; ``to_static`` keeps dygraph semantics and adds
   ``cond`` / ``while`` nodes (``jit/dy2static.py``), so the saved program branches per input;
 * HIP-graph replay of the forward for inference-shaped calls (``backend='hip_graph'`` or
   ``build_strategy.use_hip_graph``): launch-bound small-batch decoding collapses into one
-  graph launch per call.
+  graph launch per call;
+* bytecode-level translation (``backend='sot'``, or ``full_graph=False`` with PADDLE_AMD_SOT=1):
+  jit/sot.py captures the tensor work as static Programs run by the Executor, graph breaks fall
+  back to Python.
 ``jit.load`` returns a ``TranslatedLayer`` that interprets the saved program without the
 Python class that produced it.
 """
@@ -120,8 +123,17 @@ class StaticFunction:
         bs = self._build_strategy
         return bool(bs is not None and getattr(bs, 'use_hip_graph', False))
 
+    def _use_sot(self):
+        from . import sot
+        return self._backend == 'sot' or (not self._full_graph and self._backend is None and sot.default_enabled())
+
     def __call__(self, *args, **kwargs):
         self._last_specs = [_spec_of(a, i) for i, a in enumerate(args)]
+        if _to_static_enabled[0] and self._use_sot():
+            if getattr(self, '_sot_fn', None) is None:
+                from .sot import symbolic_translate
+                self._sot_fn = symbolic_translate(self._fn)
+            return self._sot_fn(*args, **kwargs)
         if (_to_static_enabled[0] and self._use_graph() and not kwargs and not torch.is_grad_enabled()
                 and torch.cuda.is_available()):
             if self._graphed is None:

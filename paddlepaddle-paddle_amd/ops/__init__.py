@@ -9,6 +9,7 @@ import os
 import torch
 
 from . import _native
+from ..core.tensor import SOT_ACTIVE as _SOT
 
 _disabled = os.environ.get('PADDLE_AMD_DISABLE_HIP_KERNELS', '0') == '1'
 
@@ -22,8 +23,10 @@ def set_enabled(v):
     _disabled = not v
 
 
-def use_hip(t):
+def use_hip(t, _compiling=torch.compiler.is_compiling):
     if _disabled or not isinstance(t, torch.Tensor) or t.device.type != 'cuda':
+        return False
+    if _SOT[0] and _compiling():  # bytecode translation (jit/sot.py): torch composites, mapped back by the Executor
         return False
     if _native.lib is None and _native._load() is None:
         raise RuntimeError("paddle_amd HIP kernel library not available on a GPU process: " + str(_native.load_error))
