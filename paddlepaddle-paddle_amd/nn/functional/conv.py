@@ -221,10 +221,50 @@ def _conv_t(x, weight, bias, stride, padding, output_padding, dilation, groups, 
             # transposed conv on the stride-class data-gradient kernel (channels-last, NCHW as views)
             y = ops.conv.conv_transpose2d_nhwc(xn.contiguous(), w, b, s, p, d, ohw)
             return _w(y if cl else y.permute(0, 3, 1, 2))
+    if nd == 3 and groups == 1 and ops.use_hip(t) and w.dim() == 5:
+        y = _conv_t3d_depth_taps(t, w, b, s, p, d, op)
+        if y is not None:
+            return _w(y if cl else y.permute(0, 4, 1, 2, 3))
     out = fn(t, w, b, s, p, op, groups, d)
     if cl:
         out = out.permute(0, *range(2, nd + 2), 1)
     return _w(out)
+
+
+def _conv_t3d_depth_taps(t, w, b, s, p, d, op):
+    """conv3d_transpose on the 2-D transposed-conv kernels: every depth tap z of the filter is one
+    batched 2-D transposed convolution of all input depth slices (folded into the batch, channels
+    last) with the tap's 2-D filter w[:, :, z]; input slice i lands on output depth
+    i * s[0] - p[0] + z * d[0] (index_add, slices outside [0, D_out) dropped).  Differentiable
+    through the 2-D kernels' backward.  Returns NDHWC, or None outside the kernels' contract."""
+    N, C, D, H, W = t.shape
+    kd = w.shape[2]
+    Do = (D - 1) * s[0] - 2 * p[0] + d[0] * (kd - 1) + op[0] + 1
+    ohw = tuple((t.shape[3 + i] - 1) * s[1 + i] - 2 * p[1 + i] + d[1 + i] * (w.shape[3 + i] - 1) + op[1 + i] + 1
+                for i in range(2))
+    if Do <= 0 or min(ohw) <= 0:
+        return None
+    xn = t.permute(0, 2, 3, 4, 1).reshape(N * D, H, W, C)
+    if not ops.conv.convt_supported(xn, w[:, :, 0], 1, s[1:], p[1:], d[1:], ohw):
+        return None
+    xn = xn.contiguous()
+    y = None
+    src = torch.arange(D, device=t.device)
+    for z in range(kd):
+        dst = src * s[0] - p[0] + z * d[0]
+        keep = (dst >= 0) & (dst < Do)
+        if not bool(keep.any()):
+            continue
+        yz = ops.conv.conv_transpose2d_nhwc(xn, w[:, :, z].contiguous(), None, s[1:], p[1:], d[1:], ohw)
+        yz = yz.reshape(N, D, ohw[0], ohw[1], -1)
+        if y is None:
+            y = yz.new_zeros(N, Do, ohw[0], ohw[1], yz.shape[-1])
+        y = y.index_add(1, dst[keep], yz[:, keep])
+    if y is None:
+        return None
+    if b is not None:
+        y = y + b.to(y.dtype)
+    return y
 
 
 def conv1d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1,

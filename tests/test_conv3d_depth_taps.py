@@ -61,3 +61,29 @@ def test_cin_padding_matches_conv2d(monkeypatch, C, Cout, groups, k, s):
     g = torch.randn_like(ref)
     for a, r in zip(torch.autograd.grad(y, (x, w, b), g), torch.autograd.grad(ref, (x, w, b), g)):
         torch.testing.assert_close(a, r)
+
+
+def _nhwc_convt2d(x, w, b, s, p, d, ohw):
+    H, W = x.shape[1], x.shape[2]
+    op = tuple(ohw[i] - ((x.shape[1 + i] - 1) * s[i] - 2 * p[i] + d[i] * (w.shape[2 + i] - 1) + 1) for i in range(2))
+    y = torch.nn.functional.conv_transpose2d(x.permute(0, 3, 1, 2), w, b, s, p, op, 1, d)
+    return y.permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize('D,k,s,p,dil,op', [(4, 3, 1, 1, 1, 0), (5, 3, 2, 1, 1, 1), (4, 2, 2, 0, 1, 0), (6, 3, 1, 2, 2, 0)])
+def test_convt3d_depth_taps_match_conv_transpose3d(monkeypatch, D, k, s, p, dil, op):
+    """conv3d_transpose depth-tap decomposition (_conv_t3d_depth_taps) vs torch conv_transpose3d,
+    forward and gradients (torch transposed 2-D convs stand in for the HIP kernels)."""
+    monkeypatch.setattr(C.ops.conv, 'convt_supported', lambda *a, **kw: True)
+    monkeypatch.setattr(C.ops.conv, 'conv_transpose2d_nhwc', _nhwc_convt2d)
+    torch.manual_seed(D * 7 + k)
+    x = torch.randn(2, 3, D, 5, 6, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(3, 4, k, k, k, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(4, dtype=torch.float64, requires_grad=True)
+    y = C._conv_t3d_depth_taps(x, w, b, (s, s, s), (p, p, p), (dil, dil, dil), (op, op, op)).permute(0, 4, 1, 2, 3)
+    ref = torch.nn.functional.conv_transpose3d(x, w, b, s, p, op, 1, dil)
+    assert y.shape == ref.shape
+    torch.testing.assert_close(y, ref)
+    g = torch.randn_like(ref)
+    for a, r in zip(torch.autograd.grad(y, (x, w, b), g), torch.autograd.grad(ref, (x, w, b), g)):
+        torch.testing.assert_close(a, r)

@@ -538,3 +538,35 @@ def test_conv3d_depth_taps_on_hip_kernels(C, Cout, D, k, s, p, fmt):
     _close(dx, xr.grad, 3e-2, 1e-2, 'dgrad')
     _close(wp.grad._t, wr.grad, 5e-2, 2e-2, 'wgrad')
     _close(bp.grad._t, br.grad, 5e-2, 2e-2, 'bgrad')
+
+
+@pytest.mark.parametrize('C,Cout,D,k,s,p,op', [(32, 64, 4, 3, 1, 1, 0), (64, 32, 5, 3, 2, 1, 1), (32, 32, 4, 2, 2, 0, 0)])
+def test_conv3d_transpose_depth_taps_on_hip_kernels(C, Cout, D, k, s, p, op):
+    """conv3d_transpose folded onto the 2-D transposed-conv kernels (one batched transposed 2-D
+    convolution per depth tap, slices index-added into the output depth): forward, data / filter /
+    bias gradients vs fp32 torch, no library convolution kernel."""
+    F = paddle.nn.functional
+    x = torch.randn(2, C, D, 8, 9, device=DEV).bfloat16()
+    w = (0.05 * torch.randn(C, Cout, k, k, k, device=DEV)).bfloat16()
+    b = torch.randn(Cout, device=DEV).bfloat16()
+    xr, wr, br = (t.float().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.conv_transpose3d(xr, wr, br, s, p, op)
+    g = torch.randn_like(yr)
+    xp = paddle.to_tensor(x, stop_gradient=False)
+    wp = paddle.to_tensor(w, stop_gradient=False)
+    bp = paddle.to_tensor(b, stop_gradient=False)
+    out = []
+
+    def run():
+        y = F.conv3d_transpose(xp, wp, bp, s, p, output_padding=op)
+        y.backward(paddle.to_tensor(g.bfloat16().contiguous()))
+        out.append(y)
+    bad = _miopen_kernels(run)
+    assert bad == [], bad
+    yr.backward(g)
+    y = out[0]._t
+    assert tuple(y.shape) == tuple(yr.shape)
+    _close(y, yr, 3e-2, 1e-2, 'fwd')
+    _close(xp.grad._t, xr.grad, 3e-2, 1e-2, 'dgrad')
+    _close(wp.grad._t, wr.grad, 5e-2, 2e-2, 'wgrad')
+    _close(bp.grad._t, br.grad, 5e-2, 2e-2, 'bgrad')
