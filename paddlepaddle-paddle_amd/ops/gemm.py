@@ -138,15 +138,20 @@ def mm_bn_stats(a, b):
 
 
 def _splitk_for(M, N_, K):
-    """Split-K factor for outputs with too few 256x256 tiles to fill 256 CUs (the 2048x2048
-    out-projection weight gradient: 64 tiles x 4 slices, profiles/r2_gemm_sched.log)."""
+    """Split-K factor for outputs with too few 256x256 tiles to fill 256 CUs: the largest of 2..16
+    slices (>= 2048 k each) that keeps the blocks within one round of the chip.  Weight gradients
+    over many tokens: GPT-3 out-projection 2048x2048 64 tiles -> 4 (1058 TF), ERNIE-base at 32768
+    tokens 768x2304 27 tiles -> 8 (193 -> 126 us), 768x768 9 tiles -> 16 (183 -> 66 us), 768x3072
+    36 tiles -> 4 (profiles/r5bb_wgrad_splitk_ab.log)."""
     tiles = -(-M // 256) * -(-N_ // 256)
     if tiles >= 128:
         return 1
-    for s in (4, 2):
-        if K % (64 * s) == 0 and K // s >= 2048:
-            return s
-    return 1
+    best = 1
+    for s in (2, 4, 8, 16):
+        if K % (64 * s) or K // s < 2048 or tiles * s > 256:
+            break
+        best = s
+    return best
 
 
 _skinny = os.environ.get('PADDLE_AMD_SKINNY_GEMM', '1') != '0'
