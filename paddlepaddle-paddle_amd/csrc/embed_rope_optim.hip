@@ -73,6 +73,62 @@ __global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, T* _
   }
 }
 
+// Rotary embedding over strided rows: x / y [B, S, H, D] with D and H contiguous (head stride D)
+// and row strides ldx / ldy (elements between consecutive (b, s) rows; batch stride S * ld) — the q /
+// k slices of a fused QKV projection are read and their gradients written in place, no copies.
+// One work item = 8 rotation pairs: 16-B loads of both pair halves and of the cos / sin rows.
+// y may alias x (each item reads its pairs before writing them).
+template <typename T>
+__global__ __launch_bounds__(256) void rope_rows_kernel(const T* x, long long ldx, T* y, long long ldy,
+                                                        const float* __restrict__ cosb, const float* __restrict__ sinb,
+                                                        const int64_t* __restrict__ pos, int B, int S, int H, int D,
+                                                        int interleaved, float sign) {
+  const int half = D / 2;
+  const int g8 = half / 8;  // items per head
+  const long long n = (long long)B * S * H * g8;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const int g = (int)(i % g8);
+    const long long bsh = i / g8;
+    const int h = (int)(bsh % H);
+    const long long bs = bsh / H;
+    const int s = (int)(bs % S);
+    const int b = (int)(bs / S);
+    const int ps = pos != nullptr ? (int)pos[(long long)b * S + s] : s;
+    const T* xr = x + bs * ldx + (long long)h * D;
+    T* yr = y + bs * ldy + (long long)h * D;
+    float c[8], sn[8];
+    load_f<float, 4>(cosb + (size_t)ps * half + 8 * g, *reinterpret_cast<float(*)[4]>(&c[0]));
+    load_f<float, 4>(cosb + (size_t)ps * half + 8 * g + 4, *reinterpret_cast<float(*)[4]>(&c[4]));
+    load_f<float, 4>(sinb + (size_t)ps * half + 8 * g, *reinterpret_cast<float(*)[4]>(&sn[0]));
+    load_f<float, 4>(sinb + (size_t)ps * half + 8 * g + 4, *reinterpret_cast<float(*)[4]>(&sn[4]));
+    if (!interleaved) {  // pairs (p, p + D/2), p = 8 g .. 8 g + 7
+      float a[8], bb[8], o0[8], o1[8];
+      load_f<T, 8>(xr + 8 * g, a);
+      load_f<T, 8>(xr + half + 8 * g, bb);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float se = sign * sn[e];
+        o0[e] = a[e] * c[e] - bb[e] * se;
+        o1[e] = bb[e] * c[e] + a[e] * se;
+      }
+      store_f<T, 8>(yr + 8 * g, o0);
+      store_f<T, 8>(yr + half + 8 * g, o1);
+    } else {  // pairs (2p, 2p + 1), p = 8 g .. 8 g + 7: elements 16 g .. 16 g + 15
+      float v[16], o[16];
+      load_f<T, 8>(xr + 16 * g, *reinterpret_cast<float(*)[8]>(&v[0]));
+      load_f<T, 8>(xr + 16 * g + 8, *reinterpret_cast<float(*)[8]>(&v[8]));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float se = sign * sn[e];
+        o[2 * e] = v[2 * e] * c[e] - v[2 * e + 1] * se;
+        o[2 * e + 1] = v[2 * e + 1] * c[e] + v[2 * e] * se;
+      }
+      store_f<T, 8>(yr + 16 * g, *reinterpret_cast<float(*)[8]>(&o[0]));
+      store_f<T, 8>(yr + 16 * g + 8, *reinterpret_cast<float(*)[8]>(&o[8]));
+    }
+  }
+}
+
 // Paddle AdamW on a flat fp32 master buffer:
 //   p *= (1 - lr * wd);  m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2
 //   p -= lr * sqrt(1-b2^t)/(1-b1^t) * m / (sqrt(v) + eps * sqrt(1-b2^t))
@@ -331,6 +387,17 @@ PA_API hipError_t pa_rope(const void* x, void* y, const float* cosb, const float
   const long long npairs = (long long)B * S * H * (D / 2);
   PA_DISPATCH_DTYPE(dt, T, rope_kernel<T><<<grid_for(npairs, 256, 256 * 8), 256, 0, st>>>(
                                (const T*)x, (T*)y, cosb, sinb, pos, B, S, H, D, interleaved, sign));
+  return hipGetLastError();
+}
+
+// x, y: [B, S, H, D] rows of ldx / ldy elements (D % 16 == 0, 16-B aligned rows); y may be x.
+PA_API hipError_t pa_rope_rows(const void* x, long long ldx, void* y, long long ldy, const float* cosb,
+                               const float* sinb, const int64_t* pos, int B, int S, int H, int D, int interleaved,
+                               float sign, int dt, hipStream_t st) {
+  if (D % 16 || ldx % 8 || ldy % 8 || B <= 0 || S <= 0 || H <= 0) return hipErrorInvalidValue;
+  const long long n = (long long)B * S * H * (D / 16);
+  PA_DISPATCH_DTYPE(dt, T, rope_rows_kernel<T><<<grid_for(n, 256, 256 * 8), 256, 0, st>>>(
+                               (const T*)x, ldx, (T*)y, ldy, cosb, sinb, pos, B, S, H, D, interleaved, sign));
   return hipGetLastError();
 }
 

@@ -84,6 +84,11 @@ class LlamaAttention(nn.Layer):
         q, k, v = qkv[:, :, :self.nh], qkv[:, :, self.nh:self.nh + self.nkv], qkv[:, :, self.nh + self.nkv:]
         cos, sin = ops.rope.rope_tables(self.cfg.max_position_embeddings, self.hd, self.cfg.rope_theta, t.device)
         pos = _unwrap(position_ids) if position_ids is not None else None
+        if ops.use_hip(t) and ops.flash_attn.qkv_rope_flash_ok(qkv, self.nh, self.nkv):
+            # RoPE read from / dQKV written into the fused projection's layout (ops/flash_attn.py
+            # _QKVRopeFlash): no slice copies, no zero-filled per-slice gradients to add up
+            o = ops.flash_attn.qkv_rope_flash(qkv, self.nh, self.nkv, cos, sin, pos, causal=True)
+            return self.o_proj(_wrap(o.reshape(B, S, -1)))
         if ops.use_hip(t):
             q = ops.rope.apply_rope(q, cos, sin, pos)
             k = ops.rope.apply_rope(k, cos, sin, pos)

@@ -70,6 +70,7 @@ _SIGS = {
     'pa_embedding_fwd': [P, P, P, I, I, LL, I, P],
     'pa_embedding_bwd': [P, P, P, P, I, I, LL, I, I, P],
     'pa_rope': [P, P, P, P, P, I, I, I, I, I, F, I, P],
+    'pa_rope_rows': [P, LL, P, LL, P, P, P, I, I, I, I, I, F, I, P],
     'pa_adamw': [P, P, P, P, P, LL, P, F, F, F, F, F, F, F, P, P, I, I, P],
     'pa_sumsq': [P, LL, P, I, P],
     'pa_momentum': [P, P, P, P, LL, P, F, F, F, F, I, P, I, I, P],

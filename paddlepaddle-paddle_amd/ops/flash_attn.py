@@ -161,6 +161,71 @@ class _FlashAttnPacked(torch.autograd.Function):
         return dqkv, None, None
 
 
+class _QKVRopeFlash(torch.autograd.Function):
+    """Fused-QKV projection output [B, S, Hq + 2 Hkv, D] -> RoPE on the q / k head slices ->
+    causal flash attention.  Forward: the rotated q / k are written straight from the strided
+    slices (no .contiguous() copies), v is attended in place.  Backward: dQ / dK / dV land
+    directly in one packed gradient (MHA; GQA sums the per-q-head dK / dV into it) and dQ / dK are
+    rotated back in place — no zero-filled per-slice gradients, adds or concatenation."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, pos, nh, nkv, causal, scale):
+        from . import rope
+        B, S, Ht, D = qkv.shape
+        q = torch.empty(B, S, nh, D, dtype=qkv.dtype, device=qkv.device)
+        k = torch.empty(B, S, nkv, D, dtype=qkv.dtype, device=qkv.device)
+        rope.rope_rows(qkv[:, :, :nh], q, cos, sin, pos)
+        rope.rope_rows(qkv[:, :, nh:nh + nkv], k, cos, sin, pos)
+        v = qkv[:, :, nh + nkv:]
+        o, lse = _fwd(q, k, v, causal, scale)
+        ctx.save_for_backward(q, k, qkv, o, lse, cos, sin, pos)
+        ctx.cfg = (nh, nkv, causal, scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        from . import rope
+        q, k, qkv, o, lse, cos, sin, pos = ctx.saved_tensors
+        nh, nkv, causal, scale = ctx.cfg
+        B, S, Ht, D = qkv.shape
+        v = qkv[:, :, nh + nkv:]
+        if do.stride(-1) != 1 or any(s_ % 8 for s_ in do.stride()[:3]):
+            do = do.contiguous()
+        dqkv = torch.empty(B, S, Ht, D, dtype=qkv.dtype, device=qkv.device)
+        dq, dk, dv = dqkv[:, :, :nh], dqkv[:, :, nh:nh + nkv], dqkv[:, :, nh + nkv:]
+        delta = torch.empty(B, nh, S, dtype=torch.float32, device=qkv.device)
+        if nh == nkv:
+            _bwd_call(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, S, nh, nkv, D, scale, causal)
+        else:  # GQA: per-q-head dK / dV, summed over each kv group into the packed slices
+            dkh = torch.empty(B, S, nh, D, dtype=qkv.dtype, device=qkv.device)
+            dvh = torch.empty(B, S, nh, D, dtype=qkv.dtype, device=qkv.device)
+            _bwd_call(q, k, v, o, do, lse, delta, dq, dkh, dvh, B, S, S, nh, nkv, D, scale, causal)
+            dk.copy_(dkh.view(B, S, nkv, nh // nkv, D).sum(3))
+            dv.copy_(dvh.view(B, S, nkv, nh // nkv, D).sum(3))
+        rope.rope_rows(dq, dq, cos, sin, pos, sign=-1.0)
+        rope.rope_rows(dk, dk, cos, sin, pos, sign=-1.0)
+        return dqkv, None, None, None, None, None, None, None
+
+
+def qkv_rope_flash_ok(qkv, nh, nkv):
+    from . import rope
+    if qkv.dim() != 4 or not qkv.is_contiguous() or qkv.shape[2] != nh + 2 * nkv or nh % nkv:
+        return False
+    if not rope.rows_ok(qkv[:, :, :nh]) or qkv.dtype not in (torch.bfloat16, torch.float16):
+        return False
+    return supported(qkv[:, :, :nh], qkv[:, :, nh:nh + nkv], qkv[:, :, nh + nkv:])
+
+
+def qkv_rope_flash(qkv, nh, nkv, cos, sin, pos=None, causal=True, scale=None):
+    """Flash attention of RoPE'd q / k taken from a fused QKV projection output
+    [B, S, nh + 2 nkv, D] (``qkv_rope_flash_ok``); cos / sin: [S_max, D/2] fp32 tables;
+    pos: optional [B, S] int64 positions.  Returns o [B, S, nh, D]."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(qkv.shape[-1])
+    p = pos.contiguous().to(torch.int64) if pos is not None else None
+    return _QKVRopeFlash.apply(qkv, cos, sin, p, int(nh), int(nkv), bool(causal), float(scale))
+
+
 def flash_attention_packed(qkv, causal=False, scale=None):
     """qkv: [B, S, 3, H, D] with unit last-dim stride."""
     if scale is None:

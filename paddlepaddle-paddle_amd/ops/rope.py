@@ -49,3 +49,25 @@ def apply_rope(x, cos, sin, position_ids=None, interleaved=False):
     """x: [B, S, H, D]; cos/sin: [S_max, D/2] fp32; position_ids: optional [B, S] int64."""
     pos = position_ids.contiguous().to(torch.int64) if position_ids is not None else None
     return _Rope.apply(x, cos, sin, pos, interleaved)
+
+
+def rows_ok(x):
+    """x: [B, S, H, D] whose (head, dim) block is contiguous and whose (b, s) rows are evenly
+    strided (a contiguous tensor, or a head slice of a fused QKV projection)."""
+    if x.dim() != 4 or not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16, torch.float32):
+        return False
+    B, S, H, D = x.shape
+    if N.lib is None and N._load() is None:
+        return False
+    return (D % 16 == 0 and x.stride(3) == 1 and x.stride(2) == D and x.stride(0) == S * x.stride(1)
+            and x.stride(1) % 8 == 0 and x.data_ptr() % 16 == 0)
+
+
+def rope_rows(x, y, cos, sin, pos=None, interleaved=False, sign=1.0):
+    """y = rope(x) (sign -1: the inverse rotation) over strided rows (``rows_ok`` layouts; y may
+    be x: in place) on csrc/embed_rope_optim.hip pa_rope_rows (8 rotation pairs per work item)."""
+    B, S, H, D = x.shape
+    lib = N.lib if N.lib is not None else N._load()
+    N.check(lib.pa_rope_rows(N.ptr(x), x.stride(1), N.ptr(y), y.stride(1), N.ptr(cos), N.ptr(sin), N.ptr(pos),
+                               B, S, H, D, int(interleaved), float(sign), N.dtcode(x.dtype), N.stream()), 'rope_rows')
+    return y
