@@ -196,6 +196,8 @@ def gumbel_softmax(x, temperature=1.0, hard=False, axis=-1, name=None):
 def swiglu(x, y=None, name=None):
     """paddle.incubate.nn.functional.swiglu: silu(x) * y (y=None → split x in half)."""
     t = _u(x)
+    if y is None and ops.use_hip(t) and ops.act.swiglu_packed_ok(t):
+        return _w(ops.act.swiglu_packed(t))  # one [rows, 2C] gradient, no chunk()/cat in autograd
     if y is None:
         a, b = t.chunk(2, dim=-1)
     else:

@@ -88,6 +88,44 @@ class _Swiglu(torch.autograd.Function):
         return da.reshape(a.shape), db.reshape(b.shape)
 
 
+class _SwigluPacked(torch.autograd.Function):
+    """silu(x[..., :C]) * x[..., C:] of one [rows, 2C] tensor (the fused gate/up projection):
+    the gradient is ONE [rows, 2C] buffer written by the backward kernel, so autograd never
+    concatenates per-half gradients (the chunk() backward copied the whole 2C-wide gradient)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        cols = x.shape[-1] // 2
+        x2 = x.reshape(-1, 2 * cols)
+        rows = x2.shape[0]
+        y = torch.empty(rows, cols, dtype=x.dtype, device=x.device)
+        N.check(N.lib.pa_swiglu_fwd(N.ptr(x2), N.ptr(x2[:, cols:]), N.ptr(y), rows * cols, 2 * cols, cols,
+                                    N.dtcode(x.dtype), N.stream()), 'swiglu_fwd')
+        ctx.save_for_backward(x2)
+        ctx.xshape = x.shape
+        return y.reshape(*x.shape[:-1], cols)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, = ctx.saved_tensors
+        rows, cols = x2.shape[0], x2.shape[1] // 2
+        dy = dy.contiguous()
+        dx = torch.empty_like(x2)
+        N.check(N.lib.pa_swiglu_bwd(N.ptr(x2), N.ptr(x2[:, cols:]), N.ptr(dy), N.ptr(dx), N.ptr(dx[:, cols:]),
+                                    rows * cols, 2 * cols, cols, N.dtcode(x2.dtype), N.stream()), 'swiglu_bwd')
+        return dx.reshape(ctx.xshape)
+
+
+def swiglu_packed_ok(x):
+    cols = x.shape[-1] // 2 if x.dim() >= 1 else 0
+    return (x.is_cuda and x.is_contiguous() and x.shape[-1] % 2 == 0 and x.dtype in (torch.bfloat16, torch.float16)
+            and _vec_ok(x[..., :cols], cols))
+
+
+def swiglu_packed(x):
+    return _SwigluPacked.apply(x)
+
+
 def swiglu(a, b):
     cols = a.shape[-1]
     ok = (_vec_ok(a, cols) and a.stride(-1) == 1 and b.stride(-1) == 1 and a.stride() == b.stride()

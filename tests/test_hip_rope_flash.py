@@ -72,3 +72,21 @@ def test_qkv_rope_flash_matches_reference(nh, nkv, use_pos):
     torch.testing.assert_close(o.float(), ref, atol=3e-2, rtol=2e-2)
     err = (qkv.grad.float() - qr.grad).abs().max().item() / qr.grad.abs().max().item()
     assert err < 3e-2, err
+
+
+def test_swiglu_packed_single_gradient_buffer():
+    """F.swiglu(x) of the fused gate/up projection: one packed autograd op (no chunk / cat), values
+    and the gradient vs fp32 torch."""
+    import paddle.nn.functional as F
+    torch.manual_seed(2)
+    x = torch.randn(3, 50, 2 * 1024, device='cuda').bfloat16().requires_grad_()
+    xp = paddle.to_tensor(x.detach(), stop_gradient=False)
+    yp = F.swiglu(xp)
+    g = torch.randn(3, 50, 1024, device='cuda')
+    yp.backward(paddle.to_tensor(g.bfloat16()))
+    xr = x.detach().float().requires_grad_()
+    a, b = xr.chunk(2, -1)
+    ref = torch.nn.functional.silu(a) * b
+    ref.backward(g)
+    torch.testing.assert_close(yp._t.float(), ref, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(xp.grad._t.float(), xr.grad, atol=5e-2, rtol=3e-2)
