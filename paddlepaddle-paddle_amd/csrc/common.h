@@ -180,6 +180,22 @@ __device__ __forceinline__ void gelu_tanh_fdf2(f32x2_t x, f32x2_t& f, f32x2_t& d
   df = __builtin_elementwise_fma(w, k, sg);
 }
 
+// Exact-form GELU and its derivative for GEMM epilogues: erf by Abramowitz-Stegun 7.1.26 (|error|
+// <= 1.5e-7, far below bf16 output rounding) sharing ONE exp with the derivative's normal density:
+// z = |x|/sqrt2, t = 1/(1 + p z), erf(z) = 1 - t*poly(t)*exp(-z^2), exp(-z^2) = exp(-x^2/2).
+__device__ __forceinline__ void gelu_erf_fdf(float x, float& f, float& df) {
+  constexpr float p = 0.3275911f, a1 = 0.254829592f, a2 = -0.284496736f, a3 = 1.421413741f, a4 = -1.453152027f,
+                  a5 = 1.061405429f, l2e = 1.4426950408889634f;
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(p, z, 1.f));
+  const float e = __builtin_amdgcn_exp2f(-0.5f * l2e * x * x);
+  const float poly = t * __builtin_fmaf(t, __builtin_fmaf(t, __builtin_fmaf(t, __builtin_fmaf(t, a5, a4), a3), a2), a1);
+  const float erfz = __builtin_fmaf(-poly, e, 1.f);
+  const float cdf = 0.5f + copysignf(0.5f * erfz, x);
+  f = x * cdf;
+  df = __builtin_fmaf(x * 0.39894228040143268f, e, cdf);
+}
+
 struct GeluTanh {
   static __device__ __forceinline__ float f(float x) {
     const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);

@@ -210,6 +210,17 @@ PA_API int pa_gemm8_bf16_epi(const void* A, const void* B, void* C, const void* 
   if (!pa_gemm8_ok(M, N, K, lda, ldb, ldc, 0, transB, 1) || !aux) return (int)hipErrorInvalidValue;
   if (epi == 2) return (int)launch_epi<2>(transB, A, B, C, aux, bias, M, N, K, lda, ldb, ldc, alpha, st);
   if (epi == 3) return (int)launch_epi<3>(transB, A, B, C, aux, nullptr, M, N, K, lda, ldb, ldc, alpha, st);
+  // epi 9: epi 2 with the exact (erf) GELU, wave-staged epilogue only
+  if (epi == 9) {
+    dim3 grid(((M + BM - 1) / BM) * ((N + BN - 1) / BN), 1, 1);
+    if (transB)
+      gemm11_kernel<true, true, 209><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, (float*)aux,
+                                                          (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, 0.f, K);
+    else
+      gemm11_kernel<true, false, 209><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, (float*)aux,
+                                                           (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, 0.f, K);
+    return (int)hipGetLastError();
+  }
   // epi 4: epi 3 + column partial sums of C, one fp32 row per 128-row slab, into bias ([ceil(M/128)][N])
   if (epi == 4 && bias != nullptr) return (int)launch_epi<4>(transB, A, B, C, aux, bias, M, N, K, lda, ldb, ldc, alpha, st);
   // epi 5: plain C = alpha*A@B + batch-norm column statistics (mean, M2) of every 128-row slab into

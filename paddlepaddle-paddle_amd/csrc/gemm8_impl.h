@@ -632,9 +632,13 @@ __device__ __forceinline__ void epilogue_wstaged(const f32x4 (&acc)[8][4], uint1
                                                  int N, long long ldc, float alpha, float beta, int mb, int nb,
                                                  int lane, lds_char* region) {
   // EPI 6 / 7 / 8: inference activations after the bias (relu / gelu erf / gelu tanh), no aux
-  // output — the fc_fuse_pass epilogue of imported programs (static/ir_passes.py fused_linear)
-  static_assert(EPI == 0 || EPI == 2 || EPI == 3 || EPI == 4 || EPI == 5 || EPI == 6 || EPI == 7 || EPI == 8,
-                "staged epilogue: EPI 0/2/3/4/5/6/7/8");
+  // output — the fc_fuse_pass epilogue of imported programs (static/ir_passes.py fused_linear).
+  // EPI 9: EPI 2 with the exact (erf) GELU: C = gelu(h), aux = gelu'(h) = Phi(h) + h phi(h) — the
+  // training fc1 of static programs (static/ir_passes.py fused_ffn)
+  static_assert(EPI == 0 || EPI == 2 || EPI == 3 || EPI == 4 || EPI == 5 || EPI == 6 || EPI == 7 || EPI == 8 ||
+                    EPI == 9,
+                "staged epilogue: EPI 0/2/3/4/5/6/7/8/9");
+  constexpr bool TWO_OUT = EPI == 2 || EPI == 9;
   const int g = lane >> 4;
   const bool upper = (g & 1) != 0;
   constexpr bool AUX_IN = EPI == 3 || EPI == 4;
@@ -709,12 +713,21 @@ __device__ __forceinline__ void epilogue_wstaged(const f32x4 (&acc)[8][4], uint1
               d[e + 1] = dv.y;
             }
             *(lds_u32x4*)(reg_a + wtile(r, ch)) = pack_bf16x8(d);
+          } else if constexpr (EPI == 9) {
+            float d[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) gelu_erf_fdf(v[e], v[e], d[e]);
+            *(lds_u32x4*)(reg_a + wtile(r, ch)) = pack_bf16x8(d);
           } else if constexpr (EPI == 6) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
           } else if constexpr (EPI == 7) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+            for (int e = 0; e < 8; ++e) {
+              float dd;
+              gelu_erf_fdf(v[e], v[e], dd);
+              (void)dd;
+            }
           } else if constexpr (EPI == 8) {
 #pragma unroll
             for (int e = 0; e < 8; e += 2) {
@@ -735,7 +748,7 @@ __device__ __forceinline__ void epilogue_wstaged(const f32x4 (&acc)[8][4], uint1
     __builtin_amdgcn_wave_barrier();
     // the half, row-wise: 8 rows x 128 B per store
 #pragma unroll
-    for (int o = 0; o < (EPI == 2 ? 2 : 1); ++o) {
+    for (int o = 0; o < (TWO_OUT ? 2 : 1); ++o) {
       const lds_char* rg = o == 0 ? reg_c : reg_a;
       uint16_t* dst = o == 0 ? C : reinterpret_cast<uint16_t*>(ws);
       u32x4 v[8];

@@ -122,6 +122,34 @@ PA_API int pa_gemm8_fp8(const void* A, const void* W, void* C, const void* bias,
   return (int)hipGetLastError();
 }
 
+// fp8 GEMMs of a fused GELU feed-forward block (ops/fp8.py _FP8FFN, static training programs'
+// fuse_gemm_epilogue_pass) with the wave-staged epilogues of the bf16 MLP GEMMs: epi 9 / 2 (fc1
+// forward: h = s*A@W^T + bias, C = gelu(h), aux = gelu'(h); exact / tanh GELU), epi 4 (fc2 data
+// gradient: C = s*A@W^T * aux, per-128-row-slab column sums of C into ``bias`` as fp32
+// [ceil(M/128)][N]).  aux: bf16 [M][ldc].  Same contract and formats as pa_gemm8_fp8.
+PA_API int pa_gemm8_fp8_epi(const void* A, const void* W, void* C, const void* bias, void* aux, const void* scale_a,
+                            const void* scale_b, int M, int N, int K, long long lda, long long ldw, long long ldc,
+                            float alpha, int fmtA, int fmtB, int epi, hipStream_t st) {
+  using namespace pa::g8;
+  if (!pa_gemm8_fp8_ok(M, N, K, lda, ldw, ldc) || fmtA < 0 || fmtA > 1 || fmtB != 0 || aux == nullptr)
+    return (int)hipErrorInvalidValue;
+  if (epi == 4 && bias == nullptr) return (int)hipErrorInvalidValue;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  dim3 grid(tm * tn, 1, 1);
+  const int K2 = K / 2;
+  const long long la = lda / 2, lw = ldw / 2;
+  auto go = [&](auto kern) {
+    kern<<<grid, 512, 0, st>>>((const char*)A, (const char*)W, (uint16_t*)C, (float*)aux, (const uint16_t*)bias, M, N,
+                               K2, la, lw, ldc, alpha, 0.f, K2, 0LL, 0LL, 0LL, (const float*)scale_a,
+                               (const float*)scale_b);
+  };
+  if (epi == 9 && fmtA == 0) go(gemm11_kernel<true, true, 209, F8<0, 0>, false>);
+  else if (epi == 2 && fmtA == 0) go(gemm11_kernel<true, true, 202, F8<0, 0>, false>);
+  else if (epi == 4 && fmtA == 1) go(gemm11_kernel<true, true, 204, F8<1, 0>, false>);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
 // Split-K fp8 GEMM (the fp8 Linear weight gradient X^T dY: M x N = in x out features, K = tokens —
 // e.g. 768 x 2304 x 32768 is 27 output tiles for 256 CUs, so the K range is split over gridDim.z
 // slices writing fp32 slabs ws[z][M][N], folded by fp8_splitk_reduce with the dequant scales).

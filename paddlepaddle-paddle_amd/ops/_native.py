@@ -93,6 +93,7 @@ _SIGS = {
     'pa_gemm_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
     'pa_gemm8_fp8_ok': [I, I, I, LL, LL, LL],
     'pa_gemm8_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
+    'pa_gemm8_fp8_epi': [P, P, P, P, P, P, P, I, I, I, LL, LL, LL, F, I, I, I, P],
     'pa_gemm8_i8_ok': [I, I, I, LL, LL, LL],
     'pa_gemm8_i8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, P],
     'pa_i8_quant_rows': [P, I, I, LL, P, P, LL, P, I, P],

@@ -199,13 +199,89 @@ def fp8_linear(x, w, b=None, recipe=None, holder=None, key=None):
     """y = x @ w (+ b), w stored [in, out] (paddle layout), through the fp8 kernels."""
     recipe = recipe or _ACTIVE['recipe'] or DelayedScaling()
     if holder is None:  # static replay: state keyed by the weight storage
-        key = key if key is not None else (id(w), w.data_ptr())
-        st = _STATIC_STATES.get(key)
-        if st is None or st.recipe is not recipe:
-            st = _STATIC_STATES[key] = FP8State(recipe, w.device)
+        st = _static_state(w, recipe, key)
     else:
         st = _state_for(holder, w, recipe)
     return _FP8Linear.apply(x, w, b, st)
+
+
+def _static_state(w, recipe, key=None):
+    key = key if key is not None else (id(w), w.data_ptr())
+    st = _STATIC_STATES.get(key)
+    if st is None or st.recipe is not recipe:
+        st = _STATIC_STATES[key] = FP8State(recipe, w.device)
+    return st
+
+
+def _fp8_epi(a, w, sa, sb, epi, aux, bias=None):
+    """bf16 [M, N] = epilogue(sa*sb * a @ w^T) on the fp8 GEMM (csrc/gemm8x.hip pa_gemm8_fp8_epi)."""
+    M, N_ = a.shape[0], w.shape[0]
+    out = torch.empty(M, N_, dtype=torch.bfloat16, device=a.device)
+    N.check(N.lib.pa_gemm8_fp8_epi(N.ptr(a), N.ptr(w), N.ptr(out), N.ptr(bias), N.ptr(aux), N.ptr(sa), N.ptr(sb), M,
+                                   N_, a.shape[1], a.stride(0), w.stride(0), out.stride(0), 1.0, _FMT[a.dtype],
+                                   _FMT[w.dtype], int(epi), N.stream()), f'gemm8_fp8_epi{epi}')
+    return out
+
+
+class _FP8FFN(torch.autograd.Function):
+    """y = gelu(x @ W1 + b1) @ W2 + b2 with both Linears in fp8 (delayed scaling, the same per-weight
+    states as two fp8 Linears) and the GELU / GELU' in the fp8 GEMM epilogues: fc1 writes gelu(h)
+    and gelu'(h), fc2's data gradient multiplies by gelu'(h) and reduces the fc1 bias gradient —
+    the static fuse_gemm_epilogue_pass form of an fp8 feed-forward block (no activation kernels)."""
+
+    @staticmethod
+    def forward(ctx, x2, w1, b1, w2, b2, st1, st2, approximate):
+        xq, xqt, sx = st1.x.cast(x2)
+        w1q, w1qt, sw1 = st1.w.cast(w1)
+        h = torch.empty(x2.shape[0], w1.shape[1], dtype=torch.bfloat16, device=x2.device)
+        g = _fp8_epi(xq, w1qt, sx, sw1, 2 if approximate else 9, h, bias=b1.to(torch.bfloat16).contiguous())
+        gq, gqt, sg = st2.x.cast(g)
+        w2q, w2qt, sw2 = st2.w.cast(w2)
+        y = fp8_mm(gq, w2qt, sg, sw2, bias=b2)
+        ctx.save_for_backward(xqt, w1q, gqt, w2q, h, sx, sw1, sg, sw2)
+        ctx.st = (st1, st2)
+        ctx.dt = (x2.dtype, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xqt, w1q, gqt, w2q, h, sx, sw1, sg, sw2 = ctx.saved_tensors
+        st1, st2 = ctx.st
+        xdt, w1dt, b1dt, w2dt, b2dt = ctx.dt
+        dy2 = dy.contiguous()
+        M = dy2.shape[0]
+        dq, dqt, sd = st2.g.cast(dy2)
+        P = -(-M // 128)
+        part = torch.empty(P * w2q.shape[0], dtype=torch.float32, device=dy2.device)
+        dh = _fp8_epi(dq, w2q, sd, sw2, 4, h, bias=part)
+        from . import fused
+        db1 = torch.empty(w2q.shape[0], dtype=b1dt, device=dy2.device)
+        fused.colsum_finish_parts(part, db1, P, accumulate=False)
+        dw2 = fp8_mm(gqt, dqt, sg, sd).to(w2dt)
+        db2 = _colsum(dy2).to(b2dt)
+        hq, hqt, shh = st1.g.cast(dh)
+        dx = fp8_mm(hq, w1q, shh, sw1).to(xdt) if ctx.needs_input_grad[0] else None
+        dw1 = fp8_mm(xqt, hqt, sx, shh).to(w1dt)
+        return dx, dw1, db1, dw2, db2, None, None, None
+
+
+def ffn_ok(x2, w1, b1, w2, b2):
+    """Contract of the fp8 FFN: every operand of both fp8 GEMMs and of the epilogue kernels."""
+    if not (x2.is_cuda and x2.dim() == 2 and x2.dtype == torch.bfloat16 and _is_weight(w1) and _is_weight(w2)
+            and eligible(x2, w1) and w2.shape[0] == w1.shape[1] and b1.dim() == 1 and b2.dim() == 1
+            and b1.numel() == w1.shape[1] and b2.numel() == w2.shape[1] and x2.shape[0] % 8 == 0
+            and w2.shape[1] % 8 == 0 and N._load() is not None):
+        return False
+    M, K, F_, N2 = x2.shape[0], x2.shape[1], w1.shape[1], w2.shape[1]
+    ok = N.lib.pa_gemm8_fp8_ok
+    # fc1 [M,K]x[F,K]^T, fc2 dgrad [M,N2]x[F,N2]^T; the other four go through fp8_mm's own routing
+    return bool(ok(M, F_, K, K, K, F_)) and bool(ok(M, F_, N2, N2, N2, F_))
+
+
+def fp8_ffn(x2, w1, b1, w2, b2, approximate=False, recipe=None):
+    recipe = recipe or _STATIC_RECIPE['recipe'] or DelayedScaling()
+    st1, st2 = _static_state(w1, recipe), _static_state(w2, recipe)
+    return _FP8FFN.apply(x2, w1, b1, w2, b2, st1, st2, bool(approximate))
 
 
 # ----------------------------------------------------------------------------- autocast state

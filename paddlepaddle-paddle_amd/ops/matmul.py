@@ -236,6 +236,70 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
+class _FFNGeluFn(torch.autograd.Function):
+    """y = gelu(x @ W1 + b1) @ W2 + b2 (W [in, out]) for static training programs (the reference's
+    fuse_gemm_epilogue_pass, paddle/fluid/framework/ir/fuse_gemm_epilogue_pass.cc: linear + act
+    forward and linear_grad + act_grad backward as GEMM epilogues).  fc1's epilogue writes gelu(h)
+    and gelu'(h) (csrc/gemm8.hip epi 9 exact / 2 tanh); the backward's fc2 data-gradient GEMM
+    multiplies by gelu'(h) in its epilogue and reduces the fc1 bias gradient there (epi 4): no
+    activation kernel either way.  Returns gradients (ops.linear._MLPGelu is the flat-buffer
+    form of the training engines)."""
+
+    @staticmethod
+    def forward(ctx, x2, w1, b1, w2, b2, approximate):
+        from . import gemm
+        h = torch.empty(x2.shape[0], w1.shape[1], dtype=x2.dtype, device=x2.device)  # gelu'(x@W1 + b1)
+        g = gemm.mm_epi(x2, w1, 2 if approximate else 9, h, bias=b1)
+        y = _mm2d(g, w2, bias=b2)
+        if y is None:
+            y = torch.addmm(b2, g, w2)
+        ctx.save_for_backward(x2, w1, w2, h, g)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import gemm, fused
+        x2, w1, w2, h, g = ctx.saved_tensors
+        dy2 = dy.contiguous()
+        M = dy2.shape[0]
+        P = -(-M // 128)
+        part = torch.empty(P * w2.shape[0], dtype=torch.float32, device=dy2.device)
+        dh = gemm.mm_epi(dy2, w2.t(), 3, h, colsum_part=part)
+        db1 = torch.empty(w2.shape[0], dtype=dy2.dtype, device=dy2.device)
+        fused.colsum_finish_parts(part, db1, P, accumulate=False)
+        dw2 = matmul(g.t(), dy2)
+        db2 = fused.colsum(dy2).to(dy2.dtype)
+        dw1 = matmul(x2.t(), dh)
+        dx = matmul(dh, w1.t()) if ctx.needs_input_grad[0] else None
+        return dx, dw1, db1, dw2, db2, None
+
+
+def ffn_gelu_ok(x2, w1, b1, w2, b2):
+    """Contract of _FFNGeluFn: bf16 GPU operands, 2-D k-contiguous input, both biases, the fused-
+    epilogue GEMM shapes of fc1 and of the fc2 data gradient."""
+    from . import gemm
+    ts = (x2, w1, b1, w2, b2)
+    if any(not isinstance(t, torch.Tensor) or t.dtype != torch.bfloat16 or not t.is_cuda for t in ts):
+        return False
+    if x2.dim() != 2 or w1.dim() != 2 or w2.dim() != 2 or b1.dim() != 1 or b2.dim() != 1 or not _use(x2, w1):
+        return False
+    F_ = w1.shape[1]
+    if x2.shape[1] != w1.shape[0] or w2.shape[0] != F_ or b1.numel() != F_ or b2.numel() != w2.shape[1]:
+        return False
+    if not (x2.is_contiguous() and b1.is_contiguous() and b2.is_contiguous() and w1.is_contiguous()
+            and w2.is_contiguous()):
+        return False
+    if x2.shape[0] % 8 or F_ % 8 or w2.shape[1] % 8:
+        return False
+    # fc1 with its epilogue, and the fc2 data gradient dy [M, N2] @ W2^T (a transposed view) -> [M, F]
+    return gemm.epi_ok(x2, w1, F_) and bool(N.lib.pa_gemm8_ok(x2.shape[0], F_, w2.shape[1], w2.shape[1], w2.shape[1],
+                                                            F_, 0, 1, 1))
+
+
+def ffn_gelu(x2, w1, b1, w2, b2, approximate=False):
+    return _FFNGeluFn.apply(x2, w1, b1, w2, b2, bool(approximate))
+
+
 def linear(x, w, bias=None):
     """paddle F.linear (W stored [in, out]) outside the training engines."""
     if w.dim() != 2 or x.dim() < 1 or not _use(x, w) or (bias is not None and not _use(x, bias)):

@@ -191,7 +191,7 @@ class OptimizerWithMixedPrecision:
         data-parallel ranks), step unless found, clear, update the dynamic loss scale."""
         if not self._use_scaling:
             self._optimizer.step()
-            self._optimizer.clear_grad()
+            release_grads(self._optimizer)
             return
         params = [p._t for p in (self._params or []) if p._t.requires_grad]
         grads = [t.grad for t in params if t.grad is not None]
@@ -208,7 +208,7 @@ class OptimizerWithMixedPrecision:
         self.found_inf = found
         if not found:
             self._optimizer.step()
-        self._optimizer.clear_grad()
+        release_grads(self._optimizer)
         if self._dynamic:
             cnt = self._counts_t
             update_loss_scaling_(found_t, sc, cnt[0:1], cnt[1:2], self._incr_every, self._decr_every,
@@ -218,6 +218,17 @@ class OptimizerWithMixedPrecision:
                 self._good, self._bad = 0, (self._bad + 1) % max(1, self._decr_every)
             else:
                 self._bad, self._good = 0, (self._good + 1) % max(1, self._incr_every)
+
+
+def release_grads(opt):
+    """End of a static training step: drop the gradients instead of zero-filling them.  A static
+    program's gradients live for one step (the reference's append_backward creates them per step
+    and only for parameters on the loss path), so the next backward assigns fresh ones — no fill
+    kernel per parameter now and no accumulate-add per parameter then."""
+    try:
+        opt.clear_grad(set_to_zero=False)
+    except TypeError:
+        opt.clear_grad()
 
 
 def decorate(optimizer, amp_lists=None, level='O1', dtype='float16', master_weight=None, master_grad=False,

@@ -216,7 +216,8 @@ def _exec_nodes(prog, nodes, env, smap, dev):
             else:
                 loss.backward()
                 n.target.step()
-                n.target.clear_grad()
+                from .amp import release_grads
+                release_grads(n.target)
         elif n.kind == 'backward':
             loss = env[n.args[0].vid]
             loss.backward()

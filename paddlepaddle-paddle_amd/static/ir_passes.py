@@ -21,6 +21,8 @@ Passes (names follow the reference where one exists):
   fused_dropout_add_layernorm     dropout(x) + residual -> layer_norm  ==> one norm kernel each way
   skip_layernorm_fuse_pass        x + residual -> layer_norm           ==> fused add + norm kernel
   layer_norm_fuse_pass            layer_norm                           ==> csrc/norm.hip
+  fuse_gemm_epilogue_pass         addmm -> gelu -> addmm (recorded FFN) ==> GELU and GELU' in the GEMM
+                                  epilogues, forward and backward (training programs)
   fc_fuse_pass                    x @ W + b (-> relu / gelu)           ==> GEMM (+ bias + act kernel)
   softmax_fuse_pass               standalone last-dim softmax           ==> csrc/softmax_xent.hip
   quant_linear_fuse_pass          quantize_linear -> dequantize_linear (activation) + dequantize_linear
@@ -39,7 +41,7 @@ import torch.nn.functional as TF
 from .program import Node, Ref, Const
 
 DEFAULT_PASSES = ('quant_linear_fuse_pass', 'multihead_matmul_fuse_pass_v2', 'fused_dropout_add_layernorm', 'skip_layernorm_fuse_pass',
-                  'layer_norm_fuse_pass', 'fc_fuse_pass', 'softmax_fuse_pass')
+                  'fuse_gemm_epilogue_pass', 'layer_norm_fuse_pass', 'fc_fuse_pass', 'softmax_fuse_pass')
 
 # FLAGS_static_ir_fusion: 'auto' (default: GPU programs), '1' / 'always' (every device, used by the
 # CPU tests of the rewrites), '0' (off)
@@ -204,6 +206,36 @@ def fused_linear(x, w, bias=None, act=None, trans_w=False):
     return fn(y) if fn is not None else y
 
 
+def _replay_addmm(b, x, w):
+    """torch.addmm as the Executor replays a recorded one (static.amp fp8 and GEMM substitutions)."""
+    from .executor import _SUBS, _gemm_subs
+    subs = _SUBS['map']
+    fn = subs.get(torch.addmm, torch.addmm) if subs else torch.addmm
+    fn = _gemm_subs().get(fn, fn)
+    return fn(b, x, w)
+
+
+def fused_ffn(x, w1, b1, w2, b2, approximate='none'):
+    """gelu(x @ W1 + b1) @ W2 + b2 of a recorded feed-forward block (x 2-D).  Training on bf16 GPU
+    operands: one autograd op with the GELU (and its derivative) in the GEMM epilogues
+    (ops.matmul.ffn_gelu; under a static.amp fp8 replay the fp8 form, ops.fp8.fp8_ffn); inference: fc1's epilogue applies the GELU (fused_linear); otherwise
+    exactly the recorded addmm -> gelu -> addmm (with the replay's fp8 / GEMM substitutions)."""
+    from .executor import _SUBS
+    if _SUBS['map'] is not None and _hip(x) and torch.is_grad_enabled():
+        from ..ops import fp8 as F8
+        if _SUBS['map'] is F8.STATIC_SUBS and F8.ffn_ok(x, w1, b1, w2, b2):  # static.amp fp8 replay
+            return F8.fp8_ffn(x, w1, b1, w2, b2, approximate == 'tanh')
+    if _SUBS['map'] is None and _hip(x):
+        from ..ops import matmul as hm
+        if torch.is_grad_enabled() and any(t.requires_grad for t in (x, w1, b1, w2, b2)):
+            if hm.ffn_gelu_ok(x, w1, b1, w2, b2):
+                return hm.ffn_gelu(x, w1, b1, w2, b2, approximate == 'tanh')
+        elif x.dtype == w1.dtype == b1.dtype and x.dtype in (torch.bfloat16, torch.float16):
+            act = 'gelu_tanh' if approximate == 'tanh' else 'gelu'
+            return _replay_addmm(b2, fused_linear(x, w1, b1, act), w2)
+    return _replay_addmm(b2, TF.gelu(_replay_addmm(b1, x, w1), approximate=approximate), w2)
+
+
 def fused_softmax(x, dim=-1):
     if _hip(x) and x.dtype in (torch.bfloat16, torch.float16) and dim in (-1, x.dim() - 1) and x.shape[-1] % 8 == 0:
         from ..ops import softmax as S
@@ -211,7 +243,8 @@ def fused_softmax(x, dim=-1):
     return torch.softmax(x, dim)
 
 
-FUSED_TARGETS = (fused_attention, fused_attention_packed, fused_layer_norm, fused_dropout_add_layer_norm, fused_linear, fused_softmax)
+FUSED_TARGETS = (fused_attention, fused_attention_packed, fused_layer_norm, fused_dropout_add_layer_norm, fused_linear,
+                 fused_softmax, fused_ffn)
 
 
 # ============================================================================ node vocabulary
@@ -825,6 +858,57 @@ def _fc(g, i):
     return body, {tail: node}
 
 
+def _sole_user(g, vid, body):
+    """Index of the single user of ``vid`` (a value private to the chain), else None."""
+    if vid is None or isinstance(vid, (list, tuple)) or vid in g.external:
+        return None
+    uj = list(g.uses.get(vid, ()))
+    return uj[0] if len(uj) == 1 and uj[0] not in body else None
+
+
+def _ffn(g, i):
+    """Recorded feed-forward blocks addmm(b1, x, W1) -> (reshape) -> gelu -> (reshape) ->
+    addmm(b2, ., W2) (nn.Linear -> F.gelu -> nn.Linear) as one fused_ffn node — the reference's
+    training-side fuse_gemm_epilogue_pass (linear + gelu forward, linear_grad + gelu_grad backward)."""
+    n = g.nodes[i]
+    if _kind(n) != 'addmm' or n.kwargs or len(n.args) != 3:
+        return None
+    b1, x, w1 = n.args
+    if not isinstance(x, Ref) or not isinstance(w1, Const) or not isinstance(b1, Const):
+        return None
+    body, cur, approx = [i], _one_out(n), None
+    while True:  # reshapes, then the gelu, then reshapes, then fc2
+        j = _sole_user(g, cur, body)
+        if j is None:
+            return None
+        m = g.nodes[j]
+        k = _kind(m)
+        if not m.args or not isinstance(m.args[0], Ref) or m.args[0].vid != cur:
+            if k == 'addmm' and approx is not None and len(m.args) == 3 and isinstance(m.args[1], Ref) and \
+                    m.args[1].vid == cur and not m.kwargs:
+                break
+            return None
+        if k == 'reshape':
+            pass
+        elif k == 'gelu' and approx is None and m.target is TF.gelu and len(m.args) <= 2:
+            approx = m.args[1] if len(m.args) == 2 else m.kwargs.get('approximate', 'none')
+            if set(m.kwargs) - {'approximate'} or approx not in ('none', 'tanh'):
+                return None
+        else:
+            return None
+        body.append(j)
+        cur = _one_out(m)
+    b2, _, w2 = m.args
+    if not isinstance(w2, Const) or not isinstance(b2, Const):
+        return None
+    body.append(j)
+    if not g.private(body[:-1], users=body[-1:]):
+        return None
+    node = Node('torch', fused_ffn, [x, w1, b1, w2, b2], {'approximate': approx}, _one_out(m),
+                dict(n.meta or {}, fused='fuse_gemm_epilogue_pass'))
+    return body, {j: node}
+
+
 def _softmax(g, i):
     n = g.nodes[i]
     k = _kind(n)
@@ -889,6 +973,7 @@ _PASSES = {
     'multihead_matmul_fuse_pass_v2': _attention,
     'fused_dropout_add_layernorm': lambda g, i: _add_ln(g, i, True),
     'skip_layernorm_fuse_pass': lambda g, i: _add_ln(g, i, False),
+    'fuse_gemm_epilogue_pass': _ffn,
     'layer_norm_fuse_pass': _layer_norm,
     'fc_fuse_pass': _fc,
     'softmax_fuse_pass': _softmax,

@@ -75,7 +75,8 @@ class StaticMinimize:
         else:
             opt = self._plain()
             opt.step()
-            opt.clear_grad()
+            from .amp import release_grads
+            release_grads(opt)
 
     def _allreduce_grads(self):
         """Average the gradients over the data-parallel group in flat buckets (missing gradients

@@ -10,7 +10,7 @@ pytestmark = pytest.mark.gpu
 import paddle  # noqa: E402
 from paddle import static  # noqa: E402
 from paddle.static import ir_passes as IP  # noqa: E402
-from paddle.ops import flash_attn as FA, norm as NORM, fused as FUSED  # noqa: E402
+from paddle.ops import flash_attn as FA, norm as NORM, fused as FUSED, matmul as HM  # noqa: E402
 
 from test_ir_passes import _build, _feed  # noqa: E402
 
@@ -63,8 +63,9 @@ def test_ernie_static_fused_kernels_match_unfused_program():
 
 
 def test_ernie_static_amp_bf16_training_fused():
-    """AMP-O2 bf16 training with dropout: the fused program takes the flash kernel (mask + dropout)
-    and the fused dropout + add + LayerNorm kernels, and trains (finite, decreasing loss)."""
+    """AMP-O2 bf16 training with dropout: the fused program takes the flash kernel (mask + dropout),
+    the fused dropout + add + LayerNorm kernels and the GELU-epilogue FFN op, and trains (finite,
+    decreasing loss)."""
     old = IP.set_mode('auto')
     try:
         paddle.set_device('gpu:0')
@@ -84,14 +85,15 @@ def test_ernie_static_amp_bf16_training_fused():
                 opt.minimize(loss)
             exe = static.Executor(paddle.CUDAPlace(0))
             opt.amp_init(paddle.CUDAPlace(0))
-            with _Count(FA, 'flash_attention_packed_ex') as ca, _Count(FUSED, 'dropout_add_norm') as cd:
+            with _Count(FA, 'flash_attention_packed_ex') as ca, _Count(FUSED, 'dropout_add_norm') as cd, \
+                    _Count(HM, 'ffn_gelu') as cf:
                 losses = [float(np.asarray(exe.run(main, feed=_feed(), fetch_list=[loss])[0]).reshape(-1)[0])
                           for _ in range(8)]
         finally:
             paddle.disable_static()
     finally:
         IP.set_mode(old)
-    assert ca.n == 16 and cd.n == 32, (ca.n, cd.n)
+    assert ca.n == 16 and cd.n == 32 and cf.n == 16, (ca.n, cd.n, cf.n)  # cf: GELU FFNs in the GEMM epilogues
     assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
     assert torch.cuda.is_available()
 

@@ -50,9 +50,10 @@ def fusion_mode():
 
 
 @pytest.mark.parametrize('train,drop,expect', [
-    (False, 0.1, {'multihead_matmul_fuse_pass_v2': 2, 'skip_layernorm_fuse_pass': 5}),
-    (True, 0.1, {'multihead_matmul_fuse_pass_v2': 2, 'fused_dropout_add_layernorm': 4, 'skip_layernorm_fuse_pass': 1}),
-    (True, 0.0, {'multihead_matmul_fuse_pass_v2': 2, 'skip_layernorm_fuse_pass': 5}),
+    (False, 0.1, {'multihead_matmul_fuse_pass_v2': 2, 'skip_layernorm_fuse_pass': 5, 'fuse_gemm_epilogue_pass': 2}),
+    (True, 0.1, {'multihead_matmul_fuse_pass_v2': 2, 'fused_dropout_add_layernorm': 4, 'skip_layernorm_fuse_pass': 1,
+                 'fuse_gemm_epilogue_pass': 2}),
+    (True, 0.0, {'multihead_matmul_fuse_pass_v2': 2, 'skip_layernorm_fuse_pass': 5, 'fuse_gemm_epilogue_pass': 2}),
 ])
 def test_ernie_program_fused_equals_unfused(fusion_mode, train, drop, expect):
     feed = _feed()
