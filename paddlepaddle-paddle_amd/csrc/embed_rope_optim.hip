@@ -28,15 +28,52 @@ __global__ __launch_bounds__(256) void embedding_fwd(const int64_t* __restrict__
 // dw32[ids[i], :] += dy[i, :]  (fp32 accumulation; 256-byte contiguous atomics per wave instruction)
 template <typename T>
 __global__ __launch_bounds__(256) void embedding_bwd(const int64_t* __restrict__ ids, const T* __restrict__ dy,
-                                                     float* __restrict__ dw32, int n, int dim, int64_t vocab) {
+                                                     float* __restrict__ dw32, int n, int dim, int64_t vocab,
+                                                     int64_t pad) {
   const int row = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= n) return;
   int64_t id = ids[row];
-  if (id < 0 || id >= vocab) return;
+  if (id < 0 || id >= vocab || id == pad) return;
   const T* src = dy + (size_t)row * dim;
   float* dst = dw32 + id * dim;
   for (int j = lane; j < dim; j += 64) atomicAdd(dst + j, to_f(src[j]));
+}
+
+// Tiny tables (vocab <= 8: token-type / segment embeddings, where every row of the batch hits one
+// of a few table rows): a thread owns two columns and sums its chunk of rows into per-vocab-row
+// registers (the row's id is wave-uniform), then adds the V partial sums to dw32 — one atomic per
+// (block, table element) instead of one per (batch row, element) on a few hot addresses.
+template <typename T>
+__global__ __launch_bounds__(256) void embedding_bwd_tiny(const int64_t* __restrict__ ids, const T* __restrict__ dy,
+                                                          float* __restrict__ dw32, int n, int dim, int vocab,
+                                                          int64_t pad, int rows_per_block) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 2;
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(n, r0 + rows_per_block);
+  float acc[8][2];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k][0] = acc[k][1] = 0.f;
+  if (c < dim) {
+#pragma unroll 8
+    for (int row = r0; row < r1; ++row) {
+      const int64_t id = ids[row];
+      const T* src = dy + (size_t)row * dim + c;
+      const float v0 = to_f(src[0]), v1 = to_f(src[1]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool hit = id == k && id != pad;
+        acc[k][0] += hit ? v0 : 0.f;
+        acc[k][1] += hit ? v1 : 0.f;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k < vocab && (acc[k][0] != 0.f || acc[k][1] != 0.f)) {
+        atomicAdd(dw32 + (size_t)k * dim + c, acc[k][0]);
+        atomicAdd(dw32 + (size_t)k * dim + c + 1, acc[k][1]);
+      }
+    }
+  }
 }
 
 template <typename T>
@@ -369,11 +406,26 @@ PA_API hipError_t pa_embedding_fwd(const int64_t* ids, const void* w, void* out,
   return hipGetLastError();
 }
 
+PA_API hipError_t pa_embedding_bwd_pad(const int64_t* ids, const void* dy, float* dw32, void* out, int n, int dim,
+                                       long long vocab, int accumulate, long long pad, int dt, hipStream_t st);
+
 // dw32 must be zeroed by the caller (hipMemsetAsync); out (param dtype) = dw32 (+ out if accumulate)
 PA_API hipError_t pa_embedding_bwd(const int64_t* ids, const void* dy, float* dw32, void* out, int n, int dim,
                                    long long vocab, int accumulate, int dt, hipStream_t st) {
+  return pa_embedding_bwd_pad(ids, dy, dw32, out, n, dim, vocab, accumulate, -1, dt, st);
+}
+
+// embedding gradient with a padding row (its gradient stays zero, torch / paddle padding_idx)
+PA_API hipError_t pa_embedding_bwd_pad(const int64_t* ids, const void* dy, float* dw32, void* out, int n, int dim,
+                                       long long vocab, int accumulate, long long pad, int dt, hipStream_t st) {
   PA_DISPATCH_DTYPE(dt, T, {
-    embedding_bwd<T><<<(n + 3) / 4, 256, 0, st>>>(ids, (const T*)dy, dw32, n, dim, vocab);
+    if (vocab <= 8 && dim % 2 == 0) {
+      const int rpb = 128;
+      dim3 grid((dim / 2 + 255) / 256, (n + rpb - 1) / rpb);
+      embedding_bwd_tiny<T><<<grid, 256, 0, st>>>(ids, (const T*)dy, dw32, n, dim, (int)vocab, pad, rpb);
+    } else {
+      embedding_bwd<T><<<(n + 3) / 4, 256, 0, st>>>(ids, (const T*)dy, dw32, n, dim, vocab, pad);
+    }
     if (out != nullptr && (void*)out != (void*)dw32) {
       const long long tot = vocab * dim;
       cast_f32<T><<<grid_for(tot, 256, 256 * 8), 256, 0, st>>>(dw32, (T*)out, tot, accumulate);

@@ -144,8 +144,8 @@ def embedding(x, weight, padding_idx=None, max_norm=None, norm_type=2.0, sparse=
     ids, w = _u(x), _u(weight)
     if padding_idx is not None and padding_idx < 0:
         padding_idx += w.shape[0]
-    if ops.use_hip(w) and ops.use_hip(ids) and padding_idx is None and max_norm is None:
-        return _w(ops.embedding.embedding(ids, w))
+    if ops.use_hip(w) and ops.use_hip(ids) and max_norm is None:
+        return _w(ops.embedding.embedding(ids, w, padding_idx))
     return _w(TF.embedding(ids, w, padding_idx, max_norm, norm_type, scale_grad_by_freq, sparse))
 
 

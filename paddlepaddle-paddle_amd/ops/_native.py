@@ -69,6 +69,7 @@ _SIGS = {
     'pa_dropout_bwd': [P, P, LL, F, U32, U32, I, P],
     'pa_embedding_fwd': [P, P, P, I, I, LL, I, P],
     'pa_embedding_bwd': [P, P, P, P, I, I, LL, I, I, P],
+    'pa_embedding_bwd_pad': [P, P, P, P, I, I, LL, I, LL, I, P],
     'pa_rope': [P, P, P, P, P, I, I, I, I, I, F, I, P],
     'pa_rope_rows': [P, LL, P, LL, P, P, P, I, I, I, I, I, F, I, P],
     'pa_adamw': [P, P, P, P, P, LL, P, F, F, F, F, F, F, F, P, P, I, I, P],

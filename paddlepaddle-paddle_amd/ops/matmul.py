@@ -421,4 +421,10 @@ def static_substitutions():
     return {torch.matmul: matmul, torch.mm: matmul, torch.bmm: matmul,
             torch.Tensor.matmul: _tensor_matmul, torch.Tensor.__matmul__: _tensor_matmul,
             torch.addmm: addmm, torch.einsum: einsum,
-            torch.nn.functional.linear: lambda x, w, b=None: linear(x, w.t(), b)}
+            torch.nn.functional.linear: lambda x, w, b=None: linear(x, w.t(), b),
+            torch.nn.functional.embedding: _embedding_sub}
+
+
+def _embedding_sub(*a, **k):
+    from .embedding import static_embedding
+    return static_embedding(*a, **k)

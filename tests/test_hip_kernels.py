@@ -184,6 +184,28 @@ def test_embedding():
     _close(w.grad, ref, 5e-2, 1e-2, 'emb grad')
 
 
+@pytest.mark.parametrize("V,D,pad", [(4, 768, None), (2, 768, 0), (512, 768, None), (40000, 768, 0)])
+def test_embedding_padding_and_small_tables(V, D, pad):
+    """padding_idx rows get no gradient; tiny tables (V <= 8: token types) reduce in registers per
+    column, larger ones by atomics per row; vs an fp32 index_add reference."""
+    torch.manual_seed(0)
+    w = (torch.randn(V, D, device=DEV) * 0.02).bfloat16().requires_grad_()
+    ids = torch.randint(0, V, (64, 512), device=DEV)
+    if pad is not None:
+        ids[:, 400:] = pad
+    y = ops.embedding.embedding(ids, w, pad)
+    _close(y, w.detach()[ids], 0, name='emb fwd')
+    g = torch.randn(64, 512, D, device=DEV, dtype=torch.bfloat16)
+    y.backward(g)
+    ref = torch.zeros(V, D, device=DEV).index_add_(0, ids.reshape(-1), g.reshape(-1, D).float())
+    if pad is not None:
+        ref[pad] = 0
+    err = ((w.grad.float() - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
+    if pad is not None:
+        assert w.grad[pad].abs().max().item() == 0
+
+
 @pytest.mark.parametrize("interleaved", [False, True])
 def test_rope(interleaved):
     from paddle.incubate.nn.functional import _rope_ref
