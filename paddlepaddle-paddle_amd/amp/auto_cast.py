@@ -25,6 +25,7 @@ from ..core import dtype as _dt
 from ..core import amp_dispatch as _disp
 from ..core.place import current_device
 from .amp_lists import _update_list
+from ..core.tensor import register_param as _register_param
 
 _state = {'enable': False, 'level': 'O0', 'dtype': torch.float16, 'use_promote': True}
 
@@ -126,6 +127,7 @@ def decorate(models, optimizers=None, level='O1', dtype='float16', master_weight
                     req = p._t.requires_grad
                     with torch.no_grad():
                         p._t = p._t.detach().to(dt).requires_grad_(req)
+                        _register_param(p)
                     if master_grad:
                         p.__dict__['_master_grad'] = True
         m.__dict__['_casted_by_pure_fp16'] = True

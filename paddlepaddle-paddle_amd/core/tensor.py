@@ -431,6 +431,12 @@ def _print_precision():
 _PARAMS = weakref.WeakValueDictionary()  # id(storage tensor) -> Parameter (static programs map consts back)
 
 
+def register_param(p):
+    """Re-key a Parameter after its storage tensor was replaced (dtype casts of AMP O2 /
+    Layer.to): kernels that accumulate gradients into flat slots look parameters up by tensor."""
+    _PARAMS[id(p._t)] = p
+
+
 class Parameter(Tensor):
     """EagerParamBase: a trainable leaf (reference: python/paddle/base/framework.py EagerParamBase)."""
     __slots__ = ()

@@ -17,6 +17,7 @@ from ...core.place import current_device, to_device
 from ...framework.param_attr import ParamAttr
 from ...utils import unique_name
 from .. import initializer as I
+from ...core.tensor import register_param as _register_param
 
 
 def _camel_to_snake(name):
@@ -340,6 +341,7 @@ class Layer:
                     new = fn(p._t.detach())
                 req = p._t.requires_grad
                 p._t = new.detach().requires_grad_(req)
+                _register_param(p)
             for n, b in l._buffers.items():
                 if b is None or (floating_only and not b._t.is_floating_point()):
                     continue

@@ -140,6 +140,27 @@ def _colsum(dy2):
     return dy2.float().sum(0)
 
 
+def _slot_fp8_wgrad(a, b, sa, sb, w):
+    """W.grad += sa*sb * a @ b^T by the fp8 GEMM (beta = 1) straight into w's flat gradient slot;
+    False when w has no bf16 slot or the operands are outside the kernel contract."""
+    from .matmul import _param_of
+    from .gemm import hip_fp8_ok, hip_fp8_mm
+    from ..parallel.flat_buffer import flat_grad_slot, notify_grad_ready
+    p = _param_of(w) if a.is_cuda else None
+    gw = flat_grad_slot(p) if p is not None else None
+    if gw is None or gw.dtype != torch.bfloat16 or not gw.is_contiguous() or gw.shape != w.shape or \
+            not hip_fp8_ok(a, b):
+        return False
+    hip_fp8_mm(a, b, scale_a=sa, scale_b=sb, out=gw, beta=1.0)
+    notify_grad_ready(p)
+    return True
+
+
+def _slot_bias(dy2, b, part=None, nparts=0):
+    from .matmul import slot_bgrad
+    return b is not None and dy2.is_cuda and slot_bgrad(dy2, b, part, nparts)
+
+
 class FP8State:
     """The three metas of one fp8 Linear (kept on the weight Parameter)."""
 
@@ -163,6 +184,7 @@ class _FP8Linear(torch.autograd.Function):
         ctx.save_for_backward(xqt, wq, sx, sw)
         ctx.st, ctx.xshape, ctx.has_b, ctx.wdt, ctx.xdt = st, x.shape, b is not None, w.dtype, x.dtype
         ctx.bdt = b.dtype if b is not None else None
+        ctx.w_t, ctx.b_t = w, b
         return y.reshape(*x.shape[:-1], Nout)
 
     @staticmethod
@@ -176,9 +198,9 @@ class _FP8Linear(torch.autograd.Function):
         dx = dw = db = None
         if need_dx:
             dx = fp8_mm(gq, wq, sg, sw).reshape(ctx.xshape).to(ctx.xdt)
-        if need_dw:
+        if need_dw and not _slot_fp8_wgrad(xqt, gqt, sx, sg, ctx.w_t):
             dw = fp8_mm(xqt, gqt, sx, sg).to(ctx.wdt)
-        if ctx.has_b and ctx.needs_input_grad[2]:
+        if ctx.has_b and ctx.needs_input_grad[2] and not _slot_bias(dy2.contiguous(), ctx.b_t):
             db = _colsum(dy2).to(ctx.bdt)
         return dx, dw, db, None
 
@@ -241,6 +263,7 @@ class _FP8FFN(torch.autograd.Function):
         ctx.save_for_backward(xqt, w1q, gqt, w2q, h, sx, sw1, sg, sw2)
         ctx.st = (st1, st2)
         ctx.dt = (x2.dtype, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
+        ctx.params = (w1, b1, w2, b2)
         return y
 
     @staticmethod
@@ -255,13 +278,16 @@ class _FP8FFN(torch.autograd.Function):
         part = torch.empty(P * w2q.shape[0], dtype=torch.float32, device=dy2.device)
         dh = _fp8_epi(dq, w2q, sd, sw2, 4, h, bias=part)
         from . import fused
-        db1 = torch.empty(w2q.shape[0], dtype=b1dt, device=dy2.device)
-        fused.colsum_finish_parts(part, db1, P, accumulate=False)
-        dw2 = fp8_mm(gqt, dqt, sg, sd).to(w2dt)
-        db2 = _colsum(dy2).to(b2dt)
+        w1, b1, w2, b2 = ctx.params
+        db1 = None
+        if not _slot_bias(dy2, b1, part, P):
+            db1 = torch.empty(w2q.shape[0], dtype=b1dt, device=dy2.device)
+            fused.colsum_finish_parts(part, db1, P, accumulate=False)
+        dw2 = None if _slot_fp8_wgrad(gqt, dqt, sg, sd, w2) else fp8_mm(gqt, dqt, sg, sd).to(w2dt)
+        db2 = None if _slot_bias(dy2, b2) else _colsum(dy2).to(b2dt)
         hq, hqt, shh = st1.g.cast(dh)
         dx = fp8_mm(hq, w1q, shh, sw1).to(xdt) if ctx.needs_input_grad[0] else None
-        dw1 = fp8_mm(xqt, hqt, sx, shh).to(w1dt)
+        dw1 = None if _slot_fp8_wgrad(xqt, hqt, sx, shh, w1) else fp8_mm(xqt, hqt, sx, shh).to(w1dt)
         return dx, dw1, db1, dw2, db2, None, None, None
 
 

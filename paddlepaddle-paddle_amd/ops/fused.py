@@ -137,6 +137,7 @@ class _DropAddNorm(torch.autograd.Function):
         ctx.seed, ctx.off, ctx.p, ctx.rms, ctx.boxes = seed, off, p, rms, boxes
         ctx.has_b, ctx.has_xb = b is not None, xb is not None
         ctx.b_t = b
+        ctx.set_materialize_grads(False)  # an unused sum output (post-LN blocks) costs no zero tensor
         return y, s
 
     @staticmethod
@@ -144,7 +145,7 @@ class _DropAddNorm(torch.autograd.Function):
         s, w, mean, rstd, xb = ctx.saved_tensors
         cols = s.shape[-1]
         rows = s.numel() // cols
-        dy = dy.contiguous()
+        dy = dy.contiguous() if dy is not None else torch.zeros_like(s)
         ds = ds.contiguous() if ds is not None else None
         dres, dx = torch.empty_like(s), torch.empty_like(s)
         np_ = N.lib.pa_norm_bwd_nparts(rows)

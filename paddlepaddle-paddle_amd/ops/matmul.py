@@ -208,6 +208,44 @@ def matmul(a, b):
     return torch.matmul(a, b) if y is None else y
 
 
+def _param_of(t):
+    from ..core.tensor import _PARAMS
+    p = _PARAMS.get(id(t))
+    return p if p is not None and p._t is t else None
+
+
+def slot_wgrad(x2, g2, w):
+    """W.grad += x2^T @ g2 written by the weight-gradient GEMM (beta = 1) straight into w's flat
+    gradient slot (multi-tensor optimizers keep gradients in flat buffers): no AccumulateGrad add
+    pass.  False when w has no slot / the kernel contract fails (the caller returns the gradient)."""
+    from ..parallel.flat_buffer import flat_grad_slot, notify_grad_ready
+    p = _param_of(w)
+    gw = flat_grad_slot(p) if p is not None else None
+    if gw is None or gw.shape != w.shape or not gemm.wgrad_accumulate(x2, g2, gw):
+        return False
+    notify_grad_ready(p)
+    return True
+
+
+def slot_bgrad(g2, b, part=None, nparts=0):
+    """b.grad += column sums of g2 (or the finish of ``nparts`` fp32 partial rows ``part``) in b's
+    flat gradient slot; False when b has no slot."""
+    from ..parallel.flat_buffer import flat_grad_slot, notify_grad_ready
+    from . import fused
+    p = _param_of(b)
+    gb = flat_grad_slot(p) if p is not None else None
+    if gb is None or gb.numel() != b.numel() or not gb.is_contiguous():
+        return False
+    if part is not None:
+        fused.colsum_finish_parts(part, gb, nparts, accumulate=True)
+    elif fused.colsum_ok(g2):
+        fused.colsum(g2, gb, accumulate=True)
+    else:
+        return False
+    notify_grad_ready(p)
+    return True
+
+
 class _LinearFn(torch.autograd.Function):
     """y = x @ W + b (W [in, out]) with all three GEMMs hand-written (the training-engine form,
     ops.linear, accumulates into flat gradient buffers; this one returns gradients)."""
@@ -221,6 +259,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x2, w)
         ctx.xshape = x.shape
         ctx.has_bias = bias is not None
+        ctx.bias_t = bias
         return y.view(*x.shape[:-1], w.shape[1])
 
     @staticmethod
@@ -228,11 +267,15 @@ class _LinearFn(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         g2 = g.reshape(-1, g.shape[-1])
         dx = matmul(g2, w.t()).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
-        dw = matmul(x2.t(), g2) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1] and not slot_wgrad(x2, g2, w):
+            dw = matmul(x2.t(), g2)
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             from . import fused
-            db = fused.colsum(g2.contiguous()).to(g2.dtype) if fused.colsum_ok(g2.contiguous()) else g2.sum(0)
+            g2c = g2.contiguous()
+            if not slot_bgrad(g2c, ctx.bias_t):
+                db = fused.colsum(g2c).to(g2.dtype) if fused.colsum_ok(g2c) else g2.sum(0)
         return dx, dw, db
 
 
@@ -254,6 +297,7 @@ class _FFNGeluFn(torch.autograd.Function):
         if y is None:
             y = torch.addmm(b2, g, w2)
         ctx.save_for_backward(x2, w1, w2, h, g)
+        ctx.biases = (b1, b2)
         return y
 
     @staticmethod
@@ -265,11 +309,14 @@ class _FFNGeluFn(torch.autograd.Function):
         P = -(-M // 128)
         part = torch.empty(P * w2.shape[0], dtype=torch.float32, device=dy2.device)
         dh = gemm.mm_epi(dy2, w2.t(), 3, h, colsum_part=part)
-        db1 = torch.empty(w2.shape[0], dtype=dy2.dtype, device=dy2.device)
-        fused.colsum_finish_parts(part, db1, P, accumulate=False)
-        dw2 = matmul(g.t(), dy2)
-        db2 = fused.colsum(dy2).to(dy2.dtype)
-        dw1 = matmul(x2.t(), dh)
+        b1, b2 = ctx.biases
+        db1 = None
+        if not slot_bgrad(None, b1, part, P):
+            db1 = torch.empty(w2.shape[0], dtype=dy2.dtype, device=dy2.device)
+            fused.colsum_finish_parts(part, db1, P, accumulate=False)
+        dw2 = None if slot_wgrad(g, dy2, w2) else matmul(g.t(), dy2)
+        db2 = None if slot_bgrad(dy2, b2) else fused.colsum(dy2).to(dy2.dtype)
+        dw1 = None if slot_wgrad(x2, dh, w1) else matmul(x2.t(), dh)
         dx = matmul(dh, w1.t()) if ctx.needs_input_grad[0] else None
         return dx, dw1, db1, dw2, db2, None
 

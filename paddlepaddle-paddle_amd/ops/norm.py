@@ -92,11 +92,14 @@ class _AddNorm(torch.autograd.Function):
         y, s, mean, rstd = _fwd(x, r, w, b, eps, rms)
         ctx.save_for_backward(s, w, mean, rstd)
         ctx.rms, ctx.has_b = rms, b is not None
+        ctx.set_materialize_grads(False)  # an unused sum output (post-LN blocks) costs no zero tensor
         return y, s
 
     @staticmethod
     def backward(ctx, dy, ds):
         s, w, mean, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(s)
         dx, dw, db = _bwd(dy, s, w, mean, rstd, ds, ctx.rms, ctx.has_b)
         return dx, dx, dw, db, None, None
 

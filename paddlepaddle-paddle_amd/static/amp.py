@@ -22,6 +22,7 @@ import torch
 
 from ..core import dtype as _dt
 from ..amp.amp_lists import white_list as _white_list, black_list as _black_list
+from ..core.tensor import register_param as _register_param
 
 
 class AutoMixedPrecisionLists:
@@ -66,6 +67,7 @@ def cast_parameters_to_fp16(place=None, program=None, scope=None, to_fp16_var_na
         req = t.requires_grad
         with torch.no_grad():
             p._t = t.detach().to(dtype).requires_grad_(req)
+        _register_param(p)
         n += 1
     return n
 

@@ -19,7 +19,7 @@ def main():
         step()
     torch.cuda.synchronize()
     from torch.profiler import profile, ProfilerActivity
-    with profile(activities=[ProfilerActivity.CPU], record_shapes=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU], record_shapes=True, with_stack=True) as prof:
         step()
         torch.cuda.synchronize()
     keys = ('aten::add', 'aten::add_', 'aten::fill_', 'aten::zero_', 'aten::copy_', 'aten::zeros', 'aten::mul',
@@ -28,6 +28,10 @@ def main():
     rows.sort(key=lambda e: -e.count)
     for e in rows[:40]:
         print(f"{e.key:14s} x{e.count:4d}  {str(e.input_shapes)[:150]}")
+    print("--- stacks of the add_ calls")
+    for e in prof.key_averages(group_by_stack_n=6):
+        if e.key in ('aten::add_', 'aten::zero_', 'aten::fill_'):
+            print(f"{e.key} x{e.count}:", " <- ".join(str(f) for f in e.stack[:6]))
 
 
 if __name__ == '__main__':
