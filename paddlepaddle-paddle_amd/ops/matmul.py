@@ -73,6 +73,50 @@ def _bstride(t, nb):
     return 0 if st is None else st
 
 
+# Per-problem choice between the hand-written kernel and the library for PLAIN GEMMs (no fused
+# epilogue beyond a bias): measured once per (shape, layout, dtype) outside stream capture, the
+# library taken only when it is >= 2 % faster (reference: the matmul autotune cache of
+# paddle/phi/kernels/autotune/ behind paddle.incubate.autotune).  Off in multi-rank jobs, where
+# replicated computations must pick the same kernel on every rank (PADDLE_AMD_GEMM_AUTOTUNE=0: off).
+_TUNE = {'on': os.environ.get('PADDLE_AMD_GEMM_AUTOTUNE', '1') != '0', 'cache': {}, 'margin': 1.02}
+
+
+def _time_ms(fn, reps=10):
+    for _ in range(2):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def _tune_off():
+    if not _TUNE['on'] or torch.cuda.is_current_stream_capturing():
+        return True
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def _tuned(key, hip_fn, lib_fn):
+    """hip_fn() or lib_fn(), whichever measured faster for ``key`` (hip_fn when tuning is off or
+    the problem was first seen inside a capture)."""
+    c = _TUNE['cache'].get(key)
+    if c is None:
+        if _tune_off():
+            return hip_fn()
+        th, tl = _time_ms(hip_fn), _time_ms(lib_fn)
+        c = _TUNE['cache'][key] = 'lib' if tl * _TUNE['margin'] < th else 'hip'
+    return hip_fn() if c == 'hip' else lib_fn()
+
+
+def tuned_choices():
+    """{problem key: 'hip' | 'lib'} of the GEMM autotune cache."""
+    return dict(_TUNE['cache'])
+
+
 def _mm2d(a, b, bias=None, alpha=1.0):
     """a [M,K] @ b [K,N] (+ bias) for bf16 / fp16 on the hand-written kernels; None if outside."""
     if a.data_ptr() % 16 or b.data_ptr() % 16:
@@ -85,7 +129,9 @@ def _mm2d(a, b, bias=None, alpha=1.0):
             if r is not None:
                 return r
         if gemm.hip_mm_ok(a, b, 1) and (bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous())):
-            return gemm.mm(a, b, bias=bias)
+            key = ('mm', a.shape, b.shape, a.stride(), b.stride(), bias is not None)
+            return _tuned(key, lambda: gemm.mm(a, b, bias=bias),
+                          lambda: torch.addmm(bias, a, b) if bias is not None else torch.mm(a, b))
         return None
     r = _gemmx(a.unsqueeze(0), b.unsqueeze(0), 1, bias=bias, alpha=alpha)
     return None if r is None else r[0]
@@ -151,7 +197,8 @@ def _matmul_raw(a, b):
         sb_ = K * N_
     a3 = ae.as_strided((batch if sa else 1, M, K), (sa if sa else 0, ae.stride(-2), ae.stride(-1)))
     b3 = be.as_strided((batch if sb_ else 1, K, N_), (sb_ if sb_ else 0, be.stride(-2), be.stride(-1)))
-    y = _gemmx(a3, b3, batch)
+    y = _tuned(('bmm', a3.shape, b3.shape, a3.stride(), b3.stride(), a3.dtype),
+               lambda: _gemmx(a3, b3, batch), lambda: torch.matmul(ae, be).reshape(batch, M, N_))
     return None if y is None else y.view(*bs, M, N_)
 
 

@@ -400,3 +400,27 @@ def test_gemm_act_epilogue(act, M, K, N, trans):
            'gelu_tanh': torch.nn.functional.gelu(h, approximate='tanh')}[act]
     err = (y.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-2, err
+
+
+def test_gemm_autotune_cache_picks_faster_and_matches(monkeypatch):
+    """Per-shape GEMM autotune (ops/matmul.py _tuned): a plain matmul is measured once on the
+    hand-written kernel and the library, the choice is cached, and either choice matches fp32."""
+    from paddle.ops import matmul as HM
+    monkeypatch.setitem(HM._TUNE, 'on', True)
+    monkeypatch.setitem(HM._TUNE, 'cache', {})
+    torch.manual_seed(0)
+    a = torch.randn(2048, 1024, device='cuda').bfloat16()
+    b = torch.randn(1024, 3072, device='cuda').bfloat16()
+    y = HM.matmul(a, b)
+    y2 = HM.matmul(a, b)
+    ch = HM.tuned_choices()
+    assert len(ch) == 1 and list(ch.values())[0] in ('hip', 'lib'), ch
+    ref = a.float() @ b.float()
+    for t in (y, y2):
+        err = ((t.float() - ref).norm() / ref.norm()).item()
+        assert err < 1e-2, err
+    q, k = torch.randn(4, 8, 256, 64, device='cuda').bfloat16(), torch.randn(4, 8, 256, 64, device='cuda').bfloat16()
+    s = HM.matmul(q, k.transpose(-1, -2))
+    assert any(key[0] == 'bmm' for key in HM.tuned_choices())
+    rs = q.float() @ k.float().transpose(-1, -2)
+    assert ((s.float() - rs).norm() / rs.norm()).item() < 1e-2

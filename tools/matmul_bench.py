@@ -45,13 +45,18 @@ def main():
         x, w = r(8, 2048, 1024, dt=dt), r(1024, 4096, dt=dt)
         cases.append((f'einsum bsh,hd {str(dt)[6:]}', 2.0 * 8 * 2048 * 1024 * 4096,
                       lambda x=x, w=w: hm.einsum('bsh,hd->bsd', x, w), lambda x=x, w=w: torch.einsum('bsh,hd->bsd', x, w)))
+    if os.environ.get('PADDLE_AMD_GEMM_AUTOTUNE', '1') != '0':
+        hm._TUNE['on'] = True  # routed paddle.matmul: per-shape choice of kernel vs library
     with torch.no_grad():
         for name, fl, fh, ft in cases:
+            before = set(hm.tuned_choices())
+            fh()
+            picks = [v for k, v in hm.tuned_choices().items() if k not in before]
             th, tt = bench(fh), bench(ft)
             th2 = bench(fh)
             th = min(th, th2)
-            print(f"{name:44s} hip {th*1e6:9.1f} us {fl/th/1e12:6.0f} TF | library {tt*1e6:9.1f} us "
-                  f"{fl/tt/1e12:6.0f} TF | {tt/th:4.2f}x", flush=True)
+            print(f"{name:44s} paddle {th*1e6:9.1f} us {fl/th/1e12:6.0f} TF | library {tt*1e6:9.1f} us "
+                  f"{fl/tt/1e12:6.0f} TF | {tt/th:4.2f}x  autotune: {','.join(picks) or 'hip'}", flush=True)
 
 
 if __name__ == '__main__':
