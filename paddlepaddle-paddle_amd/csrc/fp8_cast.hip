@@ -22,42 +22,12 @@
 // the tile (byte reads: 4 lanes share a dword, conflict free) and stores them as 4 x 16-B
 // chunks of the q^T row — every q / q^T row segment a wave writes is a whole 128-B line.
 // Edge tiles take the guarded element path.
-#include "common.h"
+#include "fp8_util.h"
 
 namespace pa {
 namespace f8 {
 
 constexpr int T = 128;
-
-template <int FMT>
-__device__ __forceinline__ float fmax_of() { return FMT == 0 ? 448.f : 57344.f; }
-
-// two floats -> two fp8 bytes (low 16 bits of the result), saturating (clamped before the cvt)
-template <int FMT>
-__device__ __forceinline__ uint32_t cvt2(float a, float b) {
-  const float m = fmax_of<FMT>();
-  a = fminf(fmaxf(a, -m), m);
-  b = fminf(fmaxf(b, -m), m);
-  if constexpr (FMT == 0)
-    return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false) & 0xFFFFu;
-  else
-    return (uint32_t)__builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false) & 0xFFFFu;
-}
-
-__device__ __forceinline__ float scale_from_hist(const float* __restrict__ hist, int L, int cur, float fmax,
-                                                 float margin_mul) {
-  float am = 0.f;
-  const int nxt = (cur + 1) % L;
-  for (int j = 0; j < L; ++j)
-    if (j != cur && j != nxt) am = fmaxf(am, hist[j]);
-  if (!(am > 0.f) || !isfinite(am)) return 1.f;
-  const float s = fmax / am * margin_mul;
-  return isfinite(s) ? s : 1.f;
-}
-
-__device__ __forceinline__ void atomic_max_pos(float* addr, float v) {
-  atomicMax(reinterpret_cast<unsigned int*>(addr), __float_as_uint(v));
-}
 
 template <int FMT>
 __global__ __launch_bounds__(256) void cast_transpose_kernel(const bf16_t* __restrict__ x, int R, int C, long long ldx,
@@ -279,6 +249,32 @@ PA_API int pa_fp8_cast_transpose(const void* x, int R, int C, long long ldx, voi
   else
     f8::cast_transpose_kernel<1><<<grid, 256, 0, st>>>((const bf16_t*)x, R, C, ldx, (uint8_t*)q, (uint8_t*)qt,
                                                          (float*)hist, L, cur, (float*)scale_inv, margin_mul);
+  return (int)hipGetLastError();
+}
+
+namespace pa {
+namespace f8 {
+// The delayed-scaling bookkeeping of one cast, for producers that quantise inside their own
+// epilogue (gemm8x.hip pa_gemm8_fp8_epi_q): scale from the history (cur / cur+1 excluded, as in
+// the cast kernels), its inverse for the consuming GEMM, and the next slot zeroed.
+__global__ void scale_prep_kernel(float* __restrict__ hist, int L, int cur, float fmax, float margin_mul,
+                                  float* __restrict__ scale, float* __restrict__ scale_inv) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const float s = scale_from_hist(hist, L, cur, fmax, margin_mul);
+    scale[0] = s;
+    scale_inv[0] = 1.f / s;
+    hist[(cur + 1) % L] = 0.f;
+  }
+}
+}  // namespace f8
+}  // namespace pa
+
+PA_API int pa_fp8_scale_prep(void* hist, int L, int cur, int fmt, float margin_mul, void* scale, void* scale_inv,
+                             hipStream_t st) {
+  if (L < 3 || cur < 0 || cur >= L || fmt < 0 || fmt > 1 || !hist || !scale || !scale_inv)
+    return (int)hipErrorInvalidValue;
+  pa::f8::scale_prep_kernel<<<1, 64, 0, st>>>((float*)hist, L, cur, fmt == 0 ? 448.f : 57344.f, margin_mul,
+                                              (float*)scale, (float*)scale_inv);
   return (int)hipGetLastError();
 }
 

@@ -36,6 +36,7 @@
 //    consecutive output columns (8-byte stores, 4-wide bias reads).
 //  * XCD-aware grouped tile order (blocks b and b+8 share an XCD L2).
 #include "common.h"
+#include "fp8_util.h"
 
 namespace pa {
 namespace g8 {
@@ -420,6 +421,8 @@ __device__ __forceinline__ int stile(int r, int c) { return r * 512 + ((c ^ (r &
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) char lds_char;
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
 
 // global [rows of the tile] -> LDS tile.  Wave w moves rows 32w .. 32w + 31, two per instruction.
 __device__ __forceinline__ void tile_in(const uint16_t* __restrict__ src, long long ld, int m0, int n0, int M, int N,
@@ -1265,13 +1268,167 @@ __global__ __launch_bounds__(512, 1) void gemm9_kernel(const char* __restrict__ 
 }
 
 
+// fp8-output form of the wave-staged epilogue (fp8 feed-forward blocks, ops/fp8.py _FP8FFN):
+//   EPI 9 (fc1: h = s*acc + bias, out = gelu(h), aux = gelu'(h)) with out quantised to e4m3;
+//   EPI 4 (fc2 data gradient: out = s*acc * aux, column partial sums of out into ``bias``) with
+//   out quantised to e5m2.
+// The bf16 ``out`` is never written: the tile goes out as fp8 q [M][ldq] AND its transpose
+// qt [N][M] (the two images an fp8 Linear needs), quantised with the delayed scale *scale_p
+// (pa_fp8_scale_prep ran the cast's bookkeeping), and the tile's amax is folded into *amax_p —
+// the separate cast + transpose pass over the bf16 tensor disappears.  Per half (64 rows x 64
+// columns) the fp8 bytes are staged as a [64][64 B] LDS tile, stored row-wise (16 B per lane)
+// and gathered column-wise for qt (16 B per lane).  Contract: M % 16 == 0, N % 16 == 0.
+template <int EPI, int FMT>
+__device__ __forceinline__ void epilogue_wstaged_q(const f32x4 (&acc)[8][4], uint8_t* __restrict__ q,
+                                                   float* __restrict__ ws, const uint16_t* __restrict__ bias, int M,
+                                                   int N, long long ldq, float alpha, uint8_t* __restrict__ qt,
+                                                   const float* __restrict__ scale_p, float* __restrict__ amax_p,
+                                                   int mb, int nb, int lane, lds_char* region) {
+  static_assert(EPI == 9 || EPI == 4, "fp8-output staged epilogue: EPI 9 / 4");
+  constexpr bool AUX_IN = EPI == 4;
+  const int g = lane >> 4;
+  const bool upper = (g & 1) != 0;
+  lds_char* reg_c = region;         // EPI 4: aux input half;  EPI 9: the fp8 tile
+  lds_char* reg_a = region + 8192;  // EPI 9: gelu' half;        EPI 4: the fp8 tile
+  lds_char* tq = AUX_IN ? reg_a : reg_c;
+  const float sc = scale_p[0];
+  float am = 0.f;
+  float cs[2][8];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[p][e] = 0.f;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int rb = mb + half * 64;
+    if (AUX_IN) {
+      u32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = 8 * j + (lane >> 3), c = lane & 7;
+        const int m = min(rb + r, M - 1), n = min(nb + c * 8, N - 8);
+        v[j] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(ws) + (long long)m * ldq + n);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) *(lds_u32x4*)(reg_c + wtile(8 * j + (lane >> 3), lane & 7)) = v[j];
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int n = nb + (upper ? 16 * (2 * p + 1) + 4 * (g - 1) : 16 * (2 * p) + 4 * g);
+      const int ch = (n - nb) >> 3;
+      float bb[8];
+      if (!AUX_IN && bias != nullptr && n < N) load_f<bf16_t, 8>(reinterpret_cast<const bf16_t*>(bias + n), bb);
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int i = half * 4 + ii;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float lo = acc[i][2 * p][e], hi = acc[i][2 * p + 1][e];
+          asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(lo), "+v"(hi));
+          v[e] = lo * alpha;
+          v[4 + e] = hi * alpha;
+        }
+        const int r = ii * 16 + (lane & 15);
+        const bool ok = rb + r < M && n < N;
+        if constexpr (AUX_IN) {
+          const Pack<bf16_t, 8> hv = __builtin_bit_cast(Pack<bf16_t, 8>, *(const lds_u32x4*)(reg_c + wtile(r, ch)));
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= (float)hv.v[e];
+          if (ok) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cs[p][e] += v[e];
+          }
+        } else {
+          if (bias != nullptr) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += bb[e];
+          }
+          float d[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) gelu_erf_fdf(v[e], v[e], d[e]);
+          *(lds_u32x4*)(reg_a + wtile(r, ch)) = pack_bf16x8(d);
+        }
+        if (ok) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(v[e]));
+        }
+        const uint32_t w0 = f8::cvt2<FMT>(v[0] * sc, v[1] * sc) | (f8::cvt2<FMT>(v[2] * sc, v[3] * sc) << 16);
+        const uint32_t w1 = f8::cvt2<FMT>(v[4] * sc, v[5] * sc) | (f8::cvt2<FMT>(v[6] * sc, v[7] * sc) << 16);
+        *(lds_u32x2*)(tq + r * 64 + ch * 8) = u32x2{w0, w1};
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if constexpr (!AUX_IN) {  // the gelu' half, row-wise (as the bf16 epilogue stores it)
+      u32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = *(const lds_u32x4*)(reg_a + wtile(8 * j + (lane >> 3), lane & 7));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = rb + 8 * j + (lane >> 3), n = nb + (lane & 7) * 8;
+        if (m < M && n < N) *reinterpret_cast<u32x4*>(reinterpret_cast<uint16_t*>(ws) + (long long)m * ldq + n) = v[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // q rows: 64 rows x 64 B, 16 B per lane
+      const int idx = lane + 64 * j, r = idx >> 2, c16 = idx & 3;
+      const u32x4 v = *(const lds_u32x4*)(tq + r * 64 + c16 * 16);
+      const int m = rb + r, n = nb + c16 * 16;
+      if (m < M && n < N) *reinterpret_cast<u32x4*>(q + (long long)m * ldq + n) = v;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // qt rows: column n of the tile, 16 consecutive rows per lane
+      const int idx = lane + 64 * j, c = idx >> 2, m16 = idx & 3;
+      uint32_t o[4];
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) w |= (uint32_t)(uint8_t)tq[(m16 * 16 + k4 * 4 + t) * 64 + c] << (8 * t);
+        o[k4] = w;
+      }
+      const int n = nb + c, m = rb + m16 * 16;
+      if (n < N && m < M) *reinterpret_cast<u32x4*>(qt + (long long)n * M + m) = u32x4{o[0], o[1], o[2], o[3]};
+    }
+    __builtin_amdgcn_wave_barrier();  // the next half overwrites the LDS tiles after these reads
+  }
+  am = wave_max(am);
+  if (lane == 0) f8::atomic_max_pos(amax_p, am);
+  if constexpr (AUX_IN) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int n = nb + (upper ? 16 * (2 * p + 1) + 4 * (g - 1) : 16 * (2 * p) + 4 * g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        cs[p][e] += __shfl_xor(cs[p][e], 1);
+        cs[p][e] += __shfl_xor(cs[p][e], 2);
+        cs[p][e] += __shfl_xor(cs[p][e], 4);
+        cs[p][e] += __shfl_xor(cs[p][e], 8);
+      }
+      if ((lane & 15) == 0 && n < N && mb < M) {
+        float* dst = reinterpret_cast<float*>(const_cast<uint16_t*>(bias)) + (long long)(mb / 128) * N + n;
+        *reinterpret_cast<float4*>(dst) = make_float4(cs[p][0], cs[p][1], cs[p][2], cs[p][3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(cs[p][4], cs[p][5], cs[p][6], cs[p][7]);
+      }
+    }
+  }
+}
+
+
 // epilogue dispatch of schedule 11 (shared by the float and the int8 accumulator forms)
 template <int EPI, typename T>
 __device__ __forceinline__ void gemm11_epilogue(const f32x4 (&acc)[8][4], uint16_t* __restrict__ C,
                                                 float* __restrict__ ws, const uint16_t* __restrict__ bias, int M, int N,
                                                 long long ldc, float alpha, float beta, int m0, int n0, int wr, int wc,
-                                                int lane, char* smem) {
-  if constexpr (EPI == 1)
+                                                int lane, char* smem, long long x0 = 0, long long x1 = 0,
+                                                long long x2 = 0) {
+  if constexpr (EPI == 210 || EPI == 211)  // fp8-output epilogues: x0 = qt, x1 = scale, x2 = amax slot
+    epilogue_wstaged_q<EPI == 210 ? 9 : 4, EPI == 210 ? 0 : 1>(
+        acc, reinterpret_cast<uint8_t*>(C), ws, bias, M, N, ldc, alpha, reinterpret_cast<uint8_t*>(x0),
+        reinterpret_cast<const float*>(x1), reinterpret_cast<float*>(x2), m0 + wr * 128, n0 + wc * 64, lane,
+        (lds_char*)smem + (wr * 4 + wc) * 16384);
+  else if constexpr (EPI == 1)
     epilogue<EPI>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128, n0 + wc * 64, lane);
   else if constexpr (EPI >= 200)  // wave-local staged epilogue of EPI - 200 (its own instantiation)
     epilogue_wstaged<EPI - 200, typename OutT<T>::type>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0 + wr * 128,
@@ -1468,9 +1625,9 @@ __global__ __launch_bounds__(512, 1) void gemm11_kernel(const char* __restrict__
 #pragma unroll
         for (int r = 0; r < 4; ++r) accf[i][j][r] = (float)acc[i][j][r] * rs * cs[j][r];
     }
-    gemm11_epilogue<EPI, T>(accf, C, ws, bias, M, N, ldc, alpha, beta, m0, n0, wr, wc, lane, smem);
+    gemm11_epilogue<EPI, T>(accf, C, ws, bias, M, N, ldc, alpha, beta, m0, n0, wr, wc, lane, smem, sA, sB, sC);
   } else {
-    gemm11_epilogue<EPI, T>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0, n0, wr, wc, lane, smem);
+    gemm11_epilogue<EPI, T>(acc, C, ws, bias, M, N, ldc, alpha, beta, m0, n0, wr, wc, lane, smem, sA, sB, sC);
   }
 }
 

@@ -150,6 +150,35 @@ PA_API int pa_gemm8_fp8_epi(const void* A, const void* W, void* C, const void* b
   return (int)hipGetLastError();
 }
 
+// The same fp8 FFN GEMMs with the OUTPUT quantised in the epilogue (gemm8_impl.h
+// epilogue_wstaged_q): epi 10 = epi 9 whose gelu(h) leaves as e4m3 q [M][N] + q^T [N][M]; epi 11 =
+// epi 4 whose product leaves as e5m2 q + q^T.  scale: the device quantisation scale
+// (pa_fp8_scale_prep), amax: the history slot receiving this tensor's amax.  No bf16 output.
+// Contract: pa_gemm8_fp8_ok, M % 16 == 0, N % 16 == 0.
+PA_API int pa_gemm8_fp8_epi_q(const void* A, const void* W, void* q, void* qt, const void* bias, void* aux,
+                              const void* scale_a, const void* scale_b, const void* scale, void* amax, int M, int N,
+                              int K, long long lda, long long ldw, float alpha, int fmtA, int epi, hipStream_t st) {
+  using namespace pa::g8;
+  if (!pa_gemm8_fp8_ok(M, N, K, lda, ldw, N) || M % 16 || N % 16 || !q || !qt || !aux || !scale || !amax)
+    return (int)hipErrorInvalidValue;
+  if ((epi == 11 && bias == nullptr) || (epi == 10 && fmtA != 0) || (epi == 11 && fmtA != 1))
+    return (int)hipErrorInvalidValue;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  dim3 grid(tm * tn, 1, 1);
+  const int K2 = K / 2;
+  const long long la = lda / 2, lw = ldw / 2;
+  const long long x0 = (long long)(size_t)qt, x1 = (long long)(size_t)scale, x2 = (long long)(size_t)amax;
+  auto go = [&](auto kern) {
+    kern<<<grid, 512, 0, st>>>((const char*)A, (const char*)W, (uint16_t*)q, (float*)aux, (const uint16_t*)bias, M, N,
+                               K2, la, lw, (long long)N, alpha, 0.f, K2, x0, x1, x2, (const float*)scale_a,
+                               (const float*)scale_b);
+  };
+  if (epi == 10) go(gemm11_kernel<true, true, 210, F8<0, 0>, false>);
+  else if (epi == 11) go(gemm11_kernel<true, true, 211, F8<1, 0>, false>);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
 // Split-K fp8 GEMM (the fp8 Linear weight gradient X^T dY: M x N = in x out features, K = tokens —
 // e.g. 768 x 2304 x 32768 is 27 output tiles for 256 CUs, so the K range is split over gridDim.z
 // slices writing fp32 slabs ws[z][M][N], folded by fp8_splitk_reduce with the dequant scales).

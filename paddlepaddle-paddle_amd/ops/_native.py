@@ -95,6 +95,8 @@ _SIGS = {
     'pa_gemm8_fp8_ok': [I, I, I, LL, LL, LL],
     'pa_gemm8_fp8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, F, I, I, P],
     'pa_gemm8_fp8_epi': [P, P, P, P, P, P, P, I, I, I, LL, LL, LL, F, I, I, I, P],
+    'pa_gemm8_fp8_epi_q': [P, P, P, P, P, P, P, P, P, P, I, I, I, LL, LL, F, I, I, P],
+    'pa_fp8_scale_prep': [P, I, I, I, F, P, P, P],
     'pa_gemm8_i8_ok': [I, I, I, LL, LL, LL],
     'pa_gemm8_i8': [P, P, P, P, P, P, I, I, I, LL, LL, LL, F, P],
     'pa_i8_quant_rows': [P, I, I, LL, P, P, LL, P, I, P],

@@ -73,6 +73,21 @@ class FP8Meta:
         s = _FMAX[self.dtype] / am * self.margin_mul
         return torch.where((am > 0) & torch.isfinite(s), s, torch.ones_like(s))
 
+    def prep_fused(self, device):
+        """Bookkeeping of a cast done inside a producer's epilogue (pa_gemm8_fp8_epi_q): returns
+        (scale, amax slot, dequant scale) device tensors and advances the history like cast().
+        Only once the history is seeded (the first cast measures the exact amax first)."""
+        assert self.calls > 0
+        L, cur = self.L, self.cur
+        sc = torch.empty(1, dtype=torch.float32, device=device)
+        sinv = torch.empty(1, dtype=torch.float32, device=device)
+        N.check(N.lib.pa_fp8_scale_prep(N.ptr(self.hist), L, cur, _FMT[self.dtype], float(self.margin_mul), N.ptr(sc),
+                                        N.ptr(sinv), N.stream()), 'fp8_scale_prep')
+        slot = self.hist[cur:cur + 1]
+        self.cur = (cur + 1) % L
+        self.calls += 1
+        return sc, slot, sinv
+
     def cast(self, x2d, want_q=True, want_qt=True):
         """x2d: [R, C] -> (q [R,C] | None, q^T [C,R] | None, dequant scale (1-elem fp32 tensor))."""
         x2d = x2d if x2d.dtype == torch.bfloat16 else x2d.to(torch.bfloat16)
@@ -235,6 +250,25 @@ def _static_state(w, recipe, key=None):
     return st
 
 
+FUSED_QUANT = True  # fp8 FFN: quantise gelu(h) / dh inside the GEMM epilogues (tests switch it)
+
+
+def _fp8_epi_q(a, w, sa, sb, epi, aux, meta, bias=None):
+    """(q [M,N], q^T [N,M], dequant scale) of epilogue(sa*sb * a @ w^T) quantised to meta's format
+    inside the GEMM (csrc/gemm8x.hip pa_gemm8_fp8_epi_q: epi 10 gelu -> e4m3, 11 dgrad*aux ->
+    e5m2), or None when the history is not seeded yet / outside the contract."""
+    M, N_ = a.shape[0], w.shape[0]
+    if not FUSED_QUANT or meta.calls == 0 or M % 16 or N_ % 16:
+        return None
+    sc, slot, sinv = meta.prep_fused(a.device)
+    q = torch.empty(M, N_, dtype=meta.dtype, device=a.device)
+    qt = torch.empty(N_, M, dtype=meta.dtype, device=a.device)
+    N.check(N.lib.pa_gemm8_fp8_epi_q(N.ptr(a), N.ptr(w), N.ptr(q), N.ptr(qt), N.ptr(bias), N.ptr(aux), N.ptr(sa),
+                                     N.ptr(sb), N.ptr(sc), N.ptr(slot), M, N_, a.shape[1], a.stride(0), w.stride(0),
+                                     1.0, _FMT[a.dtype], int(epi), N.stream()), f'gemm8_fp8_epi_q{epi}')
+    return q, qt, sinv
+
+
 def _fp8_epi(a, w, sa, sb, epi, aux, bias=None):
     """bf16 [M, N] = epilogue(sa*sb * a @ w^T) on the fp8 GEMM (csrc/gemm8x.hip pa_gemm8_fp8_epi)."""
     M, N_ = a.shape[0], w.shape[0]
@@ -256,8 +290,13 @@ class _FP8FFN(torch.autograd.Function):
         xq, xqt, sx = st1.x.cast(x2)
         w1q, w1qt, sw1 = st1.w.cast(w1)
         h = torch.empty(x2.shape[0], w1.shape[1], dtype=torch.bfloat16, device=x2.device)
-        g = _fp8_epi(xq, w1qt, sx, sw1, 2 if approximate else 9, h, bias=b1.to(torch.bfloat16).contiguous())
-        gq, gqt, sg = st2.x.cast(g)
+        bb1 = b1.to(torch.bfloat16).contiguous()
+        fq = None if approximate else _fp8_epi_q(xq, w1qt, sx, sw1, 10, h, st2.x, bias=bb1)
+        if fq is not None:  # gelu(h) leaves the fc1 GEMM already quantised (q and q^T)
+            gq, gqt, sg = fq
+        else:
+            g = _fp8_epi(xq, w1qt, sx, sw1, 2 if approximate else 9, h, bias=bb1)
+            gq, gqt, sg = st2.x.cast(g)
         w2q, w2qt, sw2 = st2.w.cast(w2)
         y = fp8_mm(gq, w2qt, sg, sw2, bias=b2)
         ctx.save_for_backward(xqt, w1q, gqt, w2q, h, sx, sw1, sg, sw2)
@@ -276,7 +315,12 @@ class _FP8FFN(torch.autograd.Function):
         dq, dqt, sd = st2.g.cast(dy2)
         P = -(-M // 128)
         part = torch.empty(P * w2q.shape[0], dtype=torch.float32, device=dy2.device)
-        dh = _fp8_epi(dq, w2q, sd, sw2, 4, h, bias=part)
+        fq = _fp8_epi_q(dq, w2q, sd, sw2, 11, h, st1.g, bias=part)
+        if fq is not None:  # dh leaves the fc2 data-gradient GEMM already quantised (q and q^T)
+            hq, hqt, shh = fq
+        else:
+            dh = _fp8_epi(dq, w2q, sd, sw2, 4, h, bias=part)
+            hq, hqt, shh = st1.g.cast(dh)
         from . import fused
         w1, b1, w2, b2 = ctx.params
         db1 = None
@@ -285,7 +329,6 @@ class _FP8FFN(torch.autograd.Function):
             fused.colsum_finish_parts(part, db1, P, accumulate=False)
         dw2 = None if _slot_fp8_wgrad(gqt, dqt, sg, sd, w2) else fp8_mm(gqt, dqt, sg, sd).to(w2dt)
         db2 = None if _slot_bias(dy2, b2) else _colsum(dy2).to(b2dt)
-        hq, hqt, shh = st1.g.cast(dh)
         dx = fp8_mm(hq, w1q, shh, sw1).to(xdt) if ctx.needs_input_grad[0] else None
         dw1 = None if _slot_fp8_wgrad(xqt, hqt, sx, shh, w1) else fp8_mm(xqt, hqt, sx, shh).to(w1dt)
         return dx, dw1, db1, dw2, db2, None, None, None

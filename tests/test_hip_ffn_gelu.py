@@ -87,3 +87,46 @@ def test_fp8_ffn_matches_unfused_fp8_linears(approximate):
     assert rel(y, yu) < 3e-2 and rel(y, yr) < 8e-2, (rel(y, yu), rel(y, yr))
     for name, gf, gu, r in zip(('dx', 'dw1', 'db1', 'dw2', 'db2'), g_fused, g_unf, ref):
         assert rel(gf, gu) < 6e-2 and rel(gf, r.grad) < 1.2e-1, (name, rel(gf, gu), rel(gf, r.grad))
+
+
+def test_fp8_ffn_fused_quantisation_matches_cast_path(monkeypatch):
+    """Once the amax histories are seeded, the fp8 FFN quantises gelu(h) (fc1 epilogue, e4m3) and
+    dh (fc2 data-gradient epilogue, e5m2) inside the GEMMs (pa_gemm8_fp8_epi_q, no cast kernel);
+    three steps fused vs the bf16-output + cast path from the same fresh states."""
+    from paddle.ops import fp8 as F8
+    torch.manual_seed(4)
+    M, H, F = 2048, 256, 1024
+    dev = 'cuda'
+    base = [torch.randn(M, H, device=dev), torch.randn(H, F, device=dev) * H ** -0.5,
+            torch.randn(F, device=dev) * 0.5, torch.randn(F, H, device=dev) * F ** -0.5,
+            torch.randn(H, device=dev) * 0.5]
+    dy = torch.randn(M, H, device=dev).bfloat16()
+    calls = []
+    orig = F8._fp8_epi_q
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        calls.append(r is not None)
+        return r
+    monkeypatch.setattr(F8, '_fp8_epi_q', spy)
+
+    def run(fused):
+        monkeypatch.setattr(F8, 'FUSED_QUANT', fused)
+        F8._STATIC_STATES.clear()
+        rec = F8.DelayedScaling(amax_history_len=4)
+        ps = [t.bfloat16().requires_grad_() for t in base]
+        for _ in range(3):
+            for p in ps:
+                p.grad = None
+            y = F8.fp8_ffn(*ps, approximate=False, recipe=rec)
+            y.backward(dy)
+        return y.detach().float(), [p.grad.float() for p in ps]
+    yf, gf = run(True)
+    assert any(calls), "fused quantisation never ran"
+    yu, gu = run(False)
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm()).item()
+    assert rel(yf, yu) < 3e-2, rel(yf, yu)
+    for name, a, b in zip(('dx', 'dw1', 'db1', 'dw2', 'db2'), gf, gu):
+        assert rel(a, b) < 6e-2, (name, rel(a, b))
