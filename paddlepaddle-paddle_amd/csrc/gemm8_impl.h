@@ -1377,19 +1377,24 @@ __device__ __forceinline__ void epilogue_wstaged_q(const f32x4 (&acc)[8][4], uin
       const int m = rb + r, n = nb + c16 * 16;
       if (m < M && n < N) *reinterpret_cast<u32x4*>(q + (long long)m * ldq + n) = v;
     }
+    {  // qt rows: lane = (column group of 4, 16-row group): 16 dword reads, a 16x4 byte transpose,
+       // 4 x 16-B stores of the columns' row segments
+      const int cg = lane >> 2, m16 = lane & 3;
+      uint32_t rw[16];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {  // qt rows: column n of the tile, 16 consecutive rows per lane
-      const int idx = lane + 64 * j, c = idx >> 2, m16 = idx & 3;
-      uint32_t o[4];
+      for (int i = 0; i < 16; ++i)
+        rw[i] = *(const __attribute__((address_space(3))) uint32_t*)(tq + (m16 * 16 + i) * 64 + 4 * cg);
+      const int m = rb + m16 * 16;
 #pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) {
-        uint32_t w = 0;
+      for (int j = 0; j < 4; ++j) {
+        uint32_t o[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) w |= (uint32_t)(uint8_t)tq[(m16 * 16 + k4 * 4 + t) * 64 + c] << (8 * t);
-        o[k4] = w;
+        for (int kq = 0; kq < 4; ++kq)
+          o[kq] = ((rw[4 * kq] >> (8 * j)) & 0xFFu) | (((rw[4 * kq + 1] >> (8 * j)) & 0xFFu) << 8) |
+                  (((rw[4 * kq + 2] >> (8 * j)) & 0xFFu) << 16) | (((rw[4 * kq + 3] >> (8 * j)) & 0xFFu) << 24);
+        const int n = nb + 4 * cg + j;
+        if (n < N && m < M) *reinterpret_cast<u32x4*>(qt + (long long)n * M + m) = u32x4{o[0], o[1], o[2], o[3]};
       }
-      const int n = nb + c, m = rb + m16 * 16;
-      if (n < N && m < M) *reinterpret_cast<u32x4*>(qt + (long long)n * M + m) = u32x4{o[0], o[1], o[2], o[3]};
     }
     __builtin_amdgcn_wave_barrier();  // the next half overwrites the LDS tiles after these reads
   }
