@@ -366,15 +366,19 @@ _FP8_WS = _new_workspace('fp8_splitk')
 
 def _fp8_splitk(M, N_, K):
     """Split-K factor of an fp8 GEMM whose 256x256 output tiles cannot fill the chip (the fp8 Linear
-    weight gradient: in x out features over a token-count K): slices of >= 1024 k each, at most
-    ~2 rounds of blocks."""
+    weight gradient: in x out features over a token-count K): the largest split with slices of >=
+    1024 k that keeps the blocks within one round of the chip (768x3072 over 32768 tokens: s = 4,
+    112 us vs 127 us at s = 8, profiles/r5ss_fp8_wgrad_splitk_ab.log)."""
     tiles = -(-M // 256) * -(-N_ // 256)
     if tiles >= 128:
         return 1
     for s in (16, 8, 4, 2):
-        if K % (128 * s) == 0 and K // s >= 1024 and tiles * s <= 384:
+        if K % (128 * s) == 0 and K // s >= 1024 and tiles * s <= FP8_SPLITK_MAX_BLOCKS[0]:
             return s
     return 1
+
+
+FP8_SPLITK_MAX_BLOCKS = [256]  # block budget of the fp8 split-K rule (tools/fp8_wgrad_splitk_ab.py)
 
 
 def hip_fp8_ok(a, w):
