@@ -513,7 +513,12 @@ extern "C" int pa_gemm8_bf16(const void* A, const void* B, void* C, const void* 
 // splitk > 1 needs ws of splitk * M * N floats.
 PA_API int pa_gemm_ok(int M, int N, int K, long long lda, long long ldb, long long ldc, int splitk) {
   if (M <= 0 || N <= 0 || K <= 0 || splitk < 1) return 0;
-  if (K % (64 * splitk) != 0 || M % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8) return 0;
+  if (K % 64 != 0 || M % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8) return 0;
+  // uneven slices (the last one shorter) only on the 8-phase kernels (pa_gemm8_ok checks them)
+  if (K % (64 * splitk) != 0) {
+    const int kb = K / 64, q = (kb + splitk - 1) / splitk;
+    if (kb - (splitk - 1) * q < 2) return 0;
+  }
   return 1;
 }
 
@@ -541,6 +546,7 @@ PA_API int pa_gemm_bf16(const void* A, const void* B, void* C, const void* bias,
   // accumulators through copies, 0.87-1.0 PF.)
   if (g_variant == 0) pa_gemm8_set_sched(transA == 0 ? 11 : 9);
   const bool v8 = (g_variant == 0 || g_variant >= 8) && pa_gemm8_ok(M, N, K, lda, ldb, ldc, transA, transB, splitk);
+  if (!v8 && K % (64 * splitk) != 0) return (int)hipErrorInvalidValue;  // the older kernels split evenly
   if (splitk == 1) {
     if (v8) return pa_gemm8_bf16(A, B, C, bias, nullptr, M, N, K, lda, ldb, ldc, transA, transB, alpha, beta, 1, st);
     return (int)dispatch<0>(transA, transB, A, B, C, nullptr, bias, M, N, K, lda, ldb, ldc, alpha, beta, 1, st);

@@ -59,6 +59,7 @@ static hipError_t launch(const void* A, const void* B, void* C, float* ws, const
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   dim3 grid(tm * tn, 1, splitk);
   if (g_sched == 12) {
+    if (K % (64 * splitk) != 0) return hipErrorInvalidValue;  // the persistent schedule splits evenly
     const int items = tm * tn * splitk;
     const int g = items >= 256 ? 256 : (items + 7) / 8 * 8;  // one block per CU, a multiple of 8 (XCDs)
     if constexpr (EPI == 0) {
@@ -71,43 +72,43 @@ static hipError_t launch(const void* A, const void* B, void* C, float* ws, const
     }
     gemm12_kernel<AK, BKM, EPI><<<g, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                    (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
-                                                   K / splitk, splitk);
+                                                   ksplit_of(K, splitk), splitk);
   } else if (g_sched == 11) {
     if constexpr (EPI == 0) {
       if (g_staged == 2) {
         gemm11_kernel<AK, BKM, 100><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                           (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
-                                                          K / splitk);
+                                                          ksplit_of(K, splitk));
         return hipGetLastError();
       }
       if (g_staged == 4) {
         gemm11_kernel<AK, BKM, 200><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                           (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
-                                                          K / splitk);
+                                                          ksplit_of(K, splitk));
         return hipGetLastError();
       }
     }
     gemm11_kernel<AK, BKM, EPI><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                       (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
-                                                      K / splitk);
+                                                      ksplit_of(K, splitk));
   }
   else if (g_sched == 9) {
     if constexpr (EPI == 0) {
       if (g_staged9) {
         gemm9_kernel<AK, BKM, 200><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                          (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
-                                                         K / splitk);
+                                                         ksplit_of(K, splitk));
         return hipGetLastError();
       }
     }
     gemm9_kernel<AK, BKM, EPI><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                      (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
-                                                     K / splitk);
+                                                     ksplit_of(K, splitk));
   }
   else
     gemm8_kernel<AK, BKM, EPI><<<grid, 512, 0, st>>>((const char*)A, (const char*)B, (uint16_t*)C, ws,
                                                      (const uint16_t*)bias, M, N, K, lda, ldb, ldc, alpha, beta,
-                                                     K / splitk);
+                                                     ksplit_of(K, splitk));
   return hipGetLastError();
 }
 
@@ -183,7 +184,7 @@ static bool span_ok(int transX, int rows, int K, long long ld) {
 PA_API int pa_gemm8_ok(int M, int N, int K, long long lda, long long ldb, long long ldc, int transA, int transB,
                        int splitk) {
   if (M <= 0 || N <= 0 || K <= 0 || splitk < 1) return 0;
-  if (K % (64 * splitk) != 0 || M % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8) return 0;
+  if (!pa::g8::splitk_uneven_ok(K, splitk) || M % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8) return 0;
   // A: transA==0 -> [M][lda]; else [K][lda].  B: transB!=0 -> [N][ldb]; else [K][ldb]
   if (!span_ok(transA, M, K, lda)) return 0;
   if (!span_ok(transB != 0 ? 0 : 1, N, K, ldb)) return 0;

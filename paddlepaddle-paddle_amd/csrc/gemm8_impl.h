@@ -41,6 +41,21 @@
 namespace pa {
 namespace g8 {
 
+// Split-K slice (in k) for ``splitk`` slices of K: ceil(K / 64 / splitk) * 64.  Uneven splits are
+// allowed when every slice is non-empty and the last one holds >= 2 k-blocks (splitk_uneven_ok);
+// the kernels shorten the last slice (nt = min(ksplit, K - kbeg) / BK).
+__host__ __device__ inline int ksplit_of(int K, int splitk) {
+  const int kb = K / 64;
+  return ((kb + splitk - 1) / splitk) * 64;
+}
+inline bool splitk_uneven_ok(int K, int splitk) {
+  if (K % 64 || splitk < 1) return false;
+  if (K % (64 * splitk) == 0) return true;  // even slices (any K % 64 == 0 unsplit)
+  const int kb = K / 64, q = (kb + splitk - 1) / splitk;
+  const int last = kb - (splitk - 1) * q;
+  return last >= 2;
+}
+
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -909,7 +924,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(const char* __restrict__ 
   tile_coords(blockIdx.x, tm * tn, tm, tn, mt, ntile);
   const int m0 = mt * BM, n0 = ntile * BN;
   const int kbeg = blockIdx.z * ksplit;
-  const int nt = ksplit / BK;
+  const int nt = min(ksplit, K - kbeg) / BK;  // uneven split-K: the last slice is shorter
 
   // this wave's DMA slots: 4 KB of A half `wr` and 4 KB of B half `wr` per K-tile
   unsigned offA[4], offB[4];
@@ -1144,7 +1159,7 @@ __global__ __launch_bounds__(512, 1) void gemm9_kernel(const char* __restrict__ 
   tile_coords(bid, tm * tn, tm, tn, mt, ntile);
   const int m0 = mt * BM, n0 = ntile * BN;
   const int kbeg = blockIdx.z * ksplit;
-  const int nt = ksplit / BK;
+  const int nt = min(ksplit, K - kbeg) / BK;  // uneven split-K: the last slice is shorter
 
   // waves 0-3 stage A, waves 4-7 stage B: 4 x 1 KB of a k-half image each per stage
   const bool isA = wr == 0;
@@ -1489,7 +1504,7 @@ __global__ __launch_bounds__(512, 1) void gemm11_kernel(const char* __restrict__
   tile_coords(blockIdx.x, tm * tn, tm, tn, mt, ntile);
   const int m0 = mt * BM, n0 = ntile * BN;
   const int kbeg = blockIdx.z * ksplit;
-  const int nt = ksplit / BK;
+  const int nt = min(ksplit, K - kbeg) / BK;  // uneven split-K: the last slice is shorter
 
   unsigned offA[4], offB[4];
 #pragma unroll

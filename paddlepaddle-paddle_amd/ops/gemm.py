@@ -138,19 +138,23 @@ def mm_bn_stats(a, b):
 
 
 def _splitk_for(M, N_, K):
-    """Split-K factor for outputs with too few 256x256 tiles to fill 256 CUs: the largest of 2..16
-    slices (>= 2048 k each) that keeps the blocks within one round of the chip.  Weight gradients
+    """Split-K factor for outputs with too few 256x256 tiles to fill 256 CUs: the split (2..32 slices
+    of >= 2048 k each, the last one possibly shorter but at least half a slice) that puts the most
+    blocks within one round of the chip.  Weight gradients
     over many tokens: GPT-3 out-projection 2048x2048 64 tiles -> 4 (1058 TF), ERNIE-base at 32768
     tokens 768x2304 27 tiles -> 8 (193 -> 126 us), 768x768 9 tiles -> 16 (183 -> 66 us), 768x3072
     36 tiles -> 4 (profiles/r5bb_wgrad_splitk_ab.log)."""
     tiles = -(-M // 256) * -(-N_ // 256)
-    if tiles >= 128:
+    if tiles >= 128 or K % 64:
         return 1
-    best = 1
-    for s in (2, 4, 8, 16):
-        if K % (64 * s) or K // s < 2048 or tiles * s > 256:
-            break
-        best = s
+    kb = K // 64
+    best, best_blocks = 1, tiles
+    for s in range(2, 33):
+        q = -(-kb // s)  # k-blocks per slice (the last slice may be shorter)
+        if q * 64 < 2048 or tiles * s > 256 or kb - (s - 1) * q < max(2, q // 2):
+            continue
+        if tiles * s > best_blocks:
+            best, best_blocks = s, tiles * s
     return best
 
 

@@ -424,3 +424,19 @@ def test_gemm_autotune_cache_picks_faster_and_matches(monkeypatch):
     assert any(key[0] == 'bmm' for key in HM.tuned_choices())
     rs = q.float() @ k.float().transpose(-1, -2)
     assert ((s.float() - rs).norm() / rs.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize('M,N,K,s', [(768, 3072, 32768, 7), (768, 2304, 32768, 9), (256, 512, 4160, 3)])
+def test_uneven_splitk_weight_gradient(M, N, K, s):
+    """Split-K with a shorter last slice (ceil(K/64/s) k-blocks per slice): the weight-gradient
+    layout (both operands m/n-major, x^T @ dy) with beta = 1 accumulation, vs fp32."""
+    from paddle.ops import gemm as G
+    torch.manual_seed(0)
+    x = torch.randn(K, M, device='cuda').bfloat16()
+    dy = torch.randn(K, N, device='cuda').bfloat16()
+    assert G.hip_mm_ok(x.t(), dy, s)
+    out = torch.randn(M, N, device='cuda').bfloat16()
+    ref = out.float() + x.float().t() @ dy.float()
+    G.hip_mm(x.t(), dy, out=out, beta=1.0, splitk=s)
+    err = ((out.float() - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err

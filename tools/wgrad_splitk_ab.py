@@ -42,7 +42,7 @@ def main():
         dy = torch.randn(T, Nout, device='cuda').bfloat16()
         gw = torch.zeros(Kin, Nout, device='cuda').bfloat16()
         res = []
-        for s in (1, 2, 4, 8, 16):
+        for s in (1, 2, 4, 7, 8, 9, 16):
             if not gemm.hip_mm_ok(x.t(), dy, s):
                 continue
             ms = t_ms(lambda: gemm.hip_mm(x.t(), dy, out=gw, beta=1.0, splitk=s))
