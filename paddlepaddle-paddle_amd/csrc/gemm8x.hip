@@ -222,7 +222,9 @@ PA_API int pa_gemm8_fp8_splitk(const void* A, const void* W, void* C, const void
                                long long ldc, float alpha, float beta, int fmtA, int fmtB, int splitk,
                                hipStream_t st) {
   using namespace pa::g8;
-  if (splitk < 2 || !ws || K % (128 * splitk) || !pa_gemm8_fp8_ok(M, N, K, lda, ldw, ldc) || fmtA < 0 || fmtA > 1 ||
+  // uneven slices allowed (the last one shorter, >= 2 k-tiles of 128 fp8 values): ksplit_of in 2-byte units
+  if (splitk < 2 || !ws || K % 128 || !splitk_uneven_ok(K / 2, splitk) || !pa_gemm8_fp8_ok(M, N, K, lda, ldw, ldc) ||
+      fmtA < 0 || fmtA > 1 ||
       fmtB < 0 || fmtB > 1)
     return (int)hipErrorInvalidValue;
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
@@ -231,7 +233,7 @@ PA_API int pa_gemm8_fp8_splitk(const void* A, const void* W, void* C, const void
   const long long la = lda / 2, lw = ldw / 2;
   auto go = [&](auto kern) {
     kern<<<grid, 512, 0, st>>>((const char*)A, (const char*)W, nullptr, (float*)ws, nullptr, M, N, K2, la, lw, N,
-                               1.f, 0.f, K2 / splitk, 0LL, 0LL, 0LL, nullptr, nullptr);
+                               1.f, 0.f, ksplit_of(K2, splitk), 0LL, 0LL, 0LL, nullptr, nullptr);
   };
   if (fmtA == 0 && fmtB == 0) go(gemm11_kernel<true, true, 1, F8<0, 0>, false>);
   else if (fmtA == 0) go(gemm11_kernel<true, true, 1, F8<0, 1>, false>);

@@ -370,16 +370,22 @@ _FP8_WS = _new_workspace('fp8_splitk')
 
 def _fp8_splitk(M, N_, K):
     """Split-K factor of an fp8 GEMM whose 256x256 output tiles cannot fill the chip (the fp8 Linear
-    weight gradient: in x out features over a token-count K): the largest split with slices of >=
-    1024 k that keeps the blocks within one round of the chip (768x3072 over 32768 tokens: s = 4,
-    112 us vs 127 us at s = 8, profiles/r5ss_fp8_wgrad_splitk_ab.log)."""
+    weight gradient: in x out features over a token-count K): the split (slices of >= 1024 k, the
+    last one possibly shorter) that puts the most blocks within one round of the chip (768x3072
+    over 32768 tokens: one round at s = 4 beat 1.1 rounds at s = 8, 112 vs 127 us,
+    profiles/r5ss_fp8_wgrad_splitk_ab.log; uneven s = 7 fills 252 CUs)."""
     tiles = -(-M // 256) * -(-N_ // 256)
-    if tiles >= 128:
+    if tiles >= 128 or K % 128:
         return 1
-    for s in (16, 8, 4, 2):
-        if K % (128 * s) == 0 and K // s >= 1024 and tiles * s <= FP8_SPLITK_MAX_BLOCKS[0]:
-            return s
-    return 1
+    kb = K // 128  # 128-value k-tiles
+    best, best_blocks = 1, tiles
+    for s in range(2, 33):
+        q = -(-kb // s)  # k-tiles per slice (the last slice may be shorter, but at least half a slice)
+        if q * 128 < 1024 or tiles * s > FP8_SPLITK_MAX_BLOCKS[0] or kb - (s - 1) * q < max(2, q // 2):
+            continue
+        if tiles * s > best_blocks:
+            best, best_blocks = s, tiles * s
+    return best
 
 
 FP8_SPLITK_MAX_BLOCKS = [256]  # block budget of the fp8 split-K rule (tools/fp8_wgrad_splitk_ab.py)

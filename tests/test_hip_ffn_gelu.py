@@ -130,3 +130,23 @@ def test_fp8_ffn_fused_quantisation_matches_cast_path(monkeypatch):
     assert rel(yf, yu) < 3e-2, rel(yf, yu)
     for name, a, b in zip(('dx', 'dw1', 'db1', 'dw2', 'db2'), gf, gu):
         assert rel(a, b) < 6e-2, (name, rel(a, b))
+
+
+@pytest.mark.parametrize('M,N', [(768, 3072), (768, 768)])
+def test_fp8_uneven_splitk_weight_gradient(M, N):
+    """fp8 weight-gradient GEMM over 32768 tokens with an uneven split-K (ops/gemm.py _fp8_splitk:
+    7 / 26 slices, the last one shorter), beta = 1 accumulation, vs the fp32 product of the
+    dequantised operands."""
+    from paddle.ops import gemm as G, fp8 as F8
+    torch.manual_seed(5)
+    K = 32768
+    s = G._fp8_splitk(M, N, K)
+    assert s > 1 and (K // 128) % s != 0, s
+    a = (torch.randn(M, K, device='cuda') * 0.5).to(F8.E4M3)
+    b = (torch.randn(N, K, device='cuda') * 0.5).to(F8.E5M2)
+    one = torch.ones(1, device='cuda')
+    out = torch.randn(M, N, device='cuda').bfloat16()
+    ref = out.float() + a.float() @ b.float().t()
+    G.hip_fp8_mm(a, b, scale_a=one, scale_b=one, out=out, beta=1.0)
+    err = ((out.float() - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
