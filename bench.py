@@ -62,6 +62,25 @@ def parse():
     return ap.parse_args()
 
 
+def _pool_len(args):
+    """Distinct pre-generated batches: one per warmup + timed step (cycled past 32)."""
+    return max(1, min(args.steps + args.warmup, 32))
+
+
+def _feeder(dsts, pool):
+    """feed(): copy the next pre-generated batch of ``pool`` into the step's input tensors ``dsts``
+    (a device-to-device copy inside the timed step, so a captured hipGraph replays with new data
+    too): every step trains on different samples, and the logged losses mean something."""
+    it = [0]
+
+    def feed():
+        src = pool[it[0] % len(pool)]
+        it[0] += 1
+        for d, s_ in zip(dsts[0], src):
+            d.copy_(s_)
+    return feed
+
+
 def build_gpt(args, world, rank, dev):
     import torch
     import paddle
@@ -82,11 +101,13 @@ def build_gpt(args, world, rank, dev):
         model, opt, _ = pdist.sharding.group_sharded_parallel(model, opt, level=args.sharding)
     B, S = args.micro_batch, args.seq
     g = torch.Generator(device=dev).manual_seed(rank)
-    ids = torch.randint(0, cfg.vocab_size, (B, S + 1), device=dev, generator=g)
-    x, y = paddle.to_tensor(ids[:, :-1]), paddle.to_tensor(ids[:, 1:])
+    pool = [torch.randint(0, cfg.vocab_size, (B, S + 1), device=dev, generator=g) for _ in range(_pool_len(args))]
+    x, y = paddle.to_tensor(pool[0][:, :-1].contiguous()), paddle.to_tensor(pool[0][:, 1:].contiguous())
+    feed = _feeder([(x._t, y._t)], [(p[:, :-1], p[:, 1:]) for p in pool])
     inner = model._layers if hasattr(model, '_layers') else model
 
     def step():
+        feed()
         logits = model(x)
         loss = inner.loss(logits, y)
         loss.backward()
@@ -119,10 +140,13 @@ def build_resnet(args, world, rank, dev):
         model = pdist.DataParallel(model)
     g = torch.Generator(device=dev).manual_seed(rank)
     res = 224 if args.resnet_model == 'resnet50' else 32
-    img = paddle.to_tensor(torch.randn(B, res, res, 3, device=dev, dtype=torch.bfloat16, generator=g))
-    lab = paddle.to_tensor(torch.randint(0, 1000, (B,), device=dev, generator=g))
+    pool = [(torch.randn(B, res, res, 3, device=dev, dtype=torch.bfloat16, generator=g),
+             torch.randint(0, 1000, (B,), device=dev, generator=g)) for _ in range(_pool_len(args))]
+    img, lab = paddle.to_tensor(pool[0][0].clone()), paddle.to_tensor(pool[0][1].clone())
+    feed = _feeder([(img._t, lab._t)], pool)
 
     def step():
+        feed()
         out = model(img)
         loss = paddle.nn.functional.cross_entropy(out, lab)
         loss.backward()
@@ -153,11 +177,13 @@ def build_llama(args, world, rank, dev):
     model, opt, _ = pdist.sharding.group_sharded_parallel(model, opt, level='os_g')
     B, S = args.llama_batch, args.llama_seq
     g = torch.Generator(device=dev).manual_seed(rank)
-    ids = torch.randint(0, cfg.vocab_size, (B, S + 1), device=dev, generator=g)
-    x, y = paddle.to_tensor(ids[:, :-1]), paddle.to_tensor(ids[:, 1:])
+    pool = [torch.randint(0, cfg.vocab_size, (B, S + 1), device=dev, generator=g) for _ in range(_pool_len(args))]
+    x, y = paddle.to_tensor(pool[0][:, :-1].contiguous()), paddle.to_tensor(pool[0][:, 1:].contiguous())
+    feed = _feeder([(x._t, y._t)], [(p[:, :-1], p[:, 1:]) for p in pool])
     inner = model._layers if hasattr(model, '_layers') else model
 
     def step():
+        feed()
         loss = inner.loss(model(x), y)
         loss.backward()
         opt.step()
@@ -202,14 +228,17 @@ def build_ernie_static(args, world, rank, dev, fp8):
     finally:
         paddle.disable_static()
     rng = np.random.RandomState(rank)
-    feed = {'ids': rng.randint(1, cfg.vocab_size, size=(B, S)).astype('int64'),
-            'lab': rng.randint(0, 2, size=(B,)).astype('int64')}
-
-    # the loss is fetched every step as a device tensor (return_numpy=False): the host does not wait
-    # for the device inside the loop (as the dygraph benches); measure() reads it after the timing
-    fed = {k: paddle.to_tensor(v, place=place) for k, v in feed.items()}
+    # a different pre-generated batch every step, already on the device; the loss is fetched every
+    # step as a device tensor (return_numpy=False): the host does not wait for the device inside the
+    # loop (as the dygraph benches); measure() reads it after the timing
+    feeds = [{'ids': paddle.to_tensor(rng.randint(1, cfg.vocab_size, size=(B, S)).astype('int64'), place=place),
+              'lab': paddle.to_tensor(rng.randint(0, 2, size=(B,)).astype('int64'), place=place)}
+             for _ in range(_pool_len(args))]
+    it = [0]
 
     def step():
+        fed = feeds[it[0] % len(feeds)]
+        it[0] += 1
         paddle.enable_static()
         try:
             return exe.run(main, feed=fed, fetch_list=[loss], return_numpy=False)[0]
@@ -289,12 +318,32 @@ def measure(step, steps, warmup, world, rank, dev, tag):
     return ms, float(loss.item())
 
 
+def _self_launch(args):
+    """``--gpus N`` (N > 1) without a launcher: start the N rank processes here, one per GPU, over
+    ``torch.distributed.run`` on 127.0.0.1, and exit with its status.  The parent never touches the
+    GPU (no HIP call before the children exist); the ranks print the one JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')  # dmabuf IPC for RCCL (the host driver's only mode)
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
+           '--master-addr=127.0.0.1', f'--master-port={port}', os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(_self_launch(args))
     import torch
     import torch.distributed as dist
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if args.cpu:
         return _main_cpu(args, world, rank)
     # one rank per GPU; the modulo only matters when rehearsing several ranks on fewer GPUs
@@ -337,7 +386,11 @@ def _run(args, world, rank, dev):
            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "bf16",
            "data": "synthetic (random token ids / random images), random-init weights",
-           "config": mcfg, "final_loss": round(final_loss, 4)}
+           "config": mcfg, "final_loss": round(final_loss, 4),
+           "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+           "backend": (("nccl (RCCL over xGMI)" if dist.get_backend() == 'nccl' else dist.get_backend())
+                       if dist.is_initialized() else "none (1 rank)")}
+    assert out["world_size"] == world == args.gpus, (out["world_size"], world, args.gpus)
     if args.model.startswith('gpt') and not args.no_resnet:
         # the second half of the BASELINE metric, same process, same K/W, GPT state released first
         del step

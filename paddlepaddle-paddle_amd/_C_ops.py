@@ -254,9 +254,12 @@ def update_loss_scaling_(x, found_inf, prev_loss_scaling, in_good_steps, in_bad_
     import torch
     f = _unwrap(found_inf)
     ff = f.float().reshape(1)
+    bad = ff != 0  # device bool, no host sync
     for t in x:
         tt = _unwrap(t)
-        tt.mul_(torch.where(ff != 0, torch.zeros_like(ff), torch.ones_like(ff)).to(tt.dtype))
+        # assign zeros (reference FusedFillIf, phi/kernels/gpu/amp_kernel.cu:212): a gradient
+        # holding inf / nan would stay nan under a multiply by 0
+        tt.masked_fill_(bad.reshape([1] * tt.dim()) if tt.dim() else bad.reshape(()), 0)
     if stop_update:
         return x, prev_loss_scaling, in_good_steps, in_bad_steps
     sc, g, b = _unwrap(prev_loss_scaling), _unwrap(in_good_steps), _unwrap(in_bad_steps)

@@ -171,8 +171,10 @@ class _Fleet:
                     raise ValueError(f"The accumulate_steps({acc}) should be greater than or equal to pp_degree({pp})")
                 return meta_parallel.PipelineParallelWithInterleave(model, hcg, self._strategy)
             return meta_parallel.PipelineParallel(model, hcg, self._strategy)
-        if mode == ParallelMode.TENSOR_PARALLEL or mode == ParallelMode.SEGMENT_PARALLEL:
+        if mode == ParallelMode.TENSOR_PARALLEL:
             return meta_parallel.TensorParallel(model, hcg, self._strategy)
+        if mode == ParallelMode.SEGMENT_PARALLEL:
+            return meta_parallel.SegmentParallel(model, hcg, self._strategy)
         if mode == ParallelMode.SHARDING_PARALLEL:
             return model  # wrapped together with the optimizer by distributed_optimizer / group_sharded_parallel
         from ...parallel.data_parallel import DataParallel
@@ -382,11 +384,13 @@ class HybridParallelOptimizer:
         # tensor-parallel (and sep) models are not wrapped in DataParallel: their gradients are
         # all-reduced over the dp group here (reference hybrid_parallel_optimizer.py: step ->
         # fused_allreduce_gradients).  Pipeline schedules sync dp themselves before stepping.
+        # Parameters of a model wrapped by TensorParallel / SegmentParallel were reduced during
+        # backward (hook-driven buckets on the dp x sep group); anything else goes here, bucketed.
         mode = self._hcg.get_parallel_mode()
-        dp = self._hcg.get_data_parallel_group()
-        if mode in (ParallelMode.TENSOR_PARALLEL, ParallelMode.SEGMENT_PARALLEL) and dp is not None \
-                and dp.nranks > 1:
-            from .utils.hybrid_parallel_util import fused_allreduce_gradients
+        from .utils.hybrid_parallel_util import dp_sep_group_and_scale, fused_allreduce_gradients
+        grp = dp_sep_group_and_scale(self._hcg)[0]
+        if mode in (ParallelMode.TENSOR_PARALLEL, ParallelMode.SEGMENT_PARALLEL) and grp is not None \
+                and grp.nranks > 1:
             fused_allreduce_gradients(list(self._inner_opt._parameter_list), self._hcg)
         self._inner_opt.step()
 

@@ -130,15 +130,16 @@ class HybridCommunicateGroup:
 
     # ---- reference accessors
     def get_parallel_mode(self):
-        if self._mp_degree == 1 and self._pp_degree == 1 and self._sharding_degree == 1 and self._sep_degree == 1:
-            return ParallelMode.DATA_PARALLEL
-        if self._mp_degree == 1 and self._pp_degree == 1 and self._sharding_degree > 1:
-            return ParallelMode.SHARDING_PARALLEL
+        # precedence pp -> mp -> sep -> sharding -> dp (reference topology.py:290-320)
         if self._pp_degree > 1:
             return ParallelMode.PIPELINE_PARALLEL
-        if self._sep_degree > 1 and self._mp_degree == 1:
-            return ParallelMode.SEGMENT_PARALLEL
-        return ParallelMode.TENSOR_PARALLEL
+        if self._mp_degree > 1:
+            return ParallelMode.TENSOR_PARALLEL  # may coexist with sep, sharding, dp
+        if self._sep_degree > 1:
+            return ParallelMode.SEGMENT_PARALLEL  # may coexist with sharding, dp
+        if self._sharding_degree > 1:
+            return ParallelMode.SHARDING_PARALLEL
+        return ParallelMode.DATA_PARALLEL
 
     def topology(self):
         return self._topo

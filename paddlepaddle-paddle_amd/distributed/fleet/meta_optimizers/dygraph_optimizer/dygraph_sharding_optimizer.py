@@ -44,9 +44,14 @@ class DygraphShardingOptimizer(ShardedOptimizer):
         super().__init__(optimizer, engine)
         self._dist_runs = {dt: self._runs(a, key=lambda p: 1.0 if getattr(p, 'is_distributed', False) else 0.0)
                            for dt, a in engine.arenas.items()}
-        dp = hcg.get_data_parallel_group()
+        from ...utils.hybrid_parallel_util import dp_sep_group_and_scale
+        dp, dp_scale = dp_sep_group_and_scale(hcg)
         if dp is not None and dp.nranks > 1:
-            engine.dp_pg = dp.pg  # overlapped gradient-shard all-reduce over the dp replicas
+            # overlapped gradient-shard all-reduce over the dp replicas (dp x sep when the sequence
+            # is split too: summed over sep, averaged over dp)
+            engine.dp_pg = dp.pg
+            if hcg.get_sep_parallel_world_size() > 1:
+                engine.dp_scale = dp_scale
             # pipeline-shared weights are summed over their stages after backward: their dp
             # all-reduce waits for step() (two in-place collectives must not race on one shard)
             engine.dp_defer = {u.index for u in engine.units if any(_shared_key(p) is not None for p in u.params)}
@@ -57,10 +62,11 @@ class DygraphShardingOptimizer(ShardedOptimizer):
         was launched during backward the moment its shard was final (ShardingEngine._launch_dp:
         chained behind the unit's reduce-scatter on the device, overlapping the remaining backward);
         here the few not yet launched go out and every one is waited for."""
-        dp = self._hcg.get_data_parallel_group()
+        from ...utils.hybrid_parallel_util import dp_sep_group_and_scale
+        dp = dp_sep_group_and_scale(self._hcg)[0]
         if dp is None or dp.nranks <= 1:
             return
-        self.engine.finish_dp_sync(dp.nranks)
+        self.engine.finish_dp_sync(self._hcg.get_data_parallel_world_size())
 
     def _shared_units(self):
         for u in self.engine.units:

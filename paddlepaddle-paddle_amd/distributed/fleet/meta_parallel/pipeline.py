@@ -198,7 +198,15 @@ class PipelineParallel(Layer):
         self.is_last = self.stage_id == self.num_stages - 1
         self._prev = hcg.prev_rank
         self._next = hcg.next_rank
-        self._dp_group = hcg.get_data_parallel_group()
+        # gradients sync over dp, or dp x sep when the sequence is also split (reference
+        # pipeline_parallel.py:185-187); replicas start from the same weights
+        from ..utils.hybrid_parallel_util import (dp_sep_group_and_scale, broadcast_dp_parameters,
+                                                  broadcast_sep_parameters)
+        self._dp_group = dp_sep_group_and_scale(hcg)[0]
+        if hcg.get_sep_parallel_world_size() > 1:
+            broadcast_sep_parameters(self._layers, hcg)
+        if hcg.get_data_parallel_world_size() > 1 and hcg.get_sharding_parallel_world_size() == 1:
+            broadcast_dp_parameters(self._layers, hcg)
         self._meta_fwd = None
         self._meta_bwd = None
         self.total_loss = None

@@ -12,7 +12,8 @@ def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, off
     """level: 'os' (stage 1), 'os_g' (stage 2), 'p_g_os' (stage 3). Returns (model, optimizer, scaler).
 
     MI355X extensions: ``reduce_dtype='float32'`` reduce-scatters gradients in fp32 (main-grad
-    precision at 8 ranks); ``alias=False`` runs the multi-rank path at world size 1;
+    precision at 8 ranks; the default for stage 3 at world > 1, ``reduce_dtype='param'`` keeps the
+    parameter dtype); ``alias=False`` runs the multi-rank path at world size 1;
     ``reshard_after_forward`` (stage 3): see parallel.sharding.ShardingEngine (None: keep the
     gathered parameters from forward to backward when the model is small against the HBM).
     ``offload=True``: optimizer state of the shard in pinned host memory, updated by the host

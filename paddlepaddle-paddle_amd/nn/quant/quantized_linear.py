@@ -53,7 +53,41 @@ def weight_quantize(x, algo="weight_only_int8", arch=None, group_size=-1):
         # of MFMA operand with one byte permute per pair (csrc/woq_gemm.hip frag_u4)
         q8 = q.to(torch.int16).reshape(n, k // 8, 2, 4) & 0xF
         q = (q8[:, :, 0] | (q8[:, :, 1] << 4)).reshape(n, k // 2).to(torch.uint8).view(torch.int8)  # [n, k/2]
+        out = _w(q)
+        out.__dict__['int4_layout'] = INT4_LAYOUT  # the packing travels with the tensor
+        return out, _w(scale.float())
     return _w(q), _w(scale.float())
+
+
+# int4 packing layouts: 1 = byte i holds k 2i (low nibble) and 2i + 1 (high) — the pre-round-5
+# format; 2 = per 32-bit word w, byte b holds k 8w + b (low) and 8w + 4 + b (high) — the current one.
+INT4_LAYOUT = 2
+
+
+def convert_int4_layout(q, from_layout=1, to_layout=INT4_LAYOUT):
+    """Re-pack an int4 weight ([n, k // 2] int8) between packing layouts (weights saved in the old
+    pair layout decode to wrong values if fed to the current kernels unconverted)."""
+    if from_layout == to_layout:
+        return q
+    t = _u(q).view(torch.uint8).to(torch.int16)
+    n = t.shape[0]
+    lo, hi = t & 0xF, (t >> 4) & 0xF
+    if from_layout == 1:
+        codes = torch.stack([lo, hi], -1).reshape(n, -1)                           # [n, k] in k order
+    else:
+        codes = torch.stack([lo.reshape(n, -1, 4), hi.reshape(n, -1, 4)], 2).reshape(n, -1)
+    k = codes.shape[1]
+    if to_layout == 1:
+        c = codes.reshape(n, k // 2, 2)
+        packed = c[..., 0] | (c[..., 1] << 4)
+    else:
+        if k % 8:
+            raise ValueError("int4 layout 2 needs k % 8 == 0")
+        c = codes.reshape(n, k // 8, 2, 4)
+        packed = (c[:, :, 0] | (c[:, :, 1] << 4)).reshape(n, k // 2)
+    out = _w(packed.to(torch.uint8).view(torch.int8).contiguous())
+    out.__dict__['int4_layout'] = to_layout
+    return out
 
 
 def _unpack(q, algo):
@@ -98,6 +132,8 @@ def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="in
         raise ValueError("weight_only_linear needs weight_scale")
     t = _u(x)
     algo = 'weight_only_int4' if weight_dtype == 'int4' else 'weight_only_int8'
+    if weight_dtype == 'int4' and getattr(weight, '__dict__', {}).get('int4_layout', INT4_LAYOUT) != INT4_LAYOUT:
+        weight = convert_int4_layout(weight, weight.__dict__['int4_layout'])  # tagged old packing
     from ... import ops
     x2 = t.reshape(-1, t.shape[-1])
     wq = _u(weight)
@@ -118,6 +154,7 @@ def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="in
 
 # outlier-column capacity of the GPU path (a multiple of 64: the 16-bit outlier GEMM's K)
 LLM_INT8_OUTLIER_CAP = 128
+_OVERFLOW = {'flag': None, 'seen': False}
 
 
 def llm_int8_linear(x, weight, bias=None, weight_scale=None, threshold=6.0):
@@ -130,10 +167,12 @@ def llm_int8_linear(x, weight, bias=None, weight_scale=None, threshold=6.0):
     outlier columns are compacted on the device into a fixed-capacity set (``LLM_INT8_OUTLIER_CAP``
     columns, outliers first by a stable device sort) whose 16-bit product runs on the hand-written
     GEMM with the bias, then the int8 MFMA GEMM (csrc/gemm8x.hip pa_gemm8_i8, int32 accumulation,
-    per-token x per-channel dequant in its epilogue) accumulates onto it (beta = 1).  Should more
-    columns than the capacity exceed the threshold, the surplus ones stay on the int8 path (their
-    rows are then quantised with a larger scale) — exact LLM.int8 up to the capacity, graceful past
-    it.  Elsewhere: the exact composite."""
+    per-token x per-channel dequant in its epilogue) accumulates onto it (beta = 1).  Every outlier
+    column is excluded from the int8 row quantisation (row scales are never inflated by them).
+    Should more columns than the capacity exceed the threshold, the surplus ones contribute nothing
+    on that call; the overflow is detected on the device and read back without a sync (pinned
+    flag, checked on the next call), which warns once and sends every later call of the process to
+    the exact composite.  Elsewhere: the exact composite."""
     if weight_scale is None:
         raise ValueError("llm_int8_linear needs weight_scale")
     t = _u(x)
@@ -143,7 +182,13 @@ def llm_int8_linear(x, weight, bias=None, weight_scale=None, threshold=6.0):
     K = t.shape[-1]
     a16 = t.reshape(-1, K)
     from ... import ops
-    if (a16.is_cuda and a16.dtype in (torch.bfloat16, torch.float16) and ops.use_hip(a16) and K % 128 == 0
+    if _OVERFLOW['flag'] is not None and bool(_OVERFLOW['flag'][0]) and not _OVERFLOW['seen']:
+        import warnings
+        _OVERFLOW['seen'] = True
+        warnings.warn(f"llm_int8_linear: more than {LLM_INT8_OUTLIER_CAP} outlier columns above the threshold; "
+                      "later calls use the exact composite path", RuntimeWarning)
+    if (not _OVERFLOW['seen'] and a16.is_cuda and a16.dtype in (torch.bfloat16, torch.float16) and ops.use_hip(a16)
+            and K % 128 == 0
             and qw_i8.dtype == torch.int8 and qw_i8.dim() == 2 and qw_i8.shape[1] == K and qw_i8.shape[0] % 8 == 0):
         y = _llm_int8_gpu(a16.contiguous(), qw_i8.contiguous(), ws, None if bias is None else _u(bias), threshold)
         if y is not None:
@@ -174,9 +219,13 @@ def _llm_int8_gpu(a, qw, ws, bias, threshold):
     order = torch.argsort((~outl).to(torch.int8), stable=True)               # outlier columns first
     idx = order[:cap]
     sel = outl.index_select(0, idx)                                          # which of them are outliers
-    excl = torch.zeros(K, dtype=torch.uint8, device=a.device)
-    excl.index_copy_(0, idx, sel.to(torch.uint8))
+    excl = outl.to(torch.uint8)                                              # every outlier column
     qa, sx = I8.quant_rows(a, excl, rows=M8)                                 # int8 [M8, K], fp32 [M8]
+    # capacity overflow: a device flag copied to pinned host memory without a sync (checked on the
+    # next call, llm_int8_linear)
+    if _OVERFLOW['flag'] is None:
+        _OVERFLOW['flag'] = torch.zeros(1, dtype=torch.bool, pin_memory=True)
+    _OVERFLOW['flag'].copy_((outl.sum() > cap).reshape(1), non_blocking=True)
     # 16-bit outlier product (+ bias) first: [M, cap] @ [cap, N]
     a_o = a.index_select(1, idx) * sel.to(a.dtype)
     w_o = (qw.index_select(1, idx).float() * ws.float()[:, None]).to(a.dtype).t().contiguous()

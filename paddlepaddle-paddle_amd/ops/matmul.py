@@ -100,9 +100,18 @@ def _tune_off():
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
+def _multi_rank():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
 def _tuned(key, hip_fn, lib_fn):
     """hip_fn() or lib_fn(), whichever measured faster for ``key`` (hip_fn when tuning is off or
-    the problem was first seen inside a capture)."""
+    the problem was first seen inside a capture).  Choices measured before the job became
+    multi-rank are dropped once it is (replicated computations must pick the same kernel on every
+    rank); ``clear_tuning()`` resets the cache."""
+    if _TUNE['cache'] and _multi_rank():
+        _TUNE['cache'].clear()
     c = _TUNE['cache'].get(key)
     if c is None:
         if _tune_off():
@@ -110,6 +119,11 @@ def _tuned(key, hip_fn, lib_fn):
         th, tl = _time_ms(hip_fn), _time_ms(lib_fn)
         c = _TUNE['cache'][key] = 'lib' if tl * _TUNE['margin'] < th else 'hip'
     return hip_fn() if c == 'hip' else lib_fn()
+
+
+def clear_tuning():
+    """Forget every measured choice (the next call of each problem measures again)."""
+    _TUNE['cache'].clear()
 
 
 def tuned_choices():

@@ -62,16 +62,22 @@ class _Bucket:
 class GradAllReducer:
     """Bucketed async all-reduce of flat gradient buffers, driven by autograd hooks."""
 
-    def __init__(self, params, group=None, bucket_mb=DEFAULT_BUCKET_MB, average=True):
+    def __init__(self, params, group=None, bucket_mb=DEFAULT_BUCKET_MB, average=True, scale=None,
+                 include_distributed=False):
+        """average: divide the sum by the group size; scale: multiply the SUM by this factor
+        instead (hybrid parallelism reduces over data x sep ranks but averages over data only —
+        reference fleet/utils/hybrid_parallel_util.py:241-262); include_distributed: also reduce
+        tensor-parallel shards (their data-parallel replicas hold the same shard)."""
         self.group = group
         self.pg = _pg(group)
         self.world = dist.get_world_size(self.pg)
         self.average = average
+        self.scale = None if scale is None else float(scale)
         self.enabled = True
         self.buffers = []
         by_dt = {}
         for p in params:
-            if p._t.requires_grad and not getattr(p, 'is_distributed', False):
+            if p._t.requires_grad and (include_distributed or not getattr(p, 'is_distributed', False)):
                 fb = p.__dict__.get('_flat', (None,))[0]
                 key = id(fb) if fb is not None else ('new', p._t.dtype)
                 by_dt.setdefault(key, []).append(p)
@@ -104,6 +110,7 @@ class GradAllReducer:
         self.buckets.append(b)
         for p in params:
             self._p2b[id(p)] = b
+            p.__dict__['_hook_reduced'] = self  # hybrid optimizers skip their own all-reduce of p
 
     def _make_hook(self, bucket):
         def hook():
@@ -119,7 +126,7 @@ class GradAllReducer:
 
     def _launch(self, b):
         g = b.buf.grad[b.lo:b.hi]
-        if self.average and dist.get_backend(self.pg) == 'nccl':
+        if self.scale is None and self.average and dist.get_backend(self.pg) == 'nccl':
             b.work = dist.all_reduce(g, dist.ReduceOp.AVG, group=self.pg, async_op=True)
         else:
             b.work = dist.all_reduce(g, dist.ReduceOp.SUM, group=self.pg, async_op=True)
@@ -135,7 +142,10 @@ class GradAllReducer:
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
-                if self.average and dist.get_backend(self.pg) != 'nccl':
+                if self.scale is not None:
+                    if self.scale != 1.0:
+                        b.buf.grad[b.lo:b.hi].mul_(self.scale)
+                elif self.average and dist.get_backend(self.pg) != 'nccl':
                     b.buf.grad[b.lo:b.hi].div_(self.world)
             b.work = None
             b.pending = len(b.params)
@@ -145,6 +155,10 @@ class GradAllReducer:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        for b in self.buckets:
+            for p in b.params:
+                if p.__dict__.get('_hook_reduced') is self:
+                    del p.__dict__['_hook_reduced']
 
 
 class DataParallel(Layer):

@@ -179,6 +179,12 @@ class ShardingEngine:
         self.reshard_after_forward = self._auto_reshard(model, params) if reshard_after_forward is None \
             else bool(reshard_after_forward)
         rd = str(reduce_dtype).replace('torch.', '').replace('paddle.', '') if reduce_dtype is not None else None
+        if rd is None and self.level == 3 and self.world > 1:
+            # stage 3 across ranks: an N-way bf16 / fp16 reduce-scatter rounds at every ring hop,
+            # so 16-bit gradients are reduced in fp32 by default (reduce_dtype='param' opts out)
+            rd = 'float32'
+        elif rd == 'param':
+            rd = None
         if rd not in (None, 'float32', 'bfloat16', 'float16'):
             raise ValueError(f"reduce_dtype must be float32 / bfloat16 / float16, got {reduce_dtype}")
         self.reduce_fp32 = rd == 'float32' and not self.alias
@@ -218,6 +224,7 @@ class ShardingEngine:
         # from there), overlapping the rest of backward; dp_final is cleared by pipeline schedules
         # for every micro-batch but the last
         self.dp_pg = None
+        self.dp_scale = None  # dp x sep groups: SUM scaled by 1/dp instead of the group average
         self.dp_final = True
         self.dp_defer = set()  # units whose dp all-reduce waits for step() (pipeline-shared weights)
         self._dp_works = []
@@ -479,7 +486,7 @@ class ShardingEngine:
             return
         gs = self.gshard(u)
         nccl = dist.get_backend(self.dp_pg) == 'nccl'
-        op = dist.ReduceOp.AVG if nccl else dist.ReduceOp.SUM
+        op = dist.ReduceOp.AVG if nccl and self.dp_scale is None else dist.ReduceOp.SUM
         if nccl and gs.is_cuda and u.rs_work is not None:
             if self._dp_stream is None:
                 self._dp_stream = torch.cuda.Stream(device=gs.device)
@@ -505,7 +512,9 @@ class ShardingEngine:
             self._dp_flush = False
         for gs, w, nccl in self._dp_works:
             w.wait()
-            if not nccl:
+            if self.dp_scale is not None:
+                gs.mul_(self.dp_scale)
+            elif not nccl:
                 gs.div_(dp_nranks)
         self._dp_works = []
         self._dp_done = set()

@@ -294,6 +294,32 @@ def test_bench_multi_rank_path_rehearsal(nproc):
     assert d['value'] > 0 and abs(d['value'] - 2 * 64 * nproc / (d['ms_per_step'] / 1e3)) < 1e-2 * d['value']
 
 
+def test_bench_gpus_flag_launches_its_own_ranks():
+    """``python bench.py --gpus 2`` with no launcher starts the 2 ranks itself (no HIP call in the
+    parent) and reports the collective world size; a launcher / --gpus mismatch is an error."""
+    import json
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES='', HIP_VISIBLE_DEVICES='', PYTHONPATH=ROOT, OMP_NUM_THREADS='1')
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+        env.pop(k, None)
+    args = ['--cpu', '--model', 'gpt-tiny', '--steps', '2', '--warmup', '1', '--resnet-model', 'resnet18',
+            '--resnet-batch', '2', '--micro-batch', '2', '--seq', '64']
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), *args, '--gpus', '2'], env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == 2 and d['world_size'] == 2 and d['config']['parallelism'] == 'sharding-3x2'
+    assert d['backend'] == 'gloo'
+    # the timed steps trained on different batches: a finite, non-memorised loss
+    assert 0.5 < d['final_loss'] < 20
+    bad = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=2',
+                          '--master-addr=127.0.0.1', f'--master-port={_port()}', os.path.join(ROOT, 'bench.py'),
+                          *args, '--gpus', '4'], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         timeout=600)
+    assert bad.returncode != 0 and 'launcher started 2' in bad.stderr
+
+
 @pytest.mark.parametrize("mode", ['fleet', 'fleet_merge', 'pass'])
 def test_static_collective_data_parallel_matches_full_batch(mode):
     out = run_workers('worker_static_dp.py', mode)
@@ -331,3 +357,11 @@ def test_dist_to_static_sharded_and_pipelined_programs(mode):
     Programs and equal single-process training (tests/dist/worker_dist_static_sp.py)."""
     out = run_workers('worker_dist_static_sp.py', mode)
     assert out.count(f'dist static {mode} OK') == 2, out[-3000:]
+
+
+@pytest.mark.parametrize("mode,nproc", [('sep', 2), ('sepmp', 4), ('sepdp', 4), ('sepsh', 4)])
+def test_segment_parallel_matches_single_process(mode, nproc):
+    """sep alone and x mp / dp / sharding: gradients summed over sep, averaged over dp
+    (reference fleet/utils/hybrid_parallel_util.py:241), weights broadcast over sep."""
+    out = run_workers('worker_sep.py', mode, nproc=nproc)
+    assert out.count(f'{mode} OK') == nproc, out[-3000:]

@@ -1,4 +1,5 @@
 """Round-5 regression tests (CPU): capture-safe kernel workspaces, weight-only linear autograd."""
+import numpy as np
 import torch
 
 import paddle
@@ -54,3 +55,49 @@ def test_amp_loss_scaling_ops_cpu():
     for _ in range(2):
         update_loss_scaling_(found, sc, g, b, 2, 1, 2.0, 0.5)
     assert sc.item() == 8.0 and g.item() == 0.0
+
+
+def test_update_loss_scaling_zeroes_nonfinite_grads_r6():
+    """found_inf zeroes gradients by assignment, so inf / nan entries become 0 too
+    (reference FusedFillIf, phi/kernels/gpu/amp_kernel.cu:212)."""
+    import paddle
+    g = paddle.to_tensor(np.array([1.0, np.inf, np.nan, -2.0], 'float32'))
+    found = paddle.to_tensor(np.array([True]))
+    sc = paddle.to_tensor(np.array([1024.0], 'float32'))
+    good = paddle.to_tensor(np.array([0], 'int32'))
+    bad = paddle.to_tensor(np.array([0], 'int32'))
+    paddle._C_ops.update_loss_scaling_([g], found, sc, good, bad, 2, 1, 2.0, 0.5)
+    np.testing.assert_array_equal(g.numpy(), np.zeros(4, 'float32'))
+    assert float(sc) == 512.0
+    g2 = paddle.to_tensor(np.array([1.0, 3.0], 'float32'))
+    paddle._C_ops.update_loss_scaling_([g2], paddle.to_tensor(np.array([False])), sc, good, bad, 2, 1, 2.0, 0.5)
+    np.testing.assert_array_equal(g2.numpy(), np.array([1.0, 3.0], 'float32'))
+
+
+def test_int4_layout_tag_and_conversion_r6():
+    """the int4 packing layout travels with the quantised weight; the old pair layout
+    converts losslessly and weight_only_linear converts a tagged old-layout weight."""
+    import paddle
+    from paddle.nn.quant import quantized_linear as Q
+    rs = np.random.RandomState(0)
+    w = paddle.to_tensor(rs.randn(16, 8).astype('float32'))
+    q, s = Q.weight_quantize(w, algo='weight_only_int4')
+    assert q.__dict__['int4_layout'] == Q.INT4_LAYOUT
+    old = Q.convert_int4_layout(q, Q.INT4_LAYOUT, 1)
+    assert old.__dict__['int4_layout'] == 1
+    np.testing.assert_array_equal(Q.convert_int4_layout(old, 1)._t.numpy(), q._t.numpy())
+    x = paddle.to_tensor(rs.randn(3, 16).astype('float32'))
+    y_new = Q.weight_only_linear(x, q, weight_scale=s, weight_dtype='int4')
+    y_old = Q.weight_only_linear(x, old, weight_scale=s, weight_dtype='int4')
+    np.testing.assert_allclose(y_old.numpy(), y_new.numpy(), rtol=1e-6)
+
+
+def test_matmul_autotune_cache_cleared_when_multi_rank_r6(monkeypatch):
+    """choices measured before the job became multi-rank are dropped."""
+    from paddle.ops import matmul as mm
+    mm._TUNE['cache'][('probe',)] = 'lib'
+    monkeypatch.setattr(mm, '_multi_rank', lambda: True)
+    out = mm._tuned(('other',), lambda: 'hip', lambda: 'lib')
+    assert out == 'hip' and ('probe',) not in mm._TUNE['cache']
+    mm.clear_tuning()
+    assert mm.tuned_choices() == {}
