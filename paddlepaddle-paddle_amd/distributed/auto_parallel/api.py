@@ -9,6 +9,7 @@ collective that is cheapest on point-to-point xGMI — Shard→Replicate all-gat
 Replicate all-reduce, Partial→Shard reduce-scatter, Shard(i)→Shard(j) all-to-all,
 Replicate→Shard a local slice (no traffic) — each issued on the mesh-dimension subgroup.
 """
+from ...framework.flags import pa_flag  # noqa: E402
 import copy
 import itertools
 
@@ -663,7 +664,7 @@ class DistModel:
     def _static_blocker(layer, optimizer, st):
         """None when the step can run as a static Program, else why it runs eagerly."""
         import os
-        if os.environ.get('PADDLE_AMD_DIST_TO_STATIC', '1') == '0':
+        if not pa_flag('dist_to_static'):
             return 'disabled by PADDLE_AMD_DIST_TO_STATIC=0'
         sharded = isinstance(optimizer, _ShardOptimizer) and optimizer._sharded is not None
         if st.pipeline.get('enable'):

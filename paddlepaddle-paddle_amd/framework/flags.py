@@ -36,6 +36,44 @@ _REGISTRY = {
 }
 
 
+# Framework switches (MI355X kernel routing and engine knobs), registered as ``FLAGS_pa_<name>``:
+# settable by set_flags / the FLAGS_pa_<name> environment variable, and — for scripts of earlier
+# rounds — by the legacy PADDLE_AMD_<NAME> variable.  Most are read once at import by the module
+# they configure (kernel routing is fixed per process).  name: (default, doc)
+PA_FLAGS = {
+    'disable_hip_kernels': (False, 'route every op to the ATen composite (A/B against the HIP kernels)'),
+    'hip_gemm': (True, 'hand-written MFMA GEMM (csrc/gemm8.hip) for Linear / matmul'),
+    'hip_matmul': (True, 'paddle.matmul / bmm / einsum on the hand-written GEMM when the operands fit'),
+    'skinny_gemm': (True, 'decode-shaped GEMMs (M <= 64) on csrc/skinny_gemm.hip'),
+    'gemm_autotune': (True, 'per-shape hand-written-vs-library choice for plain GEMMs (single rank)'),
+    'gemm_tuning': (True, 'apply the measured per-shape GEMM schedule table (ops/gemm_tuning.py)'),
+    'kmajor_fwd': (True, 'transient K-major weight copy for the Linear forward (>= 4096 rows)'),
+    'fp8_8phase': (True, '8-phase fp8 GEMM schedule (else the 2-stage kernel)'),
+    'wgrad_overlap': (False, 'weight-gradient GEMM on a side stream beside the data-gradient GEMM'),
+    'group_wgrad': (True, 'group weight-gradient GEMMs whose tile counts fill one round of the chip'),
+    'defer_fc2_bias': (True, 'GPT: fc2 bias gradient from the fused dgrad epilogue column sums'),
+    'gemm_staged': ('', 'GEMM epilogue staging level override (0/1/2; empty: built-in default)'),
+    'gemm_staged9': ('', 'weight-gradient epilogue staging override (empty: default)'),
+    'conv_staged': ('', 'conv output staging override (empty: default)'),
+    'fa_ds_bwd': ('', 'flash-attention backward form: 1 materialised dS, 0 recompute (empty: by shape)'),
+    'fa_ds_ws_mb': (8192, 'flash-attention dS workspace cap (MiB)'),
+    'hip_conv': (True, 'implicit-GEMM MFMA convolutions (csrc/conv.hip)'),
+    'hip_conv_bwd': (True, 'data / filter gradients of convolutions on the HIP kernels'),
+    'hip_conv_wgrad': (True, 'filter gradient on the HIP kernel'),
+    'conv_bn_stats': (True, 'batch-norm statistics in the conv epilogue'),
+    'conv1x1_gemm': (True, '1x1 stride-1 convolutions on the GEMM'),
+    'conv_stem': (True, 'few-channel stem convolution kernel (csrc/conv_stem.hip)'),
+    'hip_dwconv': (True, 'depthwise convolutions on csrc/dwconv.hip'),
+    'hip_gconv': (True, 'grouped convolutions on csrc/gconv.hip'),
+    'force_collectives': (False, 'run the real collectives at world size 1 (1-rank RCCL rehearsal)'),
+    'sharding_alias': (True, 'world-1 sharding units alias the optimizer arenas'),
+    'dist_to_static': (True, 'dist.to_static records a static Program (else eager SPMD)'),
+    'sot': (False, 'to_static(full_graph=False) uses the bytecode (SOT) front end'),
+    'pdmodel': (True, 'save_inference_model writes the reference ProgramDesc format when possible'),
+    'pir': ('', 'jit.save writes the PIR json program (1 / 0; empty: FLAGS_enable_pir_api)'),
+}
+
+
 def _parse(default, s):
     if isinstance(default, bool):
         return s.lower() in ('1', 'true', 'yes', 'on')
@@ -45,6 +83,15 @@ def _parse(default, s):
         return float(s)
     return s
 
+
+for _n, (_d, _doc) in PA_FLAGS.items():
+    _REGISTRY['FLAGS_pa_' + _n] = _d
+    _legacy = 'PADDLE_AMD_' + _n.upper()
+    if _legacy in os.environ and ('FLAGS_pa_' + _n) not in os.environ:
+        try:
+            _REGISTRY['FLAGS_pa_' + _n] = _parse(_d, os.environ[_legacy])
+        except ValueError:
+            pass
 
 for _k, _v in list(_REGISTRY.items()):
     if _k in os.environ:
@@ -69,6 +116,7 @@ def set_flags(flags):
         if k not in _REGISTRY:
             raise ValueError(f"Flag {k} cannot set its value through this function.")
         _REGISTRY[k] = v
+        _EXPLICIT.add(k)
         for fn in _hooks.get(k, []):
             fn(v)
 
@@ -107,3 +155,22 @@ class _FlagsView:
     def get(self, k, default=None):
         return self[k] if k in self else default
 
+
+
+_EXPLICIT = set()
+
+
+def pa_flag(name):
+    """Value of the framework switch FLAGS_pa_<name> (PA_FLAGS): a value given by set_flags wins,
+    then the live environment (FLAGS_pa_<name>, then the legacy PADDLE_AMD_<NAME>), then the
+    default — switches read at construction time follow environment changes made at run time."""
+    key = 'FLAGS_pa_' + name
+    if key not in _EXPLICIT:
+        d = PA_FLAGS[name][0]
+        for env in (key, 'PADDLE_AMD_' + name.upper()):
+            if env in os.environ:
+                try:
+                    return _parse(d, os.environ[env])
+                except ValueError:
+                    break
+    return _REGISTRY[key]

@@ -24,6 +24,7 @@ captured FX graph (eager torch ops): a translation failure never changes results
 Usage: ``paddle.jit.sot.symbolic_translate(fn)(*args)``, ``paddle.jit.to_static(fn, backend='sot')``
 (or ``full_graph=False`` with ``PADDLE_AMD_SOT=1``).
 """
+from ..framework.flags import pa_flag  # noqa: E402
 import functools
 import os
 
@@ -146,7 +147,7 @@ def symbolic_translate(fn=None, training=True, **kwargs):
 
 
 def default_enabled():
-    return os.environ.get('PADDLE_AMD_SOT', '0') == '1'
+    return pa_flag('sot')
 
 
 def reset():

@@ -14,6 +14,7 @@ MI355X mapping (per decoder block):
                           (mask regenerated in backward from a counter hash)
   LM head + loss        → hand-written GEMMs (tied, E.grad accumulated in place) + csrc/softmax_xent.hip
 """
+from ..framework.flags import pa_flag  # noqa: E402
 import math
 import os
 from dataclasses import dataclass
@@ -63,7 +64,7 @@ def gpt_config(name, **overrides):
 
 # fc2 bias handed to the next fused dropout + residual + LayerNorm (its gradient reduced in that
 # kernel's backward pass) instead of a GEMM bias epilogue + a column-sum pass (tests switch it)
-DEFER_FC2_BIAS = os.environ.get('PADDLE_AMD_DEFER_FC2_BIAS', '1') == '1'
+DEFER_FC2_BIAS = pa_flag('defer_fc2_bias')
 
 
 def _normal(std):

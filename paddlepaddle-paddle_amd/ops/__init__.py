@@ -4,6 +4,7 @@
 tensor on the GPU.  If the kernel library is missing on a GPU process it raises instead of
 silently falling back (``PADDLE_AMD_DISABLE_HIP_KERNELS=1`` opts out explicitly, for A/B).
 """
+from ..framework.flags import pa_flag  # noqa: E402
 import os
 
 import torch
@@ -11,7 +12,7 @@ import torch
 from . import _native
 from ..core.tensor import SOT_ACTIVE as _SOT
 
-_disabled = os.environ.get('PADDLE_AMD_DISABLE_HIP_KERNELS', '0') == '1'
+_disabled = pa_flag('disable_hip_kernels')
 
 
 def enabled():

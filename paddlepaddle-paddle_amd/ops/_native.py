@@ -4,6 +4,7 @@ Every launcher takes raw device pointers and the caller's current HIP stream, so
 kernels interleave correctly with the storage layer's own work and can be captured into
 hipGraphs.  A failed launch raises immediately (the hipError_t is checked per call).
 """
+from ..framework.flags import pa_flag  # noqa: E402
 import ctypes
 import os
 
@@ -182,13 +183,13 @@ def _load():
             fn.argtypes = args
             fn.restype = None if name in _VOID_RET else (ctypes.c_longlong if name in _LL_RET else ctypes.c_int)
         lib = l
-        st = os.environ.get('PADDLE_AMD_GEMM_STAGED')  # A/B: LDS-staged GEMM epilogue level (0/1/2)
+        st = (pa_flag('gemm_staged') or None)  # A/B: LDS-staged GEMM epilogue level (0/1/2)
         if st is not None:
             l.pa_gemm8_set_staged_epi(int(st))
-        cst = os.environ.get('PADDLE_AMD_CONV_STAGED')  # A/B: staged conv output stores
+        cst = (pa_flag('conv_staged') or None)  # A/B: staged conv output stores
         if cst is not None:
             l.pa_conv2d_set_staged(int(cst))
-        st9 = os.environ.get('PADDLE_AMD_GEMM_STAGED9')  # A/B: staged weight-gradient epilogue
+        st9 = (pa_flag('gemm_staged9') or None)  # A/B: staged weight-gradient epilogue
         if st9 is not None:
             l.pa_gemm8_set_staged9(int(st9))
     except OSError as e:  # pragma: no cover

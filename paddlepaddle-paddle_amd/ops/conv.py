@@ -5,7 +5,7 @@ Reference: paddle/phi/kernels/gpudnn/conv_kernel.cu (forward), conv_grad_kernel.
   fused; the weight is packed into the [Cout][R][S][C] k-contiguous image the kernel stages
   (re-packed per call).  Needs C % 32 == 0; the 3-channel RGB stem forward stays on the storage
   layer's direct convolution (an explicit im2col + 1x1 MFMA path, pa_im2col_nhwc, is available
-  behind PADDLE_AMD_CONV_IM2COL=1 but measured slower there).
+  as conv2d_fwd_im2col but measured slower there).
 * Batch-norm statistics (fused_bn_stats): the forward epilogue can also emit per-slab channel
   (mean, M2) for the batch norm that consumes the output (ops/batchnorm.py).
 * Data gradient (any stride): stride classes of input pixels, each a stride-1 implicit GEMM over
@@ -18,6 +18,7 @@ Reference: paddle/phi/kernels/gpudnn/conv_kernel.cu (forward), conv_grad_kernel.
 The storage layer's convolution backward (MIOpen) remains only as the fallback for shapes the
 kernels reject (grouped / odd channel counts) or when PADDLE_AMD_HIP_CONV_BWD=0.
 """
+from ..framework.flags import pa_flag  # noqa: E402
 import os
 
 import torch
@@ -35,9 +36,9 @@ def _param_of(t):
     p = _PARAMS.get(id(t))
     return p if p is not None and p._t is t else None
 
-_enabled = os.environ.get('PADDLE_AMD_HIP_CONV', '1') != '0'
-_bwd_enabled = os.environ.get('PADDLE_AMD_HIP_CONV_BWD', '1') != '0'
-_wgrad_hip = os.environ.get('PADDLE_AMD_HIP_CONV_WGRAD', '1') != '0'
+_enabled = pa_flag('hip_conv')
+_bwd_enabled = pa_flag('hip_conv_bwd')
+_wgrad_hip = pa_flag('hip_conv_wgrad')
 
 
 def supported(x, w, groups):
@@ -105,7 +106,7 @@ def _want_stats(b):
     return _stats_mode[0] > 0 and b is None and _stats_enabled
 
 
-_stats_enabled = os.environ.get('PADDLE_AMD_CONV_BN_STATS', '1') != '0'
+_stats_enabled = pa_flag('conv_bn_stats')
 
 
 def _parts_key(t):
@@ -164,19 +165,10 @@ def conv2d_fwd(x, w, b, stride, pad, dil):
     return _fwd_packed(x, _packed(w), b, stride, pad, dil)
 
 
-# Off by default: on the ResNet50 stem (256 x 224 x 224 x 3, 7x7/2) the im2col matrix is
-# [3.2M, 192] = 1.23 GB written and read back; im2col 0.54 ms + the 1x1 conv 0.12 ms lose to the
-# library's direct convolution (0.36 ms): 8.23k vs 8.37k img/s (profiles/r3s3_im2col_ab.log).
-_im2col_fwd = os.environ.get('PADDLE_AMD_CONV_IM2COL', '0') != '0'
-
-
-def im2col_ok(x, w):
-    """Few-channel convolutions (the RGB stem): im2col + a 1x1 convolution on the MFMA kernel."""
-    Cout, C, R, S = w.shape
-    return (_im2col_fwd and C % 32 != 0 and Cout % 8 == 0 and N.lib is not None
-            and bool(N.lib.pa_im2col_rows_ok(S, C)))
-
-
+# Not routed: on the ResNet50 stem (256 x 224 x 224 x 3, 7x7/2) the im2col matrix is [3.2M, 192]
+# = 1.23 GB written and read back; im2col 0.54 ms + the 1x1 conv 0.12 ms lose to the library's
+# direct convolution (0.36 ms, profiles/r3s3_im2col_ab.log), and the stem kernel
+# (csrc/conv_stem.hip, 0.22 ms) replaced both.  Kept as an explicit API for few-channel convs.
 def conv2d_fwd_im2col(x, w, b, stride, pad, dil):
     """y = conv(x, w) as im2col(x) [M, Kp] times the [Cout][Kp] filter image, the second step a
     1 x 1 convolution on conv_fwd_kernel (so the batch-norm statistics epilogue applies as for
@@ -346,7 +338,7 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, dil, out=None):
 # GEMM (csrc/gemm8.hip) runs them faster than the implicit-GEMM conv kernel once the GEMM's N side
 # fills its 256-wide tiles (tools/conv1x1_gemm_bench.py, profiles/r2_conv1x1_gemm.log: forward when
 # Cout >= 128, data gradient when C >= 128, filter gradient when C >= 512 and Cout >= C / 2).
-_gemm_1x1 = os.environ.get('PADDLE_AMD_CONV1X1_GEMM', '1') != '0'
+_gemm_1x1 = pa_flag('conv1x1_gemm')
 
 
 def _pointwise(w, stride, pad, dil):
@@ -450,7 +442,7 @@ class shared_dgrad:
         return False
 
 
-_stem_enabled = os.environ.get('PADDLE_AMD_CONV_STEM', '1') != '0'
+_stem_enabled = pa_flag('conv_stem')
 
 
 def stem_ok(x, w, stride, dil):
@@ -511,8 +503,6 @@ class _Conv2dNHWC(torch.autograd.Function):
                 return y
         if fwd_ok(w):
             return conv2d_fwd(x, w, b, stride, pad, dil)
-        if im2col_ok(x, w) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
-            return conv2d_fwd_im2col(x, w, b, stride, pad, dil)
         if stem_ok(x, w, stride, dil):
             return conv2d_fwd_stem(x, w, b, stride, pad)
         return _lib_conv_fwd(x, w, b, stride, pad, dil)
@@ -614,7 +604,7 @@ def conv2d_nhwc(x, w, b, stride, pad, dil):
 
 
 # ---- depthwise convolution (groups == C_in == C_out) on csrc/dwconv.hip
-_dw_enabled = os.environ.get('PADDLE_AMD_HIP_DWCONV', '1') != '0'
+_dw_enabled = pa_flag('hip_dwconv')
 
 
 def dw_supported(x, w, groups):
@@ -690,7 +680,7 @@ def dwconv2d_nhwc(x, w, b, stride, pad, dil):
 
 
 # ---- grouped convolution (1 < groups < C_in, ResNeXt / ShuffleNet-v1) on csrc/gconv.hip
-_gc_enabled = os.environ.get('PADDLE_AMD_HIP_GCONV', '1') != '0'
+_gc_enabled = pa_flag('hip_gconv')
 
 
 def _gc_geo(x, w, groups, stride, pad, dil):

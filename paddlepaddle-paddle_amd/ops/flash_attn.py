@@ -2,6 +2,7 @@
 
 Reference: paddle/phi/kernels/gpu/flash_attn_kernel.cu / flash_attn_grad_kernel.cu.
 """
+from ..framework.flags import pa_flag  # noqa: E402
 import math
 import os
 
@@ -42,11 +43,11 @@ def supported(q, k, v):
 # fwd+bwd 0.720 -> 0.651 ms, GPT-3 1.3B step 124.4k -> 125.7k tok/s, profiles/r4e_attn_ds_ab.log);
 # head_dim 64 stays on the recompute pair (1.04 -> 1.24 ms there: its dQ recompute is cheaper than
 # the dS round trip).  PADDLE_AMD_FA_DS_BWD=0 / 1: off / also for head_dim 64.
-_ds_env = os.environ.get('PADDLE_AMD_FA_DS_BWD')
+_ds_env = (pa_flag('fa_ds_bwd') or None)
 _ds_bwd = [None if _ds_env is None else _ds_env != '0']  # None: automatic (head_dim 128)
 # bounded: a dS^T image above PADDLE_AMD_FA_DS_WS_MB (default 8 GiB) takes the recompute kernels
 from .workspace import workspace as _workspace
-_DS_WS = _workspace('flash_ds', int(os.environ.get('PADDLE_AMD_FA_DS_WS_MB', '8192')) << 20)
+_DS_WS = _workspace('flash_ds', int(pa_flag('fa_ds_ws_mb')) << 20)
 
 
 def set_ds_backward(on):

@@ -9,6 +9,7 @@ block-scaled MFMA kernel (``hip_fp8_mm``, 2x the bf16 MFMA rate) with per-tensor
 
 Reference: paddle/phi/kernels/funcs/blas/blaslt_impl.cu.h, fusion/fp8_gemm.
 """
+from ..framework.flags import pa_flag  # noqa: E402
 import os
 
 import torch
@@ -69,7 +70,7 @@ def hip_mm(a, b, out=None, bias=None, alpha=1.0, beta=0.0, splitk=1):
     return out
 
 
-_hip_gemm = os.environ.get('PADDLE_AMD_HIP_GEMM', '1') != '0'
+_hip_gemm = pa_flag('hip_gemm')
 
 
 def epi_ok(a, b, out_cols):
@@ -158,7 +159,7 @@ def _splitk_for(M, N_, K):
     return best
 
 
-_skinny = os.environ.get('PADDLE_AMD_SKINNY_GEMM', '1') != '0'
+_skinny = pa_flag('skinny_gemm')
 
 
 def skinny_ok(a, b):
@@ -338,7 +339,7 @@ def transpose2d(x):
     return y
 
 
-_kmajor_fwd = os.environ.get('PADDLE_AMD_KMAJOR_FWD', '1') != '0'
+_kmajor_fwd = pa_flag('kmajor_fwd')
 
 
 def kmajor_weight(x2, w):
@@ -362,7 +363,7 @@ def kmajor_weight(x2, w):
 _FP8_FMT = {torch.float8_e4m3fn: 0, torch.float8_e5m2: 1}
 # fp8 GEMM schedule: the 8-phase kernel (csrc/gemm8x.hip pa_gemm8_fp8, default) or the round-1
 # two-stage kernel (csrc/gemm.hip pa_gemm_fp8; PADDLE_AMD_FP8_8PHASE=0, A/B only)
-_fp8_8phase = os.environ.get('PADDLE_AMD_FP8_8PHASE', '1') != '0'
+_fp8_8phase = pa_flag('fp8_8phase')
 
 
 _FP8_WS = _new_workspace('fp8_splitk')

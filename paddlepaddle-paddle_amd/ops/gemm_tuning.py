@@ -6,6 +6,7 @@ cached per shape).  Here the per-shape winners for gfx950 are measured once on t
 process loads them read-only on first device use, so the fresh-box bench pays no tuning time.
 ``autotune.set_config({'kernel': {'enable': True}})`` re-enables online tuning.
 """
+from ..framework.flags import pa_flag  # noqa: E402
 import os
 
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -15,7 +16,7 @@ _applied = [False]
 
 def apply_tuned_db(path=None):
     """Enable TunableOp in read-only mode with the committed solution table (idempotent)."""
-    if _applied[0] or os.environ.get('PADDLE_AMD_GEMM_TUNING', '1') == '0':
+    if _applied[0] or not pa_flag('gemm_tuning'):
         return False
     path = path or DB
     if not os.path.exists(path):

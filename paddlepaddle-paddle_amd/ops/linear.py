@@ -14,6 +14,7 @@ buffers (inside the training engines); everything else takes the ordinary autogr
 
 Reference analogue: paddle/phi/kernels/fusion/gpu/fused_linear_param_grad_add_kernel.cu.
 """
+from ..framework.flags import pa_flag  # noqa: E402
 import os
 
 import torch
@@ -27,7 +28,7 @@ from . import fused, gemm
 # stream right before its dgrad GEMM on the compute stream, so the two (independent) GEMMs share
 # the chip; the compute stream joins the side stream before the gradient is announced ready.
 # Pays where a GEMM leaves CUs idle (the QKV weight gradient: 192 256x256 tiles on 256 CUs).
-WGRAD_OVERLAP = os.environ.get('PADDLE_AMD_WGRAD_OVERLAP', '0') == '1'
+WGRAD_OVERLAP = pa_flag('wgrad_overlap')
 OVERLAP_MIN_TILES = 128
 _side_streams = {}
 
@@ -79,7 +80,7 @@ def _wgrad_join(tok):
 # GEMM (ops.gemm.wgrad_accumulate_grouped2).  Its grad-ready hooks are held meanwhile
 # (parallel.flat_buffer.defer_grad) and anything still pending is flushed before the engines'
 # end-of-backward work (register_pre_finish) or by an end-of-backward callback.
-GROUP_WGRAD = os.environ.get('PADDLE_AMD_GROUP_WGRAD', '1') == '1'
+GROUP_WGRAD = pa_flag('group_wgrad')
 _pending = []          # [(x2, dy2, wparam, grad slot)] — at most one deferred weight gradient
 _cb_armed = [False]
 

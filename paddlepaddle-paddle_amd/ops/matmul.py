@@ -16,6 +16,7 @@ Reference: paddle/phi/kernels/impl/matmul_kernel_impl.h:960 (MatMulFunction: bro
 strides, vector cases), python/paddle/tensor/linalg.py:177 (matmul), :2133 (bmm).  Shapes outside
 the kernel contract (K % 64, odd dims, fp32, vectors, CPU / meta tensors) take torch's library path.
 """
+from ..framework.flags import pa_flag  # noqa: E402
 import os
 
 import torch
@@ -24,7 +25,7 @@ from . import _native as N
 from . import gemm
 
 _DT = {torch.bfloat16: 1, torch.float16: 2}
-_enabled = os.environ.get('PADDLE_AMD_HIP_MATMUL', '1') != '0'
+_enabled = pa_flag('hip_matmul')
 
 
 def _use(*ts):
@@ -78,7 +79,7 @@ def _bstride(t, nb):
 # library taken only when it is >= 2 % faster (reference: the matmul autotune cache of
 # paddle/phi/kernels/autotune/ behind paddle.incubate.autotune).  Off in multi-rank jobs, where
 # replicated computations must pick the same kernel on every rank (PADDLE_AMD_GEMM_AUTOTUNE=0: off).
-_TUNE = {'on': os.environ.get('PADDLE_AMD_GEMM_AUTOTUNE', '1') != '0', 'cache': {}, 'margin': 1.02}
+_TUNE = {'on': pa_flag('gemm_autotune'), 'cache': {}, 'margin': 1.02}
 
 
 def _time_ms(fn, reps=10):

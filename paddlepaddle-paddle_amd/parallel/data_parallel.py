@@ -14,6 +14,7 @@ MI355X design:
   compute of buckets k+1…; a queued end-of-backward callback flushes partial buckets
   (unused parameters) and makes the compute stream wait on every outstanding collective.
 """
+from ..framework.flags import pa_flag  # noqa: E402
 import contextlib
 
 import torch
@@ -173,7 +174,7 @@ class DataParallel(Layer):
         self.group = group
         self._strategy = strategy
         import os
-        force = os.environ.get('PADDLE_AMD_FORCE_COLLECTIVES', '0') == '1'  # 1-rank RCCL rehearsal
+        force = pa_flag('force_collectives')  # 1-rank RCCL rehearsal
         ready = dist.is_available() and dist.is_initialized() and (dist.get_world_size(_pg(group)) > 1 or force)
         self._reducer = None
         if ready:

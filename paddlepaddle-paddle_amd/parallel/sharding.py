@@ -25,6 +25,7 @@ MI355X design — everything is a contiguous slice:
   per dtype (ops.optim.adamw_flat), followed by async all-gathers of updated shards.
 * Global-norm clipping: sum of squares of the local gradient shards, one all-reduce.
 """
+from ..framework.flags import pa_flag  # noqa: E402
 import math
 
 import torch
@@ -167,13 +168,13 @@ class ShardingEngine:
         # multi-GPU stream ordering is exercised on one GPU (the gradients then equal the world-1
         # result bit for bit: a 1-rank AVG / SUM is the identity).
         import os
-        force = os.environ.get('PADDLE_AMD_FORCE_COLLECTIVES', '0') == '1' and dist.is_initialized()
+        force = pa_flag('force_collectives') and dist.is_initialized()
         self.collectives = self.world > 1 or force
         # one rank: the "shard" is the whole buffer, so units alias the optimizer arenas and
         # nothing is ever released, gathered or copied (no degenerate collectives either)
         if alias is None:
             import os
-            alias = os.environ.get('PADDLE_AMD_SHARDING_ALIAS', '1') != '0'
+            alias = pa_flag('sharding_alias')
         self.alias = not self.collectives and bool(alias)
         self.release_grads = release_grads and self.level == 3 and not self.alias
         self.reshard_after_forward = self._auto_reshard(model, params) if reshard_after_forward is None \

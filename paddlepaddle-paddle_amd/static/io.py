@@ -9,6 +9,7 @@ Format (ours, not the reference protobuf):
   namespaces — nothing from the file is executed as code.
 * ``<prefix>.pdiparams`` — safetensors with every captured constant (parameters, buffers).
 """
+from ..framework.flags import pa_flag  # noqa: E402
 import importlib
 import json
 import os
@@ -188,7 +189,7 @@ def _fetch_vids(prog, fetch_vars):
 def _pd_export(prog, feed_names, fetch_vids):
     """Reference ProgramDesc bytes (static/pdmodel.py) or None when the program uses an operator
     outside the exportable set (or PADDLE_AMD_PDMODEL=0): then this framework's IR is written."""
-    if os.environ.get('PADDLE_AMD_PDMODEL', '1') == '0':
+    if not pa_flag('pdmodel'):
         return None
     from . import pdmodel
     try:
@@ -220,7 +221,7 @@ def serialize_program(feed_vars, fetch_vars, program=None, **kw):
 def serialize_persistables(feed_vars, fetch_vars, executor=None, program=None, **kw):
     from safetensors.torch import save
     prog = program or default_main_program()
-    if getattr(prog, '_pd_params', None) is None and os.environ.get('PADDLE_AMD_PDMODEL', '1') != '0':
+    if getattr(prog, '_pd_params', None) is None and pa_flag('pdmodel'):
         feed_names = [v.name if isinstance(v, Tensor) else v for v in feed_vars]
         _pd_export(prog, feed_names, _fetch_vids(prog, fetch_vars))
     if getattr(prog, '_pd_params', None) is not None:  # reference .pdiparams: LoDTensor streams
@@ -263,8 +264,8 @@ def _pir_mode(kwargs):
     fmt = kwargs.get('format')
     if fmt is not None:
         return str(fmt).lower() in ('pir', 'json')
-    if os.environ.get('PADDLE_AMD_PIR') is not None:
-        return os.environ['PADDLE_AMD_PIR'] == '1'
+    if pa_flag('pir') != '':
+        return str(pa_flag('pir')) == '1'
     try:
         from ..framework.flags import get_flags
         return bool(get_flags(['FLAGS_enable_pir_api']).get('FLAGS_enable_pir_api', False))

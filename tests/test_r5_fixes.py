@@ -101,3 +101,34 @@ def test_matmul_autotune_cache_cleared_when_multi_rank_r6(monkeypatch):
     assert out == 'hip' and ('probe',) not in mm._TUNE['cache']
     mm.clear_tuning()
     assert mm.tuned_choices() == {}
+
+
+def test_framework_switches_live_in_flags_registry_r6(monkeypatch):
+    """The PADDLE_AMD_* A/B switches are FLAGS_pa_* flags (set_flags / FLAGS_ env / legacy env)."""
+    import paddle
+    from paddle.framework import flags
+    assert paddle.get_flags('FLAGS_pa_hip_gemm')['FLAGS_pa_hip_gemm'] is True
+    monkeypatch.setenv('PADDLE_AMD_FORCE_COLLECTIVES', '1')
+    assert flags.pa_flag('force_collectives') is True
+    monkeypatch.setenv('FLAGS_pa_force_collectives', '0')
+    assert flags.pa_flag('force_collectives') is False
+    old = flags.pa_flag('sot')
+    paddle.set_flags({'FLAGS_pa_sot': True})
+    try:
+        monkeypatch.setenv('PADDLE_AMD_SOT', '0')
+        assert flags.pa_flag('sot') is True  # an explicit set_flags wins over the environment
+    finally:
+        flags._REGISTRY['FLAGS_pa_sot'] = old
+        flags._EXPLICIT.discard('FLAGS_pa_sot')
+    import os
+    import re
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'paddlepaddle-paddle_amd')
+    stray = []
+    for dp, _, fns in os.walk(root):
+        for fn in fns:
+            if fn.endswith('.py'):
+                for ln in open(os.path.join(dp, fn)):
+                    m = re.search(r"os\.environ[^\n]*PADDLE_AMD_([A-Z0-9_]+)", ln)
+                    if m and m.group(1) not in ('KERNEL_LIB', 'ARCH'):
+                        stray.append((fn, m.group(1)))
+    assert not stray, stray

@@ -27,8 +27,7 @@ def main():
         clk = a.get('GRBM_GUI_ACTIVE', 0) / a['n'] / 8 / t / 1e9 if t else 0
         wc = a.get('SQ_WAVE_CYCLES', 0)
         print(f"{name}\n   dispatches {int(a['n'])}  avg {t*1e6:8.1f} us  effective clock {clk:.2f} GHz")
-        for k in ('SQ_WAVE_CYCLES', 'SQ_BUSY_CYCLES', 'SQ_WAIT_ANY', 'SQ_WAIT_INST_ANY', 'SQ_ACTIVE_INST_ANY',
-                  'SQ_VALU_MFMA_BUSY_CYCLES', 'SQ_INSTS_MFMA', 'GRBM_GUI_ACTIVE'):
+        for k in sorted(x for x in a if x not in ('t', 'n')):
             if k in a:
                 extra = f"  ({a[k] / wc * 100:5.1f} % of wave cycles)" if k.startswith('SQ_WAIT') and wc else ''
                 print(f"   {k:26s} {a[k] / a['n']:16.0f}{extra}")
@@ -36,6 +35,12 @@ def main():
             # MFMA pipes: 256 CUs x 4 SIMDs; busy cycles are summed over SIMDs
             simd_cycles = a['GRBM_GUI_ACTIVE'] / 8 * 256 * 4
             print(f"   MFMA pipe busy {a['SQ_VALU_MFMA_BUSY_CYCLES'] / simd_cycles * 100:5.1f} % of SIMD cycles")
+        if 'SQ_LDS_IDX_ACTIVE' in a and 'GRBM_GUI_ACTIVE' in a:
+            # LDS-array cycles summed over CUs (one LDS per CU): share of the CU cycles the array is busy
+            cu_cycles = a['GRBM_GUI_ACTIVE'] / 8 * 256
+            print(f"   LDS array busy {a['SQ_LDS_IDX_ACTIVE'] / cu_cycles * 100:5.1f} % of CU cycles (SQ_LDS_IDX_ACTIVE)")
+        if 'SQ_INSTS_VALU' in a and 'SQ_INSTS_MFMA' in a and a['SQ_INSTS_MFMA']:
+            print(f"   VALU : MFMA instructions {a['SQ_INSTS_VALU'] / a['SQ_INSTS_MFMA']:.2f}")
 
 
 if __name__ == '__main__':
