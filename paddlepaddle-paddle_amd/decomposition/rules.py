@@ -7,8 +7,8 @@ embedding_decomp, clip_decomp).
 Each rule takes the recorded node's arguments and rebuilds the op from primitives (elementwise
 arithmetic, exp/log/tanh/erf/rsqrt, sum/amax, where/maximum/minimum, matmul, reshape/cat,
 index_select).  As in the reference rules, half-precision inputs of the normalisations and softmax
-are computed in float32 and cast back.  Reduction counts are plain ints (they may carry a dynamic-dim
-sentinel factor, which the Executor re-specialises at run time).
+are computed in float32 and cast back.  Reduction counts are ints built from the input's shape (a
+SymInt expression of the dynamic dims, evaluated by the Executor at run time).
 """
 import math
 
@@ -38,7 +38,7 @@ def _dims(x, dim):
 def _count(x, dims):
     n = 1
     for d in dims:
-        n *= int(x.shape[d])
+        n = n * x.shape[d]  # a SymInt for dynamic dims (static/symbolic.py): no int()
     return n
 
 

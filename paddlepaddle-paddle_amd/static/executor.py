@@ -12,6 +12,7 @@ import numpy as np
 import torch
 
 from ..core.tensor import Tensor, _wrap
+from . import symbolic as _sym
 from .program import (Program, Ref, Const, default_main_program, default_startup_program, SENTINELS, _paused,
                       _vid_of)
 
@@ -91,9 +92,28 @@ class CompiledProgram:
         return self
 
 
-def _subst_int(v, smap):
+class _SymEnv(dict):
+    """Symbol index -> fed extent (an unfed symbol keeps its carrier extent)."""
+
+    def __init__(self, smap):
+        super().__init__()
+        self.smap = smap
+
+    def __missing__(self, i):
+        return self.smap.get(SENTINELS[i], SENTINELS[i])
+
+
+def _subst_int(v, smap, prog=None):
+    """A recorded int at run time: a SymInt's expression (or a value-table entry's) evaluated with
+    the fed extents; other ints unchanged.  Programs without a value table (loaded from the
+    pre-symbolic format) re-specialise by factoring the carrier primes out."""
     if isinstance(v, bool) or v == 0 or not smap:
-        return v
+        return int(v) if isinstance(v, _sym.SymInt) else v
+    if isinstance(v, _sym.SymInt):
+        return v.expr.eval(_SymEnv(smap))
+    if prog is not None and getattr(prog, '_symbolic', False):
+        e = prog._symvals.get(v)
+        return e.eval(_SymEnv(smap)) if e is not None else v
     out, rest = 1, v
     hit = False
     for s in SENTINELS:
@@ -114,13 +134,13 @@ def _resolve(prog, obj, env, smap, dev):
     if isinstance(obj, bool) or obj is None:
         return obj
     if isinstance(obj, int):
-        return _subst_int(obj, smap)
+        return _subst_int(obj, smap, prog)
     if isinstance(obj, torch.device):
         return dev if obj.type == 'meta' else obj
     if isinstance(obj, str) and obj == 'meta':
         return dev
     if isinstance(obj, torch.Size):
-        return torch.Size([_subst_int(x, smap) for x in obj])
+        return torch.Size([_subst_int(x, smap, prog) for x in obj])
     if isinstance(obj, tuple) and hasattr(obj, '_fields'):
         return type(obj)(*[_resolve(prog, o, env, smap, dev) for o in obj])
     if isinstance(obj, (list, tuple)):

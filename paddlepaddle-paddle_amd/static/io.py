@@ -17,6 +17,7 @@ import os
 import torch
 
 from ..core.tensor import Tensor, _wrap
+from . import symbolic as _sym
 from .program import Program, Node, Ref, Const, default_main_program, _vid_of, _paused
 
 _NAMESPACES = ('torch', 'torch.nn.functional', 'torch._C._nn', 'torch.linalg', 'torch.special', 'torch.fft',
@@ -80,6 +81,8 @@ def _enc(v):
         return {'r': v.vid}
     if isinstance(v, Const):
         return {'c': v.cid}
+    if isinstance(v, _sym.SymInt):  # a dynamic-dim expression (static/symbolic.py)
+        return {'sym': [int(v), v.expr.to_json()]}
     if v is None or isinstance(v, (bool, int, float, str)):
         return v
     if isinstance(v, torch.dtype):
@@ -112,6 +115,8 @@ def _dec(v):
         return Ref(v['r'])
     if 'c' in v:
         return Const(v['c'])
+    if 'sym' in v:
+        return _sym.SymInt(v['sym'][0], _sym.expr_from_json(v['sym'][1]))
     if 'dt' in v:
         return _DTYPES[v['dt']]
     if 'dev' in v:
@@ -213,6 +218,8 @@ def serialize_program(feed_vars, fetch_vars, program=None, **kw):
         feeds.append({'name': name, 'vid': vid, 'shape': shape, 'dtype': str(dt).replace('torch.', '')})
     doc = {'format': 'paddle_amd.program/1', 'feeds': feeds, 'fetch': _fetch_vids(prog, fetch_vars),
            'nodes': _enc_nodes(prog.nodes),
+           'symbolic': 1 if getattr(prog, '_symbolic', False) else 0,
+           'symvals': [[k, e.to_json()] for k, e in getattr(prog, '_symvals', {}).items()],
            'consts': {str(cid): (prog._const_owner.get(cid).name if getattr(prog, '_const_owner', {}).get(cid)
                                  is not None else None) for cid in prog.consts}}
     return json.dumps(doc).encode()
@@ -246,6 +253,10 @@ def save_inference_model(path_prefix, feed_vars, fetch_vars, executor=None, prog
 
 class LoadedProgram(Program):
     """A Program rebuilt from files; fetch targets are placeholder Variables."""
+
+    def __init__(self):
+        super().__init__()
+        self._symbolic = False  # set by the loader when the file carries its dim expressions
 
 
 def deserialize_program(data, device=None):
@@ -295,6 +306,9 @@ def _deserialize_program(data, device=None):
     doc = json.loads(data.decode() if isinstance(data, (bytes, bytearray)) else data)
     prog = LoadedProgram()
     prog.nodes = _dec_nodes(doc['nodes'])
+    if doc.get('symbolic'):  # dims as expressions; files without it re-specialise by factoring
+        prog._symbolic = True
+        prog._symvals = {int(k): _sym.expr_from_json(e) for k, e in doc.get('symvals', [])}
     for fd in doc['feeds']:
         prog.feeds[fd['name']] = (fd['vid'], fd['shape'], _DTYPES[fd['dtype']])
         m = torch.empty([max(s, 1) for s in fd['shape']], dtype=_DTYPES[fd['dtype']], device='meta')

@@ -4,10 +4,12 @@ program_guard, default_main_program; python/paddle/static/input.py data, InputSp
 Design: a ``Program`` is a recorded op list (a small IR), not a protobuf desc.  While static
 mode is on, a ``TorchFunctionMode`` records every tensor operation whose inputs derive from a
 static ``Variable``.  Variables carry *meta* tensors (shape/dtype only, no memory), so building
-a program for a 1.3B model costs nothing.  Dynamic dims (``None``/-1) are given sentinel
-extents (primes just below 2^20, one per dim position); integer arguments built from them (``B*S``,
-``arange(S)``) are re-specialised at run time by factoring the sentinels out — so user code
-that reads ``x.shape`` and reshapes still runs at any feed shape.
+a program for a 1.3B model costs nothing.  Dynamic dims (``None``/-1) are symbols
+(static/symbolic.py): their meta tensors carry large-prime carrier extents, shape reads of program
+values return ``SymInt``s that carry a DimExpr through Python shape arithmetic (``B*S``,
+``arange(S)``), and the Executor evaluates the recorded expressions with the fed extents — so user
+code that reads ``x.shape`` and reshapes still runs at any feed shape, while plain integer
+constants are never touched.
 
 Real tensors touched by a recorded op (parameters, buffers, captured constants) are kept by
 reference (``Const``), so optimizer updates made at run time are seen by later runs.
@@ -21,6 +23,7 @@ import torch
 from torch.overrides import TorchFunctionMode
 
 from ..core.tensor import Tensor, _wrap
+from . import symbolic as _sym
 
 # one sentinel extent per dynamic-dim position (dim 0 = batch, dim 1 = sequence, ...): the six
 # largest primes below 2^20, so an unrelated recorded integer is a multiple of one with odds of
@@ -67,16 +70,38 @@ class Node:
         return f"{self.outs} = {self.kind}:{name}{tuple(self.args)}"
 
 
-def _has_sentinel(v):
+def _has_sentinel(v, prog=None):
+    """Does v (an op argument) depend on a dynamic dim?  SymInts do; a plain int does when the
+    program's value table holds it (a SymInt of that value escaped through ``int()`` /
+    ``operator.index``) — or, for programs loaded without a value table, when a carrier prime
+    divides it (the pre-symbolic rule)."""
     if isinstance(v, bool):
         return False
+    if isinstance(v, _sym.SymInt):
+        return True
     if isinstance(v, int):
         if v == 0:
             return False
+        if prog is not None and getattr(prog, '_symbolic', False):
+            return v in prog._symvals
         return any(v % s == 0 for s in SENTINELS)
     if isinstance(v, (list, tuple, torch.Size)):
-        return any(_has_sentinel(x) for x in v)
+        return any(_has_sentinel(x, prog) for x in v)
     return False
+
+
+# shape reads of program values answer in SymInts (static/symbolic.py)
+_SHAPE_FUNCS = {torch.Tensor.size, torch.Tensor.numel, torch.Tensor.stride, torch.Tensor.shape.__get__}
+
+
+def _symbolic_shape(out):
+    if isinstance(out, torch.Size):
+        return torch.Size([_sym.symbolize(d, SENTINELS) for d in out])
+    if isinstance(out, tuple):
+        return tuple(_sym.symbolize(d, SENTINELS) for d in out)
+    if isinstance(out, int):
+        return _sym.symbolize(out, SENTINELS)
+    return out
 
 
 class Block:
@@ -119,6 +144,8 @@ class Program:
         self._id = next(Program._ids)
         self._blocks = [Block(self)]
         self._for_test = False
+        self._symbolic = True   # dynamic dims are symbols (static/symbolic.py)
+        self._symvals = {}      # value table: SymInt values that escaped through int() -> DimExpr
 
     # ---- structure
     def global_block(self):
@@ -241,6 +268,12 @@ class _Recorder(TorchFunctionMode):
 
     def __torch_function__(self, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
+        if func in _SHAPE_FUNCS and args and isinstance(args[0], torch.Tensor) and args[0].is_meta:
+            # shape reads (also while paused): carrier extents come back as SymInts
+            prog = default_main_program()
+            out = func(*args, **kwargs)
+            with _sym.recording_table(prog._symvals):
+                return _symbolic_shape(out)
         if self.paused:
             return func(*args, **kwargs)
         prog = default_main_program()
@@ -253,8 +286,8 @@ class _Recorder(TorchFunctionMode):
         forced = getattr(prog, '_force_record_ids', None)  # decomposition: ops on captured params
         if forced and not static_input:
             static_input = any(id(t) in forced for t in metas)
-        if not static_input and not dev_meta and not (not metas and (_has_sentinel(list(args)) or
-                                                                    _has_sentinel(list(kwargs.values())))):
+        if not static_input and not dev_meta and not (not metas and (_has_sentinel(list(args), prog) or
+                                                                    _has_sentinel(list(kwargs.values()), prog))):
             if any(t.is_meta for t in metas):
                 return func(*args, **kwargs)  # meta work unrelated to this program
             return func(*args, **kwargs)
@@ -388,6 +421,13 @@ def _paused():
 
 def recording():
     return _recorder[0] is not None and not _recorder[0].paused
+
+
+def _recording_table():
+    return default_main_program()._symvals if _recorder[0] is not None else None
+
+
+_sym._GETTER[0] = _recording_table
 
 
 # ----------------------------------------------------------------- data / InputSpec
