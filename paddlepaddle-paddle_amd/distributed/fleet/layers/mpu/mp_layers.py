@@ -24,6 +24,63 @@ def _size_rank(group):
     return mp_ops._n(group), mp_ops._r(group)
 
 
+def _mp_async_allreduce():
+    """strategy.hybrid_configs['mp_configs']['mp_async_allreduce'] (default True here)."""
+    from ... import fleet as _fleet
+    st = getattr(_fleet, '_strategy', None)
+    cfg = (getattr(st, 'hybrid_configs', None) or {}).get('mp_configs', {}) if st is not None else {}
+    return bool(cfg.get('mp_async_allreduce', True))
+
+
+class _ColumnParallelLinearFn(torch.autograd.Function):
+    """Column-parallel Linear with the input-gradient all-reduce overlapped with the weight-gradient
+    GEMM (reference: distributed/passes/allreduce_matmul_grad_overlapping.py:37 and the
+    mp_async_allreduce path of mp_layers.py).  Backward: dX = dY W^T, launch its all-reduce over the
+    mp group asynchronously (RCCL on its own stream), compute dW = X^T dY and db while it runs, wait.
+    Under a zero-bubble pipeline (WeightGradStore active) dW / db are queued for the W pass instead."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, wp, bp, group):
+        ctx.save_for_backward(x, w)
+        ctx.wp, ctx.bp, ctx.group = wp, bp, group
+        from .....ops import matmul as _mm
+        return _mm.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        import torch.distributed as dist
+        x, w = ctx.saved_tensors
+        dx = torch.matmul(dy, w.t()).contiguous()
+        work = dist.all_reduce(dx, group=mp_ops._pg(ctx.group), async_op=True)
+        need_w = ctx.needs_input_grad[1]
+        need_b = ctx.needs_input_grad[2]
+        dw = db = None
+        if need_w or need_b:
+            x2 = x.reshape(-1, x.shape[-1])
+            dy2 = dy.reshape(-1, dy.shape[-1])
+            from ...meta_parallel.zero_bubble_utils import WeightGradStore, _accumulate
+            if WeightGradStore.active:
+                from .....parallel.flat_buffer import defer_grad
+                wp, bp = ctx.wp, ctx.bp
+                if need_w:
+                    defer_grad(wp)
+                if need_b:
+                    defer_grad(bp)
+                x2d, dy2d = x2.detach(), dy2.detach()
+
+                def w_pass():
+                    if need_w:
+                        _accumulate(wp, x2d.t().matmul(dy2d))
+                    if need_b:
+                        _accumulate(bp, dy2d.sum(0))
+                WeightGradStore.put(w_pass)
+            else:
+                dw = x2.t().matmul(dy2) if need_w else None  # overlaps the all-reduce of dx
+                db = dy2.sum(0) if need_b else None
+        work.wait()
+        return dx, dw, db, None, None, None
+
+
 class VocabParallelEmbedding(Layer):
     def __init__(self, num_embeddings, embedding_dim, weight_attr=None, mp_group=None, name=None):
         super().__init__()
@@ -72,6 +129,19 @@ class ColumnParallelLinear(Layer):
             self.bias = None
 
     def forward(self, x):
+        from .....framework import in_dynamic_mode
+        if self.is_mp and in_dynamic_mode() and torch.is_grad_enabled() and _mp_async_allreduce() and \
+                not self.weight.stop_gradient:
+            xt = _unwrap(x)
+            w = self.weight._t
+            b = self.bias._t if self.bias is not None else None
+            if w.dtype != xt.dtype:  # AMP: compute in the activation dtype
+                w = w.to(xt.dtype)
+                b = b.to(xt.dtype) if b is not None else None
+            out = _wrap(_ColumnParallelLinearFn.apply(xt, w, b, self.weight, self.bias, self.model_parallel_group))
+            if self.gather_output:
+                out = mp_ops._c_concat(out, group=self.model_parallel_group)
+            return out
         if self.is_mp:
             x = mp_ops._c_identity(x, group=self.model_parallel_group)
         out = F.linear(x, self.weight, self.bias)

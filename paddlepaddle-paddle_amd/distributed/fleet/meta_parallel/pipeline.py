@@ -16,6 +16,7 @@ import torch.distributed as dist
 
 from ....nn.layer.layers import Layer
 from ....core.tensor import Tensor, _wrap, _unwrap
+from .zero_bubble_utils import WeightGradStore, schedule_order
 
 
 class LayerDesc:
@@ -203,6 +204,9 @@ class PipelineParallel(Layer):
         from ..utils.hybrid_parallel_util import (dp_sep_group_and_scale, broadcast_dp_parameters,
                                                   broadcast_sep_parameters)
         self._dp_group = dp_sep_group_and_scale(hcg)[0]
+        # 'schedule_mode': '1F1B' (default) or 'ZBH1' (zero bubble, reference
+        # passes/pipeline_scheduler_pass/pipeline_zero_bubble.py)
+        self._schedule_mode = cfg.get('schedule_mode', '1F1B')
         if hcg.get_sep_parallel_world_size() > 1:
             broadcast_sep_parameters(self._layers, hcg)
         if hcg.get_data_parallel_world_size() > 1 and hcg.get_sharding_parallel_world_size() == 1:
@@ -334,7 +338,10 @@ class PipelineParallel(Layer):
         if eng is not None and hasattr(eng, 'dp_final'):
             eng.dp_final = bool(final)
 
-    def _bwd_step(self, x, out):
+    def _bwd_step(self, x, out, split=False):
+        """Backward of one micro-batch; ``split`` (zero bubble): only B runs here — the Linear
+        weight gradients are queued in the WeightGradStore and run by _w_step after the input
+        gradient has been sent."""
         if self.is_last:
             _unwrap(out).backward()
         else:
@@ -342,9 +349,26 @@ class PipelineParallel(Layer):
             g = self._take(self._grad_q)
             self._post_grad(o.device)
             o.backward(g)
+        if split:
+            WeightGradStore.flush()
         if not self.is_first:
             gx = _unwrap(x).grad
             self._isend(gx.contiguous(), self._prev, group=self._gpg())
+
+    def _w_step(self):
+        WeightGradStore.pop()
+
+    def _schedule_kind(self, optimizer):
+        kind = str(self._schedule_mode or '1F1B').upper().replace('-', '')
+        if kind in ('ZBH1', 'ZB', 'ZEROBUBBLE'):
+            if getattr(optimizer, '_syncs_dp', False):
+                # a sharding optimizer reduce-scatters inside backward: its gradient hooks must see
+                # complete weight gradients, which only the unsplit backward gives
+                import warnings
+                warnings.warn("ZBH1 pipeline schedule with a sharding optimizer: running 1F1B", RuntimeWarning)
+                return '1F1B'
+            return 'ZBH1'
+        return '1F1B'
 
     def train_batch(self, data, optimizer, lr_scheduler=None, scaler=None):
         inputs, labels = data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None)
@@ -352,30 +376,28 @@ class PipelineParallel(Layer):
         mbs_lab = self._split(labels) if (self.is_last and labels is not None) else [None] * self.accumulate_steps
         n = self.accumulate_steps
         self._begin(n, n)
-        warm = min(self.num_stages - self.stage_id - 1, n)
-        pending = []
-        losses = []
-        fi = 0
-        for _ in range(warm):
-            x, out = self._fwd_step(mbs_in[fi], mbs_lab[fi])
-            pending.append((x, out))
-            if self.is_last:
-                losses.append(_unwrap(out).detach())
-            fi += 1
-        bi = 0
-        for _ in range(n - warm):
-            x, out = self._fwd_step(mbs_in[fi], mbs_lab[fi])
-            pending.append((x, out))
-            if self.is_last:
-                losses.append(_unwrap(out).detach())
-            fi += 1
-            self._set_dp_final(optimizer, bi == n - 1)  # dp all-reduce overlap on the last micro-batch
-            self._bwd_step(*pending.pop(0))
-            bi += 1
-        while pending:
-            self._set_dp_final(optimizer, bi == n - 1)
-            self._bwd_step(*pending.pop(0))
-            bi += 1
+        kind = self._schedule_kind(optimizer)
+        split = kind == 'ZBH1'
+        # the stage's op sequence (zero_bubble_utils.schedule_order: 1F1B, or ZB-H1 with every
+        # backward split into B — input gradient, sent at once — and W — weight gradients)
+        pending, losses = {}, []
+        WeightGradStore.clear()
+        WeightGradStore.active = split
+        try:
+            for op, i in schedule_order(kind, self.num_stages, self.stage_id, n):
+                if op == 'F':
+                    x, out = self._fwd_step(mbs_in[i], mbs_lab[i])
+                    pending[i] = (x, out)
+                    if self.is_last:
+                        losses.append(_unwrap(out).detach())
+                elif op in ('B', 'BW'):
+                    self._set_dp_final(optimizer, i == n - 1)  # dp all-reduce overlap on the last micro-batch
+                    self._bwd_step(*pending.pop(i), split=split)
+                else:
+                    self._w_step()
+        finally:
+            WeightGradStore.active = False
+        assert not pending and WeightGradStore.pending() == 0
         self._set_dp_final(optimizer, True)
         assert not (self._act_q or self._grad_q or self._acts_left or self._grads_left), "unmatched pipeline receives"
         self._drain_sends()

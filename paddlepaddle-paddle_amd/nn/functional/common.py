@@ -12,11 +12,19 @@ from ... import ops
 from ...core.amp_dispatch import amp_op as _amp_op
 
 
+_ZB = [None]  # distributed.fleet.meta_parallel.zero_bubble_utils, imported on first use
+
+
 @_amp_op('matmul_v2')
 def linear(x, weight, bias=None, name=None):
     """y = x @ W + b with W stored [in_features, out_features] (paddle layout)."""
     t, w = _u(x), _u(weight)
     b = _u(bias) if bias is not None else None
+    if _ZB[0] is None:
+        from ...distributed.fleet.meta_parallel import zero_bubble_utils as _zbm
+        _ZB[0] = _zbm
+    if _ZB[0].WeightGradStore.active and w.requires_grad and torch.is_grad_enabled():
+        return _w(_ZB[0].split_linear(t, w, b, weight, bias))  # zero-bubble pipeline: dW deferred to W
     if ops.fp8._ACTIVE['enabled'] and ops.fp8.eligible(t, w):  # paddle.amp.fp8_autocast
         return _w(ops.fp8.fp8_linear(t, w, b, holder=weight if isinstance(weight, Tensor) else None))
     if isinstance(weight, Tensor) and '_flat' in weight.__dict__ and ops.linear.eligible(weight) and \

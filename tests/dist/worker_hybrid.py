@@ -135,11 +135,11 @@ class Block(nn.Layer):
         return paddle.tanh(self.fc(x))
 
 
-def pp_test(virtual=1, acc=4, tag=None):
+def pp_test(virtual=1, acc=4, tag=None, sched='1F1B'):
     world = int(os.environ['WORLD_SIZE'])
     s = fleet.DistributedStrategy()
     s.hybrid_configs = {'dp_degree': 1, 'mp_degree': 1, 'pp_degree': world}
-    s.pipeline_configs = {'accumulate_steps': acc, 'micro_batch_size': 8 // acc}
+    s.pipeline_configs = {'accumulate_steps': acc, 'micro_batch_size': 8 // acc, 'schedule_mode': sched}
     fleet.init(is_collective=True, strategy=s)
     d = 6
     nblk = 2 * world * virtual
@@ -162,7 +162,15 @@ def pp_test(virtual=1, acc=4, tag=None):
     opt = paddle.optimizer.SGD(learning_rate=0.1, parameters=pl.parameters())
     x = paddle.to_tensor(np.random.RandomState(0).randn(8, d).astype('float32'))
     y = paddle.to_tensor(np.random.RandomState(1).randn(8, d).astype('float32'))
+    if sched == 'ZBH1':
+        from paddle.distributed.fleet.meta_parallel import zero_bubble_utils as zb
+        calls = []
+        orig = zb.SplitBwLinear.backward
+        zb.SplitBwLinear.backward = staticmethod(lambda ctx, dy: (calls.append(1), orig(ctx, dy))[1])
     loss = model.train_batch([x, y], opt)
+    if sched == 'ZBH1':
+        zb.SplitBwLinear.backward = orig
+        assert calls and zb.WeightGradStore.pending() == 0  # backward really ran split (B, then W)
     # reference: same micro-batches, mean of per-micro-batch losses
     ropt = paddle.optimizer.SGD(learning_rate=0.1, parameters=[p for b in full for p in b.parameters()])
     tot = 0.0
@@ -179,7 +187,7 @@ def pp_test(virtual=1, acc=4, tag=None):
     for blk, gi in zip(pl.run_function, owned):
         np.testing.assert_allclose(blk.fc.weight.numpy(), full[gi].fc.weight.numpy(), atol=1e-5)
     tag = tag or ('pp' if virtual == 1 else 'vpp')
-    if virtual > 1:
+    if virtual > 1 and sched == '1F1B':
         # the reference's choice (fleet/model.py:168): FthenB for pp <= acc < 2 pp, else 1F1B
         want = 'interleaved_fthenb' if acc < 2 * world else 'interleaved_1f1b'
         assert model.schedule == want, (model.schedule, want)
@@ -188,4 +196,5 @@ def pp_test(virtual=1, acc=4, tag=None):
 
 if __name__ == '__main__':
     {'tp': tp_test, 'sp': sp_test, 'pp': pp_test, 'vpp': lambda: pp_test(2), 'vpp8': lambda: pp_test(2, 8, 'vpp8'),
-     'tpdp': tpdp_test}[sys.argv[1]]()
+     'tpdp': tpdp_test, 'zbh1': lambda: pp_test(1, 4, 'zbh1', 'ZBH1'),
+     'zbh1_8': lambda: pp_test(1, 8, 'zbh1_8', 'ZBH1')}[sys.argv[1]]()

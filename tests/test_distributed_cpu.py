@@ -365,3 +365,26 @@ def test_segment_parallel_matches_single_process(mode, nproc):
     (reference fleet/utils/hybrid_parallel_util.py:241), weights broadcast over sep."""
     out = run_workers('worker_sep.py', mode, nproc=nproc)
     assert out.count(f'{mode} OK') == nproc, out[-3000:]
+
+
+@pytest.mark.parametrize("mode,nproc", [('zbh1', 2), ('zbh1_8', 4)])
+def test_zero_bubble_pipeline_matches_single_device(mode, nproc):
+    """ZB-H1 (backward split into B and deferred W, dX sent before W) trains exactly like the
+    single-device model (reference passes/pipeline_scheduler_pass/pipeline_zero_bubble.py)."""
+    out = run_workers('worker_hybrid.py', mode, nproc=nproc)
+    assert out.count(f'{mode} OK') == nproc, out[-3000:]
+
+
+def test_zero_bubble_schedule_shrinks_the_bubble():
+    """The schedule shape: every stage's op list played against the others (unit F / B / W costs):
+    ZB-H1's bubble is (S-1)(F+B) against 1F1B's (S-1)(F+B+W)."""
+    sys.path.insert(0, ROOT)
+    from paddle.distributed.fleet.meta_parallel.zero_bubble_utils import simulate, schedule_order
+    for S, M in [(2, 4), (4, 8), (8, 16), (8, 32)]:
+        m1, b1 = simulate('1F1B', S, M)
+        mz, bz = simulate('ZBH1', S, M)
+        assert m1 == 3 * M + 3 * (S - 1) and mz == 3 * M + 2 * (S - 1), (S, M, m1, mz)
+        assert bz < b1
+        for s in range(S):  # every micro-batch's F, B and W exactly once per stage
+            ops = schedule_order('ZBH1', S, s, M)
+            assert sorted(ops) == sorted([(k, i) for k in 'FBW' for i in range(M)])
