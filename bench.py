@@ -81,6 +81,19 @@ def _feeder(dsts, pool):
     return feed
 
 
+class _Step:
+    """A bench step: ``feed()`` copies the next pre-generated batch into the input tensors, ``core()``
+    runs forward / backward / optimizer on them; calling the step runs both.  ``--graph`` captures
+    only ``core`` (the feed stays outside the graph, so every replay trains on new data)."""
+
+    def __init__(self, feed, core):
+        self.feed, self.core = feed, core
+
+    def __call__(self):
+        self.feed()
+        return self.core()
+
+
 def build_gpt(args, world, rank, dev):
     import torch
     import paddle
@@ -106,14 +119,14 @@ def build_gpt(args, world, rank, dev):
     feed = _feeder([(x._t, y._t)], [(p[:, :-1], p[:, 1:]) for p in pool])
     inner = model._layers if hasattr(model, '_layers') else model
 
-    def step():
-        feed()
+    def core():
         logits = model(x)
         loss = inner.loss(logits, y)
         loss.backward()
         opt.step()
         opt.clear_grad()
         return loss
+    step = _Step(feed, core)
 
     mcfg = {'model': args.model, 'global_batch': B * world, 'micro_batch_per_gpu': B, 'seq_len': S,
             'parallelism': (f"sharding-{ {'os': 1, 'os_g': 2, 'p_g_os': 3}.get(args.sharding, 0)}x{world}"
@@ -145,14 +158,14 @@ def build_resnet(args, world, rank, dev):
     img, lab = paddle.to_tensor(pool[0][0].clone()), paddle.to_tensor(pool[0][1].clone())
     feed = _feeder([(img._t, lab._t)], pool)
 
-    def step():
-        feed()
+    def core():
         out = model(img)
         loss = paddle.nn.functional.cross_entropy(out, lab)
         loss.backward()
         opt.step()
         opt.clear_grad()
         return loss
+    step = _Step(feed, core)
 
     mcfg = {'model': args.resnet_model, 'global_batch': B * world, 'image': f'{res}x{res} NHWC', 'parallelism': f"dp{world}",
             'optimizer': 'Momentum'}
@@ -182,13 +195,13 @@ def build_llama(args, world, rank, dev):
     feed = _feeder([(x._t, y._t)], [(p[:, :-1], p[:, 1:]) for p in pool])
     inner = model._layers if hasattr(model, '_layers') else model
 
-    def step():
-        feed()
+    def core():
         loss = inner.loss(model(x), y)
         loss.backward()
         opt.step()
         opt.clear_grad()
         return loss
+    step = _Step(feed, core)
     nparam = sum(p._t.numel() for p in inner.parameters())
     mcfg = {'model': 'llama2-13b (per-GPU share of TP2xPP2xsharding2)', 'layers': args.llama_layers,
             'of_layers': 40, 'hidden': 5120, 'heads': 40, 'ffn': 13824, 'vocab': cfg.vocab_size,
@@ -231,19 +244,19 @@ def build_ernie_static(args, world, rank, dev, fp8):
     # a different pre-generated batch every step, already on the device; the loss is fetched every
     # step as a device tensor (return_numpy=False): the host does not wait for the device inside the
     # loop (as the dygraph benches); measure() reads it after the timing
-    feeds = [{'ids': paddle.to_tensor(rng.randint(1, cfg.vocab_size, size=(B, S)).astype('int64'), place=place),
-              'lab': paddle.to_tensor(rng.randint(0, 2, size=(B,)).astype('int64'), place=place)}
-             for _ in range(_pool_len(args))]
-    it = [0]
+    pool = [(paddle.to_tensor(rng.randint(1, cfg.vocab_size, size=(B, S)).astype('int64'), place=place)._t,
+             paddle.to_tensor(rng.randint(0, 2, size=(B,)).astype('int64'), place=place)._t)
+            for _ in range(_pool_len(args))]
+    fed = {'ids': paddle.to_tensor(pool[0][0].clone()), 'lab': paddle.to_tensor(pool[0][1].clone())}
+    feed = _feeder([(fed['ids']._t, fed['lab']._t)], pool)
 
-    def step():
-        fed = feeds[it[0] % len(feeds)]
-        it[0] += 1
+    def core():
         paddle.enable_static()
         try:
             return exe.run(main, feed=fed, fetch_list=[loss], return_numpy=False)[0]
         finally:
             paddle.disable_static()
+    step = _Step(feed, core)
     mcfg = {'model': 'ernie-3.0-base seq-cls', 'batch': B, 'seq_len': S,
             'mode': 'static Program + Executor, static.amp O2 ' + ('fp8 (e4m3/e5m2, delayed scaling)' if fp8 else 'bf16')}
     return step, B * S * world, 'tokens/sec ERNIE-3.0 static AMP-O2', 'tokens/s', mcfg
@@ -284,7 +297,7 @@ def _maybe_graph(args, step, cfg):
         return step
     from paddle.device.cuda.graphs import capture_train_step
     cfg['hip_graph'] = True
-    return capture_train_step(step, warmup=args.warmup - 1)
+    return _Step(step.feed, capture_train_step(step.core, warmup=args.warmup - 1))
 
 
 def measure(step, steps, warmup, world, rank, dev, tag):

@@ -320,8 +320,9 @@ def _run_pipelined(prog, feed, dev, pol):
     return run_pipeline(prog, feed, dev, pol, pol.pipeline, run_forward)
 
 
-def run_program(prog, feed, dev, grad=None):
-    """Interpret ``prog``; returns the value env."""
+def run_program(prog, feed, dev, grad=None, fetch=None):
+    """Interpret ``prog``; returns the value env.  ``fetch``: the value ids the caller will read
+    (lets the dead-code / common-subexpression passes drop and merge everything else)."""
     pol = _pipeline_policy(prog)
     if pol is not None and (grad is None or grad):
         return _run_pipelined(prog, feed, dev, pol)
@@ -333,7 +334,7 @@ def run_program(prog, feed, dev, grad=None):
     ctx = contextlib.nullcontext() if needs_grad else torch.no_grad()
     from .amp import autocast_context
     from .ir_passes import ir_nodes
-    nodes = ir_nodes(prog, dev)  # the fusion-pass rewrite (static/ir_passes.py) on GPU programs
+    nodes = ir_nodes(prog, dev, fetch)  # the fusion-pass rewrite (static/ir_passes.py) on GPU programs
     with _paused(), ctx, autocast_context(prog, dev) as subs:
         prev, _SUBS['map'] = _SUBS['map'], subs
         try:
@@ -384,10 +385,10 @@ class Executor:
         if _decomp._prim_config['prim_enabled'] and not getattr(program, '_prim_decomposed', False):
             _decomp.decompose(program, [])  # incubate.autograd.enable_prim(): run on primitive ops
             program._prim_decomposed = True
-        env = run_program(program, feed, self._dev)
         fetch_list = fetch_list if fetch_list is not None else []
         if not isinstance(fetch_list, (list, tuple)):
             fetch_list = [fetch_list]
+        env = run_program(program, feed, self._dev, fetch=self._fetch_vids(program, fetch_list))
         out = []
         for f in fetch_list:
             t = self._fetch(program, env, f)
@@ -397,6 +398,24 @@ class Executor:
             else:
                 out.append(_wrap(t))
         return out
+
+    @staticmethod
+    def _fetch_vids(program, fetch_list):
+        """Value ids of the fetch targets (None when one cannot be resolved before the run)."""
+        vids = []
+        for f in fetch_list:
+            if isinstance(f, str):
+                f = program.named_vars.get(f)
+                if f is None:
+                    continue  # a parameter name: read from its live storage, not the env
+            tt = f._t if isinstance(f, Tensor) else f
+            if not isinstance(tt, torch.Tensor) or not tt.is_meta:
+                continue
+            vid = program._val.get(id(tt))
+            if vid is None:
+                return None
+            vids.append(vid)
+        return tuple(sorted(set(vids)))
 
     @staticmethod
     def _fetch(program, env, f):

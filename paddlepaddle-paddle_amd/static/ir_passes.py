@@ -15,7 +15,10 @@ Both node vocabularies are matched: torch-level nodes recorded from dygraph-styl
 (``torch.matmul`` / ``Tensor.masked_fill`` / ``F.layer_norm`` ...) and Paddle-operator nodes of
 an imported ProgramDesc (``matmul_v2`` / ``scale`` / ``softmax`` / ``layer_norm`` ...).
 
-Passes (names follow the reference where one exists):
+Passes (names follow the reference where one exists; general and convolution passes in
+static/ir_passes_ext.py: constant_folding_pass, common_subexpression_elimination_pass,
+dead_code_elimination_pass, conv2d_bn_fuse_pass, conv2d_add_act_fuse_pass,
+embedding_eltwise_layernorm_fuse_pass, fused_weight_only_linear_pass):
   multihead_matmul_fuse_pass_v2   q@k^T -> *scale -> (+mask | masked_fill) -> softmax -> (dropout)
                                   -> @v   ==>  flash attention (mask and dropout inside the kernel)
   fused_dropout_add_layernorm     dropout(x) + residual -> layer_norm  ==> one norm kernel each way
@@ -40,8 +43,14 @@ import torch.nn.functional as TF
 
 from .program import Node, Ref, Const
 
-DEFAULT_PASSES = ('quant_linear_fuse_pass', 'multihead_matmul_fuse_pass_v2', 'fused_dropout_add_layernorm', 'skip_layernorm_fuse_pass',
-                  'fuse_gemm_epilogue_pass', 'layer_norm_fuse_pass', 'fc_fuse_pass', 'softmax_fuse_pass')
+# (CSE runs after the fusions: merging two equal subgraphs first would make them shared, and a
+# fusion claims only private chains)
+DEFAULT_PASSES = ('constant_folding_pass', 'conv2d_bn_fuse_pass',
+                  'conv2d_add_act_fuse_pass', 'embedding_eltwise_layernorm_fuse_pass',
+                  'quant_linear_fuse_pass', 'multihead_matmul_fuse_pass_v2', 'fused_dropout_add_layernorm', 'skip_layernorm_fuse_pass',
+                  'fuse_gemm_epilogue_pass', 'layer_norm_fuse_pass', 'fc_fuse_pass', 'softmax_fuse_pass',
+                  'common_subexpression_elimination_pass', 'dead_code_elimination_pass')
+# opt-in (change numerics): 'fused_weight_only_linear_pass' (int8 weight-only Linears of inference programs)
 
 # FLAGS_static_ir_fusion: 'auto' (default: GPU programs), '1' / 'always' (every device, used by the
 # CPU tests of the rewrites), '0' (off)
@@ -380,6 +389,8 @@ class _Graph:
         for vid, _, _ in getattr(prog, 'feeds', {}).values():
             ext.add(vid)
         for vid in getattr(prog, '_fetch', []) or []:
+            ext.add(vid)
+        for vid in getattr(prog, '_ir_fetch', None) or ():
             ext.add(vid)
         self.external = ext
         self.meta = {}
@@ -980,17 +991,41 @@ _PASSES = {
 }
 
 
+from . import ir_passes_ext as _ext  # noqa: E402
+_ext.register()
+
+
 def pass_names():
     return list(_PASSES)
 
 
-def apply_passes(prog, nodes=None, passes=None):
+def apply_passes(prog, nodes=None, passes=None, fetch=None):
     """The node list of ``prog`` with every match of ``passes`` (default DEFAULT_PASSES, in order)
-    rewritten; returns (nodes, {pass name: match count})."""
+    rewritten; returns (nodes, {pass name: match count}).  ``fetch``: value ids read after the run
+    (a loaded program knows its own); without them the whole-list passes (dead-code and common-
+    subexpression elimination), which must know what is read, are skipped."""
     nodes = list(prog.nodes if nodes is None else nodes)
     stats = {}
+    if fetch is None and getattr(prog, '_fetch', None):
+        fetch = tuple(prog._fetch)
+    prev_fetch = getattr(prog, '_ir_fetch', None)
+    prog._ir_fetch = fetch
+    try:
+        return _apply(prog, nodes, passes, fetch, stats)
+    finally:
+        prog._ir_fetch = prev_fetch
+
+
+def _apply(prog, nodes, passes, fetch, stats):
     for name in (passes if passes is not None else DEFAULT_PASSES):
         fn = _PASSES[name]
+        if getattr(fn, '_whole_list', False):  # DCE / CSE: whole-list rewrites
+            if fetch is None:
+                continue
+            nodes, cnt = fn(prog, nodes)
+            if cnt:
+                stats[name] = stats.get(name, 0) + cnt
+            continue
         g = _Graph(prog, nodes)
         remove, replace = set(), {}
         for i in range(len(nodes)):
@@ -1021,18 +1056,18 @@ def _enabled(prog, dev):
     return dev is not None and torch.device(dev).type == 'cuda'
 
 
-def ir_nodes(prog, dev):
+def ir_nodes(prog, dev, fetch=None):
     """The node list the Executor / Predictor runs: the fused rewrite of prog.nodes (cached per
-    program version and pass list), or prog.nodes itself when fusion is off."""
+    program version, pass list and fetch set), or prog.nodes itself when fusion is off."""
     if not _enabled(prog, dev) or not prog.nodes:
         return prog.nodes
     passes = getattr(prog, '_ir_passes', None)
     passes = tuple(DEFAULT_PASSES if passes is None else passes)
-    key = (len(prog.nodes), id(prog.nodes[-1]), passes)
+    key = (len(prog.nodes), id(prog.nodes[-1]), passes, fetch)
     c = getattr(prog, '_ir_cache', None)
     if c is not None and c[0] == key:
         return c[1]
-    nodes, stats = apply_passes(prog, passes=passes)
+    nodes, stats = apply_passes(prog, passes=passes, fetch=fetch)
     prog._ir_cache = (key, nodes)
     prog._ir_stats = stats
     return nodes

@@ -1,0 +1,465 @@
+"""General and convolution IR passes over static Programs, registered into static/ir_passes.py.
+
+Reference passes (same names):
+  paddle/fluid/pir/transforms/general/constant_folding_pass.cc      constant_folding_pass
+  paddle/fluid/pir/transforms/general/dead_code_elimination_pass.cc dead_code_elimination_pass
+  paddle/fluid/pir/transforms/general/common_subexpression_elimination_pass.cc
+                                                                    common_subexpression_elimination_pass
+  paddle/fluid/pir/transforms/gpu/conv2d_bn_fuse_pass.cc            conv2d_bn_fuse_pass
+  paddle/fluid/pir/transforms/gpu/conv2d_add_act_fuse_pass.cc       conv2d_add_act_fuse_pass
+  paddle/fluid/framework/ir/embedding_eltwise_layernorm_fuse_pass.cc embedding_eltwise_layernorm_fuse_pass
+  paddle/fluid/pir/transforms/gpu/fused_weight_only_linear_pass.cc  fused_weight_only_linear_pass
+
+Design notes (MI355X): a convolution node, folded or not, runs on the hand-written implicit-GEMM
+kernels (csrc/conv.hip, channels-last with NCHW served as views) whenever its operands fit, with
+the bias in the kernel's epilogue; the folded batch norm costs nothing at run time (the predictor
+of a ResNet runs no standalone batch-norm kernel), and the residual add + ReLU of a bottleneck
+run in place on the conv output.  Folding and constant folding read parameter VALUES at rewrite
+time, so they only apply to inference programs (no backward / minimize node); dead-code and
+common-subexpression elimination are pure graph rewrites, safe for training programs too.
+"""
+import torch
+import torch.nn.functional as TF
+
+from .program import Node, Ref, Const
+from . import ir_passes as IP
+
+_RANDOM = ('rand', 'randn', 'randint', 'randperm', 'normal', 'bernoulli', 'dropout', 'multinomial', 'rand_like',
+           'randn_like', 'randint_like', 'uniform', 'exponential', 'poisson', 'alpha_dropout', 'feature_alpha_dropout')
+
+
+def _name(n):
+    t = n.target
+    if type(t).__name__ == '_OpCall':
+        return 'pd.' + t.type
+    return getattr(t, '__name__', '') or ''
+
+
+def _pure(n):
+    """A side-effect-free, deterministic torch node (safe to drop when unused, to merge when equal)."""
+    if n.kind != 'torch':
+        return False
+    nm = _name(n)
+    if nm.endswith('_') and not nm.endswith('__'):  # in-place method (add_, copy_, ...)
+        return False
+    if nm in ('__setitem__', 'copy_', 'set_', 'resize_', 'record_stream', 'backward'):
+        return False
+    if any(r in nm for r in _RANDOM):
+        return False
+    if nm.startswith('pd.'):
+        return False  # imported operators may carry outputs bound by slot (kept)
+    if n.kwargs.get('inplace') or n.kwargs.get('out') is not None:
+        return False
+    return True
+
+
+def _training(prog):
+    return any(n.kind in ('minimize', 'backward', 'grad') for n in prog.nodes)
+
+
+def _refs(obj):
+    out = []
+    IP._refs_in(obj, out)
+    return out
+
+
+# ============================================================================ fused entry points
+def conv2d_static(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1):
+    """torch.conv2d semantics (NCHW) on the hand-written kernels when the operands fit
+    (nn.functional.conv._conv routing), else torch."""
+    from ..nn.functional.conv import _conv
+    from ..core.tensor import _wrap, _unwrap
+    return _unwrap(_conv(_wrap(x), _wrap(weight), None if bias is None else _wrap(bias), stride, padding, dilation,
+                         groups, 'NCHW', 2, TF.conv2d))
+
+
+def conv2d_add_act(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, residual=None, act=None):
+    """conv2d (+ bias in the kernel epilogue) (+ residual) (-> relu), the add and the activation in
+    place on the convolution's output."""
+    y = conv2d_static(x, weight, bias, stride, padding, dilation, groups)
+    if residual is not None:
+        y = y + residual if y.requires_grad or residual.requires_grad else y.add_(residual)
+    if act == 'relu':
+        y = torch.relu(y) if y.requires_grad else y.relu_()
+    return y
+
+
+def embedding_sum_layer_norm(ids_list, tables, ln_weight, ln_bias, eps=1e-5, padding_idx=None):
+    """sum_i embedding(ids_i, table_i) -> layer_norm over the last dim; the last add and the norm run
+    as one fused add + LayerNorm kernel (csrc/norm.hip) on the GPU."""
+    embs = [TF.embedding(i, t) for i, t in zip(ids_list, tables)]
+    acc = embs[0]
+    for e in embs[1:-1]:
+        acc = acc + e
+    if len(embs) > 1:
+        return IP.fused_dropout_add_layer_norm(embs[-1], acc, ln_weight, ln_bias, eps, 0.0)[0]
+    return IP.fused_layer_norm(acc, ln_weight, ln_bias, eps)
+
+
+def const_value(c):
+    """A constant-folded value (the node binds the precomputed tensor)."""
+    return c
+
+
+# ============================================================================ passes
+_CONV = None
+
+
+def _is_conv(n):
+    global _CONV
+    if _CONV is None:
+        _CONV = {torch.conv2d, TF.conv2d, conv2d_static}
+    return n is not None and n.kind == 'torch' and n.target in _CONV
+
+
+def _conv_args(n):
+    """(x, w, b, stride, padding, dilation, groups) of a recorded conv2d node."""
+    names = ('input', 'weight', 'bias', 'stride', 'padding', 'dilation', 'groups')
+    dflt = (None, None, None, 1, 0, 1, 1)
+    vals = []
+    for i, (nm, d) in enumerate(zip(names, dflt)):
+        vals.append(n.args[i] if len(n.args) > i else n.kwargs.get(nm, d))
+    if isinstance(vals[4], str):
+        return None  # 'same' / 'valid' string padding: left to torch
+    return vals
+
+
+def _bn_args(n):
+    """(x, mean, var, weight, bias, eps) of an inference batch norm node, else None."""
+    if n.kind != 'torch':
+        return None
+    if n.target in (TF.batch_norm, torch.batch_norm):
+        a, k = n.args, n.kwargs
+        if n.target is torch.batch_norm:  # (input, weight, bias, mean, var, training, momentum, eps, cudnn)
+            if len(a) < 8 or a[5]:
+                return None
+            return a[0], a[3], a[4], a[1], a[2], a[7]
+        x = a[0]
+        mean = a[1] if len(a) > 1 else k.get('running_mean')
+        var = a[2] if len(a) > 2 else k.get('running_var')
+        w = a[3] if len(a) > 3 else k.get('weight')
+        b = a[4] if len(a) > 4 else k.get('bias')
+        training = a[5] if len(a) > 5 else k.get('training', False)
+        eps = a[7] if len(a) > 7 else k.get('eps', 1e-5)
+        if training:
+            return None
+        return x, mean, var, w, b, eps
+    return None
+
+
+def _const_t(g, c):
+    if isinstance(c, Const):
+        owner = getattr(g.prog, '_const_owner', {}).get(c.cid)
+        return owner._t if owner is not None else g.prog.consts[c.cid]
+    return None
+
+
+def _new_const(g, t):
+    return Const(g.prog._const(t))
+
+
+def _conv_bn(g, i):
+    n = g.nodes[i]
+    ba = _bn_args(n)
+    if ba is None or _training(g.prog):
+        return None
+    x, mean, var, gw, gb, eps = ba
+    if not isinstance(x, Ref):
+        return None
+    j = g.producer(x.vid, i)
+    cn = g.node(j)
+    if not _is_conv(cn) or not g.private([j], users=[i]):
+        return None
+    ca = _conv_args(cn)
+    if ca is None or not isinstance(ca[1], Const) or (ca[2] is not None and not isinstance(ca[2], Const)):
+        return None
+    tw, tm, tv = _const_t(g, ca[1]), _const_t(g, mean), _const_t(g, var)
+    if tw is None or tm is None or tv is None or (gw is not None and _const_t(g, gw) is None) or \
+            (gb is not None and _const_t(g, gb) is None):
+        return None
+    with torch.no_grad():
+        dt = tw.dtype
+        inv = torch.rsqrt(tv.float() + float(eps))
+        scale = inv * (_const_t(g, gw).float() if gw is not None else 1.0)
+        w2 = (tw.float() * scale.reshape(-1, *([1] * (tw.dim() - 1)))).to(dt)
+        b0 = _const_t(g, ca[2]).float() if ca[2] is not None else torch.zeros_like(tm, dtype=torch.float32)
+        b2 = (b0 - tm.float()) * scale + (_const_t(g, gb).float() if gb is not None else 0.0)
+        b2 = b2.to(dt)
+    node = Node('torch', conv2d_static, [ca[0], _new_const(g, w2), _new_const(g, b2), ca[3], ca[4], ca[5], ca[6]], {},
+                n.outs, dict(n.meta or {}, fused='conv2d_bn_fuse_pass'))
+    return [j, i], {i: node}
+
+
+def _relu_node(n):
+    return n is not None and n.kind == 'torch' and n.target in (torch.relu, TF.relu, torch.Tensor.relu) and \
+        not n.kwargs.get('inplace') and (len(n.args) < 2 or not n.args[1])
+
+
+def _conv_add_act(g, i):
+    """conv (-> + residual) (-> relu) as one node; inference programs."""
+    n = g.nodes[i]
+    if not _is_conv(n) or _training(g.prog):
+        return None
+    ca = _conv_args(n)
+    if ca is None:
+        return None
+    body, cur, residual, act, tail = [i], IP._one_out(n), None, None, i
+    j = IP._sole_user(g, cur, body)
+    m = g.node(j)
+    if m is not None and IP._kind(m) == 'add' and len(m.args) == 2 and not m.kwargs:
+        a, b = m.args
+        other = b if isinstance(a, Ref) and a.vid == cur else (a if isinstance(b, Ref) and b.vid == cur else None)
+        if isinstance(other, Ref) and other.vid != cur:
+            residual, tail = other, j
+            body.append(j)
+            cur = IP._one_out(m)
+            j = IP._sole_user(g, cur, body)
+            m = g.node(j)
+    if _relu_node(m) and isinstance(m.args[0], Ref) and m.args[0].vid == cur:
+        act, tail = 'relu', j
+        body.append(j)
+    if len(body) == 1 or not g.private(body[:-1], users=body[-1:]):
+        return None
+    node = Node('torch', conv2d_add_act, list(ca), {'residual': residual, 'act': act}, IP._one_out(g.nodes[tail]),
+                dict(n.meta or {}, fused='conv2d_add_act_fuse_pass'))
+    return body, {tail: node}
+
+
+def _is_embedding(n):
+    from ..ops import matmul as _hm
+    return n is not None and n.kind == 'torch' and (n.target is TF.embedding or n.target is _hm._embedding_sub) and \
+        len(n.args) >= 2 and isinstance(n.args[0], Ref) and isinstance(n.args[1], Const) and \
+        not any(k in n.kwargs and n.kwargs[k] not in (None, False, 2.0) for k in ('max_norm', 'sparse',
+                                                                                    'scale_grad_by_freq'))
+
+
+def _emb_ln(g, i):
+    """(word + position + token-type) embeddings summed -> layer_norm as one node."""
+    n = g.nodes[i]
+    la = IP._ln_args(n) if IP._kind(n) == 'layer_norm' else None
+    if la is None or _training(g.prog):
+        return None
+    x, w, b, eps = la
+    if not isinstance(x, Ref):
+        return None
+    body, embs, stack = [i], [], [x]
+    while stack:
+        r = stack.pop()
+        j = g.producer(r.vid, i)
+        m = g.node(j)
+        if m is None:
+            return None
+        if _is_embedding(m):
+            embs.append(m)
+            body.append(j)
+        elif IP._kind(m) == 'add' and len(m.args) == 2 and not m.kwargs and all(isinstance(a, Ref) for a in m.args):
+            body.append(j)
+            stack.extend(m.args)
+        else:
+            return None
+    if len(embs) < 2 or not g.private([j for j in body if j != i], users=[i]):
+        return None
+    embs.sort(key=lambda m: g.nodes.index(m))
+    node = Node('torch', embedding_sum_layer_norm, [[m.args[0] for m in embs], [m.args[1] for m in embs], w, b],
+                {'eps': eps}, IP._ln_out(n), dict(n.meta or {}, fused='embedding_eltwise_layernorm_fuse_pass'))
+    return sorted(body), {i: node}
+
+
+_PD_IMPURE = ('random', 'dropout', 'print', 'save', 'load', 'c_', 'send', 'recv', 'fetch', 'feed', 'increment',
+              'while', 'conditional_block', 'seed', 'uniform', 'gaussian', 'share', 'memcpy', 'coalesce')
+
+
+def _foldable(n):
+    if n.kind != 'torch':
+        return False
+    nm = _name(n)
+    if nm.startswith('pd.'):  # imported operators: pure ones only
+        return not any(k in nm for k in _PD_IMPURE)
+    return _pure(n)
+
+
+def const_values(*cs):
+    """Constant-folded outputs of a multi-output node."""
+    return list(cs)
+
+
+def _const_fold(g, i):
+    """A node computed from constants only, evaluated once at rewrite time (imported programs carry
+    such chains — shape constants, weight reshapes / transposes / casts; a recorded program folds
+    them while it is built).  Parameters count as constants only in inference programs."""
+    n = g.nodes[i]
+    if not _foldable(n) or n.meta.get('factory') or _refs(n.args) or _refs(n.kwargs):
+        return None
+    train = _training(g.prog)
+    consts = []
+
+    def scan(o):
+        if isinstance(o, Const):
+            consts.append(o)
+        elif isinstance(o, (list, tuple)):
+            for x in o:
+                scan(x)
+        elif isinstance(o, dict):
+            for x in o.values():
+                scan(x)
+    scan(n.args)
+    scan(n.kwargs)
+    if not consts:
+        return None
+    owners = getattr(g.prog, '_const_owner', {})
+    if train and any(owners.get(c.cid) is not None for c in consts):
+        return None
+    from .executor import _resolve
+    try:
+        with torch.no_grad():
+            val = n.target(*_resolve(g.prog, n.args, {}, {}, None), **_resolve(g.prog, n.kwargs, {}, {}, None))
+    except Exception:  # noqa: BLE001 — leave anything unusual to run time
+        return None
+    meta = dict(n.meta or {}, fused='constant_folding_pass')
+    if isinstance(n.outs, int):
+        if not isinstance(val, torch.Tensor):
+            return None
+        return [i], {i: Node('torch', const_value, [_new_const(g, val.detach())], {}, n.outs, meta)}
+    if isinstance(n.outs, list) and isinstance(val, (list, tuple)) and len(val) == len(n.outs) and \
+            all(o is None or isinstance(o, int) for o in n.outs) and \
+            all(v is None or isinstance(v, torch.Tensor) for v in val):
+        args = [None if v is None else _new_const(g, v.detach()) for v in val]
+        return [i], {i: Node('torch', const_values, args, {}, n.outs, meta)}
+    return None
+
+
+def dead_code_elimination(prog, nodes):
+    """Drop pure nodes whose outputs nothing reads (to a fixpoint); returns (nodes, removed count)."""
+    removed = 0
+    while True:
+        g = IP._Graph(prog, nodes)
+        keep = []
+        drop = 0
+        for i, n in enumerate(nodes):
+            outs = g.outs[i]
+            if _pure(n) and outs and not any(v in g.external or g.uses.get(v) for v in outs):
+                drop += 1
+                continue
+            keep.append(n)
+        if not drop:
+            return nodes, removed
+        removed += drop
+        nodes = keep
+
+
+def _key(o):
+    if isinstance(o, Ref):
+        return ('r', o.vid)
+    if isinstance(o, Const):
+        return ('c', o.cid)
+    if isinstance(o, (list, tuple)):
+        return (type(o).__name__,) + tuple(_key(x) for x in o)
+    if isinstance(o, dict):
+        return ('d',) + tuple(sorted((k, _key(v)) for k, v in o.items()))
+    if isinstance(o, slice):
+        return ('s', _key(o.start), _key(o.stop), _key(o.step))
+    try:
+        hash(o)
+        return ('v', type(o).__name__, o)
+    except TypeError:
+        return ('id', id(o))
+
+
+def common_subexpression_elimination(prog, nodes):
+    """Merge pure nodes with the same target and operands: uses of the duplicate's outputs are
+    renamed to the first occurrence's; returns (nodes, merged count)."""
+    seen = {}
+    rename = {}
+    out = []
+    merged = 0
+
+    def rn(o):
+        if isinstance(o, Ref):
+            return Ref(rename.get(o.vid, o.vid))
+        if isinstance(o, tuple) and hasattr(o, '_fields'):
+            return type(o)(*[rn(x) for x in o])
+        if isinstance(o, (list, tuple)):
+            return type(o)(rn(x) for x in o)
+        if isinstance(o, dict):
+            return {k: rn(v) for k, v in o.items()}
+        if isinstance(o, slice):
+            return slice(rn(o.start), rn(o.stop), rn(o.step))
+        return o
+    ext = IP._Graph(prog, nodes).external
+    for n in nodes:
+        if rename:
+            n = Node(n.kind, n.target, rn(n.args), rn(n.kwargs), n.outs, n.meta)
+        if _pure(n) and not n.meta.get('factory') and n.outs is not None:
+            try:
+                k = (n.target, _key(n.args), _key(n.kwargs))
+                hash(k)
+            except TypeError:
+                k = None
+            if k is not None:
+                first = seen.get(k)
+                a, b = IP._outs_of(first.outs, []) if first is not None else [], IP._outs_of(n.outs, [])
+                if first is not None and len(a) == len(b) and not any(v in ext for v in b):
+                    for x, y in zip(a, b):
+                        rename[y] = x
+                    merged += 1
+                    continue
+                seen[k] = n
+        out.append(n)
+    return out, merged
+
+
+def _woq_linear(g, i):
+    """Inference Linear with a 16-bit constant weight -> weight-only int8 (per-channel scales,
+    quantised once at rewrite time) on the decode-shaped woq kernel (csrc/woq_gemm.hip)."""
+    n = g.nodes[i]
+    if _training(g.prog) or n.kind != 'torch' or n.kwargs:
+        return None
+    if n.target is TF.linear and len(n.args) >= 2:      # torch layout W [out, in]
+        x, w = n.args[0], n.args[1]
+        b = n.args[2] if len(n.args) > 2 else None
+        tw = _const_t(g, w)
+        tw = None if tw is None else tw.t()
+    elif n.target is torch.addmm and len(n.args) == 3:  # paddle Linear: addmm(b, x, W[in, out])
+        b, x, w = n.args
+        tw = _const_t(g, w)
+        if b is not None and not isinstance(b, Const):
+            return None
+    elif n.target in (torch.matmul, torch.mm) and len(n.args) == 2:
+        x, w = n.args
+        b, tw = None, _const_t(g, w)
+    else:
+        return None
+    if not isinstance(x, Ref) or tw is None or tw.dim() != 2 or tw.dtype not in (torch.bfloat16, torch.float16):
+        return None
+    if tw.shape[0] % 64 or tw.shape[1] % 8:
+        return None
+    from ..nn.quant import weight_quantize
+    from ..core.tensor import _wrap, _unwrap
+    q, s = weight_quantize(_wrap(tw.contiguous()), algo='weight_only_int8')  # [out, in] int8, [out] scale
+    node = Node('torch', woq_linear_static, [x, _new_const(g, _unwrap(q)), _new_const(g, _unwrap(s).to(tw.dtype)),
+                                             b], {}, n.outs, dict(n.meta or {}, fused='fused_weight_only_linear_pass'))
+    return [i], {i: node}
+
+
+def woq_linear_static(x, q, scale, bias=None):
+    from ..nn.quant import weight_only_linear
+    from ..core.tensor import _wrap, _unwrap
+    return _unwrap(weight_only_linear(_wrap(x), _wrap(q), None if bias is None else _wrap(bias), _wrap(scale), 'int8'))
+
+
+def _graph_pass(fn):
+    """Adapt a whole-list rewrite (nodes -> nodes, count) to apply_passes' per-pass protocol."""
+    fn._whole_list = True
+    return fn
+
+
+def register():
+    IP._PASSES.update({
+        'constant_folding_pass': _const_fold,
+        'conv2d_bn_fuse_pass': _conv_bn,
+        'conv2d_add_act_fuse_pass': _conv_add_act,
+        'embedding_eltwise_layernorm_fuse_pass': _emb_ln,
+        'fused_weight_only_linear_pass': _woq_linear,
+        'dead_code_elimination_pass': _graph_pass(dead_code_elimination),
+        'common_subexpression_elimination_pass': _graph_pass(common_subexpression_elimination),
+    })

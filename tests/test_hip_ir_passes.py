@@ -118,3 +118,45 @@ def test_programdesc_predictor_bf16_fused_vs_unfused(tmp_path):
     assert IP.fusion_stats(p._program).get('multihead_matmul_fuse_pass_v2') == 2
     assert ca.n == 2 and cn.n == 5, (ca.n, cn.n)
     np.testing.assert_allclose(out, ref, rtol=5e-2, atol=5e-2)
+
+
+def test_resnet50_predictor_folds_batch_norm_gpu():
+    """ResNet50 inference program (bf16, NCHW) on the Executor: conv2d_bn_fuse_pass folds every
+    batch norm into its convolution, conv2d_add_act_fuse_pass takes the residual adds and ReLUs, and
+    the convolutions run on the hand-written kernels — the profiler sees no batch-norm kernel and no
+    library convolution; the output matches the unfused program."""
+    from test_hip_conv_routing import _miopen_kernels
+    paddle.set_device('gpu:0')
+    paddle.seed(2)
+    paddle.enable_static()
+    try:
+        main, st = static.Program(), static.Program()
+        with static.program_guard(main, st):
+            x = static.data('x', [None, 3, 64, 64], 'bfloat16')
+            m = paddle.vision.models.resnet50(num_classes=100)
+            m.to(dtype='bfloat16')
+            m.eval()
+            y = m(x)
+    finally:
+        paddle.disable_static()
+    xv = paddle.to_tensor(np.random.RandomState(0).randn(8, 3, 64, 64).astype('float32')).astype('bfloat16')
+
+    def run(mode):
+        old = IP.set_mode(mode)
+        paddle.enable_static()
+        try:
+            return static.Executor(paddle.CUDAPlace(0)).run(main, feed={'x': xv}, fetch_list=[y],
+                                                            return_numpy=False)[0]._t.float()
+        finally:
+            paddle.disable_static()
+            IP.set_mode(old)
+    ref = run('0')
+    got = run('auto')
+    st = IP.fusion_stats(main)
+    assert st.get('conv2d_bn_fuse_pass') == 53, st
+    assert st.get('conv2d_add_act_fuse_pass', 0) >= 49, st
+    err = (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-3)
+    assert err < 5e-2, err
+    bad = [n for n in _miopen_kernels(lambda: run('auto')) if 'batchnorm' in n.lower() or 'conv' in n.lower()
+           or 'igemm' in n.lower() or 'xdlops' in n.lower()]
+    assert bad == [], bad
