@@ -57,6 +57,8 @@ def parse_args(argv=None):
     ap.add_argument('--host', default=None, help='this node\'s name in the elastic registry')
     ap.add_argument('--elastic_ttl', type=float, default=6.0)
     ap.add_argument('--elastic_timeout', type=float, default=600.0)
+    ap.add_argument('--auto_tuner_json', default=None,
+                    help='search hybrid-parallel configs (distributed/auto_tuner): one trial job per candidate')
     ap.add_argument('training_script')
     ap.add_argument('training_script_args', nargs=argparse.REMAINDER)
     return ap.parse_args(argv)
@@ -113,7 +115,8 @@ def _collective(a, attempt, restart_count=None):
                     'PADDLE_JOB_ID': a.job_id, 'PADDLE_LOCAL_DEVICE_IDS': devices[i],
                     'PADDLE_ELASTIC_RESTART_COUNT': str(attempt if restart_count is None else restart_count)})
         cmd = [sys.executable, '-u', a.training_script] + a.training_script_args
-        procs.append(_spawn(cmd, env, os.path.join(a.log_dir, f"workerlog.{i}"), i == 0))
+        procs.append(_spawn(cmd, env, os.path.join(a.log_dir, f"workerlog.{i}"),
+                            i == 0 and not getattr(a, 'log_all', False)))
     return procs
 
 
@@ -203,8 +206,68 @@ def _ps(a, attempt):
     return procs
 
 
+def auto_tune(a):
+    """--auto_tuner_json: run the training script once per candidate of the auto tuner
+    (reference launch/main.py auto-tuner mode).  Each trial gets the candidate as JSON in
+    PADDLE_AUTO_TUNER_CFG (``paddle.distributed.auto_tuner.current_trial()``) and, per the tuner
+    config's ``run_cmd`` ({key: [flag, template]}), as script arguments; the metric is parsed from
+    worker 0's log (``metric_cfg.name: value``), an out-of-memory failure is recorded as such.
+    The history CSV and the best config land in ``log_dir``."""
+    import json
+    import re
+    from .auto_tuner import AutoTuner
+    with open(a.auto_tuner_json) as f:
+        tcfg = json.load(f)
+    tcfg.setdefault('num_gpus', a.nproc_per_node or len((a.devices or '0').split(',')))
+    tcfg.setdefault('gpus_per_node', tcfg['num_gpus'])
+    tuner = AutoTuner(tcfg)
+    metric = tuner.recorder.metric
+    pat = re.compile(re.escape(metric) + r"\s*[:=]\s*([-+0-9.eE]+)")
+    base_args = list(a.training_script_args)
+
+    def trial(cfg):
+        d = os.path.join(a.log_dir, f"trial{cfg['job_id']}")
+        os.makedirs(d, exist_ok=True)
+        a2 = argparse.Namespace(**vars(a))
+        a2.log_dir = d
+        a2.log_all = True  # worker 0 to its log too: the metric is read from there
+        a2.nproc_per_node = cfg['num_gpus']
+        args = list(base_args)
+        for k, (flag, tmpl) in (tcfg.get('run_cmd') or {}).items():
+            if cfg.get(k) is not None:
+                args += [flag, str(tmpl).format(cfg[k])]
+        a2.training_script_args = args
+        os.environ['PADDLE_AUTO_TUNER_CFG'] = json.dumps(cfg)
+        try:
+            procs = _collective(a2, 0)
+            try:
+                rc = _wait(procs)
+            finally:
+                for _, log in procs:
+                    log.close()
+        finally:
+            os.environ.pop('PADDLE_AUTO_TUNER_CFG', None)
+        text = ''
+        for fn in sorted(os.listdir(d)):
+            with open(os.path.join(d, fn), errors='replace') as f:
+                text += f.read()
+        oom = 'out of memory' in text.lower() or 'outofmemory' in text.lower()
+        vals = pat.findall(text)
+        if rc != 0 or not vals:
+            return {metric: -1, 'oom': oom}
+        return {metric: float(vals[-1]), 'oom': False}
+    best = tuner.run(trial, history_csv_path=os.path.join(a.log_dir, 'history.csv'))
+    with open(os.path.join(a.log_dir, 'best_cfg.json'), 'w') as f:
+        json.dump(best, f)
+    print(f"[launch] auto tuner best config: {best}", file=sys.stderr, flush=True)
+    return 0 if best is not None else 1
+
+
 def launch(argv=None):
     a = parse_args(argv)
+    if a.auto_tuner_json:
+        os.makedirs(a.log_dir, exist_ok=True)
+        return auto_tune(a)
     if a.run_mode not in ('collective', 'ps'):
         raise SystemExit(f"unsupported run_mode {a.run_mode!r} (collective | ps)")
     os.makedirs(a.log_dir, exist_ok=True)
