@@ -674,8 +674,6 @@ class DistModel:
                 return 'sharding inside pipeline stages runs eagerly'
         if sharded and st.amp.get('enable'):
             return 'AMP over a sharded optimizer runs eagerly'
-        if st.recompute.get('enable'):
-            return 'recompute runs eagerly'
         for p in layer.parameters():
             m = _dist_meta(p)
             if m is not None and any(not isinstance(x, Replicate) for x in m[1]):

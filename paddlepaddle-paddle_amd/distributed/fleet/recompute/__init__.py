@@ -30,7 +30,45 @@ def _rebuild(spec, flat):
     return kind(_rebuild(s, flat) for s in v)
 
 
+def _static_checkpoint(function, args, kwargs):
+    """recompute() while a static Program records: the segment's ops go into a 'checkpoint' node
+    whose body the Executor runs under torch's non-reentrant checkpoint (static/executor.py
+    _exec_checkpoint) — the recorded program recomputes the segment in backward, as the eager
+    path does (reference: the static recompute pass, distributed/passes/auto_parallel_recompute.py)."""
+    from ....static import program as P
+    prog = P.default_main_program()
+    flat = []
+    _flatten(list(args) + list(kwargs.values()), flat)
+    ins = []
+    for t in flat:
+        tt = t._t if isinstance(t, Tensor) else t
+        if isinstance(tt, torch.Tensor) and tt.is_meta and id(tt) in prog._val:
+            ins.append(P.Ref(prog._val[id(tt)]))
+    saved, prog.nodes = prog.nodes, []
+    try:
+        res = function(*args, **kwargs)
+    finally:
+        body, prog.nodes = prog.nodes, saved
+    outs = []
+    _flatten(res, outs)
+    out_vids = []
+    for t in outs:
+        tt = t._t if isinstance(t, Tensor) else t
+        if isinstance(tt, torch.Tensor) and id(tt) in prog._val:
+            out_vids.append(prog._val[id(tt)])
+    params = [c for c in getattr(prog, '_const_owner', {}).values() if c is not None and not c.stop_gradient]
+    prog.nodes.append(P.Node('checkpoint', None, ins, {'body': body, 'params': bool(params)}, out_vids,
+                             {'stage': P._STAGE[0]}))
+    return res
+
+
 def recompute(function, *args, **kwargs):
+    from ....static.program import recording
+    if recording():
+        kwargs.pop('preserve_rng_state', None)
+        kwargs.pop('use_reentrant', None)
+        kwargs.pop('offload_indices', None)
+        return _static_checkpoint(function, args, kwargs)
     preserve = kwargs.pop('preserve_rng_state', True)
     kwargs.pop('use_reentrant', None)
     offload = kwargs.pop('offload_indices', None)  # noqa: F841

@@ -288,8 +288,69 @@ def _exec_nodes(prog, nodes, env, smap, dev):
                 _exec(prog, b_nodes, env, smap, dev)
                 cur = [_resolve(prog, r, env, smap, dev) for r in b_refs]
             _bind(env, n.outs, cur)
+        elif n.kind == 'checkpoint':
+            _exec_checkpoint(prog, n, env, smap, dev)
         else:
             raise RuntimeError(f"unknown node kind {n.kind}")
+
+
+def _checkpoint_outs(prog, n):
+    """Values of a checkpoint body that anything outside it reads (declared outputs, later
+    nodes, fetchable variables): computed once, from the finished program."""
+    outs = n.meta.get('live_outs')
+    if outs is not None:
+        return outs
+    body_ids = {id(b) for b in n.kwargs['body']}
+    produced = set()
+    from .ir_passes import _outs_of, _refs_in
+    for b in n.kwargs['body']:
+        produced.update(_outs_of(b.outs, []))
+    used = set()
+
+    def scan(nodes):
+        for m in nodes:
+            if id(m) in body_ids:
+                continue
+            r = []
+            _refs_in(m.args, r)
+            _refs_in(m.kwargs, r)
+            used.update(r)
+            for k in ('body', 'branches', 'cond'):
+                sub = m.kwargs.get(k) if isinstance(m.kwargs, dict) else None
+                if isinstance(sub, list):
+                    scan(sub)
+    scan(prog.nodes)
+    for var in prog.named_vars.values():
+        vid = prog._val.get(id(getattr(var, '_t', None)))
+        if vid is not None:
+            used.add(vid)
+    outs = [v for v in _outs_of(n.outs, []) if v in produced]
+    outs += sorted((produced & used) - set(outs))
+    n.meta['live_outs'] = outs
+    return outs
+
+
+def _exec_checkpoint(prog, n, env, smap, dev):
+    """A recompute segment (fleet.recompute under static recording): the body's activations are
+    not kept for backward — torch's non-reentrant checkpoint re-runs the body in backward."""
+    from torch.utils import checkpoint as _ckpt
+    ins = [_resolve(prog, r, env, smap, dev) for r in n.args]
+    outs = _checkpoint_outs(prog, n)
+    body = n.kwargs['body']
+
+    def run(*xs):
+        env2 = dict(env)
+        for r, x in zip(n.args, xs):
+            env2[r.vid] = x
+        _exec_nodes(prog, body, env2, smap, dev)
+        return tuple(env2[v] for v in outs)
+    if torch.is_grad_enabled() and any(isinstance(x, torch.Tensor) and x.requires_grad for x in ins) or \
+            torch.is_grad_enabled() and n.kwargs.get('params'):
+        res = _ckpt.checkpoint(run, *ins, use_reentrant=False, preserve_rng_state=True)
+    else:
+        res = run(*ins)
+    for v, t in zip(outs, res):
+        env[v] = t
 
 
 _LOD = {}  # id(torch tensor) -> (tensor, level-1 offsets) for LoD values of the running replay

@@ -145,6 +145,9 @@ def _enc_nodes(nodes):
     for n in nodes:
         if n.kind in ('minimize', 'backward', 'grad'):
             continue
+        if n.kind == 'checkpoint':  # a recompute segment: its ops, inline (recompute is a training matter)
+            out.extend(_enc_nodes(n.kwargs['body']))
+            continue
         if n.kind == 'py':
             raise ValueError("programs with py_func nodes cannot be serialised")
         d = {'k': n.kind, 'o': n.outs, 'a': _enc(list(n.args))}

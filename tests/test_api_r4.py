@@ -283,3 +283,38 @@ def test_dist_to_static_program_matches_eager(monkeypatch):
     np.testing.assert_allclose(a[1], b[1], rtol=1e-6, atol=1e-7)
     for p, q in zip(a[2], b[2]):
         np.testing.assert_allclose(p, q, rtol=1e-6, atol=1e-7)
+
+
+def test_dist_to_static_recompute_records_checkpoint_nodes(monkeypatch):
+    """Strategy.recompute under dist.to_static: the step is still a static Program, each
+    sub-layer a 'checkpoint' node whose body the Executor re-runs in backward (torch's
+    non-reentrant checkpoint); losses and weights equal the eager run without recompute."""
+    import numpy as np
+    import paddle.distributed as dist
+
+    def run(recompute, static):
+        monkeypatch.setenv('PADDLE_AMD_DIST_TO_STATIC', '1' if static else '0')
+        paddle.seed(4)
+        net = paddle.nn.Sequential(paddle.nn.Linear(8, 32), paddle.nn.GELU(), paddle.nn.Linear(32, 32),
+                                   paddle.nn.Tanh(), paddle.nn.Linear(32, 4))
+        opt = paddle.optimizer.SGD(0.1, parameters=net.parameters())
+        st = dist.Strategy()
+        st.recompute.enable = recompute
+        dm = dist.to_static(net, None, paddle.nn.CrossEntropyLoss(), opt, st)
+        assert dm.is_static == static
+        rng = np.random.RandomState(0)
+        losses = []
+        for i in range(3):
+            x = paddle.to_tensor(rng.randn(6, 8).astype('float32'))
+            y = paddle.to_tensor(rng.randint(0, 4, (6,)).astype('int64'))
+            losses.append(float(dm(x, y)))
+        progs = list(getattr(dm, '_progs', {}).values())
+        return losses, [p.numpy().copy() for p in net.parameters()], progs
+
+    la, wa, progs = run(True, True)
+    lb, wb, _ = run(False, False)
+    np.testing.assert_allclose(la, lb, rtol=1e-5, atol=1e-6)
+    for p, q in zip(wa, wb):
+        np.testing.assert_allclose(p, q, rtol=1e-5, atol=1e-6)
+    kinds = [n.kind for plan in progs for n in plan[0].nodes]
+    assert kinds.count('checkpoint') >= 5, kinds
