@@ -674,12 +674,10 @@ class DistModel:
                 return 'sharding inside pipeline stages runs eagerly'
         if sharded and st.amp.get('enable'):
             return 'AMP over a sharded optimizer runs eagerly'
-        for p in layer.parameters():
-            m = _dist_meta(p)
-            if m is not None and any(not isinstance(x, Replicate) for x in m[1]):
-                return 'tensor-parallel placements run on the SPMD-propagated eager path'
-            if m is not None and not st.pipeline.get('enable'):
-                return 'parameters with dist attributes run on the SPMD-propagated eager path'
+        tp = any(m is not None and any(not isinstance(x, Replicate) for x in m[1])
+                 for m in (_dist_meta(p) for p in layer.parameters()))
+        if tp and (st.pipeline.get('enable') or sharded):
+            return 'tensor-parallel placements with pipeline / sharding run on the SPMD-propagated eager path'
         return None
 
     @staticmethod
@@ -777,6 +775,15 @@ class DistModel:
         was_dynamic = _fw.in_dynamic_mode()
         if was_dynamic:
             _fw.enable_static()
+        from .. import auto_parallel_spmd as spmd
+        spmd_on = spmd._mode[0] is not None
+        if spmd_on:
+            # SPMD propagation above the recorder: it sees the global-view ops and hands the
+            # recorder the per-shard ops plus one node per reshard collective
+            spmd.disable()
+            _prog._stop_recording()
+            _prog._start_recording()
+            spmd.enable()
         pp = self._pp_plan if (mode == 'train' and self._pp_plan is not None) else None
         hooks = []
         if pp is not None:  # ops recorded inside a stage's sublayers run on that stage
@@ -840,8 +847,12 @@ class DistModel:
                 h.remove()
             if eng is not None:
                 eng.hooks_off = False
+            if spmd_on:
+                spmd.disable()  # modes leave LIFO: SPMD first, the recorder with static mode
             if was_dynamic:
                 _fw.disable_static()
+            if spmd_on:
+                spmd.enable()
         if self._exe is None:
             self._exe = _st.Executor()
         plan = (main, [f'dm_input_{i}' for i in range(len(vals))], fetch, self._dp_of(args))
@@ -869,7 +880,15 @@ class DistModel:
                 self._pp_stale = True
             else:
                 self._sync_stage_params()
-        res = self._exe.run(prog, feed=feed, fetch_list=[fetch], return_numpy=False)[0]
+        from .. import auto_parallel_spmd as spmd
+        spmd_on = spmd._mode[0] is not None
+        if spmd_on:
+            spmd.disable()  # the program already holds the per-shard ops and reshards
+        try:
+            res = self._exe.run(prog, feed=feed, fetch_list=[fetch], return_numpy=False)[0]
+        finally:
+            if spmd_on:
+                spmd.enable()
         if eng is not None and eng.level == 3 and self._mode != 'train':
             for u in eng.units:
                 u.free_params()

@@ -23,6 +23,7 @@ That yields tensor parallelism (column/row-parallel matmuls) and data parallelis
 weights, batch-sharded activations: the weight gradient is all-reduced) from placements alone.
 Ops without a rule run on the local pieces unchanged (the pre-existing local semantics).
 """
+import contextlib
 import math
 
 import torch
@@ -235,6 +236,39 @@ class _CopyTo(torch.autograd.Function):
         return g, None
 
 
+def _recording():
+    from ..static.program import recording
+    return recording()
+
+
+def _local_ctx():
+    """Local (per-shard) math of a handler: torch functions off — except while a static Program is
+    recorded, where the op must reach the recorder (the mode below this one)."""
+    return contextlib.nullcontext() if _recording() else torch._C.DisableTorchFunction()
+
+
+def _apply(fn, t, *extra):
+    """``fn.apply(t, *extra)`` — or, while a static Program is recorded (dist.to_static with
+    tensor-parallel placements), ONE program node that runs it at replay (the collective and its
+    conjugate backward), with the output's meta shape taken from a meta run of the local math."""
+    if not _recording():
+        return fn.apply(t, *extra)
+    from ..static.program import py_node, _paused
+    from ..core.tensor import _wrap, _unwrap
+    with _paused():
+        m = torch.empty(t.shape, dtype=t.dtype, device='meta')
+        if fn is _AllGather:
+            n, dim = extra[1], extra[3]
+            shape = list(t.shape)
+            shape[dim] *= n
+            out = torch.empty(shape, dtype=t.dtype, device='meta')
+        elif fn in (_Slice, _ReduceScatter):
+            out = torch.empty_like(m.chunk(extra[1], extra[3])[extra[2]], device='meta')
+        else:
+            out = m.clone()
+    return _unwrap(py_node(lambda x: _wrap(fn.apply(_unwrap(x), *extra)), [t], [out])[0])
+
+
 def _reshard_local(t, mesh, src, dst):
     """Differentiable transition of the local piece ``t`` from placements src to dst."""
     ap = _ap()
@@ -253,24 +287,24 @@ def _reshard_local(t, mesh, src, dst):
         if isinstance(s, ap.Partial):
             avg = s.reduce_type == ap.ReduceType.kRedAvg
             if isinstance(p, ap.Shard):
-                cur = _ReduceScatter.apply(cur, grp, n, idx, p.dim)
+                cur = _apply(_ReduceScatter, cur, grp, n, idx, p.dim)
                 if avg:
                     cur = cur / n
             else:
-                cur = _AllReduce.apply(cur, grp, n, avg)
+                cur = _apply(_AllReduce, cur, grp, n, avg)
                 if isinstance(p, ap.Partial):
                     cur = cur if idx == 0 else torch.zeros_like(cur)
         elif isinstance(s, ap.Shard):
             if isinstance(p, ap.Shard):
-                cur = _AllGather.apply(cur, grp, n, idx, s.dim)
-                cur = _Slice.apply(cur, grp, n, idx, p.dim)
+                cur = _apply(_AllGather, cur, grp, n, idx, s.dim)
+                cur = _apply(_Slice, cur, grp, n, idx, p.dim)
             else:
-                cur = _AllGather.apply(cur, grp, n, idx, s.dim)
+                cur = _apply(_AllGather, cur, grp, n, idx, s.dim)
                 if isinstance(p, ap.Partial) and idx != 0:
                     cur = cur * 0
         else:  # Replicate -> Shard / Partial
             if isinstance(p, ap.Shard):
-                cur = _Slice.apply(cur, grp, n, idx, p.dim)
+                cur = _apply(_Slice, cur, grp, n, idx, p.dim)
             elif isinstance(p, ap.Partial) and idx != 0:
                 cur = cur * 0
         src[d] = p
@@ -362,9 +396,9 @@ def _run(func, args, kwargs, tensor_pos, rule_out, mesh, out_gshape_fn, keep_par
             for d in active:
                 if d not in dm_req and mesh.shape[d] > 1:
                     grp, _ = mesh.dim_group(d)
-                    local = _CopyTo.apply(local, grp)
+                    local = _apply(_CopyTo, local, grp)
         args[pos] = local
-    with torch._C.DisableTorchFunction():
+    with _local_ctx():
         out = func(*args, **kwargs)
     pl = placements_of(out_dm, {d: ap.ReduceType.kRedSum for d in out_partial}, mesh.ndim)
     if isinstance(out, torch.Tensor):
@@ -443,6 +477,21 @@ def _h_linear(func, name, args, kwargs):
     kw = {k: v for k, v in kwargs.items() if k != 'bias'}
     return _run(func, args2, kw, list(range(len(tensors))), (reqs, out, partial), mesh,
                 lambda o: _gshape(o, out, mesh))
+
+
+def _h_addmm(func, name, args, kwargs):
+    """addmm(bias, x, W[in, out]) — the 2-D form paddle's F.linear lowers to: the matmul rule, the
+    partial sum resolved, then the (possibly sharded) bias added by the elementwise rule."""
+    inp, x, w = args[0], args[1], args[2]
+    beta, alpha = kwargs.get('beta', 1), kwargs.get('alpha', 1)
+    y = _h_matmul(torch.mm, 'mm', (x, w), {})
+    mesh = _mesh_of([y, inp, x, w])
+    y = _resolve_partial(y, mesh)
+    if alpha != 1:
+        y = _h_elementwise(torch.mul, 'mul', (y, alpha), {})
+    if beta != 1:
+        inp = _h_elementwise(torch.mul, 'mul', (inp, beta), {})
+    return _h_elementwise(torch.add, 'add', (y, inp), {})
 
 
 def _axis_arg(args, kwargs, name='dim'):
@@ -563,7 +612,7 @@ def _h_reshape(func, name, args, kwargs):
         out = [-1] * len(shp)
     # local target shape: divide sharded output dims
     local_shape = [v // (mesh.shape[out[i]] if out[i] >= 0 else 1) for i, v in enumerate(shp)]
-    with torch._C.DisableTorchFunction():
+    with _local_ctx():
         y = func(x, local_shape) if name != 'view' else x.view(local_shape)
     ap = _ap()
     return tag(y, mesh, placements_of(out, {d: ap.ReduceType.kRedSum for d in part}, mesh.ndim), shp)
@@ -612,6 +661,8 @@ def _dispatch(name):
         return _h_matmul
     if name == 'linear':
         return _h_linear
+    if name == 'addmm':
+        return _h_addmm
     if name in _REDUCE:
         return _h_reduce
     if name in _SOFTMAX:

@@ -359,6 +359,13 @@ def test_dist_to_static_sharded_and_pipelined_programs(mode):
     assert out.count(f'dist static {mode} OK') == 2, out[-3000:]
 
 
+def test_dist_to_static_tensor_parallel_program():
+    """dist.to_static with column / row-parallel placements records the SPMD-propagated step
+    (per-shard ops + reshard collectives as program nodes) and equals single-process training."""
+    out = run_workers('worker_dist_static_tp.py')
+    assert out.count('dist static tp OK') == 2, out[-3000:]
+
+
 @pytest.mark.parametrize("mode,nproc", [('sep', 2), ('sepmp', 4), ('sepdp', 4), ('sepsh', 4)])
 def test_segment_parallel_matches_single_process(mode, nproc):
     """sep alone and x mp / dp / sharding: gradients summed over sep, averaged over dp
