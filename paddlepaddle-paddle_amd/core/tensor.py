@@ -84,7 +84,7 @@ class Tensor:
 
     @property
     def dtype(self):
-        return self._t.dtype
+        return _dt.from_torch(self._t.dtype)
 
     @property
     def place(self):

@@ -452,7 +452,7 @@ def fp8_gemm(x, y, transpose_x=False, transpose_y=False, bias=None, scale=1.0, o
         a = a.transpose(-1, -2)
     if transpose_y:
         b = b.transpose(-1, -2)
-    od = {'bfloat16': torch.bfloat16, 'float16': torch.float16, 'float32': torch.float32}.get(str(output_dtype),
+    od = {'bfloat16': torch.bfloat16, 'float16': torch.float16, 'float32': torch.float32}.get(str(output_dtype).replace('paddle.', ''),
                                                                                                torch.bfloat16)
     if a.dtype not in (torch.float8_e4m3fn, torch.float8_e5m2):
         a, sa = fp8_quantize(a)
