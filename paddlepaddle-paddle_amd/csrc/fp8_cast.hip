@@ -124,17 +124,14 @@ __global__ __launch_bounds__(256) void cast_transpose_kernel(const bf16_t* __res
 constexpr int P2 = T + 4;
 
 template <int FMT>
-__global__ __launch_bounds__(256) void cast_transpose_full_kernel(const bf16_t* __restrict__ x, int R, int C,
-                                                                  long long ldx, uint8_t* __restrict__ q,
-                                                                  uint8_t* __restrict__ qt, float* __restrict__ hist,
-                                                                  int L, int cur, float* __restrict__ scale_inv,
-                                                                  float margin_mul) {
-  __shared__ __attribute__((aligned(16))) uint8_t tile[T * P2];
-  __shared__ float red[4];
+__device__ __forceinline__ void cast_tile_full(uint8_t* tile, float* red, const bf16_t* __restrict__ x, int R, int C,
+                                               long long ldx, uint8_t* __restrict__ q, uint8_t* __restrict__ qt,
+                                               float* __restrict__ hist, int L, int cur,
+                                               float* __restrict__ scale_inv, float margin_mul, int bx, int by) {
   const float fmax = fmax_of<FMT>();
   const float s = scale_from_hist(hist, L, cur, fmax, margin_mul);
   const int tid = threadIdx.x;
-  const int r0 = blockIdx.y * T, c0 = blockIdx.x * T;
+  const int r0 = by * T, c0 = bx * T;
   float am = 0.f;
   float v[8][8];
 #pragma unroll
@@ -188,11 +185,55 @@ __global__ __launch_bounds__(256) void cast_transpose_full_kernel(const bf16_t* 
   if (tid == 0) {
     const float b = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
     atomic_max_pos(hist + cur, b);
-    if (blockIdx.x == 0 && blockIdx.y == 0) {
+    if (bx == 0 && by == 0) {
       hist[(cur + 1) % L] = 0.f;
       scale_inv[0] = 1.f / s;
     }
   }
+}
+
+template <int FMT>
+__global__ __launch_bounds__(256) void cast_transpose_full_kernel(const bf16_t* __restrict__ x, int R, int C,
+                                                                  long long ldx, uint8_t* __restrict__ q,
+                                                                  uint8_t* __restrict__ qt, float* __restrict__ hist,
+                                                                  int L, int cur, float* __restrict__ scale_inv,
+                                                                  float margin_mul) {
+  __shared__ __attribute__((aligned(16))) uint8_t tile[T * P2];
+  __shared__ float red[4];
+  cast_tile_full<FMT>(tile, red, x, R, C, ldx, q, qt, hist, L, cur, scale_inv, margin_mul, blockIdx.x, blockIdx.y);
+}
+
+// Many casts in ONE launch (the weights of an fp8 static program, cast once at the start of each
+// step instead of one small launch per Linear): the 1-D grid is the concatenation of every job's
+// 128x128 tiles; a block finds its job by binary search over the jobs' first-tile indices.  Every
+// job is a full-tile one (R, C multiples of 128) of the same fp8 format.
+struct CastJob {
+  const bf16_t* x;
+  uint8_t* q;
+  uint8_t* qt;
+  float* hist;
+  float* scale_inv;
+  long long ldx;
+  int R, C, L, cur, tiles_x, tile0;
+  float margin_mul;
+  int pad;
+};
+static_assert(sizeof(CastJob) == 80, "CastJob layout is packed by ops/fp8.py");
+
+template <int FMT>
+__global__ __launch_bounds__(256) void cast_transpose_multi_kernel(const CastJob* __restrict__ jobs, int njobs) {
+  __shared__ __attribute__((aligned(16))) uint8_t tile[T * P2];
+  __shared__ float red[4];
+  const int bid = blockIdx.x;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].tile0 <= bid) lo = mid; else hi = mid - 1;
+  }
+  const CastJob& j = jobs[lo];
+  const int t = bid - j.tile0;
+  cast_tile_full<FMT>(tile, red, j.x, j.R, j.C, j.ldx, j.q, j.qt, j.hist, j.L, j.cur, j.scale_inv, j.margin_mul,
+                      t % j.tiles_x, t / j.tiles_x);
 }
 
 // amax of a bf16 [R, C] tensor folded into *out (first use of a tensor: seeds the history)
@@ -249,6 +290,17 @@ PA_API int pa_fp8_cast_transpose(const void* x, int R, int C, long long ldx, voi
   else
     f8::cast_transpose_kernel<1><<<grid, 256, 0, st>>>((const bf16_t*)x, R, C, ldx, (uint8_t*)q, (uint8_t*)qt,
                                                          (float*)hist, L, cur, (float*)scale_inv, margin_mul);
+  return (int)hipGetLastError();
+}
+
+// jobs: device array of f8::CastJob (80 B each, tile0 ascending, full 128x128 tiles), total_tiles
+// = the grid; fmt 0 = e4m3fn, 1 = e5m2 for every job.
+PA_API int pa_fp8_cast_transpose_multi(const void* jobs, int njobs, int total_tiles, int fmt, hipStream_t st) {
+  if (!jobs || njobs <= 0 || total_tiles <= 0 || fmt < 0 || fmt > 1) return (int)hipErrorInvalidValue;
+  if (fmt == 0)
+    f8::cast_transpose_multi_kernel<0><<<total_tiles, 256, 0, st>>>((const f8::CastJob*)jobs, njobs);
+  else
+    f8::cast_transpose_multi_kernel<1><<<total_tiles, 256, 0, st>>>((const f8::CastJob*)jobs, njobs);
   return (int)hipGetLastError();
 }
 

@@ -20,6 +20,8 @@ On CPU (or for shapes outside the kernel contract) the same math runs in torch (
 the same delayed scale, dequantised matmul), so the scaling logic is testable without a GPU.
 """
 import contextlib
+import struct
+import weakref
 
 import torch
 
@@ -87,6 +89,14 @@ class FP8Meta:
         self.cur = (cur + 1) % L
         self.calls += 1
         return sc, slot, sinv
+
+    def cast_weight(self, w, want_q=True, want_qt=True):
+        """cast() of a weight, served from this step's batched pre-cast (begin_static_step) when
+        there is one for this storage."""
+        pre = self.__dict__.get('_pre')
+        if pre is not None and pre[0] == _STEP[0] and pre[1] == w.data_ptr():
+            return pre[2], pre[3], pre[4]
+        return self.cast(w, want_q, want_qt)
 
     def cast(self, x2d, want_q=True, want_qt=True):
         """x2d: [R, C] -> (q [R,C] | None, q^T [C,R] | None, dequant scale (1-elem fp32 tensor))."""
@@ -194,7 +204,8 @@ class _FP8Linear(torch.autograd.Function):
         x2 = x.reshape(-1, K)
         need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         xq, xqt, sx = st.x.cast(x2, want_q=True, want_qt=need_dw)
-        wq, wqt, sw = st.w.cast(w, want_q=need_dx, want_qt=True)  # wqt: [N, K]
+        st.wref = weakref.ref(w)
+        wq, wqt, sw = st.w.cast_weight(w, want_q=need_dx, want_qt=True)  # wqt: [N, K]
         y = fp8_mm(xq, wqt, sx, sw, bias=b)
         ctx.save_for_backward(xqt, wq, sx, sw)
         ctx.st, ctx.xshape, ctx.has_b, ctx.wdt, ctx.xdt = st, x.shape, b is not None, w.dtype, x.dtype
@@ -230,6 +241,48 @@ def _state_for(weight_holder, w, recipe):
 
 
 _STATIC_STATES = {}
+_STEP = [0]  # generation of the batched weight pre-cast (begin_static_step)
+
+
+def begin_static_step():
+    """Cast every weight of the static fp8 states seen so far (their q and q^T, delayed scaling
+    exactly as the per-Linear cast) in ONE kernel launch per fp8 format at the start of a replay,
+    instead of one small cast launch per Linear inside the step (csrc/fp8_cast.hip
+    pa_fp8_cast_transpose_multi).  Weights outside the full-tile contract keep the per-call cast."""
+    _STEP[0] += 1
+    jobs = {}
+    for st in list(_STATIC_STATES.values()):
+        ref = getattr(st, 'wref', None)
+        w = ref() if ref is not None else None
+        m = st.w
+        if (w is None or m.calls == 0 or not w.is_cuda or w.dtype != torch.bfloat16 or w.dim() != 2
+                or not w.is_contiguous() or w.shape[0] % 128 or w.shape[1] % 128 or w.data_ptr() % 16):
+            continue
+        jobs.setdefault((w.device, _FMT[m.dtype]), []).append((m, w))
+    if not jobs or (N.lib is None and N._load() is None):
+        return
+    for (dev, fmt), lst in jobs.items():
+        blob, tile0 = bytearray(), 0
+        keep = []
+        for m, w in lst:
+            R, C = w.shape
+            q = torch.empty(R, C, dtype=m.dtype, device=dev)
+            qt = torch.empty(C, R, dtype=m.dtype, device=dev)
+            sinv = torch.empty(1, dtype=torch.float32, device=dev)
+            blob += struct.pack('<5Qq6ifi', w.data_ptr(), q.data_ptr(), qt.data_ptr(), m.hist.data_ptr(),
+                                sinv.data_ptr(), C, R, C, m.L, m.cur, C // 128, tile0, float(m.margin_mul), 0)
+            tile0 += (R // 128) * (C // 128)
+            m._pre = (_STEP[0], w.data_ptr(), q, qt, sinv)
+            m.cur = (m.cur + 1) % m.L
+            m.calls += 1
+            keep.append(w)
+        table = torch.frombuffer(blob, dtype=torch.uint8).pin_memory().to(dev, non_blocking=True)
+        N.check(N.lib.pa_fp8_cast_transpose_multi(N.ptr(table), len(lst), tile0, fmt, N.stream()),
+                'fp8_cast_transpose_multi')
+        _KEEP[0] = (table, keep)  # alive until the launch has read them (the next step replaces it)
+
+
+_KEEP = [None]
 
 
 def fp8_linear(x, w, b=None, recipe=None, holder=None, key=None):
@@ -288,7 +341,8 @@ class _FP8FFN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2, w1, b1, w2, b2, st1, st2, approximate):
         xq, xqt, sx = st1.x.cast(x2)
-        w1q, w1qt, sw1 = st1.w.cast(w1)
+        st1.wref, st2.wref = weakref.ref(w1), weakref.ref(w2)
+        w1q, w1qt, sw1 = st1.w.cast_weight(w1)
         h = torch.empty(x2.shape[0], w1.shape[1], dtype=torch.bfloat16, device=x2.device)
         bb1 = b1.to(torch.bfloat16).contiguous()
         fq = None if approximate else _fp8_epi_q(xq, w1qt, sx, sw1, 10, h, st2.x, bias=bb1)
@@ -297,7 +351,7 @@ class _FP8FFN(torch.autograd.Function):
         else:
             g = _fp8_epi(xq, w1qt, sx, sw1, 2 if approximate else 9, h, bias=bb1)
             gq, gqt, sg = st2.x.cast(g)
-        w2q, w2qt, sw2 = st2.w.cast(w2)
+        w2q, w2qt, sw2 = st2.w.cast_weight(w2)
         y = fp8_mm(gq, w2qt, sg, sw2, bias=b2)
         ctx.save_for_backward(xqt, w1q, gqt, w2q, h, sx, sw1, sg, sw2)
         ctx.st = (st1, st2)

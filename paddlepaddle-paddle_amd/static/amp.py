@@ -293,6 +293,8 @@ def autocast_context(program, dev):
     from ..ops import fp8 as _fp8
     prev = _fp8._STATIC_RECIPE['recipe']
     _fp8._STATIC_RECIPE['recipe'] = cfg.get('fp8')
+    if cfg.get('fp8') is not None and dev.type == 'cuda':
+        _fp8.begin_static_step()  # this replay's weight casts: one launch
     try:
         with torch.autocast(device_type='cuda' if dev.type == 'cuda' else 'cpu', dtype=cfg['dtype']):
             yield _fp8.STATIC_SUBS if cfg.get('fp8') is not None else None

@@ -199,3 +199,44 @@ def test_ernie_static_fp8_gpu(static_mode):
         assert np.isfinite(losses).all() and losses[-1] < losses[0] * 0.6, losses
     finally:
         paddle.set_device('cpu')
+
+
+@pytest.mark.gpu
+def test_hip_batched_weight_cast_equals_per_linear_casts():
+    """begin_static_step: every static fp8 weight cast in one launch == one cast per weight
+    (q, q^T, dequant scale and the amax history, byte for byte), and the Linear consumes it."""
+    from paddle.ops import _native as N
+    assert N._load() is not None, N.load_error
+    torch.manual_seed(5)
+    shapes = [(768, 768), (768, 3072), (3072, 768), (256, 128)]
+    ws = [(torch.randn(*s, device='cuda') * 0.05).to(torch.bfloat16).requires_grad_() for s in shapes]
+    saved = dict(F8._STATIC_STATES)
+    F8._STATIC_STATES.clear()
+    try:
+        rec = F8.DelayedScaling()
+        sts = []
+        for i, w in enumerate(ws):
+            st = F8._static_state(w, rec, key=('t', i))
+            st.wref = __import__('weakref').ref(w)
+            st.w.cast(w)  # seeds the history (step 0 of a run)
+            sts.append(st)
+        refs = []
+        for st, w in zip(sts, ws):  # the per-Linear cast on a copy of each meta
+            m = F8.FP8Meta(st.w.dtype, st.w.L, 0, 'cuda')
+            m.hist.copy_(st.w.hist)
+            m.cur, m.calls = st.w.cur, st.w.calls
+            q, qt, s = m.cast(w)
+            refs.append((q.view(torch.uint8), qt.view(torch.uint8), s, m.hist, m.cur))
+        F8.begin_static_step()
+        torch.cuda.synchronize()
+        for st, w, (q, qt, s, h, cur) in zip(sts, ws, refs):
+            bq, bqt, bs = st.w.cast_weight(w)
+            assert torch.equal(bq.view(torch.uint8), q) and torch.equal(bqt.view(torch.uint8), qt)
+            assert torch.equal(bs, s) and torch.equal(st.w.hist, h) and st.w.cur == cur
+        x = torch.randn(64, 768, device='cuda', dtype=torch.bfloat16)
+        y = F8._FP8Linear.apply(x, ws[0], None, sts[0])
+        yr = x.float() @ ws[0].detach().float()
+        assert float((y.float() - yr).norm() / yr.norm()) < 0.06
+    finally:
+        F8._STATIC_STATES.clear()
+        F8._STATIC_STATES.update(saved)
