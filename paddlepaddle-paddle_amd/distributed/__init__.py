@@ -48,7 +48,7 @@ _LAZY = {'fleet': '.fleet', 'launch': '.launch', 'auto_parallel': '.auto_paralle
 _AUTO = ('ProcessMesh', 'DistAttr', 'shard_tensor', 'dtensor_from_fn', 'reshard', 'shard_layer', 'shard_dataloader',
          'ReduceType', 'Placement', 'Shard', 'Replicate', 'Partial', 'shard_optimizer', 'shard_scaler',
          'ShardingStage1', 'ShardingStage2', 'ShardingStage3', 'to_static', 'Strategy', 'DistModel',
-         'unshard_dtensor')
+         'unshard_dtensor', 'set_mesh', 'get_mesh')
 
 
 def __getattr__(name):

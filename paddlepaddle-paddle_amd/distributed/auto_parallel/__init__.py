@@ -4,7 +4,7 @@ dataloader wrappers, dist.to_static's DistModel and the static Engine (static/en
 from .api import (  # noqa: F401
     Placement, Shard, Replicate, Partial, ReduceType, ProcessMesh, DistAttr, shard_tensor, dtensor_from_fn,
     reshard, unshard_dtensor, shard_layer, ShardingStage1, ShardingStage2, ShardingStage3, shard_optimizer,
-    shard_scaler, shard_dataloader, Strategy, DistModel, to_static, is_dist_tensor,
+    shard_scaler, shard_dataloader, Strategy, DistModel, to_static, is_dist_tensor, set_mesh, get_mesh,
     _dist_meta, _attach, _local_slice, _ensure_mesh_groups, _subgroup, _ShardOptimizer,
 )
 from .static.engine import Engine  # noqa: F401

@@ -607,6 +607,21 @@ class Strategy:
         self.amp = cfg('amp', enable=False, dtype='bfloat16', level='O2')
         self.recompute = cfg('recompute', enable=False)
         self.fused_passes = cfg('fused_passes', enable=False, fused_passes_list=[])
+        # 'semi': the user's placements; 'full': the rule-based planner places the parameters
+        # (auto_parallel/static/planner.py) on get_mesh() at the first step
+        self.auto_mode = config.get('auto_mode', 'semi')
+
+
+_GLOBAL_MESH = [None]
+
+
+def set_mesh(mesh):
+    """The default process mesh of auto-parallel APIs (the fully automatic planner uses it)."""
+    _GLOBAL_MESH[0] = mesh
+
+
+def get_mesh():
+    return _GLOBAL_MESH[0]
 
 
 class DistModel:
@@ -659,6 +674,29 @@ class DistModel:
         self._static_reason = self._static_blocker(layer, optimizer, st)
         self._progs = {}
         self._exe = None
+        self._auto_pending = (getattr(st, 'auto_mode', 'semi') == 'full' and dist.is_initialized()
+                              and dist.get_world_size() > 1
+                              and all(_dist_meta(p) is None for p in layer.parameters()))
+        self.plan = None
+
+    def _auto_plan(self, args):
+        """auto_mode 'full': place the parameters by the rule-based planner (reference
+        static/planner_v2.py + tuner/rule_based_tuner.py), then build the step as usual."""
+        from .static.planner import RuleBasedPlanner
+        mesh = get_mesh() or ProcessMesh(list(range(dist.get_world_size())), dim_names=['mp'])
+        inputs = args if self._mode == 'predict' else args[:-1]
+        planner = RuleBasedPlanner(mesh)
+        was = self._layer.training
+        self._layer.eval()  # plan on the inference graph (no dropout nodes)
+        try:
+            self.plan = planner.plan(self._layer, *inputs)
+        finally:
+            if was:
+                self._layer.train()
+        planner.apply(self._layer, self.plan, self._opt)
+        self._auto_pending = False
+        self._static_reason = self._static_blocker(self._layer, self._opt, self._strategy)
+        self._progs = {}
 
     @staticmethod
     def _static_blocker(layer, optimizer, st):
@@ -912,6 +950,8 @@ class DistModel:
         self._layer.eval()
 
     def __call__(self, *args):
+        if self._auto_pending:
+            self._auto_plan(args)
         if self._static_reason is None:
             return self._static_call(args)
         if self._mode == 'predict':

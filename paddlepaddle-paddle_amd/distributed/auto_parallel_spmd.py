@@ -494,6 +494,41 @@ def _h_addmm(func, name, args, kwargs):
     return _h_elementwise(torch.add, 'add', (y, inp), {})
 
 
+def _h_sdpa(func, name, args, kwargs):
+    """scaled_dot_product_attention(q, k, v [B, H, S, D], attn_mask, ...): batch and head axes may
+    stay sharded (q's mapping, k / v / a per-batch or per-head mask follow it); sequence and head
+    dims are gathered.  Heads are independent, so every rank attends its own heads exactly."""
+    kwargs = dict(kwargs)
+    args = list(args)
+    if len(args) < 4 and isinstance(kwargs.get('attn_mask'), torch.Tensor):
+        args += [None] * (3 - len(args)) + [kwargs.pop('attn_mask')]
+    q, k, v = args[0], args[1], args[2]
+    mask = args[3] if len(args) > 3 and isinstance(args[3], torch.Tensor) else None
+    mesh = _mesh_of([t for t in (q, k, v, mask) if t is not None])
+    q, k, v = (_resolve_partial(t, mesh) for t in (q, k, v))
+    args[0], args[1], args[2] = q, k, v
+    gq, dq, _ = _spec(q, mesh)
+    gk, _, _ = _spec(k, mesh)
+    nd = len(gq)
+    lead = list(dq[:nd - 2]) if nd == 4 and gk[:nd - 2] == gq[:nd - 2] else [-1] * (nd - 2)
+    req = [lead + [-1, -1]] * 3
+    pos = [0, 1, 2]
+    if mask is not None:
+        mask = _resolve_partial(mask, mesh)
+        args[3] = mask
+        gm = _spec(mask, mesh)[0]
+        off = nd - len(gm)
+        mreq = []
+        for i, sz in enumerate(gm):
+            j = i + off
+            mreq.append(lead[j] if 0 <= j < nd - 2 and sz == gq[j] else -1)
+        req.append(mreq)
+        pos.append(3)
+    gv = _spec(v, mesh)[0]
+    out = lead + [-1, -1]
+    return _run(func, tuple(args), kwargs, pos, (req, out, set()), mesh, lambda o: list(gq[:-1]) + [gv[-1]])
+
+
 def _axis_arg(args, kwargs, name='dim'):
     if len(args) > 1 and not isinstance(args[1], torch.dtype):
         return args[1]
@@ -663,6 +698,8 @@ def _dispatch(name):
         return _h_linear
     if name == 'addmm':
         return _h_addmm
+    if name == 'scaled_dot_product_attention':
+        return _h_sdpa
     if name in _REDUCE:
         return _h_reduce
     if name in _SOFTMAX:

@@ -409,8 +409,27 @@ def ffn_gelu(x2, w1, b1, w2, b2, approximate=False):
     return _FFNGeluFn.apply(x2, w1, b1, w2, b2, bool(approximate))
 
 
+_SPMD = [None]
+
+
+def _spmd_on():
+    """The auto-parallel SPMD mode is installed: its rules see torch ops with global-view shape
+    arguments, so the Linear is issued as matmul + bias (no local-shape reshape) and stays off the
+    custom-kernel Function (which the mode cannot see)."""
+    m = _SPMD[0]
+    if m is None:
+        from ..distributed import auto_parallel_spmd as m
+        _SPMD[0] = m
+    return m._mode[0] is not None
+
+
 def linear(x, w, bias=None):
     """paddle F.linear (W stored [in, out]) outside the training engines."""
+    if _spmd_on():
+        if x.dim() == 2:
+            return torch.addmm(bias, x, w) if bias is not None else torch.mm(x, w)
+        y = torch.matmul(x, w)
+        return y + bias if bias is not None else y
     if w.dim() != 2 or x.dim() < 1 or not _use(x, w) or (bias is not None and not _use(x, bias)):
         if x.dim() == 2:
             return torch.addmm(bias, x, w) if bias is not None else torch.mm(x, w)

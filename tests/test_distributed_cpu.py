@@ -366,6 +366,13 @@ def test_dist_to_static_tensor_parallel_program():
     assert out.count('dist static tp OK') == 2, out[-3000:]
 
 
+def test_dist_to_static_full_auto_planner():
+    """strategy.auto_mode = 'full': the rule-based planner finds the attention and FFN blocks of a
+    transformer layer and places them column / row parallel; the static step equals one process."""
+    out = run_workers('worker_dist_auto_plan.py')
+    assert out.count('dist auto plan OK') == 2, out[-3000:]
+
+
 @pytest.mark.parametrize("mode,nproc", [('sep', 2), ('sepmp', 4), ('sepdp', 4), ('sepsh', 4)])
 def test_segment_parallel_matches_single_process(mode, nproc):
     """sep alone and x mp / dp / sharding: gradients summed over sep, averaged over dp
