@@ -49,7 +49,7 @@ DEFAULT_PASSES = ('constant_folding_pass', 'conv2d_bn_fuse_pass',
                   'conv2d_add_act_fuse_pass', 'embedding_eltwise_layernorm_fuse_pass',
                   'quant_linear_fuse_pass', 'multihead_matmul_fuse_pass_v2', 'fused_dropout_add_layernorm', 'skip_layernorm_fuse_pass',
                   'fuse_gemm_epilogue_pass', 'layer_norm_fuse_pass', 'fc_fuse_pass', 'softmax_fuse_pass',
-                  'common_subexpression_elimination_pass', 'dead_code_elimination_pass')
+                  'common_subexpression_elimination_pass', 'dead_code_elimination_pass', 'inplace_pass')
 # opt-in (change numerics): 'fused_weight_only_linear_pass' (int8 weight-only Linears of inference programs)
 
 # FLAGS_static_ir_fusion: 'auto' (default: GPU programs), '1' / 'always' (every device, used by the

@@ -447,6 +447,64 @@ def woq_linear_static(x, q, scale, bias=None):
     return _unwrap(weight_only_linear(_wrap(x), _wrap(q), None if bias is None else _wrap(bias), _wrap(scale), 'int8'))
 
 
+# inplace_pass (reference: paddle/fluid/pir/transforms/general/inplace_pass.cc): in an inference
+# program, an elementwise op whose first operand dies at it writes into that operand's buffer.
+_FRESH = {  # producers whose output is a new buffer (never a view of an input)
+    'addmm', 'mm', 'matmul', 'bmm', 'baddbmm', 'linear', 'conv1d', 'conv2d', 'conv3d', 'conv_transpose1d',
+    'conv_transpose2d', 'conv_transpose3d', 'layer_norm', 'group_norm', 'batch_norm', 'instance_norm',
+    'softmax', 'log_softmax', 'add', 'sub', 'mul', 'div', 'true_divide', 'tanh', 'sigmoid', 'gelu', 'relu',
+    'silu', 'exp', 'erf', 'sqrt', 'rsqrt', 'pow', 'scaled_dot_product_attention', 'embedding', 'where',
+}
+_TF_INPLACE_KW = {TF.relu, TF.silu, TF.leaky_relu, TF.elu, TF.hardtanh, TF.relu6, TF.hardswish, TF.hardsigmoid}
+_INPLACE = {torch.relu: torch.relu_, torch.tanh: torch.tanh_, torch.sigmoid: torch.sigmoid_, torch.exp: torch.exp_,
+            torch.add: torch.Tensor.add_, torch.mul: torch.Tensor.mul_, torch.sub: torch.Tensor.sub_,
+            torch.div: torch.Tensor.div_, torch.Tensor.add: torch.Tensor.add_, torch.Tensor.mul: torch.Tensor.mul_,
+            torch.Tensor.sub: torch.Tensor.sub_, torch.Tensor.div: torch.Tensor.div_,
+            torch.Tensor.__add__: torch.Tensor.add_, torch.Tensor.__mul__: torch.Tensor.mul_,
+            torch.Tensor.__sub__: torch.Tensor.sub_, torch.Tensor.__truediv__: torch.Tensor.div_}
+
+
+def inplace_pass(prog, nodes):
+    """Rewrite dying-operand elementwise ops of inference programs to their in-place forms;
+    returns (nodes, rewritten count).  The operand must be a fresh buffer (its producer allocates,
+    see _FRESH), read only by non-aliasing ops, last read here, not fetched / fed, and of the
+    result's shape and dtype (no broadcast growth, no type promotion)."""
+    if _training(prog):
+        return nodes, 0
+    g = IP._Graph(prog, nodes)
+    producers = {}
+    for i, outs in enumerate(g.outs):
+        for v in outs:
+            producers.setdefault(v, []).append(i)
+    out, cnt = [], 0
+    for i, n in enumerate(nodes):
+        tgt = n.target
+        kw_form = n.kind == 'torch' and tgt in _TF_INPLACE_KW and not n.kwargs.get('inplace')
+        if n.kind != 'torch' or not (kw_form or tgt in _INPLACE) or not n.args or not isinstance(n.args[0], Ref):
+            out.append(n)
+            continue
+        x = n.args[0].vid
+        outs = g.outs[i]
+        prod = producers.get(x, [])
+        ok = (len(outs) == 1 and outs[0] != x and x not in g.external and len(prod) == 1 and prod[0] < i
+              and nodes[prod[0]].kind == 'torch' and _name(nodes[prod[0]]) in _FRESH
+              and max(g.uses.get(x, {i})) == i
+              and all(nodes[u].kind == 'torch' and (_name(nodes[u]) in _FRESH or nodes[u].target in _INPLACE
+                                                    or nodes[u].target in _TF_INPLACE_KW) for u in g.uses.get(x, ()))
+              and sum(1 for r in _refs(n.args) + _refs(n.kwargs) if r == x) == 1)
+        mx, mo = g.meta.get(x), g.meta.get(outs[0]) if outs else None
+        ok = ok and mx is not None and mo is not None and tuple(mx.shape) == tuple(mo.shape) and mx.dtype == mo.dtype
+        if not ok:
+            out.append(n)
+            continue
+        if kw_form:
+            out.append(Node('torch', tgt, n.args, dict(n.kwargs, inplace=True), n.outs, dict(n.meta or {}, inplace=True)))
+        else:
+            out.append(Node('torch', _INPLACE[tgt], n.args, n.kwargs, n.outs, dict(n.meta or {}, inplace=True)))
+        cnt += 1
+    return out, cnt
+
+
 def _graph_pass(fn):
     """Adapt a whole-list rewrite (nodes -> nodes, count) to apply_passes' per-pass protocol."""
     fn._whole_list = True
@@ -462,4 +520,5 @@ def register():
         'fused_weight_only_linear_pass': _woq_linear,
         'dead_code_elimination_pass': _graph_pass(dead_code_elimination),
         'common_subexpression_elimination_pass': _graph_pass(common_subexpression_elimination),
+        'inplace_pass': _graph_pass(inplace_pass),
     })

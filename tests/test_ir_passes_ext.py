@@ -174,3 +174,40 @@ def test_weight_only_linear_pass_opt_in(fusion_mode):
     want = xt._t.float().numpy() @ W + B
     np.testing.assert_allclose(np.asarray(got, dtype='float32'), want, rtol=0.05, atol=0.05)
     _ = IX
+
+
+def test_inplace_pass_rewrites_dying_operands_only():
+    """inplace_pass: relu / add of a dying fresh operand become in-place; a value that is fetched,
+    viewed or read later keeps the out-of-place op; results are unchanged."""
+    from paddle.static import ir_passes as IP
+    paddle.enable_static()
+    try:
+        main, startup = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, startup):
+            x = paddle.static.data('x', [4, 8], 'float32')
+            lin = paddle.nn.Linear(8, 8)
+            h = lin(x)                      # fresh (addmm)
+            a = paddle.nn.functional.relu(h)  # h dies here -> in place
+            b = a * 2.0                     # a dies -> in place
+            v = b.reshape([8, 4])           # b is viewed: the next op must not write into b
+            c = paddle.nn.functional.relu(b)
+            out = c.sum() + v.sum()
+        exe = paddle.static.Executor()
+        xv = np.random.RandomState(0).randn(4, 8).astype('float32')
+        ref = exe.run(main, feed={'x': xv}, fetch_list=[out])[0]
+        nodes, stats = IP.apply_passes(main, passes=['inplace_pass'], fetch=(main._val[id(out._t)],))
+        assert stats.get('inplace_pass') == 2, stats
+        inplace = [n for n in nodes if (n.meta or {}).get('inplace')]
+        assert len(inplace) == 2
+        main._ir_passes = ['inplace_pass']
+        import os
+        os.environ['FLAGS_static_ir_fusion'] = '1'
+        try:
+            IP._MODE[0] = '1'
+            got = exe.run(main, feed={'x': xv}, fetch_list=[out])[0]
+        finally:
+            IP._MODE[0] = 'auto'
+            os.environ.pop('FLAGS_static_ir_fusion', None)
+        np.testing.assert_allclose(got, ref, rtol=1e-6)
+    finally:
+        paddle.disable_static()
