@@ -144,13 +144,14 @@ def test_hip_cast_transpose(R, C, dtype):
 @pytest.mark.gpu
 @pytest.mark.parametrize("R,C", [(128, 128), (384, 1152), (16384, 2048)])
 def test_hip_cast_transpose_full_tiles_bitwise(R, C):
-    """The coalesced full-tile cast kernel == the guarded per-tile kernel, byte for byte."""
+    """The persistent and the one-tile full-tile cast kernels == the guarded per-tile kernel, byte
+    for byte."""
     from paddle.ops import _native as N
     assert N._load() is not None, N.load_error
     torch.manual_seed(2)
     x = (torch.randn(R, C, device='cuda') * 3).to(torch.bfloat16)
     outs = []
-    for full in (1, 0):
+    for full in (2, 1, 0):  # persistent, one tile per block, guarded
         old = N.lib.pa_fp8_set_cast_full(full)
         try:
             m = F8.FP8Meta(torch.float8_e4m3fn, 8, 0, 'cuda')
@@ -159,8 +160,9 @@ def test_hip_cast_transpose_full_tiles_bitwise(R, C):
             outs.append((q.view(torch.uint8).clone(), qt.view(torch.uint8).clone(), sinv.clone(), m.hist.clone()))
         finally:
             N.lib.pa_fp8_set_cast_full(old)
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
 
 
 @pytest.mark.gpu
