@@ -379,7 +379,10 @@ PA_API int pa_fp8_cast_transpose(const void* x, int R, int C, long long ldx, voi
   if (grid.y > 65535) return (int)hipErrorInvalidValue;
   if (R % f8::T == 0 && C % f8::T == 0 && ldx % 8 == 0 && g_cast_full == 2) {
     const int ntiles = (R / f8::T) * (C / f8::T);
-    const int g = ntiles < 1024 ? ntiles : 1024;  // 4 blocks per CU walk the tiles
+    // at most 4 blocks per CU walk the tiles, every block the same number of them (no tail of
+    // blocks with one tile more than the rest)
+    const int per = (ntiles + 1023) / 1024;
+    const int g = (ntiles + per - 1) / per;
     if (fmt == 0)
       f8::cast_transpose_persist_kernel<0><<<g, 256, 0, st>>>((const bf16_t*)x, R, C, ldx, (uint8_t*)q, (uint8_t*)qt,
                                                               (float*)hist, L, cur, (float*)scale_inv, margin_mul);

@@ -22,12 +22,14 @@ class WeightGradStore:
     """Deferred weight-gradient closures, grouped per micro-batch backward.  ``active``: F.linear
     records SplitBwLinear (set by a zero-bubble pipeline for its whole batch)."""
     active = False
+    deferred = 0  # weight-gradient closures queued so far (diagnostics / tests)
     _cur = []
     _ready = collections.deque()
 
     @classmethod
     def put(cls, fn):
         cls._cur.append(fn)
+        cls.deferred += 1
 
     @classmethod
     def flush(cls):
@@ -103,6 +105,34 @@ def split_linear(x, w, b, weight, bias):
     AMP cast of the parameter included); weight / bias the Parameters the deferred gradients
     accumulate into."""
     return SplitBwLinear.apply(x, w, b, weight, bias)
+
+
+def _is_weight(t):
+    return isinstance(t, torch.Tensor) and t.is_leaf and t.requires_grad and t.dim() == 2
+
+
+def static_substitutions():
+    """Recorded GEMM targets of a static program -> SplitBwLinear when the right operand is a
+    trainable 2-D parameter (the static pipeline's zero-bubble forward; the Executor applies them
+    while ``WeightGradStore.active``)."""
+    def _bias(b):
+        return b if isinstance(b, torch.Tensor) and b.is_leaf and b.requires_grad else None
+
+    def addmm(b, x, w, *a, **k):
+        if not a and not k and _is_weight(w) and torch.is_grad_enabled() and b.dim() == 1:
+            return split_linear(x, w, b, w, _bias(b))
+        return torch.addmm(b, x, w, *a, **k)
+
+    def mm(x, w, *a, **k):
+        if not a and not k and _is_weight(w) and torch.is_grad_enabled() and x.dim() == 2:
+            return split_linear(x, w, None, w, None)
+        return torch.mm(x, w, *a, **k)
+
+    def matmul(x, w, *a, **k):
+        if not a and not k and _is_weight(w) and torch.is_grad_enabled() and x.dim() >= 2:
+            return split_linear(x, w, None, w, None)
+        return torch.matmul(x, w, *a, **k)
+    return {torch.addmm: addmm, torch.mm: mm, torch.matmul: matmul}
 
 
 # ------------------------------------------------------------------ schedules + simulator

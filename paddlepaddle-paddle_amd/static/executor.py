@@ -214,9 +214,13 @@ def _gemm_subs():
     return _GEMM_SUBS
 
 
+_ZB = {'map': None}  # zero-bubble static pipeline: weight GEMMs with deferred dW (static/pipeline.py)
+
+
 def _exec_nodes(prog, nodes, env, smap, dev):
     subs = _SUBS['map']
     gsubs = _gemm_subs()
+    zb = _ZB['map']
     for n in nodes:
         if n.kind == 'torch':
             args = _resolve(prog, n.args, env, smap, dev)
@@ -225,6 +229,7 @@ def _exec_nodes(prog, nodes, env, smap, dev):
                 kwargs['device'] = dev
             fn = subs.get(n.target, n.target) if subs else n.target
             try:
+                fn = zb.get(fn, fn) if zb is not None else fn
                 fn = gsubs.get(fn, fn)
             except TypeError:  # unhashable target
                 pass

@@ -10,7 +10,9 @@ a stage >= b — are sent from stage b-1 to stage b (values skipping a stage are
 preceded by a small shape/dtype header.  Schedule (``schedule_mode``):
   * FThenB: all micro-batch forwards, then all backwards (reverse stage order);
   * 1F1B: warm-up forwards (stages - stage - 1), then one-forward-one-backward, then cool-down —
-    at most ``stages`` micro-batches of activations alive per stage.
+    at most ``stages`` micro-batches of activations alive per stage;
+  * ZBH1: 1F1B's order with every backward split into B (input gradients, sent upstream at once)
+    and W (weight gradients, deferred by SplitBwLinear and run behind the send).
 Backward: the last stage runs loss/acc backward; every other stage receives the gradients of the
 values it sent and continues autograd from them; gradients of the values it received go back.
 After the last micro-batch the data-parallel all-reduce, the optimizer step and clear_grad run
@@ -220,11 +222,36 @@ def run_pipeline(prog, feed, dev, pol, cfg, run_forward):
                 _send(g, cfg.prev, comm_dev, works)
         envs[m] = recvd[m] = sent[m] = None  # free this micro-batch's activations
 
-    if cfg.schedule.upper() == 'FTHENB':
+    kind = cfg.schedule.upper()
+    if kind == 'ZBH1' and amp is not None:
+        kind = '1F1B'  # AMP's scaled backward keeps the whole backward together
+    if kind == 'FTHENB':
         for m in range(acc):
             forward(m)
         for m in range(acc):
             backward(m)
+    elif kind == 'ZBH1':
+        # zero bubble (H1): 1F1B's F / B order, each backward split into B (input gradients, sent
+        # upstream at once) and W (the deferred weight-gradient GEMMs of SplitBwLinear, run behind
+        # the send) — reference passes/pipeline_scheduler_pass/pipeline_zero_bubble.py
+        from ..distributed.fleet.meta_parallel.zero_bubble_utils import (WeightGradStore, schedule_order,
+                                                                          static_substitutions)
+        from . import executor as _ex
+        WeightGradStore.clear()
+        prev_zb, prev_active = _ex._ZB['map'], WeightGradStore.active
+        _ex._ZB['map'], WeightGradStore.active = static_substitutions(), True
+        try:
+            for op, m in schedule_order('ZBH1', S, s, acc):
+                if op == 'F':
+                    forward(m)
+                elif op == 'B':
+                    backward(m)
+                    WeightGradStore.flush()
+                else:
+                    WeightGradStore.pop()
+        finally:
+            _ex._ZB['map'], WeightGradStore.active = prev_zb, prev_active
+            WeightGradStore.clear()
     else:  # 1F1B
         warm = min(acc, S - s - 1)
         for m in range(warm):

@@ -1,6 +1,7 @@
 """Static Program pipeline parallelism over gloo ranks (reference: fleet static pipeline optimizer;
 ops placed with static.device_guard('gpu:N'), pipeline_configs accumulate_steps micro-batches).
-argv[1]: schedule ('1F1B' / 'FThenB'); argv[2]: 'pp' (pp = world), 'ppdp' (pp 2 x dp 2), 'ppamp'
+argv[1]: schedule ('1F1B' / 'FThenB' / 'ZBH1': zero bubble, weight gradients deferred behind the
+input-gradient sends); argv[2]: 'pp' (pp = world), 'ppdp' (pp 2 x dp 2), 'ppamp'
 (pp = world + static AMP fp16 with dynamic loss scaling whose first step overflows: every stage must
 skip it together) or 'ppgm' (pp = world + gradient merge k_steps 2: one update per two runs).
 Every rank builds the same program (same seed); after 3 steps each stage's parameters must equal a
@@ -75,6 +76,9 @@ def main():
         out = exe.run(main_p, feed={'x': xs[dp_rank * half:(dp_rank + 1) * half],
                                     'y': ys[dp_rank * half:(dp_rank + 1) * half]}, fetch_list=[loss])
         losses.append(float(np.asarray(out[0]).reshape(-1)[0]))
+    if sched == 'ZBH1':
+        from paddle.distributed.fleet.meta_parallel.zero_bubble_utils import WeightGradStore
+        assert WeightGradStore.deferred > 0  # the stage's Linears ran as SplitBwLinear
     got = [p.numpy().copy() for p in main_p.all_parameters()]
     if mode == 'ppamp':
         import paddle.static.amp as samp

@@ -335,7 +335,8 @@ def test_static_fleet_tensor_parallel(mode, nproc):
 
 
 @pytest.mark.parametrize("sched,mode,nproc", [('1F1B', 'pp', 2), ('FThenB', 'pp', 2), ('1F1B', 'pp', 3),
-                                              ('1F1B', 'ppdp', 4), ('1F1B', 'ppamp', 2), ('FThenB', 'ppgm', 2)])
+                                              ('1F1B', 'ppdp', 4), ('1F1B', 'ppamp', 2), ('FThenB', 'ppgm', 2),
+                                              ('ZBH1', 'pp', 2), ('ZBH1', 'pp', 3), ('ZBH1', 'ppdp', 4)])
 def test_static_fleet_pipeline_parallel(sched, mode, nproc):
     """Static-mode fleet pipeline: device_guard stages, micro-batched FThenB / 1F1B with
     send/recv of activations and gradients; every stage's parameters match a single-process run."""
@@ -351,7 +352,7 @@ def test_dist_to_static_program_data_parallel(k):
     assert out.count(f'dist static k{k} OK') == 2, out[-3000:]
 
 
-@pytest.mark.parametrize("mode", ['shard1', 'shard2', 'shard3', 'pp_1F1B', 'pp_FThenB', 'engine'])
+@pytest.mark.parametrize("mode", ['shard1', 'shard2', 'shard3', 'pp_1F1B', 'pp_FThenB', 'pp_ZBH1', 'engine'])
 def test_dist_to_static_sharded_and_pipelined_programs(mode):
     """dist.to_static / auto.Engine with sharding stage 1/2/3 or a 2-stage pipeline run as static
     Programs and equal single-process training (tests/dist/worker_dist_static_sp.py)."""
