@@ -225,6 +225,77 @@ def _conv_add_act(g, i):
     return body, {tail: node}
 
 
+def _bn_args_full(n):
+    """(x, running_mean, running_var, weight, bias, training, torch momentum, eps) of a recorded
+    torch.nn.functional.batch_norm node, else None."""
+    if n is None or n.kind != 'torch' or n.target is not TF.batch_norm:
+        return None
+    names = ('input', 'running_mean', 'running_var', 'weight', 'bias', 'training', 'momentum', 'eps')
+    defaults = (None, None, None, None, None, False, 0.1, 1e-5)
+    if set(n.kwargs) - set(names):
+        return None
+    v = list(n.args) + [None] * (len(names) - len(n.args))
+    out = [n.kwargs.get(k, v[j] if j < len(n.args) else defaults[j]) for j, k in enumerate(names)]
+    if not isinstance(out[0], Ref):
+        return None
+    return out
+
+
+def _bn_add_act(g, i):
+    """batch_norm (-> + residual) (-> relu) as one node on the channels-last HIP kernels (reference
+    paddle/fluid/framework/ir/fused_bn_add_act_pass.cc, batch_norm_act_fuse_pass.cc); training and
+    inference.  A recorded program holds the library form (its ops were recorded on meta tensors);
+    the fused node routes to csrc/batchnorm.hip on the GPU — statistics, apply, residual add and
+    ReLU in one autograd op — and runs the composite elsewhere."""
+    n = g.nodes[i]
+    ba = _bn_args_full(n)
+    if ba is None:
+        return None
+    body, cur, residual, act, tail = [i], IP._one_out(n), None, False, i
+    j = IP._sole_user(g, cur, body)
+    m = g.node(j)
+    if m is not None and IP._kind(m) == 'add' and len(m.args) == 2 and not m.kwargs:
+        a, b = m.args
+        other = b if isinstance(a, Ref) and a.vid == cur else (a if isinstance(b, Ref) and b.vid == cur else None)
+        if isinstance(other, Ref) and other.vid != cur:
+            residual, tail = other, j
+            body.append(j)
+            cur = IP._one_out(m)
+            j = IP._sole_user(g, cur, body)
+            m = g.node(j)
+    if _relu_node(m) and isinstance(m.args[0], Ref) and m.args[0].vid == cur:
+        act, tail = True, j
+        body.append(j)
+    if len(body) > 1 and not g.private(body[:-1], users=body[-1:]):
+        return None
+    node = Node('torch', batch_norm_add_act, list(ba) + [residual, act], {}, IP._one_out(g.nodes[tail]),
+                dict(n.meta or {}, fused='fused_bn_add_act_pass'))
+    return body, {tail: node}
+
+
+def batch_norm_add_act(x, run_mean, run_var, weight, bias, training, momentum, eps, residual=None, relu=False):
+    """relu?(batch_norm(x) + residual?) — x NCHW (torch batch_norm layout, torch momentum)."""
+    from ..ops import batchnorm as _bn
+    from ..ops import use_hip
+    if x.dim() == 4 and use_hip(x) and (residual is None or residual.shape == x.shape):
+        xc = x.permute(0, 2, 3, 1)
+        if _bn.supported(xc, weight) and (training or not (torch.is_grad_enabled() and any(
+                t is not None and t.requires_grad for t in (x, weight, bias, residual)))):
+            if not xc.is_contiguous():
+                xc = xc.contiguous()
+            rc = None
+            if residual is not None:
+                rc = residual.permute(0, 2, 3, 1)
+                rc = rc if rc.is_contiguous() else rc.contiguous()
+            y = _bn.bn_act_nhwc(xc, weight, bias, run_mean, run_var, eps, 1.0 - momentum, bool(training), bool(relu),
+                                residual=rc)
+            return y.permute(0, 3, 1, 2)
+    y = TF.batch_norm(x, run_mean, run_var, weight, bias, training, momentum, eps)
+    if residual is not None:
+        y = y + residual
+    return torch.relu(y) if relu else y
+
+
 def _is_embedding(n):
     from ..ops import matmul as _hm
     return n is not None and n.kind == 'torch' and (n.target is TF.embedding or n.target is _hm._embedding_sub) and \
@@ -515,6 +586,7 @@ def register():
     IP._PASSES.update({
         'constant_folding_pass': _const_fold,
         'conv2d_bn_fuse_pass': _conv_bn,
+        'fused_bn_add_act_pass': _bn_add_act,
         'conv2d_add_act_fuse_pass': _conv_add_act,
         'embedding_eltwise_layernorm_fuse_pass': _emb_ln,
         'fused_weight_only_linear_pass': _woq_linear,

@@ -160,3 +160,46 @@ def test_resnet50_predictor_folds_batch_norm_gpu():
     bad = [n for n in _miopen_kernels(lambda: run('auto')) if 'batchnorm' in n.lower() or 'conv' in n.lower()
            or 'igemm' in n.lower() or 'xdlops' in n.lower()]
     assert bad == [], bad
+
+
+def test_fused_bn_add_act_pass_static_training_gpu():
+    """A recorded conv -> BN -> ReLU / conv -> BN -> +residual -> ReLU training program on the GPU:
+    the fused_bn_add_act_pass nodes run the HIP batch-norm kernels (statistics, apply, residual, ReLU
+    in one autograd op) and three SGD steps equal the unfused (library) program."""
+    from test_ir_passes_ext import _bn_block_program
+    from paddle.ops import batchnorm as BN
+    calls = []
+    orig = BN.bn_act_nhwc
+
+    def counting(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+    rng = np.random.RandomState(0)
+    batches = [(rng.randn(16, 8, 12, 12).astype('float32'), rng.randint(0, 8, (16,)).astype('int64'))
+               for _ in range(3)]
+    paddle.set_device('gpu')
+    paddle.enable_static()
+    res = []
+    try:
+        for fused in (False, True):
+            main, startup, loss = _bn_block_program()
+            main._ir_passes = ['fused_bn_add_act_pass'] if fused else []
+            exe = static.Executor(paddle.CUDAPlace(0))
+            exe.run(startup)
+            BN.bn_act_nhwc = counting
+            try:
+                ls = [float(exe.run(main, feed={'x': xb, 'y': yb}, fetch_list=[loss])[0]) for xb, yb in batches]
+            finally:
+                BN.bn_act_nhwc = orig
+            res.append((ls, [p.numpy().copy() for p in main.all_parameters()]))
+            if fused:
+                assert main._ir_stats.get('fused_bn_add_act_pass') == 2, main._ir_stats
+                assert len(calls) == 2 * len(batches)
+            else:
+                assert not calls
+    finally:
+        paddle.disable_static()
+        paddle.set_device('cpu')
+    np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-4, atol=1e-5)
+    for a, b in zip(res[0][1], res[1][1]):
+        np.testing.assert_allclose(a, b, rtol=2e-3, atol=2e-4)

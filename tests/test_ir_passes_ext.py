@@ -211,3 +211,51 @@ def test_inplace_pass_rewrites_dying_operands_only():
         np.testing.assert_allclose(got, ref, rtol=1e-6)
     finally:
         paddle.disable_static()
+
+
+def _bn_block_program(seed=3):
+    paddle.seed(seed)
+    main, startup = paddle.static.Program(), paddle.static.Program()
+    with paddle.static.program_guard(main, startup):
+        x = paddle.static.data('x', [-1, 8, 6, 6], 'float32')
+        y = paddle.static.data('y', [-1], 'int64')
+        c1 = paddle.nn.Conv2D(8, 8, 3, padding=1)
+        b1 = paddle.nn.BatchNorm2D(8)
+        c2 = paddle.nn.Conv2D(8, 8, 3, padding=1)
+        b2 = paddle.nn.BatchNorm2D(8)
+        h = paddle.nn.functional.relu(b1(c1(x)))
+        h = paddle.nn.functional.relu(b2(c2(h)) + x)       # bn -> add(residual) -> relu
+        logits = paddle.nn.functional.adaptive_avg_pool2d(h, 1).reshape([-1, 8])
+        loss = paddle.nn.functional.cross_entropy(logits, y)
+        paddle.optimizer.SGD(0.1).minimize(loss)
+    return main, startup, loss
+
+
+def test_fused_bn_add_act_pass_training_matches_unfused():
+    """fused_bn_add_act_pass: batch_norm -> relu and batch_norm -> add -> relu of a recorded training
+    program become one node each; three SGD steps equal the unfused program."""
+    paddle.enable_static()
+    try:
+        rng = np.random.RandomState(0)
+        batches = [(rng.randn(4, 8, 6, 6).astype('float32'), rng.randint(0, 8, (4,)).astype('int64'))
+                   for _ in range(3)]
+        res = []
+        for fused in (False, True):
+            main, startup, loss = _bn_block_program()
+            exe = paddle.static.Executor()
+            exe.run(startup)
+            if fused:
+                nodes, stats = IP.apply_passes(main, passes=['fused_bn_add_act_pass'])
+                assert stats.get('fused_bn_add_act_pass') == 2, stats
+                main._ir_passes = ['fused_bn_add_act_pass']
+                IP._MODE[0] = '1'
+            try:
+                ls = [float(exe.run(main, feed={'x': xb, 'y': yb}, fetch_list=[loss])[0]) for xb, yb in batches]
+            finally:
+                IP._MODE[0] = 'auto'
+            res.append((ls, [p.numpy().copy() for p in main.all_parameters()]))
+        np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-5, atol=1e-6)
+        for a, b in zip(res[0][1], res[1][1]):
+            np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+    finally:
+        paddle.disable_static()
