@@ -68,7 +68,8 @@ PA_FLAGS = {
     'force_collectives': (False, 'run the real collectives at world size 1 (1-rank RCCL rehearsal)'),
     'sharding_alias': (True, 'world-1 sharding units alias the optimizer arenas'),
     'dist_to_static': (True, 'dist.to_static records a static Program (else eager SPMD)'),
-    'sot': (False, 'to_static(full_graph=False) uses the bytecode (SOT) front end'),
+    'sot_frontend': ('opcode', "SOT front end: 'opcode' (this framework's translator) or 'dynamo'"),
+    'sot': (True, 'to_static(full_graph=False) runs through the bytecode (SOT) translator (jit/opcode_translator.py)'),
     'pdmodel': (True, 'save_inference_model writes the reference ProgramDesc format when possible'),
     'pir': ('', 'jit.save writes the PIR json program (1 / 0; empty: FLAGS_enable_pir_api)'),
 }

@@ -1,8 +1,10 @@
 """paddle.jit (reference: python/paddle/jit/api.py — to_static:214, not_to_static:357,
 save:908, load:1480; translated_layer.py TranslatedLayer).
 
-MI355X-first: calls are not traced or compiled.  The eager path already runs the hand-written HIP
-kernels; ``to_static`` keeps dygraph semantics and adds
+``to_static(fn)`` (``full_graph=False``, the reference's 3.x default) runs ``fn`` through the SOT
+translator — this framework's own opcode translator (jit/opcode_translator.py): the tensor work
+between graph breaks becomes static Programs replayed by the Executor under guards, the rest stays
+Python (``FLAGS_pa_sot=0`` keeps plain dygraph calls).  ``to_static`` also provides
 * a recorded static Program on demand (``concrete_program``) — the same IR ``jit.save``
   serialises (``static/io.py``).  Recording runs the function after ``dy2static`` has rewritten
   its tensor-dependent ``if`` / ``while`` / ``for range`` / ``and``/``or``/``not`` into
@@ -10,9 +12,8 @@ kernels; ``to_static`` keeps dygraph semantics and adds
 * HIP-graph replay of the forward for inference-shaped calls (``backend='hip_graph'`` or
   ``build_strategy.use_hip_graph``): launch-bound small-batch decoding collapses into one
   graph launch per call;
-* bytecode-level translation (``backend='sot'``, or ``full_graph=False`` with PADDLE_AMD_SOT=1):
-  jit/sot.py captures the tensor work as static Programs run by the Executor, graph breaks fall
-  back to Python.
+* ``full_graph=True``: dygraph semantics for calls, the AST-converted recorded Program for
+  ``concrete_program`` / ``jit.save``.
 ``jit.load`` returns a ``TranslatedLayer`` that interprets the saved program without the
 Python class that produced it.
 """

@@ -3,26 +3,24 @@ symbolic_translate, the default ``to_static(full_graph=False)`` mode of Paddle 3
 
 The reference simulates the function's bytecode, builds a static program from the tensor
 operations it can follow and falls back to dygraph around what it cannot ("graph breaks"),
-guarding each captured program on the inputs it was built for.  Here the bytecode front end is
-CPython frame evaluation through ``torch._dynamo`` (the function's bytecode is symbolically
-executed; unsupported Python — data-dependent branches on tensor values, prints, calls into
-extensions — becomes a graph break and runs eagerly; guards re-translate on new shapes / types),
-and the back end is this framework's own static stack:
+guarding each captured program on the inputs it was built for.  Two front ends:
 
-* every captured FX graph is recorded into a static ``Program`` (static/program.py) on meta
-  Variables shaped like the graph's inputs, and
-* each call interprets that Program with the Executor's runner (static/executor.py
-  ``run_program``): recorded GEMMs substituted onto the hand-written MFMA kernels, the IR fusion
-  passes (attention -> flash kernel, LayerNorm / skip-LayerNorm -> norm kernels, fc + bias + act ->
-  GEMM epilogue, softmax) applied on GPU programs, autograd kept when gradients are enabled.
+* ``frontend='opcode'`` (default): this framework's own opcode translator
+  (jit/opcode_translator.py) — a CPython 3.10 bytecode interpreter that records each region of
+  the frame between graph breaks into a static ``Program`` with the static recorder, runs it on
+  the Executor and replays it under guards;
+* ``frontend='dynamo'``: CPython frame evaluation through ``torch._dynamo`` as the bytecode front
+  end, every captured FX graph recorded into a static ``Program`` on meta Variables shaped like
+  the graph's inputs (a graph the recorder cannot follow runs as captured).
 
-While a frame is being translated the paddle ops take their torch composite forms
-(``ops.use_hip`` is False under tracing), so the captured graphs are whole torch-op graphs and the
-Executor maps them back onto the HIP kernels.  A graph the recorder cannot follow runs as the
-captured FX graph (eager torch ops): a translation failure never changes results.
+Either way each call interprets the captured Programs with the Executor's runner
+(static/executor.py ``run_program``): recorded GEMMs substituted onto the hand-written MFMA kernels,
+the IR fusion passes (attention -> flash kernel, LayerNorm / skip-LayerNorm -> norm kernels, fc +
+bias + act -> GEMM epilogue, softmax) applied on GPU programs, autograd kept when gradients are
+enabled.  A translation failure never changes results.
 
 Usage: ``paddle.jit.sot.symbolic_translate(fn)(*args)``, ``paddle.jit.to_static(fn, backend='sot')``
-(or ``full_graph=False`` with ``PADDLE_AMD_SOT=1``).
+(or ``full_graph=False`` with ``FLAGS_pa_sot=1``).
 """
 from ..framework.flags import pa_flag  # noqa: E402
 import functools
@@ -36,9 +34,13 @@ _STATS = {'graphs': 0, 'recorded': 0, 'fallback': 0, 'calls': 0}
 
 
 def stats():
-    """Counters of the translator: captured graphs, graphs recorded into Programs, graphs left on
-    the FX fallback, and calls served by recorded Programs."""
-    return dict(_STATS)
+    """Counters of the translators: captured graphs (regions), graphs recorded into Programs,
+    graphs left on the FX fallback, and calls served by recorded Programs."""
+    from .opcode_translator import stats as _ot
+    o = _ot()
+    return {'graphs': _STATS['graphs'] + o['regions'], 'recorded': _STATS['recorded'] + o['recorded'],
+            'fallback': _STATS['fallback'], 'calls': _STATS['calls'] + o['runs'], 'breaks': o['breaks'],
+            'eager_calls': o['eager_calls']}
 
 
 def _paddle_dtype(dt):
@@ -126,10 +128,22 @@ def _backend(gm, example_inputs):
     return _CapturedGraph(gm, example_inputs)
 
 
-def symbolic_translate(fn=None, training=True, **kwargs):
+def symbolic_translate(fn=None, training=True, frontend=None, **kwargs):
     """Translate ``fn`` (a function or a Layer's bound forward) at the bytecode level: tensor work
-    runs as captured static Programs on the Executor, the rest of the frame stays Python."""
+    runs as captured static Programs on the Executor, the rest of the frame stays Python.
+    ``frontend``: 'opcode' (this framework's translator, default) or 'dynamo'."""
+    fe = frontend or pa_flag('sot_frontend')
+
     def wrap(f):
+        if fe != 'dynamo':
+            from .opcode_translator import OpcodeTranslator
+            tr = OpcodeTranslator(f)
+
+            @functools.wraps(f)
+            def run_ot(*args, **kw):
+                return tr(*args, **kw)
+            run_ot._sot_translator = tr
+            return run_ot
         compiled = torch.compile(f, backend=_backend, fullgraph=False, dynamic=False)
 
         @functools.wraps(f)

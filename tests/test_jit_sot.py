@@ -123,3 +123,132 @@ def test_sot_gpu_bf16_runs_on_executor_kernels(monkeypatch):
     err = (out._t.float() - ref._t.float()).abs().max().item() / ref._t.float().abs().max().item()
     assert err < 2e-2, err
     assert hits, "captured GEMMs did not run on the Executor's kernel substitutions"
+
+
+# ------------------------------------------------------------ the framework's own opcode translator
+from paddle.jit.opcode_translator import OpcodeTranslator, stats as ot_stats  # noqa: E402
+
+_SCALE = 2.0
+
+
+def _scaled(x):
+    return x * _SCALE
+
+
+class _Block(paddle.nn.Layer):
+    def __init__(self, d):
+        super().__init__()
+        self.fc = paddle.nn.Linear(d, d)
+        self.use_act = True
+
+    def forward(self, x):
+        y = self.fc(x)
+        if self.use_act:  # a Python attribute: baked, guarded
+            y = F.relu(y)
+        return y
+
+
+class _Stack(paddle.nn.Layer):
+    def __init__(self, d=8, n=3):
+        super().__init__()
+        self.blocks = paddle.nn.LayerList([_Block(d) for _ in range(n)])
+        self.drop = paddle.nn.Dropout(0.5)
+
+    def forward(self, x, extra=None):
+        outs = []
+        for b in self.blocks:              # unrolled: one region for the whole stack
+            x = b(x)
+            outs.append(x.mean())
+        h = {'y': self.drop(x), 'means': [o * 1 for o in outs]}
+        if extra is not None:
+            h['y'] = h['y'] + extra
+        return h
+
+
+def test_opcode_translator_one_region_unrolled_and_replayed():
+    paddle.seed(5)
+    net = _Stack()
+    net.eval()
+    tr = OpcodeTranslator(net.forward)
+    x = paddle.randn([4, 8])
+    before = ot_stats()
+    out = tr(x)
+    mid = ot_stats()
+    out2 = tr(x)
+    after = ot_stats()
+    ref = net(x)
+    _close(out['y'], ref['y'])
+    _close(out2['y'], ref['y'])
+    assert len(out['means']) == 3
+    assert mid['regions'] - before['regions'] == 1 and mid['breaks'] == before['breaks']  # no graph break
+    assert after['regions'] == mid['regions'] and after['hits'] - mid['hits'] == 1        # replayed, not retraced
+    out3 = tr(x, extra=paddle.ones([4, 8]))                                               # new kwargs state
+    _close(out3['y'], ref['y'] + 1)
+
+
+def test_opcode_translator_guards_attribute_global_and_training_flag():
+    global _SCALE
+    paddle.seed(6)
+    net = _Stack()
+    net.eval()
+    tr = OpcodeTranslator(net.forward)
+    x = paddle.randn([4, 8])
+    _close(tr(x)['y'], net(x)['y'])
+    net.blocks[1].use_act = False       # attribute the translation branched on
+    _close(tr(x)['y'], net(x)['y'])
+    net.train()                         # dropout on: a different region (training flags guarded)
+    paddle.seed(9)
+    y1 = tr(x)['y']
+    assert float((y1 == 0).astype('float32').mean()) > 0.2
+    net.eval()
+    tg = OpcodeTranslator(_scaled)
+    _close(tg(x), x * 2.0)
+    _SCALE = 3.0                        # global the translation read
+    try:
+        _close(tg(x), x * 3.0)
+    finally:
+        _SCALE = 2.0
+
+
+def test_opcode_translator_breaks_side_effects_and_eager_fallbacks():
+    log = []
+
+    def helper(t):
+        log.append(float(t.sum()))      # tensor value + outer list: runs concretely
+        return t * 2
+
+    def f(x):
+        y = paddle.exp(x)
+        z = helper(y)
+        s = f"{z.shape[0]} rows"        # Python string from a shape: fine inside a region
+        return z + 1, s
+
+    def gen(x):                         # generator: not modelled, runs eagerly
+        yield x * 2
+    tr = OpcodeTranslator(f)
+    x = paddle.randn([3, 4])
+    for _ in range(2):
+        out, s = tr(x)
+        _close(out, paddle.exp(x) * 2 + 1)
+        assert s == '3 rows'
+    assert len(log) == 2
+    tg = OpcodeTranslator(lambda t: list(gen(t))[0])
+    _close(tg(x), x * 2)
+
+
+def test_opcode_translator_input_gradients_and_closures():
+    w = paddle.randn([4, 4])
+
+    def f(x, k=2):
+        sq = [x * i for i in range(k)]          # list comprehension (inlined function)
+        g = lambda t: paddle.matmul(t, w)       # closure over a captured tensor
+        return g(sum(sq[1:], sq[0])).sum()
+    tr = OpcodeTranslator(f)
+    x = paddle.randn([3, 4])
+    x.stop_gradient = False
+    loss = tr(x, k=3)
+    loss.backward()
+    ref_x = x.detach()
+    ref_x.stop_gradient = False
+    (paddle.matmul(ref_x * 3, w)).sum().backward()
+    _close(x.grad, ref_x.grad)
