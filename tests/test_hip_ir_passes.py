@@ -175,7 +175,7 @@ def test_fused_bn_add_act_pass_static_training_gpu():
         calls.append(1)
         return orig(*a, **k)
     rng = np.random.RandomState(0)
-    batches = [(rng.randn(16, 8, 12, 12).astype('float32'), rng.randint(0, 8, (16,)).astype('int64'))
+    batches = [(rng.randn(32, 8, 6, 6).astype('float32'), rng.randint(0, 8, (32,)).astype("int64"))
                for _ in range(3)]
     paddle.set_device('gpu')
     paddle.enable_static()
