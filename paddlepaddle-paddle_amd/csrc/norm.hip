@@ -296,6 +296,121 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dy,
   }
 }
 
+// Narrow rows (cols <= 64 * E * NCH: ERNIE / BERT-base hidden 768): ONE WAVE PER ROW, four rows in
+// flight per block plus the next row's loads prefetched per wave, reductions by DPP / shuffles only
+// (no barriers in the row loop).  The block-per-row kernel above leaves 160 of 256 threads idle at
+// 768 columns with one row in flight per block (≈ 3 TB/s on [32768, 768]).  The four waves'
+// gamma / beta / input-bias partial sums are combined through LDS at the end, so the partial
+// layout ([nparts][cols] rows, one per block) and the finishing kernel stay the same.
+template <typename T, typename WT, int NCH, bool RMS, bool DROP>
+__global__ __launch_bounds__(256) void norm_bwd_wave_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                            const WT* __restrict__ w, const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd,
+                                                            const T* __restrict__ dsum, T* __restrict__ dx,
+                                                            float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                            int rows, int cols, T* __restrict__ dxd,
+                                                            float* __restrict__ xb_part, DropSpec dsp) {
+  dsp.seed = rng_mix(dsp.seed);  // graph-captured steps: per-replay stream
+  constexpr int E = 16 / sizeof(T);
+  constexpr int W = 64 * E * NCH;  // widest row this instantiation handles
+  __shared__ float red[4][W];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float aw[NCH][E], ab[NCH][E], wv[NCH][E], axb[DROP ? NCH : 1][E];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int j = (c * 64 + lane) * E;
+#pragma unroll
+    for (int e = 0; e < E; ++e) { aw[c][e] = 0.f; ab[c][e] = 0.f; wv[c][e] = 0.f; }
+    if constexpr (DROP) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) axb[c][e] = 0.f;
+    }
+    if (j < cols) load_f<WT, E>(w + j, wv[c]);
+  }
+  const float inv_n = 1.0f / cols;
+  Pack<T, E> px[NCH], pd[NCH], ps[NCH];
+  auto prefetch = [&](int r) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int j = (c * 64 + lane) * E;
+      if (r < rows && j < cols) {
+        const size_t b = (size_t)r * cols + j;
+        px[c] = *reinterpret_cast<const Pack<T, E>*>(x + b);
+        pd[c] = *reinterpret_cast<const Pack<T, E>*>(dy + b);
+        if (dsum != nullptr) ps[c] = *reinterpret_cast<const Pack<T, E>*>(dsum + b);
+      }
+    }
+  };
+  const int row0 = blockIdx.x * 4 + wave, stride = gridDim.x * 4;
+  prefetch(row0);
+  for (int row = row0; row < rows; row += stride) {
+    const size_t base = (size_t)row * cols;
+    const float mu = RMS ? 0.f : mean[row];
+    const float rs = rstd[row];
+    float xh[NCH][E], g[NCH][E], dsv[NCH][E];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int j = (c * 64 + lane) * E;
+      if (j < cols) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const float xv = to_f(px[c].v[e]), dv = to_f(pd[c].v[e]);
+          xh[c][e] = (xv - mu) * rs;
+          g[c][e] = dv * wv[c][e];
+          s1 += g[c][e];
+          s2 += g[c][e] * xh[c][e];
+          aw[c][e] += dv * xh[c][e];
+          ab[c][e] += dv;
+          dsv[c][e] = dsum != nullptr ? to_f(ps[c].v[e]) : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) { xh[c][e] = 0.f; g[c][e] = 0.f; dsv[c][e] = 0.f; }
+      }
+    }
+    prefetch(row + stride);
+    const float m1 = RMS ? 0.f : wave_sum(s1) * inv_n;
+    const float m2 = wave_sum(s2) * inv_n;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int j = (c * 64 + lane) * E;
+      if (j < cols) {
+        float o[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) o[e] = rs * (g[c][e] - m1 - xh[c][e] * m2) + dsv[c][e];
+        store_f<T, E>(dx + base + j, o);
+        if constexpr (DROP) {
+          float m[E];
+          drop_mask<E>(dsp, (base + j) / E, m);
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            o[e] *= m[e];
+            axb[c][e] += o[e];
+          }
+          store_f<T, E>(dxd + base + j, o);
+        }
+      }
+    }
+  }
+  // the block's partial row of each column sum: the four waves' values added through LDS
+  auto combine = [&](float (&acc)[NCH][E], float* __restrict__ part) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) red[wave][(c * 64 + lane) * E + e] = acc[c][e];
+    }
+    __syncthreads();
+    for (int j = tid; j < cols; j += 256) part[(size_t)blockIdx.x * cols + j] = red[0][j] + red[1][j] + red[2][j] + red[3][j];
+    __syncthreads();
+  };
+  combine(aw, dw_part);
+  if (!RMS) combine(ab, db_part);
+  if constexpr (DROP) {
+    if (xb_part != nullptr) combine(axb, xb_part);
+  }
+}
+
 template <typename T, typename WT, bool RMS>
 __global__ __launch_bounds__(256) void norm_bwd_generic(const T* __restrict__ dy, const T* __restrict__ x,
                                                         const WT* __restrict__ w, const float* __restrict__ mean,
@@ -384,6 +499,9 @@ hipError_t launch_fwd(const void* x, const void* res, const void* w, const void*
   return hipGetLastError();
 }
 
+// A/B switch (pa_norm_set_bwd_wave): the one-wave-per-row backward for rows of <= 128 vectors
+static int g_norm_bwd_wave = 1;
+
 template <typename T, typename WT, bool RMS>
 hipError_t launch_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
                       const void* dsum, void* dx, float* part, void* dw, void* db, int rows, int cols, int nparts,
@@ -408,8 +526,22 @@ hipError_t launch_bwd(const void* dy, const void* x, const void* w, const float*
                                                                     mean, rstd, (const T*)dsum, (T*)dx, dw_part, \
                                                                     db_part, rows, cols, nullptr, nullptr, dsp); \
   } while (0)
+#define PA_NBW(C)                                                                                                \
+  do {                                                                                                           \
+    if (drop)                                                                                                    \
+      norm_bwd_wave_kernel<T, WT, C, RMS, true><<<nparts, 256, 0, st>>>((const T*)dy, (const T*)x, (const WT*)w, \
+                                                                   mean, rstd, (const T*)dsum, (T*)dx, dw_part,  \
+                                                                   db_part, rows, cols, dxd, xb_part, dsp);      \
+    else                                                                                                         \
+      norm_bwd_wave_kernel<T, WT, C, RMS, false><<<nparts, 256, 0, st>>>((const T*)dy, (const T*)x,              \
+                                                                    (const WT*)w, mean, rstd, (const T*)dsum,    \
+                                                                    (T*)dx, dw_part, db_part, rows, cols,        \
+                                                                    nullptr, nullptr, dsp);                      \
+  } while (0)
   if (drop && (!vec_ok || chunks > 4)) return hipErrorInvalidValue;
-  if (vec_ok && chunks <= 1) PA_NB(1);
+  if (vec_ok && cols <= 64 * E && g_norm_bwd_wave) PA_NBW(1);
+  else if (vec_ok && cols <= 128 * E && g_norm_bwd_wave) PA_NBW(2);
+  else if (vec_ok && chunks <= 1) PA_NB(1);
   else if (vec_ok && chunks <= 2) PA_NB(2);
   else if (vec_ok && chunks <= 4) PA_NB(4);
   else if (vec_ok && chunks <= 8 && sizeof(T) == 2) PA_NB(8);
@@ -417,6 +549,7 @@ hipError_t launch_bwd(const void* dy, const void* x, const void* w, const float*
     norm_bwd_generic<T, WT, RMS><<<nparts, 256, 0, st>>>((const T*)dy, (const T*)x, (const WT*)w, mean, rstd,
                                                          (const T*)dsum, (T*)dx, dw_part, db_part, rows, cols);
 #undef PA_NB
+#undef PA_NBW
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // gamma / beta / input-bias gradient finishes: one launch
@@ -443,6 +576,12 @@ using namespace pa;
 
 // Number of partial rows the backward writes (callers size `part` as 2 * nparts * cols floats,
 // 3 * nparts * cols for the fused-dropout backward with a bias gradient).
+PA_API int pa_norm_set_bwd_wave(int v) {
+  const int old = g_norm_bwd_wave;
+  g_norm_bwd_wave = v;
+  return old;
+}
+
 PA_API int pa_norm_bwd_nparts(int rows) { return rows < 512 ? (rows < 1 ? 1 : rows) : 512; }
 
 PA_API hipError_t pa_layernorm_fwd(const void* x, const void* res, const void* w, const void* b, void* y,

@@ -89,6 +89,7 @@ _SIGS = {
     'pa_fp8_cast_transpose': [P, I, I, LL, P, P, P, I, I, P, I, F, P],
     'pa_fp8_amax': [P, I, I, LL, P, P],
     'pa_fp8_cast_transpose_multi': [P, I, I, I, P],
+    'pa_norm_set_bwd_wave': [I],
     'pa_fp8_set_cast_full': [I],
     'pa_woq_tune': [I, I],
     'pa_woq_set_ct': [I],

@@ -30,7 +30,8 @@ def _close(a, b, atol, rtol=0.0, name=''):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("shape", [(64, 2048), (33, 768), (8, 4096), (5, 300), (16, 12288)])
+@pytest.mark.parametrize("shape", [(64, 2048), (33, 768), (8, 4096), (5, 300), (16, 12288), (2048, 768), (600, 1000),
+                                   (1500, 256)])
 @pytest.mark.parametrize("wdt", ['same', 'f32'])
 def test_layernorm(dt, shape, wdt):
     x = torch.randn(*shape, device=DEV, dtype=dt, requires_grad=True)
@@ -420,7 +421,7 @@ def _drop_norm_call(x, xb, res, w, b, p, seed, off, rms=False):
 
 
 @pytest.mark.parametrize("rms", [False, True])
-@pytest.mark.parametrize("shape", [(512, 2048), (65, 4096), (9, 8192)])
+@pytest.mark.parametrize("shape", [(512, 2048), (65, 4096), (9, 8192), (4096, 768), (700, 1024), (37, 512)])
 def test_dropout_add_norm_fwd_bwd(rms, shape):
     N = _native
     rows, cols = shape
