@@ -305,10 +305,18 @@ class StaticCollectiveOptimizer:
             grp = hcg.get_pipe_parallel_group()
             st_id, S = hcg.get_stage_id(), hcg.get_pipe_parallel_world_size()
             ranks = list(grp.ranks)
+            mode = str(pc.get('schedule_mode', '1F1B'))
+            vpp = int(pc.get('vpp_degree', 1) or 1) if mode.upper() == 'VPP' else 1
+            grad_grp = None
+            if vpp > 1:  # interleaved stages: gradients on a communicator of their own
+                for rk in hcg.topology().get_comm_list('pipe'):  # collective: every rank, same order
+                    g = hcg._mk(rk)
+                    if hcg.global_rank in rk:
+                        grad_grp = g
             pol.pipeline = PipelineConfig(st_id, S, pc.get('accumulate_steps', 1), grp,
                                           ranks[st_id - 1] if st_id > 0 else None,
                                           ranks[st_id + 1] if st_id < S - 1 else None,
-                                          pc.get('schedule_mode', '1F1B'))
+                                          mode, vpp=vpp, grad_group=grad_grp)
         if pol.dp_group is not None:
             _broadcast_params(pol._params(), pol.dp_group)
         self._policy = pol

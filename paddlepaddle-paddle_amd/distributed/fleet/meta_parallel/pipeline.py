@@ -498,15 +498,8 @@ class PipelineParallelWithInterleave(PipelineParallel):
             return ([('F', v, m) for v in range(V) for m in range(n)] +
                     [('B', v, m) for v in reversed(range(V)) for m in range(n)])
         self.schedule = 'interleaved_1f1b'
-        total = n * V
-        fch = lambda k: (k % (P * V)) // P  # noqa: E731
-        mb = lambda k: (k // (P * V)) * P + k % P  # noqa: E731
-        warm = min(total, (P - r - 1) * 2 + (V - 1) * P)
-        seq = [('F', k) for k in range(warm)]
-        for i in range(total - warm):
-            seq += [('F', warm + i), ('B', i)]
-        seq += [('B', i) for i in range(total - warm, total)]
-        return [(kind, fch(k) if kind == 'F' else V - 1 - fch(k), mb(k)) for kind, k in seq]
+        from .zero_bubble_utils import interleaved_units
+        return interleaved_units(n, V, P, r)
 
     def train_batch(self, data, optimizer, lr_scheduler=None, scaler=None):
         inputs, labels = data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None)

@@ -161,6 +161,26 @@ def schedule_order(kind, S, s, M):
     return order
 
 
+def interleaved_units(n, V, P, r):
+    """Interleaved 1F1B (virtual pipeline stages) order of rank r of P over n micro-batches and V
+    chunks per rank: [('F' | 'B', chunk, micro-batch)] — warm-up 2(P-r-1) + (V-1)P forward units,
+    then one forward / one backward unit, then the cool-down; unit k is micro-batch
+    (k // PV) P + k % P through chunk (k % PV) // P (reversed for backward).  Needs n % P == 0; else
+    the breadth-first order (every micro-batch through chunk 0, then chunk 1, ...)."""
+    if V == 1 or n % P != 0:
+        return ([('F', v, m) for v in range(V) for m in range(n)] +
+                [('B', v, m) for v in reversed(range(V)) for m in range(n)])
+    total = n * V
+    fch = lambda k: (k % (P * V)) // P  # noqa: E731
+    mb = lambda k: (k // (P * V)) * P + k % P  # noqa: E731
+    warm = min(total, (P - r - 1) * 2 + (V - 1) * P)
+    seq = [('F', k) for k in range(warm)]
+    for i in range(total - warm):
+        seq += [('F', warm + i), ('B', i)]
+    seq += [('B', i) for i in range(total - warm, total)]
+    return [(kind, fch(k) if kind == 'F' else V - 1 - fch(k), mb(k)) for kind, k in seq]
+
+
 def simulate(kind, S, M, f=1.0, b=1.0, w=1.0):
     """Play every stage's schedule_order against the others: returns (makespan, bubble fraction).
     F(s, i) waits for F(s-1, i); B(s, i) for B(s+1, i); W(s, i) for B(s, i); a stage runs its ops

@@ -29,10 +29,17 @@ _DT = [torch.float32, torch.float16, torch.bfloat16, torch.int64, torch.int32, t
 
 
 class PipelineConfig:
-    def __init__(self, stage, nstages, acc, group, prev_rank, next_rank, schedule='1F1B'):
+    """One rank's view of a static pipeline.  ``vpp`` > 1 (schedule 'VPP'): the program's
+    device_guard stages are S * vpp chunks, chunk c on pipe rank c % S, run in the interleaved
+    1F1B order; gradients then travel on ``grad_group`` (a second communicator over the same
+    ranks), so every (src, dst) channel carries one kind of message in one order."""
+
+    def __init__(self, stage, nstages, acc, group, prev_rank, next_rank, schedule='1F1B', vpp=1, grad_group=None):
         self.stage, self.nstages, self.acc = stage, nstages, max(1, int(acc))
         self.group, self.prev, self.next = group, prev_rank, next_rank
         self.schedule = schedule
+        self.vpp = max(1, int(vpp or 1))
+        self.grad_group = grad_group
 
 
 def _stages(nodes, nstages):
@@ -109,7 +116,7 @@ def _plan(prog, nstages):
     return p[1]
 
 
-def _send(t, dst, dev, works):
+def _send(t, dst, dev, works, group=None):
     """Non-blocking send (header, then data): receives are blocking and issued in program order,
     sends never wait, so the 1F1B steady state (a stage sending activations forward while its
     successor sends gradients back) cannot deadlock.  ``works`` keeps buffers alive until waited."""
@@ -119,16 +126,16 @@ def _send(t, dst, dev, works):
     for i, s in enumerate(t.shape):
         hdr[2 + i] = s
     hdr = hdr.to(dev)
-    works.append((dist.isend(hdr, dst), hdr))
-    works.append((dist.isend(t, dst), t))
+    works.append((dist.isend(hdr, dst, group=group), hdr))
+    works.append((dist.isend(t, dst, group=group), t))
 
 
-def _recv(src, dev):
+def _recv(src, dev, group=None):
     hdr = torch.zeros(10, dtype=torch.int64, device=dev)
-    dist.recv(hdr, src)
+    dist.recv(hdr, src, group=group)
     nd, dt = int(hdr[0]), _DT[int(hdr[1])]
     t = torch.empty([int(x) for x in hdr[2:2 + nd]], dtype=dt, device=dev)
-    dist.recv(t, src)
+    dist.recv(t, src, group=group)
     return t
 
 
@@ -161,9 +168,75 @@ def _found_inf_sync(pol, cfg, dev):
     return sync
 
 
+def _run_vpp(prog, feed, dev, pol, cfg, run_forward, comm_dev, works):
+    """Interleaved (virtual-stage) pipeline step: this rank runs chunks s, s + S, ... of the
+    S * V device_guard stages (reference passes/pipeline_scheduler_pass/pipeline_vpp.py)."""
+    from ..distributed.fleet.meta_parallel.zero_bubble_utils import interleaved_units
+    s, S, V, acc = cfg.stage, cfg.nstages, cfg.vpp, cfg.acc
+    C = S * V
+    plan = _plan(prog, C)
+    ranks = list(cfg.group.ranks)
+    prev, nxt = ranks[(s - 1) % S], ranks[(s + 1) % S]
+    apg = getattr(cfg.group, 'pg', None)
+    gpg = getattr(cfg.grad_group, 'pg', None)
+    feeds = _split_feed(prog, feed, acc)
+    state, losses = {}, []
+    amp = pol._amp()
+    merge = pol.k_steps if pol.k_steps > 1 else 1
+    div = float(acc * (merge if pol.avg else 1))
+    for kind, v, m in interleaved_units(acc, V, S, s):
+        c = v * S + s
+        if kind == 'F':
+            env, rv = {}, {}
+            if c > 0:
+                for vid in plan.cross[c]:
+                    t = _recv(prev, comm_dev, apg).to(dev if dev is not None else comm_dev)
+                    if t.is_floating_point():
+                        t.requires_grad_(True)
+                    env[vid] = t
+                    rv[vid] = t
+            run_forward(plan.nodes[c], env, feeds[m])
+            sv = {}
+            if c < C - 1:
+                for vid in plan.cross[c + 1]:
+                    _send(env[vid], nxt, comm_dev, works, apg)
+                    sv[vid] = env[vid]
+            state[(v, m)] = (env, rv, sv)
+        else:
+            env, rv, sv = state.pop((v, m))
+            if c == C - 1:
+                loss = env[plan.loss_vid]
+                losses.append(loss.detach().float().reshape(-1)[0])
+                if amp is not None:
+                    amp._scaled_backward(loss, div)
+                else:
+                    (loss / div).backward()
+            else:
+                ts, gs = [], []
+                for vid in plan.cross[c + 1]:
+                    g = _recv(nxt, comm_dev, gpg)
+                    t = sv[vid]
+                    if t.requires_grad and t.is_floating_point():
+                        ts.append(t)
+                        gs.append(g.to(t.device, t.dtype))
+                if ts:
+                    torch.autograd.backward(ts, gs)
+            if c > 0:
+                for vid in plan.cross[c]:
+                    t = rv[vid]
+                    g = t.grad if (t.is_floating_point() and t.grad is not None) else torch.zeros_like(t)
+                    _send(g, prev, comm_dev, works, gpg)
+    return losses, plan
+
+
 def run_pipeline(prog, feed, dev, pol, cfg, run_forward):
     """Execute one pipelined training step of ``prog`` on this rank's stage.  ``run_forward(nodes,
     env, feed)`` binds the feeds into ``env`` and interprets ``nodes`` (executor internals)."""
+    if cfg.vpp > 1:
+        comm_dev = dev if (dev is not None and torch.device(dev).type == 'cuda') else torch.device('cpu')
+        works = []
+        losses, plan = _run_vpp(prog, feed, dev, pol, cfg, run_forward, comm_dev, works)
+        return _finish_step(pol, cfg, comm_dev, works, losses, plan)
     plan = _plan(prog, cfg.nstages)
     s, S, acc = cfg.stage, cfg.nstages, cfg.acc
     comm_dev = dev if (dev is not None and torch.device(dev).type == 'cuda') else torch.device('cpu')
@@ -265,6 +338,15 @@ def run_pipeline(prog, feed, dev, pol, cfg, run_forward):
         while b < acc:
             backward(b)
             b += 1
+    return _finish_step(pol, cfg, comm_dev, works, losses, plan)
+
+
+def _finish_step(pol, cfg, comm_dev, works, losses, plan):
+    """Wait for the sends, run the update (every k-th run under gradient merge) and broadcast the
+    mean micro-batch loss of the pipe's last stage to every stage."""
+    amp = pol._amp()
+    merge = pol.k_steps if pol.k_steps > 1 else 1
+    S = cfg.nstages
     for w, _ in works:
         w.wait()
     # the update (every k-th run under gradient merge): data-parallel reduction, then the AMP

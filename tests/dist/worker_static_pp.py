@@ -1,7 +1,8 @@
 """Static Program pipeline parallelism over gloo ranks (reference: fleet static pipeline optimizer;
 ops placed with static.device_guard('gpu:N'), pipeline_configs accumulate_steps micro-batches).
 argv[1]: schedule ('1F1B' / 'FThenB' / 'ZBH1': zero bubble, weight gradients deferred behind the
-input-gradient sends); argv[2]: 'pp' (pp = world), 'ppdp' (pp 2 x dp 2), 'ppamp'
+input-gradient sends / 'VPP': 2 virtual stages per rank, a chain of 2 * pp device_guard stages run in
+the interleaved 1F1B order); argv[2]: 'pp' (pp = world), 'ppdp' (pp 2 x dp 2), 'ppamp'
 (pp = world + static AMP fp16 with dynamic loss scaling whose first step overflows: every stage must
 skip it together) or 'ppgm' (pp = world + gradient merge k_steps 2: one update per two runs).
 Every rank builds the same program (same seed); after 3 steps each stage's parameters must equal a
@@ -37,6 +38,25 @@ def build(stages, opt_fn):
     return main, startup, loss
 
 
+def build_chain(C, opt_fn):
+    """C device_guard stages, one fc each (the last one the head): the VPP layout."""
+    paddle.seed(11)
+    main, startup = static.Program(), static.Program()
+    with static.program_guard(main, startup):
+        x = static.data('x', [None, 6], 'float32')
+        y = static.data('y', [None, 1], 'int64')
+        h = x
+        for c in range(C):
+            with static.device_guard(f'gpu:{c}'):
+                if c < C - 1:
+                    h = static.nn.fc(h, 8, activation='tanh')
+                else:
+                    logits = static.nn.fc(h, 3)
+                    loss = paddle.nn.functional.cross_entropy(logits, y)
+        opt_fn().minimize(loss)
+    return main, startup, loss
+
+
 def main():
     sched, mode = sys.argv[1], sys.argv[2]
     world = int(os.environ['WORLD_SIZE'])
@@ -55,13 +75,17 @@ def main():
     s.hybrid_configs = {'dp_degree': dp, 'mp_degree': 1, 'pp_degree': pp}
     s.pipeline = True
     s.pipeline_configs = {'accumulate_steps': acc, 'micro_batch_size': 2, 'schedule_mode': sched}
+    V = 2 if sched == 'VPP' else 1
+    if V > 1:
+        s.pipeline_configs['vpp_degree'] = V
+    builder = (lambda stages, fn: build_chain(stages * V, fn)) if V > 1 else build
     fleet.init(is_collective=True, strategy=s)
     hcg = fleet.get_hybrid_communicate_group()
     rank = dist.get_rank()
     dp_rank = hcg.get_data_parallel_rank()
     paddle.enable_static()
     sgd = lambda: paddle.optimizer.SGD(learning_rate=0.2)  # noqa: E731
-    main_p, startup, loss = build(pp, lambda: fleet.distributed_optimizer(sgd()))
+    main_p, startup, loss = builder(pp, lambda: fleet.distributed_optimizer(sgd()))
     exe = static.Executor(paddle.CPUPlace())
     exe.run(startup)
     rng = np.random.RandomState(0)
@@ -85,7 +109,7 @@ def main():
         ref_opt = lambda: samp.decorate(sgd(), level='O1', dtype='float16', **amp_cfg)  # noqa: E731
     else:
         ref_opt = sgd
-    ref_main, ref_startup, ref_loss = build(pp, ref_opt)
+    ref_main, ref_startup, ref_loss = builder(pp, ref_opt)
     ref_losses = []
     if mode == 'ppgm':  # the merged step == one full-batch step over both runs' samples
         batches = [(np.concatenate([batches[i][0], batches[i + 1][0]]),
@@ -97,6 +121,8 @@ def main():
     # parameters in creation order: fc(x) w,b and skip w,b on stage 0, the middle fc on stage
     # min(1, pp-1), the head on the last stage; a rank owns (updates) its stage's parameters only
     st = [0, 0, 0, 0, min(1, pp - 1), min(1, pp - 1), pp - 1, pp - 1]
+    if V > 1:  # chunk c of the chain lives on pipe rank c % pp
+        st = [c % pp for c in range(pp * V) for _ in range(2)]
     me = hcg.get_stage_id()
     ref = [p.numpy() for p in ref_main.all_parameters()]
     assert len(got) == len(st) == len(ref), (len(got), len(ref))

@@ -336,7 +336,8 @@ def test_static_fleet_tensor_parallel(mode, nproc):
 
 @pytest.mark.parametrize("sched,mode,nproc", [('1F1B', 'pp', 2), ('FThenB', 'pp', 2), ('1F1B', 'pp', 3),
                                               ('1F1B', 'ppdp', 4), ('1F1B', 'ppamp', 2), ('FThenB', 'ppgm', 2),
-                                              ('ZBH1', 'pp', 2), ('ZBH1', 'pp', 3), ('ZBH1', 'ppdp', 4)])
+                                              ('ZBH1', 'pp', 2), ('ZBH1', 'pp', 3), ('ZBH1', 'ppdp', 4),
+                                              ('VPP', 'pp', 2), ('VPP', 'pp', 4), ('VPP', 'ppdp', 4)])
 def test_static_fleet_pipeline_parallel(sched, mode, nproc):
     """Static-mode fleet pipeline: device_guard stages, micro-batched FThenB / 1F1B with
     send/recv of activations and gradients; every stage's parameters match a single-process run."""
