@@ -45,7 +45,8 @@ from .program import Node, Ref, Const
 
 # (CSE runs after the fusions: merging two equal subgraphs first would make them shared, and a
 # fusion claims only private chains)
-DEFAULT_PASSES = ('constant_folding_pass', 'conv2d_bn_fuse_pass',
+DEFAULT_PASSES = ('constant_folding_pass', 'identity_op_clean_pass', 'remove_redundant_transpose_pass',
+                  'matmul_scale_fuse_pass', 'rms_norm_fuse_pass', 'silu_fuse_pass', 'conv2d_bn_fuse_pass',
                   'conv2d_add_act_fuse_pass', 'fused_bn_add_act_pass', 'embedding_eltwise_layernorm_fuse_pass',
                   'quant_linear_fuse_pass', 'multihead_matmul_fuse_pass_v2', 'fused_dropout_add_layernorm', 'skip_layernorm_fuse_pass',
                   'fuse_gemm_epilogue_pass', 'layer_norm_fuse_pass', 'fc_fuse_pass', 'softmax_fuse_pass',

@@ -576,6 +576,232 @@ def inplace_pass(prog, nodes):
     return out, cnt
 
 
+# ------------------------------------------------------------------ round-6 general passes
+def _ref1(n, k=0):
+    a = n.args[k] if len(n.args) > k else None
+    return a if isinstance(a, Ref) else None
+
+
+def _scalar(v):
+    return isinstance(v, (int, float)) and not isinstance(v, bool)
+
+
+def rms_norm_static(x, weight, eps=1e-6):
+    """x * rsqrt(mean(x^2, -1) + eps) * weight — csrc/norm.hip on the GPU, the composite elsewhere."""
+    from . import ir_passes as _ip
+    if _ip._hip(x) and weight is not None and weight.dim() == 1 and weight.numel() == x.shape[-1] and \
+            x.dtype in (torch.bfloat16, torch.float16, torch.float32) and x.shape[-1] % 8 == 0 and weight.is_cuda:
+        from ..ops import norm
+        return norm.rms_norm(x, weight, float(eps))
+    xf = x.float()
+    y = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)).to(x.dtype)
+    return y * weight if weight is not None else y
+
+
+def _rms_norm(g, i):
+    """pow(x, 2) -> mean(-1, keepdim) -> + eps -> rsqrt -> x * r (-> cast) -> * weight: the composite
+    RMSNorm a recorded program holds (reference pir/transforms/gpu/rms_norm_fuse_pass.cc)."""
+    n = g.nodes[i]
+    if n.kind != 'torch' or _name(n) not in ('mul', '__mul__', 'multiply') or len(n.args) != 2 or n.kwargs:
+        return None
+    a, b = n.args
+    w, y = (b, a) if isinstance(b, Const) else ((a, b) if isinstance(a, Const) else (None, None))
+    if not isinstance(y, Ref) or w is None:
+        return None
+    tw = _const_t(g, w)
+    if tw is None or tw.dim() != 1:
+        return None
+    body = [i]
+    j = g.producer(y.vid, i)
+    m = g.node(j)
+    if m is not None and _name(m) == 'to' and _ref1(m) is not None and IP._one_out(m) == _ref1(m).vid:
+        j2 = g.producer(y.vid, j)  # the recorder's same-value cast: the product comes from before it
+        body.append(j)
+        j, m = j2, g.node(j2)
+    if m is None or _name(m) not in ('mul', '__mul__', 'multiply') or len(m.args) != 2:
+        return None
+    body.append(j)
+    x, r = m.args
+    if not (isinstance(x, Ref) and isinstance(r, Ref)):
+        return None
+    for xx, rr in ((x, r), (r, x)):
+        k = g.producer(rr.vid, j)
+        rs = g.node(k)
+        if rs is None or _name(rs) != 'rsqrt' or _ref1(rs) is None:
+            continue
+        k2 = g.producer(_ref1(rs).vid, k)
+        ad = g.node(k2)
+        if ad is None or _name(ad) not in ('add', '__add__') or len(ad.args) != 2 or not _scalar(ad.args[1]) or \
+                _ref1(ad) is None:
+            continue
+        eps = float(ad.args[1])
+        k3 = g.producer(_ref1(ad).vid, k2)
+        mn = g.node(k3)
+        if mn is None or _name(mn) != 'mean' or _ref1(mn) is None:
+            continue
+        dims = mn.args[1] if len(mn.args) > 1 else mn.kwargs.get('dim')
+        if dims not in (-1, [-1], (-1,)) or not (mn.kwargs.get('keepdim') or (len(mn.args) > 2 and mn.args[2])):
+            continue
+        k4 = g.producer(_ref1(mn).vid, k3)
+        pw = g.node(k4)
+        if pw is None or _name(pw) not in ('pow', '__pow__') or _ref1(pw) is None or _ref1(pw).vid != xx.vid or \
+                len(pw.args) < 2 or pw.args[1] != 2:
+            continue
+        chain = body + [k, k2, k3, k4]
+        if not g.private(chain[1:], users=[i]):
+            return None
+        node = Node('torch', rms_norm_static, [xx, w], {'eps': eps}, n.outs, dict(n.meta or {}, fused='rms_norm_fuse_pass'))
+        return chain, {i: node}
+    return None
+
+
+def _silu(g, i):
+    """x * sigmoid(x) -> silu(x) (reference silu_fuse_pass)."""
+    n = g.nodes[i]
+    if n.kind != 'torch' or _name(n) not in ('mul', '__mul__', 'multiply') or len(n.args) != 2 or n.kwargs:
+        return None
+    a, b = n.args
+    if not (isinstance(a, Ref) and isinstance(b, Ref)):
+        return None
+    for x, s_ in ((a, b), (b, a)):
+        j = g.producer(s_.vid, i)
+        m = g.node(j)
+        if m is not None and _name(m) == 'sigmoid' and _ref1(m) is not None and _ref1(m).vid == x.vid and \
+                len(m.args) == 1 and not m.kwargs and g.private([j], users=[i]):
+            return [j, i], {i: Node('torch', TF.silu, [x], {}, n.outs, dict(n.meta or {}, fused='silu_fuse_pass'))}
+    return None
+
+
+def _perm_of(n):
+    if _name(n) == 'permute':
+        p = n.args[1:] if len(n.args) > 2 else (n.args[1] if len(n.args) > 1 else n.kwargs.get('dims'))
+        return tuple(p) if isinstance(p, (list, tuple)) and all(isinstance(v, int) for v in p) else None
+    return None
+
+
+def identity_static(x):
+    return x
+
+
+def _transpose_pair(g, i):
+    """permute(permute(x, p1), p2) -> one permute (or x itself) (reference
+    remove_redundant_transpose_pass)."""
+    n = g.nodes[i]
+    if n.kind != 'torch':
+        return None
+    p2 = _perm_of(n)
+    x = _ref1(n)
+    if p2 is None or x is None:
+        return None
+    j = g.producer(x.vid, i)
+    m = g.node(j)
+    p1 = _perm_of(m) if m is not None and m.kind == 'torch' else None
+    if p1 is None or len(p1) != len(p2) or _ref1(m) is None or not g.private([j], users=[i]):
+        return None
+    comp = tuple(p1[k] for k in p2)
+    src = _ref1(m)
+    if comp == tuple(range(len(comp))):
+        node = Node('torch', identity_static, [src], {}, n.outs, dict(n.meta or {}, fused='remove_redundant_transpose_pass'))
+    else:
+        node = Node('torch', torch.permute, [src, list(comp)], {}, n.outs,
+                    dict(n.meta or {}, fused='remove_redundant_transpose_pass'))
+    return [j, i], {i: node}
+
+
+def _matmul_scale(g, i):
+    """Inference: (x @ W [+ b]) * c with a constant W -> x @ (c W) [+ c b] (reference
+    matmul_scale_fuse_pass)."""
+    n = g.nodes[i]
+    if _training(g.prog) or n.kind != 'torch' or _name(n) not in ('mul', '__mul__', 'multiply') or \
+            len(n.args) != 2 or n.kwargs:
+        return None
+    a, c = n.args
+    if not (isinstance(a, Ref) and _scalar(c)):
+        return None
+    j = g.producer(a.vid, i)
+    m = g.node(j)
+    if m is None or m.kind != 'torch' or m.kwargs or not g.private([j], users=[i]):
+        return None
+    nm = _name(m)
+    if nm == 'addmm' and len(m.args) == 3 and isinstance(m.args[2], Const) and isinstance(m.args[0], Const):
+        tb, tw = _const_t(g, m.args[0]), _const_t(g, m.args[2])
+        if tb is None or tw is None:
+            return None
+        with torch.no_grad():
+            args = [_new_const(g, (tb * c).to(tb.dtype)), m.args[1], _new_const(g, (tw * c).to(tw.dtype))]
+        return [j, i], {i: Node('torch', torch.addmm, args, {}, n.outs, dict(n.meta or {}, fused='matmul_scale_fuse_pass'))}
+    if nm in ('mm', 'matmul') and len(m.args) == 2 and isinstance(m.args[1], Const):
+        tw = _const_t(g, m.args[1])
+        if tw is None:
+            return None
+        with torch.no_grad():
+            args = [m.args[0], _new_const(g, (tw * c).to(tw.dtype))]
+        return [j, i], {i: Node('torch', m.target, args, {}, n.outs, dict(n.meta or {}, fused='matmul_scale_fuse_pass'))}
+    return None
+
+
+def identity_op_clean(prog, nodes):
+    """Drop identity nodes — a cast to the value's own dtype, a reshape to its own shape, x * 1,
+    x + 0, x - 0, x / 1, dropout that is off, a same-order permute — renaming their outputs to
+    their inputs (reference general/identity_op_clean_pass.cc); returns (nodes, dropped count)."""
+    g = IP._Graph(prog, nodes)
+    rename, out, cnt = {}, [], 0
+
+    def rn(o):
+        if isinstance(o, Ref):
+            return Ref(rename.get(o.vid, o.vid))
+        if isinstance(o, tuple) and hasattr(o, '_fields'):
+            return type(o)(*[rn(x) for x in o])
+        if isinstance(o, (list, tuple)):
+            return type(o)(rn(x) for x in o)
+        if isinstance(o, dict):
+            return {k: rn(v) for k, v in o.items()}
+        if isinstance(o, slice):
+            return slice(rn(o.start), rn(o.stop), rn(o.step))
+        return o
+
+    for n in nodes:
+        if rename:
+            n = Node(n.kind, n.target, rn(n.args), rn(n.kwargs), n.outs, n.meta)
+        src = _identity_src(g, n)
+        outs = IP._outs_of(n.outs, [])
+        if src is not None and len(outs) == 1 and outs[0] not in g.external and outs[0] != src:
+            rename[outs[0]] = rename.get(src, src)
+            cnt += 1
+            continue
+        out.append(n)
+    return out, cnt
+
+
+def _identity_src(g, n):
+    if n.kind != 'torch' or not n.args or not isinstance(n.args[0], Ref):
+        return None
+    nm, x = _name(n), n.args[0].vid
+    mx = g.meta.get(x)
+    outs = IP._outs_of(n.outs, [])
+    mo = g.meta.get(outs[0]) if len(outs) == 1 else None
+    if mx is None or mo is None or tuple(mx.shape) != tuple(mo.shape) or mx.dtype != mo.dtype:
+        return None
+    if nm in ('to', 'type', 'type_as', 'float', 'reshape', 'view', 'flatten'):
+        return x  # (contiguous / clone / detach change layout, aliasing or autograd: kept)
+    if nm in ('mul', '__mul__', 'multiply', 'div', 'true_divide', '__truediv__') and len(n.args) == 2 and \
+            _scalar(n.args[1]) and n.args[1] == 1 and not n.kwargs:
+        return x
+    if nm in ('add', '__add__', 'sub', '__sub__', 'subtract') and len(n.args) == 2 and _scalar(n.args[1]) and \
+            n.args[1] == 0 and not n.kwargs:
+        return x
+    if nm == 'dropout':
+        p = n.args[1] if len(n.args) > 1 else n.kwargs.get('p', 0.5)
+        tr = n.args[2] if len(n.args) > 2 else n.kwargs.get('training', True)
+        if p == 0 or not tr:
+            return x
+    if nm == 'permute':
+        p = _perm_of(n)
+        if p is not None and p == tuple(range(len(p))):
+            return x
+    return None
+
+
 def _graph_pass(fn):
     """Adapt a whole-list rewrite (nodes -> nodes, count) to apply_passes' per-pass protocol."""
     fn._whole_list = True
@@ -593,4 +819,9 @@ def register():
         'dead_code_elimination_pass': _graph_pass(dead_code_elimination),
         'common_subexpression_elimination_pass': _graph_pass(common_subexpression_elimination),
         'inplace_pass': _graph_pass(inplace_pass),
+        'identity_op_clean_pass': _graph_pass(identity_op_clean),
+        'rms_norm_fuse_pass': _rms_norm,
+        'silu_fuse_pass': _silu,
+        'remove_redundant_transpose_pass': _transpose_pair,
+        'matmul_scale_fuse_pass': _matmul_scale,
     })

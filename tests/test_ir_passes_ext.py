@@ -259,3 +259,38 @@ def test_fused_bn_add_act_pass_training_matches_unfused():
             np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
     finally:
         paddle.disable_static()
+
+
+def test_round6_general_passes_rms_silu_transpose_scale_identity():
+    """rms_norm_fuse / silu_fuse / remove_redundant_transpose / matmul_scale_fuse /
+    identity_op_clean on a recorded inference program: each rewrites its pattern and the program
+    computes the same values."""
+    paddle.enable_static()
+    try:
+        main, startup = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, startup):
+            x = paddle.static.data('x', [4, 16], 'float32')
+            h = paddle.nn.RMSNorm(16)(x)                            # composite RMSNorm
+            h = h * paddle.nn.functional.sigmoid(h)                 # silu
+            h = paddle.transpose(paddle.transpose(h, [1, 0]), [1, 0])  # cancels
+            lin = paddle.nn.Linear(16, 8)
+            h = lin(h) * 0.5                                        # scale folded into W, b
+            h = paddle.cast(h, 'float32') * 1.0 + 0.0               # identities
+            out = h.sum(axis=-1)
+        exe = paddle.static.Executor()
+        xv = np.random.RandomState(1).randn(4, 16).astype('float32')
+        ref = exe.run(main, feed={'x': xv}, fetch_list=[out])[0]
+        passes = ['identity_op_clean_pass', 'remove_redundant_transpose_pass', 'matmul_scale_fuse_pass',
+                  'rms_norm_fuse_pass', 'silu_fuse_pass']
+        nodes, stats = IP.apply_passes(main, passes=passes, fetch=(main._val[id(out._t)],))
+        for p in passes:
+            assert stats.get(p, 0) >= 1, (p, stats)
+        main._ir_passes = passes
+        IP._MODE[0] = '1'
+        try:
+            got = exe.run(main, feed={'x': xv}, fetch_list=[out])[0]
+        finally:
+            IP._MODE[0] = 'auto'
+        np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
+    finally:
+        paddle.disable_static()
