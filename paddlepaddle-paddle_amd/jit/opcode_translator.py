@@ -66,7 +66,8 @@ _SUPPORTED = set(_BINARY) | set(_UNARY) | {
     'BUILD_SLICE', 'BUILD_STRING', 'FORMAT_VALUE', 'LIST_APPEND', 'SET_ADD', 'MAP_ADD', 'LIST_EXTEND',
     'SET_UPDATE', 'LIST_TO_TUPLE', 'DICT_MERGE', 'DICT_UPDATE', 'UNPACK_SEQUENCE', 'UNPACK_EX', 'GET_ITER',
     'FOR_ITER', 'JUMP_FORWARD', 'JUMP_ABSOLUTE', 'POP_JUMP_IF_FALSE', 'POP_JUMP_IF_TRUE', 'JUMP_IF_FALSE_OR_POP',
-    'JUMP_IF_TRUE_OR_POP', 'RETURN_VALUE', 'MAKE_FUNCTION', 'EXTENDED_ARG', 'GET_LEN',
+    'JUMP_IF_TRUE_OR_POP', 'RETURN_VALUE', 'MAKE_FUNCTION', 'EXTENDED_ARG', 'GET_LEN', 'IMPORT_NAME',
+    'IMPORT_FROM',
 }
 _NO_TRANSLATE_FLAGS = inspect.CO_GENERATOR | inspect.CO_COROUTINE | inspect.CO_ASYNC_GENERATOR | \
     inspect.CO_ITERABLE_COROUTINE
@@ -516,6 +517,16 @@ def _step(fr, ctx):
         st.pop()
     elif op == 'RETURN_VALUE':
         return ('return', st.pop())
+    elif op == 'IMPORT_NAME':  # function-level import (idempotent; the module is baked into a region)
+        mod = __import__(arg, fr.globals, None, st[-1], st[-2])
+        del st[-2:]
+        st.append(mod)
+    elif op == 'IMPORT_FROM':
+        try:
+            st.append(getattr(st[-1], arg))
+        except AttributeError:
+            import importlib
+            st.append(importlib.import_module(st[-1].__name__ + '.' + arg))
     elif op == 'MAKE_FUNCTION':
         flags = ins.arg
         qual, code = st[-1], st[-2]

@@ -13,6 +13,12 @@ _tables = {}
 
 
 def rope_tables(S, D, base=10000.0, device=None):
+    if device is not None and torch.device(device).type == 'meta':
+        # a static program is being recorded: the tables become recorded factory + math nodes of
+        # that program (replayed on its device), never a cache entry shared across programs
+        inv = 1.0 / (base ** (torch.arange(0, D, 2, dtype=torch.float64, device=device) / D))
+        ang = torch.arange(S, dtype=torch.float64, device=device)[:, None] * inv[None, :]
+        return ang.cos().float().contiguous(), ang.sin().float().contiguous()
     key = (S, D, base, str(device))
     t = _tables.get(key)
     if t is None:

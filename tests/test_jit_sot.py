@@ -252,3 +252,36 @@ def test_opcode_translator_input_gradients_and_closures():
     ref_x.stop_gradient = False
     (paddle.matmul(ref_x * 3, w)).sum().backward()
     _close(x.grad, ref_x.grad)
+
+
+@pytest.mark.parametrize("family", ['gpt', 'llama', 'ernie'])
+def test_opcode_translator_model_zoo_single_region(family):
+    """GPT / Llama / ERNIE forwards translate as ONE region each (no graph break: function-level
+    imports, comprehensions, the models' own helpers inlined), equal eager, and train (gradients
+    on every parameter); two translations in a row do not share recorded tensors (the RoPE tables
+    of a recording belong to its program)."""
+    from paddle.models import gpt, llama, ernie
+    paddle.seed(7)
+    rng = np.random.RandomState(7)
+    if family == 'gpt':
+        net = gpt.GPTForPretraining(gpt.gpt_config('gpt-tiny'))
+    elif family == 'llama':
+        net = llama.LlamaForCausalLM(llama.llama_config('llama-tiny'))
+    else:
+        net = ernie.ErnieForSequenceClassification(ernie.ernie_config('ernie-tiny'))
+    ids = paddle.to_tensor(rng.randint(0, 512, (2, 16)))
+    net.eval()
+    ref = net(ids)
+    ref = ref if isinstance(ref, paddle.Tensor) else ref[0]
+    for _ in range(2):
+        tr = OpcodeTranslator(net.forward)
+        before = ot_stats()
+        out = tr(ids)
+        out = out if isinstance(out, paddle.Tensor) else out[0]
+        after = ot_stats()
+        assert after['regions'] - before['regions'] == 1 and after['breaks'] == before['breaks']
+        _close(out, ref, 1e-5)
+    net.train()
+    out = tr(ids)
+    (out if isinstance(out, paddle.Tensor) else out[0]).mean().backward()
+    assert all(p.grad is not None for p in net.parameters())
