@@ -25,8 +25,11 @@ Model.  ``OpcodeTranslator(fn)(*args)`` interprets ``fn``'s bytecode (CPython 3.
   GEMM substitutions, IR fusion passes on the GPU, autograd kept) and rebuilds the end state from
   the region's template — the Python inside the region is not re-run; anything else re-translates.
 
-Functions with generators, exception handlers or ``with`` blocks run eagerly (no translation); a
-call into such a function from a region is a graph break.  Translation never changes results:
+``with`` blocks are entered and exited concretely (graph breaks at SETUP_WITH and at the block's
+end), so the region inside runs under the context (grad mode and AMP state are part of every
+region's guard); an exception closes the open blocks and propagates.  Functions with generators or
+try / except handlers run eagerly (no translation); a call into such a function from a region is a
+graph break.  Translation never changes results:
 whatever cannot be modelled runs as plain Python.
 """
 import builtins
@@ -67,7 +70,7 @@ _SUPPORTED = set(_BINARY) | set(_UNARY) | {
     'SET_UPDATE', 'LIST_TO_TUPLE', 'DICT_MERGE', 'DICT_UPDATE', 'UNPACK_SEQUENCE', 'UNPACK_EX', 'GET_ITER',
     'FOR_ITER', 'JUMP_FORWARD', 'JUMP_ABSOLUTE', 'POP_JUMP_IF_FALSE', 'POP_JUMP_IF_TRUE', 'JUMP_IF_FALSE_OR_POP',
     'JUMP_IF_TRUE_OR_POP', 'RETURN_VALUE', 'MAKE_FUNCTION', 'EXTENDED_ARG', 'GET_LEN', 'IMPORT_NAME',
-    'IMPORT_FROM',
+    'IMPORT_FROM', 'SETUP_WITH', 'POP_BLOCK', 'WITH_EXCEPT_START', 'RERAISE', 'POP_EXCEPT',
 }
 _NO_TRANSLATE_FLAGS = inspect.CO_GENERATOR | inspect.CO_COROUTINE | inspect.CO_ASYNC_GENERATOR | \
     inspect.CO_ITERABLE_COROUTINE
@@ -76,6 +79,7 @@ _VALUE_CALLS = {builtins.float, builtins.int, builtins.bool, builtins.complex, b
                 builtins.format, builtins.hash}
 _TENSOR_VALUE_METHODS = {'numpy', 'item', 'tolist', '__bool__', '__float__', '__int__', '__index__', '__array__',
                          '__repr__', '__str__', '__format__', 'cpu_numpy'}
+_CONTEXT_METHODS = {'__enter__', '__exit__'}  # context-manager entry / exit: run concretely
 _MUTATORS = {'append', 'extend', 'insert', 'pop', 'remove', 'clear', 'update', 'setdefault', 'add', 'discard',
              'popitem', 'sort', 'reverse', '__setitem__', '__delitem__', 'set_value', 'copy_', 'fill_'}
 _LIBS = ('paddle', 'torch', 'numpy', 'builtins', 'functools', 'typing', 'collections', 'math', 'operator',
@@ -96,6 +100,8 @@ class _Code:
         self.instrs = [i for i in dis.get_instructions(code)]
         self.index = {ins.offset: k for k, ins in enumerate(self.instrs)}
         self.ok = not (code.co_flags & _NO_TRANSLATE_FLAGS) and all(i.opname in _SUPPORTED for i in self.instrs)
+        # try / finally handlers are not modelled; a POP_BLOCK then only closes a `with` block
+        self.ok = self.ok and not any(i.opname == 'SETUP_FINALLY' for i in self.instrs)
 
     @classmethod
     def of(cls, code):
@@ -152,7 +158,7 @@ class _Frame:
             self.cells[name] = cell
         self.stack = []
         self.pc = 0
-        self.block_iters = {}
+        self.withs = []  # exit methods of the active `with` blocks (entered concretely)
 
 
 class _Ctx:
@@ -163,6 +169,9 @@ class _Ctx:
         self.keep = []           # objects whose ids are in `created` (ids stay unique)
         self.guards = []         # callables: True while the region's assumptions hold
         self.depth = 0
+        self.local_vals = {}     # start-state Python locals the region read: name -> value
+        self.assigned = set()    # top-frame locals the region stored before reading
+        self.top = None          # the region's own frame (locals guards apply to it only)
 
     def mark(self, obj):
         self.created.add(id(obj))
@@ -184,6 +193,8 @@ def _call(ctx, fn, args, kwargs):
     if fn in _VALUE_CALLS and sym:
         raise _Break('tensor value')
     name = getattr(fn, '__name__', '')
+    if name in _CONTEXT_METHODS:
+        raise _Break('context manager entry / exit')
     if _is_sym(self_obj) and name in _TENSOR_VALUE_METHODS:
         raise _Break('tensor value')
     if name in _MUTATORS and self_obj is not None and not isinstance(self_obj, types.ModuleType) and \
@@ -191,6 +202,11 @@ def _call(ctx, fn, args, kwargs):
         raise _Break('mutation of a pre-existing object')
     if fn is builtins.super and not args:
         raise _Break('zero-argument super')  # handled by the caller frame
+    if fn is not getattr:  # a library call may read a pre-existing container's elements
+        for a_ in list(args) + list(kwargs.values()):
+            _guard_contents(ctx, a_)
+        if self_obj is not None and not isinstance(self_obj, types.ModuleType) and name not in _MUTATORS:
+            _guard_contents(ctx, self_obj)
     # user Python: inlined instruction by instruction (its breaks become a break at this call)
     f, pre = fn, ()
     if isinstance(fn, types.MethodType) and isinstance(fn.__func__, types.FunctionType):
@@ -240,6 +256,8 @@ def _step(fr, ctx):
 
     if op in _BINARY:
         a, b = st[-2], st[-1]
+        if op == 'BINARY_SUBSCR':
+            _guard_contents(ctx, a)
         if ctx is not None and op == 'BINARY_SUBSCR' and not _is_sym(a) and not isinstance(a, (list, tuple, dict)) \
                 and not hasattr(a, '__getitem__'):
             raise _Break('subscript')
@@ -276,8 +294,13 @@ def _step(fr, ctx):
     elif op == 'LOAD_FAST':
         if arg not in fr.locals:
             raise UnboundLocalError(arg)
-        st.append(fr.locals[arg])
+        v = fr.locals[arg]
+        if ctx is not None and fr is ctx.top and arg not in ctx.assigned and isinstance(v, _SIMPLE):
+            ctx.local_vals.setdefault(arg, v)  # keyed by type only: the value it read is a guard
+        st.append(v)
     elif op == 'STORE_FAST':
+        if ctx is not None and fr is ctx.top:
+            ctx.assigned.add(arg)
         fr.locals[arg] = st.pop()
     elif op == 'DELETE_FAST':
         del fr.locals[arg]
@@ -386,6 +409,7 @@ def _step(fr, ctx):
     elif op == 'CONTAINS_OP':
         if ctx is not None and (_is_sym(st[-1]) or _is_sym(st[-2])):
             raise _Break('membership test on a tensor')
+        _guard_contents(ctx, st[-1])
         v = (st[-2] in st[-1]) != bool(ins.arg)
         del st[-2:]
         st.append(v)
@@ -465,6 +489,7 @@ def _step(fr, ctx):
         st[-1] = tuple(st[-1])
     elif op == 'UNPACK_SEQUENCE':
         seq = st[-1]
+        _guard_contents(ctx, seq)
         items = list(_call(ctx, list, (seq,), {})) if ctx is not None else list(seq)
         if len(items) != ins.arg:
             raise ValueError(f"expected {ins.arg} values to unpack, got {len(items)}")
@@ -479,6 +504,7 @@ def _step(fr, ctx):
         st.extend(reversed(vals))
     elif op == 'GET_ITER':
         obj = st[-1]
+        _guard_contents(ctx, obj)
         it = _call(ctx, iter, (obj,), {}) if ctx is not None else iter(obj)
         st[-1] = ctx.mark(it) if ctx is not None else it
     elif op == 'GET_LEN':
@@ -517,6 +543,21 @@ def _step(fr, ctx):
         st.pop()
     elif op == 'RETURN_VALUE':
         return ('return', st.pop())
+    elif op == 'SETUP_WITH':  # runs concretely: __enter__ is a side effect of the call
+        if ctx is not None:
+            raise _Break('with-block entry')
+        cm = st.pop()
+        exit_fn = type(cm).__exit__.__get__(cm)
+        res = type(cm).__enter__(cm)
+        st.append(exit_fn)
+        fr.withs.append(exit_fn)
+        st.append(res)
+    elif op == 'POP_BLOCK':  # closes a `with` block (its exit call follows); concrete
+        if ctx is not None:
+            raise _Break('with-block exit')
+        fr.withs.pop()
+    elif op in ('WITH_EXCEPT_START', 'RERAISE', 'POP_EXCEPT'):  # exception paths: never reached
+        raise RuntimeError(f'opcode translator: {op} outside an exception')
     elif op == 'IMPORT_NAME':  # function-level import (idempotent; the module is baked into a region)
         mod = __import__(arg, fr.globals, None, st[-1], st[-2])
         del st[-2:]
@@ -589,6 +630,10 @@ def _truth(ctx, c):
         raise _Break('truth value') from e
 
 
+def _same(a, b):
+    return type(a) is type(b) and a == b
+
+
 def _safe_eq(get, v):
     try:
         return get() == v
@@ -615,9 +660,14 @@ def _state_key(fr):
     """Hashable description of the frame state a region depends on: the structure of locals,
     stack and own cells; tensors by (shape, dtype, stop_gradient, device); Python values by
     value; other objects by identity (Layers with their training flags)."""
-    parts = [fr.pc]
+    from ..core import amp_dispatch as _disp
+    a = _disp.STATE
+    parts = [fr.pc, torch.is_grad_enabled(), (a.active, a.level, a.dtype, a.white, a.black, a.use_promote),
+             len(fr.withs)]
     for name in sorted(fr.locals):
-        parts.append((name, _vkey(fr.locals[name])))
+        v = fr.locals[name]
+        # Python scalars in locals by type: the values a region reads become its local guards
+        parts.append((name, ('V', type(v)) if isinstance(v, _SIMPLE) else _vkey(v)))
     parts.append(('|stack',) + tuple(_vkey(v) for v in fr.stack))
     for name in fr.own_cells:
         c = fr.cells[name]
@@ -628,6 +678,25 @@ def _state_key(fr):
     return tuple(parts)
 
 
+def _contents(v, depth=0):
+    """Full value key of a container (elements by value) for content guards."""
+    if isinstance(v, (list, tuple)) and depth < 6:
+        return (type(v).__name__,) + tuple(_contents(x, depth + 1) for x in v)
+    if isinstance(v, dict) and depth < 6:
+        return ('dict',) + tuple((k, _contents(x, depth + 1)) for k, x in v.items())
+    if isinstance(v, _SIMPLE):
+        return ('V', type(v), v)
+    return _vkey(v, depth)
+
+
+def _guard_contents(ctx, obj):
+    """A region read the elements of a pre-existing list / dict / set: it replays only while they
+    are the same."""
+    if ctx is not None and type(obj) in (list, dict, set) and ctx.outer(obj):
+        snap = _contents(list(obj) if type(obj) is set else obj)
+        ctx.guards.append(lambda o=obj, k=snap: _contents(list(o) if type(o) is set else o) == k)
+
+
 def _vkey(v, depth=0):
     if isinstance(v, Tensor):
         t = v._t
@@ -636,15 +705,28 @@ def _vkey(v, depth=0):
         return ('t', id(v))
     if isinstance(v, _SIMPLE):
         return ('V', type(v), v)
-    if depth < 4 and type(v) in (tuple, list):
-        return (type(v).__name__, id(v) if type(v) is list else None) + tuple(_vkey(x, depth + 1) for x in v)
+    # tuples by value; lists / dicts by shape only — their Python contents are guarded where a
+    # region reads them (_guard_contents), and a list a region passes through is handed back by slot
+    if depth < 4 and type(v) is tuple:
+        return ('tuple',) + tuple(_vkey(x, depth + 1) for x in v)
+    if depth < 4 and type(v) is list:
+        return ('list',) + tuple((k, _vkey(x, depth + 1)) for k, x in enumerate(v) if isinstance(x, Tensor))
     if depth < 4 and type(v) is dict:
-        return ('dict', id(v)) + tuple((k, _vkey(x, depth + 1)) for k, x in v.items() if isinstance(k, _SIMPLE))
+        return ('dict',) + tuple((k, _vkey(x, depth + 1) if isinstance(x, (Tensor, list, tuple, dict)) else
+                                  (('V', type(x)) if isinstance(x, _SIMPLE) else _vkey(x, depth + 1)))
+                                 for k, x in v.items() if isinstance(k, _SIMPLE))
     from ..nn.layer.layers import Layer
     if isinstance(v, Layer):
         return ('L', id(v), tuple(m.training for m in v.sublayers(include_self=True)))
     if v is _NOSELF:
         return ('noself',)
+    if isinstance(v, types.MethodType) and v.__name__ == '__exit__':  # an open `with` block's exit
+        return ('exit', type(v.__self__))
+    if isinstance(v, (types.MethodType, types.BuiltinMethodType)) and getattr(v, '__self__', None) is not None \
+            and not isinstance(v.__self__, types.ModuleType):  # a bound method: its object, its name
+        return ('M', id(v.__self__), v.__name__)
+    if hasattr(type(v), '__exit__') and hasattr(type(v), '__enter__'):  # a context manager object
+        return ('cm', type(v))
     return ('O', id(v))
 
 
@@ -705,11 +787,15 @@ class _Region:
         self.guards = []
         self.out_vids = ()
         self.reason = None
+        self.local_vals = {}
 
 
-def _template(v, prog, inputs, depth=0):
+def _template(v, prog, inputs, depth=0, origin=None):
     """End-state value -> template: ('in', k) an input tensor, ('out', vid) a recorded value,
+    ('slot', path) a start-state object handed through (the replaying call's own object),
     ('tup'/'list'/'dict', ...) containers (rebuilt per replay), ('c', v) a baked value."""
+    if origin is not None and not isinstance(v, _SIMPLE + (Tensor,)) and id(v) in origin:
+        return ('slot', origin[id(v)])
     if isinstance(v, Tensor):
         if id(v) in inputs:
             return ('in', inputs[id(v)])
@@ -720,26 +806,33 @@ def _template(v, prog, inputs, depth=0):
             return ('out', vid)
         return ('c', v)
     if depth < 6 and type(v) is tuple:
-        return ('tup', [_template(x, prog, inputs, depth + 1) for x in v])
+        return ('tup', [_template(x, prog, inputs, depth + 1, origin) for x in v])
     if depth < 6 and type(v) is list:
-        return ('list', [_template(x, prog, inputs, depth + 1) for x in v])
+        return ('list', [_template(x, prog, inputs, depth + 1, origin) for x in v])
     if depth < 6 and type(v) is dict:
-        return ('dict', [(k, _template(x, prog, inputs, depth + 1)) for k, x in v.items()])
+        return ('dict', [(k, _template(x, prog, inputs, depth + 1, origin)) for k, x in v.items()])
     return ('c', v)
 
 
-def _materialize(t, env, feeds):
+def _slot_value(start, path):
+    kind, key = path
+    return start[kind][key]
+
+
+def _materialize(t, env, feeds, start=None):
     kind = t[0]
+    if kind == 'slot':
+        return _slot_value(start, t[1])
     if kind == 'in':
         return feeds[t[1]]
     if kind == 'out':
         return _wrap(env[t[1]])
     if kind == 'tup':
-        return tuple(_materialize(x, env, feeds) for x in t[1])
+        return tuple(_materialize(x, env, feeds, start) for x in t[1])
     if kind == 'list':
-        return [_materialize(x, env, feeds) for x in t[1]]
+        return [_materialize(x, env, feeds, start) for x in t[1]]
     if kind == 'dict':
-        return {k: _materialize(x, env, feeds) for k, x in t[1]}
+        return {k: _materialize(x, env, feeds, start) for k, x in t[1]}
     return t[1]
 
 
@@ -772,6 +865,7 @@ def _translate(fr):
     sfr = _Frame.__new__(_Frame)
     sfr.__dict__.update(fr.__dict__)
     ctx = _Ctx()
+    ctx.top = sfr
     started = _recorder[0] is None
     if started:
         _start_recording()
@@ -798,6 +892,16 @@ def _translate(fr):
                     pass
                 cells[name] = c
             sfr.cells = cells
+            origin = {}
+            for n_, v_ in sfr.locals.items():
+                origin.setdefault(id(v_), ('L', n_))
+            for k_, v_ in enumerate(sfr.stack):
+                origin.setdefault(id(v_), ('S', k_))
+            for n_ in fr.own_cells:
+                try:
+                    origin.setdefault(id(cells[n_].cell_contents), ('C', n_))
+                except ValueError:
+                    pass
             start = sfr.pc
             while True:
                 pc0 = sfr.pc
@@ -809,18 +913,18 @@ def _translate(fr):
                     break
                 if r is not None:
                     reg.returned = True
-                    reg.tpl_ret = _template(r[1], prog, inputs)
+                    reg.tpl_ret = _template(r[1], prog, inputs, origin=origin)
                     break
             if not reg.returned and sfr.pc == start and not prog.nodes:
                 return None  # breaks at once: nothing to translate
             reg.end_pc = sfr.pc
             if not reg.returned:
-                reg.tpl_locals = {n: _template(v, prog, inputs) for n, v in sfr.locals.items()}
-                reg.tpl_stack = [_template(v, prog, inputs) for v in sfr.stack]
+                reg.tpl_locals = {n: _template(v, prog, inputs, origin=origin) for n, v in sfr.locals.items()}
+                reg.tpl_stack = [_template(v, prog, inputs, origin=origin) for v in sfr.stack]
                 reg.tpl_cells = {}
                 for name in fr.own_cells:
                     try:
-                        reg.tpl_cells[name] = _template(sfr.cells[name].cell_contents, prog, inputs)
+                        reg.tpl_cells[name] = _template(sfr.cells[name].cell_contents, prog, inputs, origin=origin)
                     except ValueError:
                         pass
     except _Break:
@@ -834,6 +938,7 @@ def _translate(fr):
         _out_vids(t, acc)
     reg.out_vids = tuple(sorted(acc))
     reg.prog, reg.feed_names, reg.guards = prog, names, ctx.guards
+    reg.local_vals = dict(ctx.local_vals)
     _STATS['regions'] += 1
     _STATS['recorded'] += 1 if prog.nodes else 0
     _STATS['nodes'] += len(prog.nodes)
@@ -860,12 +965,18 @@ def _run_region(fr, reg):
                           grad=torch.is_grad_enabled(), fetch=reg.out_vids)
     else:
         env = {}
+    start = {'L': dict(fr.locals), 'S': list(fr.stack), 'C': {}}
+    for name in fr.own_cells:
+        try:
+            start['C'][name] = fr.cells[name].cell_contents
+        except ValueError:
+            pass
     if reg.returned:
-        return ('return', _materialize(reg.tpl_ret, env, feeds))
-    fr.locals = {n: _materialize(t, env, feeds) for n, t in reg.tpl_locals.items()}
-    fr.stack = [_materialize(t, env, feeds) for t in reg.tpl_stack]
+        return ('return', _materialize(reg.tpl_ret, env, feeds, start))
+    fr.locals = {n: _materialize(t, env, feeds, start) for n, t in reg.tpl_locals.items()}
+    fr.stack = [_materialize(t, env, feeds, start) for t in reg.tpl_stack]
     for name, t in reg.tpl_cells.items():
-        fr.cells[name].cell_contents = _materialize(t, env, feeds)
+        fr.cells[name].cell_contents = _materialize(t, env, feeds, start)
     fr.pc = reg.end_pc
     return None
 
@@ -880,6 +991,7 @@ class OpcodeTranslator:
         self.fn = fn
         self.ok = isinstance(fn, types.FunctionType) and _Code.of(fn.__code__).ok
         self.cache = {}  # state key -> [regions]
+        self.neg = set()  # pcs whose instruction always breaks at once
 
     def __call__(self, *args, **kwargs):
         if not self.ok:
@@ -887,18 +999,32 @@ class OpcodeTranslator:
             return self.fn(*((self.self_obj,) + args if self.self_obj is not None else args), **kwargs)
         full = ((self.self_obj,) + args) if self.self_obj is not None else args
         fr = _Frame(self.fn, full, kwargs)
+        try:
+            return self._run(fr)
+        except BaseException as e:
+            # exceptions are not modelled inside the frame: close its open `with` blocks the way
+            # CPython's handler would (innermost first) and propagate
+            while fr.withs:
+                fr.withs.pop()(type(e), e, e.__traceback__)
+            raise
+
+    def _run(self, fr):
         while True:
-            key = _state_key(fr)
             reg = None
-            for r in self.cache.get(key, ()):
-                if all(g() for g in r.guards):
-                    reg = r
-                    _STATS['hits'] += 1
-                    break
-            if reg is None:
-                reg = _translate(fr)
-                if reg is not None:
-                    self.cache.setdefault(key, []).append(reg)
+            if fr.pc not in self.neg:
+                key = _state_key(fr)
+                for r in self.cache.get(key, ()):
+                    if all(_same(fr.locals.get(n, _MISSING), v) for n, v in r.local_vals.items()) and \
+                            all(g() for g in r.guards):
+                        reg = r
+                        _STATS['hits'] += 1
+                        break
+                if reg is None:
+                    reg = _translate(fr)
+                    if reg is not None:
+                        self.cache.setdefault(key, []).append(reg)
+                    else:
+                        self.neg.add(fr.pc)  # breaks at its first instruction: run it concretely
             if reg is not None:
                 res = _run_region(fr, reg)
                 if res is not None:

@@ -285,3 +285,77 @@ def test_opcode_translator_model_zoo_single_region(family):
     out = tr(ids)
     (out if isinstance(out, paddle.Tensor) else out[0]).mean().backward()
     assert all(p.grad is not None for p in net.parameters())
+
+
+@pytest.mark.gpu
+def test_sot_gpt_tiny_gpu_bf16_forward_and_train():
+    """GPT-tiny in bf16 on the GPU through the opcode translator: one region replayed by the
+    Executor (GEMM substitutions, IR fusion passes) equals eager within bf16 tolerance, and a
+    training call produces gradients for every parameter."""
+    from paddle.models import gpt
+    paddle.set_device('gpu')
+    try:
+        paddle.seed(8)
+        net = gpt.GPTForPretraining(gpt.gpt_config('gpt-tiny'))
+        net.to(dtype='bfloat16')
+        ids = paddle.to_tensor(np.random.RandomState(8).randint(0, 512, (4, 64)))
+        net.eval()
+        with paddle.no_grad():
+            ref = net(ids)
+            tr = OpcodeTranslator(net.forward)
+            out = tr(ids)
+            out = tr(ids)
+        ref = ref if isinstance(ref, paddle.Tensor) else ref[0]
+        out = out if isinstance(out, paddle.Tensor) else out[0]
+        r, o = ref._t.float(), out._t.float()
+        assert float((o - r).abs().max() / r.abs().max()) < 3e-2
+        net.train()
+        y = tr(ids)
+        (y if isinstance(y, paddle.Tensor) else y[0]).astype('float32').mean().backward()
+        assert all(p.grad is not None for p in net.parameters())
+    finally:
+        paddle.set_device('cpu')
+
+
+def test_opcode_translator_with_blocks_pass_through_and_cache():
+    """`with` blocks are entered / exited concretely around translated regions (grad mode and AMP
+    state guard the regions), objects the caller passed in are handed back (not copies), per-call
+    lists and context managers do not defeat the region cache, and an exception inside a block
+    closes it."""
+    paddle.seed(10)
+    lin = paddle.nn.Linear(4, 4)
+
+    def f(x, acc):
+        with paddle.no_grad():
+            y = lin(x) * 2
+        z = lin(x) + y
+        acc.append(float(z.sum()))   # break: the caller's own list
+        out = []
+        for i in range(2):
+            out.append(z * i)
+        return out, acc
+
+    tr = OpcodeTranslator(f)
+    x = paddle.randn([3, 4])
+    acc = []
+    before = None
+    for it in range(3):
+        out, a2 = tr(x, acc)
+        assert a2 is acc and len(acc) == it + 1
+        assert paddle.is_grad_enabled()
+        ref = lin(x) + lin(x).detach() * 2
+        _close(out[1], ref)
+        assert out[1].stop_gradient is False and out[0].stop_gradient is False
+        if it == 0:
+            before = ot_stats()['regions']
+    assert ot_stats()['regions'] == before  # calls 2 and 3 replayed every region
+
+    def g(x):
+        with paddle.no_grad():
+            y = x * 2
+            raise ValueError('boom')
+        return y
+    tg = OpcodeTranslator(g)
+    with pytest.raises(ValueError):
+        tg(x)
+    assert paddle.is_grad_enabled()
