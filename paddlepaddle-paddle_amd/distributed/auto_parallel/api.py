@@ -1041,6 +1041,25 @@ class DistModel:
     def set_state_dict(self, state_dict):
         self._layer.set_state_dict(state_dict)
 
+    # ---- the distributed programs (reference api.py:2010-2068 DistModel.dist_main_program /
+    # dist_startup_program). The program of a mode is recorded at its first call: the per-shard
+    # ops plus one node per reshard collective, every value tagged with its dist attribute
+    # (``Program.dist_attr``). Parameters are created already placed (shard_tensor /
+    # shard_layer), so the startup program holds no initializers.
+    def _prog_for(self, mode):
+        mode = mode or self._mode
+        progs = [p for (m, _), p in self._progs.items() if m == mode]
+        return progs[-1][0] if progs else None
+
+    def dist_main_program(self, mode=None):
+        """The recorded distributed Program of ``mode`` (default: the current one); None before
+        that mode has run a step."""
+        return self._prog_for(mode)
+
+    def dist_startup_program(self, mode=None):
+        from ... import static as _st
+        return _st.Program() if self._prog_for(mode) is not None else None
+
 
 def to_static(layer, loader=None, loss=None, optimizer=None, strategy=None, input_spec=None):
     return DistModel(layer, loader, loss, optimizer, strategy)

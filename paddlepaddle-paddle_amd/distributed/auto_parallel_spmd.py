@@ -266,7 +266,9 @@ def _apply(fn, t, *extra):
             out = torch.empty_like(m.chunk(extra[1], extra[3])[extra[2]], device='meta')
         else:
             out = m.clone()
-    return _unwrap(py_node(lambda x: _wrap(fn.apply(_unwrap(x), *extra)), [t], [out])[0])
+    run = lambda x: _wrap(fn.apply(_unwrap(x), *extra))  # noqa: E731
+    run._spmd_fn = fn  # Program.reshard_nodes
+    return _unwrap(py_node(run, [t], [out])[0])
 
 
 def _reshard_local(t, mesh, src, dst):

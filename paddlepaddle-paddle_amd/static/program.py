@@ -201,6 +201,28 @@ class Program:
     def to_string(self, throw_on_error=False, with_details=False):
         return repr(self)
 
+    def dist_attr(self, value):
+        """(process_mesh, placements, global_shape) of a value recorded under SPMD propagation
+        (DistModel programs), None for a value with no dist attribute. ``value``: a Ref, a value
+        id or a recorded Variable."""
+        if isinstance(value, Ref):
+            value = value.vid
+        if isinstance(value, int):
+            for t in self._keep:
+                if self._val.get(id(t)) == value:
+                    return getattr(t, '_pd_dist', None)
+            return None
+        t = getattr(value, '_t', value)
+        a = getattr(t, '_pd_dist', None)
+        if a is None and isinstance(t, torch.Tensor):
+            twin = self._meta_twins.get(self._const_ids.get(id(t)))
+            a = getattr(twin, '_pd_dist', None)
+        return a
+
+    def reshard_nodes(self):
+        """The collective nodes SPMD propagation inserted (all-gather / reduce-scatter / ...)."""
+        return [n for n in self.nodes if getattr(n.target, '_spmd_fn', None) is not None]
+
     # ---- recording helpers
     def _new_value(self, meta_t):
         vid = next(self._vid)

@@ -41,6 +41,13 @@ def main():
     # the reshards are program nodes: the row-parallel output's all-reduce and the replicated
     # activation's identity / gradient all-reduce feeding the column-parallel layer
     assert sum(1 for n in plan[0].nodes if n.kind == 'py') >= 2
+    prog = dm.dist_main_program()
+    assert prog is plan[0] and dm.dist_main_program('eval') is None
+    assert len(prog.reshard_nodes()) >= 2
+    assert len(dm.dist_startup_program().nodes) == 0
+    # the column-parallel weight keeps its dist attribute (global shape [6, 12], Shard(1))
+    mesh_, pl, gshape = prog.dist_attr(net[2].weight)
+    assert list(gshape) == [6, 12] and isinstance(pl[0], dist.Shard) and pl[0].get_dim() == 1, (pl, gshape)
 
     ropt = paddle.optimizer.SGD(0.2, parameters=ref.parameters())
     rl = []
