@@ -271,9 +271,11 @@ __global__ __launch_bounds__(256) void adamw_scalar_kernel(float* __restrict__ p
 }
 
 // Memory-bound (28 B/param read+write for bf16 grads/params with fp32 master/m/v): 8 params
-// per lane per iteration (every access a full 16-byte vector, the bf16 gradient included), two
-// independent iterations in flight per lane.
-template <typename G, typename P, bool NTS>
+// per lane (every access a full 16-byte vector, the bf16 gradient included).  ONE: one vector per
+// lane over a grid that covers the buffer (no loop): 6.0 TB/s on a 1.3B-parameter buffer vs 5.7
+// for a grid-stride loop with two vectors in flight per lane, and 4.8 with nontemporal loads
+// (tools/adamw_variants.hip, profiles/r6o_adamw_variants.log) — plain loads and stores.
+template <typename G, typename P, bool NTS, bool ONE = false>
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const G* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, P* __restrict__ lowp,
                                                     long long n, const float* __restrict__ lr_ptr, float lr_host,
@@ -292,13 +294,17 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   const float eps_hat = eps * bc2;
   constexpr int E = 8;
   const long long nv = n / E;
-  const long long stride = (long long)gridDim.x * 256;
   long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  for (; i + stride < nv; i += 2 * stride) {
-    adamw_vec8<G, P, NTS>(p, g, m, v, lowp, i * E, gs, decay, b1, b2, step, eps_hat);
-    adamw_vec8<G, P, NTS>(p, g, m, v, lowp, (i + stride) * E, gs, decay, b1, b2, step, eps_hat);
+  if constexpr (ONE) {
+    if (i < nv) adamw_vec8<G, P, NTS>(p, g, m, v, lowp, i * E, gs, decay, b1, b2, step, eps_hat);
+  } else {
+    const long long stride = (long long)gridDim.x * 256;
+    for (; i + stride < nv; i += 2 * stride) {
+      adamw_vec8<G, P, NTS>(p, g, m, v, lowp, i * E, gs, decay, b1, b2, step, eps_hat);
+      adamw_vec8<G, P, NTS>(p, g, m, v, lowp, (i + stride) * E, gs, decay, b1, b2, step, eps_hat);
+    }
+    if (i < nv) adamw_vec8<G, P, NTS>(p, g, m, v, lowp, i * E, gs, decay, b1, b2, step, eps_hat);
   }
-  if (i < nv) adamw_vec8<G, P, NTS>(p, g, m, v, lowp, i * E, gs, decay, b1, b2, step, eps_hat);
   if (blockIdx.x == 0) {
     for (long long k = nv * E + threadIdx.x; k < n; k += 256) {
       const float gg = to_f(g[k]) * gs;
@@ -453,23 +459,32 @@ PA_API hipError_t pa_rope_rows(const void* x, long long ldx, void* y, long long 
   return hipGetLastError();
 }
 
-// A/B knobs for the streaming update: nontemporal 16-byte accesses, and blocks per CU
-static int g_adamw_nt = 1, g_adamw_bpc = 8;
+// A/B knobs for the streaming update: nontemporal 16-byte accesses (off: they cost 15-20 % on
+// MI355X), and blocks per CU of the grid-stride form (0 = one vector per lane, the default)
+static int g_adamw_nt = 0, g_adamw_bpc = 0;
 PA_API void pa_adamw_tune(int nt, int blocks_per_cu) {
   g_adamw_nt = nt;
-  g_adamw_bpc = blocks_per_cu > 0 ? blocks_per_cu : 8;
+  g_adamw_bpc = blocks_per_cu > 0 ? blocks_per_cu : 0;
 }
 
 // gd = grad dtype, pd = low-precision param copy dtype (-1 = none)
 PA_API hipError_t pa_adamw(float* p, const void* g, float* m, float* v, void* lowp, long long n, const float* lr_ptr,
                            float lr, float b1, float b2, float eps, float wd, float b1pow, float b2pow,
                            const float* grad_scale, const float* pows, int gd, int pd, hipStream_t st) {
-  const int grid = grid_for(n / 16 + 1, 256, 256 * g_adamw_bpc);
+  const long long nvec = n / 8;
+  const bool one = g_adamw_bpc == 0 && nvec > 0 && (nvec + 255) / 256 < (1LL << 31);
+  const int grid = one ? (int)((nvec + 255) / 256) : grid_for(n / 16 + 1, 256, 256 * g_adamw_bpc);
   // every 8-element access is a 16-byte vector (or two): all five streams must be 16-byte aligned
   const bool aligned = ((((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g | (uintptr_t)lowp) & 15) == 0);
 #define PA_ADAM(G, P)                                                                                          \
   do {                                                                                                         \
-    if (aligned && g_adamw_nt)                                                                                 \
+    if (aligned && one && !g_adamw_nt)                                                                         \
+      adamw_kernel<G, P, false, true><<<grid, 256, 0, st>>>(p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1, \
+                                                            b2, eps, wd, b1pow, b2pow, grad_scale, pows);      \
+    else if (aligned && one)                                                                                   \
+      adamw_kernel<G, P, true, true><<<grid, 256, 0, st>>>(p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1,  \
+                                                           b2, eps, wd, b1pow, b2pow, grad_scale, pows);       \
+    else if (aligned && g_adamw_nt)                                                                            \
       adamw_kernel<G, P, true><<<grid, 256, 0, st>>>(p, (const G*)g, m, v, (P*)lowp, n, lr_ptr, lr, b1, b2, eps, \
                                                      wd, b1pow, b2pow, grad_scale, pows);                      \
     else if (aligned)                                                                                          \

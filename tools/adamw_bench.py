@@ -24,7 +24,7 @@ def main():
         optim.adamw_flat(master, g, m, v, low, 1e-4, 0.9, 0.95, 1e-8, 0.01, 0.9, 0.95)
 
     for nt in (0, 1):
-        for bpc in (4, 8, 16, 32):
+        for bpc in (0, 4, 8, 16):
             _native.lib.pa_adamw_tune(nt, bpc)
             for _ in range(2):
                 run()
@@ -36,8 +36,8 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             t = e0.elapsed_time(e1) / 1e3 / 5
-            print(f"nontemporal={nt} blocks/CU={bpc}: {t*1e6:8.1f} us  {28 * n / t / 1e12:5.2f} TB/s", flush=True)
-    _native.lib.pa_adamw_tune(1, 8)
+            print(f"nontemporal={nt} blocks/CU={bpc or 'one-shot'}: {t*1e6:8.1f} us  {28 * n / t / 1e12:5.2f} TB/s", flush=True)
+    _native.lib.pa_adamw_tune(0, 0)
 
 
 if __name__ == '__main__':
