@@ -164,11 +164,129 @@ __global__ __launch_bounds__(256, 2) void dq_from_ds_kernel(const uint16_t* __re
   }
 }
 
+// dQ from dS, head_dim 128, as a stream: the kernel above is HBM-latency bound (~2.5 TB/s of dS^T:
+// one tile staged ahead in registers, two barriers per key block).  Here the dS^T and K tiles of
+// NS key blocks live in an LDS ring filled by LDS-DMA (global_load_lds_dwordx4, no register
+// round trip): NS - 1 key blocks are in flight while one is multiplied, retired by a counted
+// vmcnt, one barrier per key block.  Same grid, fragments, masking and numerics as
+// dq_from_ds_kernel (the LDS images are the same swizzled [64][128] tiles).
+template <typename T, bool CAUSAL, int EXT, int NS>
+__global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void dq_from_ds_dma_kernel(const uint16_t* __restrict__ K,
+                                                                const uint16_t* __restrict__ dsT,
+                                                                uint16_t* __restrict__ dQ, int Sq_, int Sk_, int Hq,
+                                                                int Hk, Strides ks_, Strides dqs, long long dsb,
+                                                                long long dsh, int dsld, float scale, Extra ex) {
+  static_assert(NS >= 2 && NS <= 4, "ring depth 2..4 (counted waits below)");
+  constexpr int D = 128, NT = 2, NW = 4, QB = 16 * NT * NW;  // 128 queries per block
+  constexpr int DB = D / 16;
+  constexpr int TILE = 64 * D * 2;  // one [64][128] 16-bit tile: 16 KB
+  constexpr int VM = 2 * DmaTile<D, true>::NI;  // LDS-DMA instructions per wave per key block
+  __shared__ __attribute__((aligned(16))) char smem[NS * 2 * TILE];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int nqb = (Sq_ + QB - 1) / QB;
+  int h, b, zi;
+  pair_order(Hq, (int)gridDim.y, nqb, h, b, zi);
+  const int qb = nqb - 1 - zi;
+  const int hk = h / (Hq / Hk);
+  const Seq sq_ = seq_of<EXT != 0>(ex, b, h, Hq, Sq_, Sk_);
+  const int Sq = sq_.sq, Sk = sq_.sk;
+  const int q0 = qb * QB;
+  if (q0 >= Sq) return;  // block-uniform: no barrier below is skipped by part of the block
+  const int qw = q0 + wave * 16 * NT;
+  const int off = Sk - Sq;
+  const bool vl = EXT && ex.cu_q;
+  const uint16_t* kbase = K + (vl ? 0 : (long long)b * ks_.b) + sq_.ko * ks_.s + (long long)hk * ks_.h;
+  const uint16_t* dshead = dsT + (long long)b * dsb + (long long)h * dsh + (long long)qb * 8192;
+  const long long tstride = (long long)(dsld >> 7) * 8192;
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + QB + off);
+  const int nkb = kend > 0 ? (kend + 63) / 64 : 0;
+  f32x4 acc[NT][DB];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int d = 0; d < DB; ++d) acc[t][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  DmaTile<D, true> kd, sd;
+  kd.init(wave, lane);
+  sd.init(wave, lane);
+  auto issue = [&](int kb) {
+    char* slot = smem + (kb % NS) * 2 * TILE;
+    kd.issue(kbase, ks_.s, kb * 64, Sk, slot, wave);
+    sd.issue(dshead + kb * tstride, 128, 0, 64, slot + TILE, wave);  // every tile row exists
+  };
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < nkb) issue(i);
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * 64;
+    // key blocks issued beyond kb: min(NS - 2, nkb - 1 - kb); retire kb's pieces only
+    const int ahead = min(NS - 2, nkb - 1 - kb);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * VM) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // kb resident for every wave; every wave is done with kb - 1's slot
+    if (kb + NS - 1 < nkb) issue(kb + NS - 1);
+    if (CAUSAL && k0 > qw + 16 * NT - 1 + off) continue;  // whole key block above this wave's rows
+    const char* k_lds = smem + (kb % NS) * 2 * TILE;
+    const char* s_lds = k_lds + TILE;
+    s16x8 dsf[NT][2];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) dsf[t][s] = ld_tr8<128, true>(s_lds, 32 * s, (qw - q0) / 16 + t, lane);
+    const bool need_mask = (k0 + 64 > Sk) || (CAUSAL && k0 + 63 > qw + off);
+    if (need_mask) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int q = qw + 16 * t + (lane & 15);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int key = k0 + 32 * s + 4 * g + (e & 3) + (e >= 4 ? 16 : 0);
+            const bool masked = (key >= Sk) || (CAUSAL && key > q + off);
+            dsf[t][s][e] = masked ? (short)0 : dsf[t][s][e];
+          }
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const s16x8 ka = ld_tr8<D, true>(k_lds, 32 * s, d, lane);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t][d] = Mfma<T>::run(ka, dsf[t][s], acc[t][d]);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int myq = qw + 16 * t + (lane & 15);
+    if (myq < Sq) {
+      uint16_t* row = dQ + (vl ? 0 : (long long)b * dqs.b) + (long long)h * dqs.h + (sq_.qo + myq) * dqs.s;
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        s16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2s<T>(acc[t][d][r] * scale);
+        *reinterpret_cast<s16x4*>(row + 16 * d + 4 * g) = o;
+      }
+    }
+  }
+}
+
 }  // namespace fa
 }  // namespace pa
 
 using namespace pa;
 using namespace pa::fa;
+
+// A/B switch (pa_flash_ds_set_dq_dma): the LDS-DMA ring dQ kernel at head_dim 128 (0 = the
+// register-staged kernel); host-side, read at launch.  The kernel is bound by its LDS operand
+// reads (each K fragment feeds two MFMAs), not by the prefetch depth: see the measurements below.
+static int g_dq_dma = 2;
 
 #define FAD_DISPATCH(dt, D, causal, ...)                                                                          \
   if (dt == 1 && D == 128 && causal) { using T = bf16_t; constexpr int DD = 128; constexpr bool CC = true; __VA_ARGS__; }        \
@@ -210,8 +328,24 @@ static void bwd_ds(const void* q, const void* k, const void* v, const void* o, c
   bwd_dkdv_kernel<T, DD, CC, 1, NW, F, false, true><<<dim3(Hq, B, (Sk + 16 * NW - 1) / (16 * NW)), 64 * NW, 0, st>>>(
       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk,
       (uint16_t*)dv, Sq, Sk, Hq, Hk, qs, ks, vs, dos, dks, dvs, scale, ex, (uint16_t*)dsT, dsb, dsh, dsld);
-  dq_from_ds_kernel<T, DD, CC, F><<<dim3(Hq, B, (Sq + 127) / 128), 256, 0, st>>>(
-      (const uint16_t*)k, (const uint16_t*)dsT, (uint16_t*)dq, Sq, Sk, Hq, Hk, ks, dqs, dsb, dsh, dsld, scale, ex);
+  const dim3 qgrid(Hq, B, (Sq + 127) / 128);
+  if constexpr (DD == 128) {
+    if (g_dq_dma == 2) {
+      dq_from_ds_dma_kernel<T, CC, F, 2><<<qgrid, 256, 0, st>>>((const uint16_t*)k, (const uint16_t*)dsT, (uint16_t*)dq,
+                                                                Sq, Sk, Hq, Hk, ks, dqs, dsb, dsh, dsld, scale, ex);
+      return;
+    }
+  }
+  dq_from_ds_kernel<T, DD, CC, F><<<qgrid, 256, 0, st>>>((const uint16_t*)k, (const uint16_t*)dsT, (uint16_t*)dq, Sq,
+                                                           Sk, Hq, Hk, ks, dqs, dsb, dsh, dsld, scale, ex);
+}
+
+// A/B: 0 = register-staged dQ kernel, 2 = the LDS-DMA ring (GPT-3 1.3B shape: 109.6 vs 111.5 us;
+// ring depths 3 / 4 at one block per CU were 143 / 153 us, profiles/r6q_dq_from_ds_ring_ab.log)
+PA_API int pa_flash_ds_set_dq_dma(int v) {
+  const int old = g_dq_dma;
+  g_dq_dma = v;
+  return old;
 }
 
 // Same contract as pa_flash_bwd_ex (cu_q == null: dense; mask / dropout / flashmask rows optional)

@@ -128,6 +128,7 @@ _SIGS = {
     'pa_flash_ds_ld': [I],
     'pa_flash_ds_ws_elems': [I, I, I, I],
     'pa_flash_ds_set_pair_group': [I],
+    'pa_flash_ds_set_dq_dma': [I],
     'pa_flash_bwd_ds': [P] * 11 + [I] * 6 + [LLP] * 8 + [F, I, I, P, P, I, P, LL, LL, LL, I, F, U32, U32, P, LL, LL, P,
                                                          P],
     'pa_conv2d_wgrad_ok': [I, I],

@@ -166,3 +166,26 @@ def test_ds_workspace_survives_growth_after_capture(ds_on):
     for a, b, n in zip((q, k, v), ref, 'qkv'):
         _close(a.grad, b, 1e-2, name=f'replay d{n}')
     assert bool((keep == 7.0).all())
+
+
+@pytest.mark.parametrize('causal', [False, True])
+def test_ds_dq_dma_ring_bitwise(ds_on, causal):
+    """The LDS-DMA ring dQ kernel runs the register-staged kernel's MFMA chain
+    in the same order: bitwise-equal dQ, on a ragged cross-attention shape and under varlen-free
+    GQA strides."""
+    q, k, v = _leaf(2, 333, 8, 128), _leaf(2, 461, 2, 128), _leaf(2, 461, 2, 128)
+    g = torch.randn(2, 333, 8, 128, device=DEV, dtype=torch.bfloat16)
+    got = {}
+    old = _native.lib.pa_flash_ds_set_dq_dma(0)
+    try:
+        for mode in (0, 2):
+            _native.lib.pa_flash_ds_set_dq_dma(mode)
+            for t in (q, k, v):
+                t.grad = None
+            FA.flash_attention(q, k, v, causal).backward(g)
+            got[mode] = [t.grad.clone() for t in (q, k, v)]
+    finally:
+        _native.lib.pa_flash_ds_set_dq_dma(old)
+    for mode in (2,):
+        for a, b in zip(got[0], got[mode]):
+            assert torch.equal(a, b), (mode, (a.float() - b.float()).abs().max().item())

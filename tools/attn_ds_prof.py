@@ -16,6 +16,8 @@ def main():
     ops.flash_attn.set_ds_backward(sys.argv[1] == 'ds')
     if len(sys.argv) > 2:  # block-order group of the dS module (pair_order G)
         _native.lib.pa_flash_ds_set_pair_group(int(sys.argv[2]))
+    if os.environ.get('DQ_DMA') is not None:  # dQ-from-dS kernel: 0 register-staged, 3 / 4 LDS-DMA ring depth
+        _native.lib.pa_flash_ds_set_dq_dma(int(os.environ['DQ_DMA']))
     qkv = torch.randn(16, 1024, 3, 16, 128, device='cuda', dtype=torch.bfloat16, requires_grad=True)
     g = torch.randn(16, 1024, 16, 128, device='cuda', dtype=torch.bfloat16)
     for _ in range(12):
