@@ -226,7 +226,10 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void dq_from_ds_dma_kernel(co
     if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * VM) : "memory");
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // kb resident for every wave; every wave is done with kb - 1's slot
+    // raw barrier: __syncthreads() would drain every DMA in flight (its fence waits for vmcnt(0));
+    // the "memory" clobbers keep the compiler from moving LDS reads across it
+    __builtin_amdgcn_s_barrier();  // kb resident for every wave; every wave is done with kb - 1's slot
+    asm volatile("" ::: "memory");
     if (kb + NS - 1 < nkb) issue(kb + NS - 1);
     if (CAUSAL && k0 > qw + 16 * NT - 1 + off) continue;  // whole key block above this wave's rows
     const char* k_lds = smem + (kb % NS) * 2 * TILE;
