@@ -65,6 +65,25 @@ int rows_per_block(int rows, int colblocks, int target = 2048) {
   return (int)rpb;
 }
 
+// Row order of the streaming passes (host knob pa_bn_set_interleave): 1 = row groups of
+// U x (rows per pass) dealt round-robin over the blocks (so the blocks in flight at any moment
+// stream one contiguous window of the tensor), 0 = one contiguous chunk of rows per block.  The
+// round-robin order streams faster on MI355X (fused AdamW: 5.7 TB/s grid-stride vs 4.8-5.0 with
+// contiguous per-block chunks, profiles/r6o_adamw_variants.log; ResNet50 step 29.53 vs 30.00 ms,
+// profiles/r6t_bn_row_order_ab.log).  The mean/M2 statistics pass keeps contiguous slabs (its
+// merge needs each partial's row range).
+static int kInterleave = 1;
+inline dim3 apply_grid(int rows, int cols, int E, dim3 chunk_grid) {
+  if (!kInterleave) return chunk_grid;
+  const int cpt = cols / E;
+  const int rpi = cpt >= 256 ? 1 : 256 / cpt;
+  const long long groups = ((long long)rows + (long long)U * rpi - 1) / ((long long)U * rpi);
+  // as many blocks as the chunk form (a covering grid of one row group per block measured 34.8
+  // vs 30.0 ms on the ResNet50 step: the per-block channel setup then dominates)
+  const long long cap = chunk_grid.y;
+  return dim3(chunk_grid.x, (unsigned)(groups < cap ? (groups < 1 ? 1 : groups) : cap));
+}
+
 // Sum E-wide per-lane vectors over the lanes that share a channel chunk (narrow rows), result
 // valid in the sub == 0 lanes.  red: 256 * E floats of LDS.
 template <int E>
@@ -249,13 +268,11 @@ template <typename T, typename WT, bool RELU, bool RES>
 __global__ __launch_bounds__(256) void apply_fwd(const T* __restrict__ x, const T* __restrict__ z,
                                                  const float* __restrict__ mean, const float* __restrict__ rstd,
                                                  const WT* __restrict__ gamma, const WT* __restrict__ beta,
-                                                 T* __restrict__ y, int rows, int cols, int rpb) {
+                                                 T* __restrict__ y, int rows, int cols, int rpb, int inter) {
   constexpr int E = 16 / sizeof(T);
   const Map m = lane_map<E>(cols);
   if (!m.active) return;
   const int c0 = m.c0, st = m.rpi;
-  const int r0 = blockIdx.y * rpb;
-  const int r1 = min(rows, r0 + rpb);
   float a[E], b[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
@@ -264,8 +281,7 @@ __global__ __launch_bounds__(256) void apply_fwd(const T* __restrict__ x, const 
     a[e] = g * rstd[c0 + e];
     b[e] = bt - mean[c0 + e] * a[e];
   }
-  int r = r0 + m.sub;
-  for (; r + (U - 1) * st < r1; r += U * st) {
+  auto rows_u = [&](int r) {  // rows r, r + st, ... r + (U - 1) st
     float v[U][E], zz[U][E];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -283,8 +299,8 @@ __global__ __launch_bounds__(256) void apply_fwd(const T* __restrict__ x, const 
       }
       store_f<T, E>(y + (size_t)(r + u * st) * cols + c0, v[u]);
     }
-  }
-  for (; r < r1; r += st) {
+  };
+  auto row_1 = [&](int r) {
     float v[E], zz[E];
     load_f<T, E>(x + (size_t)r * cols + c0, v);
     if constexpr (RES) load_f<T, E>(z + (size_t)r * cols + c0, zz);
@@ -296,7 +312,26 @@ __global__ __launch_bounds__(256) void apply_fwd(const T* __restrict__ x, const 
       v[e] = o;
     }
     store_f<T, E>(y + (size_t)r * cols + c0, v);
+  };
+  if (inter) {  // row groups of U * st rows dealt round-robin over the blocks (see kInterleave)
+    const long long RG = (long long)U * st;
+    for (long long g = blockIdx.y; g * RG < rows; g += gridDim.y) {
+      const int rb = (int)(g * RG) + m.sub;
+      if ((g + 1) * RG <= rows) {
+        rows_u(rb);
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (rb + u * st < rows) row_1(rb + u * st);
+      }
+    }
+    return;
   }
+  const int r0 = blockIdx.y * rpb;
+  const int r1 = min(rows, r0 + rpb);
+  int r = r0 + m.sub;
+  for (; r + (U - 1) * st < r1; r += U * st) rows_u(r);
+  for (; r < r1; r += st) row_1(r);
 }
 
 // ---- backward reduce: per channel  s1 = sum g,  s2 = sum g * (x - mean),  g = dy [* (y > 0)]
@@ -318,12 +353,10 @@ __global__ __launch_bounds__(256) void bwd_partial(const T* __restrict__ dy, con
                                                    int cols, int rpb, float* __restrict__ p1, float* __restrict__ p2,
                                                    const WT* __restrict__ gamma = nullptr,
                                                    const WT* __restrict__ beta = nullptr,
-                                                   const float* __restrict__ rstd = nullptr) {
+                                                   const float* __restrict__ rstd = nullptr, int inter = 0) {
   constexpr int E = 16 / sizeof(T);
   __shared__ float red[256 * E];
   const Map m = lane_map<E>(cols);
-  const int r0 = blockIdx.y * rpb;
-  const int r1 = min(rows, r0 + rpb);
   float mu[E], s1[E], s2[E], fa[E], fb[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) { mu[e] = 0.f; s1[e] = 0.f; s2[e] = 0.f; fa[e] = 0.f; fb[e] = 0.f; }
@@ -335,8 +368,7 @@ __global__ __launch_bounds__(256) void bwd_partial(const T* __restrict__ dy, con
 #pragma unroll
       for (int e = 0; e < E; ++e) affine_of<WT>(gamma, beta, mean, rstd, c0 + e, fa[e], fb[e]);
     }
-    int r = r0 + m.sub;
-    for (; r + (U - 1) * st < r1; r += U * st) {
+    auto rows_u = [&](int r) {
       float g[U][E], v[U][E], o[U][E];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -354,8 +386,8 @@ __global__ __launch_bounds__(256) void bwd_partial(const T* __restrict__ dy, con
           s1[e] += gg;
           s2[e] += gg * (v[u][e] - mu[e]);
         }
-    }
-    for (; r < r1; r += st) {
+    };
+    auto row_1 = [&](int r) {
       float g[E], v[E], o[E];
       load_f<T, E>(dy + (size_t)r * cols + c0, g);
       load_f<T, E>(x + (size_t)r * cols + c0, v);
@@ -368,6 +400,25 @@ __global__ __launch_bounds__(256) void bwd_partial(const T* __restrict__ dy, con
         s1[e] += gg;
         s2[e] += gg * (v[e] - mu[e]);
       }
+    };
+    if (inter) {
+      const long long RG = (long long)U * st;
+      for (long long gi = blockIdx.y; gi * RG < rows; gi += gridDim.y) {
+        const int rb = (int)(gi * RG) + m.sub;
+        if ((gi + 1) * RG <= rows) {
+          rows_u(rb);
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (rb + u * st < rows) row_1(rb + u * st);
+        }
+      }
+    } else {
+      const int r0 = blockIdx.y * rpb;
+      const int r1 = min(rows, r0 + rpb);
+      int r = r0 + m.sub;
+      for (; r + (U - 1) * st < r1; r += U * st) rows_u(r);
+      for (; r < r1; r += st) row_1(r);
     }
   }
   block_colsum<E>(s1, m, red);
@@ -429,14 +480,12 @@ __global__ __launch_bounds__(256) void bwd_apply(const T* __restrict__ dy, const
                                                  const T* __restrict__ y, const float* __restrict__ mean,
                                                  const float* __restrict__ rstd, const WT* __restrict__ gamma,
                                                  const float* __restrict__ sums, T* __restrict__ dx,
-                                                 T* __restrict__ dz, int rows, int cols, int rpb,
+                                                 T* __restrict__ dz, int rows, int cols, int rpb, int inter,
                                                  const WT* __restrict__ beta = nullptr) {
   constexpr int E = 16 / sizeof(T);
   const Map m = lane_map<E>(cols);
   if (!m.active) return;
   const int c0 = m.c0, st = m.rpi;
-  const int r0 = blockIdx.y * rpb;
-  const int r1 = min(rows, r0 + rpb);
   const float invR = 1.f / (float)rows;
   float k1[E], k2[E], k3[E], mu[E], fa[E], fb[E];  // dx = k1 * g + k2 * (x - mu) + k3
 #pragma unroll
@@ -449,8 +498,7 @@ __global__ __launch_bounds__(256) void bwd_apply(const T* __restrict__ dy, const
     k2[e] = -gr * rs * rs * sums[cols + c0 + e] * invR;
     k3[e] = -gr * sums[c0 + e] * invR;
   }
-  int r = r0 + m.sub;
-  for (; r + (U - 1) * st < r1; r += U * st) {
+  auto rows_u = [&](int r) {
     float g[U][E], v[U][E], o[U][E];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -469,8 +517,8 @@ __global__ __launch_bounds__(256) void bwd_apply(const T* __restrict__ dy, const
       store_f<T, E>(dx + (size_t)(r + u * st) * cols + c0, v[u]);
       if constexpr (RES) store_f<T, E>(dz + (size_t)(r + u * st) * cols + c0, g[u]);
     }
-  }
-  for (; r < r1; r += st) {
+  };
+  auto row_1 = [&](int r) {
     float g[E], v[E], o[E];
     load_f<T, E>(dy + (size_t)r * cols + c0, g);
     load_f<T, E>(x + (size_t)r * cols + c0, v);
@@ -483,7 +531,26 @@ __global__ __launch_bounds__(256) void bwd_apply(const T* __restrict__ dy, const
     }
     store_f<T, E>(dx + (size_t)r * cols + c0, v);
     if constexpr (RES) store_f<T, E>(dz + (size_t)r * cols + c0, g);
+  };
+  if (inter) {
+    const long long RG = (long long)U * st;
+    for (long long gi = blockIdx.y; gi * RG < rows; gi += gridDim.y) {
+      const int rb = (int)(gi * RG) + m.sub;
+      if ((gi + 1) * RG <= rows) {
+        rows_u(rb);
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (rb + u * st < rows) row_1(rb + u * st);
+      }
+    }
+    return;
   }
+  const int r0 = blockIdx.y * rpb;
+  const int r1 = min(rows, r0 + rpb);
+  int r = r0 + m.sub;
+  for (; r + (U - 1) * st < r1; r += U * st) rows_u(r);
+  for (; r < r1; r += st) row_1(r);
 }
 
 template <typename T, typename WT>
@@ -494,6 +561,7 @@ hipError_t fwd(const void* x, const void* z, const void* gamma, const void* beta
   const int cb = col_blocks(cols, E);
   const int rpb = rows_per_block(rows, cb);
   const dim3 grid(cb, (rows + rpb - 1) / rpb);
+  const dim3 agrid = apply_grid(rows, cols, E, grid);
   if (training) {
     const int rrb = rows_per_block(rows, cb, kRedBlocks);
     const int P = (rows + rrb - 1) / rrb;
@@ -501,8 +569,9 @@ hipError_t fwd(const void* x, const void* z, const void* gamma, const void* beta
     stats_finish<<<(cols + 63) / 64, 1024, 0, st>>>(ws, ws + (size_t)P * cols, P, rows, rrb, cols, eps, momentum,
                                                     mean, rstd, run_mean, run_var);
   }
-#define PA_BNF(R, Z) apply_fwd<T, WT, R, Z><<<grid, 256, 0, st>>>((const T*)x, (const T*)z, mean, rstd, \
-                                                                 (const WT*)gamma, (const WT*)beta, (T*)y, rows, cols, rpb)
+#define PA_BNF(R, Z) apply_fwd<T, WT, R, Z><<<agrid, 256, 0, st>>>((const T*)x, (const T*)z, mean, rstd, \
+                                                                  (const WT*)gamma, (const WT*)beta, (T*)y, rows, cols, \
+                                                                  rpb, kInterleave)
   if (relu && z) PA_BNF(true, true);
   else if (relu) PA_BNF(true, false);
   else if (z) PA_BNF(false, true);
@@ -521,6 +590,7 @@ hipError_t fwd_parts(const void* x, const void* z, const void* gamma, const void
   const int cb = col_blocks(cols, E);
   const int rpb = rows_per_block(rows, cb);
   const dim3 grid(cb, (rows + rpb - 1) / rpb);
+  const dim3 agrid = apply_grid(rows, cols, E, grid);
   const float* pm = parts;
   const float* pq = parts + (size_t)P * cols;
   int Pf = P, rf = prpb;
@@ -537,8 +607,9 @@ hipError_t fwd_parts(const void* x, const void* z, const void* gamma, const void
   }
   stats_finish<<<(cols + 63) / 64, 1024, 0, st>>>(pm, pq, Pf, rows, rf, cols, eps, momentum, mean, rstd, run_mean,
                                                   run_var);
-#define PA_BNF(R, Z) apply_fwd<T, WT, R, Z><<<grid, 256, 0, st>>>((const T*)x, (const T*)z, mean, rstd, \
-                                                                 (const WT*)gamma, (const WT*)beta, (T*)y, rows, cols, rpb)
+#define PA_BNF(R, Z) apply_fwd<T, WT, R, Z><<<agrid, 256, 0, st>>>((const T*)x, (const T*)z, mean, rstd, \
+                                                                  (const WT*)gamma, (const WT*)beta, (T*)y, rows, cols, \
+                                                                  rpb, kInterleave)
   if (relu && z) PA_BNF(true, true);
   else if (relu) PA_BNF(true, false);
   else if (z) PA_BNF(false, true);
@@ -561,23 +632,27 @@ hipError_t bwd(const void* dy, const void* x, const void* y, const float* mean, 
   float* p2 = ws + (size_t)P * cols;
   float* sums = ws + (size_t)2 * P * cols;
   const dim3 rgrid(cb, P);
+  const dim3 agrid = apply_grid(rows, cols, E, grid);
   const bool xm = relu && dz == nullptr;  // ReLU mask from x: y is not read
   if (xm)
     bwd_partial<T, true, WT, true><<<rgrid, 256, 0, st>>>((const T*)dy, (const T*)x, nullptr, mean, rows, cols, rrb, p1,
-                                                          p2, (const WT*)gamma, (const WT*)beta, rstd);
+                                                          p2, (const WT*)gamma, (const WT*)beta, rstd, kInterleave);
   else if (relu)
-    bwd_partial<T, true><<<rgrid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)y, mean, rows, cols, rrb, p1, p2);
+    bwd_partial<T, true, WT><<<rgrid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)y, mean, rows, cols, rrb, p1, p2,
+                                                (const WT*)nullptr, (const WT*)nullptr, nullptr, kInterleave);
   else
-    bwd_partial<T, false><<<rgrid, 256, 0, st>>>((const T*)dy, (const T*)x, nullptr, mean, rows, cols, rrb, p1, p2);
+    bwd_partial<T, false, WT><<<rgrid, 256, 0, st>>>((const T*)dy, (const T*)x, nullptr, mean, rows, cols, rrb, p1, p2,
+                                                 (const WT*)nullptr, (const WT*)nullptr, nullptr, kInterleave);
   bwd_finish<WT><<<(cols + 63) / 64, 1024, 0, st>>>(p1, p2, P, cols, rstd, (WT*)dgamma, (WT*)dbeta, sums,
                                                     accumulate);
-#define PA_BNB(R, Z) bwd_apply<T, WT, R, Z><<<grid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)y, mean, rstd, \
-                                                                 (const WT*)gamma, sums, (T*)dx, (T*)dz, rows, cols, rpb)
+#define PA_BNB(R, Z) bwd_apply<T, WT, R, Z><<<agrid, 256, 0, st>>>((const T*)dy, (const T*)x, (const T*)y, mean, \
+                                                                  rstd, (const WT*)gamma, sums, (T*)dx, (T*)dz, rows, \
+                                                                  cols, rpb, kInterleave)
   if (relu && dz) PA_BNB(true, true);
   else if (xm)
-    bwd_apply<T, WT, true, false, true><<<grid, 256, 0, st>>>((const T*)dy, (const T*)x, nullptr, mean, rstd,
-                                                              (const WT*)gamma, sums, (T*)dx, nullptr, rows, cols, rpb,
-                                                              (const WT*)beta);
+    bwd_apply<T, WT, true, false, true><<<agrid, 256, 0, st>>>((const T*)dy, (const T*)x, nullptr, mean, rstd,
+                                                               (const WT*)gamma, sums, (T*)dx, nullptr, rows, cols, rpb,
+                                                               kInterleave, (const WT*)beta);
   else if (dz) PA_BNB(false, true);
   else PA_BNB(false, false);
 #undef PA_BNB
@@ -642,6 +717,12 @@ PA_API hipError_t pa_bn_bwd(const void* dy, const void* x, const void* y, const 
 }
 
 // A/B knob: block target of the BN reduction passes (returns the previous value).
+PA_API int pa_bn_set_interleave(int v) {
+  const int old = bn::kInterleave;
+  bn::kInterleave = v;
+  return old;
+}
+
 PA_API int pa_bn_tune(int red_blocks) {
   const int old = bn::kRedBlocks;
   if (red_blocks >= 64 && red_blocks <= 8192) bn::kRedBlocks = red_blocks;

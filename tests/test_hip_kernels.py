@@ -689,6 +689,48 @@ def test_batchnorm_nhwc_fused(dt, shape, mode):
         _close(z.grad, zr.grad, tol * 2, 1e-2, 'bn dz')
 
 
+@pytest.mark.parametrize("shape", [(2, 5, 5, 96), (4, 28, 28, 256), (8, 14, 14, 4096), (3, 7, 7, 2048)])
+@pytest.mark.parametrize("mode", ['relu', 'add_relu'])
+def test_batchnorm_row_order_bitwise(shape, mode):
+    """The streaming BN passes' two row orders (round-robin row groups over a covering grid, the
+    default, vs contiguous per-block chunks) compute every element by the same expression (the
+    backward sums are added in another order): each order is deterministic, y agrees to within a
+    bf16 ulp on a handful of elements, dx / dz to rounding."""
+    from paddle.ops import batchnorm
+    from paddle.ops import _native
+    C = shape[-1]
+    x0 = (torch.randn(*shape, device=DEV) * 2 + 3).bfloat16()
+    z0 = torch.randn(*shape, device=DEV).bfloat16() if mode == 'add_relu' else None
+    dy = torch.randn(*shape, device=DEV).bfloat16()
+    out = {}
+    old = _native.lib.pa_bn_set_interleave(1)
+    try:
+        for order in (1, 0, 2):  # 2: the round-robin order again (run-to-run determinism)
+            _native.lib.pa_bn_set_interleave(1 if order == 2 else order)
+            x = x0.clone().requires_grad_()
+            z = z0.clone().requires_grad_() if z0 is not None else None
+            g = torch.ones(C, device=DEV).requires_grad_()
+            b = torch.zeros(C, device=DEV).requires_grad_()
+            rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+            y = batchnorm.bn_act_nhwc(x, g, b, rm, rv, 1e-5, 0.9, True, True, z)
+            y.backward(dy)
+            out[order] = [y.detach(), x.grad] + ([z.grad] if z is not None else [])
+    finally:
+        _native.lib.pa_bn_set_interleave(old)
+    names = ['y', 'dx', 'dz']
+    for i, (a, c) in enumerate(zip(out[1], out[2])):
+        assert torch.equal(a, c), ('nondeterministic', names[i], (a.float() - c.float()).abs().max().item())
+    # y: the same expression per element (the two loop forms may contract an FMA differently, so a
+    # rare element lands one bf16 ulp apart); dx / dz also see the backward sums, which the two
+    # orders add in different orders
+    a, c = out[1][0], out[0][0]
+    ulp = a.float().abs().clamp_min(1e-30) * 2.0 ** -7
+    assert ((a.float() - c.float()).abs() <= ulp * 1.01).all()
+    assert (a != c).sum().item() <= max(2, a.numel() // 100000)
+    for i in range(1, len(out[1])):
+        _close(out[1][i], out[0][i], 2e-2, 2e-2, names[i])
+
+
 # ---- batch-norm statistics from the conv / GEMM epilogue (ops.conv.fused_bn_stats) ----
 
 def _slab_ref(y2, rpb):
