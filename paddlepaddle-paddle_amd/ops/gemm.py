@@ -347,11 +347,14 @@ def kmajor_weight(x2, w):
 
     Both operands K-major is the hand-written GEMM's fastest layout (an LDS-staged N-major B tile
     needs a transposing read); the transpose of a 2048x8192 weight costs ~15 us, so the copy pays
-    off once the token count is large (training micro-batches): GPT-3 1.3B step 129.1-129.5 ms with
-    the copies vs 130.2-130.5 ms reading W directly (profiles/r3s3_kmajor_fwd_ab.log; round 1's
-    hipBLASLt measurement: profiles/fwd_layout_r1.log).
+    off once the token count is large (training micro-batches): GPT-3 1.3B step (16384 rows)
+    129.1-129.5 ms with the copies vs 130.2-130.5 ms reading W directly
+    (profiles/r3s3_kmajor_fwd_ab.log; round 1's hipBLASLt measurement: profiles/fwd_layout_r1.log),
+    while the Llama-2 13B layer stack (8192 rows, 5120 x 27648 weights) runs 0.7 ms faster without
+    them (profiles/r6w_llama_kmajor_ab.log): the copy costs in proportion to the weight, the gain in
+    proportion to the rows, so it is made from 12288 rows on.
     """
-    if not _kmajor_fwd or x2.shape[0] < 4096 or w.dtype not in (torch.bfloat16, torch.float16):
+    if not _kmajor_fwd or x2.shape[0] < 12288 or w.dtype not in (torch.bfloat16, torch.float16):
         return None
     if w.dim() != 2 or not w.is_contiguous() or w.shape[0] % 64 or w.shape[1] % 64 or not x2.is_cuda:
         return None

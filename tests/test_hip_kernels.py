@@ -1291,7 +1291,7 @@ def test_linear_kmajor_forward_matches_plain_layout():
     output and gradients as the [in, out] layout."""
     from paddle.ops import gemm, linear
     g = torch.Generator(device=DEV).manual_seed(3)
-    x = (torch.rand(4096, 512, device=DEV, generator=g) * 2 - 1).bfloat16()
+    x = (torch.rand(12288, 512, device=DEV, generator=g) * 2 - 1).bfloat16()
     w = ((torch.rand(512, 384, device=DEV, generator=g) * 2 - 1) * 0.05).bfloat16()
     b = torch.rand(384, device=DEV, generator=g).bfloat16()
     wt = gemm.kmajor_weight(x, w)
@@ -1299,6 +1299,7 @@ def test_linear_kmajor_forward_matches_plain_layout():
     ref = x.float() @ w.float() + b.float()
     _close(torch.addmm(b, x, wt.t()), ref, atol=0.05, rtol=0.01, name='kmajor linear')
     assert gemm.kmajor_weight(x[:64], w) is None  # small token counts keep the plain layout
+    assert gemm.kmajor_weight(x[:8192], w) is None  # 8192 rows (the Llama stack): plain layout
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
