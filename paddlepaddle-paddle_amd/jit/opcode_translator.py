@@ -805,6 +805,10 @@ def _template(v, prog, inputs, depth=0, origin=None):
                 raise _Break('a tensor the recorder did not produce')
             return ('out', vid)
         return ('c', v)
+    if type(v) in _ITER_TYPES:  # a list / tuple / range iterator: its source and position
+        red = v.__reduce__()
+        if len(red) >= 2 and red[0] is builtins.iter and len(red[1]) == 1:
+            return ('iter', _template(red[1][0], prog, inputs, depth + 1, origin), red[2] if len(red) > 2 else 0)
     if depth < 6 and type(v) is tuple:
         return ('tup', [_template(x, prog, inputs, depth + 1, origin) for x in v])
     if depth < 6 and type(v) is list:
@@ -812,6 +816,27 @@ def _template(v, prog, inputs, depth=0, origin=None):
     if depth < 6 and type(v) is dict:
         return ('dict', [(k, _template(x, prog, inputs, depth + 1, origin)) for k, x in v.items()])
     return ('c', v)
+
+
+_ITER_TYPES = (type(iter([])), type(iter(())), type(iter(range(0))), type(iter(range(1 << 70))))
+# objects the region may create and hand on baked into its template: immutable, so a replay can
+# share them (anything else created by the region — e.g. a closure over the region's symbolic
+# values — makes the region untranslatable: it would leak recording-time state into every replay)
+_SHAREABLE = _SIMPLE + (range, slice, type, types.ModuleType, types.BuiltinFunctionType, frozenset)
+
+
+def _baked_unsafe(t, ctx):
+    kind = t[0]
+    if kind == 'c':
+        v = t[1]
+        return id(v) in ctx.created and not isinstance(v, _SHAREABLE) and not isinstance(v, Tensor)
+    if kind in ('tup', 'list'):
+        return any(_baked_unsafe(x, ctx) for x in t[1])
+    if kind == 'dict':
+        return any(_baked_unsafe(x, ctx) for _, x in t[1])
+    if kind == 'iter':
+        return _baked_unsafe(t[1], ctx)
+    return False
 
 
 def _slot_value(start, path):
@@ -833,6 +858,11 @@ def _materialize(t, env, feeds, start=None):
         return [_materialize(x, env, feeds, start) for x in t[1]]
     if kind == 'dict':
         return {k: _materialize(x, env, feeds, start) for k, x in t[1]}
+    if kind == 'iter':
+        it = iter(_materialize(t[1], env, feeds, start))
+        if t[2]:
+            it.__setstate__(t[2])
+        return it
     return t[1]
 
 
@@ -932,6 +962,10 @@ def _translate(fr):
     finally:
         if started:
             _stop_recording()
+    ends = [reg.tpl_ret] if reg.returned else list(reg.tpl_locals.values()) + reg.tpl_stack + \
+        list(reg.tpl_cells.values())
+    if any(_baked_unsafe(t, ctx) for t in ends):
+        return None
     acc = set()
     for t in ([reg.tpl_ret] if reg.returned else list(reg.tpl_locals.values()) + reg.tpl_stack +
               list(reg.tpl_cells.values())):

@@ -359,3 +359,43 @@ def test_opcode_translator_with_blocks_pass_through_and_cache():
     with pytest.raises(ValueError):
         tg(x)
     assert paddle.is_grad_enabled()
+
+
+def test_opcode_translator_region_created_iterators_and_closures_replay():
+    """A region that creates an iterator (a for loop over range / a list) and breaks inside the
+    loop hands the iterator on by source and position, so every replay iterates afresh (it used
+    to bake the recording's exhausted iterator: the second call skipped the loop); a closure
+    created over the region's values is never baked into a template."""
+    import numpy as np
+    from paddle.jit import sot
+
+    def loop_setitem(x):
+        z = paddle.zeros_like(x)
+        for i in range(x.shape[0]):
+            z[i] = x[i] * i
+        return z
+
+    def loop_list(x):
+        acc = x * 0
+        for w in [1.0, 2.0, 3.0]:
+            acc[0] = acc[0] + x[0] * w
+        return acc
+
+    def closure(x):
+        c = 0
+
+        def inc():
+            nonlocal c
+            c += 1
+            return x * c
+        inc()
+        return inc()
+
+    x = paddle.randn([4, 3])
+    for fn in (loop_setitem, loop_list, closure):
+        st = sot.symbolic_translate(fn)
+        ref = fn(x).numpy()
+        for _ in range(3):
+            np.testing.assert_allclose(st(x).numpy(), ref, rtol=1e-6, atol=1e-6)
+        x2 = paddle.randn([4, 3])
+        np.testing.assert_allclose(st(x2).numpy(), fn(x2).numpy(), rtol=1e-6, atol=1e-6)
