@@ -805,6 +805,13 @@ def _template(v, prog, inputs, depth=0, origin=None):
                 raise _Break('a tensor the recorder did not produce')
             return ('out', vid)
         return ('c', v)
+    if isinstance(v, (types.MethodType, types.BuiltinMethodType)) and \
+            getattr(v, '__self__', None) is not None and not isinstance(v.__self__, types.ModuleType):
+        # a bound method (LOAD_METHOD's value left on the stack at a break): bound afresh to the
+        # replaying call's object — the recording's object may be the region's private copy
+        ts = _template(v.__self__, prog, inputs, depth + 1, origin)
+        if ts[0] != 'c':
+            return ('meth', ts, v.__name__)
     if type(v) in _ITER_TYPES:  # a list / tuple / range iterator: its source and position
         red = v.__reduce__()
         if len(red) >= 2 and red[0] is builtins.iter and len(red[1]) == 1:
@@ -834,7 +841,7 @@ def _baked_unsafe(t, ctx):
         return any(_baked_unsafe(x, ctx) for x in t[1])
     if kind == 'dict':
         return any(_baked_unsafe(x, ctx) for _, x in t[1])
-    if kind == 'iter':
+    if kind in ('iter', 'meth'):
         return _baked_unsafe(t[1], ctx)
     return False
 
@@ -858,6 +865,8 @@ def _materialize(t, env, feeds, start=None):
         return [_materialize(x, env, feeds, start) for x in t[1]]
     if kind == 'dict':
         return {k: _materialize(x, env, feeds, start) for k, x in t[1]}
+    if kind == 'meth':
+        return getattr(_materialize(t[1], env, feeds, start), t[2])
     if kind == 'iter':
         it = iter(_materialize(t[1], env, feeds, start))
         if t[2]:
@@ -876,6 +885,8 @@ def _out_vids(t, acc):
     elif kind == 'dict':
         for _, x in t[1]:
             _out_vids(x, acc)
+    elif kind in ('iter', 'meth'):
+        _out_vids(t[1], acc)
     return acc
 
 

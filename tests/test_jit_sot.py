@@ -391,8 +391,16 @@ def test_opcode_translator_region_created_iterators_and_closures_replay():
         inc()
         return inc()
 
+    def loop_break_append(x):  # a bound list.append left on the stack at a mutation break
+        r = []
+        for i in range(3):
+            if x.sum() > 1e9:
+                break
+            r.append(x + i)
+        return paddle.concat(r)
+
     x = paddle.randn([4, 3])
-    for fn in (loop_setitem, loop_list, closure):
+    for fn in (loop_setitem, loop_list, closure, loop_break_append):
         st = sot.symbolic_translate(fn)
         ref = fn(x).numpy()
         for _ in range(3):
