@@ -810,7 +810,7 @@ def _template(v, prog, inputs, depth=0, origin=None):
         # a bound method (LOAD_METHOD's value left on the stack at a break): bound afresh to the
         # replaying call's object — the recording's object may be the region's private copy
         ts = _template(v.__self__, prog, inputs, depth + 1, origin)
-        if ts[0] != 'c':
+        if ts[0] in ('slot', 'in', 'out'):  # an identity the replay reproduces (a rebuilt container would not)
             return ('meth', ts, v.__name__)
     if type(v) in _ITER_TYPES:  # a list / tuple / range iterator: its source and position
         red = v.__reduce__()
