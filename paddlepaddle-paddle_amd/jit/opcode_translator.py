@@ -144,7 +144,8 @@ class _Frame:
         if any(n.startswith('.') for n in pos):  # comprehension bodies: implicit '.0' iterator argument
             self.locals = dict(zip(pos, args))
         else:
-            bound = inspect.signature(fn).bind(*args, **kwargs)
+            # the code object's own parameters (not a functools.wraps target's signature)
+            bound = inspect.signature(fn, follow_wrapped=False).bind(*args, **kwargs)
             bound.apply_defaults()
             self.locals = dict(bound.arguments)
         self.cells = {}

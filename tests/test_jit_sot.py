@@ -407,3 +407,23 @@ def test_opcode_translator_region_created_iterators_and_closures_replay():
             np.testing.assert_allclose(st(x).numpy(), ref, rtol=1e-6, atol=1e-6)
         x2 = paddle.randn([4, 3])
         np.testing.assert_allclose(st(x2).numpy(), fn(x2).numpy(), rtol=1e-6, atol=1e-6)
+
+
+def test_opcode_translator_wrapped_functions_bind_their_own_parameters():
+    """A functools.wraps wrapper (paddle.no_grad() as a decorator: ``def w(*a, **k)``) is bound by
+    its own code object's parameters, not by the wrapped function's signature."""
+    import numpy as np
+    from paddle.jit import sot
+
+    @paddle.no_grad()
+    def f(x, scale=2.0):
+        return x * scale
+
+    def g(x):
+        return f(x) + f(x, scale=3.0)
+
+    x = paddle.randn([3, 4])
+    for fn in (f, g):
+        st = sot.symbolic_translate(fn)
+        for _ in range(2):
+            np.testing.assert_allclose(st(x).numpy(), fn(x).numpy(), rtol=1e-6)
