@@ -1060,6 +1060,52 @@ class DistModel:
         from ... import static as _st
         return _st.Program() if self._prog_for(mode) is not None else None
 
+    def serial_main_program(self, mode=None):
+        """The unpartitioned step of ``mode`` for analysis (reference api.py:2049): the forward (and
+        the loss outside 'predict') recorded with SPMD propagation off and every placed parameter at
+        its GLOBAL shape — its Program constant is a meta tensor of that shape, so the program is
+        an op graph to inspect, not to run.  None before that mode has run a step."""
+        import torch as _t
+        from ... import static as _st
+        from ... import framework as _fw
+        from .. import auto_parallel_spmd as spmd
+        mode = mode or self._mode
+        keys = [k for k in self._progs if k[0] == mode]
+        if not keys or any(len(s) != 2 for s in keys[-1][1]):
+            return None
+        specs = keys[-1][1]
+        dt_name = {_t.float32: 'float32', _t.float16: 'float16', _t.bfloat16: 'bfloat16', _t.int64: 'int64',
+                   _t.int32: 'int32', _t.float64: 'float64', _t.bool: 'bool', _t.uint8: 'uint8'}
+        main = _st.Program()
+        was_dynamic = _fw.in_dynamic_mode()
+        spmd_on = spmd._mode[0] is not None
+        if spmd_on:
+            spmd.disable()
+        if was_dynamic:
+            _fw.enable_static()
+        try:
+            for p in self._layer.parameters():
+                m = spmd.meta(p._t)
+                if m is not None:  # a placed parameter: its global-shape twin
+                    cid = main._const(p._t, owner=p)
+                    twin = _t.empty(list(m[2]), dtype=p._t.dtype, device='meta')
+                    if p._t.requires_grad:
+                        twin.requires_grad_(True)
+                    main._meta_twins[cid] = twin
+            with _st.program_guard(main, _st.Program()):
+                feeds = [_st.data(f'dm_input_{i}', [-1] + list(shape), dt_name[dtype])
+                         for i, (shape, dtype) in enumerate(specs)]
+                if mode == 'predict':
+                    self._layer(*feeds)
+                else:
+                    self._loss(self._layer(*feeds[:-1]), feeds[-1])
+        finally:
+            if was_dynamic:
+                _fw.disable_static()
+            if spmd_on:
+                spmd.enable()
+        return main
+
 
 def to_static(layer, loader=None, loss=None, optimizer=None, strategy=None, input_spec=None):
     return DistModel(layer, loader, loss, optimizer, strategy)

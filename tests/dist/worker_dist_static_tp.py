@@ -45,6 +45,12 @@ def main():
     assert prog is plan[0] and dm.dist_main_program('eval') is None
     assert len(prog.reshard_nodes()) >= 2
     assert len(dm.dist_startup_program().nodes) == 0
+    # the serial view: no reshard collectives, the column-parallel weight at its global shape
+    ser = dm.serial_main_program()
+    assert ser is not None and not ser.reshard_nodes() and len(ser.nodes) > 0
+    twin = ser._meta_twins[ser._const_ids[id(net[2].weight._t)]]
+    assert list(twin.shape) == [6, 12], twin.shape
+    assert dm.serial_main_program('predict') is None
     # the column-parallel weight keeps its dist attribute (global shape [6, 12], Shard(1))
     mesh_, pl, gshape = prog.dist_attr(net[2].weight)
     assert list(gshape) == [6, 12] and isinstance(pl[0], dist.Shard) and pl[0].get_dim() == 1, (pl, gshape)
