@@ -1060,6 +1060,11 @@ class DistModel:
         from ... import static as _st
         return _st.Program() if self._prog_for(mode) is not None else None
 
+    def serial_startup_program(self, mode=None):
+        """Parameters are created eagerly (then placed), so the serial startup program is empty."""
+        from ... import static as _st
+        return _st.Program() if self._prog_for(mode) is not None else None
+
     def serial_main_program(self, mode=None):
         """The unpartitioned step of ``mode`` for analysis (reference api.py:2049): the forward (and
         the loss outside 'predict') recorded with SPMD propagation off and every placed parameter at

@@ -50,7 +50,7 @@ def main():
     assert ser is not None and not ser.reshard_nodes() and len(ser.nodes) > 0
     twin = ser._meta_twins[ser._const_ids[id(net[2].weight._t)]]
     assert list(twin.shape) == [6, 12], twin.shape
-    assert dm.serial_main_program('predict') is None
+    assert dm.serial_main_program("predict") is None and len(dm.serial_startup_program().nodes) == 0
     # the column-parallel weight keeps its dist attribute (global shape [6, 12], Shard(1))
     mesh_, pl, gshape = prog.dist_attr(net[2].weight)
     assert list(gshape) == [6, 12] and isinstance(pl[0], dist.Shard) and pl[0].get_dim() == 1, (pl, gshape)
