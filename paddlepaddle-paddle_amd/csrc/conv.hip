@@ -907,6 +907,14 @@ PA_API int pa_im2col_nhwc(const void* x, void* out, int N, int H, int W, int C, 
   return (int)hipGetLastError();
 }
 
+// A/B (pa_conv_set_wgrad_direct): <= 16 pixel splits summed by the finishing pass itself
+static int g_wgrad_direct = 1;
+PA_API int pa_conv_set_wgrad_direct(int v) {
+  const int old = g_wgrad_direct;
+  g_wgrad_direct = v;
+  return old;
+}
+
 PA_API int pa_conv2d_wgrad_ok(int C, int Cout) { return C > 0 && C % 8 == 0 && Cout > 0 && Cout % 8 == 0; }
 
 PA_API int pa_conv2d_wgrad(const void* x, const void* dy, void* ws, void* dw, int N, int H, int W, int C, int Cout,
@@ -929,12 +937,19 @@ PA_API int pa_conv2d_wgrad(const void* x, const void* dy, void* ws, void* dw, in
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const long long total = (long long)M * Cout;  // Cout % 8 == 0: float4 groups never straddle a row
+  const long long nb = (total + 255) / 256;
+  const int blocks = (int)(nb < 2048 ? nb : 2048);
+  if (splits <= WZ && g_wgrad_direct) {
+    // few slices: the finishing pass sums them straight from the split workspace ([splits][total],
+    // coalesced per slice) — one launch and no partial round trip (the pre-sum pass was a second
+    // ~11 us launch per convolution: ~0.5 ms of the ResNet50 step)
+    wgrad_reduce_kernel<<<blocks, 256, 0, st>>>((const float*)ws, (uint16_t*)dw, splits, R * S, C, Cout, accumulate);
+    return (int)hipGetLastError();
+  }
   const int ngroups = (splits + WZ - 1) / WZ;
   float* part = (float*)ws + (long long)splits * total;  // scratch tail: ngroups x total
   const dim3 zgrid((unsigned)((total / 4 + 255) / 256), ngroups);
   wgrad_zsum_kernel<<<zgrid, 256, 0, st>>>((const float*)ws, part, splits, total / 4);
-  const long long nb = (total + 255) / 256;
-  const int blocks = (int)(nb < 2048 ? nb : 2048);
   wgrad_reduce_kernel<<<blocks, 256, 0, st>>>(part, (uint16_t*)dw, ngroups, R * S, C, Cout, accumulate);
   return (int)hipGetLastError();
 }

@@ -149,6 +149,7 @@ _SIGS = {
     'pa_gemm8_set_staged9': [I],
     'pa_bn_tune': [I],
     'pa_bn_set_interleave': [I],
+    'pa_conv_set_wgrad_direct': [I],
     'pa_act_cs_set_interleave': [I],
     'pa_colsum_finish_parts': [P, P, I, I, I, I, P],
     'pa_gemm8_bf16_epi': [P, P, P, P, P, I, I, I, LL, LL, LL, I, F, I, P],
