@@ -216,14 +216,19 @@ __device__ __forceinline__ void bf16x8_to_f(const uint4 u, float (&f)[8]) {
   }
 }
 
+// cs != null: also the per-tile column sums of x (fp32 [R / 128][C], row-tile major) — the bias
+// gradient partials of an fp8 Linear's dY, taken from the values this pass reads anyway (the
+// separate column-sum pass re-read dY: ~20 us per Linear backward at ERNIE-base shapes).
 template <int FMT>
 __global__ __launch_bounds__(256) void cast_transpose_persist_kernel(const bf16_t* __restrict__ x, int R, int C,
                                                                      long long ldx, uint8_t* __restrict__ q,
                                                                      uint8_t* __restrict__ qt,
                                                                      float* __restrict__ hist, int L, int cur,
-                                                                     float* __restrict__ scale_inv, float margin_mul) {
+                                                                     float* __restrict__ scale_inv, float margin_mul,
+                                                                     float* __restrict__ cs = nullptr) {
   __shared__ __attribute__((aligned(16))) uint8_t tile[T * P2];
   __shared__ float red[4];
+  __shared__ float csr[4][T];  // cs: the four waves' column sums of a tile
   const float s = scale_from_hist(hist, L, cur, fmax_of<FMT>(), margin_mul);
   const int tid = threadIdx.x;
   const int tx = C / T, ntiles = tx * (R / T);
@@ -250,11 +255,16 @@ __global__ __launch_bounds__(256) void cast_transpose_persist_kernel(const bf16_
         nxt[i] = *reinterpret_cast<const uint4*>(x + (long long)(nr0 + row) * ldx + nc0 + 8 * ch);
       }
     }
+    float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // cs: this thread's 8 columns (ch = tid & 15)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int k = tid + 256 * i, row = k >> 4, ch = k & 15;
       float v[8];
       bf16x8_to_f(raw[i], v);
+      if (cs) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[e] += v[e];
+      }
       uint32_t w[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -287,6 +297,21 @@ __global__ __launch_bounds__(256) void cast_transpose_persist_kernel(const bf16_
         *reinterpret_cast<uint4*>(qt + (long long)(c0 + 4 * cg + j) * R + r0 + 16 * rg) = make_uint4(o[0], o[1], o[2], o[3]);
       }
       __syncthreads();  // the tile is rewritten by the next iteration
+    }
+    if (cs) {  // lanes l, l^16, l^32, l^48 of a wave hold the same 8 columns; then the 4 waves via LDS
+      const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        csum[e] += __shfl_xor(csum[e], 16, 64);
+        csum[e] += __shfl_xor(csum[e], 32, 64);
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csr[wave][8 * lane + e] = csum[e];
+      }
+      __syncthreads();
+      if (tid < T) cs[(long long)(r0 / T) * C + c0 + tid] = (csr[0][tid] + csr[1][tid]) + (csr[2][tid] + csr[3][tid]);
+      __syncthreads();  // csr is rewritten by the next tile
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) raw[i] = nxt[i];
@@ -367,6 +392,25 @@ PA_API int pa_fp8_set_cast_full(int v) {
   const int old = g_cast_full;
   g_cast_full = v;
   return old;
+}
+
+// pa_fp8_cast_transpose plus the column sums of x per 128-row tile into cs (fp32 [R / 128][C]):
+// full-tile shapes only (R, C multiples of 128), else hipErrorInvalidValue and nothing runs.
+PA_API int pa_fp8_cast_transpose_cs(const void* x, int R, int C, long long ldx, void* q, void* qt, void* hist, int L,
+                                    int cur, void* scale_inv, int fmt, float margin_mul, float* cs, hipStream_t st) {
+  if (R <= 0 || C <= 0 || R % f8::T || C % f8::T || ldx % 8 || L < 3 || cur < 0 || cur >= L || !hist ||
+      !scale_inv || !cs)
+    return (int)hipErrorInvalidValue;
+  const int ntiles = (R / f8::T) * (C / f8::T);
+  const int per = (ntiles + 1023) / 1024;
+  const int g = (ntiles + per - 1) / per;
+  if (fmt == 0)
+    f8::cast_transpose_persist_kernel<0><<<g, 256, 0, st>>>((const bf16_t*)x, R, C, ldx, (uint8_t*)q, (uint8_t*)qt,
+                                                            (float*)hist, L, cur, (float*)scale_inv, margin_mul, cs);
+  else
+    f8::cast_transpose_persist_kernel<1><<<g, 256, 0, st>>>((const bf16_t*)x, R, C, ldx, (uint8_t*)q, (uint8_t*)qt,
+                                                            (float*)hist, L, cur, (float*)scale_inv, margin_mul, cs);
+  return (int)hipGetLastError();
 }
 
 // x: bf16 [R, C] (row stride ldx, 16-B aligned rows), q: [R, C] fp8 or null, qt: [C, R] fp8 or null.

@@ -87,6 +87,7 @@ _SIGS = {
     'pa_flash_set_fwd_sp': [I],
     'pa_gemm_fp8_ok': [I, I, I, LL, LL, LL],
     'pa_fp8_cast_transpose': [P, I, I, LL, P, P, P, I, I, P, I, F, P],
+    'pa_fp8_cast_transpose_cs': [P, I, I, LL, P, P, P, I, I, P, I, F, P, P],
     'pa_fp8_amax': [P, I, I, LL, P, P],
     'pa_fp8_cast_transpose_multi': [P, I, I, I, P],
     'pa_norm_set_bwd_wave': [I],

@@ -98,8 +98,12 @@ class FP8Meta:
             return pre[2], pre[3], pre[4]
         return self.cast(w, want_q, want_qt)
 
-    def cast(self, x2d, want_q=True, want_qt=True):
-        """x2d: [R, C] -> (q [R,C] | None, q^T [C,R] | None, dequant scale (1-elem fp32 tensor))."""
+    def cast(self, x2d, want_q=True, want_qt=True, colsum=None):
+        """x2d: [R, C] -> (q [R,C] | None, q^T [C,R] | None, dequant scale (1-elem fp32 tensor)).
+        colsum: an fp32 [R / 128 * C] buffer that also receives x2d's column sums per 128-row tile
+        (the bias-gradient partials of a dY) when the HIP full-tile kernel runs; ``self.cs_done``
+        tells whether it did."""
+        self.cs_done = False
         x2d = x2d if x2d.dtype == torch.bfloat16 else x2d.to(torch.bfloat16)
         if x2d.stride(-1) != 1 or x2d.stride(0) % 8 or x2d.data_ptr() % 16:
             x2d = x2d.contiguous()
@@ -119,7 +123,13 @@ class FP8Meta:
                 self.hist[prev] = x2d.detach().abs().max().float()
         q = torch.empty(R, C, dtype=self.dtype, device=dev) if want_q else None
         qt = torch.empty(C, R, dtype=self.dtype, device=dev) if want_qt else None
-        if use_hip:
+        if use_hip and colsum is not None and R % 128 == 0 and C % 128 == 0 and x2d.stride(0) % 8 == 0:
+            N.check(N.lib.pa_fp8_cast_transpose_cs(N.ptr(x2d), R, C, x2d.stride(0), N.ptr(q), N.ptr(qt),
+                                                   N.ptr(self.hist), L, cur, N.ptr(sinv), _FMT[self.dtype],
+                                                   float(self.margin_mul), N.ptr(colsum), N.stream()),
+                    'fp8_cast_transpose_cs')
+            self.cs_done = True
+        elif use_hip:
             N.check(N.lib.pa_fp8_cast_transpose(N.ptr(x2d), R, C, x2d.stride(0), N.ptr(q), N.ptr(qt),
                                                 N.ptr(self.hist), L, cur, N.ptr(sinv), _FMT[self.dtype],
                                                 float(self.margin_mul), N.stream()), 'fp8_cast_transpose')
@@ -220,14 +230,27 @@ class _FP8Linear(torch.autograd.Function):
         Nout = dy.shape[-1]
         dy2 = dy.reshape(-1, Nout)
         need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-        gq, gqt, sg = st.g.cast(dy2, want_q=need_dx, want_qt=need_dw)
+        need_db = ctx.has_b and ctx.needs_input_grad[2]
+        M = dy2.shape[0]
+        # the bias gradient's partial column sums come out of the dY cast (no second pass over dY)
+        part = torch.empty((M // 128) * Nout, dtype=torch.float32, device=dy2.device) \
+            if BIAS_FROM_CAST and need_db and dy2.is_cuda and M % 128 == 0 and Nout % 128 == 0 else None
+        gq, gqt, sg = st.g.cast(dy2, want_q=need_dx, want_qt=need_dw, colsum=part)
+        if not st.g.cs_done:
+            part = None
         dx = dw = db = None
         if need_dx:
             dx = fp8_mm(gq, wq, sg, sw).reshape(ctx.xshape).to(ctx.xdt)
         if need_dw and not _slot_fp8_wgrad(xqt, gqt, sx, sg, ctx.w_t):
             dw = fp8_mm(xqt, gqt, sx, sg).to(ctx.wdt)
-        if ctx.has_b and ctx.needs_input_grad[2] and not _slot_bias(dy2.contiguous(), ctx.b_t):
-            db = _colsum(dy2).to(ctx.bdt)
+        if need_db:
+            if part is not None:
+                if not _slot_bias(dy2, ctx.b_t, part, M // 128):
+                    from . import fused
+                    db = fused.colsum_finish_parts(part, torch.empty(Nout, dtype=torch.float32, device=dy2.device),
+                                                   M // 128, accumulate=False).to(ctx.bdt)
+            elif not _slot_bias(dy2.contiguous(), ctx.b_t):
+                db = _colsum(dy2).to(ctx.bdt)
         return dx, dw, db, None
 
 
@@ -303,6 +326,7 @@ def _static_state(w, recipe, key=None):
     return st
 
 
+BIAS_FROM_CAST = True  # bias gradients from the dY cast's column sums (tests / A/B switch it)
 FUSED_QUANT = True  # fp8 FFN: quantise gelu(h) / dh inside the GEMM epilogues (tests switch it)
 
 
@@ -366,7 +390,12 @@ class _FP8FFN(torch.autograd.Function):
         xdt, w1dt, b1dt, w2dt, b2dt = ctx.dt
         dy2 = dy.contiguous()
         M = dy2.shape[0]
-        dq, dqt, sd = st2.g.cast(dy2)
+        N2 = dy2.shape[1]
+        part2 = torch.empty((M // 128) * N2, dtype=torch.float32, device=dy2.device) \
+            if BIAS_FROM_CAST and M % 128 == 0 and N2 % 128 == 0 else None
+        dq, dqt, sd = st2.g.cast(dy2, colsum=part2)  # + b2's gradient partials
+        if not st2.g.cs_done:
+            part2 = None
         P = -(-M // 128)
         part = torch.empty(P * w2q.shape[0], dtype=torch.float32, device=dy2.device)
         fq = _fp8_epi_q(dq, w2q, sd, sw2, 11, h, st1.g, bias=part)
@@ -382,7 +411,11 @@ class _FP8FFN(torch.autograd.Function):
             db1 = torch.empty(w2q.shape[0], dtype=b1dt, device=dy2.device)
             fused.colsum_finish_parts(part, db1, P, accumulate=False)
         dw2 = None if _slot_fp8_wgrad(gqt, dqt, sg, sd, w2) else fp8_mm(gqt, dqt, sg, sd).to(w2dt)
-        db2 = None if _slot_bias(dy2, b2) else _colsum(dy2).to(b2dt)
+        if part2 is not None:
+            db2 = None if _slot_bias(dy2, b2, part2, M // 128) else fused.colsum_finish_parts(
+                part2, torch.empty(N2, dtype=torch.float32, device=dy2.device), M // 128, accumulate=False).to(b2dt)
+        else:
+            db2 = None if _slot_bias(dy2, b2) else _colsum(dy2).to(b2dt)
         dx = fp8_mm(hq, w1q, shh, sw1).to(xdt) if ctx.needs_input_grad[0] else None
         dw1 = None if _slot_fp8_wgrad(xqt, hqt, sx, shh, w1) else fp8_mm(xqt, hqt, sx, shh).to(w1dt)
         return dx, dw1, db1, dw2, db2, None, None, None

@@ -188,6 +188,50 @@ def test_hip_fp8_linear_vs_fp32():
     assert rel(y.detach(), yr.detach()) < 0.06
     assert rel(x.grad, xr.grad) < 0.12
     assert rel(w.grad, wr.grad) < 0.12
+    assert rel(b.grad, br.grad) < 1e-2  # the bias gradient: exact column sums of dY (from the dY cast)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,C", [(512, 768), (32768 // 8, 2304), (256, 128)])
+def test_hip_cast_transpose_column_sums(R, C):
+    """The dY cast's per-128-row-tile column sums (pa_fp8_cast_transpose_cs) == torch sums of the
+    same bf16 tiles, and its q / q^T bytes == the plain cast's."""
+    from paddle.ops import _native as N
+    assert N._load() is not None, N.load_error
+    torch.manual_seed(4)
+    x = (torch.randn(R, C, device='cuda') * 2).to(torch.bfloat16)
+    cs = torch.empty((R // 128) * C, dtype=torch.float32, device='cuda')
+    m1 = F8.FP8Meta(torch.float8_e5m2, 8, 0, 'cuda')
+    q1, qt1, s1 = m1.cast(x, colsum=cs)
+    assert m1.cs_done
+    m0 = F8.FP8Meta(torch.float8_e5m2, 8, 0, 'cuda')
+    q0, qt0, s0 = m0.cast(x)
+    torch.cuda.synchronize()
+    assert torch.equal(q1.view(torch.uint8), q0.view(torch.uint8))
+    assert torch.equal(qt1.view(torch.uint8), qt0.view(torch.uint8))
+    ref = x.float().reshape(R // 128, 128, C).sum(1).reshape(-1)
+    assert torch.allclose(cs, ref, rtol=1e-5, atol=1e-3), (cs - ref).abs().max().item()
+
+
+@pytest.mark.gpu
+def test_hip_fp8_linear_bias_grad_paths_agree():
+    """fp8 Linear bias gradient from the dY cast's column sums == the separate column-sum pass."""
+    torch.manual_seed(1)
+    M, K, Nn = 1024, 256, 384
+    x = torch.randn(M, K, device='cuda', dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(K, Nn, device='cuda') * 0.05).to(torch.bfloat16).requires_grad_()
+    g = torch.randn(M, Nn, device='cuda', dtype=torch.bfloat16)
+    got = []
+    for flag in (True, False):
+        F8.BIAS_FROM_CAST = flag
+        try:
+            b = torch.zeros(Nn, device='cuda', dtype=torch.bfloat16, requires_grad=True)
+            st = F8.FP8State(F8.DelayedScaling(), 'cuda')
+            F8._FP8Linear.apply(x, w, b, st).backward(g)
+            got.append(b.grad.float().clone())
+        finally:
+            F8.BIAS_FROM_CAST = True
+    assert torch.allclose(got[0], got[1], rtol=1e-2, atol=1e-2), (got[0] - got[1]).abs().max().item()
 
 
 @pytest.mark.gpu
