@@ -1032,6 +1032,9 @@ class OpcodeTranslator:
 
     def __init__(self, fn):
         self.self_obj = None
+        if not isinstance(fn, (types.FunctionType, types.MethodType)) and callable(fn) and \
+                isinstance(getattr(type(fn), '__call__', None), types.FunctionType):
+            fn = types.MethodType(type(fn).__call__, fn)  # a callable object (a Layer): its __call__
         if isinstance(fn, types.MethodType):
             self.self_obj, fn = fn.__self__, fn.__func__
         self.fn = fn
